@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""Benchmark: AdvancedNCF training samples/s (+ inference pairs/s) on MI355X.
+
+Workload (BASELINE.json configs[1]): 1,000,000 users x 100,000 items, D=64,
+4 attention heads, MLP [256,128,64], T=32; B=4096 interaction groups x M=5 rows (1 positive +
+4 negatives) = 20,480 samples per step per GPU.  A step is one full ModelTrainer.train_epoch
+batch: forward, BCE, backward, dense-exact Adam over all 140.8M embedding parameters + the dense
+parameters (src/model/trainer.py:253-285).  Synthetic data: users uniform, positive items
+Zipf(1.05), negatives uniform; random-init weights.  Inputs are resident in HBM before timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import _ncf_pkg  # noqa: E402
+
+METRIC = "train samples/sec + infer pairs/sec, 1M×100K d=64 AdvancedNCF @1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0
+
+
+def zipf_sampler(n_items, s, device):
+    w = 1.0 / torch.arange(1, n_items + 1, dtype=torch.float64) ** s
+    cdf = torch.cumsum(w / w.sum(), 0).to(device=device, dtype=torch.float64)
+    perm = torch.randperm(n_items, generator=torch.Generator().manual_seed(7)).to(device)
+
+    def sample(k, gen):
+        u = torch.rand(k, generator=gen, device=device, dtype=torch.float64)
+        idx = torch.searchsorted(cdf, u).clamp_max(n_items - 1)
+        return perm[idx]
+    return sample
+
+
+def make_batches(U, I, B, M, count, device, seed):
+    gen = torch.Generator(device=device).manual_seed(seed)
+    zipf = zipf_sampler(I, 1.05, device)
+    out = []
+    for _ in range(count):
+        users = torch.randint(0, U, (B,), generator=gen, device=device).repeat_interleave(M)
+        pos = zipf(B, gen)
+        neg = torch.randint(0, I, (B, M - 1), generator=gen, device=device)
+        items = torch.cat([pos[:, None], neg], 1).reshape(-1).contiguous()
+        t = torch.zeros(B, M, device=device)
+        t[:, 0] = 1
+        out.append((users.contiguous(), items, t.reshape(-1, 1)))
+    return out
+
+
+def cpu_baseline(model_sd, cfg, batches_cpu, budget_s):
+    """The CPU oracle (fp32 PyTorch restatement of the reference math, oracle/ncf_oracle.py)
+    timed on this host's cores on a bounded sample of the same workload."""
+    from oracle import ncf_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    p = {k: v.detach().cpu().clone() for k, v in model_sd.items()}
+    opt = O.AdamState(lr=1e-3, weight_decay=1e-5)
+    U, I, D, T, H, hid, B, M = cfg
+    kw = dict(negative_samples=M - 1, num_heads=H, temporal_dim=T, n_layers=len(hid))
+    u, i, t = batches_cpu[0]
+    O.train_step(p, opt, u, i, t, **kw)            # warm-up (allocations, first-touch)
+    times = []
+    k = 0
+    t_all = time.perf_counter()
+    while True:
+        u, i, t = batches_cpu[(k + 1) % len(batches_cpu)]
+        t0 = time.perf_counter()
+        O.train_step(p, opt, u, i, t, **kw)
+        times.append(time.perf_counter() - t0)
+        k += 1
+        if time.perf_counter() - t_all > budget_s or k >= 20:
+            break
+    med = sorted(times)[len(times) // 2]
+    return {"value": (B * M) / med, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{k} timed C2 train steps (B={B} groups x M={M}, full 1M x 100K tables, "
+                      f"fp32, dense Adam) after 1 warm-up; median step {med * 1e3:.1f} ms; "
+                      f"CPU {platform.processor() or platform.machine()}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--users", type=int, default=1_000_000)
+    ap.add_argument("--items", type=int, default=100_000)
+    ap.add_argument("--groups", type=int, default=4096, help="interaction groups per GPU per step")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--infer-pairs", type=int, default=65536)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    ncf = _ncf_pkg.load()
+    from ncf_amd.trainer import FusedTrainStep
+
+    U, I, D, T, H, hid = args.users, args.items, 64, 32, 4, [256, 128, 64]
+    B, M = args.groups, 5
+    N = B * M
+    torch.manual_seed(1234)
+    model = ncf.AdvancedNCF(U, I, 10, 50, D, D, T, hid, H, 0.2, M - 1)
+    init_sd = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        init_sd = {k: v.clone() for k, v in model.state_dict().items()}
+    model = model.to(dev).train()
+    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5)
+    batches = make_batches(U, I, B, M, 8, dev, seed=100 + rank)
+    torch.cuda.synchronize()
+
+    # --- warm-up
+    for s in range(args.warmup):
+        u, i, t = batches[s % len(batches)]
+        step(u, i, t)
+    torch.cuda.synchronize()
+    # per-kernel HIP events around the dominant kernel (dense-exact table Adam), timed region only
+    keys = ["mf_user", "mlp_user", "mf_item", "mlp_item"]
+    ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)] for k in keys}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        model.engine.timing = {k: ev[k][s] for k in keys}
+        u, i, t = batches[s % len(batches)]
+        step(u, i, t)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    model.engine.timing = None
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_step = elapsed / args.steps * 1e3
+    samples_s = N * world * args.steps / elapsed
+    loss = float(step.last_loss.item())
+
+    # roofline of the dominant kernel: algorithmic bytes / measured duration
+    D4 = D * 4
+    rows = {"mf_user": U, "mlp_user": U, "mf_item": I, "mlp_item": I}
+    uniq = model.engine.pending  # released; recompute touched-row estimate from the last batch
+    u_last, i_last, _ = batches[(args.steps - 1) % len(batches)]
+    touched = {"user": int(torch.unique(u_last).numel()), "item": int(torch.unique(i_last).numel())}
+    tot_bytes, tot_ms = 0.0, 0.0
+    for k in keys:
+        r = rows[k]
+        t_rows = touched["user" if k.endswith("user") else "item"]
+        per_launch = r * D * 24 + r * 4 + t_rows * D4
+        dur = sum(a.elapsed_time(b) for a, b in ev[k]) / args.steps
+        tot_bytes += per_launch
+        tot_ms += dur
+    achieved = tot_bytes / (tot_ms * 1e-3) / 1e9
+    # --- inference pairs/s: eval forward (M = 1) on resident pairs
+    model.eval()
+    npairs = args.infer_pairs
+    g = torch.Generator(device=dev).manual_seed(9)
+    iu = torch.randint(0, U, (npairs,), generator=g, device=dev)
+    ii = torch.randint(0, I, (npairs,), generator=g, device=dev)
+    eng = model.engine
+    with torch.no_grad():
+        for _ in range(3):
+            eng.forward(iu, ii, 1, False, 0.0, 0)
+        torch.cuda.synchronize()
+        ti = time.perf_counter()
+        reps = 20
+        for _ in range(reps):
+            eng.forward(iu, ii, 1, False, 0.0, 0)
+        torch.cuda.synchronize()
+        infer_s = (time.perf_counter() - ti) / reps
+    infer_pairs = npairs * world / infer_s
+
+    cpu = None
+    if init_sd is not None:
+        cpu_batches = [(u.cpu(), i.cpu(), t.cpu()) for (u, i, t) in batches[:4]]
+        cpu = cpu_baseline(init_sd, (U, I, D, T, H, hid, B, M), cpu_batches, args.cpu_budget)
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(samples_s, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic: users uniform, positive items Zipf(1.05), 4 uniform negatives; random-init weights",
+            "config": {"workload": "C2 train step: 1M users x 100K items, D=64, H=4, MLP [256,128,64], "
+                                   "T=32, dropout 0.2, Adam lr 1e-3 wd 1e-5 (dense-exact)",
+                       "global_batch": N * world, "groups_per_gpu": B, "samples_per_group": M,
+                       "parallelism": f"dp{world}" if world > 1 else "single-gpu"},
+            "roofline": {"bound": "hbm", "kernel": "k_adam_table<64> (dense-exact table Adam)",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_step": int(tot_bytes), "ms_per_step": round(tot_ms, 4)},
+            "cpu_baseline": cpu,
+            "infer_pairs_per_s": round(infer_pairs, 1),
+            "infer_config": f"eval forward (M=1), {npairs} resident (user,item) pairs per GPU",
+            "final_loss": round(loss, 6),
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Build libncf_hip.so (gfx950) in-tree.  Used by __graft_entry__.build(); safe to run by hand.
+set -euo pipefail
+ROOT="$(cd "$(dirname "$0")" && pwd)"
+SRC="$ROOT/neural-collaborative-filtering-demo_amd/csrc"
+OUT="$ROOT/neural-collaborative-filtering-demo_amd/libncf_hip.so"
+HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
+OBJ="$SRC/build"
+mkdir -p "$OBJ"
+FLAGS=(--offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$SRC" -Wall -Wno-unused-function)
+pids=()
+for f in "$SRC"/*.hip; do
+  b="$(basename "$f" .hip)"
+  "$HIPCC" "${FLAGS[@]}" -c "$f" -o "$OBJ/$b.o" &
+  pids+=($!)
+done
+for p in "${pids[@]}"; do wait "$p"; done
+"$HIPCC" --offload-arch=gfx950 -shared -fPIC "$OBJ"/*.o -o "$OUT.tmp"
+mv "$OUT.tmp" "$OUT"
+echo "built $OUT"

@@ -1,0 +1,161 @@
+/*
+ * ncf_hip.h — C-ABI of libncf_hip.so, the MI355X (gfx950) AdvancedNCF hot path.
+ *
+ * The reference (ethanshenley/Neural-Collaborative-Filtering-Demo) is pure Python; its hot path
+ * is AdvancedNCF.forward / backward + torch.optim.Adam.step (src/model/architecture.py:258-381,
+ * src/model/trainer.py:253-285), executed by ATen and torchrec kernels.  Each entry point below
+ * replaces the implicit kernel(s) of one stage of that path; the host side (Python,
+ * neural-collaborative-filtering-demo_amd/) binds them with ctypes.
+ *
+ * Conventions
+ *   - plain device pointers, int64 sizes, fp32 data, int64 ids (KeyedJaggedTensor values);
+ *   - every call is asynchronous on `stream` (a hipStream_t), never synchronises the host,
+ *     never allocates: scratch comes from a caller-provided workspace (size queries below);
+ *   - return 0 on success, a negative NCF_ERR_* code otherwise; ncf_last_error() gives a
+ *     thread-local message.  Stateless and re-entrant; ordering is by stream.
+ *   - ids outside [0, rows) never read out of bounds: they read row 0 and set bit 0 of the
+ *     caller's device `err_flag` (the host raises IndexError, like nn.EmbeddingBag).
+ */
+#ifndef NCF_HIP_H
+#define NCF_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NCF_OK 0
+#define NCF_ERR_ARG (-1)
+#define NCF_ERR_LAUNCH (-2)
+#define NCF_ERR_WORKSPACE (-3)
+
+int ncf_version(void);
+const char* ncf_last_error(void);
+int ncf_device_count(void);
+
+/* ---- a2+a3+a4: EBC lookups x4 + mf_norm/mlp_norm + GMF dot --------------------------------
+ * Replaces: EmbeddingBagCollection fwd (architecture.py:286-287), LayerNorms (:305-306,
+ * :311-312), mf_vector/mf_output (:307-308).  Writes mf_pred[n], LN'd MLP rows [n,dim] (the
+ * attention inputs) and, when non-NULL, LN'd GMF rows (kept for the backward).            */
+int ncf_gather_ln_gmf_fwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
+                          const float* mf_user, const float* mf_item, const float* mlp_user,
+                          const float* mlp_item, int64_t num_users, int64_t num_items,
+                          int64_t dim, const float* mf_gamma, const float* mf_beta,
+                          const float* mlp_gamma, const float* mlp_beta, const float* mf_out_w,
+                          const float* mf_out_b, float eps, float* mf_pred, float* mlp_user_ln,
+                          float* mlp_item_ln, float* mf_user_ln, float* mf_item_ln,
+                          int* err_flag, void* stream);
+
+/* Row gather (+ optional LayerNorm): EBC forward as read by callers (app.py:156-184) and
+ * get_user_embeddings / get_product_embeddings (architecture.py:383-407).                   */
+int ncf_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t rows,
+                    int64_t dim, const float* ln_gamma, const float* ln_beta, float eps,
+                    float* out, int* err_flag, void* stream);
+
+/* ---- dense layers: fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32) --------------------------------
+ * Replaces the addmm/mm of the attention projections (architecture.py:40-42, :57) and the MLP
+ * tower Linear layers (:230-246) fwd and bwd.  C = act(A·B + bias); A(i,k) = a_trans ?
+ * A[k*lda+i] : A[i*lda+k]; B(k,j) = b_trans ? B[j*ldb+k] : B[k*ldb+j]; flags bit0 = ReLU,
+ * bit1 = accumulate into C.                                                                */
+int ncf_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int a_trans,
+                 const float* B, int64_t ldb, int b_trans, float* C, int64_t ldc,
+                 const float* bias, int flags, void* stream);
+int64_t ncf_gemm_splitk_workspace(int64_t M, int64_t N, int splits);
+/* Long-K GEMM for weight gradients (dW = dYᵀ·X over the batch), deterministic slab reduce. */
+int ncf_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                        int a_trans, const float* B, int64_t ldb, int b_trans, float* C,
+                        int64_t ldc, int accumulate, int splits, float* workspace,
+                        int64_t workspace_floats, void* stream);
+int64_t ncf_colsum_workspace(int64_t rows, int64_t cols);
+/* Bias gradients: out[c] (+)= sum_r X[r*ld+c]. */
+int ncf_colsum(const float* X, int64_t rows, int64_t cols, int64_t ld, float* out,
+               int accumulate, float* workspace, int64_t workspace_floats, void* stream);
+
+/* p[r*ld + c] = value (zero the gradient columns of mlp.0.weight that see the all-zero
+ * temporal features, architecture.py:329-340). */
+int ncf_fill_2d(float* p, int64_t rows, int64_t cols, int64_t ld, float value, void* stream);
+
+/* ---- a5: MultiHeadAttention core over each group of `group_len` rows ----------------------
+ * Replaces MultiHeadAttention.forward's bmm/softmax/dropout/bmm (architecture.py:45-55) as
+ * called at :319-323.  q,k,v,out: [groups*group_len, dim]; probs: [groups, heads, L, L]
+ * (pre-dropout softmax, saved for backward).  group_len <= 64, head dim in {8,16,32,64}.   */
+int ncf_attention_fwd(const float* q, const float* k, const float* v, int64_t groups,
+                      int64_t group_len, int64_t heads, int64_t dim, float dropout_p,
+                      uint64_t seed, float* probs, float* out, void* stream);
+int ncf_attention_bwd(const float* q, const float* k, const float* v, const float* probs,
+                      const float* grad_out, int64_t groups, int64_t group_len, int64_t heads,
+                      int64_t dim, float dropout_p, uint64_t seed, float* grad_scores,
+                      float* grad_q, float* grad_k, float* grad_v, void* stream);
+
+/* ---- a6: TemporalEncoding (architecture.py:59-94): hour/day/month rows + pe[days mod P] -- */
+int ncf_temporal_fwd(const int64_t* hour, const int64_t* day, const int64_t* month,
+                     const int64_t* days_since, int64_t n, const float* hour_embed,
+                     const float* day_embed, const float* month_embed, const float* pe,
+                     int64_t max_period, int64_t dim, float* out, int* err_flag, void* stream);
+int ncf_temporal_bwd(const int64_t* hour, const int64_t* day, const int64_t* month, int64_t n,
+                     const float* grad_out, int64_t dim, float* grad_hour, float* grad_day,
+                     float* grad_month, void* stream);
+
+/* ---- a7: MLP tower row ops (ReLU -> LayerNorm -> Dropout), architecture.py:233-239 -------- */
+int ncf_relu_ln_dropout_fwd(float* relu_in, int64_t n, int64_t width, const float* gamma,
+                            const float* beta, float eps, float dropout_p, uint64_t seed,
+                            float* out, float* mean, float* rstd, void* stream);
+int64_t ncf_relu_ln_dropout_bwd_workspace(int64_t n, int64_t width);
+int ncf_relu_ln_dropout_bwd(const float* grad_out, const float* relu_in, const float* mean,
+                            const float* rstd, const float* gamma, int64_t n, int64_t width,
+                            float dropout_p, uint64_t seed, float* grad_lin, float* grad_gamma,
+                            float* grad_beta, float* workspace, int64_t workspace_floats,
+                            void* stream);
+
+/* ---- a8 + a12: mlp_output + final Linear(2,1) + Sigmoid (+ fused BCELoss) -----------------
+ * Replaces architecture.py:345, :353-354 and nn.BCELoss (trainer.py:78, :271).             */
+int ncf_head_fwd(const float* mlp_last, int64_t n, int64_t width, const float* mlp_out_w,
+                 const float* mlp_out_b, const float* mf_pred, const float* final_w,
+                 const float* final_b, float* mlp_pred, float* prob, void* stream);
+int64_t ncf_head_bwd_workspace(int64_t n, int64_t width, int64_t dim);
+int ncf_head_bwd(const float* prob, const float* grad_prob, const float* targets,
+                 const float* mf_pred, const float* mlp_pred, const float* mlp_last, int64_t n,
+                 int64_t width, const float* mlp_out_w, const float* final_w,
+                 const float* mf_user_ln, const float* mf_item_ln, int64_t dim,
+                 const float* mf_out_w, float* grad_mlp_last, float* grad_mf_user_ln,
+                 float* grad_mf_item_ln, float* grad_mlp_out_w, float* grad_mlp_out_b,
+                 float* grad_mf_out_w, float* grad_mf_out_b, float* grad_final_w,
+                 float* grad_final_b, float* loss, float* workspace, int64_t workspace_floats,
+                 void* stream);
+
+/* ---- a2/a3 backward: sparse segment-reduce + LayerNorm backward ----------------------------
+ * Replaces _embedding_bag_dense_backward (+ sort) of the four EBC tables and the mf_norm /
+ * mlp_norm backward.  Produces compact per-unique-id gradients and slot maps (slot[id] = c);
+ * the dense [rows, D] gradient is never materialised.                                       */
+int64_t ncf_embedding_bwd_workspace(int64_t n, int64_t dim);
+int ncf_embedding_bwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n, int64_t dim,
+                      int64_t num_users, int64_t num_items, const float* dy_mf_user,
+                      const float* dy_mlp_user, const float* dy_mf_item, const float* dy_mlp_item,
+                      const float* mf_user, const float* mlp_user, const float* mf_item,
+                      const float* mlp_item, const float* mf_gamma, const float* mlp_gamma,
+                      float eps, float* grad_mf_user, float* grad_mlp_user, float* grad_mf_item,
+                      float* grad_mlp_item, int64_t* uniq_users, int64_t* uniq_items,
+                      int32_t* slot_users, int32_t* slot_items, uint32_t* num_unique,
+                      float* grad_mf_gamma, float* grad_mf_beta, float* grad_mlp_gamma,
+                      float* grad_mlp_beta, void* workspace, int64_t workspace_bytes,
+                      void* stream);
+int ncf_slot_reset(const int64_t* uniq, const uint32_t* num_unique, int kind, int32_t* slot,
+                   int64_t max_n, void* stream);
+/* dense[uniq[c]] = grad_compact[c] (materialise a dense table gradient for non-Adam users). */
+int ncf_scatter_compact_rows(float* dense_grad, int64_t dim, const int64_t* uniq,
+                             const uint32_t* num_unique, int kind, const float* grad_compact,
+                             int64_t max_n, void* stream);
+
+/* ---- a13: torch.optim.Adam step (trainer.py:71-75, :285) ----------------------------------
+ * Dense-exact over a whole table via the slot map (every row decays every step).            */
+int ncf_adam_table(float* param, float* exp_avg, float* exp_avg_sq, int64_t rows, int64_t dim,
+                   const int32_t* slot, const float* grad_compact, double lr, double beta1,
+                   double beta2, double eps, double weight_decay, double step, void* stream);
+int ncf_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                  double lr, double beta1, double beta2, double eps, double weight_decay,
+                  double step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NCF_HIP_H */

@@ -1,0 +1,124 @@
+"""ctypes binding of libncf_hip.so (include/ncf_hip.h).
+
+The library is built for gfx950 by ``build_ext.sh`` (driven by ``__graft_entry__.build()``) and
+lives next to this file.  It links ``libamdhip64.so.7``; ``torch`` is imported first so the
+dynamic linker binds the library to the SAME HIP runtime torch uses, which makes torch's stream
+handles and device pointers valid inside it.
+
+There is no CPU fallback: if the library is missing or cannot be loaded, every compute entry
+point raises ``NCFLibraryError``.
+"""
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL: binds libncf_hip to torch's HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libncf_hip.so")
+
+
+class NCFLibraryError(RuntimeError):
+    pass
+
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int
+F32 = ctypes.c_float
+F64 = ctypes.c_double
+U64 = ctypes.c_uint64
+
+# name -> (restype, argtypes); mirrors include/ncf_hip.h exactly
+SIGNATURES = {
+    "ncf_version": (I32, []),
+    "ncf_last_error": (ctypes.c_char_p, []),
+    "ncf_device_count": (I32, []),
+    "ncf_gather_ln_gmf_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P, F32,
+                                    P, P, P, P, P, P, P]),
+    "ncf_gather_rows": (I32, [P, I64, P, I64, I64, P, P, F32, P, P, P]),
+    "ncf_gemm_f32": (I32, [I64, I64, I64, P, I64, I32, P, I64, I32, P, I64, P, I32, P]),
+    "ncf_gemm_splitk_workspace": (I64, [I64, I64, I32]),
+    "ncf_gemm_f32_splitk": (I32, [I64, I64, I64, P, I64, I32, P, I64, I32, P, I64, I32, I32, P,
+                                  I64, P]),
+    "ncf_colsum_workspace": (I64, [I64, I64]),
+    "ncf_colsum": (I32, [P, I64, I64, I64, P, I32, P, I64, P]),
+    "ncf_attention_fwd": (I32, [P, P, P, I64, I64, I64, I64, F32, U64, P, P, P]),
+    "ncf_attention_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P, P]),
+    "ncf_relu_ln_dropout_fwd": (I32, [P, I64, I64, P, P, F32, F32, U64, P, P, P, P]),
+    "ncf_relu_ln_dropout_bwd_workspace": (I64, [I64, I64]),
+    "ncf_relu_ln_dropout_bwd": (I32, [P, P, P, P, P, I64, I64, F32, U64, P, P, P, P, I64, P]),
+    "ncf_head_fwd": (I32, [P, I64, I64, P, P, P, P, P, P, P, P]),
+    "ncf_head_bwd_workspace": (I64, [I64, I64, I64]),
+    "ncf_head_bwd": (I32, [P, P, P, P, P, P, I64, I64, P, P, P, P, I64, P, P, P, P, P, P, P, P,
+                           P, P, P, P, I64, P]),
+    "ncf_embedding_bwd_workspace": (I64, [I64, I64]),
+    "ncf_embedding_bwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
+                                P, P, P, P, P, P, P, P, P, P, P, P, I64, P]),
+    "ncf_slot_reset": (I32, [P, P, I32, P, I64, P]),
+    "ncf_scatter_compact_rows": (I32, [P, I64, P, P, I32, P, I64, P]),
+    "ncf_adam_table": (I32, [P, P, P, I64, I64, P, P, F64, F64, F64, F64, F64, F64, P]),
+    "ncf_adam_flat": (I32, [P, P, P, P, I64, F64, F64, F64, F64, F64, F64, P]),
+    "ncf_fill_2d": (I32, [P, I64, I64, I64, F32, P]),
+    "ncf_temporal_fwd": (I32, [P, P, P, P, I64, P, P, P, P, I64, I64, P, P, P]),
+    "ncf_temporal_bwd": (I32, [P, P, P, I64, P, I64, P, P, P, P]),
+}
+
+_lock = threading.Lock()
+_lib = None
+_load_error = None
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the ctypes library; raise NCFLibraryError when unavailable."""
+    global _lib, _load_error
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            _load_error = f"{path} not found — run __graft_entry__.build() (or ./build_ext.sh)"
+            raise NCFLibraryError(_load_error)
+        try:
+            lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            _load_error = f"cannot load {path}: {e}"
+            raise NCFLibraryError(_load_error) from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        msg = _lib.ncf_last_error().decode(errors="replace") if _lib is not None else ""
+        if rc == -1:
+            raise ValueError(f"{name}: {msg}")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
+def call(name: str, *args):
+    lib = _lib if _lib is not None else load()
+    rc = getattr(lib, name)(*args)
+    check(rc, name)
+    return rc
+
+
+def query(name: str, *args) -> int:
+    lib = _lib if _lib is not None else load()
+    return int(getattr(lib, name)(*args))
+
+
+def ptr(t) -> int:
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,171 @@
+// Fused Adam for the AdvancedNCF parameters — torch.optim.Adam(model.parameters(), lr,
+// weight_decay) semantics exactly as the reference trainer constructs it
+// (src/model/trainer.py:71-75; step at :285):
+//   g += wd * p                    (coupled L2, every element, every step)
+//   m  = m + (1-b1) * (g - m)      (exp_avg.lerp_)
+//   v  = v * b2 + (1-b2) * g * g   (exp_avg_sq.mul_.addcmul_)
+//   p += -step_size * m / (sqrt(v) / sqrt(1-b2^t) + eps),   step_size = lr / (1-b1^t)
+// Scalars are computed on the host in double and rounded to fp32, as torch does.
+//
+// Embedding tables are updated DENSE-EXACT: the reference's dense [rows, D] gradient is zero on
+// untouched rows, but weight decay makes every row move every step, so every
+// element of every table is streamed.  Touched rows take their gradient from the compact buffer
+// written by ncf_embedding_bwd through the slot map (slot[row] = compact index or -1): the
+// per-step traffic is exactly p, m, v read+write (24 B/element) + 4 B/row slot + the touched rows.
+// HBM-bound: float4 per lane, grid-stride over the table.
+#include "ncf_common.h"
+
+namespace {
+
+struct AdamScalars {
+  float neg_step, w1, b2, c2, bc2_sqrt, eps, wd;
+};
+
+__device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, const AdamScalars& s) {
+  g = g + s.wd * p;
+  m = m + s.w1 * (g - m);
+  v = v * s.b2;
+  v = v + s.c2 * g * g;
+  const float denom = sqrtf(v) / s.bc2_sqrt + s.eps;
+  p = p + s.neg_step * (m / denom);
+}
+
+__device__ __forceinline__ void adam4(float4& p, float4& m, float4& v, float4 g, const AdamScalars& s) {
+  adam1(p.x, m.x, v.x, g.x, s);
+  adam1(p.y, m.y, v.y, g.y, s);
+  adam1(p.z, m.z, v.z, g.z, s);
+  adam1(p.w, m.w, v.w, g.w, s);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_adam_table(float* __restrict__ p, float* __restrict__ m,
+                                                    float* __restrict__ v, int64_t rows,
+                                                    const int32_t* __restrict__ slot,
+                                                    const float* __restrict__ G, AdamScalars s) {
+  const int64_t n4 = rows * (D / 4);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n4;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = e / (D / 4);
+    const int col = (int)(e % (D / 4)) * 4;
+    const int32_t sl = slot ? slot[row] : -1;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (sl >= 0) g = ld4(G + (int64_t)sl * D + col);
+    float4 pp = ld4(p + e * 4), mm = ld4(m + e * 4), vv = ld4(v + e * 4);
+    adam4(pp, mm, vv, g, s);
+    st4(p + e * 4, pp);
+    st4(m + e * 4, mm);
+    st4(v + e * 4, vv);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   int64_t n, AdamScalars s) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    adam1(pp, mm, vv, g[i], s);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+  }
+}
+
+// dense[uniq[c]] = G[c] for c < num_unique[kind]  (materialise a dense table gradient)
+template <int D>
+__global__ void k_scatter_compact(float* __restrict__ dense, const int64_t* __restrict__ uniq,
+                                  const uint32_t* __restrict__ num_unique, int kind,
+                                  const float* __restrict__ G, int64_t max_n) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = t / (D / 4);
+  const int col = (int)(t % (D / 4)) * 4;
+  if (c >= max_n || c >= (int64_t)num_unique[kind]) return;
+  st4(dense + uniq[c] * D + col, ld4(G + c * D + col));
+}
+
+AdamScalars make_scalars(double lr, double beta1, double beta2, double eps, double wd, double step) {
+  AdamScalars s;
+  const double bc1 = 1.0 - pow(beta1, step);
+  const double bc2 = 1.0 - pow(beta2, step);
+  s.neg_step = (float)(-(lr / bc1));
+  s.w1 = (float)(1.0 - beta1);
+  s.b2 = (float)beta2;
+  s.c2 = (float)(1.0 - beta2);
+  s.bc2_sqrt = (float)sqrt(bc2);
+  s.eps = (float)eps;
+  s.wd = (float)wd;
+  return s;
+}
+
+int grid_for(int64_t work) {
+  int64_t b = (work + 255) / 256;
+  if (b > 256 * 16) b = 256 * 16;  // grid-stride beyond 16 blocks per CU
+  return b < 1 ? 1 : (int)b;
+}
+
+template <int D>
+int table_d(float* p, float* m, float* v, int64_t rows, const int32_t* slot, const float* G,
+            const AdamScalars& s, hipStream_t st) {
+  hipLaunchKernelGGL(k_adam_table<D>, dim3(grid_for(rows * (D / 4))), dim3(256), 0, st, p, m, v,
+                     rows, slot, G, s);
+  NCF_CHECK_LAUNCH("ncf_adam_table");
+  return NCF_OK;
+}
+
+template <int D>
+int scatter_d(float* dense, const int64_t* uniq, const uint32_t* nu, int kind, const float* G,
+              int64_t max_n, hipStream_t st) {
+  hipLaunchKernelGGL(k_scatter_compact<D>, dim3(ncf_cdiv(max_n * (D / 4), 256)), dim3(256), 0, st,
+                     dense, uniq, nu, kind, G, max_n);
+  NCF_CHECK_LAUNCH("ncf_scatter_compact_rows");
+  return NCF_OK;
+}
+
+}  // namespace
+
+#define NCF_DISPATCH_DIM(D, FN, ...)                                          \
+  switch (D) {                                                                \
+    case 16: return FN<16>(__VA_ARGS__);                                      \
+    case 32: return FN<32>(__VA_ARGS__);                                      \
+    case 64: return FN<64>(__VA_ARGS__);                                      \
+    case 128: return FN<128>(__VA_ARGS__);                                    \
+    case 256: return FN<256>(__VA_ARGS__);                                    \
+    default: ncf_set_error("unsupported dim %lld", (long long)D); return NCF_ERR_ARG; \
+  }
+
+// One Adam step over a whole [rows, dim] table (dense-exact; see header).  `slot`/`grad_compact`
+// may be NULL (no touched rows: weight decay only).  `step` is the 1-based step count AFTER
+// increment, as torch's state['step'].
+extern "C" int ncf_adam_table(float* param, float* exp_avg, float* exp_avg_sq, int64_t rows,
+                              int64_t dim, const int32_t* slot, const float* grad_compact,
+                              double lr, double beta1, double beta2, double eps,
+                              double weight_decay, double step, void* stream) {
+  NCF_CHECK_ARG(rows >= 0 && step >= 1, "ncf_adam_table: bad args");
+  if (rows == 0) return NCF_OK;
+  NCF_CHECK_ARG(param && exp_avg && exp_avg_sq, "ncf_adam_table: null pointer");
+  const AdamScalars s = make_scalars(lr, beta1, beta2, eps, weight_decay, step);
+  NCF_DISPATCH_DIM(dim, table_d, param, exp_avg, exp_avg_sq, rows, slot, grad_compact, s,
+                   (hipStream_t)stream);
+}
+
+// Adam over a flat fp32 buffer (the dense parameters, packed contiguously by the host).
+extern "C" int ncf_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                             int64_t n, double lr, double beta1, double beta2, double eps,
+                             double weight_decay, double step, void* stream) {
+  NCF_CHECK_ARG(n >= 0 && step >= 1, "ncf_adam_flat: bad args");
+  if (n == 0) return NCF_OK;
+  NCF_CHECK_ARG(param && grad && exp_avg && exp_avg_sq, "ncf_adam_flat: null pointer");
+  const AdamScalars s = make_scalars(lr, beta1, beta2, eps, weight_decay, step);
+  hipLaunchKernelGGL(k_adam_flat, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, param,
+                     grad, exp_avg, exp_avg_sq, n, s);
+  NCF_CHECK_LAUNCH("ncf_adam_flat");
+  return NCF_OK;
+}
+
+extern "C" int ncf_scatter_compact_rows(float* dense_grad, int64_t dim, const int64_t* uniq,
+                                        const uint32_t* num_unique, int kind,
+                                        const float* grad_compact, int64_t max_n, void* stream) {
+  if (max_n <= 0) return NCF_OK;
+  NCF_DISPATCH_DIM(dim, scatter_d, dense_grad, uniq, num_unique, kind, grad_compact, max_n,
+                   (hipStream_t)stream);
+}

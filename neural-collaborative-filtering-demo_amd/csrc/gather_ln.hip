@@ -1,0 +1,161 @@
+// Embedding-row gathers fused with LayerNorm and the GMF dot product.
+//
+// Reference (ethanshenley/Neural-Collaborative-Filtering-Demo):
+//   EBC lookups            src/model/architecture.py:286-287 (tables :153-190; single-id SUM bag == row)
+//   mf_norm / mlp_norm     :305-306, :311-312 (nn.LayerNorm(D), eps 1e-5)
+//   GMF                    :307-308 (mf_output Linear(D,1) of LN(u)*LN(i))
+//
+// Layout: tables are row-major fp32 [rows, D] (D*4-byte rows, 16-B aligned).  A row is owned by a
+// group of L = D/4 lanes holding one float4 each, so a wave64 processes 64/L rows per
+// instruction with fully coalesced 16-B loads; LayerNorm moments are xor-shuffle reductions
+// inside the group (no LDS, no barriers).  Out-of-range ids never touch memory out of bounds:
+// they read row 0 and raise bit 0 of *err (the Python layer turns that into IndexError).
+#include "ncf_common.h"
+
+namespace {
+
+template <int D>
+struct RowLN {
+  static constexpr int L = D / 4;
+  __device__ __forceinline__ static float4 ln(float4 x, float4 g, float4 b, float eps) {
+    float s = group_sum<L>(x.x + x.y + x.z + x.w);
+    float mean = s * (1.0f / D);
+    float4 c = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
+    float q = group_sum<L>(c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w);
+    float rstd = 1.0f / sqrtf(q * (1.0f / D) + eps);
+    return make_float4(c.x * rstd * g.x + b.x, c.y * rstd * g.y + b.y, c.z * rstd * g.z + b.z,
+                       c.w * rstd * g.w + b.w);
+  }
+};
+
+__device__ __forceinline__ int64_t safe_id(int64_t id, int64_t rows, int* err, bool report) {
+  if (id < 0 || id >= rows) {
+    if (err && report) atomicOr(err, 1);
+    return 0;
+  }
+  return id;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_gather_ln_gmf(
+    const int64_t* __restrict__ uid, const int64_t* __restrict__ iid, int64_t n,
+    const float* __restrict__ mfU, const float* __restrict__ mfI, const float* __restrict__ mlpU,
+    const float* __restrict__ mlpI, int64_t nU, int64_t nI, const float* __restrict__ g_mf,
+    const float* __restrict__ b_mf, const float* __restrict__ g_mlp, const float* __restrict__ b_mlp,
+    const float* __restrict__ w_mf, const float* __restrict__ bias_mf, float eps,
+    float* __restrict__ mf_pred, float* __restrict__ u_mlp_ln, float* __restrict__ i_mlp_ln,
+    float* __restrict__ u_mf_ln, float* __restrict__ i_mf_ln, int* err) {
+  constexpr int L = D / 4;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = t / L;
+  const int sub = (int)(t % L);
+  if (row >= n) return;  // whole groups retire together
+  const int64_t u = safe_id(uid[row], nU, err, sub == 0);
+  const int64_t i = safe_id(iid[row], nI, err, sub == 0);
+  const int c = sub * 4;
+  const float4 xu_mf = ld4(mfU + u * D + c), xi_mf = ld4(mfI + i * D + c);
+  const float4 xu_ml = ld4(mlpU + u * D + c), xi_ml = ld4(mlpI + i * D + c);
+  const float4 gm = ld4(g_mf + c), bm = ld4(b_mf + c), gl = ld4(g_mlp + c), bl = ld4(b_mlp + c);
+  const float4 yu = RowLN<D>::ln(xu_mf, gm, bm, eps);
+  const float4 yi = RowLN<D>::ln(xi_mf, gm, bm, eps);
+  const float4 w = ld4(w_mf + c);
+  float dot = yu.x * yi.x * w.x + yu.y * yi.y * w.y + yu.z * yi.z * w.z + yu.w * yi.w * w.w;
+  dot = group_sum<L>(dot);
+  if (sub == 0) mf_pred[row] = dot + bias_mf[0];
+  st4(u_mlp_ln + row * D + c, RowLN<D>::ln(xu_ml, gl, bl, eps));
+  st4(i_mlp_ln + row * D + c, RowLN<D>::ln(xi_ml, gl, bl, eps));
+  if (u_mf_ln) st4(u_mf_ln + row * D + c, yu);
+  if (i_mf_ln) st4(i_mf_ln + row * D + c, yi);
+}
+
+// Plain row gather (EBC forward as seen by callers such as app.py:156-184) with optional LN
+// (get_user_embeddings / get_product_embeddings, architecture.py:383-407).
+template <int D>
+__global__ __launch_bounds__(256) void k_gather_rows(const int64_t* __restrict__ ids, int64_t n,
+                                                     const float* __restrict__ table, int64_t rows,
+                                                     const float* __restrict__ g,
+                                                     const float* __restrict__ b, float eps,
+                                                     float* __restrict__ out, int* err) {
+  constexpr int L = D / 4;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = t / L;
+  const int sub = (int)(t % L);
+  if (row >= n) return;
+  const int64_t id = safe_id(ids[row], rows, err, sub == 0);
+  const int c = sub * 4;
+  float4 x = ld4(table + id * D + c);
+  if (g) x = RowLN<D>::ln(x, ld4(g + c), ld4(b + c), eps);
+  st4(out + row * D + c, x);
+}
+
+template <int D>
+int launch_gather_ln_gmf(const int64_t* uid, const int64_t* iid, int64_t n, const float* mfU,
+                         const float* mfI, const float* mlpU, const float* mlpI, int64_t nU,
+                         int64_t nI, const float* g_mf, const float* b_mf, const float* g_mlp,
+                         const float* b_mlp, const float* w_mf, const float* bias_mf, float eps,
+                         float* mf_pred, float* u_mlp_ln, float* i_mlp_ln, float* u_mf_ln,
+                         float* i_mf_ln, int* err, hipStream_t st) {
+  const int64_t threads = n * (D / 4);
+  hipLaunchKernelGGL(k_gather_ln_gmf<D>, dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st, uid, iid,
+                     n, mfU, mfI, mlpU, mlpI, nU, nI, g_mf, b_mf, g_mlp, b_mlp, w_mf, bias_mf, eps,
+                     mf_pred, u_mlp_ln, i_mlp_ln, u_mf_ln, i_mf_ln, err);
+  NCF_CHECK_LAUNCH("ncf_gather_ln_gmf_fwd");
+  return NCF_OK;
+}
+
+template <int D>
+int launch_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t rows,
+                       const float* g, const float* b, float eps, float* out, int* err,
+                       hipStream_t st) {
+  const int64_t threads = n * (D / 4);
+  hipLaunchKernelGGL(k_gather_rows<D>, dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st, ids, n,
+                     table, rows, g, b, eps, out, err);
+  NCF_CHECK_LAUNCH("ncf_gather_rows");
+  return NCF_OK;
+}
+
+}  // namespace
+
+#define NCF_DISPATCH_D(D, FN, ...)                                            \
+  switch (D) {                                                                \
+    case 16: return FN<16>(__VA_ARGS__);                                      \
+    case 32: return FN<32>(__VA_ARGS__);                                      \
+    case 64: return FN<64>(__VA_ARGS__);                                      \
+    case 128: return FN<128>(__VA_ARGS__);                                    \
+    case 256: return FN<256>(__VA_ARGS__);                                    \
+    default: ncf_set_error("unsupported embedding dim %lld (16/32/64/128/256)", (long long)D); \
+      return NCF_ERR_ARG;                                                     \
+  }
+
+extern "C" int ncf_gather_ln_gmf_fwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
+                                     const float* mf_user, const float* mf_item,
+                                     const float* mlp_user, const float* mlp_item,
+                                     int64_t num_users, int64_t num_items, int64_t dim,
+                                     const float* mf_gamma, const float* mf_beta,
+                                     const float* mlp_gamma, const float* mlp_beta,
+                                     const float* mf_out_w, const float* mf_out_b, float eps,
+                                     float* mf_pred, float* mlp_user_ln, float* mlp_item_ln,
+                                     float* mf_user_ln, float* mf_item_ln, int* err_flag,
+                                     void* stream) {
+  NCF_CHECK_ARG(n >= 0, "ncf_gather_ln_gmf_fwd: n < 0");
+  if (n == 0) return NCF_OK;
+  NCF_CHECK_ARG(user_ids && item_ids && mf_user && mf_item && mlp_user && mlp_item && mf_pred &&
+                    mlp_user_ln && mlp_item_ln && mf_gamma && mf_beta && mlp_gamma && mlp_beta &&
+                    mf_out_w && mf_out_b,
+                "ncf_gather_ln_gmf_fwd: null pointer");
+  NCF_DISPATCH_D(dim, launch_gather_ln_gmf, user_ids, item_ids, n, mf_user, mf_item, mlp_user,
+                 mlp_item, num_users, num_items, mf_gamma, mf_beta, mlp_gamma, mlp_beta, mf_out_w,
+                 mf_out_b, eps, mf_pred, mlp_user_ln, mlp_item_ln, mf_user_ln, mf_item_ln,
+                 err_flag, (hipStream_t)stream);
+}
+
+extern "C" int ncf_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t rows,
+                               int64_t dim, const float* ln_gamma, const float* ln_beta, float eps,
+                               float* out, int* err_flag, void* stream) {
+  NCF_CHECK_ARG(n >= 0 && rows >= 0, "ncf_gather_rows: negative size");
+  if (n == 0) return NCF_OK;
+  NCF_CHECK_ARG(ids && table && out, "ncf_gather_rows: null pointer");
+  NCF_CHECK_ARG((ln_gamma == nullptr) == (ln_beta == nullptr), "ncf_gather_rows: gamma/beta mismatch");
+  NCF_DISPATCH_D(dim, launch_gather_rows, ids, n, table, rows, ln_gamma, ln_beta, eps, out,
+                 err_flag, (hipStream_t)stream);
+}

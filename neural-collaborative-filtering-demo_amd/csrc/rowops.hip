@@ -1,0 +1,215 @@
+// MLP-tower row ops: ReLU -> LayerNorm -> Dropout, forward and backward.
+//
+// Reference: self.mlp = n x [Linear, ReLU, LayerNorm(h), Dropout(p)] (src/model/architecture.py
+// :230-242, applied at :344).  The Linear (+ReLU, fused in the GEMM epilogue) is an MFMA GEMM
+// (gemm.hip); this file normalises each row of width W with L = min(64, W/4) lanes per row and
+// CH float4 chunks per lane (wave64: 64/L rows per wave-instruction), and in backward produces
+// the pre-ReLU gradient plus deterministic per-block partial sums of dgamma/dbeta.
+#include "ncf_common.h"
+
+namespace {
+
+template <int W>
+struct Geo {
+  static constexpr int L = (W / 4) < 64 ? (W / 4) : 64;  // lanes per row
+  static constexpr int CH = W / (4 * L);                  // float4 chunks per lane
+  static constexpr int RPW = 64 / L;                      // rows per wave-instruction
+};
+
+template <int W>
+__global__ __launch_bounds__(256) void k_relu_ln_drop_fwd(float* __restrict__ r,  // [N,W] relu(lin), in
+                                                          int64_t n, const float* __restrict__ g,
+                                                          const float* __restrict__ b, float eps,
+                                                          float p, uint64_t seed,
+                                                          float* __restrict__ out,
+                                                          float* __restrict__ mean_out,
+                                                          float* __restrict__ rstd_out) {
+  using G = Geo<W>;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = t / G::L;
+  const int sub = (int)(t % G::L);
+  if (row >= n) return;
+  float4 x[G::CH];
+  float s = 0.0f;
+#pragma unroll
+  for (int c = 0; c < G::CH; ++c) {
+    x[c] = ld4(r + row * W + (c * G::L + sub) * 4);
+    s += x[c].x + x[c].y + x[c].z + x[c].w;
+  }
+  const float mean = group_sum<G::L>(s) * (1.0f / W);
+  float q = 0.0f;
+#pragma unroll
+  for (int c = 0; c < G::CH; ++c) {
+    x[c].x -= mean; x[c].y -= mean; x[c].z -= mean; x[c].w -= mean;
+    q += x[c].x * x[c].x + x[c].y * x[c].y + x[c].z * x[c].z + x[c].w * x[c].w;
+  }
+  const float rstd = 1.0f / sqrtf(group_sum<G::L>(q) * (1.0f / W) + eps);
+  const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+#pragma unroll
+  for (int c = 0; c < G::CH; ++c) {
+    const int col = (c * G::L + sub) * 4;
+    const float4 gg = ld4(g + col), bb = ld4(b + col);
+    float4 y = make_float4(x[c].x * rstd * gg.x + bb.x, x[c].y * rstd * gg.y + bb.y,
+                           x[c].z * rstd * gg.z + bb.z, x[c].w * rstd * gg.w + bb.w);
+    if (p > 0.0f) {
+      const uint64_t base = (uint64_t)row * W + col;
+      y.x *= ncf_dropout_scale(seed, base + 0, p, inv_keep);
+      y.y *= ncf_dropout_scale(seed, base + 1, p, inv_keep);
+      y.z *= ncf_dropout_scale(seed, base + 2, p, inv_keep);
+      y.w *= ncf_dropout_scale(seed, base + 3, p, inv_keep);
+    }
+    st4(out + row * W + col, y);
+  }
+  if (sub == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// Backward.  Each block owns rows [blockIdx*rows_per_block, ...); partial dgamma/dbeta of the
+// block go to part[blockIdx][0:W] / part[blockIdx][W:2W].
+template <int W>
+__global__ __launch_bounds__(256) void k_relu_ln_drop_bwd(
+    const float* __restrict__ dout, const float* __restrict__ r, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ g, int64_t n, int rows_per_block,
+    float p, uint64_t seed, float* __restrict__ dlin, float* __restrict__ part) {
+  using G = Geo<W>;
+  __shared__ float red[256 / G::L][2 * W];
+  const int lane_grp = threadIdx.x / G::L;  // row slot inside the block iteration
+  const int sub = threadIdx.x % G::L;
+  const int slots = 256 / G::L;
+  float4 ag[G::CH], ab[G::CH];
+#pragma unroll
+  for (int c = 0; c < G::CH; ++c) { ag[c] = make_float4(0, 0, 0, 0); ab[c] = make_float4(0, 0, 0, 0); }
+  const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(n, r0 + rows_per_block);
+  for (int64_t row = r0 + lane_grp; row < r1; row += slots) {
+    const float mu = mean[row], rs = rstd[row];
+    float4 dy[G::CH], xh[G::CH];
+    float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int c = 0; c < G::CH; ++c) {
+      const int col = (c * G::L + sub) * 4;
+      float4 d = ld4(dout + row * W + col);
+      if (p > 0.0f) {
+        const uint64_t base = (uint64_t)row * W + col;
+        d.x *= ncf_dropout_scale(seed, base + 0, p, inv_keep);
+        d.y *= ncf_dropout_scale(seed, base + 1, p, inv_keep);
+        d.z *= ncf_dropout_scale(seed, base + 2, p, inv_keep);
+        d.w *= ncf_dropout_scale(seed, base + 3, p, inv_keep);
+      }
+      const float4 x = ld4(r + row * W + col);
+      const float4 gg = ld4(g + col);
+      float4 h = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
+      ag[c].x += d.x * h.x; ag[c].y += d.y * h.y; ag[c].z += d.z * h.z; ag[c].w += d.w * h.w;
+      ab[c].x += d.x; ab[c].y += d.y; ab[c].z += d.z; ab[c].w += d.w;
+      float4 gd = make_float4(d.x * gg.x, d.y * gg.y, d.z * gg.z, d.w * gg.w);
+      s1 += gd.x + gd.y + gd.z + gd.w;
+      s2 += gd.x * h.x + gd.y * h.y + gd.z * h.z + gd.w * h.w;
+      dy[c] = gd;
+      xh[c] = h;
+    }
+    const float m1 = group_sum<G::L>(s1) * (1.0f / W);
+    const float m2 = group_sum<G::L>(s2) * (1.0f / W);
+#pragma unroll
+    for (int c = 0; c < G::CH; ++c) {
+      const int col = (c * G::L + sub) * 4;
+      const float4 x = ld4(r + row * W + col);
+      float4 o;
+      o.x = x.x > 0.0f ? rs * (dy[c].x - m1 - xh[c].x * m2) : 0.0f;
+      o.y = x.y > 0.0f ? rs * (dy[c].y - m1 - xh[c].y * m2) : 0.0f;
+      o.z = x.z > 0.0f ? rs * (dy[c].z - m1 - xh[c].z * m2) : 0.0f;
+      o.w = x.w > 0.0f ? rs * (dy[c].w - m1 - xh[c].w * m2) : 0.0f;
+      st4(dlin + row * W + col, o);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < G::CH; ++c) {
+    const int col = (c * G::L + sub) * 4;
+    red[lane_grp][col + 0] = ag[c].x; red[lane_grp][col + 1] = ag[c].y;
+    red[lane_grp][col + 2] = ag[c].z; red[lane_grp][col + 3] = ag[c].w;
+    red[lane_grp][W + col + 0] = ab[c].x; red[lane_grp][W + col + 1] = ab[c].y;
+    red[lane_grp][W + col + 2] = ab[c].z; red[lane_grp][W + col + 3] = ab[c].w;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * W; i += 256) {
+    float s = 0.0f;
+    for (int k = 0; k < slots; ++k) s += red[k][i];
+    part[(int64_t)blockIdx.x * 2 * W + i] = s;
+  }
+}
+
+constexpr int RPB = 128;  // rows per backward block
+
+template <int W>
+int fwd_w(float* r, int64_t n, const float* g, const float* b, float eps, float p, uint64_t seed,
+          float* out, float* mean, float* rstd, hipStream_t st) {
+  const int64_t threads = n * Geo<W>::L;
+  hipLaunchKernelGGL(k_relu_ln_drop_fwd<W>, dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st, r, n,
+                     g, b, eps, p, seed, out, mean, rstd);
+  NCF_CHECK_LAUNCH("ncf_relu_ln_dropout_fwd");
+  return NCF_OK;
+}
+
+template <int W>
+int bwd_w(const float* dout, const float* r, const float* mean, const float* rstd, const float* g,
+          int64_t n, float p, uint64_t seed, float* dlin, float* dgamma, float* dbeta,
+          float* ws, hipStream_t st) {
+  const int nb = n == 0 ? 1 : ncf_cdiv(n, RPB);
+  hipLaunchKernelGGL(k_relu_ln_drop_bwd<W>, dim3(nb), dim3(256), 0, st, dout, r, mean, rstd, g, n,
+                     RPB, p, seed, dlin, ws);
+  NCF_CHECK_LAUNCH("ncf_relu_ln_dropout_bwd");
+  // dgamma and dbeta are contiguous halves of each partial row
+  hipLaunchKernelGGL(k_sum_partials<>, dim3(ncf_cdiv(W, 256)), dim3(256), 0, st, ws, nb,
+                     (int64_t)2 * W, (int64_t)W, dgamma, 0);
+  hipLaunchKernelGGL(k_sum_partials<>, dim3(ncf_cdiv(W, 256)), dim3(256), 0, st, ws + W, nb,
+                     (int64_t)2 * W, (int64_t)W, dbeta, 0);
+  NCF_CHECK_LAUNCH("ncf_relu_ln_dropout_bwd(reduce)");
+  return NCF_OK;
+}
+
+}  // namespace
+
+#define NCF_DISPATCH_W(W, FN, ...)                                                   \
+  switch (W) {                                                                       \
+    case 16: return FN<16>(__VA_ARGS__);                                             \
+    case 32: return FN<32>(__VA_ARGS__);                                             \
+    case 64: return FN<64>(__VA_ARGS__);                                             \
+    case 128: return FN<128>(__VA_ARGS__);                                           \
+    case 256: return FN<256>(__VA_ARGS__);                                           \
+    case 512: return FN<512>(__VA_ARGS__);                                           \
+    case 1024: return FN<1024>(__VA_ARGS__);                                         \
+    default: ncf_set_error("MLP width %lld unsupported (powers of two 16..1024)", (long long)W); \
+      return NCF_ERR_ARG;                                                            \
+  }
+
+extern "C" int64_t ncf_relu_ln_dropout_bwd_workspace(int64_t n, int64_t width) {
+  return (int64_t)(n == 0 ? 1 : ncf_cdiv(n, RPB)) * 2 * width;
+}
+
+// out = dropout(LayerNorm(r)); r already holds relu(linear) (GEMM epilogue); saves mean/rstd.
+extern "C" int ncf_relu_ln_dropout_fwd(float* relu_in, int64_t n, int64_t width,
+                                       const float* gamma, const float* beta, float eps,
+                                       float dropout_p, uint64_t seed, float* out, float* mean,
+                                       float* rstd, void* stream) {
+  NCF_CHECK_ARG(n >= 0, "ncf_relu_ln_dropout_fwd: n < 0");
+  NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_relu_ln_dropout_fwd: bad dropout");
+  if (n == 0) return NCF_OK;
+  NCF_DISPATCH_W(width, fwd_w, relu_in, n, gamma, beta, eps, dropout_p, seed, out, mean, rstd,
+                 (hipStream_t)stream);
+}
+
+extern "C" int ncf_relu_ln_dropout_bwd(const float* grad_out, const float* relu_in,
+                                       const float* mean, const float* rstd, const float* gamma,
+                                       int64_t n, int64_t width, float dropout_p, uint64_t seed,
+                                       float* grad_lin, float* grad_gamma, float* grad_beta,
+                                       float* workspace, int64_t workspace_floats, void* stream) {
+  NCF_CHECK_ARG(n >= 0, "ncf_relu_ln_dropout_bwd: n < 0");
+  if (workspace_floats < ncf_relu_ln_dropout_bwd_workspace(n, width)) {
+    ncf_set_error("ncf_relu_ln_dropout_bwd: workspace too small");
+    return NCF_ERR_WORKSPACE;
+  }
+  NCF_DISPATCH_W(width, bwd_w, grad_out, relu_in, mean, rstd, gamma, n, dropout_p, seed, grad_lin,
+                 grad_gamma, grad_beta, workspace, (hipStream_t)stream);
+}

@@ -1,0 +1,403 @@
+"""Kernel orchestration for the AdvancedNCF hot path (forward, backward, optimizer step).
+
+One ``NCFEngine`` per model.  It owns the device workspaces, the flat layout of the dense
+parameters (+ their gradient buffer) and the per-table slot maps, and it sequences the C-ABI
+kernels of libncf_hip.so on torch's current HIP stream.  Reference stages (file:line in the
+reference repo) are cited at each call.
+
+Data layout in HBM (fp32 throughout — the reference computes in fp32):
+  * embedding tables: row-major [rows, D] nn.Parameters (never copied, never densely graded);
+  * dense parameters: ONE flat buffer, each used nn.Parameter a 16-B aligned view into it, and a
+    parallel flat gradient buffer the backward kernels write into (p.grad are views of it);
+  * per-batch activations: a workspace keyed by (N, M), reused across steps (no per-step allocs).
+"""
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from . import _lib
+from ._lib import ptr
+
+LN_EPS = 1e-5
+
+
+def _align4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
+@dataclass
+class Geometry:
+    n: int          # rows (samples) in the batch
+    M: int          # rows per attention group (1 + negatives in training, 1 in eval)
+    B: int          # groups
+    D: int
+    T: int
+    H: int
+    hidden: List[int]
+
+
+class Workspace:
+    """Activation + scratch buffers for one (n, M) batch geometry."""
+
+    def __init__(self, g: Geometry, device, train: bool):
+        f = dict(device=device, dtype=torch.float32)
+        n, D = g.n, g.D
+        self.g = g
+        e = lambda *s: torch.empty(*s, **f)  # noqa: E731
+        self.mf_pred, self.mlp_pred, self.prob = e(n), e(n), e(n)
+        self.xu, self.xi, self.q, self.k, self.v, self.o, self.y = (e(n, D) for _ in range(7))
+        self.umf = e(n, D) if train else None
+        self.imf = e(n, D) if train else None
+        self.P = e(max(1, g.B * g.H * g.M * g.M))
+        self.r = [e(n, h) for h in g.hidden]
+        self.a = [e(n, h) for h in g.hidden]
+        self.mean = [e(n) for _ in g.hidden]
+        self.rstd = [e(n) for _ in g.hidden]
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.train = train
+        if not train:
+            return
+        self.dumf, self.dimf, self.dxu, self.dxi = (e(n, D) for _ in range(4))
+        self.dq, self.dk, self.dv, self.do, self.dy = (e(n, D) for _ in range(5))
+        self.dS = e(max(1, g.B * g.H * g.M * g.M))
+        self.dlin = [e(n, h) for h in g.hidden]
+        self.da = [e(n, h) for h in g.hidden]
+        self.loss = e(1)
+        # scratch sizing
+        dims = [(D, D)] + [(h, i) for h, i in zip(g.hidden, [D] + g.hidden[:-1])]
+        self.splits = {}
+        sk = 1
+        for (mo, ko) in dims:
+            s = self.splits_for(mo, ko, n)
+            self.splits[(mo, ko)] = s
+            sk = max(sk, _lib.query("ncf_gemm_splitk_workspace", mo, ko, s))
+        cs = max(_lib.query("ncf_colsum_workspace", n, w) for w in [D] + g.hidden)
+        rl = max(_lib.query("ncf_relu_ln_dropout_bwd_workspace", n, w) for w in g.hidden)
+        hd = _lib.query("ncf_head_bwd_workspace", n, g.hidden[-1], D)
+        self.scratch = e(max(sk, cs, rl, hd))
+        self.emb_ws = torch.empty(_lib.query("ncf_embedding_bwd_workspace", n, D),
+                                  dtype=torch.uint8, device=device)
+        self.G = {k: e(n, D) for k in ("mf_user", "mlp_user", "mf_item", "mlp_item")}
+        self.uniq_u = torch.empty(max(1, n), dtype=torch.int64, device=device)
+        self.uniq_i = torch.empty(max(1, n), dtype=torch.int64, device=device)
+        self.num_unique = torch.zeros(2, dtype=torch.int32, device=device)
+
+    @staticmethod
+    def splits_for(m_out: int, k_out: int, rows: int) -> int:
+        tiles = max(1, math.ceil(m_out / 64) * math.ceil(k_out / 64))
+        s = max(1, math.ceil(1024 / tiles))
+        return max(1, min(s, math.ceil(max(rows, 1) / 64)))
+
+
+class NCFEngine:
+    """Binds an AdvancedNCF module to the HIP kernels."""
+
+    def __init__(self, model):
+        self.model = model
+        self.ws: Dict[tuple, Workspace] = {}
+        self.flat = None
+        self.flat_grad = None
+        self.slot_u = None
+        self.slot_i = None
+        self.pending = None       # compact table grads of the last backward, not yet applied
+        self.dense_names: List[str] = []
+        self.offsets: Dict[str, tuple] = {}
+        self.timing = None        # optional {table: (start_event, end_event)} for the bench
+
+    # ------------------------------------------------------------------ parameter layout
+    def dense_params(self):
+        m = self.model
+        ps = [("mf_norm.weight", m.mf_norm.weight), ("mf_norm.bias", m.mf_norm.bias),
+              ("mlp_norm.weight", m.mlp_norm.weight), ("mlp_norm.bias", m.mlp_norm.bias)]
+        att = m.user_product_attention
+        for nm in ("q_proj", "k_proj", "v_proj", "out_proj"):
+            lin = getattr(att, nm)
+            ps += [(f"user_product_attention.{nm}.weight", lin.weight),
+                   (f"user_product_attention.{nm}.bias", lin.bias)]
+        for l in range(len(m.mlp_hidden_dims)):
+            lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
+            ps += [(f"mlp.{4 * l}.weight", lin.weight), (f"mlp.{4 * l}.bias", lin.bias),
+                   (f"mlp.{4 * l + 2}.weight", ln.weight), (f"mlp.{4 * l + 2}.bias", ln.bias)]
+        ps += [("mf_output.weight", m.mf_output.weight), ("mf_output.bias", m.mf_output.bias),
+               ("mlp_output.weight", m.mlp_output.weight), ("mlp_output.bias", m.mlp_output.bias),
+               ("final.0.weight", m.final[0].weight), ("final.0.bias", m.final[0].bias)]
+        return ps
+
+    def table_params(self):
+        m = self.model
+        return {"mf_user": m.mf_embedding_collection.embedding_bags["user_id"].weight,
+                "mf_item": m.mf_embedding_collection.embedding_bags["product_id"].weight,
+                "mlp_user": m.mlp_embedding_collection.embedding_bags["user_id"].weight,
+                "mlp_item": m.mlp_embedding_collection.embedding_bags["product_id"].weight}
+
+    def flatten(self):
+        """(Re)pack the used dense parameters into one 16-B aligned flat buffer (views)."""
+        ps = self.dense_params()
+        dev = ps[0][1].device
+        total, offs = 0, {}
+        for name, p in ps:
+            offs[name] = (total, p.numel(), tuple(p.shape))
+            total += _align4(p.numel())
+        flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        for name, p in ps:
+            o, n, shp = offs[name]
+            flat[o:o + n].copy_(p.data.reshape(-1))
+            p.data = flat[o:o + n].view(shp)
+        self.flat = flat
+        self.flat_grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.offsets = offs
+        self.dense_names = [n for n, _ in ps]
+        self.ws.clear()
+        self.pending = None
+        if dev.type == "cuda":
+            m = self.model
+            self.slot_u = torch.full((m.num_users,), -1, dtype=torch.int32, device=dev)
+            self.slot_i = torch.full((m.num_products,), -1, dtype=torch.int32, device=dev)
+        else:
+            self.slot_u = self.slot_i = None
+
+    def grad_view(self, name):
+        o, n, shp = self.offsets[name]
+        return self.flat_grad[o:o + n].view(shp)
+
+    def is_flat_view(self, p) -> bool:
+        if self.flat is None:
+            return False
+        base = self.flat.data_ptr()
+        return base <= p.data_ptr() < base + self.flat.numel() * 4
+
+    def ensure_layout(self):
+        ps = self.dense_params()
+        if self.flat is None or any(not self.is_flat_view(p) for _, p in ps) or \
+                self.flat.device != ps[0][1].device:
+            self.flatten()
+
+    # ------------------------------------------------------------------ helpers
+    def _check_device(self):
+        dev = self.model.mf_norm.weight.device
+        if dev.type != "cuda":
+            raise RuntimeError("ncf_amd: AdvancedNCF runs on the MI355X only (HIP kernels, no CPU "
+                               "fallback); call model.to('cuda') first")
+        _lib.load()
+        return dev
+
+    def workspace(self, n, M, train) -> Workspace:
+        key = (n, M, train)
+        w = self.ws.get(key)
+        if w is None:
+            m = self.model
+            g = Geometry(n=n, M=M, B=n // M, D=m.mlp_embedding_dim, T=m.temporal_dim,
+                         H=m.num_heads, hidden=list(m.mlp_hidden_dims))
+            w = Workspace(g, self.model.mf_norm.weight.device, train)
+            self.ws[key] = w
+        return w
+
+    @staticmethod
+    def _gemm(A, lda, a_t, Bm, ldb, b_t, C, ldc, M, N, K, bias=None, relu=False, accum=False, st=None):
+        flags = (1 if relu else 0) | (2 if accum else 0)
+        _lib.call("ncf_gemm_f32", M, N, K, ptr(A), lda, int(a_t), ptr(Bm), ldb, int(b_t), ptr(C),
+                  ldc, ptr(bias), flags, st)
+
+    def _wgrad(self, w: Workspace, dY, ldy, X, ldx, dW, ldw, m_out, k_in, n, st, accum=False):
+        """dW[m_out, k_in] = dYᵀ[m_out, n] · X[n, k_in] (split-K over the batch rows)."""
+        s = w.splits.get((m_out, k_in)) or Workspace.splits_for(m_out, k_in, n)
+        _lib.call("ncf_gemm_f32_splitk", m_out, k_in, n, ptr(dY), ldy, 1, ptr(X), ldx, 0, ptr(dW),
+                  ldw, int(accum), s, ptr(w.scratch), w.scratch.numel(), st)
+
+    def _colsum(self, w, X, rows, cols, out, st):
+        _lib.call("ncf_colsum", ptr(X), rows, cols, cols, ptr(out), 0, ptr(w.scratch),
+                  w.scratch.numel(), st)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, uid: torch.Tensor, iid: torch.Tensor, M: int, train: bool,
+                drop_p: float, seed: int) -> Workspace:
+        """AdvancedNCF.forward (architecture.py:258-381) on single-id bags; returns the workspace
+        holding prob (and, when ``train``, everything the backward needs)."""
+        dev = self._check_device()
+        self.ensure_layout()
+        m = self.model
+        n = uid.numel()
+        if n % M != 0:
+            # the reference's .view(batch_size, M, -1) (architecture.py:315) fails the same way
+            raise RuntimeError(f"batch of {n} rows is not a multiple of samples_per_interaction={M}")
+        uid = uid.to(device=dev, dtype=torch.int64).contiguous()
+        iid = iid.to(device=dev, dtype=torch.int64).contiguous()
+        w = self.workspace(n, M, train)
+        if n == 0:
+            return w
+        st = _lib.stream_ptr(dev)
+        D, H, T, hid = m.mlp_embedding_dim, m.num_heads, m.temporal_dim, list(m.mlp_hidden_dims)
+        if m.mf_embedding_dim != D:
+            raise NotImplementedError("mf_embedding_dim must equal mlp_embedding_dim on this path")
+        tb = self.table_params()
+        w.err.zero_()
+        # a2-a4: 4 gathers + mf_norm/mlp_norm + GMF  (architecture.py:286-287, 305-312)
+        _lib.call("ncf_gather_ln_gmf_fwd", ptr(uid), ptr(iid), n, ptr(tb["mf_user"]),
+                  ptr(tb["mf_item"]), ptr(tb["mlp_user"]), ptr(tb["mlp_item"]), m.num_users,
+                  m.num_products, D, ptr(m.mf_norm.weight), ptr(m.mf_norm.bias),
+                  ptr(m.mlp_norm.weight), ptr(m.mlp_norm.bias), ptr(m.mf_output.weight),
+                  ptr(m.mf_output.bias), LN_EPS, ptr(w.mf_pred), ptr(w.xu), ptr(w.xi),
+                  ptr(w.umf), ptr(w.imf), ptr(w.err), st)
+        # a5: MultiHeadAttention over each group of M rows (architecture.py:315-326)
+        att = m.user_product_attention
+        self._gemm(w.xi, D, 0, att.v_proj.weight, D, 1, w.v, D, n, D, D, bias=att.v_proj.bias, st=st)
+        if M == 1 and not train:
+            # softmax over a single key is exactly 1 -> the core returns V unchanged
+            src = w.v
+        else:
+            self._gemm(w.xu, D, 0, att.q_proj.weight, D, 1, w.q, D, n, D, D, bias=att.q_proj.bias, st=st)
+            self._gemm(w.xi, D, 0, att.k_proj.weight, D, 1, w.k, D, n, D, D, bias=att.k_proj.bias, st=st)
+            _lib.call("ncf_attention_fwd", ptr(w.q), ptr(w.k), ptr(w.v), n // M, M, H, D,
+                      drop_p if train else 0.0, seed, ptr(w.P), ptr(w.o), st)
+            src = w.o
+        self._gemm(src, D, 0, att.out_proj.weight, D, 1, w.y, D, n, D, D, bias=att.out_proj.bias, st=st)
+        # a7: MLP tower on [attn ‖ zeros_T] (architecture.py:329-344): the zero temporal columns
+        # contribute nothing, so layer 0 reads only the first D columns of mlp.0.weight
+        x, ldx, kin = w.y, D, D
+        for l, h in enumerate(hid):
+            lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
+            ldw = lin.weight.shape[1]
+            self._gemm(x, ldx, 0, lin.weight, ldw, 1, w.r[l], h, n, h, kin, bias=lin.bias,
+                       relu=True, st=st)
+            _lib.call("ncf_relu_ln_dropout_fwd", ptr(w.r[l]), n, h, ptr(ln.weight), ptr(ln.bias),
+                      LN_EPS, drop_p if train else 0.0, (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1),
+                      ptr(w.a[l]), ptr(w.mean[l]), ptr(w.rstd[l]), st)
+            x, ldx, kin = w.a[l], h, h
+        # a8: mlp_output + final Linear(2,1) + Sigmoid (architecture.py:345, 353-354)
+        _lib.call("ncf_head_fwd", ptr(x), n, hid[-1], ptr(m.mlp_output.weight),
+                  ptr(m.mlp_output.bias), ptr(w.mf_pred), ptr(m.final[0].weight),
+                  ptr(m.final[0].bias), ptr(w.mlp_pred), ptr(w.prob), st)
+        return w
+
+    def check_ids(self, w: Workspace):
+        if int(w.err.item()):
+            raise IndexError("AdvancedNCF: user/product id out of range of the embedding tables")
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, w: Workspace, uid, iid, grad_prob: Optional[torch.Tensor],
+                 targets: Optional[torch.Tensor], drop_p: float, seed: int):
+        """Gradients of every used parameter.  Dense grads land in the flat grad buffer; table
+        grads stay compact (self.pending) for the fused Adam step."""
+        m = self.model
+        g = w.g
+        n, D, H, M, hid = g.n, g.D, g.H, g.M, g.hidden
+        dev = w.prob.device
+        st = _lib.stream_ptr(dev)
+        uid = uid.to(device=dev, dtype=torch.int64).contiguous()
+        iid = iid.to(device=dev, dtype=torch.int64).contiguous()
+        gv = self.grad_view
+        # a12 + a8 backward (trainer.py:271; architecture.py:245-252)
+        gp = None if grad_prob is None else grad_prob.reshape(-1).to(torch.float32).contiguous()
+        tg = None if targets is None else targets.reshape(-1).to(device=dev, dtype=torch.float32).contiguous()
+        _lib.call("ncf_head_bwd", ptr(w.prob), ptr(gp), ptr(tg), ptr(w.mf_pred), ptr(w.mlp_pred),
+                  ptr(w.a[-1]), n, hid[-1], ptr(m.mlp_output.weight), ptr(m.final[0].weight),
+                  ptr(w.umf), ptr(w.imf), D, ptr(m.mf_output.weight), ptr(w.da[-1]), ptr(w.dumf),
+                  ptr(w.dimf), ptr(gv("mlp_output.weight")), ptr(gv("mlp_output.bias")),
+                  ptr(gv("mf_output.weight")), ptr(gv("mf_output.bias")),
+                  ptr(gv("final.0.weight")), ptr(gv("final.0.bias")), ptr(w.loss),
+                  ptr(w.scratch), w.scratch.numel(), st)
+        # a7 backward, last layer first
+        for l in reversed(range(len(hid))):
+            h = hid[l]
+            lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
+            _lib.call("ncf_relu_ln_dropout_bwd", ptr(w.da[l]), ptr(w.r[l]), ptr(w.mean[l]),
+                      ptr(w.rstd[l]), ptr(ln.weight), n, h, drop_p,
+                      (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1), ptr(w.dlin[l]),
+                      ptr(gv(f"mlp.{4 * l + 2}.weight")), ptr(gv(f"mlp.{4 * l + 2}.bias")),
+                      ptr(w.scratch), w.scratch.numel(), st)
+            xin, kin = (w.y, D) if l == 0 else (w.a[l - 1], hid[l - 1])
+            ldw = lin.weight.shape[1]
+            dW = gv(f"mlp.{4 * l}.weight")
+            self._wgrad(w, w.dlin[l], h, xin, kin, dW, ldw, h, kin, n, st)
+            if ldw > kin:  # zero temporal columns of mlp.0 (their input is all-zero)
+                _lib.call("ncf_fill_2d", ptr(dW[:, kin:]), h, ldw - kin, ldw, 0.0, st)
+            self._colsum(w, w.dlin[l], n, h, gv(f"mlp.{4 * l}.bias"), st)
+            dx = w.dy if l == 0 else w.da[l - 1]
+            self._gemm(w.dlin[l], h, 0, lin.weight, ldw, 0, dx, kin, n, kin, h, st=st)
+        # a5 backward: out_proj, core, q/k/v projections
+        att = m.user_product_attention
+        src = w.o
+        self._wgrad(w, w.dy, D, src, D, gv("user_product_attention.out_proj.weight"), D, D, D, n, st)
+        self._colsum(w, w.dy, n, D, gv("user_product_attention.out_proj.bias"), st)
+        self._gemm(w.dy, D, 0, att.out_proj.weight, D, 0, w.do, D, n, D, D, st=st)
+        _lib.call("ncf_attention_bwd", ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P), ptr(w.do), n // M, M,
+                  H, D, drop_p, seed, ptr(w.dS), ptr(w.dq), ptr(w.dk), ptr(w.dv), st)
+        for nm, dX, X in (("q_proj", w.dq, w.xu), ("k_proj", w.dk, w.xi), ("v_proj", w.dv, w.xi)):
+            self._wgrad(w, dX, D, X, D, gv(f"user_product_attention.{nm}.weight"), D, D, D, n, st)
+            self._colsum(w, dX, n, D, gv(f"user_product_attention.{nm}.bias"), st)
+        self._gemm(w.dq, D, 0, att.q_proj.weight, D, 0, w.dxu, D, n, D, D, st=st)
+        self._gemm(w.dk, D, 0, att.k_proj.weight, D, 0, w.dxi, D, n, D, D, st=st)
+        self._gemm(w.dv, D, 0, att.v_proj.weight, D, 0, w.dxi, D, n, D, D, accum=True, st=st)
+        # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)
+        tb = self.table_params()
+        G = w.G
+        _lib.call("ncf_embedding_bwd", ptr(uid), ptr(iid), n, D, m.num_users, m.num_products,
+                  ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), ptr(tb["mf_user"]),
+                  ptr(tb["mlp_user"]), ptr(tb["mf_item"]), ptr(tb["mlp_item"]),
+                  ptr(m.mf_norm.weight), ptr(m.mlp_norm.weight), LN_EPS, ptr(G["mf_user"]),
+                  ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(w.uniq_u),
+                  ptr(w.uniq_i), ptr(self.slot_u), ptr(self.slot_i), ptr(w.num_unique),
+                  ptr(gv("mf_norm.weight")), ptr(gv("mf_norm.bias")), ptr(gv("mlp_norm.weight")),
+                  ptr(gv("mlp_norm.bias")), ptr(w.emb_ws), w.emb_ws.numel(), st)
+        self.pending = w
+
+    # ------------------------------------------------------------------ optimizer
+    def table_state_tensors(self):
+        return self.table_params()
+
+    def adam_tables(self, hp_for, state_for, step: float, st):
+        """Dense-exact Adam over the four tables using the pending compact grads."""
+        w = self.pending
+        tb = self.table_params()
+        D = self.model.mlp_embedding_dim
+        for key, p in tb.items():
+            if w is None and p.grad is None:
+                continue  # torch.optim.Adam skips parameters whose grad is None
+            lr, b1, b2, eps, wd = hp_for(p)
+            s = state_for(p)
+            if w is None:
+                # dense gradient present (materialised / user-provided): elementwise Adam
+                g = p.grad.contiguous()
+                _lib.call("ncf_adam_flat", ptr(p), ptr(g), ptr(s["exp_avg"]),
+                          ptr(s["exp_avg_sq"]), p.numel(), lr, b1, b2, eps, wd, step, st)
+                continue
+            kind = 0 if key.endswith("user") else 1
+            slot = self.slot_u if kind == 0 else self.slot_i
+            ev = self.timing.get(key) if self.timing else None
+            if ev:
+                ev[0].record()
+            _lib.call("ncf_adam_table", ptr(p), ptr(s["exp_avg"]), ptr(s["exp_avg_sq"]),
+                      p.shape[0], D, ptr(slot), ptr(w.G[key]), lr, b1, b2, eps, wd, step, st)
+            if ev:
+                ev[1].record()
+        self.release_pending(st)
+
+    def release_pending(self, st):
+        w = self.pending
+        if w is None:
+            return
+        n = w.g.n
+        _lib.call("ncf_slot_reset", ptr(w.uniq_u), ptr(w.num_unique), 0, ptr(self.slot_u), n, st)
+        _lib.call("ncf_slot_reset", ptr(w.uniq_i), ptr(w.num_unique), 1, ptr(self.slot_i), n, st)
+        self.pending = None
+
+    def materialize_table_grads(self):
+        """Write dense [rows, D] gradients into the tables' .grad (for optimizers other than
+        the fused Adam, or for inspection), then release the compact buffers."""
+        w = self.pending
+        if w is None:
+            return
+        st = _lib.stream_ptr(w.prob.device)
+        D = self.model.mlp_embedding_dim
+        for key, p in self.table_params().items():
+            kind = 0 if key.endswith("user") else 1
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            else:
+                p.grad.zero_()
+            _lib.call("ncf_scatter_compact_rows", ptr(p.grad), D,
+                      ptr(w.uniq_u if kind == 0 else w.uniq_i), ptr(w.num_unique), kind,
+                      ptr(w.G[key]), w.g.n, st)
+        self.release_pending(st)

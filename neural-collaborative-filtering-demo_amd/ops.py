@@ -1,0 +1,171 @@
+"""Standalone HIP ops for the modules that also exist outside the fused AdvancedNCF step:
+MultiHeadAttention (any group length <= 64), TemporalEncoding and CategoryHierarchy.
+
+They mirror the reference modules' forward semantics (src/model/architecture.py:35-57, :86-94,
+:111-119) and run on the same kernels as the engine (MFMA projections + attention core), with
+autograd support for MultiHeadAttention and TemporalEncoding.  GPU only.
+"""
+import torch
+
+from . import _lib
+from ._lib import ptr
+from .engine import LN_EPS
+from .sparse import gather_rows
+
+
+def _require_cuda(t):
+    if not t.is_cuda:
+        raise RuntimeError("ncf_amd ops run on the MI355X only (no CPU fallback)")
+
+
+def _gemm(A, lda, a_t, B, ldb, b_t, C, ldc, M, N, K, bias=None, accum=False):
+    _lib.call("ncf_gemm_f32", M, N, K, ptr(A), lda, int(a_t), ptr(B), ldb, int(b_t), ptr(C), ldc,
+              ptr(bias), 2 if accum else 0, _lib.stream_ptr(C.device))
+
+
+def _wgrad(dY, X, dW, n, m_out, k_in):
+    s = max(1, min(256, (n + 63) // 64))
+    ws = torch.empty(_lib.query("ncf_gemm_splitk_workspace", m_out, k_in, s), device=dY.device)
+    _lib.call("ncf_gemm_f32_splitk", m_out, k_in, n, ptr(dY), m_out, 1, ptr(X), k_in, 0, ptr(dW),
+              k_in, 0, s, ptr(ws), ws.numel(), _lib.stream_ptr(dY.device))
+
+
+def _colsum(X, rows, cols, out):
+    ws = torch.empty(max(1, _lib.query("ncf_colsum_workspace", rows, cols)), device=X.device)
+    _lib.call("ncf_colsum", ptr(X), rows, cols, cols, ptr(out), 0, ptr(ws), ws.numel(),
+              _lib.stream_ptr(X.device))
+
+
+class _MHAFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mod, drop_p, seed, q_in, k_in, v_in, wq, bq, wk, bk, wv, bv, wo, bo):
+        Bn, L, D = q_in.shape
+        H = mod.num_heads
+        n = Bn * L
+        dev = q_in.device
+        xq, xk, xv = (t.reshape(n, D).contiguous().float() for t in (q_in, k_in, v_in))
+        q, k, v, o, y = (torch.empty(n, D, device=dev) for _ in range(5))
+        P = torch.empty(Bn * H * L * L, device=dev)
+        _gemm(xq, D, 0, wq, D, 1, q, D, n, D, D, bq)
+        _gemm(xk, D, 0, wk, D, 1, k, D, n, D, D, bk)
+        _gemm(xv, D, 0, wv, D, 1, v, D, n, D, D, bv)
+        _lib.call("ncf_attention_fwd", ptr(q), ptr(k), ptr(v), Bn, L, H, D, drop_p, seed, ptr(P),
+                  ptr(o), _lib.stream_ptr(dev))
+        _gemm(o, D, 0, wo, D, 1, y, D, n, D, D, bo)
+        ctx.save_for_backward(xq, xk, xv, q, k, v, P, o, wq, wk, wv, wo)
+        ctx.meta = (Bn, L, D, H, drop_p, seed)
+        return y.view(Bn, L, D)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xq, xk, xv, q, k, v, P, o, wq, wk, wv, wo = ctx.saved_tensors
+        Bn, L, D, H, drop_p, seed = ctx.meta
+        n = Bn * L
+        dev = gy.device
+        dy = gy.reshape(n, D).contiguous().float()
+        g = {nm: torch.empty(D, D, device=dev) for nm in ("wq", "wk", "wv", "wo")}
+        gb = {nm: torch.empty(D, device=dev) for nm in ("bq", "bk", "bv", "bo")}
+        _wgrad(dy, o, g["wo"], n, D, D)
+        _colsum(dy, n, D, gb["bo"])
+        do = torch.empty(n, D, device=dev)
+        _gemm(dy, D, 0, wo, D, 0, do, D, n, D, D)
+        dS = torch.empty(Bn * H * L * L, device=dev)
+        dq, dk, dv = (torch.empty(n, D, device=dev) for _ in range(3))
+        _lib.call("ncf_attention_bwd", ptr(q), ptr(k), ptr(v), ptr(P), ptr(do), Bn, L, H, D,
+                  drop_p, seed, ptr(dS), ptr(dq), ptr(dk), ptr(dv), _lib.stream_ptr(dev))
+        outs = []
+        for dX, X, W, wn, bn in ((dq, xq, wq, "wq", "bq"), (dk, xk, wk, "wk", "bk"),
+                                 (dv, xv, wv, "wv", "bv")):
+            _wgrad(dX, X, g[wn], n, D, D)
+            _colsum(dX, n, D, gb[bn])
+            gx = torch.empty(n, D, device=dev)
+            _gemm(dX, D, 0, W, D, 0, gx, D, n, D, D)
+            outs.append(gx.view(Bn, L, D))
+        return (None, None, None, outs[0], outs[1], outs[2], g["wq"], gb["bq"], g["wk"], gb["bk"],
+                g["wv"], gb["bv"], g["wo"], gb["bo"])
+
+
+def mha_forward(mod, query, key, value, mask=None):
+    """MultiHeadAttention.forward (architecture.py:35-57): query/key/value [B, L, D] (a 2-D
+    [B, D] input is a length-1 sequence, as the reference's .view(batch, -1, H, hd) makes it)."""
+    if mask is not None:
+        raise NotImplementedError("attention mask is never passed on the reference path")
+    _require_cuda(query)
+    squeeze = query.dim() == 2
+    if squeeze:
+        query, key, value = query.unsqueeze(1), key.unsqueeze(1), value.unsqueeze(1)
+    drop_p = float(mod.dropout.p) if mod.training else 0.0
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0 else 0
+    y = _MHAFunction.apply(mod, drop_p, seed, query, key, value, mod.q_proj.weight, mod.q_proj.bias,
+                           mod.k_proj.weight, mod.k_proj.bias, mod.v_proj.weight, mod.v_proj.bias,
+                           mod.out_proj.weight, mod.out_proj.bias)
+    return y.squeeze(1) if squeeze else y
+
+
+class _TemporalFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mod, hour, day, month, days_since, wh, wd, wm):
+        dev = wh.device
+        n = hour.numel()
+        T = mod.embed_dim
+        ids = [t.reshape(-1).to(device=dev, dtype=torch.int64).contiguous()
+               for t in (hour, day, month, days_since)]
+        out = torch.empty(n, T, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.call("ncf_temporal_fwd", *[ptr(t) for t in ids], n, ptr(wh), ptr(wd), ptr(wm),
+                  ptr(mod.pe), mod.max_period, T, ptr(out), ptr(err), _lib.stream_ptr(dev))
+        if int(err.item()):
+            raise IndexError("TemporalEncoding: hour/day/month index out of range")
+        ctx.save_for_backward(*ids[:3])
+        ctx.T = T
+        return out.view(*hour.shape, T)
+
+    @staticmethod
+    def backward(ctx, gy):
+        h, d, m = ctx.saved_tensors
+        T = ctx.T
+        dev = gy.device
+        gh, gd, gm = torch.empty(24, T, device=dev), torch.empty(7, T, device=dev), torch.empty(12, T, device=dev)
+        g = gy.reshape(-1, T).contiguous().float()
+        _lib.call("ncf_temporal_bwd", ptr(h), ptr(d), ptr(m), h.numel(), ptr(g), T, ptr(gh), ptr(gd),
+                  ptr(gm), _lib.stream_ptr(dev))
+        return None, None, None, None, None, gh, gd, gm
+
+
+def temporal_encoding_forward(mod, hour, day, month, days_since):
+    _require_cuda(mod.hour_embed.weight)
+    return _TemporalFunction.apply(mod, hour, day, month, days_since, mod.hour_embed.weight,
+                                   mod.day_embed.weight, mod.month_embed.weight)
+
+
+def category_hierarchy_forward(mod, department_ids, category_ids):
+    """CategoryHierarchy.forward (architecture.py:111-119) for 1-D id vectors: the attention
+    sees one key per query, so softmax == 1 and attn = out_proj(v_proj(dept)); then
+    LayerNorm(attn + cat).  Inference path (get_product_embeddings)."""
+    w = mod.department_embed.weight
+    _require_cuda(w)
+    if torch.is_grad_enabled() and w.requires_grad:
+        with torch.no_grad():
+            return category_hierarchy_forward(mod, department_ids, category_ids)
+    if mod.training and mod.dropout.p > 0:
+        raise NotImplementedError("CategoryHierarchy in training mode is not on the accelerated path")
+    dev = w.device
+    dept = gather_rows(w, department_ids.reshape(-1))
+    n, D = dept.shape
+    h = gather_rows(mod.category_embed.weight, category_ids.reshape(-1))      # residual (cat)
+    att = mod.hierarchy_attn
+    v = torch.empty(n, D, device=dev)
+    _gemm(dept, D, 0, att.v_proj.weight, D, 1, v, D, n, D, D, att.v_proj.bias)
+    _gemm(v, D, 0, att.out_proj.weight, D, 1, h, D, n, D, D, att.out_proj.bias, accum=True)
+    out = torch.empty(n, D, device=dev)
+    mean, rstd = torch.empty(n, device=dev), torch.empty(n, device=dev)
+    _lib.call("ncf_relu_ln_dropout_fwd", ptr(h), n, D, ptr(mod.norm.weight), ptr(mod.norm.bias),
+              LN_EPS, 0.0, 0, ptr(out), ptr(mean), ptr(rstd), _lib.stream_ptr(dev))
+    return out
+
+
+def forward_simple_hour(model, user_ids, product_ids, hour):
+    raise NotImplementedError(
+        "forward_simple(hour=...) builds a fresh randomly-initialised nn.Linear on every call in "
+        "the reference (architecture.py:436-442), so it has no reproducible result; only "
+        "hour=None is on the accelerated scoring path")

@@ -1,0 +1,126 @@
+"""CPU-only checks: the C-ABI library loads and exports every symbol include/ncf_hip.h declares
+(no compute calls without a GPU), the ctypes table matches the header, and the host-side mirror of
+the reference surface (state_dict keys, constructor, KJT) behaves like the reference."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+import _ncf_pkg
+from tests.conftest import ROOT, sub
+
+ncf = _ncf_pkg.load()
+from ncf_amd import _lib  # noqa: E402
+
+HEADER = os.path.join(ROOT, "include", "ncf_hip.h")
+
+
+def header_decls():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    decls = {}
+    for m in re.finditer(r"^\s*([A-Za-z_][\w\s\*]*?)\b(ncf_\w+)\s*\(([^;]*?)\)\s*;", src, re.M | re.S):
+        args = [a.strip() for a in m.group(3).split(",") if a.strip() and a.strip() != "void"]
+        decls[m.group(2)] = args
+    return decls
+
+
+def test_header_matches_ctypes_table():
+    decls = header_decls()
+    assert decls, "no declarations parsed"
+    assert set(decls) == set(_lib.SIGNATURES), set(decls) ^ set(_lib.SIGNATURES)
+    for name, args in decls.items():
+        assert len(args) == len(_lib.SIGNATURES[name][1]), name
+
+
+def test_library_exports_every_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        subprocess.run(["bash", os.path.join(ROOT, "build_ext.sh")], check=True)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    syms = {l.split()[-1] for l in out.splitlines() if l.strip()}
+    missing = set(header_decls()) - syms
+    assert not missing, missing
+    lib = _lib.load()
+    assert lib.ncf_version() == 10000
+    assert lib.ncf_last_error() is not None
+    # workspace queries are pure host arithmetic
+    assert _lib.query("ncf_gemm_splitk_workspace", 256, 64, 4) == 4 * 256 * 64
+    assert _lib.query("ncf_embedding_bwd_workspace", 20480, 64) > 0
+
+
+def test_code_object_is_gfx950():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", _lib.LIB_PATH],
+                         capture_output=True, text=True)
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob or "gfx950" in out.stdout
+
+
+def test_state_dict_keys_and_strict_load(f1):
+    m = ncf.AdvancedNCF(8031, 366, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.2, 4)
+    keys = list(m.state_dict().keys())
+    gold = list(sub(f1, "sd/").keys())
+    assert keys == gold and len(keys) == 62
+    sd = {k: torch.from_numpy(v) for k, v in sub(f1, "sd/").items()}
+    m2 = ncf.AdvancedNCF(int(f1["cfg"][0]), int(f1["cfg"][1]), 5, 24)
+    m2.load_state_dict(sd, strict=True)
+    for k, v in m2.state_dict().items():
+        assert torch.equal(v, sd[k]), k
+    # dense params are views into one flat buffer and survive load_state_dict
+    eng = m2.engine
+    assert all(eng.is_flat_view(p) for _, p in eng.dense_params())
+
+
+def test_attribute_surface():
+    m = ncf.AdvancedNCF(100, 50, 5, 24)
+    # attributes read by trainer.py:567-569, generate_embeddings.py:100-104, app.py:156-184
+    for a in ("num_users", "num_products", "mf_embedding_dim", "num_categories",
+              "num_departments", "num_heads", "temporal_dim", "negative_samples"):
+        assert hasattr(m, a)
+    assert m.user_product_attention.scale == pytest.approx(4.0)
+    assert tuple(m.final[0].weight.shape) == (1, 2)
+    assert hasattr(m.user_product_attention, "q_proj") and hasattr(m.user_product_attention, "k_proj")
+    assert tuple(m.temporal_encoding.hour_embed.weight.shape) == (24, 32)
+    assert isinstance(m.mlp_norm, torch.nn.LayerNorm)
+
+
+def test_cpu_forward_fails_loudly():
+    m = ncf.AdvancedNCF(10, 10, 5, 24)
+    kjt = ncf.KeyedJaggedTensor.from_lengths_sync(
+        keys=["user_id", "product_id"], values=torch.tensor([1, 2, 3, 4]),
+        lengths=torch.ones(4, dtype=torch.long))
+    m.eval()
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(kjt)
+
+
+def test_kjt_surface():
+    KJT = ncf.KeyedJaggedTensor
+    v = torch.tensor([5, 6, 7, 1, 2, 3])
+    k = KJT.from_lengths_sync(keys=["user_id", "product_id"], values=v,
+                              lengths=torch.ones(6, dtype=torch.long))
+    assert k.keys() == ["user_id", "product_id"]
+    d = k.single_id_split()
+    assert d["user_id"].tolist() == [5, 6, 7] and d["product_id"].tolist() == [1, 2, 3]
+    td = k.to_dict()
+    assert td["product_id"].values().tolist() == [1, 2, 3]
+    assert k.offsets().tolist() == [0, 1, 2, 3, 4, 5, 6]
+    # generate_embeddings.py:107-112 builds it with explicit offsets
+    k2 = KJT(keys=["user_id", "product_id"], values=torch.tensor([0, 9]),
+             lengths=torch.tensor([1, 1]), offsets=torch.tensor([0, 1, 2]))
+    assert k2.single_id_split()["product_id"].tolist() == [9]
+    bad = KJT.from_lengths_sync(keys=["user_id", "product_id"], values=torch.tensor([1, 2, 3, 4]),
+                                lengths=torch.tensor([2, 0, 1, 1]))
+    with pytest.raises(NotImplementedError):
+        bad.single_id_split()
+
+
+def test_to_keeps_flat_layout():
+    m = ncf.AdvancedNCF(10, 10, 5, 24)
+    w0 = m.mlp[0].weight.detach().clone()
+    m = m.double().float()
+    assert torch.equal(m.mlp[0].weight.detach(), w0.float())
+    assert all(m.engine.is_flat_view(p) for _, p in m.engine.dense_params())

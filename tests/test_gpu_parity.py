@@ -1,0 +1,396 @@
+"""GPU parity: the HIP path (through the C-ABI library) against the reference's golden vectors
+and the CPU oracle.  Runs on a real MI355X only (marker ``gpu``).
+
+Tolerances (tests/parity.py): fp32 forward abs <= 2e-6 on probabilities; gradients
+rel 1e-4 / abs 1e-6 (summation order differs from ATen's CPU kernels); post-Adam parameters abs
+1e-6 outside the sign-flip zone (<= 2*lr per step inside it)."""
+import numpy as np
+import pytest
+import torch
+
+import _ncf_pkg
+from oracle import ncf_oracle as O
+from tests.conftest import sub
+from tests.parity import assert_moment_close, assert_params_close
+
+pytestmark = pytest.mark.gpu
+ncf = _ncf_pkg.load()
+DEV = torch.device("cuda:0")
+
+
+def kjt(u, i):
+    u = torch.as_tensor(u, dtype=torch.long)
+    i = torch.as_tensor(i, dtype=torch.long)
+    return ncf.KeyedJaggedTensor.from_lengths_sync(
+        keys=["user_id", "product_id"], values=torch.cat([u, i]),
+        lengths=torch.ones(2 * u.numel(), dtype=torch.long)).to(DEV)
+
+
+def T(d):
+    return {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in d.items()}
+
+
+# ----------------------------------------------------------------------------- F1
+def test_f1_eval_known_answer(f1):
+    sd = T(sub(f1, "sd/"))
+    m = ncf.AdvancedNCF(int(f1["cfg"][0]), int(f1["cfg"][1]), 5, 24).to(DEV)
+    m.load_state_dict(sd, strict=True)
+    m.eval()
+    with torch.no_grad():
+        out = m(kjt(f1["user_ids"], f1["item_ids"])).cpu().numpy().reshape(-1)
+        # batches of 32 like local_inference.py:121-129
+        outb = np.concatenate([m(kjt(f1["user_ids"][s:s + 32], f1["item_ids"][s:s + 32]))
+                               .cpu().numpy().reshape(-1) for s in range(0, 1000, 32)])
+    assert np.abs(out - f1["csv_pred"]).max() < 2e-6
+    assert np.abs(out - f1["ref_pred"]).max() < 2e-6
+    assert np.array_equal(out, outb)
+
+
+# ----------------------------------------------------------------------------- F2/F3
+def _train_run(g, n_layers, materialize_step0):
+    U, I, D, Tt, H, B, M, steps = [int(x) for x in g["cfg"]]
+    hidden = [int(x) for x in g["hidden"]]
+    lr, wd = [float(x) for x in g["hparams"]]
+    m = ncf.AdvancedNCF(U, I, 5, 24, D, D, Tt, hidden, H, 0.0, M - 1)
+    m.load_state_dict(T(sub(g, "init/")), strict=True)
+    m = m.to(DEV)
+    opt = torch.optim.Adam(m.parameters(), lr=lr, weight_decay=wd)
+    crit = torch.nn.BCELoss()
+    rec = {}
+    for s in range(steps):
+        m.train()
+        out = m(kjt(g[f"step{s}/user_ids"], g[f"step{s}/item_ids"]))
+        loss = crit(out, torch.from_numpy(g[f"step{s}/targets"]).to(DEV))
+        opt.zero_grad()
+        loss.backward()
+        rec[f"prob{s}"] = out.detach().cpu().numpy()
+        rec[f"loss{s}"] = loss.item()
+        if s == 0 and materialize_step0:
+            m.engine.materialize_table_grads()
+            rec["grads0"] = {n: p.grad.detach().cpu().numpy().copy()
+                             for n, p in m.named_parameters() if p.grad is not None}
+        opt.step()
+        if s in (0, steps - 1):
+            rec[f"params{s}"] = {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()}
+    rec["state"] = {n: {k: (v.detach().cpu().numpy() if torch.is_tensor(v) else v)
+                        for k, v in opt.state[p].items()}
+                    for n, p in m.named_parameters() if p in opt.state}
+    rec["model"] = m
+    return rec
+
+
+@pytest.mark.parametrize("fx,nl", [("f2", 3), ("f3", 2)])
+@pytest.mark.parametrize("materialize", [False, True])
+def test_train_goldens(fx, nl, materialize, request):
+    g = request.getfixturevalue(fx)
+    steps = int(g["cfg"][7])
+    lr, wd = [float(x) for x in g["hparams"]]
+    rec = _train_run(g, nl, materialize)
+    for s in range(steps):
+        assert np.abs(rec[f"prob{s}"] - g[f"step{s}/prob"]).max() < 2e-6, s
+        assert abs(rec[f"loss{s}"] - float(g[f"step{s}/loss"])) < 2e-6, s
+    if materialize:
+        gold = sub(g, "grad0/")
+        got = rec["grads0"]
+        assert set(got) == set(gold), set(got) ^ set(gold)
+        for k, v in gold.items():
+            np.testing.assert_allclose(got[k], v, rtol=1e-4, atol=1e-6, err_msg=k)
+    for s in (0, steps - 1):
+        for k, v in sub(g, f"after{s}/param/").items():
+            geff = g["grad0/" + k] + wd * g["init/" + k]
+            assert_params_close(k, rec[f"params{s}"][k], v, geff, lr, s + 1)
+    # unused parameters (grad None in the reference) never move
+    for k in g["grad_none0"].tolist():
+        assert np.array_equal(rec[f"params{steps - 1}"][k], g["init/" + k]), k
+    for k, v in sub(g, f"after{steps - 1}/exp_avg/").items():
+        geff = g["grad0/" + k] + wd * g["init/" + k]
+        assert_moment_close(k, rec["state"][k]["exp_avg"], v, geff)
+        assert_moment_close(k, rec["state"][k]["exp_avg_sq"], g[f"after{steps - 1}/exp_avg_sq/" + k],
+                            geff, atol=1e-12)
+        assert float(rec["state"][k]["step"]) == steps
+    # eval forward on the trained weights (M = 1) and forward_simple
+    m = rec["model"]
+    m.eval()
+    with torch.no_grad():
+        ev = m(kjt(g["eval/user_ids"], g["eval/item_ids"])).cpu().numpy()
+        fs = m.forward_simple(torch.from_numpy(g["eval/user_ids"]).to(DEV),
+                              torch.from_numpy(g["eval/item_ids"]).to(DEV)).cpu().numpy()
+    assert np.abs(ev - g["eval/prob"]).max() < 1e-4
+    assert np.abs(fs - g["eval/simple"]).max() < 1e-4
+
+
+def test_train_deterministic(f2):
+    a = _train_run(f2, 3, False)
+    b = _train_run(f2, 3, False)
+    for k, v in a["params2"].items():
+        assert np.array_equal(v, b["params2"][k]), k
+
+
+# ----------------------------------------------------------------------------- larger vs oracle
+@pytest.mark.parametrize("U,I,D,H,hidden,B,M", [
+    (5000, 1000, 64, 4, [256, 128, 64], 256, 5),
+    (943, 1682, 16, 1, [64, 32], 256, 5),       # C1 shape (ML-100K)
+    (3000, 700, 128, 4, [256, 128, 64], 64, 5),  # C4 dims (hd = 32)
+])
+def test_train_vs_oracle(U, I, D, H, hidden, B, M):
+    torch.manual_seed(3)
+    m = ncf.AdvancedNCF(U, I, 5, 24, D, D, 32, hidden, H, 0.0, M - 1)
+    ref = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(DEV)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+    oopt = O.AdamState(lr=1e-3, weight_decay=1e-5)
+    gen = torch.Generator().manual_seed(4)
+    for step in range(2):
+        # Zipf-ish items (hot ids repeat many times) exercise long segments
+        users = torch.randint(0, U, (B,), generator=gen).repeat_interleave(M)
+        items = (torch.rand(B * M, generator=gen) ** 3 * I).long().clamp_max(I - 1)
+        t = torch.zeros(B, M)
+        t[:, 0] = 1
+        t = t.reshape(-1, 1)
+        m.train()
+        out = m(kjt(users, items))
+        loss = torch.nn.functional.binary_cross_entropy(out, t.to(DEV))
+        opt.zero_grad()
+        loss.backward()
+        if step == 0:
+            m.engine.materialize_table_grads()
+            grads = {n: p.grad.detach().cpu() for n, p in m.named_parameters() if p.grad is not None}
+        opt.step()
+        prob, oloss, ograds = O.train_step(ref, oopt, users, items, t, negative_samples=M - 1,
+                                           num_heads=H, temporal_dim=32, n_layers=len(hidden))
+        assert (out.detach().cpu() - prob).abs().max().item() < 5e-6
+        assert abs(loss.item() - float(oloss)) < 5e-6
+        if step == 0:
+            for k, v in ograds.items():
+                np.testing.assert_allclose(grads[k].numpy(), v.numpy(), rtol=2e-4, atol=2e-6,
+                                           err_msg=k)
+            g0 = {k: (ograds[k] + 1e-5 * v).numpy() for k, v in ref.items() if k in ograds}
+    sd = m.state_dict()
+    for k, g in g0.items():
+        assert_params_close(k, sd[k].cpu().numpy(), ref[k].numpy(), g, 1e-3, 2, atol=5e-6)
+
+
+# ----------------------------------------------------------------------------- op level (F4)
+@pytest.mark.parametrize("tag", ["mha5", "mha50", "mha5_h1"])
+def test_f4_mha(f4, tag):
+    Bn, L, D, H = [int(x) for x in f4[f"{tag}/shape"]]
+    mod = ncf.MultiHeadAttention(D, H, dropout=0.0)
+    mod.load_state_dict(T(sub(f4, f"{tag}/w/")))
+    mod = mod.to(DEV)
+    q, k, v = [torch.from_numpy(f4[f"{tag}/{n}"]).to(DEV).requires_grad_(True) for n in "qkv"]
+    y = mod(q, k, v)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), f4[f"{tag}/y"], atol=2e-5, rtol=1e-5)
+    y.backward(torch.from_numpy(f4[f"{tag}/gy"]).to(DEV))
+    for n, t in zip("qkv", (q, k, v)):
+        np.testing.assert_allclose(t.grad.cpu().numpy(), f4[f"{tag}/g{n}"], atol=2e-5, rtol=1e-4)
+    for n, p in mod.named_parameters():
+        np.testing.assert_allclose(p.grad.cpu().numpy(), f4[f"{tag}/gw/{n}"], atol=5e-5, rtol=1e-4,
+                                   err_msg=n)
+
+
+def test_f4_temporal(f4):
+    te = ncf.TemporalEncoding(32)
+    te.load_state_dict({**T(sub(f4, "te/w/")), "pe": torch.from_numpy(f4["te/pe"])})
+    te = te.to(DEV)
+    args = [torch.from_numpy(f4[f"te/{n}"]).to(DEV) for n in ("hour", "day", "month", "days_since")]
+    y = te(*args)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), f4["te/y"], atol=1e-6)
+    y.backward(torch.from_numpy(f4["te/gy"]).to(DEV))
+    for n in ("hour_embed.weight", "day_embed.weight", "month_embed.weight"):
+        mod = getattr(te, n.split(".")[0])
+        np.testing.assert_allclose(mod.weight.grad.cpu().numpy(), f4["te/gw/" + n], atol=1e-5,
+                                   rtol=1e-5)
+
+
+# ----------------------------------------------------------------------------- scoring (F5)
+def test_f5_scoring_and_embeddings(f5):
+    sd = T(sub(f5, "sd/"))
+    nu = sd["mf_embedding_collection.embedding_bags.user_id.weight"].shape[0]
+    m = ncf.AdvancedNCF(nu, 366, 5, 24).to(DEV)
+    m.load_state_dict(sd, strict=True)
+    m.eval()
+    items = torch.arange(366, device=DEV)
+    with torch.no_grad():
+        sc = torch.stack([m.forward_simple(torch.full_like(items, u), items) for u in range(nu)])
+        ts, ti = sc.topk(10, dim=1)
+        ue = m.get_user_embeddings({"user_features": kjt(torch.arange(nu), torch.zeros(nu))})
+        pid = torch.from_numpy(f5["emb_pids"])
+        pe = m.get_product_embeddings({
+            "product_features": kjt(torch.zeros_like(pid), pid),
+            "category_features": {"department_ids": torch.from_numpy(f5["emb_dept"]).to(DEV),
+                                  "category_ids": torch.from_numpy(f5["emb_cat"]).to(DEV)}})
+    np.testing.assert_allclose(sc.cpu().numpy(), f5["scores"], atol=2e-6)
+    assert (ti.cpu().numpy() == f5["top_items"]).all()
+    np.testing.assert_allclose(ue["mf"].cpu().numpy(), f5["emb_user_mf"], atol=2e-6)
+    np.testing.assert_allclose(ue["mlp"].cpu().numpy(), f5["emb_user_mlp"], atol=2e-6)
+    np.testing.assert_allclose(pe["mf"].cpu().numpy(), f5["emb_item_mf"], atol=2e-6)
+    np.testing.assert_allclose(pe["mlp"].cpu().numpy(), f5["emb_item_mlp"], atol=2e-6)
+    np.testing.assert_allclose(pe["category"].cpu().numpy(), f5["emb_item_category"], atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- kernels vs torch
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("Mm,Nn,Kk", [(77, 130, 45), (256, 64, 1000), (1, 5, 3)])
+def test_gemm_vs_torch(a_t, b_t, Mm, Nn, Kk):
+    from ncf_amd import _lib
+    g = torch.Generator().manual_seed(Mm + Nn + Kk)
+    A = torch.randn(Mm, Kk, generator=g)
+    Bm = torch.randn(Kk, Nn, generator=g) * torch.arange(1, Nn + 1)  # asymmetric
+    bias = torch.randn(Nn, generator=g)
+    As = (A.t().contiguous() if a_t else A).to(DEV)
+    Bs = (Bm.t().contiguous() if b_t else Bm).to(DEV)
+    C = torch.empty(Mm, Nn, device=DEV)
+    _lib.call("ncf_gemm_f32", Mm, Nn, Kk, As.data_ptr(), Mm if a_t else Kk, a_t, Bs.data_ptr(),
+              Kk if b_t else Nn, b_t, C.data_ptr(), Nn, bias.to(DEV).data_ptr(), 1,
+              _lib.stream_ptr(DEV))
+    ref = torch.relu(A.double() @ Bm.double() + bias.double()).float()
+    np.testing.assert_allclose(C.cpu().numpy(), ref.numpy(), atol=1e-4 * (Kk ** 0.5), rtol=1e-4)
+    # split-K path
+    ws = torch.empty(_lib.query("ncf_gemm_splitk_workspace", Mm, Nn, 7), device=DEV)
+    C2 = torch.empty(Mm, Nn, device=DEV)
+    _lib.call("ncf_gemm_f32_splitk", Mm, Nn, Kk, As.data_ptr(), Mm if a_t else Kk, a_t,
+              Bs.data_ptr(), Kk if b_t else Nn, b_t, C2.data_ptr(), Nn, 0, 7, ws.data_ptr(),
+              ws.numel(), _lib.stream_ptr(DEV))
+    ref2 = (A.double() @ Bm.double()).float()
+    np.testing.assert_allclose(C2.cpu().numpy(), ref2.numpy(), atol=1e-4 * (Kk ** 0.5), rtol=1e-4)
+
+
+def test_embedding_bwd_segment_reduce():
+    """Sort + segment-reduce + LN backward against a torch fp64 index_add reference, with heavy
+    duplication (one id repeated 3000x), empty tables rows and 3 radix passes."""
+    from ncf_amd import _lib
+    n, D, U, I = 9000, 64, 300000, 70000
+    g = torch.Generator().manual_seed(5)
+    uid = torch.randint(0, U, (n,), generator=g)
+    uid[:3000] = 123456
+    iid = (torch.rand(n, generator=g) ** 4 * I).long()
+    tabs = {k: torch.randn(U if "u" in k else I, D, generator=g) * 0.1 for k in ("mfu", "mlpu", "mfi", "mlpi")}
+    dys = {k: torch.randn(n, D, generator=g) for k in ("mfu", "mlpu", "mfi", "mlpi")}
+    gm, gl = torch.randn(D, generator=g), torch.randn(D, generator=g)
+    d = {k: v.to(DEV) for k, v in {**tabs, **{"d" + k: v for k, v in dys.items()}}.items()}
+    G = {k: torch.zeros(n, D, device=DEV) for k in ("mfu", "mlpu", "mfi", "mlpi")}
+    uu = torch.empty(n, dtype=torch.int64, device=DEV)
+    ui = torch.empty(n, dtype=torch.int64, device=DEV)
+    su = torch.full((U,), -1, dtype=torch.int32, device=DEV)
+    si = torch.full((I,), -1, dtype=torch.int32, device=DEV)
+    nu = torch.zeros(2, dtype=torch.int32, device=DEV)
+    pg = [torch.empty(D, device=DEV) for _ in range(4)]
+    ws = torch.empty(_lib.query("ncf_embedding_bwd_workspace", n, D), dtype=torch.uint8, device=DEV)
+    ud, idd, gmd, gld = uid.to(DEV), iid.to(DEV), gm.to(DEV), gl.to(DEV)
+    P = lambda t: t.data_ptr()  # noqa: E731
+    _lib.call("ncf_embedding_bwd", P(ud), P(idd), n, D, U, I, P(d["dmfu"]), P(d["dmlpu"]),
+              P(d["dmfi"]), P(d["dmlpi"]), P(d["mfu"]), P(d["mlpu"]), P(d["mfi"]), P(d["mlpi"]),
+              P(gmd), P(gld), 1e-5, P(G["mfu"]), P(G["mlpu"]), P(G["mfi"]), P(G["mlpi"]), P(uu),
+              P(ui), P(su), P(si), P(nu), P(pg[0]), P(pg[1]), P(pg[2]), P(pg[3]), P(ws), ws.numel(),
+              _lib.stream_ptr(DEV))
+    torch.cuda.synchronize()
+    # reference: autograd through gather + LayerNorm in fp64
+    def ref(tab, ids, dy, gamma):
+        t = tab.double().requires_grad_(True)
+        gam = gamma.double().requires_grad_(True)
+        bet = torch.zeros(D, dtype=torch.float64, requires_grad=True)
+        y = torch.nn.functional.layer_norm(t[ids], (D,), gam, bet, 1e-5)
+        y.backward(dy.double())
+        return t.grad, gam.grad, bet.grad
+    nun = nu.cpu().tolist()
+    uq = torch.unique(uid)
+    iq = torch.unique(iid)
+    assert nun == [uq.numel(), iq.numel()]
+    assert torch.equal(uu[:nun[0]].cpu(), uq) and torch.equal(ui[:nun[1]].cpu(), iq)
+    assert torch.equal(su[uq.to(DEV)].cpu(), torch.arange(uq.numel(), dtype=torch.int32))
+    gsum = [torch.zeros(D, dtype=torch.float64) for _ in range(4)]
+    for k, ids, uniq, gi in (("mfu", uid, uq, 0), ("mlpu", uid, uq, 2), ("mfi", iid, iq, 0), ("mlpi", iid, iq, 2)):
+        gt, gg, gb = ref(tabs[k], ids, dys[k], gm if k.startswith("mf") and not k.startswith("mlp") else gl)
+        got = G[k][:uniq.numel()].cpu().double()
+        np.testing.assert_allclose(got.numpy(), gt[uniq].numpy(), rtol=1e-4, atol=1e-4, err_msg=k)
+        gsum[gi] += gg
+        gsum[gi + 1] += gb
+    for j in range(4):
+        np.testing.assert_allclose(pg[j].cpu().double().numpy(), gsum[j].numpy(), rtol=1e-4, atol=1e-3)
+    # slot reset restores the all -1 invariant
+    _lib.call("ncf_slot_reset", P(uu), P(nu), 0, P(su), n, _lib.stream_ptr(DEV))
+    _lib.call("ncf_slot_reset", P(ui), P(nu), 1, P(si), n, _lib.stream_ptr(DEV))
+    assert int((su != -1).sum()) == 0 and int((si != -1).sum()) == 0
+
+
+def test_adam_table_kernel_matches_torch():
+    from ncf_amd import _lib
+    rows, D = 1000, 64
+    g = torch.Generator().manual_seed(9)
+    p0 = torch.randn(rows, D, generator=g)
+    touched = torch.tensor([3, 17, 999, 500])
+    grad = torch.zeros(rows, D)
+    Gc = torch.randn(4, D, generator=g)
+    grad[touched] = Gc
+    p_ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([p_ref], lr=1e-3, weight_decay=1e-5)
+    p = p0.clone().to(DEV)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    slot = torch.full((rows,), -1, dtype=torch.int32)
+    slot[touched] = torch.arange(4, dtype=torch.int32)
+    slot, Gd = slot.to(DEV), Gc.to(DEV)
+    for step in (1, 2, 3):
+        p_ref.grad = grad.clone()
+        opt.step()
+        _lib.call("ncf_adam_table", p.data_ptr(), m.data_ptr(), v.data_ptr(), rows, D,
+                  slot.data_ptr(), Gd.data_ptr(), 1e-3, 0.9, 0.999, 1e-8, 1e-5, float(step),
+                  _lib.stream_ptr(DEV))
+    np.testing.assert_allclose(p.cpu().numpy(), p_ref.detach().numpy(), atol=1e-6, rtol=0)
+    np.testing.assert_allclose(m.cpu().numpy(), opt.state[p_ref]["exp_avg"].numpy(), atol=1e-9, rtol=1e-5)
+
+
+# ----------------------------------------------------------------------------- behaviour
+def test_dropout_statistics():
+    torch.manual_seed(0)
+    m = ncf.AdvancedNCF(1000, 500, 5, 24, dropout=0.2).to(DEV)
+    n = 4096 * 5
+    u = torch.randint(0, 1000, (4096,)).repeat_interleave(5)
+    i = torch.randint(0, 500, (n,))
+    m.train()
+    k = kjt(u, i)
+    a = m(k).detach()
+    b = m(k).detach()
+    assert not torch.equal(a, b)             # fresh masks per forward
+    m.eval()
+    with torch.no_grad():
+        e1 = m(kjt(u[:100], i[:100]))
+        e2 = m(kjt(u[:100], i[:100]))
+    assert torch.equal(e1, e2)               # eval is deterministic
+    # keep rate of the MLP dropout: count exact zeros in a dropped LN output
+    w = m.engine.ws[(n, 5, True)]
+    frac = (w.a[0] == 0).float().mean().item()
+    assert abs(frac - 0.2) < 0.01, frac
+
+
+def test_out_of_range_id_raises():
+    m = ncf.AdvancedNCF(10, 10, 5, 24).to(DEV)
+    m.eval()
+    with pytest.raises(IndexError):
+        with torch.no_grad():
+            m(kjt([1, 2], [3, 10]))
+
+
+def test_batch_not_multiple_of_group():
+    m = ncf.AdvancedNCF(10, 10, 5, 24).to(DEV)
+    m.train()
+    with pytest.raises(RuntimeError, match="multiple"):
+        m(kjt([1, 2, 3], [3, 4, 5]))
+
+
+def test_non_adam_optimizer_gets_dense_table_grads(f2):
+    g = f2
+    U, I, D, Tt, H, B, M, steps = [int(x) for x in g["cfg"]]
+    m = ncf.AdvancedNCF(U, I, 5, 24, D, D, Tt, [256, 128, 64], H, 0.0, M - 1)
+    m.load_state_dict(T(sub(g, "init/")), strict=True)
+    m = m.to(DEV)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    m.train()
+    out = m(kjt(g["step0/user_ids"], g["step0/item_ids"]))
+    loss = torch.nn.BCELoss()(out, torch.from_numpy(g["step0/targets"]).to(DEV))
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
+    k = "mf_embedding_collection.embedding_bags.user_id.weight"
+    exp = g["init/" + k] - 0.1 * g["grad0/" + k]
+    np.testing.assert_allclose(m.state_dict()[k].cpu().numpy(), exp, atol=1e-6)

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Run GPU steps in order; each under its own time limit.  Stop at the first step whose exit
+# status is not 0/1 (fault, abort, segfault, timeout): nothing more touches the GPU after that.
+mkdir -p gpurun_out
+run() {  # run <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 30 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    test) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    testx) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    bench) run bench 900 python bench.py --steps 30 --warmup 5 ;;
+    benchfast) run bench 600 python bench.py --steps 30 --warmup 5 --no-cpu-baseline ;;
+    *) echo "unknown step $step" ;;
+  esac
+done
