@@ -30,6 +30,7 @@ import _ncf_pkg  # noqa: E402
 
 METRIC = "train samples/sec + infer pairs/sec, 1M×100K d=64 AdvancedNCF @1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0
+FP32_MFMA_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA = the f32 vector rate
 
 
 def zipf_sampler(n_items, s, device):
@@ -130,23 +131,17 @@ def main():
         u, i, t = batches[s % len(batches)]
         step(u, i, t)
     torch.cuda.synchronize()
-    # per-kernel HIP events around the dominant kernel (dense-exact table Adam), timed region only
-    keys = ["mf_user", "mlp_user", "mf_item", "mlp_item"]
-    ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)] for k in keys}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        model.engine.timing = {k: ev[k][s] for k in keys}
         u, i, t = batches[s % len(batches)]
         step(u, i, t)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    model.engine.timing = None
     if world > 1:
         tt = torch.tensor([elapsed], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -154,22 +149,34 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     samples_s = N * world * args.steps / elapsed
     loss = float(step.last_loss.item())
+    # second timed region, same K steps, with live per-launch HIP events (torch events on the
+    # stream the kernels run on) around every C-ABI call: per-kernel durations for the roofline.
+    # Kept separate because recording 2 events per launch costs host time that would otherwise
+    # leak into the headline number.
+    from ncf_amd import _lib as L
+    L.PROFILE = []
+    torch.cuda.synchronize()
+    for s in range(args.steps):
+        u, i, t = batches[s % len(batches)]
+        step(u, i, t)
+    torch.cuda.synchronize()
+    prof, L.PROFILE = L.PROFILE, None
 
-    # roofline of the dominant kernel: algorithmic bytes / measured duration
-    D4 = D * 4
-    rows = {"mf_user": U, "mlp_user": U, "mf_item": I, "mlp_item": I}
-    uniq = model.engine.pending  # released; recompute touched-row estimate from the last batch
-    u_last, i_last, _ = batches[(args.steps - 1) % len(batches)]
-    touched = {"user": int(torch.unique(u_last).numel()), "item": int(torch.unique(i_last).numel())}
-    tot_bytes, tot_ms = 0.0, 0.0
-    for k in keys:
-        r = rows[k]
-        t_rows = touched["user" if k.endswith("user") else "item"]
-        per_launch = r * D * 24 + r * 4 + t_rows * D4
-        dur = sum(a.elapsed_time(b) for a, b in ev[k]) / args.steps
-        tot_bytes += per_launch
-        tot_ms += dur
-    achieved = tot_bytes / (tot_ms * 1e-3) / 1e9
+    # per-entry-point GPU time; roofline of the dominant kernel class
+    per = {}
+    for name, a, e0, e1 in prof:
+        per.setdefault(name, []).append((a, e0.elapsed_time(e1)))
+    totals = {k: sum(d for _, d in v) / args.steps for k, v in per.items()}   # ms per step
+    gemm_names = ("ncf_gemm_f32", "ncf_gemm_f32_splitk")
+    gemm_ms = sum(totals.get(k, 0.0) for k in gemm_names)
+    gemm_flops = sum(2.0 * a[0] * a[1] * a[2] for k in gemm_names for a, _ in per.get(k, [])) / args.steps
+    gemm_launches = sum(len(per.get(k, [])) for k in gemm_names) / args.steps
+    achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
+    # table-update work of the deferred dense-exact Adam: algorithmic = the dense schedule's
+    # 24 B per table element per step (what the reference's Adam must move), priced per step
+    tab_ms = sum(totals.get(k, 0.0) for k in ("ncf_adam_rows_catchup", "ncf_adam_rows_apply",
+                                                "ncf_adam_sweep", "ncf_adam_table"))
+    tab_bytes = 2 * (U + I) * D * 24.0
     # --- inference pairs/s: eval forward (M = 1) on resident pairs
     model.eval()
     npairs = args.infer_pairs
@@ -212,10 +219,18 @@ def main():
                                    "T=32, dropout 0.2, Adam lr 1e-3 wd 1e-5 (dense-exact)",
                        "global_batch": N * world, "groups_per_gpu": B, "samples_per_group": M,
                        "parallelism": f"dp{world}" if world > 1 else "single-gpu"},
-            "roofline": {"bound": "hbm", "kernel": "k_adam_table<64> (dense-exact table Adam)",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "bytes_per_step": int(tot_bytes), "ms_per_step": round(tot_ms, 4)},
+            "roofline": {"bound": "mfma", "kernel": "k_gemm_f32 (fp32 MFMA v_mfma_f32_32x32x2_f32; "
+                                                    "all attention/MLP GEMM launches of a step)",
+                         "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
+                         "flops_per_step": gemm_flops, "launches_per_step": gemm_launches,
+                         "ms_per_step": round(gemm_ms, 4)},
+            "table_adam": {"kernels": "deferred dense-exact Adam (catch-up + apply + 1/64 sweep)",
+                           "ms_per_step": round(tab_ms, 4),
+                           "dense_equivalent_GBps": round(tab_bytes / (tab_ms * 1e-3) / 1e9, 1),
+                           "note": "dense schedule bytes (24 B x 140.8M elements) / time: above "
+                                   "HBM peak because untouched rows are caught up lazily"},
+            "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(totals.items(), key=lambda x: -x[1])},
             "cpu_baseline": cpu,
             "infer_pairs_per_s": round(infer_pairs, 1),
             "infer_config": f"eval forward (M=1), {npairs} resident (user,item) pairs per GPU",

@@ -96,7 +96,9 @@ int ncf_temporal_bwd(const int64_t* hour, const int64_t* day, const int64_t* mon
                      const float* grad_out, int64_t dim, float* grad_hour, float* grad_day,
                      float* grad_month, void* stream);
 
-/* ---- a7: MLP tower row ops (ReLU -> LayerNorm -> Dropout), architecture.py:233-239 -------- */
+/* ---- a7: MLP tower row ops (ReLU -> LayerNorm -> Dropout), architecture.py:233-239 --------
+ * Backward also returns grad_bias = column sums of grad_lin (the bias gradient of the Linear
+ * that feeds the ReLU; nullable).                                                            */
 int ncf_relu_ln_dropout_fwd(float* relu_in, int64_t n, int64_t width, const float* gamma,
                             const float* beta, float eps, float dropout_p, uint64_t seed,
                             float* out, float* mean, float* rstd, void* stream);
@@ -104,8 +106,8 @@ int64_t ncf_relu_ln_dropout_bwd_workspace(int64_t n, int64_t width);
 int ncf_relu_ln_dropout_bwd(const float* grad_out, const float* relu_in, const float* mean,
                             const float* rstd, const float* gamma, int64_t n, int64_t width,
                             float dropout_p, uint64_t seed, float* grad_lin, float* grad_gamma,
-                            float* grad_beta, float* workspace, int64_t workspace_floats,
-                            void* stream);
+                            float* grad_beta, float* grad_bias, float* workspace,
+                            int64_t workspace_floats, void* stream);
 
 /* ---- a8 + a12: mlp_output + final Linear(2,1) + Sigmoid (+ fused BCELoss) -----------------
  * Replaces architecture.py:345, :353-354 and nn.BCELoss (trainer.py:78, :271).             */
@@ -139,6 +141,24 @@ int ncf_embedding_bwd(const int64_t* user_ids, const int64_t* item_ids, int64_t 
                       float* grad_mf_gamma, float* grad_mf_beta, float* grad_mlp_gamma,
                       float* grad_mlp_beta, void* workspace, int64_t workspace_bytes,
                       void* stream);
+/* The two phases of ncf_embedding_bwd, separable so the dedup can run BEFORE the forward
+ * (the deferred Adam catches up exactly the batch's rows before they are gathered):
+ *   ncf_dedup_ids: stable radix sort + segment heads -> uniq ids, num_unique, optional slots;
+ *   ncf_embedding_bwd_reduce: segment-reduce + LN backward using the same workspace.        */
+int ncf_dedup_ids(const int64_t* user_ids, const int64_t* item_ids, int64_t n, int64_t dim,
+                  int64_t num_users, int64_t num_items, int64_t* uniq_users, int64_t* uniq_items,
+                  int32_t* slot_users, int32_t* slot_items, uint32_t* num_unique, void* workspace,
+                  int64_t workspace_bytes, void* stream);
+int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_users, int64_t num_items,
+                             const float* dy_mf_user, const float* dy_mlp_user,
+                             const float* dy_mf_item, const float* dy_mlp_item,
+                             const float* mf_user, const float* mlp_user, const float* mf_item,
+                             const float* mlp_item, const float* mf_gamma, const float* mlp_gamma,
+                             float eps, float* grad_mf_user, float* grad_mlp_user,
+                             float* grad_mf_item, float* grad_mlp_item, const int64_t* uniq_users,
+                             const int64_t* uniq_items, float* grad_mf_gamma, float* grad_mf_beta,
+                             float* grad_mlp_gamma, float* grad_mlp_beta, void* workspace,
+                             int64_t workspace_bytes, void* stream);
 int ncf_slot_reset(const int64_t* uniq, const uint32_t* num_unique, int kind, int32_t* slot,
                    int64_t max_n, void* stream);
 /* dense[uniq[c]] = grad_compact[c] (materialise a dense table gradient for non-Adam users). */
@@ -154,6 +174,27 @@ int ncf_adam_table(float* param, float* exp_avg, float* exp_avg_sq, int64_t rows
 int ncf_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                   double lr, double beta1, double beta2, double eps, double weight_decay,
                   double step, void* stream);
+
+/* Deferred dense-exact schedule (bit-identical to ncf_adam_table, see adam.hip): rows carry
+ * stamp[row] = last step reflected; step_table[2s], [2s+1] = fp32 scalars of step s
+ * (ncf_adam_step_scalars).  Two tables (GMF + MLP) sharing one id space go in one call
+ * (p1/m1/v1 nullable).                                                                      */
+int ncf_adam_step_scalars(double lr, double beta1, double beta2, int64_t first, int64_t count,
+                          float* out_host);
+int ncf_adam_rows_catchup(float* p0, float* m0, float* v0, float* p1, float* m1, float* v1,
+                          int64_t dim, const int64_t* row_ids, const uint32_t* count, int kind,
+                          int64_t max_n, int32_t* stamp, int32_t target, const float* step_table,
+                          double beta1, double beta2, double eps, double weight_decay,
+                          void* stream);
+int ncf_adam_rows_apply(float* p0, float* m0, float* v0, const float* g0, float* p1, float* m1,
+                        float* v1, const float* g1, int64_t dim, const int64_t* row_ids,
+                        const uint32_t* count, int kind, int64_t max_n, int32_t* stamp,
+                        int32_t step, const float* step_table, double beta1, double beta2,
+                        double eps, double weight_decay, void* stream);
+int ncf_adam_sweep(float* p0, float* m0, float* v0, float* p1, float* m1, float* v1,
+                   int64_t rows, int64_t dim, int32_t* stamp, int32_t target,
+                   const float* step_table, double beta1, double beta2, double eps,
+                   double weight_decay, void* stream);
 
 #ifdef __cplusplus
 }

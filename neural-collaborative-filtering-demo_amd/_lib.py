@@ -47,7 +47,7 @@ SIGNATURES = {
     "ncf_attention_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P, P]),
     "ncf_relu_ln_dropout_fwd": (I32, [P, I64, I64, P, P, F32, F32, U64, P, P, P, P]),
     "ncf_relu_ln_dropout_bwd_workspace": (I64, [I64, I64]),
-    "ncf_relu_ln_dropout_bwd": (I32, [P, P, P, P, P, I64, I64, F32, U64, P, P, P, P, I64, P]),
+    "ncf_relu_ln_dropout_bwd": (I32, [P, P, P, P, P, I64, I64, F32, U64, P, P, P, P, P, I64, P]),
     "ncf_head_fwd": (I32, [P, I64, I64, P, P, P, P, P, P, P, P]),
     "ncf_head_bwd_workspace": (I64, [I64, I64, I64]),
     "ncf_head_bwd": (I32, [P, P, P, P, P, P, I64, I64, P, P, P, P, I64, P, P, P, P, P, P, P, P,
@@ -55,11 +55,20 @@ SIGNATURES = {
     "ncf_embedding_bwd_workspace": (I64, [I64, I64]),
     "ncf_embedding_bwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
                                 P, P, P, P, P, P, P, P, P, P, P, P, I64, P]),
+    "ncf_dedup_ids": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, I64, P]),
+    "ncf_embedding_bwd_reduce": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
+                                       P, P, P, P, P, P, P, P, P, I64, P]),
     "ncf_slot_reset": (I32, [P, P, I32, P, I64, P]),
     "ncf_scatter_compact_rows": (I32, [P, I64, P, P, I32, P, I64, P]),
     "ncf_adam_table": (I32, [P, P, P, I64, I64, P, P, F64, F64, F64, F64, F64, F64, P]),
     "ncf_adam_flat": (I32, [P, P, P, P, I64, F64, F64, F64, F64, F64, F64, P]),
     "ncf_fill_2d": (I32, [P, I64, I64, I64, F32, P]),
+    "ncf_adam_step_scalars": (I32, [F64, F64, F64, I64, I64, P]),
+    "ncf_adam_rows_catchup": (I32, [P, P, P, P, P, P, I64, P, P, I32, I64, P, I32, P, F64, F64, F64,
+                                    F64, P]),
+    "ncf_adam_rows_apply": (I32, [P, P, P, P, P, P, P, P, I64, P, P, I32, I64, P, I32, P, F64, F64,
+                                  F64, F64, P]),
+    "ncf_adam_sweep": (I32, [P, P, P, P, P, P, I64, I64, P, I32, P, F64, F64, F64, F64, P]),
     "ncf_temporal_fwd": (I32, [P, P, P, P, I64, P, P, P, P, I64, I64, P, P, P]),
     "ncf_temporal_bwd": (I32, [P, P, P, I64, P, I64, P, P, P, P]),
 }
@@ -103,9 +112,21 @@ def check(rc: int, name: str):
         raise RuntimeError(f"{name} failed ({rc}): {msg}")
 
 
+# Optional live instrumentation (bench.py): when PROFILE is a list, every call appends
+# (name, args, start_event, end_event) recorded on torch's current stream around the launch.
+PROFILE = None
+
+
 def call(name: str, *args):
     lib = _lib if _lib is not None else load()
-    rc = getattr(lib, name)(*args)
+    if PROFILE is not None:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        rc = getattr(lib, name)(*args)
+        b.record()
+        PROFILE.append((name, args, a, b))
+    else:
+        rc = getattr(lib, name)(*args)
     check(rc, name)
     return rc
 

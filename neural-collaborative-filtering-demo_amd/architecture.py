@@ -186,6 +186,11 @@ class AdvancedNCF(nn.Module):
     def engine(self) -> NCFEngine:
         return self._engine
 
+    def state_dict(self, *args, **kwargs):
+        # a deferred optimizer may hold untouched table rows behind: materialise them first
+        self._engine.sync_tables()
+        return super().state_dict(*args, **kwargs)
+
     # ---------------------------------------------------------------- forward (:258-381)
     def forward(self, features: KeyedJaggedTensor) -> torch.Tensor:
         total_samples = features.values().size(0) // 2                  # :274
@@ -228,6 +233,7 @@ class AdvancedNCF(nn.Module):
 
     def get_user_embeddings(self, user_features: Dict) -> Dict[str, torch.Tensor]:
         """(:383-391)"""
+        self._engine.sync_tables()
         ids = user_features["user_features"].single_id_split()["user_id"]
         return {"mf": gather_rows(self.mf_embedding_collection.embedding_bags["user_id"].weight,
                                   ids, self.mf_norm.weight, self.mf_norm.bias, LN_EPS),
@@ -236,6 +242,7 @@ class AdvancedNCF(nn.Module):
 
     def get_product_embeddings(self, product_features: Dict) -> Dict[str, torch.Tensor]:
         """(:393-407)"""
+        self._engine.sync_tables()
         ids = product_features["product_features"].single_id_split()["product_id"]
         cat = self.category_hierarchy(product_features["category_features"]["department_ids"],
                                       product_features["category_features"]["category_ids"])

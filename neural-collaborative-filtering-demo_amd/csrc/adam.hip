@@ -21,20 +21,34 @@ struct AdamScalars {
   float neg_step, w1, b2, c2, bc2_sqrt, eps, wd;
 };
 
-__device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, const AdamScalars& s) {
+// One Adam element update.  FP contraction is OFF so that every kernel that applies a step
+// (dense sweep, deferred catch-up, touched-row apply) performs bit-identical arithmetic: the
+// deferred schedule then reproduces the dense-exact schedule bit for bit.
+__device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, float neg_step,
+                                      float bc2_sqrt, const AdamScalars& s) {
+#pragma clang fp contract(off)
   g = g + s.wd * p;
   m = m + s.w1 * (g - m);
   v = v * s.b2;
   v = v + s.c2 * g * g;
-  const float denom = sqrtf(v) / s.bc2_sqrt + s.eps;
-  p = p + s.neg_step * (m / denom);
+  const float denom = sqrtf(v) / bc2_sqrt + s.eps;
+  p = p + neg_step * (m / denom);
+}
+
+__device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, const AdamScalars& s) {
+  adam1(p, m, v, g, s.neg_step, s.bc2_sqrt, s);
+}
+
+__device__ __forceinline__ void adam4(float4& p, float4& m, float4& v, float4 g, float ns,
+                                      float bc, const AdamScalars& s) {
+  adam1(p.x, m.x, v.x, g.x, ns, bc, s);
+  adam1(p.y, m.y, v.y, g.y, ns, bc, s);
+  adam1(p.z, m.z, v.z, g.z, ns, bc, s);
+  adam1(p.w, m.w, v.w, g.w, ns, bc, s);
 }
 
 __device__ __forceinline__ void adam4(float4& p, float4& m, float4& v, float4 g, const AdamScalars& s) {
-  adam1(p.x, m.x, v.x, g.x, s);
-  adam1(p.y, m.y, v.y, g.y, s);
-  adam1(p.z, m.z, v.z, g.z, s);
-  adam1(p.w, m.w, v.w, g.w, s);
+  adam4(p, m, v, g, s.neg_step, s.bc2_sqrt, s);
 }
 
 template <int D>
@@ -81,6 +95,104 @@ __global__ void k_scatter_compact(float* __restrict__ dense, const int64_t* __re
   const int col = (int)(t % (D / 4)) * 4;
   if (c >= max_n || c >= (int64_t)num_unique[kind]) return;
   st4(dense + uniq[c] * D + col, ld4(G + c * D + col));
+}
+
+// ---- deferred dense-exact schedule -------------------------------------------------------
+// A row that receives no gradient at step s still takes the step with g = 0 (weight decay only).
+// Instead of streaming every untouched row every step, rows carry stamp[row] = the last step
+// their (p, m, v) reflect; before a row is READ it is caught up by replaying the missing
+// zero-gradient steps s = stamp+1 .. target with that step's scalars (table[2s] = -lr/(1-b1^s),
+// table[2s+1] = sqrt(1-b2^s)), element by element, with the very same adam1 arithmetic.
+// Results are bit-identical to the dense sweep; the cost moves from HBM traffic to VALU work.
+struct TablePtrs {
+  float *p0, *m0, *v0, *p1, *m1, *v1;  // two tables sharing the row index space (GMF + MLP)
+  const float *G0, *G1;                 // compact gradients (apply only)
+};
+
+template <int D>
+__device__ __forceinline__ void catch_up_row(const TablePtrs& t, int64_t row, int col, int32_t from,
+                                             int32_t to, const float* __restrict__ table,
+                                             const AdamScalars& s) {
+  if (from >= to) return;
+  const int64_t o = row * D + col;
+  float4 p0 = ld4(t.p0 + o), m0 = ld4(t.m0 + o), v0 = ld4(t.v0 + o);
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t.p1) {
+    float4 p1 = ld4(t.p1 + o), m1 = ld4(t.m1 + o), v1 = ld4(t.v1 + o);
+    for (int32_t q = from + 1; q <= to; ++q) {
+      const float ns = table[2 * q], bc = table[2 * q + 1];
+      adam4(p0, m0, v0, z, ns, bc, s);
+      adam4(p1, m1, v1, z, ns, bc, s);
+    }
+    st4(t.p1 + o, p1); st4(t.m1 + o, m1); st4(t.v1 + o, v1);
+  } else {
+    for (int32_t q = from + 1; q <= to; ++q) adam4(p0, m0, v0, z, table[2 * q], table[2 * q + 1], s);
+  }
+  st4(t.p0 + o, p0); st4(t.m0 + o, m0); st4(t.v0 + o, v0);
+}
+
+// rows listed in ids[0 .. count[kind]) (unique), caught up to `target`
+template <int D>
+__global__ __launch_bounds__(256) void k_adam_catchup(TablePtrs t, const int64_t* __restrict__ ids,
+                                                      const uint32_t* __restrict__ count, int kind,
+                                                      int64_t max_n, int32_t* __restrict__ stamp,
+                                                      int32_t target, const float* __restrict__ table,
+                                                      AdamScalars s) {
+  constexpr int L = D / 4;
+  const int64_t tt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = tt / L;
+  const int sub = (int)(tt % L);
+  const int64_t cnt = count ? (int64_t)count[kind] : max_n;
+  if (c >= max_n || c >= cnt) return;
+  const int64_t row = ids[c];
+  const int32_t from = stamp[row];
+  catch_up_row<D>(t, row, sub * 4, from, target, table, s);
+  if (sub == 0 && from < target) stamp[row] = target;
+}
+
+// every row of the table caught up to `target` (materialise)
+template <int D>
+__global__ __launch_bounds__(256) void k_adam_sweep(TablePtrs t, int64_t rows,
+                                                    int32_t* __restrict__ stamp, int32_t target,
+                                                    const float* __restrict__ table, AdamScalars s) {
+  constexpr int L = D / 4;
+  const int64_t n = rows * L;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = e / L;
+    const int sub = (int)(e % L);
+    const int32_t from = stamp[row];
+    catch_up_row<D>(t, row, sub * 4, from, target, table, s);
+    // all L lanes of the row read stamp before this store: they share one wave-instruction
+    if (sub == 0 && from < target) stamp[row] = target;
+  }
+}
+
+// step `step` applied to the touched rows (already current through step-1) with their gradient
+template <int D>
+__global__ __launch_bounds__(256) void k_adam_apply(TablePtrs t, const int64_t* __restrict__ ids,
+                                                    const uint32_t* __restrict__ count, int kind,
+                                                    int64_t max_n, int32_t* __restrict__ stamp,
+                                                    int32_t step, const float* __restrict__ table,
+                                                    AdamScalars s) {
+  constexpr int L = D / 4;
+  const int64_t tt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = tt / L;
+  const int sub = (int)(tt % L);
+  const int64_t cnt = count ? (int64_t)count[kind] : max_n;
+  if (c >= max_n || c >= cnt) return;
+  const int64_t row = ids[c];
+  const int64_t o = row * D + sub * 4;
+  const float ns = table[2 * step], bc = table[2 * step + 1];
+  float4 p0 = ld4(t.p0 + o), m0 = ld4(t.m0 + o), v0 = ld4(t.v0 + o);
+  adam4(p0, m0, v0, ld4(t.G0 + c * D + sub * 4), ns, bc, s);
+  st4(t.p0 + o, p0); st4(t.m0 + o, m0); st4(t.v0 + o, v0);
+  if (t.p1) {
+    float4 p1 = ld4(t.p1 + o), m1 = ld4(t.m1 + o), v1 = ld4(t.v1 + o);
+    adam4(p1, m1, v1, ld4(t.G1 + c * D + sub * 4), ns, bc, s);
+    st4(t.p1 + o, p1); st4(t.m1 + o, m1); st4(t.v1 + o, v1);
+  }
+  if (sub == 0) stamp[row] = step;
 }
 
 AdamScalars make_scalars(double lr, double beta1, double beta2, double eps, double wd, double step) {
@@ -168,4 +280,92 @@ extern "C" int ncf_scatter_compact_rows(float* dense_grad, int64_t dim, const in
   if (max_n <= 0) return NCF_OK;
   NCF_DISPATCH_DIM(dim, scatter_d, dense_grad, uniq, num_unique, kind, grad_compact, max_n,
                    (hipStream_t)stream);
+}
+
+namespace {
+AdamScalars consts_of(double beta1, double beta2, double eps, double wd) {
+  AdamScalars s = make_scalars(1.0, beta1, beta2, eps, wd, 1.0);
+  s.neg_step = 0.f;
+  s.bc2_sqrt = 1.f;
+  return s;
+}
+
+template <int D>
+int catchup_d(TablePtrs t, const int64_t* ids, const uint32_t* count, int kind, int64_t max_n,
+              int32_t* stamp, int32_t target, const float* table, AdamScalars s, hipStream_t st) {
+  hipLaunchKernelGGL(k_adam_catchup<D>, dim3(ncf_cdiv(max_n * (D / 4), 256)), dim3(256), 0, st, t,
+                     ids, count, kind, max_n, stamp, target, table, s);
+  NCF_CHECK_LAUNCH("ncf_adam_rows_catchup");
+  return NCF_OK;
+}
+
+template <int D>
+int apply_d(TablePtrs t, const int64_t* ids, const uint32_t* count, int kind, int64_t max_n,
+            int32_t* stamp, int32_t step, const float* table, AdamScalars s, hipStream_t st) {
+  hipLaunchKernelGGL(k_adam_apply<D>, dim3(ncf_cdiv(max_n * (D / 4), 256)), dim3(256), 0, st, t,
+                     ids, count, kind, max_n, stamp, step, table, s);
+  NCF_CHECK_LAUNCH("ncf_adam_rows_apply");
+  return NCF_OK;
+}
+
+template <int D>
+int sweep_d(TablePtrs t, int64_t rows, int32_t* stamp, int32_t target, const float* table,
+            AdamScalars s, hipStream_t st) {
+  hipLaunchKernelGGL(k_adam_sweep<D>, dim3(grid_for(rows * (D / 4))), dim3(256), 0, st, t, rows,
+                     stamp, target, table, s);
+  NCF_CHECK_LAUNCH("ncf_adam_sweep");
+  return NCF_OK;
+}
+}  // namespace
+
+// Host helper: scalars of steps first .. first+count-1 as out[2*(s-first)] = -lr/(1-b1^s),
+// out[2*(s-first)+1] = sqrt(1-b2^s) — the exact fp32 values the dense kernel uses.
+extern "C" int ncf_adam_step_scalars(double lr, double beta1, double beta2, int64_t first,
+                                     int64_t count, float* out_host) {
+  NCF_CHECK_ARG(first >= 1 && count >= 0 && out_host, "ncf_adam_step_scalars: bad args");
+  for (int64_t i = 0; i < count; ++i) {
+    const AdamScalars s = make_scalars(lr, beta1, beta2, 0.0, 0.0, (double)(first + i));
+    out_host[2 * i] = s.neg_step;
+    out_host[2 * i + 1] = s.bc2_sqrt;
+  }
+  return NCF_OK;
+}
+
+extern "C" int ncf_adam_rows_catchup(float* p0, float* m0, float* v0, float* p1, float* m1,
+                                     float* v1, int64_t dim, const int64_t* row_ids,
+                                     const uint32_t* count, int kind, int64_t max_n,
+                                     int32_t* stamp, int32_t target, const float* step_table,
+                                     double beta1, double beta2, double eps, double weight_decay,
+                                     void* stream) {
+  if (max_n <= 0) return NCF_OK;
+  NCF_CHECK_ARG(p0 && m0 && v0 && row_ids && stamp && step_table, "ncf_adam_rows_catchup: null");
+  TablePtrs t{p0, m0, v0, p1, m1, v1, nullptr, nullptr};
+  NCF_DISPATCH_DIM(dim, catchup_d, t, row_ids, count, kind, max_n, stamp, target, step_table,
+                   consts_of(beta1, beta2, eps, weight_decay), (hipStream_t)stream);
+}
+
+extern "C" int ncf_adam_rows_apply(float* p0, float* m0, float* v0, const float* g0, float* p1,
+                                   float* m1, float* v1, const float* g1, int64_t dim,
+                                   const int64_t* row_ids, const uint32_t* count, int kind,
+                                   int64_t max_n, int32_t* stamp, int32_t step,
+                                   const float* step_table, double beta1, double beta2,
+                                   double eps, double weight_decay, void* stream) {
+  if (max_n <= 0) return NCF_OK;
+  NCF_CHECK_ARG(p0 && m0 && v0 && g0 && row_ids && stamp && step_table && step >= 1,
+                "ncf_adam_rows_apply: bad args");
+  NCF_CHECK_ARG(!p1 || g1, "ncf_adam_rows_apply: second table without gradient");
+  TablePtrs t{p0, m0, v0, p1, m1, v1, g0, g1};
+  NCF_DISPATCH_DIM(dim, apply_d, t, row_ids, count, kind, max_n, stamp, step, step_table,
+                   consts_of(beta1, beta2, eps, weight_decay), (hipStream_t)stream);
+}
+
+extern "C" int ncf_adam_sweep(float* p0, float* m0, float* v0, float* p1, float* m1, float* v1,
+                              int64_t rows, int64_t dim, int32_t* stamp, int32_t target,
+                              const float* step_table, double beta1, double beta2, double eps,
+                              double weight_decay, void* stream) {
+  if (rows <= 0) return NCF_OK;
+  NCF_CHECK_ARG(p0 && m0 && v0 && stamp && step_table, "ncf_adam_sweep: null");
+  TablePtrs t{p0, m0, v0, p1, m1, v1, nullptr, nullptr};
+  NCF_DISPATCH_DIM(dim, sweep_d, t, rows, stamp, target, step_table,
+                   consts_of(beta1, beta2, eps, weight_decay), (hipStream_t)stream);
 }

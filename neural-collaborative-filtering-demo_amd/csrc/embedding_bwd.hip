@@ -216,13 +216,16 @@ __global__ __launch_bounds__(256) void k_seg_assign(const uint32_t* __restrict__
       const uint32_t c = base + pre + rank[r];
       start[c] = (uint32_t)i;
       uniq[c] = (int64_t)sk[i];
-      slot[sk[i]] = (int32_t)c;
+      if (slot) slot[sk[i]] = (int32_t)c;
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) start[totals[kind]] = (uint32_t)n;
 }
 
-// one L-lane group per unique id; grid-stride over c; partial dgamma/dbeta per block:
+// One WAVE per unique id (grid-stride over c).  The wave's S = 64/L sub-groups of L = D/4 lanes
+// split the id's occurrences round-robin (two loads in flight per sub-group per table), then a
+// fixed xor-tree over the sub-groups combines them (deterministic), so a hot id with hundreds of
+// occurrences costs ~len/(2S) load round trips instead of len.  Partial dgamma/dbeta per block:
 // part[kind*nbr + block][0:D mf_g | D:2D mf_b | 2D:3D mlp_g | 3D:4D mlp_b]
 template <int D>
 __global__ __launch_bounds__(256) void k_seg_reduce_ln(
@@ -238,8 +241,8 @@ __global__ __launch_bounds__(256) void k_seg_reduce_ln(
     float* __restrict__ G_mlp0, float* __restrict__ G_mf1, float* __restrict__ G_mlp1,
     float* __restrict__ part) {
   constexpr int L = D / 4;
-  constexpr int GPB = 256 / L;  // groups per block
-  __shared__ __attribute__((aligned(16))) float red[GPB][4 * D];
+  constexpr int S = 64 / L;  // sub-groups per wave
+  __shared__ __attribute__((aligned(16))) float red[4][4 * D];
   const int kind = blockIdx.y;
   const uint32_t* sv = kind ? sv1 : sv0;
   const uint32_t* start = kind ? start1 : start0;
@@ -250,22 +253,42 @@ __global__ __launch_bounds__(256) void k_seg_reduce_ln(
   const float* tml = kind ? t_mlp1 : t_mlp0;
   float* Gmf = kind ? G_mf1 : G_mf0;
   float* Gml = kind ? G_mlp1 : G_mlp0;
-  const int grp = threadIdx.x / L, sub = threadIdx.x % L;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sg = lane / L, sub = lane % L;
   const int col = sub * 4;
   const int64_t U = totals[kind];
   const float4 gm = ld4(g_mf + col), gl = ld4(g_mlp + col);
   float4 a_gm = make_float4(0, 0, 0, 0), a_bm = a_gm, a_gl = a_gm, a_bl = a_gm;
-  for (int64_t c = (int64_t)blockIdx.x * GPB + grp; c < U; c += (int64_t)gridDim.x * GPB) {
+  for (int64_t c = (int64_t)blockIdx.x * 4 + w; c < U; c += (int64_t)gridDim.x * 4) {
     const uint32_t s0 = start[c], s1 = start[c + 1];
-    float4 sm = make_float4(0, 0, 0, 0), sl = sm;
-    for (uint32_t k = s0; k < s1; ++k) {
-      const int64_t r = sv[k];
-      const float4 a = ld4(dmf + r * D + col), b = ld4(dml + r * D + col);
-      sm.x += a.x; sm.y += a.y; sm.z += a.z; sm.w += a.w;
-      sl.x += b.x; sl.y += b.y; sl.z += b.z; sl.w += b.w;
+    float4 sm = make_float4(0, 0, 0, 0), sl = sm, tm = sm, tl = sm;
+    uint32_t k = s0 + sg;
+    for (; k + S < s1; k += 2 * S) {
+      const int64_t r0 = sv[k], r1 = sv[k + S];
+      const float4 a0 = ld4(dmf + r0 * D + col), b0 = ld4(dml + r0 * D + col);
+      const float4 a1 = ld4(dmf + r1 * D + col), b1 = ld4(dml + r1 * D + col);
+      sm.x += a0.x; sm.y += a0.y; sm.z += a0.z; sm.w += a0.w;
+      sl.x += b0.x; sl.y += b0.y; sl.z += b0.z; sl.w += b0.w;
+      tm.x += a1.x; tm.y += a1.y; tm.z += a1.z; tm.w += a1.w;
+      tl.x += b1.x; tl.y += b1.y; tl.z += b1.z; tl.w += b1.w;
+    }
+    if (k < s1) {
+      const int64_t r0 = sv[k];
+      const float4 a0 = ld4(dmf + r0 * D + col), b0 = ld4(dml + r0 * D + col);
+      sm.x += a0.x; sm.y += a0.y; sm.z += a0.z; sm.w += a0.w;
+      sl.x += b0.x; sl.y += b0.y; sl.z += b0.z; sl.w += b0.w;
+    }
+    sm.x += tm.x; sm.y += tm.y; sm.z += tm.z; sm.w += tm.w;
+    sl.x += tl.x; sl.y += tl.y; sl.z += tl.z; sl.w += tl.w;
+#pragma unroll
+    for (int o = L; o < 64; o <<= 1) {  // combine sub-groups (same columns, lanes L apart)
+      sm.x += __shfl_xor(sm.x, o, 64); sm.y += __shfl_xor(sm.y, o, 64);
+      sm.z += __shfl_xor(sm.z, o, 64); sm.w += __shfl_xor(sm.w, o, 64);
+      sl.x += __shfl_xor(sl.x, o, 64); sl.y += __shfl_xor(sl.y, o, 64);
+      sl.z += __shfl_xor(sl.z, o, 64); sl.w += __shfl_xor(sl.w, o, 64);
     }
     const int64_t id = uniq[c];
-    // two LayerNorm backwards (GMF row, MLP row)
+    // two LayerNorm backwards (GMF row, MLP row); every sub-group computes, sub-group 0 stores
 #pragma unroll
     for (int tbl = 0; tbl < 2; ++tbl) {
       const float4 x = ld4((tbl ? tml : tmf) + id * D + col);
@@ -279,37 +302,36 @@ __global__ __launch_bounds__(256) void k_seg_reduce_ln(
       const float4 gd = make_float4(dy.x * gg.x, dy.y * gg.y, dy.z * gg.z, dy.w * gg.w);
       const float m1 = group_sum<L>(gd.x + gd.y + gd.z + gd.w) * (1.0f / D);
       const float m2 = group_sum<L>(gd.x * h.x + gd.y * h.y + gd.z * h.z + gd.w * h.w) * (1.0f / D);
-      const float4 dx = make_float4(rstd * (gd.x - m1 - h.x * m2), rstd * (gd.y - m1 - h.y * m2),
-                                    rstd * (gd.z - m1 - h.z * m2), rstd * (gd.w - m1 - h.w * m2));
-      st4((tbl ? Gml : Gmf) + c * D + col, dx);
-      float4& ag = tbl ? a_gl : a_gm;
-      float4& ab = tbl ? a_bl : a_bm;
-      ag.x += dy.x * h.x; ag.y += dy.y * h.y; ag.z += dy.z * h.z; ag.w += dy.w * h.w;
-      ab.x += dy.x; ab.y += dy.y; ab.z += dy.z; ab.w += dy.w;
+      if (sg == 0) {
+        const float4 dx = make_float4(rstd * (gd.x - m1 - h.x * m2), rstd * (gd.y - m1 - h.y * m2),
+                                      rstd * (gd.z - m1 - h.z * m2), rstd * (gd.w - m1 - h.w * m2));
+        st4((tbl ? Gml : Gmf) + c * D + col, dx);
+        float4& ag = tbl ? a_gl : a_gm;
+        float4& ab = tbl ? a_bl : a_bm;
+        ag.x += dy.x * h.x; ag.y += dy.y * h.y; ag.z += dy.z * h.z; ag.w += dy.w * h.w;
+        ab.x += dy.x; ab.y += dy.y; ab.z += dy.z; ab.w += dy.w;
+      }
     }
   }
-  float* rr = red[grp];
-  st4(rr + col, a_gm);
-  st4(rr + D + col, a_bm);
-  st4(rr + 2 * D + col, a_gl);
-  st4(rr + 3 * D + col, a_bl);
+  if (sg == 0) {
+    float* rr = red[w];
+    st4(rr + col, a_gm);
+    st4(rr + D + col, a_bm);
+    st4(rr + 2 * D + col, a_gl);
+    st4(rr + 3 * D + col, a_bl);
+  }
   __syncthreads();
   float* out = part + ((int64_t)kind * gridDim.x + blockIdx.x) * 4 * D;
-  for (int i = threadIdx.x; i < 4 * D; i += 256) {
-    float s = 0.0f;
-    for (int q = 0; q < GPB; ++q) s += red[q][i];
-    out[i] = s;
-  }
+  for (int i = threadIdx.x; i < 4 * D; i += 256)
+    out[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
 }
 
-__global__ void k_ln_param_finalize(const float* __restrict__ part, int parts, int D,
-                                    float* gm, float* bm, float* gl, float* bl) {
+__global__ void k_ln_param_scatter(const float* __restrict__ red, int D, float* gm, float* bm,
+                                   float* gl, float* bl) {
   for (int i = threadIdx.x; i < 4 * D; i += blockDim.x) {
-    float s = 0.0f;
-    for (int z = 0; z < parts; ++z) s += part[(int64_t)z * 4 * D + i];
     const int q = i / D, c = i % D;
     float* dst = q == 0 ? gm : q == 1 ? bm : q == 2 ? gl : bl;
-    dst[c] = s;
+    dst[c] = red[i];
   }
 }
 
@@ -325,15 +347,16 @@ struct WS {
   uint32_t *ka0, *va0, *ka1, *va1, *kb0, *vb0, *kb1, *vb1;
   uint32_t *hist, *segcnt, *totals, *start0, *start1;
   float* part;
+  float* red_scratch;
   int nb, nbr;
 };
 
 int nb_of(int64_t n) { return n == 0 ? 1 : ncf_cdiv(n, TILE); }
 int nbr_of(int64_t n, int64_t D) {
-  const int64_t gpb = 256 / (D / 4);
-  int64_t b = (n + gpb - 1) / gpb;
+  (void)D;
+  int64_t b = (n + 3) / 4;  // 4 waves (segments) per block
   if (b < 1) b = 1;
-  if (b > 512) b = 512;
+  if (b > 2048) b = 2048;
   return (int)b;
 }
 
@@ -345,7 +368,8 @@ int64_t ws_bytes(int64_t n, int64_t D) {
   b += 2 * (int64_t)nb * 4 + 256;        // segcnt
   b += 64;                               // totals
   b += 2 * (n + 2) * 4 + 256;            // starts
-  b += 2 * (int64_t)nbr * 4 * D * 4 + 256;
+  b += (2 * (int64_t)nbr + 1) * 4 * D * 4 + 256;
+  b += ncf_reduce_scratch(2 * nbr, 4 * D) * 4 + 256;
   return b + 1024;
 }
 
@@ -369,7 +393,8 @@ WS carve(void* base, int64_t n, int64_t D) {
   w.totals = (uint32_t*)take(64);
   w.start0 = (uint32_t*)take((n + 2) * 4);
   w.start1 = (uint32_t*)take((n + 2) * 4);
-  w.part = (float*)take(2 * (int64_t)w.nbr * 4 * D * 4);
+  w.part = (float*)take((2 * (int64_t)w.nbr + 1) * 4 * D * 4);
+  w.red_scratch = (float*)take(ncf_reduce_scratch(2 * w.nbr, 4 * D) * 4 + 4);
   return w;
 }
 
@@ -390,8 +415,9 @@ int seg_reduce(const WS& w, const uint32_t* sv0, const uint32_t* sv1, const int6
                      w.start1, uniq0, uniq1, w.totals, dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1,
                      tml1, gmf, gml, eps, Gmf0, Gml0, Gmf1, Gml1, w.part);
   NCF_CHECK_LAUNCH("ncf_embedding_bwd(seg_reduce)");
-  hipLaunchKernelGGL(k_ln_param_finalize, dim3(1), dim3(256), 0, st, w.part, 2 * w.nbr, D, dgm,
-                     dbm, dgl, dbl);
+  float* red = w.part + (int64_t)2 * w.nbr * 4 * D;
+  ncf_reduce_parts(w.part, 2 * w.nbr, 4 * D, 4 * D, red, 0, 4 * D, 4 * D, st, w.red_scratch);
+  hipLaunchKernelGGL(k_ln_param_scatter, dim3(1), dim3(256), 0, st, red, D, dgm, dbm, dgl, dbl);
   NCF_CHECK_LAUNCH("ncf_embedding_bwd(finalize)");
   return NCF_OK;
 }
@@ -400,11 +426,113 @@ int seg_reduce(const WS& w, const uint32_t* sv0, const uint32_t* sv1, const int6
 
 extern "C" int64_t ncf_embedding_bwd_workspace(int64_t n, int64_t dim) { return ws_bytes(n, dim); }
 
-// Inputs (kind 0 = user ids, kind 1 = item ids; n rows each):
-//   dy_*: gradients w.r.t. the LayerNorm OUTPUTS of the gathered rows [n, D]
-//   tables: the current GMF/MLP tables (LN inputs are recomputed from them)
-// Outputs per kind: num_unique (device u32 in totals_out[kind]), uniq ids [n] (first num_unique
-// valid), compact LN-input gradients G_* [n, D] (first num_unique rows valid), slot[id] = c.
+// sorted (keys, positions) after `passes` ping-pong passes
+static void sorted_bufs(const WS& w, int passes, uint32_t** k0, uint32_t** v0, uint32_t** k1,
+                        uint32_t** v1) {
+  const bool odd = passes & 1;
+  *k0 = odd ? w.kb0 : w.ka0;
+  *v0 = odd ? w.vb0 : w.va0;
+  *k1 = odd ? w.kb1 : w.ka1;
+  *v1 = odd ? w.vb1 : w.va1;
+}
+
+static int passes_for(int64_t num_users, int64_t num_items) {
+  return (bits_for(num_users > num_items ? num_users : num_items) + 7) / 8;
+}
+
+// Phase 1: stable radix sort of (id, position) for users and items + segment heads:
+// uniq ids per kind, num_unique[kind], optional slot maps.  The sorted positions and segment
+// starts stay in `workspace` for ncf_embedding_bwd_reduce (same workspace, n, row counts).
+extern "C" int ncf_dedup_ids(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
+                             int64_t dim, int64_t num_users, int64_t num_items,
+                             int64_t* uniq_users, int64_t* uniq_items, int32_t* slot_users,
+                             int32_t* slot_items, uint32_t* num_unique, void* workspace,
+                             int64_t workspace_bytes, void* stream) {
+  NCF_CHECK_ARG(n >= 0 && n < (1ll << 31), "ncf_dedup_ids: bad n");
+  NCF_CHECK_ARG(num_users < (1ll << 32) && num_items < (1ll << 32), "ncf_dedup_ids: > 2^32 rows");
+  if (workspace_bytes < ws_bytes(n, dim)) {
+    ncf_set_error("ncf_dedup_ids: workspace %lld < %lld bytes", (long long)workspace_bytes,
+                  (long long)ws_bytes(n, dim));
+    return NCF_ERR_WORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  WS w = carve(workspace, n, dim);
+  if (n > 0) {
+    hipLaunchKernelGGL(k_init_keys, dim3(ncf_cdiv(n, 256)), dim3(256), 0, st, user_ids, num_users,
+                       item_ids, num_items, n, w.ka0, w.va0, w.ka1, w.va1);
+    NCF_CHECK_LAUNCH("ncf_dedup_ids(init)");
+  }
+  const int passes = passes_for(num_users, num_items);
+  uint32_t *ki0 = w.ka0, *vi0 = w.va0, *ki1 = w.ka1, *vi1 = w.va1;
+  uint32_t *ko0 = w.kb0, *vo0 = w.vb0, *ko1 = w.kb1, *vo1 = w.vb1;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = 8 * p;
+    if (n > 0) {
+      hipLaunchKernelGGL(k_hist, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n, shift, w.nb, w.hist);
+      hipLaunchKernelGGL(k_scan_u32, dim3(2), dim3(1024), 0, st, w.hist, (int64_t)256 * w.nb,
+                         (uint32_t*)nullptr);
+      hipLaunchKernelGGL(k_scatter, dim3(w.nb, 2), dim3(256), 0, st, ki0, vi0, ki1, vi1, n, shift,
+                         w.nb, w.hist, ko0, vo0, ko1, vo1);
+      NCF_CHECK_LAUNCH("ncf_dedup_ids(sort)");
+    }
+    uint32_t* t;
+    t = ki0; ki0 = ko0; ko0 = t;
+    t = vi0; vi0 = vo0; vo0 = t;
+    t = ki1; ki1 = ko1; ko1 = t;
+    t = vi1; vi1 = vo1; vo1 = t;
+  }
+  hipLaunchKernelGGL(k_seg_count, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n, w.nb, w.segcnt);
+  hipLaunchKernelGGL(k_scan_u32, dim3(2), dim3(1024), 0, st, w.segcnt, (int64_t)w.nb, w.totals);
+  hipLaunchKernelGGL(k_seg_assign, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n, w.nb, w.segcnt,
+                     w.totals, w.start0, w.start1, uniq_users, uniq_items, slot_users, slot_items);
+  NCF_CHECK_LAUNCH("ncf_dedup_ids(segments)");
+  if (num_unique)
+    (void)hipMemcpyAsync(num_unique, w.totals, 2 * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
+  return NCF_OK;
+}
+
+// Phase 2: per unique id, sum the LN-output gradients of its occurrences (position order) and
+// apply mf_norm / mlp_norm backward once; dgamma/dbeta of both norms.  Requires the workspace
+// filled by ncf_dedup_ids for the same ids.
+extern "C" int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_users,
+                                        int64_t num_items, const float* dy_mf_user,
+                                        const float* dy_mlp_user, const float* dy_mf_item,
+                                        const float* dy_mlp_item, const float* mf_user,
+                                        const float* mlp_user, const float* mf_item,
+                                        const float* mlp_item, const float* mf_gamma,
+                                        const float* mlp_gamma, float eps, float* grad_mf_user,
+                                        float* grad_mlp_user, float* grad_mf_item,
+                                        float* grad_mlp_item, const int64_t* uniq_users,
+                                        const int64_t* uniq_items, float* grad_mf_gamma,
+                                        float* grad_mf_beta, float* grad_mlp_gamma,
+                                        float* grad_mlp_beta, void* workspace,
+                                        int64_t workspace_bytes, void* stream) {
+  NCF_CHECK_ARG(n >= 0 && n < (1ll << 31), "ncf_embedding_bwd_reduce: bad n");
+  NCF_CHECK_ARG(dim == 16 || dim == 32 || dim == 64 || dim == 128 || dim == 256,
+                "ncf_embedding_bwd_reduce: dim must be 16/32/64/128/256");
+  if (workspace_bytes < ws_bytes(n, dim)) {
+    ncf_set_error("ncf_embedding_bwd_reduce: workspace too small");
+    return NCF_ERR_WORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  WS w = carve(workspace, n, dim);
+  uint32_t *k0, *v0, *k1, *v1;
+  sorted_bufs(w, passes_for(num_users, num_items), &k0, &v0, &k1, &v1);
+  switch (dim) {
+#define SEG(DD)                                                                                   \
+  case DD:                                                                                        \
+    return seg_reduce<DD>(w, v0, v1, uniq_users, uniq_items, dy_mf_user, dy_mlp_user,             \
+                          dy_mf_item, dy_mlp_item, mf_user, mlp_user, mf_item, mlp_item,          \
+                          mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user, grad_mf_item,    \
+                          grad_mlp_item, grad_mf_gamma, grad_mf_beta, grad_mlp_gamma,             \
+                          grad_mlp_beta, st);
+    SEG(16) SEG(32) SEG(64) SEG(128) SEG(256)
+#undef SEG
+  }
+  return NCF_ERR_ARG;
+}
+
+// Both phases (dedup + reduce), with slot maps for the dense-exact table Adam.
 extern "C" int ncf_embedding_bwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
                                  int64_t dim, int64_t num_users, int64_t num_items,
                                  const float* dy_mf_user, const float* dy_mlp_user,
@@ -417,59 +545,17 @@ extern "C" int ncf_embedding_bwd(const int64_t* user_ids, const int64_t* item_id
                                  int32_t* slot_items, uint32_t* num_unique, float* grad_mf_gamma,
                                  float* grad_mf_beta, float* grad_mlp_gamma, float* grad_mlp_beta,
                                  void* workspace, int64_t workspace_bytes, void* stream) {
-  NCF_CHECK_ARG(n >= 0 && n < (1ll << 31), "ncf_embedding_bwd: bad n");
   NCF_CHECK_ARG(dim == 16 || dim == 32 || dim == 64 || dim == 128 || dim == 256,
                 "ncf_embedding_bwd: dim must be 16/32/64/128/256");
-  NCF_CHECK_ARG(num_users < (1ll << 32) && num_items < (1ll << 32), "ncf_embedding_bwd: > 2^32 rows");
-  if (workspace_bytes < ws_bytes(n, dim)) {
-    ncf_set_error("ncf_embedding_bwd: workspace %lld < %lld bytes", (long long)workspace_bytes,
-                  (long long)ws_bytes(n, dim));
-    return NCF_ERR_WORKSPACE;
-  }
-  hipStream_t st = (hipStream_t)stream;
-  WS w = carve(workspace, n, dim);
-  if (n > 0) {
-    hipLaunchKernelGGL(k_init_keys, dim3(ncf_cdiv(n, 256)), dim3(256), 0, st, user_ids, num_users,
-                       item_ids, num_items, n, w.ka0, w.va0, w.ka1, w.va1);
-    NCF_CHECK_LAUNCH("ncf_embedding_bwd(init)");
-  }
-  const int bits = bits_for(num_users > num_items ? num_users : num_items);
-  const int passes = (bits + 7) / 8;
-  uint32_t *ki0 = w.ka0, *vi0 = w.va0, *ki1 = w.ka1, *vi1 = w.va1;
-  uint32_t *ko0 = w.kb0, *vo0 = w.vb0, *ko1 = w.kb1, *vo1 = w.vb1;
-  for (int p = 0; p < passes && n > 0; ++p) {
-    const int shift = 8 * p;
-    hipLaunchKernelGGL(k_hist, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n, shift, w.nb, w.hist);
-    hipLaunchKernelGGL(k_scan_u32, dim3(2), dim3(1024), 0, st, w.hist, (int64_t)256 * w.nb,
-                       (uint32_t*)nullptr);
-    hipLaunchKernelGGL(k_scatter, dim3(w.nb, 2), dim3(256), 0, st, ki0, vi0, ki1, vi1, n, shift,
-                       w.nb, w.hist, ko0, vo0, ko1, vo1);
-    NCF_CHECK_LAUNCH("ncf_embedding_bwd(sort)");
-    uint32_t* t;
-    t = ki0; ki0 = ko0; ko0 = t;
-    t = vi0; vi0 = vo0; vo0 = t;
-    t = ki1; ki1 = ko1; ko1 = t;
-    t = vi1; vi1 = vo1; vo1 = t;
-  }
-  // sorted keys/values now in ki*/vi*
-  hipLaunchKernelGGL(k_seg_count, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n, w.nb, w.segcnt);
-  hipLaunchKernelGGL(k_scan_u32, dim3(2), dim3(1024), 0, st, w.segcnt, (int64_t)w.nb, w.totals);
-  hipLaunchKernelGGL(k_seg_assign, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n, w.nb, w.segcnt,
-                     w.totals, w.start0, w.start1, uniq_users, uniq_items, slot_users, slot_items);
-  NCF_CHECK_LAUNCH("ncf_embedding_bwd(segments)");
-  if (num_unique) (void)hipMemcpyAsync(num_unique, w.totals, 2 * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
-  switch (dim) {
-#define SEG(DD)                                                                                   \
-  case DD:                                                                                        \
-    return seg_reduce<DD>(w, vi0, vi1, uniq_users, uniq_items, dy_mf_user, dy_mlp_user,           \
-                          dy_mf_item, dy_mlp_item, mf_user, mlp_user, mf_item, mlp_item,          \
-                          mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user, grad_mf_item,    \
-                          grad_mlp_item, grad_mf_gamma, grad_mf_beta, grad_mlp_gamma,             \
-                          grad_mlp_beta, st);
-    SEG(16) SEG(32) SEG(64) SEG(128) SEG(256)
-#undef SEG
-  }
-  return NCF_ERR_ARG;
+  int rc = ncf_dedup_ids(user_ids, item_ids, n, dim, num_users, num_items, uniq_users, uniq_items,
+                         slot_users, slot_items, num_unique, workspace, workspace_bytes, stream);
+  if (rc) return rc;
+  return ncf_embedding_bwd_reduce(n, dim, num_users, num_items, dy_mf_user, dy_mlp_user,
+                                  dy_mf_item, dy_mlp_item, mf_user, mlp_user, mf_item, mlp_item,
+                                  mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user,
+                                  grad_mf_item, grad_mlp_item, uniq_users, uniq_items,
+                                  grad_mf_gamma, grad_mf_beta, grad_mlp_gamma, grad_mlp_beta,
+                                  workspace, workspace_bytes, stream);
 }
 
 // slot[uniq[c]] = -1 for c < num_unique[kind] (restores the all -1 invariant after the update)

@@ -17,11 +17,22 @@
 
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 16, LDP = 65;
+constexpr int BM = 64, BN = 64, BK = 32, LDP = 65;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 enum { F_RELU = 1, F_ACCUM = 2 };
+
+// Per K-step each of the 256 threads stages 8 A and 8 B elements.  Index e = tid + 256*r maps
+// to (row, k) with the CONTIGUOUS dimension on consecutive threads (coalesced loads); the
+// k-major LDS image [BK][64+1] makes both the transposing writes and the MFMA operand reads
+// (lane&31 -> row/col, lane>>5 -> k) bank-conflict-free.  The next K-step's global loads are
+// issued into registers before the current step's MFMAs, so their latency hides under compute.
+template <bool T_CONTIG_K>
+__device__ __forceinline__ void tile_coord(int e, int& rc, int& k) {
+  if (T_CONTIG_K) { k = e & (BK - 1); rc = e >> 5; }   // 32 consecutive k per row
+  else { rc = e & 63; k = e >> 6; }                     // 64 consecutive rows per k
+}
 
 template <bool A_T, bool B_T>
 __global__ __launch_bounds__(256) void k_gemm_f32(int M, int N, int K, const float* __restrict__ A,
@@ -44,25 +55,35 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int M, int N, int K, const flo
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
 
-  for (int k0 = kb; k0 < ke; k0 += BK) {
+  float ra[8], rb[8];
+  auto load = [&](int k0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 8; ++r) {
       const int e = tid + 256 * r;
       int m, k;
-      if (!A_T) { k = e & (BK - 1); m = e >> 4; } else { m = e & (BM - 1); k = e >> 6; }
+      tile_coord<!A_T>(e, m, k);
       const int gm = m0 + m, gk = k0 + k;
-      float v = 0.0f;
-      if (gm < M && gk < ke) v = A_T ? A[(int64_t)gk * lda + gm] : A[(int64_t)gm * lda + gk];
-      As[k][m] = v;
-      int n;
-      if (B_T) { k = e & (BK - 1); n = e >> 4; } else { n = e & (BN - 1); k = e >> 6; }
-      const int gn = n0 + n;
-      const int gk2 = k0 + k;
-      float u = 0.0f;
-      if (gn < N && gk2 < ke) u = B_T ? B[(int64_t)gn * ldb + gk2] : B[(int64_t)gk2 * ldb + gn];
-      Bs[k][n] = u;
+      ra[r] = (gm < M && gk < ke) ? (A_T ? A[(int64_t)gk * lda + gm] : A[(int64_t)gm * lda + gk]) : 0.0f;
+      int n, k2;
+      tile_coord<B_T>(e, n, k2);
+      const int gn = n0 + n, gk2 = k0 + k2;
+      rb[r] = (gn < N && gk2 < ke) ? (B_T ? B[(int64_t)gn * ldb + gk2] : B[(int64_t)gk2 * ldb + gn]) : 0.0f;
+    }
+  };
+  if (kb < ke) load(kb);
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int e = tid + 256 * r;
+      int m, k;
+      tile_coord<!A_T>(e, m, k);
+      As[k][m] = ra[r];
+      int n, k2;
+      tile_coord<B_T>(e, n, k2);
+      Bs[k2][n] = rb[r];
     }
     __syncthreads();
+    if (k0 + BK < ke) load(k0 + BK);  // prefetch next K-step; lands while the MFMAs run
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       const float a = As[kk + (lane >> 5)][wm * 32 + (lane & 31)];
@@ -88,30 +109,32 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int M, int N, int K, const flo
   }
 }
 
-// out[i] (+)= sum_z part[z*stride + i], fixed z order
-__global__ void k_sum_slabs(const float* __restrict__ part, int splits, int64_t stride, int64_t n,
-                            float* __restrict__ out, int accumulate, int64_t rows, int64_t cols,
-                            int64_t ldo) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float s = 0.0f;
-  for (int z = 0; z < splits; ++z) s += part[z * stride + i];
-  const int64_t r = i / cols, c = i % cols;
-  float* p = out + r * ldo + c;
-  *p = accumulate ? *p + s : s;
-  (void)rows;
-}
-
-// partial column sums: part[b][c] = sum over rows [b*R, (b+1)*R) of X[r][c]
-__global__ void k_colsum_partial(const float* __restrict__ X, int64_t rows, int64_t cols,
-                                 int64_t ld, int64_t rows_per_block, float* __restrict__ part) {
-  const int64_t c = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
+// partial column sums: block (x = row chunk, y = 64-column chunk); waves stride the rows,
+// lanes own columns (coalesced 256-B rows), 4-way unrolled; fixed-order LDS combine.
+__global__ __launch_bounds__(256) void k_colsum_partial(const float* __restrict__ X, int64_t rows,
+                                                        int64_t cols, int64_t ld,
+                                                        int64_t rows_per_block,
+                                                        float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.y * 64 + lane;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(rows, r0 + rows_per_block);
-  float s = 0.0f;
-  for (int64_t r = r0; r < r1; ++r) s += X[r * ld + c];
-  part[(int64_t)blockIdx.x * cols + c] = s;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < cols) {
+    int64_t r = r0 + w;
+    for (; r + 12 < r1; r += 16) {
+      a0 += X[r * ld + c];
+      a1 += X[(r + 4) * ld + c];
+      a2 += X[(r + 8) * ld + c];
+      a3 += X[(r + 12) * ld + c];
+    }
+    for (; r < r1; r += 4) a0 += X[r * ld + c];
+  }
+  red[w][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (w == 0 && c < cols)
+    part[(int64_t)blockIdx.x * cols + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 template <bool A_T, bool B_T>
@@ -152,7 +175,7 @@ extern "C" int ncf_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int
 }
 
 extern "C" int64_t ncf_gemm_splitk_workspace(int64_t M, int64_t N, int splits) {
-  return (int64_t)splits * M * N;
+  return (int64_t)splits * M * N + ncf_reduce_scratch(splits, M * N);
 }
 
 // Long-K GEMM (weight gradients dW = dYᵀ·X, K = batch rows): K split into `splits` slabs, each a
@@ -164,7 +187,7 @@ extern "C" int ncf_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float*
   NCF_CHECK_ARG(M >= 0 && N >= 0 && K >= 0 && splits >= 1, "ncf_gemm_f32_splitk: bad size");
   if (M == 0 || N == 0) return NCF_OK;
   NCF_CHECK_ARG(A && B && C && workspace, "ncf_gemm_f32_splitk: null pointer");
-  if (workspace_floats < (int64_t)splits * M * N) {
+  if (workspace_floats < (int64_t)splits * M * N + ncf_reduce_scratch(splits, M * N)) {
     ncf_set_error("ncf_gemm_f32_splitk: workspace %lld < %lld floats", (long long)workspace_floats,
                   (long long)splits * M * N);
     return NCF_ERR_WORKSPACE;
@@ -180,16 +203,25 @@ extern "C" int ncf_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float*
                       (int)ksplit, M * N, st);
     if (rc) return rc;
   }
-  const int64_t n = M * N;
-  hipLaunchKernelGGL(k_sum_slabs, dim3(ncf_cdiv(n, 256)), dim3(256), 0, st, workspace,
-                     K == 0 ? 1 : used, M * N, n, C, accumulate, M, N, ldc);
+  ncf_reduce_parts(workspace, K == 0 ? 1 : used, M * N, M * N, C, accumulate, N, ldc, st,
+                   workspace + (int64_t)used * M * N);
   NCF_CHECK_LAUNCH("ncf_gemm_f32_splitk(reduce)");
   return NCF_OK;
 }
 
+static int64_t colsum_rpb(int64_t rows, int64_t cols) {
+  // aim for ~512 blocks in total, at least 64 rows each
+  const int64_t cb = (cols + 63) / 64;
+  int64_t chunks = 512 / (cb > 0 ? cb : 1);
+  if (chunks < 1) chunks = 1;
+  int64_t rpb = (rows + chunks - 1) / chunks;
+  return rpb < 64 ? 64 : rpb;
+}
+
 extern "C" int64_t ncf_colsum_workspace(int64_t rows, int64_t cols) {
-  const int64_t rpb = 256;
-  return ((rows + rpb - 1) / rpb) * cols;
+  const int64_t rpb = colsum_rpb(rows, cols);
+  const int64_t nb = (rows + rpb - 1) / rpb + 1;
+  return nb * cols + ncf_reduce_scratch((int)nb, cols);
 }
 
 // out[c] (+)= sum_r X[r*ld + c]  (bias gradients), two deterministic passes
@@ -199,21 +231,21 @@ extern "C" int ncf_colsum(const float* X, int64_t rows, int64_t cols, int64_t ld
   NCF_CHECK_ARG(rows >= 0 && cols >= 0, "ncf_colsum: bad size");
   if (cols == 0) return NCF_OK;
   hipStream_t st = (hipStream_t)stream;
-  const int64_t rpb = 256;
+  const int64_t rpb = colsum_rpb(rows, cols);
   const int64_t nb = rows == 0 ? 1 : (rows + rpb - 1) / rpb;
-  if (workspace_floats < nb * cols) {
+  if (workspace_floats < ncf_colsum_workspace(rows, cols)) {
     ncf_set_error("ncf_colsum: workspace too small");
     return NCF_ERR_WORKSPACE;
   }
   if (rows == 0) {
     (void)hipMemsetAsync(workspace, 0, sizeof(float) * cols, st);
   } else {
-    hipLaunchKernelGGL(k_colsum_partial, dim3((unsigned)nb, ncf_cdiv(cols, 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_colsum_partial, dim3((unsigned)nb, ncf_cdiv(cols, 64)), dim3(256), 0, st,
                        X, rows, cols, ld, rpb, workspace);
     NCF_CHECK_LAUNCH("ncf_colsum(partial)");
   }
-  hipLaunchKernelGGL(k_sum_slabs, dim3(ncf_cdiv(cols, 256)), dim3(256), 0, st, workspace, (int)nb,
-                     cols, cols, out, accumulate, (int64_t)1, cols, cols);
+  ncf_reduce_parts(workspace, (int)nb, cols, cols, out, accumulate, cols, cols, st,
+                   workspace + nb * cols);
   NCF_CHECK_LAUNCH("ncf_colsum(reduce)");
   return NCF_OK;
 }

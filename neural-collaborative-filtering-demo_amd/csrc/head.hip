@@ -12,7 +12,7 @@
 
 namespace {
 
-constexpr int ROWS_PER_BLOCK = 64;
+constexpr int ROWS_PER_BLOCK = 16;
 
 __global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ a3, int64_t n, int W3,
                                                   const float* __restrict__ w_out,
@@ -103,13 +103,13 @@ __global__ __launch_bounds__(256) void k_head_bwd(
     part[(int64_t)blockIdx.x * P + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
 }
 
-__global__ void k_head_finalize(const float* __restrict__ part, int parts, int W3, int D,
-                                float* dw_out, float* db_out, float* dw_mf, float* db_mf,
-                                float* dw_fin, float* db_fin, float* loss, float inv_n) {
+// scatter the reduced head-gradient vector red[P] into the parameter gradients
+__global__ void k_head_scatter(const float* __restrict__ red, int W3, int D, float* dw_out,
+                               float* db_out, float* dw_mf, float* db_mf, float* dw_fin,
+                               float* db_fin, float* loss, float inv_n) {
   const int P = W3 + D + 6;
   for (int i = threadIdx.x; i < P; i += blockDim.x) {
-    float s = 0.0f;
-    for (int z = 0; z < parts; ++z) s += part[(int64_t)z * P + i];
+    const float s = red[i];
     if (i < W3) dw_out[i] = s;
     else if (i < W3 + D) dw_mf[i - W3] = s;
     else {
@@ -139,7 +139,9 @@ extern "C" int ncf_head_fwd(const float* mlp_last, int64_t n, int64_t width, con
 }
 
 extern "C" int64_t ncf_head_bwd_workspace(int64_t n, int64_t width, int64_t dim) {
-  return (int64_t)(n == 0 ? 1 : ncf_cdiv(n, ROWS_PER_BLOCK)) * (width + dim + 6);
+  const int nb = n == 0 ? 1 : ncf_cdiv(n, ROWS_PER_BLOCK);
+  const int64_t P = width + dim + 6;
+  return (int64_t)(nb + 1) * P + ncf_reduce_scratch(nb, P);
 }
 
 // Backward of the head.  Either grad_prob (upstream dL/dprob, e.g. from torch's BCELoss) or
@@ -169,9 +171,12 @@ extern "C" int ncf_head_bwd(const float* prob, const float* grad_prob, const flo
                      mf_item_ln, (int)dim, mf_out_w, n, grad_mlp_last, grad_mf_user_ln,
                      grad_mf_item_ln, workspace);
   NCF_CHECK_LAUNCH("ncf_head_bwd");
-  hipLaunchKernelGGL(k_head_finalize, dim3(1), dim3(256), 0, st, workspace, nb, (int)width,
-                     (int)dim, grad_mlp_out_w, grad_mlp_out_b, grad_mf_out_w, grad_mf_out_b,
-                     grad_final_w, grad_final_b, loss, inv_n);
+  const int64_t P = width + dim + 6;
+  float* red = workspace + (int64_t)nb * P;
+  ncf_reduce_parts(workspace, nb, P, P, red, 0, P, P, st, red + P);
+  hipLaunchKernelGGL(k_head_scatter, dim3(1), dim3(256), 0, st, red, (int)width, (int)dim,
+                     grad_mlp_out_w, grad_mlp_out_b, grad_mf_out_w, grad_mf_out_b, grad_final_w,
+                     grad_final_b, loss, inv_n);
   NCF_CHECK_LAUNCH("ncf_head_bwd(finalize)");
   return NCF_OK;
 }

@@ -78,3 +78,71 @@ __global__ void k_sum_partials(const float* __restrict__ part, int parts, int64_
   for (int z = 0; z < parts; ++z) s += part[(int64_t)z * stride + i];
   out[i] = accumulate ? out[i] + s : s;
 }
+
+// Deterministic parallel reduction of P partial rows:
+//   out[(i / cols) * ldo + i % cols] (+)= sum_{p < P} part[p * stride + i],  i < L
+// One 256-thread block per 64 consecutive i and per chunk of PB partials (blockIdx.y); wave w
+// sums p = w, w+4, ... (4-way unrolled, several loads in flight per lane); the 4 wave sums are
+// combined in fixed order in LDS.  With gridDim.y > 1 each chunk writes its own output row
+// (out + y * L, dense) and a second launch sums the chunks — always the same order.
+template <int Dummy = 0>
+__global__ __launch_bounds__(256) void k_reduce_parts(const float* __restrict__ part, int P,
+                                                      int PB, int64_t stride, int64_t L,
+                                                      float* __restrict__ out, int accumulate,
+                                                      int64_t cols, int64_t ldo) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  const int pb = blockIdx.y * PB;
+  const int pe = min(P, pb + PB);
+  float s = 0.0f;
+  if (i < L) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int p = pb + w;
+    for (; p + 12 < pe; p += 16) {
+      a0 += part[(int64_t)p * stride + i];
+      a1 += part[(int64_t)(p + 4) * stride + i];
+      a2 += part[(int64_t)(p + 8) * stride + i];
+      a3 += part[(int64_t)(p + 12) * stride + i];
+    }
+    for (; p < pe; p += 4) a0 += part[(int64_t)p * stride + i];
+    s = (a0 + a1) + (a2 + a3);
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && i < L) {
+    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (gridDim.y > 1) {
+      out[(int64_t)blockIdx.y * L + i] = t;
+    } else {
+      float* o = out + (i / cols) * ldo + (i % cols);
+      *o = accumulate ? *o + t : t;
+    }
+  }
+}
+
+constexpr int NCF_REDUCE_PB = 64;
+
+// scratch floats needed by ncf_reduce_parts for P partials of length L
+static inline int64_t ncf_reduce_scratch(int P, int64_t L) {
+  return P > 2 * NCF_REDUCE_PB ? (int64_t)((P + NCF_REDUCE_PB - 1) / NCF_REDUCE_PB) * L : 0;
+}
+
+// Reduce P partial rows; two deterministic stages when P is large (needs `scratch` of
+// ncf_reduce_scratch(P, L) floats; with scratch == nullptr a single stage is used).
+static inline void ncf_reduce_parts(const float* part, int P, int64_t stride, int64_t L, float* out,
+                                    int accumulate, int64_t cols, int64_t ldo, hipStream_t st,
+                                    float* scratch = nullptr) {
+  if (L <= 0) return;
+  const unsigned gx = (unsigned)((L + 63) / 64);
+  if (scratch && P > 2 * NCF_REDUCE_PB) {
+    const int chunks = (P + NCF_REDUCE_PB - 1) / NCF_REDUCE_PB;
+    hipLaunchKernelGGL(k_reduce_parts<>, dim3(gx, chunks), dim3(256), 0, st, part, P,
+                       NCF_REDUCE_PB, stride, L, scratch, 0, L, L);
+    hipLaunchKernelGGL(k_reduce_parts<>, dim3(gx, 1), dim3(256), 0, st, scratch, chunks, chunks,
+                       L, L, out, accumulate, cols, ldo);
+    return;
+  }
+  hipLaunchKernelGGL(k_reduce_parts<>, dim3(gx, 1), dim3(256), 0, st, part, P, P, stride, L, out,
+                     accumulate, cols, ldo);
+}

@@ -66,21 +66,24 @@ __global__ __launch_bounds__(256) void k_relu_ln_drop_fwd(float* __restrict__ r,
   }
 }
 
-// Backward.  Each block owns rows [blockIdx*rows_per_block, ...); partial dgamma/dbeta of the
-// block go to part[blockIdx][0:W] / part[blockIdx][W:2W].
+// Backward.  Each block owns rows [blockIdx*rows_per_block, ...); partial dgamma / dbeta / dbias
+// (column sums of the pre-ReLU gradient = bias gradient of the producing Linear) of the block go
+// to part[blockIdx][0:W | W:2W | 2W:3W].
 template <int W>
 __global__ __launch_bounds__(256) void k_relu_ln_drop_bwd(
     const float* __restrict__ dout, const float* __restrict__ r, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ g, int64_t n, int rows_per_block,
     float p, uint64_t seed, float* __restrict__ dlin, float* __restrict__ part) {
   using G = Geo<W>;
-  __shared__ float red[256 / G::L][2 * W];
+  __shared__ float red[256 / G::L][3 * W];
   const int lane_grp = threadIdx.x / G::L;  // row slot inside the block iteration
   const int sub = threadIdx.x % G::L;
   const int slots = 256 / G::L;
-  float4 ag[G::CH], ab[G::CH];
+  float4 ag[G::CH], ab[G::CH], al[G::CH];
 #pragma unroll
-  for (int c = 0; c < G::CH; ++c) { ag[c] = make_float4(0, 0, 0, 0); ab[c] = make_float4(0, 0, 0, 0); }
+  for (int c = 0; c < G::CH; ++c) {
+    ag[c] = make_float4(0, 0, 0, 0); ab[c] = make_float4(0, 0, 0, 0); al[c] = make_float4(0, 0, 0, 0);
+  }
   const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(n, r0 + rows_per_block);
@@ -122,6 +125,7 @@ __global__ __launch_bounds__(256) void k_relu_ln_drop_bwd(
       o.z = x.z > 0.0f ? rs * (dy[c].z - m1 - xh[c].z * m2) : 0.0f;
       o.w = x.w > 0.0f ? rs * (dy[c].w - m1 - xh[c].w * m2) : 0.0f;
       st4(dlin + row * W + col, o);
+      al[c].x += o.x; al[c].y += o.y; al[c].z += o.z; al[c].w += o.w;
     }
   }
 #pragma unroll
@@ -131,12 +135,14 @@ __global__ __launch_bounds__(256) void k_relu_ln_drop_bwd(
     red[lane_grp][col + 2] = ag[c].z; red[lane_grp][col + 3] = ag[c].w;
     red[lane_grp][W + col + 0] = ab[c].x; red[lane_grp][W + col + 1] = ab[c].y;
     red[lane_grp][W + col + 2] = ab[c].z; red[lane_grp][W + col + 3] = ab[c].w;
+    red[lane_grp][2 * W + col + 0] = al[c].x; red[lane_grp][2 * W + col + 1] = al[c].y;
+    red[lane_grp][2 * W + col + 2] = al[c].z; red[lane_grp][2 * W + col + 3] = al[c].w;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * W; i += 256) {
+  for (int i = threadIdx.x; i < 3 * W; i += 256) {
     float s = 0.0f;
     for (int k = 0; k < slots; ++k) s += red[k][i];
-    part[(int64_t)blockIdx.x * 2 * W + i] = s;
+    part[(int64_t)blockIdx.x * 3 * W + i] = s;
   }
 }
 
@@ -155,16 +161,16 @@ int fwd_w(float* r, int64_t n, const float* g, const float* b, float eps, float 
 template <int W>
 int bwd_w(const float* dout, const float* r, const float* mean, const float* rstd, const float* g,
           int64_t n, float p, uint64_t seed, float* dlin, float* dgamma, float* dbeta,
-          float* ws, hipStream_t st) {
+          float* dbias, float* ws, hipStream_t st) {
   const int nb = n == 0 ? 1 : ncf_cdiv(n, RPB);
   hipLaunchKernelGGL(k_relu_ln_drop_bwd<W>, dim3(nb), dim3(256), 0, st, dout, r, mean, rstd, g, n,
                      RPB, p, seed, dlin, ws);
   NCF_CHECK_LAUNCH("ncf_relu_ln_dropout_bwd");
-  // dgamma and dbeta are contiguous halves of each partial row
-  hipLaunchKernelGGL(k_sum_partials<>, dim3(ncf_cdiv(W, 256)), dim3(256), 0, st, ws, nb,
-                     (int64_t)2 * W, (int64_t)W, dgamma, 0);
-  hipLaunchKernelGGL(k_sum_partials<>, dim3(ncf_cdiv(W, 256)), dim3(256), 0, st, ws + W, nb,
-                     (int64_t)2 * W, (int64_t)W, dbeta, 0);
+  // dgamma, dbeta, dbias are the three W-wide thirds of each partial row
+  float* scr = ws + (int64_t)nb * 3 * W;
+  ncf_reduce_parts(ws, nb, 3 * W, W, dgamma, 0, W, W, st, scr);
+  ncf_reduce_parts(ws + W, nb, 3 * W, W, dbeta, 0, W, W, st, scr);
+  if (dbias) ncf_reduce_parts(ws + 2 * W, nb, 3 * W, W, dbias, 0, W, W, st, scr);
   NCF_CHECK_LAUNCH("ncf_relu_ln_dropout_bwd(reduce)");
   return NCF_OK;
 }
@@ -185,7 +191,8 @@ int bwd_w(const float* dout, const float* r, const float* mean, const float* rst
   }
 
 extern "C" int64_t ncf_relu_ln_dropout_bwd_workspace(int64_t n, int64_t width) {
-  return (int64_t)(n == 0 ? 1 : ncf_cdiv(n, RPB)) * 2 * width;
+  const int nb = n == 0 ? 1 : ncf_cdiv(n, RPB);
+  return (int64_t)nb * 3 * width + ncf_reduce_scratch(nb, width);
 }
 
 // out = dropout(LayerNorm(r)); r already holds relu(linear) (GEMM epilogue); saves mean/rstd.
@@ -204,12 +211,13 @@ extern "C" int ncf_relu_ln_dropout_bwd(const float* grad_out, const float* relu_
                                        const float* mean, const float* rstd, const float* gamma,
                                        int64_t n, int64_t width, float dropout_p, uint64_t seed,
                                        float* grad_lin, float* grad_gamma, float* grad_beta,
-                                       float* workspace, int64_t workspace_floats, void* stream) {
+                                       float* grad_bias, float* workspace,
+                                       int64_t workspace_floats, void* stream) {
   NCF_CHECK_ARG(n >= 0, "ncf_relu_ln_dropout_bwd: n < 0");
   if (workspace_floats < ncf_relu_ln_dropout_bwd_workspace(n, width)) {
     ncf_set_error("ncf_relu_ln_dropout_bwd: workspace too small");
     return NCF_ERR_WORKSPACE;
   }
   NCF_DISPATCH_W(width, bwd_w, grad_out, relu_in, mean, rstd, gamma, n, dropout_p, seed, grad_lin,
-                 grad_gamma, grad_beta, workspace, (hipStream_t)stream);
+                 grad_gamma, grad_beta, grad_bias, workspace, (hipStream_t)stream);
 }

@@ -87,8 +87,8 @@ class Workspace:
     @staticmethod
     def splits_for(m_out: int, k_out: int, rows: int) -> int:
         tiles = max(1, math.ceil(m_out / 64) * math.ceil(k_out / 64))
-        s = max(1, math.ceil(1024 / tiles))
-        return max(1, min(s, math.ceil(max(rows, 1) / 64)))
+        s = max(1, math.ceil(512 / tiles))
+        return max(1, min(s, math.ceil(max(rows, 1) / 256)))
 
 
 class NCFEngine:
@@ -105,6 +105,7 @@ class NCFEngine:
         self.dense_names: List[str] = []
         self.offsets: Dict[str, tuple] = {}
         self.timing = None        # optional {table: (start_event, end_event)} for the bench
+        self.deferred = None      # DeferredTableAdam holding rows behind, if any
 
     # ------------------------------------------------------------------ parameter layout
     def dense_params(self):
@@ -211,10 +212,18 @@ class NCFEngine:
                   w.scratch.numel(), st)
 
     # ------------------------------------------------------------------ forward
+    def sync_tables(self):
+        """Bring every table row current if a deferred optimizer holds rows behind (no-op
+        otherwise).  Called before anything other than the fused train step reads a table."""
+        if self.deferred is not None:
+            self.deferred.sync()
+
     def forward(self, uid: torch.Tensor, iid: torch.Tensor, M: int, train: bool,
-                drop_p: float, seed: int) -> Workspace:
+                drop_p: float, seed: int, prepare=None) -> Workspace:
         """AdvancedNCF.forward (architecture.py:258-381) on single-id bags; returns the workspace
-        holding prob (and, when ``train``, everything the backward needs)."""
+        holding prob (and, when ``train``, everything the backward needs).  ``prepare(w, uid,
+        iid, stream)`` runs before the gathers (the deferred Adam dedups the ids there and
+        brings exactly those rows current)."""
         dev = self._check_device()
         self.ensure_layout()
         m = self.model
@@ -233,6 +242,11 @@ class NCFEngine:
             raise NotImplementedError("mf_embedding_dim must equal mlp_embedding_dim on this path")
         tb = self.table_params()
         w.err.zero_()
+        w.deduped = False
+        if prepare is not None:
+            prepare(w, uid, iid, st)
+        else:
+            self.sync_tables()
         # a2-a4: 4 gathers + mf_norm/mlp_norm + GMF  (architecture.py:286-287, 305-312)
         _lib.call("ncf_gather_ln_gmf_fwd", ptr(uid), ptr(iid), n, ptr(tb["mf_user"]),
                   ptr(tb["mf_item"]), ptr(tb["mlp_user"]), ptr(tb["mlp_item"]), m.num_users,
@@ -306,14 +320,13 @@ class NCFEngine:
                       ptr(w.rstd[l]), ptr(ln.weight), n, h, drop_p,
                       (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1), ptr(w.dlin[l]),
                       ptr(gv(f"mlp.{4 * l + 2}.weight")), ptr(gv(f"mlp.{4 * l + 2}.bias")),
-                      ptr(w.scratch), w.scratch.numel(), st)
+                      ptr(gv(f"mlp.{4 * l}.bias")), ptr(w.scratch), w.scratch.numel(), st)
             xin, kin = (w.y, D) if l == 0 else (w.a[l - 1], hid[l - 1])
             ldw = lin.weight.shape[1]
             dW = gv(f"mlp.{4 * l}.weight")
             self._wgrad(w, w.dlin[l], h, xin, kin, dW, ldw, h, kin, n, st)
             if ldw > kin:  # zero temporal columns of mlp.0 (their input is all-zero)
                 _lib.call("ncf_fill_2d", ptr(dW[:, kin:]), h, ldw - kin, ldw, 0.0, st)
-            self._colsum(w, w.dlin[l], n, h, gv(f"mlp.{4 * l}.bias"), st)
             dx = w.dy if l == 0 else w.da[l - 1]
             self._gemm(w.dlin[l], h, 0, lin.weight, ldw, 0, dx, kin, n, kin, h, st=st)
         # a5 backward: out_proj, core, q/k/v projections
@@ -333,6 +346,17 @@ class NCFEngine:
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)
         tb = self.table_params()
         G = w.G
+        if getattr(w, "deduped", False):   # ids already sorted/deduplicated before the forward
+            _lib.call("ncf_embedding_bwd_reduce", n, D, m.num_users, m.num_products,
+                      ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), ptr(tb["mf_user"]),
+                      ptr(tb["mlp_user"]), ptr(tb["mf_item"]), ptr(tb["mlp_item"]),
+                      ptr(m.mf_norm.weight), ptr(m.mlp_norm.weight), LN_EPS, ptr(G["mf_user"]),
+                      ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(w.uniq_u),
+                      ptr(w.uniq_i), ptr(gv("mf_norm.weight")), ptr(gv("mf_norm.bias")),
+                      ptr(gv("mlp_norm.weight")), ptr(gv("mlp_norm.bias")), ptr(w.emb_ws),
+                      w.emb_ws.numel(), st)
+            self.pending = w
+            return
         _lib.call("ncf_embedding_bwd", ptr(uid), ptr(iid), n, D, m.num_users, m.num_products,
                   ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), ptr(tb["mf_user"]),
                   ptr(tb["mlp_user"]), ptr(tb["mf_item"]), ptr(tb["mlp_item"]),

@@ -99,7 +99,7 @@ def mha_forward(mod, query, key, value, mask=None):
     y = _MHAFunction.apply(mod, drop_p, seed, query, key, value, mod.q_proj.weight, mod.q_proj.bias,
                            mod.k_proj.weight, mod.k_proj.bias, mod.v_proj.weight, mod.v_proj.bias,
                            mod.out_proj.weight, mod.out_proj.bias)
-    return y.squeeze(1) if squeeze else y
+    return y  # a 2-D input comes back [B, 1, D], as the reference's .view(batch, -1, D) makes it
 
 
 class _TemporalFunction(torch.autograd.Function):
@@ -139,9 +139,14 @@ def temporal_encoding_forward(mod, hour, day, month, days_since):
 
 
 def category_hierarchy_forward(mod, department_ids, category_ids):
-    """CategoryHierarchy.forward (architecture.py:111-119) for 1-D id vectors: the attention
-    sees one key per query, so softmax == 1 and attn = out_proj(v_proj(dept)); then
-    LayerNorm(attn + cat).  Inference path (get_product_embeddings)."""
+    """CategoryHierarchy.forward (architecture.py:111-119) for 1-D id vectors of length n.
+
+    The attention sees one key per query (the reference views the 2-D [n, D] inputs as n
+    sequences of length 1), so softmax == 1 and attn = out_proj(v_proj(dept)) with shape
+    [n, 1, D].  The residual ``attn + cat_embeds`` then BROADCASTS [n, 1, D] + [n, D] ->
+    [n, n, D] (element [a, b] = attn[a] + cat[b]); LayerNorm keeps that shape.  This is the
+    reference's behaviour (pinned by F5) and is reproduced exactly.  Inference path
+    (get_product_embeddings)."""
     w = mod.department_embed.weight
     _require_cuda(w)
     if torch.is_grad_enabled() and w.requires_grad:
@@ -150,18 +155,24 @@ def category_hierarchy_forward(mod, department_ids, category_ids):
     if mod.training and mod.dropout.p > 0:
         raise NotImplementedError("CategoryHierarchy in training mode is not on the accelerated path")
     dev = w.device
-    dept = gather_rows(w, department_ids.reshape(-1))
-    n, D = dept.shape
-    h = gather_rows(mod.category_embed.weight, category_ids.reshape(-1))      # residual (cat)
+    dept_ids = department_ids.reshape(-1).to(device=dev, dtype=torch.int64)
+    cat_ids = category_ids.reshape(-1).to(device=dev, dtype=torch.int64)
+    n = dept_ids.numel()
+    dept = gather_rows(w, dept_ids)
+    D = dept.shape[1]
     att = mod.hierarchy_attn
     v = torch.empty(n, D, device=dev)
     _gemm(dept, D, 0, att.v_proj.weight, D, 1, v, D, n, D, D, att.v_proj.bias)
-    _gemm(v, D, 0, att.out_proj.weight, D, 1, h, D, n, D, D, att.out_proj.bias, accum=True)
-    out = torch.empty(n, D, device=dev)
-    mean, rstd = torch.empty(n, device=dev), torch.empty(n, device=dev)
-    _lib.call("ncf_relu_ln_dropout_fwd", ptr(h), n, D, ptr(mod.norm.weight), ptr(mod.norm.bias),
+    a_idx = torch.arange(n, device=dev).repeat_interleave(n)      # row a*n+b <- attn[a]
+    b_idx = cat_ids.repeat(n)                                      #            + cat[b]
+    vrep = gather_rows(v, a_idx)
+    h = gather_rows(mod.category_embed.weight, b_idx)
+    _gemm(vrep, D, 0, att.out_proj.weight, D, 1, h, D, n * n, D, D, att.out_proj.bias, accum=True)
+    out = torch.empty(n * n, D, device=dev)
+    mean, rstd = torch.empty(n * n, device=dev), torch.empty(n * n, device=dev)
+    _lib.call("ncf_relu_ln_dropout_fwd", ptr(h), n * n, D, ptr(mod.norm.weight), ptr(mod.norm.bias),
               LN_EPS, 0.0, 0, ptr(out), ptr(mean), ptr(rstd), _lib.stream_ptr(dev))
-    return out
+    return out.view(n, n, D)
 
 
 def forward_simple_hour(model, user_ids, product_ids, hour):

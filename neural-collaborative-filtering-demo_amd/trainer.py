@@ -26,10 +26,14 @@ log = logging.getLogger(__name__)
 class FusedTrainStep:
     """forward + BCE + backward + Adam for one batch, on the current HIP stream, no host sync.
 
-    Adam state lives in ``self.state`` with torch's keys; ``export_optimizer_state`` copies it into
-    a torch.optim.Adam's ``state`` for checkpointing in torch's format."""
+    ``deferred=True`` (default) updates the embedding tables with the deferred dense-exact
+    schedule (deferred.py: bit-identical to the dense sweep, without streaming untouched rows);
+    ``deferred=False`` sweeps every table every step (ncf_adam_table).  Adam state lives in
+    ``self.state`` with torch's keys; ``export_optimizer_state`` copies it into a
+    torch.optim.Adam's ``state`` for checkpointing in torch's format."""
 
-    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5):
+    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5,
+                 deferred: bool = True, sweep_every: int = 64):
         self.model = model
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.step_count = 0
@@ -41,6 +45,11 @@ class FusedTrainStep:
         self.m_flat = torch.zeros_like(eng.flat)
         self.v_flat = torch.zeros_like(eng.flat)
         self.last_loss = None
+        self.deferred = None
+        if deferred:
+            from .deferred import DeferredTableAdam
+            self.deferred = DeferredTableAdam(eng, lr, betas, eps, weight_decay, sweep_every,
+                                              moments=self.state)
 
     def __call__(self, user_ids: torch.Tensor, item_ids: torch.Tensor, targets: torch.Tensor,
                  M: Optional[int] = None):
@@ -49,21 +58,30 @@ class FusedTrainStep:
         M = M or (1 + m.negative_samples)
         drop_p = float(m.dropout)
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0 else 0
-        w = eng.forward(user_ids, item_ids, M, True, drop_p, seed)
+        prep = self.deferred.prepare if self.deferred is not None else None
+        w = eng.forward(user_ids, item_ids, M, True, drop_p, seed, prepare=prep)
         eng.backward(w, user_ids, item_ids, None, targets, drop_p, seed)
         self.step_count += 1
         st = _lib.stream_ptr(eng.flat.device)
         b1, b2 = self.betas
-        hp = lambda p: (self.lr, b1, b2, self.eps, self.wd)  # noqa: E731
-        key_of = {id(p): k for k, p in self.tables.items()}
-        eng.adam_tables(hp, lambda p: self.state[key_of[id(p)]], float(self.step_count), st)
+        if self.deferred is not None:
+            self.deferred.apply(w, st)
+        else:
+            hp = lambda p: (self.lr, b1, b2, self.eps, self.wd)  # noqa: E731
+            key_of = {id(p): k for k, p in self.tables.items()}
+            eng.adam_tables(hp, lambda p: self.state[key_of[id(p)]], float(self.step_count), st)
         _lib.call("ncf_adam_flat", ptr(eng.flat), ptr(eng.flat_grad), ptr(self.m_flat),
                   ptr(self.v_flat), eng.flat.numel(), self.lr, b1, b2, self.eps, self.wd,
                   float(self.step_count), st)
         self.last_loss = w.loss
         return w
 
+    def sync(self):
+        if self.deferred is not None:
+            self.deferred.sync()
+
     def export_optimizer_state(self, opt: torch.optim.Adam):
+        self.sync()
         eng = self.model.engine
         step_t = torch.tensor(float(self.step_count))
         for k, p in self.tables.items():

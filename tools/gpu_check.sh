@@ -19,6 +19,7 @@ for step in "$@"; do
     testx) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     bench) run bench 900 python bench.py --steps 30 --warmup 5 ;;
     benchfast) run bench 600 python bench.py --steps 30 --warmup 5 --no-cpu-baseline ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
   esac
 done
