@@ -101,12 +101,15 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--infer-pairs", type=int, default=65536)
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the row-sharded DP step even at world size 1 (exercises the N>1 path)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    sharded = world > 1 or args.sharded
+    if sharded:
         dist.init_process_group("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -117,12 +120,21 @@ def main():
     B, M = args.groups, 5
     N = B * M
     torch.manual_seed(1234)
-    model = ncf.AdvancedNCF(U, I, 10, 50, D, D, T, hid, H, 0.2, M - 1)
     init_sd = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        init_sd = {k: v.clone() for k, v in model.state_dict().items()}
-    model = model.to(dev).train()
-    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5)
+    if sharded:
+        # row-sharded tables (owner = id mod W) + replicated dense params; RCCL all-to-alls
+        from ncf_amd.distributed import make_sharded_step
+
+        def factory(ru, ri):
+            torch.manual_seed(1234 + rank)
+            return ncf.AdvancedNCF(ru, ri, 10, 50, D, D, T, hid, H, 0.2, M - 1).to(dev).train()
+        model, step = make_sharded_step(factory, U, I, lr=1e-3, weight_decay=1e-5)
+    else:
+        model = ncf.AdvancedNCF(U, I, 10, 50, D, D, T, hid, H, 0.2, M - 1)
+        if rank == 0 and not args.no_cpu_baseline:
+            init_sd = {k: v.clone() for k, v in model.state_dict().items()}
+        model = model.to(dev).train()
+        step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5)
     batches = make_batches(U, I, B, M, 8, dev, seed=100 + rank)
     torch.cuda.synchronize()
 
@@ -148,7 +160,8 @@ def main():
         elapsed = float(tt.item())
     ms_step = elapsed / args.steps * 1e3
     samples_s = N * world * args.steps / elapsed
-    loss = float(step.last_loss.item())
+    last = step.ops.last_loss if sharded else step.last_loss
+    loss = float(last.item()) if last is not None else float("nan")
     # second timed region, same K steps, with live per-launch HIP events (torch events on the
     # stream the kernels run on) around every C-ABI call: per-kernel durations for the roofline.
     # Kept separate because recording 2 events per launch costs host time that would otherwise
@@ -181,8 +194,8 @@ def main():
     model.eval()
     npairs = args.infer_pairs
     g = torch.Generator(device=dev).manual_seed(9)
-    iu = torch.randint(0, U, (npairs,), generator=g, device=dev)
-    ii = torch.randint(0, I, (npairs,), generator=g, device=dev)
+    iu = torch.randint(0, model.num_users, (npairs,), generator=g, device=dev)
+    ii = torch.randint(0, model.num_products, (npairs,), generator=g, device=dev)
     eng = model.engine
     with torch.no_grad():
         for _ in range(3):
@@ -218,7 +231,8 @@ def main():
             "config": {"workload": "C2 train step: 1M users x 100K items, D=64, H=4, MLP [256,128,64], "
                                    "T=32, dropout 0.2, Adam lr 1e-3 wd 1e-5 (dense-exact)",
                        "global_batch": N * world, "groups_per_gpu": B, "samples_per_group": M,
-                       "parallelism": f"dp{world}" if world > 1 else "single-gpu"},
+                       "parallelism": (f"dp{world} + row-sharded tables (RCCL all-to-all), "
+                                       "dense all-reduce") if sharded else "single-gpu"},
             "roofline": {"bound": "mfma", "kernel": "k_gemm_f32 (fp32 MFMA v_mfma_f32_32x32x2_f32; "
                                                     "all attention/MLP GEMM launches of a step)",
                          "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
@@ -237,7 +251,7 @@ def main():
             "final_loss": round(loss, 6),
         }
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if sharded:
         dist.destroy_process_group()
 
 

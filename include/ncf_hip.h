@@ -110,7 +110,8 @@ int ncf_relu_ln_dropout_bwd(const float* grad_out, const float* relu_in, const f
                             int64_t workspace_floats, void* stream);
 
 /* ---- a8 + a12: mlp_output + final Linear(2,1) + Sigmoid (+ fused BCELoss) -----------------
- * Replaces architecture.py:345, :353-354 and nn.BCELoss (trainer.py:78, :271).             */
+ * Replaces architecture.py:345, :353-354 and nn.BCELoss (trainer.py:78, :271).  With fused
+ * BCE the mean is over loss_denominator samples (> 0; the global batch under DP) or n.      */
 int ncf_head_fwd(const float* mlp_last, int64_t n, int64_t width, const float* mlp_out_w,
                  const float* mlp_out_b, const float* mf_pred, const float* final_w,
                  const float* final_b, float* mlp_pred, float* prob, void* stream);
@@ -122,8 +123,8 @@ int ncf_head_bwd(const float* prob, const float* grad_prob, const float* targets
                  const float* mf_out_w, float* grad_mlp_last, float* grad_mf_user_ln,
                  float* grad_mf_item_ln, float* grad_mlp_out_w, float* grad_mlp_out_b,
                  float* grad_mf_out_w, float* grad_mf_out_b, float* grad_final_w,
-                 float* grad_final_b, float* loss, float* workspace, int64_t workspace_floats,
-                 void* stream);
+                 float* grad_final_b, float* loss, double loss_denominator, float* workspace,
+                 int64_t workspace_floats, void* stream);
 
 /* ---- a2/a3 backward: sparse segment-reduce + LayerNorm backward ----------------------------
  * Replaces _embedding_bag_dense_backward (+ sort) of the four EBC tables and the mf_norm /
@@ -141,6 +142,17 @@ int ncf_embedding_bwd(const int64_t* user_ids, const int64_t* item_ids, int64_t 
                       float* grad_mf_gamma, float* grad_mf_beta, float* grad_mlp_gamma,
                       float* grad_mlp_beta, void* workspace, int64_t workspace_bytes,
                       void* stream);
+/* Deduplication of two id lists of different lengths (kind 0 / kind 1); ncf_dedup_ids is the
+ * n0 == n1 case. */
+int ncf_dedup_ids2(const int64_t* ids0, int64_t n0, int64_t rows0, const int64_t* ids1,
+                   int64_t n1, int64_t rows1, int64_t dim, int64_t* uniq0, int64_t* uniq1,
+                   int32_t* slot0, int32_t* slot1, uint32_t* num_unique, void* workspace,
+                   int64_t workspace_bytes, void* stream);
+/* inv[position] = compact index of its id, for the dedup held in `workspace`. */
+int ncf_dedup_inverse(int64_t n0, int64_t n1, int64_t rows0, int64_t rows1, int64_t dim,
+                      int64_t* inv0, int64_t* inv1, void* workspace, int64_t workspace_bytes,
+                      void* stream);
+
 /* The two phases of ncf_embedding_bwd, separable so the dedup can run BEFORE the forward
  * (the deferred Adam catches up exactly the batch's rows before they are gathered):
  *   ncf_dedup_ids: stable radix sort + segment heads -> uniq ids, num_unique, optional slots;
@@ -175,8 +187,26 @@ int ncf_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_av
                   double lr, double beta1, double beta2, double eps, double weight_decay,
                   double step, void* stream);
 
+/* ---- (e) row sharding over W ranks: owner(id) = id mod W, local row = id div W -------------
+ * Pack/unpack kernels around the RCCL all-to-alls (collectives run in torch.distributed).    */
+int ncf_owner_bucket(const int64_t* uniq0, const int64_t* uniq1, const uint32_t* count,
+                     int64_t max_n, int world, int64_t* send0, int64_t* send1, int32_t* perm0,
+                     int32_t* perm1, int64_t* counts, void* workspace, int64_t workspace_bytes,
+                     void* stream);
+int ncf_ids_div(const int64_t* ids, int64_t n, int world, int64_t* out, void* stream);
+int ncf_gather_shard_rows(const int64_t* ids, int64_t n, int world, const float* t0,
+                          const float* t1, int64_t rows, int64_t dim, float* out, int* err_flag,
+                          void* stream);
+int ncf_perm_rows(float* rows, const int32_t* perm, int64_t n, int64_t dim, float* mini0,
+                  float* mini1, int dir, void* stream);
+int ncf_segment_sum_rows(int64_t n0, int64_t n1, int64_t rows0, int64_t rows1, int64_t dim,
+                         const float* src0, const float* src1, float* ga0, float* gb0,
+                         float* ga1, float* gb1, void* workspace, int64_t workspace_bytes,
+                         void* stream);
+
 /* Deferred dense-exact schedule (bit-identical to ncf_adam_table, see adam.hip): rows carry
  * stamp[row] = last step reflected; step_table[2s], [2s+1] = fp32 scalars of step s
+ * (-lr/(1-b1^s), 1/sqrt(1-b2^s))
  * (ncf_adam_step_scalars).  Two tables (GMF + MLP) sharing one id space go in one call
  * (p1/m1/v1 nullable).                                                                      */
 int ncf_adam_step_scalars(double lr, double beta1, double beta2, int64_t first, int64_t count,
@@ -192,7 +222,7 @@ int ncf_adam_rows_apply(float* p0, float* m0, float* v0, const float* g0, float*
                         int32_t step, const float* step_table, double beta1, double beta2,
                         double eps, double weight_decay, void* stream);
 int ncf_adam_sweep(float* p0, float* m0, float* v0, float* p1, float* m1, float* v1,
-                   int64_t rows, int64_t dim, int32_t* stamp, int32_t target,
+                   int64_t row0, int64_t rows, int64_t dim, int32_t* stamp, int32_t target,
                    const float* step_table, double beta1, double beta2, double eps,
                    double weight_decay, void* stream);
 

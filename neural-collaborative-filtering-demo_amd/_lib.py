@@ -51,11 +51,18 @@ SIGNATURES = {
     "ncf_head_fwd": (I32, [P, I64, I64, P, P, P, P, P, P, P, P]),
     "ncf_head_bwd_workspace": (I64, [I64, I64, I64]),
     "ncf_head_bwd": (I32, [P, P, P, P, P, P, I64, I64, P, P, P, P, I64, P, P, P, P, P, P, P, P,
-                           P, P, P, P, I64, P]),
+                           P, P, P, F64, P, I64, P]),
     "ncf_embedding_bwd_workspace": (I64, [I64, I64]),
     "ncf_embedding_bwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
                                 P, P, P, P, P, P, P, P, P, P, P, P, I64, P]),
     "ncf_dedup_ids": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, I64, P]),
+    "ncf_dedup_ids2": (I32, [P, I64, I64, P, I64, I64, I64, P, P, P, P, P, P, I64, P]),
+    "ncf_dedup_inverse": (I32, [I64, I64, I64, I64, I64, P, P, P, I64, P]),
+    "ncf_owner_bucket": (I32, [P, P, P, I64, I32, P, P, P, P, P, P, I64, P]),
+    "ncf_ids_div": (I32, [P, I64, I32, P, P]),
+    "ncf_gather_shard_rows": (I32, [P, I64, I32, P, P, I64, I64, P, P, P]),
+    "ncf_perm_rows": (I32, [P, P, I64, I64, P, P, I32, P]),
+    "ncf_segment_sum_rows": (I32, [I64, I64, I64, I64, I64, P, P, P, P, P, P, P, I64, P]),
     "ncf_embedding_bwd_reduce": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
                                        P, P, P, P, P, P, P, P, P, I64, P]),
     "ncf_slot_reset": (I32, [P, P, I32, P, I64, P]),
@@ -68,7 +75,7 @@ SIGNATURES = {
                                     F64, P]),
     "ncf_adam_rows_apply": (I32, [P, P, P, P, P, P, P, P, I64, P, P, I32, I64, P, I32, P, F64, F64,
                                   F64, F64, P]),
-    "ncf_adam_sweep": (I32, [P, P, P, P, P, P, I64, I64, P, I32, P, F64, F64, F64, F64, P]),
+    "ncf_adam_sweep": (I32, [P, P, P, P, P, P, I64, I64, I64, P, I32, P, F64, F64, F64, F64, P]),
     "ncf_temporal_fwd": (I32, [P, P, P, P, I64, P, P, P, P, I64, I64, P, P, P]),
     "ncf_temporal_bwd": (I32, [P, P, P, I64, P, I64, P, P, P, P]),
 }

@@ -32,10 +32,12 @@ __device__ __forceinline__ uint32_t clamp_key(int64_t id, int64_t rows) {
 // ---- pass kernels ---------------------------------------------------------------------------
 // hist[kind][digit][block]
 __global__ __launch_bounds__(256) void k_hist(const uint32_t* __restrict__ keys0,
-                                              const uint32_t* __restrict__ keys1, int64_t n,
-                                              int shift, int nb, uint32_t* __restrict__ hist) {
+                                              const uint32_t* __restrict__ keys1, int64_t n0,
+                                              int64_t n1, int shift, int nb,
+                                              uint32_t* __restrict__ hist) {
   __shared__ uint32_t cnt[256];
   const int kind = blockIdx.y;
+  const int64_t n = kind ? n1 : n0;
   const uint32_t* keys = kind ? keys1 : keys0;
   cnt[threadIdx.x] = 0;
   __syncthreads();
@@ -83,8 +85,9 @@ __global__ __launch_bounds__(1024) void k_scan_u32(uint32_t* __restrict__ data, 
 __global__ __launch_bounds__(256) void k_scatter(const uint32_t* __restrict__ k_in0,
                                                  const uint32_t* __restrict__ v_in0,
                                                  const uint32_t* __restrict__ k_in1,
-                                                 const uint32_t* __restrict__ v_in1, int64_t n,
-                                                 int shift, int nb, const uint32_t* __restrict__ offs,
+                                                 const uint32_t* __restrict__ v_in1, int64_t n0,
+                                                 int64_t n1, int shift, int nb,
+                                                 const uint32_t* __restrict__ offs,
                                                  uint32_t* __restrict__ k_out0,
                                                  uint32_t* __restrict__ v_out0,
                                                  uint32_t* __restrict__ k_out1,
@@ -95,6 +98,7 @@ __global__ __launch_bounds__(256) void k_scatter(const uint32_t* __restrict__ k_
   const uint32_t* vin = kind ? v_in1 : v_in0;
   uint32_t* kout = kind ? k_out1 : k_out0;
   uint32_t* vout = kind ? v_out1 : v_out0;
+  const int64_t n = kind ? n1 : n0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int d = threadIdx.x; d < 1024; d += 256) (&wcnt[0][0])[d] = 0;
   __syncthreads();
@@ -146,24 +150,28 @@ __global__ __launch_bounds__(256) void k_scatter(const uint32_t* __restrict__ k_
 }
 
 __global__ void k_init_keys(const int64_t* __restrict__ ids0, int64_t rows0,
-                            const int64_t* __restrict__ ids1, int64_t rows1, int64_t n,
-                            uint32_t* __restrict__ k0, uint32_t* __restrict__ v0,
+                            const int64_t* __restrict__ ids1, int64_t rows1, int64_t n0,
+                            int64_t n1, uint32_t* __restrict__ k0, uint32_t* __restrict__ v0,
                             uint32_t* __restrict__ k1, uint32_t* __restrict__ v1) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  k0[i] = clamp_key(ids0[i], rows0);
-  v0[i] = (uint32_t)i;
-  k1[i] = clamp_key(ids1[i], rows1);
-  v1[i] = (uint32_t)i;
+  if (i < n0) {
+    k0[i] = clamp_key(ids0[i], rows0);
+    v0[i] = (uint32_t)i;
+  }
+  if (i < n1) {
+    k1[i] = clamp_key(ids1[i], rows1);
+    v1[i] = (uint32_t)i;
+  }
 }
 
 // ---- segments -------------------------------------------------------------------------------
 // per-tile count of segment heads -> cnt[kind][block]
 __global__ __launch_bounds__(256) void k_seg_count(const uint32_t* __restrict__ sk0,
-                                                   const uint32_t* __restrict__ sk1, int64_t n,
-                                                   int nb, uint32_t* __restrict__ cnt) {
+                                                   const uint32_t* __restrict__ sk1, int64_t n0,
+                                                   int64_t n1, int nb, uint32_t* __restrict__ cnt) {
   __shared__ uint32_t s;
   const int kind = blockIdx.y;
+  const int64_t n = kind ? n1 : n0;
   const uint32_t* sk = kind ? sk1 : sk0;
   if (threadIdx.x == 0) s = 0;
   __syncthreads();
@@ -179,8 +187,9 @@ __global__ __launch_bounds__(256) void k_seg_count(const uint32_t* __restrict__ 
 
 // assign compact indices: segment c starts at seg_start[c]; uniq[c] = id; slot[id] = c
 __global__ __launch_bounds__(256) void k_seg_assign(const uint32_t* __restrict__ sk0,
-                                                    const uint32_t* __restrict__ sk1, int64_t n,
-                                                    int nb, const uint32_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ sk1, int64_t n0,
+                                                    int64_t n1, int nb,
+                                                    const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ totals,
                                                     uint32_t* __restrict__ start0,
                                                     uint32_t* __restrict__ start1,
@@ -190,6 +199,7 @@ __global__ __launch_bounds__(256) void k_seg_assign(const uint32_t* __restrict__
                                                     int32_t* __restrict__ slot1) {
   __shared__ uint32_t wsum[16];
   const int kind = blockIdx.y;
+  const int64_t n = kind ? n1 : n0;
   const uint32_t* sk = kind ? sk1 : sk0;
   uint32_t* start = kind ? start1 : start0;
   int64_t* uniq = kind ? uniq1 : uniq0;
@@ -342,6 +352,154 @@ __global__ void k_slot_reset(const int64_t* __restrict__ uniq, const uint32_t* _
   slot[uniq[c]] = -1;
 }
 
+// ---- row sharding (multi-GPU): owner(id) = id mod W, local row = id div W ----------------------
+// owner bucket keys: digit = owner for valid entries, W (sorts last) for c >= count
+__global__ void k_owner_keys(const int64_t* __restrict__ uniq0, const int64_t* __restrict__ uniq1,
+                             const uint32_t* __restrict__ count, int64_t n, int W,
+                             uint32_t* __restrict__ k0, uint32_t* __restrict__ v0,
+                             uint32_t* __restrict__ k1, uint32_t* __restrict__ v1) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  k0[i] = i < (int64_t)count[0] ? (uint32_t)(uniq0[i] % W) : (uint32_t)W;
+  v0[i] = (uint32_t)i;
+  k1[i] = i < (int64_t)count[1] ? (uint32_t)(uniq1[i] % W) : (uint32_t)W;
+  v1[i] = (uint32_t)i;
+}
+
+// after one stable pass: send_ids[j] = uniq[perm[j]], counts[kind][d] from the scanned histogram
+__global__ void k_owner_finish(const int64_t* __restrict__ uniq0, const int64_t* __restrict__ uniq1,
+                               const uint32_t* __restrict__ count, const uint32_t* __restrict__ sv0,
+                               const uint32_t* __restrict__ sv1, int64_t n,
+                               const uint32_t* __restrict__ offs, int nb, int W,
+                               int64_t* __restrict__ send0, int64_t* __restrict__ send1,
+                               int32_t* __restrict__ perm0, int32_t* __restrict__ perm1,
+                               int64_t* __restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (int64_t)count[0]) { perm0[i] = (int32_t)sv0[i]; send0[i] = uniq0[sv0[i]]; }
+  if (i < (int64_t)count[1]) { perm1[i] = (int32_t)sv1[i]; send1[i] = uniq1[sv1[i]]; }
+  if (blockIdx.x == 0 && threadIdx.x < 2 * W) {
+    const int kind = threadIdx.x / W, d = threadIdx.x % W;
+    const uint32_t* o = offs + (int64_t)kind * 256 * nb;
+    counts[kind * W + d] = (int64_t)(o[(int64_t)(d + 1) * nb] - o[(int64_t)d * nb]);
+  }
+  (void)n;
+}
+
+// inverse map of a dedup: inv[position] = compact index of its id
+__global__ __launch_bounds__(256) void k_seg_inverse(const uint32_t* __restrict__ sk0,
+                                                     const uint32_t* __restrict__ sk1,
+                                                     const uint32_t* __restrict__ sv0,
+                                                     const uint32_t* __restrict__ sv1, int64_t n0,
+                                                     int64_t n1, int nb,
+                                                     const uint32_t* __restrict__ off,
+                                                     int64_t* __restrict__ inv0,
+                                                     int64_t* __restrict__ inv1) {
+  __shared__ uint32_t wsum[16];
+  const int kind = blockIdx.y;
+  const int64_t n = kind ? n1 : n0;
+  const uint32_t* sk = kind ? sk1 : sk0;
+  const uint32_t* sv = kind ? sv1 : sv0;
+  int64_t* inv = kind ? inv1 : inv0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  bool head[4];
+  uint32_t rank[4];
+  const uint64_t le = (lane == 63) ? ~0ull : ((1ull << (lane + 1)) - 1);  // inclusive
+  for (int r = 0; r < 4; ++r) {
+    const int64_t i = (int64_t)blockIdx.x * TILE + r * 256 + threadIdx.x;
+    head[r] = i < n && (i == 0 || sk[i] != sk[i - 1]);
+    const uint64_t m = __ballot(head[r]);
+    rank[r] = (uint32_t)__popcll(m & le);
+    if (lane == 0) wsum[r * 4 + w] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  const uint32_t base = off[(int64_t)kind * nb + blockIdx.x];
+  for (int r = 0; r < 4; ++r) {
+    const int64_t i = (int64_t)blockIdx.x * TILE + r * 256 + threadIdx.x;
+    if (i >= n) continue;
+    uint32_t pre = 0;
+    for (int q = 0; q < r * 4 + w; ++q) pre += wsum[q];
+    inv[sv[i]] = (int64_t)(base + pre + rank[r]) - 1;
+  }
+}
+
+// owner side: per unique local row c, sum the received gradient rows of its occurrences
+// (position order = source rank, then the sender's order: deterministic); src rows are [n][2D]
+// (GMF | MLP), outputs compact [U][D] per table.
+template <int D>
+__global__ __launch_bounds__(256) void k_seg_sum_rows(
+    const uint32_t* __restrict__ sv0, const uint32_t* __restrict__ sv1,
+    const uint32_t* __restrict__ start0, const uint32_t* __restrict__ start1,
+    const uint32_t* __restrict__ totals, const float* __restrict__ src0,
+    const float* __restrict__ src1, float* __restrict__ Ga0, float* __restrict__ Gb0,
+    float* __restrict__ Ga1, float* __restrict__ Gb1) {
+  constexpr int L = D / 4;
+  const int kind = blockIdx.y;
+  const uint32_t* sv = kind ? sv1 : sv0;
+  const uint32_t* start = kind ? start1 : start0;
+  const float* src = kind ? src1 : src0;
+  float* Ga = kind ? Ga1 : Ga0;
+  float* Gb = kind ? Gb1 : Gb0;
+  const int64_t U = totals[kind];
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int sub = (int)(t % L);
+  for (int64_t c = t / L; c < U; c += (int64_t)gridDim.x * blockDim.x / L) {
+    float4 a = make_float4(0, 0, 0, 0), b = a;
+    for (uint32_t k = start[c]; k < start[c + 1]; ++k) {
+      const int64_t r = sv[k];
+      const float4 x = ld4(src + r * 2 * D + sub * 4), y = ld4(src + r * 2 * D + D + sub * 4);
+      a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+      b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+    }
+    st4(Ga + c * D + sub * 4, a);
+    st4(Gb + c * D + sub * 4, b);
+  }
+}
+
+// rows of a shard for global ids: out[j] = (t0[id/W] | t1[id/W])
+template <int D>
+__global__ void k_gather_shard(const int64_t* __restrict__ ids, int64_t n, int W,
+                               const float* __restrict__ t0, const float* __restrict__ t1,
+                               int64_t rows, float* __restrict__ out, int* err) {
+  constexpr int L = D / 4;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t j = t / L;
+  const int sub = (int)(t % L);
+  if (j >= n) return;
+  int64_t r = ids[j] / W;
+  if (r < 0 || r >= rows) {
+    if (err && sub == 0) atomicOr(err, 2);
+    r = 0;
+  }
+  st4(out + j * 2 * D + sub * 4, ld4(t0 + r * D + sub * 4));
+  st4(out + j * 2 * D + D + sub * 4, ld4(t1 + r * D + sub * 4));
+}
+
+// mini0[perm[j]] = rows[j][0:D], mini1[perm[j]] = rows[j][D:2D]   (dir = 0)
+// out[j] = (mini0[perm[j]] | mini1[perm[j]])                       (dir = 1)
+template <int D>
+__global__ void k_perm_rows(float* __restrict__ rows, const int32_t* __restrict__ perm, int64_t n,
+                            float* __restrict__ mini0, float* __restrict__ mini1, int dir) {
+  constexpr int L = D / 4;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t j = t / L;
+  const int sub = (int)(t % L);
+  if (j >= n) return;
+  const int64_t c = perm[j];
+  float* r = rows + j * 2 * D + sub * 4;
+  if (dir == 0) {
+    st4(mini0 + c * D + sub * 4, ld4(r));
+    st4(mini1 + c * D + sub * 4, ld4(r + D));
+  } else {
+    st4(r, ld4(mini0 + c * D + sub * 4));
+    st4(r + D, ld4(mini1 + c * D + sub * 4));
+  }
+}
+
+__global__ void k_ids_div(const int64_t* __restrict__ ids, int64_t n, int W, int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = ids[i] / W;
+}
+
 // ---- workspace layout -----------------------------------------------------------------------
 struct WS {
   uint32_t *ka0, *va0, *ka1, *va1, *kb0, *vb0, *kb1, *vb1;
@@ -440,16 +598,17 @@ static int passes_for(int64_t num_users, int64_t num_items) {
   return (bits_for(num_users > num_items ? num_users : num_items) + 7) / 8;
 }
 
-// Phase 1: stable radix sort of (id, position) for users and items + segment heads:
-// uniq ids per kind, num_unique[kind], optional slot maps.  The sorted positions and segment
-// starts stay in `workspace` for ncf_embedding_bwd_reduce (same workspace, n, row counts).
-extern "C" int ncf_dedup_ids(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
-                             int64_t dim, int64_t num_users, int64_t num_items,
-                             int64_t* uniq_users, int64_t* uniq_items, int32_t* slot_users,
-                             int32_t* slot_items, uint32_t* num_unique, void* workspace,
-                             int64_t workspace_bytes, void* stream) {
-  NCF_CHECK_ARG(n >= 0 && n < (1ll << 31), "ncf_dedup_ids: bad n");
-  NCF_CHECK_ARG(num_users < (1ll << 32) && num_items < (1ll << 32), "ncf_dedup_ids: > 2^32 rows");
+// Phase 1: stable radix sort of (id, position) for two id lists (kind 0 / kind 1, lengths n0 /
+// n1) + segment heads: uniq ids per kind, num_unique[kind], optional slot maps.  The sorted
+// positions and segment starts stay in `workspace` (sized for max(n0, n1)).
+extern "C" int ncf_dedup_ids2(const int64_t* ids0, int64_t n0, int64_t rows0, const int64_t* ids1,
+                              int64_t n1, int64_t rows1, int64_t dim, int64_t* uniq0,
+                              int64_t* uniq1, int32_t* slot0, int32_t* slot1,
+                              uint32_t* num_unique, void* workspace, int64_t workspace_bytes,
+                              void* stream) {
+  const int64_t n = n0 > n1 ? n0 : n1;
+  NCF_CHECK_ARG(n0 >= 0 && n1 >= 0 && n < (1ll << 31), "ncf_dedup_ids: bad n");
+  NCF_CHECK_ARG(rows0 < (1ll << 32) && rows1 < (1ll << 32), "ncf_dedup_ids: > 2^32 rows");
   if (workspace_bytes < ws_bytes(n, dim)) {
     ncf_set_error("ncf_dedup_ids: workspace %lld < %lld bytes", (long long)workspace_bytes,
                   (long long)ws_bytes(n, dim));
@@ -458,21 +617,22 @@ extern "C" int ncf_dedup_ids(const int64_t* user_ids, const int64_t* item_ids, i
   hipStream_t st = (hipStream_t)stream;
   WS w = carve(workspace, n, dim);
   if (n > 0) {
-    hipLaunchKernelGGL(k_init_keys, dim3(ncf_cdiv(n, 256)), dim3(256), 0, st, user_ids, num_users,
-                       item_ids, num_items, n, w.ka0, w.va0, w.ka1, w.va1);
+    hipLaunchKernelGGL(k_init_keys, dim3(ncf_cdiv(n, 256)), dim3(256), 0, st, ids0, rows0, ids1,
+                       rows1, n0, n1, w.ka0, w.va0, w.ka1, w.va1);
     NCF_CHECK_LAUNCH("ncf_dedup_ids(init)");
   }
-  const int passes = passes_for(num_users, num_items);
+  const int passes = passes_for(rows0, rows1);
   uint32_t *ki0 = w.ka0, *vi0 = w.va0, *ki1 = w.ka1, *vi1 = w.va1;
   uint32_t *ko0 = w.kb0, *vo0 = w.vb0, *ko1 = w.kb1, *vo1 = w.vb1;
   for (int p = 0; p < passes; ++p) {
     const int shift = 8 * p;
     if (n > 0) {
-      hipLaunchKernelGGL(k_hist, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n, shift, w.nb, w.hist);
+      hipLaunchKernelGGL(k_hist, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n0, n1, shift, w.nb,
+                         w.hist);
       hipLaunchKernelGGL(k_scan_u32, dim3(2), dim3(1024), 0, st, w.hist, (int64_t)256 * w.nb,
                          (uint32_t*)nullptr);
-      hipLaunchKernelGGL(k_scatter, dim3(w.nb, 2), dim3(256), 0, st, ki0, vi0, ki1, vi1, n, shift,
-                         w.nb, w.hist, ko0, vo0, ko1, vo1);
+      hipLaunchKernelGGL(k_scatter, dim3(w.nb, 2), dim3(256), 0, st, ki0, vi0, ki1, vi1, n0, n1,
+                         shift, w.nb, w.hist, ko0, vo0, ko1, vo1);
       NCF_CHECK_LAUNCH("ncf_dedup_ids(sort)");
     }
     uint32_t* t;
@@ -481,14 +641,25 @@ extern "C" int ncf_dedup_ids(const int64_t* user_ids, const int64_t* item_ids, i
     t = ki1; ki1 = ko1; ko1 = t;
     t = vi1; vi1 = vo1; vo1 = t;
   }
-  hipLaunchKernelGGL(k_seg_count, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n, w.nb, w.segcnt);
+  hipLaunchKernelGGL(k_seg_count, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n0, n1, w.nb,
+                     w.segcnt);
   hipLaunchKernelGGL(k_scan_u32, dim3(2), dim3(1024), 0, st, w.segcnt, (int64_t)w.nb, w.totals);
-  hipLaunchKernelGGL(k_seg_assign, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n, w.nb, w.segcnt,
-                     w.totals, w.start0, w.start1, uniq_users, uniq_items, slot_users, slot_items);
+  hipLaunchKernelGGL(k_seg_assign, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n0, n1, w.nb,
+                     w.segcnt, w.totals, w.start0, w.start1, uniq0, uniq1, slot0, slot1);
   NCF_CHECK_LAUNCH("ncf_dedup_ids(segments)");
   if (num_unique)
     (void)hipMemcpyAsync(num_unique, w.totals, 2 * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
   return NCF_OK;
+}
+
+extern "C" int ncf_dedup_ids(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
+                             int64_t dim, int64_t num_users, int64_t num_items,
+                             int64_t* uniq_users, int64_t* uniq_items, int32_t* slot_users,
+                             int32_t* slot_items, uint32_t* num_unique, void* workspace,
+                             int64_t workspace_bytes, void* stream) {
+  return ncf_dedup_ids2(user_ids, n, num_users, item_ids, n, num_items, dim, uniq_users,
+                        uniq_items, slot_users, slot_items, num_unique, workspace,
+                        workspace_bytes, stream);
 }
 
 // Phase 2: per unique id, sum the LN-output gradients of its occurrences (position order) and
@@ -565,5 +736,133 @@ extern "C" int ncf_slot_reset(const int64_t* uniq, const uint32_t* num_unique, i
   hipLaunchKernelGGL(k_slot_reset, dim3(ncf_cdiv(max_n, 256)), dim3(256), 0, (hipStream_t)stream,
                      uniq, num_unique, kind, slot, max_n);
   NCF_CHECK_LAUNCH("ncf_slot_reset");
+  return NCF_OK;
+}
+
+// ---- row-sharding C-ABI ---------------------------------------------------------------------
+// Stable partition of the first count[kind] unique ids by owner = id mod world (world <= 255):
+// send_ids in owner order, perm[j] = index of send_ids[j] in uniq, counts[kind*world + d].
+extern "C" int ncf_owner_bucket(const int64_t* uniq0, const int64_t* uniq1, const uint32_t* count,
+                                int64_t max_n, int world, int64_t* send0, int64_t* send1,
+                                int32_t* perm0, int32_t* perm1, int64_t* counts,
+                                void* workspace, int64_t workspace_bytes, void* stream) {
+  NCF_CHECK_ARG(world >= 1 && world <= 128 && max_n >= 0, "ncf_owner_bucket: bad world/size");
+  if (workspace_bytes < ws_bytes(max_n, 16)) {
+    ncf_set_error("ncf_owner_bucket: workspace too small");
+    return NCF_ERR_WORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  WS w = carve(workspace, max_n, 16);
+  const int64_t n = max_n;
+  if (n > 0) {
+    hipLaunchKernelGGL(k_owner_keys, dim3(ncf_cdiv(n, 256)), dim3(256), 0, st, uniq0, uniq1, count,
+                       n, world, w.ka0, w.va0, w.ka1, w.va1);
+    hipLaunchKernelGGL(k_hist, dim3(w.nb, 2), dim3(256), 0, st, w.ka0, w.ka1, n, n, 0, w.nb, w.hist);
+    hipLaunchKernelGGL(k_scan_u32, dim3(2), dim3(1024), 0, st, w.hist, (int64_t)256 * w.nb,
+                       (uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_scatter, dim3(w.nb, 2), dim3(256), 0, st, w.ka0, w.va0, w.ka1, w.va1, n, n,
+                       0, w.nb, w.hist, w.kb0, w.vb0, w.kb1, w.vb1);
+    hipLaunchKernelGGL(k_owner_finish, dim3(ncf_cdiv(n > 512 ? n : 512, 256)), dim3(256), 0, st,
+                       uniq0, uniq1, count, w.vb0, w.vb1, n, w.hist, w.nb, world, send0, send1,
+                       perm0, perm1, counts);
+    NCF_CHECK_LAUNCH("ncf_owner_bucket");
+  } else {
+    (void)hipMemsetAsync(counts, 0, sizeof(int64_t) * 2 * world, st);
+  }
+  return NCF_OK;
+}
+
+// inv[position] = compact index, for the dedup held in `workspace` (ncf_dedup_ids2, same args)
+extern "C" int ncf_dedup_inverse(int64_t n0, int64_t n1, int64_t rows0, int64_t rows1, int64_t dim,
+                                 int64_t* inv0, int64_t* inv1, void* workspace,
+                                 int64_t workspace_bytes, void* stream) {
+  const int64_t n = n0 > n1 ? n0 : n1;
+  if (workspace_bytes < ws_bytes(n, dim)) {
+    ncf_set_error("ncf_dedup_inverse: workspace too small");
+    return NCF_ERR_WORKSPACE;
+  }
+  if (n == 0) return NCF_OK;
+  WS w = carve(workspace, n, dim);
+  uint32_t *k0, *v0, *k1, *v1;
+  sorted_bufs(w, passes_for(rows0, rows1), &k0, &v0, &k1, &v1);
+  hipLaunchKernelGGL(k_seg_inverse, dim3(w.nb, 2), dim3(256), 0, (hipStream_t)stream, k0, k1, v0,
+                     v1, n0, n1, w.nb, w.segcnt, inv0, inv1);
+  NCF_CHECK_LAUNCH("ncf_dedup_inverse");
+  return NCF_OK;
+}
+
+// per unique row of the dedup in `workspace`, sum the [n][2D] rows of its occurrences
+extern "C" int ncf_segment_sum_rows(int64_t n0, int64_t n1, int64_t rows0, int64_t rows1,
+                                    int64_t dim, const float* src0, const float* src1,
+                                    float* ga0, float* gb0, float* ga1, float* gb1,
+                                    void* workspace, int64_t workspace_bytes, void* stream) {
+  const int64_t n = n0 > n1 ? n0 : n1;
+  if (workspace_bytes < ws_bytes(n, dim)) {
+    ncf_set_error("ncf_segment_sum_rows: workspace too small");
+    return NCF_ERR_WORKSPACE;
+  }
+  if (n == 0) return NCF_OK;
+  WS w = carve(workspace, n, dim);
+  uint32_t *k0, *v0, *k1, *v1;
+  sorted_bufs(w, passes_for(rows0, rows1), &k0, &v0, &k1, &v1);
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = ncf_cdiv(n * (dim / 4), 256) > 2048 ? 2048 : ncf_cdiv(n * (dim / 4), 256);
+  switch (dim) {
+#define SS(DD)                                                                                   \
+  case DD:                                                                                       \
+    hipLaunchKernelGGL(k_seg_sum_rows<DD>, dim3(blocks, 2), dim3(256), 0, st, v0, v1, w.start0,  \
+                       w.start1, w.totals, src0, src1, ga0, gb0, ga1, gb1);                      \
+    break;
+    SS(16) SS(32) SS(64) SS(128) SS(256)
+#undef SS
+    default: ncf_set_error("ncf_segment_sum_rows: dim"); return NCF_ERR_ARG;
+  }
+  NCF_CHECK_LAUNCH("ncf_segment_sum_rows");
+  return NCF_OK;
+}
+
+extern "C" int ncf_gather_shard_rows(const int64_t* ids, int64_t n, int world, const float* t0,
+                                     const float* t1, int64_t rows, int64_t dim, float* out,
+                                     int* err_flag, void* stream) {
+  if (n <= 0) return NCF_OK;
+  hipStream_t st = (hipStream_t)stream;
+  switch (dim) {
+#define GS(DD)                                                                                   \
+  case DD:                                                                                       \
+    hipLaunchKernelGGL(k_gather_shard<DD>, dim3(ncf_cdiv(n * (DD / 4), 256)), dim3(256), 0, st,  \
+                       ids, n, world, t0, t1, rows, out, err_flag);                              \
+    break;
+    GS(16) GS(32) GS(64) GS(128) GS(256)
+#undef GS
+    default: ncf_set_error("ncf_gather_shard_rows: dim"); return NCF_ERR_ARG;
+  }
+  NCF_CHECK_LAUNCH("ncf_gather_shard_rows");
+  return NCF_OK;
+}
+
+// dir 0: scatter [n][2D] rows into mini tables at perm; dir 1: pack mini rows at perm into [n][2D]
+extern "C" int ncf_perm_rows(float* rows, const int32_t* perm, int64_t n, int64_t dim, float* mini0,
+                             float* mini1, int dir, void* stream) {
+  if (n <= 0) return NCF_OK;
+  hipStream_t st = (hipStream_t)stream;
+  switch (dim) {
+#define PR(DD)                                                                                   \
+  case DD:                                                                                       \
+    hipLaunchKernelGGL(k_perm_rows<DD>, dim3(ncf_cdiv(n * (DD / 4), 256)), dim3(256), 0, st,     \
+                       rows, perm, n, mini0, mini1, dir);                                        \
+    break;
+    PR(16) PR(32) PR(64) PR(128) PR(256)
+#undef PR
+    default: ncf_set_error("ncf_perm_rows: dim"); return NCF_ERR_ARG;
+  }
+  NCF_CHECK_LAUNCH("ncf_perm_rows");
+  return NCF_OK;
+}
+
+extern "C" int ncf_ids_div(const int64_t* ids, int64_t n, int world, int64_t* out, void* stream) {
+  if (n <= 0) return NCF_OK;
+  hipLaunchKernelGGL(k_ids_div, dim3(ncf_cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, ids, n,
+                     world, out);
+  NCF_CHECK_LAUNCH("ncf_ids_div");
   return NCF_OK;
 }

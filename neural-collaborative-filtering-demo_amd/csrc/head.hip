@@ -153,8 +153,8 @@ extern "C" int ncf_head_bwd(const float* prob, const float* grad_prob, const flo
                             const float* mf_out_w, float* grad_mlp_last, float* grad_mf_user_ln,
                             float* grad_mf_item_ln, float* grad_mlp_out_w, float* grad_mlp_out_b,
                             float* grad_mf_out_w, float* grad_mf_out_b, float* grad_final_w,
-                            float* grad_final_b, float* loss, float* workspace,
-                            int64_t workspace_floats, void* stream) {
+                            float* grad_final_b, float* loss, double loss_denominator,
+                            float* workspace, int64_t workspace_floats, void* stream) {
   NCF_CHECK_ARG(n >= 0 && width >= 1 && width <= 256 && dim >= 1 && dim <= 256,
                 "ncf_head_bwd: bad size (width, dim <= 256)");
   NCF_CHECK_ARG((grad_prob != nullptr) != (targets != nullptr),
@@ -165,7 +165,9 @@ extern "C" int ncf_head_bwd(const float* prob, const float* grad_prob, const flo
   }
   hipStream_t st = (hipStream_t)stream;
   const int nb = n == 0 ? 1 : ncf_cdiv(n, ROWS_PER_BLOCK);
-  const float inv_n = n > 0 ? 1.0f / (float)n : 0.0f;
+  // mean over `loss_denominator` samples (the global batch under data parallelism), else over n
+  const double den = loss_denominator > 0 ? loss_denominator : (double)n;
+  const float inv_n = den > 0 ? (float)(1.0 / den) : 0.0f;
   hipLaunchKernelGGL(k_head_bwd, dim3(nb), dim3(256), 0, st, prob, grad_prob, targets, inv_n,
                      mf_pred, mlp_pred, mlp_last, (int)width, mlp_out_w, final_w, mf_user_ln,
                      mf_item_ln, (int)dim, mf_out_w, n, grad_mlp_last, grad_mf_user_ln,

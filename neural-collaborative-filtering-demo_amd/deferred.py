@@ -11,8 +11,9 @@ its p / exp_avg / exp_avg_sq reflect).  A step then
   2. catches up exactly those rows by replaying their missed zero-gradient steps
      (``ncf_adam_rows_catchup``) so the forward gathers current values,
   3. after the backward applies this step's real gradient to those rows (``ncf_adam_rows_apply``),
-  4. every ``sweep_every`` steps (and whenever anything else reads the tables: state_dict,
-     eval forward, embedding export) sweeps the whole table current (``ncf_adam_sweep``).
+  4. a rolling sweep brings one 1/``sweep_every`` slice of every table current each step (no row
+     is ever more than ``sweep_every`` steps behind), and the whole table is swept before
+     anything else reads it (state_dict, eval forward, embedding export) (``ncf_adam_sweep``).
 Every replayed step uses the per-step fp32 scalars of the dense kernel and the same
 contraction-free arithmetic, so the result is bit-identical to the dense sweep (tested); the
 work moves from HBM traffic (24 B/element/step) to VALU (~15 flops/element/step, amortised).
@@ -78,6 +79,41 @@ class DeferredTableAdam:
         return (ptr(self.tables[a]), ptr(s[a]["exp_avg"]), ptr(s[a]["exp_avg_sq"]),
                 ptr(self.tables[b]), ptr(s[b]["exp_avg"]), ptr(s[b]["exp_avg_sq"]))
 
+    # ---- row-list primitives (also used by the row-sharded step)
+    def catchup_rows(self, kind, row_ids, count_dev, kind_index, max_n, st):
+        """Bring the listed unique rows of `kind` current through step self.t."""
+        if self.t == 0 or max_n <= 0:
+            return
+        self._ensure(self.t)
+        _lib.call("ncf_adam_rows_catchup", *self._ptrs(kind), self.engine.model.mlp_embedding_dim,
+                  ptr(row_ids), ptr(count_dev), kind_index, max_n, ptr(self.stamp[kind]), self.t,
+                  ptr(self._table), *self._consts(), st)
+
+    def apply_rows(self, kind, row_ids, count_dev, kind_index, max_n, g_mf, g_mlp, st):
+        """Step self.t + 1 on the listed rows (current through self.t) with their gradients."""
+        step = self.t + 1
+        self._ensure(step)
+        if max_n <= 0:
+            return
+        p0, m0, v0, p1, m1, v1 = self._ptrs(kind)
+        _lib.call("ncf_adam_rows_apply", p0, m0, v0, ptr(g_mf), p1, m1, v1, ptr(g_mlp),
+                  self.engine.model.mlp_embedding_dim, ptr(row_ids), ptr(count_dev), kind_index,
+                  max_n, ptr(self.stamp[kind]), step, ptr(self._table), *self._consts(), st)
+
+    def advance(self, st):
+        """Close step self.t + 1 (after apply_rows of every kind), then the rolling sweep: one
+        1/sweep_every slice of every table is brought current each step, so no row is ever more
+        than sweep_every steps behind and the catch-up work is spread evenly over the steps."""
+        self.t += 1
+        self.engine.pending = None
+        if self.sweep_every:
+            k = self.t % self.sweep_every
+            for kind in ("user", "item"):
+                rows = self.stamp[kind].numel()
+                sl = (rows + self.sweep_every - 1) // self.sweep_every
+                r0 = k * sl
+                self._sweep_range(kind, r0, max(0, min(rows, r0 + sl) - r0), st)
+
     # ---- engine hook: before the gathers of a training step
     def prepare(self, w, uid, iid, st):
         eng = self.engine
@@ -87,35 +123,27 @@ class DeferredTableAdam:
                   ptr(w.uniq_u), ptr(w.uniq_i), None, None, ptr(w.num_unique), ptr(w.emb_ws),
                   w.emb_ws.numel(), st)
         w.deduped = True
-        if self.t > 0:
-            self._ensure(self.t)
-            for kind, uniq in (("user", w.uniq_u), ("item", w.uniq_i)):
-                _lib.call("ncf_adam_rows_catchup", *self._ptrs(kind), w.g.D, ptr(uniq),
-                          ptr(w.num_unique), 0 if kind == "user" else 1, n,
-                          ptr(self.stamp[kind]), self.t, ptr(self._table), *self._consts(), st)
+        self.catchup_rows("user", w.uniq_u, w.num_unique, 0, n, st)
+        self.catchup_rows("item", w.uniq_i, w.num_unique, 1, n, st)
 
     # ---- after the backward: this step's gradient on the touched rows
     def apply(self, w, st):
-        step = self.t + 1
-        self._ensure(step)
         n = w.g.n
-        for kind, uniq, (ga, gb) in (("user", w.uniq_u, ("mf_user", "mlp_user")),
-                                     ("item", w.uniq_i, ("mf_item", "mlp_item"))):
-            p0, m0, v0, p1, m1, v1 = self._ptrs(kind)
-            _lib.call("ncf_adam_rows_apply", p0, m0, v0, ptr(w.G[ga]), p1, m1, v1, ptr(w.G[gb]),
-                      w.g.D, ptr(uniq), ptr(w.num_unique), 0 if kind == "user" else 1, n,
-                      ptr(self.stamp[kind]), step, ptr(self._table), *self._consts(), st)
-        self.t = step
-        self.engine.pending = None
-        if self.sweep_every and step % self.sweep_every == 0:
-            self._sweep(st)
+        self.apply_rows("user", w.uniq_u, w.num_unique, 0, n, w.G["mf_user"], w.G["mlp_user"], st)
+        self.apply_rows("item", w.uniq_i, w.num_unique, 1, n, w.G["mf_item"], w.G["mlp_item"], st)
+        self.advance(st)
+
+    def _sweep_range(self, kind, row0, rows, st):
+        if rows <= 0 or self.t == 0:
+            return
+        self._ensure(self.t)
+        _lib.call("ncf_adam_sweep", *self._ptrs(kind), row0, rows,
+                  self.engine.model.mlp_embedding_dim, ptr(self.stamp[kind]), self.t,
+                  ptr(self._table), *self._consts(), st)
 
     def _sweep(self, st):
-        self._ensure(self.t)
         for kind in ("user", "item"):
-            rows = self.stamp[kind].numel()
-            _lib.call("ncf_adam_sweep", *self._ptrs(kind), rows, self.engine.model.mlp_embedding_dim,
-                      ptr(self.stamp[kind]), self.t, ptr(self._table), *self._consts(), st)
+            self._sweep_range(kind, 0, self.stamp[kind].numel(), st)
         self.synced_t = self.t
 
     def sync(self):

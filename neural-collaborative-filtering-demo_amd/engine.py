@@ -219,7 +219,7 @@ class NCFEngine:
             self.deferred.sync()
 
     def forward(self, uid: torch.Tensor, iid: torch.Tensor, M: int, train: bool,
-                drop_p: float, seed: int, prepare=None) -> Workspace:
+                drop_p: float, seed: int, prepare=None, tables=None, rows=None) -> Workspace:
         """AdvancedNCF.forward (architecture.py:258-381) on single-id bags; returns the workspace
         holding prob (and, when ``train``, everything the backward needs).  ``prepare(w, uid,
         iid, stream)`` runs before the gathers (the deferred Adam dedups the ids there and
@@ -240,7 +240,8 @@ class NCFEngine:
         D, H, T, hid = m.mlp_embedding_dim, m.num_heads, m.temporal_dim, list(m.mlp_hidden_dims)
         if m.mf_embedding_dim != D:
             raise NotImplementedError("mf_embedding_dim must equal mlp_embedding_dim on this path")
-        tb = self.table_params()
+        tb = tables or self.table_params()
+        n_users, n_items = rows or (m.num_users, m.num_products)
         w.err.zero_()
         w.deduped = False
         if prepare is not None:
@@ -249,8 +250,8 @@ class NCFEngine:
             self.sync_tables()
         # a2-a4: 4 gathers + mf_norm/mlp_norm + GMF  (architecture.py:286-287, 305-312)
         _lib.call("ncf_gather_ln_gmf_fwd", ptr(uid), ptr(iid), n, ptr(tb["mf_user"]),
-                  ptr(tb["mf_item"]), ptr(tb["mlp_user"]), ptr(tb["mlp_item"]), m.num_users,
-                  m.num_products, D, ptr(m.mf_norm.weight), ptr(m.mf_norm.bias),
+                  ptr(tb["mf_item"]), ptr(tb["mlp_user"]), ptr(tb["mlp_item"]), n_users,
+                  n_items, D, ptr(m.mf_norm.weight), ptr(m.mf_norm.bias),
                   ptr(m.mlp_norm.weight), ptr(m.mlp_norm.bias), ptr(m.mf_output.weight),
                   ptr(m.mf_output.bias), LN_EPS, ptr(w.mf_pred), ptr(w.xu), ptr(w.xi),
                   ptr(w.umf), ptr(w.imf), ptr(w.err), st)
@@ -291,7 +292,8 @@ class NCFEngine:
 
     # ------------------------------------------------------------------ backward
     def backward(self, w: Workspace, uid, iid, grad_prob: Optional[torch.Tensor],
-                 targets: Optional[torch.Tensor], drop_p: float, seed: int):
+                 targets: Optional[torch.Tensor], drop_p: float, seed: int,
+                 loss_denominator: float = 0.0, tables=None, rows=None, uniq=None):
         """Gradients of every used parameter.  Dense grads land in the flat grad buffer; table
         grads stay compact (self.pending) for the fused Adam step."""
         m = self.model
@@ -311,7 +313,7 @@ class NCFEngine:
                   ptr(w.dimf), ptr(gv("mlp_output.weight")), ptr(gv("mlp_output.bias")),
                   ptr(gv("mf_output.weight")), ptr(gv("mf_output.bias")),
                   ptr(gv("final.0.weight")), ptr(gv("final.0.bias")), ptr(w.loss),
-                  ptr(w.scratch), w.scratch.numel(), st)
+                  float(loss_denominator), ptr(w.scratch), w.scratch.numel(), st)
         # a7 backward, last layer first
         for l in reversed(range(len(hid))):
             h = hid[l]
@@ -344,15 +346,17 @@ class NCFEngine:
         self._gemm(w.dk, D, 0, att.k_proj.weight, D, 0, w.dxi, D, n, D, D, st=st)
         self._gemm(w.dv, D, 0, att.v_proj.weight, D, 0, w.dxi, D, n, D, D, accum=True, st=st)
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)
-        tb = self.table_params()
+        tb = tables or self.table_params()
         G = w.G
+        uq_u, uq_i = uniq if uniq is not None else (w.uniq_u, w.uniq_i)
+        d_rows = rows or (m.num_users, m.num_products)
         if getattr(w, "deduped", False):   # ids already sorted/deduplicated before the forward
-            _lib.call("ncf_embedding_bwd_reduce", n, D, m.num_users, m.num_products,
+            _lib.call("ncf_embedding_bwd_reduce", n, D, d_rows[0], d_rows[1],
                       ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), ptr(tb["mf_user"]),
                       ptr(tb["mlp_user"]), ptr(tb["mf_item"]), ptr(tb["mlp_item"]),
                       ptr(m.mf_norm.weight), ptr(m.mlp_norm.weight), LN_EPS, ptr(G["mf_user"]),
-                      ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(w.uniq_u),
-                      ptr(w.uniq_i), ptr(gv("mf_norm.weight")), ptr(gv("mf_norm.bias")),
+                      ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(uq_u),
+                      ptr(uq_i), ptr(gv("mf_norm.weight")), ptr(gv("mf_norm.bias")),
                       ptr(gv("mlp_norm.weight")), ptr(gv("mlp_norm.bias")), ptr(w.emb_ws),
                       w.emb_ws.numel(), st)
             self.pending = w

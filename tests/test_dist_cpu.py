@@ -1,0 +1,189 @@
+"""World-size-2 gloo test of the row-sharded data-parallel step on CPU.
+
+It runs the product's exchange protocol (ncf_amd.distributed.ShardExchange + ShardedTrainStep:
+count/id/row/gradient all-to-alls, global-mean loss scaling, dense all-reduce, owner-side
+gradient sums) with a torch reference backend for the per-rank kernels (test infrastructure: the
+HIP kernels need a GPU), and checks the SURVEY §8(e) parity criterion: a 2-rank step on a global
+batch equals the 1-rank step on the concatenated batch (oracle, same init)."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.parity import assert_params_close
+
+U, I, D, T, H, HID, B, M = 97, 41, 16, 8, 2, [32, 16], 6, 5
+TABLES = {"mf_user": "mf_embedding_collection.embedding_bags.user_id.weight",
+          "mlp_user": "mlp_embedding_collection.embedding_bags.user_id.weight",
+          "mf_item": "mf_embedding_collection.embedding_bags.product_id.weight",
+          "mlp_item": "mlp_embedding_collection.embedding_bags.product_id.weight"}
+
+
+def global_setup():
+    import _ncf_pkg
+    ncf = _ncf_pkg.load()
+    torch.manual_seed(0)
+    m = ncf.AdvancedNCF(U, I, 5, 24, D, D, T, HID, H, 0.0, M - 1)
+    params = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(1)
+    batches = []
+    for _ in range(2):           # 2 steps x 2 ranks
+        per_rank = []
+        for _r in range(2):
+            u = torch.randint(0, U, (B,), generator=g).repeat_interleave(M)
+            i = torch.randint(0, I, (B * M,), generator=g)
+            t = torch.zeros(B, M)
+            t[:, 0] = 1
+            per_rank.append((u, i, t.reshape(-1, 1)))
+        batches.append(per_rank)
+    return params, batches
+
+
+class TorchShardOps:
+    """Reference backend (CPU, oracle math) implementing HipShardOps' interface."""
+
+    def __init__(self, params, rank, world):
+        from oracle import ncf_oracle as O
+        self.O = O
+        self.rank, self.W = rank, world
+        self.names = O.used_param_names(list(params), len(HID))
+        self.p = {k: v.clone() for k, v in params.items()}
+        for key, name in TABLES.items():
+            self.p[name] = params[name][rank::world].clone()      # rows with id % W == rank
+        self.dense_names = [k for k in self.names if k not in TABLES.values()]
+        self.opt = O.AdamState(lr=1e-3, weight_decay=1e-5)
+
+    def dedup(self, uid, iid):
+        uu, iu = torch.unique(uid, return_inverse=True)
+        ui, ii = torch.unique(iid, return_inverse=True)
+        return {"uniq": (uu, ui), "inv": (iu, ii), "n": uid.numel()}
+
+    def bucket(self, ded, world):
+        from ncf_amd.distributed import Plan
+        send, perm, counts = [], [], []
+        for uq in ded["uniq"]:
+            owner = uq % world
+            order = torch.sort(owner, stable=True).indices
+            send.append(uq[order])
+            perm.append(order)
+            counts.append(torch.bincount(owner, minlength=world).tolist())
+        return Plan(send=send, perm=perm, counts=counts)
+
+    def owner_prepare(self, recv):
+        return {"local": [r // self.W for r in recv]}
+
+    def owner_gather(self, own, k, recv_ids):
+        a, b = (TABLES["mf_user"], TABLES["mlp_user"]) if k == 0 else (TABLES["mf_item"], TABLES["mlp_item"])
+        loc = own["local"][k]
+        return torch.cat([self.p[a][loc], self.p[b][loc]], 1)
+
+    def compute(self, ded, plan, back, uid, iid, targets, loss_denominator):
+        O = self.O
+        leaves = {}
+        for k, (a, b) in enumerate(((TABLES["mf_user"], TABLES["mlp_user"]),
+                                    (TABLES["mf_item"], TABLES["mlp_item"]))):
+            c = len(ded["uniq"][k])
+            ma, mb = torch.empty(c, D), torch.empty(c, D)
+            ma[plan.perm[k]] = back[k][:, :D]
+            mb[plan.perm[k]] = back[k][:, D:]
+            leaves[a], leaves[b] = ma.requires_grad_(True), mb.requires_grad_(True)
+        for k in self.dense_names:
+            leaves[k] = self.p[k].clone().requires_grad_(True)
+        full = dict(self.p)
+        full.update(leaves)
+        inv_u, inv_i = ded["inv"]
+        prob = O.forward(full, inv_u, inv_i, training=True, negative_samples=M - 1, num_heads=H,
+                         temporal_dim=T, n_layers=len(HID))
+        loss = O.bce_loss(prob, targets) * (ded["n"] / loss_denominator)
+        keys = list(leaves)
+        gr = dict(zip(keys, torch.autograd.grad(loss, [leaves[k] for k in keys])))
+        self.dgrad = torch.cat([gr[k].reshape(-1) for k in self.dense_names])
+        out = []
+        for k, (a, b) in enumerate(((TABLES["mf_user"], TABLES["mlp_user"]),
+                                    (TABLES["mf_item"], TABLES["mlp_item"]))):
+            out.append(torch.cat([gr[a][plan.perm[k]], gr[b][plan.perm[k]]], 1))
+        return out, loss.detach()
+
+    def owner_apply(self, own, got):
+        self.tgrad = {}
+        for k, (a, b) in enumerate(((TABLES["mf_user"], TABLES["mlp_user"]),
+                                    (TABLES["mf_item"], TABLES["mlp_item"]))):
+            ga, gb = torch.zeros_like(self.p[a]), torch.zeros_like(self.p[b])
+            ga.index_add_(0, own["local"][k], got[k][:, :D])
+            gb.index_add_(0, own["local"][k], got[k][:, D:])
+            self.tgrad[a], self.tgrad[b] = ga, gb
+
+    def dense_grad(self):
+        return self.dgrad
+
+    def dense_step(self):
+        grads, o = dict(self.tgrad), 0
+        for k in self.dense_names:
+            n = self.p[k].numel()
+            grads[k] = self.dgrad[o:o + n].view_as(self.p[k])
+            o += n
+        self.opt.step(self.p, grads)
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import _ncf_pkg
+    _ncf_pkg.load()
+    from ncf_amd.distributed import ShardExchange, ShardedTrainStep
+    params, batches = global_setup()
+    ops = TorchShardOps(params, rank, world)
+    step = ShardedTrainStep(ops, ShardExchange(None, torch.device("cpu")))
+    losses = []
+    for s in range(len(batches)):
+        u, i, t = batches[s][rank]
+        losses.append(float(step(u, i, t)))
+    torch.save({"p": ops.p, "losses": losses}, os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sharded_step_equals_single_rank_global_batch():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+    from oracle import ncf_oracle as O
+    params, batches = global_setup()
+    ref = {k: v.clone() for k, v in params.items()}
+    opt = O.AdamState(lr=1e-3, weight_decay=1e-5)
+    g0 = None
+    for s in range(len(batches)):
+        u = torch.cat([b[0] for b in batches[s]])
+        i = torch.cat([b[1] for b in batches[s]])
+        t = torch.cat([b[2] for b in batches[s]])
+        _, loss, grads = O.train_step(ref, opt, u, i, t, negative_samples=M - 1, num_heads=H,
+                                      temporal_dim=T, n_layers=len(HID))
+        g0 = g0 or {k: (v + 1e-5 * params[k]).numpy() for k, v in grads.items()}
+        # the global loss is the sum of the ranks' contributions
+        assert abs(sum(r["losses"][s] for r in res) - float(loss)) < 1e-5
+    for name, gv in g0.items():
+        if name in TABLES.values():
+            got = torch.empty_like(ref[name])
+            for r in range(world):
+                got[r::world] = res[r]["p"][name]
+        else:
+            got = res[0]["p"][name]
+            assert torch.equal(got, res[1]["p"][name]), name     # replicas stay identical
+        assert_params_close(name, got.numpy(), ref[name].numpy(), gv, 1e-3, 2, atol=2e-6)

@@ -447,3 +447,43 @@ def test_fused_step_matches_dropin_path(f2):
     for k, v in sub(g, f"after{steps - 1}/param/").items():
         geff = g["grad0/" + k] + wd * g["init/" + k]
         assert_params_close(k, sd[k].cpu().numpy(), v, geff, lr, steps)
+
+
+# ----------------------------------------------------------------------------- sharded (RCCL)
+def test_sharded_step_world1_bitwise_equals_fused():
+    """The row-sharded DP step (owner bucketing, all-to-alls over RCCL, mini tables, owner-side
+    sums, deferred Adam on the shard) at world size 1 reproduces FusedTrainStep bit for bit; the
+    world > 1 protocol itself is covered by tests/test_dist_cpu.py (gloo, 2 ranks)."""
+    import socket
+    import torch.distributed as dist
+    from ncf_amd.distributed import make_sharded_step
+    from ncf_amd.trainer import FusedTrainStep
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        U, I, Bg = 2000, 300, 64
+
+        def factory(ru, ri):
+            torch.manual_seed(5)
+            return ncf.AdvancedNCF(ru, ri, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.0, 4).to(DEV).train()
+        ms, sharded = make_sharded_step(factory, U, I, lr=1e-3, weight_decay=1e-5)
+        mf = factory(U, I)
+        fused = FusedTrainStep(mf, lr=1e-3, weight_decay=1e-5)
+        g = torch.Generator().manual_seed(6)
+        for _ in range(5):
+            u = torch.randint(0, U, (Bg,), generator=g).repeat_interleave(5).to(DEV)
+            i = (torch.rand(Bg * 5, generator=g) ** 3 * I).long().to(DEV)
+            t = torch.zeros(Bg, 5)
+            t[:, 0] = 1
+            t = t.reshape(-1, 1).to(DEV)
+            l1 = sharded(u, i, t)
+            fused(u, i, t)
+            assert abs(float(l1.item()) - float(fused.last_loss.item())) < 1e-6
+        a, b = ms.state_dict(), mf.state_dict()
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+    finally:
+        dist.destroy_process_group()
