@@ -180,7 +180,7 @@ def main():
     for name, a, e0, e1 in prof:
         per.setdefault(name, []).append((a, e0.elapsed_time(e1)))
     totals = {k: sum(d for _, d in v) / args.steps for k, v in per.items()}   # ms per step
-    gemm_names = ("ncf_gemm_f32", "ncf_gemm_f32_splitk")
+    gemm_names = ("ncf_gemm_direct", "ncf_gemm_f32", "ncf_gemm_f32_splitk")
     gemm_ms = sum(totals.get(k, 0.0) for k in gemm_names)
     gemm_flops = sum(2.0 * a[0] * a[1] * a[2] for k in gemm_names for a, _ in per.get(k, [])) / args.steps
     gemm_launches = sum(len(per.get(k, [])) for k in gemm_names) / args.steps
@@ -233,8 +233,9 @@ def main():
                        "global_batch": N * world, "groups_per_gpu": B, "samples_per_group": M,
                        "parallelism": (f"dp{world} + row-sharded tables (RCCL all-to-all), "
                                        "dense all-reduce") if sharded else "single-gpu"},
-            "roofline": {"bound": "mfma", "kernel": "k_gemm_f32 (fp32 MFMA v_mfma_f32_32x32x2_f32; "
-                                                    "all attention/MLP GEMM launches of a step)",
+            "roofline": {"bound": "mfma", "kernel": "k_gemm_f32 + k_gemm_direct (fp32 MFMA "
+                                                    "v_mfma_f32_32x32x2_f32; all attention/MLP "
+                                                    "GEMM launches of a step)",
                          "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
                          "flops_per_step": gemm_flops, "launches_per_step": gemm_launches,

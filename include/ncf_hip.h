@@ -60,12 +60,49 @@ int ncf_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t r
 int ncf_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int a_trans,
                  const float* B, int64_t ldb, int b_trans, float* C, int64_t ldc,
                  const float* bias, int flags, void* stream);
+/* LDS-free variant for the square DxD attention projections: one wave per 32x32 tile, MFMA
+ * operands loaded straight from global memory (k permuted per 64-chunk so contiguous operands
+ * are float4 runs and strided ones are coalesced per step).  Same convention as ncf_gemm_f32. */
+int ncf_gemm_direct(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int a_trans,
+                    const float* B, int64_t ldb, int b_trans, float* C, int64_t ldc,
+                    const float* bias, int flags, void* stream);
+
+/* ---- deferred reductions --------------------------------------------------------------------
+ * Every backward call that produces a parameter gradient as a sum over batch rows writes
+ * per-block partial rows and reduces them in a fixed order (bitwise reproducible, no float
+ * atomics).  Given a non-NULL `defer` list such a call APPENDS its reduction(s) to the list
+ * instead of launching them — its workspace then holds the partials and must stay untouched
+ * until ncf_reduce_batch() has run every listed reduction (two launches for the whole list).
+ * The weight/bias gradients are off the backward's critical path, so a training step pays two
+ * launches for all of them instead of ~40.                                                   */
+typedef struct ncf_reduce_desc {
+  const float* part;  /* P partial rows, row p at part + p*stride, L floats each               */
+  float* out;         /* element i -> out[(i / cols) * ldo + i % cols]                        */
+  int64_t stride;
+  int64_t ldo;
+  int32_t L, cols, P, accumulate;
+  float scale;        /* out = scale * sum (+ previous out when accumulate)                  */
+  int32_t reserved;
+} ncf_reduce_desc;
+#define NCF_REDUCE_LIST_MAX 64
+typedef struct ncf_reduce_list {
+  int32_t count;
+  int32_t reserved;
+  ncf_reduce_desc d[NCF_REDUCE_LIST_MAX];
+} ncf_reduce_list;
+int64_t ncf_reduce_batch_scratch(const ncf_reduce_list* list);
+int ncf_reduce_batch(const ncf_reduce_list* list, float* scratch, int64_t scratch_floats,
+                     void* stream);
+
 int64_t ncf_gemm_splitk_workspace(int64_t M, int64_t N, int splits);
-/* Long-K GEMM for weight gradients (dW = dYᵀ·X over the batch), deterministic slab reduce. */
+/* Long-K GEMM for weight gradients (dW = dYᵀ·X over the batch): K split into `splits` slabs
+ * reduced in slab order.  row_sums (nullable) receives sum_k A(i,k) from the same pass — the
+ * bias gradient when A = dYᵀ.  defer: see above.                                            */
 int ncf_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                         int a_trans, const float* B, int64_t ldb, int b_trans, float* C,
-                        int64_t ldc, int accumulate, int splits, float* workspace,
-                        int64_t workspace_floats, void* stream);
+                        int64_t ldc, int accumulate, float* row_sums, int splits,
+                        float* workspace, int64_t workspace_floats, ncf_reduce_list* defer,
+                        void* stream);
 int64_t ncf_colsum_workspace(int64_t rows, int64_t cols);
 /* Bias gradients: out[c] (+)= sum_r X[r*ld+c]. */
 int ncf_colsum(const float* X, int64_t rows, int64_t cols, int64_t ld, float* out,
@@ -107,7 +144,7 @@ int ncf_relu_ln_dropout_bwd(const float* grad_out, const float* relu_in, const f
                             const float* rstd, const float* gamma, int64_t n, int64_t width,
                             float dropout_p, uint64_t seed, float* grad_lin, float* grad_gamma,
                             float* grad_beta, float* grad_bias, float* workspace,
-                            int64_t workspace_floats, void* stream);
+                            int64_t workspace_floats, ncf_reduce_list* defer, void* stream);
 
 /* ---- a8 + a12: mlp_output + final Linear(2,1) + Sigmoid (+ fused BCELoss) -----------------
  * Replaces architecture.py:345, :353-354 and nn.BCELoss (trainer.py:78, :271).  With fused
@@ -124,7 +161,7 @@ int ncf_head_bwd(const float* prob, const float* grad_prob, const float* targets
                  float* grad_mf_item_ln, float* grad_mlp_out_w, float* grad_mlp_out_b,
                  float* grad_mf_out_w, float* grad_mf_out_b, float* grad_final_w,
                  float* grad_final_b, float* loss, double loss_denominator, float* workspace,
-                 int64_t workspace_floats, void* stream);
+                 int64_t workspace_floats, ncf_reduce_list* defer, void* stream);
 
 /* ---- a2/a3 backward: sparse segment-reduce + LayerNorm backward ----------------------------
  * Replaces _embedding_bag_dense_backward (+ sort) of the four EBC tables and the mf_norm /
@@ -170,7 +207,7 @@ int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_users, int64_t 
                              float* grad_mf_item, float* grad_mlp_item, const int64_t* uniq_users,
                              const int64_t* uniq_items, float* grad_mf_gamma, float* grad_mf_beta,
                              float* grad_mlp_gamma, float* grad_mlp_beta, void* workspace,
-                             int64_t workspace_bytes, void* stream);
+                             int64_t workspace_bytes, ncf_reduce_list* defer, void* stream);
 int ncf_slot_reset(const int64_t* uniq, const uint32_t* num_unique, int kind, int32_t* slot,
                    int64_t max_n, void* stream);
 /* dense[uniq[c]] = grad_compact[c] (materialise a dense table gradient for non-Adam users). */

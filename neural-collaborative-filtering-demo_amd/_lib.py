@@ -39,19 +39,23 @@ SIGNATURES = {
     "ncf_gather_rows": (I32, [P, I64, P, I64, I64, P, P, F32, P, P, P]),
     "ncf_gemm_f32": (I32, [I64, I64, I64, P, I64, I32, P, I64, I32, P, I64, P, I32, P]),
     "ncf_gemm_splitk_workspace": (I64, [I64, I64, I32]),
-    "ncf_gemm_f32_splitk": (I32, [I64, I64, I64, P, I64, I32, P, I64, I32, P, I64, I32, I32, P,
-                                  I64, P]),
+    "ncf_gemm_f32_splitk": (I32, [I64, I64, I64, P, I64, I32, P, I64, I32, P, I64, I32, P, I32,
+                                  P, I64, P, P]),
+    "ncf_gemm_direct": (I32, [I64, I64, I64, P, I64, I32, P, I64, I32, P, I64, P, I32, P]),
+    "ncf_reduce_batch_scratch": (I64, [P]),
+    "ncf_reduce_batch": (I32, [P, P, I64, P]),
     "ncf_colsum_workspace": (I64, [I64, I64]),
     "ncf_colsum": (I32, [P, I64, I64, I64, P, I32, P, I64, P]),
     "ncf_attention_fwd": (I32, [P, P, P, I64, I64, I64, I64, F32, U64, P, P, P]),
     "ncf_attention_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P, P]),
     "ncf_relu_ln_dropout_fwd": (I32, [P, I64, I64, P, P, F32, F32, U64, P, P, P, P]),
     "ncf_relu_ln_dropout_bwd_workspace": (I64, [I64, I64]),
-    "ncf_relu_ln_dropout_bwd": (I32, [P, P, P, P, P, I64, I64, F32, U64, P, P, P, P, P, I64, P]),
+    "ncf_relu_ln_dropout_bwd": (I32, [P, P, P, P, P, I64, I64, F32, U64, P, P, P, P, P, I64, P,
+                                      P]),
     "ncf_head_fwd": (I32, [P, I64, I64, P, P, P, P, P, P, P, P]),
     "ncf_head_bwd_workspace": (I64, [I64, I64, I64]),
     "ncf_head_bwd": (I32, [P, P, P, P, P, P, I64, I64, P, P, P, P, I64, P, P, P, P, P, P, P, P,
-                           P, P, P, F64, P, I64, P]),
+                           P, P, P, F64, P, I64, P, P]),
     "ncf_embedding_bwd_workspace": (I64, [I64, I64]),
     "ncf_embedding_bwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
                                 P, P, P, P, P, P, P, P, P, P, P, P, I64, P]),
@@ -64,7 +68,7 @@ SIGNATURES = {
     "ncf_perm_rows": (I32, [P, P, I64, I64, P, P, I32, P]),
     "ncf_segment_sum_rows": (I32, [I64, I64, I64, I64, I64, P, P, P, P, P, P, P, I64, P]),
     "ncf_embedding_bwd_reduce": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
-                                       P, P, P, P, P, P, P, P, P, I64, P]),
+                                       P, P, P, P, P, P, P, P, P, I64, P, P]),
     "ncf_slot_reset": (I32, [P, P, I32, P, I64, P]),
     "ncf_scatter_compact_rows": (I32, [P, I64, P, P, I32, P, I64, P]),
     "ncf_adam_table": (I32, [P, P, P, I64, I64, P, P, F64, F64, F64, F64, F64, F64, P]),
@@ -79,6 +83,27 @@ SIGNATURES = {
     "ncf_temporal_fwd": (I32, [P, P, P, P, I64, P, P, P, P, I64, I64, P, P, P]),
     "ncf_temporal_bwd": (I32, [P, P, P, I64, P, I64, P, P, P, P]),
 }
+
+
+class ReduceDesc(ctypes.Structure):
+    """ncf_reduce_desc (include/ncf_hip.h)."""
+    _fields_ = [("part", P), ("out", P), ("stride", I64), ("ldo", I64), ("L", ctypes.c_int32),
+                ("cols", ctypes.c_int32), ("P", ctypes.c_int32), ("accumulate", ctypes.c_int32),
+                ("scale", F32), ("reserved", ctypes.c_int32)]
+
+
+REDUCE_LIST_MAX = 64
+
+
+class ReduceList(ctypes.Structure):
+    """ncf_reduce_list: deferred gradient reductions collected during one backward."""
+    _fields_ = [("count", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("d", ReduceDesc * REDUCE_LIST_MAX)]
+
+    @property
+    def address(self) -> int:
+        return ctypes.addressof(self)
+
 
 _lock = threading.Lock()
 _lib = None

@@ -568,11 +568,19 @@ int seg_reduce(const WS& w, const uint32_t* sv0, const uint32_t* sv1, const int6
                const float* dml1, const float* tmf0, const float* tml0, const float* tmf1,
                const float* tml1, const float* gmf, const float* gml, float eps, float* Gmf0,
                float* Gml0, float* Gmf1, float* Gml1, float* dgm, float* dbm, float* dgl,
-               float* dbl, hipStream_t st) {
+               float* dbl, ncf_reduce_list* defer, hipStream_t st) {
   hipLaunchKernelGGL(k_seg_reduce_ln<D>, dim3(w.nbr, 2), dim3(256), 0, st, sv0, sv1, w.start0,
                      w.start1, uniq0, uniq1, w.totals, dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1,
                      tml1, gmf, gml, eps, Gmf0, Gml0, Gmf1, Gml1, w.part);
   NCF_CHECK_LAUNCH("ncf_embedding_bwd(seg_reduce)");
+  if (defer) {
+    float* const outs[4] = {dgm, dbm, dgl, dbl};
+    for (int q = 0; q < 4; ++q) {
+      const int rc = ncf_defer(defer, w.part + q * D, 2 * w.nbr, 4 * D, D, outs[q], 0, D, D);
+      if (rc) return rc;
+    }
+    return NCF_OK;
+  }
   float* red = w.part + (int64_t)2 * w.nbr * 4 * D;
   ncf_reduce_parts(w.part, 2 * w.nbr, 4 * D, 4 * D, red, 0, 4 * D, 4 * D, st, w.red_scratch);
   hipLaunchKernelGGL(k_ln_param_scatter, dim3(1), dim3(256), 0, st, red, D, dgm, dbm, dgl, dbl);
@@ -677,7 +685,8 @@ extern "C" int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_user
                                         const int64_t* uniq_items, float* grad_mf_gamma,
                                         float* grad_mf_beta, float* grad_mlp_gamma,
                                         float* grad_mlp_beta, void* workspace,
-                                        int64_t workspace_bytes, void* stream) {
+                                        int64_t workspace_bytes, ncf_reduce_list* defer,
+                                        void* stream) {
   NCF_CHECK_ARG(n >= 0 && n < (1ll << 31), "ncf_embedding_bwd_reduce: bad n");
   NCF_CHECK_ARG(dim == 16 || dim == 32 || dim == 64 || dim == 128 || dim == 256,
                 "ncf_embedding_bwd_reduce: dim must be 16/32/64/128/256");
@@ -696,7 +705,7 @@ extern "C" int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_user
                           dy_mf_item, dy_mlp_item, mf_user, mlp_user, mf_item, mlp_item,          \
                           mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user, grad_mf_item,    \
                           grad_mlp_item, grad_mf_gamma, grad_mf_beta, grad_mlp_gamma,             \
-                          grad_mlp_beta, st);
+                          grad_mlp_beta, defer, st);
     SEG(16) SEG(32) SEG(64) SEG(128) SEG(256)
 #undef SEG
   }
@@ -726,7 +735,7 @@ extern "C" int ncf_embedding_bwd(const int64_t* user_ids, const int64_t* item_id
                                   mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user,
                                   grad_mf_item, grad_mlp_item, uniq_users, uniq_items,
                                   grad_mf_gamma, grad_mf_beta, grad_mlp_gamma, grad_mlp_beta,
-                                  workspace, workspace_bytes, stream);
+                                  workspace, workspace_bytes, nullptr, stream);
 }
 
 // slot[uniq[c]] = -1 for c < num_unique[kind] (restores the all -1 invariant after the update)

@@ -17,21 +17,25 @@
 
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 32, LDP = 65;
+// 128x64 output tile per 256-thread workgroup (4 waves as 2x2, each wave 64x32 = two 32x32
+// MFMA accumulators sharing one B fragment), BK = 32 staged through LDS as k-major images.
+// Global loads are float4 along whichever dimension is contiguous in memory (coalesced), the
+// next K-step is prefetched into registers while the current one runs on the matrix cores.
+constexpr int BM = 128, BN = 64, BK = 32;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 enum { F_RELU = 1, F_ACCUM = 2 };
 
-// Per K-step each of the 256 threads stages 8 A and 8 B elements.  Index e = tid + 256*r maps
-// to (row, k) with the CONTIGUOUS dimension on consecutive threads (coalesced loads); the
-// k-major LDS image [BK][64+1] makes both the transposing writes and the MFMA operand reads
-// (lane&31 -> row/col, lane>>5 -> k) bank-conflict-free.  The next K-step's global loads are
-// issued into registers before the current step's MFMAs, so their latency hides under compute.
-template <bool T_CONTIG_K>
-__device__ __forceinline__ void tile_coord(int e, int& rc, int& k) {
-  if (T_CONTIG_K) { k = e & (BK - 1); rc = e >> 5; }   // 32 consecutive k per row
-  else { rc = e & 63; k = e >> 6; }                     // 64 consecutive rows per k
+// guarded float4 load of up to 4 consecutive elements (count = valid elements)
+__device__ __forceinline__ float4 ld4_guard(const float* p, int count, bool vec) {
+  if (count >= 4 && vec) return ld4(p);
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (count > 0) v.x = p[0];
+  if (count > 1) v.y = p[1];
+  if (count > 2) v.z = p[2];
+  if (count > 3) v.w = p[3];
+  return v;
 }
 
 template <bool A_T, bool B_T>
@@ -39,9 +43,13 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int M, int N, int K, const flo
                                                   int64_t lda, const float* __restrict__ B,
                                                   int64_t ldb, float* __restrict__ C, int64_t ldc,
                                                   const float* __restrict__ bias, int flags,
-                                                  int ksplit, int64_t c_split_stride) {
-  __shared__ float As[BK][LDP];
-  __shared__ float Bs[BK][LDP];
+                                                  int ksplit, int64_t c_split_stride, int vec,
+                                                  float* __restrict__ rowsum_part) {
+  // k-major LDS images; row pitch padded (+1 for transposing scalar writes, +4 for b128 writes)
+  constexpr int LDA = A_T ? BM + 4 : BM + 1;
+  constexpr int LDB = B_T ? BN + 1 : BN + 4;
+  __shared__ __attribute__((aligned(16))) float As[BK * LDA];
+  __shared__ __attribute__((aligned(16))) float Bs[BK * LDB];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = tid >> 6;
@@ -51,60 +59,110 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int M, int N, int K, const flo
   const int ke = min(K, kb + ksplit);
   C += (int64_t)blockIdx.z * c_split_stride;
 
-  f32x16 acc;
+  f32x16 acc0, acc1;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  for (int r = 0; r < 16; ++r) { acc0[r] = 0.0f; acc1[r] = 0.0f; }
+  // row sums of A over this block's K range (bias gradient when A = dYᵀ): column-0 blocks only
+  const bool do_rs = rowsum_part != nullptr && blockIdx.y == 0 && tid < BM;
+  float rs = 0.0f;
 
-  float ra[8], rb[8];
+  float4 ra[4], rb[2];
   auto load = [&](int k0) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < 4; ++r) {
       const int e = tid + 256 * r;
-      int m, k;
-      tile_coord<!A_T>(e, m, k);
-      const int gm = m0 + m, gk = k0 + k;
-      ra[r] = (gm < M && gk < ke) ? (A_T ? A[(int64_t)gk * lda + gm] : A[(int64_t)gm * lda + gk]) : 0.0f;
-      int n, k2;
-      tile_coord<B_T>(e, n, k2);
-      const int gn = n0 + n, gk2 = k0 + k2;
-      rb[r] = (gn < N && gk2 < ke) ? (B_T ? B[(int64_t)gn * ldb + gk2] : B[(int64_t)gk2 * ldb + gn]) : 0.0f;
+      if (!A_T) {  // A[m][k], k contiguous
+        const int m = e >> 3, k4 = (e & 7) * 4;
+        const int gm = m0 + m, gk = k0 + k4;
+        ra[r] = gm < M ? ld4_guard(A + (int64_t)gm * lda + gk, ke - gk, vec) : make_float4(0, 0, 0, 0);
+      } else {     // A[k][m], m contiguous
+        const int m4 = (e & 31) * 4, k = e >> 5;
+        const int gm = m0 + m4, gk = k0 + k;
+        ra[r] = gk < ke ? ld4_guard(A + (int64_t)gk * lda + gm, M - gm, vec) : make_float4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int e = tid + 256 * r;
+      if (B_T) {   // B[n][k], k contiguous
+        const int n = e >> 3, k4 = (e & 7) * 4;
+        const int gn = n0 + n, gk = k0 + k4;
+        rb[r] = gn < N ? ld4_guard(B + (int64_t)gn * ldb + gk, ke - gk, vec) : make_float4(0, 0, 0, 0);
+      } else {     // B[k][n], n contiguous
+        const int n4 = (e & 15) * 4, k = e >> 4;
+        const int gn = n0 + n4, gk = k0 + k;
+        rb[r] = gk < ke ? ld4_guard(B + (int64_t)gk * ldb + gn, N - gn, vec) : make_float4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = tid + 256 * r;
+      if (!A_T) {
+        const int m = e >> 3, k4 = (e & 7) * 4;
+        As[(k4 + 0) * LDA + m] = ra[r].x; As[(k4 + 1) * LDA + m] = ra[r].y;
+        As[(k4 + 2) * LDA + m] = ra[r].z; As[(k4 + 3) * LDA + m] = ra[r].w;
+      } else {
+        const int m4 = (e & 31) * 4, k = e >> 5;
+        *reinterpret_cast<float4*>(&As[k * LDA + m4]) = ra[r];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int e = tid + 256 * r;
+      if (B_T) {
+        const int n = e >> 3, k4 = (e & 7) * 4;
+        Bs[(k4 + 0) * LDB + n] = rb[r].x; Bs[(k4 + 1) * LDB + n] = rb[r].y;
+        Bs[(k4 + 2) * LDB + n] = rb[r].z; Bs[(k4 + 3) * LDB + n] = rb[r].w;
+      } else {
+        const int n4 = (e & 15) * 4, k = e >> 4;
+        *reinterpret_cast<float4*>(&Bs[k * LDB + n4]) = rb[r];
+      }
     }
   };
   if (kb < ke) load(kb);
   for (int k0 = kb; k0 < ke; k0 += BK) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int e = tid + 256 * r;
-      int m, k;
-      tile_coord<!A_T>(e, m, k);
-      As[k][m] = ra[r];
-      int n, k2;
-      tile_coord<B_T>(e, n, k2);
-      Bs[k2][n] = rb[r];
-    }
+    store();
     __syncthreads();
-    if (k0 + BK < ke) load(k0 + BK);  // prefetch next K-step; lands while the MFMAs run
+    if (k0 + BK < ke) load(k0 + BK);  // next K-step lands while the MFMAs run
+    if (do_rs) {
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const float a = As[kk + (lane >> 5)][wm * 32 + (lane & 31)];
-      const float b = Bs[kk + (lane >> 5)][wn * 32 + (lane & 31)];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+      for (int k = 0; k < BK; ++k) rs += As[k * LDA + tid];
+    }
+    // read every fragment of the K-step first (one LDS round trip), then 32 back-to-back MFMAs
+    float fa0[BK / 2], fa1[BK / 2], fb[BK / 2];
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      const int k = 2 * kk + (lane >> 5);
+      fa0[kk] = As[k * LDA + wm * 64 + (lane & 31)];
+      fa1[kk] = As[k * LDA + wm * 64 + 32 + (lane & 31)];
+      fb[kk] = Bs[k * LDB + wn * 32 + (lane & 31)];
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa0[kk], fb[kk], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1[kk], fb[kk], acc1, 0, 0, 0);
     }
     __syncthreads();
   }
 
+  if (do_rs && m0 + tid < M) rowsum_part[(int64_t)blockIdx.z * M + m0 + tid] = rs;
   const int col = n0 + wn * 32 + (lane & 31);
   if (col >= N) return;
   const float bv = bias ? bias[col] : 0.0f;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (row < M) {
-      float v = acc[r] + bv;
-      if (flags & F_RELU) v = fmaxf(v, 0.0f);
-      float* p = C + (int64_t)row * ldc + col;
-      if (flags & F_ACCUM) v += *p;
-      *p = v;
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + wm * 64 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < M) {
+        float v = (t ? acc1[r] : acc0[r]) + bv;
+        if (flags & F_RELU) v = fmaxf(v, 0.0f);
+        float* p = C + (int64_t)row * ldc + col;
+        if (flags & F_ACCUM) v += *p;
+        *p = v;
+      }
     }
   }
 }
@@ -140,24 +198,27 @@ __global__ __launch_bounds__(256) void k_colsum_partial(const float* __restrict_
 template <bool A_T, bool B_T>
 int launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
            int64_t ldb, float* C, int64_t ldc, const float* bias, int flags, int splits,
-           int ksplit, int64_t c_split_stride, hipStream_t st) {
+           int ksplit, int64_t c_split_stride, float* rowsum, hipStream_t st) {
+  const int vec = (lda % 4 == 0) && (ldb % 4 == 0) && ((uintptr_t)A % 16 == 0) &&
+                  ((uintptr_t)B % 16 == 0) && (ksplit % 4 == 0);
   dim3 grid(ncf_cdiv(M, BM), ncf_cdiv(N, BN), splits);
   hipLaunchKernelGGL((k_gemm_f32<A_T, B_T>), grid, dim3(256), 0, st, (int)M, (int)N, (int)K, A,
-                     lda, B, ldb, C, ldc, bias, flags, ksplit, c_split_stride);
+                     lda, B, ldb, C, ldc, bias, flags, ksplit, c_split_stride, vec, rowsum);
   NCF_CHECK_LAUNCH("ncf_gemm_f32");
   return NCF_OK;
 }
 
 int dispatch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int a_trans,
              const float* B, int64_t ldb, int b_trans, float* C, int64_t ldc, const float* bias,
-             int flags, int splits, int ksplit, int64_t c_split_stride, hipStream_t st) {
+             int flags, int splits, int ksplit, int64_t c_split_stride, hipStream_t st,
+             float* rowsum = nullptr) {
   if (!a_trans && !b_trans)
-    return launch<false, false>(M, N, K, A, lda, B, ldb, C, ldc, bias, flags, splits, ksplit, c_split_stride, st);
+    return launch<false, false>(M, N, K, A, lda, B, ldb, C, ldc, bias, flags, splits, ksplit, c_split_stride, rowsum, st);
   if (!a_trans && b_trans)
-    return launch<false, true>(M, N, K, A, lda, B, ldb, C, ldc, bias, flags, splits, ksplit, c_split_stride, st);
+    return launch<false, true>(M, N, K, A, lda, B, ldb, C, ldc, bias, flags, splits, ksplit, c_split_stride, rowsum, st);
   if (a_trans && !b_trans)
-    return launch<true, false>(M, N, K, A, lda, B, ldb, C, ldc, bias, flags, splits, ksplit, c_split_stride, st);
-  return launch<true, true>(M, N, K, A, lda, B, ldb, C, ldc, bias, flags, splits, ksplit, c_split_stride, st);
+    return launch<true, false>(M, N, K, A, lda, B, ldb, C, ldc, bias, flags, splits, ksplit, c_split_stride, rowsum, st);
+  return launch<true, true>(M, N, K, A, lda, B, ldb, C, ldc, bias, flags, splits, ksplit, c_split_stride, rowsum, st);
 }
 
 }  // namespace
@@ -175,36 +236,50 @@ extern "C" int ncf_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int
 }
 
 extern "C" int64_t ncf_gemm_splitk_workspace(int64_t M, int64_t N, int splits) {
-  return (int64_t)splits * M * N + ncf_reduce_scratch(splits, M * N);
+  return (int64_t)splits * (M * N + M) + ncf_reduce_scratch(splits, M * N);
 }
 
 // Long-K GEMM (weight gradients dW = dYᵀ·X, K = batch rows): K split into `splits` slabs, each a
-// full [M,N] partial in `workspace`, summed in slab order into C (overwrite or accumulate).
+// full [M,N] partial in `workspace` (+ a [M] row-sum partial when row_sums != NULL), summed in
+// slab order into C (overwrite or accumulate) — inline, or appended to `defer`.
 extern "C" int ncf_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                                    int a_trans, const float* B, int64_t ldb, int b_trans, float* C,
-                                   int64_t ldc, int accumulate, int splits, float* workspace,
-                                   int64_t workspace_floats, void* stream) {
+                                   int64_t ldc, int accumulate, float* row_sums, int splits,
+                                   float* workspace, int64_t workspace_floats,
+                                   ncf_reduce_list* defer, void* stream) {
   NCF_CHECK_ARG(M >= 0 && N >= 0 && K >= 0 && splits >= 1, "ncf_gemm_f32_splitk: bad size");
+  NCF_CHECK_ARG(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31) && M * N < (1ll << 31),
+                "ncf_gemm_f32_splitk: size too large");
   if (M == 0 || N == 0) return NCF_OK;
   NCF_CHECK_ARG(A && B && C && workspace, "ncf_gemm_f32_splitk: null pointer");
-  if (workspace_floats < (int64_t)splits * M * N + ncf_reduce_scratch(splits, M * N)) {
+  if (workspace_floats < ncf_gemm_splitk_workspace(M, N, splits)) {
     ncf_set_error("ncf_gemm_f32_splitk: workspace %lld < %lld floats", (long long)workspace_floats,
-                  (long long)splits * M * N);
+                  (long long)ncf_gemm_splitk_workspace(M, N, splits));
     return NCF_ERR_WORKSPACE;
   }
   int64_t ksplit = (K + splits - 1) / splits;
   ksplit = (ksplit + BK - 1) / BK * BK;
-  const int used = (int)((K + ksplit - 1) / ksplit);
+  if (ksplit == 0) ksplit = BK;
+  const int used = K == 0 ? 1 : (int)((K + ksplit - 1) / ksplit);
   hipStream_t st = (hipStream_t)stream;
+  float* slabs = workspace;
+  float* rsp = workspace + (int64_t)splits * M * N;   // [used][M] row-sum partials
+  float* scratch = rsp + (int64_t)splits * M;
   if (K == 0) {
-    (void)hipMemsetAsync(workspace, 0, sizeof(float) * M * N, st);
+    (void)hipMemsetAsync(slabs, 0, sizeof(float) * M * N, st);
+    if (row_sums) (void)hipMemsetAsync(rsp, 0, sizeof(float) * M, st);
   } else {
-    int rc = dispatch(M, N, K, A, lda, a_trans, B, ldb, b_trans, workspace, N, nullptr, 0, used,
-                      (int)ksplit, M * N, st);
+    int rc = dispatch(M, N, K, A, lda, a_trans, B, ldb, b_trans, slabs, N, nullptr, 0, used,
+                      (int)ksplit, M * N, st, row_sums ? rsp : nullptr);
     if (rc) return rc;
   }
-  ncf_reduce_parts(workspace, K == 0 ? 1 : used, M * N, M * N, C, accumulate, N, ldc, st,
-                   workspace + (int64_t)used * M * N);
+  if (defer) {
+    int rc = ncf_defer(defer, slabs, used, M * N, M * N, C, accumulate, N, ldc);
+    if (!rc && row_sums) rc = ncf_defer(defer, rsp, used, M, M, row_sums, 0, M, M);
+    return rc;
+  }
+  ncf_reduce_parts(slabs, used, M * N, M * N, C, accumulate, N, ldc, st, scratch);
+  if (row_sums) ncf_reduce_parts(rsp, used, M, M, row_sums, 0, M, M, st, scratch);
   NCF_CHECK_LAUNCH("ncf_gemm_f32_splitk(reduce)");
   return NCF_OK;
 }

@@ -154,7 +154,8 @@ extern "C" int ncf_head_bwd(const float* prob, const float* grad_prob, const flo
                             float* grad_mf_item_ln, float* grad_mlp_out_w, float* grad_mlp_out_b,
                             float* grad_mf_out_w, float* grad_mf_out_b, float* grad_final_w,
                             float* grad_final_b, float* loss, double loss_denominator,
-                            float* workspace, int64_t workspace_floats, void* stream) {
+                            float* workspace, int64_t workspace_floats, ncf_reduce_list* defer,
+                            void* stream) {
   NCF_CHECK_ARG(n >= 0 && width >= 1 && width <= 256 && dim >= 1 && dim <= 256,
                 "ncf_head_bwd: bad size (width, dim <= 256)");
   NCF_CHECK_ARG((grad_prob != nullptr) != (targets != nullptr),
@@ -174,6 +175,17 @@ extern "C" int ncf_head_bwd(const float* prob, const float* grad_prob, const flo
                      grad_mf_item_ln, workspace);
   NCF_CHECK_LAUNCH("ncf_head_bwd");
   const int64_t P = width + dim + 6;
+  if (defer) {  // the partial row layout of k_head_bwd, one descriptor per parameter
+    const int64_t W3 = width;
+    int rc = ncf_defer(defer, workspace, nb, P, W3, grad_mlp_out_w, 0, W3, W3);
+    if (!rc) rc = ncf_defer(defer, workspace + W3, nb, P, dim, grad_mf_out_w, 0, dim, dim);
+    if (!rc) rc = ncf_defer(defer, workspace + W3 + dim, nb, P, 2, grad_final_w, 0, 2, 2);
+    if (!rc) rc = ncf_defer(defer, workspace + W3 + dim + 2, nb, P, 1, grad_final_b, 0, 1, 1);
+    if (!rc) rc = ncf_defer(defer, workspace + W3 + dim + 3, nb, P, 1, grad_mlp_out_b, 0, 1, 1);
+    if (!rc) rc = ncf_defer(defer, workspace + W3 + dim + 4, nb, P, 1, grad_mf_out_b, 0, 1, 1);
+    if (!rc && loss) rc = ncf_defer(defer, workspace + W3 + dim + 5, nb, P, 1, loss, 0, 1, 1, inv_n);
+    return rc;
+  }
   float* red = workspace + (int64_t)nb * P;
   ncf_reduce_parts(workspace, nb, P, P, red, 0, P, P, st, red + P);
   hipLaunchKernelGGL(k_head_scatter, dim3(1), dim3(256), 0, st, red, (int)width, (int)dim,

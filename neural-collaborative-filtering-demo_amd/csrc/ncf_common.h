@@ -7,18 +7,16 @@
 #include <string.h>
 #include <stdio.h>
 
+#include "ncf_hip.h"  // the public C-ABI: every extern "C" definition is checked against it
+
 #define NCF_WAVE 64
 
 // ---------------------------------------------------------------- error handling (host)
 // Thread-local last-error string exposed through ncf_last_error().
 void ncf_set_error(const char* fmt, ...);
 
-enum {
-  NCF_OK = 0,
-  NCF_ERR_ARG = -1,      // bad argument (shape / pointer / unsupported size)
-  NCF_ERR_LAUNCH = -2,   // hip launch failure
-  NCF_ERR_WORKSPACE = -3 // workspace too small
-};
+// NCF_OK / NCF_ERR_ARG (bad shape, pointer, unsupported size) / NCF_ERR_LAUNCH (hip launch
+// failure) / NCF_ERR_WORKSPACE (workspace too small) come from ncf_hip.h
 
 #define NCF_CHECK_ARG(cond, ...)                 \
   do {                                           \
@@ -55,17 +53,34 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 
 // Counter-based dropout RNG: a 64-bit mix of (seed, element index) -> uniform [0,1).
 // Deterministic per (seed, index); independent of launch geometry.
-__device__ __forceinline__ float ncf_uniform(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+// Dropout keep decisions.  One splitmix64 hash of (seed, idx / 4) yields four 16-bit uniforms,
+// field idx % 4 decides element idx: keep iff u >= round(p * 65536) (keep probability 1 - p to
+// 1/65536).  A float4-aligned group of four elements costs a single hash.
+__device__ __forceinline__ uint64_t ncf_hash64(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (float)(z >> 40) * (1.0f / 16777216.0f);
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint32_t ncf_drop_threshold(float p) {
+  return (uint32_t)(p * 65536.0f + 0.5f);
 }
 
 // keep-scale of element idx for dropout probability p (nn.Dropout: scale 1/(1-p))
 __device__ __forceinline__ float ncf_dropout_scale(uint64_t seed, uint64_t idx, float p, float inv_keep) {
-  return ncf_uniform(seed, idx) >= p ? inv_keep : 0.0f;
+  const uint32_t u = (uint32_t)(ncf_hash64(seed, idx >> 2) >> (16 * (idx & 3))) & 0xFFFFu;
+  return u >= ncf_drop_threshold(p) ? inv_keep : 0.0f;
+}
+
+// keep-scales of elements idx4*4 .. idx4*4+3 (same decisions as ncf_dropout_scale)
+__device__ __forceinline__ float4 ncf_dropout_scale4(uint64_t seed, uint64_t idx4, float p, float inv_keep) {
+  const uint64_t z = ncf_hash64(seed, idx4);
+  const uint32_t t = ncf_drop_threshold(p);
+  return make_float4((uint32_t)(z & 0xFFFFu) >= t ? inv_keep : 0.0f,
+                     (uint32_t)((z >> 16) & 0xFFFFu) >= t ? inv_keep : 0.0f,
+                     (uint32_t)((z >> 32) & 0xFFFFu) >= t ? inv_keep : 0.0f,
+                     (uint32_t)(z >> 48) >= t ? inv_keep : 0.0f);
 }
 
 // out[i] (+)= sum_z part[z*stride + i] over z = 0..parts-1 in order (deterministic, no atomics)
@@ -145,4 +160,27 @@ static inline void ncf_reduce_parts(const float* part, int P, int64_t stride, in
   }
   hipLaunchKernelGGL(k_reduce_parts<>, dim3(gx, 1), dim3(256), 0, st, part, P, P, stride, L, out,
                      accumulate, cols, ldo);
+}
+
+// Append one reduction to a caller's deferred list (ncf_hip.h, "deferred reductions").
+static inline int ncf_defer(ncf_reduce_list* l, const float* part, int64_t P, int64_t stride,
+                            int64_t L, float* out, int accumulate, int64_t cols, int64_t ldo,
+                            float scale = 1.0f) {
+  if (L <= 0) return NCF_OK;
+  if (l->count < 0 || l->count >= NCF_REDUCE_LIST_MAX) {
+    ncf_set_error("deferred reduction list full (%d entries)", NCF_REDUCE_LIST_MAX);
+    return NCF_ERR_ARG;
+  }
+  ncf_reduce_desc& d = l->d[l->count++];
+  d.part = part;
+  d.out = out;
+  d.stride = stride;
+  d.ldo = ldo;
+  d.L = (int32_t)L;
+  d.cols = (int32_t)cols;
+  d.P = (int32_t)P;
+  d.accumulate = accumulate;
+  d.scale = scale;
+  d.reserved = 0;
+  return NCF_OK;
 }

@@ -1,0 +1,168 @@
+// Batched deterministic reductions: every deferred gradient reduction of a backward pass in two
+// launches (ncf_hip.h, "deferred reductions").
+//
+// A training step produces ~25 parameter gradients as sums over batch rows (split-K slabs of the
+// weight gradients, per-block dgamma/dbeta/dbias partials of the row ops, the head and the
+// embedding LayerNorms).  None of them is on the critical path of the backward (only dX is), so
+// instead of two small launches each, the list is run at the end of the backward:
+//   stage 1: one 256-thread block per (descriptor, 64 outputs, chunk of <= 64 partials); a
+//            descriptor with P <= 128 partials finishes here, otherwise each chunk writes its own
+//            row of `scratch`;
+//   stage 2: sums the chunk rows of the multi-chunk descriptors in chunk order.
+// The summation order of every output depends only on (P, chunking) — never on scheduling —
+// and is the order of ncf_reduce_parts (ncf_common.h), so a deferred reduction is bit-identical
+// to the inline one.
+#include "ncf_common.h"
+
+namespace {
+
+constexpr int kPB = 64;          // partials per stage-1 chunk
+constexpr int kMaxPerLaunch = 24; // descriptors per launch (kernel-argument size)
+
+struct BatchArgs {
+  ncf_reduce_desc d[kMaxPerLaunch];
+  int64_t scr[kMaxPerLaunch];        // scratch offset (floats) of multi-chunk descriptors
+  uint32_t first[kMaxPerLaunch + 1]; // first block of descriptor i (prefix over blocks)
+  int32_t chunks[kMaxPerLaunch];
+  int32_t count;
+};
+
+__device__ __forceinline__ int find_desc(const BatchArgs& a, uint32_t b) {
+  int i = 0;
+  while (i + 1 < a.count && a.first[i + 1] <= b) ++i;
+  return i;
+}
+
+__device__ __forceinline__ void store_out(const ncf_reduce_desc& d, int64_t i, float t) {
+  float* o = d.out + (i / d.cols) * d.ldo + (i % d.cols);
+  const float v = d.scale * t;
+  *o = d.accumulate ? *o + v : v;
+}
+
+__global__ __launch_bounds__(256) void k_reduce_batch1(const BatchArgs a, float* __restrict__ scratch) {
+  __shared__ float red[4][64];
+  const int di = find_desc(a, blockIdx.x);
+  const ncf_reduce_desc& d = a.d[di];
+  const int ch = a.chunks[di];
+  const uint32_t local = blockIdx.x - a.first[di];
+  const uint32_t gx = (uint32_t)((d.L + 63) / 64);
+  const int64_t i = (int64_t)(local % gx) * 64 + (threadIdx.x & 63);
+  const int y = (int)(local / gx);
+  const int w = threadIdx.x >> 6;
+  const int pb = ch > 1 ? y * kPB : 0;
+  const int pe = ch > 1 ? min(d.P, pb + kPB) : d.P;
+  float s = 0.0f;
+  if (i < d.L) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int p = pb + w;
+    for (; p + 12 < pe; p += 16) {
+      a0 += d.part[(int64_t)p * d.stride + i];
+      a1 += d.part[(int64_t)(p + 4) * d.stride + i];
+      a2 += d.part[(int64_t)(p + 8) * d.stride + i];
+      a3 += d.part[(int64_t)(p + 12) * d.stride + i];
+    }
+    for (; p < pe; p += 4) a0 += d.part[(int64_t)p * d.stride + i];
+    s = (a0 + a1) + (a2 + a3);
+  }
+  red[w][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (w == 0 && i < d.L) {
+    const int l = threadIdx.x;
+    const float t = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+    if (ch > 1) scratch[a.scr[di] + (int64_t)y * d.L + i] = t;
+    else store_out(d, i, t);
+  }
+}
+
+// stage 2: one thread per output element of the multi-chunk descriptors
+__global__ __launch_bounds__(256) void k_reduce_batch2(const BatchArgs a,
+                                                       const float* __restrict__ scratch) {
+  const int di = find_desc(a, blockIdx.x);
+  const ncf_reduce_desc& d = a.d[di];
+  const int64_t i = (int64_t)(blockIdx.x - a.first[di]) * 256 + threadIdx.x;
+  if (i >= d.L) return;
+  const float* s = scratch + a.scr[di] + i;
+  const int pe = a.chunks[di];
+  // k_reduce_parts' order: "wave" w sums rows w, w+4, ... with 4 accumulators, fixed combine
+  float ws[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int p = w;
+    for (; p + 12 < pe; p += 16) {
+      a0 += s[(int64_t)p * d.L];
+      a1 += s[(int64_t)(p + 4) * d.L];
+      a2 += s[(int64_t)(p + 8) * d.L];
+      a3 += s[(int64_t)(p + 12) * d.L];
+    }
+    for (; p < pe; p += 4) a0 += s[(int64_t)p * d.L];
+    ws[w] = (a0 + a1) + (a2 + a3);
+  }
+  store_out(d, i, (ws[0] + ws[1]) + (ws[2] + ws[3]));
+}
+
+int chunks_of(int P) { return P > 2 * kPB ? (P + kPB - 1) / kPB : 1; }
+
+}  // namespace
+
+extern "C" int64_t ncf_reduce_batch_scratch(const ncf_reduce_list* list) {
+  if (!list) return 0;
+  int64_t f = 0;
+  for (int i = 0; i < list->count && i < NCF_REDUCE_LIST_MAX; ++i) {
+    const int c = chunks_of(list->d[i].P);
+    if (c > 1) f += (int64_t)c * list->d[i].L;
+  }
+  return f;
+}
+
+extern "C" int ncf_reduce_batch(const ncf_reduce_list* list, float* scratch,
+                                int64_t scratch_floats, void* stream) {
+  NCF_CHECK_ARG(list && list->count >= 0 && list->count <= NCF_REDUCE_LIST_MAX,
+                "ncf_reduce_batch: bad list");
+  if (scratch_floats < ncf_reduce_batch_scratch(list)) {
+    ncf_set_error("ncf_reduce_batch: scratch %lld < %lld floats", (long long)scratch_floats,
+                  (long long)ncf_reduce_batch_scratch(list));
+    return NCF_ERR_WORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  int64_t scr_off = 0;
+  for (int base = 0; base < list->count; base += kMaxPerLaunch) {
+    BatchArgs a1, a2;
+    memset(&a1, 0, sizeof(a1));
+    memset(&a2, 0, sizeof(a2));
+    uint32_t b1 = 0, b2 = 0;
+    for (int j = 0; j < kMaxPerLaunch && base + j < list->count; ++j) {
+      const ncf_reduce_desc& d = list->d[base + j];
+      NCF_CHECK_ARG(d.part && d.out && d.L >= 0 && d.P >= 1 && d.cols >= 1 && d.stride >= d.L,
+                    "ncf_reduce_batch: bad descriptor %d", base + j);
+      const int c = chunks_of(d.P);
+      const uint32_t gx = (uint32_t)((d.L + 63) / 64);
+      a1.d[a1.count] = d;
+      a1.chunks[a1.count] = c;
+      a1.first[a1.count] = b1;
+      a1.scr[a1.count] = c > 1 ? scr_off : 0;
+      b1 += gx * (uint32_t)c;
+      if (c > 1) {
+        a2.d[a2.count] = d;
+        a2.chunks[a2.count] = c;
+        a2.first[a2.count] = b2;
+        a2.scr[a2.count] = scr_off;
+        b2 += (uint32_t)((d.L + 255) / 256);
+        ++a2.count;
+        scr_off += (int64_t)c * d.L;
+      }
+      ++a1.count;
+    }
+    a1.first[a1.count] = b1;
+    a2.first[a2.count] = b2;
+    if (b1 > 0) {
+      hipLaunchKernelGGL(k_reduce_batch1, dim3(b1), dim3(256), 0, st, a1, scratch);
+      NCF_CHECK_LAUNCH("ncf_reduce_batch(stage 1)");
+    }
+    if (b2 > 0) {
+      hipLaunchKernelGGL(k_reduce_batch2, dim3(b2), dim3(256), 0, st, a2, (const float*)scratch);
+      NCF_CHECK_LAUNCH("ncf_reduce_batch(stage 2)");
+    }
+  }
+  return NCF_OK;
+}

@@ -29,11 +29,14 @@ __global__ __launch_bounds__(256) void k_relu_ln_drop_fwd(float* __restrict__ r,
   const int64_t row = t / G::L;
   const int sub = (int)(t % G::L);
   if (row >= n) return;
-  float4 x[G::CH];
+  float4 x[G::CH], gg[G::CH], bb[G::CH];
   float s = 0.0f;
 #pragma unroll
   for (int c = 0; c < G::CH; ++c) {
-    x[c] = ld4(r + row * W + (c * G::L + sub) * 4);
+    const int col = (c * G::L + sub) * 4;
+    x[c] = ld4(r + row * W + col);
+    gg[c] = ld4(g + col);
+    bb[c] = ld4(b + col);
     s += x[c].x + x[c].y + x[c].z + x[c].w;
   }
   const float mean = group_sum<G::L>(s) * (1.0f / W);
@@ -48,15 +51,11 @@ __global__ __launch_bounds__(256) void k_relu_ln_drop_fwd(float* __restrict__ r,
 #pragma unroll
   for (int c = 0; c < G::CH; ++c) {
     const int col = (c * G::L + sub) * 4;
-    const float4 gg = ld4(g + col), bb = ld4(b + col);
-    float4 y = make_float4(x[c].x * rstd * gg.x + bb.x, x[c].y * rstd * gg.y + bb.y,
-                           x[c].z * rstd * gg.z + bb.z, x[c].w * rstd * gg.w + bb.w);
+    float4 y = make_float4(x[c].x * rstd * gg[c].x + bb[c].x, x[c].y * rstd * gg[c].y + bb[c].y,
+                           x[c].z * rstd * gg[c].z + bb[c].z, x[c].w * rstd * gg[c].w + bb[c].w);
     if (p > 0.0f) {
-      const uint64_t base = (uint64_t)row * W + col;
-      y.x *= ncf_dropout_scale(seed, base + 0, p, inv_keep);
-      y.y *= ncf_dropout_scale(seed, base + 1, p, inv_keep);
-      y.z *= ncf_dropout_scale(seed, base + 2, p, inv_keep);
-      y.w *= ncf_dropout_scale(seed, base + 3, p, inv_keep);
+      const float4 k = ncf_dropout_scale4(seed, ((uint64_t)row * W + col) >> 2, p, inv_keep);
+      y.x *= k.x; y.y *= k.y; y.z *= k.z; y.w *= k.w;
     }
     st4(out + row * W + col, y);
   }
@@ -66,9 +65,10 @@ __global__ __launch_bounds__(256) void k_relu_ln_drop_fwd(float* __restrict__ r,
   }
 }
 
-// Backward.  Each block owns rows [blockIdx*rows_per_block, ...); partial dgamma / dbeta / dbias
-// (column sums of the pre-ReLU gradient = bias gradient of the producing Linear) of the block go
-// to part[blockIdx][0:W | W:2W | 2W:3W].
+// Backward.  Each block owns rows [blockIdx*rows_per_block, ...); partial dbias (column sums of
+// the pre-ReLU gradient = bias gradient of the producing Linear) / dgamma / dbeta of the block go
+// to part[blockIdx][0:W | W:2W | 2W:3W] (the order of Linear.bias, LayerNorm.weight,
+// LayerNorm.bias in the parameter list, so one strided reduce lands all three).
 template <int W>
 __global__ __launch_bounds__(256) void k_relu_ln_drop_bwd(
     const float* __restrict__ dout, const float* __restrict__ r, const float* __restrict__ mean,
@@ -96,11 +96,8 @@ __global__ __launch_bounds__(256) void k_relu_ln_drop_bwd(
       const int col = (c * G::L + sub) * 4;
       float4 d = ld4(dout + row * W + col);
       if (p > 0.0f) {
-        const uint64_t base = (uint64_t)row * W + col;
-        d.x *= ncf_dropout_scale(seed, base + 0, p, inv_keep);
-        d.y *= ncf_dropout_scale(seed, base + 1, p, inv_keep);
-        d.z *= ncf_dropout_scale(seed, base + 2, p, inv_keep);
-        d.w *= ncf_dropout_scale(seed, base + 3, p, inv_keep);
+        const float4 k = ncf_dropout_scale4(seed, ((uint64_t)row * W + col) >> 2, p, inv_keep);
+        d.x *= k.x; d.y *= k.y; d.z *= k.z; d.w *= k.w;
       }
       const float4 x = ld4(r + row * W + col);
       const float4 gg = ld4(g + col);
@@ -131,12 +128,12 @@ __global__ __launch_bounds__(256) void k_relu_ln_drop_bwd(
 #pragma unroll
   for (int c = 0; c < G::CH; ++c) {
     const int col = (c * G::L + sub) * 4;
-    red[lane_grp][col + 0] = ag[c].x; red[lane_grp][col + 1] = ag[c].y;
-    red[lane_grp][col + 2] = ag[c].z; red[lane_grp][col + 3] = ag[c].w;
-    red[lane_grp][W + col + 0] = ab[c].x; red[lane_grp][W + col + 1] = ab[c].y;
-    red[lane_grp][W + col + 2] = ab[c].z; red[lane_grp][W + col + 3] = ab[c].w;
-    red[lane_grp][2 * W + col + 0] = al[c].x; red[lane_grp][2 * W + col + 1] = al[c].y;
-    red[lane_grp][2 * W + col + 2] = al[c].z; red[lane_grp][2 * W + col + 3] = al[c].w;
+    red[lane_grp][col + 0] = al[c].x; red[lane_grp][col + 1] = al[c].y;
+    red[lane_grp][col + 2] = al[c].z; red[lane_grp][col + 3] = al[c].w;
+    red[lane_grp][W + col + 0] = ag[c].x; red[lane_grp][W + col + 1] = ag[c].y;
+    red[lane_grp][W + col + 2] = ag[c].z; red[lane_grp][W + col + 3] = ag[c].w;
+    red[lane_grp][2 * W + col + 0] = ab[c].x; red[lane_grp][2 * W + col + 1] = ab[c].y;
+    red[lane_grp][2 * W + col + 2] = ab[c].z; red[lane_grp][2 * W + col + 3] = ab[c].w;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 3 * W; i += 256) {
@@ -146,7 +143,19 @@ __global__ __launch_bounds__(256) void k_relu_ln_drop_bwd(
   }
 }
 
-constexpr int RPB = 128;  // rows per backward block
+// rows per backward block: ~1024 blocks (enough waves in flight to hide the row loads), a
+// multiple of the row slots of a block
+static inline int64_t bwd_rows_per_block(int64_t n, int64_t width) {
+  const int64_t L = width / 4 < 64 ? width / 4 : 64;
+  const int64_t slots = 256 / L;
+  int64_t rpb = (n + 1023) / 1024;
+  rpb = (rpb + slots - 1) / slots * slots;
+  return rpb < slots ? slots : rpb;
+}
+
+static inline int bwd_blocks(int64_t n, int64_t width) {
+  return n == 0 ? 1 : (int)((n + bwd_rows_per_block(n, width) - 1) / bwd_rows_per_block(n, width));
+}
 
 template <int W>
 int fwd_w(float* r, int64_t n, const float* g, const float* b, float eps, float p, uint64_t seed,
@@ -161,16 +170,29 @@ int fwd_w(float* r, int64_t n, const float* g, const float* b, float eps, float 
 template <int W>
 int bwd_w(const float* dout, const float* r, const float* mean, const float* rstd, const float* g,
           int64_t n, float p, uint64_t seed, float* dlin, float* dgamma, float* dbeta,
-          float* dbias, float* ws, hipStream_t st) {
-  const int nb = n == 0 ? 1 : ncf_cdiv(n, RPB);
+          float* dbias, float* ws, ncf_reduce_list* defer, hipStream_t st) {
+  const int nb = bwd_blocks(n, W);
   hipLaunchKernelGGL(k_relu_ln_drop_bwd<W>, dim3(nb), dim3(256), 0, st, dout, r, mean, rstd, g, n,
-                     RPB, p, seed, dlin, ws);
+                     (int)bwd_rows_per_block(n, W), p, seed, dlin, ws);
   NCF_CHECK_LAUNCH("ncf_relu_ln_dropout_bwd");
-  // dgamma, dbeta, dbias are the three W-wide thirds of each partial row
+  // dbias, dgamma, dbeta are the three W-wide thirds of each partial row: one strided reduce
+  // when the three outputs are equally spaced (consecutive parameters of the flat buffer)
   float* scr = ws + (int64_t)nb * 3 * W;
-  ncf_reduce_parts(ws, nb, 3 * W, W, dgamma, 0, W, W, st, scr);
-  ncf_reduce_parts(ws + W, nb, 3 * W, W, dbeta, 0, W, W, st, scr);
-  if (dbias) ncf_reduce_parts(ws + 2 * W, nb, 3 * W, W, dbias, 0, W, W, st, scr);
+  const ptrdiff_t s1 = dgamma - dbias, s2 = dbeta - dgamma;
+  if (defer) {
+    if (dbias && s1 == s2 && s1 >= W) return ncf_defer(defer, ws, nb, 3 * W, 3 * W, dbias, 0, W, s1);
+    int rc = dbias ? ncf_defer(defer, ws, nb, 3 * W, W, dbias, 0, W, W) : NCF_OK;
+    if (!rc) rc = ncf_defer(defer, ws + W, nb, 3 * W, W, dgamma, 0, W, W);
+    if (!rc) rc = ncf_defer(defer, ws + 2 * W, nb, 3 * W, W, dbeta, 0, W, W);
+    return rc;
+  }
+  if (dbias && s1 == s2 && s1 >= W) {
+    ncf_reduce_parts(ws, nb, 3 * W, 3 * W, dbias, 0, W, s1, st, scr);
+  } else {
+    if (dbias) ncf_reduce_parts(ws, nb, 3 * W, W, dbias, 0, W, W, st, scr);
+    ncf_reduce_parts(ws + W, nb, 3 * W, W, dgamma, 0, W, W, st, scr);
+    ncf_reduce_parts(ws + 2 * W, nb, 3 * W, W, dbeta, 0, W, W, st, scr);
+  }
   NCF_CHECK_LAUNCH("ncf_relu_ln_dropout_bwd(reduce)");
   return NCF_OK;
 }
@@ -191,8 +213,8 @@ int bwd_w(const float* dout, const float* r, const float* mean, const float* rst
   }
 
 extern "C" int64_t ncf_relu_ln_dropout_bwd_workspace(int64_t n, int64_t width) {
-  const int nb = n == 0 ? 1 : ncf_cdiv(n, RPB);
-  return (int64_t)nb * 3 * width + ncf_reduce_scratch(nb, width);
+  const int nb = bwd_blocks(n, width);
+  return (int64_t)nb * 3 * width + ncf_reduce_scratch(nb, 3 * width);
 }
 
 // out = dropout(LayerNorm(r)); r already holds relu(linear) (GEMM epilogue); saves mean/rstd.
@@ -212,12 +234,13 @@ extern "C" int ncf_relu_ln_dropout_bwd(const float* grad_out, const float* relu_
                                        int64_t n, int64_t width, float dropout_p, uint64_t seed,
                                        float* grad_lin, float* grad_gamma, float* grad_beta,
                                        float* grad_bias, float* workspace,
-                                       int64_t workspace_floats, void* stream) {
+                                       int64_t workspace_floats, ncf_reduce_list* defer,
+                                       void* stream) {
   NCF_CHECK_ARG(n >= 0, "ncf_relu_ln_dropout_bwd: n < 0");
   if (workspace_floats < ncf_relu_ln_dropout_bwd_workspace(n, width)) {
     ncf_set_error("ncf_relu_ln_dropout_bwd: workspace too small");
     return NCF_ERR_WORKSPACE;
   }
   NCF_DISPATCH_W(width, bwd_w, grad_out, relu_in, mean, rstd, gamma, n, dropout_p, seed, grad_lin,
-                 grad_gamma, grad_beta, grad_bias, workspace, (hipStream_t)stream);
+                 grad_gamma, grad_beta, grad_bias, workspace, defer, (hipStream_t)stream);
 }

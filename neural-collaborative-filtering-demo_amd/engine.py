@@ -65,18 +65,28 @@ class Workspace:
         self.dlin = [e(n, h) for h in g.hidden]
         self.da = [e(n, h) for h in g.hidden]
         self.loss = e(1)
-        # scratch sizing
-        dims = [(D, D)] + [(h, i) for h, i in zip(g.hidden, [D] + g.hidden[:-1])]
+        # Backward workspaces.  Every gradient reduction of the backward is deferred into
+        # red_list and run by one ncf_reduce_batch at its end, so each producing call site keeps
+        # its partials in its own slice of `red_ws` until then.
         self.splits = {}
-        sk = 1
-        for (mo, ko) in dims:
-            s = self.splits_for(mo, ko, n)
-            self.splits[(mo, ko)] = s
-            sk = max(sk, _lib.query("ncf_gemm_splitk_workspace", mo, ko, s))
-        cs = max(_lib.query("ncf_colsum_workspace", n, w) for w in [D] + g.hidden)
-        rl = max(_lib.query("ncf_relu_ln_dropout_bwd_workspace", n, w) for w in g.hidden)
-        hd = _lib.query("ncf_head_bwd_workspace", n, g.hidden[-1], D)
-        self.scratch = e(max(sk, cs, rl, hd))
+        sites = [("head", _lib.query("ncf_head_bwd_workspace", n, g.hidden[-1], D))]
+        kins = [D] + g.hidden[:-1]
+        for l, (h, kin) in enumerate(zip(g.hidden, kins)):
+            s = self.splits_for(h, kin, n)
+            self.splits[(h, kin)] = s
+            sites.append((f"relu{l}", _lib.query("ncf_relu_ln_dropout_bwd_workspace", n, h)))
+            sites.append((f"mlp{l}", _lib.query("ncf_gemm_splitk_workspace", h, kin, s)))
+        s = self.splits_for(D, D, n)
+        self.splits[(D, D)] = s
+        for nm in ("out_proj", "q_proj", "k_proj", "v_proj"):
+            sites.append((nm, _lib.query("ncf_gemm_splitk_workspace", D, D, s)))
+        self.site_off, off = {}, 0
+        for name, size in sites:
+            self.site_off[name] = (off, size)
+            off += _align4(size)
+        self.red_ws = e(max(off, 1))
+        self.red_list = _lib.ReduceList()
+        self.red_scratch = e(1)
         self.emb_ws = torch.empty(_lib.query("ncf_embedding_bwd_workspace", n, D),
                                   dtype=torch.uint8, device=device)
         self.G = {k: e(n, D) for k in ("mf_user", "mlp_user", "mf_item", "mlp_item")}
@@ -86,9 +96,25 @@ class Workspace:
 
     @staticmethod
     def splits_for(m_out: int, k_out: int, rows: int) -> int:
-        tiles = max(1, math.ceil(m_out / 64) * math.ceil(k_out / 64))
-        s = max(1, math.ceil(512 / tiles))
-        return max(1, min(s, math.ceil(max(rows, 1) / 256)))
+        """K-splits of a weight-gradient GEMM (measured optimum ~160 slabs at the C2 shapes,
+        tools/gemm_bench.py), >= 128 batch rows per slab."""
+        return max(1, min(160, math.ceil(max(rows, 1) / 128)))
+
+    def site(self, name: str) -> torch.Tensor:
+        off, size = self.site_off[name]
+        return self.red_ws[off:off + size]
+
+    def run_reductions(self, st):
+        """All gradient reductions deferred by this backward, in two launches."""
+        lst = self.red_list
+        if lst.count == 0:
+            return
+        need = _lib.query("ncf_reduce_batch_scratch", lst.address)
+        if self.red_scratch.numel() < need:
+            self.red_scratch = torch.empty(need, dtype=torch.float32, device=self.red_ws.device)
+        _lib.call("ncf_reduce_batch", lst.address, ptr(self.red_scratch), self.red_scratch.numel(),
+                  st)
+        lst.count = 0
 
 
 class NCFEngine:
@@ -198,18 +224,21 @@ class NCFEngine:
     @staticmethod
     def _gemm(A, lda, a_t, Bm, ldb, b_t, C, ldc, M, N, K, bias=None, relu=False, accum=False, st=None):
         flags = (1 if relu else 0) | (2 if accum else 0)
-        _lib.call("ncf_gemm_f32", M, N, K, ptr(A), lda, int(a_t), ptr(Bm), ldb, int(b_t), ptr(C),
+        # LDS-tiled 128x64 kernel, except the square DxD attention projections where the LDS-free
+        # wave-per-tile kernel is faster (tools/gemm_bench.py)
+        fn = "ncf_gemm_direct" if (N == K and N <= 64) else "ncf_gemm_f32"
+        _lib.call(fn, M, N, K, ptr(A), lda, int(a_t), ptr(Bm), ldb, int(b_t), ptr(C),
                   ldc, ptr(bias), flags, st)
 
-    def _wgrad(self, w: Workspace, dY, ldy, X, ldx, dW, ldw, m_out, k_in, n, st, accum=False):
-        """dW[m_out, k_in] = dYᵀ[m_out, n] · X[n, k_in] (split-K over the batch rows)."""
+    def _wgrad(self, w: Workspace, site: str, dY, ldy, X, ldx, dW, ldw, m_out, k_in, n, st,
+               dbias=None):
+        """dW[m_out, k_in] = dYᵀ[m_out, n] · X[n, k_in] (split-K over the batch rows); with
+        ``dbias`` also the bias gradient (row sums of dYᵀ) from the same pass.  The slab
+        reduction is deferred to the end of the backward (Workspace.run_reductions)."""
         s = w.splits.get((m_out, k_in)) or Workspace.splits_for(m_out, k_in, n)
+        ws = w.site(site)
         _lib.call("ncf_gemm_f32_splitk", m_out, k_in, n, ptr(dY), ldy, 1, ptr(X), ldx, 0, ptr(dW),
-                  ldw, int(accum), s, ptr(w.scratch), w.scratch.numel(), st)
-
-    def _colsum(self, w, X, rows, cols, out, st):
-        _lib.call("ncf_colsum", ptr(X), rows, cols, cols, ptr(out), 0, ptr(w.scratch),
-                  w.scratch.numel(), st)
+                  ldw, 0, ptr(dbias), s, ptr(ws), ws.numel(), w.red_list.address, st)
 
     # ------------------------------------------------------------------ forward
     def sync_tables(self):
@@ -304,6 +333,7 @@ class NCFEngine:
         uid = uid.to(device=dev, dtype=torch.int64).contiguous()
         iid = iid.to(device=dev, dtype=torch.int64).contiguous()
         gv = self.grad_view
+        w.red_list.count = 0
         # a12 + a8 backward (trainer.py:271; architecture.py:245-252)
         gp = None if grad_prob is None else grad_prob.reshape(-1).to(torch.float32).contiguous()
         tg = None if targets is None else targets.reshape(-1).to(device=dev, dtype=torch.float32).contiguous()
@@ -313,7 +343,8 @@ class NCFEngine:
                   ptr(w.dimf), ptr(gv("mlp_output.weight")), ptr(gv("mlp_output.bias")),
                   ptr(gv("mf_output.weight")), ptr(gv("mf_output.bias")),
                   ptr(gv("final.0.weight")), ptr(gv("final.0.bias")), ptr(w.loss),
-                  float(loss_denominator), ptr(w.scratch), w.scratch.numel(), st)
+                  float(loss_denominator), ptr(w.site("head")), w.site("head").numel(),
+                  w.red_list.address, st)
         # a7 backward, last layer first
         for l in reversed(range(len(hid))):
             h = hid[l]
@@ -322,11 +353,12 @@ class NCFEngine:
                       ptr(w.rstd[l]), ptr(ln.weight), n, h, drop_p,
                       (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1), ptr(w.dlin[l]),
                       ptr(gv(f"mlp.{4 * l + 2}.weight")), ptr(gv(f"mlp.{4 * l + 2}.bias")),
-                      ptr(gv(f"mlp.{4 * l}.bias")), ptr(w.scratch), w.scratch.numel(), st)
+                      ptr(gv(f"mlp.{4 * l}.bias")), ptr(w.site(f"relu{l}")),
+                      w.site(f"relu{l}").numel(), w.red_list.address, st)
             xin, kin = (w.y, D) if l == 0 else (w.a[l - 1], hid[l - 1])
             ldw = lin.weight.shape[1]
             dW = gv(f"mlp.{4 * l}.weight")
-            self._wgrad(w, w.dlin[l], h, xin, kin, dW, ldw, h, kin, n, st)
+            self._wgrad(w, f"mlp{l}", w.dlin[l], h, xin, kin, dW, ldw, h, kin, n, st)
             if ldw > kin:  # zero temporal columns of mlp.0 (their input is all-zero)
                 _lib.call("ncf_fill_2d", ptr(dW[:, kin:]), h, ldw - kin, ldw, 0.0, st)
             dx = w.dy if l == 0 else w.da[l - 1]
@@ -334,14 +366,14 @@ class NCFEngine:
         # a5 backward: out_proj, core, q/k/v projections
         att = m.user_product_attention
         src = w.o
-        self._wgrad(w, w.dy, D, src, D, gv("user_product_attention.out_proj.weight"), D, D, D, n, st)
-        self._colsum(w, w.dy, n, D, gv("user_product_attention.out_proj.bias"), st)
+        self._wgrad(w, "out_proj", w.dy, D, src, D, gv("user_product_attention.out_proj.weight"), D,
+                    D, D, n, st, dbias=gv("user_product_attention.out_proj.bias"))
         self._gemm(w.dy, D, 0, att.out_proj.weight, D, 0, w.do, D, n, D, D, st=st)
         _lib.call("ncf_attention_bwd", ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P), ptr(w.do), n // M, M,
                   H, D, drop_p, seed, ptr(w.dS), ptr(w.dq), ptr(w.dk), ptr(w.dv), st)
         for nm, dX, X in (("q_proj", w.dq, w.xu), ("k_proj", w.dk, w.xi), ("v_proj", w.dv, w.xi)):
-            self._wgrad(w, dX, D, X, D, gv(f"user_product_attention.{nm}.weight"), D, D, D, n, st)
-            self._colsum(w, dX, n, D, gv(f"user_product_attention.{nm}.bias"), st)
+            self._wgrad(w, nm, dX, D, X, D, gv(f"user_product_attention.{nm}.weight"), D, D, D, n,
+                        st, dbias=gv(f"user_product_attention.{nm}.bias"))
         self._gemm(w.dq, D, 0, att.q_proj.weight, D, 0, w.dxu, D, n, D, D, st=st)
         self._gemm(w.dk, D, 0, att.k_proj.weight, D, 0, w.dxi, D, n, D, D, st=st)
         self._gemm(w.dv, D, 0, att.v_proj.weight, D, 0, w.dxi, D, n, D, D, accum=True, st=st)
@@ -350,25 +382,19 @@ class NCFEngine:
         G = w.G
         uq_u, uq_i = uniq if uniq is not None else (w.uniq_u, w.uniq_i)
         d_rows = rows or (m.num_users, m.num_products)
-        if getattr(w, "deduped", False):   # ids already sorted/deduplicated before the forward
-            _lib.call("ncf_embedding_bwd_reduce", n, D, d_rows[0], d_rows[1],
-                      ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), ptr(tb["mf_user"]),
-                      ptr(tb["mlp_user"]), ptr(tb["mf_item"]), ptr(tb["mlp_item"]),
-                      ptr(m.mf_norm.weight), ptr(m.mlp_norm.weight), LN_EPS, ptr(G["mf_user"]),
-                      ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(uq_u),
-                      ptr(uq_i), ptr(gv("mf_norm.weight")), ptr(gv("mf_norm.bias")),
-                      ptr(gv("mlp_norm.weight")), ptr(gv("mlp_norm.bias")), ptr(w.emb_ws),
-                      w.emb_ws.numel(), st)
-            self.pending = w
-            return
-        _lib.call("ncf_embedding_bwd", ptr(uid), ptr(iid), n, D, m.num_users, m.num_products,
+        if not getattr(w, "deduped", False):   # sort/deduplicate now (slot maps for the Adam)
+            _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, D, m.num_users, m.num_products,
+                      ptr(w.uniq_u), ptr(w.uniq_i), ptr(self.slot_u), ptr(self.slot_i),
+                      ptr(w.num_unique), ptr(w.emb_ws), w.emb_ws.numel(), st)
+        _lib.call("ncf_embedding_bwd_reduce", n, D, d_rows[0], d_rows[1],
                   ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), ptr(tb["mf_user"]),
                   ptr(tb["mlp_user"]), ptr(tb["mf_item"]), ptr(tb["mlp_item"]),
                   ptr(m.mf_norm.weight), ptr(m.mlp_norm.weight), LN_EPS, ptr(G["mf_user"]),
-                  ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(w.uniq_u),
-                  ptr(w.uniq_i), ptr(self.slot_u), ptr(self.slot_i), ptr(w.num_unique),
-                  ptr(gv("mf_norm.weight")), ptr(gv("mf_norm.bias")), ptr(gv("mlp_norm.weight")),
-                  ptr(gv("mlp_norm.bias")), ptr(w.emb_ws), w.emb_ws.numel(), st)
+                  ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(uq_u),
+                  ptr(uq_i), ptr(gv("mf_norm.weight")), ptr(gv("mf_norm.bias")),
+                  ptr(gv("mlp_norm.weight")), ptr(gv("mlp_norm.bias")), ptr(w.emb_ws),
+                  w.emb_ws.numel(), w.red_list.address, st)
+        w.run_reductions(st)
         self.pending = w
 
     # ------------------------------------------------------------------ optimizer

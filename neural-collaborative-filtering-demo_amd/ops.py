@@ -19,21 +19,15 @@ def _require_cuda(t):
 
 
 def _gemm(A, lda, a_t, B, ldb, b_t, C, ldc, M, N, K, bias=None, accum=False):
-    _lib.call("ncf_gemm_f32", M, N, K, ptr(A), lda, int(a_t), ptr(B), ldb, int(b_t), ptr(C), ldc,
+    _lib.call("ncf_gemm_direct", M, N, K, ptr(A), lda, int(a_t), ptr(B), ldb, int(b_t), ptr(C), ldc,
               ptr(bias), 2 if accum else 0, _lib.stream_ptr(C.device))
 
 
-def _wgrad(dY, X, dW, n, m_out, k_in):
-    s = max(1, min(256, (n + 63) // 64))
+def _wgrad(dY, X, dW, n, m_out, k_in, dbias=None):
+    s = max(1, min(160, (n + 127) // 128))
     ws = torch.empty(_lib.query("ncf_gemm_splitk_workspace", m_out, k_in, s), device=dY.device)
     _lib.call("ncf_gemm_f32_splitk", m_out, k_in, n, ptr(dY), m_out, 1, ptr(X), k_in, 0, ptr(dW),
-              k_in, 0, s, ptr(ws), ws.numel(), _lib.stream_ptr(dY.device))
-
-
-def _colsum(X, rows, cols, out):
-    ws = torch.empty(max(1, _lib.query("ncf_colsum_workspace", rows, cols)), device=X.device)
-    _lib.call("ncf_colsum", ptr(X), rows, cols, cols, ptr(out), 0, ptr(ws), ws.numel(),
-              _lib.stream_ptr(X.device))
+              k_in, 0, ptr(dbias), s, ptr(ws), ws.numel(), None, _lib.stream_ptr(dY.device))
 
 
 class _MHAFunction(torch.autograd.Function):
@@ -65,8 +59,7 @@ class _MHAFunction(torch.autograd.Function):
         dy = gy.reshape(n, D).contiguous().float()
         g = {nm: torch.empty(D, D, device=dev) for nm in ("wq", "wk", "wv", "wo")}
         gb = {nm: torch.empty(D, device=dev) for nm in ("bq", "bk", "bv", "bo")}
-        _wgrad(dy, o, g["wo"], n, D, D)
-        _colsum(dy, n, D, gb["bo"])
+        _wgrad(dy, o, g["wo"], n, D, D, gb["bo"])
         do = torch.empty(n, D, device=dev)
         _gemm(dy, D, 0, wo, D, 0, do, D, n, D, D)
         dS = torch.empty(Bn * H * L * L, device=dev)
@@ -76,8 +69,7 @@ class _MHAFunction(torch.autograd.Function):
         outs = []
         for dX, X, W, wn, bn in ((dq, xq, wq, "wq", "bq"), (dk, xk, wk, "wk", "bk"),
                                  (dv, xv, wv, "wv", "bv")):
-            _wgrad(dX, X, g[wn], n, D, D)
-            _colsum(dX, n, D, gb[bn])
+            _wgrad(dX, X, g[wn], n, D, D, gb[bn])
             gx = torch.empty(n, D, device=dev)
             _gemm(dX, D, 0, W, D, 0, gx, D, n, D, D)
             outs.append(gx.view(Bn, L, D))

@@ -24,7 +24,10 @@ def assert_params_close(name, actual, ref, g_eff0, lr, steps, atol=1e-6):
         assert in_bad.max() <= 2 * lr * steps + atol, f"{name}: zone diff {in_bad.max():.3e}"
 
 
-def assert_moment_close(name, actual, ref, g_eff0, rtol=1e-3, atol=1e-8):
+def assert_moment_close(name, actual, ref, g_eff0, rtol=1e-3, atol=1e-7):
+    """Adam moments after a few steps.  exp_avg is (1-b1) * sum_k b1^k g_k (weights summing to
+    < 0.3 over 3 steps), so it inherits the gradient tolerance scaled down: abs 1e-7 (the gradient
+    abs tolerance is 1e-6), rel 1e-3 for elements accumulated from noisy near-zero gradients."""
     actual = np.asarray(actual)
     ref = np.asarray(ref)
     zone = np.abs(g_eff0) < ZONE

@@ -48,7 +48,7 @@ def test_library_exports_every_symbol():
     assert lib.ncf_version() == 10000
     assert lib.ncf_last_error() is not None
     # workspace queries are pure host arithmetic
-    assert _lib.query("ncf_gemm_splitk_workspace", 256, 64, 4) == 4 * 256 * 64
+    assert _lib.query("ncf_gemm_splitk_workspace", 256, 64, 4) == 4 * (256 * 64 + 256)
     assert _lib.query("ncf_embedding_bwd_workspace", 20480, 64) > 0
 
 
@@ -124,3 +124,21 @@ def test_to_keeps_flat_layout():
     m = m.double().float()
     assert torch.equal(m.mlp[0].weight.detach(), w0.float())
     assert all(m.engine.is_flat_view(p) for _, p in m.engine.dense_params())
+
+
+def test_reduce_list_layout_and_scratch_query():
+    """ncf_reduce_desc / ncf_reduce_list mirror the header layout; the batch scratch query is
+    host arithmetic: one [chunks, L] block per descriptor with P > 128 partials (64 per chunk)."""
+    import ctypes
+    assert ctypes.sizeof(_lib.ReduceDesc) == 56
+    assert ctypes.sizeof(_lib.ReduceList) == 8 + 56 * _lib.REDUCE_LIST_MAX
+    src = open(HEADER).read()
+    assert f"#define NCF_REDUCE_LIST_MAX {_lib.REDUCE_LIST_MAX}" in src
+    lst = _lib.ReduceList()
+    for P, L in ((100, 33), (160, 4096), (1024, 768)):
+        d = lst.d[lst.count]
+        d.part, d.out, d.stride, d.ldo, d.L, d.cols, d.P, d.scale = 8, 8, L, L, L, L, P, 1.0
+        lst.count += 1
+    assert _lib.query("ncf_reduce_batch_scratch", lst.address) == 3 * 4096 + 16 * 768
+    empty = _lib.ReduceList()
+    assert _lib.load().ncf_reduce_batch(empty.address, None, 0, None) == 0  # nothing to launch

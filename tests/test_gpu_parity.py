@@ -245,14 +245,58 @@ def test_gemm_vs_torch(a_t, b_t, Mm, Nn, Kk):
               _lib.stream_ptr(DEV))
     ref = torch.relu(A.double() @ Bm.double() + bias.double()).float()
     np.testing.assert_allclose(C.cpu().numpy(), ref.numpy(), atol=1e-4 * (Kk ** 0.5), rtol=1e-4)
-    # split-K path
+    # split-K path (+ row sums of A), inline and deferred through ncf_reduce_batch: bit-identical
     ws = torch.empty(_lib.query("ncf_gemm_splitk_workspace", Mm, Nn, 7), device=DEV)
-    C2 = torch.empty(Mm, Nn, device=DEV)
+    C2, rs = torch.empty(Mm, Nn, device=DEV), torch.empty(Mm, device=DEV)
     _lib.call("ncf_gemm_f32_splitk", Mm, Nn, Kk, As.data_ptr(), Mm if a_t else Kk, a_t,
-              Bs.data_ptr(), Kk if b_t else Nn, b_t, C2.data_ptr(), Nn, 0, 7, ws.data_ptr(),
-              ws.numel(), _lib.stream_ptr(DEV))
+              Bs.data_ptr(), Kk if b_t else Nn, b_t, C2.data_ptr(), Nn, 0, rs.data_ptr(), 7,
+              ws.data_ptr(), ws.numel(), None, _lib.stream_ptr(DEV))
     ref2 = (A.double() @ Bm.double()).float()
     np.testing.assert_allclose(C2.cpu().numpy(), ref2.numpy(), atol=1e-4 * (Kk ** 0.5), rtol=1e-4)
+    np.testing.assert_allclose(rs.cpu().numpy(), A.double().sum(1).float().numpy(),
+                               atol=1e-4 * (Kk ** 0.5), rtol=1e-4)
+    lst = _lib.ReduceList()
+    C3, rs3 = torch.empty(Mm, Nn, device=DEV), torch.empty(Mm, device=DEV)
+    _lib.call("ncf_gemm_f32_splitk", Mm, Nn, Kk, As.data_ptr(), Mm if a_t else Kk, a_t,
+              Bs.data_ptr(), Kk if b_t else Nn, b_t, C3.data_ptr(), Nn, 0, rs3.data_ptr(), 7,
+              ws.data_ptr(), ws.numel(), lst.address, _lib.stream_ptr(DEV))
+    assert lst.count == 2
+    scr = torch.empty(max(1, _lib.query("ncf_reduce_batch_scratch", lst.address)), device=DEV)
+    _lib.call("ncf_reduce_batch", lst.address, scr.data_ptr(), scr.numel(), _lib.stream_ptr(DEV))
+    assert torch.equal(C2, C3) and torch.equal(rs, rs3)
+
+
+def test_reduce_batch_matches_inline_reduce():
+    """Many descriptors (> one launch), P on both sides of the 2-stage threshold, strided outputs,
+    accumulate and scale: ncf_reduce_batch == fp64 sums, and == ncf_gemm_f32_splitk's inline
+    reduce order (checked above)."""
+    from ncf_amd import _lib
+    g = torch.Generator().manual_seed(5)
+    lst = _lib.ReduceList()
+    cases = []
+    for j in range(30):
+        P = [1, 3, 64, 128, 129, 200, 1000][j % 7]
+        L = [1, 7, 64, 65, 300][j % 5]
+        cols = 1 if j % 2 == 0 else L
+        part = torch.randn(P, L + 3, generator=g).to(DEV)      # stride L + 3
+        rows = (L + cols - 1) // cols
+        ldo = cols + 2
+        out = torch.randn(rows * ldo, generator=g).to(DEV)
+        acc, scale = j % 3 == 0, [1.0, 0.5][j % 2]
+        d = lst.d[lst.count]
+        d.part, d.out, d.stride, d.ldo = part.data_ptr(), out.data_ptr(), L + 3, ldo
+        d.L, d.cols, d.P, d.accumulate, d.scale = L, cols, P, int(acc), scale
+        lst.count += 1
+        cases.append((part, out.clone(), out, L, cols, ldo, acc, scale))
+    scr = torch.empty(max(1, _lib.query("ncf_reduce_batch_scratch", lst.address)), device=DEV)
+    _lib.call("ncf_reduce_batch", lst.address, scr.data_ptr(), scr.numel(), _lib.stream_ptr(DEV))
+    for part, before, out, L, cols, ldo, acc, scale in cases:
+        s = part[:, :L].double().sum(0).cpu() * scale
+        exp = before.double().cpu().clone()
+        for i in range(L):
+            k = (i // cols) * ldo + i % cols
+            exp[k] = s[i] + (exp[k] if acc else 0.0)
+        np.testing.assert_allclose(out.cpu().double().numpy(), exp.numpy(), rtol=1e-5, atol=1e-4)
 
 
 def test_embedding_bwd_segment_reduce():
@@ -487,3 +531,33 @@ def test_sharded_step_world1_bitwise_equals_fused():
             assert torch.equal(a[k], b[k]), k
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("Mm,Nn,Kk", [(77, 130, 45), (20480, 64, 64), (256, 96, 1000), (1, 5, 3),
+                                      (64, 256, 128)])
+def test_gemm_direct_and_splitk_rowsum_vs_torch(a_t, b_t, Mm, Nn, Kk):
+    from ncf_amd import _lib
+    g = torch.Generator().manual_seed(Mm * 7 + Nn + Kk)
+    A = torch.randn(Mm, Kk, generator=g)
+    Bm = torch.randn(Kk, Nn, generator=g) * torch.linspace(0.5, 2.0, Nn)  # asymmetric
+    bias = torch.randn(Nn, generator=g)
+    As = (A.t().contiguous() if a_t else A).to(DEV)
+    Bs = (Bm.t().contiguous() if b_t else Bm).to(DEV)
+    lda, ldb = (Mm if a_t else Kk), (Kk if b_t else Nn)
+    C = torch.full((Mm, Nn), 3.0, device=DEV)
+    _lib.call("ncf_gemm_direct", Mm, Nn, Kk, As.data_ptr(), lda, a_t, Bs.data_ptr(), ldb, b_t,
+              C.data_ptr(), Nn, bias.to(DEV).data_ptr(), 1 | 2, _lib.stream_ptr(DEV))  # relu, accum
+    ref = (torch.relu(A.double() @ Bm.double() + bias.double()) + 3.0).float()
+    np.testing.assert_allclose(C.cpu().numpy(), ref.numpy(), atol=2e-5 * (Kk ** 0.5), rtol=1e-5)
+    for splits in (1, 7):
+        ws = torch.empty(_lib.query("ncf_gemm_splitk_workspace", Mm, Nn, splits), device=DEV)
+        C2 = torch.empty(Mm, Nn, device=DEV)
+        db = torch.empty(Mm, device=DEV)
+        _lib.call("ncf_gemm_f32_splitk", Mm, Nn, Kk, As.data_ptr(), lda, a_t, Bs.data_ptr(), ldb,
+                  b_t, C2.data_ptr(), Nn, 0, db.data_ptr(), splits, ws.data_ptr(), ws.numel(),
+                  None, _lib.stream_ptr(DEV))
+        np.testing.assert_allclose(C2.cpu().numpy(), (A.double() @ Bm.double()).float().numpy(),
+                                   atol=2e-5 * (Kk ** 0.5), rtol=1e-5)
+        np.testing.assert_allclose(db.cpu().numpy(), A.double().sum(1).float().numpy(),
+                                   atol=2e-5 * (Kk ** 0.5), rtol=1e-5)
