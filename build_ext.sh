@@ -7,6 +7,7 @@ OUT="$ROOT/neural-collaborative-filtering-demo_amd/libncf_hip.so"
 HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 OBJ="$SRC/build"
 mkdir -p "$OBJ"
+rm -f "$OBJ"/*.o
 FLAGS=(--offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$SRC" -I"$ROOT/include" -Wall -Wno-unused-function)
 pids=()
 for f in "$SRC"/*.hip; do

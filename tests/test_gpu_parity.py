@@ -561,3 +561,40 @@ def test_gemm_direct_and_splitk_rowsum_vs_torch(a_t, b_t, Mm, Nn, Kk):
                                    atol=2e-5 * (Kk ** 0.5), rtol=1e-5)
         np.testing.assert_allclose(db.cpu().numpy(), A.double().sum(1).float().numpy(),
                                    atol=2e-5 * (Kk ** 0.5), rtol=1e-5)
+
+@pytest.mark.parametrize("n0,n1", [(1, 1), (1023, 1025), (5000, 3000), (70000, 20480), (0, 7)])
+@pytest.mark.parametrize("rows0,rows1", [(1, 2000), (1 << 20, 100000), (1 << 23, 3)])
+def test_dedup_ids_vs_numpy(n0, n1, rows0, rows1):
+    """Onesweep radix dedup (1, 2 and 3 passes; ragged tiles; look-back over many tiles; a
+    Zipf-hot id): uniq ids == np.unique, counts, slot maps and the inverse map."""
+    from ncf_amd import _lib
+    rng = np.random.default_rng(n0 * 31 + n1 + rows0 % 97)
+    ids = []
+    for n, rows in ((n0, rows0), (n1, rows1)):
+        x = (rng.zipf(1.2, n) - 1) % rows if n else np.zeros(0, np.int64)
+        if n > 100:
+            x[::7] = rows - 1
+        ids.append(torch.from_numpy(x.astype(np.int64)))
+    n = max(n0, n1)
+    D = 64
+    ws = torch.empty(_lib.query("ncf_embedding_bwd_workspace", n, D), dtype=torch.uint8, device=DEV)
+    uq = [torch.full((max(1, n),), -7, dtype=torch.int64, device=DEV) for _ in range(2)]
+    slot = [torch.full((r,), -1, dtype=torch.int32, device=DEV) for r in (rows0, rows1)]
+    inv = [torch.full((max(1, n),), -7, dtype=torch.int64, device=DEV) for _ in range(2)]
+    nu = torch.full((2,), 99, dtype=torch.int32, device=DEV)
+    dv = [t.to(DEV) for t in ids]
+    st = _lib.stream_ptr(DEV)
+    _lib.call("ncf_dedup_ids2", dv[0].data_ptr(), n0, rows0, dv[1].data_ptr(), n1, rows1, D,
+              uq[0].data_ptr(), uq[1].data_ptr(), slot[0].data_ptr(), slot[1].data_ptr(),
+              nu.data_ptr(), ws.data_ptr(), ws.numel(), st)
+    _lib.call("ncf_dedup_inverse", n0, n1, rows0, rows1, D, inv[0].data_ptr(), inv[1].data_ptr(),
+              ws.data_ptr(), ws.numel(), st)
+    torch.cuda.synchronize()
+    for k, (x, nk) in enumerate(zip(ids, (n0, n1))):
+        u, iv = np.unique(x.numpy(), return_inverse=True)
+        assert int(nu[k]) == len(u)
+        np.testing.assert_array_equal(uq[k][:len(u)].cpu().numpy(), u)
+        np.testing.assert_array_equal(inv[k][:nk].cpu().numpy(), iv)
+        s = slot[k].cpu().numpy()
+        np.testing.assert_array_equal(s[u], np.arange(len(u)))
+        assert (np.delete(s, u) == -1).all()
