@@ -67,6 +67,13 @@ int ncf_gemm_direct(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda
                     const float* B, int64_t ldb, int b_trans, float* C, int64_t ldc,
                     const float* bias, int flags, void* stream);
 
+/* Weights-resident streaming variant (row-major A only; K, N in {64,128,256}, N*K <= 32768):
+ * B is staged once per workgroup into LDS, waves stream 32-row tiles of A with all N output
+ * columns each (A read from HBM exactly once).  Same B / flags convention as ncf_gemm_f32.   */
+int ncf_gemm_rows(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
+                  int64_t ldb, int b_trans, float* C, int64_t ldc, const float* bias, int flags,
+                  void* stream);
+
 /* ---- deferred reductions --------------------------------------------------------------------
  * Every backward call that produces a parameter gradient as a sum over batch rows writes
  * per-block partial rows and reduces them in a fixed order (bitwise reproducible, no float
@@ -103,6 +110,22 @@ int ncf_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float* A, int64_t
                         int64_t ldc, int accumulate, float* row_sums, int splits,
                         float* workspace, int64_t workspace_floats, ncf_reduce_list* defer,
                         void* stream);
+/* Grouped weight gradients (all dW = dYᵀ·X of a step in one launch, + bias gradients = column
+ * sums of dY when dbias != NULL).  dY [n, m_out] (ld ldy), X [n, k_in] (ld ldx), dW [m_out, k_in]
+ * (ld ldw, accumulate or overwrite); the batch rows are split into `slabs` row slabs whose
+ * partials are summed in slab order (deferred to `defer` when non-NULL).                      */
+typedef struct ncf_wgrad_desc {
+  const float* dy;
+  const float* x;
+  float* dw;
+  float* dbias;
+  int64_t ldy, ldx, ldw;
+  int32_t m_out, k_in, n, slabs, accumulate, reserved;
+} ncf_wgrad_desc;
+#define NCF_WGRAD_GROUP_MAX 8
+int64_t ncf_wgrad_grouped_workspace(const ncf_wgrad_desc* descs, int count);
+int ncf_wgrad_grouped(const ncf_wgrad_desc* descs, int count, float* workspace,
+                      int64_t workspace_floats, ncf_reduce_list* defer, void* stream);
 int64_t ncf_colsum_workspace(int64_t rows, int64_t cols);
 /* Bias gradients: out[c] (+)= sum_r X[r*ld+c]. */
 int ncf_colsum(const float* X, int64_t rows, int64_t cols, int64_t ld, float* out,

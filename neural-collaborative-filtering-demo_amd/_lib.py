@@ -42,6 +42,9 @@ SIGNATURES = {
     "ncf_gemm_f32_splitk": (I32, [I64, I64, I64, P, I64, I32, P, I64, I32, P, I64, I32, P, I32,
                                   P, I64, P, P]),
     "ncf_gemm_direct": (I32, [I64, I64, I64, P, I64, I32, P, I64, I32, P, I64, P, I32, P]),
+    "ncf_gemm_rows": (I32, [I64, I64, I64, P, I64, P, I64, I32, P, I64, P, I32, P]),
+    "ncf_wgrad_grouped_workspace": (I64, [P, I32]),
+    "ncf_wgrad_grouped": (I32, [P, I32, P, I64, P, P]),
     "ncf_reduce_batch_scratch": (I64, [P]),
     "ncf_reduce_batch": (I32, [P, P, I64, P]),
     "ncf_colsum_workspace": (I64, [I64, I64]),
@@ -93,6 +96,17 @@ class ReduceDesc(ctypes.Structure):
 
 
 REDUCE_LIST_MAX = 64
+
+
+class WgradDesc(ctypes.Structure):
+    """ncf_wgrad_desc (include/ncf_hip.h)."""
+    _fields_ = [("dy", P), ("x", P), ("dw", P), ("dbias", P), ("ldy", I64), ("ldx", I64),
+                ("ldw", I64), ("m_out", ctypes.c_int32), ("k_in", ctypes.c_int32),
+                ("n", ctypes.c_int32), ("slabs", ctypes.c_int32), ("accumulate", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+WGRAD_GROUP_MAX = 8
 
 
 class ReduceList(ctypes.Structure):

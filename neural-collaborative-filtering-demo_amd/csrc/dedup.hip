@@ -25,6 +25,9 @@ using namespace ncf_seg;
 namespace {
 
 constexpr uint32_t ST_AGG = 1u << 30, ST_INCL = 2u << 30, ST_MASK = (1u << 30) - 1;
+// up to this many tiles per kind, a tile sums all predecessors' aggregates directly (one round of
+// independent loads); beyond it, the classic chained look-back (work linear in the tile count)
+constexpr int kDirectTiles = 64;
 
 __device__ __forceinline__ uint32_t ld_status(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -181,24 +184,51 @@ __global__ __launch_bounds__(256) void k_onesweep(
     }
   }
   __syncthreads();
-  // look-back: counts of this digit in all earlier tiles
-  for (int d = tid; d < R; d += 256) {
-    uint32_t excl = 0;
-    if (tile > 0) {
-      int t = tile - 1;
-      while (true) {
-        const uint32_t s = ld_status(&st[(int64_t)t * R + d]);
-        if ((s & ~ST_MASK) == 0) {
-          __builtin_amdgcn_s_sleep(1);
-          continue;
+  if (nb <= kDirectTiles) {
+    // few tiles: sum the aggregates of ALL earlier tiles directly (independent loads, 2 digits
+    // per 64-bit load, 8 tiles per batch) instead of walking an inclusive-prefix chain
+    const uint64_t* st64 = reinterpret_cast<const uint64_t*>(st);
+    for (int d0 = 2 * tid; d0 < R; d0 += 512) {
+      uint32_t e0 = 0, e1 = 0;
+      for (int tb = 0; tb < tile; tb += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = tb + j < tile ? ld_status64(&st64[((int64_t)(tb + j) * R + d0) / 2])
+                               : ((uint64_t)ST_AGG << 32 | ST_AGG);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          while (((uint32_t)v[j] & ~ST_MASK) == 0 || ((uint32_t)(v[j] >> 32) & ~ST_MASK) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            v[j] = ld_status64(&st64[((int64_t)(tb + j) * R + d0) / 2]);
+          }
+          e0 += (uint32_t)v[j] & ST_MASK;
+          e1 += (uint32_t)(v[j] >> 32) & ST_MASK;
         }
-        excl += s & ST_MASK;
-        if (s & ST_INCL) break;
-        --t;
       }
-      st_status(&st[(int64_t)tile * R + d], ST_INCL | (excl + tcnt[d]));
+      base[d0] += e0;
+      base[d0 + 1] += e1;
     }
-    base[d] += excl;
+  } else {
+    // decoupled look-back: counts of this digit in all earlier tiles
+    for (int d = tid; d < R; d += 256) {
+      uint32_t excl = 0;
+      if (tile > 0) {
+        int t = tile - 1;
+        while (true) {
+          const uint32_t s = ld_status(&st[(int64_t)t * R + d]);
+          if ((s & ~ST_MASK) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+          }
+          excl += s & ST_MASK;
+          if (s & ST_INCL) break;
+          --t;
+        }
+        st_status(&st[(int64_t)tile * R + d], ST_INCL | (excl + tcnt[d]));
+      }
+      base[d] += excl;
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -252,39 +282,61 @@ __global__ __launch_bounds__(256) void k_segments(
     }
   }
   __syncthreads();
-  if (tid == 0) {
+  if (w == 0) {
     uint64_t S = 0, Pc = 0;
     for (int q = 0; q < 16; ++q) { S += ws_s[q]; Pc += ws_p[q]; }
     uint64_t es = 0, ep = 0;
-    if (tile == 0) {
-      st_status64(&st[0], F_INCL | (S << 31) | Pc);
-    } else {
-      st_status64(&st[tile], F_AGG | (S << 31) | Pc);
-      int t = tile - 1;
-      while (true) {
-        const uint64_t s = ld_status64(&st[t]);
-        if ((s >> 62) == 0) {
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        es += (s >> 31) & M31;
-        ep += s & M31;
-        if (s & F_INCL) break;
-        --t;
+    if (nb <= kDirectTiles) {
+      // all predecessors at once: lane j reads tile j's aggregate
+      if (lane == 0) st_status64(&st[tile], F_AGG | (S << 31) | Pc);
+      uint64_t v = 0;
+      if (lane < tile) {
+        do {
+          v = ld_status64(&st[lane]);
+          if ((v >> 62) == 0) __builtin_amdgcn_s_sleep(1);
+        } while ((v >> 62) == 0);
       }
-      st_status64(&st[tile], F_INCL | ((es + S) << 31) | (ep + Pc));
+      uint32_t a = (uint32_t)((v >> 31) & M31), b = (uint32_t)(v & M31);  // totals < 2^30
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+      }
+      es = a;
+      ep = b;
+    } else if (lane == 0) {
+      if (tile == 0) {
+        st_status64(&st[0], F_INCL | (S << 31) | Pc);
+      } else {
+        st_status64(&st[tile], F_AGG | (S << 31) | Pc);
+        int t = tile - 1;
+        while (true) {
+          const uint64_t s = ld_status64(&st[t]);
+          if ((s >> 62) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+          }
+          es += (s >> 31) & M31;
+          ep += s & M31;
+          if (s & F_INCL) break;
+          --t;
+        }
+        st_status64(&st[tile], F_INCL | ((es + S) << 31) | (ep + Pc));
+      }
     }
-    s_es = (uint32_t)es;
-    s_ep = (uint32_t)ep;
-    segoff[(int64_t)kind * nbmax + tile] = (uint32_t)es;
-    if (tile == nb - 1) {
-      const uint32_t U = (uint32_t)(es + S), Pn = (uint32_t)(ep + Pc);
-      totals[kind] = U;
-      totals[2 + kind] = Pn;
-      if (num_unique) num_unique[kind] = U;
-      (kind ? start1 : start0)[U] = (uint32_t)n;
-      (kind ? pstart1 : pstart0)[Pn] = (uint32_t)n;
-      (kind ? fpiece1 : fpiece0)[U] = Pn;
+    if (lane == 0) {
+      s_es = (uint32_t)es;
+      s_ep = (uint32_t)ep;
+      segoff[(int64_t)kind * nbmax + tile] = (uint32_t)es;
+      if (tile == nb - 1) {
+        const uint32_t U = (uint32_t)(es + S), Pn = (uint32_t)(ep + Pc);
+        totals[kind] = U;
+        totals[2 + kind] = Pn;
+        if (num_unique) num_unique[kind] = U;
+        (kind ? start1 : start0)[U] = (uint32_t)n;
+        (kind ? pstart1 : pstart0)[Pn] = (uint32_t)n;
+        (kind ? fpiece1 : fpiece0)[U] = Pn;
+      }
     }
   }
   __syncthreads();
@@ -310,7 +362,7 @@ __global__ __launch_bounds__(256) void k_segments(
     if (ph[r]) {
       const uint32_t p = bp + pre_p + pr[r] - 1;
       pstart[p] = (uint32_t)i;
-      pseg[p] = c;
+      pseg[p] = c | (sh[r] ? FIRST_PIECE : 0u);
       if (sh[r]) fpiece[c] = p;
     }
   }
@@ -402,8 +454,8 @@ extern "C" int ncf_dedup_ids2(const int64_t* ids0, int64_t n0, int64_t rows0, co
   }
   hipLaunchKernelGGL(k_segments, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n0, n1, w.nb,
                      w.sstatus, w.tickets + 2 * MAXP, w.segoff, w.start0, w.start1, w.pstart0,
-                     w.pstart1, w.pseg0, w.pseg1, w.fpiece0, w.fpiece1, uniq0, uniq1, slot0, slot1,
-                     w.totals, num_unique);
+                     w.pstart1, w.pseg0, w.pseg1, w.fpiece0, w.fpiece1, uniq0, uniq1,
+                     slot0, slot1, w.totals, num_unique);
   NCF_CHECK_LAUNCH("ncf_dedup_ids(segments)");
   return NCF_OK;
 }

@@ -31,7 +31,6 @@ __global__ __launch_bounds__(256) void k_piece_reduce_ln(
     const uint32_t* __restrict__ sv0, const uint32_t* __restrict__ sv1,
     const uint32_t* __restrict__ pstart0, const uint32_t* __restrict__ pstart1,
     const uint32_t* __restrict__ pseg0, const uint32_t* __restrict__ pseg1,
-    const uint32_t* __restrict__ fpiece0, const uint32_t* __restrict__ fpiece1,
     const int64_t* __restrict__ uniq0, const int64_t* __restrict__ uniq1,
     const uint32_t* __restrict__ totals, const float* __restrict__ dy_mf0,
     const float* __restrict__ dy_mlp0, const float* __restrict__ dy_mf1,
@@ -49,8 +48,7 @@ __global__ __launch_bounds__(256) void k_piece_reduce_ln(
   const uint32_t* sv = kind ? sv1 : sv0;
   const uint32_t* pstart = kind ? pstart1 : pstart0;
   const uint32_t* pseg = kind ? pseg1 : pseg0;
-  const uint32_t* fpiece = kind ? fpiece1 : fpiece0;
-  const int64_t* uniq = kind ? uniq1 : uniq0;
+  const int64_t* uniq = kind ? uniq1 : uniq0;  // table row of each segment (caller's id space)
   const float* dmf = kind ? dy_mf1 : dy_mf0;
   const float* dml = kind ? dy_mlp1 : dy_mlp0;
   const float* tmf = kind ? t_mf1 : t_mf0;
@@ -65,8 +63,13 @@ __global__ __launch_bounds__(256) void k_piece_reduce_ln(
   const float4 gm = ld4(g_mf + col), gl = ld4(g_mlp + col);
   float4 a_gm = make_float4(0, 0, 0, 0), a_bm = a_gm, a_gl = a_gm, a_bl = a_gm;
   for (int64_t p = (int64_t)blockIdx.x * 4 + w; p < Pn; p += (int64_t)gridDim.x * 4) {
+    // the piece record (independent loads), the table rows as soon as the row is known, then
+    // the occurrence positions and their gradient rows
     const uint32_t ps = pstart[p];
     const int cnt = (int)(pstart[p + 1] - ps);  // 1..PIECE
+    const uint32_t info = pseg[p];
+    const int64_t id = uniq[info & ~FIRST_PIECE];
+    const float4 x_mf = ld4(tmf + id * D + col), x_ml = ld4(tml + id * D + col);
     sidx[w][lane] = lane < cnt ? sv[ps + lane] : 0u;
     __builtin_amdgcn_wave_barrier();
     // sub-group sg sums occurrences j = sg, sg + S, ... in order; 4 rows of loads in flight
@@ -99,13 +102,12 @@ __global__ __launch_bounds__(256) void k_piece_reduce_ln(
       sl.x += __shfl_xor(sl.x, o, 64); sl.y += __shfl_xor(sl.y, o, 64);
       sl.z += __shfl_xor(sl.z, o, 64); sl.w += __shfl_xor(sl.w, o, 64);
     }
-    const int64_t c = pseg[p];
-    const int64_t id = uniq[c];
-    const bool first = fpiece[c] == (uint32_t)p;
+    const int64_t c = info & ~FIRST_PIECE;
+    const bool first = (info & FIRST_PIECE) != 0;
     // two LayerNorm backwards (GMF row, MLP row); every sub-group computes, sub-group 0 stores
 #pragma unroll
     for (int tbl = 0; tbl < 2; ++tbl) {
-      const float4 x = ld4((tbl ? tml : tmf) + id * D + col);
+      const float4 x = tbl ? x_ml : x_mf;
       const float4 dy = tbl ? sl : sm;
       const float4 gg = tbl ? gl : gm;
       const float mean = group_sum<L>(x.x + x.y + x.z + x.w) * (1.0f / D);
@@ -196,7 +198,7 @@ int piece_reduce(const WS& w, int64_t n, const uint32_t* sv0, const uint32_t* sv
                  float eps, float* Gmf0, float* Gml0, float* Gmf1, float* Gml1, float* dgm,
                  float* dbm, float* dgl, float* dbl, ncf_reduce_list* defer, hipStream_t st) {
   hipLaunchKernelGGL(k_piece_reduce_ln<D>, dim3(w.nbr, 2), dim3(256), 0, st, sv0, sv1, w.pstart0,
-                     w.pstart1, w.pseg0, w.pseg1, w.fpiece0, w.fpiece1, uniq0, uniq1, w.totals,
+                     w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
                      dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
                      Gmf1, Gml1, w.xp0, w.xp1, w.part);
   NCF_CHECK_LAUNCH("ncf_embedding_bwd(piece_reduce)");

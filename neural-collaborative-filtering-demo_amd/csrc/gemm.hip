@@ -67,7 +67,25 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int M, int N, int K, const flo
   float rs = 0.0f;
 
   float4 ra[4], rb[2];
+  // interior tiles (block-uniform test) take unguarded float4 loads: no exec-masked branches
+  // around the prefetch, so the compiler keeps it in flight across the MFMAs
+  const bool interior = vec && m0 + BM <= M && n0 + BN <= N;
   auto load = [&](int k0) {
+    if (interior && k0 + BK <= ke) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int e = tid + 256 * r;
+        ra[r] = !A_T ? ld4(A + (int64_t)(m0 + (e >> 3)) * lda + k0 + (e & 7) * 4)
+                     : ld4(A + (int64_t)(k0 + (e >> 5)) * lda + m0 + (e & 31) * 4);
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int e = tid + 256 * r;
+        rb[r] = B_T ? ld4(B + (int64_t)(n0 + (e >> 3)) * ldb + k0 + (e & 7) * 4)
+                    : ld4(B + (int64_t)(k0 + (e >> 4)) * ldb + n0 + (e & 15) * 4);
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int e = tid + 256 * r;

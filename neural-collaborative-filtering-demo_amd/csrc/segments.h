@@ -6,8 +6,9 @@
 //   sorted (key, position) pairs      — stable LSD radix sort, 2 passes for <= 2^22 rows;
 //   segments c = 0..U-1               — start[c] (sorted position), uniq[c] (id), U = totals[kind];
 //   pieces p = 0..Pn-1                — a segment split at every sorted position multiple of
-//                                       PIECE: pstart[p], pseg[p] (its segment), first piece of
-//                                       segment c = fpiece[c], Pn = totals[2 + kind];
+//                                       PIECE: pstart[p], pseg[p] = its segment | FIRST_PIECE
+//                                       for a segment's first piece, first piece of segment
+//                                       c = fpiece[c], Pn = totals[2 + kind];
 //   segoff[kind][tile]                — segments starting before sort tile `tile`.
 #pragma once
 #include "ncf_common.h"
@@ -19,6 +20,7 @@ constexpr int PIECE = 64;         // max occurrences one wave reduces in the emb
 constexpr int MAX_BITS = 11;      // radix digit bits
 constexpr int MAXR = 1 << MAX_BITS;
 constexpr int MAXP = 3;           // passes for 32-bit keys
+constexpr uint32_t FIRST_PIECE = 1u << 31;
 
 struct WS {
   // zeroed by every dedup (one memset over [tickets, status + used part)): tickets, digit

@@ -11,6 +11,7 @@ Data layout in HBM (fp32 throughout — the reference computes in fp32):
     parallel flat gradient buffer the backward kernels write into (p.grad are views of it);
   * per-batch activations: a workspace keyed by (N, M), reused across steps (no per-step allocs).
 """
+import ctypes
 import math
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -67,19 +68,11 @@ class Workspace:
         self.loss = e(1)
         # Backward workspaces.  Every gradient reduction of the backward is deferred into
         # red_list and run by one ncf_reduce_batch at its end, so each producing call site keeps
-        # its partials in its own slice of `red_ws` until then.
-        self.splits = {}
+        # its partials in its own slice of `red_ws` until then; the weight gradients are queued
+        # in `wgrads` and run as one grouped launch (wg_ws holds their slab partials).
         sites = [("head", _lib.query("ncf_head_bwd_workspace", n, g.hidden[-1], D))]
-        kins = [D] + g.hidden[:-1]
-        for l, (h, kin) in enumerate(zip(g.hidden, kins)):
-            s = self.splits_for(h, kin, n)
-            self.splits[(h, kin)] = s
+        for l, h in enumerate(g.hidden):
             sites.append((f"relu{l}", _lib.query("ncf_relu_ln_dropout_bwd_workspace", n, h)))
-            sites.append((f"mlp{l}", _lib.query("ncf_gemm_splitk_workspace", h, kin, s)))
-        s = self.splits_for(D, D, n)
-        self.splits[(D, D)] = s
-        for nm in ("out_proj", "q_proj", "k_proj", "v_proj"):
-            sites.append((nm, _lib.query("ncf_gemm_splitk_workspace", D, D, s)))
         self.site_off, off = {}, 0
         for name, size in sites:
             self.site_off[name] = (off, size)
@@ -87,6 +80,8 @@ class Workspace:
         self.red_ws = e(max(off, 1))
         self.red_list = _lib.ReduceList()
         self.red_scratch = e(1)
+        self.wgrads = []            # weight gradients collected during a backward (grouped launch)
+        self.wg_ws = e(1)
         self.emb_ws = torch.empty(_lib.query("ncf_embedding_bwd_workspace", n, D),
                                   dtype=torch.uint8, device=device)
         self.G = {k: e(n, D) for k in ("mf_user", "mlp_user", "mf_item", "mlp_item")}
@@ -96,9 +91,27 @@ class Workspace:
 
     @staticmethod
     def splits_for(m_out: int, k_out: int, rows: int) -> int:
-        """K-splits of a weight-gradient GEMM (measured optimum ~160 slabs at the C2 shapes,
-        tools/gemm_bench.py), >= 128 batch rows per slab."""
-        return max(1, min(160, math.ceil(max(rows, 1) / 128)))
+        """Row slabs of a weight-gradient product: ~160 batch rows per wave (a few waves per SIMD
+        over the grouped launch of a step), at most 256 slabs."""
+        return max(1, min(256, math.ceil(max(rows, 1) / 160)))
+
+    def run_wgrads(self, st):
+        """Every weight gradient collected by this backward in one grouped launch; the slab
+        reductions join the deferred list."""
+        if not self.wgrads:
+            return
+        descs = (_lib.WgradDesc * len(self.wgrads))()
+        for d, (dY, ldy, X, ldx, dW, ldw, m_out, k_in, n, dbias) in zip(descs, self.wgrads):
+            d.dy, d.x, d.dw, d.dbias = ptr(dY), ptr(X), ptr(dW), ptr(dbias)
+            d.ldy, d.ldx, d.ldw = ldy, ldx, ldw
+            d.m_out, d.k_in, d.n, d.slabs, d.accumulate = m_out, k_in, n, self.splits_for(m_out, k_in, n), 0
+        addr = ctypes.addressof(descs)
+        need = _lib.query("ncf_wgrad_grouped_workspace", addr, len(self.wgrads))
+        if self.wg_ws.numel() < need:
+            self.wg_ws = torch.empty(need, dtype=torch.float32, device=self.red_ws.device)
+        _lib.call("ncf_wgrad_grouped", addr, len(self.wgrads), ptr(self.wg_ws), self.wg_ws.numel(),
+                  self.red_list.address, st)
+        self.wgrads = []
 
     def site(self, name: str) -> torch.Tensor:
         off, size = self.site_off[name]
@@ -224,21 +237,20 @@ class NCFEngine:
     @staticmethod
     def _gemm(A, lda, a_t, Bm, ldb, b_t, C, ldc, M, N, K, bias=None, relu=False, accum=False, st=None):
         flags = (1 if relu else 0) | (2 if accum else 0)
-        # LDS-tiled 128x64 kernel, except the square DxD attention projections where the LDS-free
-        # wave-per-tile kernel is faster (tools/gemm_bench.py)
-        fn = "ncf_gemm_direct" if (N == K and N <= 64) else "ncf_gemm_f32"
-        _lib.call(fn, M, N, K, ptr(A), lda, int(a_t), ptr(Bm), ldb, int(b_t), ptr(C),
+        # weights-resident streaming kernel for the small-weight layers, LDS-tiled 128x64 kernel
+        # for the 128x256 / 256x128 ones (measured per shape, tools/gemm_bench.py)
+        if not a_t and K in (64, 128, 256) and N in (64, 128, 256) and K * N <= 16384 and K <= 128:
+            _lib.call("ncf_gemm_rows", M, N, K, ptr(A), lda, ptr(Bm), ldb, int(b_t), ptr(C), ldc,
+                      ptr(bias), flags, st)
+            return
+        _lib.call("ncf_gemm_f32", M, N, K, ptr(A), lda, int(a_t), ptr(Bm), ldb, int(b_t), ptr(C),
                   ldc, ptr(bias), flags, st)
 
-    def _wgrad(self, w: Workspace, site: str, dY, ldy, X, ldx, dW, ldw, m_out, k_in, n, st,
-               dbias=None):
-        """dW[m_out, k_in] = dYᵀ[m_out, n] · X[n, k_in] (split-K over the batch rows); with
-        ``dbias`` also the bias gradient (row sums of dYᵀ) from the same pass.  The slab
-        reduction is deferred to the end of the backward (Workspace.run_reductions)."""
-        s = w.splits.get((m_out, k_in)) or Workspace.splits_for(m_out, k_in, n)
-        ws = w.site(site)
-        _lib.call("ncf_gemm_f32_splitk", m_out, k_in, n, ptr(dY), ldy, 1, ptr(X), ldx, 0, ptr(dW),
-                  ldw, 0, ptr(dbias), s, ptr(ws), ws.numel(), w.red_list.address, st)
+    @staticmethod
+    def _wgrad(w: Workspace, dY, ldy, X, ldx, dW, ldw, m_out, k_in, n, dbias=None):
+        """Queue dW[m_out, k_in] = dYᵀ[m_out, n] · X[n, k_in] (+ dbias = column sums of dY) for the
+        grouped launch at the end of the backward (Workspace.run_wgrads)."""
+        w.wgrads.append((dY, ldy, X, ldx, dW, ldw, m_out, k_in, n, dbias))
 
     # ------------------------------------------------------------------ forward
     def sync_tables(self):
@@ -334,6 +346,7 @@ class NCFEngine:
         iid = iid.to(device=dev, dtype=torch.int64).contiguous()
         gv = self.grad_view
         w.red_list.count = 0
+        w.wgrads = []
         # a12 + a8 backward (trainer.py:271; architecture.py:245-252)
         gp = None if grad_prob is None else grad_prob.reshape(-1).to(torch.float32).contiguous()
         tg = None if targets is None else targets.reshape(-1).to(device=dev, dtype=torch.float32).contiguous()
@@ -358,7 +371,7 @@ class NCFEngine:
             xin, kin = (w.y, D) if l == 0 else (w.a[l - 1], hid[l - 1])
             ldw = lin.weight.shape[1]
             dW = gv(f"mlp.{4 * l}.weight")
-            self._wgrad(w, f"mlp{l}", w.dlin[l], h, xin, kin, dW, ldw, h, kin, n, st)
+            self._wgrad(w, w.dlin[l], h, xin, kin, dW, ldw, h, kin, n)
             if ldw > kin:  # zero temporal columns of mlp.0 (their input is all-zero)
                 _lib.call("ncf_fill_2d", ptr(dW[:, kin:]), h, ldw - kin, ldw, 0.0, st)
             dx = w.dy if l == 0 else w.da[l - 1]
@@ -366,14 +379,14 @@ class NCFEngine:
         # a5 backward: out_proj, core, q/k/v projections
         att = m.user_product_attention
         src = w.o
-        self._wgrad(w, "out_proj", w.dy, D, src, D, gv("user_product_attention.out_proj.weight"), D,
-                    D, D, n, st, dbias=gv("user_product_attention.out_proj.bias"))
+        self._wgrad(w, w.dy, D, src, D, gv("user_product_attention.out_proj.weight"), D, D, D, n,
+                    dbias=gv("user_product_attention.out_proj.bias"))
         self._gemm(w.dy, D, 0, att.out_proj.weight, D, 0, w.do, D, n, D, D, st=st)
         _lib.call("ncf_attention_bwd", ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P), ptr(w.do), n // M, M,
                   H, D, drop_p, seed, ptr(w.dS), ptr(w.dq), ptr(w.dk), ptr(w.dv), st)
         for nm, dX, X in (("q_proj", w.dq, w.xu), ("k_proj", w.dk, w.xi), ("v_proj", w.dv, w.xi)):
-            self._wgrad(w, nm, dX, D, X, D, gv(f"user_product_attention.{nm}.weight"), D, D, D, n,
-                        st, dbias=gv(f"user_product_attention.{nm}.bias"))
+            self._wgrad(w, dX, D, X, D, gv(f"user_product_attention.{nm}.weight"), D, D, D, n,
+                        dbias=gv(f"user_product_attention.{nm}.bias"))
         self._gemm(w.dq, D, 0, att.q_proj.weight, D, 0, w.dxu, D, n, D, D, st=st)
         self._gemm(w.dk, D, 0, att.k_proj.weight, D, 0, w.dxi, D, n, D, D, st=st)
         self._gemm(w.dv, D, 0, att.v_proj.weight, D, 0, w.dxi, D, n, D, D, accum=True, st=st)
@@ -394,6 +407,7 @@ class NCFEngine:
                   ptr(uq_i), ptr(gv("mf_norm.weight")), ptr(gv("mf_norm.bias")),
                   ptr(gv("mlp_norm.weight")), ptr(gv("mlp_norm.bias")), ptr(w.emb_ws),
                   w.emb_ws.numel(), w.red_list.address, st)
+        w.run_wgrads(st)
         w.run_reductions(st)
         self.pending = w
 

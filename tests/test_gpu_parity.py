@@ -4,6 +4,8 @@ and the CPU oracle.  Runs on a real MI355X only (marker ``gpu``).
 Tolerances (tests/parity.py): fp32 forward abs <= 2e-6 on probabilities; gradients
 rel 1e-4 / abs 1e-6 (summation order differs from ATen's CPU kernels); post-Adam parameters abs
 1e-6 outside the sign-flip zone (<= 2*lr per step inside it)."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -598,3 +600,52 @@ def test_dedup_ids_vs_numpy(n0, n1, rows0, rows1):
         s = slot[k].cpu().numpy()
         np.testing.assert_array_equal(s[u], np.arange(len(u)))
         assert (np.delete(s, u) == -1).all()
+
+
+@pytest.mark.parametrize("shapes", [
+    [(64, 64), (64, 128), (128, 256), (256, 64)],      # C2: attention + MLP tower
+    [(16, 16), (64, 16), (32, 64), (1, 32)],           # C1 dims + a 1-row output
+])
+@pytest.mark.parametrize("n", [20480, 999, 1])
+def test_wgrad_grouped_vs_torch(shapes, n):
+    """All weight gradients of a step in one grouped launch: dW = dYᵀX (+ bias = column sums of
+    dY), strided inputs, accumulate; inline reduce and deferred reduce are bit-identical."""
+    from ncf_amd import _lib
+    g = torch.Generator().manual_seed(n + len(shapes))
+    st = _lib.stream_ptr(DEV)
+    descs = (_lib.WgradDesc * len(shapes))()
+    keep, refs = [], []
+    for k, (mo, ki) in enumerate(shapes):
+        dy = torch.randn(n, mo + 3, generator=g).to(DEV)       # ld = mo + 3 (strided)
+        x = torch.randn(n, ki + 1, generator=g).to(DEV)
+        dw = torch.randn(mo, ki + 2, generator=g).to(DEV)      # ldw = ki + 2
+        db = torch.empty(mo, device=DEV)
+        acc = k % 2
+        ref_w = dy[:, :mo].double().t() @ x[:, :ki].double() + (dw[:, :ki].double() if acc else 0)
+        refs.append((ref_w, dy[:, :mo].double().sum(0)))
+        d = descs[k]
+        d.dy, d.x, d.dw, d.dbias = dy.data_ptr(), x.data_ptr(), dw.data_ptr(), db.data_ptr()
+        d.ldy, d.ldx, d.ldw = mo + 3, ki + 1, ki + 2
+        d.m_out, d.k_in, d.n, d.slabs, d.accumulate = mo, ki, n, max(1, n // 160), acc
+        keep.append((dy, x, dw, db, dw.clone()))
+    ws = torch.empty(_lib.query("ncf_wgrad_grouped_workspace", ctypes.addressof(descs), len(shapes)),
+                     device=DEV)
+    _lib.call("ncf_wgrad_grouped", ctypes.addressof(descs), len(shapes), ws.data_ptr(), ws.numel(),
+              None, st)
+    torch.cuda.synchronize()
+    outs = [(t[2].clone(), t[3].clone()) for t in keep]
+    for (dw0, db0), (rw, rb), (mo, ki) in zip(outs, refs, shapes):
+        tol = 2e-5 * max(1.0, n ** 0.5)
+        np.testing.assert_allclose(dw0[:, :ki].cpu().double().numpy(), rw.cpu().numpy(), rtol=1e-5, atol=tol)
+        np.testing.assert_allclose(db0.cpu().double().numpy(), rb.cpu().numpy(), rtol=1e-5, atol=tol)
+    # deferred: restore the accumulate targets, run again through a reduce list
+    for t in keep:
+        t[2].copy_(t[4])
+    lst = _lib.ReduceList()
+    _lib.call("ncf_wgrad_grouped", ctypes.addressof(descs), len(shapes), ws.data_ptr(), ws.numel(),
+              lst.address, st)
+    scr = torch.empty(max(1, _lib.query("ncf_reduce_batch_scratch", lst.address)), device=DEV)
+    _lib.call("ncf_reduce_batch", lst.address, scr.data_ptr(), scr.numel(), st)
+    torch.cuda.synchronize()
+    for (dw0, db0), t in zip(outs, keep):
+        assert torch.equal(dw0, t[2]) and torch.equal(db0, t[3])

@@ -25,6 +25,7 @@ SHAPES = [
     ("mlp2_dX", N_ROWS, 256, 128, 0, 0),
     ("mlp1_dX", N_ROWS, 64, 256, 0, 0),
     ("att_dX", N_ROWS, 64, 64, 0, 0),
+    ("infer mlp1 65536", 65536, 256, 64, 0, 1),
 ]
 WGRAD = [("mlp3_dW", 64, 128), ("mlp2_dW", 128, 256), ("mlp1_dW", 256, 64), ("att_dW", 64, 64)]
 
@@ -50,10 +51,25 @@ def main():
         C = torch.empty(M, N, device=DEV)
         lda, ldb = (M if at else K), (K if bt else N)
         flops = 2.0 * M * N * K
-        for fn_name in ("ncf_gemm_f32", "ncf_gemm_direct"):
-            us = timeit(lambda: _lib.call(fn_name, M, N, K, A.data_ptr(), lda, at, B.data_ptr(), ldb,
-                                          bt, C.data_ptr(), N, None, 0, st))
-            print(f"{name:20s} {fn_name:22s} {us:8.2f} us  {flops / us / 1e6:7.1f} TF/s", flush=True)
+        ref = None
+        for fn_name in ("ncf_gemm_f32", "ncf_gemm_direct", "ncf_gemm_rows"):
+            if fn_name == "ncf_gemm_rows":
+                if at:
+                    continue
+                fn = lambda: _lib.call(fn_name, M, N, K, A.data_ptr(), lda, B.data_ptr(), ldb, bt,  # noqa: E731
+                                       C.data_ptr(), N, None, 0, st)
+            else:
+                fn = lambda: _lib.call(fn_name, M, N, K, A.data_ptr(), lda, at, B.data_ptr(), ldb,  # noqa: E731
+                                       bt, C.data_ptr(), N, None, 0, st)
+            C.zero_()
+            fn()
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = C.clone()
+            err = (C - ref).abs().max().item()
+            us = timeit(fn)
+            print(f"{name:20s} {fn_name:22s} {us:8.2f} us  {flops / us / 1e6:7.1f} TF/s  maxdiff {err:.2e}",
+                  flush=True)
     for name, Mo, Ko in WGRAD:
         dY = torch.randn(N_ROWS, Mo, device=DEV)
         X = torch.randn(N_ROWS, Ko, device=DEV)
@@ -62,15 +78,12 @@ def main():
         flops = 2.0 * Mo * Ko * N_ROWS
         for splits in (16, 40, 80, 160, 320):
             ws = torch.empty(max(_lib.query("ncf_gemm_splitk_workspace", Mo, Ko, splits),
-                                 _lib.query("ncf_gemm_wgrad_workspace", Mo, Ko, splits)), device=DEV)
+                                 0), device=DEV)
             us1 = timeit(lambda: _lib.call("ncf_gemm_f32_splitk", Mo, Ko, N_ROWS, dY.data_ptr(), Mo, 1,
-                                           X.data_ptr(), Ko, 0, C.data_ptr(), Ko, 0, splits,
-                                           ws.data_ptr(), ws.numel(), st))
-            us2 = timeit(lambda: _lib.call("ncf_gemm_wgrad", Mo, Ko, N_ROWS, dY.data_ptr(), Mo, 1,
-                                           X.data_ptr(), Ko, 0, C.data_ptr(), Ko, 0, db.data_ptr(),
-                                           splits, ws.data_ptr(), ws.numel(), st))
-            print(f"{name:20s} splits={splits:4d} tiled {us1:8.2f} us ({flops / us1 / 1e6:6.1f} TF/s)"
-                  f"  direct+bias {us2:8.2f} us ({flops / us2 / 1e6:6.1f} TF/s)", flush=True)
+                                           X.data_ptr(), Ko, 0, C.data_ptr(), Ko, 0, None, splits,
+                                           ws.data_ptr(), ws.numel(), None, st))
+            print(f"{name:20s} splits={splits:4d} tiled {us1:8.2f} us ({flops / us1 / 1e6:6.1f} TF/s)",
+                  flush=True)
 
 
 if __name__ == "__main__":
