@@ -238,6 +238,28 @@ int ncf_scatter_compact_rows(float* dense_grad, int64_t dim, const int64_t* uniq
                              const uint32_t* num_unique, int kind, const float* grad_compact,
                              int64_t max_n, void* stream);
 
+/* ---- C5: batch candidate scoring (app.py:44-75 forward_simple over all products + nlargest) ---
+ * Factorised eval logit(u, i) = q_u . p_i + bias_i (score.hip header); results ordered by
+ * (logit desc, item id asc).  dim must be 64.  Pipeline: queries -> sample logits (ncf_gemm_f32
+ * with a strided B) -> ncf_score_kth thresholds -> ncf_score_collect candidates ->
+ * ncf_score_select top-K (overflow[slot] = 1: re-run 3-4 for those slots with the returned thr). */
+int ncf_score_queries(const int64_t* user_ids, int64_t n, const float* mf_user, int64_t rows,
+                      int64_t dim, const float* mf_gamma, const float* mf_beta, float eps,
+                      const float* mf_out_w, const float* final_w, float* queries, int* err_flag,
+                      void* stream);
+int ncf_score_item_bias(const float* mlp_item, int64_t n, const float* final_w,
+                        const float* final_b, const float* mf_out_b, float* bias, void* stream);
+int ncf_score_kth(const float* logits, int64_t n_users, int64_t S, int K, const float* item_bias,
+                  int64_t stride, float* thr, void* stream);
+int ncf_score_collect(const float* queries, const int32_t* user_list, int64_t n_users,
+                      const float* items, const float* item_bias, int64_t n_items, int64_t dim,
+                      const float* thr, int64_t cap, uint32_t* count, float* cand_logit,
+                      int32_t* cand_item, void* stream);
+int ncf_score_select(const int32_t* user_list, int64_t n_users, const uint32_t* count,
+                     const float* cand_logit, const int32_t* cand_item, int64_t cap, int K,
+                     float* out_score, int64_t* out_item, float* thr, uint32_t* overflow,
+                     void* stream);
+
 /* ---- a13: torch.optim.Adam step (trainer.py:71-75, :285) ----------------------------------
  * Dense-exact over a whole table via the slot map (every row decays every step).            */
 int ncf_adam_table(float* param, float* exp_avg, float* exp_avg_sq, int64_t rows, int64_t dim,

@@ -83,6 +83,11 @@ SIGNATURES = {
     "ncf_adam_rows_apply": (I32, [P, P, P, P, P, P, P, P, I64, P, P, I32, I64, P, I32, P, F64, F64,
                                   F64, F64, P]),
     "ncf_adam_sweep": (I32, [P, P, P, P, P, P, I64, I64, I64, P, I32, P, F64, F64, F64, F64, P]),
+    "ncf_score_queries": (I32, [P, I64, P, I64, I64, P, P, F32, P, P, P, P, P]),
+    "ncf_score_item_bias": (I32, [P, I64, P, P, P, P, P]),
+    "ncf_score_kth": (I32, [P, I64, I64, I32, P, I64, P, P]),
+    "ncf_score_collect": (I32, [P, P, I64, P, P, I64, I64, P, I64, P, P, P, P]),
+    "ncf_score_select": (I32, [P, I64, P, P, P, I64, I32, P, P, P, P, P]),
     "ncf_temporal_fwd": (I32, [P, P, P, P, I64, P, P, P, P, I64, I64, P, P, P]),
     "ncf_temporal_bwd": (I32, [P, P, P, I64, P, I64, P, P, P, P]),
 }

@@ -1,0 +1,348 @@
+// Batch candidate scoring: top-K items for many users over the whole catalogue (C5: 10K users x
+// 1M items), the accelerated form of the reference's serving loop
+// `model.forward_simple(customer, all_products)` + `nlargest(top_k, 'score')`
+// (src/inference/demo/app.py:44-75; forward_simple: src/model/architecture.py:409-485).
+//
+// Factorised form: in eval with one item per group, softmax over a single key is
+// 1, so the MLP path depends on the item only, and
+//   logit(u, i) = q_u . p_i + bias_i,  q_u = w0 * LN_mf(U_mf[u]) (.) w_mf,  p_i = LN_mf(I_mf[i]),
+//   bias_i = w1 * mlp_item(i) + w0 * b_mf + b_final,     score = sigmoid(logit)  (monotone).
+// Pipeline (all deterministic: the final order is (logit desc, item id asc)):
+//   1. ncf_score_queries      q_u rows (gather + LayerNorm + scale);
+//   2. ncf_score_kth          per user, the K-th largest logit over a strided item SAMPLE (the
+//                             sample logits come from ncf_gemm_f32 with a strided B) — a lower
+//                             bound of the true K-th largest (radix select on the order-
+//                             preserving uint32 image of the float);
+//   3. ncf_score_collect      the MFMA scan: every (user, item) logit, appending (logit, item) to
+//                             the user's candidate list when logit >= threshold.  The candidate
+//                             SET is a function of the threshold only, so any append order gives
+//                             the same result;
+//   4. ncf_score_select       per user, bitonic sort of its candidates in LDS, top-K out; when a
+//                             user's list overflowed, the K-th best candidate seen is a higher
+//                             valid threshold and the host re-runs 3-4 for those users.
+// MFMA tiling of 3: a 512-thread workgroup owns 256 users (8 waves x 32), keeps each wave's q
+// rows in registers (k-permuted: MFMA step s uses k = s + 32h), and streams 32-item tiles of p
+// through double-buffered LDS ([32][65] pitch: conflict-free); per tile a wave issues 32
+// v_mfma_f32_32x32x2_f32 and filters its 32x32 logits against 16 per-lane thresholds.
+#include "ncf_common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint32_t fkey(float f) {  // order-preserving float -> uint32
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// ---- 1. queries: q = w0 * LN(U_mf[id]) (.) w_mf; L = D/4 lanes per row
+template <int D>
+__global__ void k_queries(const int64_t* __restrict__ ids, int64_t n, const float* __restrict__ table,
+                          int64_t rows, const float* __restrict__ gamma,
+                          const float* __restrict__ beta, float eps,
+                          const float* __restrict__ w_mf, const float* __restrict__ final_w,
+                          float* __restrict__ q, int* __restrict__ err) {
+  constexpr int L = D / 4;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = t / L;
+  const int c = (int)(t % L) * 4;
+  if (r >= n) return;  // whole row groups retire together (L divides 64)
+  int64_t id = ids[r];
+  if (id < 0 || id >= rows) {
+    if (err && c == 0) atomicOr(err, 1);
+    id = 0;
+  }
+  const float4 x = ld4(table + id * D + c);
+  const float mean = group_sum<L>(x.x + x.y + x.z + x.w) * (1.0f / D);
+  const float4 xc = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
+  const float var = group_sum<L>(xc.x * xc.x + xc.y * xc.y + xc.z * xc.z + xc.w * xc.w) * (1.0f / D);
+  const float rstd = 1.0f / sqrtf(var + eps);
+  const float4 g = ld4(gamma + c), b = ld4(beta + c), w = ld4(w_mf + c);
+  const float w0 = final_w[0];
+  st4(q + r * D + c, make_float4(w0 * ((xc.x * rstd * g.x + b.x) * w.x),
+                                 w0 * ((xc.y * rstd * g.y + b.y) * w.y),
+                                 w0 * ((xc.z * rstd * g.z + b.z) * w.z),
+                                 w0 * ((xc.w * rstd * g.w + b.w) * w.w)));
+}
+
+// bias_i = w1 * mlp_item_i + (w0 * b_mf + b_final)
+__global__ void k_item_bias(const float* __restrict__ mlp_item, int64_t n,
+                            const float* __restrict__ final_w, const float* __restrict__ final_b,
+                            const float* __restrict__ mf_b, float* __restrict__ bias) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bias[i] = final_w[1] * mlp_item[i] + (final_w[0] * mf_b[0] + final_b[0]);
+}
+
+// ---- 2. K-th largest of each row of a [users, S] logit matrix (radix select, 4 x 8-bit digits)
+// logit(u, j) = logits[u*S + j] + bias[j * stride] (the sample is every stride-th item)
+__global__ __launch_bounds__(256) void k_kth(const float* __restrict__ logits, int64_t S, int K,
+                                             const float* __restrict__ bias, int64_t stride,
+                                             float* __restrict__ thr) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t s_prefix, s_need;
+  const float* row = logits + (int64_t)blockIdx.x * S;
+  uint32_t prefix = 0, need = (uint32_t)(K < S ? K : S);  // rank from the top, 1-based
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (32 - 8 * pass));
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (int64_t j = threadIdx.x; j < S; j += 256) {
+      const uint32_t k = fkey(row[j] + bias[j * stride]);
+      if ((k & hmask) == (prefix & hmask)) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // walk digits from the top until the rank is reached
+      uint32_t acc = 0;
+      int d = 255;
+      for (; d > 0; --d) {
+        if (acc + hist[d] >= need) break;
+        acc += hist[d];
+      }
+      s_prefix = prefix | ((uint32_t)d << shift);
+      s_need = need - acc;
+    }
+    __syncthreads();
+    prefix = s_prefix;
+    need = s_need;
+    __syncthreads();
+  }
+  // the sample logits come from a GEMM with another k order than the collect kernel: lower the
+  // bound by a margin far above the fp32 reordering error of a 64-term dot product (a lower
+  // threshold only admits more candidates, never loses one)
+  if (threadIdx.x == 0) {
+    const float v = fkey_inv(prefix);
+    thr[blockIdx.x] = v - 1e-4f * fmaxf(1.0f, fabsf(v));
+  }
+}
+
+// ---- 3. MFMA scan + threshold filter
+constexpr int kUsersPerBlock = 256;  // 8 waves x 32
+constexpr int kItemTile = 32;
+
+template <int D>
+__global__ __launch_bounds__(512) void k_collect(
+    const float* __restrict__ q, const int32_t* __restrict__ user_list, int64_t n_users,
+    const float* __restrict__ items, const float* __restrict__ bias, int64_t n_items,
+    int64_t items_per_block, const float* __restrict__ thr, int64_t cap,
+    uint32_t* __restrict__ count, float* __restrict__ cand_logit,
+    int32_t* __restrict__ cand_item) {
+  static_assert(D == 64, "scoring kernel is specialised for D = 64 (one 64-deep k chunk)");
+  __shared__ float ps[2][kItemTile][D + 1];
+  __shared__ float bs[2][kItemTile];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  // this wave's 32 users (slot = index into the user list)
+  const int64_t slot0 = (int64_t)blockIdx.y * kUsersPerBlock + w * 32;
+  const int64_t my_slot = slot0 + i;
+  const bool uvalid = my_slot < n_users;
+  const int64_t my_user = uvalid ? (user_list ? user_list[my_slot] : my_slot) : 0;
+  float a[32];
+  {
+    const float* qp = q + my_user * D + 32 * h;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const float4 x = ld4(qp + 4 * v);
+      a[4 * v] = x.x; a[4 * v + 1] = x.y; a[4 * v + 2] = x.z; a[4 * v + 3] = x.w;
+    }
+  }
+  // thresholds of the 16 users whose logits this lane holds: row (r&3) + 8(r>>2) + 4h
+  float th[16];
+  int64_t urow[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t s = slot0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    const bool v = s < n_users;
+    urow[r] = v ? (user_list ? user_list[s] : s) : -1;
+    th[r] = v ? thr[urow[r]] : INFINITY;
+  }
+  const int64_t it0 = (int64_t)blockIdx.x * items_per_block;
+  const int64_t it1 = min(n_items, it0 + items_per_block);
+  // staging: 512 threads x one float4 = one 32 x 64 tile
+  const int sj = tid >> 4, sk = (tid & 15) * 4;
+  auto fetch = [&](int64_t t0, float4& v, float& bv) {
+    const int64_t item = t0 + sj;
+    const int64_t src = item < it1 ? item : it0;  // clamped, unconditional
+    v = ld4(items + src * D + sk);
+    bv = bias[src];
+  };
+  float4 pv;
+  float pb;
+  if (it0 < it1) fetch(it0, pv, pb);
+  int buf = 0;
+  for (int64_t t0 = it0; t0 < it1; t0 += kItemTile) {
+    ps[buf][sj][sk] = pv.x; ps[buf][sj][sk + 1] = pv.y;
+    ps[buf][sj][sk + 2] = pv.z; ps[buf][sj][sk + 3] = pv.w;
+    if ((tid & 15) == 0) bs[buf][sj] = pb;
+    __syncthreads();
+    if (t0 + kItemTile < it1) fetch(t0 + kItemTile, pv, pb);  // next tile lands during the MFMAs
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    const float* pb_row = &ps[buf][i][32 * h];
+#pragma unroll
+    for (int s = 0; s < 32; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], pb_row[s], acc, 0, 0, 0);
+    const int64_t item = t0 + i;
+    const float b = bs[buf][i];
+    if (item < it1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float lg = acc[r] + b;
+        if (lg >= th[r]) {
+          const uint32_t pos = atomicAdd(&count[urow[r]], 1u);
+          if (pos < cap) {
+            cand_logit[urow[r] * cap + pos] = lg;
+            cand_item[urow[r] * cap + pos] = (int32_t)item;
+          }
+        }
+      }
+    }
+    buf ^= 1;
+  }
+}
+
+// ---- 4. per-user selection: bitonic sort (descending) of 64-bit keys (logit key | ~item)
+constexpr int kSelectMax = 8192;
+
+__global__ __launch_bounds__(1024) void k_select(const int32_t* __restrict__ user_list,
+                                                 int64_t n_users, const uint32_t* __restrict__ count,
+                                                 const float* __restrict__ cand_logit,
+                                                 const int32_t* __restrict__ cand_item,
+                                                 int64_t cap, int K, float* __restrict__ out_score,
+                                                 int64_t* __restrict__ out_item,
+                                                 float* __restrict__ thr_out,
+                                                 uint32_t* __restrict__ overflow) {
+  extern __shared__ unsigned long long keys[];
+  const int64_t slot = blockIdx.x;
+  if (slot >= n_users) return;
+  const int64_t u = user_list ? user_list[slot] : slot;
+  const uint32_t c_all = count[u];
+  const int nc = (int)(c_all < cap ? c_all : cap);
+  int n2 = 1;
+  while (n2 < nc || n2 < K) n2 <<= 1;
+  for (int j = threadIdx.x; j < n2; j += blockDim.x) {
+    unsigned long long k = 0ull;
+    if (j < nc) {
+      const uint32_t lk = fkey(cand_logit[u * cap + j]);
+      const uint32_t id = (uint32_t)cand_item[u * cap + j];
+      k = ((unsigned long long)lk << 32) | (unsigned long long)(0xFFFFFFFFu - id);
+    }
+    keys[j] = k;
+  }
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int j = threadIdx.x; j < n2; j += blockDim.x) {
+        const int p = j ^ stride;
+        if (p > j) {
+          const bool desc = (j & size) == 0;
+          const unsigned long long x = keys[j], y = keys[p];
+          if ((x < y) == desc) { keys[j] = y; keys[p] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int j = threadIdx.x; j < K; j += blockDim.x) {
+    const unsigned long long k = keys[j];
+    const bool ok = j < nc;
+    const float lg = fkey_inv((uint32_t)(k >> 32));
+    out_score[slot * K + j] = ok ? 1.0f / (1.0f + expf(-lg)) : 0.0f;
+    out_item[slot * K + j] = ok ? (int64_t)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : -1;
+  }
+  if (threadIdx.x == 0) {
+    const bool over = c_all > (uint32_t)cap;
+    overflow[slot] = over ? 1u : 0u;
+    // a valid higher threshold for a re-run: the K-th best of the candidates seen
+    if (over && thr_out) thr_out[u] = fkey_inv((uint32_t)(keys[K - 1] >> 32));
+  }
+}
+
+}  // namespace
+
+extern "C" int ncf_score_queries(const int64_t* user_ids, int64_t n, const float* mf_user,
+                                 int64_t rows, int64_t dim, const float* mf_gamma,
+                                 const float* mf_beta, float eps, const float* mf_out_w,
+                                 const float* final_w, float* queries, int* err_flag,
+                                 void* stream) {
+  NCF_CHECK_ARG(n >= 0 && dim == 64, "ncf_score_queries: dim must be 64");
+  if (n == 0) return NCF_OK;
+  hipLaunchKernelGGL(k_queries<64>, dim3(ncf_cdiv(n * 16, 256)), dim3(256), 0, (hipStream_t)stream,
+                     user_ids, n, mf_user, rows, mf_gamma, mf_beta, eps, mf_out_w, final_w, queries,
+                     err_flag);
+  NCF_CHECK_LAUNCH("ncf_score_queries");
+  return NCF_OK;
+}
+
+extern "C" int ncf_score_item_bias(const float* mlp_item, int64_t n, const float* final_w,
+                                   const float* final_b, const float* mf_out_b, float* bias,
+                                   void* stream) {
+  NCF_CHECK_ARG(n >= 0, "ncf_score_item_bias: n < 0");
+  if (n == 0) return NCF_OK;
+  hipLaunchKernelGGL(k_item_bias, dim3(ncf_cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     mlp_item, n, final_w, final_b, mf_out_b, bias);
+  NCF_CHECK_LAUNCH("ncf_score_item_bias");
+  return NCF_OK;
+}
+
+extern "C" int ncf_score_kth(const float* logits, int64_t n_users, int64_t S, int K,
+                             const float* item_bias, int64_t stride, float* thr, void* stream) {
+  NCF_CHECK_ARG(n_users >= 0 && S >= 1 && K >= 1 && stride >= 1, "ncf_score_kth: bad size");
+  if (n_users == 0) return NCF_OK;
+  hipLaunchKernelGGL(k_kth, dim3((unsigned)n_users), dim3(256), 0, (hipStream_t)stream, logits, S,
+                     K, item_bias, stride, thr);
+  NCF_CHECK_LAUNCH("ncf_score_kth");
+  return NCF_OK;
+}
+
+extern "C" int ncf_score_collect(const float* queries, const int32_t* user_list, int64_t n_users,
+                                 const float* items, const float* item_bias, int64_t n_items,
+                                 int64_t dim, const float* thr, int64_t cap, uint32_t* count,
+                                 float* cand_logit, int32_t* cand_item, void* stream) {
+  NCF_CHECK_ARG(dim == 64, "ncf_score_collect: dim must be 64");
+  NCF_CHECK_ARG(n_users >= 0 && n_items >= 0 && n_items < (1ll << 31) && cap >= 1,
+                "ncf_score_collect: bad size");
+  if (n_users == 0 || n_items == 0) return NCF_OK;
+  // item split: enough workgroups to fill the chip (>= ~2 per CU) with >= 8 tiles each
+  const int64_t ub = (n_users + kUsersPerBlock - 1) / kUsersPerBlock;
+  int64_t splits = (1024 + ub - 1) / ub;
+  const int64_t max_splits = (n_items + 8 * kItemTile - 1) / (8 * kItemTile);
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int64_t per = (n_items + splits - 1) / splits;
+  per = (per + kItemTile - 1) / kItemTile * kItemTile;
+  splits = (n_items + per - 1) / per;
+  NCF_CHECK_ARG(ub < 65536, "ncf_score_collect: too many users per call (max %d)", 65535 * 256);
+  hipLaunchKernelGGL(k_collect<64>, dim3((unsigned)splits, (unsigned)ub), dim3(512), 0,
+                     (hipStream_t)stream, queries, user_list, n_users, items, item_bias, n_items,
+                     per, thr, cap, count, cand_logit, cand_item);
+  NCF_CHECK_LAUNCH("ncf_score_collect");
+  return NCF_OK;
+}
+
+extern "C" int ncf_score_select(const int32_t* user_list, int64_t n_users, const uint32_t* count,
+                                const float* cand_logit, const int32_t* cand_item, int64_t cap,
+                                int K, float* out_score, int64_t* out_item, float* thr,
+                                uint32_t* overflow, void* stream) {
+  NCF_CHECK_ARG(n_users >= 0 && K >= 1 && cap >= K && cap <= kSelectMax,
+                "ncf_score_select: need 1 <= K <= cap <= %d", kSelectMax);
+  if (n_users == 0) return NCF_OK;
+  int n2 = 1;
+  while (n2 < cap) n2 <<= 1;
+  const size_t lds = sizeof(unsigned long long) * (size_t)n2;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(sizeof(unsigned long long) * kSelectMax));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_select, dim3((unsigned)n_users), dim3(1024), lds, (hipStream_t)stream,
+                     user_list, n_users, count, cand_logit, cand_item, cap, K, out_score, out_item,
+                     thr, overflow);
+  NCF_CHECK_LAUNCH("ncf_score_select");
+  return NCF_OK;
+}

@@ -649,3 +649,49 @@ def test_wgrad_grouped_vs_torch(shapes, n):
     torch.cuda.synchronize()
     for (dw0, db0), t in zip(outs, keep):
         assert torch.equal(dw0, t[2]) and torch.equal(db0, t[3])
+
+
+def test_f5_score_topk_matches_reference_top10(f5):
+    """C5 scorer on the demo checkpoint: the reference's forward_simple + top-10 (golden F5)."""
+    from ncf_amd.scoring import score_topk
+    sd = T(sub(f5, "sd/"))
+    nu = sd["mf_embedding_collection.embedding_bags.user_id.weight"].shape[0]
+    m = ncf.AdvancedNCF(nu, 366, 5, 24).to(DEV)
+    m.load_state_dict(sd, strict=True)
+    m.eval()
+    s, it = score_topk(m, torch.arange(nu), k=10)
+    got = it.cpu().numpy()
+    ref_top = np.take_along_axis(f5["scores"], f5["top_items"], axis=1)
+    # same ranking; positions may differ only between reference scores tied within 1e-6
+    # (torch.topk's tie order is unspecified, ours is item id ascending)
+    np.testing.assert_allclose(np.take_along_axis(f5["scores"], got, axis=1), ref_top, atol=1e-6)
+    assert (np.sort(got, 1) == np.sort(f5["top_items"], 1)).mean() > 0.95
+    np.testing.assert_allclose(s.cpu().numpy(), ref_top, atol=2e-6)
+
+
+@pytest.mark.parametrize("k,cap", [(1, 8192), (10, 8192), (100, 8192), (100, 128)])
+def test_score_topk_vs_oracle(k, cap):
+    """Factorised scorer vs the oracle's score_factorised + a (score desc, id asc) sort: users
+    not a multiple of the 256-user tile, items not a multiple of the 32-item tile; cap=128
+    forces the overflow re-run path."""
+    from oracle import ncf_oracle as O
+    from ncf_amd.scoring import score_topk
+    torch.manual_seed(3)
+    U, I = 300, 20011
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    users = torch.randint(0, U, (37,))
+    s, it = score_topk(m, users, k=k, cap=cap)
+    p = {kk: v.detach().cpu() for kk, v in m.state_dict().items()}
+    ref = O.score_factorised(p, users, torch.arange(I), temporal_dim=32, n_layers=3).double()
+    for r in range(len(users)):
+        order = sorted(range(I), key=lambda j: (-ref[r, j].item(), j))[:k] if k <= 10 else \
+            torch.argsort(-ref[r], stable=True)[:k].tolist()
+        got = it[r].cpu().tolist()
+        # identical ranking except where the oracle's own fp32 scores tie within 1e-6
+        mism = [a for a, b in zip(got, order) if a != b]
+        if mism:
+            gs = ref[r, got].numpy()
+            os_ = ref[r, order].numpy()
+            np.testing.assert_allclose(gs, os_, atol=1e-6)
+        np.testing.assert_allclose(s[r].cpu().numpy(), ref[r, got].numpy(), atol=1e-6)
