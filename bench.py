@@ -90,6 +90,65 @@ def cpu_baseline(model_sd, cfg, batches_cpu, budget_s):
                       f"CPU {platform.processor() or platform.machine()}"}
 
 
+def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget):
+    """C5 (BASELINE.json configs[4]): n_query users x n_items top-K with the factorised MFMA
+    scorer (ncf_amd.scoring), timed with inputs resident; plus the reference serving path
+    (forward_simple over items) on the CPU oracle for a bounded slice."""
+    import ncf_amd
+    from ncf_amd import _lib as L
+    from ncf_amd.scoring import ItemIndex, score_topk
+    torch.manual_seed(4321)
+    m = ncf_amd.AdvancedNCF(n_users, n_items, 10, 50).to(dev).eval()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    idx = ItemIndex(m)
+    torch.cuda.synchronize()
+    index_ms = (time.perf_counter() - t0) * 1e3
+    users = torch.randperm(n_users, device=dev)[:n_query]
+    out = {"config": f"{n_query} users x {n_items} items (model {n_users} x {n_items}, D=64), "
+                     "top-K over the whole catalogue, factorised fp32 MFMA scan",
+           "item_index_ms": round(index_ms, 3)}
+    for k in ks:
+        score_topk(m, users, k, idx)
+        torch.cuda.synchronize()
+        best, prof = 1e9, None
+        for _ in range(3):
+            L.PROFILE = []
+            t0 = time.perf_counter()
+            score_topk(m, users, k, idx)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if dt < best:
+                best, prof = dt, L.PROFILE
+            L.PROFILE = None
+        coll = sum(e0.elapsed_time(e1) for name, _, e0, e1 in prof if name == "ncf_score_collect")
+        flops = 2.0 * 64 * n_query * n_items
+        tf = flops / (coll * 1e-3) / 1e12
+        out[f"k{k}"] = {"ms": round(best * 1e3, 3), "pairs_per_s": round(n_query * n_items / best, 1),
+                        "collect_ms": round(coll, 3),
+                        "roofline": {"bound": "mfma", "kernel": "k_collect (v_mfma_f32_32x32x2_f32)",
+                                     "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFS,
+                                     "unit": "TFLOP/s", "frac": round(tf / FP32_MFMA_PEAK_TFS, 4),
+                                     "flops_per_pair": 128}}
+    if cpu_budget > 0:
+        from oracle import ncf_oracle as O
+        p = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+        n_cpu = min(n_items, 100_000)
+        items = torch.arange(n_cpu)
+        u = torch.full((n_cpu,), int(users[0]), dtype=torch.int64)
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            O.forward_simple(p, u, items, num_heads=4, temporal_dim=32, n_layers=3)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(n_cpu / dt, 1), "unit": "pairs/s",
+                               "cores": torch.get_num_threads(), "kind": "port",
+                               "sample": f"oracle forward_simple (the reference serving path, "
+                                         f"literal per-pair forward) for 1 user x {n_cpu} items"}
+    del m, idx
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -101,6 +160,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--infer-pairs", type=int, default=65536)
+    ap.add_argument("--no-score", action="store_true", help="skip the C5 scoring measurement")
+    ap.add_argument("--score-users", type=int, default=10_000)
+    ap.add_argument("--score-items", type=int, default=1_000_000)
     ap.add_argument("--sharded", action="store_true",
                     help="use the row-sharded DP step even at world size 1 (exercises the N>1 path)")
     args = ap.parse_args()
@@ -180,9 +242,14 @@ def main():
     for name, a, e0, e1 in prof:
         per.setdefault(name, []).append((a, e0.elapsed_time(e1)))
     totals = {k: sum(d for _, d in v) / args.steps for k, v in per.items()}   # ms per step
-    gemm_names = ("ncf_gemm_direct", "ncf_gemm_f32", "ncf_gemm_f32_splitk")
+    # fp32 MFMA kernels: forward + dX GEMMs (M, N, K are the first three arguments of every
+    # ncf_gemm_* entry point) and the grouped weight-gradient launch, whose FLOPs equal the
+    # forward GEMMs' (dW = dYᵀ·X costs 2·n·out·in per Linear, like the forward) = half of fwd + dX
+    gemm_names = ("ncf_gemm_direct", "ncf_gemm_f32", "ncf_gemm_rows", "ncf_gemm_f32_splitk",
+                  "ncf_wgrad_grouped")
     gemm_ms = sum(totals.get(k, 0.0) for k in gemm_names)
-    gemm_flops = sum(2.0 * a[0] * a[1] * a[2] for k in gemm_names for a, _ in per.get(k, [])) / args.steps
+    fwd_dx = sum(2.0 * a[0] * a[1] * a[2] for k in gemm_names[:4] for a, _ in per.get(k, [])) / args.steps
+    gemm_flops = fwd_dx * (1.5 if "ncf_wgrad_grouped" in per else 1.0)
     gemm_launches = sum(len(per.get(k, [])) for k in gemm_names) / args.steps
     achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
     # table-update work of the deferred dense-exact Adam: algorithmic = the dense schedule's
@@ -213,6 +280,10 @@ def main():
     if init_sd is not None:
         cpu_batches = [(u.cpu(), i.cpu(), t.cpu()) for (u, i, t) in batches[:4]]
         cpu = cpu_baseline(init_sd, (U, I, D, T, H, hid, B, M), cpu_batches, args.cpu_budget)
+    score = None
+    if world == 1 and not args.no_score:
+        score = c5_scoring(dev, 1_000_000, args.score_items, args.score_users, (10, 100),
+                           0 if args.no_cpu_baseline else 1)
 
     if rank == 0:
         rec = {
@@ -233,9 +304,9 @@ def main():
                        "global_batch": N * world, "groups_per_gpu": B, "samples_per_group": M,
                        "parallelism": (f"dp{world} + row-sharded tables (RCCL all-to-all), "
                                        "dense all-reduce") if sharded else "single-gpu"},
-            "roofline": {"bound": "mfma", "kernel": "k_gemm_f32 + k_gemm_direct (fp32 MFMA "
-                                                    "v_mfma_f32_32x32x2_f32; all attention/MLP "
-                                                    "GEMM launches of a step)",
+            "roofline": {"bound": "mfma", "kernel": "k_gemm_rows + k_gemm_f32 + k_wgrad_grouped "
+                                                    "(fp32 MFMA v_mfma_f32_32x32x2_f32; every "
+                                                    "attention/MLP GEMM launch of a step)",
                          "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
                          "flops_per_step": gemm_flops, "launches_per_step": gemm_launches,
@@ -249,6 +320,7 @@ def main():
             "cpu_baseline": cpu,
             "infer_pairs_per_s": round(infer_pairs, 1),
             "infer_config": f"eval forward (M=1), {npairs} resident (user,item) pairs per GPU",
+            "c5_scoring": score,
             "final_loss": round(loss, 6),
         }
         print(json.dumps(rec), flush=True)
