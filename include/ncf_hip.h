@@ -46,6 +46,21 @@ int ncf_gather_ln_gmf_fwd(const int64_t* user_ids, const int64_t* item_ids, int6
                           float* mlp_item_ln, float* mf_user_ln, float* mf_item_ln,
                           int* err_flag, void* stream);
 
+/* forward_simple(hour=h) variant (architecture.py:432-458): the LN'd item rows of both paths are
+ * multiplied by (1 + scale_factor * item_scale[row]) before the GMF dot product and before
+ * they are stored; item_scale [n, dim] = the call's projection of hour_E[h] (or hour_E[h] when
+ * T == D), scale_factor = 0.3 in the reference.                                               */
+int ncf_gather_ln_gmf_scaled_fwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
+                                 const float* mf_user, const float* mf_item,
+                                 const float* mlp_user, const float* mlp_item, int64_t num_users,
+                                 int64_t num_items, int64_t dim, const float* mf_gamma,
+                                 const float* mf_beta, const float* mlp_gamma,
+                                 const float* mlp_beta, const float* mf_out_w,
+                                 const float* mf_out_b, float eps, const float* item_scale,
+                                 float scale_factor, float* mf_pred, float* mlp_user_ln,
+                                 float* mlp_item_ln, float* mf_user_ln, float* mf_item_ln,
+                                 int* err_flag, void* stream);
+
 /* Row gather (+ optional LayerNorm): EBC forward as read by callers (app.py:156-184) and
  * get_user_embeddings / get_product_embeddings (architecture.py:383-407).                   */
 int ncf_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t rows,

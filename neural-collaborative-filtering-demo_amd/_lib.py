@@ -36,6 +36,8 @@ SIGNATURES = {
     "ncf_device_count": (I32, []),
     "ncf_gather_ln_gmf_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P, F32,
                                     P, P, P, P, P, P, P]),
+    "ncf_gather_ln_gmf_scaled_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P,
+                                           F32, P, F32, P, P, P, P, P, P, P]),
     "ncf_gather_rows": (I32, [P, I64, P, I64, I64, P, P, F32, P, P, P]),
     "ncf_gemm_f32": (I32, [I64, I64, I64, P, I64, I32, P, I64, I32, P, I64, P, I32, P]),
     "ncf_gemm_splitk_workspace": (I64, [I64, I64, I32]),

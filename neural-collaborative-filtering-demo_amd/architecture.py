@@ -218,9 +218,13 @@ class AdvancedNCF(nn.Module):
         return out
 
     def forward_simple(self, user_ids, product_ids, hour=None):
-        """(:409-485) With hour=None this is the eval forward with M=1 per pair."""
+        """(:409-485) With hour=None this is the eval forward with M=1 per pair; with hour the
+        reference's temporal variant, including its fresh random projection per call."""
         if hour is not None:
             from .ops import forward_simple_hour
+            if self.training and float(self.dropout) > 0:
+                raise NotImplementedError("forward_simple in training mode (dropout active) is "
+                                          "not part of the accelerated path; call model.eval()")
             return forward_simple_hour(self, user_ids, product_ids, hour)
         eng = self._engine
         drop_p = float(self.dropout) if self.training else 0.0

@@ -44,7 +44,8 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
     const float* __restrict__ b_mf, const float* __restrict__ g_mlp, const float* __restrict__ b_mlp,
     const float* __restrict__ w_mf, const float* __restrict__ bias_mf, float eps,
     float* __restrict__ mf_pred, float* __restrict__ u_mlp_ln, float* __restrict__ i_mlp_ln,
-    float* __restrict__ u_mf_ln, float* __restrict__ i_mf_ln, int* err) {
+    float* __restrict__ u_mf_ln, float* __restrict__ i_mf_ln, int* err,
+    const float* __restrict__ item_scale, float scale_factor) {
   constexpr int L = D / 4;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t row = t / L;
@@ -57,13 +58,21 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
   const float4 xu_ml = ld4(mlpU + u * D + c), xi_ml = ld4(mlpI + i * D + c);
   const float4 gm = ld4(g_mf + c), bm = ld4(b_mf + c), gl = ld4(g_mlp + c), bl = ld4(b_mlp + c);
   const float4 yu = RowLN<D>::ln(xu_mf, gm, bm, eps);
-  const float4 yi = RowLN<D>::ln(xi_mf, gm, bm, eps);
+  float4 yi = RowLN<D>::ln(xi_mf, gm, bm, eps);
+  float4 zi = RowLN<D>::ln(xi_ml, gl, bl, eps);
+  if (item_scale) {  // forward_simple(hour): item rows *= (1 + f * proj(hour_E)) (architecture.py:444, :458)
+    const float4 s4 = ld4(item_scale + row * D + c);
+    const float4 m = make_float4(1.0f + scale_factor * s4.x, 1.0f + scale_factor * s4.y,
+                                 1.0f + scale_factor * s4.z, 1.0f + scale_factor * s4.w);
+    yi = make_float4(yi.x * m.x, yi.y * m.y, yi.z * m.z, yi.w * m.w);
+    zi = make_float4(zi.x * m.x, zi.y * m.y, zi.z * m.z, zi.w * m.w);
+  }
   const float4 w = ld4(w_mf + c);
   float dot = yu.x * yi.x * w.x + yu.y * yi.y * w.y + yu.z * yi.z * w.z + yu.w * yi.w * w.w;
   dot = group_sum<L>(dot);
   if (sub == 0) mf_pred[row] = dot + bias_mf[0];
   st4(u_mlp_ln + row * D + c, RowLN<D>::ln(xu_ml, gl, bl, eps));
-  st4(i_mlp_ln + row * D + c, RowLN<D>::ln(xi_ml, gl, bl, eps));
+  st4(i_mlp_ln + row * D + c, zi);
   if (u_mf_ln) st4(u_mf_ln + row * D + c, yu);
   if (i_mf_ln) st4(i_mf_ln + row * D + c, yi);
 }
@@ -94,11 +103,12 @@ int launch_gather_ln_gmf(const int64_t* uid, const int64_t* iid, int64_t n, cons
                          int64_t nI, const float* g_mf, const float* b_mf, const float* g_mlp,
                          const float* b_mlp, const float* w_mf, const float* bias_mf, float eps,
                          float* mf_pred, float* u_mlp_ln, float* i_mlp_ln, float* u_mf_ln,
-                         float* i_mf_ln, int* err, hipStream_t st) {
+                         float* i_mf_ln, int* err, const float* item_scale, float scale_factor,
+                         hipStream_t st) {
   const int64_t threads = n * (D / 4);
   hipLaunchKernelGGL(k_gather_ln_gmf<D>, dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st, uid, iid,
                      n, mfU, mfI, mlpU, mlpI, nU, nI, g_mf, b_mf, g_mlp, b_mlp, w_mf, bias_mf, eps,
-                     mf_pred, u_mlp_ln, i_mlp_ln, u_mf_ln, i_mf_ln, err);
+                     mf_pred, u_mlp_ln, i_mlp_ln, u_mf_ln, i_mf_ln, err, item_scale, scale_factor);
   NCF_CHECK_LAUNCH("ncf_gather_ln_gmf_fwd");
   return NCF_OK;
 }
@@ -127,6 +137,25 @@ int launch_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_
       return NCF_ERR_ARG;                                                     \
   }
 
+extern "C" int ncf_gather_ln_gmf_scaled_fwd(
+    const int64_t* user_ids, const int64_t* item_ids, int64_t n, const float* mf_user,
+    const float* mf_item, const float* mlp_user, const float* mlp_item, int64_t num_users,
+    int64_t num_items, int64_t dim, const float* mf_gamma, const float* mf_beta,
+    const float* mlp_gamma, const float* mlp_beta, const float* mf_out_w, const float* mf_out_b,
+    float eps, const float* item_scale, float scale_factor, float* mf_pred, float* mlp_user_ln,
+    float* mlp_item_ln, float* mf_user_ln, float* mf_item_ln, int* err_flag, void* stream) {
+  NCF_CHECK_ARG(n >= 0, "ncf_gather_ln_gmf_fwd: n < 0");
+  if (n == 0) return NCF_OK;
+  NCF_CHECK_ARG(user_ids && item_ids && mf_user && mf_item && mlp_user && mlp_item && mf_pred &&
+                    mlp_user_ln && mlp_item_ln && mf_gamma && mf_beta && mlp_gamma && mlp_beta &&
+                    mf_out_w && mf_out_b,
+                "ncf_gather_ln_gmf_fwd: null pointer");
+  NCF_DISPATCH_D(dim, launch_gather_ln_gmf, user_ids, item_ids, n, mf_user, mf_item, mlp_user,
+                 mlp_item, num_users, num_items, mf_gamma, mf_beta, mlp_gamma, mlp_beta, mf_out_w,
+                 mf_out_b, eps, mf_pred, mlp_user_ln, mlp_item_ln, mf_user_ln, mf_item_ln,
+                 err_flag, item_scale, scale_factor, (hipStream_t)stream);
+}
+
 extern "C" int ncf_gather_ln_gmf_fwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
                                      const float* mf_user, const float* mf_item,
                                      const float* mlp_user, const float* mlp_item,
@@ -137,16 +166,11 @@ extern "C" int ncf_gather_ln_gmf_fwd(const int64_t* user_ids, const int64_t* ite
                                      float* mf_pred, float* mlp_user_ln, float* mlp_item_ln,
                                      float* mf_user_ln, float* mf_item_ln, int* err_flag,
                                      void* stream) {
-  NCF_CHECK_ARG(n >= 0, "ncf_gather_ln_gmf_fwd: n < 0");
-  if (n == 0) return NCF_OK;
-  NCF_CHECK_ARG(user_ids && item_ids && mf_user && mf_item && mlp_user && mlp_item && mf_pred &&
-                    mlp_user_ln && mlp_item_ln && mf_gamma && mf_beta && mlp_gamma && mlp_beta &&
-                    mf_out_w && mf_out_b,
-                "ncf_gather_ln_gmf_fwd: null pointer");
-  NCF_DISPATCH_D(dim, launch_gather_ln_gmf, user_ids, item_ids, n, mf_user, mf_item, mlp_user,
-                 mlp_item, num_users, num_items, mf_gamma, mf_beta, mlp_gamma, mlp_beta, mf_out_w,
-                 mf_out_b, eps, mf_pred, mlp_user_ln, mlp_item_ln, mf_user_ln, mf_item_ln,
-                 err_flag, (hipStream_t)stream);
+  return ncf_gather_ln_gmf_scaled_fwd(user_ids, item_ids, n, mf_user, mf_item, mlp_user, mlp_item,
+                                      num_users, num_items, dim, mf_gamma, mf_beta, mlp_gamma,
+                                      mlp_beta, mf_out_w, mf_out_b, eps, nullptr, 0.0f, mf_pred,
+                                      mlp_user_ln, mlp_item_ln, mf_user_ln, mf_item_ln, err_flag,
+                                      stream);
 }
 
 extern "C" int ncf_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t rows,

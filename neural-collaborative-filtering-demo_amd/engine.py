@@ -260,11 +260,14 @@ class NCFEngine:
             self.deferred.sync()
 
     def forward(self, uid: torch.Tensor, iid: torch.Tensor, M: int, train: bool,
-                drop_p: float, seed: int, prepare=None, tables=None, rows=None) -> Workspace:
+                drop_p: float, seed: int, prepare=None, tables=None, rows=None,
+                temporal=None) -> Workspace:
         """AdvancedNCF.forward (architecture.py:258-381) on single-id bags; returns the workspace
         holding prob (and, when ``train``, everything the backward needs).  ``prepare(w, uid,
         iid, stream)`` runs before the gathers (the deferred Adam dedups the ids there and
-        brings exactly those rows current)."""
+        brings exactly those rows current).  ``temporal = (item_scale [n,D], factor, te [n,T])``
+        is forward_simple's hour path (eval, M = 1): item rows scaled in the gather and the MLP
+        fed [attention ‖ te] instead of [attention ‖ 0]."""
         dev = self._check_device()
         self.ensure_layout()
         m = self.model
@@ -289,13 +292,16 @@ class NCFEngine:
             prepare(w, uid, iid, st)
         else:
             self.sync_tables()
+        if temporal is not None and (train or M != 1):
+            raise ValueError("the temporal (hour) path is forward_simple's: eval, one item per group")
         # a2-a4: 4 gathers + mf_norm/mlp_norm + GMF  (architecture.py:286-287, 305-312)
-        _lib.call("ncf_gather_ln_gmf_fwd", ptr(uid), ptr(iid), n, ptr(tb["mf_user"]),
+        t_scale, t_factor = (temporal[0], temporal[1]) if temporal is not None else (None, 0.0)
+        _lib.call("ncf_gather_ln_gmf_scaled_fwd", ptr(uid), ptr(iid), n, ptr(tb["mf_user"]),
                   ptr(tb["mf_item"]), ptr(tb["mlp_user"]), ptr(tb["mlp_item"]), n_users,
                   n_items, D, ptr(m.mf_norm.weight), ptr(m.mf_norm.bias),
                   ptr(m.mlp_norm.weight), ptr(m.mlp_norm.bias), ptr(m.mf_output.weight),
-                  ptr(m.mf_output.bias), LN_EPS, ptr(w.mf_pred), ptr(w.xu), ptr(w.xi),
-                  ptr(w.umf), ptr(w.imf), ptr(w.err), st)
+                  ptr(m.mf_output.bias), LN_EPS, ptr(t_scale), float(t_factor), ptr(w.mf_pred),
+                  ptr(w.xu), ptr(w.xi), ptr(w.umf), ptr(w.imf), ptr(w.err), st)
         # a5: MultiHeadAttention over each group of M rows (architecture.py:315-326)
         att = m.user_product_attention
         self._gemm(w.xi, D, 0, att.v_proj.weight, D, 1, w.v, D, n, D, D, bias=att.v_proj.bias, st=st)
@@ -308,10 +314,21 @@ class NCFEngine:
             _lib.call("ncf_attention_fwd", ptr(w.q), ptr(w.k), ptr(w.v), n // M, M, H, D,
                       drop_p if train else 0.0, seed, ptr(w.P), ptr(w.o), st)
             src = w.o
-        self._gemm(src, D, 0, att.out_proj.weight, D, 1, w.y, D, n, D, D, bias=att.out_proj.bias, st=st)
-        # a7: MLP tower on [attn ‖ zeros_T] (architecture.py:329-344): the zero temporal columns
-        # contribute nothing, so layer 0 reads only the first D columns of mlp.0.weight
-        x, ldx, kin = w.y, D, D
+        if temporal is None:
+            self._gemm(src, D, 0, att.out_proj.weight, D, 1, w.y, D, n, D, D,
+                       bias=att.out_proj.bias, st=st)
+            # a7: MLP tower on [attn ‖ zeros_T] (architecture.py:329-344): the zero temporal
+            # columns contribute nothing, so layer 0 reads only the first D columns of mlp.0.weight
+            x, ldx, kin = w.y, D, D
+        else:
+            # forward_simple(hour): MLP input [attn ‖ hour_E[h]] (architecture.py:467-468)
+            te = temporal[2]
+            Tt = te.shape[1]
+            yt = torch.empty(n, D + Tt, device=dev)
+            self._gemm(src, D, 0, att.out_proj.weight, D, 1, yt, D + Tt, n, D, D,
+                       bias=att.out_proj.bias, st=st)
+            yt[:, D:].copy_(te)
+            x, ldx, kin = yt, D + Tt, D + Tt
         for l, h in enumerate(hid):
             lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
             ldw = lin.weight.shape[1]

@@ -167,8 +167,32 @@ def category_hierarchy_forward(mod, department_ids, category_ids):
     return out.view(n, n, D)
 
 
-def forward_simple_hour(model, user_ids, product_ids, hour):
-    raise NotImplementedError(
-        "forward_simple(hour=...) builds a fresh randomly-initialised nn.Linear on every call in "
-        "the reference (architecture.py:436-442), so it has no reproducible result; only "
-        "hour=None is on the accelerated scoring path")
+def forward_simple_hour(model, user_ids, product_ids, hour, projection=None):
+    """AdvancedNCF.forward_simple(user_ids, product_ids, hour) (architecture.py:409-485).
+
+    te = hour_E[hour] (TemporalEncoding.hour_embed, :434); when temporal_dim != D the reference
+    projects it with a FRESH randomly initialised nn.Linear(T, D) on every call (:436-442) — done
+    the same way here (torch's default init on the model's device) unless ``projection`` (an
+    nn.Linear or (weight, bias)) is given; both item rows are scaled by (1 + 0.3 * proj) (:444,
+    :456-458, fused into the gather kernel) and the MLP input is [attention ‖ te] (:467-468)."""
+    eng = model._engine
+    dev = eng._check_device()
+    m = model
+    D, T = m.mlp_embedding_dim, m.temporal_dim
+    hour = hour.to(device=dev, dtype=torch.int64).contiguous()
+    te = gather_rows(m.temporal_encoding.hour_embed.weight, hour)
+    n = te.shape[0]
+    if T != m.mf_embedding_dim:
+        if projection is None:
+            projection = torch.nn.Linear(T, m.mf_embedding_dim, device=dev)
+        w_p, b_p = projection if isinstance(projection, tuple) else (projection.weight, projection.bias)
+        w_p = w_p.detach().to(device=dev, dtype=torch.float32).contiguous()
+        b_p = b_p.detach().to(device=dev, dtype=torch.float32).contiguous()
+        tp = torch.empty(n, m.mf_embedding_dim, device=dev)
+        _lib.call("ncf_gemm_f32", n, m.mf_embedding_dim, T, ptr(te), T, 0, ptr(w_p), T, 1, ptr(tp),
+                  m.mf_embedding_dim, ptr(b_p), 0, _lib.stream_ptr(dev))
+    else:
+        tp = te
+    w = eng.forward(user_ids, product_ids, 1, False, 0.0, 0, temporal=(tp, 0.3, te))
+    eng.check_ids(w)
+    return w.prob.clone()

@@ -7,7 +7,7 @@ as the thing measured or shipped.  The product path (the ``ncf_amd`` package) ne
 and fails loudly when its HIP library is missing.
 
 Parity pin: ``tests/test_oracle_golden.py`` checks every function here against the golden
-fixtures F1-F5 that ``tests/golden/make_goldens.py`` produced by running the reference itself
+fixtures F1-F6 that ``tests/golden/make_goldens.py`` produced by running the reference itself
 (including the reference's own committed known answer ``src/inference/demo/data/predictions.csv``).
 
 Citations are into the reference (ethanshenley/Neural-Collaborative-Filtering-Demo).
@@ -115,6 +115,29 @@ def forward_simple(p, user_ids, product_ids, *, num_heads, temporal_dim, n_layer
     """AdvancedNCF.forward_simple(hour=None) (architecture.py:409-485) == eval forward."""
     return forward(p, user_ids, product_ids, training=False, negative_samples=0,
                    num_heads=num_heads, temporal_dim=temporal_dim, n_layers=n_layers).squeeze(-1)
+
+
+def forward_simple_hour(p, user_ids, product_ids, hour, proj_w, proj_b, *, num_heads,
+                        n_layers) -> Tensor:
+    """AdvancedNCF.forward_simple(hour=h) (architecture.py:409-485).  The reference builds a
+    fresh nn.Linear(T, D) inside the call when T != D (:437-442); its weights are inputs here.
+    Item rows of both paths are scaled by (1 + 0.3 * proj(hour_E[h])) (:444, :456-458); the MLP
+    input is [attention ‖ hour_E[h]] (:467-468)."""
+    te = p["temporal_encoding.hour_embed.weight"][hour]
+    D = p[K_MF_U].shape[1]
+    tp = linear(te, proj_w, proj_b) if te.shape[1] != D else te
+    g, b = p["mf_norm.weight"], p["mf_norm.bias"]
+    u_mf = layer_norm(p[K_MF_U][user_ids], g, b)
+    i_mf = layer_norm(p[K_MF_I][product_ids], g, b) * (1 + 0.3 * tp)
+    mf_pred = linear(u_mf * i_mf, p["mf_output.weight"], p["mf_output.bias"])
+    g, b = p["mlp_norm.weight"], p["mlp_norm.bias"]
+    u_mlp = layer_norm(p[K_MLP_U][user_ids], g, b)
+    i_mlp = layer_norm(p[K_MLP_I][product_ids], g, b) * (1 + 0.3 * tp)
+    att = mha(p, ATT, u_mlp[:, None], i_mlp[:, None], i_mlp[:, None], num_heads)[:, 0]
+    h = mlp_tower(p, torch.cat([att, te], 1), n_layers)
+    mlp_pred = linear(h, p["mlp_output.weight"], p["mlp_output.bias"])
+    z = linear(torch.cat([mf_pred, mlp_pred], 1), p["final.0.weight"], p["final.0.bias"])
+    return torch.sigmoid(z).squeeze(-1)
 
 
 def score_factorised(p, user_ids, item_ids, *, temporal_dim, n_layers):

@@ -48,3 +48,8 @@ def f4():
 @pytest.fixture(scope="session")
 def f5():
     return load_npz("f5_scoring.npz")
+
+
+@pytest.fixture(scope="session")
+def f6():
+    return load_npz("f6_hour.npz")

@@ -28,6 +28,10 @@ Fixtures written to tests/golden/*.npz (inputs and expected outputs only):
   F4 f4_ops.npz            MultiHeadAttention (L=5 and L=50) and TemporalEncoding fwd+bwd
   F5 f5_scoring.npz        forward_simple(hour=None) 8 users x 366 items + top-10,
                            get_user_embeddings / get_product_embeddings on the demo model
+  F6 f6_hour.npz           forward_simple(hour=h) on the demo model (users of F5) x 366 items.
+                           The reference draws a fresh nn.Linear(T, D) inside every call
+                           (architecture.py:437-442); seeding torch right before the call fixes
+                           its init, and the same seed reproduces its weights, stored here.
 """
 import argparse
 import csv
@@ -261,13 +265,41 @@ def make_f5(AdvancedNCF, KJT, sd):
     print("F5 written; top-1 items", top_i[:, 0].tolist())
 
 
+def make_f6(AdvancedNCF, sd):
+    model = AdvancedNCF(8031, 366, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.2, 4)
+    model.load_state_dict(sd, strict=True)
+    model.eval()
+    f5_users = [5021, 0, 17, 4096, 8030, 1234, 777, 3141]
+    calls = [(0, 0), (1, 13), (2, 23), (4, 7)]       # (index into F5's users, hour)
+    items = torch.arange(366)
+    scores, ws, bs = [], [], []
+    with torch.no_grad():
+        for c, (ui, hour) in enumerate(calls):
+            torch.manual_seed(1000 + c)
+            scores.append(model.forward_simple(torch.full((366,), f5_users[ui]), items,
+                                               torch.full((366,), hour)))
+            torch.manual_seed(1000 + c)
+            lin = nn.Linear(32, 64)                   # the projection the call above drew
+            ws.append(lin.weight.detach().clone())
+            bs.append(lin.bias.detach().clone())
+    np.savez_compressed(os.path.join(HERE, "f6_hour.npz"),
+                        user_pos=np.array([c[0] for c in calls]), hours=np.array([c[1] for c in calls]),
+                        scores=torch.stack(scores).numpy(), proj_w=torch.stack(ws).numpy(),
+                        proj_b=torch.stack(bs).numpy())
+    print("F6 written; scores[0][:4]", scores[0][:4].tolist())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--only", default=None, help="write one fixture only (e.g. f6)")
     a = ap.parse_args()
     torch.set_num_threads(8)
     AdvancedNCF, MHA, TE, KJT = import_reference(a.reference)
     sd = load_demo_state(a.reference)
+    if a.only == "f6":
+        make_f6(AdvancedNCF, sd)
+        return
     make_f1(a.reference, AdvancedNCF, KJT, sd)
     make_train("f2_train_c2.npz", AdvancedNCF, KJT, U=300, I=120, D=64, T=32,
                hidden=[256, 128, 64], H=4, B=8, M=5, steps=3, seed=0, lr=1e-3, wd=1e-5)
@@ -275,6 +307,7 @@ def main():
                hidden=[64, 32], H=1, B=16, M=5, steps=3, seed=1, lr=1e-3, wd=1e-5)
     make_f4(MHA, TE)
     make_f5(AdvancedNCF, KJT, sd)
+    make_f6(AdvancedNCF, sd)
 
 
 if __name__ == "__main__":

@@ -695,3 +695,33 @@ def test_score_topk_vs_oracle(k, cap):
             os_ = ref[r, order].numpy()
             np.testing.assert_allclose(gs, os_, atol=1e-6)
         np.testing.assert_allclose(s[r].cpu().numpy(), ref[r, got].numpy(), atol=1e-6)
+
+
+def test_f6_forward_simple_hour(f5, f6):
+    """forward_simple(hour=h) vs the reference (F6: its per-call projection reproduced by seed),
+    and the drop-in call that draws its own projection like the reference does."""
+    from ncf_amd.ops import forward_simple_hour
+    from oracle import ncf_oracle as O
+    sd = T(sub(f5, "sd/"))
+    nu = sd["mf_embedding_collection.embedding_bags.user_id.weight"].shape[0]
+    m = ncf.AdvancedNCF(nu, 366, 5, 24).to(DEV)
+    m.load_state_dict(sd, strict=True)
+    m.eval()
+    items = torch.arange(366, device=DEV)
+    with torch.no_grad():
+        for c in range(len(f6["hours"])):
+            u = torch.full_like(items, int(f6["user_pos"][c]))
+            h = torch.full_like(items, int(f6["hours"][c]))
+            s = forward_simple_hour(m, u, items, h, projection=(
+                torch.from_numpy(f6["proj_w"][c]), torch.from_numpy(f6["proj_b"][c])))
+            np.testing.assert_allclose(s.cpu().numpy(), f6["scores"][c], atol=2e-6)
+        # the module call draws nn.Linear(T, D) on the model's device from torch's RNG
+        torch.manual_seed(77)
+        got = m.forward_simple(torch.zeros_like(items), items, torch.full_like(items, 5))
+        torch.manual_seed(77)
+        lin = torch.nn.Linear(32, 64, device=DEV)
+    p = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ref = O.forward_simple_hour(p, torch.zeros(366, dtype=torch.int64), torch.arange(366),
+                                torch.full((366,), 5), lin.weight.detach().cpu(),
+                                lin.bias.detach().cpu(), num_heads=4, n_layers=3)
+    np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), atol=2e-6)

@@ -114,3 +114,16 @@ def test_f5_scoring(f5):
     np.testing.assert_allclose(lit.numpy(), f5["scores"], atol=1e-6)
     ts, ti = lit.topk(10, dim=1)
     assert (ti.numpy() == f5["top_items"]).all()
+
+
+def test_f6_forward_simple_hour(f5, f6):
+    """forward_simple(hour=h): the reference's per-call random projection, reproduced by seed and
+    stored in F6, pins the restatement of the hour path (architecture.py:432-468)."""
+    p = T(sub(f5, "sd/"))
+    items = torch.arange(p[O.K_MF_I].shape[0])
+    for c in range(len(f6["hours"])):
+        u = torch.full_like(items, int(f6["user_pos"][c]))
+        h = torch.full_like(items, int(f6["hours"][c]))
+        s = O.forward_simple_hour(p, u, items, h, torch.from_numpy(f6["proj_w"][c]),
+                                  torch.from_numpy(f6["proj_b"][c]), num_heads=4, n_layers=3)
+        np.testing.assert_allclose(s.numpy(), f6["scores"][c], atol=1e-6)
