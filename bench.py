@@ -161,6 +161,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--infer-pairs", type=int, default=65536)
     ap.add_argument("--no-score", action="store_true", help="skip the C5 scoring measurement")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as a captured hipGraph (measured ~3%% slower than host "
+                         "launches on MI355X: the host enqueue is already below the GPU time)")
     ap.add_argument("--score-users", type=int, default=10_000)
     ap.add_argument("--score-items", type=int, default=1_000_000)
     ap.add_argument("--sharded", action="store_true",
@@ -196,7 +199,7 @@ def main():
         if rank == 0 and not args.no_cpu_baseline:
             init_sd = {k: v.clone() for k, v in model.state_dict().items()}
         model = model.to(dev).train()
-        step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5)
+        step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, graph=args.graph)
     batches = make_batches(U, I, B, M, 8, dev, seed=100 + rank)
     torch.cuda.synchronize()
 
@@ -231,9 +234,10 @@ def main():
     from ncf_amd import _lib as L
     L.PROFILE = []
     torch.cuda.synchronize()
+    run = step.eager if hasattr(step, "eager") else step   # the launches a graph replay runs
     for s in range(args.steps):
         u, i, t = batches[s % len(batches)]
-        step(u, i, t)
+        run(u, i, t)
     torch.cuda.synchronize()
     prof, L.PROFILE = L.PROFILE, None
 
@@ -255,7 +259,10 @@ def main():
     # table-update work of the deferred dense-exact Adam: algorithmic = the dense schedule's
     # 24 B per table element per step (what the reference's Adam must move), priced per step
     tab_ms = sum(totals.get(k, 0.0) for k in ("ncf_adam_rows_catchup", "ncf_adam_rows_apply",
-                                                "ncf_adam_sweep", "ncf_adam_table"))
+                                                "ncf_adam_sweep", "ncf_adam_table",
+                                                "ncf_adam_rows_catchup_clock",
+                                                "ncf_adam_rows_apply_clock",
+                                                "ncf_adam_sweep_rolling"))
     tab_bytes = 2 * (U + I) * D * 24.0
     # --- inference pairs/s: eval forward (M = 1) on resident pairs
     model.eval()
@@ -302,6 +309,9 @@ def main():
             "config": {"workload": "C2 train step: 1M users x 100K items, D=64, H=4, MLP [256,128,64], "
                                    "T=32, dropout 0.2, Adam lr 1e-3 wd 1e-5 (dense-exact)",
                        "global_batch": N * world, "groups_per_gpu": B, "samples_per_group": M,
+                       "launch": ("host launches (row-sharded step)" if sharded else
+                                  "hipGraph replay of the captured step" if args.graph else
+                                  "host launches"),
                        "parallelism": (f"dp{world} + row-sharded tables (RCCL all-to-all), "
                                        "dense all-reduce") if sharded else "single-gpu"},
             "roofline": {"bound": "mfma", "kernel": "k_gemm_rows + k_gemm_f32 + k_wgrad_grouped "
@@ -313,7 +323,7 @@ def main():
                          "ms_per_step": round(gemm_ms, 4)},
             "table_adam": {"kernels": "deferred dense-exact Adam (catch-up + apply + 1/64 sweep)",
                            "ms_per_step": round(tab_ms, 4),
-                           "dense_equivalent_GBps": round(tab_bytes / (tab_ms * 1e-3) / 1e9, 1),
+                           "dense_equivalent_GBps": round(tab_bytes / max(tab_ms * 1e-3, 1e-12) / 1e9, 1),
                            "note": "dense schedule bytes (24 B x 140.8M elements) / time: above "
                                    "HBM peak because untouched rows are caught up lazily"},
             "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(totals.items(), key=lambda x: -x[1])},

@@ -29,6 +29,17 @@ extern "C" {
 #define NCF_ERR_LAUNCH (-2)
 #define NCF_ERR_WORKSPACE (-3)
 
+/* Step clock: the per-step values of a training step kept on the device, so a whole step can be
+ * captured once as a hipGraph and replayed (nothing step-dependent in any kernel argument).
+ * t = steps completed; seed = this step's dropout stream.  Kernels that take a clock read it;
+ * ncf_step_clock_advance() closes a step (t += 1, next seed = splitmix64(base_seed + t)).   */
+typedef struct ncf_step_clock {
+  int32_t t;
+  int32_t reserved;
+  uint64_t seed;
+} ncf_step_clock;
+int ncf_step_clock_advance(ncf_step_clock* clock, uint64_t base_seed, void* stream);
+
 int ncf_version(void);
 const char* ncf_last_error(void);
 int ncf_device_count(void);
@@ -154,13 +165,16 @@ int ncf_fill_2d(float* p, int64_t rows, int64_t cols, int64_t ld, float value, v
  * Replaces MultiHeadAttention.forward's bmm/softmax/dropout/bmm (architecture.py:45-55) as
  * called at :319-323.  q,k,v,out: [groups*group_len, dim]; probs: [groups, heads, L, L]
  * (pre-dropout softmax, saved for backward).  group_len <= 64, head dim in {8,16,32,64}.   */
+/* Dropout masks depend on seed + (clock ? clock->seed : 0).                                */
 int ncf_attention_fwd(const float* q, const float* k, const float* v, int64_t groups,
                       int64_t group_len, int64_t heads, int64_t dim, float dropout_p,
-                      uint64_t seed, float* probs, float* out, void* stream);
+                      uint64_t seed, const ncf_step_clock* clock, float* probs, float* out,
+                      void* stream);
 int ncf_attention_bwd(const float* q, const float* k, const float* v, const float* probs,
                       const float* grad_out, int64_t groups, int64_t group_len, int64_t heads,
-                      int64_t dim, float dropout_p, uint64_t seed, float* grad_scores,
-                      float* grad_q, float* grad_k, float* grad_v, void* stream);
+                      int64_t dim, float dropout_p, uint64_t seed, const ncf_step_clock* clock,
+                      float* grad_scores, float* grad_q, float* grad_k, float* grad_v,
+                      void* stream);
 
 /* ---- a6: TemporalEncoding (architecture.py:59-94): hour/day/month rows + pe[days mod P] -- */
 int ncf_temporal_fwd(const int64_t* hour, const int64_t* day, const int64_t* month,
@@ -176,11 +190,13 @@ int ncf_temporal_bwd(const int64_t* hour, const int64_t* day, const int64_t* mon
  * that feeds the ReLU; nullable).                                                            */
 int ncf_relu_ln_dropout_fwd(float* relu_in, int64_t n, int64_t width, const float* gamma,
                             const float* beta, float eps, float dropout_p, uint64_t seed,
-                            float* out, float* mean, float* rstd, void* stream);
+                            const ncf_step_clock* clock, float* out, float* mean, float* rstd,
+                            void* stream);
 int64_t ncf_relu_ln_dropout_bwd_workspace(int64_t n, int64_t width);
 int ncf_relu_ln_dropout_bwd(const float* grad_out, const float* relu_in, const float* mean,
                             const float* rstd, const float* gamma, int64_t n, int64_t width,
-                            float dropout_p, uint64_t seed, float* grad_lin, float* grad_gamma,
+                            float dropout_p, uint64_t seed, const ncf_step_clock* clock,
+                            float* grad_lin, float* grad_gamma,
                             float* grad_beta, float* grad_bias, float* workspace,
                             int64_t workspace_floats, ncf_reduce_list* defer, void* stream);
 
@@ -322,6 +338,31 @@ int ncf_adam_sweep(float* p0, float* m0, float* v0, float* p1, float* m1, float*
                    int64_t row0, int64_t rows, int64_t dim, int32_t* stamp, int32_t target,
                    const float* step_table, double beta1, double beta2, double eps,
                    double weight_decay, void* stream);
+/* Clock-driven forms (hipGraph-capturable): catch-up target = clock->t + target_rel; apply step
+ * = clock->t + step_rel; the rolling sweep closes step s = clock->t + step_rel and brings slice
+ * (s mod sweep_every) of `slice` rows current through s; the flat Adam applies step
+ * clock->t + step_rel with the scalars of step_table (bit-identical to ncf_adam_flat).       */
+int ncf_adam_rows_catchup_clock(float* p0, float* m0, float* v0, float* p1, float* m1, float* v1,
+                                int64_t dim, const int64_t* row_ids, const uint32_t* count,
+                                int kind, int64_t max_n, int32_t* stamp, int32_t target_rel,
+                                const ncf_step_clock* clock, const float* step_table,
+                                double beta1, double beta2, double eps, double weight_decay,
+                                void* stream);
+int ncf_adam_rows_apply_clock(float* p0, float* m0, float* v0, const float* g0, float* p1,
+                              float* m1, float* v1, const float* g1, int64_t dim,
+                              const int64_t* row_ids, const uint32_t* count, int kind,
+                              int64_t max_n, int32_t* stamp, int32_t step_rel,
+                              const ncf_step_clock* clock, const float* step_table, double beta1,
+                              double beta2, double eps, double weight_decay, void* stream);
+int ncf_adam_sweep_rolling(float* p0, float* m0, float* v0, float* p1, float* m1, float* v1,
+                           int64_t total_rows, int64_t slice, int32_t sweep_every, int64_t dim,
+                           int32_t* stamp, int32_t step_rel, const ncf_step_clock* clock,
+                           const float* step_table, double beta1, double beta2, double eps,
+                           double weight_decay, void* stream);
+int ncf_adam_flat_clock(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                        int64_t n, const float* step_table, int32_t step_rel,
+                        const ncf_step_clock* clock, double beta1, double beta2, double eps,
+                        double weight_decay, void* stream);
 
 #ifdef __cplusplus
 }

@@ -51,12 +51,12 @@ SIGNATURES = {
     "ncf_reduce_batch": (I32, [P, P, I64, P]),
     "ncf_colsum_workspace": (I64, [I64, I64]),
     "ncf_colsum": (I32, [P, I64, I64, I64, P, I32, P, I64, P]),
-    "ncf_attention_fwd": (I32, [P, P, P, I64, I64, I64, I64, F32, U64, P, P, P]),
-    "ncf_attention_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P, P]),
-    "ncf_relu_ln_dropout_fwd": (I32, [P, I64, I64, P, P, F32, F32, U64, P, P, P, P]),
+    "ncf_attention_fwd": (I32, [P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P]),
+    "ncf_attention_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P, P, P]),
+    "ncf_relu_ln_dropout_fwd": (I32, [P, I64, I64, P, P, F32, F32, U64, P, P, P, P, P]),
     "ncf_relu_ln_dropout_bwd_workspace": (I64, [I64, I64]),
-    "ncf_relu_ln_dropout_bwd": (I32, [P, P, P, P, P, I64, I64, F32, U64, P, P, P, P, P, I64, P,
-                                      P]),
+    "ncf_relu_ln_dropout_bwd": (I32, [P, P, P, P, P, I64, I64, F32, U64, P, P, P, P, P, P, I64,
+                                      P, P]),
     "ncf_head_fwd": (I32, [P, I64, I64, P, P, P, P, P, P, P, P]),
     "ncf_head_bwd_workspace": (I64, [I64, I64, I64]),
     "ncf_head_bwd": (I32, [P, P, P, P, P, P, I64, I64, P, P, P, P, I64, P, P, P, P, P, P, P, P,
@@ -85,6 +85,14 @@ SIGNATURES = {
     "ncf_adam_rows_apply": (I32, [P, P, P, P, P, P, P, P, I64, P, P, I32, I64, P, I32, P, F64, F64,
                                   F64, F64, P]),
     "ncf_adam_sweep": (I32, [P, P, P, P, P, P, I64, I64, I64, P, I32, P, F64, F64, F64, F64, P]),
+    "ncf_step_clock_advance": (I32, [P, U64, P]),
+    "ncf_adam_rows_catchup_clock": (I32, [P, P, P, P, P, P, I64, P, P, I32, I64, P, I32, P, P, F64,
+                                          F64, F64, F64, P]),
+    "ncf_adam_rows_apply_clock": (I32, [P, P, P, P, P, P, P, P, I64, P, P, I32, I64, P, I32, P, P,
+                                        F64, F64, F64, F64, P]),
+    "ncf_adam_sweep_rolling": (I32, [P, P, P, P, P, P, I64, I64, I32, I64, P, I32, P, P, F64, F64,
+                                     F64, F64, P]),
+    "ncf_adam_flat_clock": (I32, [P, P, P, P, I64, P, I32, P, F64, F64, F64, F64, P]),
     "ncf_score_queries": (I32, [P, I64, P, I64, I64, P, P, F32, P, P, P, P, P]),
     "ncf_score_item_bias": (I32, [P, I64, P, P, P, P, P]),
     "ncf_score_kth": (I32, [P, I64, I64, I32, P, I64, P, P]),

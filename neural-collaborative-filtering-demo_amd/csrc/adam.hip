@@ -140,13 +140,15 @@ __global__ __launch_bounds__(256) void k_adam_catchup(TablePtrs t, const int64_t
                                                       const uint32_t* __restrict__ count, int kind,
                                                       int64_t max_n, int32_t* __restrict__ stamp,
                                                       int32_t target, const float* __restrict__ table,
-                                                      AdamScalars s) {
+                                                      AdamScalars s,
+                                                      const ncf_step_clock* __restrict__ clock) {
   constexpr int L = D / 4;
   const int64_t tt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t c = tt / L;
   const int sub = (int)(tt % L);
   const int64_t cnt = count ? (int64_t)count[kind] : max_n;
   if (c >= max_n || c >= cnt) return;
+  if (clock) target += clock->t;
   const int64_t row = ids[c];
   const int32_t from = stamp[row];
   catch_up_row<D>(t, row, sub * 4, from, target, table, s);
@@ -177,13 +179,15 @@ __global__ __launch_bounds__(256) void k_adam_apply(TablePtrs t, const int64_t* 
                                                     const uint32_t* __restrict__ count, int kind,
                                                     int64_t max_n, int32_t* __restrict__ stamp,
                                                     int32_t step, const float* __restrict__ table,
-                                                    AdamScalars s) {
+                                                    AdamScalars s,
+                                                    const ncf_step_clock* __restrict__ clock) {
   constexpr int L = D / 4;
   const int64_t tt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t c = tt / L;
   const int sub = (int)(tt % L);
   const int64_t cnt = count ? (int64_t)count[kind] : max_n;
   if (c >= max_n || c >= cnt) return;
+  if (clock) step += clock->t;
   const int64_t row = ids[c];
   const int64_t o = row * D + sub * 4;
   const float ns = table[2 * step], bc = table[2 * step + 1];
@@ -196,6 +200,60 @@ __global__ __launch_bounds__(256) void k_adam_apply(TablePtrs t, const int64_t* 
     st4(t.p1 + o, p1); st4(t.m1 + o, m1); st4(t.v1 + o, v1);
   }
   if (sub == 0) stamp[row] = step;
+}
+
+// rolling sweep of a captured step: closes step s = clock->t + step_rel, slice (s mod every)
+template <int D>
+__global__ __launch_bounds__(256) void k_adam_sweep_rolling(TablePtrs t, int64_t total_rows,
+                                                            int64_t slice, int32_t every,
+                                                            int32_t* __restrict__ stamp,
+                                                            int32_t step_rel,
+                                                            const ncf_step_clock* __restrict__ clock,
+                                                            const float* __restrict__ table,
+                                                            AdamScalars s) {
+  constexpr int L = D / 4;
+  const int32_t target = clock->t + step_rel;
+  const int64_t row0 = (int64_t)(target % every) * slice;
+  const int64_t rows = max((int64_t)0, min(slice, total_rows - row0));
+  const int64_t n = rows * L;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = row0 + e / L;
+    const int sub = (int)(e % L);
+    const int32_t from = stamp[row];
+    catch_up_row<D>(t, row, sub * 4, from, target, table, s);
+    if (sub == 0 && from < target) stamp[row] = target;
+  }
+}
+
+// flat Adam of step clock->t + step_rel with the step table's scalars
+__global__ __launch_bounds__(256) void k_adam_flat_clock(float* __restrict__ p,
+                                                         const float* __restrict__ g,
+                                                         float* __restrict__ m,
+                                                         float* __restrict__ v, int64_t n,
+                                                         const float* __restrict__ table,
+                                                         int32_t step_rel,
+                                                         const ncf_step_clock* __restrict__ clock,
+                                                         AdamScalars s) {
+  const int32_t step = clock->t + step_rel;
+  const float ns = table[2 * step], bc = table[2 * step + 1];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    adam1(pp, mm, vv, g[i], ns, bc, s);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+  }
+}
+
+__global__ void k_clock_advance(ncf_step_clock* clock, uint64_t base_seed) {
+  const int32_t t = clock->t + 1;
+  clock->t = t;
+  uint64_t z = base_seed + 0x9E3779B97F4A7C15ull * (uint64_t)(t + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  clock->seed = (z ^ (z >> 31)) & 0x3FFFFFFFFFFFFFFFull;
 }
 
 AdamScalars make_scalars(double lr, double beta1, double beta2, double eps, double wd, double step) {
@@ -295,19 +353,31 @@ AdamScalars consts_of(double beta1, double beta2, double eps, double wd) {
 
 template <int D>
 int catchup_d(TablePtrs t, const int64_t* ids, const uint32_t* count, int kind, int64_t max_n,
-              int32_t* stamp, int32_t target, const float* table, AdamScalars s, hipStream_t st) {
+              int32_t* stamp, int32_t target, const float* table, AdamScalars s,
+              const ncf_step_clock* clock, hipStream_t st) {
   hipLaunchKernelGGL(k_adam_catchup<D>, dim3(ncf_cdiv(max_n * (D / 4), 256)), dim3(256), 0, st, t,
-                     ids, count, kind, max_n, stamp, target, table, s);
+                     ids, count, kind, max_n, stamp, target, table, s, clock);
   NCF_CHECK_LAUNCH("ncf_adam_rows_catchup");
   return NCF_OK;
 }
 
 template <int D>
 int apply_d(TablePtrs t, const int64_t* ids, const uint32_t* count, int kind, int64_t max_n,
-            int32_t* stamp, int32_t step, const float* table, AdamScalars s, hipStream_t st) {
+            int32_t* stamp, int32_t step, const float* table, AdamScalars s,
+            const ncf_step_clock* clock, hipStream_t st) {
   hipLaunchKernelGGL(k_adam_apply<D>, dim3(ncf_cdiv(max_n * (D / 4), 256)), dim3(256), 0, st, t,
-                     ids, count, kind, max_n, stamp, step, table, s);
+                     ids, count, kind, max_n, stamp, step, table, s, clock);
   NCF_CHECK_LAUNCH("ncf_adam_rows_apply");
+  return NCF_OK;
+}
+
+template <int D>
+int rolling_d(TablePtrs t, int64_t total, int64_t slice, int32_t every, int32_t* stamp,
+              int32_t step_rel, const ncf_step_clock* clock, const float* table, AdamScalars s,
+              hipStream_t st) {
+  hipLaunchKernelGGL(k_adam_sweep_rolling<D>, dim3(grid_for(slice * (D / 4))), dim3(256), 0, st, t,
+                     total, slice, every, stamp, step_rel, clock, table, s);
+  NCF_CHECK_LAUNCH("ncf_adam_sweep_rolling");
   return NCF_OK;
 }
 
@@ -344,7 +414,7 @@ extern "C" int ncf_adam_rows_catchup(float* p0, float* m0, float* v0, float* p1,
   NCF_CHECK_ARG(p0 && m0 && v0 && row_ids && stamp && step_table, "ncf_adam_rows_catchup: null");
   TablePtrs t{p0, m0, v0, p1, m1, v1, nullptr, nullptr};
   NCF_DISPATCH_DIM(dim, catchup_d, t, row_ids, count, kind, max_n, stamp, target, step_table,
-                   consts_of(beta1, beta2, eps, weight_decay), (hipStream_t)stream);
+                   consts_of(beta1, beta2, eps, weight_decay), nullptr, (hipStream_t)stream);
 }
 
 extern "C" int ncf_adam_rows_apply(float* p0, float* m0, float* v0, const float* g0, float* p1,
@@ -359,7 +429,7 @@ extern "C" int ncf_adam_rows_apply(float* p0, float* m0, float* v0, const float*
   NCF_CHECK_ARG(!p1 || g1, "ncf_adam_rows_apply: second table without gradient");
   TablePtrs t{p0, m0, v0, p1, m1, v1, g0, g1};
   NCF_DISPATCH_DIM(dim, apply_d, t, row_ids, count, kind, max_n, stamp, step, step_table,
-                   consts_of(beta1, beta2, eps, weight_decay), (hipStream_t)stream);
+                   consts_of(beta1, beta2, eps, weight_decay), nullptr, (hipStream_t)stream);
 }
 
 // rows [row0, row0 + rows) caught up to `target` (a rolling sweep passes one slice per step)
@@ -372,4 +442,73 @@ extern "C" int ncf_adam_sweep(float* p0, float* m0, float* v0, float* p1, float*
   TablePtrs t{p0, m0, v0, p1, m1, v1, nullptr, nullptr};
   NCF_DISPATCH_DIM(dim, sweep_d, t, row0, rows, stamp, target, step_table,
                    consts_of(beta1, beta2, eps, weight_decay), (hipStream_t)stream);
+}
+
+// ---- clock-driven forms (hipGraph-capturable training step)
+extern "C" int ncf_step_clock_advance(ncf_step_clock* clock, uint64_t base_seed, void* stream) {
+  NCF_CHECK_ARG(clock, "ncf_step_clock_advance: null clock");
+  hipLaunchKernelGGL(k_clock_advance, dim3(1), dim3(1), 0, (hipStream_t)stream, clock, base_seed);
+  NCF_CHECK_LAUNCH("ncf_step_clock_advance");
+  return NCF_OK;
+}
+
+extern "C" int ncf_adam_rows_catchup_clock(float* p0, float* m0, float* v0, float* p1, float* m1,
+                                           float* v1, int64_t dim, const int64_t* row_ids,
+                                           const uint32_t* count, int kind, int64_t max_n,
+                                           int32_t* stamp, int32_t target_rel,
+                                           const ncf_step_clock* clock, const float* step_table,
+                                           double beta1, double beta2, double eps,
+                                           double weight_decay, void* stream) {
+  if (max_n <= 0) return NCF_OK;
+  NCF_CHECK_ARG(p0 && m0 && v0 && row_ids && stamp && step_table && clock,
+                "ncf_adam_rows_catchup_clock: null");
+  TablePtrs t{p0, m0, v0, p1, m1, v1, nullptr, nullptr};
+  NCF_DISPATCH_DIM(dim, catchup_d, t, row_ids, count, kind, max_n, stamp, target_rel, step_table,
+                   consts_of(beta1, beta2, eps, weight_decay), clock, (hipStream_t)stream);
+}
+
+extern "C" int ncf_adam_rows_apply_clock(float* p0, float* m0, float* v0, const float* g0,
+                                         float* p1, float* m1, float* v1, const float* g1,
+                                         int64_t dim, const int64_t* row_ids,
+                                         const uint32_t* count, int kind, int64_t max_n,
+                                         int32_t* stamp, int32_t step_rel,
+                                         const ncf_step_clock* clock, const float* step_table,
+                                         double beta1, double beta2, double eps,
+                                         double weight_decay, void* stream) {
+  if (max_n <= 0) return NCF_OK;
+  NCF_CHECK_ARG(p0 && m0 && v0 && g0 && row_ids && stamp && step_table && clock,
+                "ncf_adam_rows_apply_clock: bad args");
+  NCF_CHECK_ARG(!p1 || g1, "ncf_adam_rows_apply_clock: second table without gradient");
+  TablePtrs t{p0, m0, v0, p1, m1, v1, g0, g1};
+  NCF_DISPATCH_DIM(dim, apply_d, t, row_ids, count, kind, max_n, stamp, step_rel, step_table,
+                   consts_of(beta1, beta2, eps, weight_decay), clock, (hipStream_t)stream);
+}
+
+extern "C" int ncf_adam_sweep_rolling(float* p0, float* m0, float* v0, float* p1, float* m1,
+                                      float* v1, int64_t total_rows, int64_t slice,
+                                      int32_t sweep_every, int64_t dim, int32_t* stamp,
+                                      int32_t step_rel, const ncf_step_clock* clock,
+                                      const float* step_table, double beta1, double beta2,
+                                      double eps, double weight_decay, void* stream) {
+  if (total_rows <= 0 || slice <= 0) return NCF_OK;
+  NCF_CHECK_ARG(p0 && m0 && v0 && stamp && step_table && clock && sweep_every >= 1,
+                "ncf_adam_sweep_rolling: bad args");
+  TablePtrs t{p0, m0, v0, p1, m1, v1, nullptr, nullptr};
+  NCF_DISPATCH_DIM(dim, rolling_d, t, total_rows, slice, sweep_every, stamp, step_rel, clock,
+                   step_table, consts_of(beta1, beta2, eps, weight_decay), (hipStream_t)stream);
+}
+
+extern "C" int ncf_adam_flat_clock(float* param, const float* grad, float* exp_avg,
+                                   float* exp_avg_sq, int64_t n, const float* step_table,
+                                   int32_t step_rel, const ncf_step_clock* clock, double beta1,
+                                   double beta2, double eps, double weight_decay, void* stream) {
+  NCF_CHECK_ARG(n >= 0, "ncf_adam_flat_clock: bad args");
+  if (n == 0) return NCF_OK;
+  NCF_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && step_table && clock,
+                "ncf_adam_flat_clock: null pointer");
+  hipLaunchKernelGGL(k_adam_flat_clock, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                     param, grad, exp_avg, exp_avg_sq, n, step_table, step_rel, clock,
+                     consts_of(beta1, beta2, eps, weight_decay));
+  NCF_CHECK_LAUNCH("ncf_adam_flat_clock");
+  return NCF_OK;
 }

@@ -19,10 +19,11 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const float* __restrict__ Q,
                                                   const float* __restrict__ Kt,
                                                   const float* __restrict__ V, int64_t B, int L,
                                                   int H, float scale, float p_drop,
-                                                  uint64_t seed, float* __restrict__ P,
+                                                  uint64_t seed, const ncf_step_clock* clock, float* __restrict__ P,
                                                   float* __restrict__ O) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= B * H * L) return;
+  if (clock) seed += clock->seed;  // per-step stream of a captured step
   const int i = (int)(t % L);
   const int h = (int)((t / L) % H);
   const int64_t b = t / ((int64_t)L * H);
@@ -78,10 +79,11 @@ __global__ __launch_bounds__(256) void k_attn_bwd_q(const float* __restrict__ dO
                                                     const float* __restrict__ Kt,
                                                     const float* __restrict__ V,
                                                     const float* __restrict__ P, int64_t B, int L,
-                                                    int H, float scale, float p_drop, uint64_t seed,
+                                                    int H, float scale, float p_drop, uint64_t seed, const ncf_step_clock* clock,
                                                     float* __restrict__ dS, float* __restrict__ dQ) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= B * H * L) return;
+  if (clock) seed += clock->seed;  // per-step stream of a captured step
   const int i = (int)(t % L);
   const int h = (int)((t / L) % H);
   const int64_t b = t / ((int64_t)L * H);
@@ -132,10 +134,11 @@ __global__ __launch_bounds__(256) void k_attn_bwd_kv(const float* __restrict__ Q
                                                      const float* __restrict__ P,
                                                      const float* __restrict__ dS, int64_t B,
                                                      int L, int H, float scale, float p_drop,
-                                                     uint64_t seed, float* __restrict__ dK,
+                                                     uint64_t seed, const ncf_step_clock* clock, float* __restrict__ dK,
                                                      float* __restrict__ dV) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= B * H * L) return;
+  if (clock) seed += clock->seed;  // per-step stream of a captured step
   const int j = (int)(t % L);
   const int h = (int)((t / L) % H);
   const int64_t b = t / ((int64_t)L * H);
@@ -169,49 +172,49 @@ __global__ __launch_bounds__(256) void k_attn_bwd_kv(const float* __restrict__ Q
 
 template <int HD, int LMAX>
 int fwd_l(const float* Q, const float* K, const float* V, int64_t B, int L, int H, float p,
-          uint64_t seed, float* P, float* O, hipStream_t st) {
+          uint64_t seed, const ncf_step_clock* clock, float* P, float* O, hipStream_t st) {
   const int64_t n = B * H * L;
   hipLaunchKernelGGL((k_attn_fwd<HD, LMAX>), dim3(ncf_cdiv(n, 256)), dim3(256), 0, st, Q, K, V, B,
-                     L, H, sqrtf((float)HD), p, seed, P, O);
+                     L, H, sqrtf((float)HD), p, seed, clock, P, O);
   NCF_CHECK_LAUNCH("ncf_attention_fwd");
   return NCF_OK;
 }
 
 template <int HD, int LMAX>
 int bwd_l(const float* Q, const float* K, const float* V, const float* P, const float* dO,
-          int64_t B, int L, int H, float p, uint64_t seed, float* dS, float* dQ, float* dK,
+          int64_t B, int L, int H, float p, uint64_t seed, const ncf_step_clock* clock, float* dS, float* dQ, float* dK,
           float* dV, hipStream_t st) {
   const int64_t n = B * H * L;
   const float scale = sqrtf((float)HD);
   hipLaunchKernelGGL((k_attn_bwd_q<HD, LMAX>), dim3(ncf_cdiv(n, 256)), dim3(256), 0, st, dO, K, V,
-                     P, B, L, H, scale, p, seed, dS, dQ);
+                     P, B, L, H, scale, p, seed, clock, dS, dQ);
   NCF_CHECK_LAUNCH("ncf_attention_bwd(q)");
   hipLaunchKernelGGL((k_attn_bwd_kv<HD>), dim3(ncf_cdiv(n, 256)), dim3(256), 0, st, Q, dO, P, dS,
-                     B, L, H, scale, p, seed, dK, dV);
+                     B, L, H, scale, p, seed, clock, dK, dV);
   NCF_CHECK_LAUNCH("ncf_attention_bwd(kv)");
   return NCF_OK;
 }
 
 template <int HD>
 int fwd_hd(const float* Q, const float* K, const float* V, int64_t B, int L, int H, float p,
-           uint64_t seed, float* P, float* O, hipStream_t st) {
-  if (L <= 8) return fwd_l<HD, 8>(Q, K, V, B, L, H, p, seed, P, O, st);
-  return fwd_l<HD, 64>(Q, K, V, B, L, H, p, seed, P, O, st);
+           uint64_t seed, const ncf_step_clock* clock, float* P, float* O, hipStream_t st) {
+  if (L <= 8) return fwd_l<HD, 8>(Q, K, V, B, L, H, p, seed, clock, P, O, st);
+  return fwd_l<HD, 64>(Q, K, V, B, L, H, p, seed, clock, P, O, st);
 }
 
 template <int HD>
 int bwd_hd(const float* Q, const float* K, const float* V, const float* P, const float* dO,
-           int64_t B, int L, int H, float p, uint64_t seed, float* dS, float* dQ, float* dK,
+           int64_t B, int L, int H, float p, uint64_t seed, const ncf_step_clock* clock, float* dS, float* dQ, float* dK,
            float* dV, hipStream_t st) {
-  if (L <= 8) return bwd_l<HD, 8>(Q, K, V, P, dO, B, L, H, p, seed, dS, dQ, dK, dV, st);
-  return bwd_l<HD, 64>(Q, K, V, P, dO, B, L, H, p, seed, dS, dQ, dK, dV, st);
+  if (L <= 8) return bwd_l<HD, 8>(Q, K, V, P, dO, B, L, H, p, seed, clock, dS, dQ, dK, dV, st);
+  return bwd_l<HD, 64>(Q, K, V, P, dO, B, L, H, p, seed, clock, dS, dQ, dK, dV, st);
 }
 
 }  // namespace
 
 extern "C" int ncf_attention_fwd(const float* q, const float* k, const float* v, int64_t groups,
                                  int64_t group_len, int64_t heads, int64_t dim, float dropout_p,
-                                 uint64_t seed, float* probs, float* out, void* stream) {
+                                 uint64_t seed, const ncf_step_clock* clock, float* probs, float* out, void* stream) {
   NCF_CHECK_ARG(groups >= 0 && group_len >= 1 && group_len <= 64 && heads >= 1 && dim % heads == 0,
                 "ncf_attention_fwd: bad shape (groups=%lld L=%lld H=%lld D=%lld; L<=64)",
                 (long long)groups, (long long)group_len, (long long)heads, (long long)dim);
@@ -220,10 +223,10 @@ extern "C" int ncf_attention_fwd(const float* q, const float* k, const float* v,
   hipStream_t st = (hipStream_t)stream;
   const int L = (int)group_len, H = (int)heads;
   switch (dim / heads) {
-    case 8: return fwd_hd<8>(q, k, v, groups, L, H, dropout_p, seed, probs, out, st);
-    case 16: return fwd_hd<16>(q, k, v, groups, L, H, dropout_p, seed, probs, out, st);
-    case 32: return fwd_hd<32>(q, k, v, groups, L, H, dropout_p, seed, probs, out, st);
-    case 64: return fwd_hd<64>(q, k, v, groups, L, H, dropout_p, seed, probs, out, st);
+    case 8: return fwd_hd<8>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st);
+    case 16: return fwd_hd<16>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st);
+    case 32: return fwd_hd<32>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st);
+    case 64: return fwd_hd<64>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st);
   }
   ncf_set_error("ncf_attention_fwd: head dim %lld unsupported (8/16/32/64)", (long long)(dim / heads));
   return NCF_ERR_ARG;
@@ -231,7 +234,7 @@ extern "C" int ncf_attention_fwd(const float* q, const float* k, const float* v,
 
 extern "C" int ncf_attention_bwd(const float* q, const float* k, const float* v, const float* probs,
                                  const float* grad_out, int64_t groups, int64_t group_len,
-                                 int64_t heads, int64_t dim, float dropout_p, uint64_t seed,
+                                 int64_t heads, int64_t dim, float dropout_p, uint64_t seed, const ncf_step_clock* clock,
                                  float* grad_scores, float* grad_q, float* grad_k, float* grad_v,
                                  void* stream) {
   NCF_CHECK_ARG(groups >= 0 && group_len >= 1 && group_len <= 64 && heads >= 1 && dim % heads == 0,
@@ -240,10 +243,10 @@ extern "C" int ncf_attention_bwd(const float* q, const float* k, const float* v,
   hipStream_t st = (hipStream_t)stream;
   const int L = (int)group_len, H = (int)heads;
   switch (dim / heads) {
-    case 8: return bwd_hd<8>(q, k, v, probs, grad_out, groups, L, H, dropout_p, seed, grad_scores, grad_q, grad_k, grad_v, st);
-    case 16: return bwd_hd<16>(q, k, v, probs, grad_out, groups, L, H, dropout_p, seed, grad_scores, grad_q, grad_k, grad_v, st);
-    case 32: return bwd_hd<32>(q, k, v, probs, grad_out, groups, L, H, dropout_p, seed, grad_scores, grad_q, grad_k, grad_v, st);
-    case 64: return bwd_hd<64>(q, k, v, probs, grad_out, groups, L, H, dropout_p, seed, grad_scores, grad_q, grad_k, grad_v, st);
+    case 8: return bwd_hd<8>(q, k, v, probs, grad_out, groups, L, H, dropout_p, seed, clock, grad_scores, grad_q, grad_k, grad_v, st);
+    case 16: return bwd_hd<16>(q, k, v, probs, grad_out, groups, L, H, dropout_p, seed, clock, grad_scores, grad_q, grad_k, grad_v, st);
+    case 32: return bwd_hd<32>(q, k, v, probs, grad_out, groups, L, H, dropout_p, seed, clock, grad_scores, grad_q, grad_k, grad_v, st);
+    case 64: return bwd_hd<64>(q, k, v, probs, grad_out, groups, L, H, dropout_p, seed, clock, grad_scores, grad_q, grad_k, grad_v, st);
   }
   ncf_set_error("ncf_attention_bwd: head dim unsupported");
   return NCF_ERR_ARG;

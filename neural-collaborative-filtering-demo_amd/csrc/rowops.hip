@@ -20,7 +20,7 @@ template <int W>
 __global__ __launch_bounds__(256) void k_relu_ln_drop_fwd(float* __restrict__ r,  // [N,W] relu(lin), in
                                                           int64_t n, const float* __restrict__ g,
                                                           const float* __restrict__ b, float eps,
-                                                          float p, uint64_t seed,
+                                                          float p, uint64_t seed, const ncf_step_clock* clock,
                                                           float* __restrict__ out,
                                                           float* __restrict__ mean_out,
                                                           float* __restrict__ rstd_out) {
@@ -29,6 +29,7 @@ __global__ __launch_bounds__(256) void k_relu_ln_drop_fwd(float* __restrict__ r,
   const int64_t row = t / G::L;
   const int sub = (int)(t % G::L);
   if (row >= n) return;
+  if (clock) seed += clock->seed;  // per-step stream of a captured step
   float4 x[G::CH], gg[G::CH], bb[G::CH];
   float s = 0.0f;
 #pragma unroll
@@ -73,9 +74,10 @@ template <int W>
 __global__ __launch_bounds__(256) void k_relu_ln_drop_bwd(
     const float* __restrict__ dout, const float* __restrict__ r, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ g, int64_t n, int rows_per_block,
-    float p, uint64_t seed, float* __restrict__ dlin, float* __restrict__ part) {
+    float p, uint64_t seed, const ncf_step_clock* clock, float* __restrict__ dlin, float* __restrict__ part) {
   using G = Geo<W>;
   __shared__ float red[256 / G::L][3 * W];
+  if (clock) seed += clock->seed;
   const int lane_grp = threadIdx.x / G::L;  // row slot inside the block iteration
   const int sub = threadIdx.x % G::L;
   const int slots = 256 / G::L;
@@ -158,22 +160,22 @@ static inline int bwd_blocks(int64_t n, int64_t width) {
 }
 
 template <int W>
-int fwd_w(float* r, int64_t n, const float* g, const float* b, float eps, float p, uint64_t seed,
+int fwd_w(float* r, int64_t n, const float* g, const float* b, float eps, float p, uint64_t seed, const ncf_step_clock* clock,
           float* out, float* mean, float* rstd, hipStream_t st) {
   const int64_t threads = n * Geo<W>::L;
   hipLaunchKernelGGL(k_relu_ln_drop_fwd<W>, dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st, r, n,
-                     g, b, eps, p, seed, out, mean, rstd);
+                     g, b, eps, p, seed, clock, out, mean, rstd);
   NCF_CHECK_LAUNCH("ncf_relu_ln_dropout_fwd");
   return NCF_OK;
 }
 
 template <int W>
 int bwd_w(const float* dout, const float* r, const float* mean, const float* rstd, const float* g,
-          int64_t n, float p, uint64_t seed, float* dlin, float* dgamma, float* dbeta,
+          int64_t n, float p, uint64_t seed, const ncf_step_clock* clock, float* dlin, float* dgamma, float* dbeta,
           float* dbias, float* ws, ncf_reduce_list* defer, hipStream_t st) {
   const int nb = bwd_blocks(n, W);
   hipLaunchKernelGGL(k_relu_ln_drop_bwd<W>, dim3(nb), dim3(256), 0, st, dout, r, mean, rstd, g, n,
-                     (int)bwd_rows_per_block(n, W), p, seed, dlin, ws);
+                     (int)bwd_rows_per_block(n, W), p, seed, clock, dlin, ws);
   NCF_CHECK_LAUNCH("ncf_relu_ln_dropout_bwd");
   // dbias, dgamma, dbeta are the three W-wide thirds of each partial row: one strided reduce
   // when the three outputs are equally spaced (consecutive parameters of the flat buffer)
@@ -220,18 +222,18 @@ extern "C" int64_t ncf_relu_ln_dropout_bwd_workspace(int64_t n, int64_t width) {
 // out = dropout(LayerNorm(r)); r already holds relu(linear) (GEMM epilogue); saves mean/rstd.
 extern "C" int ncf_relu_ln_dropout_fwd(float* relu_in, int64_t n, int64_t width,
                                        const float* gamma, const float* beta, float eps,
-                                       float dropout_p, uint64_t seed, float* out, float* mean,
+                                       float dropout_p, uint64_t seed, const ncf_step_clock* clock, float* out, float* mean,
                                        float* rstd, void* stream) {
   NCF_CHECK_ARG(n >= 0, "ncf_relu_ln_dropout_fwd: n < 0");
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_relu_ln_dropout_fwd: bad dropout");
   if (n == 0) return NCF_OK;
-  NCF_DISPATCH_W(width, fwd_w, relu_in, n, gamma, beta, eps, dropout_p, seed, out, mean, rstd,
+  NCF_DISPATCH_W(width, fwd_w, relu_in, n, gamma, beta, eps, dropout_p, seed, clock, out, mean, rstd,
                  (hipStream_t)stream);
 }
 
 extern "C" int ncf_relu_ln_dropout_bwd(const float* grad_out, const float* relu_in,
                                        const float* mean, const float* rstd, const float* gamma,
-                                       int64_t n, int64_t width, float dropout_p, uint64_t seed,
+                                       int64_t n, int64_t width, float dropout_p, uint64_t seed, const ncf_step_clock* clock,
                                        float* grad_lin, float* grad_gamma, float* grad_beta,
                                        float* grad_bias, float* workspace,
                                        int64_t workspace_floats, ncf_reduce_list* defer,
@@ -241,6 +243,6 @@ extern "C" int ncf_relu_ln_dropout_bwd(const float* grad_out, const float* relu_
     ncf_set_error("ncf_relu_ln_dropout_bwd: workspace too small");
     return NCF_ERR_WORKSPACE;
   }
-  NCF_DISPATCH_W(width, bwd_w, grad_out, relu_in, mean, rstd, gamma, n, dropout_p, seed, grad_lin,
+  NCF_DISPATCH_W(width, bwd_w, grad_out, relu_in, mean, rstd, gamma, n, dropout_p, seed, clock, grad_lin,
                  grad_gamma, grad_beta, grad_bias, workspace, defer, (hipStream_t)stream);
 }

@@ -23,7 +23,7 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMaxG = NCF_WGRAD_GROUP_MAX;
-constexpr int kUnroll = 8;  // MFMA steps (16 rows) of loads in flight per wave
+constexpr int kUnroll = 8;  // MFMA steps (16 rows) per pipeline stage
 
 struct GroupArgs {
   ncf_wgrad_desc d[kMaxG];
@@ -66,22 +66,30 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(const GroupArgs a) {
   for (int q = 0; q < 16; ++q) { c00[q] = 0.f; c01[q] = 0.f; c10[q] = 0.f; c11[q] = 0.f; }
   float rs0 = 0.f, rs1 = 0.f;  // bias partials (row sums of dYᵀ = column sums of dY)
   const bool want_bias = d.dbias != nullptr && tj == 0;
-  for (int rb = r0; rb < r1; rb += 2 * kUnroll) {
-    float a0[kUnroll], a1[kUnroll], b0[kUnroll], b1[kUnroll];
+  // software pipeline: the loads of the next 2*kUnroll rows are issued before the MFMAs of the
+  // current ones (register double buffer; sched_barrier keeps the scheduler from sinking them)
+  float a0[kUnroll], a1[kUnroll], b0[kUnroll], b1[kUnroll];
+  auto load = [&](int rb, float* x0, float* x1, float* y0, float* y1) {
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int r = rb + 2 * u + h;
       const bool vr = r < r1;
       const int64_t rr = vr ? r : r0;
-      a0[u] = pa0[rr * d.ldy];
-      a1[u] = pa1[rr * d.ldy];
-      b0[u] = pb0[rr * d.ldx];
-      b1[u] = pb1[rr * d.ldx];
-      a0[u] = (vr && va0) ? a0[u] : 0.f;
-      a1[u] = (vr && va1) ? a1[u] : 0.f;
-      b0[u] = (vr && vb0) ? b0[u] : 0.f;
-      b1[u] = (vr && vb1) ? b1[u] : 0.f;
+      x0[u] = pa0[rr * d.ldy];
+      x1[u] = pa1[rr * d.ldy];
+      y0[u] = pb0[rr * d.ldx];
+      y1[u] = pb1[rr * d.ldx];
+      x0[u] = (vr && va0) ? x0[u] : 0.f;
+      x1[u] = (vr && va1) ? x1[u] : 0.f;
+      y0[u] = (vr && vb0) ? y0[u] : 0.f;
+      y1[u] = (vr && vb1) ? y1[u] : 0.f;
     }
+  };
+  load(r0, a0, a1, b0, b1);
+  for (int rb = r0; rb < r1; rb += 2 * kUnroll) {
+    float n0[kUnroll], n1[kUnroll], m0[kUnroll], m1[kUnroll];
+    load(rb + 2 * kUnroll < r1 ? rb + 2 * kUnroll : r0, n0, n1, m0, m1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], b0[u], c00, 0, 0, 0);
@@ -90,6 +98,8 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(const GroupArgs a) {
       c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], b1[u], c11, 0, 0, 0);
       if (want_bias) { rs0 += a0[u]; rs1 += a1[u]; }
     }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) { a0[u] = n0[u]; a1[u] = n1[u]; b0[u] = m0[u]; b1[u] = m1[u]; }
   }
   // slab partial [m_out][k_in]: C row (m index) = (r&3) + 8(r>>2) + 4h, column (k_in index) = i
   float* P = a.part[g] + (int64_t)slab * d.m_out * d.k_in;

@@ -29,8 +29,11 @@ _KINDS = (("user", "mf_user", "mlp_user"), ("item", "mf_item", "mlp_item"))
 
 class DeferredTableAdam:
     def __init__(self, engine, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
-                 sweep_every: int = 64, moments=None):
+                 sweep_every: int = 64, moments=None, clock=None):
         self.engine = engine
+        # clock (ncf_step_clock, device): every step-dependent value is read on the device, so
+        # the launches of a step do not depend on the host counter (hipGraph capture)
+        self.clock = clock
         self.lr, self.betas, self.eps, self.wd = float(lr), tuple(betas), float(eps), float(weight_decay)
         self.sweep_every = int(sweep_every)
         self.tables = engine.table_params()
@@ -82,6 +85,14 @@ class DeferredTableAdam:
     # ---- row-list primitives (also used by the row-sharded step)
     def catchup_rows(self, kind, row_ids, count_dev, kind_index, max_n, st):
         """Bring the listed unique rows of `kind` current through step self.t."""
+        if self.clock is not None:
+            if max_n > 0:
+                self._ensure(self.t + 1)
+                _lib.call("ncf_adam_rows_catchup_clock", *self._ptrs(kind),
+                          self.engine.model.mlp_embedding_dim, ptr(row_ids), ptr(count_dev),
+                          kind_index, max_n, ptr(self.stamp[kind]), 0, ptr(self.clock),
+                          ptr(self._table), *self._consts(), st)
+            return
         if self.t == 0 or max_n <= 0:
             return
         self._ensure(self.t)
@@ -96,6 +107,12 @@ class DeferredTableAdam:
         if max_n <= 0:
             return
         p0, m0, v0, p1, m1, v1 = self._ptrs(kind)
+        if self.clock is not None:
+            _lib.call("ncf_adam_rows_apply_clock", p0, m0, v0, ptr(g_mf), p1, m1, v1, ptr(g_mlp),
+                      self.engine.model.mlp_embedding_dim, ptr(row_ids), ptr(count_dev),
+                      kind_index, max_n, ptr(self.stamp[kind]), 1, ptr(self.clock),
+                      ptr(self._table), *self._consts(), st)
+            return
         _lib.call("ncf_adam_rows_apply", p0, m0, v0, ptr(g_mf), p1, m1, v1, ptr(g_mlp),
                   self.engine.model.mlp_embedding_dim, ptr(row_ids), ptr(count_dev), kind_index,
                   max_n, ptr(self.stamp[kind]), step, ptr(self._table), *self._consts(), st)
@@ -106,7 +123,14 @@ class DeferredTableAdam:
         than sweep_every steps behind and the catch-up work is spread evenly over the steps."""
         self.t += 1
         self.engine.pending = None
-        if self.sweep_every:
+        if self.sweep_every and self.clock is not None:
+            for kind in ("user", "item"):
+                rows = self.stamp[kind].numel()
+                sl = (rows + self.sweep_every - 1) // self.sweep_every
+                _lib.call("ncf_adam_sweep_rolling", *self._ptrs(kind), rows, sl, self.sweep_every,
+                          self.engine.model.mlp_embedding_dim, ptr(self.stamp[kind]), 1,
+                          ptr(self.clock), ptr(self._table), *self._consts(), st)
+        elif self.sweep_every:
             k = self.t % self.sweep_every
             for kind in ("user", "item"):
                 rows = self.stamp[kind].numel()

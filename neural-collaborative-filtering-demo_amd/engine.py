@@ -13,6 +13,7 @@ Data layout in HBM (fp32 throughout — the reference computes in fp32):
 """
 import ctypes
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -81,7 +82,7 @@ class Workspace:
         self.red_list = _lib.ReduceList()
         self.red_scratch = e(1)
         self.wgrads = []            # weight gradients collected during a backward (grouped launch)
-        self.wg_ws = e(1)
+        self.wg_ws = []             # partials of the grouped launches in flight (one per slot)
         self.emb_ws = torch.empty(_lib.query("ncf_embedding_bwd_workspace", n, D),
                                   dtype=torch.uint8, device=device)
         self.G = {k: e(n, D) for k in ("mf_user", "mlp_user", "mf_item", "mlp_item")}
@@ -93,11 +94,12 @@ class Workspace:
     def splits_for(m_out: int, k_out: int, rows: int) -> int:
         """Row slabs of a weight-gradient product: ~160 batch rows per wave (a few waves per SIMD
         over the grouped launch of a step), at most 256 slabs."""
-        return max(1, min(256, math.ceil(max(rows, 1) / 160)))
+        return max(1, min(256, math.ceil(max(rows, 1) / int(os.environ.get("NCF_WGRAD_ROWS", "160")))))
 
-    def run_wgrads(self, st):
-        """Every weight gradient collected by this backward in one grouped launch; the slab
-        reductions join the deferred list."""
+    def run_wgrads(self, st, slot: int = 0):
+        """The weight gradients queued since the last call, as one grouped launch on stream
+        ``st``; their slab reductions join the deferred list.  ``slot`` selects the partials
+        buffer (groups in flight at the same time need distinct ones)."""
         if not self.wgrads:
             return
         descs = (_lib.WgradDesc * len(self.wgrads))()
@@ -107,9 +109,12 @@ class Workspace:
             d.m_out, d.k_in, d.n, d.slabs, d.accumulate = m_out, k_in, n, self.splits_for(m_out, k_in, n), 0
         addr = ctypes.addressof(descs)
         need = _lib.query("ncf_wgrad_grouped_workspace", addr, len(self.wgrads))
-        if self.wg_ws.numel() < need:
-            self.wg_ws = torch.empty(need, dtype=torch.float32, device=self.red_ws.device)
-        _lib.call("ncf_wgrad_grouped", addr, len(self.wgrads), ptr(self.wg_ws), self.wg_ws.numel(),
+        while len(self.wg_ws) <= slot:
+            self.wg_ws.append(torch.empty(1, dtype=torch.float32, device=self.red_ws.device))
+        if self.wg_ws[slot].numel() < need:
+            self.wg_ws[slot] = torch.empty(need, dtype=torch.float32, device=self.red_ws.device)
+        ws = self.wg_ws[slot]
+        _lib.call("ncf_wgrad_grouped", addr, len(self.wgrads), ptr(ws), ws.numel(),
                   self.red_list.address, st)
         self.wgrads = []
 
@@ -145,6 +150,43 @@ class NCFEngine:
         self.offsets: Dict[str, tuple] = {}
         self.timing = None        # optional {table: (start_event, end_event)} for the bench
         self.deferred = None      # DeferredTableAdam holding rows behind, if any
+        self.clock = None         # ncf_step_clock (device) of a clock-driven / captured step
+        self.concurrent = False   # fork independent work onto side streams (graph mode)
+        self._side = None         # side streams (fork / join)
+        self._events = None
+        self._ev_i = 0
+
+    # ------------------------------------------------------------------ side streams
+    # The step is a chain of latency-bound kernels that each fill a fraction of the GPU; work
+    # that is independent of the chain (weight gradients, the q/k projections, the second id
+    # kind) is forked onto side streams that start after everything queued so far on the
+    # current stream and are joined back before their results are read.  Same kernels, same
+    # inputs: results are bit-identical to the serial order.
+    def fork(self, dev, k: int = 1):
+        if not self.concurrent:   # serial: "side streams" are the current stream itself
+            return [torch.cuda.current_stream(dev)] * k
+        if self._side is None or self._side[0].device != dev:
+            self._side = [torch.cuda.Stream(dev) for _ in range(2)]
+            self._events = [torch.cuda.Event() for _ in range(16)]
+        cur = torch.cuda.current_stream(dev)
+        ev = self._next_event()
+        ev.record(cur)
+        for sd in self._side[:k]:
+            sd.wait_event(ev)
+        return self._side[:k]
+
+    def join(self, dev, streams):
+        if not self.concurrent:
+            return
+        cur = torch.cuda.current_stream(dev)
+        for sd in streams:
+            ev = self._next_event()
+            ev.record(sd)
+            cur.wait_event(ev)
+
+    def _next_event(self):
+        self._ev_i = (self._ev_i + 1) % len(self._events)
+        return self._events[self._ev_i]
 
     # ------------------------------------------------------------------ parameter layout
     def dense_params(self):
@@ -304,15 +346,21 @@ class NCFEngine:
                   ptr(w.xu), ptr(w.xi), ptr(w.umf), ptr(w.imf), ptr(w.err), st)
         # a5: MultiHeadAttention over each group of M rows (architecture.py:315-326)
         att = m.user_product_attention
-        self._gemm(w.xi, D, 0, att.v_proj.weight, D, 1, w.v, D, n, D, D, bias=att.v_proj.bias, st=st)
         if M == 1 and not train:
             # softmax over a single key is exactly 1 -> the core returns V unchanged
+            self._gemm(w.xi, D, 0, att.v_proj.weight, D, 1, w.v, D, n, D, D, bias=att.v_proj.bias, st=st)
             src = w.v
         else:
-            self._gemm(w.xu, D, 0, att.q_proj.weight, D, 1, w.q, D, n, D, D, bias=att.q_proj.bias, st=st)
-            self._gemm(w.xi, D, 0, att.k_proj.weight, D, 1, w.k, D, n, D, D, bias=att.k_proj.bias, st=st)
+            side = self.fork(dev, 2)
+            for sd, (X, lin, Y) in zip(side, ((w.xu, att.q_proj, w.q), (w.xi, att.k_proj, w.k))):
+                with torch.cuda.stream(sd):
+                    self._gemm(X, D, 0, lin.weight, D, 1, Y, D, n, D, D, bias=lin.bias,
+                               st=_lib.stream_ptr(dev))
+            self._gemm(w.xi, D, 0, att.v_proj.weight, D, 1, w.v, D, n, D, D, bias=att.v_proj.bias,
+                       st=st)
+            self.join(dev, side)
             _lib.call("ncf_attention_fwd", ptr(w.q), ptr(w.k), ptr(w.v), n // M, M, H, D,
-                      drop_p if train else 0.0, seed, ptr(w.P), ptr(w.o), st)
+                      drop_p if train else 0.0, seed, ptr(self.clock), ptr(w.P), ptr(w.o), st)
             src = w.o
         if temporal is None:
             self._gemm(src, D, 0, att.out_proj.weight, D, 1, w.y, D, n, D, D,
@@ -336,7 +384,7 @@ class NCFEngine:
                        relu=True, st=st)
             _lib.call("ncf_relu_ln_dropout_fwd", ptr(w.r[l]), n, h, ptr(ln.weight), ptr(ln.bias),
                       LN_EPS, drop_p if train else 0.0, (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1),
-                      ptr(w.a[l]), ptr(w.mean[l]), ptr(w.rstd[l]), st)
+                      ptr(self.clock), ptr(w.a[l]), ptr(w.mean[l]), ptr(w.rstd[l]), st)
             x, ldx, kin = w.a[l], h, h
         # a8: mlp_output + final Linear(2,1) + Sigmoid (architecture.py:345, 353-354)
         _lib.call("ncf_head_fwd", ptr(x), n, hid[-1], ptr(m.mlp_output.weight),
@@ -364,6 +412,7 @@ class NCFEngine:
         gv = self.grad_view
         w.red_list.count = 0
         w.wgrads = []
+        joins = []   # side streams to join before the deferred reductions
         # a12 + a8 backward (trainer.py:271; architecture.py:245-252)
         gp = None if grad_prob is None else grad_prob.reshape(-1).to(torch.float32).contiguous()
         tg = None if targets is None else targets.reshape(-1).to(device=dev, dtype=torch.float32).contiguous()
@@ -381,7 +430,7 @@ class NCFEngine:
             lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
             _lib.call("ncf_relu_ln_dropout_bwd", ptr(w.da[l]), ptr(w.r[l]), ptr(w.mean[l]),
                       ptr(w.rstd[l]), ptr(ln.weight), n, h, drop_p,
-                      (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1), ptr(w.dlin[l]),
+                      (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1), ptr(self.clock), ptr(w.dlin[l]),
                       ptr(gv(f"mlp.{4 * l + 2}.weight")), ptr(gv(f"mlp.{4 * l + 2}.bias")),
                       ptr(gv(f"mlp.{4 * l}.bias")), ptr(w.site(f"relu{l}")),
                       w.site(f"relu{l}").numel(), w.red_list.address, st)
@@ -391,6 +440,10 @@ class NCFEngine:
             self._wgrad(w, w.dlin[l], h, xin, kin, dW, ldw, h, kin, n)
             if ldw > kin:  # zero temporal columns of mlp.0 (their input is all-zero)
                 _lib.call("ncf_fill_2d", ptr(dW[:, kin:]), h, ldw - kin, ldw, 0.0, st)
+            if l == 0:   # every MLP weight gradient is ready: one grouped launch on a side stream
+                joins.extend(self.fork(dev, 1))
+                with torch.cuda.stream(joins[-1]):
+                    w.run_wgrads(_lib.stream_ptr(dev), slot=0)
             dx = w.dy if l == 0 else w.da[l - 1]
             self._gemm(w.dlin[l], h, 0, lin.weight, ldw, 0, dx, kin, n, kin, h, st=st)
         # a5 backward: out_proj, core, q/k/v projections
@@ -400,13 +453,21 @@ class NCFEngine:
                     dbias=gv("user_product_attention.out_proj.bias"))
         self._gemm(w.dy, D, 0, att.out_proj.weight, D, 0, w.do, D, n, D, D, st=st)
         _lib.call("ncf_attention_bwd", ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P), ptr(w.do), n // M, M,
-                  H, D, drop_p, seed, ptr(w.dS), ptr(w.dq), ptr(w.dk), ptr(w.dv), st)
+                  H, D, drop_p, seed, ptr(self.clock), ptr(w.dS), ptr(w.dq), ptr(w.dk), ptr(w.dv), st)
         for nm, dX, X in (("q_proj", w.dq, w.xu), ("k_proj", w.dk, w.xi), ("v_proj", w.dv, w.xi)):
             self._wgrad(w, dX, D, X, D, gv(f"user_product_attention.{nm}.weight"), D, D, D, n,
                         dbias=gv(f"user_product_attention.{nm}.bias"))
-        self._gemm(w.dq, D, 0, att.q_proj.weight, D, 0, w.dxu, D, n, D, D, st=st)
+        # attention weight gradients and dxu on side streams, dxi on this one
+        side = self.fork(dev, 2)
+        with torch.cuda.stream(side[0]):
+            w.run_wgrads(_lib.stream_ptr(dev), slot=1)
+        with torch.cuda.stream(side[1]):
+            self._gemm(w.dq, D, 0, att.q_proj.weight, D, 0, w.dxu, D, n, D, D,
+                       st=_lib.stream_ptr(dev))
         self._gemm(w.dk, D, 0, att.k_proj.weight, D, 0, w.dxi, D, n, D, D, st=st)
         self._gemm(w.dv, D, 0, att.v_proj.weight, D, 0, w.dxi, D, n, D, D, accum=True, st=st)
+        self.join(dev, side[1:])
+        joins.append(side[0])
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)
         tb = tables or self.table_params()
         G = w.G
@@ -424,7 +485,7 @@ class NCFEngine:
                   ptr(uq_i), ptr(gv("mf_norm.weight")), ptr(gv("mf_norm.bias")),
                   ptr(gv("mlp_norm.weight")), ptr(gv("mlp_norm.bias")), ptr(w.emb_ws),
                   w.emb_ws.numel(), w.red_list.address, st)
-        w.run_wgrads(st)
+        self.join(dev, joins)
         w.run_reductions(st)
         self.pending = w
 

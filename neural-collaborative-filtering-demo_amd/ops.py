@@ -43,7 +43,7 @@ class _MHAFunction(torch.autograd.Function):
         _gemm(xq, D, 0, wq, D, 1, q, D, n, D, D, bq)
         _gemm(xk, D, 0, wk, D, 1, k, D, n, D, D, bk)
         _gemm(xv, D, 0, wv, D, 1, v, D, n, D, D, bv)
-        _lib.call("ncf_attention_fwd", ptr(q), ptr(k), ptr(v), Bn, L, H, D, drop_p, seed, ptr(P),
+        _lib.call("ncf_attention_fwd", ptr(q), ptr(k), ptr(v), Bn, L, H, D, drop_p, seed, None, ptr(P),
                   ptr(o), _lib.stream_ptr(dev))
         _gemm(o, D, 0, wo, D, 1, y, D, n, D, D, bo)
         ctx.save_for_backward(xq, xk, xv, q, k, v, P, o, wq, wk, wv, wo)
@@ -65,7 +65,7 @@ class _MHAFunction(torch.autograd.Function):
         dS = torch.empty(Bn * H * L * L, device=dev)
         dq, dk, dv = (torch.empty(n, D, device=dev) for _ in range(3))
         _lib.call("ncf_attention_bwd", ptr(q), ptr(k), ptr(v), ptr(P), ptr(do), Bn, L, H, D,
-                  drop_p, seed, ptr(dS), ptr(dq), ptr(dk), ptr(dv), _lib.stream_ptr(dev))
+                  drop_p, seed, None, ptr(dS), ptr(dq), ptr(dk), ptr(dv), _lib.stream_ptr(dev))
         outs = []
         for dX, X, W, wn, bn in ((dq, xq, wq, "wq", "bq"), (dk, xk, wk, "wk", "bk"),
                                  (dv, xv, wv, "wv", "bv")):
@@ -163,7 +163,7 @@ def category_hierarchy_forward(mod, department_ids, category_ids):
     out = torch.empty(n * n, D, device=dev)
     mean, rstd = torch.empty(n * n, device=dev), torch.empty(n * n, device=dev)
     _lib.call("ncf_relu_ln_dropout_fwd", ptr(h), n * n, D, ptr(mod.norm.weight), ptr(mod.norm.bias),
-              LN_EPS, 0.0, 0, ptr(out), ptr(mean), ptr(rstd), _lib.stream_ptr(dev))
+              LN_EPS, 0.0, 0, None, ptr(out), ptr(mean), ptr(rstd), _lib.stream_ptr(dev))
     return out.view(n, n, D)
 
 

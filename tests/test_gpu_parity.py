@@ -443,11 +443,13 @@ def test_non_adam_optimizer_gets_dense_table_grads(f2):
 
 
 # ----------------------------------------------------------------------------- deferred Adam
-def _fused_run(deferred, steps, sweep_every=64, U=3000, I=500, B=64, seed=11):
+def _fused_run(deferred, steps, sweep_every=64, U=3000, I=500, B=64, seed=11, dropout=0.0,
+               **kw):
     from ncf_amd.trainer import FusedTrainStep
     torch.manual_seed(seed)
-    m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.0, 4).to(DEV)
-    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5, deferred=deferred, sweep_every=sweep_every)
+    m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, dropout, 4).to(DEV)
+    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5, deferred=deferred, sweep_every=sweep_every,
+                          **kw)
     g = torch.Generator().manual_seed(seed + 1)
     for s in range(steps):
         u = torch.randint(0, U, (B,), generator=g).repeat_interleave(5).to(DEV)
@@ -467,6 +469,29 @@ def test_deferred_adam_bitwise_equals_dense(sweep_every):
     periodic sweep at 64; sweep_every=0 exercises long catch-up chains only)."""
     a_sd, a_m = _fused_run(False, 70)
     b_sd, b_m = _fused_run(True, 70, sweep_every=sweep_every)
+    for k in a_sd:
+        assert torch.equal(a_sd[k], b_sd[k]), k
+    for k in a_m:
+        assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
+
+
+def test_clock_mode_bitwise_equals_dense():
+    """The step-clock form of the deferred schedule (every step value read on the device) is
+    still bit-identical to the dense sweep."""
+    a_sd, a_m = _fused_run(False, 70)
+    b_sd, b_m = _fused_run(True, 70, clock=True)
+    for k in a_sd:
+        assert torch.equal(a_sd[k], b_sd[k]), k
+    for k in a_m:
+        assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
+
+
+def test_graph_replay_bitwise_equals_eager_clock():
+    """hipGraph capture + replay of the whole training step (dropout on: the per-step stream
+    comes from the device clock) == the same clock-driven steps run eagerly, bit for bit, across
+    a rolling-sweep wrap (70 steps)."""
+    a_sd, a_m = _fused_run(True, 70, dropout=0.2, clock=True)
+    b_sd, b_m = _fused_run(True, 70, dropout=0.2, graph=True)
     for k in a_sd:
         assert torch.equal(a_sd[k], b_sd[k]), k
     for k in a_m:
