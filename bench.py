@@ -161,6 +161,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--infer-pairs", type=int, default=65536)
     ap.add_argument("--no-score", action="store_true", help="skip the C5 scoring measurement")
+    ap.add_argument("--no-clock", action="store_true",
+                    help="host-driven Adam step arguments instead of the device step clock")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as a captured hipGraph (measured ~3%% slower than host "
                          "launches on MI355X: the host enqueue is already below the GPU time)")
@@ -199,7 +201,8 @@ def main():
         if rank == 0 and not args.no_cpu_baseline:
             init_sd = {k: v.clone() for k, v in model.state_dict().items()}
         model = model.to(dev).train()
-        step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, graph=args.graph)
+        step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, graph=args.graph,
+                              clock=False if args.no_clock else None)
     batches = make_batches(U, I, B, M, 8, dev, seed=100 + rank)
     torch.cuda.synchronize()
 

@@ -359,6 +359,30 @@ int ncf_adam_sweep_rolling(float* p0, float* m0, float* v0, float* p1, float* m1
                            int32_t* stamp, int32_t step_rel, const ncf_step_clock* clock,
                            const float* step_table, double beta1, double beta2, double eps,
                            double weight_decay, void* stream);
+/* Both id kinds in one launch each (blockIdx.y = kind): pairs[k] holds kind k's GMF + MLP
+ * tables (sharing the row index), their moments, compact gradients (apply), the step's unique
+ * rows and the stamps; count[k] = unique rows of kind k (ncf_dedup_ids).                      */
+typedef struct ncf_table_pair {
+  float *p0, *m0, *v0, *p1, *m1, *v1;
+  const float *g0, *g1;
+  const int64_t* row_ids;
+  int32_t* stamp;
+  int64_t rows;
+} ncf_table_pair;
+int ncf_adam_pairs_catchup_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
+                                 const uint32_t* count, int64_t max_n, int32_t target_rel,
+                                 const ncf_step_clock* clock, const float* step_table,
+                                 double beta1, double beta2, double eps, double weight_decay,
+                                 void* stream);
+int ncf_adam_pairs_apply_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
+                               const uint32_t* count, int64_t max_n, int32_t step_rel,
+                               const ncf_step_clock* clock, const float* step_table, double beta1,
+                               double beta2, double eps, double weight_decay, void* stream);
+int ncf_adam_pairs_sweep_rolling(const ncf_table_pair* pairs, int npairs, int64_t dim,
+                                 int32_t sweep_every, int32_t step_rel,
+                                 const ncf_step_clock* clock, const float* step_table,
+                                 double beta1, double beta2, double eps, double weight_decay,
+                                 void* stream);
 int ncf_adam_flat_clock(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                         int64_t n, const float* step_table, int32_t step_rel,
                         const ncf_step_clock* clock, double beta1, double beta2, double eps,

@@ -92,6 +92,9 @@ SIGNATURES = {
                                         F64, F64, F64, F64, P]),
     "ncf_adam_sweep_rolling": (I32, [P, P, P, P, P, P, I64, I64, I32, I64, P, I32, P, P, F64, F64,
                                      F64, F64, P]),
+    "ncf_adam_pairs_catchup_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
+    "ncf_adam_pairs_apply_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
+    "ncf_adam_pairs_sweep_rolling": (I32, [P, I32, I64, I32, I32, P, P, F64, F64, F64, F64, P]),
     "ncf_adam_flat_clock": (I32, [P, P, P, P, I64, P, I32, P, F64, F64, F64, F64, P]),
     "ncf_score_queries": (I32, [P, I64, P, I64, I64, P, P, F32, P, P, P, P, P]),
     "ncf_score_item_bias": (I32, [P, I64, P, P, P, P, P]),
@@ -122,6 +125,12 @@ class WgradDesc(ctypes.Structure):
 
 
 WGRAD_GROUP_MAX = 8
+
+
+class TablePair(ctypes.Structure):
+    """ncf_table_pair (include/ncf_hip.h)."""
+    _fields_ = [("p0", P), ("m0", P), ("v0", P), ("p1", P), ("m1", P), ("v1", P), ("g0", P),
+                ("g1", P), ("row_ids", P), ("stamp", P), ("rows", I64)]
 
 
 class ReduceList(ctypes.Structure):

@@ -247,6 +247,85 @@ __global__ __launch_bounds__(256) void k_adam_flat_clock(float* __restrict__ p,
   }
 }
 
+// ---- both id kinds per launch (blockIdx.y = kind)
+struct PairArgs {
+  TablePtrs t[2];
+  const int64_t* ids[2];
+  int32_t* stamp[2];
+  int64_t rows[2];
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void k_pairs_catchup(const PairArgs a, const uint32_t* __restrict__ count,
+                                                       int64_t max_n, int32_t target_rel,
+                                                       const ncf_step_clock* __restrict__ clock,
+                                                       const float* __restrict__ table,
+                                                       AdamScalars s) {
+  constexpr int L = D / 4;
+  const int k = blockIdx.y;
+  const int64_t tt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = tt / L;
+  const int sub = (int)(tt % L);
+  if (c >= max_n || c >= (int64_t)count[k]) return;
+  const int32_t target = clock->t + target_rel;
+  const int64_t row = a.ids[k][c];
+  int32_t* stamp = a.stamp[k];
+  const int32_t from = stamp[row];
+  catch_up_row<D>(a.t[k], row, sub * 4, from, target, table, s);
+  if (sub == 0 && from < target) stamp[row] = target;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_pairs_apply(const PairArgs a, const uint32_t* __restrict__ count,
+                                                     int64_t max_n, int32_t step_rel,
+                                                     const ncf_step_clock* __restrict__ clock,
+                                                     const float* __restrict__ table, AdamScalars s) {
+  constexpr int L = D / 4;
+  const int k = blockIdx.y;
+  const int64_t tt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = tt / L;
+  const int sub = (int)(tt % L);
+  if (c >= max_n || c >= (int64_t)count[k]) return;
+  const int32_t step = clock->t + step_rel;
+  const TablePtrs& t = a.t[k];
+  const int64_t row = a.ids[k][c];
+  const int64_t o = row * D + sub * 4;
+  const float ns = table[2 * step], bc = table[2 * step + 1];
+  float4 p0 = ld4(t.p0 + o), m0 = ld4(t.m0 + o), v0 = ld4(t.v0 + o);
+  adam4(p0, m0, v0, ld4(t.G0 + c * D + sub * 4), ns, bc, s);
+  st4(t.p0 + o, p0); st4(t.m0 + o, m0); st4(t.v0 + o, v0);
+  if (t.p1) {
+    float4 p1 = ld4(t.p1 + o), m1 = ld4(t.m1 + o), v1 = ld4(t.v1 + o);
+    adam4(p1, m1, v1, ld4(t.G1 + c * D + sub * 4), ns, bc, s);
+    st4(t.p1 + o, p1); st4(t.m1 + o, m1); st4(t.v1 + o, v1);
+  }
+  if (sub == 0) a.stamp[k][row] = step;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_pairs_sweep(const PairArgs a, int32_t every,
+                                                     int32_t step_rel,
+                                                     const ncf_step_clock* __restrict__ clock,
+                                                     const float* __restrict__ table, AdamScalars s) {
+  constexpr int L = D / 4;
+  const int k = blockIdx.y;
+  const int32_t target = clock->t + step_rel;
+  const int64_t total = a.rows[k];
+  const int64_t slice = (total + every - 1) / every;
+  const int64_t row0 = (int64_t)(target % every) * slice;
+  const int64_t rows = max((int64_t)0, min(slice, total - row0));
+  const int64_t n = rows * L;
+  int32_t* stamp = a.stamp[k];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = row0 + e / L;
+    const int sub = (int)(e % L);
+    const int32_t from = stamp[row];
+    catch_up_row<D>(a.t[k], row, sub * 4, from, target, table, s);
+    if (sub == 0 && from < target) stamp[row] = target;
+  }
+}
+
 __global__ void k_clock_advance(ncf_step_clock* clock, uint64_t base_seed) {
   const int32_t t = clock->t + 1;
   clock->t = t;
@@ -381,6 +460,48 @@ int rolling_d(TablePtrs t, int64_t total, int64_t slice, int32_t every, int32_t*
   return NCF_OK;
 }
 
+PairArgs pair_args(const ncf_table_pair* p, int n) {
+  PairArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int k = 0; k < n && k < 2; ++k) {
+    a.t[k] = TablePtrs{p[k].p0, p[k].m0, p[k].v0, p[k].p1, p[k].m1, p[k].v1, p[k].g0, p[k].g1};
+    a.ids[k] = p[k].row_ids;
+    a.stamp[k] = p[k].stamp;
+    a.rows[k] = p[k].rows;
+  }
+  return a;
+}
+
+template <int D>
+int pairs_catchup_d(PairArgs a, int n, const uint32_t* count, int64_t max_n, int32_t rel,
+                    const ncf_step_clock* clock, const float* table, AdamScalars s,
+                    hipStream_t st) {
+  hipLaunchKernelGGL(k_pairs_catchup<D>, dim3(ncf_cdiv(max_n * (D / 4), 256), n), dim3(256), 0, st,
+                     a, count, max_n, rel, clock, table, s);
+  NCF_CHECK_LAUNCH("ncf_adam_pairs_catchup_clock");
+  return NCF_OK;
+}
+
+template <int D>
+int pairs_apply_d(PairArgs a, int n, const uint32_t* count, int64_t max_n, int32_t rel,
+                  const ncf_step_clock* clock, const float* table, AdamScalars s, hipStream_t st) {
+  hipLaunchKernelGGL(k_pairs_apply<D>, dim3(ncf_cdiv(max_n * (D / 4), 256), n), dim3(256), 0, st,
+                     a, count, max_n, rel, clock, table, s);
+  NCF_CHECK_LAUNCH("ncf_adam_pairs_apply_clock");
+  return NCF_OK;
+}
+
+template <int D>
+int pairs_sweep_d(PairArgs a, int n, int32_t every, int32_t rel, const ncf_step_clock* clock,
+                  const float* table, AdamScalars s, hipStream_t st) {
+  int64_t slice = 0;
+  for (int k = 0; k < n; ++k) slice = max(slice, (a.rows[k] + every - 1) / every);
+  hipLaunchKernelGGL(k_pairs_sweep<D>, dim3(grid_for(slice * (D / 4)), n), dim3(256), 0, st, a,
+                     every, rel, clock, table, s);
+  NCF_CHECK_LAUNCH("ncf_adam_pairs_sweep_rolling");
+  return NCF_OK;
+}
+
 template <int D>
 int sweep_d(TablePtrs t, int64_t row0, int64_t rows, int32_t* stamp, int32_t target,
             const float* table, AdamScalars s, hipStream_t st) {
@@ -511,4 +632,44 @@ extern "C" int ncf_adam_flat_clock(float* param, const float* grad, float* exp_a
                      consts_of(beta1, beta2, eps, weight_decay));
   NCF_CHECK_LAUNCH("ncf_adam_flat_clock");
   return NCF_OK;
+}
+
+extern "C" int ncf_adam_pairs_catchup_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
+                                            const uint32_t* count, int64_t max_n,
+                                            int32_t target_rel, const ncf_step_clock* clock,
+                                            const float* step_table, double beta1, double beta2,
+                                            double eps, double weight_decay, void* stream) {
+  NCF_CHECK_ARG(pairs && npairs >= 1 && npairs <= 2 && count && clock && step_table,
+                "ncf_adam_pairs_catchup_clock: bad args");
+  if (max_n <= 0) return NCF_OK;
+  NCF_DISPATCH_DIM(dim, pairs_catchup_d, pair_args(pairs, npairs), npairs, count, max_n,
+                   target_rel, clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
+                   (hipStream_t)stream);
+}
+
+extern "C" int ncf_adam_pairs_apply_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
+                                          const uint32_t* count, int64_t max_n, int32_t step_rel,
+                                          const ncf_step_clock* clock, const float* step_table,
+                                          double beta1, double beta2, double eps,
+                                          double weight_decay, void* stream) {
+  NCF_CHECK_ARG(pairs && npairs >= 1 && npairs <= 2 && count && clock && step_table,
+                "ncf_adam_pairs_apply_clock: bad args");
+  for (int k = 0; k < npairs; ++k)
+    NCF_CHECK_ARG(pairs[k].g0 && (!pairs[k].p1 || pairs[k].g1), "ncf_adam_pairs_apply_clock: gradients");
+  if (max_n <= 0) return NCF_OK;
+  NCF_DISPATCH_DIM(dim, pairs_apply_d, pair_args(pairs, npairs), npairs, count, max_n, step_rel,
+                   clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
+                   (hipStream_t)stream);
+}
+
+extern "C" int ncf_adam_pairs_sweep_rolling(const ncf_table_pair* pairs, int npairs, int64_t dim,
+                                            int32_t sweep_every, int32_t step_rel,
+                                            const ncf_step_clock* clock, const float* step_table,
+                                            double beta1, double beta2, double eps,
+                                            double weight_decay, void* stream) {
+  NCF_CHECK_ARG(pairs && npairs >= 1 && npairs <= 2 && clock && step_table && sweep_every >= 1,
+                "ncf_adam_pairs_sweep_rolling: bad args");
+  NCF_DISPATCH_DIM(dim, pairs_sweep_d, pair_args(pairs, npairs), npairs, sweep_every, step_rel,
+                   clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
+                   (hipStream_t)stream);
 }

@@ -18,6 +18,8 @@ Every replayed step uses the per-step fp32 scalars of the dense kernel and the s
 contraction-free arithmetic, so the result is bit-identical to the dense sweep (tested); the
 work moves from HBM traffic (24 B/element/step) to VALU (~15 flops/element/step, amortised).
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -124,12 +126,10 @@ class DeferredTableAdam:
         self.t += 1
         self.engine.pending = None
         if self.sweep_every and self.clock is not None:
-            for kind in ("user", "item"):
-                rows = self.stamp[kind].numel()
-                sl = (rows + self.sweep_every - 1) // self.sweep_every
-                _lib.call("ncf_adam_sweep_rolling", *self._ptrs(kind), rows, sl, self.sweep_every,
-                          self.engine.model.mlp_embedding_dim, ptr(self.stamp[kind]), 1,
-                          ptr(self.clock), ptr(self._table), *self._consts(), st)
+            pairs = self._pairs()
+            _lib.call("ncf_adam_pairs_sweep_rolling", ctypes.addressof(pairs), 2,
+                      self.engine.model.mlp_embedding_dim, self.sweep_every, 1, ptr(self.clock),
+                      ptr(self._table), *self._consts(), st)
         elif self.sweep_every:
             k = self.t % self.sweep_every
             for kind in ("user", "item"):
@@ -137,6 +137,19 @@ class DeferredTableAdam:
                 sl = (rows + self.sweep_every - 1) // self.sweep_every
                 r0 = k * sl
                 self._sweep_range(kind, r0, max(0, min(rows, r0 + sl) - r0), st)
+
+    def _pairs(self, w=None):
+        """ncf_table_pair[2] (users, items) for the both-kinds launches of the clock path."""
+        pairs = (_lib.TablePair * 2)()
+        for k, (kind, a, b) in enumerate(_KINDS):
+            p0, m0, v0, p1, m1, v1 = self._ptrs(kind)
+            pr = pairs[k]
+            pr.p0, pr.m0, pr.v0, pr.p1, pr.m1, pr.v1 = p0, m0, v0, p1, m1, v1
+            pr.stamp, pr.rows = ptr(self.stamp[kind]), self.stamp[kind].numel()
+            if w is not None:
+                pr.row_ids = ptr(w.uniq_u if k == 0 else w.uniq_i)
+                pr.g0, pr.g1 = ptr(w.G[a]), ptr(w.G[b])
+        return pairs
 
     # ---- engine hook: before the gathers of a training step
     def prepare(self, w, uid, iid, st):
@@ -147,12 +160,28 @@ class DeferredTableAdam:
                   ptr(w.uniq_u), ptr(w.uniq_i), None, None, ptr(w.num_unique), ptr(w.emb_ws),
                   w.emb_ws.numel(), st)
         w.deduped = True
+        if self.clock is not None and n > 0:   # both kinds in one launch
+            self._ensure(self.t + 1)
+            pairs = self._pairs(w)
+            _lib.call("ncf_adam_pairs_catchup_clock", ctypes.addressof(pairs), 2,
+                      m.mlp_embedding_dim, ptr(w.num_unique), n, 0, ptr(self.clock),
+                      ptr(self._table), *self._consts(), st)
+            return
         self.catchup_rows("user", w.uniq_u, w.num_unique, 0, n, st)
         self.catchup_rows("item", w.uniq_i, w.num_unique, 1, n, st)
 
     # ---- after the backward: this step's gradient on the touched rows
     def apply(self, w, st):
         n = w.g.n
+        if self.clock is not None:
+            self._ensure(self.t + 1)
+            if n > 0:
+                pairs = self._pairs(w)
+                _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2,
+                          self.engine.model.mlp_embedding_dim, ptr(w.num_unique), n, 1,
+                          ptr(self.clock), ptr(self._table), *self._consts(), st)
+            self.advance(st)
+            return
         self.apply_rows("user", w.uniq_u, w.num_unique, 0, n, w.G["mf_user"], w.G["mlp_user"], st)
         self.apply_rows("item", w.uniq_i, w.num_unique, 1, n, w.G["mf_item"], w.G["mlp_item"], st)
         self.advance(st)

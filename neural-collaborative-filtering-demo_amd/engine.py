@@ -151,6 +151,7 @@ class NCFEngine:
         self.timing = None        # optional {table: (start_event, end_event)} for the bench
         self.deferred = None      # DeferredTableAdam holding rows behind, if any
         self.clock = None         # ncf_step_clock (device) of a clock-driven / captured step
+        self._zero_cols_of = None  # flat_grad whose never-written mlp.0 temporal columns are 0
         self.concurrent = False   # fork independent work onto side streams (graph mode)
         self._side = None         # side streams (fork / join)
         self._events = None
@@ -438,8 +439,11 @@ class NCFEngine:
             ldw = lin.weight.shape[1]
             dW = gv(f"mlp.{4 * l}.weight")
             self._wgrad(w, w.dlin[l], h, xin, kin, dW, ldw, h, kin, n)
-            if ldw > kin:  # zero temporal columns of mlp.0 (their input is all-zero)
+            if ldw > kin and self._zero_cols_of is not self.flat_grad:
+                # gradient columns of mlp.0 that see the all-zero temporal input: exactly 0, and
+                # no kernel ever writes them — zero once per gradient buffer
                 _lib.call("ncf_fill_2d", ptr(dW[:, kin:]), h, ldw - kin, ldw, 0.0, st)
+                self._zero_cols_of = self.flat_grad
             if l == 0:   # every MLP weight gradient is ready: one grouped launch on a side stream
                 joins.extend(self.fork(dev, 1))
                 with torch.cuda.stream(joins[-1]):

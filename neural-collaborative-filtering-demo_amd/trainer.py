@@ -54,7 +54,9 @@ class FusedTrainStep:
         self.v_flat = torch.zeros_like(eng.flat)
         self.last_loss = None
         self.graph = bool(graph)
-        self.use_clock = self.graph if clock is None else bool(clock)
+        # the device step clock is the default whenever the deferred schedule is on (both kinds
+        # per launch, no host step arguments; bit-identical to the host-driven form)
+        self.use_clock = (self.graph or deferred) if clock is None else bool(clock)
         if self.graph and not self.use_clock:
             raise ValueError("graph capture needs the step clock")
         self.clock = None
