@@ -265,7 +265,10 @@ def main():
                                                 "ncf_adam_sweep", "ncf_adam_table",
                                                 "ncf_adam_rows_catchup_clock",
                                                 "ncf_adam_rows_apply_clock",
-                                                "ncf_adam_sweep_rolling"))
+                                                "ncf_adam_sweep_rolling",
+                                                "ncf_adam_pairs_catchup_clock",
+                                                "ncf_adam_pairs_apply_clock",
+                                                "ncf_adam_pairs_sweep_rolling"))
     tab_bytes = 2 * (U + I) * D * 24.0
     # --- inference pairs/s: eval forward (M = 1) on resident pairs
     model.eval()

@@ -27,8 +27,8 @@ constexpr int kUnroll = 8;  // MFMA steps (16 rows) per pipeline stage
 
 struct GroupArgs {
   ncf_wgrad_desc d[kMaxG];
-  float* part[kMaxG];       // [slabs][m_out][k_in] slab partials
-  float* bpart[kMaxG];      // [slabs][m_out] bias partials (or null)
+  float* part[kMaxG];       // slab s at part + s*stride: [m_out][k_in] weight, then [m_out] bias
+  int64_t stride[kMaxG];
   uint32_t first[kMaxG + 1];
   int32_t tiles_j[kMaxG];   // 64-wide tiles along k_in
   int32_t tiles[kMaxG];     // tiles per slab
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(const GroupArgs a) {
     for (int u = 0; u < kUnroll; ++u) { a0[u] = n0[u]; a1[u] = n1[u]; b0[u] = m0[u]; b1[u] = m1[u]; }
   }
   // slab partial [m_out][k_in]: C row (m index) = (r&3) + 8(r>>2) + 4h, column (k_in index) = i
-  float* P = a.part[g] + (int64_t)slab * d.m_out * d.k_in;
+  float* P = a.part[g] + (int64_t)slab * a.stride[g];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int m = ti * 64 + (q & 3) + 8 * (q >> 2) + 4 * h;
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(const GroupArgs a) {
   if (want_bias) {
     rs0 += __shfl_xor(rs0, 32, 64);
     rs1 += __shfl_xor(rs1, 32, 64);
-    float* BP = a.bpart[g] + (int64_t)slab * d.m_out;
+    float* BP = a.part[g] + (int64_t)slab * a.stride[g] + (int64_t)d.m_out * d.k_in;
     if (h == 0) {
       if (va0) BP[ia0] = rs0;
       if (va1) BP[ia1] = rs1;
@@ -147,9 +147,9 @@ extern "C" int64_t ncf_wgrad_grouped_workspace(const ncf_wgrad_desc* descs, int 
   for (int g = 0; g < count; ++g) {
     const int64_t s = slabs_used(descs[g]);
     const int64_t mn = (int64_t)descs[g].m_out * descs[g].k_in;
-    f += s * mn + (descs[g].dbias ? s * descs[g].m_out : 0);
+    f += s * (mn + (descs[g].dbias ? descs[g].m_out : 0));
     f = (f + 3) / 4 * 4;
-    scratch += ncf_reduce_scratch((int)s, mn) + ncf_reduce_scratch((int)s, descs[g].m_out);
+    scratch += ncf_reduce_scratch((int)s, mn + descs[g].m_out) + ncf_reduce_scratch((int)s, descs[g].m_out);
   }
   return f + scratch;
 }
@@ -176,9 +176,8 @@ extern "C" int ncf_wgrad_grouped(const ncf_wgrad_desc* descs, int count, float* 
     const int64_t s = slabs_used(d);
     a.d[g] = d;
     a.part[g] = workspace + off;
-    off += s * d.m_out * d.k_in;
-    a.bpart[g] = d.dbias ? workspace + off : nullptr;
-    if (d.dbias) off += s * d.m_out;
+    a.stride[g] = (int64_t)d.m_out * d.k_in + (d.dbias ? d.m_out : 0);
+    off += s * a.stride[g];
     off = (off + 3) / 4 * 4;
     a.tiles_j[g] = (int32_t)((d.k_in + 63) / 64);
     a.tiles[g] = (int32_t)(((d.m_out + 63) / 64) * a.tiles_j[g]);
@@ -200,8 +199,15 @@ extern "C" int ncf_wgrad_grouped(const ncf_wgrad_desc* descs, int count, float* 
     const ncf_wgrad_desc& d = descs[g];
     const int64_t s = slabs_used(d);
     const int64_t mn = (int64_t)d.m_out * d.k_in;
-    int rc = ncf_defer(lst, a.part[g], s, mn, mn, d.dw, d.accumulate, d.k_in, d.ldw);
-    if (!rc && d.dbias) rc = ncf_defer(lst, a.bpart[g], s, d.m_out, d.m_out, d.dbias, 0, d.m_out, d.m_out);
+    int rc;
+    if (d.dbias && d.ldw == d.k_in && d.dbias == d.dw + mn && !d.accumulate) {
+      // weight and bias adjacent in the output (a Linear's flat gradient): one reduction
+      rc = ncf_defer(lst, a.part[g], s, a.stride[g], mn + d.m_out, d.dw, 0, mn + d.m_out,
+                     mn + d.m_out);
+    } else {
+      rc = ncf_defer(lst, a.part[g], s, a.stride[g], mn, d.dw, d.accumulate, d.k_in, d.ldw);
+      if (!rc && d.dbias) rc = ncf_defer(lst, a.part[g] + mn, s, a.stride[g], d.m_out, d.dbias, 0, d.m_out, d.m_out);
+    }
     if (rc) return rc;
   }
   if (!defer) {
