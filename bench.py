@@ -90,39 +90,57 @@ def cpu_baseline(model_sd, cfg, batches_cpu, budget_s):
                       f"CPU {platform.processor() or platform.machine()}"}
 
 
-def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget):
+def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
     """C5 (BASELINE.json configs[4]): n_query users x n_items top-K with the factorised MFMA
     scorer (ncf_amd.scoring), timed with inputs resident; plus the reference serving path
-    (forward_simple over items) on the CPU oracle for a bounded slice."""
+    (forward_simple over items) on the CPU oracle for a bounded slice.  With world > 1 the
+    catalogue is item-sharded: each rank scans its 1/W of the items, the per-rank
+    top-K lists are all-gathered and merged (fixed total work: strong scaling); the time is the
+    max over ranks."""
     import ncf_amd
     from ncf_amd import _lib as L
-    from ncf_amd.scoring import ItemIndex, score_topk
+    from ncf_amd.scoring import ItemIndex, shard_items, sharded_score_topk
     torch.manual_seed(4321)
     m = ncf_amd.AdvancedNCF(n_users, n_items, 10, 50).to(dev).eval()
+    users = torch.randperm(n_users, device=dev)[:n_query]
+    shard = shard_items(n_items, world, rank) if world > 1 else None
+    n_local = n_items if shard is None else shard.numel()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    idx = ItemIndex(m)
+    idx = ItemIndex(m, items=shard)
     torch.cuda.synchronize()
     index_ms = (time.perf_counter() - t0) * 1e3
-    users = torch.randperm(n_users, device=dev)[:n_query]
+
+    def timed(fn):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt)
+        return dt
+
     out = {"config": f"{n_query} users x {n_items} items (model {n_users} x {n_items}, D=64), "
-                     "top-K over the whole catalogue, factorised fp32 MFMA scan",
-           "item_index_ms": round(index_ms, 3)}
+                     "top-K over the whole catalogue, factorised fp32 MFMA scan"
+                     + (f", item-sharded over {world} GPUs (all-gather + merge)" if world > 1 else ""),
+           "scaling": "strong", "n_gpus": world, "item_index_ms": round(index_ms, 3)}
     for k in ks:
-        score_topk(m, users, k, idx)
+        sharded_score_topk(m, users, k, idx)
         torch.cuda.synchronize()
         best, prof = 1e9, None
         for _ in range(3):
             L.PROFILE = []
-            t0 = time.perf_counter()
-            score_topk(m, users, k, idx)
-            torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
+            dt = timed(lambda: sharded_score_topk(m, users, k, idx))
             if dt < best:
                 best, prof = dt, L.PROFILE
             L.PROFILE = None
         coll = sum(e0.elapsed_time(e1) for name, _, e0, e1 in prof if name == "ncf_score_collect")
-        flops = 2.0 * 64 * n_query * n_items
+        flops = 2.0 * 64 * n_query * n_local
         tf = flops / (coll * 1e-3) / 1e12
         out[f"k{k}"] = {"ms": round(best * 1e3, 3), "pairs_per_s": round(n_query * n_items / best, 1),
                         "collect_ms": round(coll, 3),
@@ -130,7 +148,7 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget):
                                      "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFS,
                                      "unit": "TFLOP/s", "frac": round(tf / FP32_MFMA_PEAK_TFS, 4),
                                      "flops_per_pair": 128}}
-    if cpu_budget > 0:
+    if cpu_budget > 0 and rank == 0 and world == 1:
         from oracle import ncf_oracle as O
         p = {k: v.detach().cpu() for k, v in m.state_dict().items()}
         n_cpu = min(n_items, 100_000)
@@ -294,9 +312,9 @@ def main():
         cpu_batches = [(u.cpu(), i.cpu(), t.cpu()) for (u, i, t) in batches[:4]]
         cpu = cpu_baseline(init_sd, (U, I, D, T, H, hid, B, M), cpu_batches, args.cpu_budget)
     score = None
-    if world == 1 and not args.no_score:
+    if not args.no_score:
         score = c5_scoring(dev, 1_000_000, args.score_items, args.score_users, (10, 100),
-                           0 if args.no_cpu_baseline else 1)
+                           0 if args.no_cpu_baseline else 1, world=world, rank=rank)
 
     if rank == 0:
         rec = {

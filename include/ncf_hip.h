@@ -290,6 +290,11 @@ int ncf_score_select(const int32_t* user_list, int64_t n_users, const uint32_t* 
                      const float* cand_logit, const int32_t* cand_item, int64_t cap, int K,
                      float* out_score, int64_t* out_item, float* thr, uint32_t* overflow,
                      void* stream);
+/* Item-sharded scoring: merge per-user lists of L = W*K (score, global item id)
+ * gathered from W item shards into the top-K by (score desc, item id asc); id < 0 = empty slot
+ * (an empty output slot is (0, -1)).  L, K <= 8192; item ids < 2^32 - 1. */
+int ncf_score_merge(const float* cand_score, const int64_t* cand_item, int64_t n_users, int64_t L,
+                    int K, float* out_score, int64_t* out_item, void* stream);
 
 /* ---- a13: torch.optim.Adam step (trainer.py:71-75, :285) ----------------------------------
  * Dense-exact over a whole table via the slot map (every row decays every step).            */

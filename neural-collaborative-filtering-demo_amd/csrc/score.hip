@@ -208,6 +208,23 @@ __global__ __launch_bounds__(512) void k_collect(
 // ---- 4. per-user selection: bitonic sort (descending) of 64-bit keys (logit key | ~item)
 constexpr int kSelectMax = 8192;
 
+// in-LDS bitonic sort of n2 (a power of two) keys, descending; the whole block participates
+__device__ __forceinline__ void bitonic_desc(unsigned long long* keys, int n2) {
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int j = threadIdx.x; j < n2; j += blockDim.x) {
+        const int p = j ^ stride;
+        if (p > j) {
+          const bool desc = (j & size) == 0;
+          const unsigned long long x = keys[j], y = keys[p];
+          if ((x < y) == desc) { keys[j] = y; keys[p] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_select(const int32_t* __restrict__ user_list,
                                                  int64_t n_users, const uint32_t* __restrict__ count,
                                                  const float* __restrict__ cand_logit,
@@ -234,19 +251,7 @@ __global__ __launch_bounds__(1024) void k_select(const int32_t* __restrict__ use
     keys[j] = k;
   }
   __syncthreads();
-  for (int size = 2; size <= n2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int j = threadIdx.x; j < n2; j += blockDim.x) {
-        const int p = j ^ stride;
-        if (p > j) {
-          const bool desc = (j & size) == 0;
-          const unsigned long long x = keys[j], y = keys[p];
-          if ((x < y) == desc) { keys[j] = y; keys[p] = x; }
-        }
-      }
-      __syncthreads();
-    }
-  }
+  bitonic_desc(keys, n2);
   for (int j = threadIdx.x; j < K; j += blockDim.x) {
     const unsigned long long k = keys[j];
     const bool ok = j < nc;
@@ -262,7 +267,58 @@ __global__ __launch_bounds__(1024) void k_select(const int32_t* __restrict__ use
   }
 }
 
+// ---- 5. merge of per-shard top-K lists (item-sharded scoring): per user, the L
+// candidates (score, global item id; id < 0 = empty) sorted by (score desc, item id asc)
+__global__ __launch_bounds__(1024) void k_merge(const float* __restrict__ cand_score,
+                                                const int64_t* __restrict__ cand_item, int64_t L,
+                                                int K, float* __restrict__ out_score,
+                                                int64_t* __restrict__ out_item) {
+  extern __shared__ unsigned long long keys[];
+  const int64_t u = blockIdx.x;
+  int n2 = 1;
+  while (n2 < L || n2 < K) n2 <<= 1;
+  for (int j = threadIdx.x; j < n2; j += blockDim.x) {
+    unsigned long long k = 0ull;
+    if (j < L) {
+      const int64_t id = cand_item[u * L + j];
+      if (id >= 0)
+        k = ((unsigned long long)fkey(cand_score[u * L + j]) << 32) |
+            (unsigned long long)(0xFFFFFFFFu - (uint32_t)id);
+    }
+    keys[j] = k;
+  }
+  __syncthreads();
+  bitonic_desc(keys, n2);
+  for (int j = threadIdx.x; j < K; j += blockDim.x) {
+    const unsigned long long k = keys[j];
+    const bool ok = k != 0ull;
+    out_score[u * K + j] = ok ? fkey_inv((uint32_t)(k >> 32)) : 0.0f;
+    out_item[u * K + j] = ok ? (int64_t)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : -1;
+  }
+}
+
 }  // namespace
+
+extern "C" int ncf_score_merge(const float* cand_score, const int64_t* cand_item, int64_t n_users,
+                               int64_t L, int K, float* out_score, int64_t* out_item,
+                               void* stream) {
+  NCF_CHECK_ARG(n_users >= 0 && K >= 1 && L >= 1 && L <= kSelectMax && K <= kSelectMax,
+                "ncf_score_merge: need 1 <= K, L <= %d", kSelectMax);
+  if (n_users == 0) return NCF_OK;
+  int n2 = 1;
+  while (n2 < L || n2 < K) n2 <<= 1;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_merge, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(sizeof(unsigned long long) * kSelectMax));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_merge, dim3((unsigned)n_users), dim3(1024),
+                     sizeof(unsigned long long) * (size_t)n2, (hipStream_t)stream, cand_score,
+                     cand_item, L, K, out_score, out_item);
+  NCF_CHECK_LAUNCH("ncf_score_merge");
+  return NCF_OK;
+}
 
 extern "C" int ncf_score_queries(const int64_t* user_ids, int64_t n, const float* mf_user,
                                  int64_t rows, int64_t dim, const float* mf_gamma,

@@ -226,6 +226,7 @@ class HipShardOps:
 
     def dense_step(self):
         self.step_count += 1
+        self.eng.updates += 1
         b1, b2 = self.betas
         _lib.call("ncf_adam_flat", ptr(self.eng.flat), ptr(self.eng.flat_grad), ptr(self.m_flat),
                   ptr(self.v_flat), self.eng.flat.numel(), self.lr, b1, b2, self.eps, self.wd,

@@ -156,6 +156,7 @@ class NCFEngine:
         self._side = None         # side streams (fork / join)
         self._events = None
         self._ev_i = 0
+        self.updates = 0          # parameter writes by the HIP kernels (torch's _version misses them)
 
     # ------------------------------------------------------------------ side streams
     # The step is a chain of latency-bound kernels that each fill a fraction of the GPU; work

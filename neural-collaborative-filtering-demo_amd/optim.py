@@ -119,6 +119,7 @@ def _pre_hook(opt, args, kwargs):
             step_t = torch.tensor(0.0, dtype=torch.float32)
         step_t += 1
         step = float(step_t.item())
+        eng.updates += 1
 
         def hp(p):
             g = gmap[id(p)]

@@ -10,8 +10,11 @@ at once through the factorised eval form (csrc/score.hip):
     p_i    = LN_mf(I_mf[i])                              (ncf_gather_rows, cached per model state)
     bias_i = w1 * mlp_item(i) + w0 * b_mf + b_final      (the engine's eval forward + ncf_score_item_bias)
 
-``ItemIndex`` caches the item side (p, bias) for a parameter version; ``score_topk`` runs the
-threshold / MFMA-collect / select pipeline.  ``forward_simple(hour=None)`` semantics only (the
+``ItemIndex`` caches the item side (p, bias) for a parameter version (optionally for a subset
+of the catalogue: one rank's item shard); ``score_topk`` runs the threshold / MFMA-collect /
+select pipeline; ``sharded_score_topk`` is the item-sharded multi-GPU form: every
+rank scores all queried users against its own item shard, the per-shard top-K lists are
+all-gathered (RCCL) and merged per user by ``ncf_score_merge``.  ``forward_simple(hour=None)`` semantics only (the
 hour variant draws a fresh random projection on every call, architecture.py:437-442, so it has no
 reusable item side).  GPU only; no CPU fallback.
 """
@@ -30,7 +33,8 @@ K_MF_I = "mf_embedding_collection.embedding_bags.product_id.weight"
 class ItemIndex:
     """Item-side factors of the factorised scorer for one model state."""
 
-    def __init__(self, model, chunk: int = 65536):
+    def __init__(self, model, chunk: int = 65536, items: Optional[torch.Tensor] = None):
+        """``items``: the global item ids this index covers (default: the whole catalogue)."""
         eng = model._engine
         eng.sync_tables()
         self.model = model
@@ -42,15 +46,24 @@ class ItemIndex:
         if D != 64 or model.mlp_embedding_dim != 64:
             raise NotImplementedError("the scoring kernels are specialised for D = 64")
         st = _lib.stream_ptr(dev)
-        ids = torch.arange(I, dtype=torch.int64, device=dev)
+        if items is None:
+            ids = torch.arange(I, dtype=torch.int64, device=dev)
+            self.ids = None
+        else:
+            ids = items.to(device=dev, dtype=torch.int64).contiguous()
+            if ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= I):
+                raise IndexError("ItemIndex: item id out of range of the embedding table")
+            self.ids = ids
+            I = ids.numel()
         table = model.mf_embedding_collection.embedding_bags["product_id"].weight
         self.p = torch.empty(I, D, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
-        _lib.call("ncf_gather_rows", ptr(ids), I, ptr(table), I, D, ptr(model.mf_norm.weight),
+        _lib.call("ncf_gather_rows", ptr(ids), I, ptr(table), model.num_products, D,
+                  ptr(model.mf_norm.weight),
                   ptr(model.mf_norm.bias), LN_EPS, ptr(self.p), ptr(err), st)
         # mlp_item(i): the eval forward's MLP prediction depends on the item only (M = 1)
         mlp_item = torch.empty(I, device=dev)
-        zeros = torch.zeros(min(I, chunk), dtype=torch.int64, device=dev)
+        zeros = torch.zeros(max(1, min(I, chunk)), dtype=torch.int64, device=dev)
         with torch.no_grad():
             for c0 in range(0, I, chunk):
                 c1 = min(I, c0 + chunk)
@@ -66,7 +79,8 @@ class ItemIndex:
 
 
 def _param_version(model):
-    return tuple(p._version for p in model.parameters())
+    # torch's _version sees optimizer steps through torch; engine.updates the HIP kernels' writes
+    return (model._engine.updates,) + tuple(p._version for p in model.parameters())
 
 
 def _sample_size(n_items: int, k: int, cap: int) -> int:
@@ -81,8 +95,10 @@ def score_topk(model, user_ids: torch.Tensor, k: int = 10, index: Optional[ItemI
     """Top-k (probability, item id) per user over all items, as
     ``forward_simple(user, all_items)`` + ``nlargest(k)`` would rank them.  Returns
     ``(scores [n, k] fp32, items [n, k] int64)``."""
-    if index is None or not index.valid_for(model):
+    if index is None:
         index = ItemIndex(model)
+    elif not index.valid_for(model):   # parameters changed since the index was built
+        index = ItemIndex(model, items=index.ids)
     p, bias = index.p, index.bias
     dev = p.device
     I, D = p.shape
@@ -141,4 +157,61 @@ def score_topk(model, user_ids: torch.Tensor, k: int = 10, index: Optional[ItemI
         raise RuntimeError("score_topk: candidate lists kept overflowing (degenerate scores?)")
     if int(err.item()):
         raise IndexError("score_topk: user id out of range of the embedding table")
+    if index.ids is not None:   # shard-local positions -> global item ids
+        items = index.ids[items.clamp_min(0)]
     return scores, items
+
+
+def shard_items(num_items: int, world: int, rank: int) -> torch.Tensor:
+    """Global item ids of ``rank``'s scoring shard: a contiguous block of the catalogue."""
+    per = -(-num_items // world)
+    return torch.arange(min(num_items, rank * per), min(num_items, (rank + 1) * per),
+                        dtype=torch.int64)
+
+
+def merge_topk(cand_scores: torch.Tensor, cand_items: torch.Tensor, k: int):
+    """Per-user top-k of ``[n, L]`` candidate (score, global item id) lists, ordered by score
+    desc then item id asc (empty slots: id < 0).  HIP (ncf_score_merge); GPU only."""
+    if cand_scores.device.type != "cuda":
+        raise RuntimeError("ncf_amd scoring runs on the MI355X only (no CPU fallback)")
+    n, L = cand_scores.shape
+    s = cand_scores.to(torch.float32).contiguous()
+    it = cand_items.to(torch.int64).contiguous()
+    out_s = torch.empty(n, k, device=s.device)
+    out_i = torch.empty(n, k, dtype=torch.int64, device=s.device)
+    _lib.call("ncf_score_merge", ptr(s), ptr(it), n, L, k, ptr(out_s), ptr(out_i),
+              _lib.stream_ptr(s.device))
+    return out_s, out_i
+
+
+def sharded_score_topk(model, user_ids: torch.Tensor, k: int = 10,
+                       index: Optional[ItemIndex] = None, group=None, cap: int = 8192,
+                       local_topk=None, merge=None):
+    """Item-sharded C5 scoring over ``torch.distributed``: rank r scores every
+    queried user against ``shard_items(I, W, r)``, the ``[n, k]`` local lists are all-gathered
+    (8 B per entry + id widening) and merged per user.  Every rank returns the global top-k.
+    ``local_topk(user_ids, k) -> (scores, global ids)`` and ``merge`` default to the HIP path
+    (they are parameters so the collective layout can be exercised on CPU ranks)."""
+    import torch.distributed as dist
+    W = dist.get_world_size(group) if dist.is_initialized() else 1
+    r = dist.get_rank(group) if dist.is_initialized() else 0
+    if local_topk is None:
+        if index is None or not index.valid_for(model):
+            index = ItemIndex(model, items=shard_items(model.num_products, W, r))
+        kk = min(k, index.p.shape[0])
+
+        def local_topk(u, _k):
+            s, i = score_topk(model, u, kk, index, cap)
+            if kk < _k:   # a shard smaller than k: pad with empty slots
+                s = torch.cat([s, s.new_zeros(s.shape[0], _k - kk)], 1)
+                i = torch.cat([i, i.new_full((i.shape[0], _k - kk), -1)], 1)
+            return s, i
+    merge = merge or merge_topk
+    s, i = local_topk(user_ids, k)
+    if W == 1:
+        return s, i      # already the (score desc, item id asc) top-k of the whole catalogue
+    gs = [torch.empty_like(s) for _ in range(W)]
+    gi = [torch.empty_like(i) for _ in range(W)]
+    dist.all_gather(gs, s.contiguous(), group=group)
+    dist.all_gather(gi, i.contiguous(), group=group)
+    return merge(torch.cat(gs, 1), torch.cat(gi, 1), k)

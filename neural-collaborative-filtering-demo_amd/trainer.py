@@ -118,6 +118,7 @@ class FusedTrainStep:
         if not self.graph:
             w = self._body(user_ids, item_ids, targets, M)
             self.step_count += 1
+            m.engine.updates += 1
             self.last_loss = w.loss
             return w
         dev = m.engine.flat.device
@@ -129,6 +130,7 @@ class FusedTrainStep:
                 w = self._body(user_ids, item_ids, targets, M)
                 self._eager_steps += 1
                 self.step_count += 1
+                m.engine.updates += 1
                 self.last_loss = w.loss
                 self._g = None
                 return w
@@ -141,6 +143,7 @@ class FusedTrainStep:
         # host mirrors of what the replayed launches did on the device
         self.deferred.t += 1
         self.model.engine.pending = None
+        self.model.engine.updates += 1
         self.step_count += 1
         self.last_loss = self._w.loss
         return self._w
@@ -150,6 +153,7 @@ class FusedTrainStep:
         kernels a replay runs; used for per-launch instrumentation."""
         w = self._body(user_ids, item_ids, targets, M or (1 + self.model.negative_samples))
         self.step_count += 1
+        self.model.engine.updates += 1
         self.last_loss = w.loss
         return w
 

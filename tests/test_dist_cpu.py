@@ -187,3 +187,65 @@ def test_sharded_step_equals_single_rank_global_batch():
             got = res[0]["p"][name]
             assert torch.equal(got, res[1]["p"][name]), name     # replicas stay identical
         assert_params_close(name, got.numpy(), ref[name].numpy(), gv, 1e-3, 2, atol=2e-6)
+
+
+# ----------------------------------------------------------------------------- C5 item shards
+SU, SI, SK = 23, 301, 7
+
+
+def _score_setup():
+    import _ncf_pkg
+    ncf = _ncf_pkg.load()
+    torch.manual_seed(2)
+    m = ncf.AdvancedNCF(SU, SI, 5, 24, D, D, T, HID, H, 0.0, M - 1)
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+def _ref_merge(s, i, k):
+    """(score desc, item id asc) top-k with empty slots (id < 0) last — the merge's contract."""
+    key_s = torch.where(i >= 0, s.double(), torch.full_like(s.double(), -1.0))
+    out_s, out_i = [], []
+    for r in range(s.shape[0]):
+        order = sorted(range(s.shape[1]), key=lambda j: (-key_s[r, j].item(), i[r, j].item()))[:k]
+        out_s.append(torch.stack([s[r, j] if i[r, j] >= 0 else s.new_zeros(()) for j in order]))
+        out_i.append(torch.stack([i[r, j] for j in order]))
+    return torch.stack(out_s), torch.stack(out_i)
+
+
+def _score_worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import ncf_oracle as O
+    p = _score_setup()
+    from ncf_amd.scoring import shard_items, sharded_score_topk
+    users = torch.arange(SU)
+
+    def local_topk(u, k):    # oracle scores of this rank's shard (the HIP scorer needs a GPU)
+        ids = shard_items(SI, world, rank)
+        sc = O.score_factorised(p, u, ids, temporal_dim=T, n_layers=len(HID)).float()
+        return _ref_merge(sc, ids.expand(len(u), -1), k)
+
+    s, i = sharded_score_topk(None, users, SK, local_topk=local_topk, merge=_ref_merge)
+    torch.save({"s": s, "i": i}, os.path.join(out_dir, f"score{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_item_sharded_scoring_collective_layout():
+    """the per-shard top-k lists all-gathered over 2 gloo ranks and merged equal the
+    single-rank top-k over the whole catalogue, on every rank."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_score_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f"score{r}.pt"), weights_only=True) for r in range(world)]
+    from oracle import ncf_oracle as O
+    p = _score_setup()
+    sc = O.score_factorised(p, torch.arange(SU), torch.arange(SI), temporal_dim=T,
+                            n_layers=len(HID)).float()
+    rs, ri = _ref_merge(sc, torch.arange(SI).expand(SU, -1), SK)
+    for r in res:
+        assert torch.equal(r["i"], ri)
+        assert torch.equal(r["s"], rs)

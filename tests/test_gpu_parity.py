@@ -722,6 +722,69 @@ def test_score_topk_vs_oracle(k, cap):
         np.testing.assert_allclose(s[r].cpu().numpy(), ref[r, got].numpy(), atol=1e-6)
 
 
+@pytest.mark.parametrize("W,strided", [(3, False), (4, True), (1, False)])
+@pytest.mark.parametrize("k", [10, 100])
+def test_item_sharded_scoring_equals_single(W, strided, k):
+    """SURVEY 8e item-sharded C5 scoring, all W shards emulated in one process: per-shard
+    top-k (ItemIndex over the shard's global ids) + ncf_score_merge == the one-GPU top-k."""
+    from ncf_amd.scoring import ItemIndex, merge_topk, score_topk, shard_items
+    torch.manual_seed(5)
+    U, I = 200, 5003
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    users = torch.randint(0, U, (45,))
+    ref_s, ref_i = score_topk(m, users, k=k)
+    ls, li = [], []
+    for r in range(W):
+        ids = torch.arange(r, I, W) if strided else shard_items(I, W, r)
+        s, i = score_topk(m, users, k=k, index=ItemIndex(m, items=ids))
+        assert bool(((i % W == r) if strided else ((i >= ids[0]) & (i <= ids[-1]))).all())
+        ls.append(s)
+        li.append(i)
+    gs, gi = merge_topk(torch.cat(ls, 1), torch.cat(li, 1), k)
+    torch.testing.assert_close(gs, ref_s, rtol=0, atol=0)
+    # identical ids except between exactly tied probabilities
+    diff = gi != ref_i
+    if diff.any():
+        assert bool((gs[diff] == ref_s[diff]).all())
+
+
+def test_merge_topk_empty_slots_and_ties():
+    from ncf_amd.scoring import merge_topk
+    s = torch.tensor([[0.5, 0.9, 0.5, 0.0, 0.7], [0.1, 0.0, 0.0, 0.0, 0.0]], device=DEV)
+    i = torch.tensor([[7, 3, 2, -1, 11], [4, -1, -1, -1, -1]], device=DEV)
+    gs, gi = merge_topk(s, i, 4)
+    assert gi.cpu().tolist() == [[3, 11, 2, 7], [4, -1, -1, -1]]
+    assert gs.cpu().tolist()[0] == pytest.approx([0.9, 0.7, 0.5, 0.5])
+    assert gs.cpu().tolist()[1] == [pytest.approx(0.1), 0.0, 0.0, 0.0]
+
+
+def test_item_index_tracks_fused_updates():
+    """An ItemIndex built before a FusedTrainStep is stale afterwards (the HIP Adam writes the
+    tables behind torch's _version); score_topk must rebuild it."""
+    from ncf_amd.scoring import ItemIndex, score_topk
+    from ncf_amd.trainer import FusedTrainStep
+    torch.manual_seed(6)
+    U, I, B, Mm = 50, 300, 16, 5
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    idx = ItemIndex(m)
+    step = FusedTrainStep(m, lr=5e-2)
+    u = torch.randint(0, U, (B,), device=DEV).repeat_interleave(Mm)
+    it = torch.randint(0, I, (B * Mm,), device=DEV)
+    t = torch.zeros(B, Mm, device=DEV)
+    t[:, 0] = 1
+    m.train()
+    for _ in range(3):
+        step(u, it, t.reshape(-1, 1))
+    step.sync()
+    m.eval()
+    assert not idx.valid_for(m)
+    users = torch.arange(U)
+    s_old, i_old = score_topk(m, users, 10, idx)
+    s_new, i_new = score_topk(m, users, 10, ItemIndex(m))
+    torch.testing.assert_close(s_old, s_new, rtol=0, atol=0)
+
+
 def test_f6_forward_simple_hour(f5, f6):
     """forward_simple(hour=h) vs the reference (F6: its per-call projection reproduced by seed),
     and the drop-in call that draws its own projection like the reference does."""
