@@ -175,6 +175,25 @@ int ncf_attention_bwd(const float* q, const float* k, const float* v, const floa
                       int64_t dim, float dropout_p, uint64_t seed, const ncf_step_clock* clock,
                       float* grad_scores, float* grad_q, float* grad_k, float* grad_v,
                       void* stream);
+/* The whole a5 block in one launch per direction (D = 64, M <= 6; ncf_attn_block_supported):
+ * forward  q,k,v = LN rows x W^T + b, the core above (same P layout and dropout stream), y =
+ *          o Wo^T + bo.  q = k = NULL (with M == 1, no dropout): the eval form, o = v, only y
+ *          (and v, o if given) written.  probs/o required when q is given.
+ * backward from dY: dO = dY Wo, the core backward, dXu = dQ Wq, dXi = dK Wk + dV Wv; dQ/dK/dV
+ *          written for the weight gradients.                                                 */
+int ncf_attn_block_supported(int64_t dim, int64_t heads, int64_t group_len);
+int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t groups, int64_t group_len,
+                       int64_t heads, int64_t dim, const float* wq, const float* bq,
+                       const float* wk, const float* bk, const float* wv, const float* bv,
+                       const float* wo, const float* bo, float dropout_p, uint64_t seed,
+                       const ncf_step_clock* clock, float* q, float* k, float* v, float* probs,
+                       float* o, float* y, void* stream);
+int ncf_attn_block_bwd(const float* grad_y, const float* q, const float* k, const float* v,
+                       const float* probs, int64_t groups, int64_t group_len, int64_t heads,
+                       int64_t dim, const float* wq, const float* wk, const float* wv,
+                       const float* wo, float dropout_p, uint64_t seed,
+                       const ncf_step_clock* clock, float* grad_q, float* grad_k, float* grad_v,
+                       float* grad_xu, float* grad_xi, void* stream);
 
 /* ---- a6: TemporalEncoding (architecture.py:59-94): hour/day/month rows + pe[days mod P] -- */
 int ncf_temporal_fwd(const int64_t* hour, const int64_t* day, const int64_t* month,

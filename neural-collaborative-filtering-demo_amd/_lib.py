@@ -53,6 +53,11 @@ SIGNATURES = {
     "ncf_colsum": (I32, [P, I64, I64, I64, P, I32, P, I64, P]),
     "ncf_attention_fwd": (I32, [P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P]),
     "ncf_attention_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P, P, P]),
+    "ncf_attn_block_supported": (I32, [I64, I64, I64]),
+    "ncf_attn_block_fwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, F32, U64, P,
+                                 P, P, P, P, P, P, P]),
+    "ncf_attn_block_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, P, P, P, P, F32, U64, P, P,
+                                 P, P, P, P, P]),
     "ncf_relu_ln_dropout_fwd": (I32, [P, I64, I64, P, P, F32, F32, U64, P, P, P, P, P]),
     "ncf_relu_ln_dropout_bwd_workspace": (I64, [I64, I64]),
     "ncf_relu_ln_dropout_bwd": (I32, [P, P, P, P, P, I64, I64, F32, U64, P, P, P, P, P, P, I64,

@@ -1,0 +1,502 @@
+// The whole attention block of AdvancedNCF in one launch per direction: Q/K/V projections, the
+// per-group multi-head core and out_proj, for D = 64 and groups of M <= 6 rows.
+//
+// Reference: MultiHeadAttention.forward (src/model/architecture.py:18-57) as AdvancedNCF.forward
+// calls it (:315-326): q = LN(user_mlp rows), k = v = LN(item_mlp rows), groups of
+// M = 1 + negative_samples rows, Q/K/V/out Linear(D, D), scores/sqrt(hd), softmax, dropout on
+// the weights, ·V, heads merged, out_proj.  Same math and the same dropout stream as the
+// unfused path (gemm_rows.hip x4 + attention.hip); only the fmaf order of the projections
+// differs (the k-permuted MFMA below).
+//
+// Tiling: a 512-thread workgroup owns 16 interaction groups = R = 16*M rows, so every group is
+// whole inside it and the core never leaves LDS.  The projections are 16x16 output tiles of
+// v_mfma_f32_16x16x4_f32 over K = 64: wave w owns output columns [16(w&3), +16) for the row
+// tiles of parity w>>2 (two waves per SIMD), its weight fragment (16 floats per lane) loaded
+// once.  k-permuted operands: in MFMA
+// step s, lane group g = lane>>4 supplies k = 16g + s, so each lane's A row slice and B weight
+// slice are 16 contiguous floats (4 x ds_read_b128 / global float4).  Rows are staged in LDS
+// with a 68-float pitch (conflict-free 16-row x 4-slice fragment reads).
+//
+// Forward LDS: S0 = X_u -> Q -> O, S1 = X_i -> K -> Y, S2 = V   (3 x R x 68 floats)
+// Backward LDS: S0 = dY -> dO -> dX_u, S1 = Q -> dK -> dX_i, S2 = K -> dQ, S3 = V -> dV, + dS
+#include "ncf_common.h"
+
+namespace {
+
+constexpr int kD = 64;
+constexpr int kPitch = 68;
+constexpr int kGroups = 16;   // interaction groups per workgroup
+constexpr int kMaxM = 6;
+constexpr int kThreads = 512;   // 8 waves: wave w owns column slice (w & 3), row tiles of parity (w >> 2)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// acc += A[16 rows at X, 64 k] . B (B fragment: this lane's 16 k values)
+__device__ __forceinline__ f32x4 tile_mfma(const float* __restrict__ X, const float (&b)[16],
+                                           f32x4 acc) {
+  const int l = threadIdx.x & 63;
+  const float* a = X + (l & 15) * kPitch + 16 * (l >> 4);
+  float av[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = *reinterpret_cast<const float4*>(a + 4 * q);
+    av[4 * q] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], b[s], acc, 0, 0, 0);
+  return acc;
+}
+
+// B fragment of x W^T (forward): B[k][j] = W[j][k], j = 16w + (lane & 15), k = 16g + s
+__device__ __forceinline__ void frag_wt(const float* __restrict__ W, int w, float (&b)[16]) {
+  const int l = threadIdx.x & 63;
+  const float* p = W + (16 * w + (l & 15)) * kD + 16 * (l >> 4);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = ld4(p + 4 * q);
+    b[4 * q] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
+  }
+}
+
+// B fragment of dz W (backward): B[k][j] = W[k][j], j = 16w + (lane & 15), k = 16g + s
+__device__ __forceinline__ void frag_w(const float* __restrict__ W, int w, float (&b)[16]) {
+  const int l = threadIdx.x & 63;
+  const float* p = W + (16 * (l >> 4)) * kD + 16 * w + (l & 15);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) b[s] = p[s * kD];
+}
+
+// C fragment (rows 4g + r of the row tile, column 16w + (lane & 15)) -> LDS
+__device__ __forceinline__ void put_tile(float* __restrict__ S, int rt, int w, f32x4 c) {
+  const int l = threadIdx.x & 63;
+  float* p = S + (16 * rt + 4 * (l >> 4)) * kPitch + 16 * w + (l & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p[r * kPitch] = c[r];
+}
+
+__device__ __forceinline__ void stage_in(float* __restrict__ S, const float* __restrict__ X,
+                                         int R, int rows) {
+  for (int e = threadIdx.x; e < R * 16; e += blockDim.x) {
+    const int r = e >> 4, c = (e & 15) * 4;
+    const float4 v = r < rows ? ld4(X + (int64_t)r * kD + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(S + r * kPitch + c) = v;
+  }
+}
+
+__device__ __forceinline__ void stage_out(float* __restrict__ X, const float* __restrict__ S,
+                                          int rows) {
+  for (int e = threadIdx.x; e < rows * 16; e += blockDim.x) {
+    const int r = e >> 4, c = (e & 15) * 4;
+    st4(X + (int64_t)r * kD + c, *reinterpret_cast<const float4*>(S + r * kPitch + c));
+  }
+}
+
+// out[rt] = X . W^T + bias for the M row tiles of this wave's column slice
+__device__ __forceinline__ void project(const float* __restrict__ X, const float* __restrict__ W,
+                                        const float* __restrict__ bias, int M, f32x4 (&out)[kMaxM]) {
+  const int w = (threadIdx.x >> 6) & 3;
+  float b[16];
+  frag_wt(W, w, b);
+  const float bb = bias ? bias[16 * w + (threadIdx.x & 15)] : 0.0f;
+#pragma unroll
+  for (int rt = 0; rt < kMaxM; ++rt) {
+    if (rt < M && (rt & 1) == (threadIdx.x >> 8)) {
+      f32x4 acc = {bb, bb, bb, bb};
+      // bias first, then the k chain: fmaf(..., bias) order of the unfused GEMM epilogue
+      // differs only in rounding (tolerance-level)
+      out[rt] = tile_mfma(X + 16 * rt * kPitch, b, acc);
+    }
+  }
+}
+
+template <int HD>
+__global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
+    const float* __restrict__ xu, const float* __restrict__ xi, int64_t B, int M,
+    const float* __restrict__ wq, const float* __restrict__ bq, const float* __restrict__ wk,
+    const float* __restrict__ bk, const float* __restrict__ wv, const float* __restrict__ bv,
+    const float* __restrict__ wo, const float* __restrict__ bo, float scale, float p_drop,
+    uint64_t seed, const ncf_step_clock* clock, float* __restrict__ Q, float* __restrict__ K,
+    float* __restrict__ V, float* __restrict__ P, float* __restrict__ O, float* __restrict__ Y) {
+  constexpr int H = kD / HD;
+  constexpr int kIt = (kGroups * H * kMaxM + kThreads - 1) / kThreads;
+  extern __shared__ float lds[];
+  const int R = kGroups * M;
+  float* S0 = lds;
+  float* S1 = lds + R * kPitch;
+  float* S2 = lds + 2 * R * kPitch;
+  const int64_t g0 = (int64_t)blockIdx.x * kGroups;
+  const int ng = (int)min<int64_t>(kGroups, B - g0);
+  const int rows = ng * M;
+  const int64_t r0 = g0 * M;
+  const int w = (threadIdx.x >> 6) & 3;
+  const int par = threadIdx.x >> 8;
+  const bool core = Q != nullptr;   // false: eval with one item per group (softmax == 1, o = v)
+  if (clock) seed += clock->seed;
+
+  if (core) stage_in(S0, xu + r0 * kD, R, rows);
+  stage_in(S1, xi + r0 * kD, R, rows);
+  __syncthreads();
+  f32x4 fq[kMaxM], fk[kMaxM], fv[kMaxM];
+  project(S1, wv, bv, M, fv);
+  if (core) {
+    project(S0, wq, bq, M, fq);
+    project(S1, wk, bk, M, fk);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int rt = 0; rt < kMaxM; ++rt)
+    if (rt < M && (rt & 1) == par) {
+      put_tile(S2, rt, w, fv[rt]);
+      if (core) {
+        put_tile(S0, rt, w, fq[rt]);
+        put_tile(S1, rt, w, fk[rt]);
+      }
+    }
+  __syncthreads();
+  const float* src = S2;   // the out_proj input: O, or V when there is no core
+  if (core) {
+    stage_out(Q + r0 * kD, S0, rows);
+    stage_out(K + r0 * kD, S1, rows);
+    if (V) stage_out(V + r0 * kD, S2, rows);
+    // core: one lane per (group, head, query row), as k_attn_fwd (same P layout, same dropout
+    // index (t*M + j) with t = (b*H + h)*M + i)
+    const float inv_keep = p_drop > 0.0f ? 1.0f / (1.0f - p_drop) : 1.0f;
+    const int ntask = ng * H * M;
+    float o[kIt][HD];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int t = threadIdx.x + kThreads * it;
+      if (t < ntask) {
+        const int i = t % M, h = (t / M) % H, gl = t / (M * H);
+        const int64_t tg = ((g0 + gl) * H + h) * M + i;
+        const float* q = S0 + (gl * M + i) * kPitch + h * HD;
+        float s[kMaxM];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < kMaxM; ++j)
+          if (j < M) {
+            const float* k = S1 + (gl * M + j) * kPitch + h * HD;
+            float acc = 0.0f;
+#pragma unroll
+            for (int d = 0; d < HD; ++d) acc = fmaf(q[d], k[d], acc);
+            s[j] = acc / scale;
+            mx = fmaxf(mx, s[j]);
+          }
+        float sum = 0.0f;
+#pragma unroll
+        for (int j = 0; j < kMaxM; ++j)
+          if (j < M) {
+            s[j] = expf(s[j] - mx);
+            sum += s[j];
+          }
+#pragma unroll
+        for (int d = 0; d < HD; ++d) o[it][d] = 0.0f;
+#pragma unroll
+        for (int j = 0; j < kMaxM; ++j)
+          if (j < M) {
+            const float pj = s[j] / sum;
+            if (P) P[tg * M + j] = pj;
+            const float pd =
+                p_drop > 0.0f ? pj * ncf_dropout_scale(seed, (uint64_t)tg * M + j, p_drop, inv_keep) : pj;
+            const float* v = S2 + (gl * M + j) * kPitch + h * HD;
+#pragma unroll
+            for (int d = 0; d < HD; ++d) o[it][d] = fmaf(pd, v[d], o[it][d]);
+          }
+      }
+    }
+    __syncthreads();   // every lane is done reading Q/K/V
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int t = threadIdx.x + kThreads * it;
+      if (t < ntask) {
+        const int i = t % M, h = (t / M) % H, gl = t / (M * H);
+        float* dst = S0 + (gl * M + i) * kPitch + h * HD;
+#pragma unroll
+        for (int d = 0; d < HD; d += 4) *reinterpret_cast<float4*>(dst + d) = make_float4(o[it][d], o[it][d + 1], o[it][d + 2], o[it][d + 3]);
+      }
+    }
+    __syncthreads();
+    if (O) stage_out(O + r0 * kD, S0, rows);
+    src = S0;
+  } else if (V) {
+    stage_out(V + r0 * kD, S2, rows);
+  }
+  // out_proj -> S1 (K is dead) -> Y
+  f32x4 fy[kMaxM];
+  project(src, wo, bo, M, fy);
+#pragma unroll
+  for (int rt = 0; rt < kMaxM; ++rt)
+    if (rt < M && (rt & 1) == par) put_tile(S1, rt, w, fy[rt]);
+  __syncthreads();
+  stage_out(Y + r0 * kD, S1, rows);
+}
+
+template <int HD>
+__global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
+    const float* __restrict__ dY, const float* __restrict__ Qg, const float* __restrict__ Kg,
+    const float* __restrict__ Vg, const float* __restrict__ P, int64_t B, int M,
+    const float* __restrict__ wq, const float* __restrict__ wk, const float* __restrict__ wv,
+    const float* __restrict__ wo, float scale, float p_drop, uint64_t seed,
+    const ncf_step_clock* clock, float* __restrict__ dQ, float* __restrict__ dK,
+    float* __restrict__ dV, float* __restrict__ dXu, float* __restrict__ dXi) {
+  constexpr int H = kD / HD;
+  constexpr int kIt = (kGroups * H * kMaxM + kThreads - 1) / kThreads;
+  extern __shared__ float lds[];
+  const int R = kGroups * M;
+  float* S0 = lds;
+  float* S1 = lds + R * kPitch;
+  float* S2 = lds + 2 * R * kPitch;
+  float* S3 = lds + 3 * R * kPitch;
+  float* dS = lds + 4 * R * kPitch;   // [16][H][M][M]
+  const int64_t g0 = (int64_t)blockIdx.x * kGroups;
+  const int ng = (int)min<int64_t>(kGroups, B - g0);
+  const int rows = ng * M;
+  const int64_t r0 = g0 * M;
+  const int w = (threadIdx.x >> 6) & 3;
+  const int par = threadIdx.x >> 8;
+  if (clock) seed += clock->seed;
+  const float inv_keep = p_drop > 0.0f ? 1.0f / (1.0f - p_drop) : 1.0f;
+
+  stage_in(S0, dY + r0 * kD, R, rows);
+  stage_in(S1, Qg + r0 * kD, R, rows);
+  stage_in(S2, Kg + r0 * kD, R, rows);
+  stage_in(S3, Vg + r0 * kD, R, rows);
+  __syncthreads();
+  // dO = dY . Wo
+  {
+    float b[16];
+    frag_w(wo, w, b);
+    f32x4 fo[kMaxM];
+#pragma unroll
+    for (int rt = 0; rt < kMaxM; ++rt)
+      if (rt < M && (rt & 1) == par) fo[rt] = tile_mfma(S0 + 16 * rt * kPitch, b, f32x4{0.f, 0.f, 0.f, 0.f});
+    __syncthreads();
+#pragma unroll
+    for (int rt = 0; rt < kMaxM; ++rt)
+      if (rt < M && (rt & 1) == par) put_tile(S0, rt, w, fo[rt]);
+    __syncthreads();
+  }
+  const int ntask = ng * H * M;
+  // core, query side (as k_attn_bwd_q): dS and dQ per (group, head, query row)
+  {
+    float dq[kIt][HD];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int t = threadIdx.x + kThreads * it;
+      if (t < ntask) {
+        const int i = t % M, h = (t / M) % H, gl = t / (M * H);
+        const int64_t tg = ((g0 + gl) * H + h) * M + i;
+        const float* go = S0 + (gl * M + i) * kPitch + h * HD;
+        const float* prow = P + tg * M;
+        float dp[kMaxM], pr[kMaxM];
+        float tsum = 0.0f;
+#pragma unroll
+        for (int j = 0; j < kMaxM; ++j)
+          if (j < M) {
+            const float* v = S3 + (gl * M + j) * kPitch + h * HD;
+            float acc = 0.0f;
+#pragma unroll
+            for (int d = 0; d < HD; ++d) acc = fmaf(go[d], v[d], acc);
+            if (p_drop > 0.0f) acc *= ncf_dropout_scale(seed, (uint64_t)tg * M + j, p_drop, inv_keep);
+            dp[j] = acc;
+            pr[j] = prow[j];
+            tsum = fmaf(pr[j], acc, tsum);
+          }
+#pragma unroll
+        for (int d = 0; d < HD; ++d) dq[it][d] = 0.0f;
+        float* dsrow = dS + ((gl * H + h) * M + i) * M;
+#pragma unroll
+        for (int j = 0; j < kMaxM; ++j)
+          if (j < M) {
+            const float ds = pr[j] * (dp[j] - tsum);
+            dsrow[j] = ds;
+            const float* k = S2 + (gl * M + j) * kPitch + h * HD;
+#pragma unroll
+            for (int d = 0; d < HD; ++d) dq[it][d] = fmaf(ds, k[d], dq[it][d]);
+          }
+      }
+    }
+    __syncthreads();   // K, V no longer read; dS complete
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int t = threadIdx.x + kThreads * it;
+      if (t < ntask) {
+        const int i = t % M, h = (t / M) % H, gl = t / (M * H);
+        float* dst = S2 + (gl * M + i) * kPitch + h * HD;
+#pragma unroll
+        for (int d = 0; d < HD; ++d) dst[d] = dq[it][d] / scale;
+      }
+    }
+  }
+  // core, key side (as k_attn_bwd_kv): dK, dV per (group, head, key row)
+  {
+    float dk[kIt][HD];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int t = threadIdx.x + kThreads * it;
+      if (t < ntask) {
+        const int j = t % M, h = (t / M) % H, gl = t / (M * H);
+        float dv[HD];
+#pragma unroll
+        for (int d = 0; d < HD; ++d) { dk[it][d] = 0.0f; dv[d] = 0.0f; }
+        const int64_t bh = (g0 + gl) * H + h;
+        for (int i = 0; i < M; ++i) {
+          const int64_t row = bh * M + i;
+          const float ds = dS[((gl * H + h) * M + i) * M + j];
+          float pd = P[row * M + j];
+          if (p_drop > 0.0f) pd *= ncf_dropout_scale(seed, (uint64_t)row * M + j, p_drop, inv_keep);
+          const float* q = S1 + (gl * M + i) * kPitch + h * HD;
+          const float* go = S0 + (gl * M + i) * kPitch + h * HD;
+#pragma unroll
+          for (int d = 0; d < HD; ++d) {
+            dk[it][d] = fmaf(ds, q[d], dk[it][d]);
+            dv[d] = fmaf(pd, go[d], dv[d]);
+          }
+        }
+        float* dst = S3 + (gl * M + j) * kPitch + h * HD;   // V is dead
+#pragma unroll
+        for (int d = 0; d < HD; ++d) dst[d] = dv[d];
+      }
+    }
+    __syncthreads();   // Q no longer read
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int t = threadIdx.x + kThreads * it;
+      if (t < ntask) {
+        const int j = t % M, h = (t / M) % H, gl = t / (M * H);
+        float* dst = S1 + (gl * M + j) * kPitch + h * HD;
+#pragma unroll
+        for (int d = 0; d < HD; ++d) dst[d] = dk[it][d] / scale;
+      }
+    }
+    __syncthreads();
+  }
+  stage_out(dQ + r0 * kD, S2, rows);
+  stage_out(dK + r0 * kD, S1, rows);
+  stage_out(dV + r0 * kD, S3, rows);
+  // dX_u = dQ . Wq ; dX_i = dK . Wk + dV . Wv
+  f32x4 fu[kMaxM], fi[kMaxM];
+  {
+    float b[16];
+    frag_w(wq, w, b);
+#pragma unroll
+    for (int rt = 0; rt < kMaxM; ++rt)
+      if (rt < M && (rt & 1) == par) fu[rt] = tile_mfma(S2 + 16 * rt * kPitch, b, f32x4{0.f, 0.f, 0.f, 0.f});
+    frag_w(wk, w, b);
+#pragma unroll
+    for (int rt = 0; rt < kMaxM; ++rt)
+      if (rt < M && (rt & 1) == par) fi[rt] = tile_mfma(S1 + 16 * rt * kPitch, b, f32x4{0.f, 0.f, 0.f, 0.f});
+    frag_w(wv, w, b);
+#pragma unroll
+    for (int rt = 0; rt < kMaxM; ++rt)
+      if (rt < M && (rt & 1) == par) fi[rt] = tile_mfma(S3 + 16 * rt * kPitch, b, fi[rt]);
+  }
+#pragma unroll
+  for (int rt = 0; rt < kMaxM; ++rt)
+    if (rt < M && (rt & 1) == par) put_tile(S0, rt, w, fu[rt]);   // dO is dead
+  __syncthreads();   // S1..S3 no longer read (MFMA operands, stage_out)
+#pragma unroll
+  for (int rt = 0; rt < kMaxM; ++rt)
+    if (rt < M && (rt & 1) == par) put_tile(S1, rt, w, fi[rt]);
+  __syncthreads();
+  stage_out(dXu + r0 * kD, S0, rows);
+  stage_out(dXi + r0 * kD, S1, rows);
+}
+
+size_t fwd_lds(int M) { return sizeof(float) * 3 * kGroups * M * kPitch; }
+size_t bwd_lds(int M, int H) {
+  return sizeof(float) * (4 * kGroups * M * kPitch + kGroups * H * M * M);
+}
+
+template <typename Kern>
+void allow_lds(Kern k, size_t bytes) {
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+}  // namespace
+
+extern "C" int ncf_attn_block_supported(int64_t dim, int64_t heads, int64_t group_len) {
+  if (dim != kD || heads < 1 || dim % heads != 0) return 0;
+  const int64_t hd = dim / heads;
+  if (hd != 8 && hd != 16 && hd != 32 && hd != 64) return 0;
+  return group_len >= 1 && group_len <= kMaxM ? 1 : 0;
+}
+
+extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t groups,
+                                  int64_t group_len, int64_t heads, int64_t dim, const float* wq,
+                                  const float* bq, const float* wk, const float* bk,
+                                  const float* wv, const float* bv, const float* wo,
+                                  const float* bo, float dropout_p, uint64_t seed,
+                                  const ncf_step_clock* clock, float* q, float* k, float* v,
+                                  float* probs, float* o, float* y, void* stream) {
+  NCF_CHECK_ARG(groups >= 0 && ncf_attn_block_supported(dim, heads, group_len),
+                "ncf_attn_block_fwd: unsupported shape (D=%lld H=%lld M=%lld; need D=64, M<=%d)",
+                (long long)dim, (long long)heads, (long long)group_len, kMaxM);
+  NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_attn_block_fwd: dropout_p out of [0,1)");
+  NCF_CHECK_ARG(y != nullptr && (q != nullptr) == (k != nullptr) &&
+                (q != nullptr || (group_len == 1 && dropout_p == 0.0f)),
+                "ncf_attn_block_fwd: q/k must both be given unless M == 1 without dropout");
+  NCF_CHECK_ARG(q == nullptr || (probs != nullptr && o != nullptr),
+                "ncf_attn_block_fwd: the core path needs probs and o");
+  if (groups == 0) return NCF_OK;
+  const int M = (int)group_len;
+  const size_t lds = fwd_lds(M);
+  const dim3 grid((unsigned)ncf_cdiv(groups, kGroups));
+  hipStream_t st = (hipStream_t)stream;
+  const float scale = sqrtf((float)(dim / heads));
+#define NCF_ABF(HD)                                                                              \
+  case HD: {                                                                                     \
+    static bool attr = false;                                                                    \
+    if (!attr) { allow_lds(k_attn_block_fwd<HD>, fwd_lds(kMaxM)); attr = true; }                 \
+    hipLaunchKernelGGL(k_attn_block_fwd<HD>, grid, dim3(kThreads), lds, st, xu, xi, groups, M, wq, bq, \
+                       wk, bk, wv, bv, wo, bo, scale, dropout_p, seed, clock, q, k, v, probs, o,  \
+                       y);                                                                       \
+    break;                                                                                       \
+  }
+  switch (dim / heads) {
+    NCF_ABF(8)
+    NCF_ABF(16)
+    NCF_ABF(32)
+    NCF_ABF(64)
+  }
+#undef NCF_ABF
+  NCF_CHECK_LAUNCH("ncf_attn_block_fwd");
+  return NCF_OK;
+}
+
+extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const float* k,
+                                  const float* v, const float* probs, int64_t groups,
+                                  int64_t group_len, int64_t heads, int64_t dim, const float* wq,
+                                  const float* wk, const float* wv, const float* wo,
+                                  float dropout_p, uint64_t seed, const ncf_step_clock* clock,
+                                  float* grad_q, float* grad_k, float* grad_v, float* grad_xu,
+                                  float* grad_xi, void* stream) {
+  NCF_CHECK_ARG(groups >= 0 && ncf_attn_block_supported(dim, heads, group_len),
+                "ncf_attn_block_bwd: unsupported shape (D=%lld H=%lld M=%lld; need D=64, M<=%d)",
+                (long long)dim, (long long)heads, (long long)group_len, kMaxM);
+  NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_attn_block_bwd: dropout_p out of [0,1)");
+  if (groups == 0) return NCF_OK;
+  const int M = (int)group_len, H = (int)heads;
+  const size_t lds = bwd_lds(M, H);
+  const dim3 grid((unsigned)ncf_cdiv(groups, kGroups));
+  hipStream_t st = (hipStream_t)stream;
+  const float scale = sqrtf((float)(dim / heads));
+#define NCF_ABB(HD)                                                                               \
+  case HD: {                                                                                      \
+    static bool attr = false;                                                                     \
+    if (!attr) { allow_lds(k_attn_block_bwd<HD>, bwd_lds(kMaxM, kD / HD)); attr = true; }         \
+    hipLaunchKernelGGL(k_attn_block_bwd<HD>, grid, dim3(kThreads), lds, st, grad_y, q, k, v, probs,     \
+                       groups, M, wq, wk, wv, wo, scale, dropout_p, seed, clock, grad_q, grad_k,  \
+                       grad_v, grad_xu, grad_xi);                                                 \
+    break;                                                                                        \
+  }
+  switch (dim / heads) {
+    NCF_ABB(8)
+    NCF_ABB(16)
+    NCF_ABB(32)
+    NCF_ABB(64)
+  }
+#undef NCF_ABB
+  NCF_CHECK_LAUNCH("ncf_attn_block_bwd");
+  return NCF_OK;
+}

@@ -348,6 +348,52 @@ class NCFEngine:
                   ptr(w.xu), ptr(w.xi), ptr(w.umf), ptr(w.imf), ptr(w.err), st)
         # a5: MultiHeadAttention over each group of M rows (architecture.py:315-326)
         att = m.user_product_attention
+        if temporal is None and self.attn_block(D, H, M):
+            # projections + core + out_proj in one launch (attn_block.hip)
+            core = train or M != 1
+            _lib.call("ncf_attn_block_fwd", ptr(w.xu), ptr(w.xi), n // M, M, H, D,
+                      ptr(att.q_proj.weight), ptr(att.q_proj.bias), ptr(att.k_proj.weight),
+                      ptr(att.k_proj.bias), ptr(att.v_proj.weight), ptr(att.v_proj.bias),
+                      ptr(att.out_proj.weight), ptr(att.out_proj.bias),
+                      drop_p if train else 0.0, seed, ptr(self.clock),
+                      ptr(w.q) if core else None, ptr(w.k) if core else None,
+                      ptr(w.v) if core else None, ptr(w.P) if core else None,
+                      ptr(w.o) if core else None, ptr(w.y), st)
+            # a7: MLP tower on [attn ‖ zeros_T] (architecture.py:329-344): the zero temporal
+            # columns contribute nothing, so layer 0 reads only the first D columns of mlp.0.weight
+            x, ldx, kin = w.y, D, D
+        else:
+            x, ldx, kin = self._attention_unfused(w, M, train, drop_p, seed, temporal, st)
+        for l, h in enumerate(hid):
+            lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
+            ldw = lin.weight.shape[1]
+            self._gemm(x, ldx, 0, lin.weight, ldw, 1, w.r[l], h, n, h, kin, bias=lin.bias,
+                       relu=True, st=st)
+            _lib.call("ncf_relu_ln_dropout_fwd", ptr(w.r[l]), n, h, ptr(ln.weight), ptr(ln.bias),
+                      LN_EPS, drop_p if train else 0.0, (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1),
+                      ptr(self.clock), ptr(w.a[l]), ptr(w.mean[l]), ptr(w.rstd[l]), st)
+            x, ldx, kin = w.a[l], h, h
+        # a8: mlp_output + final Linear(2,1) + Sigmoid (architecture.py:345, 353-354)
+        _lib.call("ncf_head_fwd", ptr(x), n, hid[-1], ptr(m.mlp_output.weight),
+                  ptr(m.mlp_output.bias), ptr(w.mf_pred), ptr(m.final[0].weight),
+                  ptr(m.final[0].bias), ptr(w.mlp_pred), ptr(w.prob), st)
+        return w
+
+    def attn_block(self, D: int, H: int, M: int) -> bool:
+        """Whether the one-launch attention block (attn_block.hip) covers this geometry;
+        NCF_ATTN_BLOCK=0 forces the unfused launches (A/B measurement, parity tests)."""
+        if os.environ.get("NCF_ATTN_BLOCK", "1") == "0":
+            return False
+        return bool(_lib.query("ncf_attn_block_supported", D, H, M))
+
+    def _attention_unfused(self, w, M, train, drop_p, seed, temporal, st):
+        """a5 as separate launches (q/k/v projections, core, out_proj): any D, M <= 64, and the
+        forward_simple(hour) MLP input [attn ‖ hour_E]."""
+        m = self.model
+        dev = w.xu.device
+        n = w.g.n
+        D, H = w.g.D, w.g.H
+        att = m.user_product_attention
         if M == 1 and not train:
             # softmax over a single key is exactly 1 -> the core returns V unchanged
             self._gemm(w.xi, D, 0, att.v_proj.weight, D, 1, w.v, D, n, D, D, bias=att.v_proj.bias, st=st)
@@ -379,20 +425,7 @@ class NCFEngine:
                        bias=att.out_proj.bias, st=st)
             yt[:, D:].copy_(te)
             x, ldx, kin = yt, D + Tt, D + Tt
-        for l, h in enumerate(hid):
-            lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
-            ldw = lin.weight.shape[1]
-            self._gemm(x, ldx, 0, lin.weight, ldw, 1, w.r[l], h, n, h, kin, bias=lin.bias,
-                       relu=True, st=st)
-            _lib.call("ncf_relu_ln_dropout_fwd", ptr(w.r[l]), n, h, ptr(ln.weight), ptr(ln.bias),
-                      LN_EPS, drop_p if train else 0.0, (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1),
-                      ptr(self.clock), ptr(w.a[l]), ptr(w.mean[l]), ptr(w.rstd[l]), st)
-            x, ldx, kin = w.a[l], h, h
-        # a8: mlp_output + final Linear(2,1) + Sigmoid (architecture.py:345, 353-354)
-        _lib.call("ncf_head_fwd", ptr(x), n, hid[-1], ptr(m.mlp_output.weight),
-                  ptr(m.mlp_output.bias), ptr(w.mf_pred), ptr(m.final[0].weight),
-                  ptr(m.final[0].bias), ptr(w.mlp_pred), ptr(w.prob), st)
-        return w
+        return x, ldx, kin
 
     def check_ids(self, w: Workspace):
         if int(w.err.item()):
@@ -453,26 +486,20 @@ class NCFEngine:
             self._gemm(w.dlin[l], h, 0, lin.weight, ldw, 0, dx, kin, n, kin, h, st=st)
         # a5 backward: out_proj, core, q/k/v projections
         att = m.user_product_attention
-        src = w.o
-        self._wgrad(w, w.dy, D, src, D, gv("user_product_attention.out_proj.weight"), D, D, D, n,
-                    dbias=gv("user_product_attention.out_proj.bias"))
-        self._gemm(w.dy, D, 0, att.out_proj.weight, D, 0, w.do, D, n, D, D, st=st)
-        _lib.call("ncf_attention_bwd", ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P), ptr(w.do), n // M, M,
-                  H, D, drop_p, seed, ptr(self.clock), ptr(w.dS), ptr(w.dq), ptr(w.dk), ptr(w.dv), st)
-        for nm, dX, X in (("q_proj", w.dq, w.xu), ("k_proj", w.dk, w.xi), ("v_proj", w.dv, w.xi)):
-            self._wgrad(w, dX, D, X, D, gv(f"user_product_attention.{nm}.weight"), D, D, D, n,
-                        dbias=gv(f"user_product_attention.{nm}.bias"))
-        # attention weight gradients and dxu on side streams, dxi on this one
-        side = self.fork(dev, 2)
-        with torch.cuda.stream(side[0]):
-            w.run_wgrads(_lib.stream_ptr(dev), slot=1)
-        with torch.cuda.stream(side[1]):
-            self._gemm(w.dq, D, 0, att.q_proj.weight, D, 0, w.dxu, D, n, D, D,
-                       st=_lib.stream_ptr(dev))
-        self._gemm(w.dk, D, 0, att.k_proj.weight, D, 0, w.dxi, D, n, D, D, st=st)
-        self._gemm(w.dv, D, 0, att.v_proj.weight, D, 0, w.dxi, D, n, D, D, accum=True, st=st)
-        self.join(dev, side[1:])
-        joins.append(side[0])
+        if self.attn_block(D, H, M):
+            _lib.call("ncf_attn_block_bwd", ptr(w.dy), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P),
+                      n // M, M, H, D, ptr(att.q_proj.weight), ptr(att.k_proj.weight),
+                      ptr(att.v_proj.weight), ptr(att.out_proj.weight), drop_p, seed,
+                      ptr(self.clock), ptr(w.dq), ptr(w.dk), ptr(w.dv), ptr(w.dxu), ptr(w.dxi), st)
+            for nm, dY, X in (("out_proj", w.dy, w.o), ("q_proj", w.dq, w.xu),
+                              ("k_proj", w.dk, w.xi), ("v_proj", w.dv, w.xi)):
+                self._wgrad(w, dY, D, X, D, gv(f"user_product_attention.{nm}.weight"), D, D, D, n,
+                            dbias=gv(f"user_product_attention.{nm}.bias"))
+            joins.extend(self.fork(dev, 1))
+            with torch.cuda.stream(joins[-1]):
+                w.run_wgrads(_lib.stream_ptr(dev), slot=1)
+        else:
+            self._attention_bwd_unfused(w, drop_p, seed, joins, st)
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)
         tb = tables or self.table_params()
         G = w.G
@@ -493,6 +520,35 @@ class NCFEngine:
         self.join(dev, joins)
         w.run_reductions(st)
         self.pending = w
+
+    def _attention_bwd_unfused(self, w, drop_p, seed, joins, st):
+        """a5 backward as separate launches (any geometry the unfused forward takes)."""
+        m = self.model
+        g = w.g
+        n, D, H, M = g.n, g.D, g.H, g.M
+        dev = w.prob.device
+        gv = self.grad_view
+        att = m.user_product_attention
+        src = w.o
+        self._wgrad(w, w.dy, D, src, D, gv("user_product_attention.out_proj.weight"), D, D, D, n,
+                    dbias=gv("user_product_attention.out_proj.bias"))
+        self._gemm(w.dy, D, 0, att.out_proj.weight, D, 0, w.do, D, n, D, D, st=st)
+        _lib.call("ncf_attention_bwd", ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P), ptr(w.do), n // M, M,
+                  H, D, drop_p, seed, ptr(self.clock), ptr(w.dS), ptr(w.dq), ptr(w.dk), ptr(w.dv), st)
+        for nm, dX, X in (("q_proj", w.dq, w.xu), ("k_proj", w.dk, w.xi), ("v_proj", w.dv, w.xi)):
+            self._wgrad(w, dX, D, X, D, gv(f"user_product_attention.{nm}.weight"), D, D, D, n,
+                        dbias=gv(f"user_product_attention.{nm}.bias"))
+        # attention weight gradients and dxu on side streams, dxi on this one
+        side = self.fork(dev, 2)
+        with torch.cuda.stream(side[0]):
+            w.run_wgrads(_lib.stream_ptr(dev), slot=1)
+        with torch.cuda.stream(side[1]):
+            self._gemm(w.dq, D, 0, att.q_proj.weight, D, 0, w.dxu, D, n, D, D,
+                       st=_lib.stream_ptr(dev))
+        self._gemm(w.dk, D, 0, att.k_proj.weight, D, 0, w.dxi, D, n, D, D, st=st)
+        self._gemm(w.dv, D, 0, att.v_proj.weight, D, 0, w.dxi, D, n, D, D, accum=True, st=st)
+        self.join(dev, side[1:])
+        joins.append(side[0])
 
     # ------------------------------------------------------------------ optimizer
     def table_state_tensors(self):

@@ -463,6 +463,53 @@ def _fused_run(deferred, steps, sweep_every=64, U=3000, I=500, B=64, seed=11, dr
     return sd, mom
 
 
+@pytest.mark.parametrize("H,M,B", [(4, 5, 37), (1, 5, 16), (8, 3, 50), (2, 6, 33), (4, 1, 20)])
+def test_attn_block_matches_unfused(monkeypatch, H, M, B):
+    """The one-launch attention block (attn_block.hip) vs the unfused launches (projection
+    GEMMs + attention.hip core), dropout on (same stream): one fused train step's probabilities,
+    dense gradients and compact table gradients agree to the grads tolerance.  B not a multiple
+    of the 16-group tile exercises the ragged last workgroup."""
+    from ncf_amd.trainer import FusedTrainStep
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("NCF_ATTN_BLOCK", flag)
+        torch.manual_seed(21)
+        m = ncf.AdvancedNCF(400, 300, 5, 24, 64, 64, 32, [256, 128, 64], H, 0.2, M - 1).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+        assert m.engine.attn_block(64, H, M) == (flag == "1")
+        g = torch.Generator().manual_seed(22)
+        u = torch.randint(0, 400, (B,), generator=g).repeat_interleave(M).to(DEV)
+        i = torch.randint(0, 300, (B * M,), generator=g).to(DEV)
+        t = torch.zeros(B, M)
+        t[:, 0] = 1
+        w = step(u, i, t.reshape(-1, 1).to(DEV))
+        torch.cuda.synchronize()
+        nu = w.num_unique.cpu().tolist()   # compact rows in use: [users, items]
+        out.append((w.prob.cpu().clone(), m.engine.flat_grad.cpu().clone(),
+                    {k: v[:nu[0 if k.endswith("user") else 1]].cpu().clone() for k, v in w.G.items()},
+                    w.y.cpu().clone()))
+    (p0, g0, G0, y0), (p1, g1, G1, y1) = out
+    torch.testing.assert_close(y1, y0, rtol=0, atol=2e-6)
+    torch.testing.assert_close(p1, p0, rtol=0, atol=2e-6)
+    torch.testing.assert_close(g1, g0, rtol=1e-4, atol=1e-6)
+    for k in G0:
+        torch.testing.assert_close(G1[k], G0[k], rtol=1e-4, atol=1e-6)
+
+
+def test_attn_block_eval_forward_matches_unfused(monkeypatch):
+    """Eval (M = 1): the block's no-core form (o = v) vs the unfused v/out projections."""
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("NCF_ATTN_BLOCK", flag)
+        torch.manual_seed(23)
+        m = ncf.AdvancedNCF(300, 200, 5, 24).to(DEV).eval()
+        u = torch.randint(0, 300, (1000,), device=DEV)
+        i = torch.randint(0, 200, (1000,), device=DEV)
+        with torch.no_grad():
+            res.append(m.forward_simple(u, i).cpu())
+    torch.testing.assert_close(res[1], res[0], rtol=0, atol=2e-6)
+
+
 @pytest.mark.parametrize("sweep_every", [64, 0])
 def test_deferred_adam_bitwise_equals_dense(sweep_every):
     """The deferred schedule reproduces the dense-exact sweep bit for bit (70 steps: crosses a
