@@ -77,6 +77,11 @@ int ncf_gather_ln_gmf_scaled_fwd(const int64_t* user_ids, const int64_t* item_id
 int ncf_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t rows,
                     int64_t dim, const float* ln_gamma, const float* ln_beta, float eps,
                     float* out, int* err_flag, void* stream);
+/* 8f rank 2, ANN feed (generate_embeddings.py:201-221): ncf_gather_rows + each row divided by
+ * its L2 norm when l2_normalize != 0 (the product "mlp" vectors for the JSONL export). */
+int ncf_embedding_export(const int64_t* ids, int64_t n, const float* table, int64_t rows,
+                         int64_t dim, const float* ln_gamma, const float* ln_beta, float eps,
+                         int l2_normalize, float* out, int* err_flag, void* stream);
 
 /* ---- dense layers: fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32) --------------------------------
  * Replaces the addmm/mm of the attention projections (architecture.py:40-42, :57) and the MLP
@@ -194,6 +199,59 @@ int ncf_attn_block_bwd(const float* grad_y, const float* q, const float* k, cons
                        const float* wo, float dropout_p, uint64_t seed,
                        const ncf_step_clock* clock, float* grad_q, float* grad_k, float* grad_v,
                        float* grad_xu, float* grad_xi, void* stream);
+
+/* ---- a7 + a8 fused: the MLP tower in one launch per direction (input 64, hidden [256,128,64];
+ * ncf_mlp_fused_supported).  Layer l = mlp.{4l} Linear (w [N_l][ldw], first K_l columns used:
+ * mlp.0's temporal columns see zeros), mlp.{4l+2} LayerNorm (gamma, beta); dropout seed of layer
+ * l = (seed + 0x9E37*(l+1)) & (2^63-1) (+ clock), the unfused path's stream.
+ * Forward: r = relu(x W^T + b), mean/rstd, a = dropout(LN(r)) per layer (r/a/mean/rstd may be
+ *   NULL: not saved), then mlp_pred = a_2 . mlp_out_w + mlp_out_b and
+ *   prob = sigmoid(final_w[0] mf_pred + final_w[1] mlp_pred + final_b) (the ncf_head_fwd math).
+ * Backward: from dL/da_2 (ncf_head_bwd's grad_mlp_last) -> dlin per layer (written: the weight
+ *   gradients' dY), grad_x = dL/dx [n,64]; dbias/dgamma/dbeta per layer through the workspace
+ *   (deferred into `defer` when given).                                                       */
+typedef struct ncf_mlp_layer {
+  const float* w;
+  int64_t ldw;
+  const float* b;
+  const float* gamma;
+  const float* beta;
+  float* r;
+  float* a;
+  float* mean;
+  float* rstd;
+  float* dlin;
+  float* dbias;
+  float* dgamma;
+  float* dbeta;
+} ncf_mlp_layer;
+int ncf_mlp_fused_supported(int64_t dim, int64_t n_layers, const int64_t* hidden);
+int ncf_mlp_fwd(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
+                int64_t n_layers, const int64_t* hidden, float eps, float dropout_p, uint64_t seed,
+                const ncf_step_clock* clock, const float* mlp_out_w, const float* mlp_out_b,
+                const float* mf_pred, const float* final_w, const float* final_b, float* mlp_pred,
+                float* prob, void* stream);
+int64_t ncf_mlp_bwd_workspace(int64_t n);
+int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
+                int64_t n_layers, const int64_t* hidden, float dropout_p, uint64_t seed,
+                const ncf_step_clock* clock, float* grad_x, float* workspace,
+                int64_t workspace_floats, ncf_reduce_list* defer, void* stream);
+
+/* ---- 8f rank 1: device-side training batches (data_prep.py:95-161, 181-313) --------------
+ * ncf_alias_build (HOST function, once per dataset): Walker/Vose alias table of the
+ *   inverse-popularity weights.
+ * ncf_sample_negatives: per interaction b, rows b*(1+k) .. b*(1+k)+k of the KJT batch:
+ *   out_users = user, out_items = [pos, k negatives], out_targets = [1, 0, ...].  A negative is
+ *   an alias-table draw rejected when it is the positive or in the user's history (CSR:
+ *   hist_items[hist_offsets[u] .. hist_offsets[u+1]) sorted ascending; NULL offsets = no
+ *   history), up to max_attempts draws, then uniform over the items outside history + {pos}
+ *   (any item but pos when that set is empty).  Deterministic in (inputs, seed). */
+int ncf_alias_build(const double* weights, int64_t n, float* prob, int32_t* alias);
+int ncf_sample_negatives(const int64_t* users, const int64_t* pos_items, int64_t batch,
+                         int64_t negatives, const float* alias_prob, const int32_t* alias_idx,
+                         int64_t n_items, const int64_t* hist_offsets, const int32_t* hist_items,
+                         int64_t n_users, uint64_t seed, int64_t max_attempts, int64_t* out_users,
+                         int64_t* out_items, float* out_targets, int* err_flag, void* stream);
 
 /* ---- a6: TemporalEncoding (architecture.py:59-94): hour/day/month rows + pe[days mod P] -- */
 int ncf_temporal_fwd(const int64_t* hour, const int64_t* day, const int64_t* month,

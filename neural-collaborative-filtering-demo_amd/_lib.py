@@ -54,6 +54,13 @@ SIGNATURES = {
     "ncf_attention_fwd": (I32, [P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P]),
     "ncf_attention_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P, P, P]),
     "ncf_attn_block_supported": (I32, [I64, I64, I64]),
+    "ncf_mlp_fused_supported": (I32, [I64, I64, P]),
+    "ncf_alias_build": (I32, [P, I64, P, P]),
+    "ncf_embedding_export": (I32, [P, I64, P, I64, I64, P, P, F32, I32, P, P, P]),
+    "ncf_sample_negatives": (I32, [P, P, I64, I64, P, P, I64, P, P, I64, U64, I64, P, P, P, P, P]),
+    "ncf_mlp_fwd": (I32, [P, I64, I64, P, I64, P, F32, F32, U64, P, P, P, P, P, P, P, P, P]),
+    "ncf_mlp_bwd_workspace": (I64, [I64]),
+    "ncf_mlp_bwd": (I32, [P, I64, I64, P, I64, P, F32, U64, P, P, P, I64, P, P]),
     "ncf_attn_block_fwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, F32, U64, P,
                                  P, P, P, P, P, P, P]),
     "ncf_attn_block_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, P, P, P, P, F32, U64, P, P,
@@ -131,6 +138,12 @@ class WgradDesc(ctypes.Structure):
 
 
 WGRAD_GROUP_MAX = 8
+
+
+class MlpLayer(ctypes.Structure):
+    """ncf_mlp_layer (include/ncf_hip.h)."""
+    _fields_ = [("w", P), ("ldw", I64), ("b", P), ("gamma", P), ("beta", P), ("r", P), ("a", P),
+                ("mean", P), ("rstd", P), ("dlin", P), ("dbias", P), ("dgamma", P), ("dbeta", P)]
 
 
 class TablePair(ctypes.Structure):

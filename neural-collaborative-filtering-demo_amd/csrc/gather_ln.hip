@@ -79,8 +79,10 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
 
 // Plain row gather (EBC forward as seen by callers such as app.py:156-184) with optional LN
 // (get_user_embeddings / get_product_embeddings, architecture.py:383-407).
-template <int D>
-__global__ __launch_bounds__(256) void k_gather_rows(const int64_t* __restrict__ ids, int64_t n,
+// L2 = true: each (LN'd) row divided by its Euclidean norm (the ANN export of
+// generate_embeddings.py:209-211, final_vec / np.linalg.norm(final_vec))
+template <int D, bool L2>
+__global__ __launch_bounds__(256) void k_gather_rows_t(const int64_t* __restrict__ ids, int64_t n,
                                                      const float* __restrict__ table, int64_t rows,
                                                      const float* __restrict__ g,
                                                      const float* __restrict__ b, float eps,
@@ -94,6 +96,10 @@ __global__ __launch_bounds__(256) void k_gather_rows(const int64_t* __restrict__
   const int c = sub * 4;
   float4 x = ld4(table + id * D + c);
   if (g) x = RowLN<D>::ln(x, ld4(g + c), ld4(b + c), eps);
+  if (L2) {
+    const float nrm = sqrtf(group_sum<L>(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w));
+    x = make_float4(x.x / nrm, x.y / nrm, x.z / nrm, x.w / nrm);
+  }
   st4(out + row * D + c, x);
 }
 
@@ -118,9 +124,20 @@ int launch_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_
                        const float* g, const float* b, float eps, float* out, int* err,
                        hipStream_t st) {
   const int64_t threads = n * (D / 4);
-  hipLaunchKernelGGL(k_gather_rows<D>, dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st, ids, n,
-                     table, rows, g, b, eps, out, err);
+  hipLaunchKernelGGL((k_gather_rows_t<D, false>), dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st,
+                     ids, n, table, rows, g, b, eps, out, err);
   NCF_CHECK_LAUNCH("ncf_gather_rows");
+  return NCF_OK;
+}
+
+template <int D>
+int launch_gather_rows_l2(const int64_t* ids, int64_t n, const float* table, int64_t rows,
+                          const float* g, const float* b, float eps, float* out, int* err,
+                          hipStream_t st) {
+  const int64_t threads = n * (D / 4);
+  hipLaunchKernelGGL((k_gather_rows_t<D, true>), dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st,
+                     ids, n, table, rows, g, b, eps, out, err);
+  NCF_CHECK_LAUNCH("ncf_embedding_export");
   return NCF_OK;
 }
 
@@ -181,5 +198,19 @@ extern "C" int ncf_gather_rows(const int64_t* ids, int64_t n, const float* table
   NCF_CHECK_ARG(ids && table && out, "ncf_gather_rows: null pointer");
   NCF_CHECK_ARG((ln_gamma == nullptr) == (ln_beta == nullptr), "ncf_gather_rows: gamma/beta mismatch");
   NCF_DISPATCH_D(dim, launch_gather_rows, ids, n, table, rows, ln_gamma, ln_beta, eps, out,
+                 err_flag, (hipStream_t)stream);
+}
+
+extern "C" int ncf_embedding_export(const int64_t* ids, int64_t n, const float* table, int64_t rows,
+                                    int64_t dim, const float* ln_gamma, const float* ln_beta,
+                                    float eps, int l2_normalize, float* out, int* err_flag,
+                                    void* stream) {
+  NCF_CHECK_ARG(n >= 0 && rows >= 0, "ncf_embedding_export: negative size");
+  if (n == 0) return NCF_OK;
+  NCF_CHECK_ARG(ids && table && out, "ncf_embedding_export: null pointer");
+  NCF_CHECK_ARG((ln_gamma == nullptr) == (ln_beta == nullptr), "ncf_embedding_export: gamma/beta mismatch");
+  if (!l2_normalize)
+    return ncf_gather_rows(ids, n, table, rows, dim, ln_gamma, ln_beta, eps, out, err_flag, stream);
+  NCF_DISPATCH_D(dim, launch_gather_rows_l2, ids, n, table, rows, ln_gamma, ln_beta, eps, out,
                  err_flag, (hipStream_t)stream);
 }

@@ -1,0 +1,425 @@
+// The MLP tower of AdvancedNCF in one launch per direction: 3 x [Linear -> ReLU -> LayerNorm ->
+// Dropout] (+ mlp_output and the final fusion in the forward), for input width 64 and hidden
+// widths [256, 128, 64] (the reference defaults, C2).
+//
+// Reference: self.mlp (src/model/architecture.py:230-242, applied :344), mlp_output (:246, :345),
+// final Linear(2,1) + Sigmoid (:249-252, :353-354).  Same math and dropout stream as the
+// unfused path (GEMM with ReLU epilogue + rowops.hip + head.hip): LayerNorm of the ReLU output
+// with the two-pass mean/variance, dropout keep decisions from ncf_dropout_scale4 at element
+// index row*W + col with the per-layer seed (seed + 0x9E37*(l+1)) & (2^63-1) (+ the step clock).
+// Only the fmaf order of the Linear layers (k-permuted MFMA below) differs.
+//
+// Tiling: a 256-thread workgroup (4 waves) owns kRows = 16 rows for the whole tower; the rows
+// live in LDS between layers (buffers Q [16][260] and P [16][196], 29 KB: five workgroups per
+// CU, so the 1280 workgroups of a 20,480-row step are resident at once and hide each other's
+// latencies).  Row ops run in place; a layer's output goes to the other buffer.
+//  * Linear: 16x16 output tiles of v_mfma_f32_16x16x4_f32; wave w takes column slices w + 4q.  k-permuted operands: in MFMA step s lane group g = lane>>4
+//    supplies k = g*K/4 + s, so a lane's A row slice (LDS) and weight row slice (global/L2) are
+//    contiguous float4 runs.  Two accumulators (even / odd float4 chunks) halve the dependent
+//    MFMA chain.
+//  * Row ops: 16 lanes per row, width/64 float4 chunks per lane (the column map of rowops.hip).
+// Forward writes what the backward and the weight gradients read (r, a, mean, rstd; NULL
+// pointers skip them in eval).  Backward starts from dL/da of the last layer (head.hip), writes
+// dlin per layer (the weight gradients' dY) and dX of the tower input, and leaves per-workgroup
+// partial column sums [dbias | dgamma | dbeta] per layer for one deferred reduction each.
+#include "ncf_common.h"
+
+namespace {
+
+constexpr int kRows = 16;
+constexpr int kThreads = 256;
+constexpr int kPQ = 260;   // pitch of buffer Q (<= 256 columns)
+constexpr int kPP = 196;   // pitch of buffer P (<= 128 columns; 4 x 3 x 256 scratch floats)
+constexpr int K0 = 64, N0 = 256, N1 = 128, N2 = 64;
+constexpr int kPartW = 3 * (N0 + N1 + N2);   // partial floats per workgroup
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct TowerArgs {
+  ncf_mlp_layer l[3];
+  uint64_t seed[3];
+};
+
+__device__ __forceinline__ float4 lds4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void lds4_st(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ f32x4 mfma4(float4 a, float4 b, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+  return acc;
+}
+
+// Y[16 x N] = relu(X[16 x K] . W^T + b)   (W row-major [N][ldw], first K columns)
+template <int K, int N, int PX, int PY>
+__device__ __forceinline__ void lin_fwd(const float* __restrict__ X, float* __restrict__ Y,
+                                        const float* __restrict__ W, int64_t ldw,
+                                        const float* __restrict__ bias) {
+  constexpr int KQ = K / 4;
+  constexpr int PER = N / 64;
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  const float* ap = X + i * PX + g * KQ;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int cs = wv + 4 * q;
+    const float* wp = W + (int64_t)(16 * cs + i) * ldw + g * KQ;
+    const float bb = bias[16 * cs + i];
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KQ / 4; ++c) {
+      const float4 b = ld4(wp + 4 * c);
+      const float4 a = lds4(ap + 4 * c);
+      if (c & 1) acc1 = mfma4(a, b, acc1);
+      else acc0 = mfma4(a, b, acc0);
+    }
+    float* yp = Y + (4 * g) * PY + 16 * cs + i;   // C: rows 4g + r, column 16cs + (lane & 15)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) yp[r * PY] = fmaxf(acc0[r] + acc1[r] + bb, 0.0f);
+  }
+}
+
+// G[16 x NO] = DL[16 x KC] . W   (W row-major [KC][ldw], first NO columns)
+template <int KC, int NO, int PD, int PG>
+__device__ __forceinline__ void lin_bwd(const float* __restrict__ DL, float* __restrict__ G,
+                                        const float* __restrict__ W, int64_t ldw) {
+  constexpr int KQ = KC / 4;
+  constexpr int PER = NO / 64;
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  const float* ap = DL + i * PD + g * KQ;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int cs = wv + 4 * q;
+    const float* wp = W + (int64_t)(g * KQ) * ldw + 16 * cs + i;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KQ / 4; ++c) {
+      const float4 b = make_float4(wp[(4 * c) * ldw], wp[(4 * c + 1) * ldw], wp[(4 * c + 2) * ldw],
+                                   wp[(4 * c + 3) * ldw]);
+      const float4 a = lds4(ap + 4 * c);
+      if (c & 1) acc1 = mfma4(a, b, acc1);
+      else acc0 = mfma4(a, b, acc0);
+    }
+    float* gp = G + (4 * g) * PG + 16 * cs + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gp[r * PG] = acc0[r] + acc1[r];
+  }
+}
+
+// LayerNorm + dropout of the ReLU rows in Y, in place (the next layer's input); saves r, a,
+// mean, rstd.  Returns the row's dot product with hw (the mlp_output weight) when hw != NULL.
+template <int N, int PY>
+__device__ __forceinline__ float ln_fwd(float* __restrict__ Y, int64_t row0, int rows,
+                                        const ncf_mlp_layer& L, float eps, float p, uint64_t seed,
+                                        const float* __restrict__ hw) {
+  constexpr int CH = N / 64;
+  const int rr = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int64_t row = row0 + rr;
+  const bool ok = rr < rows;
+  float4 x[CH];
+  float s = 0.0f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 16 + sub) * 4;
+    x[c] = lds4(Y + rr * PY + col);
+    if (ok && L.r) st4(L.r + row * N + col, x[c]);
+    s += x[c].x + x[c].y + x[c].z + x[c].w;
+  }
+  const float mean = group_sum<16>(s) * (1.0f / N);
+  float qv = 0.0f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    x[c].x -= mean; x[c].y -= mean; x[c].z -= mean; x[c].w -= mean;
+    qv += x[c].x * x[c].x + x[c].y * x[c].y + x[c].z * x[c].z + x[c].w * x[c].w;
+  }
+  const float rstd = 1.0f / sqrtf(group_sum<16>(qv) * (1.0f / N) + eps);
+  const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  float dot = 0.0f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 16 + sub) * 4;
+    const float4 gg = ld4(L.gamma + col), bb = ld4(L.beta + col);
+    float4 y = make_float4(x[c].x * rstd * gg.x + bb.x, x[c].y * rstd * gg.y + bb.y,
+                           x[c].z * rstd * gg.z + bb.z, x[c].w * rstd * gg.w + bb.w);
+    if (p > 0.0f) {
+      const float4 k = ncf_dropout_scale4(seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
+      y.x *= k.x; y.y *= k.y; y.z *= k.z; y.w *= k.w;
+    }
+    lds4_st(Y + rr * PY + col, y);
+    if (ok && L.a) st4(L.a + row * N + col, y);
+    if (hw) {
+      const float4 h = ld4(hw + col);
+      dot = fmaf(y.x, h.x, dot); dot = fmaf(y.y, h.y, dot);
+      dot = fmaf(y.z, h.z, dot); dot = fmaf(y.w, h.w, dot);
+    }
+  }
+  if (ok && sub == 0 && L.mean) {
+    L.mean[row] = mean;
+    L.rstd[row] = rstd;
+  }
+  return hw ? group_sum<16>(dot) : 0.0f;
+}
+
+// Backward of dropout -> LayerNorm -> ReLU for the 16 rows, in place: G (dL/da) -> dL/dlin
+// (also to HBM); this workgroup's column sums [dbias | dgamma | dbeta] -> part[0 : 3N), through
+// the free buffer S (4 waves x 3N floats).
+template <int N, int PG>
+__device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict__ S, int64_t row0,
+                                       int rows, const ncf_mlp_layer& L, float p, uint64_t seed,
+                                       float* __restrict__ part) {
+  constexpr int CH = N / 64;
+  const int rr = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int wv = threadIdx.x >> 6;
+  const int64_t row = row0 + rr;
+  const bool ok = rr < rows;
+  const float mu = ok ? L.mean[row] : 0.0f, rs = ok ? L.rstd[row] : 0.0f;
+  const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  float4 gd[CH], xh[CH];
+  uint32_t pos = 0;   // ReLU mask: bit 4c + e <=> r > 0
+  float s1 = 0.0f, s2 = 0.0f;
+#define NCF_R4(v)                                  \
+  v += __shfl_xor(v, 16, 64);                      \
+  v += __shfl_xor(v, 32, 64);
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 16 + sub) * 4;
+    float4 d = lds4(G + rr * PG + col);
+    if (p > 0.0f) {
+      const float4 k = ncf_dropout_scale4(seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
+      d.x *= k.x; d.y *= k.y; d.z *= k.z; d.w *= k.w;
+    }
+    const float4 x = ok ? ld4(L.r + row * N + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 gg = ld4(L.gamma + col);
+    const float4 h = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
+    pos |= ((x.x > 0.0f ? 1u : 0u) | (x.y > 0.0f ? 2u : 0u) | (x.z > 0.0f ? 4u : 0u) |
+            (x.w > 0.0f ? 8u : 0u)) << (4 * c);
+    float4 ag = make_float4(d.x * h.x, d.y * h.y, d.z * h.z, d.w * h.w);
+    float4 ab = d;
+    gd[c] = make_float4(d.x * gg.x, d.y * gg.y, d.z * gg.z, d.w * gg.w);
+    s1 += gd[c].x + gd[c].y + gd[c].z + gd[c].w;
+    s2 += gd[c].x * h.x + gd[c].y * h.y + gd[c].z * h.z + gd[c].w * h.w;
+    xh[c] = h;
+    // dgamma / dbeta column sums over the wave's 4 rows -> S (the free buffer)
+    NCF_R4(ag.x) NCF_R4(ag.y) NCF_R4(ag.z) NCF_R4(ag.w)
+    NCF_R4(ab.x) NCF_R4(ab.y) NCF_R4(ab.z) NCF_R4(ab.w)
+    if ((threadIdx.x & 63) < 16) {
+      lds4_st(S + wv * 3 * N + N + col, ag);
+      lds4_st(S + wv * 3 * N + 2 * N + col, ab);
+    }
+  }
+  const float m1 = group_sum<16>(s1) * (1.0f / N);
+  const float m2 = group_sum<16>(s2) * (1.0f / N);
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 16 + sub) * 4;
+    const uint32_t mk = pos >> (4 * c);
+    float4 o;
+    o.x = (mk & 1u) ? rs * (gd[c].x - m1 - xh[c].x * m2) : 0.0f;
+    o.y = (mk & 2u) ? rs * (gd[c].y - m1 - xh[c].y * m2) : 0.0f;
+    o.z = (mk & 4u) ? rs * (gd[c].z - m1 - xh[c].z * m2) : 0.0f;
+    o.w = (mk & 8u) ? rs * (gd[c].w - m1 - xh[c].w * m2) : 0.0f;
+    lds4_st(G + rr * PG + col, o);
+    if (ok) st4(L.dlin + row * N + col, o);
+    // dbias column sums over the wave's 4 rows -> S
+    NCF_R4(o.x) NCF_R4(o.y) NCF_R4(o.z) NCF_R4(o.w)
+    if ((threadIdx.x & 63) < 16) lds4_st(S + wv * 3 * N + col, o);
+  }
+#undef NCF_R4
+  __syncthreads();
+  for (int e = threadIdx.x; e < 3 * N; e += kThreads) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s += S[w * 3 * N + e];
+    part[e] = s;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kThreads, 5) void k_mlp_fwd(
+    const float* __restrict__ xin, int64_t n, TowerArgs a, float eps, float p,
+    const ncf_step_clock* clock, const float* __restrict__ w_out, const float* __restrict__ b_out,
+    const float* __restrict__ mf_pred, const float* __restrict__ w_fin,
+    const float* __restrict__ b_fin, float* __restrict__ mlp_pred, float* __restrict__ prob) {
+  extern __shared__ float lds[];
+  float* Q = lds;                  // [16][kPQ]: layer 0 out (256), layer 2 out (64)
+  float* P = lds + kRows * kPQ;    // [16][kPP]: input x (64), layer 1 out (128)
+  const int64_t row0 = (int64_t)blockIdx.x * kRows;
+  const int rows = (int)min<int64_t>(kRows, n - row0);
+  const uint64_t cs = clock ? clock->seed : 0ull;
+  for (int e = threadIdx.x; e < kRows * (K0 / 4); e += kThreads) {
+    const int r = e / (K0 / 4), c = (e % (K0 / 4)) * 4;
+    lds4_st(P + r * kPP + c,
+            r < rows ? ld4(xin + (row0 + r) * K0 + c) : make_float4(0.f, 0.f, 0.f, 0.f));
+  }
+  __syncthreads();
+  lin_fwd<K0, N0, kPP, kPQ>(P, Q, a.l[0].w, a.l[0].ldw, a.l[0].b);
+  __syncthreads();
+  ln_fwd<N0, kPQ>(Q, row0, rows, a.l[0], eps, p, a.seed[0] + cs, nullptr);
+  __syncthreads();
+  lin_fwd<N0, N1, kPQ, kPP>(Q, P, a.l[1].w, a.l[1].ldw, a.l[1].b);
+  __syncthreads();
+  ln_fwd<N1, kPP>(P, row0, rows, a.l[1], eps, p, a.seed[1] + cs, nullptr);
+  __syncthreads();
+  lin_fwd<N1, N2, kPP, kPQ>(P, Q, a.l[2].w, a.l[2].ldw, a.l[2].b);
+  __syncthreads();
+  const float dot = ln_fwd<N2, kPQ>(Q, row0, rows, a.l[2], eps, p, a.seed[2] + cs, w_out);
+  const int rr = threadIdx.x >> 4;
+  if ((threadIdx.x & 15) == 0 && rr < rows) {
+    const int64_t row = row0 + rr;
+    const float mp = dot + b_out[0];
+    mlp_pred[row] = mp;
+    const float z = w_fin[0] * mf_pred[row] + w_fin[1] * mp + b_fin[0];
+    prob[row] = 1.0f / (1.0f + expf(-z));
+  }
+}
+
+__global__ __launch_bounds__(kThreads, 5) void k_mlp_bwd(const float* __restrict__ g_last, int64_t n,
+                                                      TowerArgs a, float p,
+                                                      const ncf_step_clock* clock,
+                                                      float* __restrict__ dx,
+                                                      float* __restrict__ part) {
+  extern __shared__ float lds[];
+  float* Q = lds;
+  float* P = lds + kRows * kPQ;
+  const int64_t row0 = (int64_t)blockIdx.x * kRows;
+  const int rows = (int)min<int64_t>(kRows, n - row0);
+  const uint64_t cs = clock ? clock->seed : 0ull;
+  float* pp = part + (int64_t)blockIdx.x * kPartW;
+  for (int e = threadIdx.x; e < kRows * (N2 / 4); e += kThreads) {
+    const int r = e / (N2 / 4), c = (e % (N2 / 4)) * 4;
+    lds4_st(Q + r * kPQ + c,
+            r < rows ? ld4(g_last + (row0 + r) * N2 + c) : make_float4(0.f, 0.f, 0.f, 0.f));
+  }
+  __syncthreads();
+  ln_bwd<N2, kPQ>(Q, P, row0, rows, a.l[2], p, a.seed[2] + cs, pp);
+  lin_bwd<N2, N1, kPQ, kPP>(Q, P, a.l[2].w, a.l[2].ldw);
+  __syncthreads();
+  ln_bwd<N1, kPP>(P, Q, row0, rows, a.l[1], p, a.seed[1] + cs, pp + 3 * N2);
+  lin_bwd<N1, N0, kPP, kPQ>(P, Q, a.l[1].w, a.l[1].ldw);
+  __syncthreads();
+  ln_bwd<N0, kPQ>(Q, P, row0, rows, a.l[0], p, a.seed[0] + cs, pp + 3 * (N2 + N1));
+  lin_bwd<N0, K0, kPQ, kPP>(Q, P, a.l[0].w, a.l[0].ldw);
+  __syncthreads();
+  for (int e = threadIdx.x; e < rows * (K0 / 4); e += kThreads) {
+    const int r = e / (K0 / 4), c = (e % (K0 / 4)) * 4;
+    st4(dx + (row0 + r) * K0 + c, lds4(P + r * kPP + c));
+  }
+}
+
+constexpr size_t kLds = sizeof(float) * kRows * (kPQ + kPP);
+static_assert(4 * 3 * N0 <= kRows * kPP, "ln_bwd scratch must fit in buffer P");
+
+bool tower_ok(int64_t dim, int64_t n_layers, const int64_t* hidden) {
+  return dim == K0 && n_layers == 3 && hidden && hidden[0] == N0 && hidden[1] == N1 &&
+         hidden[2] == N2;
+}
+
+int make_args(const ncf_mlp_layer* layers, uint64_t seed, TowerArgs& a) {
+  for (int l = 0; l < 3; ++l) {
+    a.l[l] = layers[l];
+    if (!a.l[l].w || !a.l[l].b || !a.l[l].gamma || !a.l[l].beta || a.l[l].ldw < (l ? 0 : K0) ||
+        (a.l[l].ldw & 3)) {
+      ncf_set_error("ncf_mlp: layer %d needs w/b/gamma/beta and a float4-aligned ldw", l);
+      return NCF_ERR_ARG;
+    }
+    a.seed[l] = (seed + 0x9E37ull * (uint64_t)(l + 1)) & 0x7FFFFFFFFFFFFFFFull;
+  }
+  return NCF_OK;
+}
+
+}  // namespace
+
+extern "C" int ncf_mlp_fused_supported(int64_t dim, int64_t n_layers, const int64_t* hidden) {
+  return tower_ok(dim, n_layers, hidden) ? 1 : 0;
+}
+
+extern "C" int ncf_mlp_fwd(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
+                           int64_t n_layers, const int64_t* hidden, float eps, float dropout_p,
+                           uint64_t seed, const ncf_step_clock* clock, const float* mlp_out_w,
+                           const float* mlp_out_b, const float* mf_pred, const float* final_w,
+                           const float* final_b, float* mlp_pred, float* prob, void* stream) {
+  NCF_CHECK_ARG(n >= 0 && tower_ok(dim, n_layers, hidden),
+                "ncf_mlp_fwd: unsupported tower (need input 64, hidden [256,128,64])");
+  NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_mlp_fwd: dropout_p out of [0,1)");
+  if (n == 0) return NCF_OK;
+  TowerArgs a;
+  const int rc = make_args(layers, seed, a);
+  if (rc) return rc;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_mlp_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_mlp_fwd, dim3((unsigned)ncf_cdiv(n, kRows)), dim3(kThreads), kLds,
+                     (hipStream_t)stream, x, n, a, eps, dropout_p, clock, mlp_out_w, mlp_out_b,
+                     mf_pred, final_w, final_b, mlp_pred, prob);
+  NCF_CHECK_LAUNCH("ncf_mlp_fwd");
+  return NCF_OK;
+}
+
+extern "C" int64_t ncf_mlp_bwd_workspace(int64_t n) {
+  const int64_t nb = n == 0 ? 1 : ncf_cdiv(n, kRows);
+  return nb * kPartW + 3 * ncf_reduce_scratch((int)nb, 3 * N0);
+}
+
+extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim,
+                           const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
+                           float dropout_p, uint64_t seed, const ncf_step_clock* clock,
+                           float* grad_x, float* workspace, int64_t workspace_floats,
+                           ncf_reduce_list* defer, void* stream) {
+  NCF_CHECK_ARG(n >= 0 && tower_ok(dim, n_layers, hidden),
+                "ncf_mlp_bwd: unsupported tower (need input 64, hidden [256,128,64])");
+  NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_mlp_bwd: dropout_p out of [0,1)");
+  if (workspace_floats < ncf_mlp_bwd_workspace(n)) {
+    ncf_set_error("ncf_mlp_bwd: workspace too small");
+    return NCF_ERR_WORKSPACE;
+  }
+  if (n == 0) return NCF_OK;
+  TowerArgs a;
+  int rc = make_args(layers, seed, a);
+  if (rc) return rc;
+  for (int l = 0; l < 3; ++l)
+    if (!a.l[l].r || !a.l[l].mean || !a.l[l].rstd || !a.l[l].dlin || !a.l[l].dgamma ||
+        !a.l[l].dbeta || !a.l[l].dbias) {
+      ncf_set_error("ncf_mlp_bwd: layer %d needs r/mean/rstd/dlin/dbias/dgamma/dbeta", l);
+      return NCF_ERR_ARG;
+    }
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_mlp_bwd, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kLds);
+    attr = true;
+  }
+  const int nb = (int)ncf_cdiv(n, kRows);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_mlp_bwd, dim3((unsigned)nb), dim3(kThreads), kLds, st, grad_a_last, n, a,
+                     dropout_p, clock, grad_x, workspace);
+  NCF_CHECK_LAUNCH("ncf_mlp_bwd");
+  // per layer: [dbias | dgamma | dbeta] partial columns -> one strided reduction when the three
+  // outputs are equally spaced (consecutive parameters of the flat gradient buffer)
+  ncf_reduce_list local;
+  local.count = 0;
+  ncf_reduce_list* lst = defer ? defer : &local;
+  const int widths[3] = {N0, N1, N2};
+  const int64_t offs[3] = {3 * (N2 + N1), 3 * N2, 0};
+  for (int l = 0; l < 3 && !rc; ++l) {
+    const int W = widths[l];
+    const float* pp = workspace + offs[l];
+    const ncf_mlp_layer& L = a.l[l];
+    const ptrdiff_t s1 = L.dgamma - L.dbias, s2 = L.dbeta - L.dgamma;
+    if (s1 == s2 && s1 >= W) {
+      rc = ncf_defer(lst, pp, nb, kPartW, 3 * W, L.dbias, 0, W, s1);
+    } else {
+      rc = ncf_defer(lst, pp, nb, kPartW, W, L.dbias, 0, W, W);
+      if (!rc) rc = ncf_defer(lst, pp + W, nb, kPartW, W, L.dgamma, 0, W, W);
+      if (!rc) rc = ncf_defer(lst, pp + 2 * W, nb, kPartW, W, L.dbeta, 0, W, W);
+    }
+  }
+  if (rc) return rc;
+  if (!defer) {
+    float* scr = workspace + (int64_t)nb * kPartW;
+    return ncf_reduce_batch(lst, scr, workspace_floats - (int64_t)nb * kPartW, stream);
+  }
+  return NCF_OK;
+}

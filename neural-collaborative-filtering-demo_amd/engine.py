@@ -59,6 +59,7 @@ class Workspace:
         self.rstd = [e(n) for _ in g.hidden]
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
         self.train = train
+        self.cache = {}             # ctypes argument blocks built once per workspace
         if not train:
             return
         self.dumf, self.dimf, self.dxu, self.dxi = (e(n, D) for _ in range(4))
@@ -74,6 +75,7 @@ class Workspace:
         sites = [("head", _lib.query("ncf_head_bwd_workspace", n, g.hidden[-1], D))]
         for l, h in enumerate(g.hidden):
             sites.append((f"relu{l}", _lib.query("ncf_relu_ln_dropout_bwd_workspace", n, h)))
+        sites.append(("mlp", _lib.query("ncf_mlp_bwd_workspace", n)))
         self.site_off, off = {}, 0
         for name, size in sites:
             self.site_off[name] = (off, size)
@@ -156,6 +158,7 @@ class NCFEngine:
         self._side = None         # side streams (fork / join)
         self._events = None
         self._ev_i = 0
+        self._mlp_ok = {}
         self.updates = 0          # parameter writes by the HIP kernels (torch's _version misses them)
 
     # ------------------------------------------------------------------ side streams
@@ -364,6 +367,14 @@ class NCFEngine:
             x, ldx, kin = w.y, D, D
         else:
             x, ldx, kin = self._attention_unfused(w, M, train, drop_p, seed, temporal, st)
+        if temporal is None and self.mlp_fused(D, hid):
+            # a7 + a8: the whole tower and the head in one launch (mlp_tower.hip)
+            _, addr, _, haddr = self._mlp_layers(w, train, bwd=False)
+            _lib.call("ncf_mlp_fwd", ptr(x), n, D, addr, len(hid), haddr, LN_EPS,
+                      drop_p if train else 0.0, seed, ptr(self.clock), ptr(m.mlp_output.weight),
+                      ptr(m.mlp_output.bias), ptr(w.mf_pred), ptr(m.final[0].weight),
+                      ptr(m.final[0].bias), ptr(w.mlp_pred), ptr(w.prob), st)
+            return w
         for l, h in enumerate(hid):
             lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
             ldw = lin.weight.shape[1]
@@ -378,6 +389,42 @@ class NCFEngine:
                   ptr(m.mlp_output.bias), ptr(w.mf_pred), ptr(m.final[0].weight),
                   ptr(m.final[0].bias), ptr(w.mlp_pred), ptr(w.prob), st)
         return w
+
+    def mlp_fused(self, D: int, hid) -> bool:
+        """Whether the one-launch MLP tower (mlp_tower.hip) covers this geometry;
+        NCF_MLP_FUSED=0 forces the per-layer launches (A/B measurement, parity tests)."""
+        if os.environ.get("NCF_MLP_FUSED", "1") == "0":
+            return False
+        key = (D, tuple(hid))
+        ok = self._mlp_ok.get(key)
+        if ok is None:
+            h = (ctypes.c_int64 * len(hid))(*hid)
+            ok = self._mlp_ok[key] = bool(_lib.query("ncf_mlp_fused_supported", D, len(hid),
+                                                     ctypes.addressof(h)))
+        return ok
+
+    def _mlp_layers(self, w, train: bool, bwd: bool):
+        """ncf_mlp_layer[] for the fused tower (cached per workspace: the parameter and buffer
+        addresses are fixed for its lifetime)."""
+        key = ("mlp", train, bwd)
+        c = w.cache.get(key)
+        if c is None:
+            m = self.model
+            hid = list(m.mlp_hidden_dims)
+            arr = (_lib.MlpLayer * len(hid))()
+            for l, L in enumerate(arr):
+                lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
+                L.w, L.ldw, L.b = ptr(lin.weight), lin.weight.shape[1], ptr(lin.bias)
+                L.gamma, L.beta = ptr(ln.weight), ptr(ln.bias)
+                if train:
+                    L.r, L.a, L.mean, L.rstd = ptr(w.r[l]), ptr(w.a[l]), ptr(w.mean[l]), ptr(w.rstd[l])
+                if bwd:
+                    gv = self.grad_view
+                    L.dlin, L.dbias = ptr(w.dlin[l]), ptr(gv(f"mlp.{4 * l}.bias"))
+                    L.dgamma, L.dbeta = ptr(gv(f"mlp.{4 * l + 2}.weight")), ptr(gv(f"mlp.{4 * l + 2}.bias"))
+            harr = (ctypes.c_int64 * len(hid))(*hid)
+            c = w.cache[key] = (arr, ctypes.addressof(arr), harr, ctypes.addressof(harr))
+        return c
 
     def attn_block(self, D: int, H: int, M: int) -> bool:
         """Whether the one-launch attention block (attn_block.hip) covers this geometry;
@@ -460,15 +507,23 @@ class NCFEngine:
                   float(loss_denominator), ptr(w.site("head")), w.site("head").numel(),
                   w.red_list.address, st)
         # a7 backward, last layer first
+        fused = self.mlp_fused(D, hid)
+        if fused:   # relu/LN/dropout backward + dX of all layers in one launch (mlp_tower.hip)
+            _, addr, _, haddr = self._mlp_layers(w, True, bwd=True)
+            _lib.call("ncf_mlp_bwd", ptr(w.da[-1]), n, D, addr, len(hid), haddr, drop_p, seed,
+                      ptr(self.clock), ptr(w.dy), ptr(w.site("mlp")), w.site("mlp").numel(),
+                      w.red_list.address, st)
         for l in reversed(range(len(hid))):
             h = hid[l]
             lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
-            _lib.call("ncf_relu_ln_dropout_bwd", ptr(w.da[l]), ptr(w.r[l]), ptr(w.mean[l]),
-                      ptr(w.rstd[l]), ptr(ln.weight), n, h, drop_p,
-                      (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1), ptr(self.clock), ptr(w.dlin[l]),
-                      ptr(gv(f"mlp.{4 * l + 2}.weight")), ptr(gv(f"mlp.{4 * l + 2}.bias")),
-                      ptr(gv(f"mlp.{4 * l}.bias")), ptr(w.site(f"relu{l}")),
-                      w.site(f"relu{l}").numel(), w.red_list.address, st)
+            if not fused:
+                _lib.call("ncf_relu_ln_dropout_bwd", ptr(w.da[l]), ptr(w.r[l]), ptr(w.mean[l]),
+                          ptr(w.rstd[l]), ptr(ln.weight), n, h, drop_p,
+                          (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1), ptr(self.clock),
+                          ptr(w.dlin[l]), ptr(gv(f"mlp.{4 * l + 2}.weight")),
+                          ptr(gv(f"mlp.{4 * l + 2}.bias")), ptr(gv(f"mlp.{4 * l}.bias")),
+                          ptr(w.site(f"relu{l}")), w.site(f"relu{l}").numel(),
+                          w.red_list.address, st)
             xin, kin = (w.y, D) if l == 0 else (w.a[l - 1], hid[l - 1])
             ldw = lin.weight.shape[1]
             dW = gv(f"mlp.{4 * l}.weight")
@@ -482,8 +537,9 @@ class NCFEngine:
                 joins.extend(self.fork(dev, 1))
                 with torch.cuda.stream(joins[-1]):
                     w.run_wgrads(_lib.stream_ptr(dev), slot=0)
-            dx = w.dy if l == 0 else w.da[l - 1]
-            self._gemm(w.dlin[l], h, 0, lin.weight, ldw, 0, dx, kin, n, kin, h, st=st)
+            if not fused:
+                dx = w.dy if l == 0 else w.da[l - 1]
+                self._gemm(w.dlin[l], h, 0, lin.weight, ldw, 0, dx, kin, n, kin, h, st=st)
         # a5 backward: out_proj, core, q/k/v projections
         att = m.user_product_attention
         if self.attn_block(D, H, M):

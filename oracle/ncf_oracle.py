@@ -218,3 +218,39 @@ def train_step(p: Dict[str, Tensor], opt: AdamState, user_ids, item_ids, targets
     with torch.no_grad():
         opt.step(p, grads)
     return prob.detach(), loss.detach(), grads
+
+
+# ----------------------------------------------------------------------------- 8f: negatives
+def inverse_popularity_weights(products, num_products: int):
+    """src/model/data_prep.py:95-102 — per-product interaction counts, clamped to >= 1,
+    inverted and normalised (float64 numpy, as the reference's np arrays)."""
+    import numpy as np
+    counts = np.zeros(num_products)
+    for p in [int(x) for x in products]:
+        counts[p] += 1
+    counts = np.maximum(counts, 1)
+    w = 1 / counts
+    return w / w.sum()
+
+
+def negative_distribution(weights, history, positive: int, max_attempts: int = 10):
+    """Exact distribution of one ``SheetzDataset._sample_negative(user, positive)`` draw
+    (data_prep.py:134-161): up to ``max_attempts`` draws from ``weights``, rejecting the positive
+    and the user's history; then uniform over the products outside history + {positive}, or —
+    when that set is empty — uniform over every product but the positive."""
+    import numpy as np
+    n = len(weights)
+    excluded = set(int(h) for h in history) | {int(positive)}
+    ok = np.ones(n, dtype=bool)
+    ok[list(excluded)] = False
+    r = float(np.sum(np.asarray(weights)[~ok]))        # rejection probability per attempt
+    direct = np.where(ok, weights, 0.0) * sum(r ** a for a in range(max_attempts))
+    tail = r ** max_attempts
+    valid = np.flatnonzero(ok)
+    fb = np.zeros(n)
+    if valid.size:
+        fb[valid] = 1.0 / valid.size
+    else:
+        fb[:] = 1.0 / (n - 1)
+        fb[int(positive)] = 0.0
+    return direct + tail * fb

@@ -142,3 +142,64 @@ def test_reduce_list_layout_and_scratch_query():
     assert _lib.query("ncf_reduce_batch_scratch", lst.address) == 3 * 4096 + 16 * 768
     empty = _lib.ReduceList()
     assert _lib.load().ncf_reduce_batch(empty.address, None, 0, None) == 0  # nothing to launch
+
+
+# ----------------------------------------------------------------------------- 8f: negatives
+def test_inverse_popularity_weights_vs_oracle():
+    from oracle import ncf_oracle as O
+    from ncf_amd.data import inverse_popularity_weights
+    g = torch.Generator().manual_seed(3)
+    prods = torch.randint(0, 37, (500,), generator=g)
+    prods[prods == 5] = 6                      # product 5 never seen: count clamps to 1
+    np.testing.assert_allclose(inverse_popularity_weights(prods, 40),
+                               O.inverse_popularity_weights(prods.tolist(), 40), rtol=1e-12)
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 1000])
+def test_alias_table_reconstructs_weights(n):
+    """ncf_alias_build (host code in libncf_hip.so): each item's total mass over the table,
+    (prob[i] + sum_{alias[j] = i} (1 - prob[j])) / n, equals its normalised weight."""
+    from ncf_amd.data import alias_table
+    rng = np.random.default_rng(n)
+    w = rng.random(n) ** 3
+    w[rng.random(n) < 0.1] = 0.0
+    if w.sum() == 0:
+        w[0] = 1.0
+    prob, alias = alias_table(w)
+    assert prob.min() >= 0 and prob.max() <= 1 and alias.min() >= 0 and alias.max() < n
+    mass = prob.astype(np.float64).copy()
+    np.add.at(mass, alias, 1.0 - prob.astype(np.float64))
+    np.testing.assert_allclose(mass / n, w / w.sum(), atol=1e-6)
+
+
+def test_negative_distribution_oracle_cases():
+    from oracle import ncf_oracle as O
+    w = np.array([0.1, 0.2, 0.3, 0.4])
+    d = O.negative_distribution(w, [], 0)           # only the positive is rejected
+    assert d[0] == 0 and abs(d.sum() - 1) < 1e-12
+    d = O.negative_distribution(w, [0, 1, 2, 3], 2)  # bought everything: any but the positive
+    np.testing.assert_allclose(d, [1 / 3, 1 / 3, 0, 1 / 3])
+
+
+# ----------------------------------------------------------------------------- 8f: ANN export
+def test_product_index_and_distinct_rows():
+    from ncf_amd.export import distinct_products, product_index
+    assert product_index("P1A", 366) == 26 and product_index("ff", 100) == 55
+    assert product_index("P0", 7) == 0
+    rows = [{"product_id": "P10"}, {"product_id": None}, {"category_id": "x"},
+            {"product_id": "P10"}, {"product_id": "P2F"}]
+    assert distinct_products(rows, 366) == (["P10", "P2F"], [16, 47])
+
+
+def test_embeddings_jsonl_format():
+    import io
+    import json
+    from ncf_amd.export import write_embeddings_jsonl
+    e = torch.tensor([[0.6, 0.8], [1.0, 0.0]])
+    buf = io.StringIO()
+    assert write_embeddings_jsonl(buf, ["P1", "P2"], e) == 2
+    lines = buf.getvalue().splitlines()
+    assert lines[0].startswith('{"id": "P1", "embedding": [')
+    rec = [json.loads(x) for x in lines]
+    assert rec[1] == {"id": "P2", "embedding": [1.0, 0.0]}
+    assert rec[0]["embedding"] == [float(np.float32(0.6)), float(np.float32(0.8))]

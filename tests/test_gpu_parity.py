@@ -496,6 +496,57 @@ def test_attn_block_matches_unfused(monkeypatch, H, M, B):
         torch.testing.assert_close(G1[k], G0[k], rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("B,drop", [(37, 0.2), (64, 0.0), (1, 0.2)])
+def test_mlp_tower_matches_unfused(monkeypatch, B, drop):
+    """The one-launch MLP tower (mlp_tower.hip, forward + backward) vs the per-layer launches
+    (GEMM + rowops + head), same dropout stream: probabilities, saved activations, dense and
+    compact table gradients agree to the grads tolerance; n = 5B rows not a multiple of the
+    32-row tile exercises the ragged last workgroup."""
+    from ncf_amd.trainer import FusedTrainStep
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("NCF_MLP_FUSED", flag)
+        torch.manual_seed(31)
+        m = ncf.AdvancedNCF(400, 300, 5, 24, 64, 64, 32, [256, 128, 64], 4, drop, 4).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+        assert m.engine.mlp_fused(64, [256, 128, 64]) == (flag == "1")
+        g = torch.Generator().manual_seed(32)
+        u = torch.randint(0, 400, (B,), generator=g).repeat_interleave(5).to(DEV)
+        i = torch.randint(0, 300, (B * 5,), generator=g).to(DEV)
+        t = torch.zeros(B, 5)
+        t[:, 0] = 1
+        w = step(u, i, t.reshape(-1, 1).to(DEV))
+        torch.cuda.synchronize()
+        nu = w.num_unique.cpu().tolist()
+        out.append(dict(prob=w.prob.cpu().clone(), mlp=w.mlp_pred.cpu().clone(),
+                        grad=m.engine.flat_grad.cpu().clone(), dy=w.dy.cpu().clone(),
+                        a=[x.cpu().clone() for x in w.a], r=[x.cpu().clone() for x in w.r],
+                        G={k: v[:nu[0 if k.endswith("user") else 1]].cpu().clone()
+                           for k, v in w.G.items()}))
+    a, b = out
+    for k in ("prob", "mlp"):
+        torch.testing.assert_close(b[k], a[k], rtol=0, atol=2e-6)
+    for x, y in zip(b["r"] + b["a"], a["r"] + a["a"]):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(b["dy"], a["dy"], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(b["grad"], a["grad"], rtol=1e-4, atol=1e-6)
+    for k in a["G"]:
+        torch.testing.assert_close(b["G"][k], a["G"][k], rtol=1e-4, atol=1e-6)
+
+
+def test_mlp_tower_eval_matches_unfused(monkeypatch):
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("NCF_MLP_FUSED", flag)
+        torch.manual_seed(33)
+        m = ncf.AdvancedNCF(300, 200, 5, 24).to(DEV).eval()
+        u = torch.randint(0, 300, (1001,), device=DEV)
+        i = torch.randint(0, 200, (1001,), device=DEV)
+        with torch.no_grad():
+            res.append(m.forward_simple(u, i).cpu())
+    torch.testing.assert_close(res[1], res[0], rtol=0, atol=2e-6)
+
+
 def test_attn_block_eval_forward_matches_unfused(monkeypatch):
     """Eval (M = 1): the block's no-core form (o = v) vs the unfused v/out projections."""
     res = []
@@ -860,3 +911,114 @@ def test_f6_forward_simple_hour(f5, f6):
                                 torch.full((366,), 5), lin.weight.detach().cpu(),
                                 lin.bias.detach().cpu(), num_heads=4, n_layers=3)
     np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), atol=2e-6)
+
+
+# ----------------------------------------------------------------------------- 8f: negatives
+def _sampler_case():
+    """40 products; users with histories of 0..5 items, one with 38 of 40 (the fallback path is
+    frequent), one with all 40 (the 'bought everything' branch)."""
+    I = 40
+    hist = {0: [3], 1: [0, 1, 2, 3, 4], 2: [7, 30], 3: list(range(38)), 4: list(range(40))}
+    users, prods = [], []
+    for u, h in hist.items():
+        for p in h:
+            users.append(u)
+            prods.append(p)
+    users += [5] * 30                 # extra interactions skew popularity
+    prods += [9] * 30
+    return I, hist, torch.tensor(users), torch.tensor(prods)
+
+
+def test_negative_sampler_distribution_matches_reference():
+    """Per user, the empirical distribution of 200K device negatives vs the exact distribution
+    of the reference's _sample_negative (oracle.negative_distribution: inverse-popularity draws
+    with rejection of positive + history, 10 attempts, uniform fallback) — 6 sigma."""
+    from oracle import ncf_oracle as O
+    from ncf_amd.data import DeviceNegativeSampler
+    I, hist, users, prods = _sampler_case()
+    s = DeviceNegativeSampler(users, prods, 6, I, negative_samples=4, device=DEV)
+    w = O.inverse_popularity_weights(prods.tolist(), I)
+    np.testing.assert_allclose(s.weights, w, rtol=1e-12)
+    for u, h in hist.items():
+        pos = h[0]
+        idx = [k for k in range(len(users)) if users[k] == u and prods[k] == pos][0]
+        reps = 50_000
+        kjt, tgt = s.batch(torch.full((reps,), idx), seed=100 + u)
+        vals = kjt.values().view(2, reps, 5)
+        assert bool((vals[0] == u).all())
+        assert bool((vals[1][:, 0] == pos).all())
+        neg = vals[1][:, 1:].reshape(-1).cpu().numpy()
+        emp = np.bincount(neg, minlength=I) / neg.size
+        exp = O.negative_distribution(w, h, pos)
+        sig = np.sqrt(np.maximum(exp * (1 - exp), 1e-12) / neg.size)
+        assert np.all(np.abs(emp - exp) <= 6 * sig + 1e-9), (u, np.max(np.abs(emp - exp) / (sig + 1e-12)))
+        assert tgt.shape == (reps * 5, 1)
+        assert bool((tgt.view(reps, 5)[:, 0] == 1).all()) and bool((tgt.view(reps, 5)[:, 1:] == 0).all())
+
+
+def test_negative_sampler_epoch_layout_and_determinism():
+    """epoch(): every interaction exactly once, KJT layout (values [users || items], lengths 1),
+    identical batches for the same seed, different negatives for another seed; batches run
+    through the model's own forward."""
+    from ncf_amd.data import DeviceNegativeSampler
+    g = torch.Generator().manual_seed(5)
+    U, I, P = 50, 300, 1000
+    users = torch.randint(0, U, (P,), generator=g)
+    prods = torch.randint(0, I, (P,), generator=g)
+    s = DeviceNegativeSampler(users, prods, U, I, negative_samples=4, device=DEV)
+    seen, b1 = [], []
+    for kjt, t in s.epoch(batch_size=128, seed=7):
+        n = kjt.values().numel() // 2
+        assert n % 5 == 0 and t.shape == (n, 1)
+        assert bool((kjt.lengths() == 1).all()) and kjt.keys() == ["user_id", "product_id"]
+        v = kjt.values().view(2, n // 5, 5)
+        seen.append(torch.stack([v[0][:, 0], v[1][:, 0]], 1).cpu())
+        b1.append(v.cpu())
+        # negatives are never the user's positives (histories here are tiny: no fallback)
+        for uu, row in zip(v[0][:, 0].tolist(), v[1][:, 1:].tolist()):
+            hist = set(prods[users == uu].tolist())
+            assert not (set(row) & hist)
+    pairs = torch.cat(seen)
+    ref = torch.stack([users, prods], 1)
+    assert sorted(map(tuple, pairs.tolist())) == sorted(map(tuple, ref.tolist()))
+    b2 = [kjt.values().view(2, -1, 5).cpu() for kjt, _ in s.epoch(batch_size=128, seed=7)]
+    assert all(torch.equal(a, b) for a, b in zip(b1, b2))
+    b3 = [kjt.values().view(2, -1, 5).cpu() for kjt, _ in s.epoch(batch_size=128, seed=8)]
+    assert not all(torch.equal(a, b) for a, b in zip(b1, b3))
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV).train()
+    kjt, t = next(s.epoch(batch_size=64, seed=1))
+    out = m(kjt)
+    assert out.shape == t.shape
+    val = DeviceNegativeSampler(users, prods, U, I, mode="val", device=DEV)
+    kjt, t = val.batch(torch.arange(10), seed=0)
+    assert kjt.values().numel() == 20 and bool((t == 1).all())
+
+
+# ----------------------------------------------------------------------------- 8f: ANN export
+def test_product_embedding_export_vs_reference(f5):
+    """L2-normalised "mlp" product vectors (generate_embeddings.py:206-211) on the demo
+    checkpoint: the reference's get_product_embeddings rows (F5) normalised, and the oracle."""
+    import io
+    import json
+    from oracle import ncf_oracle as O
+    from ncf_amd.export import export_product_embeddings, product_embeddings
+    sd = T(sub(f5, "sd/"))
+    nu = sd["mf_embedding_collection.embedding_bags.user_id.weight"].shape[0]
+    m = ncf.AdvancedNCF(nu, 366, 5, 24).to(DEV)
+    m.load_state_dict(sd, strict=True)
+    m.eval()
+    pid = torch.from_numpy(f5["emb_pids"])
+    got = product_embeddings(m, pid).cpu().numpy()
+    ref = f5["emb_item_mlp"] / np.linalg.norm(f5["emb_item_mlp"], axis=1, keepdims=True)
+    np.testing.assert_allclose(got, ref, atol=2e-6)
+    p = {k: v.cpu() for k, v in sd.items()}
+    ln = O.layer_norm(p[O.K_MLP_I][torch.arange(366)], p["mlp_norm.weight"], p["mlp_norm.bias"])
+    ln = ln / ln.norm(dim=1, keepdim=True)
+    rows = [{"product_id": f"P{i:X}"} for i in range(400)] + [{"product_id": "P5"}]
+    buf = io.StringIO()
+    assert export_product_embeddings(m, rows, buf) == 400
+    recs = [json.loads(x) for x in buf.getvalue().splitlines()]
+    assert [r["id"] for r in recs] == [f"P{i:X}" for i in range(400)]
+    emb = np.array([r["embedding"] for r in recs])
+    np.testing.assert_allclose(emb, ln.numpy()[np.arange(400) % 366], atol=2e-6)
+    np.testing.assert_allclose(np.linalg.norm(emb, axis=1), 1.0, atol=1e-6)
