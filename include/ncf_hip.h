@@ -184,8 +184,8 @@ int ncf_attention_bwd(const float* q, const float* k, const float* v, const floa
  * forward  q,k,v = LN rows x W^T + b, the core above (same P layout and dropout stream), y =
  *          o Wo^T + bo.  q = k = NULL (with M == 1, no dropout): the eval form, o = v, only y
  *          (and v, o if given) written.  probs/o required when q is given.
- * backward from dY: dO = dY Wo, the core backward, dXu = dQ Wq, dXi = dK Wk + dV Wv; dQ/dK/dV
- *          written for the weight gradients.                                                 */
+ * backward from dY: dO = dY Wo, the core backward, dXu = dQ Wq, dXi = dK Wk + dV Wv, and the
+ *          four Linear gradients (below).                                                     */
 int ncf_attn_block_supported(int64_t dim, int64_t heads, int64_t group_len);
 int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t groups, int64_t group_len,
                        int64_t heads, int64_t dim, const float* wq, const float* bq,
@@ -193,12 +193,21 @@ int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t groups, int64_t
                        const float* wo, const float* bo, float dropout_p, uint64_t seed,
                        const ncf_step_clock* clock, float* q, float* k, float* v, float* probs,
                        float* o, float* y, void* stream);
+/* Fused weight gradients: grad_params = {q.weight, q.bias, k.weight, k.bias, v.weight, v.bias,
+ * out.weight, out.bias} (written, not accumulated) from per-workgroup partials in `workspace`
+ * (ncf_attn_block_bwd_workspace floats), reduced now or deferred into `defer`; then grad_q/k/v
+ * may be NULL.  grad_params = NULL: no weight gradients, grad_q/k/v written for a separate
+ * weight-gradient pass (o/xu/xi/workspace unused). */
+int64_t ncf_attn_block_bwd_workspace(int64_t groups);
 int ncf_attn_block_bwd(const float* grad_y, const float* q, const float* k, const float* v,
                        const float* probs, int64_t groups, int64_t group_len, int64_t heads,
                        int64_t dim, const float* wq, const float* wk, const float* wv,
                        const float* wo, float dropout_p, uint64_t seed,
-                       const ncf_step_clock* clock, float* grad_q, float* grad_k, float* grad_v,
-                       float* grad_xu, float* grad_xi, void* stream);
+                       const ncf_step_clock* clock, const float* o, const float* xu,
+                       const float* xi, float* const* grad_params, float* workspace,
+                       int64_t workspace_floats, ncf_reduce_list* defer, float* grad_q,
+                       float* grad_k, float* grad_v, float* grad_xu, float* grad_xi,
+                       void* stream);
 
 /* ---- a7 + a8 fused: the MLP tower in one launch per direction (input 64, hidden [256,128,64];
  * ncf_mlp_fused_supported).  Layer l = mlp.{4l} Linear (w [N_l][ldw], first K_l columns used:

@@ -109,6 +109,43 @@ __device__ __forceinline__ void project(const float* __restrict__ X, const float
   }
 }
 
+// Weight-gradient tiles of a Linear over this workgroup's rows: dW[a][b] = sum_r dY[r][a] X[r][b]
+// (contraction over the R rows: k-permuted, lane group g covers rows [g R/4, (g+1) R/4)), written
+// to out[64 x 64]; tiles t = wave + 8q of the 16 per weight.  Rows past the batch are zero in LDS.
+__device__ __forceinline__ void wgrad_tile(const float* __restrict__ dYs,
+                                           const float* __restrict__ Xs, int R, int tj, int tk,
+                                           float* __restrict__ out) {
+  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  const int R4 = R >> 2;
+  const float* a = dYs + (g * R4) * kPitch + 16 * tj + i;
+  const float* b = Xs + (g * R4) * kPitch + 16 * tk + i;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + 1 < R4; s += 2) {
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s * kPitch], b[s * kPitch], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[(s + 1) * kPitch], b[(s + 1) * kPitch], acc1, 0, 0, 0);
+  }
+  if (s < R4) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s * kPitch], b[s * kPitch], acc0, 0, 0, 0);
+  float* o = out + (16 * tj + 4 * g) * kD + 16 * tk + i;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o[r * kD] = acc0[r] + acc1[r];
+}
+
+// bias gradient columns: out[c] = sum_r dY[r][c]; 64 threads per vector starting at thread t0
+__device__ __forceinline__ void bias_cols(const float* __restrict__ dYs, int R, int t0,
+                                          float* __restrict__ out) {
+  const int c = (int)threadIdx.x - t0;
+  if (c < 0 || c >= kD) return;
+  float acc = 0.0f;
+  for (int r = 0; r < R; ++r) acc += dYs[r * kPitch + c];
+  out[c] = acc;
+}
+
+// per-workgroup partial of the four Linear gradients, in the flat parameter order
+// [q.weight | q.bias | k.weight | k.bias | v.weight | v.bias | out.weight | out.bias]
+constexpr int kLinW = kD * kD + kD;
+constexpr int kPartAttn = 4 * kLinW;
+
 template <int HD>
 __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
     const float* __restrict__ xu, const float* __restrict__ xi, int64_t B, int M,
@@ -237,8 +274,10 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     const float* __restrict__ Vg, const float* __restrict__ P, int64_t B, int M,
     const float* __restrict__ wq, const float* __restrict__ wk, const float* __restrict__ wv,
     const float* __restrict__ wo, float scale, float p_drop, uint64_t seed,
-    const ncf_step_clock* clock, float* __restrict__ dQ, float* __restrict__ dK,
-    float* __restrict__ dV, float* __restrict__ dXu, float* __restrict__ dXi) {
+    const ncf_step_clock* clock, const float* __restrict__ Og, const float* __restrict__ Xu,
+    const float* __restrict__ Xi, float* __restrict__ part, float* __restrict__ dQ,
+    float* __restrict__ dK, float* __restrict__ dV, float* __restrict__ dXu,
+    float* __restrict__ dXi) {
   constexpr int H = kD / HD;
   constexpr int kIt = (kGroups * H * kMaxM + kThreads - 1) / kThreads;
   extern __shared__ float lds[];
@@ -247,7 +286,9 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
   float* S1 = lds + R * kPitch;
   float* S2 = lds + 2 * R * kPitch;
   float* S3 = lds + 3 * R * kPitch;
-  float* dS = lds + 4 * R * kPitch;   // [16][H][M][M]
+  const bool wg = part != nullptr;   // fused weight gradients (partials of this workgroup)
+  float* S4 = lds + 4 * R * kPitch;                 // O -> X_u (fused weight gradients only)
+  float* dS = lds + (wg ? 5 : 4) * R * kPitch;      // [16][H][M][M]
   const int64_t g0 = (int64_t)blockIdx.x * kGroups;
   const int ng = (int)min<int64_t>(kGroups, B - g0);
   const int rows = ng * M;
@@ -261,8 +302,22 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
   stage_in(S1, Qg + r0 * kD, R, rows);
   stage_in(S2, Kg + r0 * kD, R, rows);
   stage_in(S3, Vg + r0 * kD, R, rows);
+  if (wg) stage_in(S4, Og + r0 * kD, R, rows);
   __syncthreads();
-  // dO = dY . Wo
+  float* pw = wg ? part + (int64_t)blockIdx.x * kPartAttn : nullptr;
+  // X_u / X_i rows of this workgroup, prefetched into registers for the fused weight gradients
+  constexpr int kPre = (16 * kMaxM * 16 + kThreads - 1) / kThreads;   // float4 per thread
+  float4 pu[kPre], pi[kPre];
+  if (wg) {
+#pragma unroll
+    for (int q = 0; q < kPre; ++q) {
+      const int e = threadIdx.x + kThreads * q, r = e >> 4, c = (e & 15) * 4;
+      const bool in = e < R * 16 && r < rows;
+      pu[q] = in ? ld4(Xu + (r0 + r) * kD + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      pi[q] = in ? ld4(Xi + (r0 + r) * kD + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // dO = dY . Wo  (+ out_proj's weight gradient dY^T O and bias gradient)
   {
     float b[16];
     frag_w(wo, w, b);
@@ -270,10 +325,26 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
 #pragma unroll
     for (int rt = 0; rt < kMaxM; ++rt)
       if (rt < M && (rt & 1) == par) fo[rt] = tile_mfma(S0 + 16 * rt * kPitch, b, f32x4{0.f, 0.f, 0.f, 0.f});
+    if (wg) {
+      const int wave = threadIdx.x >> 6;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int t = wave + 8 * q;
+        wgrad_tile(S0, S4, R, t >> 2, t & 3, pw + 3 * kLinW);
+      }
+      bias_cols(S0, R, 0, pw + 3 * kLinW + kD * kD);
+    }
     __syncthreads();
 #pragma unroll
     for (int rt = 0; rt < kMaxM; ++rt)
       if (rt < M && (rt & 1) == par) put_tile(S0, rt, w, fo[rt]);
+    if (wg) {   // O is consumed: X_u takes its place
+#pragma unroll
+      for (int q = 0; q < kPre; ++q) {
+        const int e = threadIdx.x + kThreads * q;
+        if (e < R * 16) *reinterpret_cast<float4*>(S4 + (e >> 4) * kPitch + (e & 15) * 4) = pu[q];
+      }
+    }
     __syncthreads();
   }
   const int ntask = ng * H * M;
@@ -371,9 +442,27 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     }
     __syncthreads();
   }
-  stage_out(dQ + r0 * kD, S2, rows);
-  stage_out(dK + r0 * kD, S1, rows);
-  stage_out(dV + r0 * kD, S3, rows);
+  if (dQ) stage_out(dQ + r0 * kD, S2, rows);
+  if (dK) stage_out(dK + r0 * kD, S1, rows);
+  if (dV) stage_out(dV + r0 * kD, S3, rows);
+  if (wg) {   // dO is consumed: X_i takes its place; then the q/k/v weight gradients
+#pragma unroll
+    for (int q = 0; q < kPre; ++q) {
+      const int e = threadIdx.x + kThreads * q;
+      if (e < R * 16) *reinterpret_cast<float4*>(S0 + (e >> 4) * kPitch + (e & 15) * 4) = pi[q];
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    for (int q = 0; q < 6; ++q) {
+      const int t = wave + 8 * q, lin = t >> 4, tt = t & 15;   // lin: 0 q, 1 k, 2 v
+      const float* dys = lin == 0 ? S2 : (lin == 1 ? S1 : S3);
+      const float* xs = lin == 0 ? S4 : S0;
+      wgrad_tile(dys, xs, R, tt >> 2, tt & 3, pw + lin * kLinW);
+    }
+    bias_cols(S2, R, 0, pw + kD * kD);
+    bias_cols(S1, R, 64, pw + kLinW + kD * kD);
+    bias_cols(S3, R, 128, pw + 2 * kLinW + kD * kD);
+  }
   // dX_u = dQ . Wq ; dX_i = dK . Wk + dV . Wv
   f32x4 fu[kMaxM], fi[kMaxM];
   {
@@ -391,21 +480,26 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     for (int rt = 0; rt < kMaxM; ++rt)
       if (rt < M && (rt & 1) == par) fi[rt] = tile_mfma(S3 + 16 * rt * kPitch, b, fi[rt]);
   }
+  if (!wg) {
+#pragma unroll
+    for (int rt = 0; rt < kMaxM; ++rt)
+      if (rt < M && (rt & 1) == par) put_tile(S0, rt, w, fu[rt]);   // dO is dead
+  }
+  __syncthreads();   // S0..S4 no longer read (MFMA operands, stage_out)
 #pragma unroll
   for (int rt = 0; rt < kMaxM; ++rt)
-    if (rt < M && (rt & 1) == par) put_tile(S0, rt, w, fu[rt]);   // dO is dead
-  __syncthreads();   // S1..S3 no longer read (MFMA operands, stage_out)
-#pragma unroll
-  for (int rt = 0; rt < kMaxM; ++rt)
-    if (rt < M && (rt & 1) == par) put_tile(S1, rt, w, fi[rt]);
+    if (rt < M && (rt & 1) == par) {
+      if (wg) put_tile(S0, rt, w, fu[rt]);
+      put_tile(S1, rt, w, fi[rt]);
+    }
   __syncthreads();
   stage_out(dXu + r0 * kD, S0, rows);
   stage_out(dXi + r0 * kD, S1, rows);
 }
 
 size_t fwd_lds(int M) { return sizeof(float) * 3 * kGroups * M * kPitch; }
-size_t bwd_lds(int M, int H) {
-  return sizeof(float) * (4 * kGroups * M * kPitch + kGroups * H * M * M);
+size_t bwd_lds(int M, int H, bool wg) {
+  return sizeof(float) * ((wg ? 5 : 4) * kGroups * M * kPitch + kGroups * H * M * M);
 }
 
 template <typename Kern>
@@ -464,30 +558,49 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
   return NCF_OK;
 }
 
+extern "C" int64_t ncf_attn_block_bwd_workspace(int64_t groups) {
+  const int64_t nb = groups <= 0 ? 1 : ncf_cdiv(groups, kGroups);
+  return nb * kPartAttn + ncf_reduce_scratch((int)nb, kPartAttn) * 4;
+}
+
 extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const float* k,
                                   const float* v, const float* probs, int64_t groups,
                                   int64_t group_len, int64_t heads, int64_t dim, const float* wq,
                                   const float* wk, const float* wv, const float* wo,
                                   float dropout_p, uint64_t seed, const ncf_step_clock* clock,
+                                  const float* o, const float* xu, const float* xi,
+                                  float* const* grad_params, float* workspace,
+                                  int64_t workspace_floats, ncf_reduce_list* defer,
                                   float* grad_q, float* grad_k, float* grad_v, float* grad_xu,
                                   float* grad_xi, void* stream) {
   NCF_CHECK_ARG(groups >= 0 && ncf_attn_block_supported(dim, heads, group_len),
                 "ncf_attn_block_bwd: unsupported shape (D=%lld H=%lld M=%lld; need D=64, M<=%d)",
                 (long long)dim, (long long)heads, (long long)group_len, kMaxM);
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_attn_block_bwd: dropout_p out of [0,1)");
+  const bool wg = grad_params != nullptr;
+  NCF_CHECK_ARG(!wg || (o && xu && xi && workspace), "ncf_attn_block_bwd: the fused weight "
+                "gradients need o, xu, xi and a workspace");
+  NCF_CHECK_ARG(wg || (grad_q && grad_k && grad_v),
+                "ncf_attn_block_bwd: without grad_params, grad_q/k/v are required");
+  if (wg && workspace_floats < ncf_attn_block_bwd_workspace(groups)) {
+    ncf_set_error("ncf_attn_block_bwd: workspace too small");
+    return NCF_ERR_WORKSPACE;
+  }
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len, H = (int)heads;
-  const size_t lds = bwd_lds(M, H);
-  const dim3 grid((unsigned)ncf_cdiv(groups, kGroups));
+  const size_t lds = bwd_lds(M, H, wg);
+  const int nb = (int)ncf_cdiv(groups, kGroups);
+  const dim3 grid((unsigned)nb);
   hipStream_t st = (hipStream_t)stream;
   const float scale = sqrtf((float)(dim / heads));
+  float* part = wg ? workspace : nullptr;
 #define NCF_ABB(HD)                                                                               \
   case HD: {                                                                                      \
     static bool attr = false;                                                                     \
-    if (!attr) { allow_lds(k_attn_block_bwd<HD>, bwd_lds(kMaxM, kD / HD)); attr = true; }         \
-    hipLaunchKernelGGL(k_attn_block_bwd<HD>, grid, dim3(kThreads), lds, st, grad_y, q, k, v, probs,     \
-                       groups, M, wq, wk, wv, wo, scale, dropout_p, seed, clock, grad_q, grad_k,  \
-                       grad_v, grad_xu, grad_xi);                                                 \
+    if (!attr) { allow_lds(k_attn_block_bwd<HD>, bwd_lds(kMaxM, kD / HD, true)); attr = true; }   \
+    hipLaunchKernelGGL(k_attn_block_bwd<HD>, grid, dim3(kThreads), lds, st, grad_y, q, k, v, probs, \
+                       groups, M, wq, wk, wv, wo, scale, dropout_p, seed, clock, o, xu, xi, part, \
+                       grad_q, grad_k, grad_v, grad_xu, grad_xi);                                 \
     break;                                                                                        \
   }
   switch (dim / heads) {
@@ -498,5 +611,35 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
   }
 #undef NCF_ABB
   NCF_CHECK_LAUNCH("ncf_attn_block_bwd");
+  if (!wg) return NCF_OK;
+  // partial rows -> the 8 parameter gradients: one reduction when they are laid out like the
+  // partial row (the flat gradient buffer), else one per Linear (weight + bias adjacent) or 8
+  ncf_reduce_list local;
+  local.count = 0;
+  ncf_reduce_list* lst = defer ? defer : &local;
+  int rc = NCF_OK;
+  bool flat = true;
+  for (int j = 1; j < 8; ++j)
+    flat = flat && grad_params[j] == grad_params[0] + (j / 2) * kLinW + (j & 1) * kD * kD;
+  if (flat) {
+    rc = ncf_defer(lst, part, nb, kPartAttn, kPartAttn, grad_params[0], 0, kPartAttn, kPartAttn);
+  } else {
+    for (int lin = 0; lin < 4 && !rc; ++lin) {
+      float* gw = grad_params[2 * lin];
+      float* gb = grad_params[2 * lin + 1];
+      const float* pp = part + lin * kLinW;
+      if (gb == gw + kD * kD) {
+        rc = ncf_defer(lst, pp, nb, kPartAttn, kLinW, gw, 0, kLinW, kLinW);
+      } else {
+        rc = ncf_defer(lst, pp, nb, kPartAttn, kD * kD, gw, 0, kD * kD, kD * kD);
+        if (!rc) rc = ncf_defer(lst, pp + kD * kD, nb, kPartAttn, kD, gb, 0, kD, kD);
+      }
+    }
+  }
+  if (rc) return rc;
+  if (!defer) {
+    const int64_t off = (int64_t)nb * kPartAttn;
+    return ncf_reduce_batch(lst, workspace + off, workspace_floats - off, stream);
+  }
   return NCF_OK;
 }

@@ -76,6 +76,7 @@ class Workspace:
         for l, h in enumerate(g.hidden):
             sites.append((f"relu{l}", _lib.query("ncf_relu_ln_dropout_bwd_workspace", n, h)))
         sites.append(("mlp", _lib.query("ncf_mlp_bwd_workspace", n)))
+        sites.append(("attn", _lib.query("ncf_attn_block_bwd_workspace", g.B)))
         self.site_off, off = {}, 0
         for name, size in sites:
             self.site_off[name] = (off, size)
@@ -543,17 +544,20 @@ class NCFEngine:
         # a5 backward: out_proj, core, q/k/v projections
         att = m.user_product_attention
         if self.attn_block(D, H, M):
+            # core + projections backward and the four Linear gradients in one launch
+            gp = w.cache.get("attn_grads")
+            if gp is None:
+                names = [f"user_product_attention.{nm}.{t}" for nm in ("q_proj", "k_proj", "v_proj",
+                                                                        "out_proj")
+                         for t in ("weight", "bias")]
+                arr = (ctypes.c_void_p * 8)(*[ptr(gv(x)) for x in names])
+                gp = w.cache["attn_grads"] = (arr, ctypes.addressof(arr))
+            ws = w.site("attn")
             _lib.call("ncf_attn_block_bwd", ptr(w.dy), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P),
                       n // M, M, H, D, ptr(att.q_proj.weight), ptr(att.k_proj.weight),
                       ptr(att.v_proj.weight), ptr(att.out_proj.weight), drop_p, seed,
-                      ptr(self.clock), ptr(w.dq), ptr(w.dk), ptr(w.dv), ptr(w.dxu), ptr(w.dxi), st)
-            for nm, dY, X in (("out_proj", w.dy, w.o), ("q_proj", w.dq, w.xu),
-                              ("k_proj", w.dk, w.xi), ("v_proj", w.dv, w.xi)):
-                self._wgrad(w, dY, D, X, D, gv(f"user_product_attention.{nm}.weight"), D, D, D, n,
-                            dbias=gv(f"user_product_attention.{nm}.bias"))
-            joins.extend(self.fork(dev, 1))
-            with torch.cuda.stream(joins[-1]):
-                w.run_wgrads(_lib.stream_ptr(dev), slot=1)
+                      ptr(self.clock), ptr(w.o), ptr(w.xu), ptr(w.xi), gp[1], ptr(ws), ws.numel(),
+                      w.red_list.address, None, None, None, ptr(w.dxu), ptr(w.dxi), st)
         else:
             self._attention_bwd_unfused(w, drop_p, seed, joins, st)
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)
