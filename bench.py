@@ -33,6 +33,30 @@ HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA = the f32 vector rate
 
 
+# C-ABI entry point -> the kernel symbol rocprofv3 reports for it
+KERNEL_SYMBOL = {"ncf_attn_block_fwd": "k_attn_block_fwd", "ncf_attn_block_bwd": "k_attn_block_bwd",
+                 "ncf_mlp_fwd": "k_mlp_fwd", "ncf_mlp_bwd": "k_mlp_bwd",
+                 "ncf_wgrad_grouped": "k_wgrad_grouped"}
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/*_pmc_traffic.json, made by tools/pmc_traffic.py from separate FETCH_SIZE and
+    WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction applied); None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not kernel or not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None
+    return {"bytes_per_launch": k["hbm_bytes_per_launch"],
+            "source": f"{os.path.basename(files[-1])} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+                      f"separate passes)"}
+
+
 def zipf_sampler(n_items, s, device):
     w = 1.0 / torch.arange(1, n_items + 1, dtype=torch.float64) ** s
     cdf = torch.cumsum(w / w.sum(), 0).to(device=device, dtype=torch.float64)
@@ -267,16 +291,36 @@ def main():
     for name, a, e0, e1 in prof:
         per.setdefault(name, []).append((a, e0.elapsed_time(e1)))
     totals = {k: sum(d for _, d in v) / args.steps for k, v in per.items()}   # ms per step
-    # fp32 MFMA kernels: forward + dX GEMMs (M, N, K are the first three arguments of every
-    # ncf_gemm_* entry point) and the grouped weight-gradient launch, whose FLOPs equal the
-    # forward GEMMs' (dW = dYᵀ·X costs 2·n·out·in per Linear, like the forward) = half of fwd + dX
-    gemm_names = ("ncf_gemm_direct", "ncf_gemm_f32", "ncf_gemm_rows", "ncf_gemm_f32_splitk",
-                  "ncf_wgrad_grouped")
-    gemm_ms = sum(totals.get(k, 0.0) for k in gemm_names)
-    fwd_dx = sum(2.0 * a[0] * a[1] * a[2] for k in gemm_names[:4] for a, _ in per.get(k, [])) / args.steps
-    gemm_flops = fwd_dx * (1.5 if "ncf_wgrad_grouped" in per else 1.0)
-    gemm_launches = sum(len(per.get(k, [])) for k in gemm_names) / args.steps
+    # fp32 MFMA kernels carrying the Linear layers.  Algorithmic FLOPs (temporal
+    # columns dropped): per sample 3 x 2 x (4 D^2 + D h1 + h1 h2 + h2 h3) = 442,368 at C2 =
+    #   ncf_attn_block_fwd  2 x 4 D^2          (q/k/v/out projections)
+    #   ncf_attn_block_bwd  2 x 8 D^2          (dO, dXu, 2 x dXi, 4 weight gradients)
+    #   ncf_mlp_fwd         2 x (D h1 + h1 h2 + h2 h3)
+    #   ncf_mlp_bwd         2 x (D h1 + h1 h2 + h2 h3)   (dX of the three Linears)
+    #   ncf_wgrad_grouped   2 x (D h1 + h1 h2 + h2 h3)   (the three MLP weight gradients)
+    # plus any unfused ncf_gemm_* launch (2 M N K, first three arguments).
+    mlp_f = 2.0 * (D * hid[0] + hid[0] * hid[1] + hid[1] * hid[2])
+    per_sample = {"ncf_attn_block_fwd": 8.0 * D * D, "ncf_attn_block_bwd": 16.0 * D * D,
+                  "ncf_mlp_fwd": mlp_f, "ncf_mlp_bwd": mlp_f, "ncf_wgrad_grouped": mlp_f}
+    gemm_names = ("ncf_gemm_direct", "ncf_gemm_f32", "ncf_gemm_rows", "ncf_gemm_f32_splitk")
+    mfma = {}
+    for k, f in per_sample.items():
+        if k in totals:
+            fl = f * N
+            mfma[k] = {"ms": round(totals[k], 4), "gflop": round(fl / 1e9, 4),
+                       "tflops": round(fl / (totals[k] * 1e-3) / 1e12, 2)}
+    gemm_ms = sum(totals.get(k, 0.0) for k in per_sample) + sum(totals.get(k, 0.0) for k in gemm_names)
+    gemm_flops = sum(f * N for k, f in per_sample.items() if k in totals) + sum(
+        2.0 * a[0] * a[1] * a[2] for k in gemm_names for a, _ in per.get(k, [])) / args.steps
+    gemm_launches = sum(len(per.get(k, [])) for k in list(per_sample) + list(gemm_names)) / args.steps
     achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
+    # the dominant MFMA kernel by time: its own roofline (per launch)
+    dom = max(mfma, key=lambda k: mfma[k]["ms"]) if mfma else None
+    dom_launches = len(per.get(dom, [])) / args.steps if dom else 0
+    dom_ms = totals[dom] / max(dom_launches, 1) if dom else 0.0
+    dom_flops = per_sample[dom] * N / max(dom_launches, 1) if dom else 0.0
+    dom_tf = dom_flops / (dom_ms * 1e-3) / 1e12 if dom else 0.0
+    traffic = pmc_traffic(KERNEL_SYMBOL.get(dom)) if dom else None
     # table-update work of the deferred dense-exact Adam: algorithmic = the dense schedule's
     # 24 B per table element per step (what the reference's Adam must move), priced per step
     tab_ms = sum(totals.get(k, 0.0) for k in ("ncf_adam_rows_catchup", "ncf_adam_rows_apply",
@@ -338,12 +382,20 @@ def main():
                                   "host launches"),
                        "parallelism": (f"dp{world} + row-sharded tables (RCCL all-to-all), "
                                        "dense all-reduce") if sharded else "single-gpu"},
-            "roofline": {"bound": "mfma", "kernel": "k_gemm_rows + k_gemm_f32 + k_wgrad_grouped "
-                                                    "(fp32 MFMA v_mfma_f32_32x32x2_f32; every "
-                                                    "attention/MLP GEMM launch of a step)",
-                         "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
-                         "flops_per_step": gemm_flops, "launches_per_step": gemm_launches,
+            "roofline": {"bound": "mfma", "kernel": KERNEL_SYMBOL.get(dom, dom),
+                         "entry_point": dom,
+                         "achieved": round(dom_tf, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": round(dom_tf / FP32_MFMA_PEAK_TFS, 4),
+                         "traffic": traffic["bytes_per_launch"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else None,
+                         "flops_per_launch": dom_flops, "ms_per_launch": round(dom_ms, 4)},
+            "mfma_class": {"kernels": "k_attn_block_fwd/bwd + k_mlp_fwd/bwd + k_wgrad_grouped "
+                                      "(fp32 MFMA v_mfma_f32_16x16x4_f32 / 32x32x2_f32: every "
+                                      "Linear of the step)",
+                           "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFS,
+                           "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFS, 4),
+                           "flops_per_step": gemm_flops, "launches_per_step": gemm_launches,
+                           "per_kernel": mfma,
                          "ms_per_step": round(gemm_ms, 4)},
             "table_adam": {"kernels": "deferred dense-exact Adam (catch-up + apply + 1/64 sweep)",
                            "ms_per_step": round(tab_ms, 4),

@@ -262,6 +262,20 @@ int ncf_sample_negatives(const int64_t* users, const int64_t* pos_items, int64_t
                          int64_t n_users, uint64_t seed, int64_t max_attempts, int64_t* out_users,
                          int64_t* out_items, float* out_targets, int* err_flag, void* stream);
 
+/* ---- 8f rank 4: ranking metrics over [groups, group_len] (src/utils/metrics.py) -----------
+ * ncf_group_metrics: out[4j + {0,1,2,3}] = sums over groups of hit@k, ndcg@k, mrr@k, map@k for
+ *   k = ks[j] (clamped to group_len); out[4nk + {0..4}] = #correct, #positives,
+ *   #correct positives, #negatives, #correct negatives at `threshold`.  Rank order per group:
+ *   prediction desc, column asc.  group_len <= 64, nk <= 16.
+ * ncf_auc_count: *sum_2u = sum over positives (targets == 1) of (#neg < s) + (#neg <= s), with
+ *   neg_sorted = the negatives' predictions ascending; AUC = sum_2u / (2 P N). */
+int64_t ncf_group_metrics_workspace(int64_t groups, int64_t nk);
+int ncf_group_metrics(const float* pred, const float* targets, int64_t groups, int64_t group_len,
+                      const int32_t* ks, int64_t nk, float threshold, double* out,
+                      void* workspace, int64_t workspace_bytes, void* stream);
+int ncf_auc_count(const float* pred, const float* targets, int64_t n, const float* neg_sorted,
+                  int64_t n_neg, unsigned long long* sum_2u, void* stream);
+
 /* ---- a6: TemporalEncoding (architecture.py:59-94): hour/day/month rows + pe[days mod P] -- */
 int ncf_temporal_fwd(const int64_t* hour, const int64_t* day, const int64_t* month,
                      const int64_t* days_since, int64_t n, const float* hour_embed,

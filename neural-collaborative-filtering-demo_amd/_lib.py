@@ -56,6 +56,9 @@ SIGNATURES = {
     "ncf_attn_block_supported": (I32, [I64, I64, I64]),
     "ncf_mlp_fused_supported": (I32, [I64, I64, P]),
     "ncf_alias_build": (I32, [P, I64, P, P]),
+    "ncf_group_metrics_workspace": (I64, [I64, I64]),
+    "ncf_group_metrics": (I32, [P, P, I64, I64, P, I64, F32, P, P, I64, P]),
+    "ncf_auc_count": (I32, [P, P, I64, P, I64, P, P]),
     "ncf_embedding_export": (I32, [P, I64, P, I64, I64, P, P, F32, I32, P, P, P]),
     "ncf_sample_negatives": (I32, [P, P, I64, I64, P, P, I64, P, P, I64, U64, I64, P, P, P, P, P]),
     "ncf_mlp_fwd": (I32, [P, I64, I64, P, I64, P, F32, F32, U64, P, P, P, P, P, P, P, P, P]),

@@ -1,0 +1,76 @@
+"""GPU ranking metrics with the reference's ``calculate_metrics`` interface.
+
+``calculate_metrics(predictions, targets, k_values, batch_size, negative_samples)`` returns the
+same dictionary as src/utils/metrics.py:9-110 — ``hit_rate@k``, ``ndcg@k``, ``mrr@k``,
+``map@k`` per k, ``auc``, ``accuracy``, ``pos_accuracy`` / ``neg_accuracy`` (when such rows
+exist) — computed where the predictions already are: the per-group work (the reference's Python
+loop over users) in one HIP launch (``ncf_group_metrics``), AUC as the Mann-Whitney statistic
+(``ncf_auc_count``; sklearn's roc_auc_score with ties counted one half) over the negatives sorted
+on the device.  Same argument checks and errors.  Tie order inside a group: prediction desc,
+column asc (torch.topk / torch.sort leave it unspecified).  GPU only (no CPU fallback).
+"""
+from typing import Dict, List, Optional
+
+import torch
+
+from . import _lib
+from ._lib import ptr
+
+
+def calculate_metrics(predictions: torch.Tensor, targets: torch.Tensor,
+                      k_values: List[int] = (1, 5, 10), batch_size: Optional[int] = None,
+                      negative_samples: Optional[int] = None) -> Dict[str, float]:
+    p = predictions.detach()
+    t = targets.detach()
+    if p.dim() == 2 and p.size(1) == 1:
+        p = p.squeeze(1)
+    if t.dim() == 2 and t.size(1) == 1:
+        t = t.squeeze(1)
+    if batch_size is None or negative_samples is None:
+        raise ValueError("Please provide both batch_size and negative_samples "
+                         "to reshape predictions into [batch_size, 1+negative_samples].")
+    M = 1 + negative_samples
+    if p.numel() != batch_size * M:
+        raise ValueError(f"Size mismatch: got {p.numel()} total preds, "
+                         f"but expected batch_size*M = {batch_size * M}.")
+    if p.device.type != "cuda":
+        raise RuntimeError("ncf_amd metrics run on the MI355X only (no CPU fallback)")
+    dev = p.device
+    p = p.to(torch.float32).contiguous()
+    t = t.to(device=dev, dtype=torch.float32).contiguous()
+    ks = [int(k) for k in k_values]
+    st = _lib.stream_ptr(dev)
+    nf = 4 * len(ks) + 5
+    ks_dev = torch.tensor(ks, dtype=torch.int32, device=dev)
+    ws = torch.empty(max(1, _lib.query("ncf_group_metrics_workspace", batch_size, len(ks))),
+                     dtype=torch.uint8, device=dev)
+    sums = torch.empty(nf, dtype=torch.float64, device=dev)
+    _lib.call("ncf_group_metrics", ptr(p), ptr(t), batch_size, M, ptr(ks_dev), len(ks), 0.5,
+              ptr(sums), ptr(ws), ws.numel(), st)
+    # AUC (metrics.py:243-256 -> sklearn.metrics.roc_auc_score)
+    neg = torch.sort(p[t == 0]).values
+    n_pos = int((t == 1).sum())
+    n_neg = neg.numel()
+    if n_pos + n_neg != t.numel():
+        raise ValueError("roc_auc_score needs binary targets (0 / 1)")
+    s2u = torch.empty(1, dtype=torch.int64, device=dev)
+    _lib.call("ncf_auc_count", ptr(p), ptr(t), p.numel(), ptr(neg), n_neg, ptr(s2u), st)
+    h = sums.cpu().tolist()
+    out: Dict[str, float] = {}
+    B = float(batch_size)
+    for j, k in enumerate(ks):
+        out[f"hit_rate@{k}"] = h[4 * j] / B
+        out[f"ndcg@{k}"] = h[4 * j + 1] / B
+        out[f"mrr@{k}"] = h[4 * j + 2] / B
+        out[f"map@{k}"] = h[4 * j + 3] / B
+    if n_pos == 0 or n_neg == 0:
+        raise ValueError("Only one class present in y_true. ROC AUC score is not defined in "
+                         "that case.")
+    out["auc"] = float(int(s2u.item())) / (2.0 * n_pos * n_neg)
+    base = 4 * len(ks)
+    out["accuracy"] = h[base] / t.numel()
+    if h[base + 1] > 0:
+        out["pos_accuracy"] = h[base + 2] / h[base + 1]
+    if h[base + 3] > 0:
+        out["neg_accuracy"] = h[base + 4] / h[base + 3]
+    return out

@@ -176,6 +176,44 @@ class FusedTrainStep:
         if self.deferred is not None:
             self.deferred.sync()
 
+    def load_optimizer_state(self, state_dict):
+        """Resume from a ``torch.optim.Adam(model.parameters())`` state_dict (what
+        export_optimizer_state / checkpoint.save_checkpoint and the reference trainer write):
+        moments and step of every trained parameter; the deferred schedule restarts with every
+        row current at that step."""
+        self.sync()
+        eng = self.model.engine
+        idx_of = {id(p): i for i, p in enumerate(self.model.parameters())}
+        st = state_dict["state"]
+
+        def entry(p, what):
+            s = st.get(idx_of[id(p)])
+            if s is None:
+                raise KeyError(f"optimizer state has no entry for {what}")
+            return s
+        step = None
+        for k, p in self.tables.items():
+            s = entry(p, k)
+            self.state[k]["exp_avg"].copy_(s["exp_avg"])
+            self.state[k]["exp_avg_sq"].copy_(s["exp_avg_sq"])
+            step = int(float(s["step"]))
+        for name, p in eng.dense_params():
+            s = entry(p, name)
+            o, n, _ = eng.offsets[name]
+            self.m_flat[o:o + n].copy_(s["exp_avg"].reshape(-1))
+            self.v_flat[o:o + n].copy_(s["exp_avg_sq"].reshape(-1))
+        self.step_count = step or 0
+        d = self.deferred
+        if d is not None:
+            d.t = d.synced_t = self.step_count
+            for stamp in d.stamp.values():
+                stamp.fill_(self.step_count)
+            d._ensure(d.t + 2)
+        if self.clock is not None:
+            self.clock[0] = self.step_count      # ncf_step_clock.t (reserved = 0)
+        self._g = None                           # re-capture from the restored state
+        eng.updates += 1
+
     def export_optimizer_state(self, opt: torch.optim.Adam):
         self.sync()
         eng = self.model.engine

@@ -254,3 +254,51 @@ def negative_distribution(weights, history, positive: int, max_attempts: int = 1
         fb[:] = 1.0 / (n - 1)
         fb[int(positive)] = 0.0
     return direct + tail * fb
+
+
+# ----------------------------------------------------------------------------- 8f: metrics
+def ranking_metrics(preds, targs, k_values, threshold=0.5):
+    """src/utils/metrics.py:9-266 restated per row with plain Python loops (the reference's own
+    loop structure), rank order (prediction desc, column asc); AUC as the Mann-Whitney statistic
+    with ties counted one half (what sklearn's roc_auc_score computes).  preds / targs: [B][M]
+    nested lists of floats."""
+    import math
+    B, M = len(preds), len(preds[0])
+    out = {}
+    for k0 in k_values:
+        k = min(k0, M)
+        hit = nd = mrr = mp = 0.0
+        for p, t in zip(preds, targs):
+            order = sorted(range(M), key=lambda j: (-p[j], j))[:k]
+            rel = [t[j] for j in order]
+            hit += 1.0 if any(r == 1 for r in rel) else 0.0
+            dcg = sum(r / math.log2(i + 2) for i, r in enumerate(rel))
+            ideal = sorted(t, reverse=True)[:k]
+            idcg = sum(r / math.log2(i + 2) for i, r in enumerate(ideal))
+            nd += 0.0 if idcg <= 0 else dcg / idcg
+            first = next((i for i, r in enumerate(rel) if r == 1), None)
+            mrr += 0.0 if first is None else 1.0 / (first + 1)
+            cum, s, c = 0, 0.0, 0
+            for i, r in enumerate(rel):
+                if r == 1:
+                    cum += 1
+                    s += cum / (i + 1)
+                    c += 1
+            mp += s / max(c, 1) if c else 0.0
+        out[f"hit_rate@{k0}"] = hit / B
+        out[f"ndcg@{k0}"] = nd / B
+        out[f"mrr@{k0}"] = mrr / B
+        out[f"map@{k0}"] = mp / B
+    flat_p = [x for row in preds for x in row]
+    flat_t = [x for row in targs for x in row]
+    pos = [x for x, y in zip(flat_p, flat_t) if y == 1]
+    neg = [x for x, y in zip(flat_p, flat_t) if y == 0]
+    u = sum((1.0 if a > b else 0.5 if a == b else 0.0) for a in pos for b in neg)
+    out["auc"] = u / (len(pos) * len(neg))
+    ok = [(x >= threshold) == (y == 1) for x, y in zip(flat_p, flat_t)]
+    out["accuracy"] = sum(ok) / len(ok)
+    if pos:
+        out["pos_accuracy"] = sum(o for o, y in zip(ok, flat_t) if y == 1) / len(pos)
+    if neg:
+        out["neg_accuracy"] = sum(o for o, y in zip(ok, flat_t) if y == 0) / len(neg)
+    return out

@@ -53,3 +53,13 @@ def f5():
 @pytest.fixture(scope="session")
 def f6():
     return load_npz("f6_hour.npz")
+
+
+@pytest.fixture(scope="session")
+def f7():
+    return load_npz("f7_metrics.npz")
+
+
+@pytest.fixture(scope="session")
+def f8():
+    return load_npz("f8_negatives.npz")

@@ -32,6 +32,11 @@ Fixtures written to tests/golden/*.npz (inputs and expected outputs only):
                            The reference draws a fresh nn.Linear(T, D) inside every call
                            (architecture.py:437-442); seeding torch right before the call fixes
                            its init, and the same seed reproduces its weights, stored here.
+  F7 f7_metrics.npz        src/utils/metrics.py calculate_metrics on seeded predictions (no ties)
+  F8 f8_negatives.npz      src/model/data_prep.py SheetzDataset on a synthetic interaction log:
+                           the train interaction list, product_weights, user histories, and the
+                           empirical distribution of 40,000 _sample_negative draws (np seed 0)
+                           for a few (user, positive) pairs
 """
 import argparse
 import csv
@@ -289,6 +294,67 @@ def make_f6(AdvancedNCF, sd):
     print("F6 written; scores[0][:4]", scores[0][:4].tolist())
 
 
+def make_f7(ref):
+    from src.utils.metrics import calculate_metrics
+    out = {}
+    for name, (B, M, seed) in {"a": (64, 5, 0), "b": (33, 8, 1)}.items():
+        g = torch.Generator().manual_seed(seed)
+        p = torch.rand(B * M, 1, generator=g)
+        t = torch.zeros(B, M)
+        t[:, 0] = 1
+        t[torch.rand(B, M, generator=g) < 0.15] = 1
+        t = t.reshape(-1, 1)
+        m = calculate_metrics(p, t, k_values=[1, 5, 10], batch_size=B, negative_samples=M - 1)
+        out[f"{name}_pred"] = p.numpy()
+        out[f"{name}_targ"] = t.numpy()
+        out[f"{name}_shape"] = np.array([B, M])
+        out[f"{name}_keys"] = np.array(list(m.keys()))
+        out[f"{name}_vals"] = np.array([float(v) for v in m.values()])
+    np.savez_compressed(os.path.join(HERE, "f7_metrics.npz"), **out)
+    print("F7 written;", dict(zip(out["a_keys"][:4], out["a_vals"][:4])))
+
+
+def make_f8(ref):
+    import pandas as pd
+    from src.model.data_prep import SheetzDataset
+    rng = np.random.default_rng(8)
+    U, I, P = 30, 40, 400
+    users = rng.integers(0, U, P)
+    prods = np.minimum(rng.zipf(1.4, P) - 1, I - 1)
+    days = rng.integers(0, 60, P)
+    ts = pd.Timestamp("2024-01-01") + pd.to_timedelta(days, unit="D")
+    inter = pd.DataFrame({"user_id": [f"U{u}" for u in users], "product_id": [f"P{p}" for p in prods],
+                          "amount": rng.random(P), "transaction_timestamp": ts})
+    ufeat = pd.DataFrame({"cardnumber": [f"U{u}" for u in range(U)],
+                          "recent_interactions": [0] * U, "preferred_categories": [""] * U})
+    pfeat = pd.DataFrame({"product_id": [f"P{p}" for p in range(I)], "total_purchases": [0] * I,
+                          "total_revenue": [0.0] * I})
+    ds = SheetzDataset(inter, ufeat, pfeat, mode="train", validation_days=10, negative_samples=4)
+    il = np.array([(u, p) for u, p, _ in ds.interaction_list], dtype=np.int64)
+    hist_u, hist_i = [], []
+    for u, items in sorted(ds.user_product_history.items()):
+        for i in sorted(items):
+            hist_u.append(u)
+            hist_i.append(i)
+    # a light user, a heavy user (the fallback path), the most popular product as positive
+    by_len = sorted(ds.user_product_history, key=lambda u: len(ds.user_product_history[u]))
+    picks = [by_len[0], by_len[len(by_len) // 2], by_len[-1]]
+    pairs, counts = [], []
+    np.random.seed(0)
+    for u in picks:
+        pos = sorted(ds.user_product_history[u])[0]
+        c = np.zeros(ds.num_products, dtype=np.int64)
+        for _ in range(40_000):
+            c[ds._sample_negative(u, pos)] += 1
+        pairs.append((u, pos))
+        counts.append(c)
+    np.savez_compressed(os.path.join(HERE, "f8_negatives.npz"), interactions=il,
+                        num_users=ds.num_users, num_products=ds.num_products,
+                        product_weights=ds.product_weights, hist_u=np.array(hist_u),
+                        hist_i=np.array(hist_i), pairs=np.array(pairs), counts=np.array(counts))
+    print("F8 written;", len(il), "train interactions; pairs", pairs)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
@@ -300,6 +366,9 @@ def main():
     if a.only == "f6":
         make_f6(AdvancedNCF, sd)
         return
+    if a.only in ("f7", "f8"):
+        (make_f7 if a.only == "f7" else make_f8)(a.reference)
+        return
     make_f1(a.reference, AdvancedNCF, KJT, sd)
     make_train("f2_train_c2.npz", AdvancedNCF, KJT, U=300, I=120, D=64, T=32,
                hidden=[256, 128, 64], H=4, B=8, M=5, steps=3, seed=0, lr=1e-3, wd=1e-5)
@@ -308,6 +377,8 @@ def main():
     make_f4(MHA, TE)
     make_f5(AdvancedNCF, KJT, sd)
     make_f6(AdvancedNCF, sd)
+    make_f7(a.reference)
+    make_f8(a.reference)
 
 
 if __name__ == "__main__":

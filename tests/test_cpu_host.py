@@ -203,3 +203,57 @@ def test_embeddings_jsonl_format():
     rec = [json.loads(x) for x in lines]
     assert rec[1] == {"id": "P2", "embedding": [1.0, 0.0]}
     assert rec[0]["embedding"] == [float(np.float32(0.6)), float(np.float32(0.8))]
+
+
+# ----------------------------------------------------------------------------- 8f: checkpoints
+def test_load_unzipped_archive_roundtrip(tmp_path):
+    """An extracted torch.save archive (the layout of the reference's demo model directory) is
+    read back through weights_only loading with its own keys, shapes and strides."""
+    import zipfile
+    from collections import OrderedDict
+    from ncf_amd.checkpoint import load_unzipped_archive
+    g = torch.Generator().manual_seed(0)
+    base = torch.randn(6, 4, generator=g)
+    sd = OrderedDict([("a.weight", torch.randn(3, 5, generator=g)), ("b", base),
+                      ("c.t", base.t()), ("d", torch.arange(7))])
+    f = tmp_path / "m.pt"
+    torch.save(sd, f)
+    out = tmp_path / "unzipped"
+    with zipfile.ZipFile(f) as z:
+        root = z.namelist()[0].split("/")[0]
+        z.extractall(tmp_path / "x")
+    os.rename(tmp_path / "x" / root, out)
+    got = load_unzipped_archive(str(out))
+    assert list(got) == list(sd)
+    for k in sd:
+        assert torch.equal(got[k], sd[k]) and got[k].stride() == sd[k].stride()
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src/inference/demo/train_20241225_002713_model"),
+                    reason="reference checkout not present")
+def test_load_reference_demo_directory():
+    """The reference's own unzipped demo checkpoint (consolidate_shards.py's input) loads with
+    all 62 keys in order and the AdvancedNCF shapes (safe loader; container-only check)."""
+    from ncf_amd.checkpoint import load_unzipped_archive
+    sd = load_unzipped_archive("/root/reference/src/inference/demo/train_20241225_002713_model")
+    assert len(sd) == 62 and list(sd)[0] == "mf_norm.weight"
+    assert sd["mf_embedding_collection.embedding_bags.user_id.weight"].shape == (8031, 64)
+    assert sd["mlp.0.weight"].shape == (256, 96)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_row_shards_roundtrip(world):
+    from collections import OrderedDict
+    from ncf_amd.checkpoint import TABLE_KEYS, consolidate_row_shards, shard_state_dict
+    g = torch.Generator().manual_seed(world)
+    U, I, D = 11, 7, 4
+    full = OrderedDict()
+    for k in TABLE_KEYS:
+        full[k] = torch.randn(U if ".user_id." in k else I, D, generator=g)
+    full["mlp.0.weight"] = torch.randn(5, 3, generator=g)
+    shards = [shard_state_dict(full, world, r) for r in range(world)]
+    assert shards[0][TABLE_KEYS[0]].shape == (-(-U // world), D)
+    back = consolidate_row_shards(shards, world, U, I)
+    assert list(back) == list(full)
+    for k in full:
+        assert torch.equal(back[k], full[k])

@@ -1022,3 +1022,114 @@ def test_product_embedding_export_vs_reference(f5):
     emb = np.array([r["embedding"] for r in recs])
     np.testing.assert_allclose(emb, ln.numpy()[np.arange(400) % 366], atol=2e-6)
     np.testing.assert_allclose(np.linalg.norm(emb, axis=1), 1.0, atol=1e-6)
+
+
+# ----------------------------------------------------------------------------- 8f: checkpoints
+def test_checkpoint_resume_is_exact(tmp_path):
+    """save_checkpoint mid-run (trainer.py:548-585 format, FusedTrainStep moments in torch Adam
+    state_dict form), load_checkpoint into a fresh model + step, continue: identical parameters
+    to the uninterrupted run (dropout 0, deferred schedule restarted fully synced)."""
+    from ncf_amd.checkpoint import load_checkpoint, save_checkpoint
+    from ncf_amd.trainer import FusedTrainStep
+    U, I, B = 300, 120, 32
+    g = torch.Generator().manual_seed(3)
+    batches = []
+    for _ in range(8):
+        u = torch.randint(0, U, (B,), generator=g).repeat_interleave(5).to(DEV)
+        i = torch.randint(0, I, (B * 5,), generator=g).to(DEV)
+        t = torch.zeros(B, 5)
+        t[:, 0] = 1
+        batches.append((u, i, t.reshape(-1, 1).to(DEV)))
+
+    def fresh():
+        torch.manual_seed(9)
+        m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.0, 4).to(DEV)
+        return m, FusedTrainStep(m, lr=1e-2, weight_decay=1e-5)
+    m1, s1 = fresh()
+    for b in batches[:4]:
+        s1(*b)
+    path = str(tmp_path / "ckpt.pt")
+    save_checkpoint(path, m1, s1, epoch=2, metrics={"loss": 0.5}, config={"learning_rate": 1e-2})
+    for b in batches[4:]:
+        s1(*b)
+    ref = {k: v.detach().cpu().clone() for k, v in m1.state_dict().items()}
+    m2, s2 = fresh()
+    assert load_checkpoint(path, m2, s2) == 3
+    for b in batches[4:]:
+        s2(*b)
+    got = m2.state_dict()
+    for k in ref:
+        assert torch.equal(got[k].cpu(), ref[k]), k
+    ck = torch.load(path, weights_only=True, map_location="cpu")
+    assert set(ck) == {"epoch", "model_state_dict", "optimizer_state_dict", "metrics", "config",
+                       "model_config"}
+    assert ck["model_config"] == {"num_users": U, "num_products": I, "embedding_dim": 64}
+
+
+# ----------------------------------------------------------------------------- 8f: metrics
+@pytest.mark.parametrize("B,M,ties", [(300, 5, False), (257, 5, True), (40, 12, False)])
+def test_calculate_metrics_vs_reference_loops(B, M, ties):
+    """ncf_amd.metrics.calculate_metrics vs the oracle restatement of src/utils/metrics.py (the
+    reference's per-row loops) and sklearn's roc_auc_score; ties exercise AUC's one-half rule
+    (both sides rank ties column-ascending)."""
+    from sklearn.metrics import roc_auc_score
+    from oracle import ncf_oracle as O
+    from ncf_amd.metrics import calculate_metrics
+    g = torch.Generator().manual_seed(B + M)
+    p = torch.rand(B, M, generator=g)
+    if ties:
+        p = (p * 10).round() / 10
+    t = torch.zeros(B, M)
+    t[:, 0] = 1
+    t[torch.rand(B, M, generator=g) < 0.1] = 1        # some groups with several positives
+    got = calculate_metrics(p.reshape(-1, 1).to(DEV), t.reshape(-1, 1).to(DEV), [1, 5, 10],
+                            batch_size=B, negative_samples=M - 1)
+    ref = O.ranking_metrics(p.tolist(), t.tolist(), [1, 5, 10])
+    assert list(got) == list(ref)
+    for k in ref:
+        assert abs(got[k] - ref[k]) < 1e-9, (k, got[k], ref[k])
+    assert abs(got["auc"] - roc_auc_score(t.reshape(-1).numpy(), p.reshape(-1).numpy())) < 1e-12
+
+
+def test_calculate_metrics_errors_like_reference():
+    from ncf_amd.metrics import calculate_metrics
+    p = torch.rand(20, device=DEV)
+    t = torch.ones(20, device=DEV)
+    with pytest.raises(ValueError, match="batch_size and negative_samples"):
+        calculate_metrics(p, t)
+    with pytest.raises(ValueError, match="Size mismatch"):
+        calculate_metrics(p, t, batch_size=3, negative_samples=4)
+    with pytest.raises(ValueError, match="Only one class"):   # validate(): M = 1, all positives
+        calculate_metrics(p, t, batch_size=20, negative_samples=0)
+
+
+def test_f7_metrics_match_reference(f7):
+    from ncf_amd.metrics import calculate_metrics
+    for c in ("a", "b"):
+        B, M = f7[f"{c}_shape"].tolist()
+        got = calculate_metrics(torch.from_numpy(f7[f"{c}_pred"]).to(DEV),
+                                torch.from_numpy(f7[f"{c}_targ"]).to(DEV), [1, 5, 10],
+                                batch_size=B, negative_samples=M - 1)
+        keys = [str(k) for k in f7[f"{c}_keys"]]
+        assert list(got) == keys
+        np.testing.assert_allclose([got[k] for k in keys], f7[f"{c}_vals"], atol=1e-6)
+
+
+def test_f8_device_sampler_matches_reference_draws(f8):
+    """Device negatives vs the reference's own _sample_negative draws (F8), per (user, positive):
+    same weights; per-item frequencies agree within 6 sigma of a two-sample difference."""
+    from ncf_amd.data import DeviceNegativeSampler
+    inter = torch.from_numpy(f8["interactions"])
+    U, I = int(f8["num_users"]), int(f8["num_products"])
+    s = DeviceNegativeSampler(inter[:, 0], inter[:, 1], U, I, negative_samples=4, device=DEV)
+    np.testing.assert_allclose(s.weights, f8["product_weights"], rtol=1e-12)
+    for (u, pos), cnt in zip(f8["pairs"], f8["counts"]):
+        idx = int(((inter[:, 0] == int(u)) & (inter[:, 1] == int(pos))).nonzero()[0])
+        kjt, _ = s.batch(torch.full((20_000,), idx), seed=int(u))
+        neg = kjt.values().view(2, -1, 5)[1][:, 1:].reshape(-1).cpu().numpy()
+        a = np.bincount(neg, minlength=I) / neg.size
+        n2 = cnt.sum()
+        b = cnt / n2
+        pool = (a * neg.size + cnt) / (neg.size + n2)
+        sig = np.sqrt(np.maximum(pool * (1 - pool), 1e-12) * (1 / neg.size + 1 / n2))
+        assert np.all(np.abs(a - b) <= 6 * sig + 1e-9), (u, np.max(np.abs(a - b) / (sig + 1e-12)))

@@ -127,3 +127,31 @@ def test_f6_forward_simple_hour(f5, f6):
         s = O.forward_simple_hour(p, u, items, h, torch.from_numpy(f6["proj_w"][c]),
                                   torch.from_numpy(f6["proj_b"][c]), num_heads=4, n_layers=3)
         np.testing.assert_allclose(s.numpy(), f6["scores"][c], atol=1e-6)
+
+
+def test_f7_metrics_oracle(f7):
+    """oracle.ranking_metrics == the reference's calculate_metrics (F7) on the same inputs."""
+    for c in ("a", "b"):
+        B, M = f7[f"{c}_shape"].tolist()
+        p = f7[f"{c}_pred"].reshape(B, M).tolist()
+        t = f7[f"{c}_targ"].reshape(B, M).tolist()
+        got = O.ranking_metrics(p, t, [1, 5, 10])
+        keys = [str(k) for k in f7[f"{c}_keys"]]
+        assert list(got) == keys
+        np.testing.assert_allclose([got[k] for k in keys], f7[f"{c}_vals"], atol=1e-6)
+
+
+def test_f8_negative_sampling_oracle(f8):
+    """oracle weights == SheetzDataset.product_weights; oracle.negative_distribution matches
+    40,000 of the reference's own _sample_negative draws per pair (6 sigma)."""
+    inter = f8["interactions"]
+    I = int(f8["num_products"])
+    w = O.inverse_popularity_weights(inter[:, 1].tolist(), I)
+    np.testing.assert_allclose(w, f8["product_weights"], rtol=1e-12)
+    hu, hi = f8["hist_u"], f8["hist_i"]
+    for (u, pos), cnt in zip(f8["pairs"], f8["counts"]):
+        exp = O.negative_distribution(w, hi[hu == u].tolist(), int(pos))
+        n = cnt.sum()
+        emp = cnt / n
+        sig = np.sqrt(np.maximum(exp * (1 - exp), 1e-12) / n)
+        assert np.all(np.abs(emp - exp) <= 6 * sig + 1e-9)
