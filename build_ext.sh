@@ -3,12 +3,12 @@
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")" && pwd)"
 SRC="$ROOT/neural-collaborative-filtering-demo_amd/csrc"
-OUT="$ROOT/neural-collaborative-filtering-demo_amd/libncf_hip.so"
+OUT="${NCF_OUT:-$ROOT/neural-collaborative-filtering-demo_amd/libncf_hip.so}"   # NCF_OUT: A/B builds
 HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
-OBJ="$SRC/build"
+OBJ="${NCF_OBJ:-$SRC/build}"
 mkdir -p "$OBJ"
 rm -f "$OBJ"/*.o
-FLAGS=(--offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$SRC" -I"$ROOT/include" -Wall -Wno-unused-function)
+FLAGS=(--offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$SRC" -I"$ROOT/include" -Wall -Wno-unused-function ${NCF_EXTRA_FLAGS:-})
 pids=()
 for f in "$SRC"/*.hip; do
   b="$(basename "$f" .hip)"

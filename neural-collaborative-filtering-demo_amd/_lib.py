@@ -15,7 +15,7 @@ import threading
 import torch  # noqa: F401  (must precede the CDLL: binds libncf_hip to torch's HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libncf_hip.so")
+LIB_PATH = os.environ.get("NCF_HIP_LIB") or os.path.join(_HERE, "libncf_hip.so")   # env: A/B builds
 
 
 class NCFLibraryError(RuntimeError):

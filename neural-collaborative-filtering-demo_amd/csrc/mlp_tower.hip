@@ -9,15 +9,18 @@
 // index row*W + col with the per-layer seed (seed + 0x9E37*(l+1)) & (2^63-1) (+ the step clock).
 // Only the fmaf order of the Linear layers (k-permuted MFMA below) differs.
 //
-// Tiling: a 256-thread workgroup (4 waves) owns kRows = 16 rows for the whole tower; the rows
-// live in LDS between layers (buffers Q [16][260] and P [16][196], 29 KB: five workgroups per
-// CU, so the 1280 workgroups of a 20,480-row step are resident at once and hide each other's
-// latencies).  Row ops run in place; a layer's output goes to the other buffer.
-//  * Linear: 16x16 output tiles of v_mfma_f32_16x16x4_f32; wave w takes column slices w + 4q.  k-permuted operands: in MFMA step s lane group g = lane>>4
-//    supplies k = g*K/4 + s, so a lane's A row slice (LDS) and weight row slice (global/L2) are
-//    contiguous float4 runs.  Two accumulators (even / odd float4 chunks) halve the dependent
-//    MFMA chain.
-//  * Row ops: 16 lanes per row, width/64 float4 chunks per lane (the column map of rowops.hip).
+// Tiling: a 512-thread workgroup (8 waves) owns kRows = 80 rows (5 MFMA row tiles) for the whole
+// tower; the rows live in LDS between layers (buffers Q [80][260] and P [80][132], 125 KB: one
+// workgroup per CU, 256 of them at 20,480 rows).  Row ops run in place; a layer's output goes to
+// the other buffer.
+//  * Linear: 16x16 output tiles of v_mfma_f32_16x16x4_f32.  A wave loads each weight chunk
+//    (4 k-steps of its column) once from L2 and feeds all its row tiles with it (independent
+//    accumulators): every weight byte serves 80 rows (~40 flop/B), where a 16-row tile left the
+//    Linear phases bound by L2 weight traffic.  k-permuted operands: in MFMA step s lane group
+//    g = lane>>4 supplies k = g*K/4 + s, so a lane's A row slice (LDS) and weight row slice are
+//    contiguous float4 runs.
+//  * Row ops: 16 lanes per row, width/64 float4 chunks per lane (the column map of rowops.hip),
+//    32 rows per pass.
 // Forward writes what the backward and the weight gradients read (r, a, mean, rstd; NULL
 // pointers skip them in eval).  Backward starts from dL/da of the last layer (head.hip), writes
 // dlin per layer (the weight gradients' dY) and dX of the tower input, and leaves per-workgroup
@@ -26,12 +29,18 @@
 
 namespace {
 
-constexpr int kRows = 16;
-constexpr int kThreads = 256;
+#ifndef NCF_BWD_RING
+#define NCF_BWD_RING 4
+#endif
+constexpr int kRT = 5;                 // 16-row MFMA row tiles per workgroup
+constexpr int kRows = 16 * kRT;        // 80 rows: 256 workgroups = one per CU at 20,480 rows
+constexpr int kThreads = 512;          // 8 waves
+constexpr int kWaves = kThreads / 64;
 constexpr int kPQ = 260;   // pitch of buffer Q (<= 256 columns)
-constexpr int kPP = 196;   // pitch of buffer P (<= 128 columns; 4 x 3 x 256 scratch floats)
+constexpr int kPP = 132;   // pitch of buffer P (<= 128 columns; also the 8 x 3 x 256 scratch)
 constexpr int K0 = 64, N0 = 256, N1 = 128, N2 = 64;
 constexpr int kPartW = 3 * (N0 + N1 + N2);   // partial floats per workgroup
+constexpr int kPasses = (kRows * 16 + kThreads - 1) / kThreads;   // row-op passes (16 lanes/row)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -51,198 +60,277 @@ __device__ __forceinline__ f32x4 mfma4(float4 a, float4 b, f32x4 acc) {
   return acc;
 }
 
-// Y[16 x N] = relu(X[16 x K] . W^T + b)   (W row-major [N][ldw], first K columns)
+// Work split of an [80 x N] Linear output over the 8 waves: NS = N/16 column slices; with
+// NS >= 8 wave w takes slices w + 8j for all 5 row tiles, with NS < 8 (N = 64) slice w % NS for
+// the row tiles rt = w / NS + S r (S = 8 / NS).  A wave loads each weight chunk once and feeds
+// it to all its row tiles (independent MFMA chains): 5 x reuse of every weight byte from L2.
+template <int N>
+struct Split {
+  static constexpr int NS = N / 16;
+  static constexpr int S = NS >= kWaves ? 1 : kWaves / NS;
+  static constexpr int CPW = NS >= kWaves ? NS / kWaves : 1;   // column slices per wave
+  static constexpr int RPW = (kRT + S - 1) / S;                 // row tiles per wave (max)
+  __device__ static int cs(int w, int j) { return NS >= kWaves ? w + kWaves * j : w % NS; }
+  __device__ static int rt(int w, int r) { return NS >= kWaves ? r : w / NS + S * r; }
+};
+
+// Y[80 x N] = relu(X[80 x K] . W^T + b)   (W row-major [N][ldw], first K columns)
 template <int K, int N, int PX, int PY>
 __device__ __forceinline__ void lin_fwd(const float* __restrict__ X, float* __restrict__ Y,
                                         const float* __restrict__ W, int64_t ldw,
                                         const float* __restrict__ bias) {
+  using Sp = Split<N>;
   constexpr int KQ = K / 4;
-  constexpr int PER = N / 64;
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-  const float* ap = X + i * PX + g * KQ;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
 #pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int cs = wv + 4 * q;
+  for (int j = 0; j < Sp::CPW; ++j) {
+    const int cs = Sp::cs(w, j);
     const float* wp = W + (int64_t)(16 * cs + i) * ldw + g * KQ;
-    const float bb = bias[16 * cs + i];
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[Sp::RPW];
+#pragma unroll
+    for (int r = 0; r < Sp::RPW; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < KQ / 4; ++c) {
       const float4 b = ld4(wp + 4 * c);
-      const float4 a = lds4(ap + 4 * c);
-      if (c & 1) acc1 = mfma4(a, b, acc1);
-      else acc0 = mfma4(a, b, acc0);
-    }
-    float* yp = Y + (4 * g) * PY + 16 * cs + i;   // C: rows 4g + r, column 16cs + (lane & 15)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) yp[r * PY] = fmaxf(acc0[r] + acc1[r] + bb, 0.0f);
+      for (int r = 0; r < Sp::RPW; ++r) {
+        const int rt = Sp::rt(w, r);
+        if (rt < kRT) acc[r] = mfma4(lds4(X + (16 * rt + i) * PX + g * KQ + 4 * c), b, acc[r]);
+      }
+    }
+    const float bb = bias[16 * cs + i];
+#pragma unroll
+    for (int r = 0; r < Sp::RPW; ++r) {
+      const int rt = Sp::rt(w, r);
+      if (rt < kRT) {
+        float* yp = Y + (16 * rt + 4 * g) * PY + 16 * cs + i;   // C: rows 4g + e, column 16cs + i
+#pragma unroll
+        for (int e = 0; e < 4; ++e) yp[e * PY] = fmaxf(acc[r][e] + bb, 0.0f);
+      }
+    }
   }
 }
 
-// G[16 x NO] = DL[16 x KC] . W   (W row-major [KC][ldw], first NO columns)
+// G[80 x NO] = DL[80 x KC] . W   (W row-major [KC][ldw], first NO columns)
 template <int KC, int NO, int PD, int PG>
 __device__ __forceinline__ void lin_bwd(const float* __restrict__ DL, float* __restrict__ G,
                                         const float* __restrict__ W, int64_t ldw) {
+  using Sp = Split<NO>;
   constexpr int KQ = KC / 4;
-  constexpr int PER = NO / 64;
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-  const float* ap = DL + i * PD + g * KQ;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
 #pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int cs = wv + 4 * q;
+  for (int j = 0; j < Sp::CPW; ++j) {
+    const int cs = Sp::cs(w, j);
     const float* wp = W + (int64_t)(g * KQ) * ldw + 16 * cs + i;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[Sp::RPW];
 #pragma unroll
-    for (int c = 0; c < KQ / 4; ++c) {
-      const float4 b = make_float4(wp[(4 * c) * ldw], wp[(4 * c + 1) * ldw], wp[(4 * c + 2) * ldw],
-                                   wp[(4 * c + 3) * ldw]);
-      const float4 a = lds4(ap + 4 * c);
-      if (c & 1) acc1 = mfma4(a, b, acc1);
-      else acc0 = mfma4(a, b, acc0);
+    for (int r = 0; r < Sp::RPW; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // strided weight columns: a ring of NCF_BWD_RING chunks keeps the scalar loads ahead
+    constexpr int NC = KQ / 4;
+    constexpr int D = NCF_BWD_RING < NC ? NCF_BWD_RING : NC;
+    auto chunk = [&](int c) {
+      const float* q = wp + (int64_t)(4 * c) * ldw;
+      return make_float4(q[0], q[ldw], q[2 * ldw], q[3 * ldw]);
+    };
+    float4 ring[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) ring[c] = chunk(c);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float4 b = ring[c % D];
+      if (c + D < NC) ring[c % D] = chunk(c + D);
+#pragma unroll
+      for (int r = 0; r < Sp::RPW; ++r) {
+        const int rt = Sp::rt(w, r);
+        if (rt < kRT) acc[r] = mfma4(lds4(DL + (16 * rt + i) * PD + g * KQ + 4 * c), b, acc[r]);
+      }
     }
-    float* gp = G + (4 * g) * PG + 16 * cs + i;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) gp[r * PG] = acc0[r] + acc1[r];
+    for (int r = 0; r < Sp::RPW; ++r) {
+      const int rt = Sp::rt(w, r);
+      if (rt < kRT) {
+        float* gp = G + (16 * rt + 4 * g) * PG + 16 * cs + i;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gp[e * PG] = acc[r][e];
+      }
+    }
   }
 }
 
 // LayerNorm + dropout of the ReLU rows in Y, in place (the next layer's input); saves r, a,
-// mean, rstd.  Returns the row's dot product with hw (the mlp_output weight) when hw != NULL.
+// mean, rstd.  16 lanes per row, kPasses passes over the 80 rows.  With hw != NULL, also the
+// head: mlp_pred = a . hw + b_out, prob = sigmoid(w0 mf_pred + w1 mlp_pred + b_fin).
 template <int N, int PY>
-__device__ __forceinline__ float ln_fwd(float* __restrict__ Y, int64_t row0, int rows,
-                                        const ncf_mlp_layer& L, float eps, float p, uint64_t seed,
-                                        const float* __restrict__ hw) {
+__device__ __forceinline__ void ln_fwd(float* __restrict__ Y, int64_t row0, int rows,
+                                       const ncf_mlp_layer& L, float eps, float p, uint64_t seed,
+                                       const float* __restrict__ hw, const float* __restrict__ b_out,
+                                       const float* __restrict__ mf_pred,
+                                       const float* __restrict__ w_fin,
+                                       const float* __restrict__ b_fin,
+                                       float* __restrict__ mlp_pred, float* __restrict__ prob) {
   constexpr int CH = N / 64;
-  const int rr = threadIdx.x >> 4, sub = threadIdx.x & 15;
-  const int64_t row = row0 + rr;
-  const bool ok = rr < rows;
-  float4 x[CH];
-  float s = 0.0f;
-#pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    const int col = (c * 16 + sub) * 4;
-    x[c] = lds4(Y + rr * PY + col);
-    if (ok && L.r) st4(L.r + row * N + col, x[c]);
-    s += x[c].x + x[c].y + x[c].z + x[c].w;
-  }
-  const float mean = group_sum<16>(s) * (1.0f / N);
-  float qv = 0.0f;
-#pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    x[c].x -= mean; x[c].y -= mean; x[c].z -= mean; x[c].w -= mean;
-    qv += x[c].x * x[c].x + x[c].y * x[c].y + x[c].z * x[c].z + x[c].w * x[c].w;
-  }
-  const float rstd = 1.0f / sqrtf(group_sum<16>(qv) * (1.0f / N) + eps);
+  const int sub = threadIdx.x & 15;
   const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
-  float dot = 0.0f;
 #pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    const int col = (c * 16 + sub) * 4;
-    const float4 gg = ld4(L.gamma + col), bb = ld4(L.beta + col);
-    float4 y = make_float4(x[c].x * rstd * gg.x + bb.x, x[c].y * rstd * gg.y + bb.y,
-                           x[c].z * rstd * gg.z + bb.z, x[c].w * rstd * gg.w + bb.w);
-    if (p > 0.0f) {
-      const float4 k = ncf_dropout_scale4(seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
-      y.x *= k.x; y.y *= k.y; y.z *= k.z; y.w *= k.w;
+  for (int pass = 0; pass < kPasses; ++pass) {
+    const int rr = (threadIdx.x >> 4) + pass * (kThreads / 16);
+    if (rr >= kRows) break;   // whole 16-lane row groups leave together
+    const int64_t row = row0 + rr;
+    const bool ok = rr < rows;
+    float4 x[CH];
+    float s = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = (c * 16 + sub) * 4;
+      x[c] = lds4(Y + rr * PY + col);
+      if (ok && L.r) st4(L.r + row * N + col, x[c]);
+      s += x[c].x + x[c].y + x[c].z + x[c].w;
     }
-    lds4_st(Y + rr * PY + col, y);
-    if (ok && L.a) st4(L.a + row * N + col, y);
+    const float mean = group_sum<16>(s) * (1.0f / N);
+    float qv = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      x[c].x -= mean; x[c].y -= mean; x[c].z -= mean; x[c].w -= mean;
+      qv += x[c].x * x[c].x + x[c].y * x[c].y + x[c].z * x[c].z + x[c].w * x[c].w;
+    }
+    const float rstd = 1.0f / sqrtf(group_sum<16>(qv) * (1.0f / N) + eps);
+    float dot = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = (c * 16 + sub) * 4;
+      const float4 gg = ld4(L.gamma + col), bb = ld4(L.beta + col);
+      float4 y = make_float4(x[c].x * rstd * gg.x + bb.x, x[c].y * rstd * gg.y + bb.y,
+                             x[c].z * rstd * gg.z + bb.z, x[c].w * rstd * gg.w + bb.w);
+      if (p > 0.0f) {
+        const float4 k = ncf_dropout_scale4(seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
+        y.x *= k.x; y.y *= k.y; y.z *= k.z; y.w *= k.w;
+      }
+      lds4_st(Y + rr * PY + col, y);
+      if (ok && L.a) st4(L.a + row * N + col, y);
+      if (hw) {
+        const float4 h = ld4(hw + col);
+        dot = fmaf(y.x, h.x, dot); dot = fmaf(y.y, h.y, dot);
+        dot = fmaf(y.z, h.z, dot); dot = fmaf(y.w, h.w, dot);
+      }
+    }
+    if (ok && sub == 0 && L.mean) {
+      L.mean[row] = mean;
+      L.rstd[row] = rstd;
+    }
     if (hw) {
-      const float4 h = ld4(hw + col);
-      dot = fmaf(y.x, h.x, dot); dot = fmaf(y.y, h.y, dot);
-      dot = fmaf(y.z, h.z, dot); dot = fmaf(y.w, h.w, dot);
+      dot = group_sum<16>(dot);
+      if (ok && sub == 0) {
+        const float mp = dot + b_out[0];
+        mlp_pred[row] = mp;
+        const float z = w_fin[0] * mf_pred[row] + w_fin[1] * mp + b_fin[0];
+        prob[row] = 1.0f / (1.0f + expf(-z));
+      }
     }
   }
-  if (ok && sub == 0 && L.mean) {
-    L.mean[row] = mean;
-    L.rstd[row] = rstd;
-  }
-  return hw ? group_sum<16>(dot) : 0.0f;
 }
 
-// Backward of dropout -> LayerNorm -> ReLU for the 16 rows, in place: G (dL/da) -> dL/dlin
+// Backward of dropout -> LayerNorm -> ReLU for the 80 rows, in place: G (dL/da) -> dL/dlin
 // (also to HBM); this workgroup's column sums [dbias | dgamma | dbeta] -> part[0 : 3N), through
-// the free buffer S (4 waves x 3N floats).
+// the free buffer S (8 waves x 3N floats).
 template <int N, int PG>
 __device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict__ S, int64_t row0,
                                        int rows, const ncf_mlp_layer& L, float p, uint64_t seed,
                                        float* __restrict__ part) {
   constexpr int CH = N / 64;
-  const int rr = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int sub = threadIdx.x & 15;
   const int wv = threadIdx.x >> 6;
-  const int64_t row = row0 + rr;
-  const bool ok = rr < rows;
-  const float mu = ok ? L.mean[row] : 0.0f, rs = ok ? L.rstd[row] : 0.0f;
   const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
-  float4 gd[CH], xh[CH];
-  uint32_t pos = 0;   // ReLU mask: bit 4c + e <=> r > 0
-  float s1 = 0.0f, s2 = 0.0f;
+  float4 sl[CH], sg[CH], sb[CH];   // this lane's column sums over its rows
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    sl[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    sg[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    sb[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int pass = 0; pass < kPasses; ++pass) {
+    const int rr = (threadIdx.x >> 4) + pass * (kThreads / 16);
+    if (rr >= kRows) break;
+    const int64_t row = row0 + rr;
+    const bool ok = rr < rows;
+    const float mu = ok ? L.mean[row] : 0.0f, rs = ok ? L.rstd[row] : 0.0f;
+    float4 gd[CH], xh[CH];
+    uint32_t pos = 0;   // ReLU mask: bit 4c + e <=> r > 0
+    float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = (c * 16 + sub) * 4;
+      float4 d = lds4(G + rr * PG + col);
+      if (p > 0.0f) {
+        const float4 k = ncf_dropout_scale4(seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
+        d.x *= k.x; d.y *= k.y; d.z *= k.z; d.w *= k.w;
+      }
+      const float4 x = ok ? ld4(L.r + row * N + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 gg = ld4(L.gamma + col);
+      const float4 h = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
+      pos |= ((x.x > 0.0f ? 1u : 0u) | (x.y > 0.0f ? 2u : 0u) | (x.z > 0.0f ? 4u : 0u) |
+              (x.w > 0.0f ? 8u : 0u)) << (4 * c);
+      sg[c].x += d.x * h.x; sg[c].y += d.y * h.y; sg[c].z += d.z * h.z; sg[c].w += d.w * h.w;
+      sb[c].x += d.x; sb[c].y += d.y; sb[c].z += d.z; sb[c].w += d.w;
+      gd[c] = make_float4(d.x * gg.x, d.y * gg.y, d.z * gg.z, d.w * gg.w);
+      s1 += gd[c].x + gd[c].y + gd[c].z + gd[c].w;
+      s2 += gd[c].x * h.x + gd[c].y * h.y + gd[c].z * h.z + gd[c].w * h.w;
+      xh[c] = h;
+    }
+    const float m1 = group_sum<16>(s1) * (1.0f / N);
+    const float m2 = group_sum<16>(s2) * (1.0f / N);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = (c * 16 + sub) * 4;
+      const uint32_t mk = pos >> (4 * c);
+      float4 o;
+      o.x = (mk & 1u) ? rs * (gd[c].x - m1 - xh[c].x * m2) : 0.0f;
+      o.y = (mk & 2u) ? rs * (gd[c].y - m1 - xh[c].y * m2) : 0.0f;
+      o.z = (mk & 4u) ? rs * (gd[c].z - m1 - xh[c].z * m2) : 0.0f;
+      o.w = (mk & 8u) ? rs * (gd[c].w - m1 - xh[c].w * m2) : 0.0f;
+      lds4_st(G + rr * PG + col, o);
+      if (ok) st4(L.dlin + row * N + col, o);
+      sl[c].x += o.x; sl[c].y += o.y; sl[c].z += o.z; sl[c].w += o.w;
+    }
+  }
+  // over the 4 row groups of the wave (lanes sub, sub + 16, sub + 32, sub + 48), then the waves
 #define NCF_R4(v)                                  \
   v += __shfl_xor(v, 16, 64);                      \
   v += __shfl_xor(v, 32, 64);
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
-    const int col = (c * 16 + sub) * 4;
-    float4 d = lds4(G + rr * PG + col);
-    if (p > 0.0f) {
-      const float4 k = ncf_dropout_scale4(seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
-      d.x *= k.x; d.y *= k.y; d.z *= k.z; d.w *= k.w;
-    }
-    const float4 x = ok ? ld4(L.r + row * N + col) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 gg = ld4(L.gamma + col);
-    const float4 h = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
-    pos |= ((x.x > 0.0f ? 1u : 0u) | (x.y > 0.0f ? 2u : 0u) | (x.z > 0.0f ? 4u : 0u) |
-            (x.w > 0.0f ? 8u : 0u)) << (4 * c);
-    float4 ag = make_float4(d.x * h.x, d.y * h.y, d.z * h.z, d.w * h.w);
-    float4 ab = d;
-    gd[c] = make_float4(d.x * gg.x, d.y * gg.y, d.z * gg.z, d.w * gg.w);
-    s1 += gd[c].x + gd[c].y + gd[c].z + gd[c].w;
-    s2 += gd[c].x * h.x + gd[c].y * h.y + gd[c].z * h.z + gd[c].w * h.w;
-    xh[c] = h;
-    // dgamma / dbeta column sums over the wave's 4 rows -> S (the free buffer)
-    NCF_R4(ag.x) NCF_R4(ag.y) NCF_R4(ag.z) NCF_R4(ag.w)
-    NCF_R4(ab.x) NCF_R4(ab.y) NCF_R4(ab.z) NCF_R4(ab.w)
-    if ((threadIdx.x & 63) < 16) {
-      lds4_st(S + wv * 3 * N + N + col, ag);
-      lds4_st(S + wv * 3 * N + 2 * N + col, ab);
-    }
-  }
-  const float m1 = group_sum<16>(s1) * (1.0f / N);
-  const float m2 = group_sum<16>(s2) * (1.0f / N);
-#pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    const int col = (c * 16 + sub) * 4;
-    const uint32_t mk = pos >> (4 * c);
-    float4 o;
-    o.x = (mk & 1u) ? rs * (gd[c].x - m1 - xh[c].x * m2) : 0.0f;
-    o.y = (mk & 2u) ? rs * (gd[c].y - m1 - xh[c].y * m2) : 0.0f;
-    o.z = (mk & 4u) ? rs * (gd[c].z - m1 - xh[c].z * m2) : 0.0f;
-    o.w = (mk & 8u) ? rs * (gd[c].w - m1 - xh[c].w * m2) : 0.0f;
-    lds4_st(G + rr * PG + col, o);
-    if (ok) st4(L.dlin + row * N + col, o);
-    // dbias column sums over the wave's 4 rows -> S
-    NCF_R4(o.x) NCF_R4(o.y) NCF_R4(o.z) NCF_R4(o.w)
-    if ((threadIdx.x & 63) < 16) lds4_st(S + wv * 3 * N + col, o);
+    NCF_R4(sl[c].x) NCF_R4(sl[c].y) NCF_R4(sl[c].z) NCF_R4(sl[c].w)
+    NCF_R4(sg[c].x) NCF_R4(sg[c].y) NCF_R4(sg[c].z) NCF_R4(sg[c].w)
+    NCF_R4(sb[c].x) NCF_R4(sb[c].y) NCF_R4(sb[c].z) NCF_R4(sb[c].w)
   }
 #undef NCF_R4
+  if ((threadIdx.x & 63) < 16) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = (c * 16 + sub) * 4;
+      lds4_st(S + wv * 3 * N + col, sl[c]);
+      lds4_st(S + wv * 3 * N + N + col, sg[c]);
+      lds4_st(S + wv * 3 * N + 2 * N + col, sb[c]);
+    }
+  }
   __syncthreads();
   for (int e = threadIdx.x; e < 3 * N; e += kThreads) {
     float s = 0.0f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) s += S[w * 3 * N + e];
+    for (int w = 0; w < kWaves; ++w) s += S[w * 3 * N + e];
     part[e] = s;
   }
   __syncthreads();
 }
 
-__global__ __launch_bounds__(kThreads, 5) void k_mlp_fwd(
+__global__ __launch_bounds__(kThreads) void k_mlp_fwd(
     const float* __restrict__ xin, int64_t n, TowerArgs a, float eps, float p,
     const ncf_step_clock* clock, const float* __restrict__ w_out, const float* __restrict__ b_out,
     const float* __restrict__ mf_pred, const float* __restrict__ w_fin,
     const float* __restrict__ b_fin, float* __restrict__ mlp_pred, float* __restrict__ prob) {
   extern __shared__ float lds[];
-  float* Q = lds;                  // [16][kPQ]: layer 0 out (256), layer 2 out (64)
-  float* P = lds + kRows * kPQ;    // [16][kPP]: input x (64), layer 1 out (128)
+  float* Q = lds;                  // [80][kPQ]: layer 0 out (256), layer 2 out (64)
+  float* P = lds + kRows * kPQ;    // [80][kPP]: input x (64), layer 1 out (128)
   const int64_t row0 = (int64_t)blockIdx.x * kRows;
   const int rows = (int)min<int64_t>(kRows, n - row0);
   const uint64_t cs = clock ? clock->seed : 0ull;
@@ -254,26 +342,21 @@ __global__ __launch_bounds__(kThreads, 5) void k_mlp_fwd(
   __syncthreads();
   lin_fwd<K0, N0, kPP, kPQ>(P, Q, a.l[0].w, a.l[0].ldw, a.l[0].b);
   __syncthreads();
-  ln_fwd<N0, kPQ>(Q, row0, rows, a.l[0], eps, p, a.seed[0] + cs, nullptr);
+  ln_fwd<N0, kPQ>(Q, row0, rows, a.l[0], eps, p, a.seed[0] + cs, nullptr, nullptr, nullptr,
+                  nullptr, nullptr, nullptr, nullptr);
   __syncthreads();
   lin_fwd<N0, N1, kPQ, kPP>(Q, P, a.l[1].w, a.l[1].ldw, a.l[1].b);
   __syncthreads();
-  ln_fwd<N1, kPP>(P, row0, rows, a.l[1], eps, p, a.seed[1] + cs, nullptr);
+  ln_fwd<N1, kPP>(P, row0, rows, a.l[1], eps, p, a.seed[1] + cs, nullptr, nullptr, nullptr,
+                  nullptr, nullptr, nullptr, nullptr);
   __syncthreads();
   lin_fwd<N1, N2, kPP, kPQ>(P, Q, a.l[2].w, a.l[2].ldw, a.l[2].b);
   __syncthreads();
-  const float dot = ln_fwd<N2, kPQ>(Q, row0, rows, a.l[2], eps, p, a.seed[2] + cs, w_out);
-  const int rr = threadIdx.x >> 4;
-  if ((threadIdx.x & 15) == 0 && rr < rows) {
-    const int64_t row = row0 + rr;
-    const float mp = dot + b_out[0];
-    mlp_pred[row] = mp;
-    const float z = w_fin[0] * mf_pred[row] + w_fin[1] * mp + b_fin[0];
-    prob[row] = 1.0f / (1.0f + expf(-z));
-  }
+  ln_fwd<N2, kPQ>(Q, row0, rows, a.l[2], eps, p, a.seed[2] + cs, w_out, b_out, mf_pred, w_fin,
+                  b_fin, mlp_pred, prob);
 }
 
-__global__ __launch_bounds__(kThreads, 5) void k_mlp_bwd(const float* __restrict__ g_last, int64_t n,
+__global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ g_last, int64_t n,
                                                       TowerArgs a, float p,
                                                       const ncf_step_clock* clock,
                                                       float* __restrict__ dx,
@@ -307,7 +390,7 @@ __global__ __launch_bounds__(kThreads, 5) void k_mlp_bwd(const float* __restrict
 }
 
 constexpr size_t kLds = sizeof(float) * kRows * (kPQ + kPP);
-static_assert(4 * 3 * N0 <= kRows * kPP, "ln_bwd scratch must fit in buffer P");
+static_assert(kWaves * 3 * N0 <= kRows * kPP, "ln_bwd scratch must fit in buffer P");
 
 bool tower_ok(int64_t dim, int64_t n_layers, const int64_t* hidden) {
   return dim == K0 && n_layers == 3 && hidden && hidden[0] == N0 && hidden[1] == N1 &&
