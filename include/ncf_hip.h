@@ -240,11 +240,38 @@ int ncf_mlp_fwd(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* lay
                 const ncf_step_clock* clock, const float* mlp_out_w, const float* mlp_out_b,
                 const float* mf_pred, const float* final_w, const float* final_b, float* mlp_pred,
                 float* prob, void* stream);
+/* Fused head backward (the ncf_head_bwd math, W3 = D = 64): with `head` given, the tower's
+ * backward starts from the loss instead of grad_a_last (which may be NULL): dL/dprob from
+ * grad_prob or the mean BCE of targets (loss_denominator as in ncf_head_bwd), the GMF row
+ * gradients, and the six head parameter gradients + loss through the same workspace / defer list.
+ * Needs layers[2].a (the forward's last activation).                                           */
+typedef struct ncf_head_args {
+  const float* prob;
+  const float* grad_prob;
+  const float* targets;
+  const float* mf_pred;
+  const float* mlp_pred;
+  const float* mf_user_ln;
+  const float* mf_item_ln;
+  const float* mlp_out_w;
+  const float* final_w;
+  const float* mf_out_w;
+  float* grad_mf_user_ln;
+  float* grad_mf_item_ln;
+  float* grad_mlp_out_w;
+  float* grad_mlp_out_b;
+  float* grad_mf_out_w;
+  float* grad_mf_out_b;
+  float* grad_final_w;
+  float* grad_final_b;
+  float* loss;
+  double loss_denominator;
+} ncf_head_args;
 int64_t ncf_mlp_bwd_workspace(int64_t n);
 int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
                 int64_t n_layers, const int64_t* hidden, float dropout_p, uint64_t seed,
-                const ncf_step_clock* clock, float* grad_x, float* workspace,
-                int64_t workspace_floats, ncf_reduce_list* defer, void* stream);
+                const ncf_step_clock* clock, const ncf_head_args* head, float* grad_x,
+                float* workspace, int64_t workspace_floats, ncf_reduce_list* defer, void* stream);
 
 /* ---- 8f rank 1: device-side training batches (data_prep.py:95-161, 181-313) --------------
  * ncf_alias_build (HOST function, once per dataset): Walker/Vose alias table of the

@@ -63,7 +63,7 @@ SIGNATURES = {
     "ncf_sample_negatives": (I32, [P, P, I64, I64, P, P, I64, P, P, I64, U64, I64, P, P, P, P, P]),
     "ncf_mlp_fwd": (I32, [P, I64, I64, P, I64, P, F32, F32, U64, P, P, P, P, P, P, P, P, P]),
     "ncf_mlp_bwd_workspace": (I64, [I64]),
-    "ncf_mlp_bwd": (I32, [P, I64, I64, P, I64, P, F32, U64, P, P, P, I64, P, P]),
+    "ncf_mlp_bwd": (I32, [P, I64, I64, P, I64, P, F32, U64, P, P, P, P, I64, P, P]),
     "ncf_attn_block_fwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, F32, U64, P,
                                  P, P, P, P, P, P, P]),
     "ncf_attn_block_bwd_workspace": (I64, [I64]),
@@ -148,6 +148,16 @@ class MlpLayer(ctypes.Structure):
     """ncf_mlp_layer (include/ncf_hip.h)."""
     _fields_ = [("w", P), ("ldw", I64), ("b", P), ("gamma", P), ("beta", P), ("r", P), ("a", P),
                 ("mean", P), ("rstd", P), ("dlin", P), ("dbias", P), ("dgamma", P), ("dbeta", P)]
+
+
+class HeadArgs(ctypes.Structure):
+    """ncf_head_args (include/ncf_hip.h)."""
+    _fields_ = [(f, P) for f in ("prob", "grad_prob", "targets", "mf_pred", "mlp_pred",
+                                 "mf_user_ln", "mf_item_ln", "mlp_out_w", "final_w", "mf_out_w",
+                                 "grad_mf_user_ln", "grad_mf_item_ln", "grad_mlp_out_w",
+                                 "grad_mlp_out_b", "grad_mf_out_w", "grad_mf_out_b",
+                                 "grad_final_w", "grad_final_b", "loss")] + \
+        [("loss_denominator", ctypes.c_double)]
 
 
 class TablePair(ctypes.Structure):

@@ -39,7 +39,12 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kPQ = 260;   // pitch of buffer Q (<= 256 columns)
 constexpr int kPP = 132;   // pitch of buffer P (<= 128 columns; also the 8 x 3 x 256 scratch)
 constexpr int K0 = 64, N0 = 256, N1 = 128, N2 = 64;
-constexpr int kPartW = 3 * (N0 + N1 + N2);   // partial floats per workgroup
+constexpr int kHeadW = 148;   // head partials: the flat layout of mf_output/mlp_output/final + loss
+constexpr int kPartW = 3 * (N0 + N1 + N2) + kHeadW;   // partial floats per workgroup
+// head partial row (offsets): the flat gradient buffer's order of the head parameters, each
+// 16-B aligned: mf_output.weight [64] @0, mf_output.bias @64, mlp_output.weight [64] @68,
+// mlp_output.bias @132, final.0.weight [2] @136, final.0.bias @140; the BCE sum @144
+constexpr int kHmfW = 0, kHmfB = 64, kHmlW = 68, kHmlB = 132, kHfW = 136, kHfB = 140, kHloss = 144;
 constexpr int kPasses = (kRows * 16 + kThreads - 1) / kThreads;   // row-op passes (16 lanes/row)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -356,11 +361,92 @@ __global__ __launch_bounds__(kThreads) void k_mlp_fwd(
                   b_fin, mlp_pred, prob);
 }
 
+// Head backward (head.hip's k_head_bwd math) for the 80 rows: dL/da_2 -> G, dL/d(LN'd GMF
+// rows) -> HBM, this workgroup's head parameter partials + BCE sum -> part[0 : kHeadW) (through
+// the free buffer S).  16 lanes per row, 4 columns per lane (W3 = D = 64).
+__device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restrict__ S,
+                                         int64_t row0, int rows, const ncf_head_args& h,
+                                         const float* __restrict__ a2, float inv_n,
+                                         float* __restrict__ part) {
+  const int sub = threadIdx.x & 15, wv = threadIdx.x >> 6, col = sub * 4;
+  const float wf0 = h.final_w[0], wf1 = h.final_w[1];
+  const float4 wo = ld4(h.mlp_out_w + col), wm = ld4(h.mf_out_w + col);
+  float4 aw = make_float4(0.f, 0.f, 0.f, 0.f), am = aw;
+  float sw0 = 0.f, sw1 = 0.f, sbf = 0.f, sbo = 0.f, sbm = 0.f, sl = 0.f;
+#pragma unroll
+  for (int pass = 0; pass < kPasses; ++pass) {
+    const int rr = (threadIdx.x >> 4) + pass * (kThreads / 16);
+    if (rr >= kRows) break;
+    const int64_t row = row0 + rr;
+    const bool ok = rr < rows;
+    float dz = 0.f, l = 0.f;
+    if (ok) {
+      const float o = h.prob[row];
+      float go;
+      if (h.targets) {
+        const float t = h.targets[row];
+        go = inv_n * (o - t) / fmaxf((1.0f - o) * o, 1e-12f);
+        l = -(t * fmaxf(logf(o), -100.0f) + (1.0f - t) * fmaxf(logf(1.0f - o), -100.0f));
+      } else {
+        go = h.grad_prob[row];
+      }
+      dz = go * (1.0f - o) * o;
+    }
+    const float dmf = dz * wf0, dml = dz * wf1;
+    lds4_st(G + rr * kPQ + col, make_float4(dml * wo.x, dml * wo.y, dml * wo.z, dml * wo.w));
+    if (ok) {
+      const float4 x = ld4(a2 + row * N2 + col);
+      aw.x += dml * x.x; aw.y += dml * x.y; aw.z += dml * x.z; aw.w += dml * x.w;
+      const float4 u = ld4(h.mf_user_ln + row * K0 + col), it = ld4(h.mf_item_ln + row * K0 + col);
+      const float4 gv = make_float4(dmf * wm.x, dmf * wm.y, dmf * wm.z, dmf * wm.w);
+      st4(h.grad_mf_user_ln + row * K0 + col, make_float4(gv.x * it.x, gv.y * it.y, gv.z * it.z, gv.w * it.w));
+      st4(h.grad_mf_item_ln + row * K0 + col, make_float4(gv.x * u.x, gv.y * u.y, gv.z * u.z, gv.w * u.w));
+      am.x += dmf * u.x * it.x; am.y += dmf * u.y * it.y; am.z += dmf * u.z * it.z; am.w += dmf * u.w * it.w;
+      if (sub == 0) {
+        sw0 += dz * h.mf_pred[row];
+        sw1 += dz * h.mlp_pred[row];
+        sbf += dz;
+        sbo += dml;
+        sbm += dmf;
+        sl += l;
+      }
+    }
+  }
+#define NCF_R4(v)                                  \
+  v += __shfl_xor(v, 16, 64);                      \
+  v += __shfl_xor(v, 32, 64);
+  NCF_R4(aw.x) NCF_R4(aw.y) NCF_R4(aw.z) NCF_R4(aw.w)
+  NCF_R4(am.x) NCF_R4(am.y) NCF_R4(am.z) NCF_R4(am.w)
+  NCF_R4(sw0) NCF_R4(sw1) NCF_R4(sbf) NCF_R4(sbo) NCF_R4(sbm) NCF_R4(sl)
+#undef NCF_R4
+  float* sw = S + wv * kHeadW;
+  if ((threadIdx.x & 63) < 16) {
+    lds4_st(sw + kHmfW + col, am);
+    lds4_st(sw + kHmlW + col, aw);
+    if (sub == 0) {
+      lds4_st(sw + kHmfB, make_float4(sbm, 0.f, 0.f, 0.f));
+      lds4_st(sw + kHmlB, make_float4(sbo, 0.f, 0.f, 0.f));
+      lds4_st(sw + kHfW, make_float4(sw0, sw1, 0.f, 0.f));
+      lds4_st(sw + kHfB, make_float4(sbf, 0.f, 0.f, 0.f));
+      lds4_st(sw + kHloss, make_float4(sl, 0.f, 0.f, 0.f));
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kHeadW; e += kThreads) {
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) v += S[w * kHeadW + e];
+    part[e] = v;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ g_last, int64_t n,
                                                       TowerArgs a, float p,
                                                       const ncf_step_clock* clock,
                                                       float* __restrict__ dx,
-                                                      float* __restrict__ part) {
+                                                      float* __restrict__ part, ncf_head_args h,
+                                                      int fused_head, float inv_n) {
   extern __shared__ float lds[];
   float* Q = lds;
   float* P = lds + kRows * kPQ;
@@ -368,12 +454,16 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
   const int rows = (int)min<int64_t>(kRows, n - row0);
   const uint64_t cs = clock ? clock->seed : 0ull;
   float* pp = part + (int64_t)blockIdx.x * kPartW;
-  for (int e = threadIdx.x; e < kRows * (N2 / 4); e += kThreads) {
-    const int r = e / (N2 / 4), c = (e % (N2 / 4)) * 4;
-    lds4_st(Q + r * kPQ + c,
-            r < rows ? ld4(g_last + (row0 + r) * N2 + c) : make_float4(0.f, 0.f, 0.f, 0.f));
+  if (fused_head) {
+    head_bwd(Q, P, row0, rows, h, a.l[2].a, inv_n, pp + 3 * (N0 + N1 + N2));
+  } else {
+    for (int e = threadIdx.x; e < kRows * (N2 / 4); e += kThreads) {
+      const int r = e / (N2 / 4), c = (e % (N2 / 4)) * 4;
+      lds4_st(Q + r * kPQ + c,
+              r < rows ? ld4(g_last + (row0 + r) * N2 + c) : make_float4(0.f, 0.f, 0.f, 0.f));
+    }
+    __syncthreads();
   }
-  __syncthreads();
   ln_bwd<N2, kPQ>(Q, P, row0, rows, a.l[2], p, a.seed[2] + cs, pp);
   lin_bwd<N2, N1, kPQ, kPP>(Q, P, a.l[2].w, a.l[2].ldw);
   __syncthreads();
@@ -443,14 +533,14 @@ extern "C" int ncf_mlp_fwd(const float* x, int64_t n, int64_t dim, const ncf_mlp
 
 extern "C" int64_t ncf_mlp_bwd_workspace(int64_t n) {
   const int64_t nb = n == 0 ? 1 : ncf_cdiv(n, kRows);
-  return nb * kPartW + 3 * ncf_reduce_scratch((int)nb, 3 * N0);
+  return nb * kPartW + 12 * ncf_reduce_scratch((int)nb, 3 * N0);
 }
 
 extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim,
                            const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
                            float dropout_p, uint64_t seed, const ncf_step_clock* clock,
-                           float* grad_x, float* workspace, int64_t workspace_floats,
-                           ncf_reduce_list* defer, void* stream) {
+                           const ncf_head_args* head, float* grad_x, float* workspace,
+                           int64_t workspace_floats, ncf_reduce_list* defer, void* stream) {
   NCF_CHECK_ARG(n >= 0 && tower_ok(dim, n_layers, hidden),
                 "ncf_mlp_bwd: unsupported tower (need input 64, hidden [256,128,64])");
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_mlp_bwd: dropout_p out of [0,1)");
@@ -468,6 +558,23 @@ extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim,
       ncf_set_error("ncf_mlp_bwd: layer %d needs r/mean/rstd/dlin/dbias/dgamma/dbeta", l);
       return NCF_ERR_ARG;
     }
+  ncf_head_args h{};
+  float inv_n = 0.0f;
+  if (head) {
+    h = *head;
+    NCF_CHECK_ARG((h.grad_prob != nullptr) != (h.targets != nullptr),
+                  "ncf_mlp_bwd: head needs exactly one of grad_prob / targets");
+    NCF_CHECK_ARG(h.prob && h.mf_pred && h.mlp_pred && h.mf_user_ln && h.mf_item_ln &&
+                      h.mlp_out_w && h.final_w && h.mf_out_w && h.grad_mf_user_ln &&
+                      h.grad_mf_item_ln && h.grad_mlp_out_w && h.grad_mlp_out_b &&
+                      h.grad_mf_out_w && h.grad_mf_out_b && h.grad_final_w && h.grad_final_b &&
+                      a.l[2].a,
+                  "ncf_mlp_bwd: incomplete head arguments (and layer 2 needs `a`)");
+    const double den = h.loss_denominator > 0 ? h.loss_denominator : (double)n;
+    inv_n = den > 0 ? (float)(1.0 / den) : 0.0f;
+  } else {
+    NCF_CHECK_ARG(grad_a_last != nullptr, "ncf_mlp_bwd: grad_a_last or head required");
+  }
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k_mlp_bwd, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -477,7 +584,7 @@ extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim,
   const int nb = (int)ncf_cdiv(n, kRows);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_mlp_bwd, dim3((unsigned)nb), dim3(kThreads), kLds, st, grad_a_last, n, a,
-                     dropout_p, clock, grad_x, workspace);
+                     dropout_p, clock, grad_x, workspace, h, head ? 1 : 0, inv_n);
   NCF_CHECK_LAUNCH("ncf_mlp_bwd");
   // per layer: [dbias | dgamma | dbeta] partial columns -> one strided reduction when the three
   // outputs are equally spaced (consecutive parameters of the flat gradient buffer)
@@ -498,6 +605,26 @@ extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim,
       if (!rc) rc = ncf_defer(lst, pp + W, nb, kPartW, W, L.dgamma, 0, W, W);
       if (!rc) rc = ncf_defer(lst, pp + 2 * W, nb, kPartW, W, L.dbeta, 0, W, W);
     }
+  }
+  if (!rc && head) {
+    // head partials: one reduction when the flat gradient buffer lays the six head parameters
+    // out like the partial row, else one per parameter; the BCE sum scaled by 1/n into loss
+    const float* hp = workspace + 3 * (N0 + N1 + N2);
+    float* base = h.grad_mf_out_w;
+    const bool flat = h.grad_mf_out_b == base + kHmfB && h.grad_mlp_out_w == base + kHmlW &&
+                      h.grad_mlp_out_b == base + kHmlB && h.grad_final_w == base + kHfW &&
+                      h.grad_final_b == base + kHfB;
+    if (flat) {
+      rc = ncf_defer(lst, hp, nb, kPartW, kHfB + 1, base, 0, kHfB + 1, kHfB + 1);
+    } else {
+      rc = ncf_defer(lst, hp + kHmfW, nb, kPartW, 64, h.grad_mf_out_w, 0, 64, 64);
+      if (!rc) rc = ncf_defer(lst, hp + kHmfB, nb, kPartW, 1, h.grad_mf_out_b, 0, 1, 1);
+      if (!rc) rc = ncf_defer(lst, hp + kHmlW, nb, kPartW, 64, h.grad_mlp_out_w, 0, 64, 64);
+      if (!rc) rc = ncf_defer(lst, hp + kHmlB, nb, kPartW, 1, h.grad_mlp_out_b, 0, 1, 1);
+      if (!rc) rc = ncf_defer(lst, hp + kHfW, nb, kPartW, 2, h.grad_final_w, 0, 2, 2);
+      if (!rc) rc = ncf_defer(lst, hp + kHfB, nb, kPartW, 1, h.grad_final_b, 0, 1, 1);
+    }
+    if (!rc && h.loss) rc = ncf_defer(lst, hp + kHloss, nb, kPartW, 1, h.loss, 0, 1, 1, inv_n);
   }
   if (rc) return rc;
   if (!defer) {

@@ -499,21 +499,35 @@ class NCFEngine:
         # a12 + a8 backward (trainer.py:271; architecture.py:245-252)
         gp = None if grad_prob is None else grad_prob.reshape(-1).to(torch.float32).contiguous()
         tg = None if targets is None else targets.reshape(-1).to(device=dev, dtype=torch.float32).contiguous()
-        _lib.call("ncf_head_bwd", ptr(w.prob), ptr(gp), ptr(tg), ptr(w.mf_pred), ptr(w.mlp_pred),
-                  ptr(w.a[-1]), n, hid[-1], ptr(m.mlp_output.weight), ptr(m.final[0].weight),
-                  ptr(w.umf), ptr(w.imf), D, ptr(m.mf_output.weight), ptr(w.da[-1]), ptr(w.dumf),
-                  ptr(w.dimf), ptr(gv("mlp_output.weight")), ptr(gv("mlp_output.bias")),
-                  ptr(gv("mf_output.weight")), ptr(gv("mf_output.bias")),
-                  ptr(gv("final.0.weight")), ptr(gv("final.0.bias")), ptr(w.loss),
-                  float(loss_denominator), ptr(w.site("head")), w.site("head").numel(),
-                  w.red_list.address, st)
-        # a7 backward, last layer first
         fused = self.mlp_fused(D, hid)
-        if fused:   # relu/LN/dropout backward + dX of all layers in one launch (mlp_tower.hip)
-            _, addr, _, haddr = self._mlp_layers(w, True, bwd=True)
-            _lib.call("ncf_mlp_bwd", ptr(w.da[-1]), n, D, addr, len(hid), haddr, drop_p, seed,
-                      ptr(self.clock), ptr(w.dy), ptr(w.site("mlp")), w.site("mlp").numel(),
+        if not fused:
+            _lib.call("ncf_head_bwd", ptr(w.prob), ptr(gp), ptr(tg), ptr(w.mf_pred), ptr(w.mlp_pred),
+                      ptr(w.a[-1]), n, hid[-1], ptr(m.mlp_output.weight), ptr(m.final[0].weight),
+                      ptr(w.umf), ptr(w.imf), D, ptr(m.mf_output.weight), ptr(w.da[-1]), ptr(w.dumf),
+                      ptr(w.dimf), ptr(gv("mlp_output.weight")), ptr(gv("mlp_output.bias")),
+                      ptr(gv("mf_output.weight")), ptr(gv("mf_output.bias")),
+                      ptr(gv("final.0.weight")), ptr(gv("final.0.bias")), ptr(w.loss),
+                      float(loss_denominator), ptr(w.site("head")), w.site("head").numel(),
                       w.red_list.address, st)
+        # a7 backward, last layer first
+        if fused:   # head + relu/LN/dropout backward + dX of all layers in one launch
+            _, addr, _, haddr = self._mlp_layers(w, True, bwd=True)
+            h = w.cache.get("head_args")
+            if h is None:
+                h = w.cache["head_args"] = _lib.HeadArgs()
+                h.mf_pred, h.mlp_pred, h.mf_user_ln, h.mf_item_ln = (
+                    ptr(w.mf_pred), ptr(w.mlp_pred), ptr(w.umf), ptr(w.imf))
+                h.mlp_out_w, h.final_w, h.mf_out_w = (
+                    ptr(m.mlp_output.weight), ptr(m.final[0].weight), ptr(m.mf_output.weight))
+                h.grad_mf_user_ln, h.grad_mf_item_ln = ptr(w.dumf), ptr(w.dimf)
+                h.grad_mlp_out_w, h.grad_mlp_out_b = ptr(gv("mlp_output.weight")), ptr(gv("mlp_output.bias"))
+                h.grad_mf_out_w, h.grad_mf_out_b = ptr(gv("mf_output.weight")), ptr(gv("mf_output.bias"))
+                h.grad_final_w, h.grad_final_b = ptr(gv("final.0.weight")), ptr(gv("final.0.bias"))
+            h.prob, h.grad_prob, h.targets, h.loss = ptr(w.prob), ptr(gp), ptr(tg), ptr(w.loss)
+            h.loss_denominator = float(loss_denominator)
+            _lib.call("ncf_mlp_bwd", None, n, D, addr, len(hid), haddr, drop_p, seed,
+                      ptr(self.clock), ctypes.addressof(h), ptr(w.dy), ptr(w.site("mlp")),
+                      w.site("mlp").numel(), w.red_list.address, st)
         for l in reversed(range(len(hid))):
             h = hid[l]
             lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]

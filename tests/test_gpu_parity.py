@@ -519,6 +519,7 @@ def test_mlp_tower_matches_unfused(monkeypatch, B, drop):
         torch.cuda.synchronize()
         nu = w.num_unique.cpu().tolist()
         out.append(dict(prob=w.prob.cpu().clone(), mlp=w.mlp_pred.cpu().clone(),
+                        loss=w.loss.cpu().clone(), dumf=w.dumf.cpu().clone(),
                         grad=m.engine.flat_grad.cpu().clone(), dy=w.dy.cpu().clone(),
                         a=[x.cpu().clone() for x in w.a], r=[x.cpu().clone() for x in w.r],
                         G={k: v[:nu[0 if k.endswith("user") else 1]].cpu().clone()
@@ -526,6 +527,8 @@ def test_mlp_tower_matches_unfused(monkeypatch, B, drop):
     a, b = out
     for k in ("prob", "mlp"):
         torch.testing.assert_close(b[k], a[k], rtol=0, atol=2e-6)
+    torch.testing.assert_close(b["loss"], a["loss"], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(b["dumf"], a["dumf"], rtol=1e-4, atol=1e-7)
     for x, y in zip(b["r"] + b["a"], a["r"] + a["a"]):
         torch.testing.assert_close(x, y, rtol=1e-5, atol=2e-5)
     torch.testing.assert_close(b["dy"], a["dy"], rtol=1e-4, atol=1e-6)
