@@ -300,8 +300,11 @@ def main():
     #   ncf_wgrad_grouped   2 x (D h1 + h1 h2 + h2 h3)   (the three MLP weight gradients)
     # plus any unfused ncf_gemm_* launch (2 M N K, first three arguments).
     mlp_f = 2.0 * (D * hid[0] + hid[0] * hid[1] + hid[1] * hid[2])
+    # (with the weight gradients fused into the tower backward, ncf_mlp_bwd carries dX + dW)
     per_sample = {"ncf_attn_block_fwd": 8.0 * D * D, "ncf_attn_block_bwd": 16.0 * D * D,
-                  "ncf_mlp_fwd": mlp_f, "ncf_mlp_bwd": mlp_f, "ncf_wgrad_grouped": mlp_f}
+                  "ncf_mlp_fwd": mlp_f,
+                  "ncf_mlp_bwd": mlp_f if "ncf_wgrad_grouped" in totals else 2.0 * mlp_f,
+                  "ncf_wgrad_grouped": mlp_f}
     gemm_names = ("ncf_gemm_direct", "ncf_gemm_f32", "ncf_gemm_rows", "ncf_gemm_f32_splitk")
     mfma = {}
     for k, f in per_sample.items():

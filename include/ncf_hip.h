@@ -233,6 +233,8 @@ typedef struct ncf_mlp_layer {
   float* dbias;
   float* dgamma;
   float* dbeta;
+  float* dw;     /* weight gradient [N_l][ldw] (first K_l columns written); all three set:
+                  * the backward computes them too (per-workgroup partials, deferred) */
 } ncf_mlp_layer;
 int ncf_mlp_fused_supported(int64_t dim, int64_t n_layers, const int64_t* hidden);
 int ncf_mlp_fwd(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
@@ -268,7 +270,8 @@ typedef struct ncf_head_args {
   double loss_denominator;
 } ncf_head_args;
 int64_t ncf_mlp_bwd_workspace(int64_t n);
-int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
+int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, const float* x,
+                const ncf_mlp_layer* layers,
                 int64_t n_layers, const int64_t* hidden, float dropout_p, uint64_t seed,
                 const ncf_step_clock* clock, const ncf_head_args* head, float* grad_x,
                 float* workspace, int64_t workspace_floats, ncf_reduce_list* defer, void* stream);

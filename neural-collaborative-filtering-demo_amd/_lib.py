@@ -63,7 +63,7 @@ SIGNATURES = {
     "ncf_sample_negatives": (I32, [P, P, I64, I64, P, P, I64, P, P, I64, U64, I64, P, P, P, P, P]),
     "ncf_mlp_fwd": (I32, [P, I64, I64, P, I64, P, F32, F32, U64, P, P, P, P, P, P, P, P, P]),
     "ncf_mlp_bwd_workspace": (I64, [I64]),
-    "ncf_mlp_bwd": (I32, [P, I64, I64, P, I64, P, F32, U64, P, P, P, P, I64, P, P]),
+    "ncf_mlp_bwd": (I32, [P, I64, I64, P, P, I64, P, F32, U64, P, P, P, P, I64, P, P]),
     "ncf_attn_block_fwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, F32, U64, P,
                                  P, P, P, P, P, P, P]),
     "ncf_attn_block_bwd_workspace": (I64, [I64]),
@@ -147,7 +147,8 @@ WGRAD_GROUP_MAX = 8
 class MlpLayer(ctypes.Structure):
     """ncf_mlp_layer (include/ncf_hip.h)."""
     _fields_ = [("w", P), ("ldw", I64), ("b", P), ("gamma", P), ("beta", P), ("r", P), ("a", P),
-                ("mean", P), ("rstd", P), ("dlin", P), ("dbias", P), ("dgamma", P), ("dbeta", P)]
+                ("mean", P), ("rstd", P), ("dlin", P), ("dbias", P), ("dgamma", P), ("dbeta", P),
+                ("dw", P)]
 
 
 class HeadArgs(ctypes.Structure):

@@ -40,7 +40,10 @@ constexpr int kPQ = 260;   // pitch of buffer Q (<= 256 columns)
 constexpr int kPP = 132;   // pitch of buffer P (<= 128 columns; also the 8 x 3 x 256 scratch)
 constexpr int K0 = 64, N0 = 256, N1 = 128, N2 = 64;
 constexpr int kHeadW = 148;   // head partials: the flat layout of mf_output/mlp_output/final + loss
-constexpr int kPartW = 3 * (N0 + N1 + N2) + kHeadW;   // partial floats per workgroup
+constexpr int kPartS = 3 * (N0 + N1 + N2) + kHeadW;   // bias/gamma/beta + head partials
+// fused weight gradients: dW0 [256 x 64] | dW1 [128 x 256] | dW2 [64 x 128] per workgroup
+constexpr int kW0 = kPartS, kW1 = kW0 + N0 * K0, kW2 = kW1 + N1 * N0;
+constexpr int kPartW = kW2 + N2 * N1;   // partial floats per workgroup
 // head partial row (offsets): the flat gradient buffer's order of the head parameters, each
 // 16-B aligned: mf_output.weight [64] @0, mf_output.bias @64, mlp_output.weight [64] @68,
 // mlp_output.bias @132, final.0.weight [2] @136, final.0.bias @140; the BCE sum @144
@@ -361,6 +364,51 @@ __global__ __launch_bounds__(kThreads) void k_mlp_fwd(
                   b_fin, mlp_pred, prob);
 }
 
+// Weight gradient of one Linear over this workgroup's 80 rows: out[n][k] = sum_r dlin[r][n] X[r][k]
+// (the partial of this workgroup; one deferred reduction sums the 256 partial rows).  16x16
+// output tiles, contraction over the rows k-permuted: lane group g covers rows [20g, 20g + 20).
+// A wave keeps its dlin column fragment (20 values) and sweeps its k tiles with it.
+template <int N, int K, int PG, int PX>
+__device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const float* __restrict__ X,
+                                            float* __restrict__ out) {
+  constexpr int TN = N / 16, TK = K / 16, R4 = kRows / 4;
+  constexpr int TNW = TN >= kWaves ? TN / kWaves : 1;        // n tiles per wave
+  constexpr int WPN = TN >= kWaves ? 1 : kWaves / TN;        // waves per n tile
+  constexpr int TKW = TK / WPN;                              // k tiles per wave
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+#pragma unroll
+  for (int jn = 0; jn < TNW; ++jn) {
+    const int tn = TN >= kWaves ? w + kWaves * jn : w % TN;
+    const int tk0 = TN >= kWaves ? 0 : (w / TN) * TKW;
+    float af[R4];
+#pragma unroll
+    for (int s = 0; s < R4; ++s) af[s] = G[(g * R4 + s) * PG + 16 * tn + i];
+#pragma unroll 2
+    for (int jk = 0; jk < TKW; ++jk) {
+      const int tk = tk0 + jk;
+      const float* xb = X + (g * R4) * PX + 16 * tk + i;
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < R4; s += 2) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], xb[s * PX], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s + 1], xb[(s + 1) * PX], acc1, 0, 0, 0);
+      }
+      float* o = out + (16 * tn + 4 * g) * K + 16 * tk + i;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e * K] = acc0[e] + acc1[e];
+    }
+  }
+}
+
+template <int K, int PX>
+__device__ __forceinline__ void stage_rows(float* __restrict__ X, const float* __restrict__ src,
+                                           int64_t row0, int rows) {
+  for (int e = threadIdx.x; e < kRows * (K / 4); e += kThreads) {
+    const int r = e / (K / 4), c = (e % (K / 4)) * 4;
+    lds4_st(X + r * PX + c, r < rows ? ld4(src + (row0 + r) * K + c) : make_float4(0.f, 0.f, 0.f, 0.f));
+  }
+}
+
 // Head backward (head.hip's k_head_bwd math) for the 80 rows: dL/da_2 -> G, dL/d(LN'd GMF
 // rows) -> HBM, this workgroup's head parameter partials + BCE sum -> part[0 : kHeadW) (through
 // the free buffer S).  16 lanes per row, 4 columns per lane (W3 = D = 64).
@@ -446,7 +494,8 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
                                                       const ncf_step_clock* clock,
                                                       float* __restrict__ dx,
                                                       float* __restrict__ part, ncf_head_args h,
-                                                      int fused_head, float inv_n) {
+                                                      int fused_head, float inv_n,
+                                                      const float* __restrict__ xin, int fused_wgrad) {
   extern __shared__ float lds[];
   float* Q = lds;
   float* P = lds + kRows * kPQ;
@@ -465,12 +514,30 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     __syncthreads();
   }
   ln_bwd<N2, kPQ>(Q, P, row0, rows, a.l[2], p, a.seed[2] + cs, pp);
+  if (fused_wgrad) {   // dW2 = dlin2^T a1 (a1 staged in P, then overwritten by dX)
+    stage_rows<N1, kPP>(P, a.l[1].a, row0, rows);
+    __syncthreads();
+    wgrad_layer<N2, N1, kPQ, kPP>(Q, P, pp + kW2);
+    __syncthreads();
+  }
   lin_bwd<N2, N1, kPQ, kPP>(Q, P, a.l[2].w, a.l[2].ldw);
   __syncthreads();
   ln_bwd<N1, kPP>(P, Q, row0, rows, a.l[1], p, a.seed[1] + cs, pp + 3 * N2);
+  if (fused_wgrad) {   // dW1 = dlin1^T a0
+    stage_rows<N0, kPQ>(Q, a.l[0].a, row0, rows);
+    __syncthreads();
+    wgrad_layer<N1, N0, kPP, kPQ>(P, Q, pp + kW1);
+    __syncthreads();
+  }
   lin_bwd<N1, N0, kPP, kPQ>(P, Q, a.l[1].w, a.l[1].ldw);
   __syncthreads();
   ln_bwd<N0, kPQ>(Q, P, row0, rows, a.l[0], p, a.seed[0] + cs, pp + 3 * (N2 + N1));
+  if (fused_wgrad) {   // dW0 = dlin0^T x (the first 64 input columns of mlp.0)
+    stage_rows<K0, kPP>(P, xin, row0, rows);
+    __syncthreads();
+    wgrad_layer<N0, K0, kPQ, kPP>(Q, P, pp + kW0);
+    __syncthreads();
+  }
   lin_bwd<N0, K0, kPQ, kPP>(Q, P, a.l[0].w, a.l[0].ldw);
   __syncthreads();
   for (int e = threadIdx.x; e < rows * (K0 / 4); e += kThreads) {
@@ -533,10 +600,10 @@ extern "C" int ncf_mlp_fwd(const float* x, int64_t n, int64_t dim, const ncf_mlp
 
 extern "C" int64_t ncf_mlp_bwd_workspace(int64_t n) {
   const int64_t nb = n == 0 ? 1 : ncf_cdiv(n, kRows);
-  return nb * kPartW + 12 * ncf_reduce_scratch((int)nb, 3 * N0);
+  return nb * kPartW + 2 * ncf_reduce_scratch((int)nb, kPartW);
 }
 
-extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim,
+extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, const float* x,
                            const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
                            float dropout_p, uint64_t seed, const ncf_step_clock* clock,
                            const ncf_head_args* head, float* grad_x, float* workspace,
@@ -558,6 +625,9 @@ extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim,
       ncf_set_error("ncf_mlp_bwd: layer %d needs r/mean/rstd/dlin/dbias/dgamma/dbeta", l);
       return NCF_ERR_ARG;
     }
+  const bool fw = a.l[0].dw && a.l[1].dw && a.l[2].dw;
+  NCF_CHECK_ARG(!fw || (x && a.l[0].a && a.l[1].a),
+                "ncf_mlp_bwd: fused weight gradients need x and layers[0..1].a");
   ncf_head_args h{};
   float inv_n = 0.0f;
   if (head) {
@@ -584,7 +654,7 @@ extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim,
   const int nb = (int)ncf_cdiv(n, kRows);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_mlp_bwd, dim3((unsigned)nb), dim3(kThreads), kLds, st, grad_a_last, n, a,
-                     dropout_p, clock, grad_x, workspace, h, head ? 1 : 0, inv_n);
+                     dropout_p, clock, grad_x, workspace, h, head ? 1 : 0, inv_n, x, fw ? 1 : 0);
   NCF_CHECK_LAUNCH("ncf_mlp_bwd");
   // per layer: [dbias | dgamma | dbeta] partial columns -> one strided reduction when the three
   // outputs are equally spaced (consecutive parameters of the flat gradient buffer)
@@ -606,10 +676,15 @@ extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim,
       if (!rc) rc = ncf_defer(lst, pp + 2 * W, nb, kPartW, W, L.dbeta, 0, W, W);
     }
   }
+  if (!rc && fw) {   // weight gradients (mlp.0's first K0 columns of its ldw-wide rows)
+    rc = ncf_defer(lst, workspace + kW0, nb, kPartW, N0 * K0, a.l[0].dw, 0, K0, a.l[0].ldw);
+    if (!rc) rc = ncf_defer(lst, workspace + kW1, nb, kPartW, N1 * N0, a.l[1].dw, 0, N0, a.l[1].ldw);
+    if (!rc) rc = ncf_defer(lst, workspace + kW2, nb, kPartW, N2 * N1, a.l[2].dw, 0, N1, a.l[2].ldw);
+  }
   if (!rc && head) {
     // head partials: one reduction when the flat gradient buffer lays the six head parameters
     // out like the partial row, else one per parameter; the BCE sum scaled by 1/n into loss
-    const float* hp = workspace + 3 * (N0 + N1 + N2);
+    const float* hp = workspace + 3 * (N0 + N1 + N2);   // (within each partial row)
     float* base = h.grad_mf_out_w;
     const bool flat = h.grad_mf_out_b == base + kHmfB && h.grad_mlp_out_w == base + kHmlW &&
                       h.grad_mlp_out_b == base + kHmlB && h.grad_final_w == base + kHfW &&

@@ -404,10 +404,16 @@ class NCFEngine:
                                                      ctypes.addressof(h)))
         return ok
 
+    @staticmethod
+    def mlp_fused_wgrad() -> bool:
+        """The tower backward also computes the three MLP weight gradients (per-workgroup
+        partials); NCF_MLP_WGRAD=0 leaves them to the grouped weight-gradient launch."""
+        return os.environ.get("NCF_MLP_WGRAD", "1") != "0"
+
     def _mlp_layers(self, w, train: bool, bwd: bool):
         """ncf_mlp_layer[] for the fused tower (cached per workspace: the parameter and buffer
         addresses are fixed for its lifetime)."""
-        key = ("mlp", train, bwd)
+        key = ("mlp", train, bwd, bwd and self.mlp_fused_wgrad())
         c = w.cache.get(key)
         if c is None:
             m = self.model
@@ -423,6 +429,8 @@ class NCFEngine:
                     gv = self.grad_view
                     L.dlin, L.dbias = ptr(w.dlin[l]), ptr(gv(f"mlp.{4 * l}.bias"))
                     L.dgamma, L.dbeta = ptr(gv(f"mlp.{4 * l + 2}.weight")), ptr(gv(f"mlp.{4 * l + 2}.bias"))
+                    if self.mlp_fused_wgrad():
+                        L.dw = ptr(gv(f"mlp.{4 * l}.weight"))
             harr = (ctypes.c_int64 * len(hid))(*hid)
             c = w.cache[key] = (arr, ctypes.addressof(arr), harr, ctypes.addressof(harr))
         return c
@@ -525,7 +533,7 @@ class NCFEngine:
                 h.grad_final_w, h.grad_final_b = ptr(gv("final.0.weight")), ptr(gv("final.0.bias"))
             h.prob, h.grad_prob, h.targets, h.loss = ptr(w.prob), ptr(gp), ptr(tg), ptr(w.loss)
             h.loss_denominator = float(loss_denominator)
-            _lib.call("ncf_mlp_bwd", None, n, D, addr, len(hid), haddr, drop_p, seed,
+            _lib.call("ncf_mlp_bwd", None, n, D, ptr(w.y), addr, len(hid), haddr, drop_p, seed,
                       ptr(self.clock), ctypes.addressof(h), ptr(w.dy), ptr(w.site("mlp")),
                       w.site("mlp").numel(), w.red_list.address, st)
         for l in reversed(range(len(hid))):
@@ -542,7 +550,8 @@ class NCFEngine:
             xin, kin = (w.y, D) if l == 0 else (w.a[l - 1], hid[l - 1])
             ldw = lin.weight.shape[1]
             dW = gv(f"mlp.{4 * l}.weight")
-            self._wgrad(w, w.dlin[l], h, xin, kin, dW, ldw, h, kin, n)
+            if not (fused and self.mlp_fused_wgrad()):
+                self._wgrad(w, w.dlin[l], h, xin, kin, dW, ldw, h, kin, n)
             if ldw > kin and self._zero_cols_of is not self.flat_grad:
                 # gradient columns of mlp.0 that see the all-zero temporal input: exactly 0, and
                 # no kernel ever writes them — zero once per gradient buffer

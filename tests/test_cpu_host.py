@@ -262,10 +262,10 @@ def test_row_shards_roundtrip(world):
 def test_struct_mirrors_match_header_layouts():
     """ctypes mirrors of ncf_mlp_layer / ncf_table_pair: every field 8 bytes, header order."""
     import ctypes
-    assert ctypes.sizeof(_lib.MlpLayer) == 13 * 8
+    assert ctypes.sizeof(_lib.MlpLayer) == 14 * 8
     assert [f[0] for f in _lib.MlpLayer._fields_] == ["w", "ldw", "b", "gamma", "beta", "r", "a",
                                                        "mean", "rstd", "dlin", "dbias", "dgamma",
-                                                       "dbeta"]
+                                                       "dbeta", "dw"]
     assert ctypes.sizeof(_lib.TablePair) == 11 * 8
     hdr = open(os.path.join(ROOT, "include", "ncf_hip.h")).read()
     body = hdr[hdr.index("typedef struct ncf_mlp_layer"):hdr.index("} ncf_mlp_layer;")]

@@ -496,14 +496,16 @@ def test_attn_block_matches_unfused(monkeypatch, H, M, B):
         torch.testing.assert_close(G1[k], G0[k], rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("B,drop", [(37, 0.2), (64, 0.0), (1, 0.2)])
-def test_mlp_tower_matches_unfused(monkeypatch, B, drop):
+@pytest.mark.parametrize("wgrad", ["1", "0"])
+@pytest.mark.parametrize("B,drop", [(37, 0.2), (64, 0.0), (1, 0.2), (300, 0.2)])
+def test_mlp_tower_matches_unfused(monkeypatch, B, drop, wgrad):
     """The one-launch MLP tower (mlp_tower.hip, forward + backward) vs the per-layer launches
     (GEMM + rowops + head), same dropout stream: probabilities, saved activations, dense and
     compact table gradients agree to the grads tolerance; n = 5B rows not a multiple of the
     32-row tile exercises the ragged last workgroup."""
     from ncf_amd.trainer import FusedTrainStep
     out = []
+    monkeypatch.setenv("NCF_MLP_WGRAD", wgrad)
     for flag in ("0", "1"):
         monkeypatch.setenv("NCF_MLP_FUSED", flag)
         torch.manual_seed(31)
