@@ -296,8 +296,9 @@ def main():
     #   ncf_attn_block_fwd  2 x 4 D^2          (q/k/v/out projections)
     #   ncf_attn_block_bwd  2 x 8 D^2          (dO, dXu, 2 x dXi, 4 weight gradients)
     #   ncf_mlp_fwd         2 x (D h1 + h1 h2 + h2 h3)
-    #   ncf_mlp_bwd         2 x (D h1 + h1 h2 + h2 h3)   (dX of the three Linears)
-    #   ncf_wgrad_grouped   2 x (D h1 + h1 h2 + h2 h3)   (the three MLP weight gradients)
+    #   ncf_mlp_bwd         2 x (D h1 + h1 h2 + h2 h3)   (dX of the three Linears), plus the
+    #                       same again for their weight gradients when computed inside it
+    #   ncf_wgrad_grouped   2 x (D h1 + h1 h2 + h2 h3)   (the MLP weight gradients, unfused path)
     # plus any unfused ncf_gemm_* launch (2 M N K, first three arguments).
     mlp_f = 2.0 * (D * hid[0] + hid[0] * hid[1] + hid[1] * hid[2])
     # (with the weight gradients fused into the tower backward, ncf_mlp_bwd carries dX + dW)
