@@ -436,7 +436,9 @@ int ncf_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_av
                   double step, void* stream);
 
 /* ---- (e) row sharding over W ranks: owner(id) = id mod W, local row = id div W -------------
- * Pack/unpack kernels around the RCCL all-to-alls (collectives run in torch.distributed).    */
+ * Pack/unpack kernels around the RCCL all-to-alls (collectives run in torch.distributed).
+ * ncf_owner_bucket: send0/send1 = the unique ids in owner order, as the owner's LOCAL rows
+ * (id div W); perm = send slot -> compact index; counts[kind * W + dst].                    */
 int ncf_owner_bucket(const int64_t* uniq0, const int64_t* uniq1, const uint32_t* count,
                      int64_t max_n, int world, int64_t* send0, int64_t* send1, int32_t* perm0,
                      int32_t* perm1, int64_t* counts, void* workspace, int64_t workspace_bytes,

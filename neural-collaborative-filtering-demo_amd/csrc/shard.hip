@@ -145,7 +145,8 @@ __global__ void k_owner_keys(const int64_t* __restrict__ uniq0, const int64_t* _
   v1[i] = (uint32_t)i;
 }
 
-// after one stable pass: send_ids[j] = uniq[perm[j]], counts[kind][d] from the scanned histogram
+// after one stable pass: send_ids[j] = uniq[perm[j]] div W, counts[kind][d] from the scanned
+// histogram
 __global__ void k_owner_finish(const int64_t* __restrict__ uniq0, const int64_t* __restrict__ uniq1,
                                const uint32_t* __restrict__ count, const uint32_t* __restrict__ sv0,
                                const uint32_t* __restrict__ sv1, int64_t n,
@@ -154,8 +155,9 @@ __global__ void k_owner_finish(const int64_t* __restrict__ uniq0, const int64_t*
                                int32_t* __restrict__ perm0, int32_t* __restrict__ perm1,
                                int64_t* __restrict__ counts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < (int64_t)count[0]) { perm0[i] = (int32_t)sv0[i]; send0[i] = uniq0[sv0[i]]; }
-  if (i < (int64_t)count[1]) { perm1[i] = (int32_t)sv1[i]; send1[i] = uniq1[sv1[i]]; }
+  // the owner's LOCAL row (id div W) is what travels: owners index their shard directly
+  if (i < (int64_t)count[0]) { perm0[i] = (int32_t)sv0[i]; send0[i] = uniq0[sv0[i]] / W; }
+  if (i < (int64_t)count[1]) { perm1[i] = (int32_t)sv1[i]; send1[i] = uniq1[sv1[i]] / W; }
   if (blockIdx.x == 0 && threadIdx.x < 2 * W) {
     const int kind = threadIdx.x / W, d = threadIdx.x % W;
     const uint32_t* o = offs + (int64_t)kind * 256 * nb;

@@ -20,7 +20,9 @@ The exchange protocol (``ShardExchange`` + ``ShardedTrainStep``) is device-agnos
 backend does the per-rank work: ``HipShardOps`` (this file, the product path) or, in the CPU
 ``gloo`` tests, a torch reference backend.
 """
+import ctypes
 import math
+import random
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -39,6 +41,18 @@ class ShardExchange:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.device = device
+
+    def exchange_counts_dev(self, counts: torch.Tensor):
+        """Device counts [2 * W] (kind-major) -> (send, recv) host lists per kind, with ONE
+        device-to-host copy for both (the only host sync of a step)."""
+        W = self.world
+        send = counts.view(2, W).t().contiguous()          # [W, 2]: per destination
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=self.group)
+        both = torch.cat([send, recv]).cpu().tolist()
+        s, r = both[:W], both[W:]
+        return ([[s[d][0] for d in range(W)], [s[d][1] for d in range(W)]],
+                [[r[x][0] for x in range(W)], [r[x][1] for x in range(W)]])
 
     def exchange_counts(self, counts: List[List[int]]) -> List[List[int]]:
         """counts[kind][dst] -> recv[kind][src] (one all_to_all of a [W, 2] int64 tensor)."""
@@ -65,8 +79,9 @@ class ShardExchange:
 class Plan:
     send: list          # per kind: unique ids in owner order
     perm: list          # per kind: send slot -> local compact index
-    counts: list        # per kind: per-owner counts (host ints)
+    counts: Optional[list] = None   # per kind: per-owner counts (host ints)
     recv_counts: Optional[list] = None
+    counts_dev: Optional[torch.Tensor] = None   # device counts (HIP backend: one sync later)
 
 
 class ShardedTrainStep:
@@ -80,7 +95,10 @@ class ShardedTrainStep:
         n = user_ids.numel()
         ded = ops.dedup(user_ids, item_ids)
         plan = ops.bucket(ded, X.world)
-        plan.recv_counts = X.exchange_counts(plan.counts)
+        if plan.counts_dev is not None:
+            plan.counts, plan.recv_counts = X.exchange_counts_dev(plan.counts_dev)
+        else:
+            plan.recv_counts = X.exchange_counts(plan.counts)
         recv = [X.exchange(plan.send[k], plan.counts[k], plan.recv_counts[k]) for k in (0, 1)]
         own = ops.owner_prepare(recv)
         rows = [ops.owner_gather(own, k, recv[k]) for k in (0, 1)]
@@ -109,11 +127,17 @@ class HipShardOps:
         self.D = model.mlp_embedding_dim
         self.M = 1 + model.negative_samples
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
-        self.deferred = DeferredTableAdam(self.eng, lr, betas, eps, weight_decay, sweep_every)
+        self.dev = self.eng.flat.device
+        # device step clock: the table Adam launches read their step on the device (both kinds
+        # per launch), the host never waits for it
+        self.base_seed = random.getrandbits(62)
+        self.clock = torch.tensor([0, self.base_seed], dtype=torch.int64, device=self.dev)
+        self.deferred = DeferredTableAdam(self.eng, lr, betas, eps, weight_decay, sweep_every,
+                                          clock=self.clock)
         self.m_flat = torch.zeros_like(self.eng.flat)
         self.v_flat = torch.zeros_like(self.eng.flat)
         self.step_count = 0
-        self.dev = self.eng.flat.device
+        self.rng = random.Random(self.base_seed)     # dropout seeds without a device sync
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.last_loss = None
 
@@ -146,32 +170,40 @@ class HipShardOps:
         _lib.call("ncf_owner_bucket", ptr(w.uniq_u), ptr(w.uniq_i), ptr(w.num_unique), n, world,
                   ptr(send[0]), ptr(send[1]), ptr(perm[0]), ptr(perm[1]), ptr(counts), ptr(ws),
                   ws.numel(), self._st())
-        c = counts.cpu().tolist()                                    # host sync: split sizes
-        return Plan(send=send, perm=perm, counts=[c[:world], c[world:]])
+        return Plan(send=send, perm=perm, counts_dev=counts)      # split sizes fetched later
 
-    # 3. owner side: dedup received ids, catch their rows up
+    # 3. owner side: dedup received ids (already local rows), catch their rows up
     def owner_prepare(self, recv):
         st = self._st()
         rn = [r.numel() for r in recv]
-        local = [torch.empty(max(k, 1), dtype=torch.int64, device=self.dev) for k in rn]
-        for k in (0, 1):
-            _lib.call("ncf_ids_div", ptr(recv[k]), rn[k], self.W, ptr(local[k]), st)
         nmax = max(rn)
         uq = [torch.empty(max(nmax, 1), dtype=torch.int64, device=self.dev) for _ in range(2)]
         cnt = torch.zeros(2, dtype=torch.int32, device=self.dev)
         ws = self._ws(nmax)
-        _lib.call("ncf_dedup_ids2", ptr(local[0]), rn[0], self.Ru, ptr(local[1]), rn[1], self.Ri,
+        _lib.call("ncf_dedup_ids2", ptr(recv[0]), rn[0], self.Ru, ptr(recv[1]), rn[1], self.Ri,
                   self.D, ptr(uq[0]), ptr(uq[1]), None, None, ptr(cnt), ptr(ws), ws.numel(), st)
-        self.deferred.catchup_rows("user", uq[0], cnt, 0, rn[0], st)
-        self.deferred.catchup_rows("item", uq[1], cnt, 1, rn[1], st)
+        d = self.deferred
+        if nmax > 0:
+            d._ensure(d.t + 1)
+            pairs = self._pairs(uq)
+            _lib.call("ncf_adam_pairs_catchup_clock", ctypes.addressof(pairs), 2, self.D,
+                      ptr(cnt), nmax, 0, ptr(self.clock), ptr(d._table), *d._consts(), st)
         return {"rn": rn, "uniq": uq, "cnt": cnt, "ws": ws}
+
+    def _pairs(self, uq, G=None):
+        pairs = self.deferred._pairs()
+        for k in (0, 1):
+            pairs[k].row_ids = ptr(uq[k])
+            if G is not None:
+                pairs[k].g0, pairs[k].g1 = ptr(G[2 * k]), ptr(G[2 * k + 1])
+        return pairs
 
     def owner_gather(self, own, k, recv_ids):
         n = recv_ids.numel()
         out = torch.empty(max(n, 1), 2 * self.D, device=self.dev)
         tb = self.eng.table_params()
         t0, t1 = (tb["mf_user"], tb["mlp_user"]) if k == 0 else (tb["mf_item"], tb["mlp_item"])
-        _lib.call("ncf_gather_shard_rows", ptr(recv_ids), n, self.W, ptr(t0), ptr(t1),
+        _lib.call("ncf_gather_shard_rows", ptr(recv_ids), n, 1, ptr(t0), ptr(t1),
                   self.Ru if k == 0 else self.Ri, self.D, ptr(out), ptr(self.err), self._st())
         return out[:n]
 
@@ -188,7 +220,7 @@ class HipShardOps:
                   ptr(mini["mf_item"]), ptr(mini["mlp_item"]), 0, st)
         m = self.model
         drop_p = float(m.dropout)
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0 else 0
+        seed = self.rng.getrandbits(62) if drop_p > 0 else 0
         inv_u, inv_i = ded["inv"]
 
         def mark(wk, u, i, s):
@@ -217,9 +249,14 @@ class HipShardOps:
         G = [torch.empty(max(rn[k], 1), self.D, device=self.dev) for k in (0, 0, 1, 1)]
         _lib.call("ncf_segment_sum_rows", rn[0], rn[1], self.Ru, self.Ri, self.D, ptr(got[0]),
                   ptr(got[1]), ptr(G[0]), ptr(G[1]), ptr(G[2]), ptr(G[3]), ptr(ws), ws.numel(), st)
-        self.deferred.apply_rows("user", uq[0], cnt, 0, rn[0], G[0], G[1], st)
-        self.deferred.apply_rows("item", uq[1], cnt, 1, rn[1], G[2], G[3], st)
-        self.deferred.advance(st)
+        d = self.deferred
+        nmax = max(rn)
+        d._ensure(d.t + 1)
+        if nmax > 0:
+            pairs = self._pairs(uq, G)
+            _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2, self.D, ptr(cnt),
+                      nmax, 1, ptr(self.clock), ptr(d._table), *d._consts(), st)
+        d.advance(st)                               # rolling sweep of step t + 1 (clock)
 
     def dense_grad(self):
         return self.eng.flat_grad
@@ -228,9 +265,11 @@ class HipShardOps:
         self.step_count += 1
         self.eng.updates += 1
         b1, b2 = self.betas
-        _lib.call("ncf_adam_flat", ptr(self.eng.flat), ptr(self.eng.flat_grad), ptr(self.m_flat),
-                  ptr(self.v_flat), self.eng.flat.numel(), self.lr, b1, b2, self.eps, self.wd,
-                  float(self.step_count), self._st())
+        st = self._st()
+        _lib.call("ncf_adam_flat_clock", ptr(self.eng.flat), ptr(self.eng.flat_grad),
+                  ptr(self.m_flat), ptr(self.v_flat), self.eng.flat.numel(),
+                  ptr(self.deferred._table), 1, ptr(self.clock), b1, b2, self.eps, self.wd, st)
+        _lib.call("ncf_step_clock_advance", ptr(self.clock), self.base_seed, st)
 
 
 def shard_rows(rows: int, world: int) -> int:

@@ -22,6 +22,9 @@ for step in "$@"; do
     prof) run prof 900 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     benchshard) run benchshard 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29531 bench.py --sharded --steps 30 --warmup 5 --no-cpu-baseline ;;
     gemm) run gemm 300 python tools/gemm_bench.py ;;
+    profshard) export MASTER_ADDR=127.0.0.1 MASTER_PORT=29533 RANK=0 LOCAL_RANK=0 WORLD_SIZE=1
+      run profshard 900 rocprofv3 --kernel-trace --stats -T -d gpurun_out/profshard -o run --output-format csv -- python3 bench.py --sharded --steps 20 --warmup 5 --no-cpu-baseline --no-score
+      unset MASTER_ADDR MASTER_PORT RANK LOCAL_RANK WORLD_SIZE ;;
     score) run score 600 python tools/score_bench.py ;;
     *) echo "unknown step $step" ;;
   esac
