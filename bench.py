@@ -336,6 +336,37 @@ def main():
                                                 "ncf_adam_pairs_apply_clock",
                                                 "ncf_adam_pairs_sweep_rolling"))
     tab_bytes = 2 * (U + I) * D * 24.0
+    # embedding gather / scatter: algorithmic HBM bytes per launch
+    #   gather  (ncf_gather_ln_gmf_scaled_fwd): 4 rows of D fp32 + 2 int64 ids in, 4 LN'd rows
+    #           (MLP + GMF, training) + mf_pred out = N (16 D + 16 + 16 D + 4)
+    #   scatter (ncf_embedding_bwd_reduce): 4 gradient rows in per sample, per unique row the 2
+    #           table rows (LN recompute) in and 2 compact gradient rows out = N (16 D + 16) +
+    #           (n_u + n_i) 16 D
+    nu_ni = None
+    try:
+        ws_any = next(iter(model.engine.ws.values()))
+        nu_ni = [int(x) for x in ws_any.num_unique.cpu().tolist()]
+    except Exception:
+        pass
+    hbm = {}
+    for name, kern, nbytes in (
+            ("gather", "ncf_gather_ln_gmf_scaled_fwd", N * (16 * D + 16 + 16 * D + 4)),
+            ("scatter", "ncf_embedding_bwd_reduce",
+             N * (16 * D + 16) + (sum(nu_ni) * 16 * D if nu_ni else 0))):
+        if kern in totals:
+            launches = len(per.get(kern, [])) / args.steps
+            ms = totals[kern] / max(launches, 1)
+            gbs = nbytes / (ms * 1e-3) / 1e9
+            pm = pmc_traffic({"ncf_gather_ln_gmf_scaled_fwd": "k_gather_ln_gmf",
+                              "ncf_embedding_bwd_reduce": "k_piece_reduce_ln"}[kern])
+            hbm[name] = {"entry_point": kern, "bytes_per_launch": nbytes, "ms_per_launch": round(ms, 4),
+                         "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS,
+                         "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "traffic": pm["bytes_per_launch"] if pm else None}
+    if "scatter" in hbm:
+        hbm["scatter"]["unique_rows"] = nu_ni
+        hbm["scatter"]["note"] = ("segment reduce + LN backward only; the id sort before it "
+                                  "(ncf_dedup_ids) is listed in kernel_ms_per_step")
     # --- inference pairs/s: eval forward (M = 1) on resident pairs
     model.eval()
     npairs = args.infer_pairs
@@ -401,6 +432,7 @@ def main():
                            "flops_per_step": gemm_flops, "launches_per_step": gemm_launches,
                            "per_kernel": mfma,
                          "ms_per_step": round(gemm_ms, 4)},
+            "embedding_hbm": hbm,
             "table_adam": {"kernels": "deferred dense-exact Adam (catch-up + apply + 1/64 sweep)",
                            "ms_per_step": round(tab_ms, 4),
                            "dense_equivalent_GBps": round(tab_bytes / max(tab_ms * 1e-3, 1e-12) / 1e9, 1),
