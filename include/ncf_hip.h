@@ -216,9 +216,11 @@ int ncf_attn_block_bwd(const float* grad_y, const float* q, const float* k, cons
  * Forward: r = relu(x W^T + b), mean/rstd, a = dropout(LN(r)) per layer (r/a/mean/rstd may be
  *   NULL: not saved), then mlp_pred = a_2 . mlp_out_w + mlp_out_b and
  *   prob = sigmoid(final_w[0] mf_pred + final_w[1] mlp_pred + final_b) (the ncf_head_fwd math).
- * Backward: from dL/da_2 (ncf_head_bwd's grad_mlp_last) -> dlin per layer (written: the weight
- *   gradients' dY), grad_x = dL/dx [n,64]; dbias/dgamma/dbeta per layer through the workspace
- *   (deferred into `defer` when given).                                                       */
+ * Backward: from dL/da_2 (ncf_head_bwd's grad_mlp_last) -> dlin per layer (written when
+ *   non-NULL: the weight gradients' dY; required unless the dw are set), grad_x = dL/dx [n,64];
+ *   dbias/dgamma/dbeta per layer through the workspace (deferred into `defer` when given).
+ *   r/mean/rstd are required; where `a` is NULL the backward recomputes a = dropout(LN(r))
+ *   bit-identically from r/mean/rstd and the dropout stream (so the forward need not save it). */
 typedef struct ncf_mlp_layer {
   const float* w;
   int64_t ldw;

@@ -112,26 +112,62 @@ struct TablePtrs {
   const float *G0, *G1;                 // compact gradients (apply only)
 };
 
+// Replay layout: lane = column.  One row (of both tables of a pair) per wave when D >= 64
+// (EPL = D/64 columns per lane, stride 64), 64/D rows per wave when D < 64.  With one row per
+// wave the replay bounds (from, to) are wave-uniform: the step loop is scalar, the per-step
+// scalars come through the scalar cache, and no lane idles on another row's longer catch-up.
 template <int D>
-__device__ __forceinline__ void catch_up_row(const TablePtrs& t, int64_t row, int col, int32_t from,
+struct Replay {
+  static constexpr int LPR = D < 64 ? D : 64;   // lanes per row
+  static constexpr int EPL = D / LPR;           // columns per lane
+};
+
+template <int D>
+__device__ __forceinline__ void catch_up_row(const TablePtrs& t, int64_t row, int sub, int32_t from,
                                              int32_t to, const float* __restrict__ table,
                                              const AdamScalars& s) {
+  constexpr int EPL = Replay<D>::EPL, LPR = Replay<D>::LPR;
+  if (Replay<D>::LPR == 64) {   // the whole wave holds this row: make the bounds scalar
+    from = __builtin_amdgcn_readfirstlane(from);
+    to = __builtin_amdgcn_readfirstlane(to);
+  }
   if (from >= to) return;
-  const int64_t o = row * D + col;
-  float4 p0 = ld4(t.p0 + o), m0 = ld4(t.m0 + o), v0 = ld4(t.v0 + o);
-  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int64_t o = row * D + sub;
+  float p0[EPL], m0[EPL], v0[EPL], p1[EPL], m1[EPL], v1[EPL];
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) {
+    p0[j] = t.p0[o + j * LPR]; m0[j] = t.m0[o + j * LPR]; v0[j] = t.v0[o + j * LPR];
+  }
   if (t.p1) {
-    float4 p1 = ld4(t.p1 + o), m1 = ld4(t.m1 + o), v1 = ld4(t.v1 + o);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      p1[j] = t.p1[o + j * LPR]; m1[j] = t.m1[o + j * LPR]; v1[j] = t.v1[o + j * LPR];
+    }
+#pragma unroll 2
     for (int32_t q = from + 1; q <= to; ++q) {
       const float ns = table[2 * q], bc = table[2 * q + 1];
-      adam4(p0, m0, v0, z, ns, bc, s);
-      adam4(p1, m1, v1, z, ns, bc, s);
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) {
+        adam1(p0[j], m0[j], v0[j], 0.0f, ns, bc, s);
+        adam1(p1[j], m1[j], v1[j], 0.0f, ns, bc, s);
+      }
     }
-    st4(t.p1 + o, p1); st4(t.m1 + o, m1); st4(t.v1 + o, v1);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      t.p1[o + j * LPR] = p1[j]; t.m1[o + j * LPR] = m1[j]; t.v1[o + j * LPR] = v1[j];
+    }
   } else {
-    for (int32_t q = from + 1; q <= to; ++q) adam4(p0, m0, v0, z, table[2 * q], table[2 * q + 1], s);
+#pragma unroll 2
+    for (int32_t q = from + 1; q <= to; ++q) {
+      const float ns = table[2 * q], bc = table[2 * q + 1];
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) adam1(p0[j], m0[j], v0[j], 0.0f, ns, bc, s);
+    }
   }
-  st4(t.p0 + o, p0); st4(t.m0 + o, m0); st4(t.v0 + o, v0);
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) {
+    t.p0[o + j * LPR] = p0[j]; t.m0[o + j * LPR] = m0[j]; t.v0[o + j * LPR] = v0[j];
+  }
 }
 
 // rows listed in ids[0 .. count[kind]) (unique), caught up to `target`
@@ -142,7 +178,7 @@ __global__ __launch_bounds__(256) void k_adam_catchup(TablePtrs t, const int64_t
                                                       int32_t target, const float* __restrict__ table,
                                                       AdamScalars s,
                                                       const ncf_step_clock* __restrict__ clock) {
-  constexpr int L = D / 4;
+  constexpr int L = Replay<D>::LPR;   // lanes per row
   const int64_t tt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t c = tt / L;
   const int sub = (int)(tt % L);
@@ -151,7 +187,7 @@ __global__ __launch_bounds__(256) void k_adam_catchup(TablePtrs t, const int64_t
   if (clock) target += clock->t;
   const int64_t row = ids[c];
   const int32_t from = stamp[row];
-  catch_up_row<D>(t, row, sub * 4, from, target, table, s);
+  catch_up_row<D>(t, row, sub, from, target, table, s);
   if (sub == 0 && from < target) stamp[row] = target;
 }
 
@@ -160,14 +196,14 @@ template <int D>
 __global__ __launch_bounds__(256) void k_adam_sweep(TablePtrs t, int64_t row0, int64_t rows,
                                                     int32_t* __restrict__ stamp, int32_t target,
                                                     const float* __restrict__ table, AdamScalars s) {
-  constexpr int L = D / 4;
+  constexpr int L = Replay<D>::LPR;   // lanes per row
   const int64_t n = rows * L;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t row = row0 + e / L;
     const int sub = (int)(e % L);
     const int32_t from = stamp[row];
-    catch_up_row<D>(t, row, sub * 4, from, target, table, s);
+    catch_up_row<D>(t, row, sub, from, target, table, s);
     // all L lanes of the row read stamp before this store: they share one wave-instruction
     if (sub == 0 && from < target) stamp[row] = target;
   }
@@ -211,7 +247,7 @@ __global__ __launch_bounds__(256) void k_adam_sweep_rolling(TablePtrs t, int64_t
                                                             const ncf_step_clock* __restrict__ clock,
                                                             const float* __restrict__ table,
                                                             AdamScalars s) {
-  constexpr int L = D / 4;
+  constexpr int L = Replay<D>::LPR;   // lanes per row
   const int32_t target = clock->t + step_rel;
   const int64_t row0 = (int64_t)(target % every) * slice;
   const int64_t rows = max((int64_t)0, min(slice, total_rows - row0));
@@ -221,7 +257,7 @@ __global__ __launch_bounds__(256) void k_adam_sweep_rolling(TablePtrs t, int64_t
     const int64_t row = row0 + e / L;
     const int sub = (int)(e % L);
     const int32_t from = stamp[row];
-    catch_up_row<D>(t, row, sub * 4, from, target, table, s);
+    catch_up_row<D>(t, row, sub, from, target, table, s);
     if (sub == 0 && from < target) stamp[row] = target;
   }
 }
@@ -261,7 +297,7 @@ __global__ __launch_bounds__(256) void k_pairs_catchup(const PairArgs a, const u
                                                        const ncf_step_clock* __restrict__ clock,
                                                        const float* __restrict__ table,
                                                        AdamScalars s) {
-  constexpr int L = D / 4;
+  constexpr int L = Replay<D>::LPR;   // lanes per row
   const int k = blockIdx.y;
   const int64_t tt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t c = tt / L;
@@ -271,7 +307,7 @@ __global__ __launch_bounds__(256) void k_pairs_catchup(const PairArgs a, const u
   const int64_t row = a.ids[k][c];
   int32_t* stamp = a.stamp[k];
   const int32_t from = stamp[row];
-  catch_up_row<D>(a.t[k], row, sub * 4, from, target, table, s);
+  catch_up_row<D>(a.t[k], row, sub, from, target, table, s);
   if (sub == 0 && from < target) stamp[row] = target;
 }
 
@@ -307,7 +343,7 @@ __global__ __launch_bounds__(256) void k_pairs_sweep(const PairArgs a, int32_t e
                                                      int32_t step_rel,
                                                      const ncf_step_clock* __restrict__ clock,
                                                      const float* __restrict__ table, AdamScalars s) {
-  constexpr int L = D / 4;
+  constexpr int L = Replay<D>::LPR;   // lanes per row
   const int k = blockIdx.y;
   const int32_t target = clock->t + step_rel;
   const int64_t total = a.rows[k];
@@ -321,7 +357,7 @@ __global__ __launch_bounds__(256) void k_pairs_sweep(const PairArgs a, int32_t e
     const int64_t row = row0 + e / L;
     const int sub = (int)(e % L);
     const int32_t from = stamp[row];
-    catch_up_row<D>(a.t[k], row, sub * 4, from, target, table, s);
+    catch_up_row<D>(a.t[k], row, sub, from, target, table, s);
     if (sub == 0 && from < target) stamp[row] = target;
   }
 }
@@ -434,7 +470,7 @@ template <int D>
 int catchup_d(TablePtrs t, const int64_t* ids, const uint32_t* count, int kind, int64_t max_n,
               int32_t* stamp, int32_t target, const float* table, AdamScalars s,
               const ncf_step_clock* clock, hipStream_t st) {
-  hipLaunchKernelGGL(k_adam_catchup<D>, dim3(ncf_cdiv(max_n * (D / 4), 256)), dim3(256), 0, st, t,
+  hipLaunchKernelGGL(k_adam_catchup<D>, dim3(ncf_cdiv(max_n * Replay<D>::LPR, 256)), dim3(256), 0, st, t,
                      ids, count, kind, max_n, stamp, target, table, s, clock);
   NCF_CHECK_LAUNCH("ncf_adam_rows_catchup");
   return NCF_OK;
@@ -454,7 +490,7 @@ template <int D>
 int rolling_d(TablePtrs t, int64_t total, int64_t slice, int32_t every, int32_t* stamp,
               int32_t step_rel, const ncf_step_clock* clock, const float* table, AdamScalars s,
               hipStream_t st) {
-  hipLaunchKernelGGL(k_adam_sweep_rolling<D>, dim3(grid_for(slice * (D / 4))), dim3(256), 0, st, t,
+  hipLaunchKernelGGL(k_adam_sweep_rolling<D>, dim3(grid_for(slice * Replay<D>::LPR)), dim3(256), 0, st, t,
                      total, slice, every, stamp, step_rel, clock, table, s);
   NCF_CHECK_LAUNCH("ncf_adam_sweep_rolling");
   return NCF_OK;
@@ -476,7 +512,7 @@ template <int D>
 int pairs_catchup_d(PairArgs a, int n, const uint32_t* count, int64_t max_n, int32_t rel,
                     const ncf_step_clock* clock, const float* table, AdamScalars s,
                     hipStream_t st) {
-  hipLaunchKernelGGL(k_pairs_catchup<D>, dim3(ncf_cdiv(max_n * (D / 4), 256), n), dim3(256), 0, st,
+  hipLaunchKernelGGL(k_pairs_catchup<D>, dim3(ncf_cdiv(max_n * Replay<D>::LPR, 256), n), dim3(256), 0, st,
                      a, count, max_n, rel, clock, table, s);
   NCF_CHECK_LAUNCH("ncf_adam_pairs_catchup_clock");
   return NCF_OK;
@@ -496,7 +532,7 @@ int pairs_sweep_d(PairArgs a, int n, int32_t every, int32_t rel, const ncf_step_
                   const float* table, AdamScalars s, hipStream_t st) {
   int64_t slice = 0;
   for (int k = 0; k < n; ++k) slice = max(slice, (a.rows[k] + every - 1) / every);
-  hipLaunchKernelGGL(k_pairs_sweep<D>, dim3(grid_for(slice * (D / 4)), n), dim3(256), 0, st, a,
+  hipLaunchKernelGGL(k_pairs_sweep<D>, dim3(grid_for(slice * Replay<D>::LPR), n), dim3(256), 0, st, a,
                      every, rel, clock, table, s);
   NCF_CHECK_LAUNCH("ncf_adam_pairs_sweep_rolling");
   return NCF_OK;
@@ -505,7 +541,7 @@ int pairs_sweep_d(PairArgs a, int n, int32_t every, int32_t rel, const ncf_step_
 template <int D>
 int sweep_d(TablePtrs t, int64_t row0, int64_t rows, int32_t* stamp, int32_t target,
             const float* table, AdamScalars s, hipStream_t st) {
-  hipLaunchKernelGGL(k_adam_sweep<D>, dim3(grid_for(rows * (D / 4))), dim3(256), 0, st, t, row0,
+  hipLaunchKernelGGL(k_adam_sweep<D>, dim3(grid_for(rows * Replay<D>::LPR)), dim3(256), 0, st, t, row0,
                      rows, stamp, target, table, s);
   NCF_CHECK_LAUNCH("ncf_adam_sweep");
   return NCF_OK;

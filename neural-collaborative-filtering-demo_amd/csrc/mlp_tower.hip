@@ -60,6 +60,35 @@ struct TowerArgs {
 __device__ __forceinline__ float4 lds4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void lds4_st(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
+// LayerNorm affine of a centred float4 (x - mean) and the dropout keep-scales: ONE definition
+// shared by the forward (ln_fwd) and the backward's recompute of the activation a = Dropout(LN(r))
+// (act4), so both produce the same bits.
+__device__ __forceinline__ float4 ln_affine(float4 xc, float rstd, float4 gg, float4 bb) {
+  return make_float4(__builtin_fmaf(xc.x * rstd, gg.x, bb.x), __builtin_fmaf(xc.y * rstd, gg.y, bb.y),
+                     __builtin_fmaf(xc.z * rstd, gg.z, bb.z), __builtin_fmaf(xc.w * rstd, gg.w, bb.w));
+}
+
+__device__ __forceinline__ float4 drop4(float4 y, uint64_t seed, uint64_t idx4, float p, float inv_keep) {
+  if (p > 0.0f) {
+    const float4 k = ncf_dropout_scale4(seed, idx4, p, inv_keep);
+    y.x *= k.x; y.y *= k.y; y.z *= k.z; y.w *= k.w;
+  }
+  return y;
+}
+
+// a[row][col..col+3] of layer L recomputed from the saved pre-LN rows r and the row statistics
+// (the forward does not store a when the backward recomputes it: 4 B/element of HBM writes and
+// reads saved, r is read anyway)
+template <int N>
+__device__ __forceinline__ float4 act4(const ncf_mlp_layer& L, int64_t row, int col, float p,
+                                       uint64_t seed, float inv_keep) {
+  const float mu = L.mean[row], rs = L.rstd[row];
+  const float4 x = ld4(L.r + row * N + col);
+  const float4 y = ln_affine(make_float4(x.x - mu, x.y - mu, x.z - mu, x.w - mu), rs,
+                             ld4(L.gamma + col), ld4(L.beta + col));
+  return drop4(y, seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
+}
+
 __device__ __forceinline__ f32x4 mfma4(float4 a, float4 b, f32x4 acc) {
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
@@ -176,59 +205,88 @@ __device__ __forceinline__ void ln_fwd(float* __restrict__ Y, int64_t row0, int 
                                        const float* __restrict__ w_fin,
                                        const float* __restrict__ b_fin,
                                        float* __restrict__ mlp_pred, float* __restrict__ prob) {
-  constexpr int CH = N / 64;
+  // The kPasses row passes of a lane run interleaved (independent chains: the shuffle
+  // reductions of one pass hide behind the arithmetic of the others).  A pass whose row is past
+  // the tile (rr >= kRows: waves 4-7 in the last pass) computes on zeros and stores nothing.
+  // No fp contraction here: the unrolled passes must round identically, so a row's result does
+  // not depend on which pass (= its position in the tile, i.e. the batch) computes it; the
+  // fused multiply-adds are explicit.
+#pragma clang fp contract(off)
+  constexpr int CH = N / 64, NP = kPasses;
   const int sub = threadIdx.x & 15;
   const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  float4 x[NP][CH];
+  float s[NP], mean[NP], rstd[NP];
 #pragma unroll
-  for (int pass = 0; pass < kPasses; ++pass) {
-    const int rr = (threadIdx.x >> 4) + pass * (kThreads / 16);
-    if (rr >= kRows) break;   // whole 16-lane row groups leave together
+  for (int q = 0; q < NP; ++q) {
+    const int rr = (threadIdx.x >> 4) + q * (kThreads / 16);
+    s[q] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = (c * 16 + sub) * 4;
+      x[q][c] = rr < kRows ? lds4(Y + rr * PY + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      s[q] += x[q][c].x + x[q][c].y + x[q][c].z + x[q][c].w;
+    }
+  }
+  if (L.r) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int rr = (threadIdx.x >> 4) + q * (kThreads / 16);
+      if (rr < rows) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) st4(L.r + (row0 + rr) * N + (c * 16 + sub) * 4, x[q][c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NP; ++q) mean[q] = group_sum<16>(s[q]) * (1.0f / N);
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    s[q] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      float4& v = x[q][c];
+      v.x -= mean[q]; v.y -= mean[q]; v.z -= mean[q]; v.w -= mean[q];
+      s[q] = __builtin_fmaf(v.x, v.x, s[q]); s[q] = __builtin_fmaf(v.y, v.y, s[q]);
+      s[q] = __builtin_fmaf(v.z, v.z, s[q]); s[q] = __builtin_fmaf(v.w, v.w, s[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NP; ++q) rstd[q] = 1.0f / sqrtf(group_sum<16>(s[q]) * (1.0f / N) + eps);
+  float dot[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int rr = (threadIdx.x >> 4) + q * (kThreads / 16);
     const int64_t row = row0 + rr;
     const bool ok = rr < rows;
-    float4 x[CH];
-    float s = 0.0f;
+    dot[q] = 0.0f;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int col = (c * 16 + sub) * 4;
-      x[c] = lds4(Y + rr * PY + col);
-      if (ok && L.r) st4(L.r + row * N + col, x[c]);
-      s += x[c].x + x[c].y + x[c].z + x[c].w;
-    }
-    const float mean = group_sum<16>(s) * (1.0f / N);
-    float qv = 0.0f;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      x[c].x -= mean; x[c].y -= mean; x[c].z -= mean; x[c].w -= mean;
-      qv += x[c].x * x[c].x + x[c].y * x[c].y + x[c].z * x[c].z + x[c].w * x[c].w;
-    }
-    const float rstd = 1.0f / sqrtf(group_sum<16>(qv) * (1.0f / N) + eps);
-    float dot = 0.0f;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int col = (c * 16 + sub) * 4;
-      const float4 gg = ld4(L.gamma + col), bb = ld4(L.beta + col);
-      float4 y = make_float4(x[c].x * rstd * gg.x + bb.x, x[c].y * rstd * gg.y + bb.y,
-                             x[c].z * rstd * gg.z + bb.z, x[c].w * rstd * gg.w + bb.w);
-      if (p > 0.0f) {
-        const float4 k = ncf_dropout_scale4(seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
-        y.x *= k.x; y.y *= k.y; y.z *= k.z; y.w *= k.w;
-      }
-      lds4_st(Y + rr * PY + col, y);
+      const float4 y = drop4(ln_affine(x[q][c], rstd[q], ld4(L.gamma + col), ld4(L.beta + col)),
+                             seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
+      if (rr < kRows) lds4_st(Y + rr * PY + col, y);
       if (ok && L.a) st4(L.a + row * N + col, y);
       if (hw) {
         const float4 h = ld4(hw + col);
-        dot = fmaf(y.x, h.x, dot); dot = fmaf(y.y, h.y, dot);
-        dot = fmaf(y.z, h.z, dot); dot = fmaf(y.w, h.w, dot);
+        dot[q] = fmaf(y.x, h.x, dot[q]); dot[q] = fmaf(y.y, h.y, dot[q]);
+        dot[q] = fmaf(y.z, h.z, dot[q]); dot[q] = fmaf(y.w, h.w, dot[q]);
       }
     }
     if (ok && sub == 0 && L.mean) {
-      L.mean[row] = mean;
-      L.rstd[row] = rstd;
+      L.mean[row] = mean[q];
+      L.rstd[row] = rstd[q];
     }
-    if (hw) {
-      dot = group_sum<16>(dot);
-      if (ok && sub == 0) {
-        const float mp = dot + b_out[0];
+  }
+  if (hw) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) dot[q] = group_sum<16>(dot[q]);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int rr = (threadIdx.x >> 4) + q * (kThreads / 16);
+      const int64_t row = row0 + rr;
+      if (rr < rows && sub == 0) {
+        const float mp = dot[q] + b_out[0];
         mlp_pred[row] = mp;
         const float z = w_fin[0] * mf_pred[row] + w_fin[1] * mp + b_fin[0];
         prob[row] = 1.0f / (1.0f + expf(-z));
@@ -297,7 +355,7 @@ __device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict_
       o.z = (mk & 4u) ? rs * (gd[c].z - m1 - xh[c].z * m2) : 0.0f;
       o.w = (mk & 8u) ? rs * (gd[c].w - m1 - xh[c].w * m2) : 0.0f;
       lds4_st(G + rr * PG + col, o);
-      if (ok) st4(L.dlin + row * N + col, o);
+      if (ok && L.dlin) st4(L.dlin + row * N + col, o);
       sl[c].x += o.x; sl[c].y += o.y; sl[c].z += o.z; sl[c].w += o.w;
     }
   }
@@ -400,6 +458,20 @@ __device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const f
   }
 }
 
+// the activation rows a of layer L into LDS: loaded when the forward saved them, else
+// recomputed from r (act4)
+template <int K, int PX>
+__device__ __forceinline__ void stage_act(float* __restrict__ X, const ncf_mlp_layer& L,
+                                          int64_t row0, int rows, float p, uint64_t seed) {
+  const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  for (int e = threadIdx.x; e < kRows * (K / 4); e += kThreads) {
+    const int r = e / (K / 4), c = (e % (K / 4)) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < rows) v = L.a ? ld4(L.a + (row0 + r) * K + c) : act4<K>(L, row0 + r, c, p, seed, inv_keep);
+    lds4_st(X + r * PX + c, v);
+  }
+}
+
 template <int K, int PX>
 __device__ __forceinline__ void stage_rows(float* __restrict__ X, const float* __restrict__ src,
                                            int64_t row0, int rows) {
@@ -414,8 +486,9 @@ __device__ __forceinline__ void stage_rows(float* __restrict__ X, const float* _
 // the free buffer S).  16 lanes per row, 4 columns per lane (W3 = D = 64).
 __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restrict__ S,
                                          int64_t row0, int rows, const ncf_head_args& h,
-                                         const float* __restrict__ a2, float inv_n,
-                                         float* __restrict__ part) {
+                                         const ncf_mlp_layer& L2, float p, uint64_t seed,
+                                         float inv_n, float* __restrict__ part) {
+  const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int sub = threadIdx.x & 15, wv = threadIdx.x >> 6, col = sub * 4;
   const float wf0 = h.final_w[0], wf1 = h.final_w[1];
   const float4 wo = ld4(h.mlp_out_w + col), wm = ld4(h.mf_out_w + col);
@@ -443,7 +516,7 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
     const float dmf = dz * wf0, dml = dz * wf1;
     lds4_st(G + rr * kPQ + col, make_float4(dml * wo.x, dml * wo.y, dml * wo.z, dml * wo.w));
     if (ok) {
-      const float4 x = ld4(a2 + row * N2 + col);
+      const float4 x = L2.a ? ld4(L2.a + row * N2 + col) : act4<N2>(L2, row, col, p, seed, inv_keep);
       aw.x += dml * x.x; aw.y += dml * x.y; aw.z += dml * x.z; aw.w += dml * x.w;
       const float4 u = ld4(h.mf_user_ln + row * K0 + col), it = ld4(h.mf_item_ln + row * K0 + col);
       const float4 gv = make_float4(dmf * wm.x, dmf * wm.y, dmf * wm.z, dmf * wm.w);
@@ -504,7 +577,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
   const uint64_t cs = clock ? clock->seed : 0ull;
   float* pp = part + (int64_t)blockIdx.x * kPartW;
   if (fused_head) {
-    head_bwd(Q, P, row0, rows, h, a.l[2].a, inv_n, pp + 3 * (N0 + N1 + N2));
+    head_bwd(Q, P, row0, rows, h, a.l[2], p, a.seed[2] + cs, inv_n, pp + 3 * (N0 + N1 + N2));
   } else {
     for (int e = threadIdx.x; e < kRows * (N2 / 4); e += kThreads) {
       const int r = e / (N2 / 4), c = (e % (N2 / 4)) * 4;
@@ -515,7 +588,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
   }
   ln_bwd<N2, kPQ>(Q, P, row0, rows, a.l[2], p, a.seed[2] + cs, pp);
   if (fused_wgrad) {   // dW2 = dlin2^T a1 (a1 staged in P, then overwritten by dX)
-    stage_rows<N1, kPP>(P, a.l[1].a, row0, rows);
+    stage_act<N1, kPP>(P, a.l[1], row0, rows, p, a.seed[1] + cs);
     __syncthreads();
     wgrad_layer<N2, N1, kPQ, kPP>(Q, P, pp + kW2);
     __syncthreads();
@@ -524,7 +597,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
   __syncthreads();
   ln_bwd<N1, kPP>(P, Q, row0, rows, a.l[1], p, a.seed[1] + cs, pp + 3 * N2);
   if (fused_wgrad) {   // dW1 = dlin1^T a0
-    stage_rows<N0, kPQ>(Q, a.l[0].a, row0, rows);
+    stage_act<N0, kPQ>(Q, a.l[0], row0, rows, p, a.seed[0] + cs);
     __syncthreads();
     wgrad_layer<N1, N0, kPP, kPQ>(P, Q, pp + kW1);
     __syncthreads();
@@ -620,14 +693,15 @@ extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, con
   int rc = make_args(layers, seed, a);
   if (rc) return rc;
   for (int l = 0; l < 3; ++l)
-    if (!a.l[l].r || !a.l[l].mean || !a.l[l].rstd || !a.l[l].dlin || !a.l[l].dgamma ||
-        !a.l[l].dbeta || !a.l[l].dbias) {
-      ncf_set_error("ncf_mlp_bwd: layer %d needs r/mean/rstd/dlin/dbias/dgamma/dbeta", l);
+    if (!a.l[l].r || !a.l[l].mean || !a.l[l].rstd || !a.l[l].dgamma || !a.l[l].dbeta ||
+        !a.l[l].dbias) {
+      ncf_set_error("ncf_mlp_bwd: layer %d needs r/mean/rstd/dbias/dgamma/dbeta", l);
       return NCF_ERR_ARG;
     }
   const bool fw = a.l[0].dw && a.l[1].dw && a.l[2].dw;
-  NCF_CHECK_ARG(!fw || (x && a.l[0].a && a.l[1].a),
-                "ncf_mlp_bwd: fused weight gradients need x and layers[0..1].a");
+  NCF_CHECK_ARG(fw || (a.l[0].dlin && a.l[1].dlin && a.l[2].dlin),
+                "ncf_mlp_bwd: without fused weight gradients every layer needs dlin");
+  NCF_CHECK_ARG(!fw || x, "ncf_mlp_bwd: fused weight gradients need x");
   ncf_head_args h{};
   float inv_n = 0.0f;
   if (head) {
@@ -637,9 +711,8 @@ extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, con
     NCF_CHECK_ARG(h.prob && h.mf_pred && h.mlp_pred && h.mf_user_ln && h.mf_item_ln &&
                       h.mlp_out_w && h.final_w && h.mf_out_w && h.grad_mf_user_ln &&
                       h.grad_mf_item_ln && h.grad_mlp_out_w && h.grad_mlp_out_b &&
-                      h.grad_mf_out_w && h.grad_mf_out_b && h.grad_final_w && h.grad_final_b &&
-                      a.l[2].a,
-                  "ncf_mlp_bwd: incomplete head arguments (and layer 2 needs `a`)");
+                      h.grad_mf_out_w && h.grad_mf_out_b && h.grad_final_w && h.grad_final_b,
+                  "ncf_mlp_bwd: incomplete head arguments");
     const double den = h.loss_denominator > 0 ? h.loss_denominator : (double)n;
     inv_n = den > 0 ? (float)(1.0 / den) : 0.0f;
   } else {

@@ -413,7 +413,8 @@ class NCFEngine:
     def _mlp_layers(self, w, train: bool, bwd: bool):
         """ncf_mlp_layer[] for the fused tower (cached per workspace: the parameter and buffer
         addresses are fixed for its lifetime)."""
-        key = ("mlp", train, bwd, bwd and self.mlp_fused_wgrad())
+        fw = self.mlp_fused_wgrad()
+        key = ("mlp", train, bwd, fw)
         c = w.cache.get(key)
         if c is None:
             m = self.model
@@ -424,13 +425,18 @@ class NCFEngine:
                 L.w, L.ldw, L.b = ptr(lin.weight), lin.weight.shape[1], ptr(lin.bias)
                 L.gamma, L.beta = ptr(ln.weight), ptr(ln.bias)
                 if train:
-                    L.r, L.a, L.mean, L.rstd = ptr(w.r[l]), ptr(w.a[l]), ptr(w.mean[l]), ptr(w.rstd[l])
+                    # with the weight gradients fused into the tower backward, that kernel
+                    # recomputes the activations a from r: the forward does not store them
+                    L.r, L.mean, L.rstd = ptr(w.r[l]), ptr(w.mean[l]), ptr(w.rstd[l])
+                    L.a = None if fw else ptr(w.a[l])
                 if bwd:
                     gv = self.grad_view
-                    L.dlin, L.dbias = ptr(w.dlin[l]), ptr(gv(f"mlp.{4 * l}.bias"))
+                    L.dbias = ptr(gv(f"mlp.{4 * l}.bias"))
                     L.dgamma, L.dbeta = ptr(gv(f"mlp.{4 * l + 2}.weight")), ptr(gv(f"mlp.{4 * l + 2}.bias"))
-                    if self.mlp_fused_wgrad():
+                    if fw:   # dlin stays in LDS (consumed by the fused weight gradients)
                         L.dw = ptr(gv(f"mlp.{4 * l}.weight"))
+                    else:
+                        L.dlin = ptr(w.dlin[l])
             harr = (ctypes.c_int64 * len(hid))(*hid)
             c = w.cache[key] = (arr, ctypes.addressof(arr), harr, ctypes.addressof(harr))
         return c

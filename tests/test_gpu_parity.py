@@ -387,7 +387,10 @@ def test_adam_table_kernel_matches_torch():
 
 
 # ----------------------------------------------------------------------------- behaviour
-def test_dropout_statistics():
+def test_dropout_statistics(monkeypatch):
+    # per-layer weight-gradient launches: the forward then saves the dropped activations a
+    # (the fused tower backward recomputes them instead)
+    monkeypatch.setenv("NCF_MLP_WGRAD", "0")
     torch.manual_seed(0)
     m = ncf.AdvancedNCF(1000, 500, 5, 24, dropout=0.2).to(DEV)
     n = 4096 * 5
@@ -531,7 +534,10 @@ def test_mlp_tower_matches_unfused(monkeypatch, B, drop, wgrad):
         torch.testing.assert_close(b[k], a[k], rtol=0, atol=2e-6)
     torch.testing.assert_close(b["loss"], a["loss"], rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(b["dumf"], a["dumf"], rtol=1e-4, atol=1e-7)
-    for x, y in zip(b["r"] + b["a"], a["r"] + a["a"]):
+    # with the weight gradients fused, the tower forward does not save a (its backward
+    # recomputes it from r), so a is compared only on the per-layer weight-gradient path
+    acts = (lambda o: o["r"] + o["a"]) if wgrad == "0" else (lambda o: o["r"])
+    for x, y in zip(acts(b), acts(a)):
         torch.testing.assert_close(x, y, rtol=1e-5, atol=2e-5)
     torch.testing.assert_close(b["dy"], a["dy"], rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(b["grad"], a["grad"], rtol=1e-4, atol=1e-6)
