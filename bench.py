@@ -248,18 +248,24 @@ def main():
     batches = make_batches(U, I, B, M, 8, dev, seed=100 + rank)
     torch.cuda.synchronize()
 
+    def run_steps(fn, first, count):
+        """count steps over the resident batches from index `first`; the row-sharded step plans
+        the following batch under each step (pipelined input distribution)."""
+        for s in range(first, first + count):
+            u, i, t = batches[s % len(batches)]
+            if sharded:
+                fn(u, i, t, next=batches[(s + 1) % len(batches)][:2])
+            else:
+                fn(u, i, t)
+
     # --- warm-up
-    for s in range(args.warmup):
-        u, i, t = batches[s % len(batches)]
-        step(u, i, t)
+    run_steps(step, 0, args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        u, i, t = batches[s % len(batches)]
-        step(u, i, t)
+    run_steps(step, args.warmup, args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -280,9 +286,7 @@ def main():
     L.PROFILE = []
     torch.cuda.synchronize()
     run = step.eager if hasattr(step, "eager") else step   # the launches a graph replay runs
-    for s in range(args.steps):
-        u, i, t = batches[s % len(batches)]
-        run(u, i, t)
+    run_steps(run, args.warmup + args.steps, args.steps)
     torch.cuda.synchronize()
     prof, L.PROFILE = L.PROFILE, None
 

@@ -437,24 +437,66 @@ int ncf_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_av
                   double lr, double beta1, double beta2, double eps, double weight_decay,
                   double step, void* stream);
 
-/* ---- (e) row sharding over W ranks: owner(id) = id mod W, local row = id div W -------------
- * Pack/unpack kernels around the RCCL all-to-alls (collectives run in torch.distributed).
- * ncf_owner_bucket: send0/send1 = the unique ids in owner order, as the owner's LOCAL rows
- * (id div W); perm = send slot -> compact index; counts[kind * W + dst].                    */
-int ncf_owner_bucket(const int64_t* uniq0, const int64_t* uniq1, const uint32_t* count,
-                     int64_t max_n, int world, int64_t* send0, int64_t* send1, int32_t* perm0,
-                     int32_t* perm1, int64_t* counts, void* workspace, int64_t workspace_bytes,
-                     void* stream);
-int ncf_ids_div(const int64_t* ids, int64_t n, int world, int64_t* out, void* stream);
-int ncf_gather_shard_rows(const int64_t* ids, int64_t n, int world, const float* t0,
-                          const float* t1, int64_t rows, int64_t dim, float* out, int* err_flag,
-                          void* stream);
-int ncf_perm_rows(float* rows, const int32_t* perm, int64_t n, int64_t dim, float* mini0,
-                  float* mini1, int dir, void* stream);
-int ncf_segment_sum_rows(int64_t n0, int64_t n1, int64_t rows0, int64_t rows1, int64_t dim,
-                         const float* src0, const float* src1, float* ga0, float* gb0,
-                         float* ga1, float* gb1, void* workspace, int64_t workspace_bytes,
-                         void* stream);
+/* ---- (e) row sharding over W ranks: owner(id) = id mod W, local row = id div W ------------
+ * The per-rank kernels of the row-sharded step (exchange.hip; the protocol and the RCCL
+ * all-to-alls are in distributed.py).  R = ceil(rows / W) local rows per shard.
+ *
+ * ncf_shard_plan (requester): keys = (id mod W) * R + id div W, deduplicated (the radix dedup of
+ *   ncf_dedup_ids2, whose segments stay in `workspace` for ncf_embedding_bwd_reduce); compact
+ *   index c = rank of the row's key, so compact order = owner order.  Writes uniq keys,
+ *   num_unique[2], inv (position -> compact index), counts[W][2] (rows per destination: users,
+ *   items), send[] = the local rows in destination-major order (per destination: its user rows,
+ *   then its item rows; exactly the all-to-all input), spos0/1[c] = send position of compact c.
+ *   bounds: scratch of 3 * (W + 1) int32.  err_flag |= 1 / 2 for an out-of-range user / item id.
+ * ncf_shard_recv: layout of a received buffer (per source s: kind-0 entries at
+ *   [start[s], start[s] + n0[s]), kind-1 entries up to start[s + 1]).
+ * ncf_shard_owner_prepare (owner): deduplicates the received local rows without a sort (a row
+ *   occurs at most once per source): uniq0/1 (count[2]), uidx0/1 (row -> unique index; per local
+ *   row), mark0/1 (per local row, claim tokens; zero-initialised, token > 0 new every call),
+ *   pos0/1[u * W + s] = received position of row u from source s, -1 if none.  err |= 4 on an
+ *   out-of-range row.
+ * ncf_shard_owner_gather: out[j] = (t?0[row] | t?1[row]) for received entry j ([total][2 dim]).
+ * ncf_shard_owner_gradsum: g?0[u] / g?1[u] = sum over s = 0..W-1 of the halves of got[pos[u][s]]
+ *   (fixed rank order: deterministic).
+ * ncf_shard_rows: requester rows in (dir 0: mini tables m?0/m?1 [c] = halves of buf[spos?[c]])
+ *   and gradients out (dir 1: buf[spos?[c]] = (m?0[c] | m?1[c])).                            */
+#define NCF_SHARD_MAX_WORLD 64
+typedef struct ncf_shard_plan_out {
+  int64_t* keys0;
+  int64_t* keys1;
+  int64_t* uniq0;
+  int64_t* uniq1;
+  uint32_t* num_unique;
+  int64_t* inv0;
+  int64_t* inv1;
+  int64_t* counts;
+  int32_t* send;
+  int32_t* spos0;
+  int32_t* spos1;
+  int32_t* bounds;
+} ncf_shard_plan_out;
+typedef struct ncf_shard_recv {
+  int32_t world;
+  int32_t start[NCF_SHARD_MAX_WORLD + 1];
+  int32_t n0[NCF_SHARD_MAX_WORLD];
+} ncf_shard_recv;
+int ncf_shard_plan(const int64_t* user_ids, const int64_t* item_ids, int64_t n, int world,
+                   int64_t num_users, int64_t num_items, int64_t dim, const ncf_shard_plan_out* out,
+                   void* workspace, int64_t workspace_bytes, int* err_flag, void* stream);
+int ncf_shard_owner_prepare(const int32_t* recv, const ncf_shard_recv* layout, int32_t token,
+                            int32_t* mark0, int32_t* mark1, int32_t* uidx0, int32_t* uidx1,
+                            int64_t rows0, int64_t rows1, int64_t* uniq0, int64_t* uniq1,
+                            uint32_t* count, int32_t* pos0, int32_t* pos1, int* err_flag,
+                            void* stream);
+int ncf_shard_owner_gather(const int32_t* recv, const ncf_shard_recv* layout, const float* t00,
+                           const float* t01, int64_t rows0, const float* t10, const float* t11,
+                           int64_t rows1, int64_t dim, float* out, void* stream);
+int ncf_shard_owner_gradsum(const float* got, const int32_t* pos0, const int32_t* pos1,
+                            const uint32_t* count, int64_t max_unique, int world, int64_t dim,
+                            float* g00, float* g01, float* g10, float* g11, void* stream);
+int ncf_shard_rows(float* buf, const int32_t* spos0, const int32_t* spos1,
+                   const uint32_t* num_unique, int64_t max_n, int64_t dim, float* m00, float* m01,
+                   float* m10, float* m11, int dir, void* stream);
 
 /* Deferred dense-exact schedule (bit-identical to ncf_adam_table, see adam.hip): rows carry
  * stamp[row] = last step reflected; step_table[2s], [2s+1] = fp32 scalars of step s

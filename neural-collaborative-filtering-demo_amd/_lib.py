@@ -83,11 +83,12 @@ SIGNATURES = {
     "ncf_dedup_ids": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, I64, P]),
     "ncf_dedup_ids2": (I32, [P, I64, I64, P, I64, I64, I64, P, P, P, P, P, P, I64, P]),
     "ncf_dedup_inverse": (I32, [I64, I64, I64, I64, I64, P, P, P, I64, P]),
-    "ncf_owner_bucket": (I32, [P, P, P, I64, I32, P, P, P, P, P, P, I64, P]),
-    "ncf_ids_div": (I32, [P, I64, I32, P, P]),
-    "ncf_gather_shard_rows": (I32, [P, I64, I32, P, P, I64, I64, P, P, P]),
-    "ncf_perm_rows": (I32, [P, P, I64, I64, P, P, I32, P]),
-    "ncf_segment_sum_rows": (I32, [I64, I64, I64, I64, I64, P, P, P, P, P, P, P, I64, P]),
+    "ncf_shard_plan": (I32, [P, P, I64, I32, I64, I64, I64, P, P, I64, P, P]),
+    "ncf_shard_owner_prepare": (I32, [P, P, ctypes.c_int32, P, P, P, P, I64, I64, P, P, P, P, P,
+                                      P, P]),
+    "ncf_shard_owner_gather": (I32, [P, P, P, P, I64, P, P, I64, I64, P, P]),
+    "ncf_shard_owner_gradsum": (I32, [P, P, P, P, I64, I32, I64, P, P, P, P, P]),
+    "ncf_shard_rows": (I32, [P, P, P, P, I64, I64, P, P, P, P, I32, P]),
     "ncf_embedding_bwd_reduce": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
                                        P, P, P, P, P, P, P, P, P, I64, P, P]),
     "ncf_slot_reset": (I32, [P, P, I32, P, I64, P]),
@@ -165,6 +166,22 @@ class TablePair(ctypes.Structure):
     """ncf_table_pair (include/ncf_hip.h)."""
     _fields_ = [("p0", P), ("m0", P), ("v0", P), ("p1", P), ("m1", P), ("v1", P), ("g0", P),
                 ("g1", P), ("row_ids", P), ("stamp", P), ("rows", I64)]
+
+
+SHARD_MAX_WORLD = 64
+
+
+class ShardPlanOut(ctypes.Structure):
+    """ncf_shard_plan_out (include/ncf_hip.h)."""
+    _fields_ = [(f, P) for f in ("keys0", "keys1", "uniq0", "uniq1", "num_unique", "inv0", "inv1",
+                                 "counts", "send", "spos0", "spos1", "bounds")]
+
+
+class ShardRecv(ctypes.Structure):
+    """ncf_shard_recv (include/ncf_hip.h): per source s, kind-0 entries at [start[s],
+    start[s] + n0[s]), kind-1 entries up to start[s + 1]."""
+    _fields_ = [("world", ctypes.c_int32), ("start", ctypes.c_int32 * (SHARD_MAX_WORLD + 1)),
+                ("n0", ctypes.c_int32 * SHARD_MAX_WORLD)]
 
 
 class ReduceList(ctypes.Structure):
@@ -246,4 +263,11 @@ def ptr(t) -> int:
 
 
 def stream_ptr(device=None) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    """Raw hipStream_t of torch's current stream on `device` (int, torch.device or None)."""
+    if device is None:
+        idx = torch.cuda.current_device()
+    elif isinstance(device, int):
+        idx = device
+    else:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+    return torch._C._cuda_getCurrentRawStream(idx)

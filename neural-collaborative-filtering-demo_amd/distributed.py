@@ -1,29 +1,38 @@
 """Row-sharded multi-GPU training step — one process per GPU, RCCL over xGMI.
 
 Partitioning: every embedding table is row-sharded by ``owner(id) = id mod W``, local row
-``id div W`` (each rank holds ``ceil(rows / W)`` rows of each of the four tables, their Adam
+``id div W`` (each rank holds ``R = ceil(rows / W)`` rows of each of the four tables, their Adam
 moments and deferred-Adam stamps).  Dense parameters are replicated.  Each rank trains on its own
 batch of B groups (weak scaling); the W local batches form one global batch whose loss is the mean
 over all W*N samples — a W-rank step equals the 1-rank step on the concatenated batch.
 
-Per step and per id kind (users, items):
-  1. dedup the local ids (radix sort), bucket the unique ids by owner          [kernels]
-  2. all_to_all of per-owner counts (host splits), then of the ids             [RCCL]
-  3. owners dedup what they received, bring those rows current (deferred
-     dense-exact Adam catch-up) and gather the GMF+MLP rows                    [kernels]
-  4. all_to_all of the rows back; requesters scatter them into mini tables     [RCCL, kernels]
-  5. forward + backward on the mini tables with remapped ids (the 1-GPU kernels)
-  6. all_to_all of the compact row gradients to the owners, who sum them in a
-     fixed order (source rank, then sender order) and apply the step          [RCCL, kernels]
-  7. one all_reduce of the flat dense-gradient buffer, replicated dense Adam   [RCCL, kernel]
-The exchange protocol (``ShardExchange`` + ``ShardedTrainStep``) is device-agnostic; the ops
-backend does the per-rank work: ``HipShardOps`` (this file, the product path) or, in the CPU
-``gloo`` tests, a torch reference backend.
+A step has a PLAN and a RUN:
+  plan  (requester)  re-key ids as (owner, local row), dedup (radix sort): the compact order of
+                     the unique rows is the owner order, so the all-to-all send buffer comes
+                     straight out of the dedup; all_to_all of the per-destination counts and ONE
+                     device-to-host copy of them (RCCL needs the split sizes on the host)
+  run   1. all_to_all of the local rows (users then items per destination)          [RCCL]
+        2. owners dedup what they received without a sort (per-row claim tokens), bring
+           those rows current (deferred dense-exact Adam catch-up), gather GMF+MLP rows
+        3. all_to_all of the rows back; requesters unpack them into mini tables        [RCCL]
+        4. forward + backward on the mini tables (the 1-GPU kernels; the dedup's segments
+           drive the backward's segment reduce)
+        5. all_to_all of the compact row gradients to the owners, who sum them per row in
+           rank order (deterministic) and apply the step; rolling sweep                [RCCL]
+        6. one all_reduce of the flat dense-gradient buffer, replicated dense Adam     [RCCL]
+The plan of step t+1 is pipelined under the run of step t (``step(u, i, t, next=(u', i'))``, the
+role of torchrec's TrainPipelineSparseDist): its kernels run on a side stream and its count
+exchange on a second communicator, so the host-side wait for the split sizes overlaps the GPU
+work of step t instead of draining the GPU every step.
+
+The protocol (``ShardExchange`` + ``ShardedTrainStep``) is device-agnostic; the ops backend does
+the per-rank work: ``HipShardOps`` (this file, the product path) or, in the CPU ``gloo`` tests, a
+torch reference backend.
 """
 import ctypes
 import math
 import random
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import List, Optional
 
 import torch
@@ -34,39 +43,54 @@ from ._lib import ptr
 
 
 class ShardExchange:
-    """The collectives of the sharded step (torch.distributed: RCCL on GPU, gloo on CPU)."""
+    """The collectives of the sharded step (torch.distributed: RCCL on GPU, gloo on CPU).
+    ``plan_group`` (a second communicator) carries the count exchange of the pipelined plan so
+    it never queues behind the run's collectives."""
 
-    def __init__(self, group=None, device=None):
+    def __init__(self, group=None, device=None, plan_group=None):
         self.group = group
+        self.plan_group = plan_group if plan_group is not None else group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.device = device
 
-    def exchange_counts_dev(self, counts: torch.Tensor):
-        """Device counts [2 * W] (kind-major) -> (send, recv) host lists per kind, with ONE
-        device-to-host copy for both (the only host sync of a step)."""
+    def counts_issue(self, plan):
+        """Start the exchange of plan.counts ([W][2] per destination: users, items; device
+        tensor or host lists).  On the GPU the all_to_all runs on the plan's side stream and
+        communicator and the result lands in pinned host memory with an event: nothing waits."""
         W = self.world
-        send = counts.view(2, W).t().contiguous()          # [W, 2]: per destination
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send, group=self.group)
-        both = torch.cat([send, recv]).cpu().tolist()
-        s, r = both[:W], both[W:]
-        return ([[s[d][0] for d in range(W)], [s[d][1] for d in range(W)]],
-                [[r[x][0] for x in range(W)], [r[x][1] for x in range(W)]])
+        if plan.stream is None:                      # CPU (gloo): synchronous
+            send = torch.tensor(plan.counts, dtype=torch.int64, device=self.device).view(W, 2)
+            recv = torch.empty_like(send)
+            dist.all_to_all_single(recv, send, group=self.plan_group)
+            both = torch.cat([send, recv]).tolist()
+            plan.send_counts, plan.recv_counts = both[:W], both[W:]
+            return
+        with torch.cuda.stream(plan.stream):
+            send = plan.counts.view(W, 2)
+            both = plan.extra["counts_both"]          # device [2W, 2]: send rows, then recv rows
+            dist.all_to_all_single(both[W:], send, group=self.plan_group)
+            both[:W].copy_(send)
+            plan.extra["counts_host"].copy_(both, non_blocking=True)
+            plan.extra["counts_ev"].record()
 
-    def exchange_counts(self, counts: List[List[int]]) -> List[List[int]]:
-        """counts[kind][dst] -> recv[kind][src] (one all_to_all of a [W, 2] int64 tensor)."""
+    def counts_wait(self, plan):
+        """plan.send_counts / plan.recv_counts as host lists [W][2] (the step's only host
+        wait: for a plan issued a step ahead it has long completed)."""
+        if plan.send_counts is not None:
+            return
         W = self.world
-        send = torch.tensor([[counts[0][d], counts[1][d]] for d in range(W)], dtype=torch.int64,
-                            device=self.device)
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send, group=self.group)
-        r = recv.cpu().tolist()
-        return [[r[s][0] for s in range(W)], [r[s][1] for s in range(W)]]
+        plan.extra["counts_ev"].synchronize()
+        both = plan.extra["counts_host"].tolist()
+        plan.send_counts, plan.recv_counts = both[:W], both[W:]
+
+    def exchange_counts(self, plan):
+        self.counts_issue(plan)
+        self.counts_wait(plan)
 
     def exchange(self, t: torch.Tensor, send_splits: List[int], recv_splits: List[int]):
         out = torch.empty((sum(recv_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_to_all_single(out, t[:sum(send_splits)].contiguous(), recv_splits, send_splits,
+        dist.all_to_all_single(out, t[:sum(send_splits)], recv_splits, send_splits,
                                group=self.group)
         return out
 
@@ -77,35 +101,55 @@ class ShardExchange:
 
 @dataclass
 class Plan:
-    send: list          # per kind: unique ids in owner order
-    perm: list          # per kind: send slot -> local compact index
-    counts: Optional[list] = None   # per kind: per-owner counts (host ints)
+    """One step's requester-side plan.  ``send`` holds the local rows in destination-major order
+    (per destination: users then items); ``counts`` the per-destination row counts [W][2]."""
+    send: object
+    counts: object
+    stream: Optional[object] = None
+    send_counts: Optional[list] = None     # host [W][2], after ShardExchange.exchange_counts
     recv_counts: Optional[list] = None
-    counts_dev: Optional[torch.Tensor] = None   # device counts (HIP backend: one sync later)
+    extra: dict = field(default_factory=dict)
+
+    def splits(self):
+        return ([a + b for a, b in self.send_counts], [a + b for a, b in self.recv_counts])
+
+    def totals(self):
+        return (sum(c[0] for c in self.send_counts), sum(c[1] for c in self.send_counts))
 
 
 class ShardedTrainStep:
-    """One data-parallel + row-sharded training step: the protocol above over an ops backend."""
+    """One data-parallel + row-sharded training step: the protocol above over an ops backend.
+    ``step(u, i, t, next=(u2, i2))`` also plans the following step (pipelined)."""
 
     def __init__(self, ops, exchange: ShardExchange):
         self.ops, self.x = ops, exchange
+        self._pending = None      # (user_ids, item_ids, Plan) planned ahead
 
-    def __call__(self, user_ids, item_ids, targets):
+    def plan(self, user_ids, item_ids):
+        p = self.ops.plan(user_ids, item_ids, self.x.world)
+        self.x.counts_issue(p)
+        return p
+
+    def __call__(self, user_ids, item_ids, targets, next=None):
         ops, X = self.ops, self.x
-        n = user_ids.numel()
-        ded = ops.dedup(user_ids, item_ids)
-        plan = ops.bucket(ded, X.world)
-        if plan.counts_dev is not None:
-            plan.counts, plan.recv_counts = X.exchange_counts_dev(plan.counts_dev)
+        ops.mark_entry()          # ids of this call and of `next` exist from here on
+        pend, self._pending = self._pending, None
+        if pend is not None and pend[0] is user_ids and pend[1] is item_ids:
+            plan = pend[2]        # issued one call ago: its counts are (almost surely) home
         else:
-            plan.recv_counts = X.exchange_counts(plan.counts)
-        recv = [X.exchange(plan.send[k], plan.counts[k], plan.recv_counts[k]) for k in (0, 1)]
-        own = ops.owner_prepare(recv)
-        rows = [ops.owner_gather(own, k, recv[k]) for k in (0, 1)]
-        back = [X.exchange(rows[k], plan.recv_counts[k], plan.counts[k]) for k in (0, 1)]
-        grads, loss = ops.compute(ded, plan, back, user_ids, item_ids, targets,
-                                  loss_denominator=n * X.world)
-        got = [X.exchange(grads[k], plan.counts[k], plan.recv_counts[k]) for k in (0, 1)]
+            plan = self.plan(user_ids, item_ids)
+        X.counts_wait(plan)
+        if next is not None:      # plan step t+1 now: it runs under this step's GPU work
+            self._pending = (next[0], next[1], self.plan(next[0], next[1]))
+        ops.begin(plan)
+        send_splits, recv_splits = plan.splits()
+        recv = X.exchange(plan.send, send_splits, recv_splits)
+        own = ops.owner_prepare(recv, plan)
+        rows = ops.owner_gather(own, recv)
+        back = X.exchange(rows, recv_splits, send_splits)
+        grads, loss = ops.compute(plan, back, user_ids, item_ids, targets,
+                                  loss_denominator=user_ids.numel() * X.world)
+        got = X.exchange(grads, send_splits, recv_splits)
         ops.owner_apply(own, got)
         X.all_reduce_(ops.dense_grad())
         ops.dense_step()
@@ -118,9 +162,11 @@ class HipShardOps:
     def __init__(self, model, num_users: int, num_items: int, world: int, lr=1e-3,
                  betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, sweep_every=64):
         from .deferred import DeferredTableAdam
+        if world > _lib.SHARD_MAX_WORLD:
+            raise ValueError(f"world size {world} > {_lib.SHARD_MAX_WORLD}")
         self.model, self.U, self.I, self.W = model, num_users, num_items, world
-        self.Ru, self.Ri = model.num_users, model.num_products      # shard rows
-        if self.Ru < math.ceil(num_users / world) or self.Ri < math.ceil(num_items / world):
+        self.Ru, self.Ri = math.ceil(num_users / world), math.ceil(num_items / world)
+        if model.num_users < self.Ru or model.num_products < self.Ri:
             raise ValueError("shard model too small for the global tables")
         self.eng = model.engine
         self.eng.ensure_layout()
@@ -140,122 +186,201 @@ class HipShardOps:
         self.rng = random.Random(self.base_seed)     # dropout seeds without a device sync
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.last_loss = None
+        # owner side: claim tokens and row -> unique index, one int32 per local row and kind
+        ru, ri = model.num_users, model.num_products
+        self.mark = [torch.zeros(ru, dtype=torch.int32, device=self.dev),
+                     torch.zeros(ri, dtype=torch.int32, device=self.dev)]
+        self.uidx = [torch.zeros(ru, dtype=torch.int32, device=self.dev),
+                     torch.zeros(ri, dtype=torch.int32, device=self.dev)]
+        self.token = 0
+        self.cnt = torch.zeros(2, dtype=torch.int32, device=self.dev)
+        self.plan_stream = torch.cuda.Stream(self.dev)
+        self._sets = [None, None]     # double-buffered plan buffers (plan t+1 while t runs)
+        self._k = 0
+        self._bufs = {}
 
     def _st(self):
         return _lib.stream_ptr(self.dev)
 
-    def _ws(self, n):
-        return torch.empty(_lib.query("ncf_embedding_bwd_workspace", max(n, 1), self.D),
-                           dtype=torch.uint8, device=self.dev)
+    def _buf(self, name, shape, dtype=torch.float32):
+        """Grow-only scratch buffer (no allocator traffic in the steady state)."""
+        n = math.prod(shape)
+        b = self._bufs.get(name)
+        if b is None or b.numel() < n:
+            b = self._bufs[name] = torch.empty(max(n, 1), dtype=dtype, device=self.dev)
+        return b[:n].view(*shape)
 
-    # 1. local dedup + inverse map
-    def dedup(self, uid, iid):
+    def _plan_set(self, n):
+        k = self._k % 2
+        self._k += 1
+        s = self._sets[k]
+        if s is None or s["n"] < n:
+            i64 = dict(dtype=torch.int64, device=self.dev)
+            i32 = dict(dtype=torch.int32, device=self.dev)
+            cap = max(n, 1)
+            s = self._sets[k] = dict(
+                n=n, keys=[torch.empty(cap, **i64) for _ in range(2)],
+                uniq=[torch.empty(cap, **i64) for _ in range(2)],
+                num_unique=torch.zeros(2, dtype=torch.int32, device=self.dev),
+                inv=[torch.empty(cap, **i64) for _ in range(2)],
+                counts=torch.zeros(self.W, 2, **i64), send=torch.empty(2 * cap, **i32),
+                spos=[torch.empty(cap, **i32) for _ in range(2)],
+                bounds=torch.empty(3 * (self.W + 1), **i32),
+                counts_both=torch.zeros(2 * self.W, 2, **i64),
+                counts_host=torch.zeros(2 * self.W, 2, dtype=torch.int64, pin_memory=True),
+                counts_ev=torch.cuda.Event(),
+                ws=torch.empty(_lib.query("ncf_embedding_bwd_workspace", cap, self.D),
+                               dtype=torch.uint8, device=self.dev),
+                ready=torch.cuda.Event())
+            o = s["out"] = _lib.ShardPlanOut()
+            o.keys0, o.keys1 = ptr(s["keys"][0]), ptr(s["keys"][1])
+            o.uniq0, o.uniq1 = ptr(s["uniq"][0]), ptr(s["uniq"][1])
+            o.num_unique = ptr(s["num_unique"])
+            o.inv0, o.inv1 = ptr(s["inv"][0]), ptr(s["inv"][1])
+            o.counts, o.send = ptr(s["counts"]), ptr(s["send"])
+            o.spos0, o.spos1 = ptr(s["spos"][0]), ptr(s["spos"][1])
+            o.bounds = ptr(s["bounds"])
+        return s
+
+    def mark_entry(self):
+        """Event on the compute stream at the start of a step call: the step's ids and the
+        next step's ids are complete there, and so is the run that last used the plan buffer
+        set the next plan will fill (two sets alternate).  A plan waits for this event only,
+        not for the run enqueued after it, so it overlaps that run."""
+        self._entry = torch.cuda.Event()
+        self._entry.record()
+
+    # plan: requester-side dedup in owner order (side stream)
+    def plan(self, uid, iid, world):
         n = uid.numel()
-        w = self.eng.workspace(n, self.M, True)
-        st = self._st()
-        _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, self.D, self.U, self.I, ptr(w.uniq_u),
-                  ptr(w.uniq_i), None, None, ptr(w.num_unique), ptr(w.emb_ws), w.emb_ws.numel(), st)
-        inv_u = torch.empty(n, dtype=torch.int64, device=self.dev)
-        inv_i = torch.empty(n, dtype=torch.int64, device=self.dev)
-        _lib.call("ncf_dedup_inverse", n, n, self.U, self.I, self.D, ptr(inv_u), ptr(inv_i),
-                  ptr(w.emb_ws), w.emb_ws.numel(), st)
-        return {"w": w, "n": n, "inv": (inv_u, inv_i)}
+        s = self._plan_set(n)
+        if getattr(self, "_entry", None) is None:
+            self.mark_entry()
+        ps = self.plan_stream
+        ps.wait_event(self._entry)
+        _lib.call("ncf_shard_plan", ptr(uid), ptr(iid), n, self.W, self.U, self.I, self.D,
+                  ctypes.addressof(s["out"]), ptr(s["ws"]), s["ws"].numel(), ptr(self.err),
+                  ps.cuda_stream)
+        s["ready"].record(ps)
+        return Plan(send=s["send"], counts=s["counts"], stream=self.plan_stream,
+                    extra={"set": s, "n": n, "counts_both": s["counts_both"],
+                           "counts_host": s["counts_host"], "counts_ev": s["counts_ev"]})
 
-    def bucket(self, ded, world):
-        w, n = ded["w"], ded["n"]
-        send = [torch.empty(max(n, 1), dtype=torch.int64, device=self.dev) for _ in range(2)]
-        perm = [torch.empty(max(n, 1), dtype=torch.int32, device=self.dev) for _ in range(2)]
-        counts = torch.zeros(2 * world, dtype=torch.int64, device=self.dev)
-        ws = self._ws(n)
-        _lib.call("ncf_owner_bucket", ptr(w.uniq_u), ptr(w.uniq_i), ptr(w.num_unique), n, world,
-                  ptr(send[0]), ptr(send[1]), ptr(perm[0]), ptr(perm[1]), ptr(counts), ptr(ws),
-                  ws.numel(), self._st())
-        return Plan(send=send, perm=perm, counts_dev=counts)      # split sizes fetched later
+    def begin(self, plan):
+        torch.cuda.current_stream(self.dev).wait_event(plan.extra["set"]["ready"])
 
-    # 3. owner side: dedup received ids (already local rows), catch their rows up
-    def owner_prepare(self, recv):
+    # 2. owner side: sort-free dedup of the received rows, catch-up, gather
+    def _layout(self, counts):
+        L = self._recv_layout = getattr(self, "_recv_layout", None) or _lib.ShardRecv()
+        L.world = self.W
+        off = 0
+        for s in range(self.W):
+            L.start[s] = off
+            L.n0[s] = counts[s][0]
+            off += counts[s][0] + counts[s][1]
+        L.start[self.W] = off
+        return L
+
+    def owner_prepare(self, recv, plan):
         st = self._st()
-        rn = [r.numel() for r in recv]
-        nmax = max(rn)
-        uq = [torch.empty(max(nmax, 1), dtype=torch.int64, device=self.dev) for _ in range(2)]
-        cnt = torch.zeros(2, dtype=torch.int32, device=self.dev)
-        ws = self._ws(nmax)
-        _lib.call("ncf_dedup_ids2", ptr(recv[0]), rn[0], self.Ru, ptr(recv[1]), rn[1], self.Ri,
-                  self.D, ptr(uq[0]), ptr(uq[1]), None, None, ptr(cnt), ptr(ws), ws.numel(), st)
+        L = self._layout(plan.recv_counts)
+        tu = sum(c[0] for c in plan.recv_counts)
+        ti = sum(c[1] for c in plan.recv_counts)
+        nmax = max(tu, ti)
+        uq = [self._buf("own_uq0", (max(tu, 1),), torch.int64),
+              self._buf("own_uq1", (max(ti, 1),), torch.int64)]
+        pos = [self._buf("own_pos0", (max(tu, 1), self.W), torch.int32),
+               self._buf("own_pos1", (max(ti, 1), self.W), torch.int32)]
+        self.token += 1
+        _lib.call("ncf_shard_owner_prepare", ptr(recv), ctypes.addressof(L), self.token,
+                  ptr(self.mark[0]), ptr(self.mark[1]), ptr(self.uidx[0]), ptr(self.uidx[1]),
+                  self.mark[0].numel(), self.mark[1].numel(), ptr(uq[0]), ptr(uq[1]),
+                  ptr(self.cnt), ptr(pos[0]), ptr(pos[1]), ptr(self.err), st)
         d = self.deferred
         if nmax > 0:
             d._ensure(d.t + 1)
             pairs = self._pairs(uq)
             _lib.call("ncf_adam_pairs_catchup_clock", ctypes.addressof(pairs), 2, self.D,
-                      ptr(cnt), nmax, 0, ptr(self.clock), ptr(d._table), *d._consts(), st)
-        return {"rn": rn, "uniq": uq, "cnt": cnt, "ws": ws}
+                      ptr(self.cnt), nmax, 0, ptr(self.clock), ptr(d._table), *d._consts(), st)
+        return {"layout": L, "uniq": uq, "pos": pos, "nmax": nmax}
 
     def _pairs(self, uq, G=None):
-        pairs = self.deferred._pairs()
-        for k in (0, 1):
-            pairs[k].row_ids = ptr(uq[k])
-            if G is not None:
-                pairs[k].g0, pairs[k].g1 = ptr(G[2 * k]), ptr(G[2 * k + 1])
+        """ncf_table_pair[2] for the owner's unique rows (cached: the buffers are stable)."""
+        key = (ptr(uq[0]), ptr(uq[1])) + (tuple(ptr(g) for g in G) if G is not None else ())
+        cache = self.__dict__.setdefault("_pairs_cache", {})
+        pairs = cache.get(key)
+        if pairs is None:
+            pairs = cache[key] = self.deferred._pairs()
+            for k in (0, 1):
+                pairs[k].row_ids = ptr(uq[k])
+                if G is not None:
+                    pairs[k].g0, pairs[k].g1 = ptr(G[2 * k]), ptr(G[2 * k + 1])
         return pairs
 
-    def owner_gather(self, own, k, recv_ids):
-        n = recv_ids.numel()
-        out = torch.empty(max(n, 1), 2 * self.D, device=self.dev)
+    def owner_gather(self, own, recv):
+        L = own["layout"]
+        total = L.start[self.W]
+        out = self._buf("own_rows", (max(total, 1), 2 * self.D))
         tb = self.eng.table_params()
-        t0, t1 = (tb["mf_user"], tb["mlp_user"]) if k == 0 else (tb["mf_item"], tb["mlp_item"])
-        _lib.call("ncf_gather_shard_rows", ptr(recv_ids), n, 1, ptr(t0), ptr(t1),
-                  self.Ru if k == 0 else self.Ri, self.D, ptr(out), ptr(self.err), self._st())
-        return out[:n]
+        _lib.call("ncf_shard_owner_gather", ptr(recv), ctypes.addressof(L), ptr(tb["mf_user"]),
+                  ptr(tb["mlp_user"]), self.mark[0].numel(), ptr(tb["mf_item"]),
+                  ptr(tb["mlp_item"]), self.mark[1].numel(), self.D, ptr(out), self._st())
+        return out[:total]
 
-    # 5. forward + backward on the mini tables
-    def compute(self, ded, plan, back, uid, iid, targets, loss_denominator):
+    # 3.-4. forward + backward on the mini tables
+    def compute(self, plan, back, uid, iid, targets, loss_denominator):
         st = self._st()
-        eng, w = self.eng, ded["w"]
-        nu, ni = sum(plan.counts[0]), sum(plan.counts[1])
-        mini = {k: torch.empty(max(c, 1), self.D, device=self.dev)
-                for k, c in (("mf_user", nu), ("mlp_user", nu), ("mf_item", ni), ("mlp_item", ni))}
-        _lib.call("ncf_perm_rows", ptr(back[0]), ptr(plan.perm[0]), nu, self.D,
-                  ptr(mini["mf_user"]), ptr(mini["mlp_user"]), 0, st)
-        _lib.call("ncf_perm_rows", ptr(back[1]), ptr(plan.perm[1]), ni, self.D,
-                  ptr(mini["mf_item"]), ptr(mini["mlp_item"]), 0, st)
+        eng, s = self.eng, plan.extra["set"]
+        n = plan.extra["n"]
+        nu, ni = plan.totals()
+        D = self.D
+        # mini tables: four [n][D] slabs of one buffer sized for the batch (unique rows <= n)
+        base = ptr(self._buf("mini", (4, max(n, 1), D)))
+        slab = 4 * max(n, 1) * D
+        mini = {"mf_user": base, "mlp_user": base + slab, "mf_item": base + 2 * slab,
+                "mlp_item": base + 3 * slab}
+        _lib.call("ncf_shard_rows", ptr(back), ptr(s["spos"][0]), ptr(s["spos"][1]),
+                  ptr(s["num_unique"]), max(nu, ni), D, mini["mf_user"], mini["mlp_user"],
+                  mini["mf_item"], mini["mlp_item"], 0, st)
         m = self.model
         drop_p = float(m.dropout)
         seed = self.rng.getrandbits(62) if drop_p > 0 else 0
-        inv_u, inv_i = ded["inv"]
+        inv_u, inv_i = s["inv"][0][:n], s["inv"][1][:n]
+        w = eng.workspace(n, self.M, True)
+        w.emb_ws = s["ws"]            # the plan's dedup segments drive the segment reduce
 
-        def mark(wk, u, i, s):
+        def mark(wk, u, i, st_):
             wk.deduped = True
         eng.forward(inv_u, inv_i, self.M, True, drop_p, seed, prepare=mark, tables=mini,
                     rows=(max(nu, 1), max(ni, 1)))
-        ar_u = torch.arange(max(nu, 1), dtype=torch.int64, device=self.dev)
-        ar_i = torch.arange(max(ni, 1), dtype=torch.int64, device=self.dev)
+        ar = self._buf("arange", (max(n, 1),), torch.int64)
+        if self._bufs.get("arange_n") != ar.numel():
+            torch.arange(ar.numel(), out=ar)
+            self._bufs["arange_n"] = ar.numel()
         eng.backward(w, inv_u, inv_i, None, targets, drop_p, seed,
-                     loss_denominator=loss_denominator, tables=mini, rows=(self.U, self.I),
-                     uniq=(ar_u, ar_i))
+                     loss_denominator=loss_denominator, tables=mini,
+                     rows=(self.W * self.Ru, self.W * self.Ri), uniq=(ar, ar))
         eng.pending = None
-        out = []
-        for k, (a, b), c in ((0, ("mf_user", "mlp_user"), nu), (1, ("mf_item", "mlp_item"), ni)):
-            g = torch.empty(max(c, 1), 2 * self.D, device=self.dev)
-            _lib.call("ncf_perm_rows", ptr(g), ptr(plan.perm[k]), c, self.D, ptr(w.G[a]),
-                      ptr(w.G[b]), 1, st)
-            out.append(g[:c])
+        g = self._buf("send_grads", (max(nu + ni, 1), 2 * D))
+        _lib.call("ncf_shard_rows", ptr(g), ptr(s["spos"][0]), ptr(s["spos"][1]),
+                  ptr(s["num_unique"]), max(nu, ni), D, ptr(w.G["mf_user"]), ptr(w.G["mlp_user"]),
+                  ptr(w.G["mf_item"]), ptr(w.G["mlp_item"]), 1, st)
         self.last_loss = w.loss
-        return out, w.loss
+        return g[:nu + ni], w.loss
 
-    # 6. owner side: sum received gradients per unique row, apply the step
+    # 5. owner side: sum received gradients per unique row (rank order), apply the step
     def owner_apply(self, own, got):
         st = self._st()
-        rn, uq, cnt, ws = own["rn"], own["uniq"], own["cnt"], own["ws"]
-        G = [torch.empty(max(rn[k], 1), self.D, device=self.dev) for k in (0, 0, 1, 1)]
-        _lib.call("ncf_segment_sum_rows", rn[0], rn[1], self.Ru, self.Ri, self.D, ptr(got[0]),
-                  ptr(got[1]), ptr(G[0]), ptr(G[1]), ptr(G[2]), ptr(G[3]), ptr(ws), ws.numel(), st)
+        uq, pos, nmax = own["uniq"], own["pos"], own["nmax"]
+        G = [self._buf(f"own_g{j}", (max(nmax, 1), self.D)) for j in range(4)]
+        _lib.call("ncf_shard_owner_gradsum", ptr(got), ptr(pos[0]), ptr(pos[1]), ptr(self.cnt),
+                  nmax, self.W, self.D, ptr(G[0]), ptr(G[1]), ptr(G[2]), ptr(G[3]), st)
         d = self.deferred
-        nmax = max(rn)
         d._ensure(d.t + 1)
         if nmax > 0:
             pairs = self._pairs(uq, G)
-            _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2, self.D, ptr(cnt),
-                      nmax, 1, ptr(self.clock), ptr(d._table), *d._consts(), st)
+            _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2, self.D,
+                      ptr(self.cnt), nmax, 1, ptr(self.clock), ptr(d._table), *d._consts(), st)
         d.advance(st)                               # rolling sweep of step t + 1 (clock)
 
     def dense_grad(self):
@@ -271,19 +396,29 @@ class HipShardOps:
                   ptr(self.deferred._table), 1, ptr(self.clock), b1, b2, self.eps, self.wd, st)
         _lib.call("ncf_step_clock_advance", ptr(self.clock), self.base_seed, st)
 
+    def check(self):
+        """Raise IndexError if any step saw an out-of-range id (one host sync)."""
+        e = int(self.err.item())
+        if e:
+            raise IndexError(f"row-sharded step: out-of-range ids (flags {e:#x})")
+
 
 def shard_rows(rows: int, world: int) -> int:
     return (rows + world - 1) // world
 
 
-def make_sharded_step(model_factory, num_users, num_items, group=None, **adam):
+def make_sharded_step(model_factory, num_users, num_items, group=None, plan_group=None, **adam):
     """Build the local shard model (tables of ceil(rows / W) rows) and its sharded step.
-    Dense parameters are broadcast from rank 0 so every replica starts identical."""
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    Dense parameters are broadcast from rank 0 so every replica starts identical.  A second
+    communicator for the pipelined plan's count exchange is created unless given."""
+    world = dist.get_world_size(group)
     model = model_factory(shard_rows(num_users, world), shard_rows(num_items, world))
     dev = model.mf_norm.weight.device
     eng = model.engine
     eng.ensure_layout()
     dist.broadcast(eng.flat, src=0, group=group)
+    if plan_group is None:
+        ranks = list(range(world)) if group is None else dist.get_process_group_ranks(group)
+        plan_group = dist.new_group(ranks)
     ops = HipShardOps(model, num_users, num_items, world, **adam)
-    return model, ShardedTrainStep(ops, ShardExchange(group, dev))
+    return model, ShardedTrainStep(ops, ShardExchange(group, dev, plan_group))

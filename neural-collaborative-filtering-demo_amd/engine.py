@@ -25,6 +25,11 @@ from ._lib import ptr
 LN_EPS = 1e-5
 
 
+def _tptr(t) -> int:
+    """A table given as a tensor or as a raw device pointer (int)."""
+    return t if isinstance(t, int) else ptr(t)
+
+
 def _align4(n: int) -> int:
     return (n + 3) // 4 * 4
 
@@ -234,6 +239,7 @@ class NCFEngine:
             flat[o:o + n].copy_(p.data.reshape(-1))
             p.data = flat[o:o + n].view(shp)
         self.flat = flat
+        self._layout_key = self._pp_cache = None    # re-validated by ensure_layout
         self.flat_grad = torch.zeros(total, dtype=torch.float32, device=dev)
         self.offsets = offs
         self.dense_names = [n for n, _ in ps]
@@ -250,6 +256,10 @@ class NCFEngine:
         o, n, shp = self.offsets[name]
         return self.flat_grad[o:o + n].view(shp)
 
+    def gptr(self, name) -> int:
+        """Device pointer of a parameter's slice of the flat gradient buffer."""
+        return self.flat_grad.data_ptr() + 4 * self.offsets[name][0]
+
     def is_flat_view(self, p) -> bool:
         if self.flat is None:
             return False
@@ -257,10 +267,36 @@ class NCFEngine:
         return base <= p.data_ptr() < base + self.flat.numel() * 4
 
     def ensure_layout(self):
+        """Re-pack when a dense parameter no longer views the flat buffer (.to(), assignment).
+        Fast path: the parameter objects and their data pointers as recorded at the last pack
+        (one data_ptr per parameter, no module traversal)."""
+        key = getattr(self, "_layout_key", None)
+        if key is not None and self.flat is not None:
+            plist, ptrs = key
+            if all(p.data_ptr() == q for p, q in zip(plist, ptrs)) and \
+                    self.model.mf_norm.weight is plist[0]:
+                return
         ps = self.dense_params()
         if self.flat is None or any(not self.is_flat_view(p) for _, p in ps) or \
                 self.flat.device != ps[0][1].device:
             self.flatten()
+            ps = self.dense_params()
+        plist = [p for _, p in ps]
+        self._layout_key = (plist, [p.data_ptr() for p in plist])
+        self._pp_cache = None
+
+    def pp(self) -> dict:
+        """Device pointers of the parameters and tables the launches pass (cached; valid while
+        the layout checked by ensure_layout holds)."""
+        c = getattr(self, "_pp_cache", None)
+        if c is None:
+            m = self.model
+            att = m.user_product_attention
+            c = {name: ptr(p) for name, p in self.dense_params()}
+            c.update({"t_" + k: ptr(v) for k, v in self.table_params().items()})
+            c["att_w"] = tuple(ptr(getattr(att, nm).weight) for nm in ("q_proj", "k_proj", "v_proj", "out_proj"))
+            self._pp_cache = c
+        return c
 
     # ------------------------------------------------------------------ helpers
     def _check_device(self):
@@ -332,7 +368,11 @@ class NCFEngine:
         D, H, T, hid = m.mlp_embedding_dim, m.num_heads, m.temporal_dim, list(m.mlp_hidden_dims)
         if m.mf_embedding_dim != D:
             raise NotImplementedError("mf_embedding_dim must equal mlp_embedding_dim on this path")
-        tb = tables or self.table_params()
+        pp = self.pp()
+        if tables is None:
+            tbp = (pp["t_mf_user"], pp["t_mf_item"], pp["t_mlp_user"], pp["t_mlp_item"])
+        else:
+            tbp = tuple(_tptr(tables[k]) for k in ("mf_user", "mf_item", "mlp_user", "mlp_item"))
         n_users, n_items = rows or (m.num_users, m.num_products)
         w.err.zero_()
         w.deduped = False
@@ -344,21 +384,21 @@ class NCFEngine:
             raise ValueError("the temporal (hour) path is forward_simple's: eval, one item per group")
         # a2-a4: 4 gathers + mf_norm/mlp_norm + GMF  (architecture.py:286-287, 305-312)
         t_scale, t_factor = (temporal[0], temporal[1]) if temporal is not None else (None, 0.0)
-        _lib.call("ncf_gather_ln_gmf_scaled_fwd", ptr(uid), ptr(iid), n, ptr(tb["mf_user"]),
-                  ptr(tb["mf_item"]), ptr(tb["mlp_user"]), ptr(tb["mlp_item"]), n_users,
-                  n_items, D, ptr(m.mf_norm.weight), ptr(m.mf_norm.bias),
-                  ptr(m.mlp_norm.weight), ptr(m.mlp_norm.bias), ptr(m.mf_output.weight),
-                  ptr(m.mf_output.bias), LN_EPS, ptr(t_scale), float(t_factor), ptr(w.mf_pred),
+        _lib.call("ncf_gather_ln_gmf_scaled_fwd", ptr(uid), ptr(iid), n, *tbp, n_users,
+                  n_items, D, pp["mf_norm.weight"], pp["mf_norm.bias"],
+                  pp["mlp_norm.weight"], pp["mlp_norm.bias"], pp["mf_output.weight"],
+                  pp["mf_output.bias"], LN_EPS, ptr(t_scale), float(t_factor), ptr(w.mf_pred),
                   ptr(w.xu), ptr(w.xi), ptr(w.umf), ptr(w.imf), ptr(w.err), st)
         # a5: MultiHeadAttention over each group of M rows (architecture.py:315-326)
         att = m.user_product_attention
         if temporal is None and self.attn_block(D, H, M):
             # projections + core + out_proj in one launch (attn_block.hip)
             core = train or M != 1
+            a_ = "user_product_attention."
             _lib.call("ncf_attn_block_fwd", ptr(w.xu), ptr(w.xi), n // M, M, H, D,
-                      ptr(att.q_proj.weight), ptr(att.q_proj.bias), ptr(att.k_proj.weight),
-                      ptr(att.k_proj.bias), ptr(att.v_proj.weight), ptr(att.v_proj.bias),
-                      ptr(att.out_proj.weight), ptr(att.out_proj.bias),
+                      pp[a_ + "q_proj.weight"], pp[a_ + "q_proj.bias"], pp[a_ + "k_proj.weight"],
+                      pp[a_ + "k_proj.bias"], pp[a_ + "v_proj.weight"], pp[a_ + "v_proj.bias"],
+                      pp[a_ + "out_proj.weight"], pp[a_ + "out_proj.bias"],
                       drop_p if train else 0.0, seed, ptr(self.clock),
                       ptr(w.q) if core else None, ptr(w.k) if core else None,
                       ptr(w.v) if core else None, ptr(w.P) if core else None,
@@ -372,9 +412,9 @@ class NCFEngine:
             # a7 + a8: the whole tower and the head in one launch (mlp_tower.hip)
             _, addr, _, haddr = self._mlp_layers(w, train, bwd=False)
             _lib.call("ncf_mlp_fwd", ptr(x), n, D, addr, len(hid), haddr, LN_EPS,
-                      drop_p if train else 0.0, seed, ptr(self.clock), ptr(m.mlp_output.weight),
-                      ptr(m.mlp_output.bias), ptr(w.mf_pred), ptr(m.final[0].weight),
-                      ptr(m.final[0].bias), ptr(w.mlp_pred), ptr(w.prob), st)
+                      drop_p if train else 0.0, seed, ptr(self.clock), pp["mlp_output.weight"],
+                      pp["mlp_output.bias"], ptr(w.mf_pred), pp["final.0.weight"],
+                      pp["final.0.bias"], ptr(w.mlp_pred), ptr(w.prob), st)
             return w
         for l, h in enumerate(hid):
             lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
@@ -542,7 +582,16 @@ class NCFEngine:
             _lib.call("ncf_mlp_bwd", None, n, D, ptr(w.y), addr, len(hid), haddr, drop_p, seed,
                       ptr(self.clock), ctypes.addressof(h), ptr(w.dy), ptr(w.site("mlp")),
                       w.site("mlp").numel(), w.red_list.address, st)
-        for l in reversed(range(len(hid))):
+        fused_all = fused and self.mlp_fused_wgrad()
+        if fused_all and self._zero_cols_of is not self.flat_grad:
+            # gradient columns of mlp.0 that see the all-zero temporal input: exactly 0, and no
+            # kernel ever writes them — zero once per gradient buffer
+            ldw = m.mlp[0].weight.shape[1]
+            if ldw > D:
+                _lib.call("ncf_fill_2d", ptr(gv("mlp.0.weight")[:, D:]), hid[0], ldw - D, ldw,
+                          0.0, st)
+            self._zero_cols_of = self.flat_grad
+        for l in (() if fused_all else reversed(range(len(hid)))):
             h = hid[l]
             lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
             if not fused:
@@ -571,7 +620,7 @@ class NCFEngine:
                 dx = w.dy if l == 0 else w.da[l - 1]
                 self._gemm(w.dlin[l], h, 0, lin.weight, ldw, 0, dx, kin, n, kin, h, st=st)
         # a5 backward: out_proj, core, q/k/v projections
-        att = m.user_product_attention
+        pp = self.pp()
         if self.attn_block(D, H, M):
             # core + projections backward and the four Linear gradients in one launch
             gp = w.cache.get("attn_grads")
@@ -583,14 +632,16 @@ class NCFEngine:
                 gp = w.cache["attn_grads"] = (arr, ctypes.addressof(arr))
             ws = w.site("attn")
             _lib.call("ncf_attn_block_bwd", ptr(w.dy), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P),
-                      n // M, M, H, D, ptr(att.q_proj.weight), ptr(att.k_proj.weight),
-                      ptr(att.v_proj.weight), ptr(att.out_proj.weight), drop_p, seed,
+                      n // M, M, H, D, *pp["att_w"], drop_p, seed,
                       ptr(self.clock), ptr(w.o), ptr(w.xu), ptr(w.xi), gp[1], ptr(ws), ws.numel(),
                       w.red_list.address, None, None, None, ptr(w.dxu), ptr(w.dxi), st)
         else:
             self._attention_bwd_unfused(w, drop_p, seed, joins, st)
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)
-        tb = tables or self.table_params()
+        if tables is None:
+            tbp = (pp["t_mf_user"], pp["t_mlp_user"], pp["t_mf_item"], pp["t_mlp_item"])
+        else:
+            tbp = tuple(_tptr(tables[k]) for k in ("mf_user", "mlp_user", "mf_item", "mlp_item"))
         G = w.G
         uq_u, uq_i = uniq if uniq is not None else (w.uniq_u, w.uniq_i)
         d_rows = rows or (m.num_users, m.num_products)
@@ -599,12 +650,11 @@ class NCFEngine:
                       ptr(w.uniq_u), ptr(w.uniq_i), ptr(self.slot_u), ptr(self.slot_i),
                       ptr(w.num_unique), ptr(w.emb_ws), w.emb_ws.numel(), st)
         _lib.call("ncf_embedding_bwd_reduce", n, D, d_rows[0], d_rows[1],
-                  ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), ptr(tb["mf_user"]),
-                  ptr(tb["mlp_user"]), ptr(tb["mf_item"]), ptr(tb["mlp_item"]),
-                  ptr(m.mf_norm.weight), ptr(m.mlp_norm.weight), LN_EPS, ptr(G["mf_user"]),
+                  ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), *tbp,
+                  pp["mf_norm.weight"], pp["mlp_norm.weight"], LN_EPS, ptr(G["mf_user"]),
                   ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(uq_u),
-                  ptr(uq_i), ptr(gv("mf_norm.weight")), ptr(gv("mf_norm.bias")),
-                  ptr(gv("mlp_norm.weight")), ptr(gv("mlp_norm.bias")), ptr(w.emb_ws),
+                  ptr(uq_i), self.gptr("mf_norm.weight"), self.gptr("mf_norm.bias"),
+                  self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
                   w.emb_ws.numel(), w.red_list.address, st)
         self.join(dev, joins)
         w.run_reductions(st)

@@ -58,64 +58,93 @@ class TorchShardOps:
         self.dense_names = [k for k in self.names if k not in TABLES.values()]
         self.opt = O.AdamState(lr=1e-3, weight_decay=1e-5)
 
-    def dedup(self, uid, iid):
-        uu, iu = torch.unique(uid, return_inverse=True)
-        ui, ii = torch.unique(iid, return_inverse=True)
-        return {"uniq": (uu, ui), "inv": (iu, ii), "n": uid.numel()}
+    def mark_entry(self):
+        pass
 
-    def bucket(self, ded, world):
+    def begin(self, plan):
+        pass
+
+    def plan(self, uid, iid, world):
+        """Keys (id mod W) * R + id div W, deduplicated: compact order = owner order; the send
+        buffer is destination-major (per destination: its user rows, then its item rows)."""
         from ncf_amd.distributed import Plan
-        send, perm, counts = [], [], []
-        for uq in ded["uniq"]:
-            owner = uq % world
-            order = torch.sort(owner, stable=True).indices
-            send.append(uq[order])
-            perm.append(order)
-            counts.append(torch.bincount(owner, minlength=world).tolist())
-        return Plan(send=send, perm=perm, counts=counts)
+        W = world
+        uniq, inv, local, owner = [], [], [], []
+        for ids, rows in ((uid, U), (iid, I)):
+            R = -(-rows // W)
+            keys = (ids % W) * R + ids // W
+            uq, iv = torch.unique(keys, return_inverse=True)
+            uniq.append(uq)
+            inv.append(iv)
+            owner.append(uq // R)
+            local.append(uq % R)
+        counts = [[int((owner[k] == d).sum()) for k in (0, 1)] for d in range(W)]
+        send, spos = [], [torch.empty(len(uniq[0]), dtype=torch.long),
+                          torch.empty(len(uniq[1]), dtype=torch.long)]
+        off = 0
+        for d in range(W):
+            for k in (0, 1):
+                sel = (owner[k] == d).nonzero().reshape(-1)
+                spos[k][sel] = torch.arange(off, off + len(sel))
+                send.append(local[k][sel])
+                off += len(sel)
+        return Plan(send=torch.cat(send), counts=counts,
+                    extra={"inv": inv, "spos": spos, "n": uid.numel()})
 
-    def owner_prepare(self, recv):
-        return {"local": [r // self.W for r in recv]}
+    def owner_prepare(self, recv, plan):
+        kind = torch.empty(len(recv), dtype=torch.long)
+        src = torch.empty(len(recv), dtype=torch.long)
+        off = 0
+        for s_, (a, b) in enumerate(plan.recv_counts):
+            kind[off:off + a], kind[off + a:off + a + b] = 0, 1
+            src[off:off + a + b] = s_
+            off += a + b
+        return {"kind": kind, "src": src, "rows": recv.long()}
 
-    def owner_gather(self, own, k, recv_ids):
-        a, b = (TABLES["mf_user"], TABLES["mlp_user"]) if k == 0 else (TABLES["mf_item"], TABLES["mlp_item"])
-        loc = own["local"][k]
-        return torch.cat([self.p[a][loc], self.p[b][loc]], 1)
-
-    def compute(self, ded, plan, back, uid, iid, targets, loss_denominator):
-        O = self.O
-        leaves = {}
+    def owner_gather(self, own, recv):
+        out = torch.empty(len(recv), 2 * D)
         for k, (a, b) in enumerate(((TABLES["mf_user"], TABLES["mlp_user"]),
                                     (TABLES["mf_item"], TABLES["mlp_item"]))):
-            c = len(ded["uniq"][k])
-            ma, mb = torch.empty(c, D), torch.empty(c, D)
-            ma[plan.perm[k]] = back[k][:, :D]
-            mb[plan.perm[k]] = back[k][:, D:]
-            leaves[a], leaves[b] = ma.requires_grad_(True), mb.requires_grad_(True)
+            sel = own["kind"] == k
+            loc = own["rows"][sel]
+            out[sel] = torch.cat([self.p[a][loc], self.p[b][loc]], 1)
+        return out
+
+    def compute(self, plan, back, uid, iid, targets, loss_denominator):
+        O = self.O
+        leaves = {}
+        spos = plan.extra["spos"]
+        for k, (a, b) in enumerate(((TABLES["mf_user"], TABLES["mlp_user"]),
+                                    (TABLES["mf_item"], TABLES["mlp_item"]))):
+            rows = back[spos[k]]
+            leaves[a] = rows[:, :D].clone().requires_grad_(True)
+            leaves[b] = rows[:, D:].clone().requires_grad_(True)
         for k in self.dense_names:
             leaves[k] = self.p[k].clone().requires_grad_(True)
         full = dict(self.p)
         full.update(leaves)
-        inv_u, inv_i = ded["inv"]
+        inv_u, inv_i = plan.extra["inv"]
         prob = O.forward(full, inv_u, inv_i, training=True, negative_samples=M - 1, num_heads=H,
                          temporal_dim=T, n_layers=len(HID))
-        loss = O.bce_loss(prob, targets) * (ded["n"] / loss_denominator)
+        loss = O.bce_loss(prob, targets) * (plan.extra["n"] / loss_denominator)
         keys = list(leaves)
         gr = dict(zip(keys, torch.autograd.grad(loss, [leaves[k] for k in keys])))
         self.dgrad = torch.cat([gr[k].reshape(-1) for k in self.dense_names])
-        out = []
+        out = torch.empty(len(spos[0]) + len(spos[1]), 2 * D)
         for k, (a, b) in enumerate(((TABLES["mf_user"], TABLES["mlp_user"]),
                                     (TABLES["mf_item"], TABLES["mlp_item"]))):
-            out.append(torch.cat([gr[a][plan.perm[k]], gr[b][plan.perm[k]]], 1))
+            out[spos[k]] = torch.cat([gr[a], gr[b]], 1)
         return out, loss.detach()
 
     def owner_apply(self, own, got):
+        """Per-row sums in source-rank order (the received order is rank-major)."""
         self.tgrad = {}
         for k, (a, b) in enumerate(((TABLES["mf_user"], TABLES["mlp_user"]),
                                     (TABLES["mf_item"], TABLES["mlp_item"]))):
+            sel = own["kind"] == k
             ga, gb = torch.zeros_like(self.p[a]), torch.zeros_like(self.p[b])
-            ga.index_add_(0, own["local"][k], got[k][:, :D])
-            gb.index_add_(0, own["local"][k], got[k][:, D:])
+            ga.index_add_(0, own["rows"][sel], got[sel][:, :D])
+            gb.index_add_(0, own["rows"][sel], got[sel][:, D:])
             self.tgrad[a], self.tgrad[b] = ga, gb
 
     def dense_grad(self):
@@ -141,11 +170,13 @@ def _worker(rank, world, port, out_dir):
     from ncf_amd.distributed import ShardExchange, ShardedTrainStep
     params, batches = global_setup()
     ops = TorchShardOps(params, rank, world)
-    step = ShardedTrainStep(ops, ShardExchange(None, torch.device("cpu")))
+    plan_group = dist.new_group(list(range(world)))      # the plan's own communicator
+    step = ShardedTrainStep(ops, ShardExchange(None, torch.device("cpu"), plan_group))
     losses = []
     for s in range(len(batches)):
         u, i, t = batches[s][rank]
-        losses.append(float(step(u, i, t)))
+        nxt = batches[s + 1][rank][:2] if s + 1 < len(batches) else None   # pipelined plan
+        losses.append(float(step(u, i, t, next=nxt)))
     torch.save({"p": ops.p, "losses": losses}, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()

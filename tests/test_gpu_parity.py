@@ -653,15 +653,20 @@ def test_sharded_step_world1_bitwise_equals_fused():
         mf = factory(U, I)
         fused = FusedTrainStep(mf, lr=1e-3, weight_decay=1e-5)
         g = torch.Generator().manual_seed(6)
-        for _ in range(5):
+        batches = []
+        for _ in range(6):
             u = torch.randint(0, U, (Bg,), generator=g).repeat_interleave(5).to(DEV)
             i = (torch.rand(Bg * 5, generator=g) ** 3 * I).long().to(DEV)
             t = torch.zeros(Bg, 5)
             t[:, 0] = 1
-            t = t.reshape(-1, 1).to(DEV)
-            l1 = sharded(u, i, t)
+            batches.append((u, i, t.reshape(-1, 1).to(DEV)))
+        for s, (u, i, t) in enumerate(batches):
+            # steps 1-4 plan their successor ahead (pipelined); steps 0 and 5 plan inline
+            nxt = batches[s + 1][:2] if 1 <= s < len(batches) - 1 else None
+            l1 = sharded(u, i, t, next=nxt)
             fused(u, i, t)
             assert abs(float(l1.item()) - float(fused.last_loss.item())) < 1e-6
+        sharded.ops.check()
         a, b = ms.state_dict(), mf.state_dict()
         for k in a:
             assert torch.equal(a[k], b[k]), k
