@@ -1149,3 +1149,142 @@ def test_f8_device_sampler_matches_reference_draws(f8):
         pool = (a * neg.size + cnt) / (neg.size + n2)
         sig = np.sqrt(np.maximum(pool * (1 - pool), 1e-12) * (1 / neg.size + 1 / n2))
         assert np.all(np.abs(a - b) <= 6 * sig + 1e-9), (u, np.max(np.abs(a - b) / (sig + 1e-12)))
+
+
+@pytest.mark.parametrize("W,D", [(3, 64), (2, 16), (8, 32)])
+def test_shard_exchange_kernels_emulated_ranks(W, D):
+    """The row-sharded step's exchange kernels (exchange.hip) for W ranks emulated on one GPU:
+    plan (owner-ordered keys, counts, destination-major send layout, spos, inverse), the
+    all-to-all emulated by slicing, owner-side sort-free dedup (unique rows, pos table), owner
+    gather, rank-ordered gradient sums (bitwise vs a sequential fp32 sum), rows in/out."""
+    from ncf_amd import _lib
+    U, I, n = 1000, 300, 60
+    Ru, Ri = -(-U // W), -(-I // W)
+    g = torch.Generator().manual_seed(W * 100 + D)
+    i64 = dict(dtype=torch.int64, device=DEV)
+    i32 = dict(dtype=torch.int32, device=DEV)
+    err = torch.zeros(1, **i32)
+    plans = []
+    for r in range(W):
+        uid = torch.randint(0, U, (n,), generator=g)
+        iid = (torch.rand(n, generator=g) ** 2 * I).long()
+        bufs = dict(keys=[torch.empty(n, **i64) for _ in range(2)],
+                    uniq=[torch.empty(n, **i64) for _ in range(2)],
+                    nu=torch.zeros(2, **i32), inv=[torch.empty(n, **i64) for _ in range(2)],
+                    counts=torch.zeros(W, 2, **i64), send=torch.empty(2 * n, **i32),
+                    spos=[torch.empty(n, **i32) for _ in range(2)],
+                    bounds=torch.empty(3 * (W + 1), **i32),
+                    ws=torch.empty(_lib.query("ncf_embedding_bwd_workspace", n, D),
+                                   dtype=torch.uint8, device=DEV))
+        o = _lib.ShardPlanOut()
+        o.keys0, o.keys1 = bufs["keys"][0].data_ptr(), bufs["keys"][1].data_ptr()
+        o.uniq0, o.uniq1 = bufs["uniq"][0].data_ptr(), bufs["uniq"][1].data_ptr()
+        o.num_unique = bufs["nu"].data_ptr()
+        o.inv0, o.inv1 = bufs["inv"][0].data_ptr(), bufs["inv"][1].data_ptr()
+        o.counts, o.send = bufs["counts"].data_ptr(), bufs["send"].data_ptr()
+        o.spos0, o.spos1 = bufs["spos"][0].data_ptr(), bufs["spos"][1].data_ptr()
+        o.bounds = bufs["bounds"].data_ptr()
+        ud, idv = uid.to(DEV), iid.to(DEV)      # kept alive until the kernels ran
+        _lib.call("ncf_shard_plan", ud.data_ptr(), idv.data_ptr(), n, W, U, I, D,
+                  ctypes.addressof(o), bufs["ws"].data_ptr(), bufs["ws"].numel(),
+                  err.data_ptr(), None)
+        torch.cuda.synchronize()
+        # reference plan
+        counts = bufs["counts"].cpu()
+        send = bufs["send"].cpu()
+        layout_off = [0]
+        for d in range(W):
+            layout_off.append(layout_off[-1] + int(counts[d].sum()))
+        for k, (ids, R) in enumerate(((uid, Ru), (iid, Ri))):
+            keys = (ids % W) * R + ids // W
+            uq, inv = torch.unique(keys, return_inverse=True)
+            c = int(bufs["nu"][k])
+            assert c == len(uq)
+            assert torch.equal(bufs["uniq"][k][:c].cpu(), uq)
+            assert torch.equal(bufs["inv"][k].cpu(), inv)
+            own = uq // R
+            assert counts[:, k].tolist() == torch.bincount(own, minlength=W).tolist()
+            sp = bufs["spos"][k][:c].cpu().long()
+            assert torch.equal(send[sp], (uq % R).int())
+            for d in range(W):                      # destination-major, users before items
+                sel = sp[own == d]
+                base = layout_off[d] + (0 if k == 0 else int(counts[d][0]))
+                assert torch.equal(sel, torch.arange(base, base + len(sel)))
+        plans.append(dict(bufs=bufs, counts=counts, send=send, off=layout_off, uid=uid, iid=iid))
+    assert int(err) == 0
+    # owners: emulated all-to-all + sort-free dedup + gather + gradient sums
+    tables = [torch.randn(Ru, D, generator=g).to(DEV), torch.randn(Ru, D, generator=g).to(DEV),
+              torch.randn(Ri, D, generator=g).to(DEV), torch.randn(Ri, D, generator=g).to(DEV)]
+    mark = [torch.zeros(Ru, **i32), torch.zeros(Ri, **i32)]
+    uidx = [torch.zeros(Ru, **i32), torch.zeros(Ri, **i32)]
+    for token, o_ in enumerate(range(W), start=1):
+        parts, L = [], _lib.ShardRecv()
+        L.world, off = W, 0
+        for s in range(W):
+            p = plans[s]
+            parts.append(p["send"][p["off"][o_]:p["off"][o_ + 1]])
+            L.start[s], L.n0[s] = off, int(p["counts"][o_][0])
+            off += len(parts[-1])
+        L.start[W] = off
+        recv = torch.cat(parts).to(DEV)
+        tot = off
+        uq = [torch.empty(max(tot, 1), **i64) for _ in range(2)]
+        pos = [torch.empty(max(tot, 1) * W, **i32) for _ in range(2)]
+        cnt = torch.zeros(2, **i32)
+        _lib.call("ncf_shard_owner_prepare", recv.data_ptr(), ctypes.addressof(L), token,
+                  mark[0].data_ptr(), mark[1].data_ptr(), uidx[0].data_ptr(), uidx[1].data_ptr(),
+                  Ru, Ri, uq[0].data_ptr(), uq[1].data_ptr(), cnt.data_ptr(), pos[0].data_ptr(),
+                  pos[1].data_ptr(), err.data_ptr(), None)
+        rows = torch.empty(max(tot, 1), 2 * D, device=DEV)
+        _lib.call("ncf_shard_owner_gather", recv.data_ptr(), ctypes.addressof(L),
+                  tables[0].data_ptr(), tables[1].data_ptr(), Ru, tables[2].data_ptr(),
+                  tables[3].data_ptr(), Ri, D, rows.data_ptr(), None)
+        got = torch.randn(max(tot, 1), 2 * D, generator=g).to(DEV)
+        G = [torch.empty(max(tot, 1), D, device=DEV) for _ in range(4)]
+        _lib.call("ncf_shard_owner_gradsum", got.data_ptr(), pos[0].data_ptr(), pos[1].data_ptr(),
+                  cnt.data_ptr(), tot, W, D, G[0].data_ptr(), G[1].data_ptr(), G[2].data_ptr(),
+                  G[3].data_ptr(), None)
+        torch.cuda.synchronize()
+        rc, gc = recv.cpu().long(), got.cpu()
+        kind = torch.zeros(tot, dtype=torch.long)
+        src = torch.zeros(tot, dtype=torch.long)
+        for s in range(W):
+            kind[L.start[s] + L.n0[s]:L.start[s + 1]] = 1
+            src[L.start[s]:L.start[s + 1]] = s
+        for k in (0, 1):
+            sel = (kind == k).nonzero().reshape(-1)
+            c = int(cnt[k])
+            urows = uq[k][:c].cpu()
+            assert sorted(urows.tolist()) == sorted(set(rc[sel].tolist()))
+            P = pos[k][:c * W].cpu().view(c, W)
+            for u, row in enumerate(urows.tolist()):
+                for s in range(W):
+                    hit = sel[(rc[sel] == row) & (src[sel] == s)]
+                    assert P[u, s] == (int(hit[0]) if len(hit) else -1)
+                acc = torch.zeros(2 * D)
+                for s in range(W):                   # rank order, sequential fp32
+                    if P[u, s] >= 0:
+                        acc = acc + gc[int(P[u, s])]
+                assert torch.equal(G[2 * k][u].cpu(), acc[:D])
+                assert torch.equal(G[2 * k + 1][u].cpu(), acc[D:])
+            t0, t1 = tables[2 * k].cpu(), tables[2 * k + 1].cpu()
+            assert torch.equal(rows[sel].cpu(), torch.cat([t0[rc[sel]], t1[rc[sel]]], 1))
+    assert int(err) == 0
+    # requester rows in / gradients out
+    p = plans[0]
+    b = p["bufs"]
+    nmax = n
+    back = torch.randn(2 * n, 2 * D, generator=g).to(DEV)
+    mini = [torch.zeros(n, D, device=DEV) for _ in range(4)]
+    _lib.call("ncf_shard_rows", back.data_ptr(), b["spos"][0].data_ptr(), b["spos"][1].data_ptr(),
+              b["nu"].data_ptr(), nmax, D, *[m_.data_ptr() for m_ in mini], 0, None)
+    out = torch.zeros(2 * n, 2 * D, device=DEV)
+    _lib.call("ncf_shard_rows", out.data_ptr(), b["spos"][0].data_ptr(), b["spos"][1].data_ptr(),
+              b["nu"].data_ptr(), nmax, D, *[m_.data_ptr() for m_ in mini], 1, None)
+    torch.cuda.synchronize()
+    for k in (0, 1):
+        c = int(b["nu"][k])
+        sp = b["spos"][k][:c].long()
+        assert torch.equal(mini[2 * k][:c], back[sp, :D])
+        assert torch.equal(mini[2 * k + 1][:c], back[sp, D:])
+        assert torch.equal(out[sp], back[sp])
