@@ -31,7 +31,7 @@ _KINDS = (("user", "mf_user", "mlp_user"), ("item", "mf_item", "mlp_item"))
 
 class DeferredTableAdam:
     def __init__(self, engine, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
-                 sweep_every: int = 64, moments=None, clock=None):
+                 sweep_every: int = 64, moments=None, clock=None, overlap_sweep=None):
         self.engine = engine
         # clock (ncf_step_clock, device): every step-dependent value is read on the device, so
         # the launches of a step do not depend on the host counter (hipGraph capture)
@@ -50,6 +50,20 @@ class DeferredTableAdam:
         self._table = torch.zeros(0, dtype=torch.float32, device=dev)
         self._filled = 0
         self._lr_filled = None
+        # Overlapped rolling sweep (clock path, opt-in): the sweep closing step T is launched
+        # during step T+1, after its catch-up (right before its MLP tower), on a side stream, and
+        # joined before step T+1's table apply.  Rows of step T+1's batch are current by then
+        # (stamp >= T) and skipped; every other row of the slice is touched by the sweep alone.
+        # Same arithmetic, bit-identical results.  Off by default: measured on MI355X, the
+        # VALU-bound sweep slows the tower kernels it shares the CUs with by about as much as it
+        # hides (0.366 vs 0.361 ms/step single-GPU, 0.485 vs 0.46 row-sharded).
+        self.overlap = bool(overlap_sweep)
+        if self.overlap and clock is None:
+            raise ValueError("the overlapped sweep needs the device step clock")
+        self._owed = False        # a closed step whose rolling sweep has not been launched
+        self._side = None
+        self._ev = None
+        self._joined = True
         engine.deferred = self
 
     # ---- per-step scalar table (index 2s / 2s+1 = step s)
@@ -122,14 +136,14 @@ class DeferredTableAdam:
     def advance(self, st):
         """Close step self.t + 1 (after apply_rows of every kind), then the rolling sweep: one
         1/sweep_every slice of every table is brought current each step, so no row is ever more
-        than sweep_every steps behind and the catch-up work is spread evenly over the steps."""
+        than sweep_every steps behind and the catch-up work is spread evenly over the steps.
+        With the overlapped sweep it is only owed here and launched by the next sweep_fork."""
         self.t += 1
         self.engine.pending = None
-        if self.sweep_every and self.clock is not None:
-            pairs = self._pairs()
-            _lib.call("ncf_adam_pairs_sweep_rolling", ctypes.addressof(pairs), 2,
-                      self.engine.model.mlp_embedding_dim, self.sweep_every, 1, ptr(self.clock),
-                      ptr(self._table), *self._consts(), st)
+        if self.sweep_every and self.clock is not None and self.overlap:
+            self._owed = True
+        elif self.sweep_every and self.clock is not None:
+            self._rolling(st, 1)
         elif self.sweep_every:
             k = self.t % self.sweep_every
             for kind in ("user", "item"):
@@ -137,6 +151,47 @@ class DeferredTableAdam:
                 sl = (rows + self.sweep_every - 1) // self.sweep_every
                 r0 = k * sl
                 self._sweep_range(kind, r0, max(0, min(rows, r0 + sl) - r0), st)
+
+    def _rolling(self, st, step_rel):
+        """Rolling sweep closing step clock->t + step_rel (slice of that step)."""
+        pairs = self.__dict__.get("_sweep_pairs") or self.__dict__.setdefault("_sweep_pairs",
+                                                                               self._pairs())
+        _lib.call("ncf_adam_pairs_sweep_rolling", ctypes.addressof(pairs), 2,
+                  self.engine.model.mlp_embedding_dim, self.sweep_every, step_rel,
+                  ptr(self.clock), ptr(self._table), *self._consts(), st)
+
+    def sweep_fork(self):
+        """During step T+1 (clock->t = T, after its catch-up; the engine forks right before the
+        MLP tower): launch the owed sweep of step T on the side stream; it overlaps everything
+        the current stream does until sweep_join."""
+        if not self._owed:
+            return
+        dev = self.clock.device
+        if self._side is None:
+            self._side = torch.cuda.Stream(dev)
+            self._ev = (torch.cuda.Event(), torch.cuda.Event())
+        cur = torch.cuda.current_stream(dev)
+        self._ev[0].record(cur)
+        self._side.wait_event(self._ev[0])
+        with torch.cuda.stream(self._side):     # (so per-launch instrumentation times it there)
+            self._rolling(self._side.cuda_stream, 0)
+        self._ev[1].record(self._side)
+        self._owed, self._joined = False, False
+
+    def sweep_join(self):
+        """The current stream waits for the side-stream sweep (before the step's apply and the
+        clock advance that would change the sweep's target under it)."""
+        if not self._joined:
+            torch.cuda.current_stream(self.clock.device).wait_event(self._ev[1])
+            self._joined = True
+
+    def flush(self, st):
+        """Settle any owed / in-flight sweep on the current stream (before full sweeps or
+        anything that reads the tables from the host side)."""
+        self.sweep_join()
+        if self._owed:
+            self._rolling(st, 0)
+            self._owed = False
 
     def _pairs(self, w=None):
         """ncf_table_pair[2] (users, items) for the both-kinds launches of the clock path."""
@@ -175,6 +230,7 @@ class DeferredTableAdam:
         n = w.g.n
         if self.clock is not None:
             self._ensure(self.t + 1)
+            self.sweep_join()
             if n > 0:
                 pairs = self._pairs(w)
                 _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2,
@@ -195,6 +251,8 @@ class DeferredTableAdam:
                   ptr(self._table), *self._consts(), st)
 
     def _sweep(self, st):
+        if self.clock is not None:
+            self.flush(st)
         for kind in ("user", "item"):
             self._sweep_range(kind, 0, self.stamp[kind].numel(), st)
         self.synced_t = self.t

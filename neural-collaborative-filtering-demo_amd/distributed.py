@@ -377,6 +377,7 @@ class HipShardOps:
                   nmax, self.W, self.D, ptr(G[0]), ptr(G[1]), ptr(G[2]), ptr(G[3]), st)
         d = self.deferred
         d._ensure(d.t + 1)
+        d.sweep_join()
         if nmax > 0:
             pairs = self._pairs(uq, G)
             _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2, self.D,

@@ -374,7 +374,7 @@ class NCFEngine:
         else:
             tbp = tuple(_tptr(tables[k]) for k in ("mf_user", "mf_item", "mlp_user", "mlp_item"))
         n_users, n_items = rows or (m.num_users, m.num_products)
-        w.err.zero_()
+        # w.err is sticky (zeroed at creation and by check_ids): no per-step fill launch
         w.deduped = False
         if prepare is not None:
             prepare(w, uid, iid, st)
@@ -408,6 +408,10 @@ class NCFEngine:
             x, ldx, kin = w.y, D, D
         else:
             x, ldx, kin = self._attention_unfused(w, M, train, drop_p, seed, temporal, st)
+        if train and self.deferred is not None and self.deferred.overlap:
+            # the previous step's rolling table sweep (VALU-bound) runs on a side stream under
+            # the MFMA-bound tower forward/backward (joined before this step's table apply)
+            self.deferred.sweep_fork()
         if temporal is None and self.mlp_fused(D, hid):
             # a7 + a8: the whole tower and the head in one launch (mlp_tower.hip)
             _, addr, _, haddr = self._mlp_layers(w, train, bwd=False)
@@ -530,7 +534,10 @@ class NCFEngine:
         return x, ldx, kin
 
     def check_ids(self, w: Workspace):
+        """Raise IndexError if a forward on this workspace since the last check saw an
+        out-of-range id (the flag is sticky between checks; one host sync)."""
         if int(w.err.item()):
+            w.err.zero_()
             raise IndexError("AdvancedNCF: user/product id out of range of the embedding tables")
 
     # ------------------------------------------------------------------ backward

@@ -40,7 +40,8 @@ class FusedTrainStep:
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5,
                  deferred: bool = True, sweep_every: int = 64, graph: bool = False,
-                 clock: Optional[bool] = None, warmup: int = 2, concurrent: Optional[bool] = None):
+                 clock: Optional[bool] = None, warmup: int = 2, concurrent: Optional[bool] = None,
+                 overlap_sweep: bool = False):
         self.model = model
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.step_count = 0
@@ -71,7 +72,8 @@ class FusedTrainStep:
         if deferred:
             from .deferred import DeferredTableAdam
             self.deferred = DeferredTableAdam(eng, lr, betas, eps, weight_decay, sweep_every,
-                                              moments=self.state, clock=self.clock)
+                                              moments=self.state, clock=self.clock,
+                                              overlap_sweep=overlap_sweep and self.clock is not None)
         self.warmup = warmup
         # independent kernels on side streams.  Off by default: measured slower on MI355X, eager
         # (0.63 vs 0.54 ms) and captured (0.71 vs 0.58 ms) — a cross-queue dependency costs more

@@ -595,6 +595,18 @@ def test_clock_mode_bitwise_equals_dense():
         assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_overlapped_sweep_bitwise_equals_dense(graph):
+    """The opt-in overlapped rolling sweep (side stream under the tower, joined before the
+    apply) is bit-identical to the dense sweep, eager and hipGraph-captured."""
+    a_sd, a_m = _fused_run(False, 70)
+    b_sd, b_m = _fused_run(True, 70, clock=True, graph=graph, overlap_sweep=True)
+    for k in a_sd:
+        assert torch.equal(a_sd[k], b_sd[k]), k
+    for k in a_m:
+        assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
+
+
 def test_graph_replay_bitwise_equals_eager_clock():
     """hipGraph capture + replay of the whole training step (dropout on: the per-step stream
     comes from the device clock) == the same clock-driven steps run eagerly, bit for bit, across
