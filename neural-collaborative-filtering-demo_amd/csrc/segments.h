@@ -17,9 +17,12 @@ namespace ncf_seg {
 
 constexpr int TILE = 1024;        // keys per sort tile (256 threads x 4)
 constexpr int PIECE = 64;         // max occurrences one wave reduces in the embedding backward
-constexpr int MAX_BITS = 11;      // radix digit bits
+#ifndef NCF_RADIX_BITS
+#define NCF_RADIX_BITS 11
+#endif
+constexpr int MAX_BITS = NCF_RADIX_BITS;   // radix digit bits (at most)
 constexpr int MAXR = 1 << MAX_BITS;
-constexpr int MAXP = 3;           // passes for 32-bit keys
+constexpr int MAXP = (32 + MAX_BITS - 1) / MAX_BITS;   // passes for 32-bit keys
 constexpr uint32_t FIRST_PIECE = 1u << 31;
 
 struct WS {
