@@ -4,7 +4,7 @@ import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv"
 anchor = sys.argv[2] if len(sys.argv) > 2 else "k_gather_ln_gmf"
-rows = list(csv.DictReader(open(path)))
+rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(anchor)]
 a, b = idx[len(idx) // 2], idx[len(idx) // 2 + 1]
 tot = 0.0
