@@ -55,7 +55,10 @@ static inline int64_t extras_max(int64_t n) { return n / PIECE + 2; }
 static inline int nbr_of(int64_t n) {
   int64_t b = (pieces_max(n) + 3) / 4;  // 4 waves (pieces) per block
   if (b < 1) b = 1;
-  if (b > 2048) b = 2048;
+#ifndef NCF_PIECE_BLOCKS_MAX
+#define NCF_PIECE_BLOCKS_MAX 2048
+#endif
+  if (b > NCF_PIECE_BLOCKS_MAX) b = NCF_PIECE_BLOCKS_MAX;
   return (int)b;
 }
 

@@ -19,7 +19,8 @@ A step has a PLAN and a RUN:
            drive the backward's segment reduce)
         5. all_to_all of the compact row gradients to the owners, who sum them per row in
            rank order (deterministic) and apply the step; rolling sweep                [RCCL]
-        6. one all_reduce of the flat dense-gradient buffer, replicated dense Adam     [RCCL]
+        6. one all_reduce of the flat dense-gradient buffer (on the second communicator,
+           beside step 5), replicated dense Adam                                       [RCCL]
 The plan of step t+1 is pipelined under the run of step t (``step(u, i, t, next=(u', i'))``, the
 role of torchrec's TrainPipelineSparseDist): its kernels run on a side stream and its count
 exchange on a second communicator, so the host-side wait for the split sizes overlaps the GPU
@@ -98,6 +99,15 @@ class ShardExchange:
         dist.all_reduce(t, group=self.group)
         return t
 
+    def all_reduce_start(self, t: torch.Tensor):
+        """Start the dense-gradient all-reduce on the plan communicator: its RCCL kernel runs
+        beside the row-gradient all-to-all and the owners' table update on the main one."""
+        return dist.all_reduce(t, group=self.plan_group, async_op=True)
+
+    def all_reduce_wait(self, work):
+        if work is not None:
+            work.wait()
+
 
 @dataclass
 class Plan:
@@ -149,9 +159,10 @@ class ShardedTrainStep:
         back = X.exchange(rows, recv_splits, send_splits)
         grads, loss = ops.compute(plan, back, user_ids, item_ids, targets,
                                   loss_denominator=user_ids.numel() * X.world)
+        ar = X.all_reduce_start(ops.dense_grad())
         got = X.exchange(grads, send_splits, recv_splits)
         ops.owner_apply(own, got)
-        X.all_reduce_(ops.dense_grad())
+        X.all_reduce_wait(ar)
         ops.dense_step()
         return loss
 

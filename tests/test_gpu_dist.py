@@ -80,6 +80,10 @@ def _worker(rank, world, port, out_dir):
             t.copy_(h)
             return t
 
+        def all_reduce_start(self, t):
+            self.all_reduce_(t)
+            return None
+
     R = {"user": -(-U // world), "item": -(-I // world)}
     model = ncf.AdvancedNCF(R["user"], R["item"], 5, 24, D, D, T, HID, H, 0.0, M - 1)
     sd = dict(params)
