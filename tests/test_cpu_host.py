@@ -271,3 +271,18 @@ def test_struct_mirrors_match_header_layouts():
     body = hdr[hdr.index("typedef struct ncf_mlp_layer"):hdr.index("} ncf_mlp_layer;")]
     names = re.findall(r"\*?\s*(\w+);", body)
     assert names == [f[0] for f in _lib.MlpLayer._fields_]
+
+
+def test_shard_struct_mirrors_match_header():
+    """ctypes mirrors of ncf_shard_plan_out (12 pointers, header order) and ncf_shard_recv
+    (world, start[W_MAX + 1], n0[W_MAX] int32) as include/ncf_hip.h declares them."""
+    import ctypes
+    hdr = open(os.path.join(ROOT, "include", "ncf_hip.h")).read()
+    body = hdr[hdr.index("typedef struct ncf_shard_plan_out"):hdr.index("} ncf_shard_plan_out;")]
+    names = re.findall(r"\*\s*(\w+);", body)
+    assert names == [f[0] for f in _lib.ShardPlanOut._fields_]
+    assert ctypes.sizeof(_lib.ShardPlanOut) == 12 * 8
+    wmax = int(re.search(r"#define NCF_SHARD_MAX_WORLD (\d+)", hdr).group(1))
+    assert wmax == _lib.SHARD_MAX_WORLD
+    assert ctypes.sizeof(_lib.ShardRecv) == 4 * (1 + (wmax + 1) + wmax)
+    assert [f[0] for f in _lib.ShardRecv._fields_] == ["world", "start", "n0"]
