@@ -101,22 +101,22 @@ __device__ __forceinline__ f32x4 mfma4(float4 a, float4 b, f32x4 acc) {
 // NS >= 8 wave w takes slices w + 8j for all 5 row tiles, with NS < 8 (N = 64) slice w % NS for
 // the row tiles rt = w / NS + S r (S = 8 / NS).  A wave loads each weight chunk once and feeds
 // it to all its row tiles (independent MFMA chains): 5 x reuse of every weight byte from L2.
-template <int N>
+template <int N, int RT = kRT>
 struct Split {
   static constexpr int NS = N / 16;
   static constexpr int S = NS >= kWaves ? 1 : kWaves / NS;
   static constexpr int CPW = NS >= kWaves ? NS / kWaves : 1;   // column slices per wave
-  static constexpr int RPW = (kRT + S - 1) / S;                 // row tiles per wave (max)
+  static constexpr int RPW = (RT + S - 1) / S;                  // row tiles per wave (max)
   __device__ static int cs(int w, int j) { return NS >= kWaves ? w + kWaves * j : w % NS; }
   __device__ static int rt(int w, int r) { return NS >= kWaves ? r : w / NS + S * r; }
 };
 
 // Y[80 x N] = relu(X[80 x K] . W^T + b)   (W row-major [N][ldw], first K columns)
-template <int K, int N, int PX, int PY>
+template <int K, int N, int PX, int PY, int RT = kRT>
 __device__ __forceinline__ void lin_fwd(const float* __restrict__ X, float* __restrict__ Y,
                                         const float* __restrict__ W, int64_t ldw,
                                         const float* __restrict__ bias) {
-  using Sp = Split<N>;
+  using Sp = Split<N, RT>;
   constexpr int KQ = K / 4;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
 #pragma unroll
@@ -132,14 +132,14 @@ __device__ __forceinline__ void lin_fwd(const float* __restrict__ X, float* __re
 #pragma unroll
       for (int r = 0; r < Sp::RPW; ++r) {
         const int rt = Sp::rt(w, r);
-        if (rt < kRT) acc[r] = mfma4(lds4(X + (16 * rt + i) * PX + g * KQ + 4 * c), b, acc[r]);
+        if (rt < RT) acc[r] = mfma4(lds4(X + (16 * rt + i) * PX + g * KQ + 4 * c), b, acc[r]);
       }
     }
     const float bb = bias[16 * cs + i];
 #pragma unroll
     for (int r = 0; r < Sp::RPW; ++r) {
       const int rt = Sp::rt(w, r);
-      if (rt < kRT) {
+      if (rt < RT) {
         float* yp = Y + (16 * rt + 4 * g) * PY + 16 * cs + i;   // C: rows 4g + e, column 16cs + i
 #pragma unroll
         for (int e = 0; e < 4; ++e) yp[e * PY] = fmaxf(acc[r][e] + bb, 0.0f);
@@ -197,7 +197,7 @@ __device__ __forceinline__ void lin_bwd(const float* __restrict__ DL, float* __r
 // LayerNorm + dropout of the ReLU rows in Y, in place (the next layer's input); saves r, a,
 // mean, rstd.  16 lanes per row, kPasses passes over the 80 rows.  With hw != NULL, also the
 // head: mlp_pred = a . hw + b_out, prob = sigmoid(w0 mf_pred + w1 mlp_pred + b_fin).
-template <int N, int PY>
+template <int N, int PY, int RT = kRT>
 __device__ __forceinline__ void ln_fwd(float* __restrict__ Y, int64_t row0, int rows,
                                        const ncf_mlp_layer& L, float eps, float p, uint64_t seed,
                                        const float* __restrict__ hw, const float* __restrict__ b_out,
@@ -212,7 +212,7 @@ __device__ __forceinline__ void ln_fwd(float* __restrict__ Y, int64_t row0, int 
   // not depend on which pass (= its position in the tile, i.e. the batch) computes it; the
   // fused multiply-adds are explicit.
 #pragma clang fp contract(off)
-  constexpr int CH = N / 64, NP = kPasses;
+  constexpr int CH = N / 64, TR = 16 * RT, NP = (TR * 16 + kThreads - 1) / kThreads;
   const int sub = threadIdx.x & 15;
   const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   float4 x[NP][CH];
@@ -224,7 +224,7 @@ __device__ __forceinline__ void ln_fwd(float* __restrict__ Y, int64_t row0, int 
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int col = (c * 16 + sub) * 4;
-      x[q][c] = rr < kRows ? lds4(Y + rr * PY + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      x[q][c] = rr < TR ? lds4(Y + rr * PY + col) : make_float4(0.f, 0.f, 0.f, 0.f);
       s[q] += x[q][c].x + x[q][c].y + x[q][c].z + x[q][c].w;
     }
   }
@@ -265,7 +265,7 @@ __device__ __forceinline__ void ln_fwd(float* __restrict__ Y, int64_t row0, int 
       const int col = (c * 16 + sub) * 4;
       const float4 y = drop4(ln_affine(x[q][c], rstd[q], ld4(L.gamma + col), ld4(L.beta + col)),
                              seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
-      if (rr < kRows) lds4_st(Y + rr * PY + col, y);
+      if (rr < TR) lds4_st(Y + rr * PY + col, y);
       if (ok && L.a) st4(L.a + row * N + col, y);
       if (hw) {
         const float4 h = ld4(hw + col);
@@ -389,38 +389,51 @@ __device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict_
   __syncthreads();
 }
 
+// The forward in workgroups of VR valid rows staged as RT 16-row MFMA tiles (the padding rows
+// are zeros and are never stored).  VR < 16 RT lets two workgroups share a CU (A/B knob).
+template <int RT, int VR>
 __global__ __launch_bounds__(kThreads) void k_mlp_fwd(
     const float* __restrict__ xin, int64_t n, TowerArgs a, float eps, float p,
     const ncf_step_clock* clock, const float* __restrict__ w_out, const float* __restrict__ b_out,
     const float* __restrict__ mf_pred, const float* __restrict__ w_fin,
     const float* __restrict__ b_fin, float* __restrict__ mlp_pred, float* __restrict__ prob) {
+  constexpr int TR = 16 * RT;
   extern __shared__ float lds[];
-  float* Q = lds;                  // [80][kPQ]: layer 0 out (256), layer 2 out (64)
-  float* P = lds + kRows * kPQ;    // [80][kPP]: input x (64), layer 1 out (128)
-  const int64_t row0 = (int64_t)blockIdx.x * kRows;
-  const int rows = (int)min<int64_t>(kRows, n - row0);
+  float* Q = lds;                  // [TR][kPQ]: layer 0 out (256), layer 2 out (64)
+  float* P = lds + TR * kPQ;       // [TR][kPP]: input x (64), layer 1 out (128)
+  const int64_t row0 = (int64_t)blockIdx.x * VR;
+  const int rows = (int)min<int64_t>(VR, n - row0);
   const uint64_t cs = clock ? clock->seed : 0ull;
-  for (int e = threadIdx.x; e < kRows * (K0 / 4); e += kThreads) {
+  for (int e = threadIdx.x; e < TR * (K0 / 4); e += kThreads) {
     const int r = e / (K0 / 4), c = (e % (K0 / 4)) * 4;
     lds4_st(P + r * kPP + c,
             r < rows ? ld4(xin + (row0 + r) * K0 + c) : make_float4(0.f, 0.f, 0.f, 0.f));
   }
   __syncthreads();
-  lin_fwd<K0, N0, kPP, kPQ>(P, Q, a.l[0].w, a.l[0].ldw, a.l[0].b);
+  lin_fwd<K0, N0, kPP, kPQ, RT>(P, Q, a.l[0].w, a.l[0].ldw, a.l[0].b);
   __syncthreads();
-  ln_fwd<N0, kPQ>(Q, row0, rows, a.l[0], eps, p, a.seed[0] + cs, nullptr, nullptr, nullptr,
-                  nullptr, nullptr, nullptr, nullptr);
+  ln_fwd<N0, kPQ, RT>(Q, row0, rows, a.l[0], eps, p, a.seed[0] + cs, nullptr, nullptr, nullptr,
+                      nullptr, nullptr, nullptr, nullptr);
   __syncthreads();
-  lin_fwd<N0, N1, kPQ, kPP>(Q, P, a.l[1].w, a.l[1].ldw, a.l[1].b);
+  lin_fwd<N0, N1, kPQ, kPP, RT>(Q, P, a.l[1].w, a.l[1].ldw, a.l[1].b);
   __syncthreads();
-  ln_fwd<N1, kPP>(P, row0, rows, a.l[1], eps, p, a.seed[1] + cs, nullptr, nullptr, nullptr,
-                  nullptr, nullptr, nullptr, nullptr);
+  ln_fwd<N1, kPP, RT>(P, row0, rows, a.l[1], eps, p, a.seed[1] + cs, nullptr, nullptr, nullptr,
+                      nullptr, nullptr, nullptr, nullptr);
   __syncthreads();
-  lin_fwd<N1, N2, kPP, kPQ>(P, Q, a.l[2].w, a.l[2].ldw, a.l[2].b);
+  lin_fwd<N1, N2, kPP, kPQ, RT>(P, Q, a.l[2].w, a.l[2].ldw, a.l[2].b);
   __syncthreads();
-  ln_fwd<N2, kPQ>(Q, row0, rows, a.l[2], eps, p, a.seed[2] + cs, w_out, b_out, mf_pred, w_fin,
-                  b_fin, mlp_pred, prob);
+  ln_fwd<N2, kPQ, RT>(Q, row0, rows, a.l[2], eps, p, a.seed[2] + cs, w_out, b_out, mf_pred, w_fin,
+                      b_fin, mlp_pred, prob);
 }
+
+#ifndef NCF_FWD_RT
+#define NCF_FWD_RT 5
+#endif
+#ifndef NCF_FWD_VR
+#define NCF_FWD_VR 80
+#endif
+constexpr int kFwdRT = NCF_FWD_RT, kFwdVR = NCF_FWD_VR;
+static_assert(kFwdVR <= 16 * kFwdRT, "forward rows per workgroup exceed its tiles");
 
 // Weight gradient of one Linear over this workgroup's 80 rows: out[n][k] = sum_r dlin[r][n] X[r][k]
 // (the partial of this workgroup; one deferred reduction sums the 256 partial rows).  16x16
@@ -620,6 +633,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
 }
 
 constexpr size_t kLds = sizeof(float) * kRows * (kPQ + kPP);
+constexpr size_t kLdsFwd = sizeof(float) * 16 * kFwdRT * (kPQ + kPP);
 static_assert(kWaves * 3 * N0 <= kRows * kPP, "ln_bwd scratch must fit in buffer P");
 
 bool tower_ok(int64_t dim, int64_t n_layers, const int64_t* hidden) {
@@ -660,11 +674,12 @@ extern "C" int ncf_mlp_fwd(const float* x, int64_t n, int64_t dim, const ncf_mlp
   if (rc) return rc;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_mlp_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kLds);
+    (void)hipFuncSetAttribute((const void*)k_mlp_fwd<kFwdRT, kFwdVR>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsFwd);
     attr = true;
   }
-  hipLaunchKernelGGL(k_mlp_fwd, dim3((unsigned)ncf_cdiv(n, kRows)), dim3(kThreads), kLds,
+  hipLaunchKernelGGL((k_mlp_fwd<kFwdRT, kFwdVR>), dim3((unsigned)ncf_cdiv(n, kFwdVR)),
+                     dim3(kThreads), kLdsFwd,
                      (hipStream_t)stream, x, n, a, eps, dropout_p, clock, mlp_out_w, mlp_out_b,
                      mf_pred, final_w, final_b, mlp_pred, prob);
   NCF_CHECK_LAUNCH("ncf_mlp_fwd");
