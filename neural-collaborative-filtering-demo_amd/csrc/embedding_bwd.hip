@@ -26,8 +26,12 @@ using namespace ncf_seg;
 namespace {
 
 // part[kind*nbr + block][0:D mf_g | D:2D mf_b | 2D:3D mlp_g | 3D:4D mlp_b]
+#ifndef NCF_PIECE_WAVES
+#define NCF_PIECE_WAVES 4
+#endif
+constexpr int kPW = NCF_PIECE_WAVES;   // waves (pieces in flight) per block
 template <int D>
-__global__ __launch_bounds__(256) void k_piece_reduce_ln(
+__global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     const uint32_t* __restrict__ sv0, const uint32_t* __restrict__ sv1,
     const uint32_t* __restrict__ pstart0, const uint32_t* __restrict__ pstart1,
     const uint32_t* __restrict__ pseg0, const uint32_t* __restrict__ pseg1,
@@ -42,8 +46,8 @@ __global__ __launch_bounds__(256) void k_piece_reduce_ln(
     float* __restrict__ xp0, float* __restrict__ xp1, float* __restrict__ part) {
   constexpr int L = D / 4;
   constexpr int S = 64 / L;  // sub-groups per wave
-  __shared__ __attribute__((aligned(16))) float red[4][4 * D];
-  __shared__ uint32_t sidx[4][PIECE];
+  __shared__ __attribute__((aligned(16))) float red[kPW][4 * D];
+  __shared__ uint32_t sidx[kPW][PIECE];
   const int kind = blockIdx.y;
   const uint32_t* sv = kind ? sv1 : sv0;
   const uint32_t* pstart = kind ? pstart1 : pstart0;
@@ -62,7 +66,7 @@ __global__ __launch_bounds__(256) void k_piece_reduce_ln(
   const int64_t Pn = totals[2 + kind];
   const float4 gm = ld4(g_mf + col), gl = ld4(g_mlp + col);
   float4 a_gm = make_float4(0, 0, 0, 0), a_bm = a_gm, a_gl = a_gm, a_bl = a_gm;
-  for (int64_t p = (int64_t)blockIdx.x * 4 + w; p < Pn; p += (int64_t)gridDim.x * 4) {
+  for (int64_t p = (int64_t)blockIdx.x * kPW + w; p < Pn; p += (int64_t)gridDim.x * kPW) {
     // the piece record (independent loads), the table rows as soon as the row is known, then
     // the occurrence positions and their gradient rows
     const uint32_t ps = pstart[p];
@@ -140,8 +144,12 @@ __global__ __launch_bounds__(256) void k_piece_reduce_ln(
   }
   __syncthreads();
   float* out = part + ((int64_t)kind * gridDim.x + blockIdx.x) * 4 * D;
-  for (int i = threadIdx.x; i < 4 * D; i += 256)
-    out[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  for (int i = threadIdx.x; i < 4 * D; i += 64 * kPW) {
+    float a = 0.0f;
+#pragma unroll
+    for (int q = 0; q < kPW; ++q) a += red[q][i];
+    out[i] = a;
+  }
 }
 
 // G[c] += extra pieces of segment c (in piece order); L lanes per segment
@@ -197,7 +205,7 @@ int piece_reduce(const WS& w, int64_t n, const uint32_t* sv0, const uint32_t* sv
                  const float* tmf1, const float* tml1, const float* gmf, const float* gml,
                  float eps, float* Gmf0, float* Gml0, float* Gmf1, float* Gml1, float* dgm,
                  float* dbm, float* dgl, float* dbl, ncf_reduce_list* defer, hipStream_t st) {
-  hipLaunchKernelGGL(k_piece_reduce_ln<D>, dim3(w.nbr, 2), dim3(256), 0, st, sv0, sv1, w.pstart0,
+  hipLaunchKernelGGL(k_piece_reduce_ln<D>, dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1, w.pstart0,
                      w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
                      dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
                      Gmf1, Gml1, w.xp0, w.xp1, w.part);
