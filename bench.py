@@ -248,12 +248,16 @@ def main():
     batches = make_batches(U, I, B, M, 8, dev, seed=100 + rank)
     torch.cuda.synchronize()
 
+    # the single-GPU step sorts the next batch's ids on a side stream under the current step
+    # (FusedTrainStep(next=...)); the instrumented eager pass below does not
+    pipelined = not sharded and not args.graph and not args.no_clock
+
     def run_steps(fn, first, count):
         """count steps over the resident batches from index `first`; the row-sharded step plans
         the following batch under each step (pipelined input distribution)."""
         for s in range(first, first + count):
             u, i, t = batches[s % len(batches)]
-            if sharded:
+            if sharded or (pipelined and fn is step):
                 fn(u, i, t, next=batches[(s + 1) % len(batches)][:2])
             else:
                 fn(u, i, t)

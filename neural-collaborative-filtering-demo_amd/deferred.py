@@ -211,9 +211,11 @@ class DeferredTableAdam:
         eng = self.engine
         m = eng.model
         n = w.g.n
-        _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, w.g.D, m.num_users, m.num_products,
-                  ptr(w.uniq_u), ptr(w.uniq_i), None, None, ptr(w.num_unique), ptr(w.emb_ws),
-                  w.emb_ws.numel(), st)
+        if not getattr(w, "prededuped", None):   # else: sorted ahead on a side stream (trainer)
+            _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, w.g.D, m.num_users, m.num_products,
+                      ptr(w.uniq_u), ptr(w.uniq_i), None, None, ptr(w.num_unique), ptr(w.emb_ws),
+                      w.emb_ws.numel(), st)
+        w.prededuped = None
         w.deduped = True
         if self.clock is not None and n > 0:   # both kinds in one launch
             self._ensure(self.t + 1)

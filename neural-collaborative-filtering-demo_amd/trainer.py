@@ -113,11 +113,72 @@ class FusedTrainStep:
                       float(self.step_count + 1), st)
         return w
 
+    # ---- pipelined dedup: the id sort of step t+1 runs on a side stream under step t
+    def _dedup_sets(self, w):
+        """Two sets of the dedup outputs (sorted segments, unique ids, counts) for workspace w:
+        the workspace's own buffers and a twin, alternating between consecutive steps."""
+        sets = w.cache.get("dedup_sets")
+        if sets is None:
+            a = dict(emb_ws=w.emb_ws, uniq_u=w.uniq_u, uniq_i=w.uniq_i, num_unique=w.num_unique)
+            b = {k: torch.empty_like(v) for k, v in a.items()}
+            sets = w.cache["dedup_sets"] = [a, b, 0]
+        return sets
+
+    def _prefetch_dedup(self, w, uid, iid, entry):
+        """Dedup of the NEXT step's ids into the idle set, on the side stream, after `entry`
+        (the start of this step: the run that last used that set is complete there)."""
+        sets = self._dedup_sets(w)
+        s = sets[1 - sets[2]]
+        eng = self.model.engine
+        m = self.model
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(eng.flat.device)
+        side = self._side
+        side.wait_event(entry)
+        u = uid.reshape(-1)
+        i = iid.reshape(-1)
+        _lib.call("ncf_dedup_ids", ptr(u), ptr(i), u.numel(), w.g.D, m.num_users,
+                  m.num_products, ptr(s["uniq_u"]), ptr(s["uniq_i"]), None, None,
+                  ptr(s["num_unique"]), ptr(s["emb_ws"]), s["emb_ws"].numel(), side.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        self._pending = (uid, iid, ev)          # the caller's objects: matched by identity
+
+    def _activate_dedup(self, w, uid, iid):
+        """Point w at this step's dedup set: the prefetched one when it was made for these ids
+        (the step then waits for its event instead of sorting), else the next set, sorted
+        inline by the deferred Adam's prepare."""
+        sets = self._dedup_sets(w)
+        pend, self._pending = getattr(self, "_pending", None), None
+        sets[2] = 1 - sets[2]
+        s = sets[sets[2]]
+        w.emb_ws, w.uniq_u, w.uniq_i, w.num_unique = s["emb_ws"], s["uniq_u"], s["uniq_i"], s["num_unique"]
+        w.prededuped = None
+        if pend is not None:
+            cur = torch.cuda.current_stream(self.model.engine.flat.device)
+            cur.wait_event(pend[2])           # (also orders a stale prefetch before reuse)
+            if pend[0] is uid and pend[1] is iid:
+                w.prededuped = True
+
     def __call__(self, user_ids: torch.Tensor, item_ids: torch.Tensor, targets: torch.Tensor,
-                 M: Optional[int] = None):
+                 M: Optional[int] = None, next=None):
+        """One step.  ``next=(user_ids, item_ids)`` of the following step lets its id sort run
+        on a side stream under this step (deferred clock path, eager; same results).  The next
+        call must pass those very tensor objects, unmodified, to use the prefetched sort."""
         m = self.model
         M = M or (1 + m.negative_samples)
         if not self.graph:
+            pipe = self.deferred is not None and self.clock is not None and (
+                next is not None or getattr(self, "_pending", None) is not None)
+            if pipe:
+                eng = m.engine
+                eng.ensure_layout()
+                w0 = eng.workspace(user_ids.numel(), M, True)
+                entry = torch.cuda.Event()
+                entry.record()
+                self._activate_dedup(w0, user_ids, item_ids)
+                if next is not None and next[0].numel() == user_ids.numel():
+                    self._prefetch_dedup(w0, next[0], next[1], entry)
             w = self._body(user_ids, item_ids, targets, M)
             self.step_count += 1
             m.engine.updates += 1

@@ -595,6 +595,38 @@ def test_clock_mode_bitwise_equals_dense():
         assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
 
 
+def test_pipelined_dedup_bitwise_equals_inline():
+    """FusedTrainStep(next=...) sorts the next batch's ids on a side stream under the current
+    step (two alternating dedup buffer sets); results are bit for bit those of the inline sort,
+    including a step whose prefetch is discarded (ids not the ones announced)."""
+    from ncf_amd.trainer import FusedTrainStep
+    U, I, B = 3000, 500, 64
+    g = torch.Generator().manual_seed(21)
+    batches = []
+    for _ in range(9):
+        u = torch.randint(0, U, (B,), generator=g).repeat_interleave(5).to(DEV)
+        i = torch.randint(0, I, (B * 5,), generator=g).to(DEV)
+        t = torch.zeros(B, 5)
+        t[:, 0] = 1
+        batches.append((u, i, t.reshape(-1, 1).to(DEV)))
+    out = []
+    for pipe in (False, True):
+        torch.manual_seed(11)
+        m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.2, 4).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+        for s_, (u, i, t) in enumerate(batches):
+            if not pipe:
+                step(u, i, t)
+            elif s_ == 4:      # announce a different batch: the prefetch must be ignored
+                step(u, i, t, next=(batches[0][0], batches[0][1]))
+            else:
+                nxt = batches[s_ + 1][:2] if s_ + 1 < len(batches) else None
+                step(u, i, t, next=nxt)
+        out.append({k: v.detach().cpu().clone() for k, v in m.state_dict().items()})
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_overlapped_sweep_bitwise_equals_dense(graph):
     """The opt-in overlapped rolling sweep (side stream under the tower, joined before the
