@@ -396,6 +396,7 @@ class HipShardOps:
         d.advance(st)                               # rolling sweep of step t + 1 (clock)
 
     def dense_grad(self):
+        self.eng.join_reductions()
         return self.eng.flat_grad
 
     def dense_step(self):

@@ -543,9 +543,13 @@ class NCFEngine:
     # ------------------------------------------------------------------ backward
     def backward(self, w: Workspace, uid, iid, grad_prob: Optional[torch.Tensor],
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,
-                 loss_denominator: float = 0.0, tables=None, rows=None, uniq=None):
+                 loss_denominator: float = 0.0, tables=None, rows=None, uniq=None,
+                 reduce_async: bool = False):
         """Gradients of every used parameter.  Dense grads land in the flat grad buffer; table
-        grads stay compact (self.pending) for the fused Adam step."""
+        grads stay compact (self.pending) for the fused Adam step.  ``reduce_async``: the
+        deferred reductions (every dense gradient) run on a side stream, beside whatever the
+        caller queues next that does not read them (the table Adam); the caller must call
+        ``join_reductions()`` before reading the dense gradients."""
         m = self.model
         g = w.g
         n, D, H, M, hid = g.n, g.D, g.H, g.M, g.hidden
@@ -664,8 +668,26 @@ class NCFEngine:
                   self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
                   w.emb_ws.numel(), w.red_list.address, st)
         self.join(dev, joins)
-        w.run_reductions(st)
+        if reduce_async:
+            if getattr(self, "_red_side", None) is None:
+                self._red_side = torch.cuda.Stream(dev)
+                self._red_ev = (torch.cuda.Event(), torch.cuda.Event())
+            side = self._red_side
+            self._red_ev[0].record()
+            side.wait_event(self._red_ev[0])
+            with torch.cuda.stream(side):
+                w.run_reductions(side.cuda_stream)
+            self._red_ev[1].record(side)
+            self._red_pending = True
+        else:
+            w.run_reductions(st)
         self.pending = w
+
+    def join_reductions(self):
+        """The current stream waits for the side-stream reductions of the last backward."""
+        if getattr(self, "_red_pending", False):
+            torch.cuda.current_stream(self.flat.device).wait_event(self._red_ev[1])
+            self._red_pending = False
 
     def _attention_bwd_unfused(self, w, drop_p, seed, joins, st):
         """a5 backward as separate launches (any geometry the unfused forward takes)."""

@@ -93,6 +93,8 @@ class FusedTrainStep:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         prep = self.deferred.prepare if self.deferred is not None else None
         w = eng.forward(user_ids, item_ids, M, True, drop_p, seed, prepare=prep)
+        # (reduce_async=True would run the dense-gradient reductions beside the table Adam:
+        # measured neutral here and slower on the row-sharded step, so off)
         eng.backward(w, user_ids, item_ids, None, targets, drop_p, seed)
         st = _lib.stream_ptr(eng.flat.device)
         b1, b2 = self.betas
@@ -102,6 +104,7 @@ class FusedTrainStep:
             hp = lambda p: (self.lr, b1, b2, self.eps, self.wd)  # noqa: E731
             key_of = {id(p): k for k, p in self.tables.items()}
             eng.adam_tables(hp, lambda p: self.state[key_of[id(p)]], float(self.step_count + 1), st)
+        eng.join_reductions()
         if self.clock is not None:
             _lib.call("ncf_adam_flat_clock", ptr(eng.flat), ptr(eng.flat_grad), ptr(self.m_flat),
                       ptr(self.v_flat), eng.flat.numel(), ptr(self.deferred._table), 1,

@@ -63,7 +63,8 @@ def _worker(rank, world, port, out_dir):
 
         def counts_issue(self, plan):
             W = self.world
-            send = plan.counts.view(W, 2).cpu()
+            with torch.cuda.stream(plan.stream):     # the plan kernels run on the side stream
+                send = plan.counts.view(W, 2).cpu()
             recv = torch.empty_like(send)
             dist.all_to_all_single(recv, send, group=self.plan_group)
             plan.send_counts, plan.recv_counts = send.tolist(), recv.tolist()

@@ -10,6 +10,9 @@ run() {  # run <name> <seconds> <cmd...>
   echo "=== $name rc=$rc"
   tail -n 30 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
+  if grep -q "HSA_STATUS_ERROR\|illegal memory access\|MEMORY_APERTURE" "gpurun_out/$name.log"; then
+    echo "STOP: $name: the GPU runtime reported a fault"; exit 3
+  fi
   return 0
 }
 for step in "$@"; do
