@@ -7,13 +7,13 @@
 // :311-312.  Here the dense [rows, D] gradient is never materialised.  On the dedup of
 // dedup.hip (sorted positions, segments = unique ids, pieces = segments cut every PIECE sorted
 // positions):
-//   k_piece_reduce_ln  one WAVE per piece (<= 64 occurrences): its sub-groups of L = D/4 lanes
-//                      (float4 per lane) sum the upstream LN-output gradients of the piece's
-//                      occurrences in position order, combine in a fixed xor tree, and apply the
+//   k_piece_reduce_ln  one group of L = D/4 lanes (float4 per lane) per piece (<= PIECE
+//                      occurrences), 64/L pieces per wave: the group sums the upstream LN-output
+//                      gradients of its piece's occurrences in position order and applies the
 //                      LayerNorm backward to the sum.  LN is per-row and its backward is LINEAR in
 //                      dy, and every occurrence of an id has the same input row, so
 //                      sum_n LNbwd(dy_n) == sum_pieces LNbwd(sum_piece dy_n): a hot id (a Zipf
-//                      head item with hundreds of occurrences) is spread over many waves instead
+//                      head item with hundreds of occurrences) is spread over many groups instead
 //                      of serialising one.  dgamma/dbeta partials per block.
 //   k_piece_fixup      adds the extra pieces of multi-piece segments to the first piece's row in
 //                      piece order.
@@ -26,10 +26,7 @@ using namespace ncf_seg;
 namespace {
 
 // part[kind*nbr + block][0:D mf_g | D:2D mf_b | 2D:3D mlp_g | 3D:4D mlp_b]
-#ifndef NCF_PIECE_WAVES
-#define NCF_PIECE_WAVES 4
-#endif
-constexpr int kPW = NCF_PIECE_WAVES;   // waves (pieces in flight) per block
+constexpr int kPW = NCF_PIECE_WAVES;   // waves per block
 template <int D>
 __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     const uint32_t* __restrict__ sv0, const uint32_t* __restrict__ sv1,
@@ -45,9 +42,8 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     float* __restrict__ G_mlp0, float* __restrict__ G_mf1, float* __restrict__ G_mlp1,
     float* __restrict__ xp0, float* __restrict__ xp1, float* __restrict__ part) {
   constexpr int L = D / 4;
-  constexpr int S = 64 / L;  // sub-groups per wave
+  constexpr int S = 64 / L;  // lane groups (pieces) per wave
   __shared__ __attribute__((aligned(16))) float red[kPW][4 * D];
-  __shared__ uint32_t sidx[kPW][PIECE];
   const int kind = blockIdx.y;
   const uint32_t* sv = kind ? sv1 : sv0;
   const uint32_t* pstart = kind ? pstart1 : pstart0;
@@ -66,49 +62,51 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
   const int64_t Pn = totals[2 + kind];
   const float4 gm = ld4(g_mf + col), gl = ld4(g_mlp + col);
   float4 a_gm = make_float4(0, 0, 0, 0), a_bm = a_gm, a_gl = a_gm, a_bl = a_gm;
-  for (int64_t p = (int64_t)blockIdx.x * kPW + w; p < Pn; p += (int64_t)gridDim.x * kPW) {
-    // the piece record (independent loads), the table rows as soon as the row is known, then
-    // the occurrence positions and their gradient rows
-    const uint32_t ps = pstart[p];
-    const int cnt = (int)(pstart[p + 1] - ps);  // 1..PIECE
-    const uint32_t info = pseg[p];
-    const int64_t id = uniq[info & ~FIRST_PIECE];
-    const float4 x_mf = ld4(tmf + id * D + col), x_ml = ld4(tml + id * D + col);
-    sidx[w][lane] = lane < cnt ? sv[ps + lane] : 0u;
-    __builtin_amdgcn_wave_barrier();
-    // sub-group sg sums occurrences j = sg, sg + S, ... in order; 4 rows of loads in flight
-    float4 sm = make_float4(0, 0, 0, 0), sl = sm;
-    for (int j0 = 0; j0 < cnt; j0 += 4 * S) {
-      float4 a[4], b[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = j0 + u * S + sg;
-        if (j < cnt) {
-          const int64_t r = sidx[w][j];
-          a[u] = ld4(dmf + r * D + col);
-          b[u] = ld4(dml + r * D + col);
-        } else {
-          a[u] = make_float4(0, 0, 0, 0);
-          b[u] = a[u];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        sm.x += a[u].x; sm.y += a[u].y; sm.z += a[u].z; sm.w += a[u].w;
-        sl.x += b[u].x; sl.y += b[u].y; sl.z += b[u].z; sl.w += b[u].w;
-      }
+  const int64_t stride = (int64_t)gridDim.x * kPW * S;
+  for (int64_t p0 = ((int64_t)blockIdx.x * kPW + w) * S; p0 < Pn; p0 += stride) {
+    // the piece records (independent loads), the table rows as soon as the row is known, the
+    // occurrence positions (lane sub of the group holds occurrence j0 + sub) and their rows
+    const int64_t p = p0 + sg;
+    const bool act = p < Pn;
+    uint32_t ps = 0, info = 0;
+    int cnt = 0;
+    float4 x_mf = make_float4(0, 0, 0, 0), x_ml = x_mf;
+    if (act) {
+      ps = pstart[p];
+      cnt = (int)(pstart[p + 1] - ps);  // 1..PIECE
+      info = pseg[p];
+      const int64_t id = uniq[info & ~FIRST_PIECE];
+      x_mf = ld4(tmf + id * D + col);
+      x_ml = ld4(tml + id * D + col);
     }
-    __builtin_amdgcn_wave_barrier();
+    int cmax = cnt;   // the wave's longest piece: loop bounds stay wave-uniform
 #pragma unroll
-    for (int o = L; o < 64; o <<= 1) {  // combine sub-groups (same columns, lanes L apart)
-      sm.x += __shfl_xor(sm.x, o, 64); sm.y += __shfl_xor(sm.y, o, 64);
-      sm.z += __shfl_xor(sm.z, o, 64); sm.w += __shfl_xor(sm.w, o, 64);
-      sl.x += __shfl_xor(sl.x, o, 64); sl.y += __shfl_xor(sl.y, o, 64);
-      sl.z += __shfl_xor(sl.z, o, 64); sl.w += __shfl_xor(sl.w, o, 64);
+    for (int o = 1; o < 64; o <<= 1) cmax = max(cmax, __shfl_xor(cmax, o, 64));
+    float4 sm = make_float4(0, 0, 0, 0), sl = sm;
+    for (int j0 = 0; j0 < cmax; j0 += L) {
+      const uint32_t r = (j0 + sub < cnt) ? sv[ps + j0 + sub] : 0u;
+      const int jn = min(L, cmax - j0);
+      for (int jj = 0; jj < jn; jj += 4) {   // 4 rows of loads in flight, summed in order
+        float4 a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t rr = __shfl(r, sg * L + jj + u, 64);
+          if (j0 + jj + u < cnt) {
+            a[u] = ld4(dmf + rr * D + col);
+            b[u] = ld4(dml + rr * D + col);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (j0 + jj + u < cnt) {
+            sm.x += a[u].x; sm.y += a[u].y; sm.z += a[u].z; sm.w += a[u].w;
+            sl.x += b[u].x; sl.y += b[u].y; sl.z += b[u].z; sl.w += b[u].w;
+          }
+      }
     }
     const int64_t c = info & ~FIRST_PIECE;
     const bool first = (info & FIRST_PIECE) != 0;
-    // two LayerNorm backwards (GMF row, MLP row); every sub-group computes, sub-group 0 stores
+    // two LayerNorm backwards (GMF row, MLP row) per group
 #pragma unroll
     for (int tbl = 0; tbl < 2; ++tbl) {
       const float4 x = tbl ? x_ml : x_mf;
@@ -122,7 +120,7 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
       const float4 gd = make_float4(dy.x * gg.x, dy.y * gg.y, dy.z * gg.z, dy.w * gg.w);
       const float m1 = group_sum<L>(gd.x + gd.y + gd.z + gd.w) * (1.0f / D);
       const float m2 = group_sum<L>(gd.x * h.x + gd.y * h.y + gd.z * h.z + gd.w * h.w) * (1.0f / D);
-      if (sg == 0) {
+      if (act) {
         const float4 dx = make_float4(rstd * (gd.x - m1 - h.x * m2), rstd * (gd.y - m1 - h.y * m2),
                                       rstd * (gd.z - m1 - h.z * m2), rstd * (gd.w - m1 - h.w * m2));
         float* dst = first ? (tbl ? Gml : Gmf) + c * D
@@ -134,6 +132,18 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
         ab.x += dy.x; ab.y += dy.y; ab.z += dy.z; ab.w += dy.w;
       }
     }
+  }
+  // the wave's groups (lanes L apart hold the same columns), then the block's waves
+#pragma unroll
+  for (int o = L; o < 64; o <<= 1) {
+    a_gm.x += __shfl_xor(a_gm.x, o, 64); a_gm.y += __shfl_xor(a_gm.y, o, 64);
+    a_gm.z += __shfl_xor(a_gm.z, o, 64); a_gm.w += __shfl_xor(a_gm.w, o, 64);
+    a_bm.x += __shfl_xor(a_bm.x, o, 64); a_bm.y += __shfl_xor(a_bm.y, o, 64);
+    a_bm.z += __shfl_xor(a_bm.z, o, 64); a_bm.w += __shfl_xor(a_bm.w, o, 64);
+    a_gl.x += __shfl_xor(a_gl.x, o, 64); a_gl.y += __shfl_xor(a_gl.y, o, 64);
+    a_gl.z += __shfl_xor(a_gl.z, o, 64); a_gl.w += __shfl_xor(a_gl.w, o, 64);
+    a_bl.x += __shfl_xor(a_bl.x, o, 64); a_bl.y += __shfl_xor(a_bl.y, o, 64);
+    a_bl.z += __shfl_xor(a_bl.z, o, 64); a_bl.w += __shfl_xor(a_bl.w, o, 64);
   }
   if (sg == 0) {
     float* rr = red[w];
@@ -172,10 +182,21 @@ __global__ __launch_bounds__(256) void k_piece_fixup(
     const uint32_t f0 = fpiece[c], f1 = fpiece[c + 1];
     if (f1 - f0 <= 1) continue;
     float4 a = ld4(Gmf + c * D + col), b = ld4(Gml + c * D + col);
-    for (int64_t e = (int64_t)f0 - c; e < (int64_t)f1 - c - 1; ++e) {
-      const float4 x = ld4(xp + e * 2 * D + col), y = ld4(xp + e * 2 * D + D + col);
-      a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
-      b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+    const int64_t e1 = (int64_t)f1 - c - 1;
+    for (int64_t e0 = (int64_t)f0 - c; e0 < e1; e0 += 8) {   // 8 rows of loads in flight
+      float4 x[8], y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (e0 + u < e1) {
+          x[u] = ld4(xp + (e0 + u) * 2 * D + col);
+          y[u] = ld4(xp + (e0 + u) * 2 * D + D + col);
+        }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (e0 + u < e1) {   // summed in piece order
+          a.x += x[u].x; a.y += x[u].y; a.z += x[u].z; a.w += x[u].w;
+          b.x += y[u].x; b.y += y[u].y; b.z += y[u].z; b.w += y[u].w;
+        }
     }
     st4(Gmf + c * D + col, a);
     st4(Gml + c * D + col, b);

@@ -16,7 +16,10 @@
 namespace ncf_seg {
 
 constexpr int TILE = 1024;        // keys per sort tile (256 threads x 4)
-constexpr int PIECE = 64;         // max occurrences one wave reduces in the embedding backward
+#ifndef NCF_PIECE
+#define NCF_PIECE 16
+#endif
+constexpr int PIECE = NCF_PIECE;  // max occurrences one lane group reduces in the embedding backward
 #ifndef NCF_RADIX_BITS
 #define NCF_RADIX_BITS 11
 #endif
@@ -52,8 +55,14 @@ struct WS {
 static inline int nb_of(int64_t n) { return n == 0 ? 1 : ncf_cdiv(n, TILE); }
 static inline int64_t pieces_max(int64_t n) { return n + n / PIECE + 2; }
 static inline int64_t extras_max(int64_t n) { return n / PIECE + 2; }
-static inline int nbr_of(int64_t n) {
-  int64_t b = (pieces_max(n) + 3) / 4;  // 4 waves (pieces) per block
+#ifndef NCF_PIECE_WAVES
+#define NCF_PIECE_WAVES 4
+#endif
+// piece-reduce blocks: NCF_PIECE_WAVES waves, each reducing 64 / (D/4) pieces at a time (one per
+// group of D/4 lanes)
+static inline int nbr_of(int64_t n, int64_t D) {
+  const int64_t per = (int64_t)NCF_PIECE_WAVES * (D >= 256 ? 1 : 256 / D);
+  int64_t b = (pieces_max(n) + per - 1) / per;
   if (b < 1) b = 1;
 #ifndef NCF_PIECE_BLOCKS_MAX
 #define NCF_PIECE_BLOCKS_MAX 2048
@@ -65,7 +74,7 @@ static inline int nbr_of(int64_t n) {
 static inline int64_t round256(int64_t b) { return (b + 255) / 256 * 256; }
 
 static inline int64_t ws_bytes(int64_t n, int64_t D) {
-  const int64_t nb = nb_of(n), nbr = nbr_of(n);
+  const int64_t nb = nb_of(n), nbr = nbr_of(n, D);
   int64_t b = 0;
   b += round256(4 * 2 * (MAXP + 1));
   b += round256(4 * (int64_t)MAXP * 2 * MAXR);
@@ -87,7 +96,7 @@ static inline int64_t ws_bytes(int64_t n, int64_t D) {
 static inline WS carve(void* base, int64_t n, int64_t D) {
   WS w;
   w.nb = nb_of(n);
-  w.nbr = nbr_of(n);
+  w.nbr = nbr_of(n, D);
   char* p = (char*)base;
   auto take = [&](int64_t bytes) {
     char* r = p;
