@@ -35,7 +35,7 @@ extern "C" {
  * ncf_step_clock_advance() closes a step (t += 1, next seed = splitmix64(base_seed + t)).   */
 typedef struct ncf_step_clock {
   int32_t t;
-  int32_t reserved;
+  int32_t reserved;   /* 0; used by ncf_adam_flat_clock_close during its launch */
   uint64_t seed;
 } ncf_step_clock;
 int ncf_step_clock_advance(ncf_step_clock* clock, uint64_t base_seed, void* stream);
@@ -568,6 +568,12 @@ int ncf_adam_flat_clock(float* param, const float* grad, float* exp_avg, float* 
                         int64_t n, const float* step_table, int32_t step_rel,
                         const ncf_step_clock* clock, double beta1, double beta2, double eps,
                         double weight_decay, void* stream);
+/* ncf_adam_flat_clock, then ncf_step_clock_advance(clock, base_seed), in one launch (the last
+ * block to finish closes the step; clock->reserved is its block counter, 0 between launches). */
+int ncf_adam_flat_clock_close(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                              int64_t n, const float* step_table, int32_t step_rel,
+                              ncf_step_clock* clock, double beta1, double beta2, double eps,
+                              double weight_decay, uint64_t base_seed, void* stream);
 
 #ifdef __cplusplus
 }

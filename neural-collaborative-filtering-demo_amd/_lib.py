@@ -113,6 +113,7 @@ SIGNATURES = {
     "ncf_adam_pairs_apply_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
     "ncf_adam_pairs_sweep_rolling": (I32, [P, I32, I64, I32, I32, P, P, F64, F64, F64, F64, P]),
     "ncf_adam_flat_clock": (I32, [P, P, P, P, I64, P, I32, P, F64, F64, F64, F64, P]),
+    "ncf_adam_flat_clock_close": (I32, [P, P, P, P, I64, P, I32, P, F64, F64, F64, F64, U64, P]),
     "ncf_score_queries": (I32, [P, I64, P, I64, I64, P, P, F32, P, P, P, P, P]),
     "ncf_score_item_bias": (I32, [P, I64, P, P, P, P, P]),
     "ncf_score_kth": (I32, [P, I64, I64, I32, P, I64, P, P]),

@@ -362,13 +362,51 @@ __global__ __launch_bounds__(256) void k_pairs_sweep(const PairArgs a, int32_t e
   }
 }
 
-__global__ void k_clock_advance(ncf_step_clock* clock, uint64_t base_seed) {
+__device__ __forceinline__ void clock_advance(ncf_step_clock* clock, uint64_t base_seed) {
   const int32_t t = clock->t + 1;
   clock->t = t;
   uint64_t z = base_seed + 0x9E3779B97F4A7C15ull * (uint64_t)(t + 1);
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   clock->seed = (z ^ (z >> 31)) & 0x3FFFFFFFFFFFFFFFull;
+}
+
+__global__ void k_clock_advance(ncf_step_clock* clock, uint64_t base_seed) {
+  clock_advance(clock, base_seed);
+}
+
+// k_adam_flat_clock + k_clock_advance in one launch: every block counts itself done in
+// clock->reserved after its threads have read the clock; the last one advances the clock and
+// re-arms the counter (0 between launches).
+__global__ __launch_bounds__(256) void k_adam_flat_close(float* __restrict__ p,
+                                                         const float* __restrict__ g,
+                                                         float* __restrict__ m,
+                                                         float* __restrict__ v, int64_t n,
+                                                         const float* __restrict__ table,
+                                                         int32_t step_rel, ncf_step_clock* clock,
+                                                         uint64_t base_seed, AdamScalars s) {
+  const int32_t step = clock->t + step_rel;
+  const float ns = table[2 * step], bc = table[2 * step + 1];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    adam1(pp, mm, vv, g[i], ns, bc, s);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+  }
+  // No fence: the only ordering needed is "every block has READ the clock before it changes",
+  // and a block's reads have returned before its counter increment is issued.  (A device-scope
+  // release here would write the L2 back per block: measured 3x slower than two launches.)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* done = reinterpret_cast<unsigned*>(&clock->reserved);
+    if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        gridDim.x - 1) {
+      *done = 0u;
+      clock_advance(clock, base_seed);
+    }
+  }
 }
 
 AdamScalars make_scalars(double lr, double beta1, double beta2, double eps, double wd, double step) {
@@ -667,6 +705,20 @@ extern "C" int ncf_adam_flat_clock(float* param, const float* grad, float* exp_a
                      param, grad, exp_avg, exp_avg_sq, n, step_table, step_rel, clock,
                      consts_of(beta1, beta2, eps, weight_decay));
   NCF_CHECK_LAUNCH("ncf_adam_flat_clock");
+  return NCF_OK;
+}
+
+extern "C" int ncf_adam_flat_clock_close(float* param, const float* grad, float* exp_avg,
+                                         float* exp_avg_sq, int64_t n, const float* step_table,
+                                         int32_t step_rel, ncf_step_clock* clock, double beta1,
+                                         double beta2, double eps, double weight_decay,
+                                         uint64_t base_seed, void* stream) {
+  NCF_CHECK_ARG(n >= 1 && param && grad && exp_avg && exp_avg_sq && step_table && clock,
+                "ncf_adam_flat_clock_close: bad args");
+  hipLaunchKernelGGL(k_adam_flat_close, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                     param, grad, exp_avg, exp_avg_sq, n, step_table, step_rel, clock, base_seed,
+                     consts_of(beta1, beta2, eps, weight_decay));
+  NCF_CHECK_LAUNCH("ncf_adam_flat_clock_close");
   return NCF_OK;
 }
 

@@ -404,10 +404,10 @@ class HipShardOps:
         self.eng.updates += 1
         b1, b2 = self.betas
         st = self._st()
-        _lib.call("ncf_adam_flat_clock", ptr(self.eng.flat), ptr(self.eng.flat_grad),
+        _lib.call("ncf_adam_flat_clock_close", ptr(self.eng.flat), ptr(self.eng.flat_grad),
                   ptr(self.m_flat), ptr(self.v_flat), self.eng.flat.numel(),
-                  ptr(self.deferred._table), 1, ptr(self.clock), b1, b2, self.eps, self.wd, st)
-        _lib.call("ncf_step_clock_advance", ptr(self.clock), self.base_seed, st)
+                  ptr(self.deferred._table), 1, ptr(self.clock), b1, b2, self.eps, self.wd,
+                  self.base_seed, st)
 
     def check(self):
         """Raise IndexError if any step saw an out-of-range id (one host sync)."""

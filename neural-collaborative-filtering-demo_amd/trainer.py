@@ -106,10 +106,10 @@ class FusedTrainStep:
             eng.adam_tables(hp, lambda p: self.state[key_of[id(p)]], float(self.step_count + 1), st)
         eng.join_reductions()
         if self.clock is not None:
-            _lib.call("ncf_adam_flat_clock", ptr(eng.flat), ptr(eng.flat_grad), ptr(self.m_flat),
-                      ptr(self.v_flat), eng.flat.numel(), ptr(self.deferred._table), 1,
-                      ptr(self.clock), b1, b2, self.eps, self.wd, st)
-            _lib.call("ncf_step_clock_advance", ptr(self.clock), self.base_seed, st)
+            _lib.call("ncf_adam_flat_clock_close", ptr(eng.flat), ptr(eng.flat_grad),
+                      ptr(self.m_flat), ptr(self.v_flat), eng.flat.numel(),
+                      ptr(self.deferred._table), 1, ptr(self.clock), b1, b2, self.eps, self.wd,
+                      self.base_seed, st)
         else:
             _lib.call("ncf_adam_flat", ptr(eng.flat), ptr(eng.flat_grad), ptr(self.m_flat),
                       ptr(self.v_flat), eng.flat.numel(), self.lr, b1, b2, self.eps, self.wd,
