@@ -424,7 +424,8 @@ def main():
                                   "hipGraph replay of the captured step" if args.graph else
                                   "host launches"),
                        "parallelism": (f"dp{world} + row-sharded tables (RCCL all-to-all), "
-                                       "dense all-reduce") if sharded else "single-gpu"},
+                                       "dense all-reduce") if sharded else "single-gpu",
+                       **({"exchange": type(step.x).__name__} if sharded else {})},
             "roofline": {"bound": "mfma", "kernel": KERNEL_SYMBOL.get(dom, dom),
                          "entry_point": dom,
                          "achieved": round(dom_tf, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",

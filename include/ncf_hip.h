@@ -498,6 +498,21 @@ int ncf_shard_rows(float* buf, const int32_t* spos0, const int32_t* spos1,
                    const uint32_t* num_unique, int64_t max_n, int64_t dim, float* m00, float* m01,
                    float* m10, float* m11, int dir, void* stream);
 
+/* RCCL communicators and the collectives of the row-sharded step on the caller's stream
+ * (replace torch.distributed.all_to_all_single(out, in, recv_splits, send_splits) and
+ * all_reduce(SUM) of the exchange phases; no c10d layer in between).  RCCL is resolved from the
+ * librccl.so.1 already loaded in the process (ncf_comm_available() == 0 when there is none).
+ * ncf_comm_unique_id (one rank) -> the same 128 bytes to every rank -> ncf_comm_init on all of
+ * them (collective).  ncf_comm_alltoallv: send_rows / recv_rows are HOST arrays of `world`
+ * per-peer row counts; peer p's rows sit at the prefix-sum offsets; a row is row_bytes bytes. */
+int ncf_comm_available(void);
+int ncf_comm_unique_id(uint8_t* id, int64_t bytes);
+int ncf_comm_init(const uint8_t* id, int64_t bytes, int world, int rank, void** comm);
+int ncf_comm_destroy(void* comm);
+int ncf_comm_alltoallv(void* comm, const void* send, const int64_t* send_rows, void* recv,
+                       const int64_t* recv_rows, int64_t row_bytes, void* stream);
+int ncf_comm_allreduce_sum_f32(void* comm, float* buf, int64_t n, void* stream);
+
 /* Deferred dense-exact schedule (bit-identical to ncf_adam_table, see adam.hip): rows carry
  * stamp[row] = last step reflected; step_table[2s], [2s+1] = fp32 scalars of step s
  * (-lr/(1-b1^s), 1/sqrt(1-b2^s))

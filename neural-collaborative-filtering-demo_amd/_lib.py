@@ -89,6 +89,12 @@ SIGNATURES = {
     "ncf_shard_owner_gather": (I32, [P, P, P, P, I64, P, P, I64, I64, P, P]),
     "ncf_shard_owner_gradsum": (I32, [P, P, P, P, I64, I32, I64, P, P, P, P, P]),
     "ncf_shard_rows": (I32, [P, P, P, P, I64, I64, P, P, P, P, I32, P]),
+    "ncf_comm_available": (I32, []),
+    "ncf_comm_unique_id": (I32, [P, I64]),
+    "ncf_comm_init": (I32, [P, I64, I32, I32, P]),
+    "ncf_comm_destroy": (I32, [P]),
+    "ncf_comm_alltoallv": (I32, [P, P, P, P, P, I64, P]),
+    "ncf_comm_allreduce_sum_f32": (I32, [P, P, I64, P]),
     "ncf_embedding_bwd_reduce": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
                                        P, P, P, P, P, P, P, P, P, I64, P, P]),
     "ncf_slot_reset": (I32, [P, P, I32, P, I64, P]),

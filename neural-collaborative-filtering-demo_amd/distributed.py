@@ -32,6 +32,7 @@ torch reference backend.
 """
 import ctypes
 import math
+import os
 import random
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -107,6 +108,92 @@ class ShardExchange:
     def all_reduce_wait(self, work):
         if work is not None:
             work.wait()
+
+
+class RcclExchange(ShardExchange):
+    """The same collectives issued through the C-ABI (``ncf_comm_*``: grouped ncclSend/ncclRecv
+    and ncclAllReduce on the step's own HIP streams) on two RCCL communicators of this library:
+    ``main`` for the run's exchanges, ``side`` for the pipelined count exchange and the dense
+    all-reduce (the roles of ``group`` / ``plan_group``).  The communicators are created over
+    ``group`` (unique ids broadcast by its rank 0).  Same results as ``ShardExchange``; none of
+    the c10d per-call work (Work objects, stream-sync events, allocator bookkeeping)."""
+
+    def __init__(self, group=None, device=None, plan_group=None):
+        super().__init__(group, device, plan_group)
+        if not _lib.query("ncf_comm_available"):
+            raise RuntimeError("RcclExchange: librccl is not loaded in this process")
+        self.main = self._comm()
+        self.side = self._comm()
+        W = self.world
+        self._sr = (ctypes.c_int64 * W)()       # host split arrays (reused every call)
+        self._rr = (ctypes.c_int64 * W)()
+        self._one = (ctypes.c_int64 * W)(*([1] * W))
+        self._side_stream = None
+        self._ev_in, self._ev_out = torch.cuda.Event(), torch.cuda.Event()
+
+    def _comm(self):
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if self.rank == 0:
+            _lib.call("ncf_comm_unique_id", uid.data_ptr(), 128)
+        t = uid.to(self.device)
+        dist.broadcast(t, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0,
+                       group=self.group)
+        uid = t.cpu()
+        c = ctypes.c_void_p()
+        _lib.call("ncf_comm_init", uid.data_ptr(), 128, self.world, self.rank, ctypes.byref(c))
+        return c
+
+    def close(self):
+        for name in ("main", "side"):
+            c = getattr(self, name, None)
+            if c is not None:
+                _lib.call("ncf_comm_destroy", c)
+                setattr(self, name, None)
+
+    def counts_issue(self, plan):
+        if plan.stream is None:
+            raise RuntimeError("RcclExchange needs a plan on a GPU side stream")
+        W = self.world
+        both = plan.extra["counts_both"]              # device [2W, 2] int64: send rows, recv rows
+        with torch.cuda.stream(plan.stream):
+            send = plan.counts.view(W, 2)
+            _lib.call("ncf_comm_alltoallv", self.side, ptr(send), self._one, ptr(both[W:]),
+                      self._one, 16, plan.stream.cuda_stream)
+            both[:W].copy_(send)
+            plan.extra["counts_host"].copy_(both, non_blocking=True)
+            plan.extra["counts_ev"].record()
+        self._side_stream = plan.stream
+
+    def exchange(self, t: torch.Tensor, send_splits: List[int], recv_splits: List[int]):
+        sr, rr = self._sr, self._rr
+        for p in range(self.world):
+            sr[p], rr[p] = send_splits[p], recv_splits[p]
+        out = torch.empty((sum(recv_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        row = t.element_size() * (math.prod(t.shape[1:]) if t.dim() > 1 else 1)
+        _lib.call("ncf_comm_alltoallv", self.main, ptr(t), sr, ptr(out), rr, row,
+                  _lib.stream_ptr(t.device))
+        return out
+
+    def all_reduce_(self, t: torch.Tensor):
+        _lib.call("ncf_comm_allreduce_sum_f32", self.main, ptr(t), t.numel(),
+                  _lib.stream_ptr(t.device))
+        return t
+
+    def all_reduce_start(self, t: torch.Tensor):
+        """The dense all-reduce on the side communicator and stream (behind the next plan's
+        count exchange there), beside the row-gradient exchange on the main one."""
+        ss = self._side_stream
+        if ss is None:
+            return self.all_reduce_(t)
+        self._ev_in.record()
+        ss.wait_event(self._ev_in)
+        _lib.call("ncf_comm_allreduce_sum_f32", self.side, ptr(t), t.numel(), ss.cuda_stream)
+        self._ev_out.record(ss)
+        return self._ev_out
+
+    def all_reduce_wait(self, work):
+        if isinstance(work, torch.cuda.Event):
+            torch.cuda.current_stream(self.device).wait_event(work)
 
 
 @dataclass
@@ -420,10 +507,13 @@ def shard_rows(rows: int, world: int) -> int:
     return (rows + world - 1) // world
 
 
-def make_sharded_step(model_factory, num_users, num_items, group=None, plan_group=None, **adam):
+def make_sharded_step(model_factory, num_users, num_items, group=None, plan_group=None,
+                      exchange=None, **adam):
     """Build the local shard model (tables of ceil(rows / W) rows) and its sharded step.
     Dense parameters are broadcast from rank 0 so every replica starts identical.  A second
-    communicator for the pipelined plan's count exchange is created unless given."""
+    communicator for the pipelined plan's count exchange is created unless given.
+    ``exchange``: "rccl" (the C-ABI collectives, default on the nccl backend) or "torch"
+    (torch.distributed collectives); env NCF_EXCHANGE overrides the default."""
     world = dist.get_world_size(group)
     model = model_factory(shard_rows(num_users, world), shard_rows(num_items, world))
     dev = model.mf_norm.weight.device
@@ -434,4 +524,9 @@ def make_sharded_step(model_factory, num_users, num_items, group=None, plan_grou
         ranks = list(range(world)) if group is None else dist.get_process_group_ranks(group)
         plan_group = dist.new_group(ranks)
     ops = HipShardOps(model, num_users, num_items, world, **adam)
-    return model, ShardedTrainStep(ops, ShardExchange(group, dev, plan_group))
+    kind = exchange or os.environ.get("NCF_EXCHANGE") or (
+        "rccl" if dist.get_backend(group) == "nccl" else "torch")
+    if kind not in ("rccl", "torch"):
+        raise ValueError(f"exchange must be 'rccl' or 'torch', not {kind!r}")
+    X = (RcclExchange if kind == "rccl" else ShardExchange)(group, dev, plan_group)
+    return model, ShardedTrainStep(ops, X)

@@ -674,10 +674,12 @@ def test_fused_step_matches_dropin_path(f2):
 
 
 # ----------------------------------------------------------------------------- sharded (RCCL)
-def test_sharded_step_world1_bitwise_equals_fused():
+@pytest.mark.parametrize("exchange", ["rccl", "torch"])
+def test_sharded_step_world1_bitwise_equals_fused(exchange):
     """The row-sharded DP step (owner bucketing, all-to-alls over RCCL, mini tables, owner-side
-    sums, deferred Adam on the shard) at world size 1 reproduces FusedTrainStep bit for bit; the
-    world > 1 protocol itself is covered by tests/test_dist_cpu.py (gloo, 2 ranks)."""
+    sums, deferred Adam on the shard) at world size 1 reproduces FusedTrainStep bit for bit, with
+    the C-ABI collectives (RcclExchange) and with torch.distributed's; the world > 1 protocol
+    itself is covered by tests/test_dist_cpu.py (gloo, 2 ranks) and test_gpu_dist.py."""
     import socket
     import torch.distributed as dist
     from ncf_amd.distributed import make_sharded_step
@@ -693,7 +695,9 @@ def test_sharded_step_world1_bitwise_equals_fused():
         def factory(ru, ri):
             torch.manual_seed(5)
             return ncf.AdvancedNCF(ru, ri, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.0, 4).to(DEV).train()
-        ms, sharded = make_sharded_step(factory, U, I, lr=1e-3, weight_decay=1e-5)
+        ms, sharded = make_sharded_step(factory, U, I, lr=1e-3, weight_decay=1e-5,
+                                        exchange=exchange)
+        assert type(sharded.x).__name__ == ("RcclExchange" if exchange == "rccl" else "ShardExchange")
         mf = factory(U, I)
         fused = FusedTrainStep(mf, lr=1e-3, weight_decay=1e-5)
         g = torch.Generator().manual_seed(6)
@@ -714,8 +718,46 @@ def test_sharded_step_world1_bitwise_equals_fused():
         a, b = ms.state_dict(), mf.state_dict()
         for k in a:
             assert torch.equal(a[k], b[k]), k
+        if exchange == "rccl":
+            sharded.x.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_comm_alltoallv_and_allreduce_single_rank():
+    """ncf_comm_alltoallv / ncf_comm_allreduce_sum_f32 on a one-rank communicator: the
+    all-to-all is a copy of the first send_rows rows (any row width, empty splits), the sum
+    all-reduce is the identity."""
+    import ctypes
+    from ncf_amd import _lib
+    assert _lib.query("ncf_comm_available") == 1
+    uid = torch.zeros(128, dtype=torch.uint8)
+    _lib.call("ncf_comm_unique_id", uid.data_ptr(), 128)
+    comm = ctypes.c_void_p()
+    _lib.call("ncf_comm_init", uid.data_ptr(), 128, 1, 0, ctypes.byref(comm))
+    try:
+        st = torch.cuda.current_stream().cuda_stream
+        g = torch.Generator().manual_seed(3)
+        for rows, width, dt in [(1000, 128, torch.float32), (37, 1, torch.int32), (0, 16, torch.int64),
+                                (5, 3, torch.int64)]:
+            src = (torch.randn(rows + 4, width, generator=g) * 100).to(dt).to(DEV)
+            dst = torch.full((max(rows, 1), width), -7, dtype=dt, device=DEV)
+            n = (ctypes.c_int64 * 1)(rows)
+            _lib.call("ncf_comm_alltoallv", comm, src.data_ptr(), n, dst.data_ptr(), n,
+                      width * src.element_size(), st)
+            torch.cuda.synchronize()
+            if rows:
+                assert torch.equal(dst[:rows], src[:rows])
+        x = torch.randn(4099, generator=g).to(DEV)
+        y = x.clone()
+        _lib.call("ncf_comm_allreduce_sum_f32", comm, y.data_ptr(), y.numel(), st)
+        torch.cuda.synchronize()
+        assert torch.equal(x, y)
+        with pytest.raises(ValueError):   # negative split
+            bad = (ctypes.c_int64 * 1)(-1)
+            _lib.call("ncf_comm_alltoallv", comm, x.data_ptr(), bad, y.data_ptr(), bad, 4, st)
+    finally:
+        _lib.call("ncf_comm_destroy", comm)
 
 
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
