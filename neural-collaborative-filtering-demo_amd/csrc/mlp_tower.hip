@@ -52,6 +52,20 @@ constexpr int kPasses = (kRows * 16 + kThreads - 1) / kThreads;   // row-op pass
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Phase timestamps (diagnostic builds only, -DNCF_MLP_STAMPS; tools/mlp_stamps.py): thread 0 of
+// each workgroup records the shader clock after every barrier of the tower kernels.
+#ifdef NCF_MLP_STAMPS
+__device__ unsigned long long g_mlp_stamps[2][1024][16];
+#define NCF_STAMP(dir, k)                                                                  \
+  do {                                                                                     \
+    if (threadIdx.x == 0) g_mlp_stamps[dir][blockIdx.x & 1023][k] = clock64();            \
+  } while (0)
+#else
+#define NCF_STAMP(dir, k) \
+  do {                    \
+  } while (0)
+#endif
+
 struct TowerArgs {
   ncf_mlp_layer l[3];
   uint64_t seed[3];
@@ -404,26 +418,37 @@ __global__ __launch_bounds__(kThreads) void k_mlp_fwd(
   const int64_t row0 = (int64_t)blockIdx.x * VR;
   const int rows = (int)min<int64_t>(VR, n - row0);
   const uint64_t cs = clock ? clock->seed : 0ull;
+  NCF_STAMP(0, 0);
   for (int e = threadIdx.x; e < TR * (K0 / 4); e += kThreads) {
     const int r = e / (K0 / 4), c = (e % (K0 / 4)) * 4;
     lds4_st(P + r * kPP + c,
             r < rows ? ld4(xin + (row0 + r) * K0 + c) : make_float4(0.f, 0.f, 0.f, 0.f));
   }
   __syncthreads();
+  NCF_STAMP(0, 1);
   lin_fwd<K0, N0, kPP, kPQ, RT>(P, Q, a.l[0].w, a.l[0].ldw, a.l[0].b);
   __syncthreads();
+  NCF_STAMP(0, 2);
   ln_fwd<N0, kPQ, RT>(Q, row0, rows, a.l[0], eps, p, a.seed[0] + cs, nullptr, nullptr, nullptr,
                       nullptr, nullptr, nullptr, nullptr);
   __syncthreads();
+  NCF_STAMP(0, 3);
   lin_fwd<N0, N1, kPQ, kPP, RT>(Q, P, a.l[1].w, a.l[1].ldw, a.l[1].b);
   __syncthreads();
+  NCF_STAMP(0, 4);
   ln_fwd<N1, kPP, RT>(P, row0, rows, a.l[1], eps, p, a.seed[1] + cs, nullptr, nullptr, nullptr,
                       nullptr, nullptr, nullptr, nullptr);
   __syncthreads();
+  NCF_STAMP(0, 5);
   lin_fwd<N1, N2, kPP, kPQ, RT>(P, Q, a.l[2].w, a.l[2].ldw, a.l[2].b);
   __syncthreads();
+  NCF_STAMP(0, 6);
   ln_fwd<N2, kPQ, RT>(Q, row0, rows, a.l[2], eps, p, a.seed[2] + cs, w_out, b_out, mf_pred, w_fin,
                       b_fin, mlp_pred, prob);
+#ifdef NCF_MLP_STAMPS
+  __syncthreads();
+#endif
+  NCF_STAMP(0, 7);
 }
 
 #ifndef NCF_FWD_RT
@@ -589,6 +614,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
   const int rows = (int)min<int64_t>(kRows, n - row0);
   const uint64_t cs = clock ? clock->seed : 0ull;
   float* pp = part + (int64_t)blockIdx.x * kPartW;
+  NCF_STAMP(1, 0);
   if (fused_head) {
     head_bwd(Q, P, row0, rows, h, a.l[2], p, a.seed[2] + cs, inv_n, pp + 3 * (N0 + N1 + N2));
   } else {
@@ -599,37 +625,54 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     }
     __syncthreads();
   }
+  NCF_STAMP(1, 1);
   ln_bwd<N2, kPQ>(Q, P, row0, rows, a.l[2], p, a.seed[2] + cs, pp);
+  NCF_STAMP(1, 2);
   if (fused_wgrad) {   // dW2 = dlin2^T a1 (a1 staged in P, then overwritten by dX)
     stage_act<N1, kPP>(P, a.l[1], row0, rows, p, a.seed[1] + cs);
     __syncthreads();
+    NCF_STAMP(1, 3);
     wgrad_layer<N2, N1, kPQ, kPP>(Q, P, pp + kW2);
     __syncthreads();
+    NCF_STAMP(1, 4);
   }
   lin_bwd<N2, N1, kPQ, kPP>(Q, P, a.l[2].w, a.l[2].ldw);
   __syncthreads();
+  NCF_STAMP(1, 5);
   ln_bwd<N1, kPP>(P, Q, row0, rows, a.l[1], p, a.seed[1] + cs, pp + 3 * N2);
+  NCF_STAMP(1, 6);
   if (fused_wgrad) {   // dW1 = dlin1^T a0
     stage_act<N0, kPQ>(Q, a.l[0], row0, rows, p, a.seed[0] + cs);
     __syncthreads();
+    NCF_STAMP(1, 7);
     wgrad_layer<N1, N0, kPP, kPQ>(P, Q, pp + kW1);
     __syncthreads();
+    NCF_STAMP(1, 8);
   }
   lin_bwd<N1, N0, kPP, kPQ>(P, Q, a.l[1].w, a.l[1].ldw);
   __syncthreads();
+  NCF_STAMP(1, 9);
   ln_bwd<N0, kPQ>(Q, P, row0, rows, a.l[0], p, a.seed[0] + cs, pp + 3 * (N2 + N1));
+  NCF_STAMP(1, 10);
   if (fused_wgrad) {   // dW0 = dlin0^T x (the first 64 input columns of mlp.0)
     stage_rows<K0, kPP>(P, xin, row0, rows);
     __syncthreads();
+    NCF_STAMP(1, 11);
     wgrad_layer<N0, K0, kPQ, kPP>(Q, P, pp + kW0);
     __syncthreads();
+    NCF_STAMP(1, 12);
   }
   lin_bwd<N0, K0, kPQ, kPP>(Q, P, a.l[0].w, a.l[0].ldw);
   __syncthreads();
+  NCF_STAMP(1, 13);
   for (int e = threadIdx.x; e < rows * (K0 / 4); e += kThreads) {
     const int r = e / (K0 / 4), c = (e % (K0 / 4)) * 4;
     st4(dx + (row0 + r) * K0 + c, lds4(P + r * kPP + c));
   }
+#ifdef NCF_MLP_STAMPS
+  __syncthreads();
+#endif
+  NCF_STAMP(1, 14);
 }
 
 constexpr size_t kLds = sizeof(float) * kRows * (kPQ + kPP);
@@ -655,6 +698,15 @@ int make_args(const ncf_mlp_layer* layers, uint64_t seed, TowerArgs& a) {
 }
 
 }  // namespace
+
+#ifdef NCF_MLP_STAMPS
+// diagnostic builds only (not in ncf_hip.h): copy the phase stamps [2][1024][16] to the host
+extern "C" int ncf_debug_mlp_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mlp_stamps), sizeof(g_mlp_stamps)) == hipSuccess
+             ? NCF_OK
+             : NCF_ERR_LAUNCH;
+}
+#endif
 
 extern "C" int ncf_mlp_fused_supported(int64_t dim, int64_t n_layers, const int64_t* hidden) {
   return tower_ok(dim, n_layers, hidden) ? 1 : 0;
