@@ -53,7 +53,7 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 
 // Counter-based dropout RNG: a 64-bit mix of (seed, element index) -> uniform [0,1).
 // Deterministic per (seed, index); independent of launch geometry.
-// Dropout keep decisions.  One splitmix64 hash of (seed, idx / 4) yields four 16-bit uniforms,
+// Dropout keep decisions.  One 64-bit hash (ncf_drop_bits) of (seed, idx / 4) yields four 16-bit uniforms,
 // field idx % 4 decides element idx: keep iff u >= round(p * 65536) (keep probability 1 - p to
 // 1/65536).  A float4-aligned group of four elements costs a single hash.
 __device__ __forceinline__ uint64_t ncf_hash64(uint64_t seed, uint64_t i) {
@@ -67,15 +67,36 @@ __device__ __forceinline__ uint32_t ncf_drop_threshold(float p) {
   return (uint32_t)(p * 65536.0f + 0.5f);
 }
 
+// 32-bit avalanche mixer (two multiply-xorshift rounds; full avalanche, low bias)
+__device__ __forceinline__ uint32_t ncf_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// the 64 dropout bits of float4 group idx4: two 32-bit mixes of the group index under keys
+// derived from the 64-bit seed (and the index's high word).  32-bit multiplies only: the
+// 64-bit splitmix of ncf_hash64 costs ~2.5x the VALU work, and the dropout masks are
+// recomputed in every LayerNorm of the tower, forward and backward.
+__device__ __forceinline__ uint64_t ncf_drop_bits(uint64_t seed, uint64_t idx4) {
+  const uint32_t k = (uint32_t)seed ^ ncf_mix32((uint32_t)(seed >> 32) ^ (uint32_t)(idx4 >> 32));
+  const uint32_t i = (uint32_t)idx4;
+  const uint32_t h0 = ncf_mix32(i ^ k), h1 = ncf_mix32(i ^ k ^ 0x9E3779B9u);
+  return ((uint64_t)h1 << 32) | h0;
+}
+
 // keep-scale of element idx for dropout probability p (nn.Dropout: scale 1/(1-p))
 __device__ __forceinline__ float ncf_dropout_scale(uint64_t seed, uint64_t idx, float p, float inv_keep) {
-  const uint32_t u = (uint32_t)(ncf_hash64(seed, idx >> 2) >> (16 * (idx & 3))) & 0xFFFFu;
+  const uint32_t u = (uint32_t)(ncf_drop_bits(seed, idx >> 2) >> (16 * (idx & 3))) & 0xFFFFu;
   return u >= ncf_drop_threshold(p) ? inv_keep : 0.0f;
 }
 
 // keep-scales of elements idx4*4 .. idx4*4+3 (same decisions as ncf_dropout_scale)
 __device__ __forceinline__ float4 ncf_dropout_scale4(uint64_t seed, uint64_t idx4, float p, float inv_keep) {
-  const uint64_t z = ncf_hash64(seed, idx4);
+  const uint64_t z = ncf_drop_bits(seed, idx4);
   const uint32_t t = ncf_drop_threshold(p);
   return make_float4((uint32_t)(z & 0xFFFFu) >= t ? inv_keep : 0.0f,
                      (uint32_t)((z >> 16) & 0xFFFFu) >= t ? inv_keep : 0.0f,
