@@ -90,11 +90,31 @@ class ShardExchange:
         self.counts_issue(plan)
         self.counts_wait(plan)
 
-    def exchange(self, t: torch.Tensor, send_splits: List[int], recv_splits: List[int]):
+    def exchange(self, t: torch.Tensor, send_splits: List[int], recv_splits: List[int],
+                 side: bool = False):
         out = torch.empty((sum(recv_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_to_all_single(out, t[:sum(send_splits)], recv_splits, send_splits,
-                               group=self.group)
+                               group=self.plan_group if side else self.group)
         return out
+
+    def exchange_ahead(self, plan):
+        """The first exchange of a plan issued a step ahead (its local rows to their owners), run
+        on the plan's side stream and communicator as soon as its counts are home, so the next
+        step starts with its rows already at the owners.  Returns (recv, event)."""
+        send_splits, recv_splits = plan.splits()
+        if plan.stream is None:
+            return self.exchange(plan.send, send_splits, recv_splits, side=True), None
+        with torch.cuda.stream(plan.stream):
+            out = self.exchange(plan.send, send_splits, recv_splits, side=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        return out, ev
+
+    def wait_ahead(self, out, ev):
+        if ev is not None:
+            cur = torch.cuda.current_stream(out.device)
+            cur.wait_event(ev)
+            out.record_stream(cur)
 
     def all_reduce_(self, t: torch.Tensor):
         dist.all_reduce(t, group=self.group)
@@ -164,14 +184,15 @@ class RcclExchange(ShardExchange):
             plan.extra["counts_ev"].record()
         self._side_stream = plan.stream
 
-    def exchange(self, t: torch.Tensor, send_splits: List[int], recv_splits: List[int]):
+    def exchange(self, t: torch.Tensor, send_splits: List[int], recv_splits: List[int],
+                 side: bool = False):
         sr, rr = self._sr, self._rr
         for p in range(self.world):
             sr[p], rr[p] = send_splits[p], recv_splits[p]
         out = torch.empty((sum(recv_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         row = t.element_size() * (math.prod(t.shape[1:]) if t.dim() > 1 else 1)
-        _lib.call("ncf_comm_alltoallv", self.main, ptr(t), sr, ptr(out), rr, row,
-                  _lib.stream_ptr(t.device))
+        _lib.call("ncf_comm_alltoallv", self.side if side else self.main, ptr(t), sr, ptr(out),
+                  rr, row, _lib.stream_ptr(t.device))
         return out
 
     def all_reduce_(self, t: torch.Tensor):
@@ -218,9 +239,11 @@ class ShardedTrainStep:
     """One data-parallel + row-sharded training step: the protocol above over an ops backend.
     ``step(u, i, t, next=(u2, i2))`` also plans the following step (pipelined)."""
 
-    def __init__(self, ops, exchange: ShardExchange):
+    def __init__(self, ops, exchange: ShardExchange, ahead: Optional[bool] = None):
         self.ops, self.x = ops, exchange
-        self._pending = None      # (user_ids, item_ids, Plan) planned ahead
+        self._pending = None      # [user_ids, item_ids, Plan, (recv, event) | None] planned ahead
+        # send the next step's rows to their owners during this step (env NCF_SHARD_AHEAD=0: off)
+        self.ahead = ahead if ahead is not None else os.environ.get("NCF_SHARD_AHEAD", "1") != "0"
 
     def plan(self, user_ids, item_ids):
         p = self.ops.plan(user_ids, item_ids, self.x.world)
@@ -231,21 +254,30 @@ class ShardedTrainStep:
         ops, X = self.ops, self.x
         ops.mark_entry()          # ids of this call and of `next` exist from here on
         pend, self._pending = self._pending, None
+        ahead = None
         if pend is not None and pend[0] is user_ids and pend[1] is item_ids:
-            plan = pend[2]        # issued one call ago: its counts are (almost surely) home
+            plan, ahead = pend[2], pend[3]   # planned (and its rows sent) one call ago
         else:
             plan = self.plan(user_ids, item_ids)
         X.counts_wait(plan)
         if next is not None:      # plan step t+1 now: it runs under this step's GPU work
-            self._pending = (next[0], next[1], self.plan(next[0], next[1]))
+            self._pending = [next[0], next[1], self.plan(next[0], next[1]), None]
         ops.begin(plan)
         send_splits, recv_splits = plan.splits()
-        recv = X.exchange(plan.send, send_splits, recv_splits)
+        if ahead is not None:
+            recv = ahead[0]
+            X.wait_ahead(*ahead)
+        else:
+            recv = X.exchange(plan.send, send_splits, recv_splits)
         own = ops.owner_prepare(recv, plan)
         rows = ops.owner_gather(own, recv)
         back = X.exchange(rows, recv_splits, send_splits)
         grads, loss = ops.compute(plan, back, user_ids, item_ids, targets,
                                   loss_denominator=user_ids.numel() * X.world)
+        if self.ahead and self._pending is not None:   # step t+1's rows to their owners now
+            nxt = self._pending[2]
+            X.counts_wait(nxt)
+            self._pending[3] = X.exchange_ahead(nxt)
         ar = X.all_reduce_start(ops.dense_grad())
         got = X.exchange(grads, send_splits, recv_splits)
         ops.owner_apply(own, got)
