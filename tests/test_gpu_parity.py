@@ -1374,3 +1374,35 @@ def test_shard_exchange_kernels_emulated_ranks(W, D):
         assert torch.equal(mini[2 * k][:c], back[sp, :D])
         assert torch.equal(mini[2 * k + 1][:c], back[sp, D:])
         assert torch.equal(out[sp], back[sp])
+
+
+def test_adam_flat_clock_close_equals_two_launches():
+    """ncf_adam_flat_clock_close (flat Adam + step-clock advance in one launch, the last block
+    closing the step) == ncf_adam_flat_clock followed by ncf_step_clock_advance, bit for bit, over
+    several steps; the block counter is re-armed (0) after every launch."""
+    import numpy as np
+    from ncf_amd import _lib
+    g = torch.Generator().manual_seed(11)
+    n = 300_001                       # > one block, not a multiple of 256
+    lr, b1, b2, eps, wd, seed = 1e-3, 0.9, 0.999, 1e-8, 1e-5, 12345
+    host = np.zeros(2 * 9, dtype=np.float32)      # step scalars of steps 1..8 at index 2s, 2s+1
+    _lib.call("ncf_adam_step_scalars", lr, b1, b2, 1, 8, host[2:].ctypes.data)
+    table = torch.from_numpy(host).to(DEV)
+    ps = [torch.randn(n, generator=g).to(DEV) for _ in range(2)]
+    ps[1].copy_(ps[0])
+    ms = [torch.zeros(n, device=DEV) for _ in range(2)]
+    vs = [torch.zeros(n, device=DEV) for _ in range(2)]
+    clocks = [torch.tensor([0, seed], dtype=torch.int64, device=DEV) for _ in range(2)]
+    st = torch.cuda.current_stream().cuda_stream
+    for _ in range(4):
+        grad = torch.randn(n, generator=g).to(DEV)
+        _lib.call("ncf_adam_flat_clock", ps[0].data_ptr(), grad.data_ptr(), ms[0].data_ptr(),
+                  vs[0].data_ptr(), n, table.data_ptr(), 1, clocks[0].data_ptr(), b1, b2, eps, wd, st)
+        _lib.call("ncf_step_clock_advance", clocks[0].data_ptr(), seed, st)
+        _lib.call("ncf_adam_flat_clock_close", ps[1].data_ptr(), grad.data_ptr(), ms[1].data_ptr(),
+                  vs[1].data_ptr(), n, table.data_ptr(), 1, clocks[1].data_ptr(), b1, b2, eps, wd,
+                  seed, st)
+    torch.cuda.synchronize()
+    for a, b in ((ps[0], ps[1]), (ms[0], ms[1]), (vs[0], vs[1]), (clocks[0], clocks[1])):
+        assert torch.equal(a, b)
+    assert int(clocks[1][0].item()) == 4          # t = 4, reserved (high word) = 0
