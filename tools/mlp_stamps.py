@@ -20,6 +20,8 @@ import bench  # noqa: E402
 ncf = _ncf_pkg.load()
 FWD = ["stage x", "lin0 (64->256)", "ln0", "lin1 (256->128)", "ln1", "lin2 (128->64)",
        "ln2 + head"]
+FWD_PIPE = ["stage x", "lin0 A", "lin0 B | ln0 A", "lin1 A | ln0 B", "lin1 B | ln1 A",
+            "lin2 A | ln1 B", "lin2 B | ln2 A", "ln2 B + head"]
 BWD = ["head bwd", "ln2 bwd", "stage a1", "wgrad2", "lin2 bwd", "ln1 bwd", "stage a0", "wgrad1",
        "lin1 bwd", "ln0 bwd", "stage x", "wgrad0", "lin0 bwd", "dx store"]
 
@@ -40,7 +42,8 @@ def main():
     rc = lib.ncf_debug_mlp_stamps(ctypes.c_void_p(buf.ctypes.data))
     assert rc == 0, "not a -DNCF_MLP_STAMPS build?"
     nwg = (B * M + 79) // 80
-    for d, names in ((0, FWD), (1, BWD)):
+    fwd = FWD_PIPE if buf[0, 0, 8] != 0 else FWD   # the pipelined forward stamps 9 points
+    for d, names in ((0, fwd), (1, BWD)):
         st = buf[d, :nwg, :len(names) + 1].astype(np.int64)
         dur = np.diff(st, axis=1)
         tot = st[:, -1] - st[:, 0]
