@@ -674,8 +674,8 @@ def test_fused_step_matches_dropin_path(f2):
 
 
 # ----------------------------------------------------------------------------- sharded (RCCL)
-@pytest.mark.parametrize("exchange", ["rccl", "torch"])
-def test_sharded_step_world1_bitwise_equals_fused(exchange):
+@pytest.mark.parametrize("exchange,ahead", [("rccl", True), ("rccl", False), ("torch", True)])
+def test_sharded_step_world1_bitwise_equals_fused(exchange, ahead):
     """The row-sharded DP step (owner bucketing, all-to-alls over RCCL, mini tables, owner-side
     sums, deferred Adam on the shard) at world size 1 reproduces FusedTrainStep bit for bit, with
     the C-ABI collectives (RcclExchange) and with torch.distributed's; the world > 1 protocol
@@ -698,6 +698,7 @@ def test_sharded_step_world1_bitwise_equals_fused(exchange):
         ms, sharded = make_sharded_step(factory, U, I, lr=1e-3, weight_decay=1e-5,
                                         exchange=exchange)
         assert type(sharded.x).__name__ == ("RcclExchange" if exchange == "rccl" else "ShardExchange")
+        sharded.ahead = ahead          # next step's first all-to-all during this step, or not
         mf = factory(U, I)
         fused = FusedTrainStep(mf, lr=1e-3, weight_decay=1e-5)
         g = torch.Generator().manual_seed(6)
