@@ -56,7 +56,7 @@ static inline int nb_of(int64_t n) { return n == 0 ? 1 : ncf_cdiv(n, TILE); }
 static inline int64_t pieces_max(int64_t n) { return n + n / PIECE + 2; }
 static inline int64_t extras_max(int64_t n) { return n / PIECE + 2; }
 #ifndef NCF_PIECE_WAVES
-#define NCF_PIECE_WAVES 4
+#define NCF_PIECE_WAVES 8
 #endif
 // piece-reduce blocks: NCF_PIECE_WAVES waves, each reducing 64 / (D/4) pieces at a time (one per
 // group of D/4 lanes)

@@ -11,7 +11,7 @@ for rep in 1 2; do
 import json, sys
 d = json.loads([l for l in open(f"gpurun_out/ab_{sys.argv[1]}_{sys.argv[2]}.log") if l.startswith("{")][-1])
 k = d["kernel_ms_per_step"]
-print(sys.argv[1], sys.argv[2], d["ms_per_step"], {x: k.get(x) for x in ("ncf_mlp_fwd", "ncf_mlp_bwd", "ncf_wgrad_grouped", "ncf_attn_block_fwd", "ncf_attn_block_bwd")})
+print(sys.argv[1], sys.argv[2], d["ms_per_step"], {x: k.get(x) for x in ("ncf_mlp_fwd", "ncf_mlp_bwd", "ncf_embedding_bwd_reduce", "ncf_reduce_batch", "ncf_attn_block_fwd", "ncf_attn_block_bwd")})
 PY
   done
 done
