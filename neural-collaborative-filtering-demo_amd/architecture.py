@@ -8,6 +8,7 @@ Reference citations are src/model/architecture.py:<line> unless stated.
 """
 import logging
 import math
+import weakref
 from typing import Dict, List, Optional
 
 import torch
@@ -85,34 +86,58 @@ class CategoryHierarchy(nn.Module):
 
 
 class _NCFTrainFunction(torch.autograd.Function):
-    """Forward + backward of AdvancedNCF.forward in training mode.  Inputs after the ids are the
-    model's parameters (so autograd connects the graph); their gradients are written by the
-    kernels directly (dense: views of the engine's flat gradient buffer; tables: compact, applied
-    by the fused Adam or materialised on demand)."""
+    """Forward + backward of AdvancedNCF.forward in training mode.  The last input is the
+    model's grad anchor (a 0-element tensor that requires grad), which connects the output to
+    autograd at the cost of one input instead of every parameter's; the gradients are written
+    by the kernels directly (dense: views of the engine's flat gradient buffer, assigned as
+    .grad; tables: compact rows, applied by the fused Adam or materialised on demand).
+
+    With a deferred table schedule attached (optim.py binding / FusedTrainStep), the forward
+    deduplicates the batch ids and catches exactly those rows up first (deferred.prepare)."""
 
     @staticmethod
-    def forward(ctx, engine, uid, iid, M, drop_p, seed, *params):
-        w = engine.forward(uid, iid, M, True, drop_p, seed)
+    def forward(ctx, engine, uid, iid, M, drop_p, seed, anchor):
+        d = engine.deferred
+        # a step left unapplied (e.g. accumulation) keeps its rows' gradients in the
+        # workspace this forward reuses: make them dense table .grad before they are overwritten
+        _settle_pending(engine, uid.device)
+        w = engine.forward(uid, iid, M, True, drop_p, seed,
+                           prepare=d.prepare if d is not None else None)
         ctx.engine, ctx.w, ctx.drop_p, ctx.seed = engine, w, drop_p, seed
         ctx.save_for_backward(uid, iid)
-        ctx.n_params = len(params)
         return w.prob.view(-1, 1).clone()
 
     @staticmethod
     def backward(ctx, grad_out):
         uid, iid = ctx.saved_tensors
         eng = ctx.engine
-        dense = eng.dense_params()
-        prev = [(p, p.grad.clone()) for _, p in dense if p.grad is not None]
-        if eng.pending is not None:
-            eng.release_pending(_lib.stream_ptr(grad_out.device))
+        views = eng.grad_views()
+        prev = [(p, p.grad.clone()) for p, _ in views if p.grad is not None and p.requires_grad]
+        _settle_pending(eng, grad_out.device)
         eng.backward(ctx.w, uid, iid, grad_out.contiguous(), None, ctx.drop_p, ctx.seed)
-        for name, p in dense:
-            p.grad = eng.grad_view(name)
+        for p, v in views:
+            if p.requires_grad:
+                p.grad = v
         for p, g in prev:  # gradient accumulation across backward() calls
             p.grad.add_(g)
-        _optim.note_pending(eng)
-        return (None,) * (6 + ctx.n_params)
+        eng.grad_version = eng.flat_grad._version
+        return (None,) * 7
+
+
+def _settle_pending(eng, device):
+    """Compact table gradients of a backward whose optimizer step has not run yet: kept (as
+    dense table .grad, summed with the next ones) when the dense gradients of that backward
+    are still there untouched — gradient accumulation — and dropped when they were cleared
+    in between (zero_grad: set to None, or zeroed in place, which bumps their version)."""
+    if eng.pending is None:
+        return
+    views = eng.grad_views()
+    kept = any(p.grad is v for p, v in views) and \
+        getattr(eng, "grad_version", None) == eng.flat_grad._version
+    if kept:
+        eng.materialize_table_grads(accumulate=True)
+    else:
+        eng.release_pending(_lib.stream_ptr(device))
 
 
 class AdvancedNCF(nn.Module):
@@ -173,7 +198,17 @@ class AdvancedNCF(nn.Module):
         self.mf_norm = nn.LayerNorm(mf_embedding_dim)                    # :255-256 (re-created;
         self.mlp_norm = nn.LayerNorm(mlp_embedding_dim)                  #  keeps key order)
         object.__setattr__(self, "_engine", NCFEngine(self))
+        # autograd anchor of the training forward (not a parameter or buffer: no state_dict key)
+        object.__setattr__(self, "_anchor", torch.zeros(0, requires_grad=True))
         self._engine.flatten()
+        eref = weakref.ref(self._engine)
+
+        def sync():
+            e = eref()
+            if e is not None:
+                e.sync_tables()
+        self.mf_embedding_collection.set_sync(sync)
+        self.mlp_embedding_collection.set_sync(sync)
         _optim.register(self)
 
     # keep the dense flat layout valid across .to()/.cuda()/.float()
@@ -191,6 +226,18 @@ class AdvancedNCF(nn.Module):
         self._engine.sync_tables()
         return super().state_dict(*args, **kwargs)
 
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        # rows a deferred optimizer still owes zero-gradient steps must settle BEFORE they are
+        # overwritten: otherwise the owed steps (decay + old moments) would later be replayed
+        # onto the loaded values.  After the sweep every row is current, so the loaded rows
+        # simply continue from the optimizer's current step (as with torch's dense Adam).
+        self._engine.sync_tables()
+        out = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self._engine.updates += 1
+        if assign:
+            self._engine.flatten()
+        return out
+
     # ---------------------------------------------------------------- forward (:258-381)
     def forward(self, features: KeyedJaggedTensor) -> torch.Tensor:
         total_samples = features.values().size(0) // 2                  # :274
@@ -203,15 +250,20 @@ class AdvancedNCF(nn.Module):
         eng = self._engine
         train = self.training and torch.is_grad_enabled()
         drop_p = float(self.dropout) if self.training else 0.0
+        # (with a device step clock attached the kernels add its per-step seed)
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0 else 0
         if train:
-            params = [p for p in self.parameters() if p.requires_grad]
-            out = _NCFTrainFunction.apply(eng, uid, iid, M, drop_p, seed, *params)
+            out = _NCFTrainFunction.apply(eng, uid, iid, M, drop_p, seed, self._anchor)
         else:
             w = eng.forward(uid, iid, M, False, drop_p, seed)
             out = w.prob.view(-1, 1).clone()
-        if getattr(self, "validate_ids", True):
-            eng.check_ids(eng.ws[(uid.numel(), M, train)])
+        v = getattr(self, "validate_ids", True)
+        if v:
+            ws = eng.ws[(uid.numel(), M, train)]
+            if train and v != "sync":
+                eng.check_ids_async(ws)      # no host sync inside the training loop
+            else:
+                eng.check_ids(ws)
         if not hasattr(self, "_first_forward_done"):                    # :365-372
             log.info("First forward pass: output %s", tuple(out.shape))
             self._first_forward_done = True

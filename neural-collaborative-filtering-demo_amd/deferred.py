@@ -36,7 +36,8 @@ class DeferredTableAdam:
         # clock (ncf_step_clock, device): every step-dependent value is read on the device, so
         # the launches of a step do not depend on the host counter (hipGraph capture)
         self.clock = clock
-        self.lr, self.betas, self.eps, self.wd = float(lr), tuple(betas), float(eps), float(weight_decay)
+        self.lr, self.eps, self.wd = float(lr), float(eps), float(weight_decay)
+        self.betas = (float(betas[0]), float(betas[1]))
         self.sweep_every = int(sweep_every)
         self.tables = engine.table_params()
         dev = self.tables["mf_user"].device
@@ -45,11 +46,13 @@ class DeferredTableAdam:
         m = engine.model
         self.stamp = {"user": torch.zeros(m.num_users, dtype=torch.int32, device=dev),
                       "item": torch.zeros(m.num_products, dtype=torch.int32, device=dev)}
+        if engine.deferred is not None and engine.deferred is not self:
+            engine.deferred.detach()    # the previous schedule settles its lagging rows first
         self.t = 0
         self.synced_t = 0
         self._table = torch.zeros(0, dtype=torch.float32, device=dev)
         self._filled = 0
-        self._lr_filled = None
+        self._hp_filled = None      # (lr, beta1, beta2) the filled scalars were computed with
         # Overlapped rolling sweep (clock path, opt-in): the sweep closing step T is launched
         # during step T+1, after its catch-up (right before its MLP tower), on a side stream, and
         # joined before step T+1's table apply.  Rows of step T+1's batch are current by then
@@ -68,12 +71,19 @@ class DeferredTableAdam:
 
     # ---- per-step scalar table (index 2s / 2s+1 = step s)
     def _ensure(self, upto: int):
-        if upto <= self._filled and self._lr_filled == self.lr:
-            return
         b1, b2 = self.betas
-        first = 1 if self._lr_filled != self.lr else self._filled + 1
-        # lr changes only affect steps not yet taken
-        first = max(1, min(first, self.t + 1))
+        hp = (self.lr, b1, b2)
+        if upto <= self._filled and self._hp_filled == hp:
+            return
+        if self._hp_filled is None:
+            first = 1
+        elif self._hp_filled != hp:
+            # an lr (or beta) change affects only steps not yet taken: the scalars of steps
+            # <= t stay as they were, so rows still behind replay those steps as taken
+            first = min(self._filled + 1, self.t + 1)
+        else:
+            first = self._filled + 1
+        first = max(1, first)
         last = max(upto, first) + 4096
         host = np.empty(2 * (last - first + 1), dtype=np.float32)
         _lib.call("ncf_adam_step_scalars", self.lr, b1, b2, first, last - first + 1,
@@ -86,7 +96,31 @@ class DeferredTableAdam:
                 grown[:self._table.numel()].copy_(self._table)
             self._table = grown
         self._table[2 * first:2 * (last + 1)].copy_(torch.from_numpy(host))
-        self._filled, self._lr_filled = last, self.lr
+        self._filled, self._hp_filled = last, hp
+
+    def set_hparams(self, lr, betas, eps, weight_decay):
+        """Change the hyper-parameters for the steps not yet taken.  lr lives only in the
+        per-step scalar table (refilled from step t + 1); betas / eps / weight_decay also enter
+        every replayed zero-gradient step, so rows still behind are first brought current with
+        the old values (one full sweep, only when they change)."""
+        betas = (float(betas[0]), float(betas[1]))
+        if (betas, float(eps), float(weight_decay)) != (self.betas, self.eps, self.wd):
+            self.sync()
+            self.betas, self.eps, self.wd = betas, float(eps), float(weight_decay)
+        self.lr = float(lr)
+
+    def mark_current(self, t: int):
+        """Every row of every table holds its value after step t (e.g. a dense step, or state
+        just loaded): restart the schedule there."""
+        self.t = self.synced_t = int(t)
+        for stamp in self.stamp.values():
+            stamp.fill_(int(t))
+        self._owed, self._joined = False, True
+
+    def rebind_moments(self, moments):
+        """Use other exp_avg / exp_avg_sq tensors (e.g. after an optimizer state load)."""
+        self.state = moments
+        self.__dict__.pop("_sweep_pairs", None)
 
     def _consts(self):
         b1, b2 = self.betas

@@ -219,11 +219,12 @@ class NCFEngine:
         return ps
 
     def table_params(self):
+        # raw parameters: kernel plumbing must not trigger the bags' bring-current-on-read
         m = self.model
-        return {"mf_user": m.mf_embedding_collection.embedding_bags["user_id"].weight,
-                "mf_item": m.mf_embedding_collection.embedding_bags["product_id"].weight,
-                "mlp_user": m.mlp_embedding_collection.embedding_bags["user_id"].weight,
-                "mlp_item": m.mlp_embedding_collection.embedding_bags["product_id"].weight}
+        mf, mlp = m.mf_embedding_collection.embedding_bags, m.mlp_embedding_collection.embedding_bags
+        return {"mf_user": mf["user_id"].raw_weight(), "mf_item": mf["product_id"].raw_weight(),
+                "mlp_user": mlp["user_id"].raw_weight(),
+                "mlp_item": mlp["product_id"].raw_weight()}
 
     def flatten(self):
         """(Re)pack the used dense parameters into one 16-B aligned flat buffer (views)."""
@@ -342,6 +343,11 @@ class NCFEngine:
         otherwise).  Called before anything other than the fused train step reads a table."""
         if self.deferred is not None:
             self.deferred.sync()
+
+    def lagging(self) -> bool:
+        """Whether a deferred optimizer holds table rows behind (a sync_tables would sweep)."""
+        d = self.deferred
+        return d is not None and d.t != 0 and d.synced_t != d.t
 
     def forward(self, uid: torch.Tensor, iid: torch.Tensor, M: int, train: bool,
                 drop_p: float, seed: int, prepare=None, tables=None, rows=None,
@@ -540,6 +546,34 @@ class NCFEngine:
             w.err.zero_()
             raise IndexError("AdvancedNCF: user/product id out of range of the embedding tables")
 
+    ID_CHECK_EVERY = 16
+
+    def check_ids_async(self, w: Workspace):
+        """Training-mode id validation without a host sync.  Every ID_CHECK_EVERY-th call
+        copies the sticky error flag of w to pinned host memory behind an event; a later call
+        whose event has completed reads it and raises IndexError.  An out-of-range id never
+        touches memory out of bounds (the kernels read / update row 0 instead and raise the
+        flag), so the error surfaces at most a few steps after the faulty batch ran on the
+        GPU; ``check_ids`` (eval, and ``model.validate_ids = "sync"``) is immediate."""
+        a = getattr(self, "_err_async", None)
+        if a is None:
+            a = self._err_async = {"host": torch.zeros(1, dtype=torch.int32, pin_memory=True),
+                                   "ev": torch.cuda.Event(), "pending": False, "k": 0}
+        if a["pending"]:
+            if not a["ev"].query():
+                return
+            a["pending"] = False
+            if int(a["host"][0]):
+                w.err.zero_()
+                raise IndexError("AdvancedNCF: user/product id out of range of the embedding "
+                                 "tables (seen by a training step in flight)")
+        a["k"] += 1
+        if a["k"] % self.ID_CHECK_EVERY:
+            return
+        a["host"].copy_(w.err, non_blocking=True)
+        a["ev"].record()
+        a["pending"] = True
+
     # ------------------------------------------------------------------ backward
     def backward(self, w: Workspace, uid, iid, grad_prob: Optional[torch.Tensor],
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,
@@ -656,10 +690,12 @@ class NCFEngine:
         G = w.G
         uq_u, uq_i = uniq if uniq is not None else (w.uniq_u, w.uniq_i)
         d_rows = rows or (m.num_users, m.num_products)
+        w.slots_set = False
         if not getattr(w, "deduped", False):   # sort/deduplicate now (slot maps for the Adam)
             _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, D, m.num_users, m.num_products,
                       ptr(w.uniq_u), ptr(w.uniq_i), ptr(self.slot_u), ptr(self.slot_i),
                       ptr(w.num_unique), ptr(w.emb_ws), w.emb_ws.numel(), st)
+            w.slots_set = True
         _lib.call("ncf_embedding_bwd_reduce", n, D, d_rows[0], d_rows[1],
                   ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), *tbp,
                   pp["mf_norm.weight"], pp["mlp_norm.weight"], LN_EPS, ptr(G["mf_user"]),
@@ -749,30 +785,50 @@ class NCFEngine:
                 ev[1].record()
         self.release_pending(st)
 
+    def reset_slots(self, w, st):
+        """Clear the slot-map entries a backward's inline dedup set (rows of w)."""
+        n = w.g.n
+        _lib.call("ncf_slot_reset", ptr(w.uniq_u), ptr(w.num_unique), 0, ptr(self.slot_u), n, st)
+        _lib.call("ncf_slot_reset", ptr(w.uniq_i), ptr(w.num_unique), 1, ptr(self.slot_i), n, st)
+        w.slots_set = False
+
     def release_pending(self, st):
         w = self.pending
         if w is None:
             return
-        n = w.g.n
-        _lib.call("ncf_slot_reset", ptr(w.uniq_u), ptr(w.num_unique), 0, ptr(self.slot_u), n, st)
-        _lib.call("ncf_slot_reset", ptr(w.uniq_i), ptr(w.num_unique), 1, ptr(self.slot_i), n, st)
+        self.reset_slots(w, st)
         self.pending = None
 
-    def materialize_table_grads(self):
+    def materialize_table_grads(self, accumulate: bool = False):
         """Write dense [rows, D] gradients into the tables' .grad (for optimizers other than
-        the fused Adam, or for inspection), then release the compact buffers."""
+        the fused Adam, gradient accumulation, or inspection), then release the compact
+        buffers.  ``accumulate``: add to an existing .grad instead of replacing it.  Tables
+        with requires_grad=False get no gradient (as autograd gives them none)."""
         w = self.pending
         if w is None:
             return
         st = _lib.stream_ptr(w.prob.device)
         D = self.model.mlp_embedding_dim
         for key, p in self.table_params().items():
+            if not p.requires_grad:
+                continue
             kind = 0 if key.endswith("user") else 1
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-            else:
-                p.grad.zero_()
-            _lib.call("ncf_scatter_compact_rows", ptr(p.grad), D,
+            add = accumulate and p.grad is not None
+            dst = torch.zeros_like(p) if (add or p.grad is None) else p.grad.zero_()
+            _lib.call("ncf_scatter_compact_rows", ptr(dst), D,
                       ptr(w.uniq_u if kind == 0 else w.uniq_i), ptr(w.num_unique), kind,
                       ptr(w.G[key]), w.g.n, st)
+            if add:
+                p.grad.add_(dst)
+            elif p.grad is None:
+                p.grad = dst
         self.release_pending(st)
+
+    def grad_views(self):
+        """{name: view of the flat gradient buffer} of the dense parameters (cached per
+        buffer: assigning them as .grad after each backward allocates nothing)."""
+        c = getattr(self, "_grad_views", None)
+        if c is None or c[0] is not self.flat_grad:
+            c = self._grad_views = (self.flat_grad,
+                                    [(p, self.grad_view(n)) for n, p in self.dense_params()])
+        return c[1]

@@ -9,6 +9,7 @@ loop over users) in one HIP launch (``ncf_group_metrics``), AUC as the Mann-Whit
 on the device.  Same argument checks and errors.  Tie order inside a group: prediction desc,
 column asc (torch.topk / torch.sort leave it unspecified).  GPU only (no CPU fallback).
 """
+import warnings
 from typing import Dict, List, Optional
 
 import torch
@@ -64,9 +65,13 @@ def calculate_metrics(predictions: torch.Tensor, targets: torch.Tensor,
         out[f"mrr@{k}"] = h[4 * j + 2] / B
         out[f"map@{k}"] = h[4 * j + 3] / B
     if n_pos == 0 or n_neg == 0:
-        raise ValueError("Only one class present in y_true. ROC AUC score is not defined in "
-                         "that case.")
-    out["auc"] = float(int(s2u.item())) / (2.0 * n_pos * n_neg)
+        # scikit-learn 1.6 (the reference's pin, requirements.txt:16) returns nan with an
+        # UndefinedMetricWarning here; the reference's validate() always hits it (M = 1)
+        warnings.warn("Only one class is present in y_true. ROC AUC score is not defined in "
+                      "that case.", RuntimeWarning)
+        out["auc"] = float("nan")
+    else:
+        out["auc"] = float(int(s2u.item())) / (2.0 * n_pos * n_neg)
     base = 4 * len(ks)
     out["accuracy"] = h[base] / t.numel()
     if h[base + 1] > 0:

@@ -4,19 +4,27 @@ The reference builds ``torch.optim.Adam(self.model.parameters(), lr=..., weight_
 (src/model/trainer.py:71-75) and calls ``optimizer.zero_grad(); loss.backward();
 optimizer.step()`` (:275-285).  That call site stays unchanged: a global optimizer step
 pre-hook recognises the parameters of every live AdvancedNCF and updates them with the HIP
-kernels instead of torch's per-tensor loop —
+kernels instead of torch's per-tensor loop.  The first ``step()`` of a plain Adam binds the
+(model, optimizer) pair (``_Binding``); from then on
 
-  * embedding tables: dense-exact Adam (every row decays) streaming the table once,
-    touched rows' gradients read from the compact segment-reduce output via the slot map;
+  * embedding tables: the deferred dense-exact schedule (deferred.py) — the next training
+    forward catches up exactly its rows, ``step()`` applies the step's gradient to them and
+    sweeps one 1/64 slice of every table (bit-identical to torch's dense Adam, where coupled
+    weight decay moves every row every step, SURVEY fact 7);
   * dense parameters: one flat Adam launch over the packed buffer;
 
-with the optimizer's own lr / betas / eps / weight_decay, and state kept in
-``optimizer.state[p]`` under torch's keys (``step``, ``exp_avg``, ``exp_avg_sq``) so
-``optimizer.state_dict()`` / ``load_state_dict`` keep torch's format.  Their ``.grad`` is hidden
-for the duration of torch's own step (so torch skips them) and restored afterwards.
+all on the device step clock, with no host synchronisation.  The optimizer's own lr / betas /
+eps / weight_decay are read every step (lr changes apply to steps not yet taken).  State is kept
+in ``optimizer.state[p]`` under torch's keys (``step``, ``exp_avg``, ``exp_avg_sq``): every
+parameter of the model shares one CPU ``step`` tensor, the moments are the kernels' own buffers
+(dense ones views of a flat buffer), and the optimizer's ``state_dict`` / ``load_state_dict``
+hooks bring lagging table rows current first, so the torch format stays exact.  The
+parameters' ``.grad`` are hidden for the duration of torch's own step (so torch skips them) and
+restored afterwards.
 
-Optimizers other than plain Adam (amsgrad, maximize, foreach/fused overrides are fine; other
-classes) receive materialised dense table gradients and run unchanged.
+``SCHEDULE = "dense"`` keeps the dense per-step table sweep instead (A/B and tests).  Optimizers
+other than plain Adam (amsgrad, maximize, capturable, differentiable, tensor lr, other classes)
+receive materialised dense table gradients and run unchanged.
 """
 import weakref
 
@@ -28,6 +36,8 @@ from ._lib import ptr
 
 _models = weakref.WeakSet()
 _hooks = {}
+SCHEDULE = "deferred"      # or "dense": the per-step full-table sweep (ncf_adam_table)
+SWEEP_EVERY = 64
 
 
 def register(model):
@@ -37,16 +47,12 @@ def register(model):
         _hooks["post"] = _topt.register_optimizer_step_post_hook(_post_hook)
 
 
-def note_pending(engine):
-    pass
-
-
 def _is_plain_adam(opt):
     if type(opt) is not torch.optim.Adam:
         return False
     for g in opt.param_groups:
         if g.get("amsgrad") or g.get("maximize") or g.get("differentiable") or \
-                g.get("decoupled_weight_decay", False):
+                g.get("capturable") or g.get("decoupled_weight_decay", False):
             return False
         if isinstance(g["lr"], torch.Tensor):
             return False
@@ -54,13 +60,19 @@ def _is_plain_adam(opt):
 
 
 def _models_in(opt):
+    """The AdvancedNCF models whose four tables this optimizer holds (cached on the optimizer,
+    re-derived when its parameter groups change)."""
+    key = tuple(len(g["params"]) for g in opt.param_groups)
+    c = opt.__dict__.get("_ncf_models")
+    if c is not None and c[0] == key:
+        out = [r() for r in c[1]]
+        if all(m is not None for m in out):
+            return [m for m in out if m.engine.flat is not None and m.engine.flat.is_cuda]
     ids = {id(p) for g in opt.param_groups for p in g["params"]}
-    out = []
-    for m in list(_models):
-        tb = m.engine.table_params()
-        if all(id(p) in ids for p in tb.values()) and tb["mf_user"].is_cuda:
-            out.append(m)
-    return out
+    found = [m for m in list(_models)
+             if all(id(p) in ids for p in m.engine.table_params().values())]
+    opt.__dict__["_ncf_models"] = (key, [weakref.ref(m) for m in found])
+    return [m for m in found if m.engine.flat is not None and m.engine.flat.is_cuda]
 
 
 def _group_of(opt):
@@ -71,99 +83,258 @@ def _group_of(opt):
     return gmap
 
 
-def _state(opt, p, step_t):
-    st = opt.state[p]
-    if "exp_avg" not in st:
-        st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-        st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-    st["step"] = step_t
-    return st
+def _hp(g):
+    b1, b2 = g["betas"]
+    return float(g["lr"]), (float(b1), float(b2)), float(g["eps"]), float(g["weight_decay"])
 
 
-class _DenseMoments:
-    """Flat exp_avg / exp_avg_sq buffers parallel to the engine's flat parameter buffer."""
+def _fresh_moments(p):
+    return torch.zeros_like(p, memory_format=torch.contiguous_format)
 
-    def __init__(self, engine):
-        self.m = torch.zeros_like(engine.flat)
-        self.v = torch.zeros_like(engine.flat)
-        self.flat_ptr = engine.flat.data_ptr()
+
+class _Binding:
+    """One (AdvancedNCF, torch.optim.Adam) pair on the fused path: the deferred table schedule,
+    the flat dense moments and the device step clock, adopted from / exposed as the optimizer's
+    torch-format state."""
+
+    def __init__(self, model, opt, group):
+        from .deferred import DeferredTableAdam
+        eng = model.engine
+        eng.ensure_layout()
+        self.model = weakref.ref(model)
+        self.opt = weakref.ref(opt)
+        self.eng = eng
+        dev = eng.flat.device
+        self.tables = eng.table_params()
+        self.dense = eng.dense_params()
+        self.flat_ptr = eng.flat.data_ptr()
+        self.hp = _hp(group)
+        self.uniform = True          # every parameter so far stepped on the shared counter
+        self.step_t = torch.tensor(0.0)
+        self.m_flat = torch.zeros_like(eng.flat)
+        self.v_flat = torch.zeros_like(eng.flat)
+        self.moments = {k: {"exp_avg": _fresh_moments(p), "exp_avg_sq": _fresh_moments(p)}
+                        for k, p in self.tables.items()}
+        if eng.deferred is not None:          # another schedule (a FusedTrainStep) let go
+            eng.deferred.detach()
+        self.base_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self.clock = torch.tensor([0, self.base_seed], dtype=torch.int64, device=dev)
+        lr, betas, eps, wd = self.hp
+        self.D = None
+        if SCHEDULE == "deferred":
+            self.D = DeferredTableAdam(eng, lr, betas, eps, wd, SWEEP_EVERY,
+                                       moments=self.moments, clock=self.clock)
+            eng.clock = self.clock
+        self.adopt(opt)
+
+    # ---- torch-format state <-> kernel buffers
+    def adopt(self, opt):
+        """Take over whatever the optimizer's state holds for this model (fresh, or loaded by
+        load_state_dict: copied into the kernel buffers) and expose the kernel buffers there.
+        Every row is current at that step afterwards."""
+        eng = self.eng
+        st = opt.state
+        s0 = st.get(self.tables["mf_user"], {})
+        step = int(float(s0["step"])) if "step" in s0 else 0
+        self.step = step
+        self.step_t.fill_(float(step))
+        for k, p in self.tables.items():
+            s = st[p]
+            mine = self.moments[k]
+            for key in ("exp_avg", "exp_avg_sq"):
+                t = s.get(key)
+                if t is not None and t is not mine[key]:
+                    mine[key].copy_(t)
+                s[key] = mine[key]
+            s["step"] = self.step_t
+        for name, p in self.dense:
+            o, n, shp = eng.offsets[name]
+            s = st[p]
+            for key, buf in (("exp_avg", self.m_flat), ("exp_avg_sq", self.v_flat)):
+                view = buf[o:o + n].view(shp)
+                t = s.get(key)
+                if t is not None and t.data_ptr() != view.data_ptr():
+                    view.copy_(t.reshape(shp))
+                s[key] = view
+            s["step"] = self.step_t
+        self.uniform = True
+        if self.D is not None:
+            self.D.rebind_moments(self.moments)
+            self.D.mark_current(step)
+            self.D._ensure(step + 1)
+            self.clock[0] = step            # ncf_step_clock.t (reserved = 0)
+
+    def sync(self):
+        """Bring every lagging table row (and its moments) current: the tables and the
+        optimizer state then hold exactly torch's dense values."""
+        if self.D is not None:
+            self.D.sync()
+
+    def detach(self):
+        self.sync()
+        eng = self.eng
+        if self.D is not None and eng.deferred is self.D:
+            eng.deferred = None
+        if eng.clock is self.clock:
+            eng.clock = None
+        self.D = None
+
+    def valid(self, model):
+        return self.eng is model.engine and self.eng.flat is not None and \
+            self.eng.flat.data_ptr() == self.flat_ptr and \
+            (self.D is None or self.eng.deferred is self.D)
+
+    # ---- one optimizer step
+    def step_tables_dense_grads(self, hp, st):
+        """Tables holding dense .grad (gradient accumulation, frozen tables, user gradients):
+        bring every row current, then torch's elementwise Adam on each graded table."""
+        lr, (b1, b2), eps, wd = hp
+        self.sync()
+        stepped = False
+        for k, p in self.tables.items():
+            if p.grad is None:
+                continue
+            m = self.moments[k]
+            _lib.call("ncf_adam_flat", ptr(p), ptr(p.grad.contiguous()), ptr(m["exp_avg"]),
+                      ptr(m["exp_avg_sq"]), p.numel(), lr, b1, b2, eps, wd,
+                      float(self.step + 1), st)
+            stepped = True
+        return stepped
+
+    def run(self, opt, gmap):
+        """The fused step of this model; returns the parameters whose .grad torch must not
+        see during its own step."""
+        eng = self.eng
+        dev = eng.flat.device
+        st = _lib.stream_ptr(dev)
+        groups = {id(gmap[id(p)]) for p in self.tables.values()} | \
+            {id(gmap[id(p)]) for _, p in self.dense}
+        if len(groups) != 1:
+            raise NotImplementedError("ncf_amd: the fused Adam needs every AdvancedNCF parameter "
+                                      "in one param_group (lr/betas/eps/weight_decay shared)")
+        hp = _hp(gmap[id(self.tables["mf_user"])])
+        if hp != self.hp:
+            if self.D is not None:
+                self.D.set_hparams(*hp)
+            self.hp = hp
+        lr, (b1, b2), eps, wd = hp
+        w = eng.pending
+        frozen = any(not p.requires_grad for p in self.tables.values())
+        if w is not None and (frozen or any(p.grad is not None for p in self.tables.values())):
+            eng.materialize_table_grads(accumulate=True)
+            w = None
+        dense_with = [(n, p) for n, p in self.dense if p.grad is not None]
+        table_grads = [p for p in self.tables.values() if p.grad is not None]
+        if w is None and not table_grads and not dense_with:
+            return []
+        eng.updates += 1
+        # --- tables
+        d = self.D
+        clocked = d is not None and w is not None
+        if clocked:
+            d.apply(w, st)             # this step's rows + the rolling 1/64 sweep (clock)
+            if getattr(w, "slots_set", False):
+                eng.reset_slots(w, st)
+            eng.pending = None
+        elif w is not None:            # SCHEDULE == "dense": sweep every row of every table
+            hpf = lambda p: (lr, b1, b2, eps, wd)  # noqa: E731
+            key_of = {id(p): k for k, p in self.tables.items()}
+            eng.adam_tables(hpf, lambda p: self.moments[key_of[id(p)]], float(self.step + 1), st)
+        elif table_grads:
+            self.step_tables_dense_grads(hp, st)
+            if d is not None:
+                d.mark_current(self.step + 1)
+        # --- dense parameters (their .grad normally ARE views of the flat gradient buffer)
+        for name, p in dense_with:
+            gv = eng.grad_view(name)
+            if p.grad.data_ptr() != gv.data_ptr():
+                gv.copy_(p.grad)
+        all_dense = len(dense_with) == len(self.dense)
+        # the clock counts table steps (the deferred schedule's t): it advances iff they stepped
+        tables_stepped = d is not None and (clocked or bool(table_grads))
+        if all_dense and self.uniform and clocked:
+            # the step's dense Adam + the clock advance in one launch (as FusedTrainStep)
+            _lib.call("ncf_adam_flat_clock_close", ptr(eng.flat), ptr(eng.flat_grad),
+                      ptr(self.m_flat), ptr(self.v_flat), eng.flat.numel(), ptr(d._table), 1,
+                      ptr(self.clock), b1, b2, eps, wd, self.base_seed, st)
+        else:
+            step = float(self.step + 1)
+            if all_dense and self.uniform:
+                _lib.call("ncf_adam_flat", ptr(eng.flat), ptr(eng.flat_grad), ptr(self.m_flat),
+                          ptr(self.v_flat), eng.flat.numel(), lr, b1, b2, eps, wd, step, st)
+            else:
+                # some dense parameters without a gradient (frozen / unused): each graded one
+                # on its own (they share the model's step counter)
+                self.uniform = self.uniform and all_dense
+                for name, p in dense_with:
+                    o, n, _ = eng.offsets[name]
+                    _lib.call("ncf_adam_flat", ptr(eng.flat) + 4 * o, ptr(eng.flat_grad) + 4 * o,
+                              ptr(self.m_flat) + 4 * o, ptr(self.v_flat) + 4 * o, n, lr, b1, b2,
+                              eps, wd, step, st)
+            if tables_stepped:
+                _lib.call("ncf_step_clock_advance", ptr(self.clock), self.base_seed, st)
+        self.step += 1
+        self.step_t += 1
+        return [p for _, p in self.dense] + list(self.tables.values())
+
+
+def _bindings(opt):
+    b = opt.__dict__.get("_ncf_bind")
+    if b is None:
+        b = opt.__dict__["_ncf_bind"] = {}
+        opt.register_state_dict_pre_hook(_opt_state_dict_pre)
+        opt.register_load_state_dict_pre_hook(_opt_load_pre)
+        opt.register_load_state_dict_post_hook(_opt_load_post)
+    return b
+
+
+def _opt_state_dict_pre(opt):
+    for b in list(opt.__dict__.get("_ncf_bind", {}).values()):
+        b.sync()
+
+
+def _opt_load_pre(opt, state_dict):
+    for b in list(opt.__dict__.get("_ncf_bind", {}).values()):
+        b.sync()       # nothing owed from the old run may be replayed onto the loaded rows
+    return None
+
+
+def _opt_load_post(opt):
+    for b in list(opt.__dict__.get("_ncf_bind", {}).values()):
+        b.adopt(opt)
+
+
+def binding_of(opt, model):
+    """The fused-path binding of (optimizer, model), if that pair has stepped."""
+    return opt.__dict__.get("_ncf_bind", {}).get(id(model))
 
 
 def _pre_hook(opt, args, kwargs):
     models = _models_in(opt)
     if not models:
         return None
-    stash = []
     if not _is_plain_adam(opt):
         for m in models:
+            b = opt.__dict__.get("_ncf_bind", {}).pop(id(m), None)
+            if b is not None:
+                b.detach()
+            elif m.engine.deferred is not None:
+                m.engine.deferred.detach()
             m.engine.materialize_table_grads()
         return None
     gmap = _group_of(opt)
+    binds = _bindings(opt)
+    stash = []
     for m in models:
-        eng = m.engine
-        eng.ensure_layout() if eng.flat is None else None
-        dev = eng.flat.device
-        st = _lib.stream_ptr(dev)
-        dense = eng.dense_params()
-        tables = eng.table_params()
-        have_dense = all(p.grad is not None for _, p in dense)
-        have_tables = eng.pending is not None or any(p.grad is not None for p in tables.values())
-        if not have_dense and not have_tables:
-            continue
-        # one step counter shared by every parameter of this model (they always step together)
-        anyp = tables["mf_user"]
-        st0 = opt.state[anyp].get("step")
-        if isinstance(st0, torch.Tensor):
-            step_t = st0
-        else:
-            step_t = torch.tensor(0.0, dtype=torch.float32)
-        step_t += 1
-        step = float(step_t.item())
-        eng.updates += 1
-
-        def hp(p):
-            g = gmap[id(p)]
-            b1, b2 = g["betas"]
-            return float(g["lr"]), float(b1), float(b2), float(g["eps"]), float(g["weight_decay"])
-
-        # --- tables (dense-exact)
-        eng.adam_tables(hp, lambda p: _state(opt, p, step_t), step, st)
-        # --- dense params: flat buffers; moments exposed as views in optimizer.state
-        mom = getattr(eng, "_moments", None)
-        if mom is None or mom.flat_ptr != eng.flat.data_ptr():
-            mom = _DenseMoments(eng)
-            eng._moments = mom
-            for name, p in dense:      # adopt existing state (e.g. after load_state_dict)
-                s = opt.state.get(p)
-                o, n, shp = eng.offsets[name]
-                if s and "exp_avg" in s:
-                    mom.m[o:o + n].copy_(s["exp_avg"].reshape(-1))
-                    mom.v[o:o + n].copy_(s["exp_avg_sq"].reshape(-1))
-        for name, p in dense:
-            o, n, shp = eng.offsets[name]
-            s = opt.state[p]
-            mv, vv = mom.m[o:o + n].view(shp), mom.v[o:o + n].view(shp)
-            if s.get("exp_avg") is not None and s["exp_avg"].data_ptr() != mv.data_ptr():
-                mv.copy_(s["exp_avg"])
-                vv.copy_(s["exp_avg_sq"])
-            s["step"] = step_t
-            s["exp_avg"], s["exp_avg_sq"] = mv, vv
-            if p.grad is not None and p.grad.data_ptr() != eng.grad_view(name).data_ptr():
-                eng.grad_view(name).copy_(p.grad)
-        groups = {id(gmap[id(p)]) for _, p in dense}
-        if have_dense and len(groups) == 1:
-            lr, b1, b2, eps, wd = hp(dense[0][1])
-            _lib.call("ncf_adam_flat", ptr(eng.flat), ptr(eng.flat_grad), ptr(mom.m), ptr(mom.v),
-                      eng.flat.numel(), lr, b1, b2, eps, wd, step, st)
-        elif have_dense:
-            for name, p in dense:
-                o, n, _ = eng.offsets[name]
-                lr, b1, b2, eps, wd = hp(p)
-                _lib.call("ncf_adam_flat", ptr(eng.flat[o:]), ptr(eng.flat_grad[o:]),
-                          ptr(mom.m[o:]), ptr(mom.v[o:]), n, lr, b1, b2, eps, wd, step, st)
-        for _, p in list(dense) + list(tables.items()):
-            stash.append((p, p.grad))
-            p.grad = None
+        b = binds.get(id(m))
+        if b is None or not b.valid(m):
+            if b is not None:
+                b.detach()
+            b = binds[id(m)] = _Binding(m, opt, gmap[id(m.engine.table_params()["mf_user"])])
+        for p in b.run(opt, gmap):
+            if p.grad is not None:
+                stash.append((p, p.grad))
+                p.grad = None
     opt._ncf_stash = stash
     return None
 

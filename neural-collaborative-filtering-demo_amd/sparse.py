@@ -144,13 +144,40 @@ class KeyedJaggedTensor:
 
 
 class _Bag(nn.Module):
-    """Holds one table; the parameter is named ``weight`` like nn.EmbeddingBag."""
+    """Holds one table; the parameter is named ``weight`` like nn.EmbeddingBag.
+
+    A deferred dense-exact optimizer (deferred.py) may hold rows of the table behind the step
+    count; every read of the table through this module — ``bag.weight``, ``state_dict()`` of
+    the bag or of any module above it, the collection's forward — first brings them current
+    (``_sync``, installed by the owning AdvancedNCF).  The kernels use ``raw_weight()``."""
 
     def __init__(self, num_embeddings: int, embedding_dim: int):
         super().__init__()
         self.num_embeddings = num_embeddings
         self.embedding_dim = embedding_dim
+        self._sync = None
         self.weight = nn.Parameter(torch.empty(num_embeddings, embedding_dim))
+        self.register_state_dict_pre_hook(_bag_state_dict_pre)
+
+    @property
+    def weight(self):
+        p = self.__dict__["_parameters"].get("weight")
+        if p is None:
+            raise AttributeError("weight")
+        s = self.__dict__.get("_sync")
+        if s is not None:
+            s()
+        return p
+
+    def raw_weight(self) -> nn.Parameter:
+        """The parameter itself, without bringing lagging rows current (kernel plumbing)."""
+        return self._parameters["weight"]
+
+
+def _bag_state_dict_pre(module, prefix, keep_vars):
+    s = module.__dict__.get("_sync")
+    if s is not None:
+        s()
 
 
 class EmbeddingBagCollection(nn.Module):
@@ -190,8 +217,13 @@ class EmbeddingBagCollection(nn.Module):
             bag = self.embedding_bags[t.name]
             for f in t.feature_names:
                 if f in ids:
-                    out[f] = gather_rows(bag.weight, ids[f])
+                    out[f] = gather_rows(bag.weight, ids[f])   # (.weight: rows current)
         return out
+
+    def set_sync(self, fn):
+        """Install the callable that brings lagging table rows current before a read."""
+        for bag in self.embedding_bags.values():
+            bag._sync = fn
 
 
 def gather_rows(table: torch.Tensor, ids: torch.Tensor, gamma=None, beta=None, eps=1e-5) -> torch.Tensor:

@@ -12,7 +12,7 @@ BCE + backward kernels, fused Adam — identical math, one kernel sequence on on
 what the benchmark times (and what a production trainer uses).
 """
 import logging
-from typing import Any, Dict, Optional
+from typing import Any, Dict, Optional  # noqa: F401
 
 import torch
 import torch.nn as nn
@@ -43,6 +43,7 @@ class FusedTrainStep:
                  clock: Optional[bool] = None, warmup: int = 2, concurrent: Optional[bool] = None,
                  overlap_sweep: bool = False):
         self.model = model
+        self.deferred = None
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.step_count = 0
         eng = model.engine
@@ -83,6 +84,19 @@ class FusedTrainStep:
         self._static = None
         self._w = None
         self._eager_steps = 0
+
+    @property
+    def lr(self):
+        return self._lr
+
+    @lr.setter
+    def lr(self, value):
+        """The learning rate of the steps not yet taken, for the dense parameters and the
+        deferred table schedule alike (its per-step scalar table is refilled from step t + 1;
+        a captured graph reads that table, so it needs no re-capture)."""
+        self._lr = float(value)
+        if self.deferred is not None:
+            self.deferred.lr = self._lr
 
     def _body(self, user_ids, item_ids, targets, M):
         m = self.model
@@ -189,7 +203,10 @@ class FusedTrainStep:
             return w
         dev = m.engine.flat.device
         shape = (user_ids.numel(), item_ids.numel(), targets.numel(), M)
-        horizon_ok = self.deferred._filled >= self.deferred.t + 2
+        d = self.deferred
+        if d._hp_filled is not None and d._hp_filled != (d.lr,) + tuple(d.betas):
+            d._ensure(d._filled)        # lr changed: refill steps > t in place (same buffer)
+        horizon_ok = d._filled >= d.t + 2
         if self._g is None or self._shape != shape or not horizon_ok:
             if self._eager_steps < self.warmup or not horizon_ok:
                 # eager clock-driven steps: allocate every workspace, set kernel attributes
@@ -313,8 +330,11 @@ class ModelTrainer:
         self.model = self.model.to(self.device)
 
     def train_epoch(self, train_loader) -> float:
+        """trainer.py:216-337.  The per-batch loss is summed on the device and read once at the
+        end of the epoch (the reference reads it, and three accuracies, with .item() every
+        batch for its progress bar: four host syncs per step)."""
         self.model.train()
-        total_loss, num_batches = 0.0, 0
+        total_loss, num_batches = None, 0
         for batch_idx, (features, targets) in enumerate(train_loader):
             base_batch_size = len(features.lengths()) // len(features.keys())
             effective_batch_size = base_batch_size * (1 + self.negative_samples)
@@ -331,8 +351,83 @@ class ModelTrainer:
             self.optimizer.zero_grad()
             loss.backward()
             self.optimizer.step()
-            total_loss += loss.item()
+            total_loss = loss.detach() if total_loss is None else total_loss + loss.detach()
             num_batches += 1
-        avg = total_loss / num_batches if num_batches > 0 else float("inf")
+        avg = float(total_loss) / num_batches if num_batches > 0 else float("inf")
         log.info("Epoch complete - Average loss: %.4f", avg)
         return avg
+
+    def validate(self, val_loader) -> Dict[str, float]:
+        """trainer.py:350-410: eval forward (M = 1) over the loader, BCE loss, then
+        calculate_metrics over every prediction with k = 1, 5, 10 and no negatives (each row is
+        its own group, as in the reference); ``loss`` = mean per-batch loss."""
+        from .metrics import calculate_metrics
+        self.model.eval()
+        total_loss = None
+        outs, tgts = [], []
+        with torch.no_grad():
+            for features, targets in val_loader:
+                features = features.to(self.device)
+                targets = targets.to(self.device)
+                outputs = self.model(features)
+                loss = self.criterion(outputs, targets)
+                total_loss = loss if total_loss is None else total_loss + loss
+                outs.append(outputs)
+                tgts.append(targets)
+        all_out, all_t = torch.cat(outs, 0), torch.cat(tgts, 0)
+        metrics = calculate_metrics(predictions=all_out, targets=all_t, k_values=[1, 5, 10],
+                                    batch_size=len(all_t), negative_samples=0)
+        metrics["loss"] = float(total_loss) / len(val_loader)
+        metrics["val_loss"] = metrics["loss"]
+        for name, value in metrics.items():
+            log.info("- %s: %.4f", name, value)
+        return metrics
+
+    def train(self, train_loader, val_loader, num_epochs: int, early_stopping_patience: int = 5,
+              checkpoint_dir: Optional[str] = None) -> Dict[str, list]:
+        """trainer.py:412-546: epochs of train_epoch + validate with early stopping on the
+        validation loss and (with ``checkpoint_dir``) per-epoch checkpoints in the trainer
+        format (checkpoint.py; ``best_model.pt`` for the best, resume from the latest)."""
+        import glob
+        import os
+        from .checkpoint import load_checkpoint, save_checkpoint
+        best, patience, start = float("inf"), 0, 0
+        history = {"train_loss": [], "val_loss": [], "val_hit_rate": [], "val_ndcg": [],
+                   "learning_rate": []}
+        if checkpoint_dir:
+            os.makedirs(checkpoint_dir, exist_ok=True)
+            found = sorted(glob.glob(os.path.join(checkpoint_dir, "checkpoint_epoch_*.pt")),
+                           key=lambda p: int(p.rsplit("_", 1)[1].split(".")[0]))
+            if found:
+                start = load_checkpoint(found[-1], self.model, self.optimizer)
+        epoch, val_metrics = start, None
+        try:
+            for epoch in range(start, num_epochs):
+                history["train_loss"].append(self.train_epoch(train_loader))
+                val_metrics = self.validate(val_loader)
+                history["val_loss"].append(val_metrics["loss"])
+                history["val_hit_rate"].append(val_metrics.get("hit_rate@10"))
+                history["val_ndcg"].append(val_metrics.get("ndcg@10"))
+                history["learning_rate"].append(self.optimizer.param_groups[0]["lr"])
+                improved = val_metrics["loss"] < best
+                if improved:
+                    best, patience = val_metrics["loss"], 0
+                else:
+                    patience += 1
+                if checkpoint_dir:
+                    path = os.path.join(checkpoint_dir, f"checkpoint_epoch_{epoch + 1}.pt")
+                    save_checkpoint(path, self.model, self.optimizer, epoch, val_metrics,
+                                    self.config)
+                    if improved:
+                        save_checkpoint(os.path.join(checkpoint_dir, "best_model.pt"),
+                                        self.model, self.optimizer, epoch, val_metrics,
+                                        self.config)
+                if patience >= early_stopping_patience:
+                    log.info("Early stopping triggered after %d epochs", epoch + 1)
+                    break
+            return history
+        except Exception:
+            if checkpoint_dir:
+                save_checkpoint(os.path.join(checkpoint_dir, "emergency_checkpoint.pt"),
+                                self.model, self.optimizer, epoch, val_metrics, self.config)
+            raise

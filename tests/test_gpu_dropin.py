@@ -1,0 +1,273 @@
+"""The reference call pattern on the fused path (src/model/trainer.py:258-285: ``model(kjt)`` ->
+``nn.BCELoss`` -> ``zero_grad`` -> ``backward`` -> ``torch.optim.Adam.step``), and everything
+that reads the tables while a deferred dense-exact schedule holds rows behind.  MI355X only.
+
+Equalities here are bitwise: the deferred schedule replays every zero-gradient step with the
+arithmetic and per-step scalars of the dense sweep, so the two must agree to the bit."""
+import numpy as np
+import pytest
+import torch
+
+import _ncf_pkg
+
+pytestmark = pytest.mark.gpu
+ncf = _ncf_pkg.load()
+DEV = torch.device("cuda:0")
+U, I, B, M = 3000, 500, 64, 5
+
+
+def kjt(u, i):
+    return ncf.KeyedJaggedTensor.from_lengths_sync(
+        keys=["user_id", "product_id"], values=torch.cat([u, i]),
+        lengths=torch.ones(2 * u.numel(), dtype=torch.long, device=u.device))
+
+
+def batches(n, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n):
+        u = torch.randint(0, U, (B,), generator=g).repeat_interleave(M).to(DEV)
+        i = torch.randint(0, I, (B * M,), generator=g).to(DEV)
+        t = torch.zeros(B, M)
+        t[:, 0] = 1
+        out.append((u, i, t.reshape(-1, 1).to(DEV)))
+    return out
+
+
+def model(dropout=0.0, seed=11):
+    torch.manual_seed(seed)
+    return ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, dropout, M - 1).to(DEV)
+
+
+def reference_loop(m, opt, data, lr_at=None):
+    """trainer.py:258-285 (no clipping: the reference's guard is always False)."""
+    crit = torch.nn.BCELoss()
+    m.train()
+    for s, (u, i, t) in enumerate(data):
+        if lr_at and s in lr_at:
+            for g in opt.param_groups:
+                g["lr"] = lr_at[s]
+        out = m(kjt(u, i))
+        loss = crit(out, t)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    return loss
+
+
+def snapshot(m, opt):
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    st = opt.state_dict()["state"]
+    mom = {k: {n: (v.cpu().clone() if torch.is_tensor(v) else v) for n, v in s.items()}
+           for k, s in st.items()}
+    return sd, mom
+
+
+def assert_same(a, b):
+    for k in a[0]:
+        assert torch.equal(a[0][k], b[0][k]), k
+    assert set(a[1]) == set(b[1])
+    for k in a[1]:
+        for n in ("exp_avg", "exp_avg_sq", "step"):
+            assert torch.equal(a[1][k][n], b[1][k][n]), (k, n)
+
+
+def run_schedule(schedule, data, monkeypatch, lr_at=None):
+    from ncf_amd import optim
+    monkeypatch.setattr(optim, "SCHEDULE", schedule)
+    m = model()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+    reference_loop(m, opt, data, lr_at)
+    return snapshot(m, opt), m, opt
+
+
+def test_hooked_deferred_bitwise_equals_dense_hook(monkeypatch):
+    """torch.optim.Adam.step() through the hook: the deferred schedule (catch-up in the
+    forward, apply + 1/64 sweep in the step) == the dense per-step table sweep, bit for bit,
+    over 70 steps (crossing a full sweep cycle), params and the optimizer's torch-format state."""
+    data = batches(70)
+    a, _, _ = run_schedule("dense", data, monkeypatch)
+    b, m, opt = run_schedule("deferred", data, monkeypatch)
+    assert_same(a, b)
+    from ncf_amd import optim
+    assert optim.binding_of(opt, m).D is not None     # the deferred path really ran
+
+
+def test_hooked_lr_change_bitwise_equals_dense_hook(monkeypatch):
+    """An lr change mid-run (a scheduler) applies to the steps not yet taken; rows still behind
+    replay the earlier steps with the lr those steps had."""
+    data = batches(40, seed=8)
+    lr_at = {13: 3e-3, 29: 5e-4}
+    a, _, _ = run_schedule("dense", data, monkeypatch, lr_at)
+    b, _, _ = run_schedule("deferred", data, monkeypatch, lr_at)
+    assert_same(a, b)
+
+
+def test_hooked_state_dict_roundtrip_resumes_exactly(monkeypatch):
+    """opt.state_dict() / model.state_dict() mid-run (rows current first), loaded into a fresh
+    model + torch Adam, then continued == the uninterrupted run."""
+    data = batches(30, seed=9)
+    whole, _, _ = run_schedule("deferred", data, monkeypatch)
+    m1 = model()
+    o1 = torch.optim.Adam(m1.parameters(), lr=1e-3, weight_decay=1e-5)
+    reference_loop(m1, o1, data[:17])
+    msd = {k: v.clone() for k, v in m1.state_dict().items()}
+    osd = o1.state_dict()
+    m2 = model(seed=99)
+    o2 = torch.optim.Adam(m2.parameters(), lr=1e-3, weight_decay=1e-5)
+    m2.load_state_dict(msd)
+    o2.load_state_dict(osd)
+    reference_loop(m2, o2, data[17:])
+    assert_same(whole, snapshot(m2, o2))
+
+
+def test_load_state_dict_mid_run_does_not_replay_old_steps(tmp_path):
+    """a checkpoint loaded into a model whose deferred schedule still owes rows
+    zero-gradient steps must not get those steps replayed onto the loaded rows.  Train 12 steps,
+    load the step-5 checkpoint into the same model + step, continue: == a fresh model resumed
+    from the same checkpoint."""
+    from ncf_amd.checkpoint import load_checkpoint, save_checkpoint
+    from ncf_amd.trainer import FusedTrainStep
+    data = batches(20, seed=12)
+
+    def fresh():
+        m = model(seed=4)
+        return m, FusedTrainStep(m, lr=1e-2, weight_decay=1e-5)
+    m1, s1 = fresh()
+    for b in data[:5]:
+        s1(*b)
+    path = str(tmp_path / "ck.pt")
+    save_checkpoint(path, m1, s1, epoch=0)
+    for b in data[5:12]:
+        s1(*b)
+    load_checkpoint(path, m1, s1)          # rows of steps 6..12 still lag here
+    for b in data[12:]:
+        s1(*b)
+    m2, s2 = fresh()
+    load_checkpoint(path, m2, s2)
+    for b in data[12:]:
+        s2(*b)
+    a, b_ = m1.state_dict(), m2.state_dict()
+    for k in a:
+        assert torch.equal(a[k], b_[k]), k
+
+
+def test_direct_table_readers_see_current_rows():
+    """after FusedTrainSteps on the deferred schedule, every direct read of the
+    tables — the collection's forward (app.py:156 ``model.mlp_embedding_collection(kjt)``), a
+    bag's ``.weight``, a submodule's state_dict — equals the dense schedule's rows bitwise."""
+    from ncf_amd.trainer import FusedTrainStep
+    data = batches(10, seed=13)
+    res = []
+    for deferred in (False, True):
+        m = model(seed=21)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5, deferred=deferred)
+        for b in data:
+            step(*b)
+        ids = torch.arange(0, U, 7, device=DEV)
+        feats = kjt(ids, ids % I)
+        coll = m.mlp_embedding_collection(feats)
+        if deferred:
+            assert not m.engine.lagging()          # the read above brought every row current
+        w = m.mf_embedding_collection.embedding_bags["product_id"].weight.detach().clone()
+        sub = m.mlp_embedding_collection.state_dict()
+        res.append((coll["user_id"].cpu(), coll["product_id"].cpu(), w.cpu(),
+                    {k: v.cpu().clone() for k, v in sub.items()}))
+    for x, y in zip(res[0][:3], res[1][:3]):
+        assert torch.equal(x, y)
+    for k in res[0][3]:
+        assert torch.equal(res[0][3][k], res[1][3][k]), k
+
+
+def test_bag_weight_read_syncs_lagging_rows():
+    from ncf_amd.trainer import FusedTrainStep
+    m = model(seed=22)
+    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+    for b in batches(3, seed=14):
+        step(*b)
+    assert m.engine.lagging()
+    _ = m.mlp_embedding_collection.embedding_bags["user_id"].weight
+    assert not m.engine.lagging()
+
+
+def test_gradient_accumulation_equals_doubled_loss(monkeypatch):
+    """Two backward() calls before one step() accumulate (table rows included): == one
+    backward of twice the loss (the same batch; x2 is exact in fp32)."""
+    from ncf_amd import optim
+    monkeypatch.setattr(optim, "SCHEDULE", "deferred")
+    data = batches(6, seed=15)
+    crit = torch.nn.BCELoss()
+    out = []
+    for accumulate in (True, False):
+        m = model(seed=23)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+        m.train()
+        for u, i, t in data:
+            opt.zero_grad()
+            if accumulate:
+                crit(m(kjt(u, i)), t).backward()
+                crit(m(kjt(u, i)), t).backward()
+            else:
+                (2.0 * crit(m(kjt(u, i)), t)).backward()
+            opt.step()
+        out.append(snapshot(m, opt))
+    for k in out[0][0]:
+        torch.testing.assert_close(out[0][0][k], out[1][0][k], rtol=0, atol=1e-7, msg=k)
+
+
+def test_zero_grad_between_backwards_discards_first(monkeypatch):
+    """backward, zero_grad, backward, step == backward, step (the first gradient dropped)."""
+    data = batches(4, seed=16)
+    crit = torch.nn.BCELoss()
+    out = []
+    for extra in (True, False):
+        m = model(seed=24)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+        m.train()
+        for s, (u, i, t) in enumerate(data):
+            if extra:
+                crit(m(kjt(data[-1 - s][0], data[-1 - s][1])), data[-1 - s][2]).backward()
+                opt.zero_grad(set_to_none=(s % 2 == 0))
+            loss = crit(m(kjt(u, i)), t)
+            opt.zero_grad(set_to_none=(s % 2 == 1))
+            loss.backward()
+            opt.step()
+        out.append(snapshot(m, opt))
+    assert_same(out[0], out[1])
+
+
+def test_out_of_range_id_in_training_raises_without_sync():
+    m = model(seed=25)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    crit = torch.nn.BCELoss()
+    u, i, t = batches(1, seed=17)[0]
+    i = i.clone()
+    i[3] = I + 5
+    m.train()
+    with pytest.raises(IndexError):
+        for _ in range(4 * m.engine.ID_CHECK_EVERY):
+            loss = crit(m(kjt(u, i)), t)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            torch.cuda.synchronize()
+    m.validate_ids = "sync"
+    with pytest.raises(IndexError):
+        m(kjt(u, i))
+
+
+def test_trainer_train_epoch_runs_reference_loop():
+    """ModelTrainer.train_epoch (trainer.py:216-337 mirror) over a device-sampled epoch."""
+    from ncf_amd.trainer import ModelTrainer
+    m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.2, 4)
+    tr = ModelTrainer(m, {"num_users": U, "num_products": I, "batch_size": B,
+                          "learning_rate": 1e-3, "weight_decay": 1e-5})
+    loader = []
+    for u, i, t in batches(8, seed=18):
+        loader.append((kjt(u, i), t))
+    a = tr.train_epoch(loader)
+    b = tr.train_epoch(loader)
+    assert np.isfinite(a) and np.isfinite(b) and b < a
+    ev = tr.validate([(kjt(u[::M].contiguous(), i[::M].contiguous()), t[::M].contiguous())
+                      for (u, i, t) in batches(3, seed=19)])
+    assert np.isfinite(ev["val_loss"]) and 0.0 <= ev["accuracy"] <= 1.0
