@@ -19,3 +19,12 @@ for p in "${pids[@]}"; do wait "$p"; done
 "$HIPCC" --offload-arch=gfx950 -shared -fPIC "$OBJ"/*.o -o "$OUT.tmp"
 mv "$OUT.tmp" "$OUT"
 echo "built $OUT"
+# CPython fast-call binding of the C-ABI (generated from _lib.SIGNATURES; ctypes stays the
+# loader and hands it the resolved entry points)
+PYINC="$(python3 -c 'import sysconfig; print(sysconfig.get_paths()["include"])')"
+PYSUF="$(python3 -c 'import sysconfig; print(sysconfig.get_config_var("EXT_SUFFIX"))')"
+python3 "$SRC/gen_fastcall.py" "$OBJ/_ncffast.c"
+FAST="$(dirname "$OUT")/_ncffast$PYSUF"
+gcc -O2 -shared -fPIC -I"$PYINC" "$OBJ/_ncffast.c" -o "$FAST.tmp"
+mv "$FAST.tmp" "$FAST"
+echo "built $FAST"

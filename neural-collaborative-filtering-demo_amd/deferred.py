@@ -19,6 +19,7 @@ contraction-free arithmetic, so the result is bit-identical to the dense sweep (
 work moves from HBM traffic (24 B/element/step) to VALU (~15 flops/element/step, amortised).
 """
 import ctypes
+import itertools
 
 import numpy as np
 import torch
@@ -27,12 +28,14 @@ from . import _lib
 from ._lib import ptr
 
 _KINDS = (("user", "mf_user", "mlp_user"), ("item", "mf_item", "mlp_item"))
+_SERIAL = itertools.count(1)      # distinguishes schedules in workspace caches (ids recycle)
 
 
 class DeferredTableAdam:
     def __init__(self, engine, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  sweep_every: int = 64, moments=None, clock=None, overlap_sweep=None):
         self.engine = engine
+        self._serial = next(_SERIAL)
         # clock (ncf_step_clock, device): every step-dependent value is read on the device, so
         # the launches of a step do not depend on the host counter (hipGraph capture)
         self.clock = clock
@@ -121,6 +124,17 @@ class DeferredTableAdam:
         """Use other exp_avg / exp_avg_sq tensors (e.g. after an optimizer state load)."""
         self.state = moments
         self.__dict__.pop("_sweep_pairs", None)
+        self._gen = getattr(self, "_gen", 0) + 1
+
+    def _pairs_for(self, w):
+        """_pairs(w), cached on the workspace (its buffers, the tables and the moments are
+        fixed while the key holds)."""
+        key = ("pairs", self._serial, getattr(self, "_gen", 0), w.uniq_u.data_ptr(),
+               w.uniq_i.data_ptr())
+        p = w.cache.get(key)
+        if p is None:
+            p = w.cache[key] = self._pairs(w)
+        return p
 
     def _consts(self):
         b1, b2 = self.betas
@@ -253,7 +267,7 @@ class DeferredTableAdam:
         w.deduped = True
         if self.clock is not None and n > 0:   # both kinds in one launch
             self._ensure(self.t + 1)
-            pairs = self._pairs(w)
+            pairs = self._pairs_for(w)
             _lib.call("ncf_adam_pairs_catchup_clock", ctypes.addressof(pairs), 2,
                       m.mlp_embedding_dim, ptr(w.num_unique), n, 0, ptr(self.clock),
                       ptr(self._table), *self._consts(), st)
@@ -268,7 +282,7 @@ class DeferredTableAdam:
             self._ensure(self.t + 1)
             self.sweep_join()
             if n > 0:
-                pairs = self._pairs(w)
+                pairs = self._pairs_for(w)
                 _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2,
                           self.engine.model.mlp_embedding_dim, ptr(w.num_unique), n, 1,
                           ptr(self.clock), ptr(self._table), *self._consts(), st)

@@ -274,8 +274,7 @@ class NCFEngine:
         key = getattr(self, "_layout_key", None)
         if key is not None and self.flat is not None:
             plist, ptrs = key
-            if all(p.data_ptr() == q for p, q in zip(plist, ptrs)) and \
-                    self.model.mf_norm.weight is plist[0]:
+            if [p.data_ptr() for p in plist] == ptrs and self.model.mf_norm.weight is plist[0]:
                 return
         ps = self.dense_params()
         if self.flat is None or any(not self.is_flat_view(p) for _, p in ps) or \
@@ -496,7 +495,11 @@ class NCFEngine:
         NCF_ATTN_BLOCK=0 forces the unfused launches (A/B measurement, parity tests)."""
         if os.environ.get("NCF_ATTN_BLOCK", "1") == "0":
             return False
-        return bool(_lib.query("ncf_attn_block_supported", D, H, M))
+        key = ("attn", D, H, M)
+        ok = self._mlp_ok.get(key)
+        if ok is None:
+            ok = self._mlp_ok[key] = bool(_lib.query("ncf_attn_block_supported", D, H, M))
+        return ok
 
     def _attention_unfused(self, w, M, train, drop_p, seed, temporal, st):
         """a5 as separate launches (q/k/v projections, core, out_proj): any D, M <= 64, and the

@@ -19,8 +19,8 @@ in ``optimizer.state[p]`` under torch's keys (``step``, ``exp_avg``, ``exp_avg_s
 parameter of the model shares one CPU ``step`` tensor, the moments are the kernels' own buffers
 (dense ones views of a flat buffer), and the optimizer's ``state_dict`` / ``load_state_dict``
 hooks bring lagging table rows current first, so the torch format stays exact.  The
-parameters' ``.grad`` are hidden for the duration of torch's own step (so torch skips them) and
-restored afterwards.
+parameters the fused step updated are taken out of the param groups for the duration of
+torch's own step (so torch's loop never sees them) and put back afterwards.
 
 ``SCHEDULE = "dense"`` keeps the dense per-step table sweep instead (A/B and tests).  Optimizers
 other than plain Adam (amsgrad, maximize, capturable, differentiable, tensor lr, other classes)
@@ -76,10 +76,17 @@ def _models_in(opt):
 
 
 def _group_of(opt):
+    """{id(param): its param_group} (cached on the optimizer while its groups keep their
+    parameter lists)."""
+    key = tuple((id(g), len(g["params"])) for g in opt.param_groups)
+    c = opt.__dict__.get("_ncf_gmap")
+    if c is not None and c[0] == key:
+        return c[1]
     gmap = {}
     for g in opt.param_groups:
         for p in g["params"]:
             gmap[id(p)] = g
+    opt.__dict__["_ncf_gmap"] = (key, gmap)
     return gmap
 
 
@@ -207,12 +214,16 @@ class _Binding:
         eng = self.eng
         dev = eng.flat.device
         st = _lib.stream_ptr(dev)
-        groups = {id(gmap[id(p)]) for p in self.tables.values()} | \
-            {id(gmap[id(p)]) for _, p in self.dense}
-        if len(groups) != 1:
-            raise NotImplementedError("ncf_amd: the fused Adam needs every AdvancedNCF parameter "
-                                      "in one param_group (lr/betas/eps/weight_decay shared)")
-        hp = _hp(gmap[id(self.tables["mf_user"])])
+        group = gmap[id(self.tables["mf_user"])]
+        if self.__dict__.get("_group") is not group:
+            groups = {id(gmap[id(p)]) for p in self.tables.values()} | \
+                {id(gmap[id(p)]) for _, p in self.dense}
+            if len(groups) != 1:
+                raise NotImplementedError("ncf_amd: the fused Adam needs every AdvancedNCF "
+                                          "parameter in one param_group (lr/betas/eps/"
+                                          "weight_decay shared)")
+            self._group = group
+        hp = _hp(group)
         if hp != self.hp:
             if self.D is not None:
                 self.D.set_hparams(*hp)
@@ -245,10 +256,10 @@ class _Binding:
             if d is not None:
                 d.mark_current(self.step + 1)
         # --- dense parameters (their .grad normally ARE views of the flat gradient buffer)
-        for name, p in dense_with:
-            gv = eng.grad_view(name)
-            if p.grad.data_ptr() != gv.data_ptr():
-                gv.copy_(p.grad)
+        for p, gv in eng.grad_views():
+            g = p.grad
+            if g is not None and g is not gv and g.data_ptr() != gv.data_ptr():
+                gv.copy_(g)
         all_dense = len(dense_with) == len(self.dense)
         # the clock counts table steps (the deferred schedule's t): it advances iff they stepped
         tables_stepped = d is not None and (clocked or bool(table_grads))
@@ -275,7 +286,14 @@ class _Binding:
                 _lib.call("ncf_step_clock_advance", ptr(self.clock), self.base_seed, st)
         self.step += 1
         self.step_t += 1
-        return [p for _, p in self.dense] + list(self.tables.values())
+        return self._all_params
+
+    @property
+    def _all_params(self):
+        c = self.__dict__.get("_allp")
+        if c is None:
+            c = self._allp = [p for _, p in self.dense] + list(self.tables.values())
+        return c
 
 
 def _bindings(opt):
@@ -309,7 +327,33 @@ def binding_of(opt, model):
     return opt.__dict__.get("_ncf_bind", {}).get(id(model))
 
 
+def _restore_groups(opt):
+    swap = opt.__dict__.pop("_ncf_swap", None)
+    if swap:
+        for g, ps in swap:
+            g["params"] = ps
+
+
+def _hide(opt, hidden):
+    """Take the parameters the fused step just updated out of the param groups for the
+    duration of torch's own step (restored by the post hook): torch's loop then never sees
+    them — one list swap per group instead of hiding and restoring every .grad."""
+    cache = opt.__dict__.setdefault("_ncf_keep", {})
+    hk = frozenset(hidden)
+    swap = []
+    for g in opt.param_groups:
+        ps = g["params"]
+        c = cache.get(id(g))
+        if c is None or c[0] is not ps or c[1] != len(ps) or c[2] != hk:
+            c = cache[id(g)] = (ps, len(ps), hk, [p for p in ps if id(p) not in hidden])
+        if len(c[3]) != len(ps):
+            swap.append((g, ps))
+            g["params"] = c[3]
+    opt._ncf_swap = swap
+
+
 def _pre_hook(opt, args, kwargs):
+    _restore_groups(opt)        # (a previous step that raised inside torch's body)
     models = _models_in(opt)
     if not models:
         return None
@@ -324,24 +368,18 @@ def _pre_hook(opt, args, kwargs):
         return None
     gmap = _group_of(opt)
     binds = _bindings(opt)
-    stash = []
+    hidden = set()
     for m in models:
         b = binds.get(id(m))
         if b is None or not b.valid(m):
             if b is not None:
                 b.detach()
             b = binds[id(m)] = _Binding(m, opt, gmap[id(m.engine.table_params()["mf_user"])])
-        for p in b.run(opt, gmap):
-            if p.grad is not None:
-                stash.append((p, p.grad))
-                p.grad = None
-    opt._ncf_stash = stash
+        hidden.update(id(p) for p in b.run(opt, gmap))
+    if hidden:
+        _hide(opt, hidden)
     return None
 
 
 def _post_hook(opt, args, kwargs):
-    stash = getattr(opt, "_ncf_stash", None)
-    if stash:
-        for p, g in stash:
-            p.grad = g
-        opt._ncf_stash = None
+    _restore_groups(opt)

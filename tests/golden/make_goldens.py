@@ -127,6 +127,9 @@ def make_f1(ref, AdvancedNCF, KJT, sd):
 
 
 # ----------------------------------------------------------------------------- F2/F3
+ZONE = 1e-6   # = tests/parity.py ZONE
+
+
 def make_batch(g, U, I, B, M):
     users = torch.randint(0, U, (B,), generator=g)
     pos = torch.randint(0, I, (B,), generator=g)
@@ -159,6 +162,13 @@ def make_train(fname, AdvancedNCF, KJT, U, I, D, T, hidden, H, B, M, steps, seed
         loss.backward()
         out[f"step{s}/prob"] = prob.detach().numpy()
         out[f"step{s}/loss"] = np.float32(loss.item())
+        # sign-flip zone of THIS step (tests/parity.py): elements whose effective Adam
+        # gradient g + wd * p is below ZONE while g itself is not exactly 0 (summation noise
+        # decides its sign), as packed bits per parameter
+        for n, p in model.named_parameters():
+            if p.grad is not None:
+                z = ((p.grad + wd * p.detach()).abs() < ZONE) & (p.grad != 0)
+                out[f"zone{s}/{n}"] = np.packbits(z.numpy().reshape(-1))
         if s == 0:
             for n, p in model.named_parameters():
                 if p.grad is not None:
@@ -355,6 +365,13 @@ def make_f8(ref):
     print("F8 written;", len(il), "train interactions; pairs", pairs)
 
 
+def make_train_fixtures(AdvancedNCF, KJT):
+    make_train("f2_train_c2.npz", AdvancedNCF, KJT, U=300, I=120, D=64, T=32,
+               hidden=[256, 128, 64], H=4, B=8, M=5, steps=3, seed=0, lr=1e-3, wd=1e-5)
+    make_train("f3_train_c1.npz", AdvancedNCF, KJT, U=200, I=300, D=16, T=32,
+               hidden=[64, 32], H=1, B=16, M=5, steps=3, seed=1, lr=1e-3, wd=1e-5)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
@@ -366,14 +383,14 @@ def main():
     if a.only == "f6":
         make_f6(AdvancedNCF, sd)
         return
+    if a.only == "train":
+        make_train_fixtures(AdvancedNCF, KJT)
+        return
     if a.only in ("f7", "f8"):
         (make_f7 if a.only == "f7" else make_f8)(a.reference)
         return
     make_f1(a.reference, AdvancedNCF, KJT, sd)
-    make_train("f2_train_c2.npz", AdvancedNCF, KJT, U=300, I=120, D=64, T=32,
-               hidden=[256, 128, 64], H=4, B=8, M=5, steps=3, seed=0, lr=1e-3, wd=1e-5)
-    make_train("f3_train_c1.npz", AdvancedNCF, KJT, U=200, I=300, D=16, T=32,
-               hidden=[64, 32], H=1, B=16, M=5, steps=3, seed=1, lr=1e-3, wd=1e-5)
+    make_train_fixtures(AdvancedNCF, KJT)
     make_f4(MHA, TE)
     make_f5(AdvancedNCF, KJT, sd)
     make_f6(AdvancedNCF, sd)

@@ -1,36 +1,69 @@
 """Shared parity tolerances.
 
-fp32 forward: abs 1e-6.  Gradients: rel 1e-4 / abs 1e-7 (summation order differs).
-Post-Adam parameters: abs 1e-6, EXCEPT the 'sign-flip zone': at Adam's first steps the update
-is ~ lr * g/(|g|+eps), so an element whose effective gradient g + wd*p is below ZONE is driven by
-fp32 summation noise (e.g. user_product_attention.k_proj.bias, whose true gradient is exactly 0
-because softmax is shift-invariant over keys).  Those elements may differ by <= 2*lr per step.
+fp32 forward: abs 1e-6 on probabilities.  Gradients: rel 1e-4 / abs 1e-7 (summation order
+differs).  Post-Adam parameters: abs 1e-6, EXCEPT inside the 'sign-flip zone': at Adam's first
+steps the update is ~ lr * g/(|g|+eps), so an element whose effective gradient g + wd*p is
+below ZONE while g itself is not exactly zero has its step sign decided by fp32 summation noise.
+
+The zone is defined per step (the fixtures carry one bit mask per step: tests/golden/
+make_goldens.py), and it is capped: per tensor at most 0.1% of the elements (one element in
+tensors under 1000 elements) may differ, only elements that were in the zone at some step, each
+by at most 2*lr per zone step.
+
+One tensor is exempt from the cap: user_product_attention.k_proj.bias.  Its exact gradient is
+identically zero (softmax is invariant to a shift shared by all keys of a query), so every one of
+its elements is noise-driven in the reference and here alike; it gets the 2*lr-per-step bound.
 """
 import numpy as np
 
 ZONE = 1e-6
+ZONE_CAP = 1e-3                     # fraction of a tensor's elements allowed to differ
+ANALYTIC_ZERO_GRAD = {"user_product_attention.k_proj.bias"}
 
 
-def assert_params_close(name, actual, ref, g_eff0, lr, steps, atol=1e-6):
+def zone_masks(fixture, name, steps):
+    """The per-step sign-flip masks of parameter `name` for the first `steps` steps."""
+    n = fixture["init/" + name].size
+    shape = fixture["init/" + name].shape
+    return [np.unpackbits(fixture[f"zone{s}/{name}"])[:n].astype(bool).reshape(shape)
+            for s in range(steps)]
+
+
+def zone_from_grads(grads, params, wd):
+    """A step's zone from that step's reference gradients and parameters (oracle runs)."""
+    g = np.asarray(grads)
+    return (np.abs(g + wd * np.asarray(params)) < ZONE) & (g != 0)
+
+
+def assert_params_close(name, actual, ref, zones, lr, atol=1e-6):
+    """``zones``: one boolean mask per step taken (zone_masks / zone_from_grads)."""
     actual = np.asarray(actual, np.float32)
     ref = np.asarray(ref, np.float32)
     d = np.abs(actual - ref)
-    zone = np.abs(g_eff0) < ZONE
-    out_bad = (d > atol) & ~zone
+    bad = d > atol
+    if name in ANALYTIC_ZERO_GRAD:
+        assert d.max() <= 2 * lr * len(zones) + atol, f"{name}: diff {d.max():.3e}"
+        return
+    nz = np.sum(zones, axis=0) if zones else np.zeros(d.shape, np.int64)
+    out_bad = bad & (nz == 0)
     assert not out_bad.any(), (f"{name}: {out_bad.sum()} elements outside the sign-flip zone "
                                f"differ by up to {d[out_bad].max():.3e}")
-    in_bad = d[zone]
-    if in_bad.size:
-        assert in_bad.max() <= 2 * lr * steps + atol, f"{name}: zone diff {in_bad.max():.3e}"
+    cap = max(1, int(ZONE_CAP * d.size))     # (one element for tensors under 1000)
+    assert bad.sum() <= cap, (f"{name}: {bad.sum()} zone elements differ (cap {cap} = "
+                              f"{ZONE_CAP:.1%} of {d.size})")
+    if bad.any():
+        assert (d[bad] <= 2 * lr * nz[bad] + atol).all(), f"{name}: zone diff {d[bad].max():.3e}"
 
 
-def assert_moment_close(name, actual, ref, g_eff0, rtol=1e-3, atol=1e-7):
+def assert_moment_close(name, actual, ref, zones, rtol=1e-3, atol=1e-7):
     """Adam moments after a few steps.  exp_avg is (1-b1) * sum_k b1^k g_k (weights summing to
     < 0.3 over 3 steps), so it inherits the gradient tolerance scaled down: abs 1e-7 (the gradient
     abs tolerance is 1e-6), rel 1e-3 for elements accumulated from noisy near-zero gradients."""
     actual = np.asarray(actual)
     ref = np.asarray(ref)
-    zone = np.abs(g_eff0) < ZONE
+    zone = np.any(zones, axis=0) if zones else np.zeros(np.shape(ref), bool)
+    if name in ANALYTIC_ZERO_GRAD:
+        zone = np.ones(np.shape(ref), bool)
     d = np.abs(actual - ref)
     bad = (d > atol + rtol * np.abs(ref)) & ~zone
     assert not bad.any(), f"{name}: {bad.sum()} moment elements differ (max {d[bad].max():.3e})"

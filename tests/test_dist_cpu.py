@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from tests.parity import assert_params_close
+from tests.parity import assert_params_close, zone_from_grads
 
 U, I, D, T, H, HID, B, M = 97, 41, 16, 8, 2, [32, 16], 6, 5
 TABLES = {"mf_user": "mf_embedding_collection.embedding_bags.user_id.weight",
@@ -199,17 +199,19 @@ def test_sharded_step_equals_single_rank_global_batch():
     params, batches = global_setup()
     ref = {k: v.clone() for k, v in params.items()}
     opt = O.AdamState(lr=1e-3, weight_decay=1e-5)
-    g0 = None
+    zones = {}
     for s in range(len(batches)):
         u = torch.cat([b[0] for b in batches[s]])
         i = torch.cat([b[1] for b in batches[s]])
         t = torch.cat([b[2] for b in batches[s]])
+        before = {k: v.clone() for k, v in ref.items()}
         _, loss, grads = O.train_step(ref, opt, u, i, t, negative_samples=M - 1, num_heads=H,
                                       temporal_dim=T, n_layers=len(HID))
-        g0 = g0 or {k: (v + 1e-5 * params[k]).numpy() for k, v in grads.items()}
+        for k, v in grads.items():
+            zones.setdefault(k, []).append(zone_from_grads(v.numpy(), before[k].numpy(), 1e-5))
         # the global loss is the sum of the ranks' contributions
         assert abs(sum(r["losses"][s] for r in res) - float(loss)) < 1e-5
-    for name, gv in g0.items():
+    for name, zs in zones.items():
         if name in TABLES.values():
             got = torch.empty_like(ref[name])
             for r in range(world):
@@ -217,7 +219,7 @@ def test_sharded_step_equals_single_rank_global_batch():
         else:
             got = res[0]["p"][name]
             assert torch.equal(got, res[1]["p"][name]), name     # replicas stay identical
-        assert_params_close(name, got.numpy(), ref[name].numpy(), gv, 1e-3, 2, atol=2e-6)
+        assert_params_close(name, got.numpy(), ref[name].numpy(), zs, 1e-3, atol=2e-6)
 
 
 # ----------------------------------------------------------------------------- C5 item shards

@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from tests.parity import assert_params_close
+from tests.parity import assert_params_close, zone_from_grads
 
 pytestmark = pytest.mark.gpu
 
@@ -128,16 +128,18 @@ def test_hip_sharded_step_world2_equals_single_rank_global_batch():
     _, params, batches = setup()
     ref = {k: v.clone() for k, v in params.items()}
     opt = O.AdamState(lr=1e-3, weight_decay=1e-5)
-    g0 = None
+    zones = {}
     for s in range(STEPS):
         u = torch.cat([b[0] for b in batches[s]])
         i = torch.cat([b[1] for b in batches[s]])
         t = torch.cat([b[2] for b in batches[s]])
+        before = {k: v.clone() for k, v in ref.items()}
         _, loss, grads = O.train_step(ref, opt, u, i, t, negative_samples=M - 1, num_heads=H,
                                       temporal_dim=T, n_layers=len(HID))
-        g0 = g0 or {k: (v + 1e-5 * params[k]).numpy() for k, v in grads.items()}
+        for k, v in grads.items():
+            zones.setdefault(k, []).append(zone_from_grads(v.numpy(), before[k].numpy(), 1e-5))
         assert abs(sum(r["losses"][s] for r in res) - float(loss)) < 2e-6
-    for name, gv in g0.items():
+    for name, zs in zones.items():
         if name in TABLES.values():
             got = torch.empty_like(ref[name])
             for r in range(world):
@@ -145,4 +147,4 @@ def test_hip_sharded_step_world2_equals_single_rank_global_batch():
         else:
             got = res[0]["p"][name]
             assert torch.equal(got, res[1]["p"][name]), name     # replicas stay identical
-        assert_params_close(name, got.numpy(), ref[name].numpy(), gv, 1e-3, STEPS, atol=2e-6)
+        assert_params_close(name, got.numpy(), ref[name].numpy(), zs, 1e-3, atol=2e-6)

@@ -13,7 +13,8 @@ import torch
 import _ncf_pkg
 from oracle import ncf_oracle as O
 from tests.conftest import sub
-from tests.parity import assert_moment_close, assert_params_close
+from tests.parity import (assert_moment_close, assert_params_close, zone_from_grads,
+                          zone_masks)
 
 pytestmark = pytest.mark.gpu
 ncf = _ncf_pkg.load()
@@ -43,8 +44,9 @@ def test_f1_eval_known_answer(f1):
         # batches of 32 like local_inference.py:121-129
         outb = np.concatenate([m(kjt(f1["user_ids"][s:s + 32], f1["item_ids"][s:s + 32]))
                                .cpu().numpy().reshape(-1) for s in range(0, 1000, 32)])
-    assert np.abs(out - f1["csv_pred"]).max() < 2e-6
-    assert np.abs(out - f1["ref_pred"]).max() < 2e-6
+    # fp32 forward abs 1e-6 (the reference's own re-run is 2.98e-7 from the CSV)
+    assert np.abs(out - f1["csv_pred"]).max() < 1e-6
+    assert np.abs(out - f1["ref_pred"]).max() < 1e-6
     assert np.array_equal(out, outb)
 
 
@@ -99,16 +101,15 @@ def test_train_goldens(fx, nl, materialize, request):
             np.testing.assert_allclose(got[k], v, rtol=1e-4, atol=1e-6, err_msg=k)
     for s in (0, steps - 1):
         for k, v in sub(g, f"after{s}/param/").items():
-            geff = g["grad0/" + k] + wd * g["init/" + k]
-            assert_params_close(k, rec[f"params{s}"][k], v, geff, lr, s + 1)
+            assert_params_close(k, rec[f"params{s}"][k], v, zone_masks(g, k, s + 1), lr)
     # unused parameters (grad None in the reference) never move
     for k in g["grad_none0"].tolist():
         assert np.array_equal(rec[f"params{steps - 1}"][k], g["init/" + k]), k
     for k, v in sub(g, f"after{steps - 1}/exp_avg/").items():
-        geff = g["grad0/" + k] + wd * g["init/" + k]
-        assert_moment_close(k, rec["state"][k]["exp_avg"], v, geff)
+        zs = zone_masks(g, k, steps)
+        assert_moment_close(k, rec["state"][k]["exp_avg"], v, zs)
         assert_moment_close(k, rec["state"][k]["exp_avg_sq"], g[f"after{steps - 1}/exp_avg_sq/" + k],
-                            geff, atol=1e-12)
+                            zs, atol=1e-12)
         assert float(rec["state"][k]["step"]) == steps
     # eval forward on the trained weights (M = 1) and forward_simple
     m = rec["model"]
@@ -142,6 +143,7 @@ def test_train_vs_oracle(U, I, D, H, hidden, B, M):
     opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
     oopt = O.AdamState(lr=1e-3, weight_decay=1e-5)
     gen = torch.Generator().manual_seed(4)
+    zones = {}
     for step in range(2):
         # Zipf-ish items (hot ids repeat many times) exercise long segments
         users = torch.randint(0, U, (B,), generator=gen).repeat_interleave(M)
@@ -158,18 +160,20 @@ def test_train_vs_oracle(U, I, D, H, hidden, B, M):
             m.engine.materialize_table_grads()
             grads = {n: p.grad.detach().cpu() for n, p in m.named_parameters() if p.grad is not None}
         opt.step()
+        before = {k: v.clone() for k, v in ref.items()}
         prob, oloss, ograds = O.train_step(ref, oopt, users, items, t, negative_samples=M - 1,
                                            num_heads=H, temporal_dim=32, n_layers=len(hidden))
+        for k, v in ograds.items():
+            zones.setdefault(k, []).append(zone_from_grads(v.numpy(), before[k].numpy(), 1e-5))
         assert (out.detach().cpu() - prob).abs().max().item() < 5e-6
         assert abs(loss.item() - float(oloss)) < 5e-6
         if step == 0:
             for k, v in ograds.items():
                 np.testing.assert_allclose(grads[k].numpy(), v.numpy(), rtol=2e-4, atol=2e-6,
                                            err_msg=k)
-            g0 = {k: (ograds[k] + 1e-5 * v).numpy() for k, v in ref.items() if k in ograds}
     sd = m.state_dict()
-    for k, g in g0.items():
-        assert_params_close(k, sd[k].cpu().numpy(), ref[k].numpy(), g, 1e-3, 2, atol=5e-6)
+    for k, zs in zones.items():
+        assert_params_close(k, sd[k].cpu().numpy(), ref[k].numpy(), zs, 1e-3, atol=5e-6)
 
 
 # ----------------------------------------------------------------------------- op level (F4)
@@ -669,8 +673,7 @@ def test_fused_step_matches_dropin_path(f2):
     sd = m.state_dict()
     lr, wd = 1e-3, 1e-5
     for k, v in sub(g, f"after{steps - 1}/param/").items():
-        geff = g["grad0/" + k] + wd * g["init/" + k]
-        assert_params_close(k, sd[k].cpu().numpy(), v, geff, lr, steps)
+        assert_params_close(k, sd[k].cpu().numpy(), v, zone_masks(g, k, steps), lr)
 
 
 # ----------------------------------------------------------------------------- sharded (RCCL)
