@@ -122,6 +122,50 @@ struct Replay {
   static constexpr int EPL = D / LPR;           // columns per lane
 };
 
+// The replay of zero-gradient steps from+1 .. to on EPL columns of one (pair of) table row(s).
+// With wave-uniform bounds (one row per wave) the per-step scalars are scalar loads; they are
+// fetched 8 steps (16 floats) at a time, one chunk AHEAD of the steps that use them, so the
+// scalar-load latency hides behind 8 steps of VALU work instead of stalling every step (the
+// step table is padded >= 4096 steps past any target, deferred.py _ensure).  Same adam1 calls in
+// the same order: results are bit-identical to the step-by-step loop.
+template <int EPL, bool PAIR>
+__device__ __forceinline__ void replay_uniform(float* p0, float* m0, float* v0, float* p1,
+                                               float* m1, float* v1, int32_t from, int32_t to,
+                                               const float* __restrict__ table,
+                                               const AdamScalars& s) {
+  constexpr int C = 8;                 // steps per chunk
+  int32_t q = from + 1;
+  float sc[2 * C];
+#pragma unroll
+  for (int k = 0; k < 2 * C; ++k) sc[k] = table[2 * q + k];
+  while (q + C - 1 <= to) {
+    float nx[2 * C];
+#pragma unroll
+    for (int k = 0; k < 2 * C; ++k) nx[k] = table[2 * (q + C) + k];
+    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this chunk's steps
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) {
+        adam1(p0[j], m0[j], v0[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+        if (PAIR) adam1(p1[j], m1[j], v1[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 2 * C; ++k) sc[k] = nx[k];
+    q += C;
+  }
+#pragma unroll
+  for (int k = 0; k < C - 1; ++k) {    // the last to - q + 1 < C steps
+    if (q + k > to) break;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      adam1(p0[j], m0[j], v0[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+      if (PAIR) adam1(p1[j], m1[j], v1[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+    }
+  }
+}
+
 template <int D>
 __device__ __forceinline__ void catch_up_row(const TablePtrs& t, int64_t row, int sub, int32_t from,
                                              int32_t to, const float* __restrict__ table,
@@ -143,19 +187,25 @@ __device__ __forceinline__ void catch_up_row(const TablePtrs& t, int64_t row, in
     for (int j = 0; j < EPL; ++j) {
       p1[j] = t.p1[o + j * LPR]; m1[j] = t.m1[o + j * LPR]; v1[j] = t.v1[o + j * LPR];
     }
+    if (Replay<D>::LPR == 64) {
+      replay_uniform<EPL, true>(p0, m0, v0, p1, m1, v1, from, to, table, s);
+    } else {
 #pragma unroll 2
-    for (int32_t q = from + 1; q <= to; ++q) {
-      const float ns = table[2 * q], bc = table[2 * q + 1];
+      for (int32_t q = from + 1; q <= to; ++q) {
+        const float ns = table[2 * q], bc = table[2 * q + 1];
 #pragma unroll
-      for (int j = 0; j < EPL; ++j) {
-        adam1(p0[j], m0[j], v0[j], 0.0f, ns, bc, s);
-        adam1(p1[j], m1[j], v1[j], 0.0f, ns, bc, s);
+        for (int j = 0; j < EPL; ++j) {
+          adam1(p0[j], m0[j], v0[j], 0.0f, ns, bc, s);
+          adam1(p1[j], m1[j], v1[j], 0.0f, ns, bc, s);
+        }
       }
     }
 #pragma unroll
     for (int j = 0; j < EPL; ++j) {
       t.p1[o + j * LPR] = p1[j]; t.m1[o + j * LPR] = m1[j]; t.v1[o + j * LPR] = v1[j];
     }
+  } else if (Replay<D>::LPR == 64) {
+    replay_uniform<EPL, false>(p0, m0, v0, p1, m1, v1, from, to, table, s);
   } else {
 #pragma unroll 2
     for (int32_t q = from + 1; q <= to; ++q) {

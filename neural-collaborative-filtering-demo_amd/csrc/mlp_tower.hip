@@ -72,6 +72,28 @@ struct TowerArgs {
 };
 
 __device__ __forceinline__ float4 lds4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// Stores of data no later phase of THIS kernel reads (weight-gradient / column-sum partials,
+// the GMF row gradients): non-temporal, so the 232 KB of partials per workgroup do not evict
+// the pre-LayerNorm rows r that the next phases re-read from L2.
+#ifndef NCF_MLP_NT
+#define NCF_MLP_NT 0   // measured: 80 -> 88 us per k_mlp_bwd with nt partials (knob kept)
+#endif
+__device__ __forceinline__ void st_nt(float* p, float v) {
+#if NCF_MLP_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ void st4_nt(float* p, float4 v) {
+#if NCF_MLP_NT
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(v4{v.x, v.y, v.z, v.w}, reinterpret_cast<v4*>(p));
+#else
+  st4(p, v);
+#endif
+}
 __device__ __forceinline__ void lds4_st(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 // LayerNorm affine of a centred float4 (x - mean) and the dropout keep-scales: ONE definition
@@ -398,7 +420,7 @@ __device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict_
     float s = 0.0f;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) s += S[w * 3 * N + e];
-    part[e] = s;
+    st_nt(part + e, s);
   }
   __syncthreads();
 }
@@ -491,7 +513,7 @@ __device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const f
       }
       float* o = out + (16 * tn + 4 * g) * K + 16 * tk + i;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e * K] = acc0[e] + acc1[e];
+      for (int e = 0; e < 4; ++e) st_nt(o + e * K, acc0[e] + acc1[e]);
     }
   }
 }
@@ -558,8 +580,8 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
       aw.x += dml * x.x; aw.y += dml * x.y; aw.z += dml * x.z; aw.w += dml * x.w;
       const float4 u = ld4(h.mf_user_ln + row * K0 + col), it = ld4(h.mf_item_ln + row * K0 + col);
       const float4 gv = make_float4(dmf * wm.x, dmf * wm.y, dmf * wm.z, dmf * wm.w);
-      st4(h.grad_mf_user_ln + row * K0 + col, make_float4(gv.x * it.x, gv.y * it.y, gv.z * it.z, gv.w * it.w));
-      st4(h.grad_mf_item_ln + row * K0 + col, make_float4(gv.x * u.x, gv.y * u.y, gv.z * u.z, gv.w * u.w));
+      st4_nt(h.grad_mf_user_ln + row * K0 + col, make_float4(gv.x * it.x, gv.y * it.y, gv.z * it.z, gv.w * it.w));
+      st4_nt(h.grad_mf_item_ln + row * K0 + col, make_float4(gv.x * u.x, gv.y * u.y, gv.z * u.z, gv.w * u.w));
       am.x += dmf * u.x * it.x; am.y += dmf * u.y * it.y; am.z += dmf * u.z * it.z; am.w += dmf * u.w * it.w;
       if (sub == 0) {
         sw0 += dz * h.mf_pred[row];
@@ -595,7 +617,7 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
     float v = 0.0f;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) v += S[w * kHeadW + e];
-    part[e] = v;
+    st_nt(part + e, v);
   }
   __syncthreads();
 }
