@@ -201,6 +201,38 @@ def dropin_train(ncf, dev, cfg, batches, warmup, steps):
     return out
 
 
+def bf16_train(ncf, dev, cfg, batches, warmup, steps):
+    """The C2 configuration as BASELINE.json configs[1] states it ("bf16"; SURVEY 8(d): tables
+    bf16, Adam moments fp32): the same step as the headline with the four tables held as bf16
+    (FusedTrainStep(table_dtype=torch.bfloat16)); every other tensor and all arithmetic fp32.
+    A separate, labelled line: the fp32 step is the parity path and the headline."""
+    from ncf_amd.trainer import FusedTrainStep
+    U, I, D, T, H, hid, B, M = cfg
+    torch.manual_seed(1234)
+    m = ncf.AdvancedNCF(U, I, 10, 50, D, D, T, hid, H, 0.2, M - 1).to(dev).train()
+    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5, table_dtype=torch.bfloat16)
+
+    def run(first, count):
+        for s in range(first, first + count):
+            u, i, t = batches[s % len(batches)]
+            step(u, i, t, next=batches[(s + 1) % len(batches)][:2])
+    run(0, warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(warmup, steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"config": "C2 with bf16 tables (fp32 Adam moments, fp32 compute), FusedTrainStep",
+           "value": round(B * M * steps / dt, 1), "unit": "samples/s",
+           "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warmup,
+           "table_bytes": 2 * (U + I) * D * 2, "final_loss": round(float(step.last_loss.item()), 6),
+           "tolerance": "vs fp32 oracle: loss within 1% per step over 100 steps, eval prob "
+                        "abs <= 2e-2 (tests/test_gpu_bf16.py)"}
+    del step, m
+    torch.cuda.empty_cache()
+    return out
+
+
 C4 = dict(U=50_000_000, I=5_000_000, D=128, T=32, H=4, hid=[256, 128, 64], B=4096, M=5)
 
 
@@ -573,6 +605,11 @@ def main():
                               args.steps)
         dropin["vs_fused_step"] = round(dropin["value"] / samples_s, 4)
 
+    bf16 = None
+    if not sharded:
+        bf16 = bf16_train(ncf, dev, (U, I, D, T, H, hid, B, M), batches, args.warmup, args.steps)
+        bf16["vs_fp32_step"] = round(bf16["value"] / samples_s, 4)
+
     c4 = None
     if not sharded and not args.no_c4:
         # C4 (170 GB resident) in a child process: its own allocator, nothing of it survives
@@ -652,6 +689,7 @@ def main():
             "infer_pairs_per_s": round(infer_pairs, 1),
             "infer_config": f"eval forward (M=1), {npairs} resident (user,item) pairs per GPU",
             "c5_scoring": score,
+            "c2_bf16_tables": bf16,
             "c4_train": c4,
             "final_loss": round(loss, 6),
         }

@@ -74,6 +74,15 @@ int ncf_gather_ln_gmf_scaled_fwd(const int64_t* user_ids, const int64_t* item_id
 
 /* Row gather (+ optional LayerNorm): EBC forward as read by callers (app.py:156-184) and
  * get_user_embeddings / get_product_embeddings (architecture.py:383-407).                   */
+/* bf16-table configuration: the training gather over bf16 table rows (fp32 outputs). */
+int ncf_gather_ln_gmf_bf16_fwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
+                               const uint16_t* mf_user, const uint16_t* mf_item,
+                               const uint16_t* mlp_user, const uint16_t* mlp_item,
+                               int64_t num_users, int64_t num_items, int64_t dim,
+                               const float* mf_gamma, const float* mf_beta, const float* mlp_gamma,
+                               const float* mlp_beta, const float* mf_out_w, const float* mf_out_b,
+                               float eps, float* mf_pred, float* mlp_user_ln, float* mlp_item_ln,
+                               float* mf_user_ln, float* mf_item_ln, int* err_flag, void* stream);
 int ncf_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t rows,
                     int64_t dim, const float* ln_gamma, const float* ln_beta, float eps,
                     float* out, int* err_flag, void* stream);
@@ -394,6 +403,19 @@ int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_users, int64_t 
                              const int64_t* uniq_items, float* grad_mf_gamma, float* grad_mf_beta,
                              float* grad_mlp_gamma, float* grad_mlp_beta, void* workspace,
                              int64_t workspace_bytes, ncf_reduce_list* defer, void* stream);
+/* bf16-table configuration: the same reduce with bf16 table rows (uint16 bit patterns). */
+int ncf_embedding_bwd_reduce_bf16(int64_t n, int64_t dim, int64_t num_users, int64_t num_items,
+                                  const float* dy_mf_user, const float* dy_mlp_user,
+                                  const float* dy_mf_item, const float* dy_mlp_item,
+                                  const uint16_t* mf_user, const uint16_t* mlp_user,
+                                  const uint16_t* mf_item, const uint16_t* mlp_item,
+                                  const float* mf_gamma, const float* mlp_gamma, float eps,
+                                  float* grad_mf_user, float* grad_mlp_user, float* grad_mf_item,
+                                  float* grad_mlp_item, const int64_t* uniq_users,
+                                  const int64_t* uniq_items, float* grad_mf_gamma,
+                                  float* grad_mf_beta, float* grad_mlp_gamma, float* grad_mlp_beta,
+                                  void* workspace, int64_t workspace_bytes, ncf_reduce_list* defer,
+                                  void* stream);
 int ncf_slot_reset(const int64_t* uniq, const uint32_t* num_unique, int kind, int32_t* slot,
                    int64_t max_n, void* stream);
 /* dense[uniq[c]] = grad_compact[c] (materialise a dense table gradient for non-Adam users). */
@@ -558,12 +580,17 @@ int ncf_adam_sweep_rolling(float* p0, float* m0, float* v0, float* p1, float* m1
 /* Both id kinds in one launch each (blockIdx.y = kind): pairs[k] holds kind k's GMF + MLP
  * tables (sharing the row index), their moments, compact gradients (apply), the step's unique
  * rows and the stamps; count[k] = unique rows of kind k (ncf_dedup_ids).                      */
+/* param_dtype: NCF_DTYPE_F32, or NCF_DTYPE_BF16 when p0 / p1 point at bf16 rows (the moments stay
+ * fp32; the parameter is rounded to bf16, nearest even, after every step it takes).           */
+#define NCF_DTYPE_F32 0
+#define NCF_DTYPE_BF16 1
 typedef struct ncf_table_pair {
   float *p0, *m0, *v0, *p1, *m1, *v1;
   const float *g0, *g1;
   const int64_t* row_ids;
   int32_t* stamp;
   int64_t rows;
+  int64_t param_dtype;
 } ncf_table_pair;
 int ncf_adam_pairs_catchup_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
                                  const uint32_t* count, int64_t max_n, int32_t target_rel,
@@ -579,6 +606,16 @@ int ncf_adam_pairs_sweep_rolling(const ncf_table_pair* pairs, int npairs, int64_
                                  const ncf_step_clock* clock, const float* step_table,
                                  double beta1, double beta2, double eps, double weight_decay,
                                  void* stream);
+/* bf16 parameter rows (C2 "bf16": tables bf16, Adam moments fp32): ncf_adam_table and
+ * ncf_adam_sweep with the parameter rounded to bf16 after every step.                        */
+int ncf_adam_table_bf16(uint16_t* param, float* exp_avg, float* exp_avg_sq, int64_t rows,
+                        int64_t dim, const int32_t* slot, const float* grad_compact, double lr,
+                        double beta1, double beta2, double eps, double weight_decay, double step,
+                        void* stream);
+int ncf_adam_sweep_bf16(uint16_t* p0, float* m0, float* v0, uint16_t* p1, float* m1, float* v1,
+                        int64_t row0, int64_t rows, int64_t dim, int32_t* stamp, int32_t target,
+                        const float* step_table, double beta1, double beta2, double eps,
+                        double weight_decay, void* stream);
 int ncf_adam_flat_clock(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                         int64_t n, const float* step_table, int32_t step_rel,
                         const ncf_step_clock* clock, double beta1, double beta2, double eps,

@@ -38,6 +38,8 @@ SIGNATURES = {
                                     P, P, P, P, P, P, P]),
     "ncf_gather_ln_gmf_scaled_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P,
                                            F32, P, F32, P, P, P, P, P, P, P]),
+    "ncf_gather_ln_gmf_bf16_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P,
+                                         F32, P, P, P, P, P, P, P]),
     "ncf_gather_rows": (I32, [P, I64, P, I64, I64, P, P, F32, P, P, P]),
     "ncf_gemm_f32": (I32, [I64, I64, I64, P, I64, I32, P, I64, I32, P, I64, P, I32, P]),
     "ncf_gemm_splitk_workspace": (I64, [I64, I64, I32]),
@@ -97,6 +99,8 @@ SIGNATURES = {
     "ncf_comm_allreduce_sum_f32": (I32, [P, P, I64, P]),
     "ncf_embedding_bwd_reduce": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
                                        P, P, P, P, P, P, P, P, P, I64, P, P]),
+    "ncf_embedding_bwd_reduce_bf16": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32,
+                                            P, P, P, P, P, P, P, P, P, P, P, I64, P, P]),
     "ncf_slot_reset": (I32, [P, P, I32, P, I64, P]),
     "ncf_scatter_compact_rows": (I32, [P, I64, P, P, I32, P, I64, P]),
     "ncf_adam_table": (I32, [P, P, P, I64, I64, P, P, F64, F64, F64, F64, F64, F64, P]),
@@ -118,6 +122,8 @@ SIGNATURES = {
     "ncf_adam_pairs_catchup_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
     "ncf_adam_pairs_apply_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
     "ncf_adam_pairs_sweep_rolling": (I32, [P, I32, I64, I32, I32, P, P, F64, F64, F64, F64, P]),
+    "ncf_adam_table_bf16": (I32, [P, P, P, I64, I64, P, P, F64, F64, F64, F64, F64, F64, P]),
+    "ncf_adam_sweep_bf16": (I32, [P, P, P, P, P, P, I64, I64, I64, P, I32, P, F64, F64, F64, F64, P]),
     "ncf_adam_flat_clock": (I32, [P, P, P, P, I64, P, I32, P, F64, F64, F64, F64, P]),
     "ncf_adam_flat_clock_close": (I32, [P, P, P, P, I64, P, I32, P, F64, F64, F64, F64, U64, P]),
     "ncf_score_queries": (I32, [P, I64, P, I64, I64, P, P, F32, P, P, P, P, P]),
@@ -172,7 +178,10 @@ class HeadArgs(ctypes.Structure):
 class TablePair(ctypes.Structure):
     """ncf_table_pair (include/ncf_hip.h)."""
     _fields_ = [("p0", P), ("m0", P), ("v0", P), ("p1", P), ("m1", P), ("v1", P), ("g0", P),
-                ("g1", P), ("row_ids", P), ("stamp", P), ("rows", I64)]
+                ("g1", P), ("row_ids", P), ("stamp", P), ("rows", I64), ("param_dtype", I64)]
+
+
+DTYPE_F32, DTYPE_BF16 = 0, 1
 
 
 SHARD_MAX_WORLD = 64

@@ -234,6 +234,8 @@ class AdvancedNCF(nn.Module):
         self._engine.sync_tables()
         out = super().load_state_dict(state_dict, strict=strict, assign=assign)
         self._engine.updates += 1
+        if self._engine.deferred is not None:     # bf16 tables take the loaded values
+            self._engine.deferred.reload_params()
         if assign:
             self._engine.flatten()
         return out

@@ -54,7 +54,7 @@ __device__ __forceinline__ void adam4(float4& p, float4& m, float4& v, float4 g,
   adam4(p, m, v, g, s.neg_step, s.inv_bc2_sqrt, s);
 }
 
-template <int D>
+template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void k_adam_table(float* __restrict__ p, float* __restrict__ m,
                                                     float* __restrict__ v, int64_t rows,
                                                     const int32_t* __restrict__ slot,
@@ -67,9 +67,9 @@ __global__ __launch_bounds__(256) void k_adam_table(float* __restrict__ p, float
     const int32_t sl = slot ? slot[row] : -1;
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
     if (sl >= 0) g = ld4(G + (int64_t)sl * D + col);
-    float4 pp = ld4(p + e * 4), mm = ld4(m + e * 4), vv = ld4(v + e * 4);
+    float4 pp = ldp4<BF>(p, e * 4), mm = ld4(m + e * 4), vv = ld4(v + e * 4);
     adam4(pp, mm, vv, g, s);
-    st4(p + e * 4, pp);
+    stp4<BF>(p, e * 4, pp);
     st4(m + e * 4, mm);
     st4(v + e * 4, vv);
   }
@@ -128,7 +128,7 @@ struct Replay {
 // scalar-load latency hides behind 8 steps of VALU work instead of stalling every step (the
 // step table is padded >= 4096 steps past any target, deferred.py _ensure).  Same adam1 calls in
 // the same order: results are bit-identical to the step-by-step loop.
-template <int EPL, bool PAIR>
+template <int EPL, bool PAIR, bool BF = false>
 __device__ __forceinline__ void replay_uniform(float* p0, float* m0, float* v0, float* p1,
                                                float* m1, float* v1, int32_t from, int32_t to,
                                                const float* __restrict__ table,
@@ -148,7 +148,9 @@ __device__ __forceinline__ void replay_uniform(float* p0, float* m0, float* v0, 
 #pragma unroll
       for (int j = 0; j < EPL; ++j) {
         adam1(p0[j], m0[j], v0[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+        if (BF) p0[j] = ncf_round_bf16(p0[j]);   // bf16 tables: stored (rounded) every step
         if (PAIR) adam1(p1[j], m1[j], v1[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+        if (PAIR && BF) p1[j] = ncf_round_bf16(p1[j]);
       }
     }
 #pragma unroll
@@ -161,12 +163,14 @@ __device__ __forceinline__ void replay_uniform(float* p0, float* m0, float* v0, 
 #pragma unroll
     for (int j = 0; j < EPL; ++j) {
       adam1(p0[j], m0[j], v0[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+      if (BF) p0[j] = ncf_round_bf16(p0[j]);
       if (PAIR) adam1(p1[j], m1[j], v1[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+      if (PAIR && BF) p1[j] = ncf_round_bf16(p1[j]);
     }
   }
 }
 
-template <int D>
+template <int D, bool BF = false>
 __device__ __forceinline__ void catch_up_row(const TablePtrs& t, int64_t row, int sub, int32_t from,
                                              int32_t to, const float* __restrict__ table,
                                              const AdamScalars& s) {
@@ -180,15 +184,15 @@ __device__ __forceinline__ void catch_up_row(const TablePtrs& t, int64_t row, in
   float p0[EPL], m0[EPL], v0[EPL], p1[EPL], m1[EPL], v1[EPL];
 #pragma unroll
   for (int j = 0; j < EPL; ++j) {
-    p0[j] = t.p0[o + j * LPR]; m0[j] = t.m0[o + j * LPR]; v0[j] = t.v0[o + j * LPR];
+    p0[j] = ldp<BF>(t.p0, o + j * LPR); m0[j] = t.m0[o + j * LPR]; v0[j] = t.v0[o + j * LPR];
   }
   if (t.p1) {
 #pragma unroll
     for (int j = 0; j < EPL; ++j) {
-      p1[j] = t.p1[o + j * LPR]; m1[j] = t.m1[o + j * LPR]; v1[j] = t.v1[o + j * LPR];
+      p1[j] = ldp<BF>(t.p1, o + j * LPR); m1[j] = t.m1[o + j * LPR]; v1[j] = t.v1[o + j * LPR];
     }
     if (Replay<D>::LPR == 64) {
-      replay_uniform<EPL, true>(p0, m0, v0, p1, m1, v1, from, to, table, s);
+      replay_uniform<EPL, true, BF>(p0, m0, v0, p1, m1, v1, from, to, table, s);
     } else {
 #pragma unroll 2
       for (int32_t q = from + 1; q <= to; ++q) {
@@ -197,26 +201,30 @@ __device__ __forceinline__ void catch_up_row(const TablePtrs& t, int64_t row, in
         for (int j = 0; j < EPL; ++j) {
           adam1(p0[j], m0[j], v0[j], 0.0f, ns, bc, s);
           adam1(p1[j], m1[j], v1[j], 0.0f, ns, bc, s);
+          if (BF) { p0[j] = ncf_round_bf16(p0[j]); p1[j] = ncf_round_bf16(p1[j]); }
         }
       }
     }
 #pragma unroll
     for (int j = 0; j < EPL; ++j) {
-      t.p1[o + j * LPR] = p1[j]; t.m1[o + j * LPR] = m1[j]; t.v1[o + j * LPR] = v1[j];
+      stp<BF>(t.p1, o + j * LPR, p1[j]); t.m1[o + j * LPR] = m1[j]; t.v1[o + j * LPR] = v1[j];
     }
   } else if (Replay<D>::LPR == 64) {
-    replay_uniform<EPL, false>(p0, m0, v0, p1, m1, v1, from, to, table, s);
+    replay_uniform<EPL, false, BF>(p0, m0, v0, p1, m1, v1, from, to, table, s);
   } else {
 #pragma unroll 2
     for (int32_t q = from + 1; q <= to; ++q) {
       const float ns = table[2 * q], bc = table[2 * q + 1];
 #pragma unroll
-      for (int j = 0; j < EPL; ++j) adam1(p0[j], m0[j], v0[j], 0.0f, ns, bc, s);
+      for (int j = 0; j < EPL; ++j) {
+        adam1(p0[j], m0[j], v0[j], 0.0f, ns, bc, s);
+        if (BF) p0[j] = ncf_round_bf16(p0[j]);
+      }
     }
   }
 #pragma unroll
   for (int j = 0; j < EPL; ++j) {
-    t.p0[o + j * LPR] = p0[j]; t.m0[o + j * LPR] = m0[j]; t.v0[o + j * LPR] = v0[j];
+    stp<BF>(t.p0, o + j * LPR, p0[j]); t.m0[o + j * LPR] = m0[j]; t.v0[o + j * LPR] = v0[j];
   }
 }
 
@@ -242,7 +250,7 @@ __global__ __launch_bounds__(256) void k_adam_catchup(TablePtrs t, const int64_t
 }
 
 // every row of the table caught up to `target` (materialise)
-template <int D>
+template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void k_adam_sweep(TablePtrs t, int64_t row0, int64_t rows,
                                                     int32_t* __restrict__ stamp, int32_t target,
                                                     const float* __restrict__ table, AdamScalars s) {
@@ -253,7 +261,7 @@ __global__ __launch_bounds__(256) void k_adam_sweep(TablePtrs t, int64_t row0, i
     const int64_t row = row0 + e / L;
     const int sub = (int)(e % L);
     const int32_t from = stamp[row];
-    catch_up_row<D>(t, row, sub, from, target, table, s);
+    catch_up_row<D, BF>(t, row, sub, from, target, table, s);
     // all L lanes of the row read stamp before this store: they share one wave-instruction
     if (sub == 0 && from < target) stamp[row] = target;
   }
@@ -339,9 +347,10 @@ struct PairArgs {
   const int64_t* ids[2];
   int32_t* stamp[2];
   int64_t rows[2];
+  int bf;            // parameter rows are bf16 (host-side dispatch only)
 };
 
-template <int D>
+template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void k_pairs_catchup(const PairArgs a, const uint32_t* __restrict__ count,
                                                        int64_t max_n, int32_t target_rel,
                                                        const ncf_step_clock* __restrict__ clock,
@@ -357,11 +366,11 @@ __global__ __launch_bounds__(256) void k_pairs_catchup(const PairArgs a, const u
   const int64_t row = a.ids[k][c];
   int32_t* stamp = a.stamp[k];
   const int32_t from = stamp[row];
-  catch_up_row<D>(a.t[k], row, sub, from, target, table, s);
+  catch_up_row<D, BF>(a.t[k], row, sub, from, target, table, s);
   if (sub == 0 && from < target) stamp[row] = target;
 }
 
-template <int D>
+template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void k_pairs_apply(const PairArgs a, const uint32_t* __restrict__ count,
                                                      int64_t max_n, int32_t step_rel,
                                                      const ncf_step_clock* __restrict__ clock,
@@ -377,18 +386,18 @@ __global__ __launch_bounds__(256) void k_pairs_apply(const PairArgs a, const uin
   const int64_t row = a.ids[k][c];
   const int64_t o = row * D + sub * 4;
   const float ns = table[2 * step], bc = table[2 * step + 1];
-  float4 p0 = ld4(t.p0 + o), m0 = ld4(t.m0 + o), v0 = ld4(t.v0 + o);
+  float4 p0 = ldp4<BF>(t.p0, o), m0 = ld4(t.m0 + o), v0 = ld4(t.v0 + o);
   adam4(p0, m0, v0, ld4(t.G0 + c * D + sub * 4), ns, bc, s);
-  st4(t.p0 + o, p0); st4(t.m0 + o, m0); st4(t.v0 + o, v0);
+  stp4<BF>(t.p0, o, p0); st4(t.m0 + o, m0); st4(t.v0 + o, v0);
   if (t.p1) {
-    float4 p1 = ld4(t.p1 + o), m1 = ld4(t.m1 + o), v1 = ld4(t.v1 + o);
+    float4 p1 = ldp4<BF>(t.p1, o), m1 = ld4(t.m1 + o), v1 = ld4(t.v1 + o);
     adam4(p1, m1, v1, ld4(t.G1 + c * D + sub * 4), ns, bc, s);
-    st4(t.p1 + o, p1); st4(t.m1 + o, m1); st4(t.v1 + o, v1);
+    stp4<BF>(t.p1, o, p1); st4(t.m1 + o, m1); st4(t.v1 + o, v1);
   }
   if (sub == 0) a.stamp[k][row] = step;
 }
 
-template <int D>
+template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void k_pairs_sweep(const PairArgs a, int32_t every,
                                                      int32_t step_rel,
                                                      const ncf_step_clock* __restrict__ clock,
@@ -407,7 +416,7 @@ __global__ __launch_bounds__(256) void k_pairs_sweep(const PairArgs a, int32_t e
     const int64_t row = row0 + e / L;
     const int sub = (int)(e % L);
     const int32_t from = stamp[row];
-    catch_up_row<D>(a.t[k], row, sub, from, target, table, s);
+    catch_up_row<D, BF>(a.t[k], row, sub, from, target, table, s);
     if (sub == 0 && from < target) stamp[row] = target;
   }
 }
@@ -481,9 +490,11 @@ int grid_for(int64_t work) {
 
 template <int D>
 int table_d(float* p, float* m, float* v, int64_t rows, const int32_t* slot, const float* G,
-            const AdamScalars& s, hipStream_t st) {
-  hipLaunchKernelGGL(k_adam_table<D>, dim3(grid_for(rows * (D / 4))), dim3(256), 0, st, p, m, v,
-                     rows, slot, G, s);
+            const AdamScalars& s, hipStream_t st, bool bf = false) {
+  if (bf)
+    hipLaunchKernelGGL((k_adam_table<D, true>), dim3(grid_for(rows * (D / 4))), dim3(256), 0, st, p, m, v, rows, slot, G, s);
+  else
+    hipLaunchKernelGGL((k_adam_table<D, false>), dim3(grid_for(rows * (D / 4))), dim3(256), 0, st, p, m, v, rows, slot, G, s);
   NCF_CHECK_LAUNCH("ncf_adam_table");
   return NCF_OK;
 }
@@ -593,6 +604,7 @@ PairArgs pair_args(const ncf_table_pair* p, int n) {
     a.stamp[k] = p[k].stamp;
     a.rows[k] = p[k].rows;
   }
+  a.bf = p[0].param_dtype == NCF_DTYPE_BF16;
   return a;
 }
 
@@ -600,8 +612,10 @@ template <int D>
 int pairs_catchup_d(PairArgs a, int n, const uint32_t* count, int64_t max_n, int32_t rel,
                     const ncf_step_clock* clock, const float* table, AdamScalars s,
                     hipStream_t st) {
-  hipLaunchKernelGGL(k_pairs_catchup<D>, dim3(ncf_cdiv(max_n * Replay<D>::LPR, 256), n), dim3(256), 0, st,
-                     a, count, max_n, rel, clock, table, s);
+  if (a.bf)
+    hipLaunchKernelGGL((k_pairs_catchup<D, true>), dim3(ncf_cdiv(max_n * Replay<D>::LPR, 256), n), dim3(256), 0, st, a, count, max_n, rel, clock, table, s);
+  else
+    hipLaunchKernelGGL((k_pairs_catchup<D, false>), dim3(ncf_cdiv(max_n * Replay<D>::LPR, 256), n), dim3(256), 0, st, a, count, max_n, rel, clock, table, s);
   NCF_CHECK_LAUNCH("ncf_adam_pairs_catchup_clock");
   return NCF_OK;
 }
@@ -609,8 +623,10 @@ int pairs_catchup_d(PairArgs a, int n, const uint32_t* count, int64_t max_n, int
 template <int D>
 int pairs_apply_d(PairArgs a, int n, const uint32_t* count, int64_t max_n, int32_t rel,
                   const ncf_step_clock* clock, const float* table, AdamScalars s, hipStream_t st) {
-  hipLaunchKernelGGL(k_pairs_apply<D>, dim3(ncf_cdiv(max_n * (D / 4), 256), n), dim3(256), 0, st,
-                     a, count, max_n, rel, clock, table, s);
+  if (a.bf)
+    hipLaunchKernelGGL((k_pairs_apply<D, true>), dim3(ncf_cdiv(max_n * (D / 4), 256), n), dim3(256), 0, st, a, count, max_n, rel, clock, table, s);
+  else
+    hipLaunchKernelGGL((k_pairs_apply<D, false>), dim3(ncf_cdiv(max_n * (D / 4), 256), n), dim3(256), 0, st, a, count, max_n, rel, clock, table, s);
   NCF_CHECK_LAUNCH("ncf_adam_pairs_apply_clock");
   return NCF_OK;
 }
@@ -620,17 +636,21 @@ int pairs_sweep_d(PairArgs a, int n, int32_t every, int32_t rel, const ncf_step_
                   const float* table, AdamScalars s, hipStream_t st) {
   int64_t slice = 0;
   for (int k = 0; k < n; ++k) slice = max(slice, (a.rows[k] + every - 1) / every);
-  hipLaunchKernelGGL(k_pairs_sweep<D>, dim3(grid_for(slice * Replay<D>::LPR), n), dim3(256), 0, st, a,
-                     every, rel, clock, table, s);
+  if (a.bf)
+    hipLaunchKernelGGL((k_pairs_sweep<D, true>), dim3(grid_for(slice * Replay<D>::LPR), n), dim3(256), 0, st, a, every, rel, clock, table, s);
+  else
+    hipLaunchKernelGGL((k_pairs_sweep<D, false>), dim3(grid_for(slice * Replay<D>::LPR), n), dim3(256), 0, st, a, every, rel, clock, table, s);
   NCF_CHECK_LAUNCH("ncf_adam_pairs_sweep_rolling");
   return NCF_OK;
 }
 
 template <int D>
 int sweep_d(TablePtrs t, int64_t row0, int64_t rows, int32_t* stamp, int32_t target,
-            const float* table, AdamScalars s, hipStream_t st) {
-  hipLaunchKernelGGL(k_adam_sweep<D>, dim3(grid_for(rows * Replay<D>::LPR)), dim3(256), 0, st, t, row0,
-                     rows, stamp, target, table, s);
+            const float* table, AdamScalars s, hipStream_t st, bool bf = false) {
+  if (bf)
+    hipLaunchKernelGGL((k_adam_sweep<D, true>), dim3(grid_for(rows * Replay<D>::LPR)), dim3(256), 0, st, t, row0, rows, stamp, target, table, s);
+  else
+    hipLaunchKernelGGL((k_adam_sweep<D, false>), dim3(grid_for(rows * Replay<D>::LPR)), dim3(256), 0, st, t, row0, rows, stamp, target, table, s);
   NCF_CHECK_LAUNCH("ncf_adam_sweep");
   return NCF_OK;
 }
@@ -687,6 +707,33 @@ extern "C" int ncf_adam_sweep(float* p0, float* m0, float* v0, float* p1, float*
   TablePtrs t{p0, m0, v0, p1, m1, v1, nullptr, nullptr};
   NCF_DISPATCH_DIM(dim, sweep_d, t, row0, rows, stamp, target, step_table,
                    consts_of(beta1, beta2, eps, weight_decay), (hipStream_t)stream);
+}
+
+// bf16 parameter rows (fp32 moments): the same step / sweep, the parameter rounded to bf16
+// (nearest even) after every step it takes
+extern "C" int ncf_adam_table_bf16(uint16_t* param, float* exp_avg, float* exp_avg_sq, int64_t rows,
+                                   int64_t dim, const int32_t* slot, const float* grad_compact,
+                                   double lr, double beta1, double beta2, double eps,
+                                   double weight_decay, double step, void* stream) {
+  NCF_CHECK_ARG(rows >= 0 && step >= 1, "ncf_adam_table_bf16: bad args");
+  if (rows == 0) return NCF_OK;
+  NCF_CHECK_ARG(param && exp_avg && exp_avg_sq, "ncf_adam_table_bf16: null pointer");
+  const AdamScalars s = make_scalars(lr, beta1, beta2, eps, weight_decay, step);
+  NCF_DISPATCH_DIM(dim, table_d, reinterpret_cast<float*>(param), exp_avg, exp_avg_sq, rows, slot,
+                   grad_compact, s, (hipStream_t)stream, true);
+}
+
+extern "C" int ncf_adam_sweep_bf16(uint16_t* p0, float* m0, float* v0, uint16_t* p1, float* m1,
+                                   float* v1, int64_t row0, int64_t rows, int64_t dim,
+                                   int32_t* stamp, int32_t target, const float* step_table,
+                                   double beta1, double beta2, double eps, double weight_decay,
+                                   void* stream) {
+  if (rows <= 0) return NCF_OK;
+  NCF_CHECK_ARG(p0 && m0 && v0 && stamp && step_table && row0 >= 0, "ncf_adam_sweep_bf16: bad args");
+  TablePtrs t{reinterpret_cast<float*>(p0), m0, v0, reinterpret_cast<float*>(p1), m1, v1, nullptr,
+              nullptr};
+  NCF_DISPATCH_DIM(dim, sweep_d, t, row0, rows, stamp, target, step_table,
+                   consts_of(beta1, beta2, eps, weight_decay), (hipStream_t)stream, true);
 }
 
 // ---- clock-driven forms (hipGraph-capturable training step)

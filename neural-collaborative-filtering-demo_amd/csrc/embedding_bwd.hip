@@ -27,7 +27,7 @@ namespace {
 
 // part[kind*nbr + block][0:D mf_g | D:2D mf_b | 2D:3D mlp_g | 3D:4D mlp_b]
 constexpr int kPW = NCF_PIECE_WAVES;   // waves per block
-template <int D>
+template <int D, bool BF = false>
 __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     const uint32_t* __restrict__ sv0, const uint32_t* __restrict__ sv1,
     const uint32_t* __restrict__ pstart0, const uint32_t* __restrict__ pstart1,
@@ -76,8 +76,8 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
       cnt = (int)(pstart[p + 1] - ps);  // 1..PIECE
       info = pseg[p];
       const int64_t id = uniq[info & ~FIRST_PIECE];
-      x_mf = ld4(tmf + id * D + col);
-      x_ml = ld4(tml + id * D + col);
+      x_mf = ldp4<BF>(tmf, id * D + col);   // (BF: bf16 table rows, widened exactly)
+      x_ml = ldp4<BF>(tml, id * D + col);
     }
     int cmax = cnt;   // the wave's longest piece: loop bounds stay wave-uniform
 #pragma unroll
@@ -225,11 +225,18 @@ int piece_reduce(const WS& w, int64_t n, const uint32_t* sv0, const uint32_t* sv
                  const float* dmf1, const float* dml1, const float* tmf0, const float* tml0,
                  const float* tmf1, const float* tml1, const float* gmf, const float* gml,
                  float eps, float* Gmf0, float* Gml0, float* Gmf1, float* Gml1, float* dgm,
-                 float* dbm, float* dgl, float* dbl, ncf_reduce_list* defer, hipStream_t st) {
-  hipLaunchKernelGGL(k_piece_reduce_ln<D>, dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1, w.pstart0,
-                     w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
-                     dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
-                     Gmf1, Gml1, w.xp0, w.xp1, w.part);
+                 float* dbm, float* dgl, float* dbl, ncf_reduce_list* defer, hipStream_t st,
+                 bool bf = false) {
+  if (bf)
+    hipLaunchKernelGGL((k_piece_reduce_ln<D, true>), dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1,
+                       w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
+                       dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
+                       Gmf1, Gml1, w.xp0, w.xp1, w.part);
+  else
+    hipLaunchKernelGGL((k_piece_reduce_ln<D, false>), dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1,
+                       w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
+                       dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
+                       Gmf1, Gml1, w.xp0, w.xp1, w.part);
   NCF_CHECK_LAUNCH("ncf_embedding_bwd(piece_reduce)");
   constexpr int L = D / 4;
   const int64_t fb = ncf_cdiv(n * L, 256);
@@ -257,7 +264,7 @@ int piece_reduce(const WS& w, int64_t n, const uint32_t* sv0, const uint32_t* sv
 // Phase 2: per unique id, sum the LN-output gradients of its occurrences (position order) and
 // apply mf_norm / mlp_norm backward; dgamma/dbeta of both norms.  Requires the workspace filled
 // by ncf_dedup_ids for the same ids.
-extern "C" int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_users,
+static int embedding_bwd_reduce(bool bf, int64_t n, int64_t dim, int64_t num_users,
                                         int64_t num_items, const float* dy_mf_user,
                                         const float* dy_mlp_user, const float* dy_mf_item,
                                         const float* dy_mlp_item, const float* mf_user,
@@ -289,11 +296,53 @@ extern "C" int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_user
                             dy_mf_item, dy_mlp_item, mf_user, mlp_user, mf_item, mlp_item,        \
                             mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user, grad_mf_item,  \
                             grad_mlp_item, grad_mf_gamma, grad_mf_beta, grad_mlp_gamma,           \
-                            grad_mlp_beta, defer, st);
+                            grad_mlp_beta, defer, st, bf);
     SEG(16) SEG(32) SEG(64) SEG(128) SEG(256)
 #undef SEG
   }
   return NCF_ERR_ARG;
+}
+
+extern "C" int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_users,
+                                        int64_t num_items, const float* dy_mf_user,
+                                        const float* dy_mlp_user, const float* dy_mf_item,
+                                        const float* dy_mlp_item, const float* mf_user,
+                                        const float* mlp_user, const float* mf_item,
+                                        const float* mlp_item, const float* mf_gamma,
+                                        const float* mlp_gamma, float eps, float* grad_mf_user,
+                                        float* grad_mlp_user, float* grad_mf_item,
+                                        float* grad_mlp_item, const int64_t* uniq_users,
+                                        const int64_t* uniq_items, float* grad_mf_gamma,
+                                        float* grad_mf_beta, float* grad_mlp_gamma,
+                                        float* grad_mlp_beta, void* workspace,
+                                        int64_t workspace_bytes, ncf_reduce_list* defer,
+                                        void* stream) {
+  return embedding_bwd_reduce(false, n, dim, num_users, num_items, dy_mf_user, dy_mlp_user,
+                              dy_mf_item, dy_mlp_item, mf_user, mlp_user, mf_item, mlp_item,
+                              mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user, grad_mf_item,
+                              grad_mlp_item, uniq_users, uniq_items, grad_mf_gamma, grad_mf_beta,
+                              grad_mlp_gamma, grad_mlp_beta, workspace, workspace_bytes, defer,
+                              stream);
+}
+
+// The same with bf16 table rows (the LayerNorm recompute reads them; gradients stay fp32).
+extern "C" int ncf_embedding_bwd_reduce_bf16(
+    int64_t n, int64_t dim, int64_t num_users, int64_t num_items, const float* dy_mf_user,
+    const float* dy_mlp_user, const float* dy_mf_item, const float* dy_mlp_item,
+    const uint16_t* mf_user, const uint16_t* mlp_user, const uint16_t* mf_item,
+    const uint16_t* mlp_item, const float* mf_gamma, const float* mlp_gamma, float eps,
+    float* grad_mf_user, float* grad_mlp_user, float* grad_mf_item, float* grad_mlp_item,
+    const int64_t* uniq_users, const int64_t* uniq_items, float* grad_mf_gamma,
+    float* grad_mf_beta, float* grad_mlp_gamma, float* grad_mlp_beta, void* workspace,
+    int64_t workspace_bytes, ncf_reduce_list* defer, void* stream) {
+  return embedding_bwd_reduce(true, n, dim, num_users, num_items, dy_mf_user, dy_mlp_user,
+                              dy_mf_item, dy_mlp_item, reinterpret_cast<const float*>(mf_user),
+                              reinterpret_cast<const float*>(mlp_user),
+                              reinterpret_cast<const float*>(mf_item),
+                              reinterpret_cast<const float*>(mlp_item), mf_gamma, mlp_gamma, eps,
+                              grad_mf_user, grad_mlp_user, grad_mf_item, grad_mlp_item, uniq_users,
+                              uniq_items, grad_mf_gamma, grad_mf_beta, grad_mlp_gamma,
+                              grad_mlp_beta, workspace, workspace_bytes, defer, stream);
 }
 
 // Both phases (dedup + reduce), with slot maps for the dense-exact table Adam.

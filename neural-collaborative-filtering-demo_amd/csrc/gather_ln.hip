@@ -36,7 +36,7 @@ __device__ __forceinline__ int64_t safe_id(int64_t id, int64_t rows, int* err, b
   return id;
 }
 
-template <int D>
+template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void k_gather_ln_gmf(
     const int64_t* __restrict__ uid, const int64_t* __restrict__ iid, int64_t n,
     const float* __restrict__ mfU, const float* __restrict__ mfI, const float* __restrict__ mlpU,
@@ -54,8 +54,9 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
   const int64_t u = safe_id(uid[row], nU, err, sub == 0);
   const int64_t i = safe_id(iid[row], nI, err, sub == 0);
   const int c = sub * 4;
-  const float4 xu_mf = ld4(mfU + u * D + c), xi_mf = ld4(mfI + i * D + c);
-  const float4 xu_ml = ld4(mlpU + u * D + c), xi_ml = ld4(mlpI + i * D + c);
+  // (BF: the table rows are bf16; widened exactly to fp32 here, everything after is fp32)
+  const float4 xu_mf = ldp4<BF>(mfU, u * D + c), xi_mf = ldp4<BF>(mfI, i * D + c);
+  const float4 xu_ml = ldp4<BF>(mlpU, u * D + c), xi_ml = ldp4<BF>(mlpI, i * D + c);
   const float4 gm = ld4(g_mf + c), bm = ld4(b_mf + c), gl = ld4(g_mlp + c), bl = ld4(b_mlp + c);
   const float4 yu = RowLN<D>::ln(xu_mf, gm, bm, eps);
   float4 yi = RowLN<D>::ln(xi_mf, gm, bm, eps);
@@ -103,7 +104,7 @@ __global__ __launch_bounds__(256) void k_gather_rows_t(const int64_t* __restrict
   st4(out + row * D + c, x);
 }
 
-template <int D>
+template <int D, bool BF = false>
 int launch_gather_ln_gmf(const int64_t* uid, const int64_t* iid, int64_t n, const float* mfU,
                          const float* mfI, const float* mlpU, const float* mlpI, int64_t nU,
                          int64_t nI, const float* g_mf, const float* b_mf, const float* g_mlp,
@@ -112,7 +113,7 @@ int launch_gather_ln_gmf(const int64_t* uid, const int64_t* iid, int64_t n, cons
                          float* i_mf_ln, int* err, const float* item_scale, float scale_factor,
                          hipStream_t st) {
   const int64_t threads = n * (D / 4);
-  hipLaunchKernelGGL(k_gather_ln_gmf<D>, dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st, uid, iid,
+  hipLaunchKernelGGL((k_gather_ln_gmf<D, BF>), dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st, uid, iid,
                      n, mfU, mfI, mlpU, mlpI, nU, nI, g_mf, b_mf, g_mlp, b_mlp, w_mf, bias_mf, eps,
                      mf_pred, u_mlp_ln, i_mlp_ln, u_mf_ln, i_mf_ln, err, item_scale, scale_factor);
   NCF_CHECK_LAUNCH("ncf_gather_ln_gmf_fwd");
@@ -142,6 +143,19 @@ int launch_gather_rows_l2(const int64_t* ids, int64_t n, const float* table, int
 }
 
 }  // namespace
+
+template <int D>
+int launch_gather_ln_gmf_bf16(const int64_t* uid, const int64_t* iid, int64_t n, const float* mfU,
+                              const float* mfI, const float* mlpU, const float* mlpI, int64_t nU,
+                              int64_t nI, const float* g_mf, const float* b_mf, const float* g_mlp,
+                              const float* b_mlp, const float* w_mf, const float* bias_mf,
+                              float eps, float* mf_pred, float* u_mlp_ln, float* i_mlp_ln,
+                              float* u_mf_ln, float* i_mf_ln, int* err, const float* item_scale,
+                              float scale_factor, hipStream_t st) {
+  return launch_gather_ln_gmf<D, true>(uid, iid, n, mfU, mfI, mlpU, mlpI, nU, nI, g_mf, b_mf, g_mlp,
+                                       b_mlp, w_mf, bias_mf, eps, mf_pred, u_mlp_ln, i_mlp_ln,
+                                       u_mf_ln, i_mf_ln, err, item_scale, scale_factor, st);
+}
 
 #define NCF_DISPATCH_D(D, FN, ...)                                            \
   switch (D) {                                                                \
@@ -213,4 +227,29 @@ extern "C" int ncf_embedding_export(const int64_t* ids, int64_t n, const float* 
     return ncf_gather_rows(ids, n, table, rows, dim, ln_gamma, ln_beta, eps, out, err_flag, stream);
   NCF_DISPATCH_D(dim, launch_gather_rows_l2, ids, n, table, rows, ln_gamma, ln_beta, eps, out,
                  err_flag, (hipStream_t)stream);
+}
+
+// The training gather of the bf16-table configuration: the four tables hold bf16 rows (uint16
+// bit patterns); LayerNorm, GMF and every output stay fp32.
+extern "C" int ncf_gather_ln_gmf_bf16_fwd(
+    const int64_t* user_ids, const int64_t* item_ids, int64_t n, const uint16_t* mf_user,
+    const uint16_t* mf_item, const uint16_t* mlp_user, const uint16_t* mlp_item, int64_t num_users,
+    int64_t num_items, int64_t dim, const float* mf_gamma, const float* mf_beta,
+    const float* mlp_gamma, const float* mlp_beta, const float* mf_out_w, const float* mf_out_b,
+    float eps, float* mf_pred, float* mlp_user_ln, float* mlp_item_ln, float* mf_user_ln,
+    float* mf_item_ln, int* err_flag, void* stream) {
+  NCF_CHECK_ARG(n >= 0, "ncf_gather_ln_gmf_bf16_fwd: n < 0");
+  if (n == 0) return NCF_OK;
+  NCF_CHECK_ARG(user_ids && item_ids && mf_user && mf_item && mlp_user && mlp_item && mf_pred &&
+                    mlp_user_ln && mlp_item_ln && mf_gamma && mf_beta && mlp_gamma && mlp_beta &&
+                    mf_out_w && mf_out_b,
+                "ncf_gather_ln_gmf_bf16_fwd: null pointer");
+  const float* t0 = reinterpret_cast<const float*>(mf_user);
+  const float* t1 = reinterpret_cast<const float*>(mf_item);
+  const float* t2 = reinterpret_cast<const float*>(mlp_user);
+  const float* t3 = reinterpret_cast<const float*>(mlp_item);
+  NCF_DISPATCH_D(dim, launch_gather_ln_gmf_bf16, user_ids, item_ids, n, t0, t1, t2, t3, num_users,
+                 num_items, mf_gamma, mf_beta, mlp_gamma, mlp_beta, mf_out_w, mf_out_b, eps,
+                 mf_pred, mlp_user_ln, mlp_item_ln, mf_user_ln, mf_item_ln, err_flag, nullptr,
+                 0.0f, (hipStream_t)stream);
 }

@@ -51,6 +51,49 @@ __device__ __forceinline__ float wave_sum(float v) { return group_sum<64>(v); }
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
+// ---- bf16 embedding tables (the C2 "bf16" configuration: tables bf16, Adam moments fp32).
+// A bf16 value is the high half of the fp32 with the same leading bits; fp32 -> bf16 rounds to
+// nearest even (NaN kept quiet).  Table kernels templated on BF read / write their parameter
+// rows through ldp/stp (element index i of a float* that really points at bf16 when BF).
+__device__ __forceinline__ float ncf_bf2f(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ __forceinline__ uint32_t ncf_f2bf(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float ncf_round_bf16(float f) { return ncf_bf2f(ncf_f2bf(f)); }
+template <bool BF>
+__device__ __forceinline__ float ldp(const float* p, int64_t i) {
+  if constexpr (BF) return ncf_bf2f(reinterpret_cast<const uint16_t*>(p)[i]);
+  else return p[i];
+}
+template <bool BF>
+__device__ __forceinline__ void stp(float* p, int64_t i, float v) {
+  if constexpr (BF) reinterpret_cast<uint16_t*>(p)[i] = (uint16_t)ncf_f2bf(v);
+  else p[i] = v;
+}
+template <bool BF>
+__device__ __forceinline__ float4 ldp4(const float* p, int64_t i) {   // i: multiple of 4
+  if constexpr (BF) {
+    const uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(p) + i);
+    return make_float4(__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
+                       __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u));
+  } else {
+    return ld4(p + i);
+  }
+}
+template <bool BF>
+__device__ __forceinline__ void stp4(float* p, int64_t i, float4 v) {
+  if constexpr (BF) {
+    uint2 r;
+    r.x = ncf_f2bf(v.x) | (ncf_f2bf(v.y) << 16);
+    r.y = ncf_f2bf(v.z) | (ncf_f2bf(v.w) << 16);
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p) + i) = r;
+  } else {
+    st4(p + i, v);
+  }
+}
+
 // Counter-based dropout RNG: a 64-bit mix of (seed, element index) -> uniform [0,1).
 // Deterministic per (seed, index); independent of launch geometry.
 // Dropout keep decisions.  One 64-bit hash (ncf_drop_bits) of (seed, idx / 4) yields four 16-bit uniforms,

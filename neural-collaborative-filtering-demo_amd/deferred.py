@@ -33,7 +33,8 @@ _SERIAL = itertools.count(1)      # distinguishes schedules in workspace caches 
 
 class DeferredTableAdam:
     def __init__(self, engine, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
-                 sweep_every: int = 64, moments=None, clock=None, overlap_sweep=None):
+                 sweep_every: int = 64, moments=None, clock=None, overlap_sweep=None,
+                 param_tables=None):
         self.engine = engine
         self._serial = next(_SERIAL)
         # clock (ncf_step_clock, device): every step-dependent value is read on the device, so
@@ -42,10 +43,15 @@ class DeferredTableAdam:
         self.lr, self.eps, self.wd = float(lr), float(eps), float(weight_decay)
         self.betas = (float(betas[0]), float(betas[1]))
         self.sweep_every = int(sweep_every)
-        self.tables = engine.table_params()
+        # the rows the schedule updates: the fp32 table parameters, or (bf16-table
+        # configuration) bf16 tables that own the values, with the fp32 parameters a widened
+        # copy brought up to date by sync()
+        self.params = engine.table_params()
+        self.tables = dict(param_tables) if param_tables is not None else self.params
+        self.bf16 = self.tables["mf_user"].dtype == torch.bfloat16
         dev = self.tables["mf_user"].device
         self.state = moments or {k: {"exp_avg": torch.zeros_like(p), "exp_avg_sq": torch.zeros_like(p)}
-                                 for k, p in self.tables.items()}
+                                 for k, p in self.params.items()}     # (fp32 moments)
         m = engine.model
         self.stamp = {"user": torch.zeros(m.num_users, dtype=torch.int32, device=dev),
                       "item": torch.zeros(m.num_products, dtype=torch.int32, device=dev)}
@@ -249,6 +255,7 @@ class DeferredTableAdam:
             pr = pairs[k]
             pr.p0, pr.m0, pr.v0, pr.p1, pr.m1, pr.v1 = p0, m0, v0, p1, m1, v1
             pr.stamp, pr.rows = ptr(self.stamp[kind]), self.stamp[kind].numel()
+            pr.param_dtype = _lib.DTYPE_BF16 if self.bf16 else _lib.DTYPE_F32
             if w is not None:
                 pr.row_ids = ptr(w.uniq_u if k == 0 else w.uniq_i)
                 pr.g0, pr.g1 = ptr(w.G[a]), ptr(w.G[b])
@@ -296,7 +303,7 @@ class DeferredTableAdam:
         if rows <= 0 or self.t == 0:
             return
         self._ensure(self.t)
-        _lib.call("ncf_adam_sweep", *self._ptrs(kind), row0, rows,
+        _lib.call("ncf_adam_sweep_bf16" if self.bf16 else "ncf_adam_sweep", *self._ptrs(kind), row0, rows,
                   self.engine.model.mlp_embedding_dim, ptr(self.stamp[kind]), self.t,
                   ptr(self._table), *self._consts(), st)
 
@@ -306,6 +313,23 @@ class DeferredTableAdam:
         for kind in ("user", "item"):
             self._sweep_range(kind, 0, self.stamp[kind].numel(), st)
         self.synced_t = self.t
+        self.widen()
+
+    def widen(self):
+        """bf16 tables: the fp32 table parameters := the bf16 values (exactly representable)."""
+        if self.bf16:
+            with torch.no_grad():
+                for k, p in self.params.items():
+                    p.copy_(self.tables[k])
+
+    def reload_params(self):
+        """bf16 tables: take new fp32 parameter values (load_state_dict): round them into the
+        bf16 tables and widen back, every row current."""
+        if self.bf16:
+            with torch.no_grad():
+                for k, p in self.params.items():
+                    self.tables[k].copy_(p)
+            self.widen()
 
     def sync(self):
         """Catch every row up to the current step (tables + moments become the dense values)."""

@@ -350,7 +350,7 @@ class NCFEngine:
 
     def forward(self, uid: torch.Tensor, iid: torch.Tensor, M: int, train: bool,
                 drop_p: float, seed: int, prepare=None, tables=None, rows=None,
-                temporal=None) -> Workspace:
+                temporal=None, bf16: bool = False) -> Workspace:
         """AdvancedNCF.forward (architecture.py:258-381) on single-id bags; returns the workspace
         holding prob (and, when ``train``, everything the backward needs).  ``prepare(w, uid,
         iid, stream)`` runs before the gathers (the deferred Adam dedups the ids there and
@@ -389,11 +389,20 @@ class NCFEngine:
             raise ValueError("the temporal (hour) path is forward_simple's: eval, one item per group")
         # a2-a4: 4 gathers + mf_norm/mlp_norm + GMF  (architecture.py:286-287, 305-312)
         t_scale, t_factor = (temporal[0], temporal[1]) if temporal is not None else (None, 0.0)
-        _lib.call("ncf_gather_ln_gmf_scaled_fwd", ptr(uid), ptr(iid), n, *tbp, n_users,
-                  n_items, D, pp["mf_norm.weight"], pp["mf_norm.bias"],
-                  pp["mlp_norm.weight"], pp["mlp_norm.bias"], pp["mf_output.weight"],
-                  pp["mf_output.bias"], LN_EPS, ptr(t_scale), float(t_factor), ptr(w.mf_pred),
-                  ptr(w.xu), ptr(w.xi), ptr(w.umf), ptr(w.imf), ptr(w.err), st)
+        if bf16:    # bf16 tables (``tables`` holds them): rows widened to fp32 in the gather
+            if temporal is not None:
+                raise ValueError("the bf16-table configuration is a training configuration")
+            _lib.call("ncf_gather_ln_gmf_bf16_fwd", ptr(uid), ptr(iid), n, *tbp, n_users,
+                      n_items, D, pp["mf_norm.weight"], pp["mf_norm.bias"],
+                      pp["mlp_norm.weight"], pp["mlp_norm.bias"], pp["mf_output.weight"],
+                      pp["mf_output.bias"], LN_EPS, ptr(w.mf_pred), ptr(w.xu), ptr(w.xi),
+                      ptr(w.umf), ptr(w.imf), ptr(w.err), st)
+        else:
+            _lib.call("ncf_gather_ln_gmf_scaled_fwd", ptr(uid), ptr(iid), n, *tbp, n_users,
+                      n_items, D, pp["mf_norm.weight"], pp["mf_norm.bias"],
+                      pp["mlp_norm.weight"], pp["mlp_norm.bias"], pp["mf_output.weight"],
+                      pp["mf_output.bias"], LN_EPS, ptr(t_scale), float(t_factor),
+                      ptr(w.mf_pred), ptr(w.xu), ptr(w.xi), ptr(w.umf), ptr(w.imf), ptr(w.err), st)
         # a5: MultiHeadAttention over each group of M rows (architecture.py:315-326)
         att = m.user_product_attention
         if temporal is None and self.attn_block(D, H, M):
@@ -581,7 +590,7 @@ class NCFEngine:
     def backward(self, w: Workspace, uid, iid, grad_prob: Optional[torch.Tensor],
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,
                  loss_denominator: float = 0.0, tables=None, rows=None, uniq=None,
-                 reduce_async: bool = False):
+                 reduce_async: bool = False, bf16: bool = False):
         """Gradients of every used parameter.  Dense grads land in the flat grad buffer; table
         grads stay compact (self.pending) for the fused Adam step.  ``reduce_async``: the
         deferred reductions (every dense gradient) run on a side stream, beside whatever the
@@ -699,7 +708,8 @@ class NCFEngine:
                       ptr(w.uniq_u), ptr(w.uniq_i), ptr(self.slot_u), ptr(self.slot_i),
                       ptr(w.num_unique), ptr(w.emb_ws), w.emb_ws.numel(), st)
             w.slots_set = True
-        _lib.call("ncf_embedding_bwd_reduce", n, D, d_rows[0], d_rows[1],
+        _lib.call("ncf_embedding_bwd_reduce_bf16" if bf16 else "ncf_embedding_bwd_reduce", n, D,
+                  d_rows[0], d_rows[1],
                   ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), *tbp,
                   pp["mf_norm.weight"], pp["mlp_norm.weight"], LN_EPS, ptr(G["mf_user"]),
                   ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(uq_u),

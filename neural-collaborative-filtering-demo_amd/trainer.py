@@ -41,7 +41,7 @@ class FusedTrainStep:
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5,
                  deferred: bool = True, sweep_every: int = 64, graph: bool = False,
                  clock: Optional[bool] = None, warmup: int = 2, concurrent: Optional[bool] = None,
-                 overlap_sweep: bool = False):
+                 overlap_sweep: bool = False, table_dtype: torch.dtype = torch.float32):
         self.model = model
         self.deferred = None
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
@@ -52,6 +52,19 @@ class FusedTrainStep:
         self.tables = eng.table_params()
         self.state = {k: {"exp_avg": torch.zeros_like(p), "exp_avg_sq": torch.zeros_like(p)}
                       for k, p in self.tables.items()}
+        # bf16-table configuration (BASELINE.json configs[1] "bf16", SURVEY 8(d) C2: tables bf16,
+        # Adam moments fp32): the four tables live as bf16 (half the row bytes of every gather,
+        # segment reduce and table update); the model's fp32 table parameters hold the same
+        # values widened, brought up to date by sync() (state_dict, eval forward, exports).
+        if table_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("table_dtype must be torch.float32 or torch.bfloat16")
+        self.bf16 = table_dtype == torch.bfloat16
+        self.tables_lp = None
+        if self.bf16:
+            with torch.no_grad():
+                self.tables_lp = {k: p.detach().to(torch.bfloat16) for k, p in self.tables.items()}
+                for k, p in self.tables.items():
+                    p.copy_(self.tables_lp[k])
         self.m_flat = torch.zeros_like(eng.flat)
         self.v_flat = torch.zeros_like(eng.flat)
         self.last_loss = None
@@ -74,7 +87,8 @@ class FusedTrainStep:
             from .deferred import DeferredTableAdam
             self.deferred = DeferredTableAdam(eng, lr, betas, eps, weight_decay, sweep_every,
                                               moments=self.state, clock=self.clock,
-                                              overlap_sweep=overlap_sweep and self.clock is not None)
+                                              overlap_sweep=overlap_sweep and self.clock is not None,
+                                              param_tables=self.tables_lp)
         self.warmup = warmup
         # independent kernels on side streams.  Off by default: measured slower on MI355X, eager
         # (0.63 vs 0.54 ms) and captured (0.71 vs 0.58 ms) — a cross-queue dependency costs more
@@ -106,14 +120,25 @@ class FusedTrainStep:
         if drop_p > 0 and self.clock is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         prep = self.deferred.prepare if self.deferred is not None else None
-        w = eng.forward(user_ids, item_ids, M, True, drop_p, seed, prepare=prep)
+        w = eng.forward(user_ids, item_ids, M, True, drop_p, seed, prepare=prep,
+                        tables=self.tables_lp, bf16=self.bf16)
         # (reduce_async=True would run the dense-gradient reductions beside the table Adam:
         # measured neutral here and slower on the row-sharded step, so off)
-        eng.backward(w, user_ids, item_ids, None, targets, drop_p, seed)
+        eng.backward(w, user_ids, item_ids, None, targets, drop_p, seed, tables=self.tables_lp,
+                     bf16=self.bf16)
         st = _lib.stream_ptr(eng.flat.device)
         b1, b2 = self.betas
         if self.deferred is not None:
             self.deferred.apply(w, st)
+        elif self.bf16:      # dense bf16 sweep (the reference schedule of the bf16 tables)
+            D = self.model.mlp_embedding_dim
+            for key, lp in self.tables_lp.items():
+                slot = eng.slot_u if key.endswith("user") else eng.slot_i
+                s_ = self.state[key]
+                _lib.call("ncf_adam_table_bf16", ptr(lp), ptr(s_["exp_avg"]), ptr(s_["exp_avg_sq"]),
+                          lp.shape[0], D, ptr(slot), ptr(w.G[key]), self.lr, b1, b2, self.eps,
+                          self.wd, float(self.step_count + 1), st)
+            eng.release_pending(st)
         else:
             hp = lambda p: (self.lr, b1, b2, self.eps, self.wd)  # noqa: E731
             key_of = {id(p): k for k, p in self.tables.items()}
@@ -258,6 +283,10 @@ class FusedTrainStep:
     def sync(self):
         if self.deferred is not None:
             self.deferred.sync()
+        elif self.bf16:
+            with torch.no_grad():
+                for k, p in self.tables.items():
+                    p.copy_(self.tables_lp[k])
 
     def load_optimizer_state(self, state_dict):
         """Resume from a ``torch.optim.Adam(model.parameters())`` state_dict (what

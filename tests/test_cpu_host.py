@@ -266,7 +266,10 @@ def test_struct_mirrors_match_header_layouts():
     assert [f[0] for f in _lib.MlpLayer._fields_] == ["w", "ldw", "b", "gamma", "beta", "r", "a",
                                                        "mean", "rstd", "dlin", "dbias", "dgamma",
                                                        "dbeta", "dw"]
-    assert ctypes.sizeof(_lib.TablePair) == 11 * 8
+    assert ctypes.sizeof(_lib.TablePair) == 12 * 8
+    body = hdr_pair = open(os.path.join(ROOT, "include", "ncf_hip.h")).read()
+    body = hdr_pair[hdr_pair.index("typedef struct ncf_table_pair"):hdr_pair.index("} ncf_table_pair;")]
+    assert re.findall(r"(\w+)[,;]", body) == [f[0] for f in _lib.TablePair._fields_]
     hdr = open(os.path.join(ROOT, "include", "ncf_hip.h")).read()
     body = hdr[hdr.index("typedef struct ncf_mlp_layer"):hdr.index("} ncf_mlp_layer;")]
     names = re.findall(r"\*?\s*(\w+);", body)
