@@ -56,12 +56,11 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 // nearest even (NaN kept quiet).  Table kernels templated on BF read / write their parameter
 // rows through ldp/stp (element index i of a float* that really points at bf16 when BF).
 __device__ __forceinline__ float ncf_bf2f(uint32_t h) { return __uint_as_float(h << 16); }
+// one v_cvt_pk_bf16_f32 (IEEE round to nearest even) on gfx950
 __device__ __forceinline__ uint32_t ncf_f2bf(float f) {
-  const uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
-  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
-__device__ __forceinline__ float ncf_round_bf16(float f) { return ncf_bf2f(ncf_f2bf(f)); }
+__device__ __forceinline__ float ncf_round_bf16(float f) { return (float)(__bf16)f; }
 template <bool BF>
 __device__ __forceinline__ float ldp(const float* p, int64_t i) {
   if constexpr (BF) return ncf_bf2f(reinterpret_cast<const uint16_t*>(p)[i]);

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--tag", default=os.environ.get("NCF_HIP_LIB", "default"))
     ap.add_argument("--warmup", type=int, default=140)
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--bf16", action="store_true", help="bf16-table configuration")
     a = ap.parse_args()
     ncf = _ncf_pkg.load()
     from ncf_amd import _lib as L
@@ -34,7 +35,8 @@ def main():
     torch.manual_seed(1234)
     U, I, B, M = 1_000_000, 100_000, 4096, 5
     m = ncf.AdvancedNCF(U, I, 10, 50, 64, 64, 32, [256, 128, 64], 4, 0.2, 4).to(dev).train()
-    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5,
+                          table_dtype=torch.bfloat16 if a.bf16 else torch.float32)
     batches = make_batches(U, I, B, M, 8, dev, seed=100)
 
     def run(first, n, pipe=True):
