@@ -64,6 +64,8 @@ SIGNATURES = {
     "ncf_embedding_export": (I32, [P, I64, P, I64, I64, P, P, F32, I32, P, P, P]),
     "ncf_sample_negatives": (I32, [P, P, I64, I64, P, P, I64, P, P, I64, U64, I64, P, P, P, P, P]),
     "ncf_mlp_fwd": (I32, [P, I64, I64, P, I64, P, F32, F32, U64, P, P, P, P, P, P, P, P, P]),
+    "ncf_mlp_fwd_bf16": (I32, [P, I64, I64, P, I64, P, F32, F32, U64, P, P, P, P, P, P, P, P, P]),
+    "ncf_mlp_bwd_bf16": (I32, [P, I64, I64, P, P, I64, P, F32, U64, P, P, P, P, I64, P, P]),
     "ncf_mlp_bwd_workspace": (I64, [I64]),
     "ncf_mlp_bwd": (I32, [P, I64, I64, P, P, I64, P, F32, U64, P, P, P, P, I64, P, P]),
     "ncf_attn_block_fwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, F32, U64, P,

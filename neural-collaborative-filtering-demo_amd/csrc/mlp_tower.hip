@@ -125,6 +125,26 @@ __device__ __forceinline__ float4 act4(const ncf_mlp_layer& L, int64_t row, int 
   return drop4(y, seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
 }
 
+// bf16 MFMA (the bf16 configuration, BF=true): operands rounded to bf16 (v_cvt_pk_bf16_f32),
+// fp32 accumulate.  The k-permuted fp32 layout carries over unchanged: the float4 a lane group
+// feeds to 4 consecutive f32 MFMA k-steps is exactly the 4-element k slot of lane group g in
+// v_mfma_f32_16x16x16_bf16, and two adjacent float4 chunks are its 8-element slot in
+// v_mfma_f32_16x16x32_bf16 (one instruction instead of eight f32 ones).
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16v4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x4_t pk4(float a, float b, float c, float d) {
+  const bf16v4_t v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+  return __builtin_bit_cast(bf16x4_t, v);
+}
+__device__ __forceinline__ bf16x8_t pk8(float4 a, float4 b) {
+  return bf16x8_t{(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
+                  (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+}
+__device__ __forceinline__ f32x4 mfma_k32(bf16x8_t a, bf16x8_t b, f32x4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+}
+
 __device__ __forceinline__ f32x4 mfma4(float4 a, float4 b, f32x4 acc) {
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
@@ -148,7 +168,7 @@ struct Split {
 };
 
 // Y[80 x N] = relu(X[80 x K] . W^T + b)   (W row-major [N][ldw], first K columns)
-template <int K, int N, int PX, int PY, int RT = kRT>
+template <int K, int N, int PX, int PY, int RT = kRT, bool BF = false>
 __device__ __forceinline__ void lin_fwd(const float* __restrict__ X, float* __restrict__ Y,
                                         const float* __restrict__ W, int64_t ldw,
                                         const float* __restrict__ bias) {
@@ -162,13 +182,26 @@ __device__ __forceinline__ void lin_fwd(const float* __restrict__ X, float* __re
     f32x4 acc[Sp::RPW];
 #pragma unroll
     for (int r = 0; r < Sp::RPW; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (BF) {
 #pragma unroll
-    for (int c = 0; c < KQ / 4; ++c) {
-      const float4 b = ld4(wp + 4 * c);
+      for (int c = 0; c < KQ / 8; ++c) {
+        const bf16x8_t b = pk8(ld4(wp + 8 * c), ld4(wp + 8 * c + 4));
 #pragma unroll
-      for (int r = 0; r < Sp::RPW; ++r) {
-        const int rt = Sp::rt(w, r);
-        if (rt < RT) acc[r] = mfma4(lds4(X + (16 * rt + i) * PX + g * KQ + 4 * c), b, acc[r]);
+        for (int r = 0; r < Sp::RPW; ++r) {
+          const int rt = Sp::rt(w, r);
+          const float* xa = X + (16 * rt + i) * PX + g * KQ + 8 * c;
+          if (rt < RT) acc[r] = mfma_k32(pk8(lds4(xa), lds4(xa + 4)), b, acc[r]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < KQ / 4; ++c) {
+        const float4 b = ld4(wp + 4 * c);
+#pragma unroll
+        for (int r = 0; r < Sp::RPW; ++r) {
+          const int rt = Sp::rt(w, r);
+          if (rt < RT) acc[r] = mfma4(lds4(X + (16 * rt + i) * PX + g * KQ + 4 * c), b, acc[r]);
+        }
       }
     }
     const float bb = bias[16 * cs + i];
@@ -185,7 +218,7 @@ __device__ __forceinline__ void lin_fwd(const float* __restrict__ X, float* __re
 }
 
 // G[80 x NO] = DL[80 x KC] . W   (W row-major [KC][ldw], first NO columns)
-template <int KC, int NO, int PD, int PG>
+template <int KC, int NO, int PD, int PG, bool BF = false>
 __device__ __forceinline__ void lin_bwd(const float* __restrict__ DL, float* __restrict__ G,
                                         const float* __restrict__ W, int64_t ldw) {
   using Sp = Split<NO>;
@@ -208,14 +241,30 @@ __device__ __forceinline__ void lin_bwd(const float* __restrict__ DL, float* __r
     float4 ring[D];
 #pragma unroll
     for (int c = 0; c < D; ++c) ring[c] = chunk(c);
+    if constexpr (BF) {
+      static_assert(D % 2 == 0 && NC % 2 == 0, "bf16 pairs ring chunks");
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const float4 b = ring[c % D];
-      if (c + D < NC) ring[c % D] = chunk(c + D);
+      for (int c = 0; c < NC; c += 2) {
+        const bf16x8_t b = pk8(ring[c % D], ring[(c + 1) % D]);
+        if (c + D < NC) ring[c % D] = chunk(c + D);
+        if (c + 1 + D < NC) ring[(c + 1) % D] = chunk(c + 1 + D);
 #pragma unroll
-      for (int r = 0; r < Sp::RPW; ++r) {
-        const int rt = Sp::rt(w, r);
-        if (rt < kRT) acc[r] = mfma4(lds4(DL + (16 * rt + i) * PD + g * KQ + 4 * c), b, acc[r]);
+        for (int r = 0; r < Sp::RPW; ++r) {
+          const int rt = Sp::rt(w, r);
+          const float* da = DL + (16 * rt + i) * PD + g * KQ + 4 * c;
+          if (rt < kRT) acc[r] = mfma_k32(pk8(lds4(da), lds4(da + 4)), b, acc[r]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const float4 b = ring[c % D];
+        if (c + D < NC) ring[c % D] = chunk(c + D);
+#pragma unroll
+        for (int r = 0; r < Sp::RPW; ++r) {
+          const int rt = Sp::rt(w, r);
+          if (rt < kRT) acc[r] = mfma4(lds4(DL + (16 * rt + i) * PD + g * KQ + 4 * c), b, acc[r]);
+        }
       }
     }
 #pragma unroll
@@ -427,7 +476,7 @@ __device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict_
 
 // The forward in workgroups of VR valid rows staged as RT 16-row MFMA tiles (the padding rows
 // are zeros and are never stored).  VR < 16 RT lets two workgroups share a CU (A/B knob).
-template <int RT, int VR>
+template <int RT, int VR, bool BF = false>
 __global__ __launch_bounds__(kThreads) void k_mlp_fwd(
     const float* __restrict__ xin, int64_t n, TowerArgs a, float eps, float p,
     const ncf_step_clock* clock, const float* __restrict__ w_out, const float* __restrict__ b_out,
@@ -448,21 +497,21 @@ __global__ __launch_bounds__(kThreads) void k_mlp_fwd(
   }
   __syncthreads();
   NCF_STAMP(0, 1);
-  lin_fwd<K0, N0, kPP, kPQ, RT>(P, Q, a.l[0].w, a.l[0].ldw, a.l[0].b);
+  lin_fwd<K0, N0, kPP, kPQ, RT, BF>(P, Q, a.l[0].w, a.l[0].ldw, a.l[0].b);
   __syncthreads();
   NCF_STAMP(0, 2);
   ln_fwd<N0, kPQ, RT>(Q, row0, rows, a.l[0], eps, p, a.seed[0] + cs, nullptr, nullptr, nullptr,
                       nullptr, nullptr, nullptr, nullptr);
   __syncthreads();
   NCF_STAMP(0, 3);
-  lin_fwd<N0, N1, kPQ, kPP, RT>(Q, P, a.l[1].w, a.l[1].ldw, a.l[1].b);
+  lin_fwd<N0, N1, kPQ, kPP, RT, BF>(Q, P, a.l[1].w, a.l[1].ldw, a.l[1].b);
   __syncthreads();
   NCF_STAMP(0, 4);
   ln_fwd<N1, kPP, RT>(P, row0, rows, a.l[1], eps, p, a.seed[1] + cs, nullptr, nullptr, nullptr,
                       nullptr, nullptr, nullptr, nullptr);
   __syncthreads();
   NCF_STAMP(0, 5);
-  lin_fwd<N1, N2, kPP, kPQ, RT>(P, Q, a.l[2].w, a.l[2].ldw, a.l[2].b);
+  lin_fwd<N1, N2, kPP, kPQ, RT, BF>(P, Q, a.l[2].w, a.l[2].ldw, a.l[2].b);
   __syncthreads();
   NCF_STAMP(0, 6);
   ln_fwd<N2, kPQ, RT>(Q, row0, rows, a.l[2], eps, p, a.seed[2] + cs, w_out, b_out, mf_pred, w_fin,
@@ -486,7 +535,7 @@ static_assert(kFwdVR <= 16 * kFwdRT, "forward rows per workgroup exceed its tile
 // (the partial of this workgroup; one deferred reduction sums the 256 partial rows).  16x16
 // output tiles, contraction over the rows k-permuted: lane group g covers rows [20g, 20g + 20).
 // A wave keeps its dlin column fragment (20 values) and sweeps its k tiles with it.
-template <int N, int K, int PG, int PX>
+template <int N, int K, int PG, int PX, bool BF = false>
 __device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const float* __restrict__ X,
                                             float* __restrict__ out) {
   constexpr int TN = N / 16, TK = K / 16, R4 = kRows / 4;
@@ -506,10 +555,21 @@ __device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const f
       const int tk = tk0 + jk;
       const float* xb = X + (g * R4) * PX + 16 * tk + i;
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (BF) {     // 4 consecutive rows of the contraction per 16x16x16 bf16 MFMA
+        static_assert(R4 % 4 == 0, "rows per lane group");
 #pragma unroll
-      for (int s = 0; s < R4; s += 2) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], xb[s * PX], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s + 1], xb[(s + 1) * PX], acc1, 0, 0, 0);
+        for (int s = 0; s < R4; s += 4) {
+          const bf16x4_t a4 = pk4(af[s], af[s + 1], af[s + 2], af[s + 3]);
+          const bf16x4_t b4 = pk4(xb[s * PX], xb[(s + 1) * PX], xb[(s + 2) * PX], xb[(s + 3) * PX]);
+          if ((s / 4) & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, acc1, 0, 0, 0);
+          else acc0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, acc0, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < R4; s += 2) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], xb[s * PX], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s + 1], xb[(s + 1) * PX], acc1, 0, 0, 0);
+        }
       }
       float* o = out + (16 * tn + 4 * g) * K + 16 * tk + i;
 #pragma unroll
@@ -622,6 +682,7 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
   __syncthreads();
 }
 
+template <bool BF = false>
 __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ g_last, int64_t n,
                                                       TowerArgs a, float p,
                                                       const ncf_step_clock* clock,
@@ -654,11 +715,11 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_act<N1, kPP>(P, a.l[1], row0, rows, p, a.seed[1] + cs);
     __syncthreads();
     NCF_STAMP(1, 3);
-    wgrad_layer<N2, N1, kPQ, kPP>(Q, P, pp + kW2);
+    wgrad_layer<N2, N1, kPQ, kPP, BF>(Q, P, pp + kW2);
     __syncthreads();
     NCF_STAMP(1, 4);
   }
-  lin_bwd<N2, N1, kPQ, kPP>(Q, P, a.l[2].w, a.l[2].ldw);
+  lin_bwd<N2, N1, kPQ, kPP, BF>(Q, P, a.l[2].w, a.l[2].ldw);
   __syncthreads();
   NCF_STAMP(1, 5);
   ln_bwd<N1, kPP>(P, Q, row0, rows, a.l[1], p, a.seed[1] + cs, pp + 3 * N2);
@@ -667,11 +728,11 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_act<N0, kPQ>(Q, a.l[0], row0, rows, p, a.seed[0] + cs);
     __syncthreads();
     NCF_STAMP(1, 7);
-    wgrad_layer<N1, N0, kPP, kPQ>(P, Q, pp + kW1);
+    wgrad_layer<N1, N0, kPP, kPQ, BF>(P, Q, pp + kW1);
     __syncthreads();
     NCF_STAMP(1, 8);
   }
-  lin_bwd<N1, N0, kPP, kPQ>(P, Q, a.l[1].w, a.l[1].ldw);
+  lin_bwd<N1, N0, kPP, kPQ, BF>(P, Q, a.l[1].w, a.l[1].ldw);
   __syncthreads();
   NCF_STAMP(1, 9);
   ln_bwd<N0, kPQ>(Q, P, row0, rows, a.l[0], p, a.seed[0] + cs, pp + 3 * (N2 + N1));
@@ -680,11 +741,11 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_rows<K0, kPP>(P, xin, row0, rows);
     __syncthreads();
     NCF_STAMP(1, 11);
-    wgrad_layer<N0, K0, kPQ, kPP>(Q, P, pp + kW0);
+    wgrad_layer<N0, K0, kPQ, kPP, BF>(Q, P, pp + kW0);
     __syncthreads();
     NCF_STAMP(1, 12);
   }
-  lin_bwd<N0, K0, kPQ, kPP>(Q, P, a.l[0].w, a.l[0].ldw);
+  lin_bwd<N0, K0, kPQ, kPP, BF>(Q, P, a.l[0].w, a.l[0].ldw);
   __syncthreads();
   NCF_STAMP(1, 13);
   for (int e = threadIdx.x; e < rows * (K0 / 4); e += kThreads) {
@@ -734,11 +795,12 @@ extern "C" int ncf_mlp_fused_supported(int64_t dim, int64_t n_layers, const int6
   return tower_ok(dim, n_layers, hidden) ? 1 : 0;
 }
 
-extern "C" int ncf_mlp_fwd(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
-                           int64_t n_layers, const int64_t* hidden, float eps, float dropout_p,
-                           uint64_t seed, const ncf_step_clock* clock, const float* mlp_out_w,
-                           const float* mlp_out_b, const float* mf_pred, const float* final_w,
-                           const float* final_b, float* mlp_pred, float* prob, void* stream) {
+template <bool BF>
+static int mlp_fwd_impl(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
+                        int64_t n_layers, const int64_t* hidden, float eps, float dropout_p,
+                        uint64_t seed, const ncf_step_clock* clock, const float* mlp_out_w,
+                        const float* mlp_out_b, const float* mf_pred, const float* final_w,
+                        const float* final_b, float* mlp_pred, float* prob, void* stream) {
   NCF_CHECK_ARG(n >= 0 && tower_ok(dim, n_layers, hidden),
                 "ncf_mlp_fwd: unsupported tower (need input 64, hidden [256,128,64])");
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_mlp_fwd: dropout_p out of [0,1)");
@@ -748,11 +810,11 @@ extern "C" int ncf_mlp_fwd(const float* x, int64_t n, int64_t dim, const ncf_mlp
   if (rc) return rc;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_mlp_fwd<kFwdRT, kFwdVR>,
+    (void)hipFuncSetAttribute((const void*)k_mlp_fwd<kFwdRT, kFwdVR, BF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsFwd);
     attr = true;
   }
-  hipLaunchKernelGGL((k_mlp_fwd<kFwdRT, kFwdVR>), dim3((unsigned)ncf_cdiv(n, kFwdVR)),
+  hipLaunchKernelGGL((k_mlp_fwd<kFwdRT, kFwdVR, BF>), dim3((unsigned)ncf_cdiv(n, kFwdVR)),
                      dim3(kThreads), kLdsFwd,
                      (hipStream_t)stream, x, n, a, eps, dropout_p, clock, mlp_out_w, mlp_out_b,
                      mf_pred, final_w, final_b, mlp_pred, prob);
@@ -765,11 +827,12 @@ extern "C" int64_t ncf_mlp_bwd_workspace(int64_t n) {
   return nb * kPartW + 2 * ncf_reduce_scratch((int)nb, kPartW);
 }
 
-extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, const float* x,
-                           const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
-                           float dropout_p, uint64_t seed, const ncf_step_clock* clock,
-                           const ncf_head_args* head, float* grad_x, float* workspace,
-                           int64_t workspace_floats, ncf_reduce_list* defer, void* stream) {
+template <bool BF>
+static int mlp_bwd_impl(const float* grad_a_last, int64_t n, int64_t dim, const float* x,
+                        const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
+                        float dropout_p, uint64_t seed, const ncf_step_clock* clock,
+                        const ncf_head_args* head, float* grad_x, float* workspace,
+                        int64_t workspace_floats, ncf_reduce_list* defer, void* stream) {
   NCF_CHECK_ARG(n >= 0 && tower_ok(dim, n_layers, hidden),
                 "ncf_mlp_bwd: unsupported tower (need input 64, hidden [256,128,64])");
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_mlp_bwd: dropout_p out of [0,1)");
@@ -809,13 +872,13 @@ extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, con
   }
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_mlp_bwd, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kLds);
+    (void)hipFuncSetAttribute((const void*)k_mlp_bwd<BF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
     attr = true;
   }
   const int nb = (int)ncf_cdiv(n, kRows);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_mlp_bwd, dim3((unsigned)nb), dim3(kThreads), kLds, st, grad_a_last, n, a,
+  hipLaunchKernelGGL((k_mlp_bwd<BF>), dim3((unsigned)nb), dim3(kThreads), kLds, st, grad_a_last, n, a,
                      dropout_p, clock, grad_x, workspace, h, head ? 1 : 0, inv_n, x, fw ? 1 : 0);
   NCF_CHECK_LAUNCH("ncf_mlp_bwd");
   // per layer: [dbias | dgamma | dbeta] partial columns -> one strided reduction when the three
@@ -869,4 +932,44 @@ extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, con
     return ncf_reduce_batch(lst, scr, workspace_floats - (int64_t)nb * kPartW, stream);
   }
   return NCF_OK;
+}
+
+extern "C" int ncf_mlp_fwd(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
+                           int64_t n_layers, const int64_t* hidden, float eps, float dropout_p,
+                           uint64_t seed, const ncf_step_clock* clock, const float* mlp_out_w,
+                           const float* mlp_out_b, const float* mf_pred, const float* final_w,
+                           const float* final_b, float* mlp_pred, float* prob, void* stream) {
+  return mlp_fwd_impl<false>(x, n, dim, layers, n_layers, hidden, eps, dropout_p, seed, clock,
+                             mlp_out_w, mlp_out_b, mf_pred, final_w, final_b, mlp_pred, prob,
+                             stream);
+}
+
+extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, const float* x,
+                           const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
+                           float dropout_p, uint64_t seed, const ncf_step_clock* clock,
+                           const ncf_head_args* head, float* grad_x, float* workspace,
+                           int64_t workspace_floats, ncf_reduce_list* defer, void* stream) {
+  return mlp_bwd_impl<false>(grad_a_last, n, dim, x, layers, n_layers, hidden, dropout_p, seed,
+                             clock, head, grad_x, workspace, workspace_floats, defer, stream);
+}
+
+// bf16 configuration: the same tower with its three Linears (forward dX, backward dX and dW) on
+// bf16 MFMA (operands rounded to bf16, fp32 accumulate); every row op stays fp32.
+extern "C" int ncf_mlp_fwd_bf16(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
+                                int64_t n_layers, const int64_t* hidden, float eps, float dropout_p,
+                                uint64_t seed, const ncf_step_clock* clock, const float* mlp_out_w,
+                                const float* mlp_out_b, const float* mf_pred, const float* final_w,
+                                const float* final_b, float* mlp_pred, float* prob, void* stream) {
+  return mlp_fwd_impl<true>(x, n, dim, layers, n_layers, hidden, eps, dropout_p, seed, clock,
+                            mlp_out_w, mlp_out_b, mf_pred, final_w, final_b, mlp_pred, prob,
+                            stream);
+}
+
+extern "C" int ncf_mlp_bwd_bf16(const float* grad_a_last, int64_t n, int64_t dim, const float* x,
+                                const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
+                                float dropout_p, uint64_t seed, const ncf_step_clock* clock,
+                                const ncf_head_args* head, float* grad_x, float* workspace,
+                                int64_t workspace_floats, ncf_reduce_list* defer, void* stream) {
+  return mlp_bwd_impl<true>(grad_a_last, n, dim, x, layers, n_layers, hidden, dropout_p, seed,
+                            clock, head, grad_x, workspace, workspace_floats, defer, stream);
 }

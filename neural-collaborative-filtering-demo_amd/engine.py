@@ -23,6 +23,8 @@ from . import _lib
 from ._lib import ptr
 
 LN_EPS = 1e-5
+# bf16 configuration: the fused MLP tower's Linears on bf16 MFMA (NCF_BF16_MM=0: fp32 MFMA, A/B)
+BF16_MM = os.environ.get("NCF_BF16_MM", "1") != "0"
 
 
 def _tptr(t) -> int:
@@ -429,8 +431,10 @@ class NCFEngine:
         if temporal is None and self.mlp_fused(D, hid):
             # a7 + a8: the whole tower and the head in one launch (mlp_tower.hip)
             _, addr, _, haddr = self._mlp_layers(w, train, bwd=False)
-            _lib.call("ncf_mlp_fwd", ptr(x), n, D, addr, len(hid), haddr, LN_EPS,
-                      drop_p if train else 0.0, seed, ptr(self.clock), pp["mlp_output.weight"],
+            _lib.call("ncf_mlp_fwd_bf16" if bf16 and BF16_MM else "ncf_mlp_fwd", ptr(x), n, D, addr,
+                      len(hid),
+                      haddr, LN_EPS, drop_p if train else 0.0, seed, ptr(self.clock),
+                      pp["mlp_output.weight"],
                       pp["mlp_output.bias"], ptr(w.mf_pred), pp["final.0.weight"],
                       pp["final.0.bias"], ptr(w.mlp_pred), ptr(w.prob), st)
             return w
@@ -636,7 +640,9 @@ class NCFEngine:
                 h.grad_final_w, h.grad_final_b = ptr(gv("final.0.weight")), ptr(gv("final.0.bias"))
             h.prob, h.grad_prob, h.targets, h.loss = ptr(w.prob), ptr(gp), ptr(tg), ptr(w.loss)
             h.loss_denominator = float(loss_denominator)
-            _lib.call("ncf_mlp_bwd", None, n, D, ptr(w.y), addr, len(hid), haddr, drop_p, seed,
+            _lib.call("ncf_mlp_bwd_bf16" if bf16 and BF16_MM else "ncf_mlp_bwd", None, n, D,
+                      ptr(w.y), addr,
+                      len(hid), haddr, drop_p, seed,
                       ptr(self.clock), ctypes.addressof(h), ptr(w.dy), ptr(w.site("mlp")),
                       w.site("mlp").numel(), w.red_list.address, st)
         fused_all = fused and self.mlp_fused_wgrad()
