@@ -330,24 +330,32 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
         return dt
 
     out = {"config": f"{n_query} users x {n_items} items (model {n_users} x {n_items}, D=64), "
-                     "top-K over the whole catalogue, factorised fp32 MFMA scan"
+                     "top-K over the whole catalogue, factorised fp32 MFMA scan, hipGraph-captured"
                      + (f", item-sharded over {world} GPUs (all-gather + merge)" if world > 1 else ""),
            "scaling": "strong", "n_gpus": world, "item_index_ms": round(index_ms, 3)}
     for k in ks:
+        # the served form: the per-shard pipeline captured once as a hipGraph and replayed
+        # (GraphedScorer); the eager launches are timed beside it with per-launch HIP events
+        # for the scan kernel's roofline
+        sharded_score_topk(m, users, k, idx, graph=True)
+        torch.cuda.synchronize()
+        best = min(timed(lambda: sharded_score_topk(m, users, k, idx, graph=True))
+                   for _ in range(3))
         sharded_score_topk(m, users, k, idx)
         torch.cuda.synchronize()
-        best, prof = 1e9, None
+        eager, prof = 1e9, None
         for _ in range(3):
             L.PROFILE = []
             dt = timed(lambda: sharded_score_topk(m, users, k, idx))
-            if dt < best:
-                best, prof = dt, L.PROFILE
+            if dt < eager:
+                eager, prof = dt, L.PROFILE
             L.PROFILE = None
         coll = sum(e0.elapsed_time(e1) for name, _, e0, e1 in prof if name == "ncf_score_collect")
         flops = 2.0 * 64 * n_query * n_local
         tf = flops / (coll * 1e-3) / 1e12
         out[f"k{k}"] = {"ms": round(best * 1e3, 3), "pairs_per_s": round(n_query * n_items / best, 1),
-                        "collect_ms": round(coll, 3),
+                        "launch": "hipGraph replay (GraphedScorer)",
+                        "eager_ms": round(eager * 1e3, 3), "collect_ms": round(coll, 3),
                         "roofline": {"bound": "mfma", "kernel": "k_collect (v_mfma_f32_32x32x2_f32)",
                                      "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFS,
                                      "unit": "TFLOP/s", "frac": round(tf / FP32_MFMA_PEAK_TFS, 4),

@@ -45,6 +45,37 @@ def alias_table(weights: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
     return prob, alias
 
 
+class ConsistentBatchSampler:
+    """The reference's training batch sampler (src/model/data_prep.py:397-443), same
+    constructor and iteration: ``num_batches = ceil(size / batch_size)`` index lists over
+    ``range(dataset_size)`` (shuffled in place by ``np.random.shuffle`` when ``shuffle``); a short
+    last batch is extended with ``batch[:batch_size - len(batch)]``, i.e. with repeats of its own
+    first indices, so it stays short when it holds fewer than half a batch (data_prep.py:436-438).
+    For ``torch.utils.data.DataLoader(batch_sampler=...)`` on the host; on the device
+    ``DeviceNegativeSampler.epoch`` applies the same padding rule."""
+
+    def __init__(self, dataset_size: int, batch_size: int, shuffle: bool = True):
+        self.dataset_size = dataset_size
+        self.batch_size = batch_size
+        self.shuffle = shuffle
+        self.num_batches = (dataset_size + batch_size - 1) // batch_size
+        self.last_batch_size = dataset_size % batch_size or batch_size
+
+    def __iter__(self):
+        indices = list(range(self.dataset_size))
+        if self.shuffle:
+            np.random.shuffle(indices)
+        for b in range(self.num_batches):
+            batch = indices[b * self.batch_size:(b + 1) * self.batch_size]
+            short = self.batch_size - len(batch)
+            if short > 0:
+                batch.extend(batch[:short])
+            yield batch
+
+    def __len__(self) -> int:
+        return self.num_batches
+
+
 class DeviceNegativeSampler:
     """Interaction list + negative sampler + collate, resident on the GPU."""
 
@@ -107,10 +138,18 @@ class DeviceNegativeSampler:
         return kjt, tgt.unsqueeze(1)
 
     def epoch(self, batch_size: int, seed: int = 0, shuffle: bool = True,
-              drop_last: bool = False) -> Iterator[Tuple[KeyedJaggedTensor, torch.Tensor]]:
+              drop_last: bool = False, pad_last: Optional[bool] = None
+              ) -> Iterator[Tuple[KeyedJaggedTensor, torch.Tensor]]:
         """One pass over the interactions in batches (the DataLoader + collate loop of
-        trainer.py:134-140, 253-258), order and negatives a function of ``seed``."""
+        trainer.py:134-140, 253-258), order and negatives a function of ``seed``.
+
+        ``pad_last`` (default: train mode) is the reference's training loader, whose
+        ``ConsistentBatchSampler`` (data_prep.py:397-443, used at trainer.py:127-140) pads a short
+        last batch with the first indices of that same batch (at most doubling it); without it
+        the last batch is short (the validation loader, trainer.py:142-148)."""
         n = len(self)
+        if pad_last is None:
+            pad_last = self.mode == "train"
         if shuffle:
             g = torch.Generator(device=self.device).manual_seed(seed)
             order = torch.randperm(n, generator=g, device=self.device)
@@ -120,6 +159,8 @@ class DeviceNegativeSampler:
             chunk = order[s:s + batch_size]
             if drop_last and chunk.numel() < batch_size:
                 break
+            if pad_last and chunk.numel() < batch_size:
+                chunk = torch.cat([chunk, chunk[:batch_size - chunk.numel()]])
             yield self.batch(chunk, (seed * 1_000_003 + b) & (2 ** 63 - 1))
 
     def check(self):

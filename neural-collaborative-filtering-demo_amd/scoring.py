@@ -12,7 +12,8 @@ at once through the factorised eval form (csrc/score.hip):
 
 ``ItemIndex`` caches the item side (p, bias) for a parameter version (optionally for a subset
 of the catalogue: one rank's item shard); ``score_topk`` runs the threshold / MFMA-collect /
-select pipeline; ``sharded_score_topk`` is the item-sharded multi-GPU form: every
+select pipeline (``GraphedScorer``: the same pipeline captured once as a hipGraph and replayed);
+``sharded_score_topk`` is the item-sharded multi-GPU form: every
 rank scores all queried users against its own item shard, the per-shard top-K lists are
 all-gathered (RCCL) and merged per user by ``ncf_score_merge``.  ``forward_simple(hour=None)`` semantics only (the
 hour variant draws a fresh random projection on every call, architecture.py:437-442, so it has no
@@ -90,6 +91,85 @@ def _sample_size(n_items: int, k: int, cap: int) -> int:
     return min(n_items, s)
 
 
+class _TopKRun:
+    """Buffers and launch sequence of one top-k pipeline for ``n`` users (shared by the eager
+    ``score_topk`` and the captured ``GraphedScorer``)."""
+
+    def __init__(self, index: "ItemIndex", n: int, k: int, cap: int):
+        p = index.p
+        dev = p.device
+        I, D = p.shape
+        if not 1 <= k <= min(I, cap):
+            raise ValueError(f"k must be in [1, {min(I, cap)}]")
+        self.index, self.n, self.k, self.cap = index, n, k, cap
+        self.S = _sample_size(I, k, cap)
+        self.stride = I // self.S
+        e = lambda *sh, dt=torch.float32: torch.empty(*sh, dtype=dt, device=dev)  # noqa: E731
+        self.uid = e(max(n, 1), dt=torch.int64)
+        self.q, self.sample, self.thr = e(max(n, 1), D), e(max(n, 1), self.S), e(max(n, 1))
+        self.count = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+        self.cand_l, self.cand_i = e(max(n, 1), cap), e(max(n, 1), cap, dt=torch.int32)
+        self.overflow = e(max(n, 1), dt=torch.int32)
+        self.scores, self.items = e(n, k), e(n, k, dt=torch.int64)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def launch(self, model, st):
+        """queries -> threshold sample (MFMA GEMM over strided item rows) -> k-th threshold ->
+        MFMA collect -> select, on stream ``st``; reads self.uid[:n]."""
+        idx, n, k, cap = self.index, self.n, self.k, self.cap
+        p, bias = idx.p, idx.bias
+        I, D = p.shape
+        table = model.mf_embedding_collection.embedding_bags["user_id"].weight
+        _lib.call("ncf_score_queries", ptr(self.uid), n, ptr(table), model.num_users, D,
+                  ptr(model.mf_norm.weight), ptr(model.mf_norm.bias), LN_EPS,
+                  ptr(model.mf_output.weight), ptr(model.final[0].weight), ptr(self.q),
+                  ptr(self.err), st)
+        _lib.call("ncf_gemm_f32", n, self.S, D, ptr(self.q), D, 0, ptr(p), D * self.stride, 1,
+                  ptr(self.sample), self.S, None, 0, st)
+        _lib.call("ncf_score_kth", ptr(self.sample), n, self.S, k, ptr(bias), self.stride,
+                  ptr(self.thr), st)
+        self.count.zero_()
+        _lib.call("ncf_score_collect", ptr(self.q), None, n, ptr(p), ptr(bias), I, D, ptr(self.thr),
+                  cap, ptr(self.count), ptr(self.cand_l), ptr(self.cand_i), st)
+        _lib.call("ncf_score_select", None, n, ptr(self.count), ptr(self.cand_l), ptr(self.cand_i),
+                  cap, k, ptr(self.scores), ptr(self.items), ptr(self.thr), ptr(self.overflow), st)
+
+    def redo_overflow(self, st):
+        """Re-run the users whose candidate list overflowed (eager; rare: the threshold sample
+        targets cap / 2 candidates)."""
+        idx, k, cap = self.index, self.k, self.cap
+        p, bias = idx.p, idx.bias
+        I, D = p.shape
+        dev = p.device
+        overflow = self.overflow[:self.n]
+        for _ in range(32):
+            redo = torch.nonzero(overflow).flatten()
+            if redo.numel() == 0:
+                return
+            rows = redo.to(torch.int32)
+            self.count[redo] = 0
+            sub_s = torch.empty(rows.numel(), k, device=dev)
+            sub_i = torch.empty(rows.numel(), k, dtype=torch.int64, device=dev)
+            sub_o = torch.empty(rows.numel(), dtype=torch.int32, device=dev)
+            _lib.call("ncf_score_collect", ptr(self.q), ptr(rows), rows.numel(), ptr(p), ptr(bias),
+                      I, D, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),
+                      ptr(self.cand_i), st)
+            _lib.call("ncf_score_select", ptr(rows), rows.numel(), ptr(self.count),
+                      ptr(self.cand_l), ptr(self.cand_i), cap, k, ptr(sub_s), ptr(sub_i),
+                      ptr(self.thr), ptr(sub_o), st)
+            self.scores[redo] = sub_s
+            self.items[redo] = sub_i
+            overflow.zero_()
+            overflow[redo] = sub_o
+        raise RuntimeError("score_topk: candidate lists kept overflowing (degenerate scores?)")
+
+    def result(self):
+        items = self.items
+        if self.index.ids is not None:   # shard-local positions -> global item ids
+            items = self.index.ids[items.clamp_min(0)]
+        return self.scores, items
+
+
 def score_topk(model, user_ids: torch.Tensor, k: int = 10, index: Optional[ItemIndex] = None,
                cap: int = 8192) -> Tuple[torch.Tensor, torch.Tensor]:
     """Top-k (probability, item id) per user over all items, as
@@ -99,67 +179,75 @@ def score_topk(model, user_ids: torch.Tensor, k: int = 10, index: Optional[ItemI
         index = ItemIndex(model)
     elif not index.valid_for(model):   # parameters changed since the index was built
         index = ItemIndex(model, items=index.ids)
-    p, bias = index.p, index.bias
-    dev = p.device
-    I, D = p.shape
-    if not 1 <= k <= min(I, cap):
-        raise ValueError(f"k must be in [1, {min(I, cap)}]")
-    st = _lib.stream_ptr(dev)
+    dev = index.p.device
     uid = user_ids.to(device=dev, dtype=torch.int64).contiguous()
     n = uid.numel()
-    scores = torch.empty(n, k, device=dev)
-    items = torch.empty(n, k, dtype=torch.int64, device=dev)
+    run = _TopKRun(index, n, k, cap)
     if n == 0:
-        return scores, items
-    # 1. queries
-    q = torch.empty(n, D, device=dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
-    table = model.mf_embedding_collection.embedding_bags["user_id"].weight
-    _lib.call("ncf_score_queries", ptr(uid), n, ptr(table), model.num_users, D,
-              ptr(model.mf_norm.weight), ptr(model.mf_norm.bias), LN_EPS,
-              ptr(model.mf_output.weight), ptr(model.final[0].weight), ptr(q), ptr(err), st)
-    # 2. thresholds from a strided sample of items (logits via the MFMA GEMM, strided B rows)
-    S = _sample_size(I, k, cap)
-    stride = I // S
-    sample = torch.empty(n, S, device=dev)
-    _lib.call("ncf_gemm_f32", n, S, D, ptr(q), D, 0, ptr(p), D * stride, 1, ptr(sample), S, None,
-              0, st)
-    thr = torch.empty(n, device=dev)
-    _lib.call("ncf_score_kth", ptr(sample), n, S, k, ptr(bias), stride, ptr(thr), st)
-    del sample
-    # 3./4. collect + select; re-run the users whose candidate list overflowed
-    count = torch.zeros(n, dtype=torch.int32, device=dev)
-    cand_l = torch.empty(n, cap, device=dev)
-    cand_i = torch.empty(n, cap, dtype=torch.int32, device=dev)
-    overflow = torch.empty(n, dtype=torch.int32, device=dev)
-    _lib.call("ncf_score_collect", ptr(q), None, n, ptr(p), ptr(bias), I, D, ptr(thr), cap,
-              ptr(count), ptr(cand_l), ptr(cand_i), st)
-    _lib.call("ncf_score_select", None, n, ptr(count), ptr(cand_l), ptr(cand_i), cap, k,
-              ptr(scores), ptr(items), ptr(thr), ptr(overflow), st)
-    for _ in range(32):
-        redo = torch.nonzero(overflow).flatten()
-        if redo.numel() == 0:
-            break
-        rows = redo.to(torch.int32)
-        count[redo] = 0
-        sub_s = torch.empty(rows.numel(), k, device=dev)
-        sub_i = torch.empty(rows.numel(), k, dtype=torch.int64, device=dev)
-        sub_o = torch.empty(rows.numel(), dtype=torch.int32, device=dev)
-        _lib.call("ncf_score_collect", ptr(q), ptr(rows), rows.numel(), ptr(p), ptr(bias), I, D,
-                  ptr(thr), cap, ptr(count), ptr(cand_l), ptr(cand_i), st)
-        _lib.call("ncf_score_select", ptr(rows), rows.numel(), ptr(count), ptr(cand_l),
-                  ptr(cand_i), cap, k, ptr(sub_s), ptr(sub_i), ptr(thr), ptr(sub_o), st)
-        scores[redo] = sub_s
-        items[redo] = sub_i
-        overflow.zero_()
-        overflow[redo] = sub_o
-    else:
-        raise RuntimeError("score_topk: candidate lists kept overflowing (degenerate scores?)")
-    if int(err.item()):
+        return run.result()
+    st = _lib.stream_ptr(dev)
+    run.uid[:n].copy_(uid)
+    run.launch(model, st)
+    run.redo_overflow(st)
+    if int(run.err.item()):
         raise IndexError("score_topk: user id out of range of the embedding table")
-    if index.ids is not None:   # shard-local positions -> global item ids
-        items = index.ids[items.clamp_min(0)]
-    return scores, items
+    return run.result()
+
+
+class GraphedScorer:
+    """C5 as a captured hipGraph (BASELINE configs[4]): the whole top-k pipeline for a fixed
+    number of users (queries, threshold sample GEMM, k-th threshold, MFMA collect, select, and
+    the overflow / id-error flags) recorded once with ``torch.cuda.CUDAGraph`` and replayed per
+    call, so a call costs one graph launch and one 8-byte flag read instead of the per-launch
+    host work.  Users whose candidate list overflowed are re-run eagerly (same results as
+    ``score_topk``); a parameter change since capture rebuilds the index and re-captures.
+
+        scorer = GraphedScorer(model, n_users=10_000, k=10)
+        scores, items = scorer(user_ids)        # [n, k] each, like score_topk
+    """
+
+    def __init__(self, model, n_users: int, k: int = 10, index: Optional[ItemIndex] = None,
+                 cap: int = 8192):
+        self.model, self.n, self.k, self.cap = model, int(n_users), int(k), cap
+        if self.n < 1:
+            raise ValueError("GraphedScorer needs n_users >= 1")
+        self.index = index if index is not None and index.valid_for(model) else ItemIndex(
+            model, items=None if index is None else index.ids)
+        self._capture()
+
+    def _capture(self):
+        idx = self.index
+        dev = idx.p.device
+        self.run = run = _TopKRun(idx, self.n, self.k, self.cap)
+        run.uid.zero_()
+        st = _lib.stream_ptr(dev)
+        run.launch(self.model, st)           # warm-up: kernel attributes, lazy module loads
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            run.launch(self.model, _lib.stream_ptr(dev))
+            self.flags = torch.stack([run.overflow[:self.n].amax(), run.err[0]])
+            self.out = run.result()
+        self.version = idx.version
+
+    def __call__(self, user_ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        if not self.index.valid_for(self.model):
+            self.index = ItemIndex(self.model, items=self.index.ids)
+            self._capture()
+        run = self.run
+        uid = user_ids.reshape(-1)
+        if uid.numel() != self.n:
+            raise ValueError(f"GraphedScorer was captured for {self.n} users, got {uid.numel()}")
+        run.uid.copy_(uid)
+        run.err.zero_()
+        self.graph.replay()
+        over, err = self.flags.tolist()
+        if err:
+            raise IndexError("score_topk: user id out of range of the embedding table")
+        if over:
+            run.redo_overflow(_lib.stream_ptr(run.uid.device))
+            return run.result()
+        return self.out
 
 
 def shard_items(num_items: int, world: int, rank: int) -> torch.Tensor:
@@ -186,7 +274,7 @@ def merge_topk(cand_scores: torch.Tensor, cand_items: torch.Tensor, k: int):
 
 def sharded_score_topk(model, user_ids: torch.Tensor, k: int = 10,
                        index: Optional[ItemIndex] = None, group=None, cap: int = 8192,
-                       local_topk=None, merge=None):
+                       local_topk=None, merge=None, graph: bool = False):
     """Item-sharded C5 scoring over ``torch.distributed``: rank r scores every
     queried user against ``shard_items(I, W, r)``, the ``[n, k]`` local lists are all-gathered
     (8 B per entry + id widening) and merged per user.  Every rank returns the global top-k.
@@ -201,7 +289,14 @@ def sharded_score_topk(model, user_ids: torch.Tensor, k: int = 10,
         kk = min(k, index.p.shape[0])
 
         def local_topk(u, _k):
-            s, i = score_topk(model, u, kk, index, cap)
+            if graph:   # the shard's pipeline as a captured hipGraph (cached on the index)
+                gs = index.__dict__.setdefault("_graphed", {})
+                sc = gs.get((u.numel(), kk, cap))
+                if sc is None:
+                    sc = gs[(u.numel(), kk, cap)] = GraphedScorer(model, u.numel(), kk, index, cap)
+                s, i = sc(u)
+            else:
+                s, i = score_topk(model, u, kk, index, cap)
             if kk < _k:   # a shard smaller than k: pad with empty slots
                 s = torch.cat([s, s.new_zeros(s.shape[0], _k - kk)], 1)
                 i = torch.cat([i, i.new_full((i.shape[0], _k - kk), -1)], 1)

@@ -37,6 +37,9 @@ Fixtures written to tests/golden/*.npz (inputs and expected outputs only):
                            the train interaction list, product_weights, user histories, and the
                            empirical distribution of 40,000 _sample_negative draws (np seed 0)
                            for a few (user, positive) pairs
+  F9 f9_batches.npz        src/model/data_prep.py ConsistentBatchSampler: the index batches of
+                           several (dataset_size, batch_size) cases, unshuffled and shuffled
+                           under np.random.seed (last-batch padding with repeats of the batch)
 """
 import argparse
 import csv
@@ -365,6 +368,26 @@ def make_f8(ref):
     print("F8 written;", len(il), "train interactions; pairs", pairs)
 
 
+def make_f9(ref):
+    from src.model.data_prep import ConsistentBatchSampler
+    cases = [(10, 4, 0), (10, 8, 0), (8, 4, 0), (1, 4, 0), (37, 5, 0), (10, 3, 1), (23, 7, 1),
+             (6, 20, 1)]
+    flat, bounds, meta = [], [0], []
+    for size, bs, shuffle in cases:
+        if shuffle:
+            np.random.seed(size * 100 + bs)
+        sm = ConsistentBatchSampler(size, bs, shuffle=bool(shuffle))
+        batches = list(iter(sm))
+        assert len(batches) == len(sm)
+        for b in batches:
+            flat.extend(int(x) for x in b)
+            bounds.append(len(flat))
+        meta.append((size, bs, shuffle, len(batches)))
+    np.savez_compressed(os.path.join(HERE, "f9_batches.npz"), cases=np.array(meta, dtype=np.int64),
+                        indices=np.array(flat, dtype=np.int64), bounds=np.array(bounds, dtype=np.int64))
+    print("F9 written;", len(meta), "cases")
+
+
 def make_train_fixtures(AdvancedNCF, KJT):
     make_train("f2_train_c2.npz", AdvancedNCF, KJT, U=300, I=120, D=64, T=32,
                hidden=[256, 128, 64], H=4, B=8, M=5, steps=3, seed=0, lr=1e-3, wd=1e-5)
@@ -386,8 +409,8 @@ def main():
     if a.only == "train":
         make_train_fixtures(AdvancedNCF, KJT)
         return
-    if a.only in ("f7", "f8"):
-        (make_f7 if a.only == "f7" else make_f8)(a.reference)
+    if a.only in ("f7", "f8", "f9"):
+        {"f7": make_f7, "f8": make_f8, "f9": make_f9}[a.only](a.reference)
         return
     make_f1(a.reference, AdvancedNCF, KJT, sd)
     make_train_fixtures(AdvancedNCF, KJT)
@@ -396,6 +419,7 @@ def main():
     make_f6(AdvancedNCF, sd)
     make_f7(a.reference)
     make_f8(a.reference)
+    make_f9(a.reference)
 
 
 if __name__ == "__main__":

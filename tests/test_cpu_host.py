@@ -259,6 +259,26 @@ def test_row_shards_roundtrip(world):
         assert torch.equal(back[k], full[k])
 
 
+def test_consistent_batch_sampler_vs_reference():
+    """ncf_amd.data.ConsistentBatchSampler against the reference's own batches (F9,
+    src/model/data_prep.py:397-443): sizes, last-batch padding with repeats of that batch (still
+    short when it holds under half a batch), np.random.shuffle order under the same seed."""
+    from ncf_amd.data import ConsistentBatchSampler
+    d = np.load(os.path.join(ROOT, "tests", "golden", "f9_batches.npz"))
+    idx, bounds = d["indices"], d["bounds"]
+    b = 0
+    for size, bs, shuffle, nb in d["cases"].tolist():
+        if shuffle:
+            np.random.seed(size * 100 + bs)
+        sm = ConsistentBatchSampler(size, bs, shuffle=bool(shuffle))
+        got = list(iter(sm))
+        assert len(sm) == nb == len(got)
+        for g in got:
+            assert g == idx[bounds[b]:bounds[b + 1]].tolist(), (size, bs, shuffle)
+            b += 1
+    assert b == len(bounds) - 1
+
+
 def test_struct_mirrors_match_header_layouts():
     """ctypes mirrors of ncf_mlp_layer / ncf_table_pair: every field 8 bytes, header order."""
     import ctypes

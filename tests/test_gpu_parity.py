@@ -953,6 +953,37 @@ def test_item_sharded_scoring_equals_single(W, strided, k):
         assert bool((gs[diff] == ref_s[diff]).all())
 
 
+@pytest.mark.parametrize("k,cap,shard", [(10, 8192, False), (100, 128, False), (10, 8192, True)])
+def test_graphed_scorer_equals_eager(k, cap, shard):
+    """C5 as a captured hipGraph (GraphedScorer, BASELINE configs[4]) == the eager score_topk
+    bit for bit, over several replays with different users; cap=128 takes the eager overflow
+    re-run after the replay; an item shard maps to global ids inside the graph; a parameter
+    change rebuilds the index and re-captures."""
+    from ncf_amd.scoring import GraphedScorer, ItemIndex, score_topk, shard_items
+    torch.manual_seed(9)
+    U, I = 300, 20011
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    idx = ItemIndex(m, items=shard_items(I, 3, 1)) if shard else None
+    sc = GraphedScorer(m, 37, k=k, index=idx, cap=cap)
+    for rep in range(3):
+        users = torch.randint(0, U, (37,), device=DEV)
+        gs, gi = sc(users)
+        es, ei = score_topk(m, users, k=k, index=idx, cap=cap)
+        assert torch.equal(gs, es) and torch.equal(gi, ei), rep
+    with pytest.raises(ValueError):
+        sc(torch.zeros(5, dtype=torch.int64, device=DEV))
+    with torch.no_grad():
+        m.final[0].bias.add_(0.25)
+    users = torch.randint(0, U, (37,), device=DEV)
+    gs, gi = sc(users)
+    es, ei = score_topk(m, users, k=k, index=None if not shard else
+                        ItemIndex(m, items=shard_items(I, 3, 1)), cap=cap)
+    assert torch.equal(gs, es) and torch.equal(gi, ei)
+    with pytest.raises(IndexError):
+        sc(torch.full((37,), U, dtype=torch.int64, device=DEV))
+
+
 def test_merge_topk_empty_slots_and_ties():
     from ncf_amd.scoring import merge_topk
     s = torch.tensor([[0.5, 0.9, 0.5, 0.0, 0.7], [0.1, 0.0, 0.0, 0.0, 0.0]], device=DEV)
@@ -1073,7 +1104,7 @@ def test_negative_sampler_epoch_layout_and_determinism():
     prods = torch.randint(0, I, (P,), generator=g)
     s = DeviceNegativeSampler(users, prods, U, I, negative_samples=4, device=DEV)
     seen, b1 = [], []
-    for kjt, t in s.epoch(batch_size=128, seed=7):
+    for kjt, t in s.epoch(batch_size=128, seed=7, pad_last=False):
         n = kjt.values().numel() // 2
         assert n % 5 == 0 and t.shape == (n, 1)
         assert bool((kjt.lengths() == 1).all()) and kjt.keys() == ["user_id", "product_id"]
@@ -1088,7 +1119,12 @@ def test_negative_sampler_epoch_layout_and_determinism():
     ref = torch.stack([users, prods], 1)
     assert sorted(map(tuple, pairs.tolist())) == sorted(map(tuple, ref.tolist()))
     b2 = [kjt.values().view(2, -1, 5).cpu() for kjt, _ in s.epoch(batch_size=128, seed=7)]
-    assert all(torch.equal(a, b) for a, b in zip(b1, b2))
+    # train mode pads the short last batch (1000 = 7 x 128 + 104) with its own first 24 groups
+    # (ConsistentBatchSampler, data_prep.py:433-438); the groups before the padding are the same
+    assert len(b2) == len(b1) and b2[-1].shape[1] == 128 and b1[-1].shape[1] == 104
+    assert all(torch.equal(a, b) for a, b in zip(b1[:-1], b2[:-1]))
+    assert torch.equal(b2[-1][:, :104, 0], b1[-1][:, :, 0])
+    assert torch.equal(b2[-1][:, 104:, 0], b1[-1][:, :24, 0])
     b3 = [kjt.values().view(2, -1, 5).cpu() for kjt, _ in s.epoch(batch_size=128, seed=8)]
     assert not all(torch.equal(a, b) for a, b in zip(b1, b3))
     m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV).train()
