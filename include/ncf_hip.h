@@ -191,8 +191,9 @@ int ncf_attention_bwd(const float* q, const float* k, const float* v, const floa
                       void* stream);
 /* The whole a5 block in one launch per direction (D = 64, M <= 6; ncf_attn_block_supported):
  * forward  q,k,v = LN rows x W^T + b, the core above (same P layout and dropout stream), y =
- *          o Wo^T + bo.  q = k = NULL (with M == 1, no dropout): the eval form, o = v, only y
- *          (and v, o if given) written.  probs/o required when q is given.
+ *          o Wo^T + bo.  q = k = NULL: nothing is stashed (with M == 1 and no dropout this is
+ *          the eval form, o = v; otherwise the core runs in LDS only, for ncf_attn_block_bwd_rc);
+ *          probs/o required when q is given.
  * backward from dY: dO = dY Wo, the core backward, dXu = dQ Wq, dXi = dK Wk + dV Wv, and the
  *          four Linear gradients (below).                                                     */
 int ncf_attn_block_supported(int64_t dim, int64_t heads, int64_t group_len);
@@ -217,6 +218,18 @@ int ncf_attn_block_bwd(const float* grad_y, const float* q, const float* k, cons
                        int64_t workspace_floats, ncf_reduce_list* defer, float* grad_q,
                        float* grad_k, float* grad_v, float* grad_xu, float* grad_xi,
                        void* stream);
+/* The same backward (fused weight gradients) after a forward that stashed nothing: q, k, v are
+ * re-projected from xu / xi (+ the biases) and the core forward (probabilities, o) is re-run in
+ * LDS with the forward's own arithmetic (same bits), instead of reading q/k/v/o/probs from HBM.
+ * ncf_attn_block_rc_supported: the shapes whose recomputed probabilities fit in LDS beside dS. */
+int ncf_attn_block_rc_supported(int64_t dim, int64_t heads, int64_t group_len);
+int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const float* xi, int64_t groups,
+                          int64_t group_len, int64_t heads, int64_t dim, const float* wq,
+                          const float* bq, const float* wk, const float* bk, const float* wv,
+                          const float* bv, const float* wo, float dropout_p, uint64_t seed,
+                          const ncf_step_clock* clock, float* const* grad_params,
+                          float* workspace, int64_t workspace_floats, ncf_reduce_list* defer,
+                          float* grad_xu, float* grad_xi, void* stream);
 
 /* ---- a7 + a8 fused: the MLP tower in one launch per direction (input 64, hidden [256,128,64];
  * ncf_mlp_fused_supported).  Layer l = mlp.{4l} Linear (w [N_l][ldw], first K_l columns used:

@@ -141,6 +141,77 @@ __device__ __forceinline__ void bias_cols(const float* __restrict__ dYs, int R, 
   out[c] = acc;
 }
 
+// The per-group multi-head core of the forward, one lane per (group, head, query row), as
+// k_attn_fwd (same P layout and dropout index (t*M + j) with t = (b*H + h)*M + i): softmax of
+// Qs.Ks^T / scale, dropout on the weights, times Vs -> Os (rows in LDS, pitch kPitch).  The
+// probabilities go to Pg (global, [B][H][M][M]) and/or Pl (LDS, [16][H][M][M]) when given.  Os
+// may alias Qs: every lane finishes reading Q/K/V before the first store.  Shared by the forward
+// and the backward's recompute, so both produce the same bits.
+template <int HD>
+__device__ __forceinline__ void attn_core_fwd(const float* Qs, const float* Ks, const float* Vs,
+                                              float* Os, float* Pl, float* __restrict__ Pg,
+                                              int64_t g0, int ng, int M, float scale,
+                                              float p_drop, uint64_t seed) {
+  constexpr int H = kD / HD;
+  constexpr int kIt = (kGroups * H * kMaxM + kThreads - 1) / kThreads;
+  const float inv_keep = p_drop > 0.0f ? 1.0f / (1.0f - p_drop) : 1.0f;
+  const int ntask = ng * H * M;
+  float o[kIt][HD];
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int t = threadIdx.x + kThreads * it;
+    if (t < ntask) {
+      const int i = t % M, h = (t / M) % H, gl = t / (M * H);
+      const int64_t tg = ((g0 + gl) * H + h) * M + i;
+      const float* q = Qs + (gl * M + i) * kPitch + h * HD;
+      float s[kMaxM];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < kMaxM; ++j)
+        if (j < M) {
+          const float* k = Ks + (gl * M + j) * kPitch + h * HD;
+          float acc = 0.0f;
+#pragma unroll
+          for (int d = 0; d < HD; ++d) acc = fmaf(q[d], k[d], acc);
+          s[j] = acc / scale;
+          mx = fmaxf(mx, s[j]);
+        }
+      float sum = 0.0f;
+#pragma unroll
+      for (int j = 0; j < kMaxM; ++j)
+        if (j < M) {
+          s[j] = expf(s[j] - mx);
+          sum += s[j];
+        }
+#pragma unroll
+      for (int d = 0; d < HD; ++d) o[it][d] = 0.0f;
+#pragma unroll
+      for (int j = 0; j < kMaxM; ++j)
+        if (j < M) {
+          const float pj = s[j] / sum;
+          if (Pg) Pg[tg * M + j] = pj;
+          if (Pl) Pl[((gl * H + h) * M + i) * M + j] = pj;
+          const float pd =
+              p_drop > 0.0f ? pj * ncf_dropout_scale(seed, (uint64_t)tg * M + j, p_drop, inv_keep) : pj;
+          const float* v = Vs + (gl * M + j) * kPitch + h * HD;
+#pragma unroll
+          for (int d = 0; d < HD; ++d) o[it][d] = fmaf(pd, v[d], o[it][d]);
+        }
+    }
+  }
+  __syncthreads();   // every lane is done reading Q/K/V
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int t = threadIdx.x + kThreads * it;
+    if (t < ntask) {
+      const int i = t % M, h = (t / M) % H, gl = t / (M * H);
+      float* dst = Os + (gl * M + i) * kPitch + h * HD;
+#pragma unroll
+      for (int d = 0; d < HD; d += 4) *reinterpret_cast<float4*>(dst + d) = make_float4(o[it][d], o[it][d + 1], o[it][d + 2], o[it][d + 3]);
+    }
+  }
+}
+
 // per-workgroup partial of the four Linear gradients, in the flat parameter order
 // [q.weight | q.bias | k.weight | k.bias | v.weight | v.bias | out.weight | out.bias]
 constexpr int kLinW = kD * kD + kD;
@@ -153,9 +224,8 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
     const float* __restrict__ bk, const float* __restrict__ wv, const float* __restrict__ bv,
     const float* __restrict__ wo, const float* __restrict__ bo, float scale, float p_drop,
     uint64_t seed, const ncf_step_clock* clock, float* __restrict__ Q, float* __restrict__ K,
-    float* __restrict__ V, float* __restrict__ P, float* __restrict__ O, float* __restrict__ Y) {
-  constexpr int H = kD / HD;
-  constexpr int kIt = (kGroups * H * kMaxM + kThreads - 1) / kThreads;
+    float* __restrict__ V, float* __restrict__ P, float* __restrict__ O, float* __restrict__ Y,
+    int core) {
   extern __shared__ float lds[];
   const int R = kGroups * M;
   float* S0 = lds;
@@ -167,7 +237,8 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
   const int64_t r0 = g0 * M;
   const int w = (threadIdx.x >> 6) & 3;
   const int par = threadIdx.x >> 8;
-  const bool core = Q != nullptr;   // false: eval with one item per group (softmax == 1, o = v)
+  // core == 0: eval with one item per group (softmax == 1, o = v).  Q/K/P/O may be NULL with
+  // the core on: nothing is stashed (the backward recomputes it from X_u / X_i)
   if (clock) seed += clock->seed;
 
   if (core) stage_in(S0, xu + r0 * kD, R, rows);
@@ -192,66 +263,10 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
   __syncthreads();
   const float* src = S2;   // the out_proj input: O, or V when there is no core
   if (core) {
-    stage_out(Q + r0 * kD, S0, rows);
-    stage_out(K + r0 * kD, S1, rows);
+    if (Q) stage_out(Q + r0 * kD, S0, rows);
+    if (K) stage_out(K + r0 * kD, S1, rows);
     if (V) stage_out(V + r0 * kD, S2, rows);
-    // core: one lane per (group, head, query row), as k_attn_fwd (same P layout, same dropout
-    // index (t*M + j) with t = (b*H + h)*M + i)
-    const float inv_keep = p_drop > 0.0f ? 1.0f / (1.0f - p_drop) : 1.0f;
-    const int ntask = ng * H * M;
-    float o[kIt][HD];
-#pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-      const int t = threadIdx.x + kThreads * it;
-      if (t < ntask) {
-        const int i = t % M, h = (t / M) % H, gl = t / (M * H);
-        const int64_t tg = ((g0 + gl) * H + h) * M + i;
-        const float* q = S0 + (gl * M + i) * kPitch + h * HD;
-        float s[kMaxM];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < kMaxM; ++j)
-          if (j < M) {
-            const float* k = S1 + (gl * M + j) * kPitch + h * HD;
-            float acc = 0.0f;
-#pragma unroll
-            for (int d = 0; d < HD; ++d) acc = fmaf(q[d], k[d], acc);
-            s[j] = acc / scale;
-            mx = fmaxf(mx, s[j]);
-          }
-        float sum = 0.0f;
-#pragma unroll
-        for (int j = 0; j < kMaxM; ++j)
-          if (j < M) {
-            s[j] = expf(s[j] - mx);
-            sum += s[j];
-          }
-#pragma unroll
-        for (int d = 0; d < HD; ++d) o[it][d] = 0.0f;
-#pragma unroll
-        for (int j = 0; j < kMaxM; ++j)
-          if (j < M) {
-            const float pj = s[j] / sum;
-            if (P) P[tg * M + j] = pj;
-            const float pd =
-                p_drop > 0.0f ? pj * ncf_dropout_scale(seed, (uint64_t)tg * M + j, p_drop, inv_keep) : pj;
-            const float* v = S2 + (gl * M + j) * kPitch + h * HD;
-#pragma unroll
-            for (int d = 0; d < HD; ++d) o[it][d] = fmaf(pd, v[d], o[it][d]);
-          }
-      }
-    }
-    __syncthreads();   // every lane is done reading Q/K/V
-#pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-      const int t = threadIdx.x + kThreads * it;
-      if (t < ntask) {
-        const int i = t % M, h = (t / M) % H, gl = t / (M * H);
-        float* dst = S0 + (gl * M + i) * kPitch + h * HD;
-#pragma unroll
-        for (int d = 0; d < HD; d += 4) *reinterpret_cast<float4*>(dst + d) = make_float4(o[it][d], o[it][d + 1], o[it][d + 2], o[it][d + 3]);
-      }
-    }
+    attn_core_fwd<HD>(S0, S1, S2, S0, nullptr, P, g0, ng, M, scale, p_drop, seed);
     __syncthreads();
     if (O) stage_out(O + r0 * kD, S0, rows);
     src = S0;
@@ -268,16 +283,20 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
   stage_out(Y + r0 * kD, S1, rows);
 }
 
-template <int HD>
+// RC (recompute): nothing was stashed by the forward.  Q, K, V are re-projected from X_u / X_i
+// and the core forward (P, O) re-run in LDS with the forward's own code (attn_core_fwd: the same
+// bits), instead of reading 4 stashed [rows][64] blocks and P back from HBM.
+template <int HD, bool RC>
 __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     const float* __restrict__ dY, const float* __restrict__ Qg, const float* __restrict__ Kg,
-    const float* __restrict__ Vg, const float* __restrict__ P, int64_t B, int M,
+    const float* __restrict__ Vg, const float* __restrict__ Pg, int64_t B, int M,
     const float* __restrict__ wq, const float* __restrict__ wk, const float* __restrict__ wv,
     const float* __restrict__ wo, float scale, float p_drop, uint64_t seed,
     const ncf_step_clock* clock, const float* __restrict__ Og, const float* __restrict__ Xu,
     const float* __restrict__ Xi, float* __restrict__ part, float* __restrict__ dQ,
     float* __restrict__ dK, float* __restrict__ dV, float* __restrict__ dXu,
-    float* __restrict__ dXi) {
+    float* __restrict__ dXi, const float* __restrict__ bq, const float* __restrict__ bk,
+    const float* __restrict__ bv) {
   constexpr int H = kD / HD;
   constexpr int kIt = (kGroups * H * kMaxM + kThreads - 1) / kThreads;
   extern __shared__ float lds[];
@@ -286,9 +305,10 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
   float* S1 = lds + R * kPitch;
   float* S2 = lds + 2 * R * kPitch;
   float* S3 = lds + 3 * R * kPitch;
-  const bool wg = part != nullptr;   // fused weight gradients (partials of this workgroup)
+  const bool wg = RC || part != nullptr;   // fused weight gradients (partials of this workgroup)
   float* S4 = lds + 4 * R * kPitch;                 // O -> X_u (fused weight gradients only)
   float* dS = lds + (wg ? 5 : 4) * R * kPitch;      // [16][H][M][M]
+  float* Pl = dS + kGroups * H * M * M;             // RC: the recomputed P, same layout
   const int64_t g0 = (int64_t)blockIdx.x * kGroups;
   const int ng = (int)min<int64_t>(kGroups, B - g0);
   const int rows = ng * M;
@@ -299,16 +319,57 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
   const float inv_keep = p_drop > 0.0f ? 1.0f / (1.0f - p_drop) : 1.0f;
 
   stage_in(S0, dY + r0 * kD, R, rows);
-  stage_in(S1, Qg + r0 * kD, R, rows);
-  stage_in(S2, Kg + r0 * kD, R, rows);
-  stage_in(S3, Vg + r0 * kD, R, rows);
-  if (wg) stage_in(S4, Og + r0 * kD, R, rows);
+  constexpr int kPre = (16 * kMaxM * 16 + kThreads - 1) / kThreads;   // float4 per thread
+  float4 pu[kPre], pi[kPre];   // X_u / X_i rows for the fused weight gradients
+  if constexpr (RC) {
+    stage_in(S1, Xu + r0 * kD, R, rows);
+    stage_in(S2, Xi + r0 * kD, R, rows);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPre; ++q) {   // (zero rows past the batch: staged as zeros)
+      const int e = threadIdx.x + kThreads * q;
+      const bool in = e < R * 16;
+      pu[q] = in ? *reinterpret_cast<const float4*>(S1 + (e >> 4) * kPitch + (e & 15) * 4)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      pi[q] = in ? *reinterpret_cast<const float4*>(S2 + (e >> 4) * kPitch + (e & 15) * 4)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    f32x4 fq[kMaxM], fk[kMaxM], fv[kMaxM];
+    project(S1, wq, bq, M, fq);
+    project(S2, wk, bk, M, fk);
+    project(S2, wv, bv, M, fv);
+    __syncthreads();
+    // rows past the batch (a ragged last workgroup) hold zeros, as the stashing form stages
+    // them: the bias columns of dQ/dK/dV later sum over all R rows of these buffers
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    const int rsub = 4 * ((threadIdx.x & 63) >> 4);
+#pragma unroll
+    for (int rt = 0; rt < kMaxM; ++rt)
+      if (rt < M && (rt & 1) == par) {
+        const bool pad = 16 * rt + rsub + 3 >= rows;
+        f32x4 a = fq[rt], b = fk[rt], c = fv[rt];
+        if (pad) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (16 * rt + rsub + e >= rows) { a[e] = 0.f; b[e] = 0.f; c[e] = 0.f; }
+        }
+        put_tile(S1, rt, w, a);
+        put_tile(S2, rt, w, b);
+        put_tile(S3, rt, w, c);
+        if (16 * rt + rsub + 3 >= rows) put_tile(S4, rt, w, z4);   // O of padded rows
+      }
+    __syncthreads();
+    attn_core_fwd<HD>(S1, S2, S3, S4, Pl, nullptr, g0, ng, M, scale, p_drop, seed);
+  } else {
+    stage_in(S1, Qg + r0 * kD, R, rows);
+    stage_in(S2, Kg + r0 * kD, R, rows);
+    stage_in(S3, Vg + r0 * kD, R, rows);
+    if (wg) stage_in(S4, Og + r0 * kD, R, rows);
+  }
   __syncthreads();
   float* pw = wg ? part + (int64_t)blockIdx.x * kPartAttn : nullptr;
   // X_u / X_i rows of this workgroup, prefetched into registers for the fused weight gradients
-  constexpr int kPre = (16 * kMaxM * 16 + kThreads - 1) / kThreads;   // float4 per thread
-  float4 pu[kPre], pi[kPre];
-  if (wg) {
+  if (wg && !RC) {
 #pragma unroll
     for (int q = 0; q < kPre; ++q) {
       const int e = threadIdx.x + kThreads * q, r = e >> 4, c = (e & 15) * 4;
@@ -358,7 +419,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
         const int i = t % M, h = (t / M) % H, gl = t / (M * H);
         const int64_t tg = ((g0 + gl) * H + h) * M + i;
         const float* go = S0 + (gl * M + i) * kPitch + h * HD;
-        const float* prow = P + tg * M;
+        const float* prow = RC ? Pl + ((gl * H + h) * M + i) * M : Pg + tg * M;
         float dp[kMaxM], pr[kMaxM];
         float tsum = 0.0f;
 #pragma unroll
@@ -414,7 +475,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
         for (int i = 0; i < M; ++i) {
           const int64_t row = bh * M + i;
           const float ds = dS[((gl * H + h) * M + i) * M + j];
-          float pd = P[row * M + j];
+          float pd = RC ? Pl[((gl * H + h) * M + i) * M + j] : Pg[row * M + j];
           if (p_drop > 0.0f) pd *= ncf_dropout_scale(seed, (uint64_t)row * M + j, p_drop, inv_keep);
           const float* q = S1 + (gl * M + i) * kPitch + h * HD;
           const float* go = S0 + (gl * M + i) * kPitch + h * HD;
@@ -497,9 +558,10 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
   stage_out(dXi + r0 * kD, S1, rows);
 }
 
+constexpr size_t kMaxLds = 160 * 1024;   // LDS per workgroup (gfx950)
 size_t fwd_lds(int M) { return sizeof(float) * 3 * kGroups * M * kPitch; }
-size_t bwd_lds(int M, int H, bool wg) {
-  return sizeof(float) * ((wg ? 5 : 4) * kGroups * M * kPitch + kGroups * H * M * M);
+size_t bwd_lds(int M, int H, bool wg, bool rc = false) {
+  return sizeof(float) * ((wg ? 5 : 4) * kGroups * M * kPitch + (rc ? 2 : 1) * kGroups * H * M * M);
 }
 
 template <typename Kern>
@@ -527,11 +589,13 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
                 "ncf_attn_block_fwd: unsupported shape (D=%lld H=%lld M=%lld; need D=64, M<=%d)",
                 (long long)dim, (long long)heads, (long long)group_len, kMaxM);
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_attn_block_fwd: dropout_p out of [0,1)");
-  NCF_CHECK_ARG(y != nullptr && (q != nullptr) == (k != nullptr) &&
-                (q != nullptr || (group_len == 1 && dropout_p == 0.0f)),
-                "ncf_attn_block_fwd: q/k must both be given unless M == 1 without dropout");
+  NCF_CHECK_ARG(y != nullptr && (q != nullptr) == (k != nullptr),
+                "ncf_attn_block_fwd: q and k are given together (or neither)");
   NCF_CHECK_ARG(q == nullptr || (probs != nullptr && o != nullptr),
-                "ncf_attn_block_fwd: the core path needs probs and o");
+                "ncf_attn_block_fwd: a stashing forward needs probs and o");
+  // the core runs unless the eval form applies (M == 1 without dropout: softmax == 1, o = v);
+  // without q/k it stashes nothing (training with ncf_attn_block_bwd_rc)
+  const int core = (q != nullptr || group_len > 1 || dropout_p > 0.0f) ? 1 : 0;
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len;
   const size_t lds = fwd_lds(M);
@@ -544,7 +608,7 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
     if (!attr) { allow_lds(k_attn_block_fwd<HD>, fwd_lds(kMaxM)); attr = true; }                 \
     hipLaunchKernelGGL(k_attn_block_fwd<HD>, grid, dim3(kThreads), lds, st, xu, xi, groups, M, wq, bq, \
                        wk, bk, wv, bv, wo, bo, scale, dropout_p, seed, clock, q, k, v, probs, o,  \
-                       y);                                                                       \
+                       y, core);                                                                 \
     break;                                                                                       \
   }
   switch (dim / heads) {
@@ -557,6 +621,43 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
   NCF_CHECK_LAUNCH("ncf_attn_block_fwd");
   return NCF_OK;
 }
+
+namespace {
+// the per-workgroup partial rows -> the 8 parameter gradients: one reduction when they are laid
+// out like the partial row (the flat gradient buffer), else one per Linear (weight + bias
+// adjacent) or 8; deferred into `defer` when given
+int defer_partials(float* const* grad_params, const float* part, int nb, float* workspace,
+                   int64_t workspace_floats, ncf_reduce_list* defer, void* stream) {
+  ncf_reduce_list local;
+  local.count = 0;
+  ncf_reduce_list* lst = defer ? defer : &local;
+  int rc = NCF_OK;
+  bool flat = true;
+  for (int j = 1; j < 8; ++j)
+    flat = flat && grad_params[j] == grad_params[0] + (j / 2) * kLinW + (j & 1) * kD * kD;
+  if (flat) {
+    rc = ncf_defer(lst, part, nb, kPartAttn, kPartAttn, grad_params[0], 0, kPartAttn, kPartAttn);
+  } else {
+    for (int lin = 0; lin < 4 && !rc; ++lin) {
+      float* gw = grad_params[2 * lin];
+      float* gb = grad_params[2 * lin + 1];
+      const float* pp = part + lin * kLinW;
+      if (gb == gw + kD * kD) {
+        rc = ncf_defer(lst, pp, nb, kPartAttn, kLinW, gw, 0, kLinW, kLinW);
+      } else {
+        rc = ncf_defer(lst, pp, nb, kPartAttn, kD * kD, gw, 0, kD * kD, kD * kD);
+        if (!rc) rc = ncf_defer(lst, pp + kD * kD, nb, kPartAttn, kD, gb, 0, kD, kD);
+      }
+    }
+  }
+  if (rc) return rc;
+  if (!defer) {
+    const int64_t off = (int64_t)nb * kPartAttn;
+    return ncf_reduce_batch(lst, workspace + off, workspace_floats - off, stream);
+  }
+  return NCF_OK;
+}
+}  // namespace
 
 extern "C" int64_t ncf_attn_block_bwd_workspace(int64_t groups) {
   const int64_t nb = groups <= 0 ? 1 : ncf_cdiv(groups, kGroups);
@@ -597,10 +698,10 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
 #define NCF_ABB(HD)                                                                               \
   case HD: {                                                                                      \
     static bool attr = false;                                                                     \
-    if (!attr) { allow_lds(k_attn_block_bwd<HD>, bwd_lds(kMaxM, kD / HD, true)); attr = true; }   \
-    hipLaunchKernelGGL(k_attn_block_bwd<HD>, grid, dim3(kThreads), lds, st, grad_y, q, k, v, probs, \
-                       groups, M, wq, wk, wv, wo, scale, dropout_p, seed, clock, o, xu, xi, part, \
-                       grad_q, grad_k, grad_v, grad_xu, grad_xi);                                 \
+    if (!attr) { allow_lds(k_attn_block_bwd<HD, false>, bwd_lds(kMaxM, kD / HD, true)); attr = true; } \
+    hipLaunchKernelGGL((k_attn_block_bwd<HD, false>), grid, dim3(kThreads), lds, st, grad_y, q, k, v, \
+                       probs, groups, M, wq, wk, wv, wo, scale, dropout_p, seed, clock, o, xu, xi, \
+                       part, grad_q, grad_k, grad_v, grad_xu, grad_xi, nullptr, nullptr, nullptr); \
     break;                                                                                        \
   }
   switch (dim / heads) {
@@ -612,34 +713,64 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
 #undef NCF_ABB
   NCF_CHECK_LAUNCH("ncf_attn_block_bwd");
   if (!wg) return NCF_OK;
-  // partial rows -> the 8 parameter gradients: one reduction when they are laid out like the
-  // partial row (the flat gradient buffer), else one per Linear (weight + bias adjacent) or 8
-  ncf_reduce_list local;
-  local.count = 0;
-  ncf_reduce_list* lst = defer ? defer : &local;
-  int rc = NCF_OK;
-  bool flat = true;
-  for (int j = 1; j < 8; ++j)
-    flat = flat && grad_params[j] == grad_params[0] + (j / 2) * kLinW + (j & 1) * kD * kD;
-  if (flat) {
-    rc = ncf_defer(lst, part, nb, kPartAttn, kPartAttn, grad_params[0], 0, kPartAttn, kPartAttn);
-  } else {
-    for (int lin = 0; lin < 4 && !rc; ++lin) {
-      float* gw = grad_params[2 * lin];
-      float* gb = grad_params[2 * lin + 1];
-      const float* pp = part + lin * kLinW;
-      if (gb == gw + kD * kD) {
-        rc = ncf_defer(lst, pp, nb, kPartAttn, kLinW, gw, 0, kLinW, kLinW);
-      } else {
-        rc = ncf_defer(lst, pp, nb, kPartAttn, kD * kD, gw, 0, kD * kD, kD * kD);
-        if (!rc) rc = ncf_defer(lst, pp + kD * kD, nb, kPartAttn, kD, gb, 0, kD, kD);
-      }
-    }
+  return defer_partials(grad_params, part, nb, workspace, workspace_floats, defer, stream);
+}
+
+// the recompute backward holds the recomputed probabilities beside dS in LDS
+extern "C" int ncf_attn_block_rc_supported(int64_t dim, int64_t heads, int64_t group_len) {
+  return ncf_attn_block_supported(dim, heads, group_len) &&
+                 bwd_lds((int)group_len, (int)heads, true, true) <= kMaxLds
+             ? 1
+             : 0;
+}
+
+extern "C" int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const float* xi,
+                                     int64_t groups, int64_t group_len, int64_t heads,
+                                     int64_t dim, const float* wq, const float* bq,
+                                     const float* wk, const float* bk, const float* wv,
+                                     const float* bv, const float* wo, float dropout_p,
+                                     uint64_t seed, const ncf_step_clock* clock,
+                                     float* const* grad_params, float* workspace,
+                                     int64_t workspace_floats, ncf_reduce_list* defer,
+                                     float* grad_xu, float* grad_xi, void* stream) {
+  NCF_CHECK_ARG(groups >= 0 && ncf_attn_block_supported(dim, heads, group_len),
+                "ncf_attn_block_bwd_rc: unsupported shape (D=%lld H=%lld M=%lld; need D=64, M<=%d)",
+                (long long)dim, (long long)heads, (long long)group_len, kMaxM);
+  NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_attn_block_bwd_rc: dropout_p out of [0,1)");
+  NCF_CHECK_ARG(grad_y && xu && xi && wq && bq && wk && bk && wv && bv && wo && grad_params &&
+                    workspace && grad_xu && grad_xi,
+                "ncf_attn_block_bwd_rc: null argument");
+  if (workspace_floats < ncf_attn_block_bwd_workspace(groups)) {
+    ncf_set_error("ncf_attn_block_bwd_rc: workspace too small");
+    return NCF_ERR_WORKSPACE;
   }
-  if (rc) return rc;
-  if (!defer) {
-    const int64_t off = (int64_t)nb * kPartAttn;
-    return ncf_reduce_batch(lst, workspace + off, workspace_floats - off, stream);
+  NCF_CHECK_ARG(ncf_attn_block_rc_supported(dim, heads, group_len),
+                "ncf_attn_block_bwd_rc: M=%lld H=%lld needs more LDS than a workgroup has",
+                (long long)group_len, (long long)heads);
+  if (groups == 0) return NCF_OK;
+  const int M = (int)group_len, H = (int)heads;
+  const size_t lds = bwd_lds(M, H, true, true);
+  const int nb = (int)ncf_cdiv(groups, kGroups);
+  const dim3 grid((unsigned)nb);
+  hipStream_t st = (hipStream_t)stream;
+  const float scale = sqrtf((float)(dim / heads));
+#define NCF_ABR(HD)                                                                               \
+  case HD: {                                                                                      \
+    static bool attr = false;                                                                     \
+    if (!attr) { allow_lds(k_attn_block_bwd<HD, true>, kMaxLds); attr = true; }                 \
+    hipLaunchKernelGGL((k_attn_block_bwd<HD, true>), grid, dim3(kThreads), lds, st, grad_y, nullptr, \
+                       nullptr, nullptr, nullptr, groups, M, wq, wk, wv, wo, scale, dropout_p, seed, \
+                       clock, nullptr, xu, xi, workspace, nullptr, nullptr, nullptr, grad_xu, grad_xi, \
+                       bq, bk, bv);                                                               \
+    break;                                                                                        \
   }
-  return NCF_OK;
+  switch (dim / heads) {
+    NCF_ABR(8)
+    NCF_ABR(16)
+    NCF_ABR(32)
+    NCF_ABR(64)
+  }
+#undef NCF_ABR
+  NCF_CHECK_LAUNCH("ncf_attn_block_bwd_rc");
+  return defer_partials(grad_params, workspace, nb, workspace, workspace_floats, defer, stream);
 }

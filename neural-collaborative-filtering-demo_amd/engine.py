@@ -297,6 +297,7 @@ class NCFEngine:
             c = {name: ptr(p) for name, p in self.dense_params()}
             c.update({"t_" + k: ptr(v) for k, v in self.table_params().items()})
             c["att_w"] = tuple(ptr(getattr(att, nm).weight) for nm in ("q_proj", "k_proj", "v_proj", "out_proj"))
+            c["att_b"] = tuple(ptr(getattr(att, nm).bias) for nm in ("q_proj", "k_proj", "v_proj"))
             self._pp_cache = c
         return c
 
@@ -409,7 +410,8 @@ class NCFEngine:
         att = m.user_product_attention
         if temporal is None and self.attn_block(D, H, M):
             # projections + core + out_proj in one launch (attn_block.hip)
-            core = train or M != 1
+            # training: nothing stashed when the backward recomputes q/k/v/P/o (attn_rc)
+            core = (train or M != 1) and not (train and self.attn_rc(D, H, M))
             a_ = "user_product_attention."
             _lib.call("ncf_attn_block_fwd", ptr(w.xu), ptr(w.xi), n // M, M, H, D,
                       pp[a_ + "q_proj.weight"], pp[a_ + "q_proj.bias"], pp[a_ + "k_proj.weight"],
@@ -512,6 +514,20 @@ class NCFEngine:
         ok = self._mlp_ok.get(key)
         if ok is None:
             ok = self._mlp_ok[key] = bool(_lib.query("ncf_attn_block_supported", D, H, M))
+        return ok
+
+    def attn_rc(self, D: int, H: int, M: int) -> bool:
+        """Whether the training forward of the attention block stashes nothing and its backward
+        recomputes q/k/v, the probabilities and o from the LN'd rows (ncf_attn_block_bwd_rc:
+        27.9 MB less HBM traffic per C2 step).  Off by default (NCF_ATTN_RC=1 turns it on):
+        measured at C2 the forward gains 3 us and the backward loses 6-7 us (its serial
+        re-projection + core prologue costs more than reading the stash back)."""
+        if os.environ.get("NCF_ATTN_RC", "0") == "0":
+            return False
+        key = ("attn_rc", D, H, M)
+        ok = self._mlp_ok.get(key)
+        if ok is None:
+            ok = self._mlp_ok[key] = bool(_lib.query("ncf_attn_block_rc_supported", D, H, M))
         return ok
 
     def _attention_unfused(self, w, M, train, drop_p, seed, temporal, st):
@@ -694,10 +710,18 @@ class NCFEngine:
                 arr = (ctypes.c_void_p * 8)(*[ptr(gv(x)) for x in names])
                 gp = w.cache["attn_grads"] = (arr, ctypes.addressof(arr))
             ws = w.site("attn")
-            _lib.call("ncf_attn_block_bwd", ptr(w.dy), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P),
-                      n // M, M, H, D, *pp["att_w"], drop_p, seed,
-                      ptr(self.clock), ptr(w.o), ptr(w.xu), ptr(w.xi), gp[1], ptr(ws), ws.numel(),
-                      w.red_list.address, None, None, None, ptr(w.dxu), ptr(w.dxi), st)
+            if self.attn_rc(D, H, M):
+                wq, wk, wv, wo = pp["att_w"]
+                bq, bk, bv = pp["att_b"]
+                _lib.call("ncf_attn_block_bwd_rc", ptr(w.dy), ptr(w.xu), ptr(w.xi), n // M, M, H, D,
+                          wq, bq, wk, bk, wv, bv, wo, drop_p, seed, ptr(self.clock), gp[1],
+                          ptr(ws), ws.numel(), w.red_list.address, ptr(w.dxu), ptr(w.dxi), st)
+            else:
+                _lib.call("ncf_attn_block_bwd", ptr(w.dy), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P),
+                          n // M, M, H, D, *pp["att_w"], drop_p, seed,
+                          ptr(self.clock), ptr(w.o), ptr(w.xu), ptr(w.xi), gp[1], ptr(ws),
+                          ws.numel(), w.red_list.address, None, None, None, ptr(w.dxu),
+                          ptr(w.dxi), st)
         else:
             self._attention_bwd_unfused(w, drop_p, seed, joins, st)
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)

@@ -503,6 +503,42 @@ def test_attn_block_matches_unfused(monkeypatch, H, M, B):
         torch.testing.assert_close(G1[k], G0[k], rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("H,M,B,drop", [(4, 5, 37, 0.2), (1, 5, 16, 0.2), (8, 3, 50, 0.2),
+                                         (2, 6, 33, 0.0), (4, 1, 20, 0.2)])
+def test_attn_block_recompute_bitwise_equals_stash(monkeypatch, H, M, B, drop):
+    """The recompute backward (ncf_attn_block_bwd_rc: q/k/v re-projected and the core forward
+    re-run in LDS, nothing stashed by the forward) against the stashing form: same code for the
+    projections and the core, so the step's probabilities, every dense gradient and the compact
+    table gradients are bit-identical, dropout on, ragged last workgroup."""
+    from ncf_amd.trainer import FusedTrainStep
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("NCF_ATTN_RC", flag)
+        torch.manual_seed(23)
+        m = ncf.AdvancedNCF(400, 300, 5, 24, 64, 64, 32, [256, 128, 64], H, drop, M - 1).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+        assert m.engine.attn_rc(64, H, M) == (flag == "1")
+        g = torch.Generator().manual_seed(24)
+        u = torch.randint(0, 400, (B,), generator=g).repeat_interleave(M).to(DEV)
+        i = torch.randint(0, 300, (B * M,), generator=g).to(DEV)
+        t = torch.zeros(B, M)
+        t[:, 0] = 1
+        for _ in range(2):
+            w = step(u, i, t.reshape(-1, 1).to(DEV))
+        torch.cuda.synchronize()
+        nu = w.num_unique.cpu().tolist()
+        out.append((w.prob.cpu().clone(), m.engine.flat_grad.cpu().clone(),
+                    {k: v[:nu[0 if k.endswith("user") else 1]].cpu().clone() for k, v in w.G.items()},
+                    {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}))
+    (p0, g0, G0, s0), (p1, g1, G1, s1) = out
+    assert torch.equal(p0, p1)
+    assert torch.equal(g0, g1)
+    for k in G0:
+        assert torch.equal(G0[k], G1[k]), k
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
+
+
 @pytest.mark.parametrize("wgrad", ["1", "0"])
 @pytest.mark.parametrize("B,drop", [(37, 0.2), (64, 0.0), (1, 0.2), (300, 0.2)])
 def test_mlp_tower_matches_unfused(monkeypatch, B, drop, wgrad):
