@@ -12,7 +12,8 @@ FLAGS=(--offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$SRC" -I"$ROOT/include" -Wa
 pids=()
 for f in "$SRC"/*.hip; do
   b="$(basename "$f" .hip)"
-  "$HIPCC" "${FLAGS[@]}" -c "$f" -o "$OBJ/$b.o" &
+  per="NCF_FLAGS_$b"                     # per-file extra flags (A/B builds), e.g. NCF_FLAGS_adam
+  "$HIPCC" "${FLAGS[@]}" ${!per:-} -c "$f" -o "$OBJ/$b.o" &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done

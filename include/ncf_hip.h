@@ -484,6 +484,11 @@ int ncf_adam_table(float* param, float* exp_avg, float* exp_avg_sq, int64_t rows
 int ncf_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                   double lr, double beta1, double beta2, double eps, double weight_decay,
                   double step, void* stream);
+/* One Adam step over a table given its dense gradient (n = rows * dim elements): elements whose
+ * gradient is exactly zero take the zero-gradient form of the row-sparse schedules (adam.hip). */
+int ncf_adam_table_dense_grad(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                              int64_t n, double lr, double beta1, double beta2, double eps,
+                              double weight_decay, double step, void* stream);
 
 /* ---- (e) row sharding over W ranks: owner(id) = id mod W, local row = id div W ------------
  * The per-rank kernels of the row-sharded step (exchange.hip; the protocol and the RCCL
@@ -562,12 +567,13 @@ int ncf_comm_alltoallv(void* comm, const void* send, const int64_t* send_rows, v
 int ncf_comm_allreduce_sum_f32(void* comm, float* buf, int64_t n, void* stream);
 
 /* Deferred dense-exact schedule (bit-identical to ncf_adam_table, see adam.hip): rows carry
- * stamp[row] = last step reflected; step_table[2s], [2s+1] = fp32 scalars of step s
- * (-lr/(1-b1^s), 1/sqrt(1-b2^s))
- * (ncf_adam_step_scalars).  Two tables (GMF + MLP) sharing one id space go in one call
+ * stamp[row] = last step reflected; step_table[4s .. 4s+3] = fp32 scalars of step s
+ * (-lr/(1-b1^s), 1/sqrt(1-b2^s) for a gradient step; their ratio and eps / (-lr/(1-b1^s)) for
+ * the folded zero-gradient step of untouched rows) (ncf_adam_step_scalars, `count` steps from
+ * `first`, 4 floats each).  Two tables (GMF + MLP) sharing one id space go in one call
  * (p1/m1/v1 nullable).                                                                      */
-int ncf_adam_step_scalars(double lr, double beta1, double beta2, int64_t first, int64_t count,
-                          float* out_host);
+int ncf_adam_step_scalars(double lr, double beta1, double beta2, double eps, int64_t first,
+                          int64_t count, float* out_host);
 int ncf_adam_rows_catchup(float* p0, float* m0, float* v0, float* p1, float* m1, float* v1,
                           int64_t dim, const int64_t* row_ids, const uint32_t* count, int kind,
                           int64_t max_n, int32_t* stamp, int32_t target, const float* step_table,

@@ -110,8 +110,9 @@ SIGNATURES = {
     "ncf_scatter_compact_rows": (I32, [P, I64, P, P, I32, P, I64, P]),
     "ncf_adam_table": (I32, [P, P, P, I64, I64, P, P, F64, F64, F64, F64, F64, F64, P]),
     "ncf_adam_flat": (I32, [P, P, P, P, I64, F64, F64, F64, F64, F64, F64, P]),
+    "ncf_adam_table_dense_grad": (I32, [P, P, P, P, I64, F64, F64, F64, F64, F64, F64, P]),
     "ncf_fill_2d": (I32, [P, I64, I64, I64, F32, P]),
-    "ncf_adam_step_scalars": (I32, [F64, F64, F64, I64, I64, P]),
+    "ncf_adam_step_scalars": (I32, [F64, F64, F64, F64, I64, I64, P]),
     "ncf_adam_rows_catchup": (I32, [P, P, P, P, P, P, I64, P, P, I32, I64, P, I32, P, F64, F64, F64,
                                     F64, P]),
     "ncf_adam_rows_apply": (I32, [P, P, P, P, P, P, P, P, I64, P, P, I32, I64, P, I32, P, F64, F64,

@@ -19,6 +19,8 @@ namespace {
 
 struct AdamScalars {
   float neg_step, w1, b2, c2, inv_bc2_sqrt, eps, wd;
+  float b1, k1, k2;   // zero-gradient step: beta1, (1-beta1) wd, (1-beta2) wd^2
+  float ra, rb;       // zero-gradient step s: inv_bc2_sqrt / neg_step, eps / neg_step
 };
 
 // One Adam element update, written as explicit fmas with the hardware square root and
@@ -36,6 +38,21 @@ __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, flo
   v = __builtin_fmaf(s.c2 * g, g, v * s.b2);
   const float denom = __builtin_fmaf(__builtin_amdgcn_sqrtf(v), inv_bc, s.eps);
   p = __builtin_fmaf(neg_step * m, __builtin_amdgcn_rcpf(denom), p);
+}
+
+// The step of an element whose gradient is zero (an untouched table row: weight decay only),
+// the same update with the constants folded (9 VALU ops, 2 transcendental, instead of 11):
+//   m = b1 m + ((1-b1) wd) p;   v = b2 v + ((1-b2) wd^2) p p
+//   p += m / (sqrt(v) ra + rb),   ra = inv_bc2_sqrt / neg_step, rb = eps / neg_step
+// Used by every schedule for exactly the untouched elements (the dense sweep for rows without a
+// gradient slot, the deferred replay for the zero-gradient steps it owes), so the schedules stay
+// bit-identical to each other; against torch's Adam it differs by rounding (~1 ulp of m, v).
+__device__ __forceinline__ void adam0(float& p, float& m, float& v, float ra, float rb,
+                                      const AdamScalars& s) {
+  m = __builtin_fmaf(s.b1, m, s.k1 * p);
+  v = __builtin_fmaf(s.k2 * p, p, v * s.b2);
+  const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(v), ra, rb);
+  p = __builtin_fmaf(m, __builtin_amdgcn_rcpf(den), p);
 }
 
 __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, const AdamScalars& s) {
@@ -65,10 +82,15 @@ __global__ __launch_bounds__(256) void k_adam_table(float* __restrict__ p, float
     const int64_t row = e / (D / 4);
     const int col = (int)(e % (D / 4)) * 4;
     const int32_t sl = slot ? slot[row] : -1;
-    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (sl >= 0) g = ld4(G + (int64_t)sl * D + col);
     float4 pp = ldp4<BF>(p, e * 4), mm = ld4(m + e * 4), vv = ld4(v + e * 4);
-    adam4(pp, mm, vv, g, s);
+    if (sl >= 0) {
+      adam4(pp, mm, vv, ld4(G + (int64_t)sl * D + col), s);
+    } else {   // no gradient row this step: the zero-gradient form (as the deferred replay)
+      adam0(pp.x, mm.x, vv.x, s.ra, s.rb, s);
+      adam0(pp.y, mm.y, vv.y, s.ra, s.rb, s);
+      adam0(pp.z, mm.z, vv.z, s.ra, s.rb, s);
+      adam0(pp.w, mm.w, vv.w, s.ra, s.rb, s);
+    }
     stp4<BF>(p, e * 4, pp);
     st4(m + e * 4, mm);
     st4(v + e * 4, vv);
@@ -82,6 +104,27 @@ __global__ __launch_bounds__(256) void k_adam_flat(float* __restrict__ p, const 
        i += (int64_t)gridDim.x * blockDim.x) {
     float pp = p[i], mm = m[i], vv = v[i];
     adam1(pp, mm, vv, g[i], s);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+  }
+}
+
+// A table with a dense [rows, D] gradient (gradient accumulation and the other dense-.grad
+// cases of the optimizer hook): an element whose gradient is exactly zero takes the
+// zero-gradient form, as the row-sparse schedules step the rows that got no gradient (a touched
+// row's gradient is never exactly zero in practice: it comes through the LayerNorm backward).
+__global__ __launch_bounds__(256) void k_adam_table_dense_grad(float* __restrict__ p,
+                                                               const float* __restrict__ g,
+                                                               float* __restrict__ m,
+                                                               float* __restrict__ v, int64_t n,
+                                                               AdamScalars s) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    const float gg = g[i];
+    if (gg == 0.0f) adam0(pp, mm, vv, s.ra, s.rb, s);
+    else adam1(pp, mm, vv, gg, s);
     p[i] = pp;
     m[i] = mm;
     v[i] = vv;
@@ -104,8 +147,10 @@ __global__ void k_scatter_compact(float* __restrict__ dense, const int64_t* __re
 // A row that receives no gradient at step s still takes the step with g = 0 (weight decay only).
 // Instead of streaming every untouched row every step, rows carry stamp[row] = the last step
 // their (p, m, v) reflect; before a row is READ it is caught up by replaying the missing
-// zero-gradient steps s = stamp+1 .. target with that step's scalars (table[2s] = -lr/(1-b1^s),
-// table[2s+1] = 1/sqrt(1-b2^s)), element by element, with the very same adam1 arithmetic.
+// zero-gradient steps s = stamp+1 .. target with that step's scalars (step table, 4 floats per
+// step: [4s] = -lr/(1-b1^s), [4s+1] = 1/sqrt(1-b2^s) for the gradient step adam1, [4s+2] / [4s+3]
+// = ra / rb for the zero-gradient step adam0), element by element, with the very same adam0
+// arithmetic as the dense sweep's untouched rows.
 // Results are bit-identical to the dense sweep; the cost moves from HBM traffic to VALU work.
 struct TablePtrs {
   float *p0, *m0, *v0, *p1, *m1, *v1;  // two tables sharing the row index space (GMF + MLP)
@@ -137,19 +182,25 @@ __device__ __forceinline__ void replay_uniform(float* p0, float* m0, float* v0, 
   int32_t q = from + 1;
   float sc[2 * C];
 #pragma unroll
-  for (int k = 0; k < 2 * C; ++k) sc[k] = table[2 * q + k];
+  for (int k = 0; k < C; ++k) {
+    sc[2 * k] = table[4 * (q + k) + 2];
+    sc[2 * k + 1] = table[4 * (q + k) + 3];
+  }
   while (q + C - 1 <= to) {
     float nx[2 * C];
 #pragma unroll
-    for (int k = 0; k < 2 * C; ++k) nx[k] = table[2 * (q + C) + k];
+    for (int k = 0; k < C; ++k) {
+      nx[2 * k] = table[4 * (q + C + k) + 2];
+      nx[2 * k + 1] = table[4 * (q + C + k) + 3];
+    }
     __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this chunk's steps
 #pragma unroll
     for (int k = 0; k < C; ++k) {
 #pragma unroll
       for (int j = 0; j < EPL; ++j) {
-        adam1(p0[j], m0[j], v0[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+        adam0(p0[j], m0[j], v0[j], sc[2 * k], sc[2 * k + 1], s);
         if (BF) p0[j] = ncf_round_bf16(p0[j]);   // bf16 tables: stored (rounded) every step
-        if (PAIR) adam1(p1[j], m1[j], v1[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+        if (PAIR) adam0(p1[j], m1[j], v1[j], sc[2 * k], sc[2 * k + 1], s);
         if (PAIR && BF) p1[j] = ncf_round_bf16(p1[j]);
       }
     }
@@ -162,9 +213,9 @@ __device__ __forceinline__ void replay_uniform(float* p0, float* m0, float* v0, 
     if (q + k > to) break;
 #pragma unroll
     for (int j = 0; j < EPL; ++j) {
-      adam1(p0[j], m0[j], v0[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+      adam0(p0[j], m0[j], v0[j], sc[2 * k], sc[2 * k + 1], s);
       if (BF) p0[j] = ncf_round_bf16(p0[j]);
-      if (PAIR) adam1(p1[j], m1[j], v1[j], 0.0f, sc[2 * k], sc[2 * k + 1], s);
+      if (PAIR) adam0(p1[j], m1[j], v1[j], sc[2 * k], sc[2 * k + 1], s);
       if (PAIR && BF) p1[j] = ncf_round_bf16(p1[j]);
     }
   }
@@ -196,11 +247,11 @@ __device__ __forceinline__ void catch_up_row(const TablePtrs& t, int64_t row, in
     } else {
 #pragma unroll 2
       for (int32_t q = from + 1; q <= to; ++q) {
-        const float ns = table[2 * q], bc = table[2 * q + 1];
+        const float ra = table[4 * q + 2], rb = table[4 * q + 3];
 #pragma unroll
         for (int j = 0; j < EPL; ++j) {
-          adam1(p0[j], m0[j], v0[j], 0.0f, ns, bc, s);
-          adam1(p1[j], m1[j], v1[j], 0.0f, ns, bc, s);
+          adam0(p0[j], m0[j], v0[j], ra, rb, s);
+          adam0(p1[j], m1[j], v1[j], ra, rb, s);
           if (BF) { p0[j] = ncf_round_bf16(p0[j]); p1[j] = ncf_round_bf16(p1[j]); }
         }
       }
@@ -214,10 +265,10 @@ __device__ __forceinline__ void catch_up_row(const TablePtrs& t, int64_t row, in
   } else {
 #pragma unroll 2
     for (int32_t q = from + 1; q <= to; ++q) {
-      const float ns = table[2 * q], bc = table[2 * q + 1];
+      const float ra = table[4 * q + 2], rb = table[4 * q + 3];
 #pragma unroll
       for (int j = 0; j < EPL; ++j) {
-        adam1(p0[j], m0[j], v0[j], 0.0f, ns, bc, s);
+        adam0(p0[j], m0[j], v0[j], ra, rb, s);
         if (BF) p0[j] = ncf_round_bf16(p0[j]);
       }
     }
@@ -284,7 +335,7 @@ __global__ __launch_bounds__(256) void k_adam_apply(TablePtrs t, const int64_t* 
   if (clock) step += clock->t;
   const int64_t row = ids[c];
   const int64_t o = row * D + sub * 4;
-  const float ns = table[2 * step], bc = table[2 * step + 1];
+  const float ns = table[4 * step], bc = table[4 * step + 1];
   float4 p0 = ld4(t.p0 + o), m0 = ld4(t.m0 + o), v0 = ld4(t.v0 + o);
   adam4(p0, m0, v0, ld4(t.G0 + c * D + sub * 4), ns, bc, s);
   st4(t.p0 + o, p0); st4(t.m0 + o, m0); st4(t.v0 + o, v0);
@@ -330,7 +381,7 @@ __global__ __launch_bounds__(256) void k_adam_flat_clock(float* __restrict__ p,
                                                          const ncf_step_clock* __restrict__ clock,
                                                          AdamScalars s) {
   const int32_t step = clock->t + step_rel;
-  const float ns = table[2 * step], bc = table[2 * step + 1];
+  const float ns = table[4 * step], bc = table[4 * step + 1];
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     float pp = p[i], mm = m[i], vv = v[i];
@@ -385,7 +436,7 @@ __global__ __launch_bounds__(256) void k_pairs_apply(const PairArgs a, const uin
   const TablePtrs& t = a.t[k];
   const int64_t row = a.ids[k][c];
   const int64_t o = row * D + sub * 4;
-  const float ns = table[2 * step], bc = table[2 * step + 1];
+  const float ns = table[4 * step], bc = table[4 * step + 1];
   float4 p0 = ldp4<BF>(t.p0, o), m0 = ld4(t.m0 + o), v0 = ld4(t.v0 + o);
   adam4(p0, m0, v0, ld4(t.G0 + c * D + sub * 4), ns, bc, s);
   stp4<BF>(t.p0, o, p0); st4(t.m0 + o, m0); st4(t.v0 + o, v0);
@@ -445,7 +496,7 @@ __global__ __launch_bounds__(256) void k_adam_flat_close(float* __restrict__ p,
                                                          int32_t step_rel, ncf_step_clock* clock,
                                                          uint64_t base_seed, AdamScalars s) {
   const int32_t step = clock->t + step_rel;
-  const float ns = table[2 * step], bc = table[2 * step + 1];
+  const float ns = table[4 * step], bc = table[4 * step + 1];
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     float pp = p[i], mm = m[i], vv = v[i];
@@ -479,6 +530,14 @@ AdamScalars make_scalars(double lr, double beta1, double beta2, double eps, doub
   s.inv_bc2_sqrt = (float)(1.0 / sqrt(bc2));
   s.eps = (float)eps;
   s.wd = (float)wd;
+  s.b1 = (float)beta1;
+  s.k1 = (float)((1.0 - beta1) * wd);
+  s.k2 = (float)((1.0 - beta2) * wd * wd);
+  // zero-gradient form: ns folded into the denominator (lr == 0: a finite huge denominator, the
+  // step vanishes instead of 0 * inf)
+  const double ns = -(lr / bc1);
+  s.ra = ns != 0.0 ? (float)((1.0 / sqrt(bc2)) / ns) : -3.0e38f;
+  s.rb = ns != 0.0 ? (float)(eps / ns) : -3.0e38f;
   return s;
 }
 
@@ -546,6 +605,20 @@ extern "C" int ncf_adam_flat(float* param, const float* grad, float* exp_avg, fl
   hipLaunchKernelGGL(k_adam_flat, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, param,
                      grad, exp_avg, exp_avg_sq, n, s);
   NCF_CHECK_LAUNCH("ncf_adam_flat");
+  return NCF_OK;
+}
+
+extern "C" int ncf_adam_table_dense_grad(float* param, const float* grad, float* exp_avg,
+                                         float* exp_avg_sq, int64_t n, double lr, double beta1,
+                                         double beta2, double eps, double weight_decay,
+                                         double step, void* stream) {
+  NCF_CHECK_ARG(n >= 0 && step >= 1, "ncf_adam_table_dense_grad: bad args");
+  if (n == 0) return NCF_OK;
+  NCF_CHECK_ARG(param && grad && exp_avg && exp_avg_sq, "ncf_adam_table_dense_grad: null pointer");
+  const AdamScalars s = make_scalars(lr, beta1, beta2, eps, weight_decay, step);
+  hipLaunchKernelGGL(k_adam_table_dense_grad, dim3(grid_for(n)), dim3(256), 0,
+                     (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq, n, s);
+  NCF_CHECK_LAUNCH("ncf_adam_table_dense_grad");
   return NCF_OK;
 }
 
@@ -658,13 +731,15 @@ int sweep_d(TablePtrs t, int64_t row0, int64_t rows, int32_t* stamp, int32_t tar
 
 // Host helper: scalars of steps first .. first+count-1 as out[2*(s-first)] = -lr/(1-b1^s),
 // out[2*(s-first)+1] = sqrt(1-b2^s) — the exact fp32 values the dense kernel uses.
-extern "C" int ncf_adam_step_scalars(double lr, double beta1, double beta2, int64_t first,
-                                     int64_t count, float* out_host) {
+extern "C" int ncf_adam_step_scalars(double lr, double beta1, double beta2, double eps,
+                                     int64_t first, int64_t count, float* out_host) {
   NCF_CHECK_ARG(first >= 1 && count >= 0 && out_host, "ncf_adam_step_scalars: bad args");
   for (int64_t i = 0; i < count; ++i) {
-    const AdamScalars s = make_scalars(lr, beta1, beta2, 0.0, 0.0, (double)(first + i));
-    out_host[2 * i] = s.neg_step;
-    out_host[2 * i + 1] = s.inv_bc2_sqrt;
+    const AdamScalars s = make_scalars(lr, beta1, beta2, eps, 0.0, (double)(first + i));
+    out_host[4 * i] = s.neg_step;
+    out_host[4 * i + 1] = s.inv_bc2_sqrt;
+    out_host[4 * i + 2] = s.ra;
+    out_host[4 * i + 3] = s.rb;
   }
   return NCF_OK;
 }

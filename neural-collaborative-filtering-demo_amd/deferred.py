@@ -78,10 +78,11 @@ class DeferredTableAdam:
         self._joined = True
         engine.deferred = self
 
-    # ---- per-step scalar table (index 2s / 2s+1 = step s)
+    # ---- per-step scalar table (index 4s .. 4s+3 = step s: gradient-step and zero-gradient-step
+    #      scalars, ncf_adam_step_scalars)
     def _ensure(self, upto: int):
         b1, b2 = self.betas
-        hp = (self.lr, b1, b2)
+        hp = (self.lr, b1, b2, self.eps)
         if upto <= self._filled and self._hp_filled == hp:
             return
         if self._hp_filled is None:
@@ -94,17 +95,17 @@ class DeferredTableAdam:
             first = self._filled + 1
         first = max(1, first)
         last = max(upto, first) + 4096
-        host = np.empty(2 * (last - first + 1), dtype=np.float32)
-        _lib.call("ncf_adam_step_scalars", self.lr, b1, b2, first, last - first + 1,
+        host = np.empty(4 * (last - first + 1), dtype=np.float32)
+        _lib.call("ncf_adam_step_scalars", self.lr, b1, b2, self.eps, first, last - first + 1,
                   host.ctypes.data)
-        need = 2 * (last + 1)
+        need = 4 * (last + 1)
         if self._table.numel() < need:
             grown = torch.zeros(max(need, 2 * self._table.numel()), dtype=torch.float32,
                                 device=self._table.device)
             if self._table.numel():
                 grown[:self._table.numel()].copy_(self._table)
             self._table = grown
-        self._table[2 * first:2 * (last + 1)].copy_(torch.from_numpy(host))
+        self._table[4 * first:4 * (last + 1)].copy_(torch.from_numpy(host))
         self._filled, self._hp_filled = last, hp
 
     def set_hparams(self, lr, betas, eps, weight_decay):

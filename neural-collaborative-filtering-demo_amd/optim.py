@@ -202,7 +202,7 @@ class _Binding:
             if p.grad is None:
                 continue
             m = self.moments[k]
-            _lib.call("ncf_adam_flat", ptr(p), ptr(p.grad.contiguous()), ptr(m["exp_avg"]),
+            _lib.call("ncf_adam_table_dense_grad", ptr(p), ptr(p.grad.contiguous()), ptr(m["exp_avg"]),
                       ptr(m["exp_avg_sq"]), p.numel(), lr, b1, b2, eps, wd,
                       float(self.step + 1), st)
             stepped = True

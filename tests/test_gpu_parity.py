@@ -1463,8 +1463,8 @@ def test_adam_flat_clock_close_equals_two_launches():
     g = torch.Generator().manual_seed(11)
     n = 300_001                       # > one block, not a multiple of 256
     lr, b1, b2, eps, wd, seed = 1e-3, 0.9, 0.999, 1e-8, 1e-5, 12345
-    host = np.zeros(2 * 9, dtype=np.float32)      # step scalars of steps 1..8 at index 2s, 2s+1
-    _lib.call("ncf_adam_step_scalars", lr, b1, b2, 1, 8, host[2:].ctypes.data)
+    host = np.zeros(4 * 9, dtype=np.float32)      # step scalars of steps 1..8 at index 4s..4s+3
+    _lib.call("ncf_adam_step_scalars", lr, b1, b2, eps, 1, 8, host[4:].ctypes.data)
     table = torch.from_numpy(host).to(DEV)
     ps = [torch.randn(n, generator=g).to(DEV) for _ in range(2)]
     ps[1].copy_(ps[0])
