@@ -128,10 +128,31 @@ extern "C" int ncf_comm_alltoallv(void* comm, const void* send, const int64_t* s
   NCF_CHECK_ARG((so == 0 || send) && (ro == 0 || recv), "ncf_comm_alltoallv: null buffer");
   const char* sb = static_cast<const char*>(send);
   char* rb = static_cast<char*>(recv);
+  // this rank's own share is a device copy on the stream (RCCL's send-to-self runs it through
+  // its kernel at a fraction of the copy rate); RCCL carries only the peers' shares, and a
+  // world of 1 launches no RCCL kernel at all
+  int64_t so_self = 0, ro_self = 0;
+  for (int p = 0; p < c->rank; ++p) {
+    so_self += send_rows[p];
+    ro_self += recv_rows[p];
+  }
+  NCF_CHECK_ARG(send_rows[c->rank] == recv_rows[c->rank], "ncf_comm_alltoallv: self counts differ");
+  if (send_rows[c->rank] &&
+      hipMemcpyAsync(rb + ro_self * row_bytes, sb + so_self * row_bytes,
+                     (size_t)(send_rows[c->rank] * row_bytes), hipMemcpyDeviceToDevice, st) != hipSuccess) {
+    ncf_set_error("ncf_comm_alltoallv: self copy failed");
+    return NCF_ERR_LAUNCH;
+  }
+  if (c->world == 1) return NCF_OK;
   NCF_RCCL("ncf_comm_alltoallv(group start)", rccl().group_start());
   so = 0;
   ro = 0;
   for (int p = 0; p < c->world; ++p) {
+    if (p == c->rank) {
+      so += send_rows[p];
+      ro += recv_rows[p];
+      continue;
+    }
     if (send_rows[p]) {
       const ncclResult_t rc =
           rccl().send(sb + so * row_bytes, (size_t)(send_rows[p] * row_bytes), ncclInt8, p, c->comm, st);
@@ -159,6 +180,7 @@ extern "C" int ncf_comm_allreduce_sum_f32(void* comm, float* buf, int64_t n, voi
   NCF_CHECK_ARG(comm && n >= 0 && (n == 0 || buf), "ncf_comm_allreduce_sum_f32: bad args");
   if (n == 0) return NCF_OK;
   const Comm* c = static_cast<const Comm*>(comm);
+  if (c->world == 1) return NCF_OK;   // the sum over one rank is the buffer itself
   NCF_RCCL("ncf_comm_allreduce_sum_f32",
            rccl().all_reduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, (hipStream_t)stream));
   return NCF_OK;

@@ -91,7 +91,7 @@ class ShardExchange:
         self.counts_wait(plan)
 
     def exchange(self, t: torch.Tensor, send_splits: List[int], recv_splits: List[int],
-                 side: bool = False):
+                 side: bool = False, slot: Optional[str] = None):
         out = torch.empty((sum(recv_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_to_all_single(out, t[:sum(send_splits)], recv_splits, send_splits,
                                group=self.plan_group if side else self.group)
@@ -150,6 +150,7 @@ class RcclExchange(ShardExchange):
         self._one = (ctypes.c_int64 * W)(*([1] * W))
         self._side_stream = None
         self._ev_in, self._ev_out = torch.cuda.Event(), torch.cuda.Event()
+        self._slots = {}
 
     def _comm(self):
         uid = torch.zeros(128, dtype=torch.uint8)
@@ -185,11 +186,22 @@ class RcclExchange(ShardExchange):
         self._side_stream = plan.stream
 
     def exchange(self, t: torch.Tensor, send_splits: List[int], recv_splits: List[int],
-                 side: bool = False):
+                 side: bool = False, slot: Optional[str] = None):
+        """``slot``: a grow-only output buffer reused by every call with that name (the caller
+        consumes it in stream order before the next such call), else a fresh tensor."""
         sr, rr = self._sr, self._rr
         for p in range(self.world):
             sr[p], rr[p] = send_splits[p], recv_splits[p]
-        out = torch.empty((sum(recv_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        shape = (sum(recv_splits),) + tuple(t.shape[1:])
+        if slot is None:
+            out = torch.empty(shape, dtype=t.dtype, device=t.device)
+        else:
+            buf = self._slots.get(slot)
+            n = math.prod(shape)
+            if buf is None or buf.numel() < n or buf.dtype != t.dtype:
+                buf = self._slots[slot] = torch.empty(max(n, 1) * 5 // 4, dtype=t.dtype,
+                                                      device=t.device)
+            out = buf[:n].view(shape)
         row = t.element_size() * (math.prod(t.shape[1:]) if t.dim() > 1 else 1)
         _lib.call("ncf_comm_alltoallv", self.side if side else self.main, ptr(t), sr, ptr(out),
                   rr, row, _lib.stream_ptr(t.device))
@@ -271,7 +283,7 @@ class ShardedTrainStep:
             recv = X.exchange(plan.send, send_splits, recv_splits)
         own = ops.owner_prepare(recv, plan)
         rows = ops.owner_gather(own, recv)
-        back = X.exchange(rows, recv_splits, send_splits)
+        back = X.exchange(rows, recv_splits, send_splits, slot="rows")
         grads, loss = ops.compute(plan, back, user_ids, item_ids, targets,
                                   loss_denominator=user_ids.numel() * X.world)
         if self.ahead and self._pending is not None:   # step t+1's rows to their owners now
@@ -279,7 +291,7 @@ class ShardedTrainStep:
             X.counts_wait(nxt)
             self._pending[3] = X.exchange_ahead(nxt)
         ar = X.all_reduce_start(ops.dense_grad())
-        got = X.exchange(grads, send_splits, recv_splits)
+        got = X.exchange(grads, send_splits, recv_splits, slot="grads")
         ops.owner_apply(own, got)
         X.all_reduce_wait(ar)
         ops.dense_step()

@@ -224,7 +224,9 @@ class GraphedScorer:
         run.launch(self.model, st)           # warm-up: kernel attributes, lazy module loads
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # thread_local: other threads' HIP calls (e.g. a process group's watchdog polling its
+        # events) stay legal while this thread captures
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             run.launch(self.model, _lib.stream_ptr(dev))
             self.flags = torch.stack([run.overflow[:self.n].amax(), run.err[0]])
             self.out = run.result()

@@ -69,7 +69,7 @@ def _worker(rank, world, port, out_dir):
             dist.all_to_all_single(recv, send, group=self.plan_group)
             plan.send_counts, plan.recv_counts = send.tolist(), recv.tolist()
 
-        def exchange(self, t, send_splits, recv_splits, side=False):
+        def exchange(self, t, send_splits, recv_splits, side=False, slot=None):
             src = t[:sum(send_splits)].cpu()
             out = torch.empty((sum(recv_splits),) + tuple(t.shape[1:]), dtype=t.dtype)
             dist.all_to_all_single(out, src, recv_splits, send_splits,
