@@ -629,6 +629,15 @@ int ncf_adam_pairs_catchup_clock(const ncf_table_pair* pairs, int npairs, int64_
                                  const ncf_step_clock* clock, const float* step_table,
                                  double beta1, double beta2, double eps, double weight_decay,
                                  void* stream);
+/* The same catch-up, marking every listed row in flight (stamp = target | NCF_STAMP_LOCK,
+ * 0x40000000) until the step's ncf_adam_pairs_apply_clock writes its stamp: a catch-up of the
+ * next batch's rows running meanwhile on another stream (target_rel one step further) skips them. */
+#define NCF_STAMP_LOCK 0x40000000
+int ncf_adam_pairs_catchup_lock_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
+                                      const uint32_t* count, int64_t max_n, int32_t target_rel,
+                                      const ncf_step_clock* clock, const float* step_table,
+                                      double beta1, double beta2, double eps, double weight_decay,
+                                      void* stream);
 int ncf_adam_pairs_apply_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
                                const uint32_t* count, int64_t max_n, int32_t step_rel,
                                const ncf_step_clock* clock, const float* step_table, double beta1,

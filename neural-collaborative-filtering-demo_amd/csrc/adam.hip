@@ -406,7 +406,7 @@ __global__ __launch_bounds__(256) void k_pairs_catchup(const PairArgs a, const u
                                                        int64_t max_n, int32_t target_rel,
                                                        const ncf_step_clock* __restrict__ clock,
                                                        const float* __restrict__ table,
-                                                       AdamScalars s) {
+                                                       AdamScalars s, int lock) {
   constexpr int L = Replay<D>::LPR;   // lanes per row
   const int k = blockIdx.y;
   const int64_t tt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -418,7 +418,9 @@ __global__ __launch_bounds__(256) void k_pairs_catchup(const PairArgs a, const u
   int32_t* stamp = a.stamp[k];
   const int32_t from = stamp[row];
   catch_up_row<D, BF>(a.t[k], row, sub, from, target, table, s);
-  if (sub == 0 && from < target) stamp[row] = target;
+  // lock: every listed row is marked in flight (current through target, its gradient step still
+  // to come: the step's apply writes the plain stamp back); replays of other rows skip it
+  if (sub == 0 && (lock || from < target)) stamp[row] = lock ? (target | NCF_STAMP_LOCK) : target;
 }
 
 template <int D, bool BF = false>
@@ -684,11 +686,11 @@ PairArgs pair_args(const ncf_table_pair* p, int n) {
 template <int D>
 int pairs_catchup_d(PairArgs a, int n, const uint32_t* count, int64_t max_n, int32_t rel,
                     const ncf_step_clock* clock, const float* table, AdamScalars s,
-                    hipStream_t st) {
+                    hipStream_t st, int lock = 0) {
   if (a.bf)
-    hipLaunchKernelGGL((k_pairs_catchup<D, true>), dim3(ncf_cdiv(max_n * Replay<D>::LPR, 256), n), dim3(256), 0, st, a, count, max_n, rel, clock, table, s);
+    hipLaunchKernelGGL((k_pairs_catchup<D, true>), dim3(ncf_cdiv(max_n * Replay<D>::LPR, 256), n), dim3(256), 0, st, a, count, max_n, rel, clock, table, s, lock);
   else
-    hipLaunchKernelGGL((k_pairs_catchup<D, false>), dim3(ncf_cdiv(max_n * Replay<D>::LPR, 256), n), dim3(256), 0, st, a, count, max_n, rel, clock, table, s);
+    hipLaunchKernelGGL((k_pairs_catchup<D, false>), dim3(ncf_cdiv(max_n * Replay<D>::LPR, 256), n), dim3(256), 0, st, a, count, max_n, rel, clock, table, s, lock);
   NCF_CHECK_LAUNCH("ncf_adam_pairs_catchup_clock");
   return NCF_OK;
 }
@@ -892,6 +894,23 @@ extern "C" int ncf_adam_flat_clock_close(float* param, const float* grad, float*
                      consts_of(beta1, beta2, eps, weight_decay));
   NCF_CHECK_LAUNCH("ncf_adam_flat_clock_close");
   return NCF_OK;
+}
+
+// the same catch-up, marking every listed row in flight (stamp = target | NCF_STAMP_LOCK) until
+// the step's ncf_adam_pairs_apply_clock: a catch-up of the NEXT batch's rows running
+// concurrently (another stream, target one step further) leaves them alone
+extern "C" int ncf_adam_pairs_catchup_lock_clock(const ncf_table_pair* pairs, int npairs,
+                                                 int64_t dim, const uint32_t* count, int64_t max_n,
+                                                 int32_t target_rel, const ncf_step_clock* clock,
+                                                 const float* step_table, double beta1,
+                                                 double beta2, double eps, double weight_decay,
+                                                 void* stream) {
+  NCF_CHECK_ARG(pairs && npairs >= 1 && npairs <= 2 && count && clock && step_table,
+                "ncf_adam_pairs_catchup_lock_clock: bad args");
+  if (max_n <= 0) return NCF_OK;
+  NCF_DISPATCH_DIM(dim, pairs_catchup_d, pair_args(pairs, npairs), npairs, count, max_n,
+                   target_rel, clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
+                   (hipStream_t)stream, 1);
 }
 
 extern "C" int ncf_adam_pairs_catchup_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,

@@ -76,6 +76,14 @@ class DeferredTableAdam:
         self._side = None
         self._ev = None
         self._joined = True
+        # Early catch-up (clock path, set by FusedTrainStep(next=...) through request_early):
+        # the NEXT batch's rows that this step does not touch are brought current through THIS
+        # step (its zero-gradient update included) on a side stream, under this step's forward /
+        # backward, instead of at the start of the next step.  This step's own rows are locked
+        # by its catch-up (stamp | NCF_STAMP_LOCK, cleared by its apply) so the early replay
+        # skips them; the step's rolling sweep waits for it.  Same replays, bit-identical.
+        self._early_req = None    # (side stream, ncf_table_pair[2] of the next rows, max_n)
+        self._early_ev = None
         engine.deferred = self
 
     # ---- per-step scalar table (index 4s .. 4s+3 = step s: gradient-step and zero-gradient-step
@@ -276,12 +284,41 @@ class DeferredTableAdam:
         if self.clock is not None and n > 0:   # both kinds in one launch
             self._ensure(self.t + 1)
             pairs = self._pairs_for(w)
-            _lib.call("ncf_adam_pairs_catchup_clock", ctypes.addressof(pairs), 2,
+            req, self._early_req = self._early_req, None
+            _lib.call("ncf_adam_pairs_catchup_lock_clock" if req else
+                      "ncf_adam_pairs_catchup_clock", ctypes.addressof(pairs), 2,
                       m.mlp_embedding_dim, ptr(w.num_unique), n, 0, ptr(self.clock),
                       ptr(self._table), *self._consts(), st)
+            if req:
+                side, npairs, ncount, nmax = req
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.clock.device))
+                side.wait_event(ev)
+                _lib.call("ncf_adam_pairs_catchup_clock", ctypes.addressof(npairs), 2,
+                          m.mlp_embedding_dim, ptr(ncount), nmax, 1, ptr(self.clock),
+                          ptr(self._table), *self._consts(), side.cuda_stream)
+                self._early_ev = torch.cuda.Event()
+                self._early_ev.record(side)
             return
         self.catchup_rows("user", w.uniq_u, w.num_unique, 0, n, st)
         self.catchup_rows("item", w.uniq_i, w.num_unique, 1, n, st)
+
+    def request_early(self, side, uniq_u, uniq_i, num_unique, n):
+        """Ask the next prepare() (this step's) to catch up the next batch's unique rows
+        (uniq_u / uniq_i, counts num_unique, from a dedup ordered on `side`) on `side`."""
+        key = ("early", self._serial, getattr(self, "_gen", 0), uniq_u.data_ptr(),
+               uniq_i.data_ptr())
+        cache = self.__dict__.setdefault("_early_pairs", {})
+        pairs = cache.get(key)
+        if pairs is None:
+            pairs = cache[key] = self._pairs()
+            pairs[0].row_ids, pairs[1].row_ids = ptr(uniq_u), ptr(uniq_i)
+        self._early_req = (side, pairs, num_unique, n)
+
+    def early_join(self):
+        if self._early_ev is not None:
+            torch.cuda.current_stream(self.clock.device).wait_event(self._early_ev)
+            self._early_ev = None
 
     # ---- after the backward: this step's gradient on the touched rows
     def apply(self, w, st):
@@ -289,6 +326,7 @@ class DeferredTableAdam:
         if self.clock is not None:
             self._ensure(self.t + 1)
             self.sweep_join()
+            self.early_join()   # (before the sweep, which may reach the same rows)
             if n > 0:
                 pairs = self._pairs_for(w)
                 _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2,

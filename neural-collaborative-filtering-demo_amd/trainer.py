@@ -11,6 +11,7 @@ the reference trainer is out of scope; batches are (KeyedJaggedTensor, targets[N
 BCE + backward kernels, fused Adam — identical math, one kernel sequence on one stream.  It is
 what the benchmark times (and what a production trainer uses).
 """
+import os
 import logging
 from typing import Any, Dict, Optional  # noqa: F401
 
@@ -69,6 +70,11 @@ class FusedTrainStep:
         self.v_flat = torch.zeros_like(eng.flat)
         self.last_loss = None
         self.graph = bool(graph)
+        # with next=..., the next batch's rows untouched by this step can be caught up under
+        # this step on the side stream (DeferredTableAdam.request_early; NCF_EARLY_CATCHUP=1).
+        # Off by default: measured at C2 it moves ~5 us of catch-up off the critical path but
+        # slows the attention / tower kernels it shares the CUs with by more (0.337 -> 0.350 ms)
+        self.early = os.environ.get("NCF_EARLY_CATCHUP", "0") != "0"
         # the device step clock is the default whenever the deferred schedule is on (both kinds
         # per launch, no host step arguments; bit-identical to the host-driven form)
         self.use_clock = (self.graph or deferred) if clock is None else bool(clock)
@@ -185,6 +191,11 @@ class FusedTrainStep:
         ev = torch.cuda.Event()
         ev.record(side)
         self._pending = (uid, iid, ev)          # the caller's objects: matched by identity
+        if self.early and not self.bf16:
+            # and, once this step's catch-up has locked its rows, the rows of the next batch
+            # that this step does not touch are brought current on the same side stream
+            self.deferred.request_early(side, s["uniq_u"], s["uniq_i"], s["num_unique"],
+                                        u.numel())
 
     def _activate_dedup(self, w, uid, iid):
         """Point w at this step's dedup set: the prefetched one when it was made for these ids
