@@ -4,7 +4,15 @@ import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv"
 anchor = sys.argv[2] if len(sys.argv) > 2 else "k_gather_ln_gmf"
+def short(name):
+    """'void (anonymous namespace)::k_mlp_bwd<false>(float const*, ...)' -> 'k_mlp_bwd'"""
+    name = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    return name.split("(")[0].split("<")[0]
+
+
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+for r in rows:
+    r["Kernel_Name"] = short(r["Kernel_Name"])
 idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(anchor)]
 a, b = idx[len(idx) // 2], idx[len(idx) // 2 + 1]
 tot = 0.0
