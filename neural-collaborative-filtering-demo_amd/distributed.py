@@ -188,7 +188,11 @@ class RcclExchange(ShardExchange):
     def exchange(self, t: torch.Tensor, send_splits: List[int], recv_splits: List[int],
                  side: bool = False, slot: Optional[str] = None):
         """``slot``: a grow-only output buffer reused by every call with that name (the caller
-        consumes it in stream order before the next such call), else a fresh tensor."""
+        consumes it in stream order before the next such call), else a fresh tensor.
+        Over one rank the all-to-all is the identity: the input itself is returned (no copy; every
+        caller consumes the output in stream order before it next writes the input)."""
+        if self.world == 1:
+            return t[:send_splits[0]]
         sr, rr = self._sr, self._rr
         for p in range(self.world):
             sr[p], rr[p] = send_splits[p], recv_splits[p]
