@@ -57,6 +57,9 @@ def pmc_traffic(kernel):
                       f"separate passes)"}
 
 
+ISO_STEPS = 40   # steps of the roofline kernel's isolated (sweep not overlapped) measurement
+
+
 def zipf_sampler(n_items, s, device):
     w = 1.0 / torch.arange(1, n_items + 1, dtype=torch.float64) ** s
     cdf = torch.cumsum(w / w.sum(), 0).to(device=device, dtype=torch.float64)
@@ -537,6 +540,27 @@ def main():
     dom_flops = per_sample[dom] * N / max(dom_launches, 1) if dom else 0.0
     dom_tf = dom_flops / (dom_ms * 1e-3) / 1e12 if dom else 0.0
     traffic = pmc_traffic(KERNEL_SYMBOL.get(dom)) if dom else None
+    # The rolling table sweep runs on a side stream beside the backward (deferred.py, overlapped
+    # sweep): the times above are the kernels as they run in the step, sharing the CUs with it.
+    # The dominant kernel alone: a short third region with the sweep back on the step's stream.
+    iso = None
+    dfr0 = getattr(step, "deferred", None)
+    if dom and dfr0 is not None and getattr(dfr0, "overlap", False):
+        dfr0.flush(L.stream_ptr(dev))
+        dfr0.overlap = False
+        L.PROFILE = []
+        run_steps(run, args.warmup + 2 * args.steps, ISO_STEPS)
+        torch.cuda.synchronize()
+        prof2, L.PROFILE = L.PROFILE, None
+        dfr0.overlap = True
+        ds = [e0.elapsed_time(e1) for name, _, e0, e1 in prof2 if name == dom]
+        if ds:
+            iso_ms = sum(ds) / len(ds)
+            iso_tf = dom_flops / (iso_ms * 1e-3) / 1e12
+            iso = {"ms_per_launch": round(iso_ms, 4), "achieved": round(iso_tf, 2),
+                   "frac": round(iso_tf / FP32_MFMA_PEAK_TFS, 4), "steps": ISO_STEPS,
+                   "note": "the same kernel with the rolling sweep on the step's own stream "
+                           "(not overlapped)"}
     # table-update work of the deferred dense-exact Adam: algorithmic = the dense schedule's
     # 24 B per table element per step (what the reference's Adam must move), priced per step
     tab_ms = sum(totals.get(k, 0.0) for k in ("ncf_adam_rows_catchup", "ncf_adam_rows_apply",
@@ -672,7 +696,9 @@ def main():
                          "frac": round(dom_tf / FP32_MFMA_PEAK_TFS, 4),
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
-                         "flops_per_launch": dom_flops, "ms_per_launch": round(dom_ms, 4)},
+                         "flops_per_launch": dom_flops, "ms_per_launch": round(dom_ms, 4),
+                         **({"overlap": "measured in the step, beside the rolling table sweep "
+                                        "on a side stream", "isolated": iso} if iso else {})},
             "mfma_class": {"kernels": "k_attn_block_fwd/bwd + k_mlp_fwd/bwd + k_wgrad_grouped "
                                       "(fp32 MFMA v_mfma_f32_16x16x4_f32 / 32x32x2_f32: every "
                                       "Linear of the step)",
@@ -686,6 +712,9 @@ def main():
             "table_adam": {"kernels": "deferred dense-exact Adam (catch-up + apply + 1/64 sweep)",
                            "ms_per_step": round(tab_ms, 4),
                            "sweep_us_per_step": round(1e3 * sweep_ms, 2),
+                           "sweep_overlapped": bool(dfr is not None and getattr(dfr, "overlap", False)),
+                           "sweep_note": "with sweep_overlapped the sweep's time is its span on the "
+                                         "side stream, beside the backward kernels",
                            "sweep_every": sweep_every,
                            "steps_before_timing": args.warmup,
                            "dense_equivalent_GBps": round(tab_bytes / max(tab_ms * 1e-3, 1e-12) / 1e9, 1),

@@ -19,6 +19,7 @@ contraction-free arithmetic, so the result is bit-identical to the dense sweep (
 work moves from HBM traffic (24 B/element/step) to VALU (~15 flops/element/step, amortised).
 """
 import ctypes
+import os
 import itertools
 
 import numpy as np
@@ -62,16 +63,25 @@ class DeferredTableAdam:
         self._table = torch.zeros(0, dtype=torch.float32, device=dev)
         self._filled = 0
         self._hp_filled = None      # (lr, beta1, beta2) the filled scalars were computed with
-        # Overlapped rolling sweep (clock path, opt-in): the sweep closing step T is launched
-        # during step T+1, after its catch-up (right before its MLP tower), on a side stream, and
-        # joined before step T+1's table apply.  Rows of step T+1's batch are current by then
-        # (stamp >= T) and skipped; every other row of the slice is touched by the sweep alone.
-        # Same arithmetic, bit-identical results.  Off by default: measured on MI355X, the
-        # VALU-bound sweep slows the tower kernels it shares the CUs with by about as much as it
-        # hides (0.366 vs 0.361 ms/step single-GPU, 0.485 vs 0.46 row-sharded).
+        # Overlapped rolling sweep (clock path; FusedTrainStep and the optimizer hook turn it
+        # on): the sweep closing step T is launched during step T+1, after its catch-up, on a
+        # side stream, and joined before step T+1's table apply.  Rows of step T+1's batch are
+        # current by then (stamp >= T) and skipped; every other row of the slice is touched by
+        # the sweep alone.  Same arithmetic, bit-identical results (tested).
         self.overlap = bool(overlap_sweep)
         if self.overlap and clock is None:
             raise ValueError("the overlapped sweep needs the device step clock")
+        # Where the engine forks it ("mlp_bwd": before the MLP tower backward; "tower": before
+        # the tower forward; "attn_bwd", "emb_bwd", "reduce": before those backward launches)
+        # and where the step joins it ("apply": before the table apply; "close": before the
+        # step's last launch, which advances the clock the sweep reads).  Measured at C2 (one
+        # MI355X, ms/step): not overlapped 0.337; forked at tower 0.325, mlp_bwd 0.313-0.317,
+        # attn_bwd 0.327, emb_bwd 0.342, reduce 0.322-0.325 (join point: no difference).  The
+        # VALU-bound replay fills the issue slots the latency-bound tower and attention
+        # backward leave idle (it stretches k_mlp_bwd from 80 to ~92 us and itself from 50
+        # to ~96 us, both off the critical path's sum).
+        self.fork_at = os.environ.get("NCF_SWEEP_FORK", "mlp_bwd")
+        self.join_at = os.environ.get("NCF_SWEEP_JOIN", "apply")
         self._owed = False        # a closed step whose rolling sweep has not been launched
         self._side = None
         self._ev = None
@@ -325,7 +335,8 @@ class DeferredTableAdam:
         n = w.g.n
         if self.clock is not None:
             self._ensure(self.t + 1)
-            self.sweep_join()
+            if self.join_at == "apply" or self._early_ev is not None:
+                self.sweep_join()
             self.early_join()   # (before the sweep, which may reach the same rows)
             if n > 0:
                 pairs = self._pairs_for(w)

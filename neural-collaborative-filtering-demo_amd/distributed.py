@@ -325,7 +325,9 @@ class HipShardOps:
         self.base_seed = random.getrandbits(62)
         self.clock = torch.tensor([0, self.base_seed], dtype=torch.int64, device=self.dev)
         self.deferred = DeferredTableAdam(self.eng, lr, betas, eps, weight_decay, sweep_every,
-                                          clock=self.clock)
+                                          clock=self.clock,
+                                          overlap_sweep=os.environ.get("NCF_SHARD_OVERLAP_SWEEP",
+                                                                       "0") != "0")
         self.m_flat = torch.zeros_like(self.eng.flat)
         self.v_flat = torch.zeros_like(self.eng.flat)
         self.step_count = 0

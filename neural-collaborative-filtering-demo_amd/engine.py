@@ -426,10 +426,8 @@ class NCFEngine:
             x, ldx, kin = w.y, D, D
         else:
             x, ldx, kin = self._attention_unfused(w, M, train, drop_p, seed, temporal, st)
-        if train and self.deferred is not None and self.deferred.overlap:
-            # the previous step's rolling table sweep (VALU-bound) runs on a side stream under
-            # the MFMA-bound tower forward/backward (joined before this step's table apply)
-            self.deferred.sweep_fork()
+        if train:
+            self._sweep_fork("tower")
         if temporal is None and self.mlp_fused(D, hid):
             # a7 + a8: the whole tower and the head in one launch (mlp_tower.hip)
             _, addr, _, haddr = self._mlp_layers(w, train, bwd=False)
@@ -607,6 +605,13 @@ class NCFEngine:
         a["pending"] = True
 
     # ------------------------------------------------------------------ backward
+    def _sweep_fork(self, at: str):
+        """Launch the previous step's owed rolling sweep on its side stream when the overlapped
+        sweep is on and `at` is its fork point (DeferredTableAdam.fork_at)."""
+        d = self.deferred
+        if d is not None and d.overlap and d.fork_at == at:
+            d.sweep_fork()
+
     def backward(self, w: Workspace, uid, iid, grad_prob: Optional[torch.Tensor],
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,
                  loss_denominator: float = 0.0, tables=None, rows=None, uniq=None,
@@ -641,6 +646,7 @@ class NCFEngine:
                       float(loss_denominator), ptr(w.site("head")), w.site("head").numel(),
                       w.red_list.address, st)
         # a7 backward, last layer first
+        self._sweep_fork("mlp_bwd")
         if fused:   # head + relu/LN/dropout backward + dX of all layers in one launch
             _, addr, _, haddr = self._mlp_layers(w, True, bwd=True)
             h = w.cache.get("head_args")
@@ -699,6 +705,7 @@ class NCFEngine:
                 dx = w.dy if l == 0 else w.da[l - 1]
                 self._gemm(w.dlin[l], h, 0, lin.weight, ldw, 0, dx, kin, n, kin, h, st=st)
         # a5 backward: out_proj, core, q/k/v projections
+        self._sweep_fork("attn_bwd")
         pp = self.pp()
         if self.attn_block(D, H, M):
             # core + projections backward and the four Linear gradients in one launch
@@ -725,6 +732,7 @@ class NCFEngine:
         else:
             self._attention_bwd_unfused(w, drop_p, seed, joins, st)
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)
+        self._sweep_fork("emb_bwd")
         if tables is None:
             tbp = (pp["t_mf_user"], pp["t_mlp_user"], pp["t_mf_item"], pp["t_mlp_item"])
         else:
@@ -747,6 +755,7 @@ class NCFEngine:
                   self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
                   w.emb_ws.numel(), w.red_list.address, st)
         self.join(dev, joins)
+        self._sweep_fork("reduce")
         if reduce_async:
             if getattr(self, "_red_side", None) is None:
                 self._red_side = torch.cuda.Stream(dev)

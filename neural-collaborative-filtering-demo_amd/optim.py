@@ -26,6 +26,7 @@ torch's own step (so torch's loop never sees them) and put back afterwards.
 other than plain Adam (amsgrad, maximize, capturable, differentiable, tensor lr, other classes)
 receive materialised dense table gradients and run unchanged.
 """
+import os
 import weakref
 
 import torch
@@ -130,7 +131,8 @@ class _Binding:
         self.D = None
         if SCHEDULE == "deferred":
             self.D = DeferredTableAdam(eng, lr, betas, eps, wd, SWEEP_EVERY,
-                                       moments=self.moments, clock=self.clock)
+                                       moments=self.moments, clock=self.clock,
+                                       overlap_sweep=os.environ.get("NCF_OVERLAP_SWEEP", "1") != "0")
             eng.clock = self.clock
         self.adopt(opt)
 

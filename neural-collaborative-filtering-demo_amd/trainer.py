@@ -42,7 +42,7 @@ class FusedTrainStep:
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5,
                  deferred: bool = True, sweep_every: int = 64, graph: bool = False,
                  clock: Optional[bool] = None, warmup: int = 2, concurrent: Optional[bool] = None,
-                 overlap_sweep: bool = False, table_dtype: torch.dtype = torch.float32):
+                 overlap_sweep: Optional[bool] = None, table_dtype: torch.dtype = torch.float32):
         self.model = model
         self.deferred = None
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
@@ -89,6 +89,8 @@ class FusedTrainStep:
             self.clock = torch.tensor([0, self.base_seed], dtype=torch.int64, device=dev)
             eng.clock = self.clock
         self.deferred = None
+        if overlap_sweep is None:    # the overlapped rolling sweep (deferred.py): on by default
+            overlap_sweep = os.environ.get("NCF_OVERLAP_SWEEP", "1") != "0"
         if deferred:
             from .deferred import DeferredTableAdam
             self.deferred = DeferredTableAdam(eng, lr, betas, eps, weight_decay, sweep_every,
@@ -151,6 +153,8 @@ class FusedTrainStep:
             eng.adam_tables(hp, lambda p: self.state[key_of[id(p)]], float(self.step_count + 1), st)
         eng.join_reductions()
         if self.clock is not None:
+            if self.deferred is not None:
+                self.deferred.sweep_join()   # (the clock advance below changes its target)
             _lib.call("ncf_adam_flat_clock_close", ptr(eng.flat), ptr(eng.flat_grad),
                       ptr(self.m_flat), ptr(self.v_flat), eng.flat.numel(),
                       ptr(self.deferred._table), 1, ptr(self.clock), b1, b2, self.eps, self.wd,
