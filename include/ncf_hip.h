@@ -647,6 +647,13 @@ int ncf_adam_pairs_sweep_rolling(const ncf_table_pair* pairs, int npairs, int64_
                                  const ncf_step_clock* clock, const float* step_table,
                                  double beta1, double beta2, double eps, double weight_decay,
                                  void* stream);
+/* Part `part` of `nparts` (consecutive row ranges) of that slice: the parts of one step may run at
+ * different points of it, on any stream, before the clock advances (the overlapped sweep). */
+int ncf_adam_pairs_sweep_rolling_part(const ncf_table_pair* pairs, int npairs, int64_t dim,
+                                      int32_t sweep_every, int32_t step_rel, int32_t part,
+                                      int32_t nparts, const ncf_step_clock* clock,
+                                      const float* step_table, double beta1, double beta2,
+                                      double eps, double weight_decay, void* stream);
 /* bf16 parameter rows (C2 "bf16": tables bf16, Adam moments fp32): ncf_adam_table and
  * ncf_adam_sweep with the parameter rounded to bf16 after every step.                        */
 int ncf_adam_table_bf16(uint16_t* param, float* exp_avg, float* exp_avg_sq, int64_t rows,

@@ -450,18 +450,22 @@ __global__ __launch_bounds__(256) void k_pairs_apply(const PairArgs a, const uin
   if (sub == 0) a.stamp[k][row] = step;
 }
 
+// part `part` of `nparts` (consecutive row ranges) of the slice of step clock->t + step_rel
 template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void k_pairs_sweep(const PairArgs a, int32_t every,
                                                      int32_t step_rel,
                                                      const ncf_step_clock* __restrict__ clock,
-                                                     const float* __restrict__ table, AdamScalars s) {
+                                                     const float* __restrict__ table, AdamScalars s,
+                                                     int part, int nparts) {
   constexpr int L = Replay<D>::LPR;   // lanes per row
   const int k = blockIdx.y;
   const int32_t target = clock->t + step_rel;
   const int64_t total = a.rows[k];
   const int64_t slice = (total + every - 1) / every;
-  const int64_t row0 = (int64_t)(target % every) * slice;
-  const int64_t rows = max((int64_t)0, min(slice, total - row0));
+  const int64_t s0 = (int64_t)(target % every) * slice;
+  const int64_t srows = max((int64_t)0, min(slice, total - s0));
+  const int64_t row0 = s0 + srows * part / nparts;
+  const int64_t rows = s0 + srows * (part + 1) / nparts - row0;
   const int64_t n = rows * L;
   int32_t* stamp = a.stamp[k];
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
@@ -708,13 +712,14 @@ int pairs_apply_d(PairArgs a, int n, const uint32_t* count, int64_t max_n, int32
 
 template <int D>
 int pairs_sweep_d(PairArgs a, int n, int32_t every, int32_t rel, const ncf_step_clock* clock,
-                  const float* table, AdamScalars s, hipStream_t st) {
+                  const float* table, AdamScalars s, hipStream_t st, int part = 0, int nparts = 1) {
   int64_t slice = 0;
   for (int k = 0; k < n; ++k) slice = max(slice, (a.rows[k] + every - 1) / every);
+  slice = (slice + nparts - 1) / nparts;
   if (a.bf)
-    hipLaunchKernelGGL((k_pairs_sweep<D, true>), dim3(grid_for(slice * Replay<D>::LPR), n), dim3(256), 0, st, a, every, rel, clock, table, s);
+    hipLaunchKernelGGL((k_pairs_sweep<D, true>), dim3(grid_for(slice * Replay<D>::LPR), n), dim3(256), 0, st, a, every, rel, clock, table, s, part, nparts);
   else
-    hipLaunchKernelGGL((k_pairs_sweep<D, false>), dim3(grid_for(slice * Replay<D>::LPR), n), dim3(256), 0, st, a, every, rel, clock, table, s);
+    hipLaunchKernelGGL((k_pairs_sweep<D, false>), dim3(grid_for(slice * Replay<D>::LPR), n), dim3(256), 0, st, a, every, rel, clock, table, s, part, nparts);
   NCF_CHECK_LAUNCH("ncf_adam_pairs_sweep_rolling");
   return NCF_OK;
 }
@@ -951,4 +956,21 @@ extern "C" int ncf_adam_pairs_sweep_rolling(const ncf_table_pair* pairs, int npa
   NCF_DISPATCH_DIM(dim, pairs_sweep_d, pair_args(pairs, npairs), npairs, sweep_every, step_rel,
                    clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
                    (hipStream_t)stream);
+}
+
+// One of `nparts` consecutive row ranges of that slice (both kinds): the parts of a step can run
+// at different points of it (the overlapped sweep, deferred.py); together they are the slice.
+extern "C" int ncf_adam_pairs_sweep_rolling_part(const ncf_table_pair* pairs, int npairs,
+                                                 int64_t dim, int32_t sweep_every, int32_t step_rel,
+                                                 int32_t part, int32_t nparts,
+                                                 const ncf_step_clock* clock,
+                                                 const float* step_table, double beta1,
+                                                 double beta2, double eps, double weight_decay,
+                                                 void* stream) {
+  NCF_CHECK_ARG(pairs && npairs >= 1 && npairs <= 2 && clock && step_table && sweep_every >= 1 &&
+                    nparts >= 1 && part >= 0 && part < nparts,
+                "ncf_adam_pairs_sweep_rolling_part: bad args");
+  NCF_DISPATCH_DIM(dim, pairs_sweep_d, pair_args(pairs, npairs), npairs, sweep_every, step_rel,
+                   clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
+                   (hipStream_t)stream, part, nparts);
 }

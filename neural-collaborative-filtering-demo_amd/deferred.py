@@ -80,9 +80,11 @@ class DeferredTableAdam:
         # VALU-bound replay fills the issue slots the latency-bound tower and attention
         # backward leave idle (it stretches k_mlp_bwd from 80 to ~92 us and itself from 50
         # to ~96 us, both off the critical path's sum).
-        self.fork_at = os.environ.get("NCF_SWEEP_FORK", "mlp_bwd")
+        # Several comma-separated fork points split the slice into that many consecutive row
+        # ranges, one launched at each (ncf_adam_pairs_sweep_rolling_part).
+        self.fork_points = os.environ.get("NCF_SWEEP_FORK", "mlp_bwd").split(",")
         self.join_at = os.environ.get("NCF_SWEEP_JOIN", "apply")
-        self._owed = False        # a closed step whose rolling sweep has not been launched
+        self._owed = []           # parts of a closed step's rolling sweep not launched yet
         self._side = None
         self._ev = None
         self._joined = True
@@ -143,7 +145,7 @@ class DeferredTableAdam:
         self.t = self.synced_t = int(t)
         for stamp in self.stamp.values():
             stamp.fill_(int(t))
-        self._owed, self._joined = False, True
+        self._owed, self._joined = [], True
 
     def rebind_moments(self, moments):
         """Use other exp_avg / exp_avg_sq tensors (e.g. after an optimizer state load)."""
@@ -214,7 +216,7 @@ class DeferredTableAdam:
         self.t += 1
         self.engine.pending = None
         if self.sweep_every and self.clock is not None and self.overlap:
-            self._owed = True
+            self._owed = list(range(len(self.fork_points)))
         elif self.sweep_every and self.clock is not None:
             self._rolling(st, 1)
         elif self.sweep_every:
@@ -225,19 +227,29 @@ class DeferredTableAdam:
                 r0 = k * sl
                 self._sweep_range(kind, r0, max(0, min(rows, r0 + sl) - r0), st)
 
-    def _rolling(self, st, step_rel):
-        """Rolling sweep closing step clock->t + step_rel (slice of that step)."""
+    def _rolling(self, st, step_rel, part=0, nparts=1):
+        """Rolling sweep closing step clock->t + step_rel (slice of that step; part `part` of
+        `nparts` consecutive row ranges of it)."""
         pairs = self.__dict__.get("_sweep_pairs") or self.__dict__.setdefault("_sweep_pairs",
                                                                                self._pairs())
-        _lib.call("ncf_adam_pairs_sweep_rolling", ctypes.addressof(pairs), 2,
-                  self.engine.model.mlp_embedding_dim, self.sweep_every, step_rel,
-                  ptr(self.clock), ptr(self._table), *self._consts(), st)
+        D = self.engine.model.mlp_embedding_dim
+        if nparts == 1:
+            _lib.call("ncf_adam_pairs_sweep_rolling", ctypes.addressof(pairs), 2, D,
+                      self.sweep_every, step_rel, ptr(self.clock), ptr(self._table),
+                      *self._consts(), st)
+        else:
+            _lib.call("ncf_adam_pairs_sweep_rolling_part", ctypes.addressof(pairs), 2, D,
+                      self.sweep_every, step_rel, part, nparts, ptr(self.clock), ptr(self._table),
+                      *self._consts(), st)
 
-    def sweep_fork(self):
-        """During step T+1 (clock->t = T, after its catch-up; the engine forks right before the
-        MLP tower): launch the owed sweep of step T on the side stream; it overlaps everything
-        the current stream does until sweep_join."""
-        if not self._owed:
+    def sweep_fork(self, at="mlp_bwd"):
+        """During step T+1 (clock->t = T, after its catch-up), at the engine's fork point `at`:
+        launch the part of the owed sweep of step T registered there on the side stream; it
+        overlaps everything the current stream does until sweep_join."""
+        if at not in self.fork_points:
+            return
+        part = self.fork_points.index(at)
+        if part not in self._owed:
             return
         dev = self.clock.device
         if self._side is None:
@@ -247,9 +259,10 @@ class DeferredTableAdam:
         self._ev[0].record(cur)
         self._side.wait_event(self._ev[0])
         with torch.cuda.stream(self._side):     # (so per-launch instrumentation times it there)
-            self._rolling(self._side.cuda_stream, 0)
+            self._rolling(self._side.cuda_stream, 0, part, len(self.fork_points))
         self._ev[1].record(self._side)
-        self._owed, self._joined = False, False
+        self._owed.remove(part)
+        self._joined = False
 
     def sweep_join(self):
         """The current stream waits for the side-stream sweep (before the step's apply and the
@@ -258,13 +271,18 @@ class DeferredTableAdam:
             torch.cuda.current_stream(self.clock.device).wait_event(self._ev[1])
             self._joined = True
 
+    def _settle(self, st):
+        """Parts of the owed sweep whose fork point this step did not pass: on stream st, now
+        (before the step's apply closes the next step)."""
+        for part in self._owed:
+            self._rolling(st, 0, part, len(self.fork_points))
+        self._owed = []
+
     def flush(self, st):
         """Settle any owed / in-flight sweep on the current stream (before full sweeps or
         anything that reads the tables from the host side)."""
         self.sweep_join()
-        if self._owed:
-            self._rolling(st, 0)
-            self._owed = False
+        self._settle(st)
 
     def _pairs(self, w=None):
         """ncf_table_pair[2] (users, items) for the both-kinds launches of the clock path."""
@@ -337,6 +355,7 @@ class DeferredTableAdam:
             self._ensure(self.t + 1)
             if self.join_at == "apply" or self._early_ev is not None:
                 self.sweep_join()
+            self._settle(st)
             self.early_join()   # (before the sweep, which may reach the same rows)
             if n > 0:
                 pairs = self._pairs_for(w)

@@ -526,6 +526,7 @@ class HipShardOps:
         d = self.deferred
         d._ensure(d.t + 1)
         d.sweep_join()
+        d._settle(st)
         if nmax > 0:
             pairs = self._pairs(uq, G)
             _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2, self.D,

@@ -607,10 +607,10 @@ class NCFEngine:
     # ------------------------------------------------------------------ backward
     def _sweep_fork(self, at: str):
         """Launch the previous step's owed rolling sweep on its side stream when the overlapped
-        sweep is on and `at` is its fork point (DeferredTableAdam.fork_at)."""
+        sweep is on and `at` is one of its fork points (DeferredTableAdam.fork_points)."""
         d = self.deferred
-        if d is not None and d.overlap and d.fork_at == at:
-            d.sweep_fork()
+        if d is not None and d.overlap:
+            d.sweep_fork(at)
 
     def backward(self, w: Workspace, uid, iid, grad_prob: Optional[torch.Tensor],
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,

@@ -702,12 +702,21 @@ def test_early_catchup_bitwise_equals_dense(monkeypatch, sweep_every):
     assert int(max(st["user"].max(), st["item"].max())) < (1 << 30)   # no lock left behind
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_overlapped_sweep_bitwise_equals_dense(graph):
-    """The opt-in overlapped rolling sweep (side stream under the tower, joined before the
-    apply) is bit-identical to the dense sweep, eager and hipGraph-captured."""
+@pytest.mark.parametrize("graph,fork,join", [(False, "mlp_bwd", "apply"), (True, "mlp_bwd", "apply"),
+                                             (False, "tower,mlp_bwd,reduce", "close"),
+                                             (True, "tower,attn_bwd", "apply"),
+                                             (False, "emb_bwd,nowhere", "apply"),
+                                             (False, "off", "apply")])
+def test_overlapped_sweep_bitwise_equals_dense(monkeypatch, graph, fork, join):
+    """The overlapped rolling sweep (side stream; the default fork point is the tower
+    backward, joined before the apply; or split into consecutive parts forked at several points
+    (ncf_adam_pairs_sweep_rolling_part), a part whose fork point the step never passes settled
+    before the apply; or joined only before the clock advance) is bit-identical to the dense
+    sweep, eager and hipGraph-captured ("off": the sweep on the step's own stream)."""
+    monkeypatch.setenv("NCF_SWEEP_FORK", fork)
+    monkeypatch.setenv("NCF_SWEEP_JOIN", join)
     a_sd, a_m = _fused_run(False, 70)
-    b_sd, b_m = _fused_run(True, 70, clock=True, graph=graph, overlap_sweep=True)
+    b_sd, b_m = _fused_run(True, 70, clock=True, graph=graph, overlap_sweep=fork != "off")
     for k in a_sd:
         assert torch.equal(a_sd[k], b_sd[k]), k
     for k in a_m:

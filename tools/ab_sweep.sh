@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B the overlapped rolling sweep's fork/join points on the C2 step (tools/kernel_ab.py):
-#   bash tools/ab_sweep.sh "off" "tower:apply" "emb_bwd:close" ...   (2 rounds)
+#   bash tools/ab_sweep.sh off "mlp_bwd:apply" "tower,mlp_bwd:apply" ...   (2 rounds)
+# (fork points before the colon, comma-separated: one part of the slice per point)
 for rep in 1 2; do
   for cfg in "$@"; do
     if [ "$cfg" = off ]; then
