@@ -150,6 +150,7 @@ class NCFEngine:
 
     def __init__(self, model):
         self.model = model
+        self.fork_hook = None     # callable(at): side-stream work the caller forks at that point
         self.ws: Dict[tuple, Workspace] = {}
         self.flat = None
         self.flat_grad = None
@@ -611,6 +612,9 @@ class NCFEngine:
         d = self.deferred
         if d is not None and d.overlap:
             d.sweep_fork(at)
+        hook = self.fork_hook
+        if hook is not None:
+            hook(at)
 
     def backward(self, w: Workspace, uid, iid, grad_prob: Optional[torch.Tensor],
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,

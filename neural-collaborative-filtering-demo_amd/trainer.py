@@ -24,6 +24,14 @@ from ._lib import ptr
 log = logging.getLogger(__name__)
 
 
+# Where the next batch's id sort is launched on the side stream: "entry" (the step's start) or
+# one of the engine's fork points ("tower", "mlp_bwd", "attn_bwd", "emb_bwd", "reduce").
+# Measured at C2 with the rolling sweep forked at mlp_bwd (ms/step): entry 0.319-0.321, tower
+# 0.325, mlp_bwd 0.341, attn_bwd 0.312-0.314, emb_bwd 0.318-0.319, reduce 0.332-0.334: beside the
+# attention / embedding backward, after the sweep has taken the tower backward's idle slots.
+DEDUP_FORK = os.environ.get("NCF_DEDUP_FORK", "attn_bwd")
+
+
 class FusedTrainStep:
     """forward + BCE + backward + Adam for one batch, on the current HIP stream, no host sync.
 
@@ -235,8 +243,20 @@ class FusedTrainStep:
                 entry.record()
                 self._activate_dedup(w0, user_ids, item_ids)
                 if next is not None and next[0].numel() == user_ids.numel():
-                    self._prefetch_dedup(w0, next[0], next[1], entry)
+                    if DEDUP_FORK == "entry":
+                        self._prefetch_dedup(w0, next[0], next[1], entry)
+                    else:   # launched from the engine's fork point DEDUP_FORK of this step
+                        pre = (w0, next[0], next[1])
+
+                        def hook(at, pre=pre):
+                            if at == DEDUP_FORK and eng.fork_hook is hook:
+                                eng.fork_hook = None
+                                ev = torch.cuda.Event()
+                                ev.record()
+                                self._prefetch_dedup(pre[0], pre[1], pre[2], ev)
+                        eng.fork_hook = hook
             w = self._body(user_ids, item_ids, targets, M)
+            m.engine.fork_hook = None     # (a fork point the step did not pass: no prefetch)
             self.step_count += 1
             m.engine.updates += 1
             self.last_loss = w.loss
