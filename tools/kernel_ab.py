@@ -36,6 +36,7 @@ def main():
     U, I, B, M = 1_000_000, 100_000, 4096, 5
     m = ncf.AdvancedNCF(U, I, 10, 50, 64, 64, 32, [256, 128, 64], 4, 0.2, 4).to(dev).train()
     step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5,
+                          sweep_every=int(os.environ.get("AB_SWEEP_EVERY", "64")),
                           table_dtype=torch.bfloat16 if a.bf16 else torch.float32)
     batches = make_batches(U, I, B, M, 8, dev, seed=100)
 
