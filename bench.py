@@ -31,6 +31,7 @@ import _ncf_pkg  # noqa: E402
 METRIC = "train samples/sec + infer pairs/sec, 1M×100K d=64 AdvancedNCF @1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA = the f32 vector rate
+BF16_MFMA_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 
 
 # C-ABI entry point -> the kernel symbol rocprofv3 reports for it
@@ -306,7 +307,7 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
     max over ranks."""
     import ncf_amd
     from ncf_amd import _lib as L
-    from ncf_amd.scoring import ItemIndex, shard_items, sharded_score_topk
+    from ncf_amd.scoring import SPLIT_SCAN, ItemIndex, shard_items, sharded_score_topk
     torch.manual_seed(4321)
     m = ncf_amd.AdvancedNCF(n_users, n_items, 10, 50).to(dev).eval()
     users = torch.randperm(n_users, device=dev)[:n_query]
@@ -333,7 +334,9 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
         return dt
 
     out = {"config": f"{n_query} users x {n_items} items (model {n_users} x {n_items}, D=64), "
-                     "top-K over the whole catalogue, factorised fp32 MFMA scan, hipGraph-captured"
+                     "top-K over the whole catalogue, factorised fp32-accurate MFMA scan "
+                     + ("(bf16 matrix cores, 3-term operand split)" if SPLIT_SCAN else "(fp32 MFMA)")
+                     + ", hipGraph-captured"
                      + (f", item-sharded over {world} GPUs (all-gather + merge)" if world > 1 else ""),
            "scaling": "strong", "n_gpus": world, "item_index_ms": round(index_ms, 3)}
     for k in ks:
@@ -353,16 +356,26 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
             if dt < eager:
                 eager, prof = dt, L.PROFILE
             L.PROFILE = None
-        coll = sum(e0.elapsed_time(e1) for name, _, e0, e1 in prof if name == "ncf_score_collect")
-        flops = 2.0 * 64 * n_query * n_local
-        tf = flops / (coll * 1e-3) / 1e12
+        kname = "ncf_score_collect_split" if SPLIT_SCAN else "ncf_score_collect"
+        coll = sum(e0.elapsed_time(e1) for name, _, e0, e1 in prof if name == kname)
+        algo_tf = 2.0 * 64 * n_query * n_local / (coll * 1e-3) / 1e12   # 128 flop per pair
+        if SPLIT_SCAN:
+            # executed matrix work: six bf16 products of the 3-term operand splits per pair
+            tf, peak = 6 * algo_tf, BF16_MFMA_PEAK_TFS
+            kdesc = "k_collect3 (v_mfma_f32_32x32x16_bf16, 6 split products per pair)"
+        else:
+            tf, peak = algo_tf, FP32_MFMA_PEAK_TFS
+            kdesc = "k_collect (v_mfma_f32_32x32x2_f32)"
         out[f"k{k}"] = {"ms": round(best * 1e3, 3), "pairs_per_s": round(n_query * n_items / best, 1),
                         "launch": "hipGraph replay (GraphedScorer)",
                         "eager_ms": round(eager * 1e3, 3), "collect_ms": round(coll, 3),
-                        "roofline": {"bound": "mfma", "kernel": "k_collect (v_mfma_f32_32x32x2_f32)",
-                                     "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFS,
-                                     "unit": "TFLOP/s", "frac": round(tf / FP32_MFMA_PEAK_TFS, 4),
-                                     "flops_per_pair": 128}}
+                        "roofline": {"bound": "mfma", "kernel": kdesc,
+                                     "achieved": round(tf, 2), "peak": peak,
+                                     "unit": "TFLOP/s", "frac": round(tf / peak, 4),
+                                     "flops_per_pair": 768 if SPLIT_SCAN else 128,
+                                     "algorithmic_tflops": round(algo_tf, 2),
+                                     "algorithmic_frac_of_fp32_peak":
+                                         round(algo_tf / FP32_MFMA_PEAK_TFS, 4)}}
     if cpu_budget > 0 and rank == 0 and world == 1:
         from oracle import ncf_oracle as O
         p = {k: v.detach().cpu() for k, v in m.state_dict().items()}

@@ -466,6 +466,17 @@ int ncf_score_collect(const float* queries, const int32_t* user_list, int64_t n_
                       const float* items, const float* item_bias, int64_t n_items, int64_t dim,
                       const float* thr, int64_t cap, uint32_t* count, float* cand_logit,
                       int32_t* cand_item, void* stream);
+/* ncf_score_collect on the bf16 matrix cores at fp32 accuracy: every operand split into three
+ * bf16 terms (24 significant bits), six products per logit accumulated in fp32.  items3: the
+ * three bf16 planes [3][n_items][dim] of `items` (ncf_score_split_items).  Same candidate sets
+ * (the logits differ from the fp32 scan's by accumulation rounding only, far inside the
+ * threshold's margin). */
+int ncf_score_split_items(const float* items, int64_t n_items, int64_t dim, uint16_t* items3,
+                          void* stream);
+int ncf_score_collect_split(const float* queries, const int32_t* user_list, int64_t n_users,
+                            const uint16_t* items3, const float* item_bias, int64_t n_items,
+                            int64_t dim, const float* thr, int64_t cap, uint32_t* count,
+                            float* cand_logit, int32_t* cand_item, void* stream);
 int ncf_score_select(const int32_t* user_list, int64_t n_users, const uint32_t* count,
                      const float* cand_logit, const int32_t* cand_item, int64_t cap, int K,
                      float* out_score, int64_t* out_item, float* thr, uint32_t* overflow,

@@ -28,6 +28,8 @@
 // and flushed to the global per-user lists in parallel bursts: a global atomic per hit made the
 // wave wait thousands of cycles in nearly every tile (17.1 -> 14.7 ms at C5 top-10).
 #include "ncf_common.h"
+#include <algorithm>
+#include <type_traits>
 
 namespace {
 
@@ -286,6 +288,222 @@ __global__ __launch_bounds__(512) void k_collect(
   flush(ccount);
 }
 
+// ---- 3'. the same scan on bf16 matrix cores with fp32 accuracy.  Every operand is split into
+// three bf16 terms, x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1):
+// 24 significant bits, the fp32 significand), and a logit is the fp32 accumulation of the six
+// products whose order is >= 2^-24 relative, a0 b0 + a0 b1 + a1 b0 + a0 b2 + a1 b1 + a2 b0
+// (v_mfma_f32_32x32x16_bf16: each bf16 x bf16 product is exact in fp32).  The dropped terms are
+// below 2^-26 of a product, so a logit differs from the fp32 MFMA scan's by fp32 rounding of
+// the accumulation only — far inside the threshold's 1e-4 relative margin (k_kth), so the
+// candidate set is unchanged.  6 bf16 MFMAs (32 cycles each) replace 32 fp32 ones (64 cycles)
+// per 32 x 32 x 64 tile.  The item rows are split once per index (k_split3: three bf16 planes).
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(float x, __bf16& x0, __bf16& x1, __bf16& x2) {
+  x0 = (__bf16)x;
+  const float r1 = x - (float)x0;
+  x1 = (__bf16)r1;
+  x2 = (__bf16)(r1 - (float)x1);
+}
+
+__global__ void k_split3(const float* __restrict__ p, int64_t n, uint16_t* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  __bf16 x0, x1, x2;
+  split3(p[e], x0, x1, x2);
+  out[e] = __builtin_bit_cast(uint16_t, x0);
+  out[n + e] = __builtin_bit_cast(uint16_t, x1);
+  out[2 * n + e] = __builtin_bit_cast(uint16_t, x2);
+}
+
+constexpr int kP3 = 72;        // LDS pitch of a staged bf16 item row (64 + 8)
+constexpr int kSlice3 = 256;   // candidates staged per wave (its own LDS slice: no atomics)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// One workgroup = 8 waves x 32 users (two waves per SIMD) scanning one item split in 32-item
+// tiles.  Per tile, a wave runs 4 steps x 6 bf16 MFMAs into one 32 x 32 accumulator, then
+// filters it against its users' thresholds.  Three LDS tile buffers and one barrier per tile; the
+// B operands of tile t + 1 are read from LDS while tile t is multiplied.  Hits go to the wave's
+// own LDS slice (offsets from ballots, no atomics) and the wave writes its slice to the global
+// lists itself when it fills (no workgroup barrier).
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_collect3(
+    const float* __restrict__ q, const int32_t* __restrict__ user_list, int64_t n_users,
+    const uint16_t* __restrict__ items3, const float* __restrict__ bias, int64_t n_items,
+    int64_t items_per_block, int ub, const float* __restrict__ thr, int64_t cap,
+    uint32_t* __restrict__ count, float* __restrict__ cand_logit,
+    int32_t* __restrict__ cand_item) {
+  constexpr int D = 64;
+  __shared__ __attribute__((aligned(16))) uint16_t ps[3][3][kItemTile][kP3];
+  __shared__ float bs[3][kItemTile];
+  __shared__ float cl[8 * kSlice3];
+  __shared__ int32_t ci[8 * kSlice3], cu[8 * kSlice3];
+  const int bx = (int)(blockIdx.x / ub), by = (int)(blockIdx.x % ub);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int64_t slot0 = (int64_t)by * 256 + w * 32;
+  const int64_t my_slot = slot0 + i;
+  const int64_t my_user = my_slot < n_users ? (user_list ? user_list[my_slot] : my_slot) : 0;
+  // this lane's query values q[user][32h + 8t + j] split into three bf16 terms, per MFMA step t
+  bf16x8_t a0[4], a1[4], a2[4];
+  {
+    const float* qp = q + my_user * D + 32 * h;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float4 x = ld4(qp + 8 * t), y = ld4(qp + 8 * t + 4);
+      const float v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        __bf16 b0, b1, b2;
+        split3(v[j], b0, b1, b2);
+        a0[t][j] = b0; a1[t][j] = b1; a2[t][j] = b2;
+      }
+    }
+  }
+  // thresholds of the 16 users whose logits this lane holds: row (r&3) + 8(r>>2) + 4h (their
+  // user ids are looked up again on a hit only: 32 fewer live registers in the loop)
+  auto user_of = [&](int r) -> int64_t {
+    const int64_t s = slot0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    return user_list ? (int64_t)user_list[s] : s;
+  };
+  float th[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t s = slot0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    th[r] = s < n_users ? thr[user_of(r)] : INFINITY;
+  }
+  const int64_t it0 = (int64_t)bx * items_per_block;
+  const int64_t it1 = min(n_items, it0 + items_per_block);
+  // staging: thread (item sj, column group sk) holds 4 bf16 of each of the 3 planes of the next
+  // tile to store (a one-tile register ring: its load has a whole tile to land)
+  const int sj = tid >> 4, sk = (tid & 15) * 4;
+  uint2 pv[3];
+  float pb = 0.f;
+  auto fetch = [&](int64_t t0) {
+    const int64_t item = t0 + sj;
+    const int64_t src = item < it1 ? item : it0;  // clamped, unconditional
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      pv[pl] = *reinterpret_cast<const uint2*>(items3 + (int64_t)pl * n_items * D + src * D + sk);
+    pb = bias[src];
+  };
+  auto put = [&](int bb) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint2*>(&ps[bb][pl][sj][sk]) = pv[pl];
+    if (sk == 0) bs[bb][sj] = pb;
+  };
+  bf16x8_t bq[4][3];   // B operands of the tile being multiplied
+  auto rd = [&](int bb, int t) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      bq[t][pl] = *reinterpret_cast<const bf16x8_t*>(&ps[bb][pl][i][32 * h + 8 * t]);
+  };
+  // the wave's candidate slice: staged entries (wave-uniform), written out when it would overflow
+  float* wl = cl + w * kSlice3;
+  int32_t* wi = ci + w * kSlice3;
+  int32_t* wu = cu + w * kSlice3;
+  uint32_t staged = 0;
+  auto emit = [&](int64_t u, float lg, int32_t item) {
+    const uint32_t pos = atomicAdd(&count[u], 1u);
+    if (pos < cap) {
+      cand_logit[u * cap + pos] = lg;
+      cand_item[u * cap + pos] = item;
+    }
+  };
+  auto wflush = [&]() {
+    for (uint32_t e = lane; e < staged; e += 64) emit(wu[e], wl[e], wi[e]);
+    staged = 0;
+  };
+  auto filt = [&](const f32x16& acc, int bb, int64_t t0) {
+    const int32_t item = (int32_t)(t0 + i);
+    const float b = bs[bb][i];
+    const bool ivalid = t0 + i < it1;
+    // Cheap reject first: max_r (acc[r] - th[r]) + b on packed fp32 (8 v_pk_add + 8 max).  The
+    // margin keeps every lane the exact test below could accept (they round differently by at
+    // most an ulp of |b|; the subtraction near a hit is exact, Sterbenz).
+    {
+      f32x2 m2 = {-INFINITY, -INFINITY};
+#pragma unroll
+      for (int r = 0; r < 16; r += 2)
+        m2 = __builtin_elementwise_max(m2, f32x2{acc[r], acc[r + 1]} - f32x2{th[r], th[r + 1]});
+      const bool near = ivalid && fmaxf(m2.x, m2.y) + b >= -1e-6f * fabsf(b);
+      if (!__ballot(near)) return;
+    }
+    // exact hits, one wave mask per user row; slice offsets from popcounts and mbcnt
+    uint64_t hit[16];
+    uint32_t total = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      hit[r] = __ballot(ivalid && acc[r] + b >= th[r]);
+      total += (uint32_t)__popcll(hit[r]);
+    }
+    if (total == 0) return;
+    if (staged + total > (uint32_t)kSlice3) wflush();
+    const bool direct = total > (uint32_t)kSlice3;   // (a tile of > 256 hits: straight out)
+    uint32_t base = staged;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (hit[r] == 0) continue;   // wave-uniform
+      if ((hit[r] >> lane) & 1) {
+        const float lg = acc[r] + b;
+        const int64_t u = user_of(r);
+        if (direct) {
+          emit(u, lg, item);
+        } else {
+          const uint32_t at = base + __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(hit[r] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hit[r], 0u));
+          wl[at] = lg;
+          wi[at] = item;
+          wu[at] = (int32_t)u;
+        }
+      }
+      base += (uint32_t)__popcll(hit[r]);
+    }
+    if (!direct) staged = base;
+  };
+  // Iteration t multiplies tile t (buffer t % 3, operands in registers, the reads of tile t + 1
+  // issued behind each step's MFMAs), filters it, stores tile t + 2 into buffer (t + 2) % 3 (it
+  // held tile t - 1, whose reads completed before the previous barrier), loads tile t + 3 into
+  // the ring, and ends at the barrier that publishes tile t + 2.
+  if (it0 < it1) {
+    fetch(it0);
+    put(0);
+    if (it0 + kItemTile < it1) {
+      fetch(it0 + kItemTile);
+      put(1);
+    }
+    if (it0 + 2 * kItemTile < it1) fetch(it0 + 2 * kItemTile);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) rd(0, t);
+    int bc = 0;
+    for (int64_t t0 = it0; t0 < it1; t0 += kItemTile) {
+      const int bn = bc == 2 ? 0 : bc + 1, bn2 = bn == 2 ? 0 : bn + 1;
+      const bool has_next = t0 + kItemTile < it1;
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[t], bq[t][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[t], bq[t][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[t], bq[t][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[t], bq[t][2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[t], bq[t][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[t], bq[t][0], acc, 0, 0, 0);
+        if (has_next) rd(bn, t);
+      }
+      filt(acc, bc, t0);
+      if (t0 + 2 * kItemTile < it1) {
+        put(bn2);
+        if (t0 + 3 * kItemTile < it1) fetch(t0 + 3 * kItemTile);
+      }
+      __syncthreads();
+      bc = bn;
+    }
+  }
+  wflush();
+}
+
 // ---- 4. per-user selection: bitonic sort (descending) of 64-bit keys (logit key | ~item)
 constexpr int kSelectMax = 8192;
 
@@ -458,6 +676,60 @@ extern "C" int ncf_score_collect(const float* queries, const int32_t* user_list,
                      (hipStream_t)stream, queries, user_list, n_users, items, item_bias, n_items,
                      per, thr, cap, count, cand_logit, cand_item);
   NCF_CHECK_LAUNCH("ncf_score_collect");
+  return NCF_OK;
+}
+
+// three bf16 planes [3][n_items][dim] of the item rows (the operand split of
+// ncf_score_collect_split; built once per item index)
+extern "C" int ncf_score_split_items(const float* items, int64_t n_items, int64_t dim,
+                                     uint16_t* items3, void* stream) {
+  NCF_CHECK_ARG(n_items >= 0 && dim >= 1 && items && items3, "ncf_score_split_items: bad args");
+  const int64_t n = n_items * dim;
+  if (n == 0) return NCF_OK;
+  hipLaunchKernelGGL(k_split3, dim3((unsigned)ncf_cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     items, n, items3);
+  NCF_CHECK_LAUNCH("ncf_score_split_items");
+  return NCF_OK;
+}
+
+// ncf_score_collect on bf16 matrix cores with fp32 accuracy (three-term operand split, six
+// products; items3 from ncf_score_split_items): the same candidate sets
+extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user_list,
+                                       int64_t n_users, const uint16_t* items3,
+                                       const float* item_bias, int64_t n_items, int64_t dim,
+                                       const float* thr, int64_t cap, uint32_t* count,
+                                       float* cand_logit, int32_t* cand_item, void* stream) {
+  NCF_CHECK_ARG(dim == 64, "ncf_score_collect_split: dim must be 64");
+  NCF_CHECK_ARG(n_users >= 0 && n_items >= 0 && n_items < (1ll << 31) && cap >= 1,
+                "ncf_score_collect_split: bad size");
+  if (n_users == 0 || n_items == 0) return NCF_OK;
+  // Grid: (item split x user block) workgroups (one per CU: 8 waves at two per SIMD), sized in
+  // whole rounds of the chip's CUs — every workgroup scans the same number of tiles, so a partial
+  // last round would cost a whole round.  At least ~4 rounds, >= 8 tiles per workgroup.
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n_cu = v;
+    else
+      n_cu = 256;
+  }
+  const int64_t ub = (n_users + 255) / 256;
+  NCF_CHECK_ARG(ub < (1ll << 24), "ncf_score_collect_split: too many users per call");
+  const int64_t max_splits = std::max<int64_t>(1, (n_items + 8 * kItemTile - 1) / (8 * kItemTile));
+  int64_t splits = (4 * n_cu + ub - 1) / ub;
+  const int64_t rounds = (splits * ub + n_cu - 1) / n_cu;
+  splits = std::max<int64_t>(1, rounds * n_cu / ub);
+  if (splits > max_splits) splits = max_splits;
+  int64_t per = (n_items + splits - 1) / splits;
+  per = (per + kItemTile - 1) / kItemTile * kItemTile;
+  splits = (n_items + per - 1) / per;
+  NCF_CHECK_ARG(splits * ub < (1ll << 31), "ncf_score_collect_split: grid too large");
+  hipLaunchKernelGGL(k_collect3, dim3((unsigned)(splits * ub)), dim3(512), 0, (hipStream_t)stream,
+                     queries, user_list, n_users, items3, item_bias, n_items, per, (int)ub, thr,
+                     cap, count, cand_logit, cand_item);
+  NCF_CHECK_LAUNCH("ncf_score_collect_split");
   return NCF_OK;
 }
 

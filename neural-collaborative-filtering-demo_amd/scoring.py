@@ -19,6 +19,7 @@ all-gathered (RCCL) and merged per user by ``ncf_score_merge``.  ``forward_simpl
 hour variant draws a fresh random projection on every call, architecture.py:437-442, so it has no
 reusable item side).  GPU only; no CPU fallback.
 """
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -73,6 +74,11 @@ class ItemIndex:
         self.bias = torch.empty(I, device=dev)
         _lib.call("ncf_score_item_bias", ptr(mlp_item), I, ptr(model.final[0].weight),
                   ptr(model.final[0].bias), ptr(model.mf_output.bias), ptr(self.bias), st)
+        # the item rows as three bf16 planes for the split-operand MFMA scan (fp32 accuracy)
+        self.p3 = None
+        if SPLIT_SCAN:
+            self.p3 = torch.empty(3, I, D, dtype=torch.int16, device=dev)
+            _lib.call("ncf_score_split_items", ptr(self.p), I, D, ptr(self.p3), st)
         self.version = _param_version(model)
 
     def valid_for(self, model) -> bool:
@@ -82,6 +88,22 @@ class ItemIndex:
 def _param_version(model):
     # torch's _version sees optimizer steps through torch; engine.updates the HIP kernels' writes
     return (model._engine.updates,) + tuple(p._version for p in model.parameters())
+
+
+# the candidate scan on bf16 matrix cores with split operands (fp32 accuracy, same candidate
+# sets; NCF_SCORE_SPLIT=0: the fp32 MFMA scan)
+SPLIT_SCAN = os.environ.get("NCF_SCORE_SPLIT", "1") != "0"
+
+
+def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st):
+    """ncf_score_collect(_split) of n queried users over the index's items."""
+    I, D = idx.p.shape
+    if idx.p3 is not None:
+        _lib.call("ncf_score_collect_split", q, rows, n, ptr(idx.p3), ptr(idx.bias), I, D, thr,
+                  cap, count, cand_l, cand_i, st)
+    else:
+        _lib.call("ncf_score_collect", q, rows, n, ptr(idx.p), ptr(idx.bias), I, D, thr, cap,
+                  count, cand_l, cand_i, st)
 
 
 def _sample_size(n_items: int, k: int, cap: int) -> int:
@@ -129,8 +151,8 @@ class _TopKRun:
         _lib.call("ncf_score_kth", ptr(self.sample), n, self.S, k, ptr(bias), self.stride,
                   ptr(self.thr), st)
         self.count.zero_()
-        _lib.call("ncf_score_collect", ptr(self.q), None, n, ptr(p), ptr(bias), I, D, ptr(self.thr),
-                  cap, ptr(self.count), ptr(self.cand_l), ptr(self.cand_i), st)
+        _collect(idx, ptr(self.q), None, n, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),
+                 ptr(self.cand_i), st)
         _lib.call("ncf_score_select", None, n, ptr(self.count), ptr(self.cand_l), ptr(self.cand_i),
                   cap, k, ptr(self.scores), ptr(self.items), ptr(self.thr), ptr(self.overflow), st)
 
@@ -151,9 +173,8 @@ class _TopKRun:
             sub_s = torch.empty(rows.numel(), k, device=dev)
             sub_i = torch.empty(rows.numel(), k, dtype=torch.int64, device=dev)
             sub_o = torch.empty(rows.numel(), dtype=torch.int32, device=dev)
-            _lib.call("ncf_score_collect", ptr(self.q), ptr(rows), rows.numel(), ptr(p), ptr(bias),
-                      I, D, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),
-                      ptr(self.cand_i), st)
+            _collect(idx, ptr(self.q), ptr(rows), rows.numel(), ptr(self.thr), cap,
+                     ptr(self.count), ptr(self.cand_l), ptr(self.cand_i), st)
             _lib.call("ncf_score_select", ptr(rows), rows.numel(), ptr(self.count),
                       ptr(self.cand_l), ptr(self.cand_i), cap, k, ptr(sub_s), ptr(sub_i),
                       ptr(self.thr), ptr(sub_o), st)

@@ -1006,6 +1006,31 @@ def test_score_topk_vs_oracle(k, cap):
         np.testing.assert_allclose(s[r].cpu().numpy(), ref[r, got].numpy(), atol=1e-6)
 
 
+@pytest.mark.parametrize("k,cap", [(10, 8192), (100, 8192), (50, 256)])
+def test_split_bf16_scan_equals_fp32_scan(k, cap):
+    """The C5 candidate scan on bf16 matrix cores with 3-term operand splits (k_collect3, the
+    default) against the fp32 MFMA scan (k_collect) on the same index: the same top-k items
+    (except between scores equal within fp32 accumulation rounding) and scores within 1e-6.
+    700 of 5000 users (three 256-user blocks, the last partial), 100003 items (a partial last
+    tile); cap=256 at k=50 takes the overflow re-run through a user list."""
+    from ncf_amd.scoring import ItemIndex, score_topk
+    torch.manual_seed(11)
+    U, I = 5000, 100003
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    users = torch.randperm(U)[:700]
+    idx = ItemIndex(m)
+    assert idx.p3 is not None, "split scan is the default"
+    s3, i3 = score_topk(m, users, k=k, index=idx, cap=cap)
+    idx.p3 = None                      # same index, fp32 MFMA scan
+    s1, i1 = score_topk(m, users, k=k, index=idx, cap=cap)
+    torch.testing.assert_close(s3, s1, rtol=0, atol=1e-6)
+    diff = i3 != i1
+    assert diff.float().mean().item() < 1e-3
+    if diff.any():
+        assert bool(((s3 - s1).abs()[diff] <= 1e-6).all())
+
+
 @pytest.mark.parametrize("W,strided", [(3, False), (4, True), (1, False)])
 @pytest.mark.parametrize("k", [10, 100])
 def test_item_sharded_scoring_equals_single(W, strided, k):

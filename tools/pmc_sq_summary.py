@@ -13,7 +13,9 @@ for f in glob.glob(f"gpurun_out/sq{tag}_*/**/*counter_collection.csv", recursive
         k = k.split("(")[0].split("<")[0][:40]
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in sorted(acc.items()):
-    if not any(x in k for x in ("mlp", "attn", "gather", "piece", "reduce", "pairs", "dedup")):
+    keys = sys.argv[2].split(",") if len(sys.argv) > 2 else (
+        "mlp", "attn", "gather", "piece", "reduce", "pairs", "dedup")
+    if not any(x in k for x in keys):
         continue
     print(k)
     for c, v in sorted(d.items()):
