@@ -460,6 +460,8 @@ int ncf_score_queries(const int64_t* user_ids, int64_t n, const float* mf_user, 
                       void* stream);
 int ncf_score_item_bias(const float* mlp_item, int64_t n, const float* final_w,
                         const float* final_b, const float* mf_out_b, float* bias, void* stream);
+/* ncf_score_kth: logit(u, j) = logits[u*S + j] + item_bias[j*stride]; item_bias may be NULL
+ * when the sample logits already include the bias (the sample GEMM's column bias). */
 int ncf_score_kth(const float* logits, int64_t n_users, int64_t S, int K, const float* item_bias,
                   int64_t stride, float* thr, void* stream);
 int ncf_score_collect(const float* queries, const int32_t* user_list, int64_t n_users,

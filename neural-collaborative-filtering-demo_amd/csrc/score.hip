@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void k_kth(const float* __restrict__ logits, i
     hist[threadIdx.x] = 0;
     __syncthreads();
     for (int64_t j = threadIdx.x; j < S; j += 256) {
-      const uint32_t k = fkey(row[j] + bias[j * stride]);
+      const uint32_t k = fkey(bias ? row[j] + bias[j * stride] : row[j]);
       if ((k & hmask) == (prefix & hmask)) atomicAdd(&hist[(k >> shift) & 255u], 1u);
     }
     __syncthreads();
@@ -123,6 +123,124 @@ __global__ __launch_bounds__(256) void k_kth(const float* __restrict__ logits, i
     const float v = fkey_inv(prefix);
     thr[blockIdx.x] = v - 1e-4f * fmaxf(1.0f, fabsf(v));
   }
+}
+
+// The same threshold with the row held in LDS: the logits (+ the sampled bias, a strided gather)
+// are read from HBM once, with float4 loads, and the select runs over LDS in value space: 256
+// linear bins over [min, max], then 256 sub-bins of the bin holding the K-th largest; the
+// threshold is the smallest logit in the sub-bin holding it (at least K sample logits are >= it;
+// it is below the exact K-th by less than (max - min) / 65536, far inside the margin).  Linear
+// bins spread the logits over many bins (the exponent byte of the radix keys puts nearly all of
+// them in one or two, and their LDS atomics serialise).  For S <= kKthLdsMax.
+constexpr int64_t kKthLdsMax = 30720;   // 120 KB of logits
+
+// wave 0: the highest bin d with (count of bins >= d) >= need; returns d, and the count above d
+// in *above (lane l holds bins 4l..4l+3)
+__device__ __forceinline__ int kth_walk(const uint32_t* hist, uint32_t need, uint32_t* above) {
+  const int l = threadIdx.x;
+  const uint32_t c0 = hist[4 * l], c1 = hist[4 * l + 1], c2 = hist[4 * l + 2], c3 = hist[4 * l + 3];
+  uint32_t suf = c0 + c1 + c2 + c3;   // inclusive suffix over lanes, from the top
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_down(suf, o, 64);
+    if (l + o < 64) suf += x;
+  }
+  const uint64_t m = __ballot(suf >= need);            // lanes 0..L (suffix non-increasing)
+  const int L = 63 - __builtin_clzll(m);
+  // in lane L: walk its four bins from the top
+  uint32_t acc = suf - (c0 + c1 + c2 + c3);
+  int j = 3;
+  if (acc + c3 < need) {
+    acc += c3; j = 2;
+    if (acc + c2 < need) {
+      acc += c2; j = 1;
+      if (acc + c1 < need) { acc += c1; j = 0; }
+    }
+  }
+  *above = __shfl(acc, L, 64);
+  return 4 * L + __shfl(j, L, 64);
+}
+
+__global__ __launch_bounds__(512) void k_kth_lds(const float* __restrict__ logits, int64_t S,
+                                                 int K, const float* __restrict__ bias,
+                                                 int64_t stride, float* __restrict__ thr) {
+  extern __shared__ float kth_vals[];
+  __shared__ uint32_t hist[256], hmin[256];
+  __shared__ float rmax[8], rmin[8];
+  __shared__ int s_bin;
+  __shared__ uint32_t s_need;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* row = logits + (int64_t)blockIdx.x * S;
+  float vmax = -INFINITY, vmin = INFINITY;
+  const int64_t S4 = (S & 3) == 0 ? S / 4 : 0;   // rows start 16-B aligned when S % 4 == 0
+  for (int64_t j4 = tid; j4 < S4; j4 += 512) {
+    const float4 x = ld4(row + 4 * j4);
+    const int64_t j = 4 * j4;
+    const float4 v = bias ? make_float4(x.x + bias[j * stride], x.y + bias[(j + 1) * stride],
+                                        x.z + bias[(j + 2) * stride], x.w + bias[(j + 3) * stride])
+                          : x;
+    *reinterpret_cast<float4*>(kth_vals + j) = v;
+    vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+    vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+  }
+  for (int64_t j = 4 * S4 + tid; j < S; j += 512) {
+    const float v = bias ? row[j] + bias[j * stride] : row[j];
+    kth_vals[j] = v;
+    vmax = fmaxf(vmax, v);
+    vmin = fminf(vmin, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    vmax = fmaxf(vmax, __shfl_xor(vmax, o, 64));
+    vmin = fminf(vmin, __shfl_xor(vmin, o, 64));
+  }
+  if (lane == 0) { rmax[w] = vmax; rmin[w] = vmin; }
+  for (int j = tid; j < 256; j += 512) { hist[j] = 0; hmin[j] = 0xFFFFFFFFu; }
+  __syncthreads();
+  vmax = rmax[0]; vmin = rmin[0];
+#pragma unroll
+  for (int k = 1; k < 8; ++k) { vmax = fmaxf(vmax, rmax[k]); vmin = fminf(vmin, rmin[k]); }
+  const uint32_t need0 = (uint32_t)(K < S ? K : S);   // rank from the top, 1-based
+  float v = vmax;
+  if (vmax > vmin) {
+    // level 0: 256 bins over [vmin, vmax]; b(v) is non-decreasing in v
+    const float inv0 = 256.0f / (vmax - vmin);
+    auto bin0 = [&](float x) { return (int)fminf(fmaxf((x - vmin) * inv0, 0.0f), 255.0f); };
+    for (int64_t j = tid; j < S; j += 512) atomicAdd(&hist[bin0(kth_vals[j])], 1u);
+    __syncthreads();
+    if (w == 0) {
+      uint32_t above = 0;
+      const int b = kth_walk(hist, need0, &above);
+      if (lane == 0) {
+        s_bin = b;
+        s_need = need0 - above;
+      }
+    }
+    __syncthreads();
+    const int b0 = s_bin;
+    const uint32_t need1 = s_need;
+    for (int j = tid; j < 256; j += 512) hist[j] = 0;
+    __syncthreads();
+    // level 1: 256 sub-bins of bin b0, with the smallest logit of each (as an order key)
+    const float lo1 = vmin + (float)b0 / inv0, inv1 = inv0 * 256.0f;
+    for (int64_t j = tid; j < S; j += 512) {
+      const float x = kth_vals[j];
+      if (bin0(x) == b0) {
+        const int sb = (int)fminf(fmaxf((x - lo1) * inv1, 0.0f), 255.0f);
+        atomicAdd(&hist[sb], 1u);
+        atomicMin(&hmin[sb], fkey(x));
+      }
+    }
+    __syncthreads();
+    if (w == 0) {
+      uint32_t above = 0;
+      const int b1 = kth_walk(hist, need1, &above);
+      if (lane == 0) s_bin = b1;
+    }
+    __syncthreads();
+    v = fkey_inv(hmin[s_bin]);
+  }
+  if (tid == 0) thr[blockIdx.x] = v - 1e-4f * fmaxf(1.0f, fabsf(v));   // (the margin of k_kth)
 }
 
 // ---- 3. MFMA scan + threshold filter
@@ -648,8 +766,19 @@ extern "C" int ncf_score_kth(const float* logits, int64_t n_users, int64_t S, in
                              const float* item_bias, int64_t stride, float* thr, void* stream) {
   NCF_CHECK_ARG(n_users >= 0 && S >= 1 && K >= 1 && stride >= 1, "ncf_score_kth: bad size");
   if (n_users == 0) return NCF_OK;
-  hipLaunchKernelGGL(k_kth, dim3((unsigned)n_users), dim3(256), 0, (hipStream_t)stream, logits, S,
-                     K, item_bias, stride, thr);
+  if (S <= kKthLdsMax) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)k_kth_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(sizeof(uint32_t) * kKthLdsMax));
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_kth_lds, dim3((unsigned)n_users), dim3(512), sizeof(uint32_t) * S,
+                       (hipStream_t)stream, logits, S, K, item_bias, stride, thr);
+  } else {
+    hipLaunchKernelGGL(k_kth, dim3((unsigned)n_users), dim3(256), 0, (hipStream_t)stream, logits,
+                       S, K, item_bias, stride, thr);
+  }
   NCF_CHECK_LAUNCH("ncf_score_kth");
   return NCF_OK;
 }

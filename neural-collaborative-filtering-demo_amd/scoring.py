@@ -126,6 +126,8 @@ class _TopKRun:
         self.index, self.n, self.k, self.cap = index, n, k, cap
         self.S = _sample_size(I, k, cap)
         self.stride = I // self.S
+        # the sample's item biases, contiguous: added in the sample GEMM's epilogue
+        self.sbias = index.bias[::self.stride][:self.S].contiguous()
         e = lambda *sh, dt=torch.float32: torch.empty(*sh, dtype=dt, device=dev)  # noqa: E731
         self.uid = e(max(n, 1), dt=torch.int64)
         self.q, self.sample, self.thr = e(max(n, 1), D), e(max(n, 1), self.S), e(max(n, 1))
@@ -147,8 +149,8 @@ class _TopKRun:
                   ptr(model.mf_output.weight), ptr(model.final[0].weight), ptr(self.q),
                   ptr(self.err), st)
         _lib.call("ncf_gemm_f32", n, self.S, D, ptr(self.q), D, 0, ptr(p), D * self.stride, 1,
-                  ptr(self.sample), self.S, None, 0, st)
-        _lib.call("ncf_score_kth", ptr(self.sample), n, self.S, k, ptr(bias), self.stride,
+                  ptr(self.sample), self.S, ptr(self.sbias), 0, st)
+        _lib.call("ncf_score_kth", ptr(self.sample), n, self.S, k, None, self.stride,
                   ptr(self.thr), st)
         self.count.zero_()
         _collect(idx, ptr(self.q), None, n, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),
