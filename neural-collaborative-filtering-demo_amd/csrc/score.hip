@@ -642,45 +642,123 @@ __device__ __forceinline__ void bitonic_desc(unsigned long long* keys, int n2) {
   }
 }
 
-__global__ __launch_bounds__(1024) void k_select(const int32_t* __restrict__ user_list,
-                                                 int64_t n_users, const uint32_t* __restrict__ count,
-                                                 const float* __restrict__ cand_logit,
-                                                 const int32_t* __restrict__ cand_item,
-                                                 int64_t cap, int K, float* __restrict__ out_score,
-                                                 int64_t* __restrict__ out_item,
-                                                 float* __restrict__ thr_out,
-                                                 uint32_t* __restrict__ overflow) {
-  extern __shared__ unsigned long long keys[];
+// Per user: the K best candidates without sorting the whole list.  The candidates' order keys
+// (fkey of the logit) go to LDS; a radix select over key - min (8-bit digits from the highest bit
+// the keys differ in; the wave-scan digit walk of the threshold kernel) finds the K-th largest key
+// t; candidates above t, and the needed number of those equal to t (the smallest item ids: a
+// second radix select over ~id, only when the tie is split), are gathered and only those K are
+// sorted (bitonic over next_pow2(K) keys (logit key << 32 | ~id), descending).
+__global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user_list,
+                                                int64_t n_users, const uint32_t* __restrict__ count,
+                                                const float* __restrict__ cand_logit,
+                                                const int32_t* __restrict__ cand_item,
+                                                int64_t cap, int K, int n2K,
+                                                float* __restrict__ out_score,
+                                                int64_t* __restrict__ out_item,
+                                                float* __restrict__ thr_out,
+                                                uint32_t* __restrict__ overflow) {
+  extern __shared__ unsigned long long sel[];   // [n2K] selected keys, then uint32 keys[cap]
+  uint32_t* keys = reinterpret_cast<uint32_t*>(sel + n2K);
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t rmin[4], rmax[4];
+  __shared__ uint32_t s_dig, s_need, s_eq, s_n;
   const int64_t slot = blockIdx.x;
   if (slot >= n_users) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t u = user_list ? user_list[slot] : slot;
   const uint32_t c_all = count[u];
   const int nc = (int)(c_all < cap ? c_all : cap);
-  int n2 = 1;
-  while (n2 < nc || n2 < K) n2 <<= 1;
-  for (int j = threadIdx.x; j < n2; j += blockDim.x) {
-    unsigned long long k = 0ull;
-    if (j < nc) {
-      const uint32_t lk = fkey(cand_logit[u * cap + j]);
-      const uint32_t id = (uint32_t)cand_item[u * cap + j];
-      k = ((unsigned long long)lk << 32) | (unsigned long long)(0xFFFFFFFFu - id);
-    }
+  const float* cl = cand_logit + u * cap;
+  const int32_t* ci = cand_item + u * cap;
+  uint32_t kmin = 0xFFFFFFFFu, kmax = 0;
+  for (int j = tid; j < nc; j += 256) {
+    const uint32_t k = fkey(cl[j]);
     keys[j] = k;
+    kmin = min(kmin, k);
+    kmax = max(kmax, k);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
+    kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+  }
+  if (lane == 0) { rmin[w] = kmin; rmax[w] = kmax; }
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+  kmin = min(min(rmin[0], rmin[1]), min(rmin[2], rmin[3]));
+  kmax = max(max(rmax[0], rmax[1]), max(rmax[2], rmax[3]));
+  // radix select of one key domain: the need-th largest value among the members; returns the
+  // value, *need_left = members equal to it still needed, *n_eq = members equal to it
+  auto radix = [&](auto member, auto value, int nbits, uint32_t need, uint32_t* need_left,
+                   uint32_t* n_eq) -> uint32_t {
+    uint32_t prefix = 0, eq = 0;
+    for (int hi = nbits; hi > 0;) {
+      const int lo = hi > 8 ? hi - 8 : 0;
+      const uint32_t dm = (1u << (hi - lo)) - 1u;
+      hist[tid] = 0;
+      __syncthreads();
+      for (int j = tid; j < nc; j += 256) {
+        if (!member(j)) continue;
+        const uint32_t d = value(j);
+        if (hi >= 32 || (d >> hi) == (prefix >> hi)) atomicAdd(&hist[(d >> lo) & dm], 1u);
+      }
+      __syncthreads();
+      if (w == 0) {
+        uint32_t above = 0;
+        const int dig = kth_walk(hist, need, &above);
+        if (lane == 0) { s_dig = (uint32_t)dig; s_need = need - above; s_eq = hist[dig]; }
+      }
+      __syncthreads();
+      prefix |= s_dig << lo;
+      need = s_need;
+      eq = s_eq;
+      hi = lo;
+      __syncthreads();
+    }
+    *need_left = need;
+    *n_eq = eq;
+    return prefix;
+  };
+  uint32_t t = 0, t2 = 0;       // take key > t; key == t: all (tie_all) or ~id >= t2
+  bool tie_all = true;
+  if (nc > K) {
+    const uint32_t span = kmax - kmin;
+    const int nb = span ? 32 - __builtin_clz(span) : 0;
+    uint32_t need = (uint32_t)K, eq = (uint32_t)nc;
+    const uint32_t d = radix([&](int) { return true; }, [&](int j) { return keys[j] - kmin; }, nb,
+                             (uint32_t)K, &need, &eq);
+    t = kmin + d;
+    if (eq > need) {   // the tie at t is split: the smallest ids among the keys equal to t
+      tie_all = false;
+      uint32_t need2 = 0, eq2 = 0;
+      t2 = radix([&](int j) { return keys[j] == t; },
+                 [&](int j) { return 0xFFFFFFFFu - (uint32_t)ci[j]; }, 32, need, &need2, &eq2);
+    }
+  }
+  for (int j = tid; j < nc; j += 256) {
+    const uint32_t k = keys[j];
+    if (nc > K && k < t) continue;
+    const uint32_t nid = 0xFFFFFFFFu - (uint32_t)ci[j];
+    if (nc > K && k == t && !tie_all && nid < t2) continue;
+    sel[atomicAdd(&s_n, 1u)] = ((unsigned long long)k << 32) | (unsigned long long)nid;
   }
   __syncthreads();
-  bitonic_desc(keys, n2);
-  for (int j = threadIdx.x; j < K; j += blockDim.x) {
-    const unsigned long long k = keys[j];
-    const bool ok = j < nc;
+  const int ns = (int)s_n;   // = min(nc, K)
+  for (int j = ns + tid; j < n2K; j += 256) sel[j] = 0ull;
+  __syncthreads();
+  bitonic_desc(sel, n2K);
+  for (int j = tid; j < K; j += 256) {
+    const unsigned long long k = sel[j];
+    const bool ok = j < ns;
     const float lg = fkey_inv((uint32_t)(k >> 32));
     out_score[slot * K + j] = ok ? 1.0f / (1.0f + expf(-lg)) : 0.0f;
     out_item[slot * K + j] = ok ? (int64_t)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : -1;
   }
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     const bool over = c_all > (uint32_t)cap;
     overflow[slot] = over ? 1u : 0u;
     // a valid higher threshold for a re-run: the K-th best of the candidates seen
-    if (over && thr_out) thr_out[u] = fkey_inv((uint32_t)(keys[K - 1] >> 32));
+    if (over && thr_out) thr_out[u] = fkey_inv((uint32_t)(sel[K - 1] >> 32));
   }
 }
 
@@ -869,18 +947,18 @@ extern "C" int ncf_score_select(const int32_t* user_list, int64_t n_users, const
   NCF_CHECK_ARG(n_users >= 0 && K >= 1 && cap >= K && cap <= kSelectMax,
                 "ncf_score_select: need 1 <= K <= cap <= %d", kSelectMax);
   if (n_users == 0) return NCF_OK;
-  int n2 = 1;
-  while (n2 < cap) n2 <<= 1;
-  const size_t lds = sizeof(unsigned long long) * (size_t)n2;
+  int n2K = 1;
+  while (n2K < K) n2K <<= 1;
+  const size_t lds = sizeof(unsigned long long) * (size_t)n2K + sizeof(uint32_t) * (size_t)cap;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(sizeof(unsigned long long) * kSelectMax));
+                              (int)((sizeof(unsigned long long) + sizeof(uint32_t)) * kSelectMax));
     attr = true;
   }
-  hipLaunchKernelGGL(k_select, dim3((unsigned)n_users), dim3(1024), lds, (hipStream_t)stream,
-                     user_list, n_users, count, cand_logit, cand_item, cap, K, out_score, out_item,
-                     thr, overflow);
+  hipLaunchKernelGGL(k_select, dim3((unsigned)n_users), dim3(256), lds, (hipStream_t)stream,
+                     user_list, n_users, count, cand_logit, cand_item, cap, K, n2K, out_score,
+                     out_item, thr, overflow);
   NCF_CHECK_LAUNCH("ncf_score_select");
   return NCF_OK;
 }

@@ -106,9 +106,18 @@ def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st):
                   count, cand_l, cand_i, st)
 
 
+# Expected candidates per user the threshold sample aims at: ~1024 (a bigger sample costs a
+# longer sample GEMM and k-th select, a smaller one more scan hits and select work; measured
+# 1024 -> 7.5 ms, 2048 -> 7.7, cap / 2 = 4096 -> 8.3 at top-10 over 1M items), with the sample
+# kept within the k-th kernel's LDS-resident size (top-100: ~3300), and never above cap / 2.
+SAMPLE_CANDS = int(os.environ.get("NCF_SCORE_CANDS", "1024"))
+KTH_LDS_MAX = 30720   # score.hip kKthLdsMax
+
+
 def _sample_size(n_items: int, k: int, cap: int) -> int:
-    """Items in the threshold sample: expected candidates ~ k * n_items / S <= cap / 2."""
-    s = max(4096, -(-2 * k * n_items // cap))
+    """Items in the threshold sample S: expected candidates ~ k * n_items / S."""
+    s = max(4096, -(-k * n_items // max(1, SAMPLE_CANDS)))
+    s = max(min(s, KTH_LDS_MAX), -(-2 * k * n_items // cap))
     s = -(-s // 256) * 256
     return min(n_items, s)
 
