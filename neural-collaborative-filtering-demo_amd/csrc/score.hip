@@ -435,6 +435,10 @@ __global__ void k_split3(const float* __restrict__ p, int64_t n, uint16_t* __res
 }
 
 constexpr int kP3 = 72;        // LDS pitch of a staged bf16 item row (64 + 8)
+#ifndef NCF_SCORE3_UB
+#define NCF_SCORE3_UB 2
+#endif
+constexpr int kUB3 = NCF_SCORE3_UB;   // 32-user blocks per wave
 constexpr int kSlice3 = 256;   // candidates staged per wave (its own LDS slice: no atomics)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -444,6 +448,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // B operands of tile t + 1 are read from LDS while tile t is multiplied.  Hits go to the wave's
 // own LDS slice (offsets from ballots, no atomics) and the wave writes its slice to the global
 // lists itself when it fills (no workgroup barrier).
+template <int UB>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_collect3(
     const float* __restrict__ q, const int32_t* __restrict__ user_list, int64_t n_users,
     const uint16_t* __restrict__ items3, const float* __restrict__ bias, int64_t n_items,
@@ -458,12 +463,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int bx = (int)(blockIdx.x / ub), by = (int)(blockIdx.x % ub);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5;
-  const int64_t slot0 = (int64_t)by * 256 + w * 32;
-  const int64_t my_slot = slot0 + i;
-  const int64_t my_user = my_slot < n_users ? (user_list ? user_list[my_slot] : my_slot) : 0;
+  // the wave's UB blocks of 32 users (UB = 2: every staged B operand feeds two MFMA chains)
+  const int64_t slot0 = (int64_t)by * (256 * UB) + w * (32 * UB);
   // this lane's query values q[user][32h + 8t + j] split into three bf16 terms, per MFMA step t
-  bf16x8_t a0[4], a1[4], a2[4];
-  {
+  bf16x8_t a0[UB][4], a1[UB][4], a2[UB][4];
+#pragma unroll
+  for (int ub = 0; ub < UB; ++ub) {
+    const int64_t my_slot = slot0 + 32 * ub + i;
+    const int64_t my_user = my_slot < n_users ? (user_list ? user_list[my_slot] : my_slot) : 0;
     const float* qp = q + my_user * D + 32 * h;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -473,22 +480,33 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
       for (int j = 0; j < 8; ++j) {
         __bf16 b0, b1, b2;
         split3(v[j], b0, b1, b2);
-        a0[t][j] = b0; a1[t][j] = b1; a2[t][j] = b2;
+        a0[ub][t][j] = b0; a1[ub][t][j] = b1; a2[ub][t][j] = b2;
       }
     }
   }
   // thresholds of the 16 users whose logits this lane holds: row (r&3) + 8(r>>2) + 4h (their
   // user ids are looked up again on a hit only: 32 fewer live registers in the loop)
-  auto user_of = [&](int r) -> int64_t {
-    const int64_t s = slot0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+  auto user_of = [&](int r, int ub) -> int64_t {
+    const int64_t s = slot0 + 32 * ub + (r & 3) + 8 * (r >> 2) + 4 * h;
     return user_list ? (int64_t)user_list[s] : s;
   };
-  float th[16];
+  // thresholds of the wave's users in LDS (in registers they would cost 16 VGPRs per user block)
+  __shared__ __attribute__((aligned(16))) float ths[8 * 32 * UB];
+  float* wth = ths + w * (32 * UB);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t s = slot0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    th[r] = s < n_users ? thr[user_of(r)] : INFINITY;
+  for (int ub = 0; ub < UB; ++ub) {
+    const int64_t s = slot0 + 32 * ub + i;
+    const float v = s < n_users ? thr[user_list ? (int64_t)user_list[s] : s] : INFINITY;
+    if (h == 0) wth[32 * ub + i] = v;
   }
+  // this lane's 16 thresholds of user block ub: rows (r&3) + 8(r>>2) + 4h, four float4 reads
+  auto th_of = [&](int ub, float (&t)[16]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float4 x = *reinterpret_cast<const float4*>(wth + 32 * ub + 8 * c + 4 * h);
+      t[4 * c] = x.x; t[4 * c + 1] = x.y; t[4 * c + 2] = x.z; t[4 * c + 3] = x.w;
+    }
+  };
   const int64_t it0 = (int64_t)bx * items_per_block;
   const int64_t it1 = min(n_items, it0 + items_per_block);
   // staging: thread (item sj, column group sk) holds 4 bf16 of each of the 3 planes of the next
@@ -509,11 +527,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint2*>(&ps[bb][pl][sj][sk]) = pv[pl];
     if (sk == 0) bs[bb][sj] = pb;
   };
-  bf16x8_t bq[4][3];   // B operands of the tile being multiplied
+  bf16x8_t bq[UB == 1 ? 4 : 1][3];   // (UB = 1) B operands of the tile being multiplied
   auto rd = [&](int bb, int t) {
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
-      bq[t][pl] = *reinterpret_cast<const bf16x8_t*>(&ps[bb][pl][i][32 * h + 8 * t]);
+      bq[UB == 1 ? t : 0][pl] = *reinterpret_cast<const bf16x8_t*>(&ps[bb][pl][i][32 * h + 8 * t]);
   };
   // the wave's candidate slice: staged entries (wave-uniform), written out when it would overflow
   float* wl = cl + w * kSlice3;
@@ -531,7 +549,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (uint32_t e = lane; e < staged; e += 64) emit(wu[e], wl[e], wi[e]);
     staged = 0;
   };
-  auto filt = [&](const f32x16& acc, int bb, int64_t t0) {
+  auto filt = [&](const f32x16& acc, int ub, int bb, int64_t t0) {
+    float th[16];
+    th_of(ub, th);
     const int32_t item = (int32_t)(t0 + i);
     const float b = bs[bb][i];
     const bool ivalid = t0 + i < it1;
@@ -563,7 +583,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
       if (hit[r] == 0) continue;   // wave-uniform
       if ((hit[r] >> lane) & 1) {
         const float lg = acc[r] + b;
-        const int64_t u = user_of(r);
+        const int64_t u = user_of(r, ub);
         if (direct) {
           emit(u, lg, item);
         } else {
@@ -591,26 +611,45 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
     if (it0 + 2 * kItemTile < it1) fetch(it0 + 2 * kItemTile);
     __syncthreads();
+    if constexpr (UB == 1) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) rd(0, t);
+      for (int t = 0; t < 4; ++t) rd(0, t);
+    }
     int bc = 0;
     for (int64_t t0 = it0; t0 < it1; t0 += kItemTile) {
       const int bn = bc == 2 ? 0 : bc + 1, bn2 = bn == 2 ? 0 : bn + 1;
       const bool has_next = t0 + kItemTile < it1;
-      f32x16 acc;
+      f32x16 acc[UB];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+      for (int ub = 0; ub < UB; ++ub)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[ub][r] = 0.0f;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[t], bq[t][0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[t], bq[t][1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[t], bq[t][0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[t], bq[t][2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[t], bq[t][1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[t], bq[t][0], acc, 0, 0, 0);
-        if (has_next) rd(bn, t);
+        bf16x8_t b0, b1, b2;
+        if constexpr (UB == 1) {
+          b0 = bq[t][0]; b1 = bq[t][1]; b2 = bq[t][2];
+        } else {
+          b0 = *reinterpret_cast<const bf16x8_t*>(&ps[bc][0][i][32 * h + 8 * t]);
+          b1 = *reinterpret_cast<const bf16x8_t*>(&ps[bc][1][i][32 * h + 8 * t]);
+          b2 = *reinterpret_cast<const bf16x8_t*>(&ps[bc][2][i][32 * h + 8 * t]);
+        }
+#pragma unroll
+        for (int ub = 0; ub < UB; ++ub) {
+          f32x16& c = acc[ub];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b1, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[ub][t], b0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b2, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[ub][t], b1, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[ub][t], b0, c, 0, 0, 0);
+        }
+        if constexpr (UB == 1) {
+          if (has_next) rd(bn, t);
+        }
       }
-      filt(acc, bc, t0);
+#pragma unroll
+      for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, bc, t0);
       if (t0 + 2 * kItemTile < it1) {
         put(bn2);
         if (t0 + 3 * kItemTile < it1) fetch(t0 + 3 * kItemTile);
@@ -922,7 +961,7 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
     else
       n_cu = 256;
   }
-  const int64_t ub = (n_users + 255) / 256;
+  const int64_t ub = (n_users + 256 * kUB3 - 1) / (256 * kUB3);
   NCF_CHECK_ARG(ub < (1ll << 24), "ncf_score_collect_split: too many users per call");
   const int64_t max_splits = std::max<int64_t>(1, (n_items + 8 * kItemTile - 1) / (8 * kItemTile));
   int64_t splits = (4 * n_cu + ub - 1) / ub;
@@ -933,7 +972,8 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
   per = (per + kItemTile - 1) / kItemTile * kItemTile;
   splits = (n_items + per - 1) / per;
   NCF_CHECK_ARG(splits * ub < (1ll << 31), "ncf_score_collect_split: grid too large");
-  hipLaunchKernelGGL(k_collect3, dim3((unsigned)(splits * ub)), dim3(512), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_collect3<kUB3>, dim3((unsigned)(splits * ub)), dim3(512), 0,
+                     (hipStream_t)stream,
                      queries, user_list, n_users, items3, item_bias, n_items, per, (int)ub, thr,
                      cap, count, cand_logit, cand_item);
   NCF_CHECK_LAUNCH("ncf_score_collect_split");
