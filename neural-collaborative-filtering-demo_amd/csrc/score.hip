@@ -439,6 +439,10 @@ constexpr int kP3 = 72;        // LDS pitch of a staged bf16 item row (64 + 8)
 #define NCF_SCORE3_UB 2
 #endif
 constexpr int kUB3 = NCF_SCORE3_UB;   // 32-user blocks per wave
+#ifndef NCF_SCORE3_NW
+#define NCF_SCORE3_NW 8
+#endif
+constexpr int kNW3 = NCF_SCORE3_NW;   // waves per workgroup (measured: 8 at one per CU 6.6 ms, 4 at two per CU 6.9)
 constexpr int kSlice3 = 256;   // candidates staged per wave (its own LDS slice: no atomics)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -448,8 +452,8 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // B operands of tile t + 1 are read from LDS while tile t is multiplied.  Hits go to the wave's
 // own LDS slice (offsets from ballots, no atomics) and the wave writes its slice to the global
 // lists itself when it fills (no workgroup barrier).
-template <int UB>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_collect3(
+template <int UB, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_collect3(
     const float* __restrict__ q, const int32_t* __restrict__ user_list, int64_t n_users,
     const uint16_t* __restrict__ items3, const float* __restrict__ bias, int64_t n_items,
     int64_t items_per_block, int ub, const float* __restrict__ thr, int64_t cap,
@@ -458,13 +462,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   constexpr int D = 64;
   __shared__ __attribute__((aligned(16))) uint16_t ps[3][3][kItemTile][kP3];
   __shared__ float bs[3][kItemTile];
-  __shared__ float cl[8 * kSlice3];
-  __shared__ int32_t ci[8 * kSlice3], cu[8 * kSlice3];
+  __shared__ float cl[NW * kSlice3];
+  __shared__ int32_t ci[NW * kSlice3], cu[NW * kSlice3];
   const int bx = (int)(blockIdx.x / ub), by = (int)(blockIdx.x % ub);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5;
   // the wave's UB blocks of 32 users (UB = 2: every staged B operand feeds two MFMA chains)
-  const int64_t slot0 = (int64_t)by * (256 * UB) + w * (32 * UB);
+  const int64_t slot0 = (int64_t)by * (32 * NW * UB) + w * (32 * UB);
   // this lane's query values q[user][32h + 8t + j] split into three bf16 terms, per MFMA step t
   bf16x8_t a0[UB][4], a1[UB][4], a2[UB][4];
 #pragma unroll
@@ -491,7 +495,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     return user_list ? (int64_t)user_list[s] : s;
   };
   // thresholds of the wave's users in LDS (in registers they would cost 16 VGPRs per user block)
-  __shared__ __attribute__((aligned(16))) float ths[8 * 32 * UB];
+  __shared__ __attribute__((aligned(16))) float ths[NW * 32 * UB];
   float* wth = ths + w * (32 * UB);
 #pragma unroll
   for (int ub = 0; ub < UB; ++ub) {
@@ -511,20 +515,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int64_t it1 = min(n_items, it0 + items_per_block);
   // staging: thread (item sj, column group sk) holds 4 bf16 of each of the 3 planes of the next
   // tile to store (a one-tile register ring: its load has a whole tile to land)
-  const int sj = tid >> 4, sk = (tid & 15) * 4;
-  uint2 pv[3];
+  constexpr int E = kItemTile * 64 / (64 * NW);   // bf16 per plane per thread: 4 or 8
+  using V = typename std::conditional<E == 8, uint4, uint2>::type;
+  const int sj = tid / (64 / E), sk = (tid % (64 / E)) * E;
+  V pv[3];
   float pb = 0.f;
   auto fetch = [&](int64_t t0) {
     const int64_t item = t0 + sj;
     const int64_t src = item < it1 ? item : it0;  // clamped, unconditional
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
-      pv[pl] = *reinterpret_cast<const uint2*>(items3 + (int64_t)pl * n_items * D + src * D + sk);
+      pv[pl] = *reinterpret_cast<const V*>(items3 + (int64_t)pl * n_items * D + src * D + sk);
     pb = bias[src];
   };
   auto put = [&](int bb) {
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint2*>(&ps[bb][pl][sj][sk]) = pv[pl];
+    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<V*>(&ps[bb][pl][sj][sk]) = pv[pl];
     if (sk == 0) bs[bb][sj] = pb;
   };
   bf16x8_t bq[UB == 1 ? 4 : 1][3];   // (UB = 1) B operands of the tile being multiplied
@@ -961,18 +967,20 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
     else
       n_cu = 256;
   }
-  const int64_t ub = (n_users + 256 * kUB3 - 1) / (256 * kUB3);
+  const int64_t upb = 32 * kNW3 * kUB3;   // users per workgroup
+  const int64_t ub = (n_users + upb - 1) / upb;
   NCF_CHECK_ARG(ub < (1ll << 24), "ncf_score_collect_split: too many users per call");
   const int64_t max_splits = std::max<int64_t>(1, (n_items + 8 * kItemTile - 1) / (8 * kItemTile));
-  int64_t splits = (4 * n_cu + ub - 1) / ub;
-  const int64_t rounds = (splits * ub + n_cu - 1) / n_cu;
-  splits = std::max<int64_t>(1, rounds * n_cu / ub);
+  const int64_t slots = (int64_t)n_cu * (8 / kNW3);   // resident workgroups (2 waves/SIMD)
+  int64_t splits = (4 * slots + ub - 1) / ub;
+  const int64_t rounds = (splits * ub + slots - 1) / slots;
+  splits = std::max<int64_t>(1, rounds * slots / ub);
   if (splits > max_splits) splits = max_splits;
   int64_t per = (n_items + splits - 1) / splits;
   per = (per + kItemTile - 1) / kItemTile * kItemTile;
   splits = (n_items + per - 1) / per;
   NCF_CHECK_ARG(splits * ub < (1ll << 31), "ncf_score_collect_split: grid too large");
-  hipLaunchKernelGGL(k_collect3<kUB3>, dim3((unsigned)(splits * ub)), dim3(512), 0,
+  hipLaunchKernelGGL((k_collect3<kUB3, kNW3>), dim3((unsigned)(splits * ub)), dim3(64 * kNW3), 0,
                      (hipStream_t)stream,
                      queries, user_list, n_users, items3, item_bias, n_items, per, (int)ub, thr,
                      cap, count, cand_logit, cand_item);
