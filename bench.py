@@ -46,16 +46,16 @@ def pmc_traffic(kernel):
     WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction applied); None when absent."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
-    if not kernel or not files:
+    if not kernel:
         return None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    k = d.get("kernels", {}).get(kernel)
-    if not k:
-        return None
-    return {"bytes_per_launch": k["hbm_bytes_per_launch"],
-            "source": f"{os.path.basename(files[-1])} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
-                      f"separate passes)"}
+    for fn in reversed(files):   # the newest summary that has the kernel
+        with open(fn) as f:
+            k = json.load(f).get("kernels", {}).get(kernel)
+        if k:
+            return {"bytes_per_launch": k["hbm_bytes_per_launch"],
+                    "source": f"{os.path.basename(fn)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+                              f"separate passes)"}
+    return None
 
 
 ISO_STEPS = 40   # steps of the roofline kernel's isolated (sweep not overlapped) measurement
@@ -357,6 +357,8 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
                 eager, prof = dt, L.PROFILE
             L.PROFILE = None
         kname = "ncf_score_collect_split" if SPLIT_SCAN else "ncf_score_collect"
+        # (mean over the k = 10 and k = 100 launches of the profiled micro-benchmark)
+        ctraffic = pmc_traffic("k_collect3" if SPLIT_SCAN else "k_collect")
         coll = sum(e0.elapsed_time(e1) for name, _, e0, e1 in prof if name == kname)
         algo_tf = 2.0 * 64 * n_query * n_local / (coll * 1e-3) / 1e12   # 128 flop per pair
         if SPLIT_SCAN:
@@ -373,6 +375,8 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
                                      "achieved": round(tf, 2), "peak": peak,
                                      "unit": "TFLOP/s", "frac": round(tf / peak, 4),
                                      "flops_per_pair": 768 if SPLIT_SCAN else 128,
+                                     "traffic": ctraffic["bytes_per_launch"] if ctraffic else None,
+                                     "traffic_source": ctraffic["source"] if ctraffic else None,
                                      "algorithmic_tflops": round(algo_tf, 2),
                                      "algorithmic_frac_of_fp32_peak":
                                          round(algo_tf / FP32_MFMA_PEAK_TFS, 4)}}
