@@ -769,9 +769,11 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
   if (nc > K) {
     const uint32_t span = kmax - kmin;
     const int nb = span ? 32 - __builtin_clz(span) : 0;
-    uint32_t need = (uint32_t)K, eq = (uint32_t)nc;
-    const uint32_t d = radix([&](int) { return true; }, [&](int j) { return keys[j] - kmin; }, nb,
-                             (uint32_t)K, &need, &eq);
+    uint32_t need = (uint32_t)K, eq = (uint32_t)nc;   // (span 0: every key equals kmin)
+    const uint32_t d = nb == 0 ? 0u
+                               : radix([&](int) { return true; },
+                                       [&](int j) { return keys[j] - kmin; }, nb, (uint32_t)K,
+                                       &need, &eq);
     t = kmin + d;
     if (eq > need) {   // the tie at t is split: the smallest ids among the keys equal to t
       tie_all = false;
@@ -785,10 +787,11 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
     if (nc > K && k < t) continue;
     const uint32_t nid = 0xFFFFFFFFu - (uint32_t)ci[j];
     if (nc > K && k == t && !tie_all && nid < t2) continue;
-    sel[atomicAdd(&s_n, 1u)] = ((unsigned long long)k << 32) | (unsigned long long)nid;
+    const uint32_t pos = atomicAdd(&s_n, 1u);   // (exactly min(nc, K) arrive)
+    if (pos < (uint32_t)n2K) sel[pos] = ((unsigned long long)k << 32) | (unsigned long long)nid;
   }
   __syncthreads();
-  const int ns = (int)s_n;   // = min(nc, K)
+  const int ns = min((int)s_n, K);   // = min(nc, K)
   for (int j = ns + tid; j < n2K; j += 256) sel[j] = 0ull;
   __syncthreads();
   bitonic_desc(sel, n2K);

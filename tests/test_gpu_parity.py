@@ -1031,12 +1031,35 @@ def test_split_bf16_scan_equals_fp32_scan(k, cap):
         assert bool(((s3 - s1).abs()[diff] <= 1e-6).all())
 
 
-@pytest.mark.parametrize("k,cap", [(100, 8192), (10, 8192), (5, 4096)])
-def test_score_topk_exact_ties_by_item_id(k, cap):
-    """Select with a tie group straddling the k-th place: all but the last 10 items share one
-    item row (identical logits for every user), so the k best are the larger of the 10 distinct
+@pytest.mark.parametrize("U,I,k", [(40, 1003, 10), (40, 1003, 1), (20, 64, 64), (33, 4099, 37)])
+def test_score_topk_small_catalogues(U, I, k):
+    """Small and odd catalogues: a threshold sample of S = I (not a multiple of 4: the k-th
+    kernel's scalar tail), k = I (every item a candidate: the select's take-all path), k = 1."""
+    from oracle import ncf_oracle as O
+    from ncf_amd.scoring import score_topk
+    torch.manual_seed(31)
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    users = torch.arange(U)
+    s, it = score_topk(m, users, k=k)
+    p = {kk: v.detach().cpu() for kk, v in m.state_dict().items()}
+    ref = O.score_factorised(p, users, torch.arange(I), temporal_dim=32, n_layers=3).double()
+    for r in range(U):
+        order = torch.argsort(-ref[r], stable=True)[:k].tolist()
+        got = it[r].cpu().tolist()
+        assert sorted(got) == sorted(order) or np.allclose(
+            np.sort(ref[r, got].numpy()), np.sort(ref[r, order].numpy()), atol=1e-6)
+        np.testing.assert_allclose(s[r].cpu().numpy(), ref[r, got].numpy(), atol=1e-6)
+        assert bool((s[r][:-1] >= s[r][1:]).all())
+
+
+@pytest.mark.parametrize("k,cap,distinct", [(100, 8192, 10), (10, 8192, 10), (5, 4096, 10),
+                                            (10, 8192, 0)])
+def test_score_topk_exact_ties_by_item_id(k, cap, distinct):
+    """Select with a tie group straddling the k-th place: all but the last `distinct` items share
+    one item row (identical logits for every user), so the k best are the larger of the distinct
     items and then the tied items in ascending id order — the select's second radix pass over
-    ids.  Checked against the oracle's scores sorted by (score desc, id asc).  (A cap below the
+    ids (distinct = 0: every logit equal, min = max in the threshold and select kernels).  Checked against the oracle's scores sorted by (score desc, id asc).  (A cap below the
     tie group's size overflows for good: score_topk raises, as documented.)"""
     from oracle import ncf_oracle as O
     from ncf_amd.scoring import score_topk
@@ -1047,16 +1070,16 @@ def test_score_topk_exact_ties_by_item_id(k, cap):
     with torch.no_grad():
         for t in m.parameters():
             if t.dim() == 2 and t.shape[0] == I:     # the item tables
-                t[:I - 10] = t[0]
+                t[:I - distinct] = t[0]
     users = torch.arange(0, U, 3)
     s, it = score_topk(m, users, k=k, cap=cap)
     p = {kk: v.detach().cpu() for kk, v in m.state_dict().items()}
     ref = O.score_factorised(p, users, torch.arange(I), temporal_dim=32, n_layers=3)
     for r in range(len(users)):
         tie = ref[r, 0].item()
-        distinct = [(ref[r, j].item(), j) for j in range(I - 10, I)]
-        assert all(abs(v - tie) > 1e-5 for v, _ in distinct)   # (no near-tie with the group)
-        above = [j for v, j in sorted(distinct, reverse=True) if v > tie]
+        others = [(ref[r, j].item(), j) for j in range(I - distinct, I)]
+        assert all(abs(v - tie) > 1e-5 for v, _ in others)   # (no near-tie with the group)
+        above = [j for v, j in sorted(others, reverse=True) if v > tie]
         want = (above + list(range(k)))[:k]     # then the tied items, ascending ids
         assert it[r].cpu().tolist() == want
         np.testing.assert_allclose(s[r].cpu().numpy(), ref[r, want].numpy(), atol=1e-6)
