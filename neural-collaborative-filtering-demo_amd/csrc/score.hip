@@ -443,6 +443,9 @@ constexpr int kUB3 = NCF_SCORE3_UB;   // 32-user blocks per wave
 #define NCF_SCORE3_NW 8
 #endif
 constexpr int kNW3 = NCF_SCORE3_NW;   // waves per workgroup (measured: 8 at one per CU 6.6 ms, 4 at two per CU 6.9)
+#ifndef NCF_SCORE3_XCD
+#define NCF_SCORE3_XCD 1
+#endif
 constexpr int kSlice3 = 256;   // candidates staged per wave (its own LDS slice: no atomics)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -464,7 +467,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   __shared__ float bs[3][kItemTile];
   __shared__ float cl[NW * kSlice3];
   __shared__ int32_t ci[NW * kSlice3], cu[NW * kSlice3];
+#if NCF_SCORE3_XCD
+  // consecutive workgroups go round-robin to the 8 XCDs (each with its own L2): give every XCD a
+  // contiguous run of the split-major order, so the user blocks of one item split share an L2
+  int M = (int)blockIdx.x;
+  {
+    const int per = (int)(gridDim.x / 8);
+    if (per > 0 && (int)blockIdx.x < 8 * per) M = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  }
+  const int bx = M / ub, by = M % ub;
+#else
   const int bx = (int)(blockIdx.x / ub), by = (int)(blockIdx.x % ub);
+#endif
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5;
   // the wave's UB blocks of 32 users (UB = 2: every staged B operand feeds two MFMA chains)
