@@ -173,15 +173,29 @@ __global__ __launch_bounds__(512) void k_kth_lds(const float* __restrict__ logit
   const float* row = logits + (int64_t)blockIdx.x * S;
   float vmax = -INFINITY, vmin = INFINITY;
   const int64_t S4 = (S & 3) == 0 ? S / 4 : 0;   // rows start 16-B aligned when S % 4 == 0
-  for (int64_t j4 = tid; j4 < S4; j4 += 512) {
-    const float4 x = ld4(row + 4 * j4);
-    const int64_t j = 4 * j4;
-    const float4 v = bias ? make_float4(x.x + bias[j * stride], x.y + bias[(j + 1) * stride],
-                                        x.z + bias[(j + 2) * stride], x.w + bias[(j + 3) * stride])
-                          : x;
-    *reinterpret_cast<float4*>(kth_vals + j) = v;
-    vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
-    vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+  // 4 float4 loads in flight per thread (a dependent load per iteration leaves the row's HBM
+  // latency exposed 15 times at S = 30720)
+  for (int64_t base = tid; base < S4; base += 4 * 512) {
+    float4 xs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j4 = base + (int64_t)u * 512;
+      xs[u] = j4 < S4 ? ld4(row + 4 * j4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j4 = base + (int64_t)u * 512;
+      if (j4 >= S4) break;
+      const float4 x = xs[u];
+      const int64_t j = 4 * j4;
+      const float4 v = bias ? make_float4(x.x + bias[j * stride], x.y + bias[(j + 1) * stride],
+                                          x.z + bias[(j + 2) * stride],
+                                          x.w + bias[(j + 3) * stride])
+                            : x;
+      *reinterpret_cast<float4*>(kth_vals + j) = v;
+      vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+      vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+    }
   }
   for (int64_t j = 4 * S4 + tid; j < S; j += 512) {
     const float v = bias ? row[j] + bias[j * stride] : row[j];
