@@ -55,6 +55,21 @@ __global__ __launch_bounds__(256) void k_reduce_batch1(const BatchArgs a, float*
   if (i < d.L) {
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     int p = pb + w;
+    // 16 loads in flight per thread (a full 64-partial chunk in one batch), summed in the order
+    // of the loop below (accumulator j % 4 takes partial p + 4j): the same bits, without the
+    // four dependent rounds of HBM latency
+    for (; p + 60 < pe; p += 64) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = d.part[(int64_t)(p + 4 * j) * d.stride + i];
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+        a0 += v[j];
+        a1 += v[j + 1];
+        a2 += v[j + 2];
+        a3 += v[j + 3];
+      }
+    }
     for (; p + 12 < pe; p += 16) {
       a0 += d.part[(int64_t)p * d.stride + i];
       a1 += d.part[(int64_t)(p + 4) * d.stride + i];
