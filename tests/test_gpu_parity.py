@@ -1031,17 +1031,20 @@ def test_split_bf16_scan_equals_fp32_scan(k, cap):
         assert bool(((s3 - s1).abs()[diff] <= 1e-6).all())
 
 
-@pytest.mark.parametrize("U,I,k", [(40, 1003, 10), (40, 1003, 1), (20, 64, 64), (33, 4099, 37)])
-def test_score_topk_small_catalogues(U, I, k):
+@pytest.mark.parametrize("U,I,k,cap", [(40, 1003, 10, 8192), (40, 1003, 1, 8192), (20, 64, 64, 8192),
+                                       (33, 4099, 37, 8192), (24, 40000, 100, 256)])
+def test_score_topk_small_catalogues(U, I, k, cap):
     """Small and odd catalogues: a threshold sample of S = I (not a multiple of 4: the k-th
-    kernel's scalar tail), k = I (every item a candidate: the select's take-all path), k = 1."""
+    kernel's scalar tail), k = I (every item a candidate: the select's take-all path), k = 1;
+    k = 100 with cap = 256 needs a sample of 31488 > the LDS-resident 30720 logits (the streaming
+    radix k-th kernel)."""
     from oracle import ncf_oracle as O
     from ncf_amd.scoring import score_topk
     torch.manual_seed(31)
     m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
     m.eval()
     users = torch.arange(U)
-    s, it = score_topk(m, users, k=k)
+    s, it = score_topk(m, users, k=k, cap=cap)
     p = {kk: v.detach().cpu() for kk, v in m.state_dict().items()}
     ref = O.score_factorised(p, users, torch.arange(I), temporal_dim=32, n_layers=3).double()
     for r in range(U):
