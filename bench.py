@@ -307,7 +307,7 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
     max over ranks."""
     import ncf_amd
     from ncf_amd import _lib as L
-    from ncf_amd.scoring import SPLIT_SCAN, ItemIndex, shard_items, sharded_score_topk
+    from ncf_amd.scoring import SPLIT_SCAN, SPLIT_TERMS, ItemIndex, shard_items, sharded_score_topk
     torch.manual_seed(4321)
     m = ncf_amd.AdvancedNCF(n_users, n_items, 10, 50).to(dev).eval()
     users = torch.randperm(n_users, device=dev)[:n_query]
@@ -335,7 +335,9 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
 
     out = {"config": f"{n_query} users x {n_items} items (model {n_users} x {n_items}, D=64), "
                      "top-K over the whole catalogue, factorised fp32-accurate MFMA scan "
-                     + ("(bf16 matrix cores, 3-term operand split)" if SPLIT_SCAN else "(fp32 MFMA)")
+                     + (f"(bf16 matrix cores, {SPLIT_TERMS}-term operand split"
+                        + (", candidates re-scored in fp32)" if SPLIT_TERMS == 2 else ")")
+                        if SPLIT_SCAN else "(fp32 MFMA)")
                      + ", hipGraph-captured"
                      + (f", item-sharded over {world} GPUs (all-gather + merge)" if world > 1 else ""),
            "scaling": "strong", "n_gpus": world, "item_index_ms": round(index_ms, 3)}
@@ -362,9 +364,11 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
         coll = sum(e0.elapsed_time(e1) for name, _, e0, e1 in prof if name == kname)
         algo_tf = 2.0 * 64 * n_query * n_local / (coll * 1e-3) / 1e12   # 128 flop per pair
         if SPLIT_SCAN:
-            # executed matrix work: six bf16 products of the 3-term operand splits per pair
-            tf, peak = 6 * algo_tf, BF16_MFMA_PEAK_TFS
-            kdesc = "k_collect3 (v_mfma_f32_32x32x16_bf16, 6 split products per pair)"
+            # executed matrix work: the bf16 products of the operand splits per pair (2 terms:
+            # a0b0 + a0b1 + a1b0; 3 terms: six)
+            nprod = 3 if SPLIT_TERMS == 2 else 6
+            tf, peak = nprod * algo_tf, BF16_MFMA_PEAK_TFS
+            kdesc = f"k_collect3 (v_mfma_f32_32x32x16_bf16, {nprod} split products per pair)"
         else:
             tf, peak = algo_tf, FP32_MFMA_PEAK_TFS
             kdesc = "k_collect (v_mfma_f32_32x32x2_f32)"
@@ -374,7 +378,7 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
                         "roofline": {"bound": "mfma", "kernel": kdesc,
                                      "achieved": round(tf, 2), "peak": peak,
                                      "unit": "TFLOP/s", "frac": round(tf / peak, 4),
-                                     "flops_per_pair": 768 if SPLIT_SCAN else 128,
+                                     "flops_per_pair": 128 * (nprod if SPLIT_SCAN else 1),
                                      "traffic": ctraffic["bytes_per_launch"] if ctraffic else None,
                                      "traffic_source": ctraffic["source"] if ctraffic else None,
                                      "algorithmic_tflops": round(algo_tf, 2),

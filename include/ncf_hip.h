@@ -478,7 +478,20 @@ int ncf_score_split_items(const float* items, int64_t n_items, int64_t dim, uint
 int ncf_score_collect_split(const float* queries, const int32_t* user_list, int64_t n_users,
                             const uint16_t* items3, const float* item_bias, int64_t n_items,
                             int64_t dim, const float* thr, int64_t cap, uint32_t* count,
-                            float* cand_logit, int32_t* cand_item, void* stream);
+                            float* cand_logit, int32_t* cand_item, int terms, void* stream);
+/* terms = 2: the scan takes only x0 + x1 of each operand (three products a0b0 + a0b1 + a1b0):
+ * its logits are within 1e-4 * |q_u| * max_i |p_i| of fp32, so the thresholds are first lowered
+ * by that (ncf_score_margin, with max_i |p_i| from ncf_score_item_norm_max) and the candidates'
+ * logits recomputed in fp32 by ncf_score_select_rescored. */
+int ncf_score_item_norm_max(const float* items, int64_t n_items, int64_t dim, uint32_t* out_bits,
+                            void* stream);
+int ncf_score_margin(const float* queries, const int32_t* user_list, int64_t n_users, int64_t dim,
+                     const uint32_t* item_norm_max, float c, float* thr, void* stream);
+int ncf_score_select_rescored(const int32_t* user_list, int64_t n_users, const uint32_t* count,
+                              const int32_t* cand_item, int64_t cap, int K, const float* queries,
+                              const float* items, const float* item_bias, int64_t dim,
+                              float* out_score, int64_t* out_item, float* thr, uint32_t* overflow,
+                              void* stream);
 int ncf_score_select(const int32_t* user_list, int64_t n_users, const uint32_t* count,
                      const float* cand_logit, const int32_t* cand_item, int64_t cap, int K,
                      float* out_score, int64_t* out_item, float* thr, uint32_t* overflow,

@@ -257,6 +257,41 @@ __global__ __launch_bounds__(512) void k_kth_lds(const float* __restrict__ logit
   if (tid == 0) thr[blockIdx.x] = v - 1e-4f * fmaxf(1.0f, fabsf(v));   // (the margin of k_kth)
 }
 
+// max_i ||p_i||_2 over the item rows (D = 64; one wave per row; non-negative floats order like
+// their bit patterns, so one integer atomicMax per row)
+__global__ __launch_bounds__(256) void k_row_norm_max(const float* __restrict__ p, int64_t n,
+                                                      uint32_t* __restrict__ out_bits) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const float x = row < n ? p[row * 64 + lane] : 0.0f;
+  float ss = x * x;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if (lane == 0 && row < n) atomicMax(out_bits, __float_as_uint(sqrtf(ss)));
+}
+
+// thr[u] -= c * ||q_u||_2 * max_i ||p_i||_2 (+ an ulp-scale allowance): the two-term split
+// scan's logits are within that of the fp32 logit (Cauchy-Schwarz over the dropped terms), so
+// the lowered threshold keeps every item the fp32 threshold would
+__global__ __launch_bounds__(256) void k_score_margin(const float* __restrict__ q,
+                                                      const int32_t* __restrict__ user_list,
+                                                      int64_t n, const uint32_t* __restrict__ pmax,
+                                                      float c, float* __restrict__ thr) {
+  const int64_t slot = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (slot >= n) return;
+  const int64_t u = user_list ? (int64_t)user_list[slot] : slot;
+  const float x = q[u * 64 + lane];
+  float ss = x * x;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if (lane == 0) {
+    const float t = thr[u];
+    const float e = c * sqrtf(ss) * __uint_as_float(*pmax);
+    thr[u] = t - (e * 1.0001f + 1e-6f * fabsf(t));
+  }
+}
+
 // ---- 3. MFMA scan + threshold filter
 constexpr int kUsersPerBlock = 256;  // 8 waves x 32
 constexpr int kItemTile = 32;
@@ -469,7 +504,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // B operands of tile t + 1 are read from LDS while tile t is multiplied.  Hits go to the wave's
 // own LDS slice (offsets from ballots, no atomics) and the wave writes its slice to the global
 // lists itself when it fills (no workgroup barrier).
-template <int UB, int NW>
+template <int UB, int NW, int T>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_collect3(
     const float* __restrict__ q, const int32_t* __restrict__ user_list, int64_t n_users,
     const uint16_t* __restrict__ items3, const float* __restrict__ bias, int64_t n_items,
@@ -477,7 +512,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     uint32_t* __restrict__ count, float* __restrict__ cand_logit,
     int32_t* __restrict__ cand_item) {
   constexpr int D = 64;
-  __shared__ __attribute__((aligned(16))) uint16_t ps[3][3][kItemTile][kP3];
+  __shared__ __attribute__((aligned(16))) uint16_t ps[3][T][kItemTile][kP3];
   __shared__ float bs[3][kItemTile];
   __shared__ float cl[NW * kSlice3];
   __shared__ int32_t ci[NW * kSlice3], cu[NW * kSlice3];
@@ -546,25 +581,25 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   constexpr int E = kItemTile * 64 / (64 * NW);   // bf16 per plane per thread: 4 or 8
   using V = typename std::conditional<E == 8, uint4, uint2>::type;
   const int sj = tid / (64 / E), sk = (tid % (64 / E)) * E;
-  V pv[3];
+  V pv[T];
   float pb = 0.f;
   auto fetch = [&](int64_t t0) {
     const int64_t item = t0 + sj;
     const int64_t src = item < it1 ? item : it0;  // clamped, unconditional
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < T; ++pl)
       pv[pl] = *reinterpret_cast<const V*>(items3 + (int64_t)pl * n_items * D + src * D + sk);
     pb = bias[src];
   };
   auto put = [&](int bb) {
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<V*>(&ps[bb][pl][sj][sk]) = pv[pl];
+    for (int pl = 0; pl < T; ++pl) *reinterpret_cast<V*>(&ps[bb][pl][sj][sk]) = pv[pl];
     if (sk == 0) bs[bb][sj] = pb;
   };
   bf16x8_t bq[UB == 1 ? 4 : 1][3];   // (UB = 1) B operands of the tile being multiplied
   auto rd = [&](int bb, int t) {
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < T; ++pl)
       bq[UB == 1 ? t : 0][pl] = *reinterpret_cast<const bf16x8_t*>(&ps[bb][pl][i][32 * h + 8 * t]);
   };
   // the wave's candidate slice: staged entries (wave-uniform), written out when it would overflow
@@ -662,11 +697,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       for (int t = 0; t < 4; ++t) {
         bf16x8_t b0, b1, b2;
         if constexpr (UB == 1) {
-          b0 = bq[t][0]; b1 = bq[t][1]; b2 = bq[t][2];
+          b0 = bq[t][0]; b1 = bq[t][1]; b2 = bq[t][T - 1];
         } else {
           b0 = *reinterpret_cast<const bf16x8_t*>(&ps[bc][0][i][32 * h + 8 * t]);
           b1 = *reinterpret_cast<const bf16x8_t*>(&ps[bc][1][i][32 * h + 8 * t]);
-          b2 = *reinterpret_cast<const bf16x8_t*>(&ps[bc][2][i][32 * h + 8 * t]);
+          if constexpr (T == 3)
+            b2 = *reinterpret_cast<const bf16x8_t*>(&ps[bc][T - 1][i][32 * h + 8 * t]);
         }
 #pragma unroll
         for (int ub = 0; ub < UB; ++ub) {
@@ -674,9 +710,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
           c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b0, c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b1, c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[ub][t], b0, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b2, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[ub][t], b1, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[ub][t], b0, c, 0, 0, 0);
+          if constexpr (T == 3) {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b2, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[ub][t], b1, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[ub][t], b0, c, 0, 0, 0);
+          }
         }
         if constexpr (UB == 1) {
           if (has_next) rd(bn, t);
@@ -721,11 +759,18 @@ __device__ __forceinline__ void bitonic_desc(unsigned long long* keys, int n2) {
 // t; candidates above t, and the needed number of those equal to t (the smallest item ids: a
 // second radix select over ~id, only when the tie is split), are gathered and only those K are
 // sorted (bitonic over next_pow2(K) keys (logit key << 32 | ~id), descending).
+// RS (rescore): the candidates' logits are recomputed in fp32 from the query and item rows
+// (logit = bias + sum_k q_k p_k, fmaf in k order) instead of taken from the scan — for the
+// two-term split scan, whose logits are only bounds.
+template <bool RS>
 __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user_list,
                                                 int64_t n_users, const uint32_t* __restrict__ count,
                                                 const float* __restrict__ cand_logit,
                                                 const int32_t* __restrict__ cand_item,
                                                 int64_t cap, int K, int n2K,
+                                                const float* __restrict__ q,
+                                                const float* __restrict__ items,
+                                                const float* __restrict__ item_bias,
                                                 float* __restrict__ out_score,
                                                 int64_t* __restrict__ out_item,
                                                 float* __restrict__ thr_out,
@@ -744,8 +789,33 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
   const float* cl = cand_logit + u * cap;
   const int32_t* ci = cand_item + u * cap;
   uint32_t kmin = 0xFFFFFFFFu, kmax = 0;
+  float qr[RS ? 64 : 1];
+  if constexpr (RS) {
+#pragma unroll
+    for (int k = 0; k < 64; k += 4) {
+      const float4 x = ld4(q + u * 64 + k);
+      qr[k] = x.x; qr[k + 1] = x.y; qr[k + 2] = x.z; qr[k + 3] = x.w;
+    }
+  }
   for (int j = tid; j < nc; j += 256) {
-    const uint32_t k = fkey(cl[j]);
+    float lg;
+    if constexpr (RS) {
+      const int64_t it = ci[j];
+      const float* pr = items + it * 64;
+      float d = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 64; k += 4) {
+        const float4 x = ld4(pr + k);
+        d = fmaf(qr[k], x.x, d);
+        d = fmaf(qr[k + 1], x.y, d);
+        d = fmaf(qr[k + 2], x.z, d);
+        d = fmaf(qr[k + 3], x.w, d);
+      }
+      lg = d + item_bias[it];
+    } else {
+      lg = cl[j];
+    }
+    const uint32_t k = fkey(lg);
     keys[j] = k;
     kmin = min(kmin, k);
     kmax = max(kmax, k);
@@ -975,13 +1045,37 @@ extern "C" int ncf_score_split_items(const float* items, int64_t n_items, int64_
   return NCF_OK;
 }
 
+extern "C" int ncf_score_item_norm_max(const float* items, int64_t n_items, int64_t dim,
+                                       uint32_t* out_bits, void* stream) {
+  NCF_CHECK_ARG(dim == 64 && n_items >= 0 && out_bits, "ncf_score_item_norm_max: dim must be 64");
+  (void)hipMemsetAsync(out_bits, 0, sizeof(uint32_t), (hipStream_t)stream);
+  if (n_items == 0) return NCF_OK;
+  hipLaunchKernelGGL(k_row_norm_max, dim3((unsigned)ncf_cdiv(n_items, 4)), dim3(256), 0,
+                     (hipStream_t)stream, items, n_items, out_bits);
+  NCF_CHECK_LAUNCH("ncf_score_item_norm_max");
+  return NCF_OK;
+}
+
+extern "C" int ncf_score_margin(const float* queries, const int32_t* user_list, int64_t n_users,
+                                int64_t dim, const uint32_t* item_norm_max, float c, float* thr,
+                                void* stream) {
+  NCF_CHECK_ARG(dim == 64 && n_users >= 0 && c >= 0.0f, "ncf_score_margin: dim must be 64");
+  if (n_users == 0) return NCF_OK;
+  hipLaunchKernelGGL(k_score_margin, dim3((unsigned)ncf_cdiv(n_users, 4)), dim3(256), 0,
+                     (hipStream_t)stream, queries, user_list, n_users, item_norm_max, c, thr);
+  NCF_CHECK_LAUNCH("ncf_score_margin");
+  return NCF_OK;
+}
+
 // ncf_score_collect on bf16 matrix cores with fp32 accuracy (three-term operand split, six
 // products; items3 from ncf_score_split_items): the same candidate sets
 extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user_list,
                                        int64_t n_users, const uint16_t* items3,
                                        const float* item_bias, int64_t n_items, int64_t dim,
                                        const float* thr, int64_t cap, uint32_t* count,
-                                       float* cand_logit, int32_t* cand_item, void* stream) {
+                                       float* cand_logit, int32_t* cand_item, int terms,
+                                       void* stream) {
+  NCF_CHECK_ARG(terms == 2 || terms == 3, "ncf_score_collect_split: terms must be 2 or 3");
   NCF_CHECK_ARG(dim == 64, "ncf_score_collect_split: dim must be 64");
   NCF_CHECK_ARG(n_users >= 0 && n_items >= 0 && n_items < (1ll << 31) && cap >= 1,
                 "ncf_score_collect_split: bad size");
@@ -1011,10 +1105,16 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
   per = (per + kItemTile - 1) / kItemTile * kItemTile;
   splits = (n_items + per - 1) / per;
   NCF_CHECK_ARG(splits * ub < (1ll << 31), "ncf_score_collect_split: grid too large");
-  hipLaunchKernelGGL((k_collect3<kUB3, kNW3>), dim3((unsigned)(splits * ub)), dim3(64 * kNW3), 0,
-                     (hipStream_t)stream,
-                     queries, user_list, n_users, items3, item_bias, n_items, per, (int)ub, thr,
-                     cap, count, cand_logit, cand_item);
+  if (terms == 3)
+    hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 3>), dim3((unsigned)(splits * ub)),
+                       dim3(64 * kNW3), 0, (hipStream_t)stream, queries, user_list, n_users,
+                       items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
+                       cand_item);
+  else
+    hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 2>), dim3((unsigned)(splits * ub)),
+                       dim3(64 * kNW3), 0, (hipStream_t)stream, queries, user_list, n_users,
+                       items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
+                       cand_item);
   NCF_CHECK_LAUNCH("ncf_score_collect_split");
   return NCF_OK;
 }
@@ -1031,13 +1131,42 @@ extern "C" int ncf_score_select(const int32_t* user_list, int64_t n_users, const
   const size_t lds = sizeof(unsigned long long) * (size_t)n2K + sizeof(uint32_t) * (size_t)cap;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_select<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)((sizeof(unsigned long long) + sizeof(uint32_t)) * kSelectMax));
     attr = true;
   }
-  hipLaunchKernelGGL(k_select, dim3((unsigned)n_users), dim3(256), lds, (hipStream_t)stream,
-                     user_list, n_users, count, cand_logit, cand_item, cap, K, n2K, out_score,
-                     out_item, thr, overflow);
+  hipLaunchKernelGGL(k_select<false>, dim3((unsigned)n_users), dim3(256), lds, (hipStream_t)stream,
+                     user_list, n_users, count, cand_logit, cand_item, cap, K, n2K, nullptr,
+                     nullptr, nullptr, out_score, out_item, thr, overflow);
   NCF_CHECK_LAUNCH("ncf_score_select");
+  return NCF_OK;
+}
+
+// ncf_score_select with every candidate's logit recomputed in fp32 from queries [.., 64] and
+// items [n_items, 64] + item_bias (the two-term split scan's candidates)
+extern "C" int ncf_score_select_rescored(const int32_t* user_list, int64_t n_users,
+                                         const uint32_t* count, const int32_t* cand_item,
+                                         int64_t cap, int K, const float* queries,
+                                         const float* items, const float* item_bias,
+                                         int64_t dim, float* out_score, int64_t* out_item,
+                                         float* thr, uint32_t* overflow, void* stream) {
+  NCF_CHECK_ARG(dim == 64 && queries && items && item_bias,
+                "ncf_score_select_rescored: dim must be 64, rows non-null");
+  NCF_CHECK_ARG(n_users >= 0 && K >= 1 && cap >= K && cap <= kSelectMax,
+                "ncf_score_select_rescored: need 1 <= K <= cap <= %d", kSelectMax);
+  if (n_users == 0) return NCF_OK;
+  int n2K = 1;
+  while (n2K < K) n2K <<= 1;
+  const size_t lds = sizeof(unsigned long long) * (size_t)n2K + sizeof(uint32_t) * (size_t)cap;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_select<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)((sizeof(unsigned long long) + sizeof(uint32_t)) * kSelectMax));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_select<true>, dim3((unsigned)n_users), dim3(256), lds, (hipStream_t)stream,
+                     user_list, n_users, count, nullptr, cand_item, cap, K, n2K, queries, items,
+                     item_bias, out_score, out_item, thr, overflow);
+  NCF_CHECK_LAUNCH("ncf_score_select_rescored");
   return NCF_OK;
 }

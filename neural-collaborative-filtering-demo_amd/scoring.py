@@ -76,9 +76,13 @@ class ItemIndex:
                   ptr(model.final[0].bias), ptr(model.mf_output.bias), ptr(self.bias), st)
         # the item rows as three bf16 planes for the split-operand MFMA scan (fp32 accuracy)
         self.p3 = None
+        self.pmax = None   # max_i |p_i| (float bits) for the two-term scan's threshold margin
         if SPLIT_SCAN:
             self.p3 = torch.empty(3, I, D, dtype=torch.int16, device=dev)
             _lib.call("ncf_score_split_items", ptr(self.p), I, D, ptr(self.p3), st)
+            if SPLIT_TERMS == 2:
+                self.pmax = torch.empty(1, dtype=torch.int32, device=dev)
+                _lib.call("ncf_score_item_norm_max", ptr(self.p), I, D, ptr(self.pmax), st)
         self.version = _param_version(model)
 
     def valid_for(self, model) -> bool:
@@ -93,14 +97,22 @@ def _param_version(model):
 # the candidate scan on bf16 matrix cores with split operands (fp32 accuracy, same candidate
 # sets; NCF_SCORE_SPLIT=0: the fp32 MFMA scan)
 SPLIT_SCAN = os.environ.get("NCF_SCORE_SPLIT", "1") != "0"
+# terms per operand of the split scan: 2 (three products; the thresholds lowered by the scan's
+# error bound, the candidates re-scored in fp32: measured 4.8 / 7.1 ms at top-10 / top-100) or 3
+# (six products, fp32-accurate logits straight from the scan: 6.8 / 8.5 ms)
+SPLIT_TERMS = int(os.environ.get("NCF_SCORE_TERMS", "2"))
+MARGIN_C = 1e-4   # >= the two-term scan's |logit error| / (|q| max|p|) (score.hip: ~6.1e-5)
 
 
 def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st):
     """ncf_score_collect(_split) of n queried users over the index's items."""
     I, D = idx.p.shape
     if idx.p3 is not None:
+        terms = 2 if idx.pmax is not None else 3
+        if terms == 2:   # lower the thresholds by the two-term scan's error bound first
+            _lib.call("ncf_score_margin", q, rows, n, D, ptr(idx.pmax), MARGIN_C, thr, st)
         _lib.call("ncf_score_collect_split", q, rows, n, ptr(idx.p3), ptr(idx.bias), I, D, thr,
-                  cap, count, cand_l, cand_i, st)
+                  cap, count, cand_l, cand_i, terms, st)
     else:
         _lib.call("ncf_score_collect", q, rows, n, ptr(idx.p), ptr(idx.bias), I, D, thr, cap,
                   count, cand_l, cand_i, st)
@@ -112,6 +124,18 @@ def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st):
 # kept within the k-th kernel's LDS-resident size (top-100: ~3300), and never above cap / 2.
 SAMPLE_CANDS = int(os.environ.get("NCF_SCORE_CANDS", "1024"))
 KTH_LDS_MAX = 30720   # score.hip kKthLdsMax
+
+
+def _select(idx, rows, n, run, k, out_s, out_i, overflow, st):
+    """ncf_score_select(_rescored) of n users' candidate lists (fp32 re-scoring after the
+    two-term scan)."""
+    if idx.pmax is not None:
+        _lib.call("ncf_score_select_rescored", rows, n, ptr(run.count), ptr(run.cand_i), run.cap,
+                  k, ptr(run.q), ptr(idx.p), ptr(idx.bias), idx.p.shape[1], out_s, out_i,
+                  ptr(run.thr), overflow, st)
+    else:
+        _lib.call("ncf_score_select", rows, n, ptr(run.count), ptr(run.cand_l), ptr(run.cand_i),
+                  run.cap, k, out_s, out_i, ptr(run.thr), overflow, st)
 
 
 def _sample_size(n_items: int, k: int, cap: int) -> int:
@@ -164,8 +188,7 @@ class _TopKRun:
         self.count.zero_()
         _collect(idx, ptr(self.q), None, n, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),
                  ptr(self.cand_i), st)
-        _lib.call("ncf_score_select", None, n, ptr(self.count), ptr(self.cand_l), ptr(self.cand_i),
-                  cap, k, ptr(self.scores), ptr(self.items), ptr(self.thr), ptr(self.overflow), st)
+        _select(idx, None, n, self, k, ptr(self.scores), ptr(self.items), ptr(self.overflow), st)
 
     def redo_overflow(self, st):
         """Re-run the users whose candidate list overflowed (eager; rare: the threshold sample
@@ -186,9 +209,7 @@ class _TopKRun:
             sub_o = torch.empty(rows.numel(), dtype=torch.int32, device=dev)
             _collect(idx, ptr(self.q), ptr(rows), rows.numel(), ptr(self.thr), cap,
                      ptr(self.count), ptr(self.cand_l), ptr(self.cand_i), st)
-            _lib.call("ncf_score_select", ptr(rows), rows.numel(), ptr(self.count),
-                      ptr(self.cand_l), ptr(self.cand_i), cap, k, ptr(sub_s), ptr(sub_i),
-                      ptr(self.thr), ptr(sub_o), st)
+            _select(idx, ptr(rows), rows.numel(), self, k, ptr(sub_s), ptr(sub_i), ptr(sub_o), st)
             self.scores[redo] = sub_s
             self.items[redo] = sub_i
             overflow.zero_()

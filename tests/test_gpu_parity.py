@@ -1008,8 +1008,9 @@ def test_score_topk_vs_oracle(k, cap):
 
 @pytest.mark.parametrize("k,cap", [(10, 8192), (100, 8192), (50, 256)])
 def test_split_bf16_scan_equals_fp32_scan(k, cap):
-    """The C5 candidate scan on bf16 matrix cores with 3-term operand splits (k_collect3, the
-    default) against the fp32 MFMA scan (k_collect) on the same index: the same top-k items
+    """The C5 candidate scan on bf16 matrix cores with 2-term operand splits (the default: margin-
+    lowered thresholds, candidates re-scored in fp32) and with 3-term splits (k_collect3) against
+    the fp32 MFMA scan (k_collect) on the same index: the same top-k items
     (except between scores equal within fp32 accumulation rounding) and scores within 1e-6.
     700 of 5000 users (three 256-user blocks, the last partial), 100003 items (a partial last
     tile); cap=256 at k=50 takes the overflow re-run through a user list."""
@@ -1020,15 +1021,18 @@ def test_split_bf16_scan_equals_fp32_scan(k, cap):
     m.eval()
     users = torch.randperm(U)[:700]
     idx = ItemIndex(m)
-    assert idx.p3 is not None, "split scan is the default"
+    assert idx.p3 is not None and idx.pmax is not None, "two-term split scan is the default"
+    s2, i2 = score_topk(m, users, k=k, index=idx, cap=cap)
+    idx.pmax = None                    # same index, three-term scan (logits from the scan)
     s3, i3 = score_topk(m, users, k=k, index=idx, cap=cap)
     idx.p3 = None                      # same index, fp32 MFMA scan
     s1, i1 = score_topk(m, users, k=k, index=idx, cap=cap)
-    torch.testing.assert_close(s3, s1, rtol=0, atol=1e-6)
-    diff = i3 != i1
-    assert diff.float().mean().item() < 1e-3
-    if diff.any():
-        assert bool(((s3 - s1).abs()[diff] <= 1e-6).all())
+    for s_, i_ in ((s3, i3), (s2, i2)):
+        torch.testing.assert_close(s_, s1, rtol=0, atol=1e-6)
+        diff = i_ != i1
+        assert diff.float().mean().item() < 1e-3
+        if diff.any():
+            assert bool(((s_ - s1).abs()[diff] <= 1e-6).all())
 
 
 @pytest.mark.parametrize("U,I,k,cap", [(40, 1003, 10, 8192), (40, 1003, 1, 8192), (20, 64, 64, 8192),
