@@ -488,10 +488,11 @@ int ncf_score_item_norm_max(const float* items, int64_t n_items, int64_t dim, ui
 int ncf_score_margin(const float* queries, const int32_t* user_list, int64_t n_users, int64_t dim,
                      const uint32_t* item_norm_max, float c, float* thr, void* stream);
 int ncf_score_select_rescored(const int32_t* user_list, int64_t n_users, const uint32_t* count,
-                              const int32_t* cand_item, int64_t cap, int K, const float* queries,
-                              const float* items, const float* item_bias, int64_t dim,
-                              float* out_score, int64_t* out_item, float* thr, uint32_t* overflow,
-                              void* stream);
+                              const float* cand_logit, const int32_t* cand_item, int64_t cap,
+                              int K, const float* queries, const float* items,
+                              const float* item_bias, int64_t dim, const uint32_t* item_norm_max,
+                              float c, float* out_score, int64_t* out_item, float* thr,
+                              uint32_t* overflow, void* stream);
 int ncf_score_select(const int32_t* user_list, int64_t n_users, const uint32_t* count,
                      const float* cand_logit, const int32_t* cand_item, int64_t cap, int K,
                      float* out_score, int64_t* out_item, float* thr, uint32_t* overflow,

@@ -759,9 +759,11 @@ __device__ __forceinline__ void bitonic_desc(unsigned long long* keys, int n2) {
 // t; candidates above t, and the needed number of those equal to t (the smallest item ids: a
 // second radix select over ~id, only when the tie is split), are gathered and only those K are
 // sorted (bitonic over next_pow2(K) keys (logit key << 32 | ~id), descending).
-// RS (rescore): the candidates' logits are recomputed in fp32 from the query and item rows
-// (logit = bias + sum_k q_k p_k, fmaf in k order) instead of taken from the scan — for the
-// two-term split scan, whose logits are only bounds.
+// RS (rescore, the two-term split scan's candidates): the scan's logits are within E =
+// c |q_u| max|p| of fp32, so the exact top K lie among the candidates whose scan logit is >=
+// (the scan's K-th largest) - 2E; only those are re-scored in fp32 (logit = bias + sum_k q_k p_k,
+// fmaf in k order) and the select runs on the re-scored keys (the others keyed 0: below every
+// real logit's key).
 template <bool RS>
 __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user_list,
                                                 int64_t n_users, const uint32_t* __restrict__ count,
@@ -771,6 +773,7 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
                                                 const float* __restrict__ q,
                                                 const float* __restrict__ items,
                                                 const float* __restrict__ item_bias,
+                                                const uint32_t* __restrict__ pmax, float c,
                                                 float* __restrict__ out_score,
                                                 int64_t* __restrict__ out_item,
                                                 float* __restrict__ thr_out,
@@ -778,7 +781,7 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
   extern __shared__ unsigned long long sel[];   // [n2K] selected keys, then uint32 keys[cap]
   uint32_t* keys = reinterpret_cast<uint32_t*>(sel + n2K);
   __shared__ uint32_t hist[256];
-  __shared__ uint32_t rmin[4], rmax[4];
+  __shared__ uint32_t rmin[4], rmax[4], rcnt[4];
   __shared__ uint32_t s_dig, s_need, s_eq, s_n;
   const int64_t slot = blockIdx.x;
   if (slot >= n_users) return;
@@ -788,48 +791,29 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
   const int nc = (int)(c_all < cap ? c_all : cap);
   const float* cl = cand_logit + u * cap;
   const int32_t* ci = cand_item + u * cap;
-  uint32_t kmin = 0xFFFFFFFFu, kmax = 0;
-  float qr[RS ? 64 : 1];
-  if constexpr (RS) {
-#pragma unroll
-    for (int k = 0; k < 64; k += 4) {
-      const float4 x = ld4(q + u * 64 + k);
-      qr[k] = x.x; qr[k + 1] = x.y; qr[k + 2] = x.z; qr[k + 3] = x.w;
+  // block min / max of the keys of the members (key != 0) and their number
+  auto key_range = [&](uint32_t& kmin, uint32_t& kmax, uint32_t& nmem) {
+    kmin = 0xFFFFFFFFu; kmax = 0; nmem = 0;
+    for (int j = tid; j < nc; j += 256) {
+      const uint32_t k = keys[j];
+      if (k == 0) continue;
+      kmin = min(kmin, k);
+      kmax = max(kmax, k);
+      ++nmem;
     }
-  }
-  for (int j = tid; j < nc; j += 256) {
-    float lg;
-    if constexpr (RS) {
-      const int64_t it = ci[j];
-      const float* pr = items + it * 64;
-      float d = 0.0f;
 #pragma unroll
-      for (int k = 0; k < 64; k += 4) {
-        const float4 x = ld4(pr + k);
-        d = fmaf(qr[k], x.x, d);
-        d = fmaf(qr[k + 1], x.y, d);
-        d = fmaf(qr[k + 2], x.z, d);
-        d = fmaf(qr[k + 3], x.w, d);
-      }
-      lg = d + item_bias[it];
-    } else {
-      lg = cl[j];
+    for (int o = 32; o > 0; o >>= 1) {
+      kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
+      kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+      nmem += (uint32_t)__shfl_xor((int)nmem, o, 64);
     }
-    const uint32_t k = fkey(lg);
-    keys[j] = k;
-    kmin = min(kmin, k);
-    kmax = max(kmax, k);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
-    kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
-  }
-  if (lane == 0) { rmin[w] = kmin; rmax[w] = kmax; }
-  if (tid == 0) s_n = 0;
-  __syncthreads();
-  kmin = min(min(rmin[0], rmin[1]), min(rmin[2], rmin[3]));
-  kmax = max(max(rmax[0], rmax[1]), max(rmax[2], rmax[3]));
+    if (lane == 0) { rmin[w] = kmin; rmax[w] = kmax; rcnt[w] = nmem; }
+    __syncthreads();
+    kmin = min(min(rmin[0], rmin[1]), min(rmin[2], rmin[3]));
+    kmax = max(max(rmax[0], rmax[1]), max(rmax[2], rmax[3]));
+    nmem = (rcnt[0] + rcnt[1]) + (rcnt[2] + rcnt[3]);
+    __syncthreads();
+  };
   // radix select of one key domain: the need-th largest value among the members; returns the
   // value, *need_left = members equal to it still needed, *n_eq = members equal to it
   auto radix = [&](auto member, auto value, int nbits, uint32_t need, uint32_t* need_left,
@@ -862,17 +846,62 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
     *n_eq = eq;
     return prefix;
   };
-  uint32_t t = 0, t2 = 0;       // take key > t; key == t: all (tie_all) or ~id >= t2
-  bool tie_all = true;
-  if (nc > K) {
+  // the key of the K-th largest member (span 0: every member equal)
+  auto kth_key = [&](uint32_t kmin, uint32_t kmax, uint32_t nmem, uint32_t* need,
+                     uint32_t* eq) -> uint32_t {
     const uint32_t span = kmax - kmin;
     const int nb = span ? 32 - __builtin_clz(span) : 0;
-    uint32_t need = (uint32_t)K, eq = (uint32_t)nc;   // (span 0: every key equals kmin)
-    const uint32_t d = nb == 0 ? 0u
-                               : radix([&](int) { return true; },
-                                       [&](int j) { return keys[j] - kmin; }, nb, (uint32_t)K,
-                                       &need, &eq);
-    t = kmin + d;
+    *need = (uint32_t)K;
+    *eq = nmem;
+    if (nb == 0) return kmin;
+    return kmin + radix([&](int j) { return keys[j] != 0; }, [&](int j) { return keys[j] - kmin; },
+                        nb, (uint32_t)K, need, eq);
+  };
+  if (tid == 0) s_n = 0;
+  for (int j = tid; j < nc; j += 256) keys[j] = fkey(cl[j]);
+  __syncthreads();
+  uint32_t kmin, kmax, nmem;
+  key_range(kmin, kmax, nmem);
+  if constexpr (RS) {
+    float qr[64];
+    float qq = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 64; k += 4) {
+      const float4 x = ld4(q + u * 64 + k);
+      qr[k] = x.x; qr[k + 1] = x.y; qr[k + 2] = x.z; qr[k + 3] = x.w;
+      qq += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+    }
+    float lo = -INFINITY;   // re-score the candidates with a scan logit >= lo
+    if (nmem > (uint32_t)K) {
+      uint32_t need, eq;
+      const float va = fkey_inv(kth_key(kmin, kmax, nmem, &need, &eq));
+      const float e = c * sqrtf(qq) * __uint_as_float(*pmax);
+      lo = va - (2.0f * e * 1.0001f + 1e-6f * fabsf(va));
+    }
+    for (int j = tid; j < nc; j += 256) {
+      if (cl[j] < lo) { keys[j] = 0; continue; }
+      const int64_t it = ci[j];
+      const float* pr = items + it * 64;
+      float d = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 64; k += 4) {
+        const float4 x = ld4(pr + k);
+        d = fmaf(qr[k], x.x, d);
+        d = fmaf(qr[k + 1], x.y, d);
+        d = fmaf(qr[k + 2], x.z, d);
+        d = fmaf(qr[k + 3], x.w, d);
+      }
+      keys[j] = fkey(d + item_bias[it]);
+    }
+    __syncthreads();
+    key_range(kmin, kmax, nmem);
+  }
+  const int ne = (int)nmem;     // members (RS: the re-scored candidates)
+  uint32_t t = 0, t2 = 0;       // take key > t; key == t: all (tie_all) or ~id >= t2
+  bool tie_all = true;
+  if (ne > K) {
+    uint32_t need = (uint32_t)K, eq = nmem;
+    t = kth_key(kmin, kmax, nmem, &need, &eq);
     if (eq > need) {   // the tie at t is split: the smallest ids among the keys equal to t
       tie_all = false;
       uint32_t need2 = 0, eq2 = 0;
@@ -882,14 +911,15 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
   }
   for (int j = tid; j < nc; j += 256) {
     const uint32_t k = keys[j];
-    if (nc > K && k < t) continue;
+    if (k == 0) continue;
+    if (ne > K && k < t) continue;
     const uint32_t nid = 0xFFFFFFFFu - (uint32_t)ci[j];
-    if (nc > K && k == t && !tie_all && nid < t2) continue;
-    const uint32_t pos = atomicAdd(&s_n, 1u);   // (exactly min(nc, K) arrive)
+    if (ne > K && k == t && !tie_all && nid < t2) continue;
+    const uint32_t pos = atomicAdd(&s_n, 1u);   // (exactly min(ne, K) arrive)
     if (pos < (uint32_t)n2K) sel[pos] = ((unsigned long long)k << 32) | (unsigned long long)nid;
   }
   __syncthreads();
-  const int ns = min((int)s_n, K);   // = min(nc, K)
+  const int ns = min((int)s_n, K);   // = min(ne, K)
   for (int j = ns + tid; j < n2K; j += 256) sel[j] = 0ull;
   __syncthreads();
   bitonic_desc(sel, n2K);
@@ -1137,7 +1167,7 @@ extern "C" int ncf_score_select(const int32_t* user_list, int64_t n_users, const
   }
   hipLaunchKernelGGL(k_select<false>, dim3((unsigned)n_users), dim3(256), lds, (hipStream_t)stream,
                      user_list, n_users, count, cand_logit, cand_item, cap, K, n2K, nullptr,
-                     nullptr, nullptr, out_score, out_item, thr, overflow);
+                     nullptr, nullptr, nullptr, 0.0f, out_score, out_item, thr, overflow);
   NCF_CHECK_LAUNCH("ncf_score_select");
   return NCF_OK;
 }
@@ -1145,12 +1175,14 @@ extern "C" int ncf_score_select(const int32_t* user_list, int64_t n_users, const
 // ncf_score_select with every candidate's logit recomputed in fp32 from queries [.., 64] and
 // items [n_items, 64] + item_bias (the two-term split scan's candidates)
 extern "C" int ncf_score_select_rescored(const int32_t* user_list, int64_t n_users,
-                                         const uint32_t* count, const int32_t* cand_item,
-                                         int64_t cap, int K, const float* queries,
-                                         const float* items, const float* item_bias,
-                                         int64_t dim, float* out_score, int64_t* out_item,
-                                         float* thr, uint32_t* overflow, void* stream) {
-  NCF_CHECK_ARG(dim == 64 && queries && items && item_bias,
+                                         const uint32_t* count, const float* cand_logit,
+                                         const int32_t* cand_item, int64_t cap, int K,
+                                         const float* queries, const float* items,
+                                         const float* item_bias, int64_t dim,
+                                         const uint32_t* item_norm_max, float c,
+                                         float* out_score, int64_t* out_item, float* thr,
+                                         uint32_t* overflow, void* stream) {
+  NCF_CHECK_ARG(dim == 64 && queries && items && item_bias && item_norm_max,
                 "ncf_score_select_rescored: dim must be 64, rows non-null");
   NCF_CHECK_ARG(n_users >= 0 && K >= 1 && cap >= K && cap <= kSelectMax,
                 "ncf_score_select_rescored: need 1 <= K <= cap <= %d", kSelectMax);
@@ -1165,8 +1197,8 @@ extern "C" int ncf_score_select_rescored(const int32_t* user_list, int64_t n_use
     attr = true;
   }
   hipLaunchKernelGGL(k_select<true>, dim3((unsigned)n_users), dim3(256), lds, (hipStream_t)stream,
-                     user_list, n_users, count, nullptr, cand_item, cap, K, n2K, queries, items,
-                     item_bias, out_score, out_item, thr, overflow);
+                     user_list, n_users, count, cand_logit, cand_item, cap, K, n2K, queries, items,
+                     item_bias, item_norm_max, c, out_score, out_item, thr, overflow);
   NCF_CHECK_LAUNCH("ncf_score_select_rescored");
   return NCF_OK;
 }

@@ -130,9 +130,10 @@ def _select(idx, rows, n, run, k, out_s, out_i, overflow, st):
     """ncf_score_select(_rescored) of n users' candidate lists (fp32 re-scoring after the
     two-term scan)."""
     if idx.pmax is not None:
-        _lib.call("ncf_score_select_rescored", rows, n, ptr(run.count), ptr(run.cand_i), run.cap,
-                  k, ptr(run.q), ptr(idx.p), ptr(idx.bias), idx.p.shape[1], out_s, out_i,
-                  ptr(run.thr), overflow, st)
+        _lib.call("ncf_score_select_rescored", rows, n, ptr(run.count), ptr(run.cand_l),
+                  ptr(run.cand_i), run.cap, k, ptr(run.q), ptr(idx.p), ptr(idx.bias),
+                  idx.p.shape[1], ptr(idx.pmax), MARGIN_C, out_s, out_i, ptr(run.thr), overflow,
+                  st)
     else:
         _lib.call("ncf_score_select", rows, n, ptr(run.count), ptr(run.cand_l), ptr(run.cand_i),
                   run.cap, k, out_s, out_i, ptr(run.thr), overflow, st)
