@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round-2 session-4 evidence (C5 scoring rework): the GPU suite, the default bench line and
-# rocprofv3 kernel-trace stats of the C5 micro-benchmark.  Every GPU step under its own limit.
+# Round-2 session-4 evidence (C5 scoring rework): the GPU suite, the default bench line,
+# rocprofv3 kernel-trace stats and PMC HBM traffic of the C5 micro-benchmark.  Every GPU step
+# under its own time limit; stop at the first failure.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -9,4 +10,7 @@ step gputests_r02d 600 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --t
 tail -2 gpurun_out/gputests_r02d.log
 step bench_r02d 900 python3 -u bench.py
 step profc5_r02d 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profc5_r02d -o run --output-format csv -- python3 tools/score_bench.py
+for C in FETCH_SIZE WRITE_SIZE; do
+  step pmc_$C 300 rocprofv3 --pmc $C -d gpurun_out/pmc_$C -o run --output-format csv -- python3 tools/score_bench.py --reps 1
+done
 echo done
