@@ -10,23 +10,23 @@
 // Pipeline (all deterministic: the final order is (logit desc, item id asc)):
 //   1. ncf_score_queries      q_u rows (gather + LayerNorm + scale);
 //   2. ncf_score_kth          per user, the K-th largest logit over a strided item SAMPLE (the
-//                             sample logits come from ncf_gemm_f32 with a strided B) — a lower
-//                             bound of the true K-th largest (radix select on the order-
-//                             preserving uint32 image of the float);
-//   3. ncf_score_collect      the MFMA scan: every (user, item) logit, appending (logit, item) to
-//                             the user's candidate list when logit >= threshold.  The candidate
-//                             SET is a function of the threshold only, so any append order gives
-//                             the same result;
-//   4. ncf_score_select       per user, bitonic sort of its candidates in LDS, top-K out; when a
-//                             user's list overflowed, the K-th best candidate seen is a higher
-//                             valid threshold and the host re-runs 3-4 for those users.
-// MFMA tiling of 3: a 512-thread workgroup owns 256 users (8 waves x 32), keeps each wave's q
-// rows in registers (k-permuted: MFMA step s uses k = s + 32h), and streams 32-item tiles of p
-// through double-buffered LDS ([32][65] pitch: conflict-free); per tile a wave issues 32
-// v_mfma_f32_32x32x2_f32 and filters its 32x32 logits against 16 per-lane thresholds.  Hits are
-// staged in LDS (one LDS atomic per wave and tile, from a wave prefix of the lanes' hit counts)
-// and flushed to the global per-user lists in parallel bursts: a global atomic per hit made the
-// wave wait thousands of cycles in nearly every tile (17.1 -> 14.7 ms at C5 top-10).
+//                             sample logits, bias included, come from ncf_gemm_f32 with a strided
+//                             B) — a lower bound of the true K-th largest (k_kth_lds: the row in
+//                             LDS, two levels of 256 linear value bins; k_kth: radix select over
+//                             the order-preserving uint32 image of the float, streamed);
+//   3. ncf_score_collect_split  the MFMA scan (k_collect3: bf16 matrix cores on operands split into
+//                             bf16 terms; ncf_score_collect: the fp32 MFMA scan), appending
+//                             (logit, item) to the user's candidate list when logit >= threshold.
+//                             The candidate SET is a function of the threshold only, so any append
+//                             order gives the same result.  With two terms the scan's logits are
+//                             bounds (within E_u = c |q_u| max|p|): ncf_score_margin lowers the
+//                             thresholds by E_u first;
+//   4. ncf_score_select(_rescored)  per user, radix select of the K-th candidate key in LDS, the K
+//                             winners sorted (after two-term scans: the candidates within 2 E_u of
+//                             the scan's K-th re-scored in fp32 first); when a user's list
+//                             overflowed, the K-th best candidate seen is a higher valid threshold
+//                             and the host re-runs 3-4 for those users.
+// Tilings: see k_collect (fp32) and k_collect3 (split bf16) below.
 #include "ncf_common.h"
 #include <algorithm>
 #include <type_traits>
@@ -293,6 +293,12 @@ __global__ __launch_bounds__(256) void k_score_margin(const float* __restrict__ 
 }
 
 // ---- 3. MFMA scan + threshold filter
+// fp32 tiling (k_collect): a 512-thread workgroup owns 256 users (8 waves x 32), keeps each
+// wave's q rows in registers (k-permuted: MFMA step s uses k = s + 32h), and streams 32-item tiles
+// of p through double-buffered LDS ([32][65] pitch: conflict-free); per tile a wave issues 32
+// v_mfma_f32_32x32x2_f32 and filters its 32x32 logits against 16 per-lane thresholds.  Hits are
+// staged in LDS (one LDS atomic per wave and tile) and flushed to the global per-user lists in
+// parallel bursts (a global atomic per hit made the wave wait thousands of cycles per tile).
 constexpr int kUsersPerBlock = 256;  // 8 waves x 32
 constexpr int kItemTile = 32;
 #ifndef NCF_SCORE_PD
