@@ -490,10 +490,13 @@ __global__ void k_split3(const float* __restrict__ p, int64_t n, uint16_t* __res
 }
 
 constexpr int kP3 = 72;        // LDS pitch of a staged bf16 item row (64 + 8)
+// 32-user blocks per wave: 4 with two-term operands (each staged B operand feeds four MFMA
+// chains; 256 VGPRs, no spill), 2 with three terms (their query registers take 1.5x as many)
 #ifndef NCF_SCORE3_UB
-#define NCF_SCORE3_UB 2
+#define NCF_SCORE3_UB 4
 #endif
-constexpr int kUB3 = NCF_SCORE3_UB;   // 32-user blocks per wave
+constexpr int kUB3 = NCF_SCORE3_UB;            // (two-term scan)
+constexpr int kUB3t = NCF_SCORE3_UB > 2 ? 2 : NCF_SCORE3_UB;   // (three-term scan)
 #ifndef NCF_SCORE3_NW
 #define NCF_SCORE3_NW 8
 #endif
@@ -641,37 +644,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       const bool near = ivalid && fmaxf(m2.x, m2.y) + b >= -1e-6f * fabsf(b);
       if (!__ballot(near)) return;
     }
-    // exact hits, one wave mask per user row; slice offsets from popcounts and mbcnt
-    uint64_t hit[16];
-    uint32_t total = 0;
+    // exact hits row by row: one wave mask per user row, slice offsets from mbcnt; the slice is
+    // written out first when the row's hits would not fit (a row has at most 64)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      hit[r] = __ballot(ivalid && acc[r] + b >= th[r]);
-      total += (uint32_t)__popcll(hit[r]);
-    }
-    if (total == 0) return;
-    if (staged + total > (uint32_t)kSlice3) wflush();
-    const bool direct = total > (uint32_t)kSlice3;   // (a tile of > 256 hits: straight out)
-    uint32_t base = staged;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if (hit[r] == 0) continue;   // wave-uniform
-      if ((hit[r] >> lane) & 1) {
-        const float lg = acc[r] + b;
-        const int64_t u = user_of(r, ub);
-        if (direct) {
-          emit(u, lg, item);
-        } else {
-          const uint32_t at = base + __builtin_amdgcn_mbcnt_hi(
-              (uint32_t)(hit[r] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hit[r], 0u));
-          wl[at] = lg;
-          wi[at] = item;
-          wu[at] = (int32_t)u;
-        }
+      const uint64_t hm = __ballot(ivalid && acc[r] + b >= th[r]);
+      if (hm == 0) continue;   // wave-uniform
+      const uint32_t nh = (uint32_t)__popcll(hm);
+      if (staged + nh > (uint32_t)kSlice3) wflush();
+      if ((hm >> lane) & 1) {
+        const uint32_t at = staged + __builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+        wl[at] = acc[r] + b;
+        wi[at] = item;
+        wu[at] = (int32_t)user_of(r, ub);
       }
-      base += (uint32_t)__popcll(hit[r]);
+      staged += nh;
     }
-    if (!direct) staged = base;
   };
   // Iteration t multiplies tile t (buffer t % 3, operands in registers, the reads of tile t + 1
   // issued behind each step's MFMAs), filters it, stores tile t + 2 into buffer (t + 2) % 3 (it
@@ -1128,7 +1117,8 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
     else
       n_cu = 256;
   }
-  const int64_t upb = 32 * kNW3 * kUB3;   // users per workgroup
+  const int nub = terms == 2 ? kUB3 : kUB3t;
+  const int64_t upb = 32 * kNW3 * nub;   // users per workgroup
   const int64_t ub = (n_users + upb - 1) / upb;
   NCF_CHECK_ARG(ub < (1ll << 24), "ncf_score_collect_split: too many users per call");
   const int64_t max_splits = std::max<int64_t>(1, (n_items + 8 * kItemTile - 1) / (8 * kItemTile));
@@ -1142,7 +1132,7 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
   splits = (n_items + per - 1) / per;
   NCF_CHECK_ARG(splits * ub < (1ll << 31), "ncf_score_collect_split: grid too large");
   if (terms == 3)
-    hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 3>), dim3((unsigned)(splits * ub)),
+    hipLaunchKernelGGL((k_collect3<kUB3t, kNW3, 3>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), 0, (hipStream_t)stream, queries, user_list, n_users,
                        items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
                        cand_item);
