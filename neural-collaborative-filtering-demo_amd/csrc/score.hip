@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void k_kth(const float* __restrict__ logits, i
 // it is below the exact K-th by less than (max - min) / 65536, far inside the margin).  Linear
 // bins spread the logits over many bins (the exponent byte of the radix keys puts nearly all of
 // them in one or two, and their LDS atomics serialise).  For S <= kKthLdsMax.
-constexpr int64_t kKthLdsMax = 30720;   // 120 KB of logits
+constexpr int64_t kKthLdsMax = 38912;   // 152 KB of logits (of the 160 KB of LDS)
 
 // wave 0: the highest bin d with (count of bins >= d) >= need; returns d, and the count above d
 // in *above (lane l holds bins 4l..4l+3)

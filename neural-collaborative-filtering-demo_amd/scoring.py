@@ -121,9 +121,10 @@ def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st):
 # Expected candidates per user the threshold sample aims at: ~1024 (a bigger sample costs a
 # longer sample GEMM and k-th select, a smaller one more scan hits and select work; measured
 # 1024 -> 7.5 ms, 2048 -> 7.7, cap / 2 = 4096 -> 8.3 at top-10 over 1M items), with the sample
-# kept within the k-th kernel's LDS-resident size (top-100: ~3300), and never above cap / 2.
+# kept within the k-th kernel's LDS-resident size (top-100: ~2570; a 30720-logit cap: 6.26 ms,
+# 38912: 5.90 ms), and never above cap / 2.
 SAMPLE_CANDS = int(os.environ.get("NCF_SCORE_CANDS", "1024"))
-KTH_LDS_MAX = 30720   # score.hip kKthLdsMax
+KTH_LDS_MAX = int(os.environ.get("NCF_SCORE_KTH_MAX", "38912"))   # <= score.hip kKthLdsMax
 
 
 def _select(idx, rows, n, run, k, out_s, out_i, overflow, st):
