@@ -11,6 +11,16 @@ Zipf(1.05), negatives uniform; random-init weights.  Inputs are resident in HBM 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
+``--gpus N`` without a torchrun environment (no WORLD_SIZE) starts the N rank processes itself
+(torchrun's env: RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) before this
+process touches the GPU, and exits with their status; fewer than N visible GPUs is an error.
+
+Every timed leg first runs ``prime`` steps (2 x the deferred Adam's sweep_every = 128 by
+default) before its W counted warm-up steps: the deferred table schedule replays, per swept
+row, the zero-gradient steps since that row's stamp, and every stamp starts at 0, so before
+step 2 x sweep_every a sweep replays less than its steady-state share.  Priming puts every leg
+in steady state whatever W is (``adam_steady_state`` per leg).
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -18,6 +28,8 @@ import json
 import math
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -59,6 +71,83 @@ def pmc_traffic(kernel):
 
 
 ISO_STEPS = 40   # steps of the roofline kernel's isolated (sweep not overlapped) measurement
+SWEEP_EVERY = 64  # the deferred table Adam's rolling-sweep period (FusedTrainStep / optim.py)
+
+
+def prime_steps(args) -> int:
+    """Untimed steps run before the counted warm-up of every training leg: 2 x sweep_every
+    (the deferred schedule's steady state, see the module docstring) unless --prime says."""
+    return 2 * SWEEP_EVERY if args.prime < 0 else args.prime
+
+
+def steady_state(prime: int, warmup: int, sweep_every) -> bool:
+    """Whether a leg's timed steps run with the deferred sweep in steady state: every row has
+    been swept at least once after its first sweep cycle before timing starts."""
+    return bool(sweep_every) and prime + warmup >= 2 * int(sweep_every)
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, dry: bool) -> int:
+    """`bench.py --gpus n` outside torchrun: start n rank processes of this script with
+    torchrun's environment, one per GPU, and return their exit status (the first failure; the
+    other ranks are then stopped, by PID).  Runs before anything here touches the GPU
+    (torch.cuda.device_count() does not initialise it on this image)."""
+    if not dry:
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} asked for {n} GPUs but only {have} are visible; "
+                  "refusing to run a smaller job", file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:          # a rank failed: the others would wait in collectives
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def dry_launch() -> None:
+    """--dry-launch: each rank joins a gloo group from the env and checks that all ranks agree
+    on the world size (no GPU); rank 0 prints one JSON line.  Tests the --gpus N launcher."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([world, rank, 1], dtype=torch.int64)
+    if world > 1:
+        lst = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(lst, t)
+        dist.destroy_process_group()
+    else:
+        lst = [t]
+    if rank == 0:
+        print(json.dumps({"dry_launch": True, "n_gpus": world,
+                          "ranks": sorted(int(x[1]) for x in lst),
+                          "worlds_agree": all(int(x[0]) == world for x in lst),
+                          "local_ranks_env": os.environ.get("LOCAL_RANK")}), flush=True)
 
 
 def zipf_sampler(n_items, s, device):
@@ -146,7 +235,7 @@ def cpu_baseline(model_sd, cfg, batches_cpu, budget_s):
                       f"{threads} threads on {cpu_model}"}
 
 
-def dropin_train(ncf, dev, cfg, batches, warmup, steps):
+def dropin_train(ncf, dev, cfg, batches, warmup, steps, prime=0):
     """The reference's own call pattern on the fused path (src/model/trainer.py:258-285):
     ``out = model(kjt); loss = nn.BCELoss()(out, t); optimizer.zero_grad(); loss.backward();
     optimizer.step()`` with ``torch.optim.Adam(model.parameters(), lr, weight_decay)`` — the
@@ -178,15 +267,15 @@ def dropin_train(ncf, dev, cfg, batches, warmup, steps):
                 loss.item()
         return loss
 
-    run(0, warmup)
+    run(0, prime + warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    loss = run(warmup, steps)
+    loss = run(prime + warmup, steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     n_item = min(steps, 100)
     t1 = time.perf_counter()
-    run(warmup + steps, n_item, item=True)
+    run(prime + warmup + steps, n_item, item=True)
     torch.cuda.synchronize()
     dt_item = time.perf_counter() - t1
     from ncf_amd import optim as _o
@@ -195,6 +284,9 @@ def dropin_train(ncf, dev, cfg, batches, warmup, steps):
                       "(trainer.py:258-285), deferred dense-exact table schedule via the step hook",
            "value": round(B * M * steps / dt, 1), "unit": "samples/s",
            "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warmup,
+           "prime_steps": prime,
+           "adam_steady_state": steady_state(prime, warmup, b.D.sweep_every if b is not None
+                                             and b.D is not None else None),
            "schedule": "deferred" if b is not None and b.D is not None else "dense",
            "final_loss": round(float(loss.detach()), 6),
            "with_loss_item": {"ms_per_step": round(dt_item / n_item * 1e3, 4),
@@ -205,7 +297,7 @@ def dropin_train(ncf, dev, cfg, batches, warmup, steps):
     return out
 
 
-def bf16_train(ncf, dev, cfg, batches, warmup, steps):
+def bf16_train(ncf, dev, cfg, batches, warmup, steps, prime=0):
     """The C2 configuration as BASELINE.json configs[1] states it ("bf16"; SURVEY 8(d): tables
     bf16, Adam moments fp32): the same step as the headline with the four tables held as bf16
     (FusedTrainStep(table_dtype=torch.bfloat16)); every other tensor and all arithmetic fp32.
@@ -220,15 +312,17 @@ def bf16_train(ncf, dev, cfg, batches, warmup, steps):
         for s in range(first, first + count):
             u, i, t = batches[s % len(batches)]
             step(u, i, t, next=batches[(s + 1) % len(batches)][:2])
-    run(0, warmup)
+    run(0, prime + warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(warmup, steps)
+    run(prime + warmup, steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out = {"config": "C2 with bf16 tables (fp32 Adam moments, fp32 compute), FusedTrainStep",
            "value": round(B * M * steps / dt, 1), "unit": "samples/s",
            "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warmup,
+           "prime_steps": prime,
+           "adam_steady_state": steady_state(prime, warmup, step.deferred.sweep_every),
            "table_bytes": 2 * (U + I) * D * 2, "final_loss": round(float(step.last_loss.item()), 6),
            "tolerance": "vs fp32 oracle: loss within 1% per step over 100 steps, eval prob "
                         "abs <= 2e-2 (tests/test_gpu_bf16.py)"}
@@ -240,7 +334,7 @@ def bf16_train(ncf, dev, cfg, batches, warmup, steps):
 C4 = dict(U=50_000_000, I=5_000_000, D=128, T=32, H=4, hid=[256, 128, 64], B=4096, M=5)
 
 
-def c4_train(ncf, dev, warmup, steps):
+def c4_train(ncf, dev, warmup, steps, prime=0):
     """BASELINE.json configs[3] / SURVEY 8(d) C4 on ONE MI355X: 50M users x 5M items, D=128,
     H=4 (hd 32), MLP [256,128,64], B=4096 groups x M=5.  The four fp32 tables (56.3 GB) and
     their Adam moments (112.6 GB) are resident in one GPU's 288 GB HBM, built there directly
@@ -268,15 +362,15 @@ def c4_train(ncf, dev, warmup, steps):
         for s in range(first, first + count):
             u, i, t = batches[s % len(batches)]
             step(u, i, t, next=batches[(s + 1) % len(batches)][:2])
-    run(0, warmup)
+    run(0, prime + warmup)
     torch.cuda.synchronize()
     ta = time.perf_counter()
-    run(warmup, steps)
+    run(prime + warmup, steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - ta
     loss = float(step.last_loss.item())
     L.PROFILE = []
-    for s in range(warmup + steps, warmup + steps + 20):
+    for s in range(prime + warmup + steps, prime + warmup + steps + 20):
         u, i, t = batches[s % len(batches)]
         step(u, i, t)
     torch.cuda.synchronize()
@@ -289,6 +383,8 @@ def c4_train(ncf, dev, warmup, steps):
                      "dropout 0.2, Adam lr 1e-3 wd 1e-5 (dense-exact, deferred), 1 GPU",
            "value": round(B * M * steps / dt, 1), "unit": "samples/s",
            "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warmup,
+           "prime_steps": prime,
+           "adam_steady_state": steady_state(prime, warmup, step.deferred.sweep_every),
            "table_params": 2 * (U + I) * D, "hbm_peak_GB": round(mem / 1e9, 1),
            "build_s": round(build_s, 1), "final_loss": round(loss, 6),
            "finite": bool(math.isfinite(loss)),
@@ -410,7 +506,12 @@ def main():
     # that its rolling sweep replays fewer zero-gradient steps per row than it will later, so
     # the default warm-up covers that transient and the timed region spans >= 3 sweep cycles
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=160)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--prime", type=int, default=-1,
+                    help="untimed priming steps before the warm-up of every training leg "
+                         "(default 2 x sweep_every = 128: deferred-Adam steady state)")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="test the --gpus N launcher: ranks join a gloo group and report (no GPU)")
     ap.add_argument("--users", type=int, default=1_000_000)
     ap.add_argument("--items", type=int, default=100_000)
     ap.add_argument("--groups", type=int, default=4096, help="interaction groups per GPU per step")
@@ -433,10 +534,17 @@ def main():
                     help="c4: only the C4 (50M x 5M, D=128) training line on one GPU")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 line of the default run")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started here before anything touches the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.dry_launch))
+    if args.dry_launch:
+        dry_launch()
+        return
+    prime = prime_steps(args)
     if args.config == "c4":
         torch.cuda.set_device(0)
         ncf = _ncf_pkg.load()
-        rec = c4_train(ncf, torch.device("cuda", 0), args.warmup, args.steps)
+        rec = c4_train(ncf, torch.device("cuda", 0), args.warmup, args.steps, prime)
         print(json.dumps({"metric": METRIC, **rec, "n_gpus": 1, "higher_is_better": True,
                           "dtype": "fp32", "data": "synthetic (users uniform, items Zipf(1.05))"}),
               flush=True)
@@ -445,6 +553,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr,
+              flush=True)
     sharded = world > 1 or args.sharded
     if sharded:
         dist.init_process_group("nccl")
@@ -490,14 +601,14 @@ def main():
             else:
                 fn(u, i, t)
 
-    # --- warm-up
-    run_steps(step, 0, args.warmup)
+    # --- priming (deferred-Adam steady state) + warm-up
+    run_steps(step, 0, prime + args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_steps(step, args.warmup, args.steps)
+    run_steps(step, prime + args.warmup, args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -518,7 +629,7 @@ def main():
     L.PROFILE = []
     torch.cuda.synchronize()
     run = step.eager if hasattr(step, "eager") else step   # the launches a graph replay runs
-    run_steps(run, args.warmup + args.steps, args.steps)
+    run_steps(run, prime + args.warmup + args.steps, args.steps)
     torch.cuda.synchronize()
     prof, L.PROFILE = L.PROFILE, None
 
@@ -570,7 +681,7 @@ def main():
         dfr0.flush(L.stream_ptr(dev))
         dfr0.overlap = False
         L.PROFILE = []
-        run_steps(run, args.warmup + 2 * args.steps, ISO_STEPS)
+        run_steps(run, prime + args.warmup + 2 * args.steps, ISO_STEPS)
         torch.cuda.synchronize()
         prof2, L.PROFILE = L.PROFILE, None
         dfr0.overlap = True
@@ -601,7 +712,7 @@ def main():
     # steady state: every stamp has been refreshed by a full sweep cycle after the first one
     # (rows start at stamp 0, so during steps < 2 x sweep_every a swept slice replays fewer
     # zero-gradient steps than later)
-    steady = bool(sweep_every) and args.warmup >= 2 * sweep_every
+    steady = steady_state(prime, args.warmup, sweep_every)
     # embedding gather / scatter: algorithmic HBM bytes per launch
     #   gather  (ncf_gather_ln_gmf_scaled_fwd): 4 rows of D fp32 + 2 int64 ids in, 4 LN'd rows
     #           (MLP + GMF, training) + mf_pred out = N (16 D + 16 + 16 D + 4)
@@ -655,12 +766,13 @@ def main():
     dropin = None
     if not sharded and not args.no_dropin:
         dropin = dropin_train(ncf, dev, (U, I, D, T, H, hid, B, M), batches, args.warmup,
-                              args.steps)
+                              args.steps, prime)
         dropin["vs_fused_step"] = round(dropin["value"] / samples_s, 4)
 
     bf16 = None
     if not sharded:
-        bf16 = bf16_train(ncf, dev, (U, I, D, T, H, hid, B, M), batches, args.warmup, args.steps)
+        bf16 = bf16_train(ncf, dev, (U, I, D, T, H, hid, B, M), batches, args.warmup, args.steps,
+                          prime)
         bf16["vs_fp32_step"] = round(bf16["value"] / samples_s, 4)
 
     c4 = None
@@ -670,7 +782,8 @@ def main():
         import subprocess
         try:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--config", "c4",
-                                "--warmup", str(args.warmup), "--steps", str(args.steps)],
+                                "--warmup", str(args.warmup), "--steps", str(args.steps),
+                                "--prime", str(prime)],
                                capture_output=True, text=True, timeout=600)
             line = [x for x in r.stdout.splitlines() if x.startswith("{")]
             c4 = json.loads(line[-1]) if r.returncode == 0 and line else {
@@ -730,6 +843,7 @@ def main():
                          "ms_per_step": round(gemm_ms, 4)},
             "embedding_hbm": hbm,
             "adam_steady_state": steady,
+            "prime_steps": prime,
             "table_adam": {"kernels": "deferred dense-exact Adam (catch-up + apply + 1/64 sweep)",
                            "ms_per_step": round(tab_ms, 4),
                            "sweep_us_per_step": round(1e3 * sweep_ms, 2),
@@ -737,7 +851,7 @@ def main():
                            "sweep_note": "with sweep_overlapped the sweep's time is its span on the "
                                          "side stream, beside the backward kernels",
                            "sweep_every": sweep_every,
-                           "steps_before_timing": args.warmup,
+                           "steps_before_timing": prime + args.warmup,
                            "dense_equivalent_GBps": round(tab_bytes / max(tab_ms * 1e-3, 1e-12) / 1e9, 1),
                            "note": "dense schedule bytes (24 B x 140.8M elements) / time: above "
                                    "HBM peak because untouched rows are caught up lazily"},
