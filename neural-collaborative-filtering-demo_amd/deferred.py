@@ -107,14 +107,19 @@ class DeferredTableAdam:
             return
         if self._hp_filled is None:
             first = 1
+            last = max(upto, first) + 4096
         elif self._hp_filled != hp:
             # an lr (or beta) change affects only steps not yet taken: the scalars of steps
-            # <= t stay as they were, so rows still behind replay those steps as taken
+            # <= t stay as they were, so rows still behind replay those steps as taken.  The
+            # filled horizon is refilled in place (no growth unless `upto` lies beyond it): a
+            # captured step graph holds this buffer's address
             first = min(self._filled + 1, self.t + 1)
+            last = self._filled if upto <= self._filled else upto + 4096
         else:
             first = self._filled + 1
+            last = max(upto, first) + 4096
         first = max(1, first)
-        last = max(upto, first) + 4096
+        last = max(last, first)
         host = np.empty(4 * (last - first + 1), dtype=np.float32)
         _lib.call("ncf_adam_step_scalars", self.lr, b1, b2, self.eps, first, last - first + 1,
                   host.ctypes.data)

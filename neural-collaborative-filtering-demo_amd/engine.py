@@ -64,7 +64,7 @@ class Workspace:
         self.a = [e(n, h) for h in g.hidden]
         self.mean = [e(n) for _ in g.hidden]
         self.rstd = [e(n) for _ in g.hidden]
-        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.err = None             # the engine-wide sticky id-error flag (NCFEngine.workspace)
         self.train = train
         self.cache = {}             # ctypes argument blocks built once per workspace
         if not train:
@@ -318,9 +318,21 @@ class NCFEngine:
             m = self.model
             g = Geometry(n=n, M=M, B=n // M, D=m.mlp_embedding_dim, T=m.temporal_dim,
                          H=m.num_heads, hidden=list(m.mlp_hidden_dims))
-            w = Workspace(g, self.model.mf_norm.weight.device, train)
+            dev = self.model.mf_norm.weight.device
+            w = Workspace(g, dev, train)
+            w.err = self.err_flag(dev)
             self.ws[key] = w
         return w
+
+    def err_flag(self, dev) -> torch.Tensor:
+        """One sticky out-of-range-id flag per engine, shared by every workspace's kernels: a
+        bad id in any batch geometry (a short last batch included) raises it until a check
+        reads and clears it."""
+        f = getattr(self, "_err", None)
+        if f is None or f.device != dev:
+            f = self._err = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._err_async = None
+        return f
 
     @staticmethod
     def _gemm(A, lda, a_t, Bm, ldb, b_t, C, ldc, M, N, K, bias=None, relu=False, accum=False, st=None):
@@ -346,6 +358,10 @@ class NCFEngine:
         otherwise).  Called before anything other than the fused train step reads a table."""
         if self.deferred is not None:
             self.deferred.sync()
+        if getattr(self, "_err_async", None) is not None:
+            # a training run checked ids asynchronously: settle what its last steps saw
+            self._err_async = None
+            self.check_ids(None)
 
     def lagging(self) -> bool:
         """Whether a deferred optimizer holds table rows behind (a sync_tables would sweep)."""
@@ -570,11 +586,14 @@ class NCFEngine:
             x, ldx, kin = yt, D + Tt, D + Tt
         return x, ldx, kin
 
-    def check_ids(self, w: Workspace):
-        """Raise IndexError if a forward on this workspace since the last check saw an
-        out-of-range id (the flag is sticky between checks; one host sync)."""
-        if int(w.err.item()):
-            w.err.zero_()
+    def check_ids(self, w: Optional[Workspace] = None):
+        """Raise IndexError if any forward of this engine since the last check saw an
+        out-of-range id (the engine-wide flag is sticky between checks; one host sync)."""
+        f = getattr(self, "_err", None)
+        if f is None:
+            return
+        if int(f.item()):
+            f.zero_()
             raise IndexError("AdvancedNCF: user/product id out of range of the embedding tables")
 
     ID_CHECK_EVERY = 16
@@ -586,6 +605,7 @@ class NCFEngine:
         touches memory out of bounds (the kernels read / update row 0 instead and raise the
         flag), so the error surfaces at most a few steps after the faulty batch ran on the
         GPU; ``check_ids`` (eval, and ``model.validate_ids = "sync"``) is immediate."""
+        f = w.err
         a = getattr(self, "_err_async", None)
         if a is None:
             a = self._err_async = {"host": torch.zeros(1, dtype=torch.int32, pin_memory=True),
@@ -595,13 +615,13 @@ class NCFEngine:
                 return
             a["pending"] = False
             if int(a["host"][0]):
-                w.err.zero_()
+                f.zero_()
                 raise IndexError("AdvancedNCF: user/product id out of range of the embedding "
                                  "tables (seen by a training step in flight)")
         a["k"] += 1
         if a["k"] % self.ID_CHECK_EVERY:
             return
-        a["host"].copy_(w.err, non_blocking=True)
+        a["host"].copy_(f, non_blocking=True)
         a["ev"].record()
         a["pending"] = True
 

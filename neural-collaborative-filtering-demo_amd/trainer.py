@@ -257,6 +257,8 @@ class FusedTrainStep:
                         eng.fork_hook = hook
             w = self._body(user_ids, item_ids, targets, M)
             m.engine.fork_hook = None     # (a fork point the step did not pass: no prefetch)
+            if getattr(m, "validate_ids", True):
+                m.engine.check_ids_async(w)     # out-of-range ids raise a few steps later
             self.step_count += 1
             m.engine.updates += 1
             self.last_loss = w.loss
@@ -264,8 +266,15 @@ class FusedTrainStep:
         dev = m.engine.flat.device
         shape = (user_ids.numel(), item_ids.numel(), targets.numel(), M)
         d = self.deferred
-        if d._hp_filled is not None and d._hp_filled != (d.lr,) + tuple(d.betas):
-            d._ensure(d._filled)        # lr changed: refill steps > t in place (same buffer)
+        if d._hp_filled is not None and d._hp_filled != (d.lr,) + tuple(d.betas) + (d.eps,):
+            # lr changed: refill steps > t in place.  The graph reads the table by address, so
+            # it stays valid unless the buffer moved (then re-capture)
+            table_at = d._table.data_ptr()
+            d._ensure(d._filled)
+            if d._table.data_ptr() != table_at:
+                self._g = None
+        if self._g is not None and self._g_consts != d._consts():
+            self._g = None              # betas / eps / weight decay are launch arguments
         horizon_ok = d._filled >= d.t + 2
         if self._g is None or self._shape != shape or not horizon_ok:
             if self._eager_steps < self.warmup or not horizon_ok:
@@ -313,7 +322,7 @@ class FusedTrainStep:
             self._w = self._body(*self._static, M)
         d.t, self.step_count = t0, sc        # capturing executes nothing
         self.model.engine.pending = None
-        self._g, self._shape = g, shape
+        self._g, self._shape, self._g_consts = g, shape, d._consts()
 
     def sync(self):
         if self.deferred is not None:

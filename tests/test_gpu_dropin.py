@@ -256,6 +256,52 @@ def test_out_of_range_id_in_training_raises_without_sync():
         m(kjt(u, i))
 
 
+def test_bad_id_in_a_rare_batch_geometry_is_reported():
+    """The id-error flag is engine-wide: a bad id in a short last batch (its own workspace,
+    used once) is reported by the asynchronous check of later full batches, or at the latest
+    by the next table read (state_dict), and the flag that fired is the one cleared."""
+    m = model()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+    crit = torch.nn.BCELoss()
+    data = batches(2, seed=31)
+    u, i, t = data[0]
+    short = (u[:2 * M].clone(), i[:2 * M].clone(), t[:2 * M])
+    short[1][1] = I + 7
+    m.train()
+
+    def step(u, i, t):
+        loss = crit(m(kjt(u, i)), t)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    step(*short)
+    with pytest.raises(IndexError):
+        for _ in range(4 * m.engine.ID_CHECK_EVERY):
+            step(*data[1])
+            torch.cuda.synchronize()
+    step(*data[1])                       # cleared: the following good steps run
+    m.state_dict()
+    step(*short)                         # one more bad short batch, then a table read
+    torch.cuda.synchronize()
+    with pytest.raises(IndexError):
+        m.state_dict()
+    m.state_dict()
+
+
+def test_fused_step_reports_bad_ids():
+    """FusedTrainStep checks ids asynchronously too (it used to never look at the flag)."""
+    from ncf_amd.trainer import FusedTrainStep
+    m = model()
+    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+    u, i, t = batches(1, seed=32)[0]
+    i = i.clone()
+    i[7] = I
+    with pytest.raises(IndexError):
+        for _ in range(4 * m.engine.ID_CHECK_EVERY):
+            step(u, i, t)
+            torch.cuda.synchronize()
+
+
 def test_trainer_train_epoch_runs_reference_loop():
     """ModelTrainer.train_epoch (trainer.py:216-337 mirror) over a device-sampled epoch."""
     from ncf_amd.trainer import ModelTrainer

@@ -91,7 +91,8 @@ def test_train_goldens(fx, nl, materialize, request):
     lr, wd = [float(x) for x in g["hparams"]]
     rec = _train_run(g, nl, materialize)
     for s in range(steps):
-        assert np.abs(rec[f"prob{s}"] - g[f"step{s}/prob"]).max() < 2e-6, s
+        # fp32 forward abs 1e-6 (measured <= 3.9e-7 for F2, round 3)
+        assert np.abs(rec[f"prob{s}"] - g[f"step{s}/prob"]).max() < 1e-6, s
         assert abs(rec[f"loss{s}"] - float(g[f"step{s}/loss"])) < 2e-6, s
     if materialize:
         gold = sub(g, "grad0/")
@@ -451,7 +452,7 @@ def test_non_adam_optimizer_gets_dense_table_grads(f2):
 
 # ----------------------------------------------------------------------------- deferred Adam
 def _fused_run(deferred, steps, sweep_every=64, U=3000, I=500, B=64, seed=11, dropout=0.0,
-               **kw):
+               lr_at=None, **kw):
     from ncf_amd.trainer import FusedTrainStep
     torch.manual_seed(seed)
     m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, dropout, 4).to(DEV)
@@ -463,6 +464,8 @@ def _fused_run(deferred, steps, sweep_every=64, U=3000, I=500, B=64, seed=11, dr
         i = torch.randint(0, I, (B * 5,), generator=g).to(DEV)
         t = torch.zeros(B, 5)
         t[:, 0] = 1
+        if lr_at and s in lr_at:
+            step.lr = lr_at[s]          # (a scheduler's change between steps)
         step(u, i, t.reshape(-1, 1).to(DEV))
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}   # syncs deferred rows
     step.sync()
@@ -729,6 +732,22 @@ def test_graph_replay_bitwise_equals_eager_clock():
     a rolling-sweep wrap (70 steps)."""
     a_sd, a_m = _fused_run(True, 70, dropout=0.2, clock=True)
     b_sd, b_m = _fused_run(True, 70, dropout=0.2, graph=True)
+    for k in a_sd:
+        assert torch.equal(a_sd[k], b_sd[k]), k
+    for k in a_m:
+        assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
+
+
+def test_graph_replay_lr_change_bitwise_equals_eager_clock():
+    """An lr change between steps (ReduceLROnPlateau-style, the reference's scheduler) under
+    graph=True: the per-step scalar table is refilled in place, so the captured graph keeps
+    reading live scalars (or is re-captured when the buffer had to move); bit for bit the same
+    as the eager clock path taking the same changes."""
+    lr_at = {10: 5e-4, 40: 2.5e-4, 41: 3e-4}
+    a_sd, a_m = _fused_run(True, 70, dropout=0.2, clock=True, lr_at=lr_at)
+    b_sd, b_m = _fused_run(True, 70, dropout=0.2, graph=True, lr_at=lr_at)
+    c_sd, _ = _fused_run(True, 70, dropout=0.2, clock=True)
+    assert any(not torch.equal(a_sd[k], c_sd[k]) for k in a_sd)      # the changes took effect
     for k in a_sd:
         assert torch.equal(a_sd[k], b_sd[k]), k
     for k in a_m:
