@@ -1,5 +1,6 @@
 // The whole attention block of AdvancedNCF in one launch per direction: Q/K/V projections, the
-// per-group multi-head core and out_proj, for D = 64 and groups of M <= 6 rows.
+// per-group multi-head core and out_proj, for D = 64 (C2) or D = 128 (C4) and groups of M <= 6
+// rows.
 //
 // Reference: MultiHeadAttention.forward (src/model/architecture.py:18-57) as AdvancedNCF.forward
 // calls it (:315-326): q = LN(user_mlp rows), k = v = LN(item_mlp rows), groups of
@@ -8,136 +9,175 @@
 // unfused path (gemm_rows.hip x4 + attention.hip); only the fmaf order of the projections
 // differs (the k-permuted MFMA below).
 //
-// Tiling: a 512-thread workgroup owns 16 interaction groups = R = 16*M rows, so every group is
-// whole inside it and the core never leaves LDS.  The projections are 16x16 output tiles of
-// v_mfma_f32_16x16x4_f32 over K = 64: wave w owns output columns [16(w&3), +16) for the row
-// tiles of parity w>>2 (two waves per SIMD), its weight fragment (16 floats per lane) loaded
-// once.  k-permuted operands: in MFMA
-// step s, lane group g = lane>>4 supplies k = 16g + s, so each lane's A row slice and B weight
-// slice are 16 contiguous floats (4 x ds_read_b128 / global float4).  Rows are staged in LDS
-// with a 68-float pitch (conflict-free 16-row x 4-slice fragment reads).
+// Tiling: a 512-thread workgroup owns G interaction groups (G = 16 at D = 64, 8 at D = 128: the
+// backward's five row buffers must fit the 160 KB of LDS) = R = G*M rows, padded with zero rows
+// to NT = ceil(R/16) row tiles, so every group is whole inside it and the core never leaves LDS.
+// The projections are 16x16 output tiles of v_mfma_f32_16x16x4_f32 over K = D: with CS = D/16
+// column slices, wave w owns output columns [16(w%CS), +16) for the row tiles rt = w/CS (mod
+// 8/CS) (D = 64: two waves per column slice, row tiles of either parity; D = 128: one wave per
+// slice, every row tile), its weight fragment (D/4 floats per lane) loaded once.  k-permuted
+// operands: in MFMA step s, lane group g = lane>>4 supplies k = (D/4)g + s, so each lane's A row
+// slice and B weight slice are D/4 contiguous floats (ds_read_b128 / global float4 runs).  Rows
+// are staged in LDS with a (D+4)-float pitch (conflict-free 16-row x 4-slice fragment reads).
 //
-// Forward LDS: S0 = X_u -> Q -> O, S1 = X_i -> K -> Y, S2 = V   (3 x R x 68 floats)
+// Forward LDS: S0 = X_u -> Q -> O, S1 = X_i -> K -> Y, S2 = V   (3 x 16NT x (D+4) floats)
 // Backward LDS: S0 = dY -> dO -> dX_u, S1 = Q -> dK -> dX_i, S2 = K -> dQ, S3 = V -> dV, + dS
 #include "ncf_common.h"
 
 namespace {
 
-constexpr int kD = 64;
-constexpr int kPitch = 68;
-constexpr int kGroups = 16;   // interaction groups per workgroup
 constexpr int kMaxM = 6;
-constexpr int kThreads = 512;   // 8 waves: wave w owns column slice (w & 3), row tiles of parity (w >> 2)
+constexpr int kThreads = 512;   // 8 waves
+
+// Geometry per embedding width D (64: C2, 128: C4)
+template <int D>
+struct AG {
+  static constexpr int kPitch = D + 4;
+  static constexpr int kGroups = D == 64 ? 16 : 8;   // interaction groups per workgroup
+  static constexpr int CS = D / 16;                  // 16-column output slices
+  static constexpr int RP = 8 / CS;                  // waves per column slice (row-tile stride)
+  static constexpr int KF = D / 4;                   // k values of one lane's MFMA fragment
+  static constexpr int NTmax = (kGroups * kMaxM + 15) / 16;   // row tiles per workgroup (max)
+  static constexpr int kLinW = D * D + D;            // one Linear's weight + bias
+  static constexpr int kPartAttn = 4 * kLinW;        // the four Linears' partials
+  __device__ __host__ static int nt(int M) { return (kGroups * M + 15) / 16; }
+};
+static_assert(AG<64>::NTmax == kMaxM && AG<128>::NTmax == 3, "row tiles");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// acc += A[16 rows at X, 64 k] . B (B fragment: this lane's 16 k values)
-__device__ __forceinline__ f32x4 tile_mfma(const float* __restrict__ X, const float (&b)[16],
+// acc += A[16 rows at X, D k] . B (B fragment: this lane's D/4 k values)
+template <int D>
+__device__ __forceinline__ f32x4 tile_mfma(const float* __restrict__ X, const float (&b)[D / 4],
                                            f32x4 acc) {
+  constexpr int KF = D / 4;
   const int l = threadIdx.x & 63;
-  const float* a = X + (l & 15) * kPitch + 16 * (l >> 4);
-  float av[16];
+  const float* a = X + (l & 15) * AG<D>::kPitch + KF * (l >> 4);
+  float av[KF];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < KF / 4; ++q) {
     const float4 v = *reinterpret_cast<const float4*>(a + 4 * q);
     av[4 * q] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
   }
 #pragma unroll
-  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], b[s], acc, 0, 0, 0);
+  for (int s = 0; s < KF; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], b[s], acc, 0, 0, 0);
   return acc;
 }
 
-// B fragment of x W^T (forward): B[k][j] = W[j][k], j = 16w + (lane & 15), k = 16g + s
-__device__ __forceinline__ void frag_wt(const float* __restrict__ W, int w, float (&b)[16]) {
+// B fragment of x W^T (forward): B[k][j] = W[j][k], j = 16w + (lane & 15), k = (D/4)g + s
+template <int D>
+__device__ __forceinline__ void frag_wt(const float* __restrict__ W, int w, float (&b)[D / 4]) {
+  constexpr int KF = D / 4;
   const int l = threadIdx.x & 63;
-  const float* p = W + (16 * w + (l & 15)) * kD + 16 * (l >> 4);
+  const float* p = W + (16 * w + (l & 15)) * D + KF * (l >> 4);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < KF / 4; ++q) {
     const float4 v = ld4(p + 4 * q);
     b[4 * q] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
   }
 }
 
-// B fragment of dz W (backward): B[k][j] = W[k][j], j = 16w + (lane & 15), k = 16g + s
-__device__ __forceinline__ void frag_w(const float* __restrict__ W, int w, float (&b)[16]) {
+// B fragment of dz W (backward): B[k][j] = W[k][j], j = 16w + (lane & 15), k = (D/4)g + s
+template <int D>
+__device__ __forceinline__ void frag_w(const float* __restrict__ W, int w, float (&b)[D / 4]) {
+  constexpr int KF = D / 4;
   const int l = threadIdx.x & 63;
-  const float* p = W + (16 * (l >> 4)) * kD + 16 * w + (l & 15);
+  const float* p = W + (KF * (l >> 4)) * D + 16 * w + (l & 15);
 #pragma unroll
-  for (int s = 0; s < 16; ++s) b[s] = p[s * kD];
+  for (int s = 0; s < KF; ++s) b[s] = p[s * D];
 }
 
 // C fragment (rows 4g + r of the row tile, column 16w + (lane & 15)) -> LDS
+template <int D>
 __device__ __forceinline__ void put_tile(float* __restrict__ S, int rt, int w, f32x4 c) {
+  constexpr int P = AG<D>::kPitch;
   const int l = threadIdx.x & 63;
-  float* p = S + (16 * rt + 4 * (l >> 4)) * kPitch + 16 * w + (l & 15);
+  float* p = S + (16 * rt + 4 * (l >> 4)) * P + 16 * w + (l & 15);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) p[r * kPitch] = c[r];
+  for (int r = 0; r < 4; ++r) p[r * P] = c[r];
 }
 
+// Rp (padded) rows into LDS; rows >= `rows` are zeros
+template <int D>
 __device__ __forceinline__ void stage_in(float* __restrict__ S, const float* __restrict__ X,
-                                         int R, int rows) {
-  for (int e = threadIdx.x; e < R * 16; e += blockDim.x) {
-    const int r = e >> 4, c = (e & 15) * 4;
-    const float4 v = r < rows ? ld4(X + (int64_t)r * kD + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(S + r * kPitch + c) = v;
+                                         int Rp, int rows) {
+  constexpr int L = D / 4;
+  for (int e = threadIdx.x; e < Rp * L; e += blockDim.x) {
+    const int r = e / L, c = (e % L) * 4;
+    const float4 v = r < rows ? ld4(X + (int64_t)r * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(S + r * AG<D>::kPitch + c) = v;
   }
 }
 
+template <int D>
 __device__ __forceinline__ void stage_out(float* __restrict__ X, const float* __restrict__ S,
                                           int rows) {
-  for (int e = threadIdx.x; e < rows * 16; e += blockDim.x) {
-    const int r = e >> 4, c = (e & 15) * 4;
-    st4(X + (int64_t)r * kD + c, *reinterpret_cast<const float4*>(S + r * kPitch + c));
+  constexpr int L = D / 4;
+  for (int e = threadIdx.x; e < rows * L; e += blockDim.x) {
+    const int r = e / L, c = (e % L) * 4;
+    st4(X + (int64_t)r * D + c, *reinterpret_cast<const float4*>(S + r * AG<D>::kPitch + c));
   }
 }
 
-// out[rt] = X . W^T + bias for the M row tiles of this wave's column slice
+// whether row tile rt is this wave's (column slice w % CS, row tiles w / CS + RP j)
+template <int D>
+__device__ __forceinline__ bool my_tile(int rt, int NT) {
+  return rt < NT && rt % AG<D>::RP == (int)(threadIdx.x >> 6) / AG<D>::CS;
+}
+template <int D>
+__device__ __forceinline__ int my_slice() { return (int)(threadIdx.x >> 6) % AG<D>::CS; }
+
+// out[rt] = X . W^T + bias for this wave's row tiles of its column slice
+template <int D>
 __device__ __forceinline__ void project(const float* __restrict__ X, const float* __restrict__ W,
-                                        const float* __restrict__ bias, int M, f32x4 (&out)[kMaxM]) {
-  const int w = (threadIdx.x >> 6) & 3;
-  float b[16];
-  frag_wt(W, w, b);
+                                        const float* __restrict__ bias, int NT, f32x4 (&out)[kMaxM]) {
+  const int w = my_slice<D>();
+  float b[D / 4];
+  frag_wt<D>(W, w, b);
   const float bb = bias ? bias[16 * w + (threadIdx.x & 15)] : 0.0f;
 #pragma unroll
-  for (int rt = 0; rt < kMaxM; ++rt) {
-    if (rt < M && (rt & 1) == (threadIdx.x >> 8)) {
+  for (int rt = 0; rt < AG<D>::NTmax; ++rt) {
+    if (my_tile<D>(rt, NT)) {
       f32x4 acc = {bb, bb, bb, bb};
       // bias first, then the k chain: fmaf(..., bias) order of the unfused GEMM epilogue
       // differs only in rounding (tolerance-level)
-      out[rt] = tile_mfma(X + 16 * rt * kPitch, b, acc);
+      out[rt] = tile_mfma<D>(X + 16 * rt * AG<D>::kPitch, b, acc);
     }
   }
 }
 
 // Weight-gradient tiles of a Linear over this workgroup's rows: dW[a][b] = sum_r dY[r][a] X[r][b]
-// (contraction over the R rows: k-permuted, lane group g covers rows [g R/4, (g+1) R/4)), written
-// to out[64 x 64]; tiles t = wave + 8q of the 16 per weight.  Rows past the batch are zero in LDS.
+// (contraction over the Rp padded rows: k-permuted, lane group g covers rows [g Rp/4, (g+1)
+// Rp/4)), written to out[D x D].  Rows past the batch are zero in LDS.
+template <int D>
 __device__ __forceinline__ void wgrad_tile(const float* __restrict__ dYs,
-                                           const float* __restrict__ Xs, int R, int tj, int tk,
+                                           const float* __restrict__ Xs, int Rp, int tj, int tk,
                                            float* __restrict__ out) {
+  constexpr int P = AG<D>::kPitch;
   const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-  const int R4 = R >> 2;
-  const float* a = dYs + (g * R4) * kPitch + 16 * tj + i;
-  const float* b = Xs + (g * R4) * kPitch + 16 * tk + i;
+  const int R4 = Rp >> 2;
+  const float* a = dYs + (g * R4) * P + 16 * tj + i;
+  const float* b = Xs + (g * R4) * P + 16 * tk + i;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   int s = 0;
   for (; s + 1 < R4; s += 2) {
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s * kPitch], b[s * kPitch], acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[(s + 1) * kPitch], b[(s + 1) * kPitch], acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s * P], b[s * P], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[(s + 1) * P], b[(s + 1) * P], acc1, 0, 0, 0);
   }
-  if (s < R4) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s * kPitch], b[s * kPitch], acc0, 0, 0, 0);
-  float* o = out + (16 * tj + 4 * g) * kD + 16 * tk + i;
+  if (s < R4) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s * P], b[s * P], acc0, 0, 0, 0);
+  float* o = out + (16 * tj + 4 * g) * D + 16 * tk + i;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) o[r * kD] = acc0[r] + acc1[r];
+  for (int r = 0; r < 4; ++r) o[r * D] = acc0[r] + acc1[r];
 }
 
-// bias gradient columns: out[c] = sum_r dY[r][c]; 64 threads per vector starting at thread t0
-__device__ __forceinline__ void bias_cols(const float* __restrict__ dYs, int R, int t0,
+// bias gradient columns: out[c] = sum_r dY[r][c]; D threads per vector starting at thread t0
+template <int D>
+__device__ __forceinline__ void bias_cols(const float* __restrict__ dYs, int Rp, int t0,
                                           float* __restrict__ out) {
   const int c = (int)threadIdx.x - t0;
-  if (c < 0 || c >= kD) return;
+  if (c < 0 || c >= D) return;
   float acc = 0.0f;
-  for (int r = 0; r < R; ++r) acc += dYs[r * kPitch + c];
+  for (int r = 0; r < Rp; ++r) acc += dYs[r * AG<D>::kPitch + c];
   out[c] = acc;
 }
 
@@ -147,13 +187,13 @@ __device__ __forceinline__ void bias_cols(const float* __restrict__ dYs, int R, 
 // probabilities go to Pg (global, [B][H][M][M]) and/or Pl (LDS, [16][H][M][M]) when given.  Os
 // may alias Qs: every lane finishes reading Q/K/V before the first store.  Shared by the forward
 // and the backward's recompute, so both produce the same bits.
-template <int HD>
+template <int D, int HD>
 __device__ __forceinline__ void attn_core_fwd(const float* Qs, const float* Ks, const float* Vs,
                                               float* Os, float* Pl, float* __restrict__ Pg,
                                               int64_t g0, int ng, int M, float scale,
                                               float p_drop, uint64_t seed) {
-  constexpr int H = kD / HD;
-  constexpr int kIt = (kGroups * H * kMaxM + kThreads - 1) / kThreads;
+  constexpr int H = D / HD, kPitch = AG<D>::kPitch;
+  constexpr int kIt = (AG<D>::kGroups * H * kMaxM + kThreads - 1) / kThreads;
   const float inv_keep = p_drop > 0.0f ? 1.0f / (1.0f - p_drop) : 1.0f;
   const int ntask = ng * H * M;
   float o[kIt][HD];
@@ -214,10 +254,9 @@ __device__ __forceinline__ void attn_core_fwd(const float* Qs, const float* Ks, 
 
 // per-workgroup partial of the four Linear gradients, in the flat parameter order
 // [q.weight | q.bias | k.weight | k.bias | v.weight | v.bias | out.weight | out.bias]
-constexpr int kLinW = kD * kD + kD;
-constexpr int kPartAttn = 4 * kLinW;
+// (AG<D>::kPartAttn floats)
 
-template <int HD>
+template <int D, int HD>
 __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
     const float* __restrict__ xu, const float* __restrict__ xi, int64_t B, int M,
     const float* __restrict__ wq, const float* __restrict__ bq, const float* __restrict__ wk,
@@ -226,67 +265,68 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
     uint64_t seed, const ncf_step_clock* clock, float* __restrict__ Q, float* __restrict__ K,
     float* __restrict__ V, float* __restrict__ P, float* __restrict__ O, float* __restrict__ Y,
     int core) {
+  using G = AG<D>;
+  constexpr int kPitch = G::kPitch;
   extern __shared__ float lds[];
-  const int R = kGroups * M;
+  const int NT = G::nt(M), Rp = 16 * NT;
   float* S0 = lds;
-  float* S1 = lds + R * kPitch;
-  float* S2 = lds + 2 * R * kPitch;
-  const int64_t g0 = (int64_t)blockIdx.x * kGroups;
-  const int ng = (int)min<int64_t>(kGroups, B - g0);
+  float* S1 = lds + Rp * kPitch;
+  float* S2 = lds + 2 * Rp * kPitch;
+  const int64_t g0 = (int64_t)blockIdx.x * G::kGroups;
+  const int ng = (int)min<int64_t>(G::kGroups, B - g0);
   const int rows = ng * M;
   const int64_t r0 = g0 * M;
-  const int w = (threadIdx.x >> 6) & 3;
-  const int par = threadIdx.x >> 8;
+  const int w = my_slice<D>();
   // core == 0: eval with one item per group (softmax == 1, o = v).  Q/K/P/O may be NULL with
   // the core on: nothing is stashed (the backward recomputes it from X_u / X_i)
   if (clock) seed += clock->seed;
 
-  if (core) stage_in(S0, xu + r0 * kD, R, rows);
-  stage_in(S1, xi + r0 * kD, R, rows);
+  if (core) stage_in<D>(S0, xu + r0 * D, Rp, rows);
+  stage_in<D>(S1, xi + r0 * D, Rp, rows);
   __syncthreads();
   f32x4 fq[kMaxM], fk[kMaxM], fv[kMaxM];
-  project(S1, wv, bv, M, fv);
+  project<D>(S1, wv, bv, NT, fv);
   if (core) {
-    project(S0, wq, bq, M, fq);
-    project(S1, wk, bk, M, fk);
+    project<D>(S0, wq, bq, NT, fq);
+    project<D>(S1, wk, bk, NT, fk);
   }
   __syncthreads();
 #pragma unroll
-  for (int rt = 0; rt < kMaxM; ++rt)
-    if (rt < M && (rt & 1) == par) {
-      put_tile(S2, rt, w, fv[rt]);
+  for (int rt = 0; rt < G::NTmax; ++rt)
+    if (my_tile<D>(rt, NT)) {
+      put_tile<D>(S2, rt, w, fv[rt]);
       if (core) {
-        put_tile(S0, rt, w, fq[rt]);
-        put_tile(S1, rt, w, fk[rt]);
+        put_tile<D>(S0, rt, w, fq[rt]);
+        put_tile<D>(S1, rt, w, fk[rt]);
       }
     }
   __syncthreads();
   const float* src = S2;   // the out_proj input: O, or V when there is no core
   if (core) {
-    if (Q) stage_out(Q + r0 * kD, S0, rows);
-    if (K) stage_out(K + r0 * kD, S1, rows);
-    if (V) stage_out(V + r0 * kD, S2, rows);
-    attn_core_fwd<HD>(S0, S1, S2, S0, nullptr, P, g0, ng, M, scale, p_drop, seed);
+    if (Q) stage_out<D>(Q + r0 * D, S0, rows);
+    if (K) stage_out<D>(K + r0 * D, S1, rows);
+    if (V) stage_out<D>(V + r0 * D, S2, rows);
+    attn_core_fwd<D, HD>(S0, S1, S2, S0, nullptr, P, g0, ng, M, scale, p_drop, seed);
     __syncthreads();
-    if (O) stage_out(O + r0 * kD, S0, rows);
+    if (O) stage_out<D>(O + r0 * D, S0, rows);
     src = S0;
   } else if (V) {
-    stage_out(V + r0 * kD, S2, rows);
+    stage_out<D>(V + r0 * D, S2, rows);
   }
   // out_proj -> S1 (K is dead) -> Y
   f32x4 fy[kMaxM];
-  project(src, wo, bo, M, fy);
+  project<D>(src, wo, bo, NT, fy);
 #pragma unroll
-  for (int rt = 0; rt < kMaxM; ++rt)
-    if (rt < M && (rt & 1) == par) put_tile(S1, rt, w, fy[rt]);
+  for (int rt = 0; rt < G::NTmax; ++rt)
+    if (my_tile<D>(rt, NT)) put_tile<D>(S1, rt, w, fy[rt]);
   __syncthreads();
-  stage_out(Y + r0 * kD, S1, rows);
+  stage_out<D>(Y + r0 * D, S1, rows);
 }
 
 // RC (recompute): nothing was stashed by the forward.  Q, K, V are re-projected from X_u / X_i
 // and the core forward (P, O) re-run in LDS with the forward's own code (attn_core_fwd: the same
 // bits), instead of reading 4 stashed [rows][64] blocks and P back from HBM.
-template <int HD, bool RC>
+template <int D, int HD, bool RC>
 __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     const float* __restrict__ dY, const float* __restrict__ Qg, const float* __restrict__ Kg,
     const float* __restrict__ Vg, const float* __restrict__ Pg, int64_t B, int M,
@@ -297,55 +337,56 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     float* __restrict__ dK, float* __restrict__ dV, float* __restrict__ dXu,
     float* __restrict__ dXi, const float* __restrict__ bq, const float* __restrict__ bk,
     const float* __restrict__ bv) {
-  constexpr int H = kD / HD;
+  using G = AG<D>;
+  constexpr int kPitch = G::kPitch, kGroups = G::kGroups, kLinW = G::kLinW, L4 = D / 4;
+  constexpr int H = D / HD;
   constexpr int kIt = (kGroups * H * kMaxM + kThreads - 1) / kThreads;
   extern __shared__ float lds[];
-  const int R = kGroups * M;
+  const int NT = G::nt(M), Rp = 16 * NT;
   float* S0 = lds;
-  float* S1 = lds + R * kPitch;
-  float* S2 = lds + 2 * R * kPitch;
-  float* S3 = lds + 3 * R * kPitch;
+  float* S1 = lds + Rp * kPitch;
+  float* S2 = lds + 2 * Rp * kPitch;
+  float* S3 = lds + 3 * Rp * kPitch;
   const bool wg = RC || part != nullptr;   // fused weight gradients (partials of this workgroup)
-  float* S4 = lds + 4 * R * kPitch;                 // O -> X_u (fused weight gradients only)
-  float* dS = lds + (wg ? 5 : 4) * R * kPitch;      // [16][H][M][M]
+  float* S4 = lds + 4 * Rp * kPitch;                // O -> X_u (fused weight gradients only)
+  float* dS = lds + (wg ? 5 : 4) * Rp * kPitch;     // [G][H][M][M]
   float* Pl = dS + kGroups * H * M * M;             // RC: the recomputed P, same layout
   const int64_t g0 = (int64_t)blockIdx.x * kGroups;
   const int ng = (int)min<int64_t>(kGroups, B - g0);
   const int rows = ng * M;
   const int64_t r0 = g0 * M;
-  const int w = (threadIdx.x >> 6) & 3;
-  const int par = threadIdx.x >> 8;
+  const int w = my_slice<D>();
   if (clock) seed += clock->seed;
   const float inv_keep = p_drop > 0.0f ? 1.0f / (1.0f - p_drop) : 1.0f;
 
-  stage_in(S0, dY + r0 * kD, R, rows);
-  constexpr int kPre = (16 * kMaxM * 16 + kThreads - 1) / kThreads;   // float4 per thread
+  stage_in<D>(S0, dY + r0 * D, Rp, rows);
+  constexpr int kPre = (16 * G::NTmax * L4 + kThreads - 1) / kThreads;   // float4 per thread
   float4 pu[kPre], pi[kPre];   // X_u / X_i rows for the fused weight gradients
   if constexpr (RC) {
-    stage_in(S1, Xu + r0 * kD, R, rows);
-    stage_in(S2, Xi + r0 * kD, R, rows);
+    stage_in<D>(S1, Xu + r0 * D, Rp, rows);
+    stage_in<D>(S2, Xi + r0 * D, Rp, rows);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kPre; ++q) {   // (zero rows past the batch: staged as zeros)
       const int e = threadIdx.x + kThreads * q;
-      const bool in = e < R * 16;
-      pu[q] = in ? *reinterpret_cast<const float4*>(S1 + (e >> 4) * kPitch + (e & 15) * 4)
+      const bool in = e < Rp * L4;
+      pu[q] = in ? *reinterpret_cast<const float4*>(S1 + (e / L4) * kPitch + (e % L4) * 4)
                  : make_float4(0.f, 0.f, 0.f, 0.f);
-      pi[q] = in ? *reinterpret_cast<const float4*>(S2 + (e >> 4) * kPitch + (e & 15) * 4)
+      pi[q] = in ? *reinterpret_cast<const float4*>(S2 + (e / L4) * kPitch + (e % L4) * 4)
                  : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     f32x4 fq[kMaxM], fk[kMaxM], fv[kMaxM];
-    project(S1, wq, bq, M, fq);
-    project(S2, wk, bk, M, fk);
-    project(S2, wv, bv, M, fv);
+    project<D>(S1, wq, bq, NT, fq);
+    project<D>(S2, wk, bk, NT, fk);
+    project<D>(S2, wv, bv, NT, fv);
     __syncthreads();
     // rows past the batch (a ragged last workgroup) hold zeros, as the stashing form stages
     // them: the bias columns of dQ/dK/dV later sum over all R rows of these buffers
     const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
     const int rsub = 4 * ((threadIdx.x & 63) >> 4);
 #pragma unroll
-    for (int rt = 0; rt < kMaxM; ++rt)
-      if (rt < M && (rt & 1) == par) {
+    for (int rt = 0; rt < G::NTmax; ++rt)
+      if (my_tile<D>(rt, NT)) {
         const bool pad = 16 * rt + rsub + 3 >= rows;
         f32x4 a = fq[rt], b = fk[rt], c = fv[rt];
         if (pad) {
@@ -353,57 +394,57 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
           for (int e = 0; e < 4; ++e)
             if (16 * rt + rsub + e >= rows) { a[e] = 0.f; b[e] = 0.f; c[e] = 0.f; }
         }
-        put_tile(S1, rt, w, a);
-        put_tile(S2, rt, w, b);
-        put_tile(S3, rt, w, c);
-        if (16 * rt + rsub + 3 >= rows) put_tile(S4, rt, w, z4);   // O of padded rows
+        put_tile<D>(S1, rt, w, a);
+        put_tile<D>(S2, rt, w, b);
+        put_tile<D>(S3, rt, w, c);
+        if (16 * rt + rsub + 3 >= rows) put_tile<D>(S4, rt, w, z4);   // O of padded rows
       }
     __syncthreads();
-    attn_core_fwd<HD>(S1, S2, S3, S4, Pl, nullptr, g0, ng, M, scale, p_drop, seed);
+    attn_core_fwd<D, HD>(S1, S2, S3, S4, Pl, nullptr, g0, ng, M, scale, p_drop, seed);
   } else {
-    stage_in(S1, Qg + r0 * kD, R, rows);
-    stage_in(S2, Kg + r0 * kD, R, rows);
-    stage_in(S3, Vg + r0 * kD, R, rows);
-    if (wg) stage_in(S4, Og + r0 * kD, R, rows);
+    stage_in<D>(S1, Qg + r0 * D, Rp, rows);
+    stage_in<D>(S2, Kg + r0 * D, Rp, rows);
+    stage_in<D>(S3, Vg + r0 * D, Rp, rows);
+    if (wg) stage_in<D>(S4, Og + r0 * D, Rp, rows);
   }
   __syncthreads();
-  float* pw = wg ? part + (int64_t)blockIdx.x * kPartAttn : nullptr;
+  float* pw = wg ? part + (int64_t)blockIdx.x * G::kPartAttn : nullptr;
   // X_u / X_i rows of this workgroup, prefetched into registers for the fused weight gradients
   if (wg && !RC) {
 #pragma unroll
     for (int q = 0; q < kPre; ++q) {
-      const int e = threadIdx.x + kThreads * q, r = e >> 4, c = (e & 15) * 4;
-      const bool in = e < R * 16 && r < rows;
-      pu[q] = in ? ld4(Xu + (r0 + r) * kD + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      pi[q] = in ? ld4(Xi + (r0 + r) * kD + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int e = threadIdx.x + kThreads * q, r = e / L4, c = (e % L4) * 4;
+      const bool in = e < Rp * L4 && r < rows;
+      pu[q] = in ? ld4(Xu + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      pi[q] = in ? ld4(Xi + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
   // dO = dY . Wo  (+ out_proj's weight gradient dY^T O and bias gradient)
   {
-    float b[16];
-    frag_w(wo, w, b);
+    float b[D / 4];
+    frag_w<D>(wo, w, b);
     f32x4 fo[kMaxM];
 #pragma unroll
-    for (int rt = 0; rt < kMaxM; ++rt)
-      if (rt < M && (rt & 1) == par) fo[rt] = tile_mfma(S0 + 16 * rt * kPitch, b, f32x4{0.f, 0.f, 0.f, 0.f});
+    for (int rt = 0; rt < G::NTmax; ++rt)
+      if (my_tile<D>(rt, NT)) fo[rt] = tile_mfma<D>(S0 + 16 * rt * kPitch, b, f32x4{0.f, 0.f, 0.f, 0.f});
     if (wg) {
       const int wave = threadIdx.x >> 6;
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < G::CS * G::CS / 8; ++q) {   // the D/16 x D/16 tiles over 8 waves
         const int t = wave + 8 * q;
-        wgrad_tile(S0, S4, R, t >> 2, t & 3, pw + 3 * kLinW);
+        wgrad_tile<D>(S0, S4, Rp, t / G::CS, t % G::CS, pw + 3 * kLinW);
       }
-      bias_cols(S0, R, 0, pw + 3 * kLinW + kD * kD);
+      bias_cols<D>(S0, Rp, 0, pw + 3 * kLinW + D * D);
     }
     __syncthreads();
 #pragma unroll
-    for (int rt = 0; rt < kMaxM; ++rt)
-      if (rt < M && (rt & 1) == par) put_tile(S0, rt, w, fo[rt]);
+    for (int rt = 0; rt < G::NTmax; ++rt)
+      if (my_tile<D>(rt, NT)) put_tile<D>(S0, rt, w, fo[rt]);
     if (wg) {   // O is consumed: X_u takes its place
 #pragma unroll
       for (int q = 0; q < kPre; ++q) {
         const int e = threadIdx.x + kThreads * q;
-        if (e < R * 16) *reinterpret_cast<float4*>(S4 + (e >> 4) * kPitch + (e & 15) * 4) = pu[q];
+        if (e < Rp * L4) *reinterpret_cast<float4*>(S4 + (e / L4) * kPitch + (e % L4) * 4) = pu[q];
       }
     }
     __syncthreads();
@@ -503,78 +544,95 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     }
     __syncthreads();
   }
-  if (dQ) stage_out(dQ + r0 * kD, S2, rows);
-  if (dK) stage_out(dK + r0 * kD, S1, rows);
-  if (dV) stage_out(dV + r0 * kD, S3, rows);
+  if (dQ) stage_out<D>(dQ + r0 * D, S2, rows);
+  if (dK) stage_out<D>(dK + r0 * D, S1, rows);
+  if (dV) stage_out<D>(dV + r0 * D, S3, rows);
   if (wg) {   // dO is consumed: X_i takes its place; then the q/k/v weight gradients
 #pragma unroll
     for (int q = 0; q < kPre; ++q) {
       const int e = threadIdx.x + kThreads * q;
-      if (e < R * 16) *reinterpret_cast<float4*>(S0 + (e >> 4) * kPitch + (e & 15) * 4) = pi[q];
+      if (e < Rp * L4) *reinterpret_cast<float4*>(S0 + (e / L4) * kPitch + (e % L4) * 4) = pi[q];
     }
     __syncthreads();
     const int wave = threadIdx.x >> 6;
-    for (int q = 0; q < 6; ++q) {
-      const int t = wave + 8 * q, lin = t >> 4, tt = t & 15;   // lin: 0 q, 1 k, 2 v
+    constexpr int TPL = G::CS * G::CS;   // 16x16 tiles per weight
+    for (int q = 0; q < 3 * TPL / 8; ++q) {
+      const int t = wave + 8 * q, lin = t / TPL, tt = t % TPL;   // lin: 0 q, 1 k, 2 v
       const float* dys = lin == 0 ? S2 : (lin == 1 ? S1 : S3);
       const float* xs = lin == 0 ? S4 : S0;
-      wgrad_tile(dys, xs, R, tt >> 2, tt & 3, pw + lin * kLinW);
+      wgrad_tile<D>(dys, xs, Rp, tt / G::CS, tt % G::CS, pw + lin * kLinW);
     }
-    bias_cols(S2, R, 0, pw + kD * kD);
-    bias_cols(S1, R, 64, pw + kLinW + kD * kD);
-    bias_cols(S3, R, 128, pw + 2 * kLinW + kD * kD);
+    bias_cols<D>(S2, Rp, 0, pw + D * D);
+    bias_cols<D>(S1, Rp, D, pw + kLinW + D * D);
+    bias_cols<D>(S3, Rp, 2 * D, pw + 2 * kLinW + D * D);
   }
   // dX_u = dQ . Wq ; dX_i = dK . Wk + dV . Wv
   f32x4 fu[kMaxM], fi[kMaxM];
   {
-    float b[16];
-    frag_w(wq, w, b);
+    float b[D / 4];
+    frag_w<D>(wq, w, b);
 #pragma unroll
-    for (int rt = 0; rt < kMaxM; ++rt)
-      if (rt < M && (rt & 1) == par) fu[rt] = tile_mfma(S2 + 16 * rt * kPitch, b, f32x4{0.f, 0.f, 0.f, 0.f});
-    frag_w(wk, w, b);
+    for (int rt = 0; rt < G::NTmax; ++rt)
+      if (my_tile<D>(rt, NT)) fu[rt] = tile_mfma<D>(S2 + 16 * rt * kPitch, b, f32x4{0.f, 0.f, 0.f, 0.f});
+    frag_w<D>(wk, w, b);
 #pragma unroll
-    for (int rt = 0; rt < kMaxM; ++rt)
-      if (rt < M && (rt & 1) == par) fi[rt] = tile_mfma(S1 + 16 * rt * kPitch, b, f32x4{0.f, 0.f, 0.f, 0.f});
-    frag_w(wv, w, b);
+    for (int rt = 0; rt < G::NTmax; ++rt)
+      if (my_tile<D>(rt, NT)) fi[rt] = tile_mfma<D>(S1 + 16 * rt * kPitch, b, f32x4{0.f, 0.f, 0.f, 0.f});
+    frag_w<D>(wv, w, b);
 #pragma unroll
-    for (int rt = 0; rt < kMaxM; ++rt)
-      if (rt < M && (rt & 1) == par) fi[rt] = tile_mfma(S3 + 16 * rt * kPitch, b, fi[rt]);
+    for (int rt = 0; rt < G::NTmax; ++rt)
+      if (my_tile<D>(rt, NT)) fi[rt] = tile_mfma<D>(S3 + 16 * rt * kPitch, b, fi[rt]);
   }
   if (!wg) {
 #pragma unroll
-    for (int rt = 0; rt < kMaxM; ++rt)
-      if (rt < M && (rt & 1) == par) put_tile(S0, rt, w, fu[rt]);   // dO is dead
+    for (int rt = 0; rt < G::NTmax; ++rt)
+      if (my_tile<D>(rt, NT)) put_tile<D>(S0, rt, w, fu[rt]);   // dO is dead
   }
   __syncthreads();   // S0..S4 no longer read (MFMA operands, stage_out)
 #pragma unroll
-  for (int rt = 0; rt < kMaxM; ++rt)
-    if (rt < M && (rt & 1) == par) {
-      if (wg) put_tile(S0, rt, w, fu[rt]);
-      put_tile(S1, rt, w, fi[rt]);
+  for (int rt = 0; rt < G::NTmax; ++rt)
+    if (my_tile<D>(rt, NT)) {
+      if (wg) put_tile<D>(S0, rt, w, fu[rt]);
+      put_tile<D>(S1, rt, w, fi[rt]);
     }
   __syncthreads();
-  stage_out(dXu + r0 * kD, S0, rows);
-  stage_out(dXi + r0 * kD, S1, rows);
+  stage_out<D>(dXu + r0 * D, S0, rows);
+  stage_out<D>(dXi + r0 * D, S1, rows);
 }
 
 constexpr size_t kMaxLds = 160 * 1024;   // LDS per workgroup (gfx950)
-size_t fwd_lds(int M) { return sizeof(float) * 3 * kGroups * M * kPitch; }
+template <int D>
+size_t fwd_lds(int M) { return sizeof(float) * 3 * 16 * AG<D>::nt(M) * AG<D>::kPitch; }
+template <int D>
 size_t bwd_lds(int M, int H, bool wg, bool rc = false) {
-  return sizeof(float) * ((wg ? 5 : 4) * kGroups * M * kPitch + (rc ? 2 : 1) * kGroups * H * M * M);
+  using G = AG<D>;
+  return sizeof(float) * ((wg ? 5 : 4) * 16 * G::nt(M) * G::kPitch +
+                          (rc ? 2 : 1) * G::kGroups * H * M * M);
 }
+size_t fwd_lds_d(int D, int M) { return D == 64 ? fwd_lds<64>(M) : fwd_lds<128>(M); }
+size_t bwd_lds_d(int D, int M, int H, bool wg, bool rc = false) {
+  return D == 64 ? bwd_lds<64>(M, H, wg, rc) : bwd_lds<128>(M, H, wg, rc);
+}
+int groups_per_wg(int64_t D) { return D == 64 ? AG<64>::kGroups : AG<128>::kGroups; }
+int64_t part_floats(int64_t D) { return D == 64 ? AG<64>::kPartAttn : AG<128>::kPartAttn; }
 
 template <typename Kern>
 void allow_lds(Kern k, size_t bytes) {
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+// head widths the kernels are built for: hd in {8, 16, 32, 64} at D = 64, {16, 32, 64} at
+// D = 128 (the core keeps a head row of hd floats per lane in registers)
+bool hd_ok(int64_t dim, int64_t hd) {
+  if (dim == 64) return hd == 8 || hd == 16 || hd == 32 || hd == 64;
+  return hd == 16 || hd == 32 || hd == 64;
+}
+
 }  // namespace
 
 extern "C" int ncf_attn_block_supported(int64_t dim, int64_t heads, int64_t group_len) {
-  if (dim != kD || heads < 1 || dim % heads != 0) return 0;
-  const int64_t hd = dim / heads;
-  if (hd != 8 && hd != 16 && hd != 32 && hd != 64) return 0;
+  if ((dim != 64 && dim != 128) || heads < 1 || dim % heads != 0) return 0;
+  if (!hd_ok(dim, dim / heads)) return 0;
   return group_len >= 1 && group_len <= kMaxM ? 1 : 0;
 }
 
@@ -586,8 +644,8 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
                                   const ncf_step_clock* clock, float* q, float* k, float* v,
                                   float* probs, float* o, float* y, void* stream) {
   NCF_CHECK_ARG(groups >= 0 && ncf_attn_block_supported(dim, heads, group_len),
-                "ncf_attn_block_fwd: unsupported shape (D=%lld H=%lld M=%lld; need D=64, M<=%d)",
-                (long long)dim, (long long)heads, (long long)group_len, kMaxM);
+                "ncf_attn_block_fwd: unsupported shape (D=%lld H=%lld M=%lld; need D=64 or 128, "
+                "M<=%d)", (long long)dim, (long long)heads, (long long)group_len, kMaxM);
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_attn_block_fwd: dropout_p out of [0,1)");
   NCF_CHECK_ARG(y != nullptr && (q != nullptr) == (k != nullptr),
                 "ncf_attn_block_fwd: q and k are given together (or neither)");
@@ -598,25 +656,25 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
   const int core = (q != nullptr || group_len > 1 || dropout_p > 0.0f) ? 1 : 0;
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len;
-  const size_t lds = fwd_lds(M);
-  const dim3 grid((unsigned)ncf_cdiv(groups, kGroups));
+  const size_t lds = fwd_lds_d((int)dim, M);
+  const dim3 grid((unsigned)ncf_cdiv(groups, groups_per_wg(dim)));
   hipStream_t st = (hipStream_t)stream;
   const float scale = sqrtf((float)(dim / heads));
-#define NCF_ABF(HD)                                                                              \
-  case HD: {                                                                                     \
+#define NCF_ABF(D_, HD)                                                                          \
+  if (dim == D_ && dim / heads == HD) {                                                          \
     static bool attr = false;                                                                    \
-    if (!attr) { allow_lds(k_attn_block_fwd<HD>, fwd_lds(kMaxM)); attr = true; }                 \
-    hipLaunchKernelGGL(k_attn_block_fwd<HD>, grid, dim3(kThreads), lds, st, xu, xi, groups, M, wq, bq, \
-                       wk, bk, wv, bv, wo, bo, scale, dropout_p, seed, clock, q, k, v, probs, o,  \
-                       y, core);                                                                 \
-    break;                                                                                       \
+    if (!attr) { allow_lds(k_attn_block_fwd<D_, HD>, fwd_lds<D_>(kMaxM)); attr = true; }         \
+    hipLaunchKernelGGL((k_attn_block_fwd<D_, HD>), grid, dim3(kThreads), lds, st, xu, xi, groups, \
+                       M, wq, bq, wk, bk, wv, bv, wo, bo, scale, dropout_p, seed, clock, q, k, v, \
+                       probs, o, y, core);                                                       \
   }
-  switch (dim / heads) {
-    NCF_ABF(8)
-    NCF_ABF(16)
-    NCF_ABF(32)
-    NCF_ABF(64)
-  }
+  NCF_ABF(64, 8)
+  NCF_ABF(64, 16)
+  NCF_ABF(64, 32)
+  NCF_ABF(64, 64)
+  NCF_ABF(128, 16)
+  NCF_ABF(128, 32)
+  NCF_ABF(128, 64)
 #undef NCF_ABF
   NCF_CHECK_LAUNCH("ncf_attn_block_fwd");
   return NCF_OK;
@@ -626,42 +684,51 @@ namespace {
 // the per-workgroup partial rows -> the 8 parameter gradients: one reduction when they are laid
 // out like the partial row (the flat gradient buffer), else one per Linear (weight + bias
 // adjacent) or 8; deferred into `defer` when given
-int defer_partials(float* const* grad_params, const float* part, int nb, float* workspace,
-                   int64_t workspace_floats, ncf_reduce_list* defer, void* stream) {
+int defer_partials(int64_t D, float* const* grad_params, const float* part, int nb,
+                   float* workspace, int64_t workspace_floats, ncf_reduce_list* defer,
+                   void* stream) {
+  const int64_t PA = part_floats(D), LW = D * D + D, DD = D * D;
   ncf_reduce_list local;
   local.count = 0;
   ncf_reduce_list* lst = defer ? defer : &local;
   int rc = NCF_OK;
   bool flat = true;
   for (int j = 1; j < 8; ++j)
-    flat = flat && grad_params[j] == grad_params[0] + (j / 2) * kLinW + (j & 1) * kD * kD;
+    flat = flat && grad_params[j] == grad_params[0] + (j / 2) * LW + (j & 1) * DD;
   if (flat) {
-    rc = ncf_defer(lst, part, nb, kPartAttn, kPartAttn, grad_params[0], 0, kPartAttn, kPartAttn);
+    rc = ncf_defer(lst, part, nb, PA, PA, grad_params[0], 0, PA, PA);
   } else {
     for (int lin = 0; lin < 4 && !rc; ++lin) {
       float* gw = grad_params[2 * lin];
       float* gb = grad_params[2 * lin + 1];
-      const float* pp = part + lin * kLinW;
-      if (gb == gw + kD * kD) {
-        rc = ncf_defer(lst, pp, nb, kPartAttn, kLinW, gw, 0, kLinW, kLinW);
+      const float* pp = part + lin * LW;
+      if (gb == gw + DD) {
+        rc = ncf_defer(lst, pp, nb, PA, LW, gw, 0, LW, LW);
       } else {
-        rc = ncf_defer(lst, pp, nb, kPartAttn, kD * kD, gw, 0, kD * kD, kD * kD);
-        if (!rc) rc = ncf_defer(lst, pp + kD * kD, nb, kPartAttn, kD, gb, 0, kD, kD);
+        rc = ncf_defer(lst, pp, nb, PA, DD, gw, 0, DD, DD);
+        if (!rc) rc = ncf_defer(lst, pp + DD, nb, PA, D, gb, 0, D, D);
       }
     }
   }
   if (rc) return rc;
   if (!defer) {
-    const int64_t off = (int64_t)nb * kPartAttn;
+    const int64_t off = (int64_t)nb * PA;
     return ncf_reduce_batch(lst, workspace + off, workspace_floats - off, stream);
   }
   return NCF_OK;
 }
 }  // namespace
 
+// sized for either supported width (the larger of D = 64 / 128)
 extern "C" int64_t ncf_attn_block_bwd_workspace(int64_t groups) {
-  const int64_t nb = groups <= 0 ? 1 : ncf_cdiv(groups, kGroups);
-  return nb * kPartAttn + ncf_reduce_scratch((int)nb, kPartAttn) * 4;
+  int64_t best = 0;
+  for (int64_t D : {64, 128}) {
+    const int64_t nb = groups <= 0 ? 1 : ncf_cdiv(groups, groups_per_wg(D));
+    const int64_t PA = part_floats(D);
+    const int64_t ws = nb * PA + ncf_reduce_scratch((int)nb, (int)PA) * 4;
+    best = ws > best ? ws : best;
+  }
+  return best;
 }
 
 extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const float* k,
@@ -675,8 +742,8 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
                                   float* grad_q, float* grad_k, float* grad_v, float* grad_xu,
                                   float* grad_xi, void* stream) {
   NCF_CHECK_ARG(groups >= 0 && ncf_attn_block_supported(dim, heads, group_len),
-                "ncf_attn_block_bwd: unsupported shape (D=%lld H=%lld M=%lld; need D=64, M<=%d)",
-                (long long)dim, (long long)heads, (long long)group_len, kMaxM);
+                "ncf_attn_block_bwd: unsupported shape (D=%lld H=%lld M=%lld; need D=64 or 128, "
+                "M<=%d)", (long long)dim, (long long)heads, (long long)group_len, kMaxM);
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_attn_block_bwd: dropout_p out of [0,1)");
   const bool wg = grad_params != nullptr;
   NCF_CHECK_ARG(!wg || (o && xu && xi && workspace), "ncf_attn_block_bwd: the fused weight "
@@ -689,37 +756,37 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
   }
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len, H = (int)heads;
-  const size_t lds = bwd_lds(M, H, wg);
-  const int nb = (int)ncf_cdiv(groups, kGroups);
+  const size_t lds = bwd_lds_d((int)dim, M, H, wg);
+  const int nb = (int)ncf_cdiv(groups, groups_per_wg(dim));
   const dim3 grid((unsigned)nb);
   hipStream_t st = (hipStream_t)stream;
   const float scale = sqrtf((float)(dim / heads));
   float* part = wg ? workspace : nullptr;
-#define NCF_ABB(HD)                                                                               \
-  case HD: {                                                                                      \
+#define NCF_ABB(D_, HD)                                                                           \
+  if (dim == D_ && dim / heads == HD) {                                                           \
     static bool attr = false;                                                                     \
-    if (!attr) { allow_lds(k_attn_block_bwd<HD, false>, bwd_lds(kMaxM, kD / HD, true)); attr = true; } \
-    hipLaunchKernelGGL((k_attn_block_bwd<HD, false>), grid, dim3(kThreads), lds, st, grad_y, q, k, v, \
-                       probs, groups, M, wq, wk, wv, wo, scale, dropout_p, seed, clock, o, xu, xi, \
+    if (!attr) { allow_lds(k_attn_block_bwd<D_, HD, false>, bwd_lds<D_>(kMaxM, D_ / HD, true)); attr = true; } \
+    hipLaunchKernelGGL((k_attn_block_bwd<D_, HD, false>), grid, dim3(kThreads), lds, st, grad_y, q, k, \
+                       v, probs, groups, M, wq, wk, wv, wo, scale, dropout_p, seed, clock, o, xu, xi, \
                        part, grad_q, grad_k, grad_v, grad_xu, grad_xi, nullptr, nullptr, nullptr); \
-    break;                                                                                        \
   }
-  switch (dim / heads) {
-    NCF_ABB(8)
-    NCF_ABB(16)
-    NCF_ABB(32)
-    NCF_ABB(64)
-  }
+  NCF_ABB(64, 8)
+  NCF_ABB(64, 16)
+  NCF_ABB(64, 32)
+  NCF_ABB(64, 64)
+  NCF_ABB(128, 16)
+  NCF_ABB(128, 32)
+  NCF_ABB(128, 64)
 #undef NCF_ABB
   NCF_CHECK_LAUNCH("ncf_attn_block_bwd");
   if (!wg) return NCF_OK;
-  return defer_partials(grad_params, part, nb, workspace, workspace_floats, defer, stream);
+  return defer_partials(dim, grad_params, part, nb, workspace, workspace_floats, defer, stream);
 }
 
 // the recompute backward holds the recomputed probabilities beside dS in LDS
 extern "C" int ncf_attn_block_rc_supported(int64_t dim, int64_t heads, int64_t group_len) {
   return ncf_attn_block_supported(dim, heads, group_len) &&
-                 bwd_lds((int)group_len, (int)heads, true, true) <= kMaxLds
+                 bwd_lds_d((int)dim, (int)group_len, (int)heads, true, true) <= kMaxLds
              ? 1
              : 0;
 }
@@ -734,8 +801,8 @@ extern "C" int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const
                                      int64_t workspace_floats, ncf_reduce_list* defer,
                                      float* grad_xu, float* grad_xi, void* stream) {
   NCF_CHECK_ARG(groups >= 0 && ncf_attn_block_supported(dim, heads, group_len),
-                "ncf_attn_block_bwd_rc: unsupported shape (D=%lld H=%lld M=%lld; need D=64, M<=%d)",
-                (long long)dim, (long long)heads, (long long)group_len, kMaxM);
+                "ncf_attn_block_bwd_rc: unsupported shape (D=%lld H=%lld M=%lld; need D=64 or "
+                "128, M<=%d)", (long long)dim, (long long)heads, (long long)group_len, kMaxM);
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_attn_block_bwd_rc: dropout_p out of [0,1)");
   NCF_CHECK_ARG(grad_y && xu && xi && wq && bq && wk && bk && wv && bv && wo && grad_params &&
                     workspace && grad_xu && grad_xi,
@@ -749,28 +816,28 @@ extern "C" int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const
                 (long long)group_len, (long long)heads);
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len, H = (int)heads;
-  const size_t lds = bwd_lds(M, H, true, true);
-  const int nb = (int)ncf_cdiv(groups, kGroups);
+  const size_t lds = bwd_lds_d((int)dim, M, H, true, true);
+  const int nb = (int)ncf_cdiv(groups, groups_per_wg(dim));
   const dim3 grid((unsigned)nb);
   hipStream_t st = (hipStream_t)stream;
   const float scale = sqrtf((float)(dim / heads));
-#define NCF_ABR(HD)                                                                               \
-  case HD: {                                                                                      \
+#define NCF_ABR(D_, HD)                                                                           \
+  if (dim == D_ && dim / heads == HD) {                                                           \
     static bool attr = false;                                                                     \
-    if (!attr) { allow_lds(k_attn_block_bwd<HD, true>, kMaxLds); attr = true; }                 \
-    hipLaunchKernelGGL((k_attn_block_bwd<HD, true>), grid, dim3(kThreads), lds, st, grad_y, nullptr, \
-                       nullptr, nullptr, nullptr, groups, M, wq, wk, wv, wo, scale, dropout_p, seed, \
-                       clock, nullptr, xu, xi, workspace, nullptr, nullptr, nullptr, grad_xu, grad_xi, \
-                       bq, bk, bv);                                                               \
-    break;                                                                                        \
+    if (!attr) { allow_lds(k_attn_block_bwd<D_, HD, true>, kMaxLds); attr = true; }              \
+    hipLaunchKernelGGL((k_attn_block_bwd<D_, HD, true>), grid, dim3(kThreads), lds, st, grad_y,     \
+                       nullptr, nullptr, nullptr, nullptr, groups, M, wq, wk, wv, wo, scale,       \
+                       dropout_p, seed, clock, nullptr, xu, xi, workspace, nullptr, nullptr,       \
+                       nullptr, grad_xu, grad_xi, bq, bk, bv);                                     \
   }
-  switch (dim / heads) {
-    NCF_ABR(8)
-    NCF_ABR(16)
-    NCF_ABR(32)
-    NCF_ABR(64)
-  }
+  NCF_ABR(64, 8)
+  NCF_ABR(64, 16)
+  NCF_ABR(64, 32)
+  NCF_ABR(64, 64)
+  NCF_ABR(128, 16)
+  NCF_ABR(128, 32)
+  NCF_ABR(128, 64)
 #undef NCF_ABR
   NCF_CHECK_LAUNCH("ncf_attn_block_bwd_rc");
-  return defer_partials(grad_params, workspace, nb, workspace, workspace_floats, defer, stream);
+  return defer_partials(dim, grad_params, workspace, nb, workspace, workspace_floats, defer, stream);
 }

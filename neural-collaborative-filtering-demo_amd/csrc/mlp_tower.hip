@@ -1,6 +1,6 @@
 // The MLP tower of AdvancedNCF in one launch per direction: 3 x [Linear -> ReLU -> LayerNorm ->
-// Dropout] (+ mlp_output and the final fusion in the forward), for input width 64 and hidden
-// widths [256, 128, 64] (the reference defaults, C2).
+// Dropout] (+ mlp_output and the final fusion in the forward), for input width K0 = 64 (C2) or
+// 128 (C4: mlp_embedding_dim = 128) and hidden widths [256, 128, 64] (the reference defaults).
 //
 // Reference: self.mlp (src/model/architecture.py:230-242, applied :344), mlp_output (:246, :345),
 // final Linear(2,1) + Sigmoid (:249-252, :353-354).  Same math and dropout stream as the
@@ -38,16 +38,23 @@ constexpr int kThreads = 512;          // 8 waves
 constexpr int kWaves = kThreads / 64;
 constexpr int kPQ = 260;   // pitch of buffer Q (<= 256 columns)
 constexpr int kPP = 132;   // pitch of buffer P (<= 128 columns; also the 8 x 3 x 256 scratch)
-constexpr int K0 = 64, N0 = 256, N1 = 128, N2 = 64;
-constexpr int kHeadW = 148;   // head partials: the flat layout of mf_output/mlp_output/final + loss
-constexpr int kPartS = 3 * (N0 + N1 + N2) + kHeadW;   // bias/gamma/beta + head partials
-// fused weight gradients: dW0 [256 x 64] | dW1 [128 x 256] | dW2 [64 x 128] per workgroup
-constexpr int kW0 = kPartS, kW1 = kW0 + N0 * K0, kW2 = kW1 + N1 * N0;
-constexpr int kPartW = kW2 + N2 * N1;   // partial floats per workgroup
-// head partial row (offsets): the flat gradient buffer's order of the head parameters, each
-// 16-B aligned: mf_output.weight [64] @0, mf_output.bias @64, mlp_output.weight [64] @68,
-// mlp_output.bias @132, final.0.weight [2] @136, final.0.bias @140; the BCE sum @144
-constexpr int kHmfW = 0, kHmfB = 64, kHmlW = 68, kHmlB = 132, kHfW = 136, kHfB = 140, kHloss = 144;
+constexpr int N0 = 256, N1 = 128, N2 = 64;
+// Partial-row layout per input width K0 (= D, the embedding width: 64 or 128).
+// Head partials (offsets): the flat gradient buffer's order of the head parameters, each 16-B
+// aligned: mf_output.weight [K0] @0, mf_output.bias @K0, mlp_output.weight [64] @K0+4,
+// mlp_output.bias @K0+68, final.0.weight [2] @K0+72, final.0.bias @K0+76; the BCE sum @K0+80
+// (K0 = 64: 0, 64, 68, 132, 136, 140, 144).  Then the fused weight gradients dW0 [256 x K0] |
+// dW1 [128 x 256] | dW2 [64 x 128].
+template <int K0>
+struct Lay {
+  static constexpr int kHmfW = 0, kHmfB = K0, kHmlW = K0 + 4, kHmlB = kHmlW + N2, kHfW = kHmlB + 4,
+                       kHfB = kHfW + 4, kHloss = kHfB + 4;
+  static constexpr int kHeadW = kHloss + 4;
+  static constexpr int kPartS = 3 * (N0 + N1 + N2) + kHeadW;   // bias/gamma/beta + head partials
+  static constexpr int kW0 = kPartS, kW1 = kW0 + N0 * K0, kW2 = kW1 + N1 * N0;
+  static constexpr int kPartW = kW2 + N2 * N1;   // partial floats per workgroup
+};
+static_assert(Lay<64>::kHeadW == 148 && Lay<64>::kPartW == 58836, "C2 partial layout");
 constexpr int kPasses = (kRows * 16 + kThreads - 1) / kThreads;   // row-op passes (16 lanes/row)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -476,7 +483,7 @@ __device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict_
 
 // The forward in workgroups of VR valid rows staged as RT 16-row MFMA tiles (the padding rows
 // are zeros and are never stored).  VR < 16 RT lets two workgroups share a CU (A/B knob).
-template <int RT, int VR, bool BF = false>
+template <int K0, int RT, int VR, bool BF = false>
 __global__ __launch_bounds__(kThreads) void k_mlp_fwd(
     const float* __restrict__ xin, int64_t n, TowerArgs a, float eps, float p,
     const ncf_step_clock* clock, const float* __restrict__ w_out, const float* __restrict__ b_out,
@@ -603,16 +610,26 @@ __device__ __forceinline__ void stage_rows(float* __restrict__ X, const float* _
 
 // Head backward (head.hip's k_head_bwd math) for the 80 rows: dL/da_2 -> G, dL/d(LN'd GMF
 // rows) -> HBM, this workgroup's head parameter partials + BCE sum -> part[0 : kHeadW) (through
-// the free buffer S).  16 lanes per row, 4 columns per lane (W3 = D = 64).
+// the free buffer S).  16 lanes per row, 4 columns per lane (W3 = 64) and K0/64 float4 chunks
+// of the GMF rows (D = K0).
+template <int K0>
 __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restrict__ S,
                                          int64_t row0, int rows, const ncf_head_args& h,
                                          const ncf_mlp_layer& L2, float p, uint64_t seed,
                                          float inv_n, float* __restrict__ part) {
+  using T = Lay<K0>;
+  constexpr int CM = K0 / 64;   // float4 chunks of a GMF row per lane
   const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int sub = threadIdx.x & 15, wv = threadIdx.x >> 6, col = sub * 4;
   const float wf0 = h.final_w[0], wf1 = h.final_w[1];
-  const float4 wo = ld4(h.mlp_out_w + col), wm = ld4(h.mf_out_w + col);
-  float4 aw = make_float4(0.f, 0.f, 0.f, 0.f), am = aw;
+  const float4 wo = ld4(h.mlp_out_w + col);
+  float4 wm[CM], am[CM];
+#pragma unroll
+  for (int c = 0; c < CM; ++c) {
+    wm[c] = ld4(h.mf_out_w + 64 * c + col);
+    am[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float4 aw = make_float4(0.f, 0.f, 0.f, 0.f);
   float sw0 = 0.f, sw1 = 0.f, sbf = 0.f, sbo = 0.f, sbm = 0.f, sl = 0.f;
 #pragma unroll
   for (int pass = 0; pass < kPasses; ++pass) {
@@ -638,11 +655,16 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
     if (ok) {
       const float4 x = L2.a ? ld4(L2.a + row * N2 + col) : act4<N2>(L2, row, col, p, seed, inv_keep);
       aw.x += dml * x.x; aw.y += dml * x.y; aw.z += dml * x.z; aw.w += dml * x.w;
-      const float4 u = ld4(h.mf_user_ln + row * K0 + col), it = ld4(h.mf_item_ln + row * K0 + col);
-      const float4 gv = make_float4(dmf * wm.x, dmf * wm.y, dmf * wm.z, dmf * wm.w);
-      st4_nt(h.grad_mf_user_ln + row * K0 + col, make_float4(gv.x * it.x, gv.y * it.y, gv.z * it.z, gv.w * it.w));
-      st4_nt(h.grad_mf_item_ln + row * K0 + col, make_float4(gv.x * u.x, gv.y * u.y, gv.z * u.z, gv.w * u.w));
-      am.x += dmf * u.x * it.x; am.y += dmf * u.y * it.y; am.z += dmf * u.z * it.z; am.w += dmf * u.w * it.w;
+#pragma unroll
+      for (int c = 0; c < CM; ++c) {
+        const int64_t o = row * K0 + 64 * c + col;
+        const float4 u = ld4(h.mf_user_ln + o), it = ld4(h.mf_item_ln + o);
+        const float4 gv = make_float4(dmf * wm[c].x, dmf * wm[c].y, dmf * wm[c].z, dmf * wm[c].w);
+        st4_nt(h.grad_mf_user_ln + o, make_float4(gv.x * it.x, gv.y * it.y, gv.z * it.z, gv.w * it.w));
+        st4_nt(h.grad_mf_item_ln + o, make_float4(gv.x * u.x, gv.y * u.y, gv.z * u.z, gv.w * u.w));
+        am[c].x += dmf * u.x * it.x; am[c].y += dmf * u.y * it.y;
+        am[c].z += dmf * u.z * it.z; am[c].w += dmf * u.w * it.w;
+      }
       if (sub == 0) {
         sw0 += dz * h.mf_pred[row];
         sw1 += dz * h.mlp_pred[row];
@@ -657,32 +679,34 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
   v += __shfl_xor(v, 16, 64);                      \
   v += __shfl_xor(v, 32, 64);
   NCF_R4(aw.x) NCF_R4(aw.y) NCF_R4(aw.z) NCF_R4(aw.w)
-  NCF_R4(am.x) NCF_R4(am.y) NCF_R4(am.z) NCF_R4(am.w)
+#pragma unroll
+  for (int c = 0; c < CM; ++c) { NCF_R4(am[c].x) NCF_R4(am[c].y) NCF_R4(am[c].z) NCF_R4(am[c].w) }
   NCF_R4(sw0) NCF_R4(sw1) NCF_R4(sbf) NCF_R4(sbo) NCF_R4(sbm) NCF_R4(sl)
 #undef NCF_R4
-  float* sw = S + wv * kHeadW;
+  float* sw = S + wv * T::kHeadW;
   if ((threadIdx.x & 63) < 16) {
-    lds4_st(sw + kHmfW + col, am);
-    lds4_st(sw + kHmlW + col, aw);
+#pragma unroll
+    for (int c = 0; c < CM; ++c) lds4_st(sw + T::kHmfW + 64 * c + col, am[c]);
+    lds4_st(sw + T::kHmlW + col, aw);
     if (sub == 0) {
-      lds4_st(sw + kHmfB, make_float4(sbm, 0.f, 0.f, 0.f));
-      lds4_st(sw + kHmlB, make_float4(sbo, 0.f, 0.f, 0.f));
-      lds4_st(sw + kHfW, make_float4(sw0, sw1, 0.f, 0.f));
-      lds4_st(sw + kHfB, make_float4(sbf, 0.f, 0.f, 0.f));
-      lds4_st(sw + kHloss, make_float4(sl, 0.f, 0.f, 0.f));
+      lds4_st(sw + T::kHmfB, make_float4(sbm, 0.f, 0.f, 0.f));
+      lds4_st(sw + T::kHmlB, make_float4(sbo, 0.f, 0.f, 0.f));
+      lds4_st(sw + T::kHfW, make_float4(sw0, sw1, 0.f, 0.f));
+      lds4_st(sw + T::kHfB, make_float4(sbf, 0.f, 0.f, 0.f));
+      lds4_st(sw + T::kHloss, make_float4(sl, 0.f, 0.f, 0.f));
     }
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < kHeadW; e += kThreads) {
+  for (int e = threadIdx.x; e < T::kHeadW; e += kThreads) {
     float v = 0.0f;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) v += S[w * kHeadW + e];
+    for (int w = 0; w < kWaves; ++w) v += S[w * T::kHeadW + e];
     st_nt(part + e, v);
   }
   __syncthreads();
 }
 
-template <bool BF = false>
+template <int K0, bool BF = false>
 __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ g_last, int64_t n,
                                                       TowerArgs a, float p,
                                                       const ncf_step_clock* clock,
@@ -696,10 +720,11 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
   const int64_t row0 = (int64_t)blockIdx.x * kRows;
   const int rows = (int)min<int64_t>(kRows, n - row0);
   const uint64_t cs = clock ? clock->seed : 0ull;
-  float* pp = part + (int64_t)blockIdx.x * kPartW;
+  using T = Lay<K0>;
+  float* pp = part + (int64_t)blockIdx.x * T::kPartW;
   NCF_STAMP(1, 0);
   if (fused_head) {
-    head_bwd(Q, P, row0, rows, h, a.l[2], p, a.seed[2] + cs, inv_n, pp + 3 * (N0 + N1 + N2));
+    head_bwd<K0>(Q, P, row0, rows, h, a.l[2], p, a.seed[2] + cs, inv_n, pp + 3 * (N0 + N1 + N2));
   } else {
     for (int e = threadIdx.x; e < kRows * (N2 / 4); e += kThreads) {
       const int r = e / (N2 / 4), c = (e % (N2 / 4)) * 4;
@@ -715,7 +740,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_act<N1, kPP>(P, a.l[1], row0, rows, p, a.seed[1] + cs);
     __syncthreads();
     NCF_STAMP(1, 3);
-    wgrad_layer<N2, N1, kPQ, kPP, BF>(Q, P, pp + kW2);
+    wgrad_layer<N2, N1, kPQ, kPP, BF>(Q, P, pp + T::kW2);
     __syncthreads();
     NCF_STAMP(1, 4);
   }
@@ -728,7 +753,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_act<N0, kPQ>(Q, a.l[0], row0, rows, p, a.seed[0] + cs);
     __syncthreads();
     NCF_STAMP(1, 7);
-    wgrad_layer<N1, N0, kPP, kPQ, BF>(P, Q, pp + kW1);
+    wgrad_layer<N1, N0, kPP, kPQ, BF>(P, Q, pp + T::kW1);
     __syncthreads();
     NCF_STAMP(1, 8);
   }
@@ -741,7 +766,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_rows<K0, kPP>(P, xin, row0, rows);
     __syncthreads();
     NCF_STAMP(1, 11);
-    wgrad_layer<N0, K0, kPQ, kPP, BF>(Q, P, pp + kW0);
+    wgrad_layer<N0, K0, kPQ, kPP, BF>(Q, P, pp + T::kW0);
     __syncthreads();
     NCF_STAMP(1, 12);
   }
@@ -761,16 +786,18 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
 constexpr size_t kLds = sizeof(float) * kRows * (kPQ + kPP);
 constexpr size_t kLdsFwd = sizeof(float) * 16 * kFwdRT * (kPQ + kPP);
 static_assert(kWaves * 3 * N0 <= kRows * kPP, "ln_bwd scratch must fit in buffer P");
+static_assert(kWaves * Lay<128>::kHeadW <= kRows * kPP, "head scratch must fit in buffer P");
+static_assert(128 <= kPP - 4, "a 128-wide input fits buffer P");
 
 bool tower_ok(int64_t dim, int64_t n_layers, const int64_t* hidden) {
-  return dim == K0 && n_layers == 3 && hidden && hidden[0] == N0 && hidden[1] == N1 &&
-         hidden[2] == N2;
+  return (dim == 64 || dim == 128) && n_layers == 3 && hidden && hidden[0] == N0 &&
+         hidden[1] == N1 && hidden[2] == N2;
 }
 
-int make_args(const ncf_mlp_layer* layers, uint64_t seed, TowerArgs& a) {
+int make_args(const ncf_mlp_layer* layers, uint64_t seed, int64_t dim, TowerArgs& a) {
   for (int l = 0; l < 3; ++l) {
     a.l[l] = layers[l];
-    if (!a.l[l].w || !a.l[l].b || !a.l[l].gamma || !a.l[l].beta || a.l[l].ldw < (l ? 0 : K0) ||
+    if (!a.l[l].w || !a.l[l].b || !a.l[l].gamma || !a.l[l].beta || a.l[l].ldw < (l ? 0 : dim) ||
         (a.l[l].ldw & 3)) {
       ncf_set_error("ncf_mlp: layer %d needs w/b/gamma/beta and a float4-aligned ldw", l);
       return NCF_ERR_ARG;
@@ -795,6 +822,22 @@ extern "C" int ncf_mlp_fused_supported(int64_t dim, int64_t n_layers, const int6
   return tower_ok(dim, n_layers, hidden) ? 1 : 0;
 }
 
+template <int K0, bool BF>
+static void launch_fwd(const float* x, int64_t n, const TowerArgs& a, float eps, float dropout_p,
+                       const ncf_step_clock* clock, const float* mlp_out_w, const float* mlp_out_b,
+                       const float* mf_pred, const float* final_w, const float* final_b,
+                       float* mlp_pred, float* prob, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_mlp_fwd<K0, kFwdRT, kFwdVR, BF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsFwd);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_mlp_fwd<K0, kFwdRT, kFwdVR, BF>), dim3((unsigned)ncf_cdiv(n, kFwdVR)),
+                     dim3(kThreads), kLdsFwd, st, x, n, a, eps, dropout_p, clock, mlp_out_w,
+                     mlp_out_b, mf_pred, final_w, final_b, mlp_pred, prob);
+}
+
 template <bool BF>
 static int mlp_fwd_impl(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
                         int64_t n_layers, const int64_t* hidden, float eps, float dropout_p,
@@ -802,29 +845,95 @@ static int mlp_fwd_impl(const float* x, int64_t n, int64_t dim, const ncf_mlp_la
                         const float* mlp_out_b, const float* mf_pred, const float* final_w,
                         const float* final_b, float* mlp_pred, float* prob, void* stream) {
   NCF_CHECK_ARG(n >= 0 && tower_ok(dim, n_layers, hidden),
-                "ncf_mlp_fwd: unsupported tower (need input 64, hidden [256,128,64])");
+                "ncf_mlp_fwd: unsupported tower (need input 64 or 128, hidden [256,128,64])");
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_mlp_fwd: dropout_p out of [0,1)");
   if (n == 0) return NCF_OK;
   TowerArgs a;
-  const int rc = make_args(layers, seed, a);
+  const int rc = make_args(layers, seed, dim, a);
   if (rc) return rc;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_mlp_fwd<kFwdRT, kFwdVR, BF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsFwd);
-    attr = true;
-  }
-  hipLaunchKernelGGL((k_mlp_fwd<kFwdRT, kFwdVR, BF>), dim3((unsigned)ncf_cdiv(n, kFwdVR)),
-                     dim3(kThreads), kLdsFwd,
-                     (hipStream_t)stream, x, n, a, eps, dropout_p, clock, mlp_out_w, mlp_out_b,
-                     mf_pred, final_w, final_b, mlp_pred, prob);
+  hipStream_t st = (hipStream_t)stream;
+  if (dim == 64)
+    launch_fwd<64, BF>(x, n, a, eps, dropout_p, clock, mlp_out_w, mlp_out_b, mf_pred, final_w,
+                       final_b, mlp_pred, prob, st);
+  else
+    launch_fwd<128, BF>(x, n, a, eps, dropout_p, clock, mlp_out_w, mlp_out_b, mf_pred, final_w,
+                        final_b, mlp_pred, prob, st);
   NCF_CHECK_LAUNCH("ncf_mlp_fwd");
   return NCF_OK;
 }
 
+// sized for the widest supported input (K0 = 128), so one workspace serves either width
 extern "C" int64_t ncf_mlp_bwd_workspace(int64_t n) {
   const int64_t nb = n == 0 ? 1 : ncf_cdiv(n, kRows);
-  return nb * kPartW + 2 * ncf_reduce_scratch((int)nb, kPartW);
+  constexpr int W = Lay<128>::kPartW;
+  return nb * W + 2 * ncf_reduce_scratch((int)nb, W);
+}
+
+template <int K0>
+static int defer_tower(const TowerArgs& a, const ncf_head_args* head, const ncf_head_args& h,
+                       float inv_n, bool fw, int nb, float* workspace, ncf_reduce_list* lst) {
+  using T = Lay<K0>;
+  constexpr int PW = T::kPartW;
+  int rc = NCF_OK;
+  // per layer: [dbias | dgamma | dbeta] partial columns -> one strided reduction when the three
+  // outputs are equally spaced (consecutive parameters of the flat gradient buffer)
+  const int widths[3] = {N0, N1, N2};
+  const int64_t offs[3] = {3 * (N2 + N1), 3 * N2, 0};
+  for (int l = 0; l < 3 && !rc; ++l) {
+    const int W = widths[l];
+    const float* pp = workspace + offs[l];
+    const ncf_mlp_layer& L = a.l[l];
+    const ptrdiff_t s1 = L.dgamma - L.dbias, s2 = L.dbeta - L.dgamma;
+    if (s1 == s2 && s1 >= W) {
+      rc = ncf_defer(lst, pp, nb, PW, 3 * W, L.dbias, 0, W, s1);
+    } else {
+      rc = ncf_defer(lst, pp, nb, PW, W, L.dbias, 0, W, W);
+      if (!rc) rc = ncf_defer(lst, pp + W, nb, PW, W, L.dgamma, 0, W, W);
+      if (!rc) rc = ncf_defer(lst, pp + 2 * W, nb, PW, W, L.dbeta, 0, W, W);
+    }
+  }
+  if (!rc && fw) {   // weight gradients (mlp.0's first K0 columns of its ldw-wide rows)
+    rc = ncf_defer(lst, workspace + T::kW0, nb, PW, N0 * K0, a.l[0].dw, 0, K0, a.l[0].ldw);
+    if (!rc) rc = ncf_defer(lst, workspace + T::kW1, nb, PW, N1 * N0, a.l[1].dw, 0, N0, a.l[1].ldw);
+    if (!rc) rc = ncf_defer(lst, workspace + T::kW2, nb, PW, N2 * N1, a.l[2].dw, 0, N1, a.l[2].ldw);
+  }
+  if (!rc && head) {
+    // head partials: one reduction when the flat gradient buffer lays the six head parameters
+    // out like the partial row, else one per parameter; the BCE sum scaled by 1/n into loss
+    const float* hp = workspace + 3 * (N0 + N1 + N2);   // (within each partial row)
+    float* base = h.grad_mf_out_w;
+    const bool flat = h.grad_mf_out_b == base + T::kHmfB && h.grad_mlp_out_w == base + T::kHmlW &&
+                      h.grad_mlp_out_b == base + T::kHmlB && h.grad_final_w == base + T::kHfW &&
+                      h.grad_final_b == base + T::kHfB;
+    if (flat) {
+      rc = ncf_defer(lst, hp, nb, PW, T::kHfB + 1, base, 0, T::kHfB + 1, T::kHfB + 1);
+    } else {
+      rc = ncf_defer(lst, hp + T::kHmfW, nb, PW, K0, h.grad_mf_out_w, 0, K0, K0);
+      if (!rc) rc = ncf_defer(lst, hp + T::kHmfB, nb, PW, 1, h.grad_mf_out_b, 0, 1, 1);
+      if (!rc) rc = ncf_defer(lst, hp + T::kHmlW, nb, PW, N2, h.grad_mlp_out_w, 0, N2, N2);
+      if (!rc) rc = ncf_defer(lst, hp + T::kHmlB, nb, PW, 1, h.grad_mlp_out_b, 0, 1, 1);
+      if (!rc) rc = ncf_defer(lst, hp + T::kHfW, nb, PW, 2, h.grad_final_w, 0, 2, 2);
+      if (!rc) rc = ncf_defer(lst, hp + T::kHfB, nb, PW, 1, h.grad_final_b, 0, 1, 1);
+    }
+    if (!rc && h.loss) rc = ncf_defer(lst, hp + T::kHloss, nb, PW, 1, h.loss, 0, 1, 1, inv_n);
+  }
+  return rc;
+}
+
+template <int K0, bool BF>
+static void launch_bwd(const float* grad_a_last, int64_t n, const TowerArgs& a, float dropout_p,
+                       const ncf_step_clock* clock, float* grad_x, float* workspace,
+                       const ncf_head_args& h, int fused_head, float inv_n, const float* x, int fw,
+                       hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_mlp_bwd<K0, BF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_mlp_bwd<K0, BF>), dim3((unsigned)ncf_cdiv(n, kRows)), dim3(kThreads), kLds,
+                     st, grad_a_last, n, a, dropout_p, clock, grad_x, workspace, h, fused_head,
+                     inv_n, x, fw);
 }
 
 template <bool BF>
@@ -834,7 +943,7 @@ static int mlp_bwd_impl(const float* grad_a_last, int64_t n, int64_t dim, const 
                         const ncf_head_args* head, float* grad_x, float* workspace,
                         int64_t workspace_floats, ncf_reduce_list* defer, void* stream) {
   NCF_CHECK_ARG(n >= 0 && tower_ok(dim, n_layers, hidden),
-                "ncf_mlp_bwd: unsupported tower (need input 64, hidden [256,128,64])");
+                "ncf_mlp_bwd: unsupported tower (need input 64 or 128, hidden [256,128,64])");
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_mlp_bwd: dropout_p out of [0,1)");
   if (workspace_floats < ncf_mlp_bwd_workspace(n)) {
     ncf_set_error("ncf_mlp_bwd: workspace too small");
@@ -842,7 +951,7 @@ static int mlp_bwd_impl(const float* grad_a_last, int64_t n, int64_t dim, const 
   }
   if (n == 0) return NCF_OK;
   TowerArgs a;
-  int rc = make_args(layers, seed, a);
+  int rc = make_args(layers, seed, dim, a);
   if (rc) return rc;
   for (int l = 0; l < 3; ++l)
     if (!a.l[l].r || !a.l[l].mean || !a.l[l].rstd || !a.l[l].dgamma || !a.l[l].dbeta ||
@@ -870,66 +979,25 @@ static int mlp_bwd_impl(const float* grad_a_last, int64_t n, int64_t dim, const 
   } else {
     NCF_CHECK_ARG(grad_a_last != nullptr, "ncf_mlp_bwd: grad_a_last or head required");
   }
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_mlp_bwd<BF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
-    attr = true;
-  }
   const int nb = (int)ncf_cdiv(n, kRows);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL((k_mlp_bwd<BF>), dim3((unsigned)nb), dim3(kThreads), kLds, st, grad_a_last, n, a,
-                     dropout_p, clock, grad_x, workspace, h, head ? 1 : 0, inv_n, x, fw ? 1 : 0);
+  if (dim == 64)
+    launch_bwd<64, BF>(grad_a_last, n, a, dropout_p, clock, grad_x, workspace, h, head ? 1 : 0,
+                       inv_n, x, fw ? 1 : 0, st);
+  else
+    launch_bwd<128, BF>(grad_a_last, n, a, dropout_p, clock, grad_x, workspace, h, head ? 1 : 0,
+                        inv_n, x, fw ? 1 : 0, st);
   NCF_CHECK_LAUNCH("ncf_mlp_bwd");
-  // per layer: [dbias | dgamma | dbeta] partial columns -> one strided reduction when the three
-  // outputs are equally spaced (consecutive parameters of the flat gradient buffer)
   ncf_reduce_list local;
   local.count = 0;
   ncf_reduce_list* lst = defer ? defer : &local;
-  const int widths[3] = {N0, N1, N2};
-  const int64_t offs[3] = {3 * (N2 + N1), 3 * N2, 0};
-  for (int l = 0; l < 3 && !rc; ++l) {
-    const int W = widths[l];
-    const float* pp = workspace + offs[l];
-    const ncf_mlp_layer& L = a.l[l];
-    const ptrdiff_t s1 = L.dgamma - L.dbias, s2 = L.dbeta - L.dgamma;
-    if (s1 == s2 && s1 >= W) {
-      rc = ncf_defer(lst, pp, nb, kPartW, 3 * W, L.dbias, 0, W, s1);
-    } else {
-      rc = ncf_defer(lst, pp, nb, kPartW, W, L.dbias, 0, W, W);
-      if (!rc) rc = ncf_defer(lst, pp + W, nb, kPartW, W, L.dgamma, 0, W, W);
-      if (!rc) rc = ncf_defer(lst, pp + 2 * W, nb, kPartW, W, L.dbeta, 0, W, W);
-    }
-  }
-  if (!rc && fw) {   // weight gradients (mlp.0's first K0 columns of its ldw-wide rows)
-    rc = ncf_defer(lst, workspace + kW0, nb, kPartW, N0 * K0, a.l[0].dw, 0, K0, a.l[0].ldw);
-    if (!rc) rc = ncf_defer(lst, workspace + kW1, nb, kPartW, N1 * N0, a.l[1].dw, 0, N0, a.l[1].ldw);
-    if (!rc) rc = ncf_defer(lst, workspace + kW2, nb, kPartW, N2 * N1, a.l[2].dw, 0, N1, a.l[2].ldw);
-  }
-  if (!rc && head) {
-    // head partials: one reduction when the flat gradient buffer lays the six head parameters
-    // out like the partial row, else one per parameter; the BCE sum scaled by 1/n into loss
-    const float* hp = workspace + 3 * (N0 + N1 + N2);   // (within each partial row)
-    float* base = h.grad_mf_out_w;
-    const bool flat = h.grad_mf_out_b == base + kHmfB && h.grad_mlp_out_w == base + kHmlW &&
-                      h.grad_mlp_out_b == base + kHmlB && h.grad_final_w == base + kHfW &&
-                      h.grad_final_b == base + kHfB;
-    if (flat) {
-      rc = ncf_defer(lst, hp, nb, kPartW, kHfB + 1, base, 0, kHfB + 1, kHfB + 1);
-    } else {
-      rc = ncf_defer(lst, hp + kHmfW, nb, kPartW, 64, h.grad_mf_out_w, 0, 64, 64);
-      if (!rc) rc = ncf_defer(lst, hp + kHmfB, nb, kPartW, 1, h.grad_mf_out_b, 0, 1, 1);
-      if (!rc) rc = ncf_defer(lst, hp + kHmlW, nb, kPartW, 64, h.grad_mlp_out_w, 0, 64, 64);
-      if (!rc) rc = ncf_defer(lst, hp + kHmlB, nb, kPartW, 1, h.grad_mlp_out_b, 0, 1, 1);
-      if (!rc) rc = ncf_defer(lst, hp + kHfW, nb, kPartW, 2, h.grad_final_w, 0, 2, 2);
-      if (!rc) rc = ncf_defer(lst, hp + kHfB, nb, kPartW, 1, h.grad_final_b, 0, 1, 1);
-    }
-    if (!rc && h.loss) rc = ncf_defer(lst, hp + kHloss, nb, kPartW, 1, h.loss, 0, 1, 1, inv_n);
-  }
+  rc = dim == 64 ? defer_tower<64>(a, head, h, inv_n, fw, nb, workspace, lst)
+                 : defer_tower<128>(a, head, h, inv_n, fw, nb, workspace, lst);
   if (rc) return rc;
   if (!defer) {
-    float* scr = workspace + (int64_t)nb * kPartW;
-    return ncf_reduce_batch(lst, scr, workspace_floats - (int64_t)nb * kPartW, stream);
+    const int64_t PW = dim == 64 ? Lay<64>::kPartW : Lay<128>::kPartW;
+    float* scr = workspace + (int64_t)nb * PW;
+    return ncf_reduce_batch(lst, scr, workspace_floats - (int64_t)nb * PW, stream);
   }
   return NCF_OK;
 }

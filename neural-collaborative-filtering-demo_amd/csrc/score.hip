@@ -1051,17 +1051,30 @@ extern "C" int ncf_score_kth(const float* logits, int64_t n_users, int64_t S, in
                              const float* item_bias, int64_t stride, float* thr, void* stream) {
   NCF_CHECK_ARG(n_users >= 0 && S >= 1 && K >= 1 && stride >= 1, "ncf_score_kth: bad size");
   if (n_users == 0) return NCF_OK;
-  if (S <= kKthLdsMax) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)k_kth_lds<512>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(uint32_t) * kKthLdsMax));
-      (void)hipFuncSetAttribute((const void*)k_kth_lds<1024>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(uint32_t) * kKthLdsMax));
-      attr = true;
+  // The LDS-resident sample needs 4 S bytes of dynamic LDS (152 KB at kKthLdsMax: a 160 KB
+  // part).  The limit is taken from the device once: a part with less LDS, or an attribute the
+  // runtime refuses, sends every sample to the streaming k_kth instead of failing the launch.
+  static int64_t lds_max = -1;
+  if (lds_max < 0) {
+    int dev = 0, smem = 0;
+    int64_t lim = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&smem, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess) {
+      lim = ((int64_t)smem - 8192) / (int64_t)sizeof(uint32_t);   // static LDS of k_kth_lds < 8 KB
+      lim = lim < kKthLdsMax ? lim : kKthLdsMax;
     }
+    const int bytes = (int)(sizeof(uint32_t) * (lim > 0 ? lim : 1));
+    if (lim <= 0 ||
+        hipFuncSetAttribute((const void*)k_kth_lds<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            bytes) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_kth_lds<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      lim = 0;
+    }
+    lds_max = lim;
+  }
+  if (S <= lds_max) {
     // measured: S = 38912 (top-100) 0.75 -> 0.55 ms with 1024 threads; S = 9984 (top-10) 0.12 ms
     // with 512 against 0.16 with 1024
     if (S > 16384)

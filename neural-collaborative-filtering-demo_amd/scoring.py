@@ -259,6 +259,10 @@ class GraphedScorer:
 
         scorer = GraphedScorer(model, n_users=10_000, k=10)
         scores, items = scorer(user_ids)        # [n, k] each, like score_topk
+
+    The graph writes into static output tensors.  By default a call returns fresh copies of
+    them (like ``score_topk``); ``scorer(user_ids, copy=False)`` returns the static tensors
+    themselves, which the NEXT call overwrites in place.
     """
 
     def __init__(self, model, n_users: int, k: int = 10, index: Optional[ItemIndex] = None,
@@ -287,7 +291,8 @@ class GraphedScorer:
             self.out = run.result()
         self.version = idx.version
 
-    def __call__(self, user_ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    def __call__(self, user_ids: torch.Tensor,
+                 copy: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
         if not self.index.valid_for(self.model):
             self.index = ItemIndex(self.model, items=self.index.ids)
             self._capture()
@@ -303,8 +308,10 @@ class GraphedScorer:
             raise IndexError("score_topk: user id out of range of the embedding table")
         if over:
             run.redo_overflow(_lib.stream_ptr(run.uid.device))
-            return run.result()
-        return self.out
+            out = run.result()
+        else:
+            out = self.out
+        return (out[0].clone(), out[1].clone()) if copy else out
 
 
 def shard_items(num_items: int, world: int, rank: int) -> torch.Tensor:

@@ -473,20 +473,23 @@ def _fused_run(deferred, steps, sweep_every=64, U=3000, I=500, B=64, seed=11, dr
     return sd, mom
 
 
-@pytest.mark.parametrize("H,M,B", [(4, 5, 37), (1, 5, 16), (8, 3, 50), (2, 6, 33), (4, 1, 20)])
-def test_attn_block_matches_unfused(monkeypatch, H, M, B):
+@pytest.mark.parametrize("D,H,M,B", [(64, 4, 5, 37), (64, 1, 5, 16), (64, 8, 3, 50), (64, 2, 6, 33),
+                                     (64, 4, 1, 20), (128, 4, 5, 37), (128, 8, 6, 19),
+                                     (128, 2, 3, 41), (128, 4, 1, 9)])
+def test_attn_block_matches_unfused(monkeypatch, D, H, M, B):
     """The one-launch attention block (attn_block.hip) vs the unfused launches (projection
     GEMMs + attention.hip core), dropout on (same stream): one fused train step's probabilities,
     dense gradients and compact table gradients agree to the grads tolerance.  B not a multiple
-    of the 16-group tile exercises the ragged last workgroup."""
+    of the 16-group (D = 64) / 8-group (D = 128, C4) tile exercises the ragged last workgroup;
+    D = 128 with M = 5 also has zero padding rows inside every tile (40 rows in 3 row tiles)."""
     from ncf_amd.trainer import FusedTrainStep
     out = []
     for flag in ("0", "1"):
         monkeypatch.setenv("NCF_ATTN_BLOCK", flag)
         torch.manual_seed(21)
-        m = ncf.AdvancedNCF(400, 300, 5, 24, 64, 64, 32, [256, 128, 64], H, 0.2, M - 1).to(DEV)
+        m = ncf.AdvancedNCF(400, 300, 5, 24, D, D, 32, [256, 128, 64], H, 0.2, M - 1).to(DEV)
         step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
-        assert m.engine.attn_block(64, H, M) == (flag == "1")
+        assert m.engine.attn_block(D, H, M) == (flag == "1")
         g = torch.Generator().manual_seed(22)
         u = torch.randint(0, 400, (B,), generator=g).repeat_interleave(M).to(DEV)
         i = torch.randint(0, 300, (B * M,), generator=g).to(DEV)
@@ -506,9 +509,11 @@ def test_attn_block_matches_unfused(monkeypatch, H, M, B):
         torch.testing.assert_close(G1[k], G0[k], rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("H,M,B,drop", [(4, 5, 37, 0.2), (1, 5, 16, 0.2), (8, 3, 50, 0.2),
-                                         (2, 6, 33, 0.0), (4, 1, 20, 0.2)])
-def test_attn_block_recompute_bitwise_equals_stash(monkeypatch, H, M, B, drop):
+@pytest.mark.parametrize("D,H,M,B,drop", [(64, 4, 5, 37, 0.2), (64, 1, 5, 16, 0.2),
+                                           (64, 8, 3, 50, 0.2), (64, 2, 6, 33, 0.0),
+                                           (64, 4, 1, 20, 0.2), (128, 4, 5, 37, 0.2),
+                                           (128, 8, 6, 19, 0.0)])
+def test_attn_block_recompute_bitwise_equals_stash(monkeypatch, D, H, M, B, drop):
     """The recompute backward (ncf_attn_block_bwd_rc: q/k/v re-projected and the core forward
     re-run in LDS, nothing stashed by the forward) against the stashing form: same code for the
     projections and the core, so the step's probabilities, every dense gradient and the compact
@@ -518,9 +523,9 @@ def test_attn_block_recompute_bitwise_equals_stash(monkeypatch, H, M, B, drop):
     for flag in ("0", "1"):
         monkeypatch.setenv("NCF_ATTN_RC", flag)
         torch.manual_seed(23)
-        m = ncf.AdvancedNCF(400, 300, 5, 24, 64, 64, 32, [256, 128, 64], H, drop, M - 1).to(DEV)
+        m = ncf.AdvancedNCF(400, 300, 5, 24, D, D, 32, [256, 128, 64], H, drop, M - 1).to(DEV)
         step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
-        assert m.engine.attn_rc(64, H, M) == (flag == "1")
+        assert m.engine.attn_rc(D, H, M) == (flag == "1")
         g = torch.Generator().manual_seed(24)
         u = torch.randint(0, 400, (B,), generator=g).repeat_interleave(M).to(DEV)
         i = torch.randint(0, 300, (B * M,), generator=g).to(DEV)
@@ -543,21 +548,22 @@ def test_attn_block_recompute_bitwise_equals_stash(monkeypatch, H, M, B, drop):
 
 
 @pytest.mark.parametrize("wgrad", ["1", "0"])
-@pytest.mark.parametrize("B,drop", [(37, 0.2), (64, 0.0), (1, 0.2), (300, 0.2)])
-def test_mlp_tower_matches_unfused(monkeypatch, B, drop, wgrad):
+@pytest.mark.parametrize("B,drop,D", [(37, 0.2, 64), (64, 0.0, 64), (1, 0.2, 64), (300, 0.2, 64),
+                                      (37, 0.2, 128), (64, 0.0, 128), (300, 0.2, 128)])
+def test_mlp_tower_matches_unfused(monkeypatch, B, drop, D, wgrad):
     """The one-launch MLP tower (mlp_tower.hip, forward + backward) vs the per-layer launches
     (GEMM + rowops + head), same dropout stream: probabilities, saved activations, dense and
     compact table gradients agree to the grads tolerance; n = 5B rows not a multiple of the
-    32-row tile exercises the ragged last workgroup."""
+    32-row tile exercises the ragged last workgroup.  D = 128 is C4's input width."""
     from ncf_amd.trainer import FusedTrainStep
     out = []
     monkeypatch.setenv("NCF_MLP_WGRAD", wgrad)
     for flag in ("0", "1"):
         monkeypatch.setenv("NCF_MLP_FUSED", flag)
         torch.manual_seed(31)
-        m = ncf.AdvancedNCF(400, 300, 5, 24, 64, 64, 32, [256, 128, 64], 4, drop, 4).to(DEV)
+        m = ncf.AdvancedNCF(400, 300, 5, 24, D, D, 32, [256, 128, 64], 4, drop, 4).to(DEV)
         step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
-        assert m.engine.mlp_fused(64, [256, 128, 64]) == (flag == "1")
+        assert m.engine.mlp_fused(D, [256, 128, 64]) == (flag == "1")
         g = torch.Generator().manual_seed(32)
         u = torch.randint(0, 400, (B,), generator=g).repeat_interleave(5).to(DEV)
         i = torch.randint(0, 300, (B * 5,), generator=g).to(DEV)
@@ -1464,14 +1470,17 @@ def test_f8_device_sampler_matches_reference_draws(f8):
         assert np.all(np.abs(a - b) <= 6 * sig + 1e-9), (u, np.max(np.abs(a - b) / (sig + 1e-12)))
 
 
-@pytest.mark.parametrize("W,D", [(3, 64), (2, 16), (8, 32)])
-def test_shard_exchange_kernels_emulated_ranks(W, D):
+@pytest.mark.parametrize("W,D,U,I", [(3, 64, 1000, 300), (2, 16, 1000, 300), (8, 32, 1000, 300),
+                                     (8, 128, 1000, 300), (8, 128, 50_000_000, 5_000_000)])
+def test_shard_exchange_kernels_emulated_ranks(W, D, U, I):
     """The row-sharded step's exchange kernels (exchange.hip) for W ranks emulated on one GPU:
     plan (owner-ordered keys, counts, destination-major send layout, spos, inverse), the
     all-to-all emulated by slicing, owner-side sort-free dedup (unique rows, pos table), owner
-    gather, rank-ordered gradient sums (bitwise vs a sequential fp32 sum), rows in/out."""
+    gather, rank-ordered gradient sums (bitwise vs a sequential fp32 sum), rows in/out.
+    The last case is C4's 8-GPU split (BASELINE configs[3]: 50M x 5M, D = 128): global ids
+    above 2^31 / D, 6.25M-row user shards (3.2 GB per emulated shard table)."""
     from ncf_amd import _lib
-    U, I, n = 1000, 300, 60
+    n = 60
     Ru, Ri = -(-U // W), -(-I // W)
     g = torch.Generator().manual_seed(W * 100 + D)
     i64 = dict(dtype=torch.int64, device=DEV)
@@ -1526,8 +1535,8 @@ def test_shard_exchange_kernels_emulated_ranks(W, D):
         plans.append(dict(bufs=bufs, counts=counts, send=send, off=layout_off, uid=uid, iid=iid))
     assert int(err) == 0
     # owners: emulated all-to-all + sort-free dedup + gather + gradient sums
-    tables = [torch.randn(Ru, D, generator=g).to(DEV), torch.randn(Ru, D, generator=g).to(DEV),
-              torch.randn(Ri, D, generator=g).to(DEV), torch.randn(Ri, D, generator=g).to(DEV)]
+    gd = torch.Generator(device=DEV).manual_seed(W * 100 + D + 1)
+    tables = [torch.randn(R_, D, generator=gd, device=DEV) for R_ in (Ru, Ru, Ri, Ri)]
     mark = [torch.zeros(Ru, **i32), torch.zeros(Ri, **i32)]
     uidx = [torch.zeros(Ru, **i32), torch.zeros(Ri, **i32)]
     for token, o_ in enumerate(range(W), start=1):
@@ -1580,8 +1589,8 @@ def test_shard_exchange_kernels_emulated_ranks(W, D):
                         acc = acc + gc[int(P[u, s])]
                 assert torch.equal(G[2 * k][u].cpu(), acc[:D])
                 assert torch.equal(G[2 * k + 1][u].cpu(), acc[D:])
-            t0, t1 = tables[2 * k].cpu(), tables[2 * k + 1].cpu()
-            assert torch.equal(rows[sel].cpu(), torch.cat([t0[rc[sel]], t1[rc[sel]]], 1))
+            ix = rc[sel].to(DEV)
+            assert torch.equal(rows[sel.to(DEV)], torch.cat([tables[2 * k][ix], tables[2 * k + 1][ix]], 1))
     assert int(err) == 0
     # requester rows in / gradients out
     p = plans[0]
