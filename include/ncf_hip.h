@@ -665,6 +665,17 @@ int ncf_adam_pairs_catchup_lock_clock(const ncf_table_pair* pairs, int npairs, i
                                       const ncf_step_clock* clock, const float* step_table,
                                       double beta1, double beta2, double eps, double weight_decay,
                                       void* stream);
+/* The catch-up of the rows named by RAW id lists (ids0 for pairs[0], ids1 for pairs[1], n
+ * occurrences each, duplicates allowed): the first occurrence of a row to raise its stamp to the
+ * target (atomicMax) replays it, the others skip: the same rows, bit-identical, with no dedup
+ * before the forward (the id sort can then run beside it on another stream).  Replaces the
+ * dedup + ncf_adam_pairs_catchup_clock pair before the gathers of the reference call pattern
+ * (src/model/trainer.py:258, the forward of a train step). */
+int ncf_adam_pairs_catchup_claim_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
+                                       const int64_t* ids0, const int64_t* ids1, int64_t n,
+                                       int32_t target_rel, const ncf_step_clock* clock,
+                                       const float* step_table, double beta1, double beta2,
+                                       double eps, double weight_decay, void* stream);
 int ncf_adam_pairs_apply_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
                                const uint32_t* count, int64_t max_n, int32_t step_rel,
                                const ncf_step_clock* clock, const float* step_table, double beta1,

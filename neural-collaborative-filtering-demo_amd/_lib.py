@@ -127,6 +127,8 @@ SIGNATURES = {
                                      F64, F64, P]),
     "ncf_adam_pairs_catchup_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
     "ncf_adam_pairs_catchup_lock_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
+    "ncf_adam_pairs_catchup_claim_clock": (I32, [P, I32, I64, P, P, I64, I32, P, P, F64, F64, F64,
+                                                 F64, P]),
     "ncf_adam_pairs_apply_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
     "ncf_adam_pairs_sweep_rolling": (I32, [P, I32, I64, I32, I32, P, P, F64, F64, F64, F64, P]),
     "ncf_adam_pairs_sweep_rolling_part": (I32, [P, I32, I64, I32, I32, I32, I32, P, P, F64, F64, F64,

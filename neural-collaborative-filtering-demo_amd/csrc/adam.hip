@@ -423,6 +423,36 @@ __global__ __launch_bounds__(256) void k_pairs_catchup(const PairArgs a, const u
   if (sub == 0 && (lock || from < target)) stamp[row] = lock ? (target | NCF_STAMP_LOCK) : target;
 }
 
+// Claim form of the pair catch-up, with no dedup before it: one row-group of lanes per
+// OCCURRENCE ids[k][0 .. n).  The first occurrence of a row to raise its stamp to `target`
+// (atomicMax) replays it; every other occurrence sees the raised stamp and skips.  Exactly one
+// replay per row, the same replay as k_pairs_catchup (bit-identical rows), so the id sort the
+// backward needs can run on another stream beside the forward.  Locked rows (stamp = t |
+// NCF_STAMP_LOCK) compare above any target and are left alone.  Out-of-range ids are skipped
+// (the gather flags them).
+template <int D, bool BF = false>
+__global__ __launch_bounds__(256) void k_pairs_catchup_claim(const PairArgs a,
+                                                             const int64_t* __restrict__ ids0,
+                                                             const int64_t* __restrict__ ids1,
+                                                             int64_t n, int32_t target_rel,
+                                                             const ncf_step_clock* __restrict__ clock,
+                                                             const float* __restrict__ table,
+                                                             AdamScalars s) {
+  constexpr int L = Replay<D>::LPR;   // lanes per row
+  const int k = blockIdx.y;
+  const int64_t tt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = tt / L;
+  const int sub = (int)(tt % L);
+  if (c >= n) return;
+  const int64_t row = (k ? ids1 : ids0)[c];
+  if (row < 0 || row >= a.rows[k]) return;
+  const int32_t target = clock->t + target_rel;
+  int32_t from = target;
+  if (sub == 0) from = atomicMax(&a.stamp[k][row], target);
+  from = __shfl(from, (int)(threadIdx.x & 63) - sub, 64);   // the claim of this row's lane group
+  catch_up_row<D, BF>(a.t[k], row, sub, from, target, table, s);
+}
+
 template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void k_pairs_apply(const PairArgs a, const uint32_t* __restrict__ count,
                                                      int64_t max_n, int32_t step_rel,
@@ -927,6 +957,39 @@ extern "C" int ncf_adam_pairs_catchup_clock(const ncf_table_pair* pairs, int npa
                 "ncf_adam_pairs_catchup_clock: bad args");
   if (max_n <= 0) return NCF_OK;
   NCF_DISPATCH_DIM(dim, pairs_catchup_d, pair_args(pairs, npairs), npairs, count, max_n,
+                   target_rel, clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
+                   (hipStream_t)stream);
+}
+
+template <int D>
+int pairs_claim_d(PairArgs a, int npairs, const int64_t* ids0, const int64_t* ids1, int64_t n,
+                  int32_t rel, const ncf_step_clock* clock, const float* table, AdamScalars s,
+                  hipStream_t st) {
+  const dim3 grid((unsigned)ncf_cdiv(n * Replay<D>::LPR, 256), npairs);
+  if (a.bf)
+    hipLaunchKernelGGL((k_pairs_catchup_claim<D, true>), grid, dim3(256), 0, st, a, ids0, ids1, n,
+                       rel, clock, table, s);
+  else
+    hipLaunchKernelGGL((k_pairs_catchup_claim<D, false>), grid, dim3(256), 0, st, a, ids0, ids1, n,
+                       rel, clock, table, s);
+  NCF_CHECK_LAUNCH("ncf_adam_pairs_catchup_claim_clock");
+  return NCF_OK;
+}
+
+// the catch-up of the rows of raw (not deduplicated) id lists: ids0 for pair 0, ids1 for pair 1,
+// n occurrences each (k_pairs_catchup_claim)
+extern "C" int ncf_adam_pairs_catchup_claim_clock(const ncf_table_pair* pairs, int npairs,
+                                                  int64_t dim, const int64_t* ids0,
+                                                  const int64_t* ids1, int64_t n,
+                                                  int32_t target_rel, const ncf_step_clock* clock,
+                                                  const float* step_table, double beta1,
+                                                  double beta2, double eps, double weight_decay,
+                                                  void* stream) {
+  NCF_CHECK_ARG(pairs && npairs >= 1 && npairs <= 2 && ids0 && (npairs < 2 || ids1) && clock &&
+                    step_table && n >= 0,
+                "ncf_adam_pairs_catchup_claim_clock: bad args");
+  if (n == 0) return NCF_OK;
+  NCF_DISPATCH_DIM(dim, pairs_claim_d, pair_args(pairs, npairs), npairs, ids0, ids1, n,
                    target_rel, clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
                    (hipStream_t)stream);
 }

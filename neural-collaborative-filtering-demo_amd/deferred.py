@@ -29,6 +29,9 @@ from . import _lib
 from ._lib import ptr
 
 _KINDS = (("user", "mf_user", "mlp_user"), ("item", "mf_item", "mlp_item"))
+# Catch-up by claim (no id sort before the forward) when the batch was not sorted ahead;
+# NCF_CLAIM_CATCHUP=0: sort inline, then catch up the unique rows (A/B)
+CLAIM_CATCHUP = os.environ.get("NCF_CLAIM_CATCHUP", "1") != "0"
 _SERIAL = itertools.count(1)      # distinguishes schedules in workspace caches (ids recycle)
 
 
@@ -308,6 +311,10 @@ class DeferredTableAdam:
         eng = self.engine
         m = eng.model
         n = w.g.n
+        if (CLAIM_CATCHUP and self.clock is not None and n > 0 and not getattr(w, "prededuped", None)
+                and self._early_req is None and not torch.cuda.is_current_stream_capturing()):
+            self._prepare_claim(w, uid, iid, st)
+            return
         if not getattr(w, "prededuped", None):   # else: sorted ahead on a side stream (trainer)
             _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, w.g.D, m.num_users, m.num_products,
                       ptr(w.uniq_u), ptr(w.uniq_i), None, None, ptr(w.num_unique), ptr(w.emb_ws),
@@ -335,6 +342,38 @@ class DeferredTableAdam:
             return
         self.catchup_rows("user", w.uniq_u, w.num_unique, 0, n, st)
         self.catchup_rows("item", w.uniq_i, w.num_unique, 1, n, st)
+
+    def _prepare_claim(self, w, uid, iid, st):
+        """The step's rows caught up straight from the raw id lists (a claim per row,
+        ncf_adam_pairs_catchup_claim_clock: no sort before the gathers), and the id sort the
+        backward and the table apply need forked onto a side stream beside the forward; the
+        engine joins it before the embedding backward (w.dedup_ev).  The reference call pattern
+        (model(kjt) -> loss.backward() -> Adam.step(), trainer.py:258-285) has no next batch to
+        sort ahead, so without this its sort sat on the critical path."""
+        m = self.engine.model
+        n = w.g.n
+        self._ensure(self.t + 1)
+        pairs = self._pairs_for(w)
+        _lib.call("ncf_adam_pairs_catchup_claim_clock", ctypes.addressof(pairs), 2,
+                  m.mlp_embedding_dim, ptr(uid), ptr(iid), n, 0, ptr(self.clock),
+                  ptr(self._table), *self._consts(), st)
+        dev = self.clock.device
+        side = getattr(self, "_dedup_side", None)
+        if side is None or side.device != dev:
+            side = self._dedup_side = torch.cuda.Stream(dev)
+            self._dedup_evs = [torch.cuda.Event() for _ in range(2)]
+        cur = torch.cuda.current_stream(dev)
+        self._dedup_evs[0].record(cur)
+        side.wait_event(self._dedup_evs[0])
+        uid.record_stream(side)
+        iid.record_stream(side)
+        _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, w.g.D, m.num_users, m.num_products,
+                  ptr(w.uniq_u), ptr(w.uniq_i), None, None, ptr(w.num_unique), ptr(w.emb_ws),
+                  w.emb_ws.numel(), side.cuda_stream)
+        self._dedup_evs[1].record(side)
+        w.dedup_ev = self._dedup_evs[1]
+        w.prededuped = None
+        w.deduped = True
 
     def request_early(self, side, uniq_u, uniq_i, num_unique, n):
         """Ask the next prepare() (this step's) to catch up the next batch's unique rows

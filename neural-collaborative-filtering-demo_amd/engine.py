@@ -765,6 +765,10 @@ class NCFEngine:
         uq_u, uq_i = uniq if uniq is not None else (w.uniq_u, w.uniq_i)
         d_rows = rows or (m.num_users, m.num_products)
         w.slots_set = False
+        ev = getattr(w, "dedup_ev", None)
+        if ev is not None:   # the id sort forked beside the forward (deferred._prepare_claim)
+            torch.cuda.current_stream(dev).wait_event(ev)
+            w.dedup_ev = None
         if not getattr(w, "deduped", False):   # sort/deduplicate now (slot maps for the Adam)
             _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, D, m.num_users, m.num_products,
                       ptr(w.uniq_u), ptr(w.uniq_i), ptr(self.slot_u), ptr(self.slot_i),
