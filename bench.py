@@ -340,8 +340,8 @@ def c4_train(ncf, dev, warmup, steps, prime=0):
     their Adam moments (112.6 GB) are resident in one GPU's 288 GB HBM, built there directly
     (torch.device context: no 56 GB host staging).  Same step as the headline (FusedTrainStep:
     forward, fused BCE, backward, deferred dense-exact Adam over all 14.08B table parameters),
-    timed after the deferred schedule's steady-state warm-up.  D = 128 runs the general
-    (unfused) attention / MLP launches."""
+    timed after the deferred schedule's steady-state warm-up.  D = 128 runs the fused attention
+    block (8 groups per workgroup) and the fused MLP tower (128-wide input)."""
     from ncf_amd import _lib as L
     from ncf_amd.trainer import FusedTrainStep
     c = C4
@@ -378,6 +378,25 @@ def c4_train(ncf, dev, warmup, steps, prime=0):
     per = {}
     for name, _, e0, e1 in prof:
         per[name] = per.get(name, 0.0) + e0.elapsed_time(e1) / 20
+    # The same kernels with the rolling sweep on the step's own stream: overlapped, the sweep
+    # (the C4 step's bound on one GPU: 14.08B table parameters) holds the CUs the Linear kernels
+    # wait for, so their in-step spans above measure the sweep, not them
+    dfr = step.deferred
+    iso = {}
+    if dfr is not None and getattr(dfr, "overlap", False):
+        dfr.overlap = False
+        L.PROFILE = []
+        for s in range(prime + warmup + steps + 20, prime + warmup + steps + 30):
+            u, i, t = batches[s % len(batches)]
+            step(u, i, t)
+        torch.cuda.synchronize()
+        prof, L.PROFILE = L.PROFILE, None
+        dfr.overlap = True
+        for name, _, e0, e1 in prof:
+            iso[name] = iso.get(name, 0.0) + e0.elapsed_time(e1) / 10
+    lin = ("ncf_attn_block_fwd", "ncf_attn_block_bwd", "ncf_mlp_fwd", "ncf_mlp_bwd",
+           "ncf_gemm_rows", "ncf_gemm_f32", "ncf_wgrad_grouped", "ncf_relu_ln_dropout_fwd",
+           "ncf_relu_ln_dropout_bwd", "ncf_attention_fwd", "ncf_attention_bwd")
     mem = torch.cuda.max_memory_allocated(dev)
     out = {"config": "C4: 50M users x 5M items, D=128, H=4, MLP [256,128,64], T=32, B=4096 x M=5, "
                      "dropout 0.2, Adam lr 1e-3 wd 1e-5 (dense-exact, deferred), 1 GPU",
@@ -388,7 +407,12 @@ def c4_train(ncf, dev, warmup, steps, prime=0):
            "table_params": 2 * (U + I) * D, "hbm_peak_GB": round(mem / 1e9, 1),
            "build_s": round(build_s, 1), "final_loss": round(loss, 6),
            "finite": bool(math.isfinite(loss)),
-           "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(per.items(), key=lambda x: -x[1])}}
+           "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(per.items(), key=lambda x: -x[1])},
+           "kernel_ms_per_step_sweep_not_overlapped": {
+               k: round(v, 4) for k, v in sorted(iso.items(), key=lambda x: -x[1])},
+           "linear_ms_per_step": round(sum(v for k, v in iso.items() if k in lin), 4),
+           "linear_kernels": "fused attention block + fused MLP tower (D = 128)"
+           if "ncf_attn_block_fwd" in iso and "ncf_mlp_fwd" in iso else "unfused"}
     del step, model, batches
     torch.cuda.empty_cache()
     return out

@@ -46,6 +46,20 @@ static_assert(AG<64>::NTmax == kMaxM && AG<128>::NTmax == 3, "row tiles");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Phase timestamps (diagnostic builds only, -DNCF_ATTN_STAMPS; tools/attn_stamps.py): thread 0
+// of each workgroup records the shader clock at the phase boundaries of the block kernels.
+#ifdef NCF_ATTN_STAMPS
+__device__ unsigned long long g_attn_stamps[2][1024][16];
+#define NCF_ASTAMP(dir, k)                                                                 \
+  do {                                                                                     \
+    if (threadIdx.x == 0) g_attn_stamps[dir][blockIdx.x & 1023][k] = clock64();           \
+  } while (0)
+#else
+#define NCF_ASTAMP(dir, k) \
+  do {                     \
+  } while (0)
+#endif
+
 // acc += A[16 rows at X, D k] . B (B fragment: this lane's D/4 k values)
 template <int D>
 __device__ __forceinline__ f32x4 tile_mfma(const float* __restrict__ X, const float (&b)[D / 4],
@@ -97,6 +111,53 @@ __device__ __forceinline__ void put_tile(float* __restrict__ S, int rt, int w, f
   for (int r = 0; r < 4; ++r) p[r * P] = c[r];
 }
 
+// Fact 6: in training every group's M rows hold ONE user, so its M LayerNorm'd user
+// rows are equal and so are their Q rows.  Whether every group of this workgroup is uniform (the
+// rows compared bit for bit, so the test is exact whatever the ids): then Q is projected for one
+// row per group, the G group rows gathered into a single row tile, and written back to all M
+// rows of each group (put_tile_expand) — the same values, one row tile of MFMA work instead of NT.
+template <int D>
+__device__ __forceinline__ bool groups_uniform(const float* __restrict__ X, int ng, int M) {
+  constexpr int L4 = D / 4, P = AG<D>::kPitch;
+  int diff = 0;
+  for (int e = threadIdx.x; e < ng * (M - 1) * L4; e += blockDim.x) {
+    const int gl = e / ((M - 1) * L4), i = 1 + (e / L4) % (M - 1), c = (e % L4) * 4;
+    const uint4 a = *reinterpret_cast<const uint4*>(X + (gl * M + i) * P + c);
+    const uint4 b = *reinterpret_cast<const uint4*>(X + (gl * M) * P + c);
+    diff |= (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
+  }
+  return __syncthreads_or(diff) == 0;
+}
+
+// group gl's first row (row gl M of X) -> row gl of Y, for the G groups of the workgroup
+template <int D>
+__device__ __forceinline__ void gather_group_rows(float* __restrict__ Y, const float* __restrict__ X,
+                                                  int M) {
+  constexpr int L4 = D / 4, P = AG<D>::kPitch;
+  for (int e = threadIdx.x; e < AG<D>::kGroups * L4; e += blockDim.x) {
+    const int gl = e / L4, c = (e % L4) * 4;
+    *reinterpret_cast<float4*>(Y + gl * P + c) = *reinterpret_cast<const float4*>(X + gl * M * P + c);
+  }
+}
+
+// C fragment of the group-row tile (row gl = 4g + r, column 16w + (lane & 15)) -> rows gl M ..
+// gl M + M - 1 of S (rows >= zero_from get 0: the padded rows of the recompute backward)
+template <int D>
+__device__ __forceinline__ void put_tile_expand(float* __restrict__ S, int w, f32x4 c, int M,
+                                                int zero_from) {
+  constexpr int P = AG<D>::kPitch;
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int gl = 4 * (l >> 4) + r;
+    if (gl < AG<D>::kGroups)
+      for (int i = 0; i < M; ++i) {
+        const int row = gl * M + i;
+        S[row * P + 16 * w + (l & 15)] = row < zero_from ? c[r] : 0.0f;
+      }
+  }
+}
+
 // Rp (padded) rows into LDS; rows >= `rows` are zeros
 template <int D>
 __device__ __forceinline__ void stage_in(float* __restrict__ S, const float* __restrict__ X,
@@ -126,6 +187,20 @@ __device__ __forceinline__ bool my_tile(int rt, int NT) {
 }
 template <int D>
 __device__ __forceinline__ int my_slice() { return (int)(threadIdx.x >> 6) % AG<D>::CS; }
+
+// out[rt] = X . W^T + bias for this wave's row tiles of its column slice, with the weight
+// fragment b (frag_wt) and bias value bb already in registers
+template <int D>
+__device__ __forceinline__ void project_f(const float* __restrict__ X, const float (&b)[D / 4],
+                                          float bb, int NT, f32x4 (&out)[kMaxM]) {
+#pragma unroll
+  for (int rt = 0; rt < AG<D>::NTmax; ++rt) {
+    if (my_tile<D>(rt, NT)) {
+      f32x4 acc = {bb, bb, bb, bb};
+      out[rt] = tile_mfma<D>(X + 16 * rt * AG<D>::kPitch, b, acc);
+    }
+  }
+}
 
 // out[rt] = X . W^T + bias for this wave's row tiles of its column slice
 template <int D>
@@ -264,7 +339,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
     const float* __restrict__ wo, const float* __restrict__ bo, float scale, float p_drop,
     uint64_t seed, const ncf_step_clock* clock, float* __restrict__ Q, float* __restrict__ K,
     float* __restrict__ V, float* __restrict__ P, float* __restrict__ O, float* __restrict__ Y,
-    int core) {
+    int core, int share_q) {
   using G = AG<D>;
   constexpr int kPitch = G::kPitch;
   extern __shared__ float lds[];
@@ -281,33 +356,63 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
   // the core on: nothing is stashed (the backward recomputes it from X_u / X_i)
   if (clock) seed += clock->seed;
 
+  NCF_ASTAMP(0, 0);
+  // the four weight fragments of this wave's column slice, loaded before the rows so their
+  // latency hides behind the staging (measured: each projection otherwise waits for its own)
+  const int cl = 16 * w + (threadIdx.x & 15);
+  float fw_v[D / 4], fw_q[D / 4], fw_k[D / 4], fw_o[D / 4];
+  frag_wt<D>(wv, w, fw_v);
+  frag_wt<D>(wo, w, fw_o);
+  const float bb_v = bv ? bv[cl] : 0.0f, bb_o = bo ? bo[cl] : 0.0f;
+  float bb_q = 0.0f, bb_k = 0.0f;
+  if (core) {
+    frag_wt<D>(wq, w, fw_q);
+    frag_wt<D>(wk, w, fw_k);
+    bb_q = bq ? bq[cl] : 0.0f;
+    bb_k = bk ? bk[cl] : 0.0f;
+  }
   if (core) stage_in<D>(S0, xu + r0 * D, Rp, rows);
   stage_in<D>(S1, xi + r0 * D, Rp, rows);
   __syncthreads();
+  NCF_ASTAMP(0, 1);
+  // one user per group (fact 6): Q from the G group rows, gathered into S2 (free until V lands)
+  const bool shq = core && M > 1 && share_q && groups_uniform<D>(S0, ng, M);
+  if (shq) {
+    gather_group_rows<D>(S2, S0, M);
+    __syncthreads();
+  }
   f32x4 fq[kMaxM], fk[kMaxM], fv[kMaxM];
-  project<D>(S1, wv, bv, NT, fv);
+  project_f<D>(S1, fw_v, bb_v, NT, fv);
   if (core) {
-    project<D>(S0, wq, bq, NT, fq);
-    project<D>(S1, wk, bk, NT, fk);
+    if (shq)
+      project_f<D>(S2, fw_q, bb_q, 1, fq);
+    else
+      project_f<D>(S0, fw_q, bb_q, NT, fq);
+    project_f<D>(S1, fw_k, bb_k, NT, fk);
   }
   __syncthreads();
+  NCF_ASTAMP(0, 2);
 #pragma unroll
   for (int rt = 0; rt < G::NTmax; ++rt)
     if (my_tile<D>(rt, NT)) {
       put_tile<D>(S2, rt, w, fv[rt]);
       if (core) {
-        put_tile<D>(S0, rt, w, fq[rt]);
+        if (!shq) put_tile<D>(S0, rt, w, fq[rt]);
         put_tile<D>(S1, rt, w, fk[rt]);
       }
     }
+  if (shq && my_tile<D>(0, 1)) put_tile_expand<D>(S0, w, fq[0], M, 1 << 30);
   __syncthreads();
+  NCF_ASTAMP(0, 3);
   const float* src = S2;   // the out_proj input: O, or V when there is no core
   if (core) {
     if (Q) stage_out<D>(Q + r0 * D, S0, rows);
     if (K) stage_out<D>(K + r0 * D, S1, rows);
     if (V) stage_out<D>(V + r0 * D, S2, rows);
+    NCF_ASTAMP(0, 4);
     attn_core_fwd<D, HD>(S0, S1, S2, S0, nullptr, P, g0, ng, M, scale, p_drop, seed);
     __syncthreads();
+    NCF_ASTAMP(0, 5);
     if (O) stage_out<D>(O + r0 * D, S0, rows);
     src = S0;
   } else if (V) {
@@ -315,12 +420,17 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
   }
   // out_proj -> S1 (K is dead) -> Y
   f32x4 fy[kMaxM];
-  project<D>(src, wo, bo, NT, fy);
+  project_f<D>(src, fw_o, bb_o, NT, fy);
 #pragma unroll
   for (int rt = 0; rt < G::NTmax; ++rt)
     if (my_tile<D>(rt, NT)) put_tile<D>(S1, rt, w, fy[rt]);
   __syncthreads();
+  NCF_ASTAMP(0, 6);
   stage_out<D>(Y + r0 * D, S1, rows);
+#ifdef NCF_ATTN_STAMPS
+  __syncthreads();
+#endif
+  NCF_ASTAMP(0, 7);
 }
 
 // RC (recompute): nothing was stashed by the forward.  Q, K, V are re-projected from X_u / X_i
@@ -336,7 +446,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     const float* __restrict__ Xi, float* __restrict__ part, float* __restrict__ dQ,
     float* __restrict__ dK, float* __restrict__ dV, float* __restrict__ dXu,
     float* __restrict__ dXi, const float* __restrict__ bq, const float* __restrict__ bk,
-    const float* __restrict__ bv) {
+    const float* __restrict__ bv, int share_q) {
   using G = AG<D>;
   constexpr int kPitch = G::kPitch, kGroups = G::kGroups, kLinW = G::kLinW, L4 = D / 4;
   constexpr int H = D / HD;
@@ -359,6 +469,17 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
   if (clock) seed += clock->seed;
   const float inv_keep = p_drop > 0.0f ? 1.0f / (1.0f - p_drop) : 1.0f;
 
+  NCF_ASTAMP(1, 0);
+  // the stash form at D = 64 (hd <= 32: registers to spare) loads its four weight fragments
+  // before the rows, so their latency hides behind the staging
+  constexpr bool PF = !RC && D == 64 && HD <= 32;
+  float pw_o[D / 4], pw_q[D / 4], pw_k[D / 4], pw_v[D / 4];
+  if constexpr (PF) {
+    frag_w<D>(wo, w, pw_o);
+    frag_w<D>(wq, w, pw_q);
+    frag_w<D>(wk, w, pw_k);
+    frag_w<D>(wv, w, pw_v);
+  }
   stage_in<D>(S0, dY + r0 * D, Rp, rows);
   constexpr int kPre = (16 * G::NTmax * L4 + kThreads - 1) / kThreads;   // float4 per thread
   float4 pu[kPre], pi[kPre];   // X_u / X_i rows for the fused weight gradients
@@ -375,8 +496,17 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
       pi[q] = in ? *reinterpret_cast<const float4*>(S2 + (e / L4) * kPitch + (e % L4) * 4)
                  : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    // one user per group (the forward's test on the same rows: the same Q bits)
+    const bool shq = M > 1 && share_q && groups_uniform<D>(S1, ng, M);
+    if (shq) {
+      gather_group_rows<D>(S3, S1, M);
+      __syncthreads();
+    }
     f32x4 fq[kMaxM], fk[kMaxM], fv[kMaxM];
-    project<D>(S1, wq, bq, NT, fq);
+    if (shq)
+      project<D>(S3, wq, bq, 1, fq);
+    else
+      project<D>(S1, wq, bq, NT, fq);
     project<D>(S2, wk, bk, NT, fk);
     project<D>(S2, wv, bv, NT, fv);
     __syncthreads();
@@ -394,11 +524,12 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
           for (int e = 0; e < 4; ++e)
             if (16 * rt + rsub + e >= rows) { a[e] = 0.f; b[e] = 0.f; c[e] = 0.f; }
         }
-        put_tile<D>(S1, rt, w, a);
+        if (!shq) put_tile<D>(S1, rt, w, a);
         put_tile<D>(S2, rt, w, b);
         put_tile<D>(S3, rt, w, c);
         if (16 * rt + rsub + 3 >= rows) put_tile<D>(S4, rt, w, z4);   // O of padded rows
       }
+    if (shq && my_tile<D>(0, 1)) put_tile_expand<D>(S1, w, fq[0], M, rows);
     __syncthreads();
     attn_core_fwd<D, HD>(S1, S2, S3, S4, Pl, nullptr, g0, ng, M, scale, p_drop, seed);
   } else {
@@ -408,6 +539,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     if (wg) stage_in<D>(S4, Og + r0 * D, Rp, rows);
   }
   __syncthreads();
+  NCF_ASTAMP(1, 1);
   float* pw = wg ? part + (int64_t)blockIdx.x * G::kPartAttn : nullptr;
   // X_u / X_i rows of this workgroup, prefetched into registers for the fused weight gradients
   if (wg && !RC) {
@@ -422,7 +554,12 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
   // dO = dY . Wo  (+ out_proj's weight gradient dY^T O and bias gradient)
   {
     float b[D / 4];
-    frag_w<D>(wo, w, b);
+    if constexpr (PF) {
+#pragma unroll
+      for (int s = 0; s < D / 4; ++s) b[s] = pw_o[s];
+    } else {
+      frag_w<D>(wo, w, b);
+    }
     f32x4 fo[kMaxM];
 #pragma unroll
     for (int rt = 0; rt < G::NTmax; ++rt)
@@ -449,6 +586,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     }
     __syncthreads();
   }
+  NCF_ASTAMP(1, 2);
   const int ntask = ng * H * M;
   // core, query side (as k_attn_bwd_q): dS and dQ per (group, head, query row)
   {
@@ -490,6 +628,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
       }
     }
     __syncthreads();   // K, V no longer read; dS complete
+    NCF_ASTAMP(1, 3);
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
       const int t = threadIdx.x + kThreads * it;
@@ -544,6 +683,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     }
     __syncthreads();
   }
+  NCF_ASTAMP(1, 4);
   if (dQ) stage_out<D>(dQ + r0 * D, S2, rows);
   if (dK) stage_out<D>(dK + r0 * D, S1, rows);
   if (dV) stage_out<D>(dV + r0 * D, S3, rows);
@@ -566,9 +706,20 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     bias_cols<D>(S1, Rp, D, pw + kLinW + D * D);
     bias_cols<D>(S3, Rp, 2 * D, pw + 2 * kLinW + D * D);
   }
+  NCF_ASTAMP(1, 5);
   // dX_u = dQ . Wq ; dX_i = dK . Wk + dV . Wv
   f32x4 fu[kMaxM], fi[kMaxM];
-  {
+  if constexpr (PF) {
+#pragma unroll
+    for (int rt = 0; rt < G::NTmax; ++rt)
+      if (my_tile<D>(rt, NT)) fu[rt] = tile_mfma<D>(S2 + 16 * rt * kPitch, pw_q, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+    for (int rt = 0; rt < G::NTmax; ++rt)
+      if (my_tile<D>(rt, NT)) fi[rt] = tile_mfma<D>(S1 + 16 * rt * kPitch, pw_k, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+    for (int rt = 0; rt < G::NTmax; ++rt)
+      if (my_tile<D>(rt, NT)) fi[rt] = tile_mfma<D>(S3 + 16 * rt * kPitch, pw_v, fi[rt]);
+  } else {
     float b[D / 4];
     frag_w<D>(wq, w, b);
 #pragma unroll
@@ -589,6 +740,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
       if (my_tile<D>(rt, NT)) put_tile<D>(S0, rt, w, fu[rt]);   // dO is dead
   }
   __syncthreads();   // S0..S4 no longer read (MFMA operands, stage_out)
+  NCF_ASTAMP(1, 6);
 #pragma unroll
   for (int rt = 0; rt < G::NTmax; ++rt)
     if (my_tile<D>(rt, NT)) {
@@ -596,8 +748,13 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
       put_tile<D>(S1, rt, w, fi[rt]);
     }
   __syncthreads();
+  NCF_ASTAMP(1, 7);
   stage_out<D>(dXu + r0 * D, S0, rows);
   stage_out<D>(dXi + r0 * D, S1, rows);
+#ifdef NCF_ATTN_STAMPS
+  __syncthreads();
+#endif
+  NCF_ASTAMP(1, 8);
 }
 
 constexpr size_t kMaxLds = 160 * 1024;   // LDS per workgroup (gfx950)
@@ -621,6 +778,13 @@ void allow_lds(Kern k, size_t bytes) {
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+// Q from one row per group when the groups hold one user each (groups_uniform; checked per
+// workgroup on the device).  NCF_ATTN_SHARE_Q=0: every row projected (A/B)
+int share_q_on() {
+  const char* e = getenv("NCF_ATTN_SHARE_Q");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 // head widths the kernels are built for: hd in {8, 16, 32, 64} at D = 64, {16, 32, 64} at
 // D = 128 (the core keeps a head row of hd floats per lane in registers)
 bool hd_ok(int64_t dim, int64_t hd) {
@@ -629,6 +793,15 @@ bool hd_ok(int64_t dim, int64_t hd) {
 }
 
 }  // namespace
+
+#ifdef NCF_ATTN_STAMPS
+// diagnostic builds only (not in ncf_hip.h): copy the phase stamps [2][1024][16] to the host
+extern "C" int ncf_debug_attn_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps)) == hipSuccess
+             ? NCF_OK
+             : NCF_ERR_LAUNCH;
+}
+#endif
 
 extern "C" int ncf_attn_block_supported(int64_t dim, int64_t heads, int64_t group_len) {
   if ((dim != 64 && dim != 128) || heads < 1 || dim % heads != 0) return 0;
@@ -654,6 +827,7 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
   // the core runs unless the eval form applies (M == 1 without dropout: softmax == 1, o = v);
   // without q/k it stashes nothing (training with ncf_attn_block_bwd_rc)
   const int core = (q != nullptr || group_len > 1 || dropout_p > 0.0f) ? 1 : 0;
+  const int share_q = share_q_on();
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len;
   const size_t lds = fwd_lds_d((int)dim, M);
@@ -666,7 +840,7 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
     if (!attr) { allow_lds(k_attn_block_fwd<D_, HD>, fwd_lds<D_>(kMaxM)); attr = true; }         \
     hipLaunchKernelGGL((k_attn_block_fwd<D_, HD>), grid, dim3(kThreads), lds, st, xu, xi, groups, \
                        M, wq, bq, wk, bk, wv, bv, wo, bo, scale, dropout_p, seed, clock, q, k, v, \
-                       probs, o, y, core);                                                       \
+                       probs, o, y, core, share_q);                                              \
   }
   NCF_ABF(64, 8)
   NCF_ABF(64, 16)
@@ -768,7 +942,7 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
     if (!attr) { allow_lds(k_attn_block_bwd<D_, HD, false>, bwd_lds<D_>(kMaxM, D_ / HD, true)); attr = true; } \
     hipLaunchKernelGGL((k_attn_block_bwd<D_, HD, false>), grid, dim3(kThreads), lds, st, grad_y, q, k, \
                        v, probs, groups, M, wq, wk, wv, wo, scale, dropout_p, seed, clock, o, xu, xi, \
-                       part, grad_q, grad_k, grad_v, grad_xu, grad_xi, nullptr, nullptr, nullptr); \
+                       part, grad_q, grad_k, grad_v, grad_xu, grad_xi, nullptr, nullptr, nullptr, 0); \
   }
   NCF_ABB(64, 8)
   NCF_ABB(64, 16)
@@ -816,6 +990,7 @@ extern "C" int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const
                 (long long)group_len, (long long)heads);
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len, H = (int)heads;
+  const int share_q = share_q_on();
   const size_t lds = bwd_lds_d((int)dim, M, H, true, true);
   const int nb = (int)ncf_cdiv(groups, groups_per_wg(dim));
   const dim3 grid((unsigned)nb);
@@ -828,7 +1003,7 @@ extern "C" int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const
     hipLaunchKernelGGL((k_attn_block_bwd<D_, HD, true>), grid, dim3(kThreads), lds, st, grad_y,     \
                        nullptr, nullptr, nullptr, nullptr, groups, M, wq, wk, wv, wo, scale,       \
                        dropout_p, seed, clock, nullptr, xu, xi, workspace, nullptr, nullptr,       \
-                       nullptr, grad_xu, grad_xi, bq, bk, bv);                                     \
+                       nullptr, grad_xu, grad_xi, bq, bk, bv, share_q);                            \
   }
   NCF_ABR(64, 8)
   NCF_ABR(64, 16)

@@ -364,6 +364,56 @@ def test_embedding_bwd_segment_reduce():
     assert int((su != -1).sum()) == 0 and int((si != -1).sum()) == 0
 
 
+@pytest.mark.parametrize("D,n", [(64, 9000), (16, 1000), (32, 4099), (128, 2051), (64, 17), (64, 1)])
+def test_position_reduce_equals_piece_reduce(monkeypatch, D, n):
+    """The position-ordered embedding backward (k_pos_reduce_ln + k_pos_fixup, NCF_EMB_POS=1)
+    against the piece-record form (the default): the same pieces summed in the same order, so every
+    compact table-gradient row agrees to fp32 rounding of the LayerNorm backward; dgamma/dbeta
+    partials sum in another order.  Heavy duplication (multi-slot segments), ragged n,
+    D = 16 .. 128."""
+    from ncf_amd import _lib
+    U, I = 5000, 700
+    g = torch.Generator().manual_seed(D + n)
+    uid = torch.randint(0, U, (n,), generator=g)
+    uid[: n // 3] = 4321
+    iid = (torch.rand(n, generator=g) ** 4 * I).long()
+    tabs = [torch.randn(r, D, generator=g).to(DEV) for r in (U, U, I, I)]
+    dys = [torch.randn(n, D, generator=g).to(DEV) for _ in range(4)]
+    gm, gl = torch.randn(D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    ud, idd = uid.to(DEV), iid.to(DEV)
+    P = lambda t: t.data_ptr()  # noqa: E731
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("NCF_EMB_POS", flag)
+        G = [torch.zeros(n, D, device=DEV) for _ in range(4)]
+        uu, ui = (torch.empty(n, dtype=torch.int64, device=DEV) for _ in range(2))
+        su = torch.full((U,), -1, dtype=torch.int32, device=DEV)
+        si = torch.full((I,), -1, dtype=torch.int32, device=DEV)
+        nu = torch.zeros(2, dtype=torch.int32, device=DEV)
+        pg = [torch.empty(D, device=DEV) for _ in range(4)]
+        ws = torch.empty(_lib.query("ncf_embedding_bwd_workspace", n, D), dtype=torch.uint8, device=DEV)
+        _lib.call("ncf_embedding_bwd", P(ud), P(idd), n, D, U, I, *[P(x) for x in dys],
+                  *[P(x) for x in (tabs[0], tabs[1], tabs[2], tabs[3])], P(gm), P(gl), 1e-5,
+                  *[P(x) for x in G], P(uu), P(ui), P(su), P(si), P(nu), *[P(x) for x in pg],
+                  P(ws), ws.numel(), _lib.stream_ptr(DEV))
+        torch.cuda.synchronize()
+        nun = nu.cpu().tolist()
+        res.append(([G[0][:nun[0]].cpu(), G[1][:nun[0]].cpu(), G[2][:nun[1]].cpu(),
+                     G[3][:nun[1]].cpu()], [x.cpu() for x in pg]))
+    (g0, p0), (g1, p1) = res
+    # the same pieces summed in the same order; the two kernels' LayerNorm backward may fuse
+    # its multiply-adds differently (-ffp-contract), so rows agree to fp32 rounding
+    diffs = [(b - a).abs().max().item() for a, b in zip(g0, g1)]
+    print(f"pos vs piece reduce D={D} n={n}: max |dG| per table {diffs}, bitwise "
+          f"{[torch.equal(a, b) for a, b in zip(g0, g1)]}")
+    # (a misassigned piece or occurrence would differ by O(1); summed over a 3000-occurrence
+    # segment's 188 pieces, per-piece rounding differences reach ~1e-5 relative)
+    for a, b in zip(g0, g1):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
+    for a, b in zip(p0, p1):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-4)
+
+
 def test_adam_table_kernel_matches_torch():
     from ncf_amd import _lib
     rows, D = 1000, 64
@@ -545,6 +595,47 @@ def test_attn_block_recompute_bitwise_equals_stash(monkeypatch, D, H, M, B, drop
         assert torch.equal(G0[k], G1[k]), k
     for k in s0:
         assert torch.equal(s0[k], s1[k]), k
+
+
+@pytest.mark.parametrize("D,H,M,B,uniform,rc", [(64, 4, 5, 37, True, "0"), (64, 4, 5, 37, True, "1"),
+                                               (128, 4, 5, 19, True, "0"),
+                                               (64, 4, 5, 37, False, "0"),
+                                               (64, 2, 3, 50, True, "1")])
+def test_attn_shared_q_matches_per_row(monkeypatch, D, H, M, B, uniform, rc):
+    """Q projected once per interaction group (fact 6: the M rows of a group hold one user;
+    attn_block.hip groups_uniform / put_tile_expand) against every row projected
+    (NCF_ATTN_SHARE_Q=0): same probabilities, gradients and table gradients.  With one user per
+    group the workgroups take the shared path; with a random user per row (uniform=False) none
+    does.  Both backward forms (stash, recompute)."""
+    from ncf_amd.trainer import FusedTrainStep
+    monkeypatch.setenv("NCF_ATTN_RC", rc)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("NCF_ATTN_SHARE_Q", flag)
+        torch.manual_seed(41)
+        m = ncf.AdvancedNCF(400, 300, 5, 24, D, D, 32, [256, 128, 64], H, 0.2, M - 1).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+        g = torch.Generator().manual_seed(42)
+        if uniform:
+            u = torch.randint(0, 400, (B,), generator=g).repeat_interleave(M).to(DEV)
+        else:
+            u = torch.randint(0, 400, (B * M,), generator=g).to(DEV)
+        i = torch.randint(0, 300, (B * M,), generator=g).to(DEV)
+        t = torch.zeros(B, M)
+        t[:, 0] = 1
+        for _ in range(2):
+            w = step(u, i, t.reshape(-1, 1).to(DEV))
+        torch.cuda.synchronize()
+        nu = w.num_unique.cpu().tolist()
+        out.append((w.prob.cpu().clone(), m.engine.flat_grad.cpu().clone(),
+                    {k: v[:nu[0 if k.endswith("user") else 1]].cpu().clone() for k, v in w.G.items()}))
+    (p0, g0, G0), (p1, g1, G1) = out
+    print(f"shared Q D={D} uniform={uniform} rc={rc}: bitwise prob {torch.equal(p0, p1)} "
+          f"grad {torch.equal(g0, g1)}; max |dprob| {(p1 - p0).abs().max().item():.3g}")
+    torch.testing.assert_close(p1, p0, rtol=0, atol=1e-6)
+    torch.testing.assert_close(g1, g0, rtol=1e-4, atol=1e-6)
+    for k in G0:
+        torch.testing.assert_close(G1[k], G0[k], rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("wgrad", ["1", "0"])
