@@ -189,7 +189,7 @@ int ncf_attention_bwd(const float* q, const float* k, const float* v, const floa
                       int64_t dim, float dropout_p, uint64_t seed, const ncf_step_clock* clock,
                       float* grad_scores, float* grad_q, float* grad_k, float* grad_v,
                       void* stream);
-/* The whole a5 block in one launch per direction (D = 64, M <= 6; ncf_attn_block_supported):
+/* The whole a5 block in one launch per direction (D = 64 or 128, M <= 6; ncf_attn_block_supported):
  * forward  q,k,v = LN rows x W^T + b, the core above (same P layout and dropout stream), y =
  *          o Wo^T + bo.  q = k = NULL: nothing is stashed (with M == 1 and no dropout this is
  *          the eval form, o = v; otherwise the core runs in LDS only, for ncf_attn_block_bwd_rc);
@@ -197,12 +197,15 @@ int ncf_attention_bwd(const float* q, const float* k, const float* v, const floa
  * backward from dY: dO = dY Wo, the core backward, dXu = dQ Wq, dXi = dK Wk + dV Wv, and the
  *          four Linear gradients (below).                                                     */
 int ncf_attn_block_supported(int64_t dim, int64_t heads, int64_t group_len);
+/* user_ids (may be NULL): the user id of every row.  A workgroup whose groups each hold one user
+ * (the reference's collate, data_prep.py:201) projects Q once per group (the same
+ * bits as per row).                                                                          */
 int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t groups, int64_t group_len,
                        int64_t heads, int64_t dim, const float* wq, const float* bq,
                        const float* wk, const float* bk, const float* wv, const float* bv,
                        const float* wo, const float* bo, float dropout_p, uint64_t seed,
                        const ncf_step_clock* clock, float* q, float* k, float* v, float* probs,
-                       float* o, float* y, void* stream);
+                       float* o, float* y, const int64_t* user_ids, void* stream);
 /* Fused weight gradients: grad_params = {q.weight, q.bias, k.weight, k.bias, v.weight, v.bias,
  * out.weight, out.bias} (written, not accumulated) from per-workgroup partials in `workspace`
  * (ncf_attn_block_bwd_workspace floats), reduced now or deferred into `defer`; then grad_q/k/v
@@ -229,7 +232,7 @@ int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const float* xi,
                           const float* bv, const float* wo, float dropout_p, uint64_t seed,
                           const ncf_step_clock* clock, float* const* grad_params,
                           float* workspace, int64_t workspace_floats, ncf_reduce_list* defer,
-                          float* grad_xu, float* grad_xi, void* stream);
+                          float* grad_xu, float* grad_xi, const int64_t* user_ids, void* stream);
 
 /* ---- a7 + a8 fused: the MLP tower in one launch per direction (input 64, hidden [256,128,64];
  * ncf_mlp_fused_supported).  Layer l = mlp.{4l} Linear (w [N_l][ldw], first K_l columns used:

@@ -69,11 +69,11 @@ SIGNATURES = {
     "ncf_mlp_bwd_workspace": (I64, [I64]),
     "ncf_mlp_bwd": (I32, [P, I64, I64, P, P, I64, P, F32, U64, P, P, P, P, I64, P, P]),
     "ncf_attn_block_fwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, F32, U64, P,
-                                 P, P, P, P, P, P, P]),
+                                 P, P, P, P, P, P, P, P]),
     "ncf_attn_block_bwd_workspace": (I64, [I64]),
     "ncf_attn_block_rc_supported": (I32, [I64, I64, I64]),
     "ncf_attn_block_bwd_rc": (I32, [P, P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, F32, U64, P,
-                                    P, P, I64, P, P, P, P]),
+                                    P, P, I64, P, P, P, P, P]),
     "ncf_attn_block_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, P, P, P, P, F32, U64, P, P,
                                  P, P, P, P, I64, P, P, P, P, P, P, P]),
     "ncf_relu_ln_dropout_fwd": (I32, [P, I64, I64, P, P, F32, F32, U64, P, P, P, P, P]),

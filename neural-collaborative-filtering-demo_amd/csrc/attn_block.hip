@@ -112,19 +112,16 @@ __device__ __forceinline__ void put_tile(float* __restrict__ S, int rt, int w, f
 }
 
 // Fact 6: in training every group's M rows hold ONE user, so its M LayerNorm'd user
-// rows are equal and so are their Q rows.  Whether every group of this workgroup is uniform (the
-// rows compared bit for bit, so the test is exact whatever the ids): then Q is projected for one
-// row per group, the G group rows gathered into a single row tile, and written back to all M
-// rows of each group (put_tile_expand) — the same values, one row tile of MFMA work instead of NT.
-template <int D>
-__device__ __forceinline__ bool groups_uniform(const float* __restrict__ X, int ng, int M) {
-  constexpr int L4 = D / 4, P = AG<D>::kPitch;
+// rows are equal and so are their Q rows.  Whether every group of this workgroup has one user id
+// (the caller's ids, uid[r0 ..]): then Q is projected for one row per group — the G group rows
+// gathered into a single row tile — and copied back to all M rows of each group: the same bits
+// as projecting every row (tested), one row tile of MFMA work instead of NT.  The test is also
+// the staging barrier (__syncthreads_or).
+__device__ __forceinline__ bool ids_uniform(const int64_t* __restrict__ uid, int ng, int M) {
   int diff = 0;
-  for (int e = threadIdx.x; e < ng * (M - 1) * L4; e += blockDim.x) {
-    const int gl = e / ((M - 1) * L4), i = 1 + (e / L4) % (M - 1), c = (e % L4) * 4;
-    const uint4 a = *reinterpret_cast<const uint4*>(X + (gl * M + i) * P + c);
-    const uint4 b = *reinterpret_cast<const uint4*>(X + (gl * M) * P + c);
-    diff |= (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
+  for (int e = threadIdx.x; e < ng * (M - 1); e += blockDim.x) {
+    const int gl = e / (M - 1), i = 1 + e % (M - 1);
+    diff |= uid[gl * M + i] != uid[gl * M];
   }
   return __syncthreads_or(diff) == 0;
 }
@@ -140,21 +137,17 @@ __device__ __forceinline__ void gather_group_rows(float* __restrict__ Y, const f
   }
 }
 
-// C fragment of the group-row tile (row gl = 4g + r, column 16w + (lane & 15)) -> rows gl M ..
-// gl M + M - 1 of S (rows >= zero_from get 0: the padded rows of the recompute backward)
+// row gl of Y -> rows gl M .. gl M + M - 1 of X for the Rp padded rows (rows >= zero_from: 0,
+// the padded rows of the recompute backward), every thread a float4 at a time
 template <int D>
-__device__ __forceinline__ void put_tile_expand(float* __restrict__ S, int w, f32x4 c, int M,
-                                                int zero_from) {
-  constexpr int P = AG<D>::kPitch;
-  const int l = threadIdx.x & 63;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int gl = 4 * (l >> 4) + r;
-    if (gl < AG<D>::kGroups)
-      for (int i = 0; i < M; ++i) {
-        const int row = gl * M + i;
-        S[row * P + 16 * w + (l & 15)] = row < zero_from ? c[r] : 0.0f;
-      }
+__device__ __forceinline__ void expand_group_rows(float* __restrict__ X, const float* __restrict__ Y,
+                                                  int M, int Rp, int zero_from) {
+  constexpr int L4 = D / 4, P = AG<D>::kPitch;
+  for (int e = threadIdx.x; e < Rp * L4; e += blockDim.x) {
+    const int r = e / L4, c = (e % L4) * 4;
+    const int gl = min(r / M, AG<D>::kGroups - 1);
+    *reinterpret_cast<float4*>(X + r * P + c) =
+        r < zero_from ? *reinterpret_cast<const float4*>(Y + gl * P + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -262,11 +255,31 @@ __device__ __forceinline__ void bias_cols(const float* __restrict__ dYs, int Rp,
 // probabilities go to Pg (global, [B][H][M][M]) and/or Pl (LDS, [16][H][M][M]) when given.  Os
 // may alias Qs: every lane finishes reading Q/K/V before the first store.  Shared by the forward
 // and the backward's recompute, so both produce the same bits.
+// Fact 6 form of the scores: with one user per group the M query rows of a group share Q, so a
+// (group, head)'s scores Q K_j^T / scale are the same for all of them — computed once per (group,
+// head, key j) into Sc[(gl H + h) M + j] with the core's own arithmetic (the same bits).
+template <int D, int HD>
+__device__ __forceinline__ void attn_scores_shared(const float* Qs, const float* Ks,
+                                                   float* __restrict__ Sc, int ng, int M,
+                                                   float scale) {
+  constexpr int H = D / HD, kPitch = AG<D>::kPitch;
+  for (int t = threadIdx.x; t < ng * H * M; t += kThreads) {
+    const int j = t % M, h = (t / M) % H, gl = t / (M * H);
+    const float* q = Qs + (gl * M) * kPitch + h * HD;   // (every row of the group holds it)
+    const float* k = Ks + (gl * M + j) * kPitch + h * HD;
+    float acc = 0.0f;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) acc = fmaf(q[d], k[d], acc);
+    Sc[t] = acc / scale;
+  }
+}
+
 template <int D, int HD>
 __device__ __forceinline__ void attn_core_fwd(const float* Qs, const float* Ks, const float* Vs,
                                               float* Os, float* Pl, float* __restrict__ Pg,
                                               int64_t g0, int ng, int M, float scale,
-                                              float p_drop, uint64_t seed) {
+                                              float p_drop, uint64_t seed,
+                                              const float* Sc = nullptr) {
   constexpr int H = D / HD, kPitch = AG<D>::kPitch;
   constexpr int kIt = (AG<D>::kGroups * H * kMaxM + kThreads - 1) / kThreads;
   const float inv_keep = p_drop > 0.0f ? 1.0f / (1.0f - p_drop) : 1.0f;
@@ -284,11 +297,15 @@ __device__ __forceinline__ void attn_core_fwd(const float* Qs, const float* Ks, 
 #pragma unroll
       for (int j = 0; j < kMaxM; ++j)
         if (j < M) {
-          const float* k = Ks + (gl * M + j) * kPitch + h * HD;
-          float acc = 0.0f;
+          if (Sc) {
+            s[j] = Sc[(gl * H + h) * M + j];
+          } else {
+            const float* k = Ks + (gl * M + j) * kPitch + h * HD;
+            float acc = 0.0f;
 #pragma unroll
-          for (int d = 0; d < HD; ++d) acc = fmaf(q[d], k[d], acc);
-          s[j] = acc / scale;
+            for (int d = 0; d < HD; ++d) acc = fmaf(q[d], k[d], acc);
+            s[j] = acc / scale;
+          }
           mx = fmaxf(mx, s[j]);
         }
       float sum = 0.0f;
@@ -339,7 +356,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
     const float* __restrict__ wo, const float* __restrict__ bo, float scale, float p_drop,
     uint64_t seed, const ncf_step_clock* clock, float* __restrict__ Q, float* __restrict__ K,
     float* __restrict__ V, float* __restrict__ P, float* __restrict__ O, float* __restrict__ Y,
-    int core, int share_q) {
+    int core, const int64_t* __restrict__ uids) {
   using G = AG<D>;
   constexpr int kPitch = G::kPitch;
   extern __shared__ float lds[];
@@ -357,12 +374,14 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
   if (clock) seed += clock->seed;
 
   NCF_ASTAMP(0, 0);
-  // the four weight fragments of this wave's column slice, loaded before the rows so their
-  // latency hides behind the staging (measured: each projection otherwise waits for its own)
+  if (core) stage_in<D>(S0, xu + r0 * D, Rp, rows);
+  stage_in<D>(S1, xi + r0 * D, Rp, rows);
+  // the projections' weight fragments of this wave's column slice, issued behind the rows' loads
+  // (in flight during the staging barrier instead of in front of each projection); out_proj's
+  // is loaded ahead of the core
   const int cl = 16 * w + (threadIdx.x & 15);
   float fw_v[D / 4], fw_q[D / 4], fw_k[D / 4], fw_o[D / 4];
   frag_wt<D>(wv, w, fw_v);
-  frag_wt<D>(wo, w, fw_o);
   const float bb_v = bv ? bv[cl] : 0.0f, bb_o = bo ? bo[cl] : 0.0f;
   float bb_q = 0.0f, bb_k = 0.0f;
   if (core) {
@@ -371,12 +390,14 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
     bb_q = bq ? bq[cl] : 0.0f;
     bb_k = bk ? bk[cl] : 0.0f;
   }
-  if (core) stage_in<D>(S0, xu + r0 * D, Rp, rows);
-  stage_in<D>(S1, xi + r0 * D, Rp, rows);
-  __syncthreads();
-  NCF_ASTAMP(0, 1);
   // one user per group (fact 6): Q from the G group rows, gathered into S2 (free until V lands)
-  const bool shq = core && M > 1 && share_q && groups_uniform<D>(S0, ng, M);
+  bool shq = false;
+  if (core && M > 1 && uids)
+    shq = ids_uniform(uids + r0, ng, M);
+  else
+    __syncthreads();
+  NCF_ASTAMP(0, 1);
+  if (!core) frag_wt<D>(wo, w, fw_o);
   if (shq) {
     gather_group_rows<D>(S2, S0, M);
     __syncthreads();
@@ -392,6 +413,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
   }
   __syncthreads();
   NCF_ASTAMP(0, 2);
+  float* Qx = S2 + Rp * kPitch + G::kGroups * 8 * kMaxM;   // [16][pitch] group-row Q tile
 #pragma unroll
   for (int rt = 0; rt < G::NTmax; ++rt)
     if (my_tile<D>(rt, NT)) {
@@ -401,8 +423,12 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
         put_tile<D>(S1, rt, w, fk[rt]);
       }
     }
-  if (shq && my_tile<D>(0, 1)) put_tile_expand<D>(S0, w, fq[0], M, 1 << 30);
+  if (shq && my_tile<D>(0, 1)) put_tile<D>(Qx, 0, w, fq[0]);
   __syncthreads();
+  if (shq) {
+    expand_group_rows<D>(S0, Qx, M, Rp, 1 << 30);
+    __syncthreads();
+  }
   NCF_ASTAMP(0, 3);
   const float* src = S2;   // the out_proj input: O, or V when there is no core
   if (core) {
@@ -410,7 +436,14 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
     if (K) stage_out<D>(K + r0 * D, S1, rows);
     if (V) stage_out<D>(V + r0 * D, S2, rows);
     NCF_ASTAMP(0, 4);
-    attn_core_fwd<D, HD>(S0, S1, S2, S0, nullptr, P, g0, ng, M, scale, p_drop, seed);
+    float* Sc = S2 + Rp * kPitch;   // [G][H][M] shared scores (past the three row buffers)
+    frag_wt<D>(wo, w, fw_o);        // (lands during the core)
+    if (shq) {
+      attn_scores_shared<D, HD>(S0, S1, Sc, ng, M, scale);
+      __syncthreads();
+    }
+    attn_core_fwd<D, HD>(S0, S1, S2, S0, nullptr, P, g0, ng, M, scale, p_drop, seed,
+                         shq ? Sc : nullptr);
     __syncthreads();
     NCF_ASTAMP(0, 5);
     if (O) stage_out<D>(O + r0 * D, S0, rows);
@@ -446,7 +479,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     const float* __restrict__ Xi, float* __restrict__ part, float* __restrict__ dQ,
     float* __restrict__ dK, float* __restrict__ dV, float* __restrict__ dXu,
     float* __restrict__ dXi, const float* __restrict__ bq, const float* __restrict__ bk,
-    const float* __restrict__ bv, int share_q) {
+    const float* __restrict__ bv, const int64_t* __restrict__ uids) {
   using G = AG<D>;
   constexpr int kPitch = G::kPitch, kGroups = G::kGroups, kLinW = G::kLinW, L4 = D / 4;
   constexpr int H = D / HD;
@@ -471,15 +504,9 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
 
   NCF_ASTAMP(1, 0);
   // the stash form at D = 64 (hd <= 32: registers to spare) loads its four weight fragments
-  // before the rows, so their latency hides behind the staging
+  // behind the rows' loads, so they land during the staging barrier
   constexpr bool PF = !RC && D == 64 && HD <= 32;
   float pw_o[D / 4], pw_q[D / 4], pw_k[D / 4], pw_v[D / 4];
-  if constexpr (PF) {
-    frag_w<D>(wo, w, pw_o);
-    frag_w<D>(wq, w, pw_q);
-    frag_w<D>(wk, w, pw_k);
-    frag_w<D>(wv, w, pw_v);
-  }
   stage_in<D>(S0, dY + r0 * D, Rp, rows);
   constexpr int kPre = (16 * G::NTmax * L4 + kThreads - 1) / kThreads;   // float4 per thread
   float4 pu[kPre], pi[kPre];   // X_u / X_i rows for the fused weight gradients
@@ -496,8 +523,8 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
       pi[q] = in ? *reinterpret_cast<const float4*>(S2 + (e / L4) * kPitch + (e % L4) * 4)
                  : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    // one user per group (the forward's test on the same rows: the same Q bits)
-    const bool shq = M > 1 && share_q && groups_uniform<D>(S1, ng, M);
+    // one user per group (the forward's test on the same ids: the same Q bits)
+    const bool shq = M > 1 && uids && ids_uniform(uids + r0, ng, M);
     if (shq) {
       gather_group_rows<D>(S3, S1, M);
       __syncthreads();
@@ -529,14 +556,25 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
         put_tile<D>(S3, rt, w, c);
         if (16 * rt + rsub + 3 >= rows) put_tile<D>(S4, rt, w, z4);   // O of padded rows
       }
-    if (shq && my_tile<D>(0, 1)) put_tile_expand<D>(S1, w, fq[0], M, rows);
+    float* Qx = Pl + kGroups * H * M * M;   // [16][pitch] group-row Q tile
+    if (shq && my_tile<D>(0, 1)) put_tile<D>(Qx, 0, w, fq[0]);
     __syncthreads();
+    if (shq) {
+      expand_group_rows<D>(S1, Qx, M, Rp, rows);
+      __syncthreads();
+    }
     attn_core_fwd<D, HD>(S1, S2, S3, S4, Pl, nullptr, g0, ng, M, scale, p_drop, seed);
   } else {
     stage_in<D>(S1, Qg + r0 * D, Rp, rows);
     stage_in<D>(S2, Kg + r0 * D, Rp, rows);
     stage_in<D>(S3, Vg + r0 * D, Rp, rows);
     if (wg) stage_in<D>(S4, Og + r0 * D, Rp, rows);
+  }
+  if constexpr (PF) {
+    frag_w<D>(wo, w, pw_o);
+    frag_w<D>(wq, w, pw_q);
+    frag_w<D>(wk, w, pw_k);
+    frag_w<D>(wv, w, pw_v);
   }
   __syncthreads();
   NCF_ASTAMP(1, 1);
@@ -757,14 +795,19 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
   NCF_ASTAMP(1, 8);
 }
 
-constexpr size_t kMaxLds = 160 * 1024;   // LDS per workgroup (gfx950)
+// LDS per workgroup (gfx950: 160 KB) available to the dynamic buffers: the kernels' static LDS
+// (the workgroup vote of groups_uniform) takes a few bytes of it
+constexpr size_t kMaxLds = 160 * 1024 - 1024;
 template <int D>
-size_t fwd_lds(int M) { return sizeof(float) * 3 * 16 * AG<D>::nt(M) * AG<D>::kPitch; }
+size_t fwd_lds(int M) {   // three row buffers + the shared scores [G][H <= 8][M] + the Q tile
+  return sizeof(float) * (3 * 16 * AG<D>::nt(M) * AG<D>::kPitch + AG<D>::kGroups * 8 * kMaxM +
+                          16 * AG<D>::kPitch);
+}
 template <int D>
 size_t bwd_lds(int M, int H, bool wg, bool rc = false) {
   using G = AG<D>;
   return sizeof(float) * ((wg ? 5 : 4) * 16 * G::nt(M) * G::kPitch +
-                          (rc ? 2 : 1) * G::kGroups * H * M * M);
+                          (rc ? 2 : 1) * G::kGroups * H * M * M + (rc ? 16 * G::kPitch : 0));
 }
 size_t fwd_lds_d(int D, int M) { return D == 64 ? fwd_lds<64>(M) : fwd_lds<128>(M); }
 size_t bwd_lds_d(int D, int M, int H, bool wg, bool rc = false) {
@@ -778,11 +821,11 @@ void allow_lds(Kern k, size_t bytes) {
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
-// Q from one row per group when the groups hold one user each (groups_uniform; checked per
-// workgroup on the device).  NCF_ATTN_SHARE_Q=0: every row projected (A/B)
-int share_q_on() {
+// Q from one row per group when the groups hold one user each (ids_uniform; checked per
+// workgroup on the device from the caller's ids).  NCF_ATTN_SHARE_Q=0: every row projected (A/B)
+const int64_t* share_ids(const int64_t* user_ids) {
   const char* e = getenv("NCF_ATTN_SHARE_Q");
-  return (e && e[0] == '0') ? 0 : 1;
+  return (e && e[0] == '0') ? nullptr : user_ids;
 }
 
 // head widths the kernels are built for: hd in {8, 16, 32, 64} at D = 64, {16, 32, 64} at
@@ -815,7 +858,8 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
                                   const float* wv, const float* bv, const float* wo,
                                   const float* bo, float dropout_p, uint64_t seed,
                                   const ncf_step_clock* clock, float* q, float* k, float* v,
-                                  float* probs, float* o, float* y, void* stream) {
+                                  float* probs, float* o, float* y, const int64_t* user_ids,
+                                  void* stream) {
   NCF_CHECK_ARG(groups >= 0 && ncf_attn_block_supported(dim, heads, group_len),
                 "ncf_attn_block_fwd: unsupported shape (D=%lld H=%lld M=%lld; need D=64 or 128, "
                 "M<=%d)", (long long)dim, (long long)heads, (long long)group_len, kMaxM);
@@ -827,7 +871,7 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
   // the core runs unless the eval form applies (M == 1 without dropout: softmax == 1, o = v);
   // without q/k it stashes nothing (training with ncf_attn_block_bwd_rc)
   const int core = (q != nullptr || group_len > 1 || dropout_p > 0.0f) ? 1 : 0;
-  const int share_q = share_q_on();
+  const int64_t* uids = share_ids(user_ids);
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len;
   const size_t lds = fwd_lds_d((int)dim, M);
@@ -840,7 +884,7 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
     if (!attr) { allow_lds(k_attn_block_fwd<D_, HD>, fwd_lds<D_>(kMaxM)); attr = true; }         \
     hipLaunchKernelGGL((k_attn_block_fwd<D_, HD>), grid, dim3(kThreads), lds, st, xu, xi, groups, \
                        M, wq, bq, wk, bk, wv, bv, wo, bo, scale, dropout_p, seed, clock, q, k, v, \
-                       probs, o, y, core, share_q);                                              \
+                       probs, o, y, core, uids);                                                 \
   }
   NCF_ABF(64, 8)
   NCF_ABF(64, 16)
@@ -942,7 +986,7 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
     if (!attr) { allow_lds(k_attn_block_bwd<D_, HD, false>, bwd_lds<D_>(kMaxM, D_ / HD, true)); attr = true; } \
     hipLaunchKernelGGL((k_attn_block_bwd<D_, HD, false>), grid, dim3(kThreads), lds, st, grad_y, q, k, \
                        v, probs, groups, M, wq, wk, wv, wo, scale, dropout_p, seed, clock, o, xu, xi, \
-                       part, grad_q, grad_k, grad_v, grad_xu, grad_xi, nullptr, nullptr, nullptr, 0); \
+                       part, grad_q, grad_k, grad_v, grad_xu, grad_xi, nullptr, nullptr, nullptr, nullptr); \
   }
   NCF_ABB(64, 8)
   NCF_ABB(64, 16)
@@ -973,7 +1017,8 @@ extern "C" int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const
                                      uint64_t seed, const ncf_step_clock* clock,
                                      float* const* grad_params, float* workspace,
                                      int64_t workspace_floats, ncf_reduce_list* defer,
-                                     float* grad_xu, float* grad_xi, void* stream) {
+                                     float* grad_xu, float* grad_xi, const int64_t* user_ids,
+                                     void* stream) {
   NCF_CHECK_ARG(groups >= 0 && ncf_attn_block_supported(dim, heads, group_len),
                 "ncf_attn_block_bwd_rc: unsupported shape (D=%lld H=%lld M=%lld; need D=64 or "
                 "128, M<=%d)", (long long)dim, (long long)heads, (long long)group_len, kMaxM);
@@ -990,7 +1035,7 @@ extern "C" int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const
                 (long long)group_len, (long long)heads);
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len, H = (int)heads;
-  const int share_q = share_q_on();
+  const int64_t* uids = share_ids(user_ids);
   const size_t lds = bwd_lds_d((int)dim, M, H, true, true);
   const int nb = (int)ncf_cdiv(groups, groups_per_wg(dim));
   const dim3 grid((unsigned)nb);
@@ -999,11 +1044,11 @@ extern "C" int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const
 #define NCF_ABR(D_, HD)                                                                           \
   if (dim == D_ && dim / heads == HD) {                                                           \
     static bool attr = false;                                                                     \
-    if (!attr) { allow_lds(k_attn_block_bwd<D_, HD, true>, kMaxLds); attr = true; }              \
+    if (!attr) { allow_lds(k_attn_block_bwd<D_, HD, true>, bwd_lds<D_>(kMaxM, D_ / HD, true, true) <= kMaxLds ? bwd_lds<D_>(kMaxM, D_ / HD, true, true) : kMaxLds); attr = true; } \
     hipLaunchKernelGGL((k_attn_block_bwd<D_, HD, true>), grid, dim3(kThreads), lds, st, grad_y,     \
                        nullptr, nullptr, nullptr, nullptr, groups, M, wq, wk, wv, wo, scale,       \
                        dropout_p, seed, clock, nullptr, xu, xi, workspace, nullptr, nullptr,       \
-                       nullptr, grad_xu, grad_xi, bq, bk, bv, share_q);                            \
+                       nullptr, grad_xu, grad_xi, bq, bk, bv, uids);                               \
   }
   NCF_ABR(64, 8)
   NCF_ABR(64, 16)

@@ -437,7 +437,7 @@ class NCFEngine:
                       drop_p if train else 0.0, seed, ptr(self.clock),
                       ptr(w.q) if core else None, ptr(w.k) if core else None,
                       ptr(w.v) if core else None, ptr(w.P) if core else None,
-                      ptr(w.o) if core else None, ptr(w.y), st)
+                      ptr(w.o) if core else None, ptr(w.y), ptr(uid), st)
             # a7: MLP tower on [attn ‖ zeros_T] (architecture.py:329-344): the zero temporal
             # columns contribute nothing, so layer 0 reads only the first D columns of mlp.0.weight
             x, ldx, kin = w.y, D, D
@@ -746,7 +746,8 @@ class NCFEngine:
                 bq, bk, bv = pp["att_b"]
                 _lib.call("ncf_attn_block_bwd_rc", ptr(w.dy), ptr(w.xu), ptr(w.xi), n // M, M, H, D,
                           wq, bq, wk, bk, wv, bv, wo, drop_p, seed, ptr(self.clock), gp[1],
-                          ptr(ws), ws.numel(), w.red_list.address, ptr(w.dxu), ptr(w.dxi), st)
+                          ptr(ws), ws.numel(), w.red_list.address, ptr(w.dxu), ptr(w.dxi),
+                          ptr(uid), st)
             else:
                 _lib.call("ncf_attn_block_bwd", ptr(w.dy), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P),
                           n // M, M, H, D, *pp["att_w"], drop_p, seed,

@@ -13,3 +13,5 @@ NCF_CLAIM_CATCHUP=0 step r3h_bench_noclaim 400 $B && summ r3h_bench_noclaim
 NCF_ATTN_SHARE_Q=0 step r3h_bench_noshq 400 $B && summ r3h_bench_noshq
 NCF_HIP_LIB=abl/lib_astamps.so step r3h_attn_stamps 200 python3 -u tools/attn_stamps.py
 grep -v amdgpu.ids gpurun_out/r3h_attn_stamps.log
+step r3h_dropin_host 300 python3 -u tools/dropin_host.py --warmup 150 --steps 100
+head -45 gpurun_out/r3h_dropin_host.log | grep -v amdgpu.ids
