@@ -163,6 +163,33 @@ __device__ __forceinline__ void stage_in(float* __restrict__ S, const float* __r
   }
 }
 
+// NB [Rp x D] row blocks into LDS with every block's loads in flight before the first LDS
+// store.  (A load-then-store loop waits one HBM latency per iteration: stamped at 12K cycles
+// for the forward's two blocks and 20K for the backward's five, of 45K / 75K per workgroup.)
+// Rows >= `rows` are zeros.
+template <int D, int NB>
+__device__ __forceinline__ void stage_in_n(float* const (&S)[NB], const float* const (&X)[NB],
+                                           int Rp, int rows) {
+  constexpr int L4 = D / 4, P = AG<D>::kPitch;
+  constexpr int IT = (16 * AG<D>::NTmax * L4 + kThreads - 1) / kThreads;
+  float4 v[NB][IT];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int e = threadIdx.x + kThreads * it, r = e / L4, c = (e % L4) * 4;
+      v[b][it] = (e < Rp * L4 && r < rows) ? ld4(X[b] + (int64_t)r * D + c)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int e = threadIdx.x + kThreads * it;
+      if (e < Rp * L4) *reinterpret_cast<float4*>(S[b] + (e / L4) * P + (e % L4) * 4) = v[b][it];
+    }
+}
+
 template <int D>
 __device__ __forceinline__ void stage_out(float* __restrict__ X, const float* __restrict__ S,
                                           int rows) {
@@ -374,8 +401,15 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
   if (clock) seed += clock->seed;
 
   NCF_ASTAMP(0, 0);
-  if (core) stage_in<D>(S0, xu + r0 * D, Rp, rows);
-  stage_in<D>(S1, xi + r0 * D, Rp, rows);
+  if (core) {
+    float* const dst[2] = {S0, S1};
+    const float* const src[2] = {xu + r0 * D, xi + r0 * D};
+    stage_in_n<D, 2>(dst, src, Rp, rows);
+  } else {
+    float* const dst[1] = {S1};
+    const float* const src[1] = {xi + r0 * D};
+    stage_in_n<D, 1>(dst, src, Rp, rows);
+  }
   // the projections' weight fragments of this wave's column slice, issued behind the rows' loads
   // (in flight during the staging barrier instead of in front of each projection); out_proj's
   // is loaded ahead of the core
@@ -507,12 +541,14 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
   // behind the rows' loads, so they land during the staging barrier
   constexpr bool PF = !RC && D == 64 && HD <= 32;
   float pw_o[D / 4], pw_q[D / 4], pw_k[D / 4], pw_v[D / 4];
-  stage_in<D>(S0, dY + r0 * D, Rp, rows);
   constexpr int kPre = (16 * G::NTmax * L4 + kThreads - 1) / kThreads;   // float4 per thread
   float4 pu[kPre], pi[kPre];   // X_u / X_i rows for the fused weight gradients
   if constexpr (RC) {
-    stage_in<D>(S1, Xu + r0 * D, Rp, rows);
-    stage_in<D>(S2, Xi + r0 * D, Rp, rows);
+    {
+      float* const dst[3] = {S0, S1, S2};
+      const float* const src[3] = {dY + r0 * D, Xu + r0 * D, Xi + r0 * D};
+      stage_in_n<D, 3>(dst, src, Rp, rows);
+    }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kPre; ++q) {   // (zero rows past the batch: staged as zeros)
@@ -564,11 +600,14 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
       __syncthreads();
     }
     attn_core_fwd<D, HD>(S1, S2, S3, S4, Pl, nullptr, g0, ng, M, scale, p_drop, seed);
+  } else if (wg) {
+    float* const dst[5] = {S0, S1, S2, S3, S4};
+    const float* const src[5] = {dY + r0 * D, Qg + r0 * D, Kg + r0 * D, Vg + r0 * D, Og + r0 * D};
+    stage_in_n<D, 5>(dst, src, Rp, rows);
   } else {
-    stage_in<D>(S1, Qg + r0 * D, Rp, rows);
-    stage_in<D>(S2, Kg + r0 * D, Rp, rows);
-    stage_in<D>(S3, Vg + r0 * D, Rp, rows);
-    if (wg) stage_in<D>(S4, Og + r0 * D, Rp, rows);
+    float* const dst[4] = {S0, S1, S2, S3};
+    const float* const src[4] = {dY + r0 * D, Qg + r0 * D, Kg + r0 * D, Vg + r0 * D};
+    stage_in_n<D, 4>(dst, src, Rp, rows);
   }
   if constexpr (PF) {
     frag_w<D>(wo, w, pw_o);

@@ -497,10 +497,19 @@ __global__ __launch_bounds__(kThreads) void k_mlp_fwd(
   const int rows = (int)min<int64_t>(VR, n - row0);
   const uint64_t cs = clock ? clock->seed : 0ull;
   NCF_STAMP(0, 0);
-  for (int e = threadIdx.x; e < TR * (K0 / 4); e += kThreads) {
-    const int r = e / (K0 / 4), c = (e % (K0 / 4)) * 4;
-    lds4_st(P + r * kPP + c,
-            r < rows ? ld4(xin + (row0 + r) * K0 + c) : make_float4(0.f, 0.f, 0.f, 0.f));
+  {   // the input rows, every load in flight before the first LDS store
+    constexpr int TOT = TR * (K0 / 4), IT = (TOT + kThreads - 1) / kThreads;
+    float4 v[IT];
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+      const int e = threadIdx.x + kThreads * j, r = e / (K0 / 4), c = (e % (K0 / 4)) * 4;
+      v[j] = (e < TOT && r < rows) ? ld4(xin + (row0 + r) * K0 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+      const int e = threadIdx.x + kThreads * j, r = e / (K0 / 4), c = (e % (K0 / 4)) * 4;
+      if (e < TOT) lds4_st(P + r * kPP + c, v[j]);
+    }
   }
   __syncthreads();
   NCF_STAMP(0, 1);
@@ -586,25 +595,74 @@ __device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const f
 }
 
 // the activation rows a of layer L into LDS: loaded when the forward saved them, else
-// recomputed from r (act4)
+// recomputed from r (act4's arithmetic: the same bits).  Loads are issued SB iterations at a
+// time before their uses: a load-then-store loop waits one HBM latency per iteration (stamped:
+// 13K cycles for a0's ten iterations per thread, of ~176K for the whole backward).
+#ifndef NCF_STAGE_BATCH
+#define NCF_STAGE_BATCH 5
+#endif
 template <int K, int PX>
 __device__ __forceinline__ void stage_act(float* __restrict__ X, const ncf_mlp_layer& L,
                                           int64_t row0, int rows, float p, uint64_t seed) {
+  constexpr int TOT = kRows * (K / 4), IT = (TOT + kThreads - 1) / kThreads;
+  constexpr int SB = NCF_STAGE_BATCH < IT ? NCF_STAGE_BATCH : IT;
   const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
-  for (int e = threadIdx.x; e < kRows * (K / 4); e += kThreads) {
-    const int r = e / (K / 4), c = (e % (K / 4)) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < rows) v = L.a ? ld4(L.a + (row0 + r) * K + c) : act4<K>(L, row0 + r, c, p, seed, inv_keep);
-    lds4_st(X + r * PX + c, v);
+  for (int b0 = 0; b0 < IT; b0 += SB) {
+    float4 x[SB];
+    float mu[SB], rs[SB];
+#pragma unroll
+    for (int j = 0; j < SB; ++j) {
+      const int e = threadIdx.x + kThreads * (b0 + j), r = e / (K / 4), c = (e % (K / 4)) * 4;
+      x[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      mu[j] = 0.0f;
+      rs[j] = 0.0f;
+      if (b0 + j < IT && e < TOT && r < rows) {
+        const int64_t row = row0 + r;
+        if (L.a) {
+          x[j] = ld4(L.a + row * K + c);
+        } else {
+          x[j] = ld4(L.r + row * K + c);
+          mu[j] = L.mean[row];
+          rs[j] = L.rstd[row];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < SB; ++j) {
+      const int e = threadIdx.x + kThreads * (b0 + j), r = e / (K / 4), c = (e % (K / 4)) * 4;
+      if (b0 + j < IT && e < TOT) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < rows) {
+          if (L.a) {
+            v = x[j];
+          } else {   // act4 on the loaded row values
+            const float4 xx = x[j];
+            const float m = mu[j];
+            const float4 y = ln_affine(make_float4(xx.x - m, xx.y - m, xx.z - m, xx.w - m), rs[j],
+                                       ld4(L.gamma + c), ld4(L.beta + c));
+            v = drop4(y, seed, ((uint64_t)(row0 + r) * K + c) >> 2, p, inv_keep);
+          }
+        }
+        lds4_st(X + r * PX + c, v);
+      }
+    }
   }
 }
 
 template <int K, int PX>
 __device__ __forceinline__ void stage_rows(float* __restrict__ X, const float* __restrict__ src,
                                            int64_t row0, int rows) {
-  for (int e = threadIdx.x; e < kRows * (K / 4); e += kThreads) {
-    const int r = e / (K / 4), c = (e % (K / 4)) * 4;
-    lds4_st(X + r * PX + c, r < rows ? ld4(src + (row0 + r) * K + c) : make_float4(0.f, 0.f, 0.f, 0.f));
+  constexpr int TOT = kRows * (K / 4), IT = (TOT + kThreads - 1) / kThreads;
+  float4 v[IT];   // every load in flight before the first store
+#pragma unroll
+  for (int j = 0; j < IT; ++j) {
+    const int e = threadIdx.x + kThreads * j, r = e / (K / 4), c = (e % (K / 4)) * 4;
+    v[j] = (e < TOT && r < rows) ? ld4(src + (row0 + r) * K + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int j = 0; j < IT; ++j) {
+    const int e = threadIdx.x + kThreads * j, r = e / (K / 4), c = (e % (K / 4)) * 4;
+    if (e < TOT) lds4_st(X + r * PX + c, v[j]);
   }
 }
 

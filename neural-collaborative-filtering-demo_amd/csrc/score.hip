@@ -528,15 +528,15 @@ constexpr int kNW3 = NCF_SCORE3_NW;   // waves per workgroup (measured: 8 at one
 // grouped by user: one global counter atomic per (user, flush) and each user's entries stored
 // contiguously, instead of one atomic and two scattered 4-byte stores per candidate (measured
 // before: 1.17 GB of writes per scan launch for ~0.14 GB of candidates).
-#ifndef NCF_SCORE3_SLICE
-#define NCF_SCORE3_SLICE 768
-#endif
-constexpr int kSlice3 = NCF_SCORE3_SLICE;
-// per wave: logit f32 | item i32 | local user u16 | rank u16 | perm u16 [kSlice3], then
+// (two-term scan: 1024 entries per wave; three-term: 896, its three tile planes take more of
+// the 160 KB)
+template <int T>
+constexpr int slice3() { return T == 3 ? 896 : 1024; }
+// per wave: logit f32 | item i32 | local user u16 | rank u16 | perm u16 [slice3], then
 // count / offset / base u32 [32 UB]
-template <int UB>
+template <int UB, int T>
 constexpr size_t slice3_bytes() {
-  return (size_t)kSlice3 * (4 + 4 + 2 + 2 + 2) + 3 * 4 * 32 * UB;
+  return (size_t)slice3<T>() * (4 + 4 + 2 + 2 + 2) + 3 * 4 * 32 * UB;
 }
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -546,6 +546,65 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // B operands of tile t + 1 are read from LDS while tile t is multiplied.  Hits go to the wave's
 // own LDS slice (offsets from ballots, no atomics) and the wave writes its slice to the global
 // lists itself when it fills (no workgroup barrier).
+// LDS writes of this wave visible to its other lanes (LDS-only fence: no global cache traffic)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+// A wave's staged candidates written out grouped by user (k_collect3): per-user counts and
+// ranks (LDS atomics), a wave scan for the group offsets, ONE global counter atomic per user
+// with candidates, then the entries stored in user-grouped order, consecutive lanes writing
+// consecutive slots of a user's list.  Only after the scan loop (inside it, or called out of
+// line from it, it pushed the loop's arrays to scratch: 40 GB of scratch writes per launch).
+template <int NU>
+__device__ __forceinline__ void flush_grouped(
+    uint32_t staged, int64_t slot0, const int32_t* __restrict__ user_list,
+    uint32_t* __restrict__ count, int64_t cap, float* __restrict__ cand_logit,
+    int32_t* __restrict__ cand_item, const float* wl, const int32_t* wi, const uint16_t* wu,
+    uint16_t* wr, uint16_t* wp, uint32_t* ucnt, uint32_t* uoff, uint32_t* ubase) {
+  const int lane = threadIdx.x & 63;
+  for (int k = lane; k < NU; k += 64) ucnt[k] = 0u;
+  wave_lds_sync();
+  for (uint32_t e = lane; e < staged; e += 64) wr[e] = (uint16_t)atomicAdd(&ucnt[wu[e]], 1u);
+  wave_lds_sync();
+  // per user: one reservation in its global list; offsets of the user groups in the slice
+  uint32_t run = 0;
+  for (int c = 0; c < NU / 64; ++c) {
+    const int k = 64 * c + lane;
+    const uint32_t n = ucnt[k];
+    uint32_t incl = n;   // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    uoff[k] = run + incl - n;
+    run += __shfl(incl, 63, 64);
+    uint32_t b = 0;
+    if (n) {
+      const int64_t s = slot0 + k;
+      b = atomicAdd(&count[user_list ? (int64_t)user_list[s] : s], n);
+    }
+    ubase[k] = b;
+  }
+  wave_lds_sync();
+  for (uint32_t e = lane; e < staged; e += 64) wp[uoff[wu[e]] + wr[e]] = (uint16_t)e;
+  wave_lds_sync();
+  for (uint32_t q = lane; q < staged; q += 64) {
+    const uint32_t e = wp[q], k = wu[e];
+    const uint32_t pos = ubase[k] + (q - uoff[k]);
+    if (pos < cap) {
+      const int64_t s = slot0 + k;
+      const int64_t u = user_list ? (int64_t)user_list[s] : s;
+      cand_logit[u * cap + pos] = wl[e];
+      cand_item[u * cap + pos] = wi[e];
+    }
+  }
+  wave_lds_sync();
+}
+
 template <int UB, int NW, int T>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_collect3(
     const float* __restrict__ q, const int32_t* __restrict__ user_list, int64_t n_users,
@@ -657,7 +716,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   };
   // the wave's candidate slice: staged entries (wave-uniform), written out when it would overflow
   constexpr int NU = 32 * UB;   // the wave's users (local index: 32 ub + row)
-  unsigned char* sb = slices3 + (size_t)w * slice3_bytes<UB>();
+  constexpr int kSlice3 = slice3<T>();
+  unsigned char* sb = slices3 + (size_t)w * slice3_bytes<UB, T>();
   float* wl = reinterpret_cast<float*>(sb);
   int32_t* wi = reinterpret_cast<int32_t*>(sb + 4 * kSlice3);
   uint16_t* wu = reinterpret_cast<uint16_t*>(sb + 8 * kSlice3);
@@ -667,53 +727,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   uint32_t* uoff = ucnt + NU;
   uint32_t* ubase = uoff + NU;
   uint32_t staged = 0;
-  auto wsync = [&]() {   // LDS writes of this wave visible to its other lanes
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
+  // a slice that fills inside the scan loop is written out one candidate at a time (one counter
+  // atomic each: what the loop's register budget allows); the rest, grouped after the loop
   auto wflush = [&]() {
-    if (staged == 0) return;
-    for (int k = lane; k < NU; k += 64) ucnt[k] = 0u;
-    wsync();
-    for (uint32_t e = lane; e < staged; e += 64) wr[e] = (uint16_t)atomicAdd(&ucnt[wu[e]], 1u);
-    wsync();
-    // per user: one reservation in its global list; offsets of the user groups in the slice
-    uint32_t run = 0;
-#pragma unroll
-    for (int c = 0; c < NU / 64; ++c) {
-      const int k = 64 * c + lane;
-      const uint32_t n = ucnt[k];
-      uint32_t incl = n;   // inclusive wave scan
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-      }
-      uoff[k] = run + incl - n;
-      run += __shfl(incl, 63, 64);
-      uint32_t b = 0;
-      if (n) {
-        const int64_t s = slot0 + k;
-        b = atomicAdd(&count[user_list ? (int64_t)user_list[s] : s], n);
-      }
-      ubase[k] = b;
-    }
-    wsync();
-    for (uint32_t e = lane; e < staged; e += 64) wp[uoff[wu[e]] + wr[e]] = (uint16_t)e;
-    wsync();
-    // user-grouped order: consecutive lanes store consecutive slots of one user's list
-    for (uint32_t q = lane; q < staged; q += 64) {
-      const uint32_t e = wp[q], k = wu[e];
-      const uint32_t pos = ubase[k] + (q - uoff[k]);
+    for (uint32_t e = lane; e < staged; e += 64) {
+      const int64_t sl = slot0 + wu[e];
+      const int64_t u = user_list ? (int64_t)user_list[sl] : sl;
+      const uint32_t pos = atomicAdd(&count[u], 1u);
       if (pos < cap) {
-        const int64_t s = slot0 + k;
-        const int64_t u = user_list ? (int64_t)user_list[s] : s;
         cand_logit[u * cap + pos] = wl[e];
         cand_item[u * cap + pos] = wi[e];
       }
     }
-    wsync();
     staged = 0;
   };
   auto filt = [&](const f32x16& acc, int ub, int bb, int64_t t0) {
@@ -814,7 +839,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       bc = bn;
     }
   }
-  wflush();
+  if (staged)
+    flush_grouped<NU>(staged, slot0, user_list, count, cap, cand_logit, cand_item, wl, wi, wu, wr,
+                      wp, ucnt, uoff, ubase);
 }
 
 // ---- 4. per-user selection: bitonic sort (descending) of 64-bit keys (logit key | ~item)
@@ -1246,15 +1273,15 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
   per = (per + kItemTile - 1) / kItemTile * kItemTile;
   splits = (n_items + per - 1) / per;
   NCF_CHECK_ARG(splits * ub < (1ll << 31), "ncf_score_collect_split: grid too large");
-  const size_t dyn = (size_t)kNW3 * (terms == 3 ? slice3_bytes<kUB3t>() : slice3_bytes<kUB3>());
+  const size_t dyn = (size_t)kNW3 * (terms == 3 ? slice3_bytes<kUB3t, 3>() : slice3_bytes<kUB3, 2>());
   static bool attr3 = false;
   if (!attr3) {
     const hipError_t e0 = hipFuncSetAttribute((const void*)k_collect3<kUB3t, kNW3, 3>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)(kNW3 * slice3_bytes<kUB3t>()));
+                                              (int)(kNW3 * slice3_bytes<kUB3t, 3>()));
     const hipError_t e1 = hipFuncSetAttribute((const void*)k_collect3<kUB3, kNW3, 2>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)(kNW3 * slice3_bytes<kUB3>()));
+                                              (int)(kNW3 * slice3_bytes<kUB3, 2>()));
     if (e0 != hipSuccess || e1 != hipSuccess) {
       ncf_set_error("ncf_score_collect_split: candidate slices need more LDS than allowed");
       return NCF_ERR_LAUNCH;
