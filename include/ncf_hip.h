@@ -44,6 +44,15 @@ int ncf_version(void);
 const char* ncf_last_error(void);
 int ncf_device_count(void);
 
+/* Cross-stream ordering (hipEventRecord / hipStreamWaitEvent, events created without timing).
+ * Replaces: the torch.cuda.Event record / wait_event pairs of the step's fork / join points
+ * (this port's own plumbing: the reference runs one stream).  As entry points they are part of
+ * a recorded launch sequence (launch tapes) and replay in order with it.     */
+int ncf_event_create(void** event);
+int ncf_event_destroy(void* event);
+int ncf_event_record(void* event, void* stream);
+int ncf_stream_wait_event(void* stream, void* event);
+
 /* ---- a2+a3+a4: EBC lookups x4 + mf_norm/mlp_norm + GMF dot --------------------------------
  * Replaces: EmbeddingBagCollection fwd (architecture.py:286-287), LayerNorms (:305-306,
  * :311-312), mf_vector/mf_output (:307-308).  Writes mf_pred[n], LN'd MLP rows [n,dim] (the

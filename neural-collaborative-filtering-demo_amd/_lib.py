@@ -33,6 +33,10 @@ U64 = ctypes.c_uint64
 SIGNATURES = {
     "ncf_version": (I32, []),
     "ncf_last_error": (ctypes.c_char_p, []),
+    "ncf_event_create": (I32, [P]),
+    "ncf_event_destroy": (I32, [P]),
+    "ncf_event_record": (I32, [P, P]),
+    "ncf_stream_wait_event": (I32, [P, P]),
     "ncf_device_count": (I32, []),
     "ncf_gather_ln_gmf_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P, F32,
                                     P, P, P, P, P, P, P]),
@@ -272,6 +276,8 @@ def _bind_fast(lib):
             continue
         _ncffast.bind(i, ctypes.cast(getattr(lib, name), ctypes.c_void_p).value)
         FAST[name] = getattr(_ncffast, name)
+    global _fast_mod
+    _fast_mod = _ncffast if hasattr(_ncffast, "tape_new") else None
 
 
 def exported_symbols():
@@ -298,6 +304,8 @@ def _invoke(lib, name, args):
             return f(*args)
         except TypeError:
             pass       # an argument the fast path does not take (e.g. a ctypes object)
+    if _recording:     # a call the tape cannot hold: the recording is unusable
+        _fast_mod.tape_invalidate()
     return getattr(lib, name)(*args)
 
 
@@ -318,7 +326,102 @@ def call(name: str, *args):
 
 def query(name: str, *args) -> int:
     lib = _lib if _lib is not None else load()
+    if _recording:     # sizes / capabilities: not launches, never part of a tape
+        prev = _fast_mod.tape_hold(1)
+        try:
+            return int(_invoke(lib, name, args))
+        finally:
+            _fast_mod.tape_hold(prev)
     return int(_invoke(lib, name, args))
+
+
+# ---- launch tapes (gen_fastcall.py): a recorded sequence of C-ABI calls replayed from C
+_recording = False
+_fast_mod = None
+
+
+class LaunchTape:
+    """The C-ABI calls one region of host code makes, recorded while it runs for real and
+    replayed later in the same order from C (no Python per call).  ``record(ranges)``: pointer
+    arguments inside one of the (base, size) ranges are re-based at replay onto the bases given
+    to ``replay`` (in the same order), every other argument is replayed as recorded.  Only
+    entry points reached through the fast-call binding are recorded; anything else reached
+    while recording makes the tape invalid (``valid`` False after the region)."""
+
+    def __init__(self):
+        if _fast_mod is None:
+            raise NCFLibraryError("launch tapes need the fast-call binding (_ncffast)")
+        self._h = _fast_mod.tape_new()
+        self.valid = False
+        self.calls = 0
+
+    def record(self, ranges=()):
+        """Context manager: record the calls of its body (which run as usual)."""
+        return _TapeRecording(self, ranges)
+
+    def size(self):
+        """(calls, patched pointer arguments, valid)"""
+        return _fast_mod.tape_size(self._h)
+
+    def replay(self, bases=()):
+        rc = _fast_mod.tape_replay(self._h, tuple(bases))
+        if rc != 0:
+            i, code = rc
+            check(code, f"launch tape call {i}")
+
+
+class _TapeRecording:
+    def __init__(self, tape, ranges):
+        self.tape = tape
+        self.ranges = tuple(int(x) for x in ranges)
+
+    def __enter__(self):
+        global _recording
+        _fast_mod.tape_begin(self.tape._h, self.ranges)
+        _recording = True
+        return self.tape
+
+    def __exit__(self, *exc):
+        global _recording
+        _recording = False
+        n, valid = _fast_mod.tape_end()
+        self.tape.calls = n
+        self.tape.valid = bool(valid) and exc[0] is None
+        return False
+
+
+def tapes_available() -> bool:
+    if _lib is None:
+        load()
+    return _fast_mod is not None
+
+
+class RawEvent:
+    """A hipEvent_t (no timing) whose record / wait go through the C-ABI
+    (ncf_event_record / ncf_stream_wait_event), so a launch tape holds them in order with the
+    kernels.  Created and destroyed outside any tape."""
+    __slots__ = ("h",)
+
+    def __init__(self):
+        lib = _lib if _lib is not None else load()
+        out = ctypes.c_void_p()
+        check(lib.ncf_event_create(ctypes.byref(out)), "ncf_event_create")
+        self.h = out.value
+
+    def record(self, stream: int):
+        call("ncf_event_record", self.h, stream)
+
+    def wait(self, stream: int):
+        """``stream`` waits for the work recorded before the last record()."""
+        call("ncf_stream_wait_event", stream, self.h)
+
+    def __del__(self):
+        h, self.h = getattr(self, "h", None), None
+        if h and _lib is not None:
+            try:
+                _lib.ncf_event_destroy(h)
+            except Exception:
+                pass
 
 
 def ptr(t) -> int:

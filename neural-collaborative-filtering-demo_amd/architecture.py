@@ -101,8 +101,11 @@ class _NCFTrainFunction(torch.autograd.Function):
         # a step left unapplied (e.g. accumulation) keeps its rows' gradients in the
         # workspace this forward reuses: make them dense table .grad before they are overwritten
         _settle_pending(engine, uid.device)
-        w = engine.forward(uid, iid, M, True, drop_p, seed,
-                           prepare=d.prepare if d is not None else None)
+        tp = engine.tapes
+        w = tp.forward(uid, iid, M, drop_p, seed) if tp is not None else None
+        if w is None:
+            w = engine.forward(uid, iid, M, True, drop_p, seed,
+                               prepare=d.prepare if d is not None else None)
         ctx.engine, ctx.w, ctx.drop_p, ctx.seed = engine, w, drop_p, seed
         ctx.save_for_backward(uid, iid)
         return w.prob.view(-1, 1).clone()
@@ -114,7 +117,10 @@ class _NCFTrainFunction(torch.autograd.Function):
         views = eng.grad_views()
         prev = [(p, p.grad.clone()) for p, _ in views if p.grad is not None and p.requires_grad]
         _settle_pending(eng, grad_out.device)
-        eng.backward(ctx.w, uid, iid, grad_out.contiguous(), None, ctx.drop_p, ctx.seed)
+        gp = grad_out.reshape(-1).to(torch.float32).contiguous()
+        tp = eng.tapes
+        if tp is None or not tp.backward(ctx.w, uid, iid, gp, ctx.drop_p, ctx.seed):
+            eng.backward(ctx.w, uid, iid, gp, None, ctx.drop_p, ctx.seed)
         for p, v in views:
             if p.requires_grad:
                 p.grad = v
@@ -252,9 +258,13 @@ class AdvancedNCF(nn.Module):
         eng = self._engine
         train = self.training and torch.is_grad_enabled()
         drop_p = float(self.dropout) if self.training else 0.0
-        # (with a device step clock attached the kernels add its per-step seed)
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0 else 0
+        # with a device step clock attached (the fused Adam bound to this model) the kernels
+        # draw their dropout stream from the clock's per-step seed, as FusedTrainStep does
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0 and eng.clock is None else 0
         if train:
+            dev = eng.flat.device if eng.flat is not None else uid.device
+            uid = uid.to(device=dev, dtype=torch.int64).contiguous()   # (the engine's own
+            iid = iid.to(device=dev, dtype=torch.int64).contiguous()   #  conversion, once)
             out = _NCFTrainFunction.apply(eng, uid, iid, M, drop_p, seed, self._anchor)
         else:
             w = eng.forward(uid, iid, M, False, drop_p, seed)

@@ -22,3 +22,37 @@ extern "C" int ncf_device_count(void) {
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
 }
+
+// Cross-stream ordering through the C-ABI (the fork / join points of a step: the id sort beside
+// the forward, the overlapped sweep): the same hipEventRecord / hipStreamWaitEvent torch's Event
+// would issue, as entry points, so a recorded launch sequence (the fast-call binding's launch
+// tape) replays them in order with the kernels.
+extern "C" int ncf_event_create(void** event) {
+  if (!event) { ncf_set_error("ncf_event_create: NULL out pointer"); return NCF_ERR_ARG; }
+  hipEvent_t e = nullptr;
+  hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  if (r != hipSuccess) { ncf_set_error("hipEventCreateWithFlags: %s", hipGetErrorString(r)); return NCF_ERR_LAUNCH; }
+  *event = (void*)e;
+  return NCF_OK;
+}
+
+extern "C" int ncf_event_destroy(void* event) {
+  if (!event) return NCF_OK;
+  hipError_t r = hipEventDestroy((hipEvent_t)event);
+  if (r != hipSuccess) { ncf_set_error("hipEventDestroy: %s", hipGetErrorString(r)); return NCF_ERR_LAUNCH; }
+  return NCF_OK;
+}
+
+extern "C" int ncf_event_record(void* event, void* stream) {
+  if (!event) { ncf_set_error("ncf_event_record: NULL event"); return NCF_ERR_ARG; }
+  hipError_t r = hipEventRecord((hipEvent_t)event, (hipStream_t)stream);
+  if (r != hipSuccess) { ncf_set_error("hipEventRecord: %s", hipGetErrorString(r)); return NCF_ERR_LAUNCH; }
+  return NCF_OK;
+}
+
+extern "C" int ncf_stream_wait_event(void* stream, void* event) {
+  if (!event) { ncf_set_error("ncf_stream_wait_event: NULL event"); return NCF_ERR_ARG; }
+  hipError_t r = hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0);
+  if (r != hipSuccess) { ncf_set_error("hipStreamWaitEvent: %s", hipGetErrorString(r)); return NCF_ERR_LAUNCH; }
+  return NCF_OK;
+}

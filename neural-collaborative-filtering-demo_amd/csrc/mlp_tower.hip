@@ -595,11 +595,11 @@ __device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const f
 }
 
 // the activation rows a of layer L into LDS: loaded when the forward saved them, else
-// recomputed from r (act4's arithmetic: the same bits).  Loads are issued SB iterations at a
-// time before their uses: a load-then-store loop waits one HBM latency per iteration (stamped:
-// 13K cycles for a0's ten iterations per thread, of ~176K for the whole backward).
+// recomputed from r (act4's arithmetic: the same bits).  NCF_STAGE_BATCH = SB iterations' loads
+// issued before their uses (measured at C2, ms/step: SB 1 0.3075, 5 0.3100, 10 0.3087 — within
+// noise; the load-then-store loop's latency overlaps the other waves' work), default 1.
 #ifndef NCF_STAGE_BATCH
-#define NCF_STAGE_BATCH 5
+#define NCF_STAGE_BATCH 1
 #endif
 template <int K, int PX>
 __device__ __forceinline__ void stage_act(float* __restrict__ X, const ncf_mlp_layer& L,

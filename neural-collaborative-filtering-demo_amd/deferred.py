@@ -262,13 +262,17 @@ class DeferredTableAdam:
         dev = self.clock.device
         if self._side is None:
             self._side = torch.cuda.Stream(dev)
-            self._ev = (torch.cuda.Event(), torch.cuda.Event())
-        cur = torch.cuda.current_stream(dev)
-        self._ev[0].record(cur)
-        self._side.wait_event(self._ev[0])
-        with torch.cuda.stream(self._side):     # (so per-launch instrumentation times it there)
-            self._rolling(self._side.cuda_stream, 0, part, len(self.fork_points))
-        self._ev[1].record(self._side)
+            self._ev = (_lib.RawEvent(), _lib.RawEvent())
+        side = self._side.cuda_stream
+        # (C-ABI event calls: a launch tape of the step holds the fork and join in order)
+        self._ev[0].record(_lib.stream_ptr(dev))
+        self._ev[0].wait(side)
+        if _lib.PROFILE is not None:     # per-launch instrumentation times it on its stream
+            with torch.cuda.stream(self._side):
+                self._rolling(side, 0, part, len(self.fork_points))
+        else:
+            self._rolling(side, 0, part, len(self.fork_points))
+        self._ev[1].record(side)
         self._owed.remove(part)
         self._joined = False
 
@@ -276,7 +280,7 @@ class DeferredTableAdam:
         """The current stream waits for the side-stream sweep (before the step's apply and the
         clock advance that would change the sweep's target under it)."""
         if not self._joined:
-            torch.cuda.current_stream(self.clock.device).wait_event(self._ev[1])
+            self._ev[1].wait(_lib.stream_ptr(self.clock.device))
             self._joined = True
 
     def _settle(self, st):
@@ -361,16 +365,19 @@ class DeferredTableAdam:
         side = getattr(self, "_dedup_side", None)
         if side is None or side.device != dev:
             side = self._dedup_side = torch.cuda.Stream(dev)
-            self._dedup_evs = [torch.cuda.Event() for _ in range(2)]
-        cur = torch.cuda.current_stream(dev)
+            self._dedup_evs = [_lib.RawEvent() for _ in range(2)]
+        cur = st
+        if getattr(w, "dedup_ev", None) is not None:   # a previous sort never joined (no backward)
+            w.dedup_ev.wait(cur)
         self._dedup_evs[0].record(cur)
-        side.wait_event(self._dedup_evs[0])
-        uid.record_stream(side)
-        iid.record_stream(side)
+        self._dedup_evs[0].wait(side.cuda_stream)
+        # uid / iid stay referenced until the engine joins the sort (w.dedup_refs): the caching
+        # allocator cannot hand their memory to work the current stream queues before the join
+        w.dedup_refs = (uid, iid)
         _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, w.g.D, m.num_users, m.num_products,
                   ptr(w.uniq_u), ptr(w.uniq_i), None, None, ptr(w.num_unique), ptr(w.emb_ws),
                   w.emb_ws.numel(), side.cuda_stream)
-        self._dedup_evs[1].record(side)
+        self._dedup_evs[1].record(side.cuda_stream)
         w.dedup_ev = self._dedup_evs[1]
         w.prededuped = None
         w.deduped = True

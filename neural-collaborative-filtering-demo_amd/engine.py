@@ -25,6 +25,7 @@ from ._lib import ptr
 LN_EPS = 1e-5
 # bf16 configuration: the fused MLP tower's Linears on bf16 MFMA (NCF_BF16_MM=0: fp32 MFMA, A/B)
 BF16_MM = os.environ.get("NCF_BF16_MM", "1") != "0"
+_WGRAD_ROWS = int(os.environ.get("NCF_WGRAD_ROWS", "160"))
 
 
 def _tptr(t) -> int:
@@ -104,7 +105,7 @@ class Workspace:
     def splits_for(m_out: int, k_out: int, rows: int) -> int:
         """Row slabs of a weight-gradient product: ~160 batch rows per wave (a few waves per SIMD
         over the grouped launch of a step), at most 256 slabs."""
-        return max(1, min(256, math.ceil(max(rows, 1) / int(os.environ.get("NCF_WGRAD_ROWS", "160")))))
+        return max(1, min(256, math.ceil(max(rows, 1) / _WGRAD_ROWS)))
 
     def run_wgrads(self, st, slot: int = 0):
         """The weight gradients queued since the last call, as one grouped launch on stream
@@ -168,6 +169,14 @@ class NCFEngine:
         self._events = None
         self._ev_i = 0
         self._mlp_ok = {}
+        # NCF_* switches read once per engine (the tests set them before building a model)
+        env = os.environ.get
+        self._env_mlp_fused = env("NCF_MLP_FUSED", "1") != "0"
+        self._env_mlp_wgrad = env("NCF_MLP_WGRAD", "1") != "0"
+        self._env_attn_block = env("NCF_ATTN_BLOCK", "1") != "0"
+        self._env_attn_rc = env("NCF_ATTN_RC", "0") != "0"
+        from .tapes import StepTapes
+        self.tapes = StepTapes(self)   # launch tapes of the reference call pattern (tapes.py)
         self.updates = 0          # parameter writes by the HIP kernels (torch's _version misses them)
 
     # ------------------------------------------------------------------ side streams
@@ -473,7 +482,7 @@ class NCFEngine:
     def mlp_fused(self, D: int, hid) -> bool:
         """Whether the one-launch MLP tower (mlp_tower.hip) covers this geometry;
         NCF_MLP_FUSED=0 forces the per-layer launches (A/B measurement, parity tests)."""
-        if os.environ.get("NCF_MLP_FUSED", "1") == "0":
+        if not self._env_mlp_fused:
             return False
         key = (D, tuple(hid))
         ok = self._mlp_ok.get(key)
@@ -483,11 +492,10 @@ class NCFEngine:
                                                      ctypes.addressof(h)))
         return ok
 
-    @staticmethod
-    def mlp_fused_wgrad() -> bool:
+    def mlp_fused_wgrad(self) -> bool:
         """The tower backward also computes the three MLP weight gradients (per-workgroup
         partials); NCF_MLP_WGRAD=0 leaves them to the grouped weight-gradient launch."""
-        return os.environ.get("NCF_MLP_WGRAD", "1") != "0"
+        return self._env_mlp_wgrad
 
     def _mlp_layers(self, w, train: bool, bwd: bool):
         """ncf_mlp_layer[] for the fused tower (cached per workspace: the parameter and buffer
@@ -523,7 +531,7 @@ class NCFEngine:
     def attn_block(self, D: int, H: int, M: int) -> bool:
         """Whether the one-launch attention block (attn_block.hip) covers this geometry;
         NCF_ATTN_BLOCK=0 forces the unfused launches (A/B measurement, parity tests)."""
-        if os.environ.get("NCF_ATTN_BLOCK", "1") == "0":
+        if not self._env_attn_block:
             return False
         key = ("attn", D, H, M)
         ok = self._mlp_ok.get(key)
@@ -537,7 +545,7 @@ class NCFEngine:
         27.9 MB less HBM traffic per C2 step).  Off by default (NCF_ATTN_RC=1 turns it on):
         measured at C2 the forward gains 3 us and the backward loses 6-7 us (its serial
         re-projection + core prologue costs more than reading the stash back)."""
-        if os.environ.get("NCF_ATTN_RC", "0") == "0":
+        if not self._env_attn_rc:
             return False
         key = ("attn_rc", D, H, M)
         ok = self._mlp_ok.get(key)
@@ -768,8 +776,8 @@ class NCFEngine:
         w.slots_set = False
         ev = getattr(w, "dedup_ev", None)
         if ev is not None:   # the id sort forked beside the forward (deferred._prepare_claim)
-            torch.cuda.current_stream(dev).wait_event(ev)
-            w.dedup_ev = None
+            ev.wait(st)
+            w.dedup_ev = w.dedup_refs = None
         if not getattr(w, "deduped", False):   # sort/deduplicate now (slot maps for the Adam)
             _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, D, m.num_users, m.num_products,
                       ptr(w.uniq_u), ptr(w.uniq_i), ptr(self.slot_u), ptr(self.slot_i),

@@ -241,9 +241,31 @@ class _Binding:
         if w is None and not table_grads and not dense_with:
             return []
         eng.updates += 1
-        # --- tables
+        # dense gradients handed in as other tensors than the flat buffer's views: copied in
+        # first (their .grad normally ARE those views)
+        for p, gv in eng.grad_views():
+            g = p.grad
+            if g is not None and g is not gv and g.data_ptr() != gv.data_ptr():
+                gv.copy_(g)
+        all_dense = len(dense_with) == len(self.dense)
         d = self.D
         clocked = d is not None and w is not None
+        if clocked and all_dense and self.uniform and not getattr(w, "slots_set", False):
+            # the common step: table apply + sweep + dense Adam with the clock advance, from
+            # the launch tape of this geometry when there is one (tapes.py)
+            def run():
+                d.apply(w, st)
+                eng.pending = None
+                _lib.call("ncf_adam_flat_clock_close", ptr(eng.flat), ptr(eng.flat_grad),
+                          ptr(self.m_flat), ptr(self.v_flat), eng.flat.numel(), ptr(d._table), 1,
+                          ptr(self.clock), b1, b2, eps, wd, self.base_seed, st)
+            tp = eng.tapes
+            if tp is None or not tp.step(w, run):
+                run()
+            self.step += 1
+            self.step_t += 1
+            return self._all_params
+        # --- tables
         if clocked:
             d.apply(w, st)             # this step's rows + the rolling 1/64 sweep (clock)
             if getattr(w, "slots_set", False):
@@ -257,12 +279,7 @@ class _Binding:
             self.step_tables_dense_grads(hp, st)
             if d is not None:
                 d.mark_current(self.step + 1)
-        # --- dense parameters (their .grad normally ARE views of the flat gradient buffer)
-        for p, gv in eng.grad_views():
-            g = p.grad
-            if g is not None and g is not gv and g.data_ptr() != gv.data_ptr():
-                gv.copy_(g)
-        all_dense = len(dense_with) == len(self.dense)
+        # --- dense parameters
         # the clock counts table steps (the deferred schedule's t): it advances iff they stepped
         tables_stepped = d is not None and (clocked or bool(table_grads))
         if all_dense and self.uniform and clocked:

@@ -1,6 +1,7 @@
 """CPU-only checks: the C-ABI library loads and exports every symbol include/ncf_hip.h declares
 (no compute calls without a GPU), the ctypes table matches the header, and the host-side mirror of
 the reference surface (state_dict keys, constructor, KJT) behaves like the reference."""
+import ctypes
 import os
 import re
 import subprocess
@@ -57,6 +58,30 @@ def test_code_object_is_gfx950():
                          capture_output=True, text=True)
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in blob or "gfx950" in out.stdout
+
+
+def test_launch_tape_records_and_rebases():
+    """tapes.py's mechanism on a host-only entry point (ncf_adam_step_scalars writes into a
+    host buffer): a recorded call replays with its pointer argument re-based onto another
+    buffer (same offset), size queries are not recorded, a call outside the fast path
+    invalidates the recording."""
+    assert _lib.tapes_available()
+    a = np.zeros(32, np.float32)
+    b = np.zeros(40, np.float32)
+    t = _lib.LaunchTape()
+    with t.record((a.ctypes.data, a.nbytes)):
+        _lib.call("ncf_adam_step_scalars", 1e-3, 0.9, 0.999, 1e-8, 3, 8, a.ctypes.data)
+        _lib.query("ncf_adam_step_scalars", 1e-3, 0.9, 0.999, 1e-8, 3, 8, a.ctypes.data)
+    assert t.valid and t.calls == 1 and t.size() == (1, 1, 1)
+    t.replay((b.ctypes.data + 32,))
+    assert np.array_equal(b[8:], a) and not b[:8].any()
+    bad = _lib.LaunchTape()
+    with bad.record():
+        _lib.call("ncf_adam_step_scalars", 1e-3, 0.9, 0.999, 1e-8, 3, 8,
+                  ctypes.c_void_p(a.ctypes.data))        # (a ctypes object: not the fast path)
+    assert not bad.valid
+    with pytest.raises(RuntimeError):
+        bad.replay()
 
 
 def test_state_dict_keys_and_strict_load(f1):

@@ -93,6 +93,56 @@ def test_hooked_deferred_bitwise_equals_dense_hook(monkeypatch):
     assert optim.binding_of(opt, m).D is not None     # the deferred path really ran
 
 
+def test_launch_tapes_bitwise_equal_eager(monkeypatch):
+    """The reference loop with its phases replayed from launch tapes (tapes.py) == the eager
+    host code, bit for bit: dropout on, an lr change (scalar table refilled in place), a
+    betas change (tapes dropped and recorded again), an eval forward and a state_dict read
+    between steps (rows swept: the next backward / step run eagerly), gradient accumulation
+    and a short last batch (another geometry)."""
+    from ncf_amd import tapes
+    data = batches(30, seed=31)
+    short = batches(2, seed=32)
+    crit = torch.nn.BCELoss()
+
+    def run(enabled):
+        monkeypatch.setattr(tapes, "ENABLED", enabled)
+        m = model(dropout=0.2, seed=33)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+        losses = []
+        m.train()
+        for s, (u, i, t) in enumerate(data):
+            if s == 11:
+                for g in opt.param_groups:
+                    g["lr"] = 2e-3
+            if s == 19:
+                for g in opt.param_groups:
+                    g["betas"] = (0.85, 0.995)
+            if s == 15:
+                m.eval()
+                with torch.no_grad():
+                    m(kjt(u[:10], i[:10]))
+                m.train()
+            if s == 17:
+                m.state_dict()
+            out = m(kjt(u, i))
+            loss = crit(out, t)
+            opt.zero_grad()
+            loss.backward()
+            if s == 23:          # accumulate a second batch into this step
+                crit(m(kjt(*short[0][:2])), short[0][2]).backward()
+            opt.step()
+            losses.append(loss.detach())
+        su, si, st_ = short[1]
+        crit(m(kjt(su[:160], si[:160])), st_[:160]).backward()
+        opt.step()
+        return snapshot(m, opt), torch.stack(losses).cpu(), m
+    a, la, _ = run(False)
+    b, lb, m = run(True)
+    assert torch.equal(la, lb)
+    assert_same(a, b)
+    assert m.engine.tapes.replays > 20, m.engine.tapes.replays
+
+
 def test_hooked_lr_change_bitwise_equals_dense_hook(monkeypatch):
     """An lr change mid-run (a scheduler) applies to the steps not yet taken; rows still behind
     replay the earlier steps with the lr those steps had."""

@@ -56,7 +56,11 @@ def main():
     th = time.perf_counter()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    print(f"host {1e3 * (th - t0) / args.steps:.4f} ms/step, wall {1e3 * (t1 - t0) / args.steps:.4f} ms/step")
+    print(f"host {1e3 * (th - t0) / args.steps:.4f} ms/step, wall {1e3 * (t1 - t0) / args.steps:.4f} ms/step"
+          f" (launch tapes: {m.engine.tapes.replays} phases replayed, {m.engine.tapes.recorded} recorded)")
+    # the backward on the calling thread, so the profile sees it (autograd otherwise runs it on
+    # its device thread)
+    torch.autograd.set_multithreading_enabled(False)
     pr = cProfile.Profile()
     pr.enable()
     for s in range(args.steps):
@@ -64,7 +68,8 @@ def main():
     pr.disable()
     torch.cuda.synchronize()
     buf = io.StringIO()
-    pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(28)
+    pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(30)
+    pstats.Stats(pr, stream=buf).sort_stats("cumulative").print_stats(30)
     print(buf.getvalue())
 
 
