@@ -202,6 +202,11 @@ class StepTapes:
         advance), replayed or recorded; False when the caller must call run() itself."""
         if not self.usable() or not self._horizon():
             return False
+        sig = self._signature()      # (betas / eps / weight decay are launch arguments here)
+        if sig != self.sig:
+            self.entries.clear()
+            self.sig = sig
+            return False
         e = None
         for cand in self.entries.values():
             if cand.w is w and cand.bwd is not None:
