@@ -52,6 +52,9 @@ int ncf_event_create(void** event);
 int ncf_event_destroy(void* event);
 int ncf_event_record(void* event, void* stream);
 int ncf_stream_wait_event(void* stream, void* event);
+int ncf_event_synchronize(void* event);   /* host wait */
+/* stream-ordered hipMemcpyAsync (hipMemcpyDefault): the sharded step's count copies */
+int ncf_memcpy_async(void* dst, const void* src, int64_t bytes, void* stream);
 
 /* ---- a2+a3+a4: EBC lookups x4 + mf_norm/mlp_norm + GMF dot --------------------------------
  * Replaces: EmbeddingBagCollection fwd (architecture.py:286-287), LayerNorms (:305-306,

@@ -37,6 +37,8 @@ SIGNATURES = {
     "ncf_event_destroy": (I32, [P]),
     "ncf_event_record": (I32, [P, P]),
     "ncf_stream_wait_event": (I32, [P, P]),
+    "ncf_event_synchronize": (I32, [P]),
+    "ncf_memcpy_async": (I32, [P, P, I64, P]),
     "ncf_device_count": (I32, []),
     "ncf_gather_ln_gmf_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P, F32,
                                     P, P, P, P, P, P, P]),
@@ -324,6 +326,16 @@ def call(name: str, *args):
     return rc
 
 
+def call_tagged(name: str, tags, *args):
+    """call(name, *args) whose scalar arguments listed in ``tags`` ({argument index: tape slot})
+    are per-step values: a launch tape recording this call replays them with the values given
+    for those slots (LaunchTape.replay bases, after the pointer ranges)."""
+    if _recording:
+        for a, slot in tags.items():
+            _fast_mod.tape_tag(a, slot)
+    return call(name, *args)
+
+
 def query(name: str, *args) -> int:
     lib = _lib if _lib is not None else load()
     if _recording:     # sizes / capabilities: not launches, never part of a tape
@@ -414,6 +426,10 @@ class RawEvent:
     def wait(self, stream: int):
         """``stream`` waits for the work recorded before the last record()."""
         call("ncf_stream_wait_event", stream, self.h)
+
+    def synchronize(self):
+        """Host wait (never part of a tape)."""
+        check(_lib.ncf_event_synchronize(self.h), "ncf_event_synchronize")
 
     def __del__(self):
         h, self.h = getattr(self, "h", None), None

@@ -56,3 +56,21 @@ extern "C" int ncf_stream_wait_event(void* stream, void* event) {
   if (r != hipSuccess) { ncf_set_error("hipStreamWaitEvent: %s", hipGetErrorString(r)); return NCF_ERR_LAUNCH; }
   return NCF_OK;
 }
+
+// Host wait for an event (the row-sharded step's split sizes: RCCL takes them on the host).
+extern "C" int ncf_event_synchronize(void* event) {
+  if (!event) { ncf_set_error("ncf_event_synchronize: NULL event"); return NCF_ERR_ARG; }
+  hipError_t r = hipEventSynchronize((hipEvent_t)event);
+  if (r != hipSuccess) { ncf_set_error("hipEventSynchronize: %s", hipGetErrorString(r)); return NCF_ERR_LAUNCH; }
+  return NCF_OK;
+}
+
+// Stream-ordered copy of `bytes` (device <-> device or device -> pinned host), so it can sit in a
+// recorded launch sequence.
+extern "C" int ncf_memcpy_async(void* dst, const void* src, int64_t bytes, void* stream) {
+  if (bytes < 0 || (bytes > 0 && (!dst || !src))) { ncf_set_error("ncf_memcpy_async: bad arguments"); return NCF_ERR_ARG; }
+  if (bytes == 0) return NCF_OK;
+  hipError_t r = hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, (hipStream_t)stream);
+  if (r != hipSuccess) { ncf_set_error("hipMemcpyAsync: %s", hipGetErrorString(r)); return NCF_ERR_LAUNCH; }
+  return NCF_OK;
+}

@@ -17,7 +17,9 @@ in between.  Pointer arguments that fall inside one of the ranges given to ``tap
 (the step's id lists, the loss gradient, the stream) are patched at replay with the new base
 addresses passed to ``tape_replay`` (same offsets).  A call that fails, or an entry point
 reached through ctypes instead of this module (``tape_invalidate``), invalidates the tape;
-``tape_hold(1)`` suspends recording (size queries).
+``tape_hold(1)`` suspends recording (size queries).  ``tape_tag(arg, slot)`` marks a scalar
+argument of the next call as a replay slot (a per-step size or counter), replayed with the value
+passed for that slot.
 
     python gen_fastcall.py OUT.c
 """
@@ -44,21 +46,41 @@ TAPE_RUNTIME = r"""
 #include <string.h>
 typedef int (*replay_fn)(const void*);
 typedef struct { int idx; int size; char* blob; } TapeOp;
-typedef struct { int op; int off; int slot; unsigned long long delta; } TapePatch;
+typedef struct { int op; int off; int slot; int width; unsigned long long delta; } TapePatch;
 typedef struct { TapeOp* ops; int n, cap; TapePatch* pt; int np, pcap; int valid; } Tape;
-#define NCF_TAPE_SLOTS 8
+#define NCF_TAPE_SLOTS 16
 static Tape* g_rec = NULL;        /* the tape being recorded, if any */
 static int g_hold = 0;            /* recording suspended (size queries) */
 static unsigned long long g_lo[NCF_TAPE_SLOTS], g_hi[NCF_TAPE_SLOTS];
 static int g_nslots = 0;
+/* scalar slots: tape_tag(arg, slot) marks argument `arg` of the NEXT recorded call as slot
+   `slot` (replayed with the value passed for that slot) */
+#define NCF_TAPE_TAGS 8
+static int g_tag_arg[NCF_TAPE_TAGS], g_tag_slot[NCF_TAPE_TAGS];
+static int g_ntags = 0;
+
+static int tape_add_patch(Tape* t, int op, int off, int slot, int width, unsigned long long delta) {
+  if (t->np == t->pcap) {
+    int cap = t->pcap ? 2 * t->pcap : 32;
+    TapePatch* p = (TapePatch*)realloc(t->pt, sizeof(TapePatch) * cap);
+    if (!p) { t->valid = 0; return 0; }
+    t->pt = p; t->pcap = cap;
+  }
+  TapePatch* p = &t->pt[t->np++];
+  p->op = op; p->off = off; p->slot = slot; p->width = width; p->delta = delta;
+  return 1;
+}
 
 static void tape_clear(Tape* t) {
   for (int i = 0; i < t->n; ++i) free(t->ops[i].blob);
   t->n = 0; t->np = 0; t->valid = 1;
 }
 
-static void tape_push(int idx, const void* args, int size, const int* poff) {
+static void tape_push(int idx, const void* args, int size, const int* poff, const int* aoff,
+                      const int* awid, int nargs) {
   Tape* t = g_rec;
+  int ntags = g_ntags;
+  g_ntags = 0;
   if (!t->valid) return;
   if (t->n == t->cap) {
     int cap = t->cap ? 2 * t->cap : 32;
@@ -72,19 +94,17 @@ static void tape_push(int idx, const void* args, int size, const int* poff) {
   int op = t->n;
   t->ops[op].idx = idx; t->ops[op].size = size; t->ops[op].blob = blob;
   t->n++;
+  for (int k = 0; k < ntags; ++k) {
+    const int a = g_tag_arg[k];
+    if (a < 0 || a >= nargs || (awid[a] != 4 && awid[a] != 8)) { t->valid = 0; return; }
+    if (!tape_add_patch(t, op, aoff[a], g_tag_slot[k], awid[a], 0)) return;
+  }
   for (int k = 0; poff[k] >= 0; ++k) {
     unsigned long long v;
     memcpy(&v, blob + poff[k], sizeof v);
     for (int s = 0; s < g_nslots; ++s) {
       if (v >= g_lo[s] && v < g_hi[s]) {
-        if (t->np == t->pcap) {
-          int cap = t->pcap ? 2 * t->pcap : 32;
-          TapePatch* p = (TapePatch*)realloc(t->pt, sizeof(TapePatch) * cap);
-          if (!p) { t->valid = 0; return; }
-          t->pt = p; t->pcap = cap;
-        }
-        TapePatch* p = &t->pt[t->np++];
-        p->op = op; p->off = poff[k]; p->slot = s; p->delta = v - g_lo[s];
+        if (!tape_add_patch(t, op, poff[k], s, 8, v - g_lo[s])) return;
         break;
       }
     }
@@ -119,7 +139,7 @@ static PyObject* py_tape_begin(PyObject* self, PyObject* a) {
   if (!t) return NULL;
   Py_ssize_t m = PyTuple_GET_SIZE(ranges);
   if (m % 2 || m / 2 > NCF_TAPE_SLOTS) {
-    PyErr_SetString(PyExc_ValueError, "tape_begin: (base, size) pairs, at most 8");
+    PyErr_SetString(PyExc_ValueError, "tape_begin: (base, size) pairs, at most 16");
     return NULL;
   }
   if (g_rec) { PyErr_SetString(PyExc_RuntimeError, "tape_begin: a tape is already recording"); return NULL; }
@@ -131,14 +151,14 @@ static PyObject* py_tape_begin(PyObject* self, PyObject* a) {
   }
   g_nslots = (int)(m / 2);
   tape_clear(t);
-  g_rec = t; g_hold = 0;
+  g_rec = t; g_hold = 0; g_ntags = 0;
   Py_RETURN_NONE;
 }
 
 /* tape_end() -> (calls recorded, valid) */
 static PyObject* py_tape_end(PyObject* self, PyObject* a) {
   Tape* t = g_rec;
-  g_rec = NULL; g_hold = 0; g_nslots = 0;
+  g_rec = NULL; g_hold = 0; g_nslots = 0; g_ntags = 0;
   if (!t) return Py_BuildValue("(ii)", 0, 0);
   return Py_BuildValue("(ii)", t->n, t->valid);
 }
@@ -151,8 +171,21 @@ static PyObject* py_tape_hold(PyObject* self, PyObject* a) {
   return PyLong_FromLong(prev);
 }
 
+/* tape_tag(arg, slot): argument `arg` (0-based) of the next recorded call is scalar slot `slot` */
+static PyObject* py_tape_tag(PyObject* self, PyObject* a) {
+  int arg, slot;
+  if (!PyArg_ParseTuple(a, "ii:tape_tag", &arg, &slot)) return NULL;
+  if (slot < 0 || slot >= NCF_TAPE_SLOTS || g_ntags >= NCF_TAPE_TAGS) {
+    PyErr_SetString(PyExc_ValueError, "tape_tag: slot out of range or too many tags");
+    return NULL;
+  }
+  if (g_rec) { g_tag_arg[g_ntags] = arg; g_tag_slot[g_ntags] = slot; g_ntags++; }
+  Py_RETURN_NONE;
+}
+
 static PyObject* py_tape_invalidate(PyObject* self, PyObject* a) {
   if (g_rec) g_rec->valid = 0;
+  g_ntags = 0;
   Py_RETURN_NONE;
 }
 
@@ -174,7 +207,7 @@ static PyObject* py_tape_replay(PyObject* self, PyObject* a) {
   if (g_rec) { PyErr_SetString(PyExc_RuntimeError, "tape_replay while recording"); return NULL; }
   unsigned long long v[NCF_TAPE_SLOTS];
   Py_ssize_t m = PyTuple_GET_SIZE(bases);
-  if (m > NCF_TAPE_SLOTS) { PyErr_SetString(PyExc_ValueError, "tape_replay: at most 8 bases"); return NULL; }
+  if (m > NCF_TAPE_SLOTS) { PyErr_SetString(PyExc_ValueError, "tape_replay: at most 16 bases"); return NULL; }
   for (Py_ssize_t s = 0; s < m; ++s) {
     v[s] = PyLong_AsUnsignedLongLongMask(PyTuple_GET_ITEM(bases, s));
     if (PyErr_Occurred()) return NULL;
@@ -183,7 +216,12 @@ static PyObject* py_tape_replay(PyObject* self, PyObject* a) {
     const TapePatch* p = &t->pt[i];
     if (p->slot >= m) { PyErr_SetString(PyExc_ValueError, "tape_replay: missing base"); return NULL; }
     unsigned long long x = v[p->slot] + p->delta;
-    memcpy(t->ops[p->op].blob + p->off, &x, sizeof x);
+    if (p->width == 8) {
+      memcpy(t->ops[p->op].blob + p->off, &x, 8);
+    } else {
+      unsigned int y = (unsigned int)x;
+      memcpy(t->ops[p->op].blob + p->off, &y, 4);
+    }
   }
   int fail = -1, rc = 0;
   Py_BEGIN_ALLOW_THREADS
@@ -232,6 +270,10 @@ def main(out):
         lines.append(f"typedef struct {{ {fields} }} A_{idx};")
         offs = [f"(int)offsetof(A_{idx}, a{j})" for j, t in enumerate(args) if kinds[id(t)][2]]
         lines.append(f"static const int po_{idx}[] = {{" + ", ".join(offs + ["-1"]) + "};")
+        aoffs = [f"(int)offsetof(A_{idx}, a{j})" for j in range(len(args))] or ["0"]
+        awids = [f"(int)sizeof(((A_{idx}*)0)->a{j})" for j in range(len(args))] or ["0"]
+        lines.append(f"static const int ao_{idx}[] = {{" + ", ".join(aoffs) + "};")
+        lines.append(f"static const int aw_{idx}[] = {{" + ", ".join(awids) + "};")
         lines.append(f"static PyObject* w_{idx}(PyObject* self, PyObject* a) {{  /* {name} */")
         for j, t in enumerate(args):
             lines.append(f"  {kinds[id(t)][1]} a{j} = 0;")
@@ -250,13 +292,13 @@ def main(out):
         lines.append(f"  r = p_{idx}({call});")
         lines.append("  Py_END_ALLOW_THREADS")
         lines.append("  if (g_rec && !g_hold) {")
-        lines.append("    if (r != 0) g_rec->valid = 0;")
+        lines.append("    if (r != 0) { g_rec->valid = 0; g_ntags = 0; }")
         if args:
             lines.append(f"    else {{ A_{idx} s; memset(&s, 0, sizeof s); " +
                          " ".join(f"s.a{j} = a{j};" for j in range(len(args))) +
-                         f" tape_push({idx}, &s, (int)sizeof s, po_{idx}); }}")
+                         f" tape_push({idx}, &s, (int)sizeof s, po_{idx}, ao_{idx}, aw_{idx}, {len(args)}); }}")
         else:
-            lines.append(f"    else {{ A_{idx} s; memset(&s, 0, sizeof s); tape_push({idx}, &s, (int)sizeof s, po_{idx}); }}")
+            lines.append(f"    else {{ A_{idx} s; memset(&s, 0, sizeof s); tape_push({idx}, &s, (int)sizeof s, po_{idx}, ao_{idx}, aw_{idx}, 0); }}")
         lines.append("  }")
         lines.append(f"  return {rconv}(r);")
         lines.append("}")
@@ -284,7 +326,7 @@ def main(out):
     lines.append("static PyMethodDef methods[] = {")
     lines.append("  {\"bind\", ncf_bind, METH_VARARGS, \"bind(index, address)\"},")
     for fn in ("tape_new", "tape_begin", "tape_end", "tape_hold", "tape_invalidate", "tape_replay",
-               "tape_size"):
+               "tape_size", "tape_tag"):
         lines.append(f"  {{\"{fn}\", py_{fn}, METH_VARARGS, NULL}},")
     for idx, name in enumerate(names):
         lines.append(f"  {{\"{name}\", w_{idx}, METH_VARARGS, NULL}},")

@@ -44,6 +44,13 @@ from . import _lib
 from ._lib import ptr
 
 
+# launch-tape slots of the row-sharded step (tapes.py): pointer ranges first (the next batch's
+# ids, the targets, the compute stream), then the per-step scalars
+SLOT_NEXT_U, SLOT_NEXT_I, SLOT_TARGETS, SLOT_STREAM = 0, 1, 2, 3
+SLOT_TOKEN, SLOT_NMAX, SLOT_NUNI = 4, 5, 6
+TAPE_SHARDED = os.environ.get("NCF_TAPE", "1") != "0"
+
+
 class ShardExchange:
     """The collectives of the sharded step (torch.distributed: RCCL on GPU, gloo on CPU).
     ``plan_group`` (a second communicator) carries the count exchange of the pipelined plan so
@@ -74,7 +81,7 @@ class ShardExchange:
             dist.all_to_all_single(both[W:], send, group=self.plan_group)
             both[:W].copy_(send)
             plan.extra["counts_host"].copy_(both, non_blocking=True)
-            plan.extra["counts_ev"].record()
+            plan.extra["counts_ev"].record(plan.stream.cuda_stream)
 
     def counts_wait(self, plan):
         """plan.send_counts / plan.recv_counts as host lists [W][2] (the step's only host
@@ -145,12 +152,28 @@ class RcclExchange(ShardExchange):
         self.main = self._comm()
         self.side = self._comm()
         W = self.world
-        self._sr = (ctypes.c_int64 * W)()       # host split arrays (reused every call)
-        self._rr = (ctypes.c_int64 * W)()
+        # host split arrays, one pair per call site: the collective reads them when it is
+        # called, so a launch tape replays each site with the sizes written there for the step
+        self._sites = {}
         self._one = (ctypes.c_int64 * W)(*([1] * W))
+        self._one_addr = ctypes.addressof(self._one)
         self._side_stream = None
-        self._ev_in, self._ev_out = torch.cuda.Event(), torch.cuda.Event()
+        self._ev_in, self._ev_out = _lib.RawEvent(), _lib.RawEvent()
+        self._ahead_ev = [_lib.RawEvent(), _lib.RawEvent()]
         self._slots = {}
+
+    def site(self, name: str, send_splits=None, recv_splits=None):
+        """(send, recv) host split arrays of call site `name` (addresses), filled when given."""
+        a = self._sites.get(name)
+        if a is None:
+            W = self.world
+            sr, rr = (ctypes.c_int64 * W)(), (ctypes.c_int64 * W)()
+            a = self._sites[name] = (sr, rr, ctypes.addressof(sr), ctypes.addressof(rr))
+        if send_splits is not None:
+            sr, rr = a[0], a[1]
+            for p in range(self.world):
+                sr[p], rr[p] = send_splits[p], recv_splits[p]
+        return a[2], a[3]
 
     def _comm(self):
         uid = torch.zeros(128, dtype=torch.uint8)
@@ -162,7 +185,7 @@ class RcclExchange(ShardExchange):
         uid = t.cpu()
         c = ctypes.c_void_p()
         _lib.call("ncf_comm_init", uid.data_ptr(), 128, self.world, self.rank, ctypes.byref(c))
-        return c
+        return c.value
 
     def close(self):
         for name in ("main", "side"):
@@ -176,40 +199,62 @@ class RcclExchange(ShardExchange):
             raise RuntimeError("RcclExchange needs a plan on a GPU side stream")
         W = self.world
         both = plan.extra["counts_both"]              # device [2W, 2] int64: send rows, recv rows
-        with torch.cuda.stream(plan.stream):
-            send = plan.counts.view(W, 2)
-            _lib.call("ncf_comm_alltoallv", self.side, ptr(send), self._one, ptr(both[W:]),
-                      self._one, 16, plan.stream.cuda_stream)
-            both[:W].copy_(send)
-            plan.extra["counts_host"].copy_(both, non_blocking=True)
-            plan.extra["counts_ev"].record()
+        ps = plan.stream.cuda_stream
+        send = plan.counts
+        # (C-ABI copies and event: the step's launch tape holds them in order)
+        _lib.call("ncf_comm_alltoallv", self.side, ptr(send), self._one_addr, ptr(both) + 16 * W,
+                  self._one_addr, 16, ps)
+        _lib.call("ncf_memcpy_async", ptr(both), ptr(send), 16 * W, ps)
+        _lib.call("ncf_memcpy_async", ptr(plan.extra["counts_host"]), ptr(both), 32 * W, ps)
+        plan.extra["counts_ev"].record(ps)
         self._side_stream = plan.stream
 
     def exchange(self, t: torch.Tensor, send_splits: List[int], recv_splits: List[int],
-                 side: bool = False, slot: Optional[str] = None):
+                 side: bool = False, slot: Optional[str] = None, stream: Optional[int] = None):
         """``slot``: a grow-only output buffer reused by every call with that name (the caller
-        consumes it in stream order before the next such call), else a fresh tensor.
-        Over one rank the all-to-all is the identity: the input itself is returned (no copy; every
-        caller consumes the output in stream order before it next writes the input)."""
+        consumes it in stream order before the next such call), else a fresh tensor; it also
+        names the call site's split arrays.  Over one rank the all-to-all is the identity: the
+        input itself is returned (no copy; every caller consumes the output in stream order
+        before it next writes the input)."""
         if self.world == 1:
             return t[:send_splits[0]]
-        sr, rr = self._sr, self._rr
-        for p in range(self.world):
-            sr[p], rr[p] = send_splits[p], recv_splits[p]
-        shape = (sum(recv_splits),) + tuple(t.shape[1:])
-        if slot is None:
-            out = torch.empty(shape, dtype=t.dtype, device=t.device)
-        else:
-            buf = self._slots.get(slot)
-            n = math.prod(shape)
-            if buf is None or buf.numel() < n or buf.dtype != t.dtype:
-                buf = self._slots[slot] = torch.empty(max(n, 1) * 5 // 4, dtype=t.dtype,
-                                                      device=t.device)
-            out = buf[:n].view(shape)
+        sr, rr = self.site(slot or ("side" if side else "main"), send_splits, recv_splits)
+        out = self.exchange_out(t, recv_splits, slot)
         row = t.element_size() * (math.prod(t.shape[1:]) if t.dim() > 1 else 1)
         _lib.call("ncf_comm_alltoallv", self.side if side else self.main, ptr(t), sr, ptr(out),
-                  rr, row, _lib.stream_ptr(t.device))
+                  rr, row, stream if stream is not None else _lib.stream_ptr(t.device))
         return out
+
+    def exchange_out(self, t: torch.Tensor, recv_splits: List[int], slot: Optional[str] = None):
+        """The output of an exchange of `t` (host side only): a view of slot buffer `slot`
+        (grow-only), or a fresh tensor; over one rank the input itself."""
+        if self.world == 1:
+            return t[:recv_splits[0]]
+        shape = (sum(recv_splits),) + tuple(t.shape[1:])
+        if slot is None:
+            return torch.empty(shape, dtype=t.dtype, device=t.device)
+        buf = self._slots.get(slot)
+        n = math.prod(shape)
+        if buf is None or buf.numel() < n or buf.dtype != t.dtype:
+            buf = self._slots[slot] = torch.empty(max(n, 1) * 5 // 4, dtype=t.dtype,
+                                                  device=t.device)
+        return buf[:n].view(shape)
+
+    def exchange_ahead(self, plan):
+        """ShardExchange.exchange_ahead on the C-ABI: output slot and event per plan-buffer set
+        (two alternate), so consecutive steps never share them."""
+        send_splits, recv_splits = plan.splits()
+        k = plan.extra["set"]["k"]
+        ps = plan.stream.cuda_stream
+        out = self.exchange(plan.send, send_splits, recv_splits, side=True, slot=f"ahead{k}",
+                            stream=ps)
+        ev = self._ahead_ev[k]
+        ev.record(ps)
+        return out, ev
+
+    def wait_ahead(self, out, ev):
+        if ev is not None:
+            ev.wait(_lib.stream_ptr(out.device))
 
     def all_reduce_(self, t: torch.Tensor):
         _lib.call("ncf_comm_allreduce_sum_f32", self.main, ptr(t), t.numel(),
@@ -222,15 +267,15 @@ class RcclExchange(ShardExchange):
         ss = self._side_stream
         if ss is None:
             return self.all_reduce_(t)
-        self._ev_in.record()
-        ss.wait_event(self._ev_in)
+        self._ev_in.record(_lib.stream_ptr(t.device))
+        self._ev_in.wait(ss.cuda_stream)
         _lib.call("ncf_comm_allreduce_sum_f32", self.side, ptr(t), t.numel(), ss.cuda_stream)
-        self._ev_out.record(ss)
+        self._ev_out.record(ss.cuda_stream)
         return self._ev_out
 
     def all_reduce_wait(self, work):
-        if isinstance(work, torch.cuda.Event):
-            torch.cuda.current_stream(self.device).wait_event(work)
+        if isinstance(work, _lib.RawEvent):
+            work.wait(_lib.stream_ptr(self.device))
 
 
 @dataclass
@@ -260,6 +305,11 @@ class ShardedTrainStep:
         self._pending = None      # [user_ids, item_ids, Plan, (recv, event) | None] planned ahead
         # send the next step's rows to their owners during this step (env NCF_SHARD_AHEAD=0: off)
         self.ahead = ahead if ahead is not None else os.environ.get("NCF_SHARD_AHEAD", "1") != "0"
+        # launch tapes (HIP ops + C-ABI collectives): the two launch segments of a step (split
+        # at the host wait for the next plan's sizes) recorded once per geometry and replayed
+        from .tapes import SegmentTapes
+        self.tapes = SegmentTapes() if (TAPE_SHARDED and isinstance(ops, HipShardOps)
+                                        and isinstance(exchange, RcclExchange)) else None
 
     def plan(self, user_ids, item_ids):
         p = self.ops.plan(user_ids, item_ids, self.x.world)
@@ -267,6 +317,8 @@ class ShardedTrainStep:
         return p
 
     def __call__(self, user_ids, item_ids, targets, next=None):
+        if self.tapes is not None and self.tapes.usable(self.ops.deferred):
+            return self._call_taped(user_ids, item_ids, targets, next)
         ops, X = self.ops, self.x
         ops.mark_entry()          # ids of this call and of `next` exist from here on
         pend, self._pending = self._pending, None
@@ -301,6 +353,144 @@ class ShardedTrainStep:
         ops.dense_step()
         return loss
 
+    # ---- the same step with its launches recorded / replayed (tapes.SegmentTapes)
+    def _signature(self):
+        ops, X = self.ops, self.x
+        d = ops.deferred
+        eng = ops.eng
+        return (id(d), d._consts(), d._table.data_ptr(), tuple(d.fork_points), d.overlap,
+                eng.flat.data_ptr(), eng.flat_grad.data_ptr(),
+                tuple(p.data_ptr() for p in eng.table_params().values()),
+                tuple(b.data_ptr() for b in ops._bufs.values() if torch.is_tensor(b)),
+                tuple(b.data_ptr() for b in X._slots.values()),
+                tuple((k, id(v)) for k, v in eng.ws.items()))
+
+    def _call_taped(self, user_ids, item_ids, targets, next=None):
+        ops, X, T = self.ops, self.x, self.tapes
+        d = ops.deferred
+        st = ops._st()
+        ops.mark_entry()
+        pend, self._pending = self._pending, None
+        ahead = None
+        if pend is not None and pend[0] is user_ids and pend[1] is item_ids:
+            plan, ahead = pend[2], pend[3]
+        else:
+            plan = self.plan(user_ids, item_ids)
+        X.counts_wait(plan)
+        n = plan.extra["n"]
+        nplan = None
+        if next is not None:
+            nu_, ni_ = next[0].reshape(-1), next[1].reshape(-1)
+            nplan = ops.plan_host(nu_, ni_)
+            self._pending = [next[0], next[1], nplan, None]
+        targets = targets.reshape(-1).to(device=ops.dev, dtype=torch.float32).contiguous()
+        send_splits, recv_splits = plan.splits()
+        own = ops.owner_host(plan)
+        nu, ni = plan.totals()
+        X.site("recv", send_splits, recv_splits)
+        X.site("rows", recv_splits, send_splits)
+        X.site("grads", send_splits, recv_splits)
+        T.horizon(d)
+        k_set = plan.extra["set"]["k"]
+        key_a = ("a", n, k_set, None if nplan is None else nplan.extra["set"]["k"],
+                 ahead is not None, own["nmax"] > 0)
+        nn_ = 8 * n if next is not None else 0
+        ranges = (ptr(next[0]) if next is not None else 0, nn_,
+                  ptr(next[1]) if next is not None else 0, nn_, ptr(targets), 4 * n, st, 1)
+        # buffers the segments write, at this step's sizes before the signature (grow-only)
+        X.exchange_out(own["rows"], send_splits, "rows")
+        if ahead is None:
+            X.exchange_out(plan.send, recv_splits, "recv")
+        sig = self._signature()
+        w = ops.eng.ws.get((n, ops.M, True))
+        if w is not None:
+            # host-side state the recorded launches read back at replay: the descriptor list
+            # the backward fills, the targets' address in the tower's head arguments
+            w.red_list.count = 0
+            w.wgrads = []
+            h = w.cache.get("head_args")
+            if h is not None:
+                h.targets, h.grad_prob = ptr(targets), None
+        scalars = (own["token"], own["nmax"], max(nu, ni))
+        if next is not None and (not next[0].is_contiguous() or not next[1].is_contiguous()
+                                 or next[0].dtype != torch.int64 or next[1].dtype != torch.int64):
+            T.skip()      # (the plan converts such ids into temporaries: not replayable)
+        res = {}
+
+        def seg_a():
+            if nplan is not None:
+                ops.plan_launch(nplan, next[0].reshape(-1), next[1].reshape(-1))
+                X.counts_issue(nplan)
+            ops.begin(plan)
+            if ahead is not None:
+                recv = ahead[0]
+                X.wait_ahead(*ahead)
+            else:
+                recv = X.exchange(plan.send, send_splits, recv_splits, slot="recv")
+            ops.owner_prepare(recv, plan, own)
+            rows = ops.owner_gather(own, recv)
+            back = X.exchange(rows, recv_splits, send_splits, slot="rows")
+            res["grads"], res["loss"] = ops.compute(plan, back, user_ids, item_ids, targets,
+                                                   loss_denominator=user_ids.numel() * X.world)
+        T.run(key_a, sig, self._pre(), ranges, scalars, seg_a, self._post_a)
+        if "grads" not in res:       # replayed: the same buffers as recorded
+            w = ops.eng.ws[(n, ops.M, True)]
+            w.red_list.count = 0
+            res["grads"] = ops._bufs["send_grads"][:(nu + ni) * 2 * ops.D].view(nu + ni, 2 * ops.D)
+            res["loss"] = w.loss
+            ops.last_loss = res["loss"]
+        # the next plan's sizes (for its rows' exchange ahead), then the rest of the step
+        nahead = None
+        if self.ahead and self._pending is not None:
+            nxt = self._pending[2]
+            X.counts_wait(nxt)
+            s_, r_ = nxt.splits()
+            nahead = nxt.extra["set"]["k"]
+            X.site(f"ahead{nahead}", s_, r_)
+            ahead_out = X.exchange_out(nxt.send, r_, f"ahead{nahead}")
+        grads = res["grads"]
+        X.exchange_out(grads, recv_splits, "grads")
+        key_b = ("b", n, k_set, nahead, own["nmax"] > 0)
+        sig = self._signature()
+
+        def seg_b():
+            if nahead is not None:
+                self._pending[3] = X.exchange_ahead(self._pending[2])
+            ar = X.all_reduce_start(ops.dense_grad())
+            got = X.exchange(grads, send_splits, recv_splits, slot="grads")
+            ops.owner_apply(own, got)
+            X.all_reduce_wait(ar)
+            ops.dense_step()
+        replayed = T.run(key_b, sig, self._pre(), (0, 0, 0, 0, 0, 0, st, 1), scalars, seg_b,
+                         self._post_b)
+        if replayed:
+            if nahead is not None:
+                self._pending[3] = (ahead_out, X._ahead_ev[nahead])
+            ops.step_count += 1
+            ops.eng.updates += 1
+        return res["loss"]
+
+    def _pre(self):
+        ops = self.ops
+        d = ops.deferred
+        return (tuple(d._owed), d._joined, ops.eng.pending is None, d._early_ev is None)
+
+    def _post_a(self, state):
+        """Host state segment A leaves: the deferred sweep's fork (None: capture it)."""
+        d = self.ops.deferred
+        if state is None:
+            return (tuple(d._owed), d._joined)
+        d._owed, d._joined = list(state[0]), state[1]
+
+    def _post_b(self, state):
+        """Segment B closes the step: the deferred schedule's step and sweep state."""
+        d = self.ops.deferred
+        if state is None:
+            return (tuple(d._owed), d._joined)
+        d.t += 1                              # DeferredTableAdam.advance
+        d._owed, d._joined = list(state[0]), state[1]
+        d.engine.pending = None
+
 
 class HipShardOps:
     """Per-rank work of the sharded step on the MI355X (HIP kernels through the C-ABI)."""
@@ -331,7 +521,6 @@ class HipShardOps:
         self.m_flat = torch.zeros_like(self.eng.flat)
         self.v_flat = torch.zeros_like(self.eng.flat)
         self.step_count = 0
-        self.rng = random.Random(self.base_seed)     # dropout seeds without a device sync
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.last_loss = None
         # owner side: claim tokens and row -> unique index, one int32 per local row and kind
@@ -363,6 +552,7 @@ class HipShardOps:
         self._k += 1
         s = self._sets[k]
         if s is None or s["n"] < n:
+            old = s
             i64 = dict(dtype=torch.int64, device=self.dev)
             i32 = dict(dtype=torch.int32, device=self.dev)
             cap = max(n, 1)
@@ -376,10 +566,10 @@ class HipShardOps:
                 bounds=torch.empty(3 * (self.W + 1), **i32),
                 counts_both=torch.zeros(2 * self.W, 2, **i64),
                 counts_host=torch.zeros(2 * self.W, 2, dtype=torch.int64, pin_memory=True),
-                counts_ev=torch.cuda.Event(),
+                counts_ev=old["counts_ev"] if old else _lib.RawEvent(),
                 ws=torch.empty(_lib.query("ncf_embedding_bwd_workspace", cap, self.D),
                                dtype=torch.uint8, device=self.dev),
-                ready=torch.cuda.Event())
+                ready=old["ready"] if old else _lib.RawEvent(), k=k)
             o = s["out"] = _lib.ShardPlanOut()
             o.keys0, o.keys1 = ptr(s["keys"][0]), ptr(s["keys"][1])
             o.uniq0, o.uniq1 = ptr(s["uniq"][0]), ptr(s["uniq"][1])
@@ -395,27 +585,37 @@ class HipShardOps:
         next step's ids are complete there, and so is the run that last used the plan buffer
         set the next plan will fill (two sets alternate).  A plan waits for this event only,
         not for the run enqueued after it, so it overlaps that run."""
-        self._entry = torch.cuda.Event()
-        self._entry.record()
+        if getattr(self, "_entry", None) is None:
+            self._entry = _lib.RawEvent()
+        self._entry.record(self._st())
 
     # plan: requester-side dedup in owner order (side stream)
-    def plan(self, uid, iid, world):
+    def plan_host(self, uid, iid):
+        """The host side of a plan: its buffer set (two alternate) and the Plan object."""
         n = uid.numel()
         s = self._plan_set(n)
-        if getattr(self, "_entry", None) is None:
-            self.mark_entry()
-        ps = self.plan_stream
-        ps.wait_event(self._entry)
-        _lib.call("ncf_shard_plan", ptr(uid), ptr(iid), n, self.W, self.U, self.I, self.D,
-                  ctypes.addressof(s["out"]), ptr(s["ws"]), s["ws"].numel(), ptr(self.err),
-                  ps.cuda_stream)
-        s["ready"].record(ps)
         return Plan(send=s["send"], counts=s["counts"], stream=self.plan_stream,
                     extra={"set": s, "n": n, "counts_both": s["counts_both"],
                            "counts_host": s["counts_host"], "counts_ev": s["counts_ev"]})
 
+    def plan_launch(self, plan, uid, iid):
+        """The plan's launches on the side stream, after the step entry."""
+        s, n = plan.extra["set"], plan.extra["n"]
+        if getattr(self, "_entry", None) is None:
+            self.mark_entry()
+        ps = self.plan_stream.cuda_stream
+        self._entry.wait(ps)
+        _lib.call("ncf_shard_plan", ptr(uid), ptr(iid), n, self.W, self.U, self.I, self.D,
+                  ctypes.addressof(s["out"]), ptr(s["ws"]), s["ws"].numel(), ptr(self.err), ps)
+        s["ready"].record(ps)
+
+    def plan(self, uid, iid, world):
+        p = self.plan_host(uid, iid)
+        self.plan_launch(p, uid, iid)
+        return p
+
     def begin(self, plan):
-        torch.cuda.current_stream(self.dev).wait_event(plan.extra["set"]["ready"])
+        plan.extra["set"]["ready"].wait(self._st())
 
     # 2. owner side: sort-free dedup of the received rows, catch-up, gather
     def _layout(self, counts):
@@ -429,8 +629,9 @@ class HipShardOps:
         L.start[self.W] = off
         return L
 
-    def owner_prepare(self, recv, plan):
-        st = self._st()
+    def owner_host(self, plan):
+        """Host side of the owner phase of a step: the receive layout (one persistent host
+        struct), the claim token and the sizes; the buffers sized for them."""
         L = self._layout(plan.recv_counts)
         tu = sum(c[0] for c in plan.recv_counts)
         ti = sum(c[1] for c in plan.recv_counts)
@@ -440,17 +641,28 @@ class HipShardOps:
         pos = [self._buf("own_pos0", (max(tu, 1), self.W), torch.int32),
                self._buf("own_pos1", (max(ti, 1), self.W), torch.int32)]
         self.token += 1
-        _lib.call("ncf_shard_owner_prepare", ptr(recv), ctypes.addressof(L), self.token,
-                  ptr(self.mark[0]), ptr(self.mark[1]), ptr(self.uidx[0]), ptr(self.uidx[1]),
-                  self.mark[0].numel(), self.mark[1].numel(), ptr(uq[0]), ptr(uq[1]),
-                  ptr(self.cnt), ptr(pos[0]), ptr(pos[1]), ptr(self.err), st)
+        total = L.start[self.W]
+        rows = self._buf("own_rows", (max(total, 1), 2 * self.D))[:total]
+        G = [self._buf(f"own_g{j}", (max(nmax, 1), self.D)) for j in range(4)]
+        return {"layout": L, "uniq": uq, "pos": pos, "nmax": nmax, "token": self.token,
+                "rows": rows, "G": G}
+
+    def owner_prepare(self, recv, plan, own=None):
+        st = self._st()
+        own = own or self.owner_host(plan)
+        L, uq, pos, nmax = own["layout"], own["uniq"], own["pos"], own["nmax"]
+        _lib.call_tagged("ncf_shard_owner_prepare", {2: SLOT_TOKEN}, ptr(recv), ctypes.addressof(L),
+                         own["token"], ptr(self.mark[0]), ptr(self.mark[1]), ptr(self.uidx[0]),
+                         ptr(self.uidx[1]), self.mark[0].numel(), self.mark[1].numel(), ptr(uq[0]),
+                         ptr(uq[1]), ptr(self.cnt), ptr(pos[0]), ptr(pos[1]), ptr(self.err), st)
         d = self.deferred
         if nmax > 0:
             d._ensure(d.t + 1)
             pairs = self._pairs(uq)
-            _lib.call("ncf_adam_pairs_catchup_clock", ctypes.addressof(pairs), 2, self.D,
-                      ptr(self.cnt), nmax, 0, ptr(self.clock), ptr(d._table), *d._consts(), st)
-        return {"layout": L, "uniq": uq, "pos": pos, "nmax": nmax}
+            _lib.call_tagged("ncf_adam_pairs_catchup_clock", {4: SLOT_NMAX},
+                             ctypes.addressof(pairs), 2, self.D, ptr(self.cnt), nmax, 0,
+                             ptr(self.clock), ptr(d._table), *d._consts(), st)
+        return own
 
     def _pairs(self, uq, G=None):
         """ncf_table_pair[2] for the owner's unique rows (cached: the buffers are stable)."""
@@ -467,13 +679,12 @@ class HipShardOps:
 
     def owner_gather(self, own, recv):
         L = own["layout"]
-        total = L.start[self.W]
-        out = self._buf("own_rows", (max(total, 1), 2 * self.D))
+        out = own["rows"]
         tb = self.eng.table_params()
         _lib.call("ncf_shard_owner_gather", ptr(recv), ctypes.addressof(L), ptr(tb["mf_user"]),
                   ptr(tb["mlp_user"]), self.mark[0].numel(), ptr(tb["mf_item"]),
                   ptr(tb["mlp_item"]), self.mark[1].numel(), self.D, ptr(out), self._st())
-        return out[:total]
+        return out
 
     # 3.-4. forward + backward on the mini tables
     def compute(self, plan, back, uid, iid, targets, loss_denominator):
@@ -487,20 +698,22 @@ class HipShardOps:
         slab = 4 * max(n, 1) * D
         mini = {"mf_user": base, "mlp_user": base + slab, "mf_item": base + 2 * slab,
                 "mlp_item": base + 3 * slab}
-        _lib.call("ncf_shard_rows", ptr(back), ptr(s["spos"][0]), ptr(s["spos"][1]),
-                  ptr(s["num_unique"]), max(nu, ni), D, mini["mf_user"], mini["mlp_user"],
-                  mini["mf_item"], mini["mlp_item"], 0, st)
+        _lib.call_tagged("ncf_shard_rows", {4: SLOT_NUNI}, ptr(back), ptr(s["spos"][0]),
+                         ptr(s["spos"][1]), ptr(s["num_unique"]), max(nu, ni), D, mini["mf_user"],
+                         mini["mlp_user"], mini["mf_item"], mini["mlp_item"], 0, st)
         m = self.model
         drop_p = float(m.dropout)
-        seed = self.rng.getrandbits(62) if drop_p > 0 else 0
+        seed = 0      # the dropout stream comes from the device clock's per-step seed
         inv_u, inv_i = s["inv"][0][:n], s["inv"][1][:n]
         w = eng.workspace(n, self.M, True)
         w.emb_ws = s["ws"]            # the plan's dedup segments drive the segment reduce
 
         def mark(wk, u, i, st_):
             wk.deduped = True
+        # (mini-table bounds: the batch size, a bound of the unique-row counts that does not
+        # change per step; the plan's inverse ids are always in range)
         eng.forward(inv_u, inv_i, self.M, True, drop_p, seed, prepare=mark, tables=mini,
-                    rows=(max(nu, 1), max(ni, 1)))
+                    rows=(max(n, 1), max(n, 1)))
         ar = self._buf("arange", (max(n, 1),), torch.int64)
         if self._bufs.get("arange_n") != ar.numel():
             torch.arange(ar.numel(), out=ar)
@@ -509,28 +722,30 @@ class HipShardOps:
                      loss_denominator=loss_denominator, tables=mini,
                      rows=(self.W * self.Ru, self.W * self.Ri), uniq=(ar, ar))
         eng.pending = None
-        g = self._buf("send_grads", (max(nu + ni, 1), 2 * D))
-        _lib.call("ncf_shard_rows", ptr(g), ptr(s["spos"][0]), ptr(s["spos"][1]),
-                  ptr(s["num_unique"]), max(nu, ni), D, ptr(w.G["mf_user"]), ptr(w.G["mlp_user"]),
-                  ptr(w.G["mf_item"]), ptr(w.G["mlp_item"]), 1, st)
+        g = self._buf("send_grads", (max(2 * n, 1), 2 * D))      # (nu + ni <= 2 n rows)
+        _lib.call_tagged("ncf_shard_rows", {4: SLOT_NUNI}, ptr(g), ptr(s["spos"][0]),
+                         ptr(s["spos"][1]), ptr(s["num_unique"]), max(nu, ni), D,
+                         ptr(w.G["mf_user"]), ptr(w.G["mlp_user"]), ptr(w.G["mf_item"]),
+                         ptr(w.G["mlp_item"]), 1, st)
         self.last_loss = w.loss
         return g[:nu + ni], w.loss
 
     # 5. owner side: sum received gradients per unique row (rank order), apply the step
     def owner_apply(self, own, got):
         st = self._st()
-        uq, pos, nmax = own["uniq"], own["pos"], own["nmax"]
-        G = [self._buf(f"own_g{j}", (max(nmax, 1), self.D)) for j in range(4)]
-        _lib.call("ncf_shard_owner_gradsum", ptr(got), ptr(pos[0]), ptr(pos[1]), ptr(self.cnt),
-                  nmax, self.W, self.D, ptr(G[0]), ptr(G[1]), ptr(G[2]), ptr(G[3]), st)
+        uq, pos, nmax, G = own["uniq"], own["pos"], own["nmax"], own["G"]
+        _lib.call_tagged("ncf_shard_owner_gradsum", {4: SLOT_NMAX}, ptr(got), ptr(pos[0]),
+                         ptr(pos[1]), ptr(self.cnt), nmax, self.W, self.D, ptr(G[0]), ptr(G[1]),
+                         ptr(G[2]), ptr(G[3]), st)
         d = self.deferred
         d._ensure(d.t + 1)
         d.sweep_join()
         d._settle(st)
         if nmax > 0:
             pairs = self._pairs(uq, G)
-            _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2, self.D,
-                      ptr(self.cnt), nmax, 1, ptr(self.clock), ptr(d._table), *d._consts(), st)
+            _lib.call_tagged("ncf_adam_pairs_apply_clock", {4: SLOT_NMAX}, ctypes.addressof(pairs),
+                             2, self.D, ptr(self.cnt), nmax, 1, ptr(self.clock), ptr(d._table),
+                             *d._consts(), st)
         d.advance(st)                               # rolling sweep of step t + 1 (clock)
 
     def dense_grad(self):

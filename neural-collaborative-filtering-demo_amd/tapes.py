@@ -234,3 +234,69 @@ class StepTapes:
             e.step, e.step_pre, e.step_post = tape, pre, (tuple(d._owed), d._joined)
             self.recorded += 1
         return True
+
+
+class SegmentTapes:
+    """Launch tapes of the row-sharded step (distributed.ShardedTrainStep): its launches split
+    at the host waits for split sizes into segments, each recorded once per key (geometry,
+    plan-buffer set, pipelining state) and replayed with the step's pointers and scalars
+    (ids of the next batch, targets, stream; claim token and row counts).  Same contract as
+    StepTapes: replayed only from the host state it was recorded in, under an unchanged
+    signature, with the host state it leaves set afterwards."""
+
+    def __init__(self):
+        self.entries = {}
+        self.sig = None
+        self.streak = {}
+        self.replays = 0
+        self.recorded = 0
+        self._skip = False
+
+    def usable(self, d) -> bool:
+        self._skip = False
+        return (ENABLED and d is not None and d.clock is not None and not d.bf16
+                and _lib.PROFILE is None and d._early_req is None and _lib.tapes_available()
+                and not torch.cuda.is_current_stream_capturing())
+
+    def skip(self):
+        """Run this step's segments eagerly (something in it is not replayable)."""
+        self._skip = True
+
+    @staticmethod
+    def horizon(d):
+        """The scalar table covers the step (outside any tape; an address change shows in the
+        caller's signature)."""
+        b1, b2 = d.betas
+        if d._filled < d.t + 2 or d._hp_filled != (d.lr, b1, b2, d.eps):
+            d._ensure(d.t + 2)
+
+    def run(self, key, sig, pre, ranges, scalars, fn, post) -> bool:
+        """Replay segment `key` (True) or run fn() eagerly, recording it once the key has come
+        round RECORD_AFTER times (False).  ``ranges``: flat (base, size) pairs of the pointer
+        slots; ``scalars``: the values of the scalar slots after them; ``post(None)`` returns
+        the host state fn() leaves, ``post(state)`` sets it after a replay."""
+        if sig != self.sig:
+            self.entries.clear()
+            self.sig = sig
+        if self._skip:
+            fn()
+            return False
+        e = self.entries.get(key)
+        if e is not None and e[1] == pre:
+            tape, _, state = e
+            tape.replay(tuple(ranges[0::2]) + tuple(scalars))
+            post(state)
+            self.replays += 1
+            return True
+        cnt = self.streak.get(key, 0) + 1
+        self.streak[key] = cnt
+        if cnt <= RECORD_AFTER:
+            fn()
+            return False
+        tape = _lib.LaunchTape()
+        with tape.record(ranges):
+            fn()
+        if tape.valid:
+            self.entries[key] = (tape, pre, post(None))
+            self.recorded += 1
+        return False

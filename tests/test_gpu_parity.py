@@ -902,14 +902,14 @@ def test_sharded_step_world1_bitwise_equals_fused(exchange, ahead):
         fused = FusedTrainStep(mf, lr=1e-3, weight_decay=1e-5)
         g = torch.Generator().manual_seed(6)
         batches = []
-        for _ in range(6):
+        for _ in range(14):
             u = torch.randint(0, U, (Bg,), generator=g).repeat_interleave(5).to(DEV)
             i = (torch.rand(Bg * 5, generator=g) ** 3 * I).long().to(DEV)
             t = torch.zeros(Bg, 5)
             t[:, 0] = 1
             batches.append((u, i, t.reshape(-1, 1).to(DEV)))
         for s, (u, i, t) in enumerate(batches):
-            # steps 1-4 plan their successor ahead (pipelined); steps 0 and 5 plan inline
+            # steps 1-12 plan their successor ahead (pipelined); steps 0 and 13 plan inline
             nxt = batches[s + 1][:2] if 1 <= s < len(batches) - 1 else None
             l1 = sharded(u, i, t, next=nxt)
             fused(u, i, t)
@@ -919,6 +919,8 @@ def test_sharded_step_world1_bitwise_equals_fused(exchange, ahead):
         for k in a:
             assert torch.equal(a[k], b[k]), k
         if exchange == "rccl":
+            # the later steps replayed their launch tapes (tapes.SegmentTapes)
+            assert sharded.tapes.replays >= 8, sharded.tapes.replays
             sharded.x.close()
     finally:
         dist.destroy_process_group()

@@ -45,8 +45,13 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(5, a.steps)
+    th = time.perf_counter()
     torch.cuda.synchronize()
-    print(f"wall {(time.perf_counter() - t0) / a.steps * 1e3:.3f} ms/step", flush=True)
+    T = step.tapes
+    print(f"wall {(time.perf_counter() - t0) / a.steps * 1e3:.3f} ms/step, host "
+          f"{(th - t0) / a.steps * 1e3:.3f} ms/step; launch tapes: "
+          + (f"{T.replays} segments replayed, {T.recorded} recorded, keys {sorted(T.entries)}"
+             if T is not None else "off"), flush=True)
     # host time per protocol phase (wrappers on the ops / exchange methods)
     acc = {}
 
