@@ -74,8 +74,9 @@ class DeferredTableAdam:
         self.overlap = bool(overlap_sweep)
         if self.overlap and clock is None:
             raise ValueError("the overlapped sweep needs the device step clock")
-        # Where the engine forks it ("mlp_bwd": before the MLP tower backward; "tower": before
-        # the tower forward; "attn_bwd", "emb_bwd", "reduce": before those backward launches)
+        # Where the engine forks it ("mlp_bwd": before the MLP tower backward; "mlp_bwd_after":
+        # right after its launch (round 3: 0.337-0.344 vs 0.312 ms); "tower": before the tower
+        # forward; "attn_bwd", "emb_bwd", "reduce": before those backward launches)
         # and where the step joins it ("apply": before the table apply; "close": before the
         # step's last launch, which advances the clock the sweep reads).  Measured at C2 (one
         # MI355X, ms/step): not overlapped 0.337; forked at tower 0.325, mlp_bwd 0.313-0.317,

@@ -699,6 +699,7 @@ class NCFEngine:
                       len(hid), haddr, drop_p, seed,
                       ptr(self.clock), ctypes.addressof(h), ptr(w.dy), ptr(w.site("mlp")),
                       w.site("mlp").numel(), w.red_list.address, st)
+            self._sweep_fork("mlp_bwd_after")     # (a fork point right behind the tower backward)
         fused_all = fused and self.mlp_fused_wgrad()
         if fused_all and self._zero_cols_of is not self.flat_grad:
             # gradient columns of mlp.0 that see the all-zero temporal input: exactly 0, and no
