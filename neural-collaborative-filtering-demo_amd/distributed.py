@@ -369,6 +369,7 @@ class ShardedTrainStep:
         ops, X, T = self.ops, self.x, self.tapes
         d = ops.deferred
         st = ops._st()
+        ops.eng.ensure_layout()   # (as eng.forward would; a re-pack moves the signature)
         ops.mark_entry()
         pend, self._pending = self._pending, None
         ahead = None

@@ -111,6 +111,7 @@ class StepTapes:
             self.streak = (None, 0)
             return None
         eng = self.eng
+        eng.ensure_layout()       # (a parameter re-assigned since: re-pack, the signature moves)
         n = uid.numel()
         key = (n, M, float(drop_p), int(seed))
         ks, cnt = self.streak
