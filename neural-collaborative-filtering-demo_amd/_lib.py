@@ -311,9 +311,13 @@ def _invoke(lib, name, args):
     return getattr(lib, name)(*args)
 
 
+# stream plumbing, not kernels: never bracketed by the instrumentation
+_NOT_TIMED = frozenset(("ncf_event_record", "ncf_stream_wait_event", "ncf_memcpy_async"))
+
+
 def call(name: str, *args):
     lib = _lib if _lib is not None else load()
-    if PROFILE is not None:
+    if PROFILE is not None and name not in _NOT_TIMED:
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         rc = _invoke(lib, name, args)
