@@ -2,7 +2,8 @@
 # Build libncf_hip.so (gfx950) in-tree.  Used by __graft_entry__.build(); safe to run by hand.
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")" && pwd)"
-SRC="$ROOT/neural-collaborative-filtering-demo_amd/csrc"
+SRC="${NCF_SRC:-$ROOT/neural-collaborative-filtering-demo_amd/csrc}"   # NCF_SRC: A/B source trees
+GEN="$ROOT/neural-collaborative-filtering-demo_amd/csrc/gen_fastcall.py"
 OUT="${NCF_OUT:-$ROOT/neural-collaborative-filtering-demo_amd/libncf_hip.so}"   # NCF_OUT: A/B builds
 HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 OBJ="${NCF_OBJ:-$SRC/build}"
@@ -24,7 +25,7 @@ echo "built $OUT"
 # loader and hands it the resolved entry points)
 PYINC="$(python3 -c 'import sysconfig; print(sysconfig.get_paths()["include"])')"
 PYSUF="$(python3 -c 'import sysconfig; print(sysconfig.get_config_var("EXT_SUFFIX"))')"
-python3 "$SRC/gen_fastcall.py" "$OBJ/_ncffast.c"
+python3 "$GEN" "$OBJ/_ncffast.c"
 FAST="$(dirname "$OUT")/_ncffast$PYSUF"
 gcc -O2 -shared -fPIC -I"$PYINC" "$OBJ/_ncffast.c" -o "$FAST.tmp"
 mv "$FAST.tmp" "$FAST"

@@ -689,6 +689,35 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
   }
   float4 aw = make_float4(0.f, 0.f, 0.f, 0.f);
   float sw0 = 0.f, sw1 = 0.f, sbf = 0.f, sbo = 0.f, sbm = 0.f, sl = 0.f;
+  // Every pass's loads first (all of this thread's rows in flight), then the math: a
+  // load-then-use loop waits one HBM latency per pass (the phase was 16.8K of the backward's
+  // 192K cycles per workgroup).  Same values, same arithmetic (act4's) as loading in the loop.
+  float ld_o[kPasses], ld_t[kPasses], ld_mu[kPasses], ld_rs[kPasses];
+  float4 ld_x[kPasses], ld_u[kPasses][CM], ld_it[kPasses][CM];
+  const float4 g2 = L2.a ? make_float4(0.f, 0.f, 0.f, 0.f) : ld4(L2.gamma + col);
+  const float4 b2 = L2.a ? make_float4(0.f, 0.f, 0.f, 0.f) : ld4(L2.beta + col);
+#pragma unroll
+  for (int pass = 0; pass < kPasses; ++pass) {
+    const int rr = (threadIdx.x >> 4) + pass * (kThreads / 16);
+    const int64_t row = row0 + rr;
+    if (rr < kRows && rr < rows) {
+      ld_o[pass] = h.prob[row];
+      ld_t[pass] = h.targets ? h.targets[row] : h.grad_prob[row];
+      if (L2.a) {
+        ld_x[pass] = ld4(L2.a + row * N2 + col);
+      } else {
+        ld_mu[pass] = L2.mean[row];
+        ld_rs[pass] = L2.rstd[row];
+        ld_x[pass] = ld4(L2.r + row * N2 + col);
+      }
+#pragma unroll
+      for (int c = 0; c < CM; ++c) {
+        const int64_t o = row * K0 + 64 * c + col;
+        ld_u[pass][c] = ld4(h.mf_user_ln + o);
+        ld_it[pass][c] = ld4(h.mf_item_ln + o);
+      }
+    }
+  }
 #pragma unroll
   for (int pass = 0; pass < kPasses; ++pass) {
     const int rr = (threadIdx.x >> 4) + pass * (kThreads / 16);
@@ -697,26 +726,31 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
     const bool ok = rr < rows;
     float dz = 0.f, l = 0.f;
     if (ok) {
-      const float o = h.prob[row];
+      const float o = ld_o[pass];
       float go;
       if (h.targets) {
-        const float t = h.targets[row];
+        const float t = ld_t[pass];
         go = inv_n * (o - t) / fmaxf((1.0f - o) * o, 1e-12f);
         l = -(t * fmaxf(logf(o), -100.0f) + (1.0f - t) * fmaxf(logf(1.0f - o), -100.0f));
       } else {
-        go = h.grad_prob[row];
+        go = ld_t[pass];
       }
       dz = go * (1.0f - o) * o;
     }
     const float dmf = dz * wf0, dml = dz * wf1;
     lds4_st(G + rr * kPQ + col, make_float4(dml * wo.x, dml * wo.y, dml * wo.z, dml * wo.w));
     if (ok) {
-      const float4 x = L2.a ? ld4(L2.a + row * N2 + col) : act4<N2>(L2, row, col, p, seed, inv_keep);
+      float4 x = ld_x[pass];
+      if (!L2.a) {   // act4 on the loaded row values
+        const float mu = ld_mu[pass], rs = ld_rs[pass];
+        const float4 y = ln_affine(make_float4(x.x - mu, x.y - mu, x.z - mu, x.w - mu), rs, g2, b2);
+        x = drop4(y, seed, ((uint64_t)row * N2 + col) >> 2, p, inv_keep);
+      }
       aw.x += dml * x.x; aw.y += dml * x.y; aw.z += dml * x.z; aw.w += dml * x.w;
 #pragma unroll
       for (int c = 0; c < CM; ++c) {
         const int64_t o = row * K0 + 64 * c + col;
-        const float4 u = ld4(h.mf_user_ln + o), it = ld4(h.mf_item_ln + o);
+        const float4 u = ld_u[pass][c], it = ld_it[pass][c];
         const float4 gv = make_float4(dmf * wm[c].x, dmf * wm[c].y, dmf * wm[c].z, dmf * wm[c].w);
         st4_nt(h.grad_mf_user_ln + o, make_float4(gv.x * it.x, gv.y * it.y, gv.z * it.z, gv.w * it.w));
         st4_nt(h.grad_mf_item_ln + o, make_float4(gv.x * u.x, gv.y * u.y, gv.z * u.z, gv.w * u.w));
