@@ -32,6 +32,8 @@ _KINDS = (("user", "mf_user", "mlp_user"), ("item", "mf_item", "mlp_item"))
 # Catch-up by claim (no id sort before the forward) when the batch was not sorted ahead;
 # NCF_CLAIM_CATCHUP=0: sort inline, then catch up the unique rows (A/B)
 CLAIM_CATCHUP = os.environ.get("NCF_CLAIM_CATCHUP", "1") != "0"
+# the id sorts forked beside a step share the overlapped sweep's side stream (A/B)
+SHARE_SIDE = os.environ.get("NCF_SHARE_SIDE", "0") != "0"
 _SERIAL = itertools.count(1)      # distinguishes schedules in workspace caches (ids recycle)
 
 
@@ -260,11 +262,8 @@ class DeferredTableAdam:
         part = self.fork_points.index(at)
         if part not in self._owed:
             return
+        side = self.side_stream().cuda_stream
         dev = self.clock.device
-        if self._side is None:
-            self._side = torch.cuda.Stream(dev)
-            self._ev = (_lib.RawEvent(), _lib.RawEvent())
-        side = self._side.cuda_stream
         # (C-ABI event calls: a launch tape of the step holds the fork and join in order)
         self._ev[0].record(_lib.stream_ptr(dev))
         self._ev[0].wait(side)
@@ -276,6 +275,14 @@ class DeferredTableAdam:
         self._ev[1].record(side)
         self._owed.remove(part)
         self._joined = False
+
+    def side_stream(self):
+        """The overlapped sweep's stream (created on first use); with NCF_SHARE_SIDE the id
+        sorts forked beside the step use it too (one side stream instead of two)."""
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.clock.device)
+            self._ev = (_lib.RawEvent(), _lib.RawEvent())
+        return self._side
 
     def sweep_join(self):
         """The current stream waits for the side-stream sweep (before the step's apply and the
@@ -365,7 +372,8 @@ class DeferredTableAdam:
         dev = self.clock.device
         side = getattr(self, "_dedup_side", None)
         if side is None or side.device != dev:
-            side = self._dedup_side = torch.cuda.Stream(dev)
+            side = self._dedup_side = (self.side_stream() if SHARE_SIDE and self.overlap
+                                       else torch.cuda.Stream(dev))
             self._dedup_evs = [_lib.RawEvent() for _ in range(2)]
         cur = st
         if getattr(w, "dedup_ev", None) is not None:   # a previous sort never joined (no backward)

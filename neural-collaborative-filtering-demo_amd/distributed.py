@@ -518,7 +518,7 @@ class HipShardOps:
         self.deferred = DeferredTableAdam(self.eng, lr, betas, eps, weight_decay, sweep_every,
                                           clock=self.clock,
                                           overlap_sweep=os.environ.get("NCF_SHARD_OVERLAP_SWEEP",
-                                                                       "0") != "0")
+                                                                       "1") != "0")
         self.m_flat = torch.zeros_like(self.eng.flat)
         self.v_flat = torch.zeros_like(self.eng.flat)
         self.step_count = 0
@@ -533,6 +533,14 @@ class HipShardOps:
         self.token = 0
         self.cnt = torch.zeros(2, dtype=torch.int32, device=self.dev)
         self.plan_stream = torch.cuda.Stream(self.dev)
+        if self.deferred.overlap and os.environ.get("NCF_SHARD_SWEEP_ON_PLAN", "1") != "0":
+            # the overlapped sweep on the plan's stream, not a stream of its own: world 1,
+            # ms/step (interleaved, 3 runs each): sweep serial 0.378-0.385, overlapped on its
+            # own stream 0.40-0.43, overlapped on the plan stream 0.361-0.365 (hardware queues
+            # are few: GPU_MAX_HW_QUEUES=4, and RCCL's communicators hold streams of their own;
+            # with 8 queues the step took 0.70 ms)
+            self.deferred._side = self.plan_stream
+            self.deferred._ev = (_lib.RawEvent(), _lib.RawEvent())
         self._sets = [None, None]     # double-buffered plan buffers (plan t+1 while t runs)
         self._k = 0
         self._bufs = {}

@@ -192,7 +192,10 @@ class FusedTrainStep:
         eng = self.model.engine
         m = self.model
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(eng.flat.device)
+            from .deferred import SHARE_SIDE
+            d = self.deferred
+            self._side = (d.side_stream() if SHARE_SIDE and d is not None and d.overlap
+                          else torch.cuda.Stream(eng.flat.device))
         side = self._side
         side.wait_event(entry)
         u = uid.reshape(-1)
