@@ -53,18 +53,22 @@ class StepTapes:
         self.recorded = 0
 
     # ---- validity
-    def _signature(self):
+    def _signature(self, light: int = 0):
         """Everything a tape holds by address or value beyond the step's ids / gradient /
-        stream: a change drops every tape."""
+        stream: a change drops every tape.  The forward checks all of it; within the step the
+        backward checks the first 4 fields and the optimizer step the first 5 (`light`) — the
+        rest cannot change between the three calls of one step without a forward."""
         eng = self.eng
         d = eng.deferred
+        head = (id(d), d._table.data_ptr(), eng.flat.data_ptr(), eng.flat_grad.data_ptr(),
+                d._consts())
+        if light:
+            return head[:light]
         tb = eng.table_params()
-        return (id(d), d._serial, getattr(d, "_gen", 0), d._consts(), d._table.data_ptr(),
-                tuple(d.fork_points), d.join_at, d.overlap, d.sweep_every,
-                eng.flat.data_ptr(), eng.flat_grad.data_ptr(),
-                tuple(p.data_ptr() for p in tb.values()),
-                tuple(s["exp_avg"].data_ptr() for s in d.state.values()),
-                eng.clock.data_ptr(), eng.err_flag(eng.flat.device).data_ptr())
+        return head + (d._serial, getattr(d, "_gen", 0), tuple(d.fork_points), d.join_at,
+                       d.overlap, d.sweep_every, tuple(p.data_ptr() for p in tb.values()),
+                       tuple(s["exp_avg"].data_ptr() for s in d.state.values()),
+                       eng.clock.data_ptr(), eng.err_flag(eng.flat.device).data_ptr())
 
     def usable(self) -> bool:
         eng = self.eng
@@ -160,7 +164,11 @@ class StepTapes:
         if not self.usable() or not self._horizon():
             return False
         n = w.g.n
-        e = self._entry((n, w.g.M, float(drop_p), int(seed)), create=False)
+        if self.sig is None or self._signature(4) != self.sig[:4]:
+            self.entries.clear()
+            self.sig = None
+            return False
+        e = self.entries.get((n, w.g.M, float(drop_p), int(seed)))
         if e is None or e.w is not w or e.fwd is None:
             return False
         eng = self.eng
@@ -203,10 +211,10 @@ class StepTapes:
         advance), replayed or recorded; False when the caller must call run() itself."""
         if not self.usable() or not self._horizon():
             return False
-        sig = self._signature()      # (betas / eps / weight decay are launch arguments here)
-        if sig != self.sig:
+        # (betas / eps / weight decay are launch arguments here: checked with the addresses)
+        if self.sig is None or self._signature(5) != self.sig[:5]:
             self.entries.clear()
-            self.sig = sig
+            self.sig = None
             return False
         e = None
         for cand in self.entries.values():
