@@ -254,11 +254,12 @@ class _Binding:
             # the common step: table apply + sweep + dense Adam with the clock advance, from
             # the launch tape of this geometry when there is one (tapes.py)
             def run():
-                d.apply(w, st)
+                s_ = _lib.stream_ptr(dev)     # (the current stream: a capture's, under one)
+                d.apply(w, s_)
                 eng.pending = None
                 _lib.call("ncf_adam_flat_clock_close", ptr(eng.flat), ptr(eng.flat_grad),
                           ptr(self.m_flat), ptr(self.v_flat), eng.flat.numel(), ptr(d._table), 1,
-                          ptr(self.clock), b1, b2, eps, wd, self.base_seed, st)
+                          ptr(self.clock), b1, b2, eps, wd, self.base_seed, s_)
             tp = eng.tapes
             if tp is None or not tp.step(w, run):
                 run()
