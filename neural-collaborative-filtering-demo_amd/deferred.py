@@ -32,6 +32,11 @@ _KINDS = (("user", "mf_user", "mlp_user"), ("item", "mf_item", "mlp_item"))
 # Catch-up by claim (no id sort before the forward) when the batch was not sorted ahead;
 # NCF_CLAIM_CATCHUP=0: sort inline, then catch up the unique rows (A/B)
 CLAIM_CATCHUP = os.environ.get("NCF_CLAIM_CATCHUP", "1") != "0"
+# where the claim path forks its id sort: beside the forward ("forward"), or at one of the
+# backward's fork points ("mlp_bwd", "attn_bwd", ...; engine._sweep_fork).  Drop-in step when
+# GPU-bound (ms): beside the forward 0.350-0.353, at the tower backward 0.393-0.399 (beside the
+# overlapped sweep), at the attention backward 0.381-0.389 (longer than that kernel)
+CLAIM_SORT_AT = os.environ.get("NCF_CLAIM_SORT_AT", "forward")
 # the id sorts forked beside a step share the overlapped sweep's side stream (A/B)
 SHARE_SIDE = os.environ.get("NCF_SHARE_SIDE", "0") != "0"
 _SERIAL = itertools.count(1)      # distinguishes schedules in workspace caches (ids recycle)
@@ -369,6 +374,26 @@ class DeferredTableAdam:
         _lib.call("ncf_adam_pairs_catchup_claim_clock", ctypes.addressof(pairs), 2,
                   m.mlp_embedding_dim, ptr(uid), ptr(iid), n, 0, ptr(self.clock),
                   ptr(self._table), *self._consts(), st)
+        if getattr(w, "dedup_ev", None) is not None:   # a previous sort never joined (no backward)
+            w.dedup_ev.wait(st)
+            w.dedup_ev = None
+        w.prededuped = None
+        w.deduped = True
+        # uid / iid stay referenced until the engine joins the sort (w.dedup_refs): the caching
+        # allocator cannot hand their memory to work the current stream queues before the join
+        w.dedup_refs = (uid, iid)
+        if CLAIM_SORT_AT == "forward":
+            self.fork_claim_sort(w, st)
+        else:   # forked by the engine's backward at that fork point (engine._sweep_fork)
+            w.sort_pending = True
+
+    def fork_claim_sort(self, w, st):
+        """The id sort of a claim-path step (w.dedup_refs) on the side stream, after everything
+        queued on stream st so far; joined through w.dedup_ev."""
+        uid, iid = w.dedup_refs
+        m = self.engine.model
+        n = w.g.n
+        w.sort_pending = None
         dev = self.clock.device
         side = getattr(self, "_dedup_side", None)
         if side is None or side.device != dev:
@@ -376,20 +401,13 @@ class DeferredTableAdam:
                                        else torch.cuda.Stream(dev))
             self._dedup_evs = [_lib.RawEvent() for _ in range(2)]
         cur = st
-        if getattr(w, "dedup_ev", None) is not None:   # a previous sort never joined (no backward)
-            w.dedup_ev.wait(cur)
         self._dedup_evs[0].record(cur)
         self._dedup_evs[0].wait(side.cuda_stream)
-        # uid / iid stay referenced until the engine joins the sort (w.dedup_refs): the caching
-        # allocator cannot hand their memory to work the current stream queues before the join
-        w.dedup_refs = (uid, iid)
         _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, w.g.D, m.num_users, m.num_products,
                   ptr(w.uniq_u), ptr(w.uniq_i), None, None, ptr(w.num_unique), ptr(w.emb_ws),
                   w.emb_ws.numel(), side.cuda_stream)
         self._dedup_evs[1].record(side.cuda_stream)
         w.dedup_ev = self._dedup_evs[1]
-        w.prededuped = None
-        w.deduped = True
 
     def request_early(self, side, uniq_u, uniq_i, num_unique, n):
         """Ask the next prepare() (this step's) to catch up the next batch's unique rows

@@ -21,6 +21,7 @@ import torch
 
 from . import _lib
 from ._lib import ptr
+from .deferred import CLAIM_SORT_AT
 
 LN_EPS = 1e-5
 # bf16 configuration: the fused MLP tower's Linears on bf16 MFMA (NCF_BF16_MM=0: fp32 MFMA, A/B)
@@ -634,12 +635,15 @@ class NCFEngine:
         a["pending"] = True
 
     # ------------------------------------------------------------------ backward
-    def _sweep_fork(self, at: str):
+    def _sweep_fork(self, at: str, w=None):
         """Launch the previous step's owed rolling sweep on its side stream when the overlapped
-        sweep is on and `at` is one of its fork points (DeferredTableAdam.fork_points)."""
+        sweep is on and `at` is one of its fork points (DeferredTableAdam.fork_points); the
+        claim path's id sort of workspace w when `at` is its fork point (CLAIM_SORT_AT)."""
         d = self.deferred
         if d is not None and d.overlap:
             d.sweep_fork(at)
+        if w is not None and getattr(w, "sort_pending", None) and at == CLAIM_SORT_AT:
+            d.fork_claim_sort(w, _lib.stream_ptr(w.prob.device))
         hook = self.fork_hook
         if hook is not None:
             hook(at)
@@ -678,7 +682,7 @@ class NCFEngine:
                       float(loss_denominator), ptr(w.site("head")), w.site("head").numel(),
                       w.red_list.address, st)
         # a7 backward, last layer first
-        self._sweep_fork("mlp_bwd")
+        self._sweep_fork("mlp_bwd", w)
         if fused:   # head + relu/LN/dropout backward + dX of all layers in one launch
             _, addr, _, haddr = self._mlp_layers(w, True, bwd=True)
             h = w.cache.get("head_args")
@@ -738,7 +742,7 @@ class NCFEngine:
                 dx = w.dy if l == 0 else w.da[l - 1]
                 self._gemm(w.dlin[l], h, 0, lin.weight, ldw, 0, dx, kin, n, kin, h, st=st)
         # a5 backward: out_proj, core, q/k/v projections
-        self._sweep_fork("attn_bwd")
+        self._sweep_fork("attn_bwd", w)
         pp = self.pp()
         if self.attn_block(D, H, M):
             # core + projections backward and the four Linear gradients in one launch
@@ -766,7 +770,7 @@ class NCFEngine:
         else:
             self._attention_bwd_unfused(w, drop_p, seed, joins, st)
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)
-        self._sweep_fork("emb_bwd")
+        self._sweep_fork("emb_bwd", w)
         if tables is None:
             tbp = (pp["t_mf_user"], pp["t_mlp_user"], pp["t_mf_item"], pp["t_mlp_item"])
         else:
@@ -775,6 +779,8 @@ class NCFEngine:
         uq_u, uq_i = uniq if uniq is not None else (w.uniq_u, w.uniq_i)
         d_rows = rows or (m.num_users, m.num_products)
         w.slots_set = False
+        if getattr(w, "sort_pending", None):   # its fork point not passed: fork it now
+            self.deferred.fork_claim_sort(w, st)
         ev = getattr(w, "dedup_ev", None)
         if ev is not None:   # the id sort forked beside the forward (deferred._prepare_claim)
             ev.wait(st)

@@ -59,8 +59,17 @@ def main():
     print(f"host {1e3 * (th - t0) / args.steps:.4f} ms/step, wall {1e3 * (t1 - t0) / args.steps:.4f} ms/step"
           f" (launch tapes: {m.engine.tapes.replays} phases replayed, {m.engine.tapes.recorded} recorded)")
     # the backward on the calling thread, so the profile sees it (autograd otherwise runs it on
-    # its device thread)
+    # its device thread); timed that way too
     torch.autograd.set_multithreading_enabled(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        one(s)
+    th = time.perf_counter()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    print(f"autograd on the calling thread: host {1e3 * (th - t0) / args.steps:.4f} ms/step, "
+          f"wall {1e3 * (t1 - t0) / args.steps:.4f} ms/step")
     pr = cProfile.Profile()
     pr.enable()
     for s in range(args.steps):
