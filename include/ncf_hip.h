@@ -493,8 +493,11 @@ int ncf_score_split_items(const float* items, int64_t n_items, int64_t dim, uint
 int ncf_score_collect_split(const float* queries, const int32_t* user_list, int64_t n_users,
                             const uint16_t* items3, const float* item_bias, int64_t n_items,
                             int64_t dim, const float* thr, int64_t cap, uint32_t* count,
-                            float* cand_logit, int32_t* cand_item, int terms, void* stream);
-/* terms = 2: the scan takes only x0 + x1 of each operand (three products a0b0 + a0b1 + a1b0):
+                            float* cand_logit, int32_t* cand_item, int terms,
+                            int64_t expected_per_user, void* stream);
+/* expected_per_user: the candidates per user the thresholds aim at (0: unknown); sizes the item
+ * split so a wave's candidates fit its LDS slice (fewer, grouped global writes).
+ * terms = 2: the scan takes only x0 + x1 of each operand (three products a0b0 + a0b1 + a1b0):
  * its logits are within 1e-4 * |q_u| * max_i |p_i| of fp32, so the thresholds are first lowered
  * by that (ncf_score_margin, with max_i |p_i| from ncf_score_item_norm_max) and the candidates'
  * logits recomputed in fp32 by ncf_score_select_rescored. */

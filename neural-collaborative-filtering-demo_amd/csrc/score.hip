@@ -1241,7 +1241,7 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
                                        const float* item_bias, int64_t n_items, int64_t dim,
                                        const float* thr, int64_t cap, uint32_t* count,
                                        float* cand_logit, int32_t* cand_item, int terms,
-                                       void* stream) {
+                                       int64_t expected_per_user, void* stream) {
   NCF_CHECK_ARG(terms == 2 || terms == 3, "ncf_score_collect_split: terms must be 2 or 3");
   NCF_CHECK_ARG(dim == 64, "ncf_score_collect_split: dim must be 64");
   NCF_CHECK_ARG(n_users >= 0 && n_items >= 0 && n_items < (1ll << 31) && cap >= 1,
@@ -1265,7 +1265,22 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
   NCF_CHECK_ARG(ub < (1ll << 24), "ncf_score_collect_split: too many users per call");
   const int64_t max_splits = std::max<int64_t>(1, (n_items + 8 * kItemTile - 1) / (8 * kItemTile));
   const int64_t slots = (int64_t)n_cu * (8 / kNW3);   // resident workgroups (2 waves/SIMD)
-  int64_t splits = (4 * slots + ub - 1) / ub;
+  static int min_rounds = 0;   // NCF_SCORE3_ROUNDS: at least this many rounds (A/B knob)
+  if (min_rounds == 0) {
+    const char* e = getenv("NCF_SCORE3_ROUNDS");
+    min_rounds = e && atoi(e) > 0 ? atoi(e) : 4;
+  }
+  int64_t splits = (min_rounds * slots + ub - 1) / ub;
+  if (expected_per_user > 0) {
+    // enough item splits that a wave's share of its users' candidates (expected x 32 UB users /
+    // splits) stays under 3/4 of its LDS slice: a slice that fills inside the scan loop is
+    // written out one candidate at a time (k_collect3).  PMC writes per scan (MB), top-10 /
+    // top-100: 64 splits 329 / 1175, 128 splits 219 / 1045, 256 splits 298 / 622; scan time
+    // unchanged
+    const int64_t slice = terms == 3 ? slice3<3>() : slice3<2>();
+    const int64_t need = (expected_per_user * 32 * nub * 4 + 3 * slice - 1) / (3 * slice);
+    splits = std::max(splits, need);
+  }
   const int64_t rounds = (splits * ub + slots - 1) / slots;
   splits = std::max<int64_t>(1, rounds * slots / ub);
   if (splits > max_splits) splits = max_splits;

@@ -104,15 +104,16 @@ SPLIT_TERMS = int(os.environ.get("NCF_SCORE_TERMS", "2"))
 MARGIN_C = 1e-4   # >= the two-term scan's |logit error| / (|q| max|p|) (score.hip: ~6.1e-5)
 
 
-def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st):
-    """ncf_score_collect(_split) of n queried users over the index's items."""
+def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st, expected=0):
+    """ncf_score_collect(_split) of n queried users over the index's items (``expected``: the
+    candidates per user the thresholds aim at, which sizes the split scan's item split)."""
     I, D = idx.p.shape
     if idx.p3 is not None:
         terms = 2 if idx.pmax is not None else 3
         if terms == 2:   # lower the thresholds by the two-term scan's error bound first
             _lib.call("ncf_score_margin", q, rows, n, D, ptr(idx.pmax), MARGIN_C, thr, st)
         _lib.call("ncf_score_collect_split", q, rows, n, ptr(idx.p3), ptr(idx.bias), I, D, thr,
-                  cap, count, cand_l, cand_i, terms, st)
+                  cap, count, cand_l, cand_i, terms, int(expected), st)
     else:
         _lib.call("ncf_score_collect", q, rows, n, ptr(idx.p), ptr(idx.bias), I, D, thr, cap,
                   count, cand_l, cand_i, st)
@@ -188,8 +189,9 @@ class _TopKRun:
         _lib.call("ncf_score_kth", ptr(self.sample), n, self.S, k, None, self.stride,
                   ptr(self.thr), st)
         self.count.zero_()
+        # expected candidates per user: k x I / S (the threshold sample's k-th over S items)
         _collect(idx, ptr(self.q), None, n, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),
-                 ptr(self.cand_i), st)
+                 ptr(self.cand_i), st, expected=-(-k * I // self.S))
         _select(idx, None, n, self, k, ptr(self.scores), ptr(self.items), ptr(self.overflow), st)
 
     def redo_overflow(self, st):
