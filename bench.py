@@ -437,6 +437,12 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
     t0 = time.perf_counter()
     idx = ItemIndex(m, items=shard)
     torch.cuda.synchronize()
+    index_cold_ms = (time.perf_counter() - t0) * 1e3
+    # the rebuild a parameter change costs (GraphedScorer rebuilds on every model update): the
+    # first build above also pays first-use allocations and code-object loads
+    t0 = time.perf_counter()
+    idx = ItemIndex(m, items=shard)
+    torch.cuda.synchronize()
     index_ms = (time.perf_counter() - t0) * 1e3
 
     def timed(fn):
@@ -460,7 +466,8 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
                         if SPLIT_SCAN else "(fp32 MFMA)")
                      + ", hipGraph-captured"
                      + (f", item-sharded over {world} GPUs (all-gather + merge)" if world > 1 else ""),
-           "scaling": "strong", "n_gpus": world, "item_index_ms": round(index_ms, 3)}
+           "scaling": "strong", "n_gpus": world, "item_index_ms": round(index_ms, 3),
+           "item_index_first_build_ms": round(index_cold_ms, 3)}
     for k in ks:
         # the served form: the per-shard pipeline captured once as a hipGraph and replayed
         # (GraphedScorer); the eager launches are timed beside it with per-launch HIP events

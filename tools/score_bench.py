@@ -34,6 +34,18 @@ def main():
     idx = ItemIndex(m)
     torch.cuda.synchronize()
     print(f"item index ({a.items} items): {(time.perf_counter() - t0) * 1e3:.2f} ms", flush=True)
+    for _ in range(2):   # a rebuild after a parameter change (warm caches and workspaces)
+        _lib.PROFILE = []
+        t0 = time.perf_counter()
+        idx = ItemIndex(m)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        prof, _lib.PROFILE = _lib.PROFILE, None
+        per = {}
+        for name, _, e0, e1 in prof:
+            per[name] = per.get(name, 0.0) + e0.elapsed_time(e1)
+        print(f"item index rebuild: {dt * 1e3:.2f} ms  "
+              + " ".join(f"{n}={v:.2f}ms" for n, v in per.items()), flush=True)
     users = torch.randperm(a.num_users, device=dev)[:a.users]
     for k in a.k:
         score_topk(m, users, k, idx)
