@@ -390,10 +390,12 @@ __device__ __forceinline__ void ln_fwd(float* __restrict__ Y, int64_t row0, int 
 // Backward of dropout -> LayerNorm -> ReLU for the 80 rows, in place: G (dL/da) -> dL/dlin
 // (also to HBM); this workgroup's column sums [dbias | dgamma | dbeta] -> part[0 : 3N), through
 // the free buffer S (8 waves x 3N floats).
+// R: the layer's pre-LN rows r staged in LDS by stage_act (pitch kPQ, mean / rstd at columns
+// N, N + 1), or NULL to read them from HBM; S may overlap R (a barrier separates them).
 template <int N, int PG>
 __device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict__ S, int64_t row0,
                                        int rows, const ncf_mlp_layer& L, float p, uint64_t seed,
-                                       float* __restrict__ part) {
+                                       float* __restrict__ part, const float* R = nullptr) {
   constexpr int CH = N / 64;
   const int sub = threadIdx.x & 15;
   const int wv = threadIdx.x >> 6;
@@ -411,7 +413,8 @@ __device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict_
     if (rr >= kRows) break;
     const int64_t row = row0 + rr;
     const bool ok = rr < rows;
-    const float mu = ok ? L.mean[row] : 0.0f, rs = ok ? L.rstd[row] : 0.0f;
+    const float mu = ok ? (R ? R[rr * kPQ + N] : L.mean[row]) : 0.0f;
+    const float rs = ok ? (R ? R[rr * kPQ + N + 1] : L.rstd[row]) : 0.0f;
     float4 gd[CH], xh[CH];
     uint32_t pos = 0;   // ReLU mask: bit 4c + e <=> r > 0
     float s1 = 0.0f, s2 = 0.0f;
@@ -423,7 +426,8 @@ __device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict_
         const float4 k = ncf_dropout_scale4(seed, ((uint64_t)row * N + col) >> 2, p, inv_keep);
         d.x *= k.x; d.y *= k.y; d.z *= k.z; d.w *= k.w;
       }
-      const float4 x = ok ? ld4(L.r + row * N + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 x = !ok ? make_float4(0.f, 0.f, 0.f, 0.f)
+                           : R ? lds4(R + rr * kPQ + col) : ld4(L.r + row * N + col);
       const float4 gg = ld4(L.gamma + col);
       const float4 h = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
       pos |= ((x.x > 0.0f ? 1u : 0u) | (x.y > 0.0f ? 2u : 0u) | (x.z > 0.0f ? 4u : 0u) |
@@ -462,6 +466,7 @@ __device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict_
     NCF_R4(sb[c].x) NCF_R4(sb[c].y) NCF_R4(sb[c].z) NCF_R4(sb[c].w)
   }
 #undef NCF_R4
+  if (R) __syncthreads();   // every wave's reads of the stash are done before S overwrites it
   if ((threadIdx.x & 63) < 16) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
@@ -598,12 +603,21 @@ __device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const f
 // recomputed from r (act4's arithmetic: the same bits).  NCF_STAGE_BATCH = SB iterations' loads
 // issued before their uses (measured at C2, ms/step: SB 1 0.3075, 5 0.3100, 10 0.3087 — within
 // noise; the load-then-store loop's latency overlaps the other waves' work), default 1.
+// measured in-step (4 interleaved runs): k_mlp_bwd 90.3 us without, 92.4 us with the r1 stash
+// (the staging loop's extra LDS stores and the barrier before the column-sum scratch); off
+#ifndef NCF_MLP_STASH_R1
+#define NCF_MLP_STASH_R1 0
+#endif
+static_assert(128 + N1 + 2 <= kPQ, "the r1 stash fits Q's columns 128..257");
 #ifndef NCF_STAGE_BATCH
 #define NCF_STAGE_BATCH 1
 #endif
+// R (recompute only, L.a == NULL): also keep the loaded r rows and their mean / rstd in LDS
+// (pitch kPQ, statistics at columns K, K + 1) for the layer's LayerNorm backward.
 template <int K, int PX>
 __device__ __forceinline__ void stage_act(float* __restrict__ X, const ncf_mlp_layer& L,
-                                          int64_t row0, int rows, float p, uint64_t seed) {
+                                          int64_t row0, int rows, float p, uint64_t seed,
+                                          float* __restrict__ R = nullptr) {
   constexpr int TOT = kRows * (K / 4), IT = (TOT + kThreads - 1) / kThreads;
   constexpr int SB = NCF_STAGE_BATCH < IT ? NCF_STAGE_BATCH : IT;
   const float inv_keep = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
@@ -644,6 +658,13 @@ __device__ __forceinline__ void stage_act(float* __restrict__ X, const ncf_mlp_l
           }
         }
         lds4_st(X + r * PX + c, v);
+        if (R) {
+          lds4_st(R + r * kPQ + c, x[j]);
+          if (c == 0) {
+            R[r * kPQ + K] = mu[j];
+            R[r * kPQ + K + 1] = rs[j];
+          }
+        }
       }
     }
   }
@@ -828,8 +849,11 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
   NCF_STAMP(1, 1);
   ln_bwd<N2, kPQ>(Q, P, row0, rows, a.l[2], p, a.seed[2] + cs, pp);
   NCF_STAMP(1, 2);
+  // r1 kept in Q's columns 128..257 (free until stage a0; dlin2 uses columns 0..63) from the
+  // a1 staging to the LayerNorm backward of layer 1: one HBM read of r1 instead of two
+  float* R1 = (NCF_MLP_STASH_R1 && fused_wgrad && !a.l[1].a) ? Q + 128 : nullptr;
   if (fused_wgrad) {   // dW2 = dlin2^T a1 (a1 staged in P, then overwritten by dX)
-    stage_act<N1, kPP>(P, a.l[1], row0, rows, p, a.seed[1] + cs);
+    stage_act<N1, kPP>(P, a.l[1], row0, rows, p, a.seed[1] + cs, R1);
     __syncthreads();
     NCF_STAMP(1, 3);
     wgrad_layer<N2, N1, kPQ, kPP, BF>(Q, P, pp + T::kW2);
@@ -839,7 +863,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
   lin_bwd<N2, N1, kPQ, kPP, BF>(Q, P, a.l[2].w, a.l[2].ldw);
   __syncthreads();
   NCF_STAMP(1, 5);
-  ln_bwd<N1, kPP>(P, Q, row0, rows, a.l[1], p, a.seed[1] + cs, pp + 3 * N2);
+  ln_bwd<N1, kPP>(P, Q, row0, rows, a.l[1], p, a.seed[1] + cs, pp + 3 * N2, R1);
   NCF_STAMP(1, 6);
   if (fused_wgrad) {   // dW1 = dlin1^T a0
     stage_act<N0, kPQ>(Q, a.l[0], row0, rows, p, a.seed[0] + cs);
