@@ -1153,6 +1153,35 @@ def test_split_bf16_scan_equals_fp32_scan(k, cap):
             assert bool(((s_ - s1).abs()[diff] <= 1e-6).all())
 
 
+@pytest.mark.parametrize("k,terms", [(10, 2), (100, 2), (100, 3)])
+def test_split_scan_item_split_sizing_is_invisible(k, terms, monkeypatch):
+    """The split scan's item split raised from the expected candidates per user (k x I / S, the
+    `expected_per_user` argument of ncf_score_collect_split: fewer per-wave LDS slice overflows)
+    against the default split (expected 0): the same top-k items and the same score bits."""
+    from ncf_amd import scoring
+    from ncf_amd.scoring import ItemIndex, score_topk
+    torch.manual_seed(12)
+    U, I = 5000, 200003
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    users = torch.randperm(U)[:700]
+    idx = ItemIndex(m)
+    if terms == 3:
+        idx.pmax = None
+    s_sized, i_sized = score_topk(m, users, k=k, index=idx)
+    seen = []
+    collect = scoring._collect
+
+    def unsized(*a, expected=0):
+        seen.append(expected)
+        return collect(*a, expected=0)
+    monkeypatch.setattr(scoring, "_collect", unsized)
+    s0, i0 = score_topk(m, users, k=k, index=idx)
+    assert seen and max(seen) > 0, "the launch passes the expected candidates per user"
+    assert torch.equal(i_sized, i0)
+    assert torch.equal(s_sized, s0)
+
+
 @pytest.mark.parametrize("U,I,k,cap", [(40, 1003, 10, 8192), (40, 1003, 1, 8192), (20, 64, 64, 8192),
                                        (33, 4099, 37, 8192), (24, 50000, 100, 256)])
 def test_score_topk_small_catalogues(U, I, k, cap):
