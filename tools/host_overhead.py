@@ -20,6 +20,8 @@ from ncf_amd.trainer import FusedTrainStep  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--pipe", action="store_true", help="pipelined dedup (next=, the bench's form)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     U, I, B, M = 1_000_000, 100_000, 4096, 5
@@ -27,12 +29,17 @@ def main():
     model = ncf.AdvancedNCF(U, I, 10, 50).to(dev).train()
     step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5)
     batches = bench.make_batches(U, I, B, M, 8, dev, seed=5)
-    for s in range(5):
-        step(*batches[s % 8])
+    def one(s):
+        if a.pipe:
+            step(*batches[s % 8], next=batches[(s + 1) % 8][:2])
+        else:
+            step(*batches[s % 8])
+    for s in range(a.warmup):
+        one(s)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s in range(a.steps):
-        step(*batches[s % 8])
+    for s in range(a.warmup, a.warmup + a.steps):
+        one(s)
     t_host = time.perf_counter() - t0
     torch.cuda.synchronize()
     t_all = time.perf_counter() - t0
