@@ -462,7 +462,7 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
     out = {"config": f"{n_query} users x {n_items} items (model {n_users} x {n_items}, D=64), "
                      "top-K over the whole catalogue, factorised fp32-accurate MFMA scan "
                      + (f"(bf16 matrix cores, {SPLIT_TERMS}-term operand split"
-                        + (", candidates re-scored in fp32)" if SPLIT_TERMS == 2 else ")")
+                        + (", candidates re-scored in fp32)" if SPLIT_TERMS < 3 else ")")
                         if SPLIT_SCAN else "(fp32 MFMA)")
                      + ", hipGraph-captured"
                      + (f", item-sharded over {world} GPUs (all-gather + merge)" if world > 1 else ""),
@@ -491,9 +491,9 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
         coll = sum(e0.elapsed_time(e1) for name, _, e0, e1 in prof if name == kname)
         algo_tf = 2.0 * 64 * n_query * n_local / (coll * 1e-3) / 1e12   # 128 flop per pair
         if SPLIT_SCAN:
-            # executed matrix work: the bf16 products of the operand splits per pair (2 terms:
-            # a0b0 + a0b1 + a1b0; 3 terms: six)
-            nprod = 3 if SPLIT_TERMS == 2 else 6
+            # executed matrix work: the bf16 products of the operand splits per pair (1 term:
+            # a0b0; 2 terms: a0b0 + a0b1 + a1b0; 3 terms: six)
+            nprod = {1: 1, 2: 3, 3: 6}[SPLIT_TERMS]
             tf, peak = nprod * algo_tf, BF16_MFMA_PEAK_TFS
             kdesc = f"k_collect3 (v_mfma_f32_32x32x16_bf16, {nprod} split products per pair)"
         else:

@@ -18,11 +18,11 @@
 //                             bf16 terms; ncf_score_collect: the fp32 MFMA scan), appending
 //                             (logit, item) to the user's candidate list when logit >= threshold.
 //                             The candidate SET is a function of the threshold only, so any append
-//                             order gives the same result.  With two terms the scan's logits are
-//                             bounds (within E_u = c |q_u| max|p|): ncf_score_margin lowers the
-//                             thresholds by E_u first;
+//                             order gives the same result.  With one or two terms the scan's
+//                             logits are bounds (within E_u = c |q_u| max|p|, c = 8e-3 / 1e-4):
+//                             ncf_score_margin lowers the thresholds by E_u first;
 //   4. ncf_score_select(_rescored)  per user, radix select of the K-th candidate key in LDS, the K
-//                             winners sorted (after two-term scans: the candidates within 2 E_u of
+//                             winners sorted (after 1/2-term scans: the candidates within 2 E_u of
 //                             the scan's K-th re-scored in fp32 first); when a user's list
 //                             overflowed, the K-th best candidate seen is a higher valid threshold
 //                             and the host re-runs 3-4 for those users.
@@ -490,6 +490,11 @@ __global__ __launch_bounds__(512) void k_collect(
 // the accumulation only — far inside the threshold's 1e-4 relative margin (k_kth), so the
 // candidate set is unchanged.  6 bf16 MFMAs (32 cycles each) replace 32 fp32 ones (64 cycles)
 // per 32 x 32 x 64 tile.  The item rows are split once per index (k_split3: three bf16 planes).
+// T = 2 keeps a0 b0 + a0 b1 + a1 b0 (error ~6e-5 |q| max|p|), T = 1 only a0 b0 (bf16 keeps 8
+// significant bits: |a0 b0 - a b| <= (2^-7 + 2^-16) |a| |b|, so E = 8e-3 |q| max|p|): both
+// lower the thresholds by E and re-score the candidates near the K-th in fp32 (k_select<true>),
+// so the top-k do not depend on T.  One product per 32 x 32 x 16 step instead of three: the
+// scan went 3.6 -> 2.1 ms at 10K x 1M (it is then no longer MFMA-issue-bound).
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void split3(float x, __bf16& x0, __bf16& x1, __bf16& x2) {
@@ -806,10 +811,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       for (int t = 0; t < 4; ++t) {
         bf16x8_t b0, b1, b2;
         if constexpr (UB == 1) {
-          b0 = bq[t][0]; b1 = bq[t][1]; b2 = bq[t][T - 1];
+          b0 = bq[t][0]; b1 = bq[t][T > 1 ? 1 : 0]; b2 = bq[t][T - 1];
         } else {
           b0 = *reinterpret_cast<const bf16x8_t*>(&ps[bc][0][i][32 * h + 8 * t]);
-          b1 = *reinterpret_cast<const bf16x8_t*>(&ps[bc][1][i][32 * h + 8 * t]);
+          if constexpr (T >= 2)
+            b1 = *reinterpret_cast<const bf16x8_t*>(&ps[bc][1][i][32 * h + 8 * t]);
           if constexpr (T == 3)
             b2 = *reinterpret_cast<const bf16x8_t*>(&ps[bc][T - 1][i][32 * h + 8 * t]);
         }
@@ -817,8 +823,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
         for (int ub = 0; ub < UB; ++ub) {
           f32x16& c = acc[ub];
           c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b0, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b1, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[ub][t], b0, c, 0, 0, 0);
+          if constexpr (T >= 2) {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b1, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[ub][t], b0, c, 0, 0, 0);
+          }
           if constexpr (T == 3) {
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b2, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[ub][t], b1, c, 0, 0, 0);
@@ -1242,7 +1250,7 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
                                        const float* thr, int64_t cap, uint32_t* count,
                                        float* cand_logit, int32_t* cand_item, int terms,
                                        int64_t expected_per_user, void* stream) {
-  NCF_CHECK_ARG(terms == 2 || terms == 3, "ncf_score_collect_split: terms must be 2 or 3");
+  NCF_CHECK_ARG(terms >= 1 && terms <= 3, "ncf_score_collect_split: terms must be 1, 2 or 3");
   NCF_CHECK_ARG(dim == 64, "ncf_score_collect_split: dim must be 64");
   NCF_CHECK_ARG(n_users >= 0 && n_items >= 0 && n_items < (1ll << 31) && cap >= 1,
                 "ncf_score_collect_split: bad size");
@@ -1259,7 +1267,7 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
     else
       n_cu = 256;
   }
-  const int nub = terms == 2 ? kUB3 : kUB3t;
+  const int nub = terms == 3 ? kUB3t : kUB3;
   const int64_t upb = 32 * kNW3 * nub;   // users per workgroup
   const int64_t ub = (n_users + upb - 1) / upb;
   NCF_CHECK_ARG(ub < (1ll << 24), "ncf_score_collect_split: too many users per call");
@@ -1277,7 +1285,7 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
     // written out one candidate at a time (k_collect3).  PMC writes per scan (MB), top-10 /
     // top-100: 64 splits 329 / 1175, 128 splits 219 / 1045, 256 splits 298 / 622; scan time
     // unchanged
-    const int64_t slice = terms == 3 ? slice3<3>() : slice3<2>();
+    const int64_t slice = terms == 3 ? slice3<3>() : terms == 2 ? slice3<2>() : slice3<1>();
     const int64_t need = (expected_per_user * 32 * nub * 4 + 3 * slice - 1) / (3 * slice);
     splits = std::max(splits, need);
   }
@@ -1288,7 +1296,9 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
   per = (per + kItemTile - 1) / kItemTile * kItemTile;
   splits = (n_items + per - 1) / per;
   NCF_CHECK_ARG(splits * ub < (1ll << 31), "ncf_score_collect_split: grid too large");
-  const size_t dyn = (size_t)kNW3 * (terms == 3 ? slice3_bytes<kUB3t, 3>() : slice3_bytes<kUB3, 2>());
+  const size_t dyn = (size_t)kNW3 * (terms == 3   ? slice3_bytes<kUB3t, 3>()
+                                     : terms == 2 ? slice3_bytes<kUB3, 2>()
+                                                  : slice3_bytes<kUB3, 1>());
   static bool attr3 = false;
   if (!attr3) {
     const hipError_t e0 = hipFuncSetAttribute((const void*)k_collect3<kUB3t, kNW3, 3>,
@@ -1297,7 +1307,10 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
     const hipError_t e1 = hipFuncSetAttribute((const void*)k_collect3<kUB3, kNW3, 2>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)(kNW3 * slice3_bytes<kUB3, 2>()));
-    if (e0 != hipSuccess || e1 != hipSuccess) {
+    const hipError_t e2 = hipFuncSetAttribute((const void*)k_collect3<kUB3, kNW3, 1>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)(kNW3 * slice3_bytes<kUB3, 1>()));
+    if (e0 != hipSuccess || e1 != hipSuccess || e2 != hipSuccess) {
       ncf_set_error("ncf_score_collect_split: candidate slices need more LDS than allowed");
       return NCF_ERR_LAUNCH;
     }
@@ -1308,8 +1321,13 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
                        items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
                        cand_item);
-  else
+  else if (terms == 2)
     hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 2>), dim3((unsigned)(splits * ub)),
+                       dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
+                       items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
+                       cand_item);
+  else
+    hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 1>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
                        items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
                        cand_item);

@@ -76,11 +76,12 @@ class ItemIndex:
                   ptr(model.final[0].bias), ptr(model.mf_output.bias), ptr(self.bias), st)
         # the item rows as three bf16 planes for the split-operand MFMA scan (fp32 accuracy)
         self.p3 = None
-        self.pmax = None   # max_i |p_i| (float bits) for the two-term scan's threshold margin
+        self.pmax = None   # max_i |p_i| (float bits) for the 1/2-term scan's threshold margin
+        self.terms = SPLIT_TERMS   # operand terms of the split scan (with pmax; else 3)
         if SPLIT_SCAN:
             self.p3 = torch.empty(3, I, D, dtype=torch.int16, device=dev)
             _lib.call("ncf_score_split_items", ptr(self.p), I, D, ptr(self.p3), st)
-            if SPLIT_TERMS == 2:
+            if SPLIT_TERMS < 3:
                 self.pmax = torch.empty(1, dtype=torch.int32, device=dev)
                 _lib.call("ncf_score_item_norm_max", ptr(self.p), I, D, ptr(self.pmax), st)
         self.version = _param_version(model)
@@ -97,21 +98,35 @@ def _param_version(model):
 # the candidate scan on bf16 matrix cores with split operands (fp32 accuracy, same candidate
 # sets; NCF_SCORE_SPLIT=0: the fp32 MFMA scan)
 SPLIT_SCAN = os.environ.get("NCF_SCORE_SPLIT", "1") != "0"
-# terms per operand of the split scan: 2 (three products; the thresholds lowered by the scan's
-# error bound, the candidates re-scored in fp32: measured 4.8 / 7.1 ms at top-10 / top-100) or 3
-# (six products, fp32-accurate logits straight from the scan: 6.8 / 8.5 ms)
-SPLIT_TERMS = int(os.environ.get("NCF_SCORE_TERMS", "2"))
-MARGIN_C = 1e-4   # >= the two-term scan's |logit error| / (|q| max|p|) (score.hip: ~6.1e-5)
+# terms per operand of the split scan: 1 (one bf16 product per pair) or 2 (three products) — the
+# thresholds lowered by the scan's error bound, the candidates near the K-th re-scored in fp32, so
+# the top-k are the same bits either way (tested) — or 3 (six products, fp32-accurate logits
+# straight from the scan).  Measured (10K users x 1M items, ms, top-10 / top-100): 1 term
+# 2.85 / 4.29 (scan 2.06 / 2.42), 2 terms 4.75 / 5.76 (scan 3.67 / 3.82), 3 terms 6.8 / 8.5
+SPLIT_TERMS = int(os.environ.get("NCF_SCORE_TERMS", "1"))
+if SPLIT_TERMS not in (1, 2, 3):
+    raise ValueError("NCF_SCORE_TERMS must be 1, 2 or 3")
+# >= the scan's |logit error| / (|q|_2 max_i |p_i|_2) (Cauchy-Schwarz over the per-term errors),
+# with the fp32 accumulation and the fp32 re-scoring's own rounding: two terms (the dropped
+# products ~2^-16 relative): ~6.1e-5; one term (bf16 keeps 8 significant bits: each operand
+# rounded within 2^-8 of itself, |a0 b0 - a b| <= (2^-7 + 2^-16) |a| |b|): 7.83e-3 + 2 x 64 x
+# 2^-24 = 7.84e-3
+MARGIN_C = {1: 8e-3, 2: 1e-4}
 
 
-def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st, expected=0):
+def _terms(idx):
+    return idx.terms if idx.pmax is not None else 3
+
+
+def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st, expected=0, terms=None):
     """ncf_score_collect(_split) of n queried users over the index's items (``expected``: the
-    candidates per user the thresholds aim at, which sizes the split scan's item split)."""
+    candidates per user the thresholds aim at, which sizes the split scan's item split;
+    ``terms``: the split scan's operand terms, default the index's)."""
     I, D = idx.p.shape
     if idx.p3 is not None:
-        terms = 2 if idx.pmax is not None else 3
-        if terms == 2:   # lower the thresholds by the two-term scan's error bound first
-            _lib.call("ncf_score_margin", q, rows, n, D, ptr(idx.pmax), MARGIN_C, thr, st)
+        terms = terms or _terms(idx)
+        if terms < 3:   # lower the thresholds by the scan's error bound first
+            _lib.call("ncf_score_margin", q, rows, n, D, ptr(idx.pmax), MARGIN_C[terms], thr, st)
         _lib.call("ncf_score_collect_split", q, rows, n, ptr(idx.p3), ptr(idx.bias), I, D, thr,
                   cap, count, cand_l, cand_i, terms, int(expected), st)
     else:
@@ -128,13 +143,14 @@ SAMPLE_CANDS = int(os.environ.get("NCF_SCORE_CANDS", "1024"))
 KTH_LDS_MAX = int(os.environ.get("NCF_SCORE_KTH_MAX", "38912"))   # <= score.hip kKthLdsMax
 
 
-def _select(idx, rows, n, run, k, out_s, out_i, overflow, st):
-    """ncf_score_select(_rescored) of n users' candidate lists (fp32 re-scoring after the
-    two-term scan)."""
+def _select(idx, rows, n, run, k, out_s, out_i, overflow, st, terms=None):
+    """ncf_score_select(_rescored) of n users' candidate lists (fp32 re-scoring after a one- or
+    two-term scan; ``terms`` as the scan's)."""
     if idx.pmax is not None:
         _lib.call("ncf_score_select_rescored", rows, n, ptr(run.count), ptr(run.cand_l),
                   ptr(run.cand_i), run.cap, k, ptr(run.q), ptr(idx.p), ptr(idx.bias),
-                  idx.p.shape[1], ptr(idx.pmax), MARGIN_C, out_s, out_i, ptr(run.thr), overflow,
+                  idx.p.shape[1], ptr(idx.pmax), MARGIN_C[terms or _terms(idx)], out_s, out_i,
+                  ptr(run.thr), overflow,
                   st)
     else:
         _lib.call("ncf_score_select", rows, n, ptr(run.count), ptr(run.cand_l), ptr(run.cand_i),
@@ -202,6 +218,10 @@ class _TopKRun:
         I, D = p.shape
         dev = p.device
         overflow = self.overflow[:self.n]
+        # the re-runs scan with at least two terms: their thresholds (the K-th re-scored logit
+        # seen) sit just below the K-th, and the one-term scan's margin (~8e-3 |q| max|p|) could
+        # keep more than cap items above the lowered threshold
+        terms = max(2, _terms(idx))
         for _ in range(32):
             redo = torch.nonzero(overflow).flatten()
             if redo.numel() == 0:
@@ -212,8 +232,9 @@ class _TopKRun:
             sub_i = torch.empty(rows.numel(), k, dtype=torch.int64, device=dev)
             sub_o = torch.empty(rows.numel(), dtype=torch.int32, device=dev)
             _collect(idx, ptr(self.q), ptr(rows), rows.numel(), ptr(self.thr), cap,
-                     ptr(self.count), ptr(self.cand_l), ptr(self.cand_i), st)
-            _select(idx, ptr(rows), rows.numel(), self, k, ptr(sub_s), ptr(sub_i), ptr(sub_o), st)
+                     ptr(self.count), ptr(self.cand_l), ptr(self.cand_i), st, terms=terms)
+            _select(idx, ptr(rows), rows.numel(), self, k, ptr(sub_s), ptr(sub_i), ptr(sub_o), st,
+                    terms=terms)
             self.scores[redo] = sub_s
             self.items[redo] = sub_i
             overflow.zero_()

@@ -1139,7 +1139,7 @@ def test_split_bf16_scan_equals_fp32_scan(k, cap):
     m.eval()
     users = torch.randperm(U)[:700]
     idx = ItemIndex(m)
-    assert idx.p3 is not None and idx.pmax is not None, "two-term split scan is the default"
+    assert idx.p3 is not None and idx.pmax is not None, "a re-scored split scan is the default"
     s2, i2 = score_topk(m, users, k=k, index=idx, cap=cap)
     idx.pmax = None                    # same index, three-term scan (logits from the scan)
     s3, i3 = score_topk(m, users, k=k, index=idx, cap=cap)
@@ -1153,7 +1153,29 @@ def test_split_bf16_scan_equals_fp32_scan(k, cap):
             assert bool(((s_ - s1).abs()[diff] <= 1e-6).all())
 
 
-@pytest.mark.parametrize("k,terms", [(10, 2), (100, 2), (100, 3)])
+@pytest.mark.parametrize("k,cap", [(10, 8192), (100, 8192), (50, 256)])
+def test_one_term_scan_equals_two_term_scan(k, cap):
+    """The one-product bf16 scan (thresholds lowered by its 2^-8 error bound, every candidate
+    within 2E of the scan's K-th re-scored in fp32) against the default two-term scan on the same
+    index: both select on the same fp32 re-scored keys, so the top-k items and scores are
+    bit-identical; cap = 256 at k = 50 takes the overflow re-run."""
+    from ncf_amd.scoring import ItemIndex, score_topk
+    torch.manual_seed(13)
+    U, I = 5000, 100003
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    users = torch.randperm(U)[:700]
+    idx = ItemIndex(m)
+    assert idx.pmax is not None
+    idx.terms = 2
+    s2, i2 = score_topk(m, users, k=k, index=idx, cap=cap)
+    idx.terms = 1
+    s1, i1 = score_topk(m, users, k=k, index=idx, cap=cap)
+    assert torch.equal(i1, i2)
+    assert torch.equal(s1, s2)
+
+
+@pytest.mark.parametrize("k,terms", [(10, 2), (100, 2), (100, 3), (10, 1)])
 def test_split_scan_item_split_sizing_is_invisible(k, terms, monkeypatch):
     """The split scan's item split raised from the expected candidates per user (k x I / S, the
     `expected_per_user` argument of ncf_score_collect_split: fewer per-wave LDS slice overflows)
@@ -1168,13 +1190,15 @@ def test_split_scan_item_split_sizing_is_invisible(k, terms, monkeypatch):
     idx = ItemIndex(m)
     if terms == 3:
         idx.pmax = None
+    else:
+        idx.terms = terms
     s_sized, i_sized = score_topk(m, users, k=k, index=idx)
     seen = []
     collect = scoring._collect
 
-    def unsized(*a, expected=0):
+    def unsized(*a, expected=0, **kw):
         seen.append(expected)
-        return collect(*a, expected=0)
+        return collect(*a, expected=0, **kw)
     monkeypatch.setattr(scoring, "_collect", unsized)
     s0, i0 = score_topk(m, users, k=k, index=idx)
     assert seen and max(seen) > 0, "the launch passes the expected candidates per user"
