@@ -140,6 +140,8 @@ def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st, expected=0, t
 # kept within the k-th kernel's LDS-resident size (top-100: ~2570; a 30720-logit cap: 6.26 ms,
 # 38912: 5.90 ms), and never above cap / 2.
 SAMPLE_CANDS = int(os.environ.get("NCF_SCORE_CANDS", "1024"))
+# the split scan's item split raised from the expected candidates per user (A/B knob)
+SIZED_SPLIT = os.environ.get("NCF_SCORE_SIZED", "1") != "0"
 KTH_LDS_MAX = int(os.environ.get("NCF_SCORE_KTH_MAX", "38912"))   # <= score.hip kKthLdsMax
 
 
@@ -207,7 +209,7 @@ class _TopKRun:
         self.count.zero_()
         # expected candidates per user: k x I / S (the threshold sample's k-th over S items)
         _collect(idx, ptr(self.q), None, n, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),
-                 ptr(self.cand_i), st, expected=-(-k * I // self.S))
+                 ptr(self.cand_i), st, expected=-(-k * I // self.S) if SIZED_SPLIT else 0)
         _select(idx, None, n, self, k, ptr(self.scores), ptr(self.items), ptr(self.overflow), st)
 
     def redo_overflow(self, st):
