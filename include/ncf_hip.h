@@ -49,6 +49,11 @@ int ncf_device_count(void);
  * (this port's own plumbing: the reference runs one stream).  As entry points they are part of
  * a recorded launch sequence (launch tapes) and replay in order with it.     */
 int ncf_event_create(void** event);
+/* scope 0: as ncf_event_create (a system-scope release when recorded: host waits see every
+ * write before it); 1: a device-scope release (hipEventReleaseToDevice: enough for another
+ * stream of this device to wait on; no host reads behind it); 2: no fence of the event's own
+ * (hipEventDisableSystemFence: the preceding kernels' own releases only)                     */
+int ncf_event_create_scoped(void** event, int32_t scope);
 int ncf_event_destroy(void* event);
 int ncf_event_record(void* event, void* stream);
 int ncf_stream_wait_event(void* stream, void* event);

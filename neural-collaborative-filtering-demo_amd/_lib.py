@@ -34,6 +34,7 @@ SIGNATURES = {
     "ncf_version": (I32, []),
     "ncf_last_error": (ctypes.c_char_p, []),
     "ncf_event_create": (I32, [P]),
+    "ncf_event_create_scoped": (I32, [P, I32]),
     "ncf_event_destroy": (I32, [P]),
     "ncf_event_record": (I32, [P, P]),
     "ncf_stream_wait_event": (I32, [P, P]),
@@ -412,17 +413,30 @@ def tapes_available() -> bool:
     return _fast_mod is not None
 
 
+# release scope of the stream-to-stream events (RawEvent(stream_only=True): the fork / join
+# points of a step, never waited on by the host): 0 system, 1 device, 2 no fence of their own
+# (hipEventDisableSystemFence: visibility to the host and other devices is what it drops; the
+# waiting streams are on this device).  Each record on the step's main queue stalls it: C2
+# fused step 0.3089-0.3103 ms with 0, 0.3107-0.3136 with 1, 0.3038-0.3050 with 2 (r3av_*; the
+# GPU suite green under 1 and 2)
+STREAM_EVENT_SCOPE = int(os.environ.get("NCF_EVENT_SCOPE", "2"))
+
+
 class RawEvent:
     """A hipEvent_t (no timing) whose record / wait go through the C-ABI
     (ncf_event_record / ncf_stream_wait_event), so a launch tape holds them in order with the
-    kernels.  Created and destroyed outside any tape."""
-    __slots__ = ("h",)
+    kernels.  Created and destroyed outside any tape.  ``stream_only``: only other streams of
+    this device wait on it (no host wait, no host read behind it), so its record needs no
+    system-scope release (STREAM_EVENT_SCOPE)."""
+    __slots__ = ("h", "host_ok")
 
-    def __init__(self):
+    def __init__(self, stream_only: bool = False):
         lib = _lib if _lib is not None else load()
         out = ctypes.c_void_p()
-        check(lib.ncf_event_create(ctypes.byref(out)), "ncf_event_create")
+        scope = STREAM_EVENT_SCOPE if stream_only else 0
+        check(lib.ncf_event_create_scoped(ctypes.byref(out), scope), "ncf_event_create_scoped")
         self.h = out.value
+        self.host_ok = scope == 0
 
     def record(self, stream: int):
         call("ncf_event_record", self.h, stream)
@@ -433,6 +447,8 @@ class RawEvent:
 
     def synchronize(self):
         """Host wait (never part of a tape)."""
+        if not self.host_ok:
+            raise RuntimeError("RawEvent: a stream-only event has no host wait")
         check(_lib.ncf_event_synchronize(self.h), "ncf_event_synchronize")
 
     def __del__(self):

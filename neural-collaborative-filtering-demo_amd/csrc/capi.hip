@@ -36,6 +36,19 @@ extern "C" int ncf_event_create(void** event) {
   return NCF_OK;
 }
 
+extern "C" int ncf_event_create_scoped(void** event, int32_t scope) {
+  if (!event) { ncf_set_error("ncf_event_create_scoped: NULL out pointer"); return NCF_ERR_ARG; }
+  if (scope < 0 || scope > 2) { ncf_set_error("ncf_event_create_scoped: scope must be 0, 1 or 2"); return NCF_ERR_ARG; }
+  const unsigned flags = hipEventDisableTiming | (scope == 1   ? hipEventReleaseToDevice
+                                                  : scope == 2 ? hipEventDisableSystemFence
+                                                               : 0u);
+  hipEvent_t e = nullptr;
+  hipError_t r = hipEventCreateWithFlags(&e, flags);
+  if (r != hipSuccess) { ncf_set_error("hipEventCreateWithFlags: %s", hipGetErrorString(r)); return NCF_ERR_LAUNCH; }
+  *event = (void*)e;
+  return NCF_OK;
+}
+
 extern "C" int ncf_event_destroy(void* event) {
   if (!event) return NCF_OK;
   hipError_t r = hipEventDestroy((hipEvent_t)event);

@@ -286,7 +286,7 @@ class DeferredTableAdam:
         sorts forked beside the step use it too (one side stream instead of two)."""
         if self._side is None:
             self._side = torch.cuda.Stream(self.clock.device)
-            self._ev = (_lib.RawEvent(), _lib.RawEvent())
+            self._ev = (_lib.RawEvent(stream_only=True), _lib.RawEvent(stream_only=True))
         return self._side
 
     def sweep_join(self):
@@ -399,7 +399,7 @@ class DeferredTableAdam:
         if side is None or side.device != dev:
             side = self._dedup_side = (self.side_stream() if SHARE_SIDE and self.overlap
                                        else torch.cuda.Stream(dev))
-            self._dedup_evs = [_lib.RawEvent() for _ in range(2)]
+            self._dedup_evs = [_lib.RawEvent(stream_only=True) for _ in range(2)]
         cur = st
         self._dedup_evs[0].record(cur)
         self._dedup_evs[0].wait(side.cuda_stream)

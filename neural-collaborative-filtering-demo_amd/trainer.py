@@ -174,6 +174,15 @@ class FusedTrainStep:
         return w
 
     # ---- pipelined dedup: the id sort of step t+1 runs on a side stream under step t
+    def _event(self):
+        """The next of a ring of stream-to-stream events (the pipelined dedup's fork / join:
+        never waited on by the host; a wait is enqueued before its event is recorded again)."""
+        ring = getattr(self, "_evring", None)
+        if ring is None:
+            ring = self._evring = [[_lib.RawEvent(stream_only=True) for _ in range(8)], 0]
+        ring[1] = (ring[1] + 1) % len(ring[0])
+        return ring[0][ring[1]]
+
     def _dedup_sets(self, w):
         """Two sets of the dedup outputs (sorted segments, unique ids, counts) for workspace w:
         the workspace's own buffers and a twin, alternating between consecutive steps."""
@@ -197,14 +206,14 @@ class FusedTrainStep:
             self._side = (d.side_stream() if SHARE_SIDE and d is not None and d.overlap
                           else torch.cuda.Stream(eng.flat.device))
         side = self._side
-        side.wait_event(entry)
+        entry.wait(side.cuda_stream)
         u = uid.reshape(-1)
         i = iid.reshape(-1)
         _lib.call("ncf_dedup_ids", ptr(u), ptr(i), u.numel(), w.g.D, m.num_users,
                   m.num_products, ptr(s["uniq_u"]), ptr(s["uniq_i"]), None, None,
                   ptr(s["num_unique"]), ptr(s["emb_ws"]), s["emb_ws"].numel(), side.cuda_stream)
-        ev = torch.cuda.Event()
-        ev.record(side)
+        ev = self._event()
+        ev.record(side.cuda_stream)
         self._pending = (uid, iid, ev)          # the caller's objects: matched by identity
         if self.early and not self.bf16:
             # and, once this step's catch-up has locked its rows, the rows of the next batch
@@ -224,7 +233,7 @@ class FusedTrainStep:
         w.prededuped = None
         if pend is not None:
             cur = torch.cuda.current_stream(self.model.engine.flat.device)
-            cur.wait_event(pend[2])           # (also orders a stale prefetch before reuse)
+            pend[2].wait(cur.cuda_stream)     # (also orders a stale prefetch before reuse)
             if pend[0] is uid and pend[1] is iid:
                 w.prededuped = True
 
@@ -242,11 +251,12 @@ class FusedTrainStep:
                 eng = m.engine
                 eng.ensure_layout()
                 w0 = eng.workspace(user_ids.numel(), M, True)
-                entry = torch.cuda.Event()
-                entry.record()
                 self._activate_dedup(w0, user_ids, item_ids)
                 if next is not None and next[0].numel() == user_ids.numel():
                     if DEDUP_FORK == "entry":
+                        # (recorded only here: an event record costs the queue a few us)
+                        entry = self._event()
+                        entry.record(_lib.stream_ptr(eng.flat.device))
                         self._prefetch_dedup(w0, next[0], next[1], entry)
                     else:   # launched from the engine's fork point DEDUP_FORK of this step
                         pre = (w0, next[0], next[1])
@@ -254,8 +264,8 @@ class FusedTrainStep:
                         def hook(at, pre=pre):
                             if at == DEDUP_FORK and eng.fork_hook is hook:
                                 eng.fork_hook = None
-                                ev = torch.cuda.Event()
-                                ev.record()
+                                ev = self._event()
+                                ev.record(_lib.stream_ptr(eng.flat.device))
                                 self._prefetch_dedup(pre[0], pre[1], pre[2], ev)
                         eng.fork_hook = hook
             w = self._body(user_ids, item_ids, targets, M)
