@@ -29,7 +29,11 @@ log = logging.getLogger(__name__)
 # Measured at C2 with the rolling sweep forked at mlp_bwd (ms/step): entry 0.319-0.321, tower
 # 0.325, mlp_bwd 0.341, attn_bwd 0.312-0.314, emb_bwd 0.318-0.319, reduce 0.332-0.334: beside the
 # attention / embedding backward, after the sweep has taken the tower backward's idle slots.
-DEDUP_FORK = os.environ.get("NCF_DEDUP_FORK", "attn_bwd")
+# "sweep" (the default): queued behind the overlapped sweep on its stream when the sweep forks
+# this step (else at attn_bwd), joined by the sweep's own join: no event record or wait of its
+# own on the step's queue, where each costs ~5 us (0.2986-0.2992 against 0.3020-0.3040 ms/step
+# at attn_bwd, r3ax_*).
+DEDUP_FORK = os.environ.get("NCF_DEDUP_FORK", "sweep")
 
 
 class FusedTrainStep:
@@ -193,13 +197,22 @@ class FusedTrainStep:
             sets = w.cache["dedup_sets"] = [a, b, 0]
         return sets
 
-    def _prefetch_dedup(self, w, uid, iid, entry):
+    def _prefetch_dedup(self, w, uid, iid, entry, side=None):
         """Dedup of the NEXT step's ids into the idle set, on the side stream, after `entry`
-        (the start of this step: the run that last used that set is complete there)."""
+        (the start of this step: the run that last used that set is complete there).  With
+        ``side`` (and no entry): on that stream, already ordered after such a point."""
         sets = self._dedup_sets(w)
         s = sets[1 - sets[2]]
         eng = self.model.engine
         m = self.model
+        if side is not None:
+            self._enqueue_dedup(s, w, uid, iid, side)
+            # the sweep's done-event re-recorded behind the sort: the step's sweep join (before
+            # the clock advance) then orders the sort too, and the next step waits for nothing
+            d = self.deferred
+            d._ev[1].record(side.cuda_stream)
+            self._pending = (uid, iid, None)
+            return
         if getattr(self, "_side", None) is None:
             from .deferred import SHARE_SIDE
             d = self.deferred
@@ -207,6 +220,10 @@ class FusedTrainStep:
                           else torch.cuda.Stream(eng.flat.device))
         side = self._side
         entry.wait(side.cuda_stream)
+        self._enqueue_dedup(s, w, uid, iid, side)
+
+    def _enqueue_dedup(self, s, w, uid, iid, side):
+        m = self.model
         u = uid.reshape(-1)
         i = iid.reshape(-1)
         _lib.call("ncf_dedup_ids", ptr(u), ptr(i), u.numel(), w.g.D, m.num_users,
@@ -233,7 +250,10 @@ class FusedTrainStep:
         w.prededuped = None
         if pend is not None:
             cur = torch.cuda.current_stream(self.model.engine.flat.device)
-            pend[2].wait(cur.cuda_stream)     # (also orders a stale prefetch before reuse)
+            if pend[2] is None:               # sorted behind the sweep: joined with it
+                self.deferred.sweep_join()
+            else:
+                pend[2].wait(cur.cuda_stream)  # (also orders a stale prefetch before reuse)
             if pend[0] is uid and pend[1] is iid:
                 w.prededuped = True
 
@@ -262,7 +282,18 @@ class FusedTrainStep:
                         pre = (w0, next[0], next[1])
 
                         def hook(at, pre=pre):
-                            if at == DEDUP_FORK and eng.fork_hook is hook:
+                            if eng.fork_hook is not hook:
+                                return
+                            d = self.deferred
+                            if DEDUP_FORK == "sweep" and d.overlap and at in d.fork_points \
+                                    and not d._joined:
+                                # the overlapped sweep was just forked here: the sort queues
+                                # behind it on its stream, ordered by the sweep's own fork
+                                # (no event record of its own on the step's queue)
+                                eng.fork_hook = None
+                                self._prefetch_dedup(pre[0], pre[1], pre[2], None,
+                                                     side=d.side_stream())
+                            elif at == DEDUP_FORK or (DEDUP_FORK == "sweep" and at == "attn_bwd"):
                                 eng.fork_hook = None
                                 ev = self._event()
                                 ev.record(_lib.stream_ptr(eng.flat.device))
