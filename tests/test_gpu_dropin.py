@@ -367,3 +367,44 @@ def test_trainer_train_epoch_runs_reference_loop():
     ev = tr.validate([(kjt(u[::M].contiguous(), i[::M].contiguous()), t[::M].contiguous())
                       for (u, i, t) in batches(3, seed=19)])
     assert np.isfinite(ev["val_loss"]) and 0.0 <= ev["accuracy"] <= 1.0
+
+
+def test_trainer_train_epochs_checkpoints_and_resume(tmp_path):
+    """ModelTrainer.train (trainer.py:412-546 mirror): per-epoch history, checkpoint_epoch_{e}.pt
+    every epoch and best_model.pt on improvement; a second trainer pointed at the same directory
+    resumes from the latest checkpoint (trainer.py:448-451, _load_checkpoint returns epoch + 1),
+    runs only the remaining epochs and ends where the uninterrupted run ends; patience 0 stops
+    after the first epoch (trainer.py:515)."""
+    from ncf_amd.trainer import ModelTrainer
+    cfg = {"num_users": U, "num_products": I, "batch_size": B, "learning_rate": 1e-3,
+           "weight_decay": 1e-5}
+    loader = [(kjt(u, i), t) for u, i, t in batches(4, seed=31)]
+    val = [(kjt(u[::M].contiguous(), i[::M].contiguous()), t[::M].contiguous())
+           for (u, i, t) in batches(2, seed=32)]
+
+    full = ModelTrainer(model(seed=41), cfg)
+    h = full.train(loader, val, num_epochs=3, early_stopping_patience=10,
+                   checkpoint_dir=str(tmp_path / "a"))
+    assert len(h["train_loss"]) == len(h["val_loss"]) == len(h["learning_rate"]) == 3
+    assert all(np.isfinite(x) for x in h["train_loss"] + h["val_loss"])
+    assert h["train_loss"][2] < h["train_loss"][0]
+    for e in (1, 2, 3):
+        assert (tmp_path / "a" / f"checkpoint_epoch_{e}.pt").exists()
+    assert (tmp_path / "a" / "best_model.pt").exists()
+    ref = {k: v.detach().cpu().clone() for k, v in full.model.state_dict().items()}
+
+    first = ModelTrainer(model(seed=41), cfg)
+    first.train(loader, val, num_epochs=2, early_stopping_patience=10,
+                checkpoint_dir=str(tmp_path / "b"))
+    resumed = ModelTrainer(model(seed=42), cfg)       # other weights: the checkpoint replaces them
+    h2 = resumed.train(loader, val, num_epochs=3, early_stopping_patience=10,
+                       checkpoint_dir=str(tmp_path / "b"))
+    assert len(h2["train_loss"]) == 1
+    assert (tmp_path / "b" / "checkpoint_epoch_3.pt").exists()
+    got = resumed.model.state_dict()
+    for k in ref:
+        torch.testing.assert_close(got[k].cpu(), ref[k], rtol=0, atol=1e-6, msg=k)
+
+    stop = ModelTrainer(model(seed=43), cfg)
+    h3 = stop.train(loader, val, num_epochs=5, early_stopping_patience=0)
+    assert len(h3["train_loss"]) == 1
