@@ -58,6 +58,10 @@ int ncf_event_destroy(void* event);
 int ncf_event_record(void* event, void* stream);
 int ncf_stream_wait_event(void* stream, void* event);
 int ncf_event_synchronize(void* event);   /* host wait */
+/* stream-ordered write of a device word / wait until it equals `value` (hipStreamWriteValue32 /
+ * hipStreamWaitValue32): the overlapped sweep's join without an event (NCF_SWEEP_JOIN=value) */
+int ncf_stream_write_u32(void* stream, uint32_t* addr, uint32_t value);
+int ncf_stream_wait_u32(void* stream, uint32_t* addr, uint32_t value);
 /* stream-ordered hipMemcpyAsync (hipMemcpyDefault): the sharded step's count copies */
 int ncf_memcpy_async(void* dst, const void* src, int64_t bytes, void* stream);
 

@@ -39,6 +39,11 @@ CLAIM_CATCHUP = os.environ.get("NCF_CLAIM_CATCHUP", "1") != "0"
 CLAIM_SORT_AT = os.environ.get("NCF_CLAIM_SORT_AT", "forward")
 # the id sorts forked beside a step share the overlapped sweep's side stream (A/B)
 SHARE_SIDE = os.environ.get("NCF_SHARE_SIDE", "0") != "0"
+# NCF_JOIN_FLAG=1: the overlapped sweep's join as a device-word write on the side stream (issued
+# at the join, so it follows everything queued there: the sweep and the next batch's id sort)
+# and a stream wait on that word (hipStreamWriteValue32 / hipStreamWaitValue32), the word reset
+# behind the wait, instead of an event record + wait
+JOIN_FLAG = os.environ.get("NCF_JOIN_FLAG", "0") != "0"
 _SERIAL = itertools.count(1)      # distinguishes schedules in workspace caches (ids recycle)
 
 
@@ -99,6 +104,11 @@ class DeferredTableAdam:
         self._side = None
         self._ev = None
         self._joined = True
+        # (the join word is zeroed here, on the constructing stream, before any fork: a zero
+        # fill enqueued at the first join could land after the side stream's write and hang it)
+        self._flag = (torch.zeros(1, dtype=torch.int32, device=self.clock.device)
+                      if JOIN_FLAG and clock is not None else None)
+        self._flag_join = False
         # Early catch-up (clock path, set by FusedTrainStep(next=...) through request_early):
         # the NEXT batch's rows that this step does not touch are brought current through THIS
         # step (its zero-gradient update included) on a side stream, under this step's forward /
@@ -277,7 +287,12 @@ class DeferredTableAdam:
                 self._rolling(side, 0, part, len(self.fork_points))
         else:
             self._rolling(side, 0, part, len(self.fork_points))
-        self._ev[1].record(side)
+        # (the word's write / wait are not graph-capturable: a captured step joins by event)
+        self._flag_join = self._flag is not None and not torch.cuda.is_current_stream_capturing()
+        if self._flag_join:
+            self._sig_side = side
+        else:
+            self._ev[1].record(side)
         self._owed.remove(part)
         self._joined = False
 
@@ -289,11 +304,26 @@ class DeferredTableAdam:
             self._ev = (_lib.RawEvent(stream_only=True), _lib.RawEvent(stream_only=True))
         return self._side
 
+    def sweep_done(self, stream: int):
+        """The side stream's work queued so far (the sweep, then the next batch's sort behind
+        it) is what the step's sweep join waits for."""
+        if self._flag_join:
+            self._sig_side = stream
+        else:
+            self._ev[1].record(stream)
+
     def sweep_join(self):
         """The current stream waits for the side-stream sweep (before the step's apply and the
         clock advance that would change the sweep's target under it)."""
         if not self._joined:
-            self._ev[1].wait(_lib.stream_ptr(self.clock.device))
+            main = _lib.stream_ptr(self.clock.device)
+            if self._flag_join:
+                f = self._flag.data_ptr()
+                _lib.call("ncf_stream_write_u32", self._sig_side, f, 1)
+                _lib.call("ncf_stream_wait_u32", main, f, 1)
+                _lib.call("ncf_stream_write_u32", main, f, 0)
+            else:
+                self._ev[1].wait(main)
             self._joined = True
 
     def _settle(self, st):

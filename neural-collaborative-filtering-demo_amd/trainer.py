@@ -210,7 +210,7 @@ class FusedTrainStep:
             # the sweep's done-event re-recorded behind the sort: the step's sweep join (before
             # the clock advance) then orders the sort too, and the next step waits for nothing
             d = self.deferred
-            d._ev[1].record(side.cuda_stream)
+            d.sweep_done(side.cuda_stream)
             self._pending = (uid, iid, None)
             return
         if getattr(self, "_side", None) is None:
