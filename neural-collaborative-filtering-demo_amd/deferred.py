@@ -42,7 +42,8 @@ SHARE_SIDE = os.environ.get("NCF_SHARE_SIDE", "0") != "0"
 # NCF_JOIN_FLAG=1: the overlapped sweep's join as a device-word write on the side stream (issued
 # at the join, so it follows everything queued there: the sweep and the next batch's id sort)
 # and a stream wait on that word (hipStreamWriteValue32 / hipStreamWaitValue32), the word reset
-# behind the wait, instead of an event record + wait
+# behind the wait, instead of an event record + wait.  Measured slower (ROCm runs each as a blit
+# kernel, 4-7 us: fused step 0.306-0.315 vs 0.3035-0.3051 ms with the event join), so off
 JOIN_FLAG = os.environ.get("NCF_JOIN_FLAG", "0") != "0"
 _SERIAL = itertools.count(1)      # distinguishes schedules in workspace caches (ids recycle)
 
