@@ -71,6 +71,17 @@ def pmc_traffic(kernel):
 
 
 ISO_STEPS = 40   # steps of the roofline kernel's isolated (sweep not overlapped) measurement
+N_BATCHES = 256  # distinct resident batches the timed legs cycle through (not 8)
+# VALU issue of the deferred-Adam replay (tools/isa_replay_count.py on csrc/adam.hip, gfx950):
+# per zero-gradient element-step of the fp32 table-pair replay loop (D = 64): 4.94 plain VALU
+# (v_mul / v_fma(c) / v_mov), 1.63 packed (v_pk_fma / v_pk_mul: 2 lane-slots each), 2
+# transcendental (v_sqrt, v_rcp: quarter rate, 4 slots each) -> 16.19 lane issue slots.  D = 128
+# (C4): 1.25 plain + 3 packed + 2 transcendental -> 15.25.  Recount with the script after any
+# change to adam0 / the replay loop.
+ADAM_REPLAY_SLOTS = {64: 16.19, 128: 15.25}
+# chip VALU issue rate: 256 CUs x 4 SIMDs x 32 lanes per cycle x 2.4 GHz = 78.64 T lane-slots/s
+# (= the 157.3 TF fp32 vector peak with an FMA counted as 2 flops; MI355X_MICROARCH.md)
+VALU_SLOTS_PEAK_T = 78.64
 SWEEP_EVERY = 64  # the deferred table Adam's rolling-sweep period (FusedTrainStep / optim.py)
 
 
@@ -235,6 +246,29 @@ def cpu_baseline(model_sd, cfg, batches_cpu, budget_s):
                       f"{threads} threads on {cpu_model}"}
 
 
+def cpu_infer_baseline(model_sd, iu, ii, H, T, n_layers, budget_s):
+    """the C2 eval forward (M = 1) on the CPU oracle over the same N resident
+    pairs, full tables, every core this process may use; median of <= 5 calls within budget."""
+    from oracle import ncf_oracle as O
+    threads, cpu_model = host_cpu()
+    torch.set_num_threads(threads)
+    p = {k: v.detach().cpu() for k, v in model_sd.items()}
+    kw = dict(training=False, negative_samples=4, num_heads=H, temporal_dim=T, n_layers=n_layers)
+    with torch.no_grad():
+        O.forward(p, iu, ii, **kw)          # warm-up
+        times = []
+        t_all = time.perf_counter()
+        while len(times) < 5 and time.perf_counter() - t_all < budget_s:
+            t0 = time.perf_counter()
+            O.forward(p, iu, ii, **kw)
+            times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    return {"value": round(iu.numel() / med, 1), "unit": "pairs/s", "cores": threads,
+            "kind": "port", "cpu_model": cpu_model,
+            "sample": f"oracle eval forward over the same {iu.numel()} pairs (full 1M x 100K "
+                      f"tables, fp32), median of {len(times)} calls: {med * 1e3:.1f} ms"}
+
+
 def dropin_train(ncf, dev, cfg, batches, warmup, steps, prime=0):
     """The reference's own call pattern on the fused path (src/model/trainer.py:258-285):
     ``out = model(kjt); loss = nn.BCELoss()(out, t); optimizer.zero_grad(); loss.backward();
@@ -278,6 +312,44 @@ def dropin_train(ncf, dev, cfg, batches, warmup, steps, prime=0):
     run(prime + warmup + steps, n_item, item=True)
     torch.cuda.synchronize()
     dt_item = time.perf_counter() - t1
+    # per-phase breakdown (a separate region: host perf_counter around each call of the loop,
+    # and a torch event on the current stream at each phase boundary).  host_us: the Python
+    # call's duration; gpu_us: stream time from the phase's first enqueued work to its last
+    # (includes any wait of the stream for the host inside the phase)
+    phases = ("forward", "bce", "zero_grad", "backward", "step")
+    nb = min(steps, 50)
+    host = {k: 0.0 for k in phases}
+    evs = []
+    first = prime + warmup + steps + n_item
+    torch.cuda.synchronize()
+    for s_ in range(first, first + nb):
+        f, t = feats[s_ % len(feats)]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)]
+        e[0].record()
+        h0 = time.perf_counter()
+        out = m(f)
+        h1 = time.perf_counter()
+        e[1].record()
+        l_ = crit(out, t)
+        h2 = time.perf_counter()
+        e[2].record()
+        opt.zero_grad()
+        h3 = time.perf_counter()
+        e[3].record()
+        l_.backward()
+        h4 = time.perf_counter()
+        e[4].record()
+        opt.step()
+        h5 = time.perf_counter()
+        e[5].record()
+        for k, a, b in zip(phases, (h0, h1, h2, h3, h4), (h1, h2, h3, h4, h5)):
+            host[k] += b - a
+        evs.append(e)
+    torch.cuda.synchronize()
+    gpu = {k: sum(e[j].elapsed_time(e[j + 1]) for e in evs) / nb * 1e3
+           for j, k in enumerate(phases)}
+    breakdown = {k: {"host_us": round(host[k] / nb * 1e6, 1), "gpu_us": round(gpu[k], 1)}
+                 for k in phases}
     from ncf_amd import optim as _o
     b = _o.binding_of(opt, m)
     out = {"pattern": "model(kjt) -> nn.BCELoss -> zero_grad -> backward -> torch.optim.Adam.step "
@@ -291,7 +363,10 @@ def dropin_train(ncf, dev, cfg, batches, warmup, steps, prime=0):
            "final_loss": round(float(loss.detach()), 6),
            "with_loss_item": {"ms_per_step": round(dt_item / n_item * 1e3, 4),
                               "value": round(B * M * n_item / dt_item, 1), "steps": n_item,
-                              "note": "plus loss.item() every batch (trainer.py:289)"}}
+                              "note": "plus loss.item() every batch (trainer.py:289)"},
+           "phases": breakdown,
+           "phases_note": f"{nb} steps after the timed ones; host_us = the Python call, gpu_us = "
+                          "stream time between torch events at the phase boundaries"}
     del m, opt, feats
     torch.cuda.empty_cache()
     return out
@@ -530,6 +605,75 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
     return out
 
 
+CATCHUP_NAMES = ("ncf_adam_pairs_catchup_claim_clock", "ncf_adam_pairs_catchup_clock")
+
+
+def table_adam_accounting(step_fn, batches, first, n, dfr, D):
+    """The deferred table Adam's exact work over n steps, from the per-row stamps: before and
+    after each step (host syncs; a separate region, the sweep on the step's own stream) the
+    stamp arrays are read, so every row's replayed / applied steps are counted.  A touched row
+    (in the batch) takes (delta - 1) zero-gradient steps in the catch-up and one gradient step in
+    the apply; any other row whose stamp moved was replayed by the rolling sweep.  Each row step
+    is 2 D element-steps (the GMF and MLP tables of the kind).  Kernel times: HIP events around
+    each launch.  Returns {part: (element_steps per step, ms per step)}."""
+    from ncf_amd import _lib as L
+    es = {"catchup": 0, "apply": 0, "sweep": 0}
+    ms = {}
+    for s_ in range(first, first + n):
+        u, i, t = batches[s_ % len(batches)]
+        torch.cuda.synchronize()
+        s0 = {k: v.clone() for k, v in dfr.stamp.items()}
+        L.PROFILE = []
+        step_fn(u, i, t)
+        torch.cuda.synchronize()
+        prof, L.PROFILE = L.PROFILE, None
+        for name, _, e0, e1 in prof:
+            ms[name] = ms.get(name, 0.0) + e0.elapsed_time(e1)
+        for kind, ids in (("user", u), ("item", i)):
+            d = (dfr.stamp[kind] - s0[kind]).long()
+            touched = torch.zeros(d.numel(), dtype=torch.bool, device=d.device)
+            touched[ids.reshape(-1)] = True
+            es["apply"] += int(touched.sum())
+            es["catchup"] += int((d[touched] - 1).clamp_min(0).sum())
+            es["sweep"] += int(d[~touched].sum())
+        del s0
+    kms = {"catchup": sum(ms.get(k, 0.0) for k in CATCHUP_NAMES),
+           "apply": ms.get("ncf_adam_pairs_apply_clock", 0.0),
+           "sweep": ms.get("ncf_adam_pairs_sweep_rolling", 0.0)}
+    return {k: (es[k] * 2 * D / n, kms[k] / n) for k in es}
+
+
+def table_adam_roofline(acct, D):
+    """VALU-issue roofline of the replay kernels (catch-up, rolling sweep: zero-gradient
+    element-steps x ADAM_REPLAY_SLOTS lane issue slots each, against VALU_SLOTS_PEAK_T) and the
+    HBM roofline of the apply (per touched element: p, m, v read and written + the gradient
+    read = 28 B)."""
+    slots = ADAM_REPLAY_SLOTS[D]
+    out = {}
+    for k in ("catchup", "sweep"):
+        n_es, t_ms = acct[k]
+        a = n_es * slots / (t_ms * 1e-3) / 1e12 if t_ms > 0 else 0.0
+        out[k] = {"bound": "valu", "element_steps": int(n_es), "ms": round(t_ms, 4),
+                  "achieved": round(a, 2), "peak": VALU_SLOTS_PEAK_T, "unit": "T lane-slots/s",
+                  "frac": round(a / VALU_SLOTS_PEAK_T, 4)}
+    n_es, t_ms = acct["apply"]
+    gbs = n_es * 28.0 / (t_ms * 1e-3) / 1e9 if t_ms > 0 else 0.0
+    out["apply"] = {"bound": "hbm", "element_steps": int(n_es), "ms": round(t_ms, 4),
+                    "bytes": int(n_es * 28), "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    z_es = acct["catchup"][0] + acct["sweep"][0]
+    z_ms = acct["catchup"][1] + acct["sweep"][1]
+    a = z_es * slots / (z_ms * 1e-3) / 1e12 if z_ms > 0 else 0.0
+    out["replay"] = {"bound": "valu", "achieved": round(a, 2), "peak": VALU_SLOTS_PEAK_T,
+                     "unit": "T lane-slots/s", "frac": round(a / VALU_SLOTS_PEAK_T, 4),
+                     "element_steps": int(z_es), "ms": round(z_ms, 4),
+                     "slots_per_element_step": slots,
+                     "slots_source": "tools/isa_replay_count.py (gfx950 ISA of the replay loop: "
+                                     "plain VALU 1, packed 2, transcendental 4 slots)"}
+    out["element_steps_per_step"] = int(z_es + n_es)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -615,7 +759,7 @@ def main():
         model = model.to(dev).train()
         step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, graph=args.graph,
                               clock=False if args.no_clock else None)
-    batches = make_batches(U, I, B, M, 8, dev, seed=100 + rank)
+    batches = make_batches(U, I, B, M, N_BATCHES, dev, seed=100 + rank)
     torch.cuda.synchronize()
 
     # the single-GPU step sorts the next batch's ids on a side stream under the current step
@@ -649,6 +793,26 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_step = elapsed / args.steps * 1e3
+    # the same timed region cycling over 8 of the resident batches (the round-3 headline's
+    # reuse cycle, whose rows and Adam state fit the 256 MB Infinity Cache), reported beside
+    # the headline once
+    cyc8 = None
+    if not sharded:
+        b8 = batches[:8]
+        torch.cuda.synchronize()
+        t8 = time.perf_counter()
+        for s_ in range(args.steps):
+            u, i, t = b8[s_ % 8]
+            if pipelined:
+                step(u, i, t, next=b8[(s_ + 1) % 8][:2])
+            else:
+                step(u, i, t)
+        torch.cuda.synchronize()
+        dt8 = time.perf_counter() - t8
+        cyc8 = {"ms_per_step": round(dt8 / args.steps * 1e3, 4),
+                "value": round(N * args.steps / dt8, 1),
+                "note": "same step cycling over 8 resident batches (round 3's bench); the "
+                        f"headline cycles over {N_BATCHES} distinct batches"}
     samples_s = N * world * args.steps / elapsed
     last = step.ops.last_loss if sharded else step.last_loss
     loss = float(last.item()) if last is not None else float("nan")
@@ -724,6 +888,17 @@ def main():
                    "frac": round(iso_tf / FP32_MFMA_PEAK_TFS, 4), "steps": ISO_STEPS,
                    "note": "the same kernel with the rolling sweep on the step's own stream "
                            "(not overlapped)"}
+    adam_rf = None
+    if dfr0 is not None and getattr(dfr0, "clock", None) is not None and not sharded:
+        dfr0.flush(L.stream_ptr(dev))
+        ov = dfr0.overlap
+        dfr0.overlap = False
+        acct = table_adam_accounting(run, batches, prime + args.warmup + 2 * args.steps + ISO_STEPS,
+                                     8, dfr0, D)
+        dfr0.overlap = ov
+        adam_rf = table_adam_roofline(acct, D)
+        adam_rf["note"] = ("8 steps with the rolling sweep on the step's own stream, per-row "
+                           "stamps read before and after each (exact element-steps)")
     # table-update work of the deferred dense-exact Adam: algorithmic = the dense schedule's
     # 24 B per table element per step (what the reference's Adam must move), priced per step
     tab_ms = sum(totals.get(k, 0.0) for k in ("ncf_adam_rows_catchup", "ncf_adam_rows_apply",
@@ -732,6 +907,7 @@ def main():
                                                 "ncf_adam_rows_apply_clock",
                                                 "ncf_adam_sweep_rolling",
                                                 "ncf_adam_pairs_catchup_clock",
+                                                "ncf_adam_pairs_catchup_claim_clock",
                                                 "ncf_adam_pairs_apply_clock",
                                                 "ncf_adam_pairs_sweep_rolling"))
     tab_bytes = 2 * (U + I) * D * 24.0
@@ -793,6 +969,48 @@ def main():
         torch.cuda.synchronize()
         infer_s = (time.perf_counter() - ti) / reps
     infer_pairs = npairs * world / infer_s
+    # per-launch profile of the eval forward (HIP events around each C-ABI call)
+    L.PROFILE = []
+    with torch.no_grad():
+        for _ in range(reps):
+            eng.forward(iu, ii, 1, False, 0.0, 0)
+    torch.cuda.synchronize()
+    prof_i, L.PROFILE = L.PROFILE, None
+    inf_ms = {}
+    for name, _, e0, e1 in prof_i:
+        inf_ms[name] = inf_ms.get(name, 0.0) + e0.elapsed_time(e1) / reps
+    # algorithmic work per pair of the executed eval path (M = 1: softmax of one key is 1, so
+    # the attention output is out_proj(v_proj(x_item)); q / k projections are dead math and not
+    # executed): gather 4 D-float rows + 2 int64 ids in, 2 LN'd MLP rows + mf_pred out; the
+    # attention block 2 x 2 D^2 flop; the tower + head 2 (D h1 + h1 h2 + h2 h3) flop
+    inf_work = {"ncf_gather_ln_gmf_scaled_fwd": ("hbm", npairs * (16 * D + 16 + 8 * D + 4)),
+                "ncf_attn_block_fwd": ("mfma", npairs * 4.0 * D * D),
+                "ncf_mlp_fwd": ("mfma", npairs * mlp_f)}
+    inf_k = {}
+    for name, (bound, work) in inf_work.items():
+        if name in inf_ms:
+            t_ = inf_ms[name] * 1e-3
+            if bound == "hbm":
+                a = work / t_ / 1e9
+                inf_k[name] = {"bound": "hbm", "ms": round(inf_ms[name], 4), "bytes": int(work),
+                               "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(a / HBM_PEAK_GBS, 4)}
+            else:
+                a = work / t_ / 1e12
+                inf_k[name] = {"bound": "mfma", "ms": round(inf_ms[name], 4), "flops": work,
+                               "achieved": round(a, 2), "peak": FP32_MFMA_PEAK_TFS,
+                               "unit": "TFLOP/s", "frac": round(a / FP32_MFMA_PEAK_TFS, 4)}
+    inf_dom = max(inf_k, key=lambda k: inf_k[k]["ms"]) if inf_k else None
+    infer = {"pairs_per_s": round(infer_pairs, 1), "ms_per_call": round(infer_s * 1e3, 4),
+             "pairs_per_call": npairs,
+             "roofline": dict(inf_k[inf_dom], kernel=KERNEL_SYMBOL.get(inf_dom, inf_dom),
+                              entry_point=inf_dom) if inf_dom else None,
+             "kernels": inf_k,
+             "flops_per_pair": 4.0 * D * D + mlp_f,
+             "kernel_ms_per_call": {k: round(v, 4) for k, v in inf_ms.items()}}
+    if init_sd is not None:
+        infer["cpu_baseline"] = cpu_infer_baseline(init_sd, iu.cpu(), ii.cpu(), H, T,
+                                                   len(hid), args.cpu_budget)
 
     dropin = None
     if not sharded and not args.no_dropin:
@@ -885,12 +1103,16 @@ def main():
                            "steps_before_timing": prime + args.warmup,
                            "dense_equivalent_GBps": round(tab_bytes / max(tab_ms * 1e-3, 1e-12) / 1e9, 1),
                            "note": "dense schedule bytes (24 B x 140.8M elements) / time: above "
-                                   "HBM peak because untouched rows are caught up lazily"},
+                                   "HBM peak because untouched rows are caught up lazily",
+                           "roofline": adam_rf},
             "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(totals.items(), key=lambda x: -x[1])},
             "cpu_baseline": cpu,
             "dropin_train": dropin,
             "infer_pairs_per_s": round(infer_pairs, 1),
             "infer_config": f"eval forward (M=1), {npairs} resident (user,item) pairs per GPU",
+            "infer": infer,
+            "headline_8_batch_cycle": cyc8,
+            "resident_batches": N_BATCHES,
             "c5_scoring": score,
             "c2_bf16_tables": bf16,
             "c4_train": c4,

@@ -58,10 +58,6 @@ int ncf_event_destroy(void* event);
 int ncf_event_record(void* event, void* stream);
 int ncf_stream_wait_event(void* stream, void* event);
 int ncf_event_synchronize(void* event);   /* host wait */
-/* stream-ordered write of a device word / wait until it equals `value` (hipStreamWriteValue32 /
- * hipStreamWaitValue32): the overlapped sweep's join without an event (NCF_SWEEP_JOIN=value) */
-int ncf_stream_write_u32(void* stream, uint32_t* addr, uint32_t value);
-int ncf_stream_wait_u32(void* stream, uint32_t* addr, uint32_t value);
 /* stream-ordered hipMemcpyAsync (hipMemcpyDefault): the sharded step's count copies */
 int ncf_memcpy_async(void* dst, const void* src, int64_t bytes, void* stream);
 
@@ -683,15 +679,9 @@ int ncf_adam_pairs_catchup_clock(const ncf_table_pair* pairs, int npairs, int64_
                                  const ncf_step_clock* clock, const float* step_table,
                                  double beta1, double beta2, double eps, double weight_decay,
                                  void* stream);
-/* The same catch-up, marking every listed row in flight (stamp = target | NCF_STAMP_LOCK,
- * 0x40000000) until the step's ncf_adam_pairs_apply_clock writes its stamp: a catch-up of the
- * next batch's rows running meanwhile on another stream (target_rel one step further) skips them. */
+/* Stamps at or above NCF_STAMP_LOCK (0x40000000) compare above any target: the catch-up kernels
+ * leave such rows alone (reserved; no entry point sets it). */
 #define NCF_STAMP_LOCK 0x40000000
-int ncf_adam_pairs_catchup_lock_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
-                                      const uint32_t* count, int64_t max_n, int32_t target_rel,
-                                      const ncf_step_clock* clock, const float* step_table,
-                                      double beta1, double beta2, double eps, double weight_decay,
-                                      void* stream);
 /* The catch-up of the rows named by RAW id lists (ids0 for pairs[0], ids1 for pairs[1], n
  * occurrences each, duplicates allowed): the first occurrence of a row to raise its stamp to the
  * target (atomicMax) replays it, the others skip: the same rows, bit-identical, with no dedup

@@ -39,8 +39,6 @@ SIGNATURES = {
     "ncf_event_record": (I32, [P, P]),
     "ncf_stream_wait_event": (I32, [P, P]),
     "ncf_event_synchronize": (I32, [P]),
-    "ncf_stream_write_u32": (I32, [P, P, I32]),
-    "ncf_stream_wait_u32": (I32, [P, P, I32]),
     "ncf_memcpy_async": (I32, [P, P, I64, P]),
     "ncf_device_count": (I32, []),
     "ncf_gather_ln_gmf_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P, F32,
@@ -135,7 +133,6 @@ SIGNATURES = {
     "ncf_adam_sweep_rolling": (I32, [P, P, P, P, P, P, I64, I64, I32, I64, P, I32, P, P, F64, F64,
                                      F64, F64, P]),
     "ncf_adam_pairs_catchup_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
-    "ncf_adam_pairs_catchup_lock_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
     "ncf_adam_pairs_catchup_claim_clock": (I32, [P, I32, I64, P, P, I64, I32, P, P, F64, F64, F64,
                                                  F64, P]),
     "ncf_adam_pairs_apply_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
@@ -315,8 +312,7 @@ def _invoke(lib, name, args):
 
 
 # stream plumbing, not kernels: never bracketed by the instrumentation
-_NOT_TIMED = frozenset(("ncf_event_record", "ncf_stream_wait_event", "ncf_memcpy_async",
-                        "ncf_stream_write_u32", "ncf_stream_wait_u32"))
+_NOT_TIMED = frozenset(("ncf_event_record", "ncf_stream_wait_event", "ncf_memcpy_async"))
 
 
 def call(name: str, *args):

@@ -931,23 +931,6 @@ extern "C" int ncf_adam_flat_clock_close(float* param, const float* grad, float*
   return NCF_OK;
 }
 
-// the same catch-up, marking every listed row in flight (stamp = target | NCF_STAMP_LOCK) until
-// the step's ncf_adam_pairs_apply_clock: a catch-up of the NEXT batch's rows running
-// concurrently (another stream, target one step further) leaves them alone
-extern "C" int ncf_adam_pairs_catchup_lock_clock(const ncf_table_pair* pairs, int npairs,
-                                                 int64_t dim, const uint32_t* count, int64_t max_n,
-                                                 int32_t target_rel, const ncf_step_clock* clock,
-                                                 const float* step_table, double beta1,
-                                                 double beta2, double eps, double weight_decay,
-                                                 void* stream) {
-  NCF_CHECK_ARG(pairs && npairs >= 1 && npairs <= 2 && count && clock && step_table,
-                "ncf_adam_pairs_catchup_lock_clock: bad args");
-  if (max_n <= 0) return NCF_OK;
-  NCF_DISPATCH_DIM(dim, pairs_catchup_d, pair_args(pairs, npairs), npairs, count, max_n,
-                   target_rel, clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
-                   (hipStream_t)stream, 1);
-}
-
 extern "C" int ncf_adam_pairs_catchup_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
                                             const uint32_t* count, int64_t max_n,
                                             int32_t target_rel, const ncf_step_clock* clock,

@@ -70,22 +70,6 @@ extern "C" int ncf_stream_wait_event(void* stream, void* event) {
   return NCF_OK;
 }
 
-// Stream-ordered 32-bit flag write / wait (hipStreamWriteValue32 / hipStreamWaitValue32 on a
-// device word): a join of two streams without an event (NCF_SWEEP_JOIN=value, deferred.py).
-extern "C" int ncf_stream_write_u32(void* stream, uint32_t* addr, uint32_t value) {
-  if (!addr) { ncf_set_error("ncf_stream_write_u32: NULL address"); return NCF_ERR_ARG; }
-  hipError_t r = hipStreamWriteValue32((hipStream_t)stream, addr, value, 0);
-  if (r != hipSuccess) { ncf_set_error("hipStreamWriteValue32: %s", hipGetErrorString(r)); return NCF_ERR_LAUNCH; }
-  return NCF_OK;
-}
-
-extern "C" int ncf_stream_wait_u32(void* stream, uint32_t* addr, uint32_t value) {
-  if (!addr) { ncf_set_error("ncf_stream_wait_u32: NULL address"); return NCF_ERR_ARG; }
-  hipError_t r = hipStreamWaitValue32((hipStream_t)stream, addr, value, hipStreamWaitValueEq, 0xffffffffu);
-  if (r != hipSuccess) { ncf_set_error("hipStreamWaitValue32: %s", hipGetErrorString(r)); return NCF_ERR_LAUNCH; }
-  return NCF_OK;
-}
-
 // Host wait for an event (the row-sharded step's split sizes: RCCL takes them on the host).
 extern "C" int ncf_event_synchronize(void* event) {
   if (!event) { ncf_set_error("ncf_event_synchronize: NULL event"); return NCF_ERR_ARG; }

@@ -1273,11 +1273,7 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
   NCF_CHECK_ARG(ub < (1ll << 24), "ncf_score_collect_split: too many users per call");
   const int64_t max_splits = std::max<int64_t>(1, (n_items + 8 * kItemTile - 1) / (8 * kItemTile));
   const int64_t slots = (int64_t)n_cu * (8 / kNW3);   // resident workgroups (2 waves/SIMD)
-  static int min_rounds = 0;   // NCF_SCORE3_ROUNDS: at least this many rounds (A/B knob)
-  if (min_rounds == 0) {
-    const char* e = getenv("NCF_SCORE3_ROUNDS");
-    min_rounds = e && atoi(e) > 0 ? atoi(e) : 4;
-  }
+  const int min_rounds = 4;    // at least this many rounds of resident workgroups
   int64_t splits = (min_rounds * slots + ub - 1) / ub;
   if (expected_per_user > 0) {
     // enough item splits that a wave's share of its users' candidates (expected x 32 UB users /

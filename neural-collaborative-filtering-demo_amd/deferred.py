@@ -30,21 +30,10 @@ from ._lib import ptr
 
 _KINDS = (("user", "mf_user", "mlp_user"), ("item", "mf_item", "mlp_item"))
 # Catch-up by claim (no id sort before the forward) when the batch was not sorted ahead;
-# NCF_CLAIM_CATCHUP=0: sort inline, then catch up the unique rows (A/B)
+# NCF_CLAIM_CATCHUP=0: sort inline, then catch up the unique rows (A/B, tested equal).  The
+# claim path forks its id sort beside the forward (measured, drop-in step GPU-bound: 0.350-0.353
+# ms against 0.381-0.399 forked at a backward fork point; round 3)
 CLAIM_CATCHUP = os.environ.get("NCF_CLAIM_CATCHUP", "1") != "0"
-# where the claim path forks its id sort: beside the forward ("forward"), or at one of the
-# backward's fork points ("mlp_bwd", "attn_bwd", ...; engine._sweep_fork).  Drop-in step when
-# GPU-bound (ms): beside the forward 0.350-0.353, at the tower backward 0.393-0.399 (beside the
-# overlapped sweep), at the attention backward 0.381-0.389 (longer than that kernel)
-CLAIM_SORT_AT = os.environ.get("NCF_CLAIM_SORT_AT", "forward")
-# the id sorts forked beside a step share the overlapped sweep's side stream (A/B)
-SHARE_SIDE = os.environ.get("NCF_SHARE_SIDE", "0") != "0"
-# NCF_JOIN_FLAG=1: the overlapped sweep's join as a device-word write on the side stream (issued
-# at the join, so it follows everything queued there: the sweep and the next batch's id sort)
-# and a stream wait on that word (hipStreamWriteValue32 / hipStreamWaitValue32), the word reset
-# behind the wait, instead of an event record + wait.  Measured slower (ROCm runs each as a blit
-# kernel, 4-7 us: fused step 0.306-0.315 vs 0.3035-0.3051 ms with the event join), so off
-JOIN_FLAG = os.environ.get("NCF_JOIN_FLAG", "0") != "0"
 _SERIAL = itertools.count(1)      # distinguishes schedules in workspace caches (ids recycle)
 
 
@@ -89,35 +78,20 @@ class DeferredTableAdam:
             raise ValueError("the overlapped sweep needs the device step clock")
         # Where the engine forks it ("mlp_bwd": before the MLP tower backward; "mlp_bwd_after":
         # right after its launch (round 3: 0.337-0.344 vs 0.312 ms); "tower": before the tower
-        # forward; "attn_bwd", "emb_bwd", "reduce": before those backward launches)
-        # and where the step joins it ("apply": before the table apply; "close": before the
-        # step's last launch, which advances the clock the sweep reads).  Measured at C2 (one
-        # MI355X, ms/step): not overlapped 0.337; forked at tower 0.325, mlp_bwd 0.313-0.317,
-        # attn_bwd 0.327, emb_bwd 0.342, reduce 0.322-0.325 (join point: no difference).  The
+        # forward; "attn_bwd", "emb_bwd", "reduce": before those backward launches); the step
+        # joins it before the table apply (a join before the clock-advancing close measured the
+        # same, round 2).  Measured at C2 (one MI355X, ms/step): not overlapped 0.337; forked at
+        # tower 0.325, mlp_bwd 0.313-0.317, attn_bwd 0.327, emb_bwd 0.342, reduce 0.322-0.325.  The
         # VALU-bound replay fills the issue slots the latency-bound tower and attention
         # backward leave idle (it stretches k_mlp_bwd from 80 to ~92 us and itself from 50
         # to ~96 us, both off the critical path's sum).
         # Several comma-separated fork points split the slice into that many consecutive row
         # ranges, one launched at each (ncf_adam_pairs_sweep_rolling_part).
         self.fork_points = os.environ.get("NCF_SWEEP_FORK", "mlp_bwd").split(",")
-        self.join_at = os.environ.get("NCF_SWEEP_JOIN", "apply")
         self._owed = []           # parts of a closed step's rolling sweep not launched yet
         self._side = None
         self._ev = None
         self._joined = True
-        # (the join word is zeroed here, on the constructing stream, before any fork: a zero
-        # fill enqueued at the first join could land after the side stream's write and hang it)
-        self._flag = (torch.zeros(1, dtype=torch.int32, device=self.clock.device)
-                      if JOIN_FLAG and clock is not None else None)
-        self._flag_join = False
-        # Early catch-up (clock path, set by FusedTrainStep(next=...) through request_early):
-        # the NEXT batch's rows that this step does not touch are brought current through THIS
-        # step (its zero-gradient update included) on a side stream, under this step's forward /
-        # backward, instead of at the start of the next step.  This step's own rows are locked
-        # by its catch-up (stamp | NCF_STAMP_LOCK, cleared by its apply) so the early replay
-        # skips them; the step's rolling sweep waits for it.  Same replays, bit-identical.
-        self._early_req = None    # (side stream, ncf_table_pair[2] of the next rows, max_n)
-        self._early_ev = None
         engine.deferred = self
 
     # ---- per-step scalar table (index 4s .. 4s+3 = step s: gradient-step and zero-gradient-step
@@ -288,18 +262,12 @@ class DeferredTableAdam:
                 self._rolling(side, 0, part, len(self.fork_points))
         else:
             self._rolling(side, 0, part, len(self.fork_points))
-        # (the word's write / wait are not graph-capturable: a captured step joins by event)
-        self._flag_join = self._flag is not None and not torch.cuda.is_current_stream_capturing()
-        if self._flag_join:
-            self._sig_side = side
-        else:
-            self._ev[1].record(side)
+        self._ev[1].record(side)
         self._owed.remove(part)
         self._joined = False
 
     def side_stream(self):
-        """The overlapped sweep's stream (created on first use); with NCF_SHARE_SIDE the id
-        sorts forked beside the step use it too (one side stream instead of two)."""
+        """The overlapped sweep's stream (created on first use)."""
         if self._side is None:
             self._side = torch.cuda.Stream(self.clock.device)
             self._ev = (_lib.RawEvent(stream_only=True), _lib.RawEvent(stream_only=True))
@@ -308,23 +276,13 @@ class DeferredTableAdam:
     def sweep_done(self, stream: int):
         """The side stream's work queued so far (the sweep, then the next batch's sort behind
         it) is what the step's sweep join waits for."""
-        if self._flag_join:
-            self._sig_side = stream
-        else:
-            self._ev[1].record(stream)
+        self._ev[1].record(stream)
 
     def sweep_join(self):
         """The current stream waits for the side-stream sweep (before the step's apply and the
         clock advance that would change the sweep's target under it)."""
         if not self._joined:
-            main = _lib.stream_ptr(self.clock.device)
-            if self._flag_join:
-                f = self._flag.data_ptr()
-                _lib.call("ncf_stream_write_u32", self._sig_side, f, 1)
-                _lib.call("ncf_stream_wait_u32", main, f, 1)
-                _lib.call("ncf_stream_write_u32", main, f, 0)
-            else:
-                self._ev[1].wait(main)
+            self._ev[1].wait(_lib.stream_ptr(self.clock.device))
             self._joined = True
 
     def _settle(self, st):
@@ -360,7 +318,7 @@ class DeferredTableAdam:
         m = eng.model
         n = w.g.n
         if (CLAIM_CATCHUP and self.clock is not None and n > 0 and not getattr(w, "prededuped", None)
-                and self._early_req is None and not torch.cuda.is_current_stream_capturing()):
+                and not torch.cuda.is_current_stream_capturing()):
             self._prepare_claim(w, uid, iid, st)
             return
         if not getattr(w, "prededuped", None):   # else: sorted ahead on a side stream (trainer)
@@ -372,21 +330,9 @@ class DeferredTableAdam:
         if self.clock is not None and n > 0:   # both kinds in one launch
             self._ensure(self.t + 1)
             pairs = self._pairs_for(w)
-            req, self._early_req = self._early_req, None
-            _lib.call("ncf_adam_pairs_catchup_lock_clock" if req else
-                      "ncf_adam_pairs_catchup_clock", ctypes.addressof(pairs), 2,
+            _lib.call("ncf_adam_pairs_catchup_clock", ctypes.addressof(pairs), 2,
                       m.mlp_embedding_dim, ptr(w.num_unique), n, 0, ptr(self.clock),
                       ptr(self._table), *self._consts(), st)
-            if req:
-                side, npairs, ncount, nmax = req
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(self.clock.device))
-                side.wait_event(ev)
-                _lib.call("ncf_adam_pairs_catchup_clock", ctypes.addressof(npairs), 2,
-                          m.mlp_embedding_dim, ptr(ncount), nmax, 1, ptr(self.clock),
-                          ptr(self._table), *self._consts(), side.cuda_stream)
-                self._early_ev = torch.cuda.Event()
-                self._early_ev.record(side)
             return
         self.catchup_rows("user", w.uniq_u, w.num_unique, 0, n, st)
         self.catchup_rows("item", w.uniq_i, w.num_unique, 1, n, st)
@@ -413,10 +359,7 @@ class DeferredTableAdam:
         # uid / iid stay referenced until the engine joins the sort (w.dedup_refs): the caching
         # allocator cannot hand their memory to work the current stream queues before the join
         w.dedup_refs = (uid, iid)
-        if CLAIM_SORT_AT == "forward":
-            self.fork_claim_sort(w, st)
-        else:   # forked by the engine's backward at that fork point (engine._sweep_fork)
-            w.sort_pending = True
+        self.fork_claim_sort(w, st)
 
     def fork_claim_sort(self, w, st):
         """The id sort of a claim-path step (w.dedup_refs) on the side stream, after everything
@@ -424,12 +367,10 @@ class DeferredTableAdam:
         uid, iid = w.dedup_refs
         m = self.engine.model
         n = w.g.n
-        w.sort_pending = None
         dev = self.clock.device
         side = getattr(self, "_dedup_side", None)
         if side is None or side.device != dev:
-            side = self._dedup_side = (self.side_stream() if SHARE_SIDE and self.overlap
-                                       else torch.cuda.Stream(dev))
+            side = self._dedup_side = torch.cuda.Stream(dev)
             self._dedup_evs = [_lib.RawEvent(stream_only=True) for _ in range(2)]
         cur = st
         self._dedup_evs[0].record(cur)
@@ -440,32 +381,13 @@ class DeferredTableAdam:
         self._dedup_evs[1].record(side.cuda_stream)
         w.dedup_ev = self._dedup_evs[1]
 
-    def request_early(self, side, uniq_u, uniq_i, num_unique, n):
-        """Ask the next prepare() (this step's) to catch up the next batch's unique rows
-        (uniq_u / uniq_i, counts num_unique, from a dedup ordered on `side`) on `side`."""
-        key = ("early", self._serial, getattr(self, "_gen", 0), uniq_u.data_ptr(),
-               uniq_i.data_ptr())
-        cache = self.__dict__.setdefault("_early_pairs", {})
-        pairs = cache.get(key)
-        if pairs is None:
-            pairs = cache[key] = self._pairs()
-            pairs[0].row_ids, pairs[1].row_ids = ptr(uniq_u), ptr(uniq_i)
-        self._early_req = (side, pairs, num_unique, n)
-
-    def early_join(self):
-        if self._early_ev is not None:
-            torch.cuda.current_stream(self.clock.device).wait_event(self._early_ev)
-            self._early_ev = None
-
     # ---- after the backward: this step's gradient on the touched rows
     def apply(self, w, st):
         n = w.g.n
         if self.clock is not None:
             self._ensure(self.t + 1)
-            if self.join_at == "apply" or self._early_ev is not None:
-                self.sweep_join()
+            self.sweep_join()
             self._settle(st)
-            self.early_join()   # (before the sweep, which may reach the same rows)
             if n > 0:
                 pairs = self._pairs_for(w)
                 _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2,

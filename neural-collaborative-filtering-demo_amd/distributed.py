@@ -306,10 +306,13 @@ class ShardedTrainStep:
         # send the next step's rows to their owners during this step (env NCF_SHARD_AHEAD=0: off)
         self.ahead = ahead if ahead is not None else os.environ.get("NCF_SHARD_AHEAD", "1") != "0"
         # launch tapes (HIP ops + C-ABI collectives): the two launch segments of a step (split
-        # at the host wait for the next plan's sizes) recorded once per geometry and replayed
+        # at the host wait for the next plan's sizes) recorded once per geometry and replayed.
+        # World 1 only: a replay of recorded RCCL collectives at world > 1 has not run on
+        # hardware (no multi-GPU box here), so that path stays eager until one covers it
         from .tapes import SegmentTapes
         self.tapes = SegmentTapes() if (TAPE_SHARDED and isinstance(ops, HipShardOps)
-                                        and isinstance(exchange, RcclExchange)) else None
+                                        and isinstance(exchange, RcclExchange)
+                                        and exchange.world == 1) else None
 
     def plan(self, user_ids, item_ids):
         p = self.ops.plan(user_ids, item_ids, self.x.world)
@@ -317,7 +320,7 @@ class ShardedTrainStep:
         return p
 
     def __call__(self, user_ids, item_ids, targets, next=None):
-        if self.tapes is not None and self.tapes.usable(self.ops.deferred):
+        if self.tapes is not None and self.tapes.usable(self.ops.deferred, self.ops.eng):
             return self._call_taped(user_ids, item_ids, targets, next)
         ops, X = self.ops, self.x
         ops.mark_entry()          # ids of this call and of `next` exist from here on
@@ -474,7 +477,7 @@ class ShardedTrainStep:
     def _pre(self):
         ops = self.ops
         d = ops.deferred
-        return (tuple(d._owed), d._joined, ops.eng.pending is None, d._early_ev is None)
+        return (tuple(d._owed), d._joined, ops.eng.pending is None)
 
     def _post_a(self, state):
         """Host state segment A leaves: the deferred sweep's fork (None: capture it)."""

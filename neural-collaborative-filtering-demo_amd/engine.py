@@ -21,7 +21,6 @@ import torch
 
 from . import _lib
 from ._lib import ptr
-from .deferred import CLAIM_SORT_AT
 
 LN_EPS = 1e-5
 # bf16 configuration: the fused MLP tower's Linears on bf16 MFMA (NCF_BF16_MM=0: fp32 MFMA, A/B)
@@ -637,13 +636,10 @@ class NCFEngine:
     # ------------------------------------------------------------------ backward
     def _sweep_fork(self, at: str, w=None):
         """Launch the previous step's owed rolling sweep on its side stream when the overlapped
-        sweep is on and `at` is one of its fork points (DeferredTableAdam.fork_points); the
-        claim path's id sort of workspace w when `at` is its fork point (CLAIM_SORT_AT)."""
+        sweep is on and `at` is one of its fork points (DeferredTableAdam.fork_points)."""
         d = self.deferred
         if d is not None and d.overlap:
             d.sweep_fork(at)
-        if w is not None and getattr(w, "sort_pending", None) and at == CLAIM_SORT_AT:
-            d.fork_claim_sort(w, _lib.stream_ptr(w.prob.device))
         hook = self.fork_hook
         if hook is not None:
             hook(at)
@@ -779,8 +775,6 @@ class NCFEngine:
         uq_u, uq_i = uniq if uniq is not None else (w.uniq_u, w.uniq_i)
         d_rows = rows or (m.num_users, m.num_products)
         w.slots_set = False
-        if getattr(w, "sort_pending", None):   # its fork point not passed: fork it now
-            self.deferred.fork_claim_sort(w, st)
         ev = getattr(w, "dedup_ev", None)
         if ev is not None:   # the id sort forked beside the forward (deferred._prepare_claim)
             ev.wait(st)

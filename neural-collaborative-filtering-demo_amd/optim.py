@@ -257,6 +257,7 @@ class _Binding:
                 s_ = _lib.stream_ptr(dev)     # (the current stream: a capture's, under one)
                 d.apply(w, s_)
                 eng.pending = None
+                d.sweep_join()        # (the clock advance below changes the sweep's target)
                 _lib.call("ncf_adam_flat_clock_close", ptr(eng.flat), ptr(eng.flat_grad),
                           ptr(self.m_flat), ptr(self.v_flat), eng.flat.numel(), ptr(d._table), 1,
                           ptr(self.clock), b1, b2, eps, wd, self.base_seed, s_)
@@ -285,6 +286,7 @@ class _Binding:
         tables_stepped = d is not None and (clocked or bool(table_grads))
         if all_dense and self.uniform and clocked:
             # the step's dense Adam + the clock advance in one launch (as FusedTrainStep)
+            d.sweep_join()
             _lib.call("ncf_adam_flat_clock_close", ptr(eng.flat), ptr(eng.flat_grad),
                       ptr(self.m_flat), ptr(self.v_flat), eng.flat.numel(), ptr(d._table), 1,
                       ptr(self.clock), b1, b2, eps, wd, self.base_seed, st)

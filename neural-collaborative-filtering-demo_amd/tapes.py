@@ -34,7 +34,7 @@ RECORD_AFTER = 2          # consecutive eager steps of one geometry before its t
 
 class _Entry:
     __slots__ = ("w", "fwd", "bwd", "step", "fwd_pre", "bwd_pre", "step_pre", "bwd_post",
-                 "step_post", "dedup_ev", "sort_pending")
+                 "step_post", "dedup_ev")
 
     def __init__(self):
         for k in self.__slots__:
@@ -65,7 +65,7 @@ class StepTapes:
         if light:
             return head[:light]
         tb = eng.table_params()
-        return head + (d._serial, getattr(d, "_gen", 0), tuple(d.fork_points), d.join_at,
+        return head + (d._serial, getattr(d, "_gen", 0), tuple(d.fork_points),
                        d.overlap, d.sweep_every, tuple(p.data_ptr() for p in tb.values()),
                        tuple(s["exp_avg"].data_ptr() for s in d.state.values()),
                        eng.clock.data_ptr(), eng.err_flag(eng.flat.device).data_ptr())
@@ -75,8 +75,7 @@ class StepTapes:
         d = eng.deferred
         return (ENABLED and d is not None and d.clock is not None and eng.clock is d.clock
                 and not d.bf16 and eng.fork_hook is None and eng.timing is None
-                and not eng.concurrent and _lib.PROFILE is None and d._early_req is None
-                and d._early_ev is None and _lib.tapes_available()
+                and not eng.concurrent and _lib.PROFILE is None and _lib.tapes_available()
                 and not torch.cuda.is_current_stream_capturing())
 
     def _horizon(self):
@@ -105,8 +104,7 @@ class StepTapes:
     def _fwd_pre(self, w):
         eng = self.eng
         return (w is not None and eng.ws.get((w.g.n, w.g.M, True)) is w, eng.pending is None,
-                w is not None and getattr(w, "dedup_ev", None) is None
-                and not getattr(w, "sort_pending", None),
+                w is not None and getattr(w, "dedup_ev", None) is None,
                 w is not None and not getattr(w, "prededuped", None))
 
     def forward(self, uid, iid, M, drop_p, seed):
@@ -134,7 +132,7 @@ class StepTapes:
             e.fwd.replay((uid.data_ptr(), iid.data_ptr(), st))
             # host state as the recorded code leaves it (deferred._prepare_claim)
             w.deduped, w.prededuped = True, None
-            w.dedup_ev, w.dedup_refs, w.sort_pending = e.dedup_ev, (uid, iid), e.sort_pending
+            w.dedup_ev, w.dedup_refs = e.dedup_ev, (uid, iid)
             self.replays += 1
             return w
         # record: the forward runs for real while the tape holds its calls
@@ -145,10 +143,8 @@ class StepTapes:
         tape = _lib.LaunchTape()
         with tape.record((uid.data_ptr(), 8 * n, iid.data_ptr(), 8 * n, st, 1)):
             w = eng.forward(uid, iid, M, True, drop_p, seed, prepare=eng.deferred.prepare)
-        if tape.valid and w is w0 and getattr(w, "deduped", False) and (
-                w.dedup_ev is not None or getattr(w, "sort_pending", None)):
+        if tape.valid and w is w0 and getattr(w, "deduped", False) and w.dedup_ev is not None:
             e.w, e.fwd, e.fwd_pre, e.dedup_ev = w, tape, pre, w.dedup_ev
-            e.sort_pending = getattr(w, "sort_pending", None)
             e.bwd = e.step = None     # recorded against this forward's host state
             self.recorded += 1
         return w
@@ -158,7 +154,6 @@ class StepTapes:
         eng = self.eng
         d = eng.deferred
         return (w is e.w, eng.pending is None, getattr(w, "dedup_ev", None) is e.dedup_ev,
-                bool(getattr(w, "sort_pending", None)) == bool(e.sort_pending),
                 tuple(d._owed), d._joined, eng._zero_cols_of is eng.flat_grad,
                 not getattr(eng, "_red_pending", False))
 
@@ -189,7 +184,7 @@ class StepTapes:
             owed, joined = e.bwd_post
             d._owed, d._joined = list(owed), joined
             w.slots_set = False
-            w.dedup_ev = w.dedup_refs = w.sort_pending = None
+            w.dedup_ev = w.dedup_refs = None
             w.red_list.count = 0
             eng.pending = w
             self.replays += 1
@@ -265,10 +260,13 @@ class SegmentTapes:
         self.recorded = 0
         self._skip = False
 
-    def usable(self, d) -> bool:
+    def usable(self, d, eng) -> bool:
+        """The same guards as StepTapes.usable: a tape sees only C-ABI calls, so torch-side
+        cross-stream ordering (engine.fork / join, a fork hook) and instrumentation rule it out."""
         self._skip = False
         return (ENABLED and d is not None and d.clock is not None and not d.bf16
-                and _lib.PROFILE is None and d._early_req is None and _lib.tapes_available()
+                and not eng.concurrent and eng.fork_hook is None and eng.timing is None
+                and _lib.PROFILE is None and _lib.tapes_available()
                 and not torch.cuda.is_current_stream_capturing())
 
     def skip(self):

@@ -82,11 +82,6 @@ class FusedTrainStep:
         self.v_flat = torch.zeros_like(eng.flat)
         self.last_loss = None
         self.graph = bool(graph)
-        # with next=..., the next batch's rows untouched by this step can be caught up under
-        # this step on the side stream (DeferredTableAdam.request_early; NCF_EARLY_CATCHUP=1).
-        # Off by default: measured at C2 it moves ~5 us of catch-up off the critical path but
-        # slows the attention / tower kernels it shares the CUs with by more (0.337 -> 0.350 ms)
-        self.early = os.environ.get("NCF_EARLY_CATCHUP", "0") != "0"
         # the device step clock is the default whenever the deferred schedule is on (both kinds
         # per launch, no host step arguments; bit-identical to the host-driven form)
         self.use_clock = (self.graph or deferred) if clock is None else bool(clock)
@@ -214,10 +209,7 @@ class FusedTrainStep:
             self._pending = (uid, iid, None)
             return
         if getattr(self, "_side", None) is None:
-            from .deferred import SHARE_SIDE
-            d = self.deferred
-            self._side = (d.side_stream() if SHARE_SIDE and d is not None and d.overlap
-                          else torch.cuda.Stream(eng.flat.device))
+            self._side = torch.cuda.Stream(eng.flat.device)
         side = self._side
         entry.wait(side.cuda_stream)
         self._enqueue_dedup(s, w, uid, iid, side)
@@ -232,11 +224,6 @@ class FusedTrainStep:
         ev = self._event()
         ev.record(side.cuda_stream)
         self._pending = (uid, iid, ev)          # the caller's objects: matched by identity
-        if self.early and not self.bf16:
-            # and, once this step's catch-up has locked its rows, the rows of the next batch
-            # that this step does not touch are brought current on the same side stream
-            self.deferred.request_early(side, s["uniq_u"], s["uniq_i"], s["num_unique"],
-                                        u.numel())
 
     def _activate_dedup(self, w, uid, iid):
         """Point w at this step's dedup set: the prefetched one when it was made for these ids

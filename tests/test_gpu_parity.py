@@ -767,54 +767,18 @@ def test_pipelined_dedup_bitwise_equals_inline():
         assert torch.equal(out[0][k], out[1][k]), k
 
 
-@pytest.mark.parametrize("sweep_every", [8, 64])
-def test_early_catchup_bitwise_equals_dense(monkeypatch, sweep_every):
-    """FusedTrainStep(next=...) with the early catch-up (the next batch's rows untouched by the
-    current step replayed through it on the side stream while the step's own rows are locked)
-    over 70 steps, small and default sweep slices, items drawn from few rows so consecutive
-    batches overlap heavily: parameters and Adam moments bit-identical to the dense sweep."""
-    from ncf_amd.trainer import FusedTrainStep
-    monkeypatch.setenv("NCF_EARLY_CATCHUP", "1")
-    a_sd, a_m = _fused_run(False, 70, sweep_every=sweep_every, I=120)
-    torch.manual_seed(11)
-    U, I, B = 3000, 120, 64
-    m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.0, 4).to(DEV)
-    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5, sweep_every=sweep_every)
-    assert step.early
-    g = torch.Generator().manual_seed(12)
-    batches = []
-    for _ in range(70):
-        u = torch.randint(0, U, (B,), generator=g).repeat_interleave(5).to(DEV)
-        i = torch.randint(0, I, (B * 5,), generator=g).to(DEV)
-        t = torch.zeros(B, 5)
-        t[:, 0] = 1
-        batches.append((u, i, t.reshape(-1, 1).to(DEV)))
-    for s_, (u, i, t) in enumerate(batches):
-        step(u, i, t, next=batches[s_ + 1][:2] if s_ + 1 < len(batches) else None)
-    b_sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
-    step.sync()
-    b_m = {k: (v["exp_avg"].cpu().clone(), v["exp_avg_sq"].cpu().clone()) for k, v in step.state.items()}
-    for k in a_sd:
-        assert torch.equal(a_sd[k], b_sd[k]), k
-    for k in a_m:
-        assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
-    st = step.deferred.stamp
-    assert int(max(st["user"].max(), st["item"].max())) < (1 << 30)   # no lock left behind
-
-
-@pytest.mark.parametrize("graph,fork,join", [(False, "mlp_bwd", "apply"), (True, "mlp_bwd", "apply"),
-                                             (False, "tower,mlp_bwd,reduce", "close"),
-                                             (True, "tower,attn_bwd", "apply"),
-                                             (False, "emb_bwd,nowhere", "apply"),
-                                             (False, "off", "apply")])
-def test_overlapped_sweep_bitwise_equals_dense(monkeypatch, graph, fork, join):
+@pytest.mark.parametrize("graph,fork", [(False, "mlp_bwd"), (True, "mlp_bwd"),
+                                        (False, "tower,mlp_bwd,reduce"),
+                                        (True, "tower,attn_bwd"),
+                                        (False, "emb_bwd,nowhere"),
+                                        (False, "off")])
+def test_overlapped_sweep_bitwise_equals_dense(monkeypatch, graph, fork):
     """The overlapped rolling sweep (side stream; the default fork point is the tower
     backward, joined before the apply; or split into consecutive parts forked at several points
     (ncf_adam_pairs_sweep_rolling_part), a part whose fork point the step never passes settled
-    before the apply; or joined only before the clock advance) is bit-identical to the dense
-    sweep, eager and hipGraph-captured ("off": the sweep on the step's own stream)."""
+    before the apply) is bit-identical to the dense sweep, eager and hipGraph-captured ("off":
+    the sweep on the step's own stream)."""
     monkeypatch.setenv("NCF_SWEEP_FORK", fork)
-    monkeypatch.setenv("NCF_SWEEP_JOIN", join)
     a_sd, a_m = _fused_run(False, 70)
     b_sd, b_m = _fused_run(True, 70, clock=True, graph=graph, overlap_sweep=fork != "off")
     for k in a_sd:

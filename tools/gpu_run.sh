@@ -1,0 +1,66 @@
+#!/bin/bash
+# One GPU-box session: tools/gpu_run.sh TAG STEP [STEP ...], run from the repo root by gpurun.
+# Steps (each under its own time limit; the first failure ends the run):
+#   tests            the whole -m gpu suite
+#   fullsize         tests/test_gpu_fullsize.py only
+#   t:<pytest -k>    the -m gpu tests matching the expression
+#   bench            python bench.py (defaults), JSON line -> gpurun_out/TAG_bench.json
+#   quick            bench.py --steps 100 --warmup 10 --no-c4 --no-score
+#   prof             rocprofv3 --kernel-trace --stats over a short bench (C2 legs only)
+#   pmc              FETCH_SIZE / WRITE_SIZE passes over the same command (tools/pmc_run.sh;
+#                    -> profiles/TAG_pmc_traffic.json, copied to gpurun_out/)
+#   c5prof           rocprofv3 --kernel-trace --stats over tools/score_bench.py
+# Output: gpurun_out/TAG_<step>.log (+ .json / prof dirs).
+set -o pipefail
+TAG=$1
+shift
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
+QUICK="bench.py --steps 60 --warmup 10 --prime 128 --no-c4 --no-score --no-cpu-baseline --no-dropin"
+for what in "$@"; do
+  echo "== $TAG $what $(date +%T)"
+  case "$what" in
+    tests)
+      timeout -k 10 1100 $PYT tests -m gpu > "$OUT/${TAG}_tests.log" 2>&1
+      rc=$? ;;
+    fullsize)
+      timeout -k 10 600 $PYT -v tests/test_gpu_fullsize.py > "$OUT/${TAG}_fullsize.log" 2>&1
+      rc=$? ;;
+    t:*)
+      timeout -k 10 600 $PYT -v tests -m gpu -k "${what#t:}" > "$OUT/${TAG}_t.log" 2>&1
+      rc=$? ;;
+    bench)
+      timeout -k 10 900 python -u bench.py > "$OUT/${TAG}_bench.log" 2>&1
+      rc=$?
+      grep '^{' "$OUT/${TAG}_bench.log" | tail -1 > "$OUT/${TAG}_bench.json" ;;
+    quick)
+      timeout -k 10 300 python -u bench.py --steps 100 --warmup 10 --no-c4 --no-score \
+        > "$OUT/${TAG}_quick.log" 2>&1
+      rc=$?
+      grep '^{' "$OUT/${TAG}_quick.log" | tail -1 > "$OUT/${TAG}_quick.json" ;;
+    prof)
+      rm -rf "$OUT/${TAG}_prof"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof" -o run -- \
+        python3 $QUICK > "$OUT/${TAG}_prof.log" 2>&1
+      rc=$? ;;
+    pmc)
+      PMC_CMD="python3 $QUICK" timeout -k 10 700 bash tools/pmc_run.sh "$TAG" \
+        > "$OUT/${TAG}_pmc.log" 2>&1
+      cp "profiles/${TAG}_pmc_traffic.json" "$OUT/" 2>/dev/null
+      rc=$? ;;
+    c5prof)
+      rm -rf "$OUT/${TAG}_c5prof"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_c5prof" -o run -- \
+        python3 tools/score_bench.py > "$OUT/${TAG}_c5prof.log" 2>&1
+      rc=$? ;;
+    *)
+      echo "unknown step $what"; exit 2 ;;
+  esac
+  echo "== $TAG $what rc=$rc $(date +%T)"
+  if [ $rc -ne 0 ]; then
+    tail -40 "$OUT/${TAG}_"*"${what%%:*}"*.log 2>/dev/null
+    exit $rc
+  fi
+done
