@@ -48,8 +48,8 @@ for what in "$@"; do
     pmc)
       PMC_CMD="python3 $QUICK" timeout -k 10 700 bash tools/pmc_run.sh "$TAG" \
         > "$OUT/${TAG}_pmc.log" 2>&1
-      cp "profiles/${TAG}_pmc_traffic.json" "$OUT/" 2>/dev/null
-      rc=$? ;;
+      rc=$?
+      cp "profiles/${TAG}_pmc_traffic.json" "$OUT/" 2>/dev/null ;;
     c5prof)
       rm -rf "$OUT/${TAG}_c5prof"
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_c5prof" -o run -- \
