@@ -6,9 +6,14 @@
   sort, overlapped sweep, deferred dense-exact Adam) and 3 through the reference call pattern
   (``model(kjt)`` -> ``nn.BCELoss`` -> ``backward`` -> ``torch.optim.Adam.step``), each against
   ``oracle.train_step`` on the same initial weights and batches (dropout 0: our dropout masks
-  are our own RNG).  Tolerances (tests/parity.py): probabilities abs 1e-6, loss
-  abs 2e-6, every parameter of the model (all 1.1M table rows, touched or not) abs 1e-6 outside
-  the per-step sign-flip zone, Adam moments at the F2 tolerances.
+  are our own RNG).  The oracle runs twice, in fp32 (the reference's precision) and in fp64
+  (the exact trajectory).  Tolerances (tests/parity.py): step 0's probabilities
+  abs 1e-6 from the fp32 oracle, loss abs 2e-6; every parameter of the model (all 1.1M table
+  rows, touched or not) abs 1e-6 from the exact trajectory outside the per-step sign-flip zone.
+  At this size the fp32 oracle is itself off the exact trajectory by more than that after the
+  first Adam step (sign-flip elements move its step-1 / step-2 probabilities 1.3e-6 / 1.2e-5,
+  and 43 hot item-row elements outside the zone by up to 3.5e-5), so later steps and those
+  elements are held to 4x the fp32 oracle's own distance (_check_step / _check_params).
 * C2 with bf16 tables: the same batches, loss within 1% of the fp32 oracle every step.
 * C5 (10K users x 1M items, top-10 and top-100, ``GraphedScorer``): 64 sampled users against
   ``oracle.score_factorised`` over all 1M items: the same ids except between oracle scores tied
@@ -22,7 +27,7 @@ import torch
 import _ncf_pkg
 import bench
 from oracle import ncf_oracle as O
-from tests.parity import assert_moment_close, assert_params_close, zone_from_grads
+from tests.parity import zone_from_grads
 
 pytestmark = pytest.mark.gpu
 ncf = _ncf_pkg.load()
@@ -30,6 +35,7 @@ DEV = torch.device("cuda:0")
 
 U, I, D, T, H, HID, B, M = 1_000_000, 100_000, 64, 32, 4, [256, 128, 64], 4096, 5
 LR, WD, STEPS = 1e-3, 1e-5, 3
+ATOL = 1e-6
 
 
 def _model(init):
@@ -40,7 +46,9 @@ def _model(init):
 
 @pytest.fixture(scope="module")
 def c2():
-    """Initial weights, the bench's batches, and the oracle's 3-step trajectory."""
+    """Initial weights, the bench's batches, and the oracle's 3-step trajectory twice: in fp32
+    (the reference's precision) and in fp64 (the exact trajectory both fp32 computations are
+    measured against)."""
     torch.set_num_threads(bench.host_cpu()[0])
     torch.manual_seed(2024)
     m = ncf.AdvancedNCF(U, I, 10, 50, D, D, T, HID, H, 0.0, M - 1)
@@ -48,51 +56,115 @@ def c2():
     del m
     batches = bench.make_batches(U, I, B, M, STEPS, DEV, seed=100)
     host = [(u.cpu(), i.cpu(), t.cpu()) for u, i, t in batches]
-    ref = {k: v.clone() for k, v in init.items()}
-    opt = O.AdamState(lr=LR, weight_decay=WD)
-    probs, losses, zones = [], [], {}
-    for u, i, t in host:
-        before = {k: v.clone() for k, v in ref.items()}
-        prob, loss, grads = O.train_step(ref, opt, u, i, t, negative_samples=M - 1, num_heads=H,
-                                         temporal_dim=T, n_layers=len(HID))
-        probs.append(prob.reshape(-1).numpy())
-        losses.append(float(loss))
-        for k, g in grads.items():
-            zones.setdefault(k, []).append(zone_from_grads(g.numpy(), before[k].numpy(), WD))
-        del before, grads
-    uniq = [(int(u.unique().numel()), int(i.unique().numel())) for u, i, _ in host]
+    out = dict(init=init, batches=batches)
+    zones = {}
+    for tag, dt in (("o32", torch.float32), ("o64", torch.float64)):
+        ref = {k: v.to(dt).clone() for k, v in init.items()}
+        opt = O.AdamState(lr=LR, weight_decay=WD)
+        probs, losses = [], []
+        for u, i, t in host:
+            before = {k: v.numpy().copy() for k, v in ref.items()} if dt == torch.float64 else None
+            prob, loss, grads = O.train_step(ref, opt, u, i, t.to(dt), negative_samples=M - 1,
+                                             num_heads=H, temporal_dim=T, n_layers=len(HID))
+            probs.append(prob.reshape(-1).double().numpy())
+            losses.append(float(loss))
+            if before is not None:   # the sign-flip zone from the exact gradients
+                for k, g in grads.items():
+                    zones.setdefault(k, []).append(zone_from_grads(g.numpy(), before[k], WD))
+            del before, grads
+        out[tag] = dict(probs=probs, losses=losses, ref=ref, state=opt.state)
+    out["zones"] = zones
     # the case must hold what only full size has: hot item segments longer than one piece
     assert max(int(torch.bincount(i).max()) for _, i, _ in host) > 64
-    return dict(init=init, batches=batches, probs=probs, losses=losses, ref=ref,
-                state=opt.state, zones=zones, uniq=uniq)
+    out["uniq"] = [(int(u.unique().numel()), int(i.unique().numel())) for u, i, _ in host]
+    # the fp32 reference's own distance from the exact trajectory (the noise floor of any fp32
+    # implementation at this size): per tensor, elements outside the zone off by > 1e-6
+    out["noise"] = {k: _dev(out["o32"]["ref"][k].double().numpy(), out["o64"]["ref"][k].numpy(),
+                            zones[k]) for k in zones}
+    return out
 
 
-def _check_params(c, sd, state):
-    """Every parameter after STEPS steps vs the oracle (all rows of every table)."""
-    for k, v in c["ref"].items():
+def _dev(a, exact, zones):
+    """(count, max) of |a - exact| > ATOL outside the sign-flip zone, and (count, max) inside."""
+    d = np.abs(np.asarray(a, np.float64) - exact)
+    nz = np.sum(zones, axis=0)
+    bad = d > ATOL
+    o, z = bad & (nz == 0), bad & (nz > 0)
+    return (int(o.sum()), float(d[o].max()) if o.any() else 0.0,
+            int(z.sum()), float(d[z].max()) if z.any() else 0.0)
+
+
+def _stats(name, rec):
+    """Write the measured deviations next to the gpu run's outputs (evidence for DESIGN.md)."""
+    import json
+    import os
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(d):
+        with open(os.path.join(d, f"fullsize_{name}.json"), "w") as f:
+            json.dump(rec, f, indent=1)
+
+
+def _check_params(c, sd, state, name, rec):
+    """Every parameter after STEPS steps against the exact (fp64) trajectory.  Outside the
+    sign-flip zone an element is within ATOL, except for as many elements as the fp32 oracle
+    itself misses there (x4, + 16), each within max(4 x the oracle's own worst, 1e-5); inside
+    the zone within 2 lr per zone step (tests/parity.py).  Adam moments outside the zone within
+    max(4 x the fp32 oracle's own worst, 1e-7 / 1e-12).  Unused parameters never move."""
+    lr_bound = 2 * LR
+    fails = []
+    rec["params"] = {}
+    for k, v in c["o64"]["ref"].items():
         got = sd[k].detach().cpu().numpy()
         if k not in c["zones"]:          # unused by forward (grad None): never moves
-            assert np.array_equal(got, c["init"][k].numpy()), k
+            if not np.array_equal(got, c["init"][k].numpy()):
+                fails.append(f"{k}: unused parameter moved")
             continue
-        assert_params_close(k, got, v.numpy(), c["zones"][k], LR)
-    for k, st in c["state"].items():
         zs = c["zones"][k]
-        assert_moment_close(k, state[k]["exp_avg"], st["exp_avg"].numpy(), zs)
-        assert_moment_close(k, state[k]["exp_avg_sq"], st["exp_avg_sq"].numpy(), zs, atol=1e-12)
-        assert float(state[k]["step"]) == STEPS, k
+        n_o, m_o, n_z, m_z = _dev(got, v.numpy(), zs)
+        nn_o, nm_o = c["noise"][k][:2]
+        rec["params"][k] = {"gpu_vs_fp64": [n_o, m_o, n_z, m_z], "fp32_oracle_vs_fp64":
+                            list(c["noise"][k])}
+        if n_o > 4 * nn_o + 16 or m_o > max(4 * nm_o, 1e-5):
+            fails.append(f"{k}: {n_o} elements outside the zone off by up to {m_o:.3e} "
+                         f"(fp32 oracle: {nn_o}, {nm_o:.3e})")
+        nz = np.sum(zs, axis=0)
+        dz = np.abs(got.astype(np.float64) - v.numpy())
+        if ((dz > ATOL) & (nz > 0) & (dz > lr_bound * nz + ATOL)).any():
+            fails.append(f"{k}: zone element beyond 2 lr per zone step")
+    rec["moments"] = {}
+    for k, st in c["o64"]["state"].items():
+        zone = np.any(c["zones"][k], axis=0)
+        for mom, atol in (("exp_avg", 1e-7), ("exp_avg_sq", 1e-12)):
+            exact = st[mom].numpy()
+            g = np.abs(np.asarray(state[k][mom], np.float64) - exact)[~zone]
+            o = np.abs(c["o32"]["state"][k][mom].double().numpy() - exact)[~zone]
+            gm, om = (float(g.max()) if g.size else 0.0), (float(o.max()) if o.size else 0.0)
+            rec["moments"][f"{k}.{mom}"] = [gm, om]
+            if gm > max(4 * om, atol):
+                fails.append(f"{k}.{mom}: {gm:.3e} off outside the zone (fp32 oracle {om:.3e})")
+        if float(state[k]["step"]) != STEPS:
+            fails.append(f"{k}: step {state[k]['step']}")
+    _stats(name, rec)
+    assert not fails, "; ".join(fails[:8])
 
 
-def _check_step(c, s, prob, loss):
-    d = np.abs(prob.reshape(-1) - c["probs"][s]).max()
-    assert d <= 1e-6, f"step {s}: |dprob| {d:.3e}"
-    assert abs(loss - c["losses"][s]) <= 2e-6, f"step {s}: loss {loss} vs {c['losses'][s]}"
-
-
-def _torch_state(m, opt):
-    names = {id(p): n for n, p in m.named_parameters()}
-    return {names[id(p)]: {k: (v.detach().cpu().numpy() if torch.is_tensor(v) and v.dim() else
-                               float(v)) for k, v in s.items()}
-            for p, s in opt.state.items()}
+def _check_step(c, s, prob, loss, rec):
+    """Step s's probabilities and loss.  Step 0 runs on the initial weights: abs 1e-6 from the
+    fp32 oracle.  Every step: within max(4 x the fp32 oracle's own distance from the exact
+    (fp64) probabilities, 2e-6) of them — after the first Adam step the sign-flip zone's
+    elements (|g + wd p| < 1e-6, moved +-lr by summation noise) put both fp32 computations
+    1e-6..1e-5 off the exact trajectory at this size.  Loss: abs 2e-6 from the fp32 oracle."""
+    p = prob.reshape(-1).astype(np.float64)
+    d32 = float(np.abs(p - c["o32"]["probs"][s]).max())
+    d64 = float(np.abs(p - c["o64"]["probs"][s]).max())
+    n64 = float(np.abs(c["o32"]["probs"][s] - c["o64"]["probs"][s]).max())
+    dl = abs(loss - c["o32"]["losses"][s])
+    rec.setdefault("steps", []).append({"dprob_vs_fp32": d32, "dprob_vs_fp64": d64,
+                                        "fp32_oracle_dprob_vs_fp64": n64, "dloss_vs_fp32": dl})
+    if s == 0:
+        assert d32 <= 1e-6, f"step 0: |dprob| {d32:.3e} from the fp32 oracle"
+    assert d64 <= max(4 * n64, 2e-6), f"step {s}: |dprob| {d64:.3e} vs fp64 (fp32 oracle {n64:.3e})"
+    assert dl <= 2e-6, f"step {s}: loss {loss} vs {c['o32']['losses'][s]}"
 
 
 def test_c2_full_size_fused_step_vs_oracle(c2):
@@ -100,19 +172,21 @@ def test_c2_full_size_fused_step_vs_oracle(c2):
     m = _model(c2["init"])
     step = FusedTrainStep(m, lr=LR, weight_decay=WD)
     bt = c2["batches"]
+    rec = {}
     for s, (u, i, t) in enumerate(bt):
         w = step(u, i, t, next=bt[s + 1][:2] if s + 1 < len(bt) else None)
-        _check_step(c2, s, w.prob.detach().cpu().numpy(), float(w.loss.item()))
+        _check_step(c2, s, w.prob.detach().cpu().numpy(), float(w.loss.item()), rec)
     assert tuple(w.num_unique.cpu().tolist()) == c2["uniq"][-1]   # (unique users, items)
     opt = torch.optim.Adam(m.parameters(), lr=LR, weight_decay=WD)
     step.export_optimizer_state(opt)
-    _check_params(c2, m.state_dict(), _torch_state(m, opt))
+    _check_params(c2, m.state_dict(), _torch_state(m, opt), "fused", rec)
 
 
 def test_c2_full_size_reference_call_pattern_vs_oracle(c2):
     m = _model(c2["init"])
     opt = torch.optim.Adam(m.parameters(), lr=LR, weight_decay=WD)
     crit = torch.nn.BCELoss()
+    rec = {}
     for s, (u, i, t) in enumerate(c2["batches"]):
         kj = ncf.KeyedJaggedTensor.from_lengths_sync(
             keys=["user_id", "product_id"], values=torch.cat([u, i]),
@@ -122,8 +196,8 @@ def test_c2_full_size_reference_call_pattern_vs_oracle(c2):
         opt.zero_grad()
         loss.backward()
         opt.step()
-        _check_step(c2, s, out.detach().cpu().numpy(), float(loss.item()))
-    _check_params(c2, m.state_dict(), _torch_state(m, opt))
+        _check_step(c2, s, out.detach().cpu().numpy(), float(loss.item()), rec)
+    _check_params(c2, m.state_dict(), _torch_state(m, opt), "dropin", rec)
 
 
 def test_c2_full_size_bf16_tables_track_oracle(c2):
@@ -132,7 +206,7 @@ def test_c2_full_size_bf16_tables_track_oracle(c2):
     step = FusedTrainStep(m, lr=LR, weight_decay=WD, table_dtype=torch.bfloat16)
     for s, (u, i, t) in enumerate(c2["batches"]):
         w = step(u, i, t)
-        rel = abs(float(w.loss.item()) - c2["losses"][s]) / c2["losses"][s]
+        rel = abs(float(w.loss.item()) - c2["o32"]["losses"][s]) / c2["o32"]["losses"][s]
         assert rel < 0.01, f"step {s}: bf16-table loss {rel:.3%} from the fp32 oracle"
 
 
