@@ -139,9 +139,9 @@ class ShardExchange:
 
 class RcclExchange(ShardExchange):
     """The same collectives issued through the C-ABI (``ncf_comm_*``: grouped ncclSend/ncclRecv
-    and ncclAllReduce on the step's own HIP streams) on two RCCL communicators of this library:
-    ``main`` for the run's exchanges, ``side`` for the pipelined count exchange and the dense
-    all-reduce (the roles of ``group`` / ``plan_group``).  The communicators are created over
+    and ncclAllReduce on the step's own HIP streams) on one RCCL communicator of this library
+    (``main``; ``side`` is the same communicator in the plan-stream role: the pipelined count
+    exchange, the rows sent ahead and the dense all-reduce).  The communicators are created over
     ``group`` (unique ids broadcast by its rank 0).  Same results as ``ShardExchange``; none of
     the c10d per-call work (Work objects, stream-sync events, allocator bookkeeping)."""
 
@@ -149,8 +149,15 @@ class RcclExchange(ShardExchange):
         super().__init__(group, device, plan_group)
         if not _lib.query("ncf_comm_available"):
             raise RuntimeError("RcclExchange: librccl is not loaded in this process")
+        # ONE communicator for every collective of the step, whichever stream issues it: RCCL
+        # runs the operations of a communicator in the order they were issued on the host (each
+        # launch is ordered behind the communicator's previous one, whatever the user stream), so
+        # every rank executes the same sequence (counts / rows-ahead / dense all-reduce on the
+        # plan stream, row exchanges on the step's stream) and no spinning collective of one
+        # communicator can wait on a hardware queue behind another communicator's (DESIGN 6:
+        # 4 hardware queues per process).  ``side`` names the plan-stream role only.
         self.main = self._comm()
-        self.side = self._comm()
+        self.side = self.main
         W = self.world
         # host split arrays, one pair per call site: the collective reads them when it is
         # called, so a launch tape replays each site with the sizes written there for the step
@@ -188,11 +195,10 @@ class RcclExchange(ShardExchange):
         return c.value
 
     def close(self):
-        for name in ("main", "side"):
-            c = getattr(self, name, None)
-            if c is not None:
-                _lib.call("ncf_comm_destroy", c)
-                setattr(self, name, None)
+        c = getattr(self, "main", None)
+        if c is not None:
+            _lib.call("ncf_comm_destroy", c)
+        self.main = self.side = None
 
     def counts_issue(self, plan):
         if plan.stream is None:
