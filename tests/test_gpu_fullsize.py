@@ -167,6 +167,13 @@ def _check_step(c, s, prob, loss, rec):
     assert dl <= 2e-6, f"step {s}: loss {loss} vs {c['o32']['losses'][s]}"
 
 
+def _torch_state(m, opt):
+    names = {id(p): n for n, p in m.named_parameters()}
+    return {names[id(p)]: {k: (v.detach().cpu().numpy() if torch.is_tensor(v) and v.dim() else
+                               float(v)) for k, v in s.items()}
+            for p, s in opt.state.items()}
+
+
 def test_c2_full_size_fused_step_vs_oracle(c2):
     from ncf_amd.trainer import FusedTrainStep
     m = _model(c2["init"])
