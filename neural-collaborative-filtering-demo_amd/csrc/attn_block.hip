@@ -404,14 +404,36 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
   if (clock) seed += clock->seed;
 
   NCF_ASTAMP(0, 0);
-  if (core) {
-    float* const dst[2] = {S0, S1};
-    const float* const src[2] = {xu + r0 * D, xi + r0 * D};
-    stage_in_n<D, 2>(dst, src, Rp, rows);
-  } else {
-    float* const dst[1] = {S1};
-    const float* const src[1] = {xi + r0 * D};
-    stage_in_n<D, 1>(dst, src, Rp, rows);
+  // one user per group (fact 6): Q is projected from the G group rows of X_u, staged straight
+  // into S2 (free until V lands) — the other M - 1 rows of each group are never read.  The
+  // item rows' loads are in flight during the test (which is a barrier).
+  bool shq = false;
+  {
+    constexpr int L4 = D / 4;
+    constexpr int IT = (16 * G::NTmax * L4 + kThreads - 1) / kThreads;
+    float4 vi[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int e = threadIdx.x + kThreads * it, r = e / L4, c = (e % L4) * 4;
+      vi[it] = (e < Rp * L4 && r < rows) ? ld4(xi + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (core && M > 1 && uids) shq = ids_uniform(uids + r0, ng, M);
+    if (shq) {
+      for (int e = threadIdx.x; e < G::kGroups * L4; e += kThreads) {
+        const int gl = e / L4, c = (e % L4) * 4;
+        const float4 v = gl < ng ? ld4(xu + (r0 + (int64_t)gl * M) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(S2 + gl * kPitch + c) = v;
+      }
+    } else if (core) {
+      float* const dst[1] = {S0};
+      const float* const src[1] = {xu + r0 * D};
+      stage_in_n<D, 1>(dst, src, Rp, rows);
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int e = threadIdx.x + kThreads * it;
+      if (e < Rp * L4) *reinterpret_cast<float4*>(S1 + (e / L4) * kPitch + (e % L4) * 4) = vi[it];
+    }
   }
   // the projections' weight fragments of this wave's column slice, issued behind the rows' loads
   // (in flight during the staging barrier instead of in front of each projection); out_proj's
@@ -427,18 +449,9 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
     bb_q = bq ? bq[cl] : 0.0f;
     bb_k = bk ? bk[cl] : 0.0f;
   }
-  // one user per group (fact 6): Q from the G group rows, gathered into S2 (free until V lands)
-  bool shq = false;
-  if (core && M > 1 && uids)
-    shq = ids_uniform(uids + r0, ng, M);
-  else
-    __syncthreads();
+  __syncthreads();
   NCF_ASTAMP(0, 1);
   if (!core) frag_wt<D>(wo, w, fw_o);
-  if (shq) {
-    gather_group_rows<D>(S2, S0, M);
-    __syncthreads();
-  }
   f32x4 fq[kMaxM], fk[kMaxM], fv[kMaxM];
   project_f<D>(S1, fw_v, bb_v, NT, fv);
   if (core) {
@@ -547,26 +560,51 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
   constexpr int kPre = (16 * G::NTmax * L4 + kThreads - 1) / kThreads;   // float4 per thread
   float4 pu[kPre], pi[kPre];   // X_u / X_i rows for the fused weight gradients
   if constexpr (RC) {
+    // one user per group (the forward's test on the same ids: the same Q bits): only the G
+    // group rows of X_u are read, straight into S3 (the Q projection's input)
+    bool shq = false;
     {
-      float* const dst[3] = {S0, S1, S2};
-      const float* const src[3] = {dY + r0 * D, Xu + r0 * D, Xi + r0 * D};
-      stage_in_n<D, 3>(dst, src, Rp, rows);
+      constexpr int IT = (16 * G::NTmax * L4 + kThreads - 1) / kThreads;
+      float4 v0[IT], v2[IT];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int e = threadIdx.x + kThreads * it, r = e / L4, c = (e % L4) * 4;
+        const bool in = e < Rp * L4 && r < rows;
+        v0[it] = in ? ld4(dY + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v2[it] = in ? ld4(Xi + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if (M > 1 && uids) shq = ids_uniform(uids + r0, ng, M);
+      if (shq) {
+        for (int e = threadIdx.x; e < kGroups * L4; e += kThreads) {
+          const int gl = e / L4, c = (e % L4) * 4;
+          const float4 v = gl < ng ? ld4(Xu + (r0 + (int64_t)gl * M) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+          *reinterpret_cast<float4*>(S3 + gl * kPitch + c) = v;
+        }
+      } else {
+        float* const dst[1] = {S1};
+        const float* const src[1] = {Xu + r0 * D};
+        stage_in_n<D, 1>(dst, src, Rp, rows);
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int e = threadIdx.x + kThreads * it;
+        if (e < Rp * L4) {
+          *reinterpret_cast<float4*>(S0 + (e / L4) * kPitch + (e % L4) * 4) = v0[it];
+          *reinterpret_cast<float4*>(S2 + (e / L4) * kPitch + (e % L4) * 4) = v2[it];
+        }
+      }
     }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kPre; ++q) {   // (zero rows past the batch: staged as zeros)
-      const int e = threadIdx.x + kThreads * q;
+      const int e = threadIdx.x + kThreads * q, r = e / L4, c = (e % L4) * 4;
       const bool in = e < Rp * L4;
-      pu[q] = in ? *reinterpret_cast<const float4*>(S1 + (e / L4) * kPitch + (e % L4) * 4)
+      // X_u of row r: its group's row (shq) or its own
+      const float* xu_r = shq ? S3 + min(r / M, kGroups - 1) * kPitch + c : S1 + r * kPitch + c;
+      pu[q] = in && (!shq || r < rows) ? *reinterpret_cast<const float4*>(xu_r)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      pi[q] = in ? *reinterpret_cast<const float4*>(S2 + r * kPitch + c)
                  : make_float4(0.f, 0.f, 0.f, 0.f);
-      pi[q] = in ? *reinterpret_cast<const float4*>(S2 + (e / L4) * kPitch + (e % L4) * 4)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    // one user per group (the forward's test on the same ids: the same Q bits)
-    const bool shq = M > 1 && uids && ids_uniform(uids + r0, ng, M);
-    if (shq) {
-      gather_group_rows<D>(S3, S1, M);
-      __syncthreads();
     }
     f32x4 fq[kMaxM], fk[kMaxM], fv[kMaxM];
     if (shq)

@@ -1,5 +1,5 @@
 """One line per bench log: ms/step and selected per-entry-point times (ms/step).
-    python tools/bench_summ.py LOG [entry_point ...]"""
+    python tools/bench_summ.py LOG [TAG=value] [entry_point ...]   (no entry points: all)"""
 import json
 import sys
 
@@ -7,7 +7,9 @@ log = sys.argv[1]
 d = [json.loads(l) for l in open(log) if l.startswith("{")][-1]
 k = d.get("kernel_ms_per_step", {})
 out = [log.split("/")[-1], f"{d['ms_per_step']:.4f}"]
-for name in sys.argv[2:]:
+names = [a for a in sys.argv[2:] if "=" not in a]
+out += [a for a in sys.argv[2:] if "=" in a]
+for name in names or sorted(k, key=lambda x: -k[x]):
     v = k.get(name)
     out.append(f"{name.replace('ncf_', '')}={v * 1e3:.1f}us" if v else f"{name}=-")
 r = d.get("roofline", {})
