@@ -10,10 +10,14 @@
   (the exact trajectory).  Tolerances (tests/parity.py): step 0's probabilities
   abs 1e-6 from the fp32 oracle, loss abs 2e-6; every parameter of the model (all 1.1M table
   rows, touched or not) abs 1e-6 from the exact trajectory outside the per-step sign-flip zone.
-  At this size the fp32 oracle is itself off the exact trajectory by more than that after the
-  first Adam step (sign-flip elements move its step-1 / step-2 probabilities 1.3e-6 / 1.2e-5,
-  and 43 hot item-row elements outside the zone by up to 3.5e-5), so later steps and those
-  elements are held to 4x the fp32 oracle's own distance (_check_step / _check_params).
+  At this size the fp32 oracle is itself far off the exact trajectory after the first Adam
+  step: Adam (eps 1e-8) turns fp32 rounding noise in near-zero gradients into +-lr steps that
+  the fp64 run does not take (measured on the MI355X box's host: step-1 / step-2 probabilities
+  3.1e-5 / 1.9e-3 off, ~20K item-table elements outside the exact zone up to 4.3e-3 off).  So
+  later steps and those elements are held to the fp32 oracle's own distance from the exact
+  trajectory (x4; the GPU measured within 1% of it in count and worst case), and the elements of
+  the fp32 oracle's own sign-flip zone to 2 lr per zone step from it (_check_step /
+  _check_params; per-tensor numbers written to gpurun_out/fullsize_*.json).
 * C2 with bf16 tables: the same batches, loss within 1% of the fp32 oracle every step.
 * C5 (10K users x 1M items, top-10 and top-100, ``GraphedScorer``): 64 sampled users against
   ``oracle.score_factorised`` over all 1M items: the same ids except between oracle scores tied
@@ -62,18 +66,19 @@ def c2():
         ref = {k: v.to(dt).clone() for k, v in init.items()}
         opt = O.AdamState(lr=LR, weight_decay=WD)
         probs, losses = [], []
+        zt = zones.setdefault(tag, {})
         for u, i, t in host:
-            before = {k: v.numpy().copy() for k, v in ref.items()} if dt == torch.float64 else None
+            before = {k: v.numpy().copy() for k, v in ref.items()}
             prob, loss, grads = O.train_step(ref, opt, u, i, t.to(dt), negative_samples=M - 1,
                                              num_heads=H, temporal_dim=T, n_layers=len(HID))
             probs.append(prob.reshape(-1).double().numpy())
             losses.append(float(loss))
-            if before is not None:   # the sign-flip zone from the exact gradients
-                for k, g in grads.items():
-                    zones.setdefault(k, []).append(zone_from_grads(g.numpy(), before[k], WD))
+            for k, g in grads.items():   # each step's sign-flip zone, from each run's gradients
+                zt.setdefault(k, []).append(zone_from_grads(g.numpy(), before[k], WD))
             del before, grads
         out[tag] = dict(probs=probs, losses=losses, ref=ref, state=opt.state)
-    out["zones"] = zones
+    out["zones"] = zones["o64"]
+    out["zones32"] = zones["o32"]
     # the case must hold what only full size has: hot item segments longer than one piece
     assert max(int(torch.bincount(i).max()) for _, i, _ in host) > 64
     out["uniq"] = [(int(u.unique().numel()), int(i.unique().numel())) for u, i, _ in host]
@@ -106,9 +111,10 @@ def _stats(name, rec):
 
 def _check_params(c, sd, state, name, rec):
     """Every parameter after STEPS steps against the exact (fp64) trajectory.  Outside the
-    sign-flip zone an element is within ATOL, except for as many elements as the fp32 oracle
+    (exact) sign-flip zone an element is within ATOL, except for as many elements as the fp32 oracle
     itself misses there (x4, + 16), each within max(4 x the oracle's own worst, 1e-5); inside
-    the zone within 2 lr per zone step (tests/parity.py).  Adam moments outside the zone within
+    the fp32 reference's own zone within 2 lr per zone step of it (tests/parity.py; the exact
+    trajectory does not take those noise-driven steps at all).  Adam moments outside the zone within
     max(4 x the fp32 oracle's own worst, 1e-7 / 1e-12).  Unused parameters never move."""
     lr_bound = 2 * LR
     fails = []
@@ -127,10 +133,14 @@ def _check_params(c, sd, state, name, rec):
         if n_o > 4 * nn_o + 16 or m_o > max(4 * nm_o, 1e-5):
             fails.append(f"{k}: {n_o} elements outside the zone off by up to {m_o:.3e} "
                          f"(fp32 oracle: {nn_o}, {nm_o:.3e})")
-        nz = np.sum(zs, axis=0)
-        dz = np.abs(got.astype(np.float64) - v.numpy())
-        if ((dz > ATOL) & (nz > 0) & (dz > lr_bound * nz + ATOL)).any():
-            fails.append(f"{k}: zone element beyond 2 lr per zone step")
+        # against the fp32 reference itself (the F2 rule, tests/parity.py): inside its own
+        # sign-flip zone an element is within 2 lr per zone step
+        z32 = c["zones32"][k]
+        nz32 = np.sum(z32, axis=0)
+        d32 = np.abs(got - c["o32"]["ref"][k].numpy())
+        rec["params"][k]["gpu_vs_fp32"] = list(_dev(got, c["o32"]["ref"][k].double().numpy(), z32))
+        if ((nz32 > 0) & (d32 > lr_bound * nz32 + ATOL)).any():
+            fails.append(f"{k}: fp32-zone element beyond 2 lr per zone step")
     rec["moments"] = {}
     for k, st in c["o64"]["state"].items():
         zone = np.any(c["zones"][k], axis=0)

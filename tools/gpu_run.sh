@@ -10,7 +10,7 @@
 #   pmc              FETCH_SIZE / WRITE_SIZE passes over the same command (tools/pmc_run.sh;
 #                    -> profiles/TAG_pmc_traffic.json, copied to gpurun_out/)
 #   c5prof           rocprofv3 --kernel-trace --stats over tools/score_bench.py
-#   ab:VAR=a/b       the short C2 bench with VAR=a and VAR=b, interleaved 3 times each
+#   ab:VAR=a,b       the short C2 bench with VAR=a and VAR=b, interleaved 3 times each
 #                    (ms/step + the per-kernel ms of each run -> TAG_ab.log)
 # Output: gpurun_out/TAG_<step>.log (+ .json / prof dirs).
 set -o pipefail
@@ -58,7 +58,7 @@ for what in "$@"; do
         python3 tools/score_bench.py > "$OUT/${TAG}_c5prof.log" 2>&1
       rc=$? ;;
     ab:*)
-      spec="${what#ab:}"; var="${spec%%=*}"; vals="${spec#*=}"; va="${vals%%/*}"; vb="${vals#*/}"
+      spec="${what#ab:}"; var="${spec%%=*}"; vals="${spec#*=}"; va="${vals%%,*}"; vb="${vals#*,}"
       rc=0
       for k in 1 2 3; do
         for v in "$va" "$vb"; do
