@@ -62,8 +62,9 @@ for what in "$@"; do
       rc=0
       for k in 1 2 3; do
         for v in "$va" "$vb"; do
-          env "$var=$v" timeout -k 10 200 python3 $QUICK > "$OUT/${TAG}_ab_${v}_$k.log" 2>&1 || { rc=$?; break 2; }
-          python3 tools/bench_summ.py "$OUT/${TAG}_ab_${v}_$k.log" "$var=$v" >> "$OUT/${TAG}_ab.log" 2>&1
+          f="$OUT/${TAG}_ab_$(basename "$v")_$k.log"
+          env "$var=$v" timeout -k 10 200 python3 $QUICK > "$f" 2>&1 || { rc=$?; break 2; }
+          python3 tools/bench_summ.py "$f" "$var=$v" >> "$OUT/${TAG}_ab.log" 2>&1
         done
       done ;;
     *)
