@@ -85,7 +85,7 @@ def c2():
     # the fp32 reference's own distance from the exact trajectory (the noise floor of any fp32
     # implementation at this size): per tensor, elements outside the zone off by > 1e-6
     out["noise"] = {k: _dev(out["o32"]["ref"][k].double().numpy(), out["o64"]["ref"][k].numpy(),
-                            zones[k]) for k in zones}
+                            z) for k, z in out["zones"].items()}
     return out
 
 
