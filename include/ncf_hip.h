@@ -484,6 +484,16 @@ int ncf_score_item_bias(const float* mlp_item, int64_t n, const float* final_w,
  * when the sample logits already include the bias (the sample GEMM's column bias). */
 int ncf_score_kth(const float* logits, int64_t n_users, int64_t S, int K, const float* item_bias,
                   int64_t stride, float* thr, void* stream);
+/* The threshold sample on bf16 matrix cores: out[u*S + j] = fp16, rounded toward -inf, of the
+ * two-term split logit q_u . p_(j*stride) + sample_bias[j] (items3: the ncf_score_split_items
+ * planes of the n_items rows), within 1e-4 |q_u| max|p| of the fp32 logit; then its k-th per
+ * user (S <= 38912).  A valid threshold is the k-th lowered by that bound (ncf_score_margin with
+ * c = 1e-4): replaces ncf_gemm_f32 + ncf_score_kth with half the bytes and 16x the MFMA rate. */
+int ncf_score_sample_split16(const float* queries, int64_t n_users, const uint16_t* items3,
+                             int64_t n_items, int64_t dim, int64_t stride,
+                             const float* sample_bias, int64_t S, uint16_t* out, void* stream);
+int ncf_score_kth16(const uint16_t* logits, int64_t n_users, int64_t S, int K, float* thr,
+                    void* stream);
 int ncf_score_collect(const float* queries, const int32_t* user_list, int64_t n_users,
                       const float* items, const float* item_bias, int64_t n_items, int64_t dim,
                       const float* thr, int64_t cap, uint32_t* count, float* cand_logit,

@@ -804,7 +804,8 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
       if (h.targets) {
         const float t = ld_t[pass];
         go = inv_n * (o - t) / fmaxf((1.0f - o) * o, 1e-12f);
-        l = -(t * fmaxf(logf(o), -100.0f) + (1.0f - t) * fmaxf(logf(1.0f - o), -100.0f));
+        if (sub == 0)   // (the BCE term: one lane of the row sums it)
+          l = -(t * fmaxf(logf(o), -100.0f) + (1.0f - t) * fmaxf(logf(1.0f - o), -100.0f));
       } else {
         go = ld_t[pass];
       }

@@ -163,19 +163,45 @@ __device__ __forceinline__ int kth_walk(const uint32_t* hist, uint32_t need, uin
 
 // NT threads: 1024 for long samples (one workgroup per CU: more loads and LDS sweeps in flight),
 // 512 for short ones (several workgroups per CU)
-template <int NT>
-__global__ __launch_bounds__(NT) void k_kth_lds(const float* __restrict__ logits, int64_t S,
+// E = float: fp32 sample logits (bias added here when given); E = _Float16: the fp16 logits of
+// k_sample16 (bias included, rounded down), kept as fp16 in LDS (2 S bytes: two workgroups per CU
+// at S = 38912).  Every comparison is on the widened fp32 value.
+template <typename E>
+__device__ __forceinline__ float4 ld_logit4(const E* p);
+template <>
+__device__ __forceinline__ float4 ld_logit4<float>(const float* p) { return ld4(p); }
+template <>
+__device__ __forceinline__ float4 ld_logit4<_Float16>(const _Float16* p) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const h4 v = *reinterpret_cast<const h4*>(p);
+  return make_float4((float)v.x, (float)v.y, (float)v.z, (float)v.w);
+}
+template <typename E>
+__device__ __forceinline__ void st_logit4(E* p, float4 v);
+template <>
+__device__ __forceinline__ void st_logit4<float>(float* p, float4 v) {
+  *reinterpret_cast<float4*>(p) = v;
+}
+template <>
+__device__ __forceinline__ void st_logit4<_Float16>(_Float16* p, float4 v) {   // (exact: v is fp16)
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  *reinterpret_cast<h4*>(p) = h4{(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+}
+
+template <int NT, typename E = float>
+__global__ __launch_bounds__(NT) void k_kth_lds(const E* __restrict__ logits, int64_t S,
                                                  int K, const float* __restrict__ bias,
                                                  int64_t stride, float* __restrict__ thr) {
-  extern __shared__ float kth_vals[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char kth_raw[];
+  E* kth_vals = reinterpret_cast<E*>(kth_raw);
   __shared__ uint32_t hist[256], hmin[256];
   __shared__ float rmax[NT / 64], rmin[NT / 64];
   __shared__ int s_bin;
   __shared__ uint32_t s_need;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const float* row = logits + (int64_t)blockIdx.x * S;
+  const E* row = logits + (int64_t)blockIdx.x * S;
   float vmax = -INFINITY, vmin = INFINITY;
-  const int64_t S4 = (S & 3) == 0 ? S / 4 : 0;   // rows start 16-B aligned when S % 4 == 0
+  const int64_t S4 = (S & 3) == 0 ? S / 4 : 0;   // rows start 4-element aligned when S % 4 == 0
   // 4 float4 loads in flight per thread (a dependent load per iteration leaves the row's HBM
   // latency exposed 15 times at S = 30720)
   for (int64_t base = tid; base < S4; base += 4 * NT) {
@@ -183,7 +209,7 @@ __global__ __launch_bounds__(NT) void k_kth_lds(const float* __restrict__ logits
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t j4 = base + (int64_t)u * NT;
-      xs[u] = j4 < S4 ? ld4(row + 4 * j4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      xs[u] = j4 < S4 ? ld_logit4<E>(row + 4 * j4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -195,14 +221,14 @@ __global__ __launch_bounds__(NT) void k_kth_lds(const float* __restrict__ logits
                                           x.z + bias[(j + 2) * stride],
                                           x.w + bias[(j + 3) * stride])
                             : x;
-      *reinterpret_cast<float4*>(kth_vals + j) = v;
+      st_logit4<E>(kth_vals + j, v);
       vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
       vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
     }
   }
   for (int64_t j = 4 * S4 + tid; j < S; j += NT) {
-    const float v = bias ? row[j] + bias[j * stride] : row[j];
-    kth_vals[j] = v;
+    const float v = bias ? (float)row[j] + bias[j * stride] : (float)row[j];
+    kth_vals[j] = (E)v;
     vmax = fmaxf(vmax, v);
     vmin = fminf(vmin, v);
   }
@@ -223,7 +249,7 @@ __global__ __launch_bounds__(NT) void k_kth_lds(const float* __restrict__ logits
     // level 0: 256 bins over [vmin, vmax]; b(v) is non-decreasing in v
     const float inv0 = 256.0f / (vmax - vmin);
     auto bin0 = [&](float x) { return (int)fminf(fmaxf((x - vmin) * inv0, 0.0f), 255.0f); };
-    for (int64_t j = tid; j < S; j += NT) atomicAdd(&hist[bin0(kth_vals[j])], 1u);
+    for (int64_t j = tid; j < S; j += NT) atomicAdd(&hist[bin0((float)kth_vals[j])], 1u);
     __syncthreads();
     if (w == 0) {
       uint32_t above = 0;
@@ -241,7 +267,7 @@ __global__ __launch_bounds__(NT) void k_kth_lds(const float* __restrict__ logits
     // level 1: 256 sub-bins of bin b0, with the smallest logit of each (as an order key)
     const float lo1 = vmin + (float)b0 / inv0, inv1 = inv0 * 256.0f;
     for (int64_t j = tid; j < S; j += NT) {
-      const float x = kth_vals[j];
+      const float x = (float)kth_vals[j];
       if (bin0(x) == b0) {
         const int sb = (int)fminf(fmaxf((x - lo1) * inv1, 0.0f), 255.0f);
         atomicAdd(&hist[sb], 1u);
@@ -883,6 +909,89 @@ __device__ __forceinline__ void bitonic_desc(unsigned long long* keys, int n2) {
 // (the scan's K-th largest) - 2E; only those are re-scored in fp32 (logit = bias + sum_k q_k p_k,
 // fmaf in k order) and the select runs on the re-scored keys (the others keyed 0: below every
 // real logit's key).
+// ---- 2'. the threshold sample on bf16 matrix cores (k_sample16, ncf_score_sample_split16):
+// logits of n users x S sample items (sample item j = item j * stride of the index) from the
+// two-term operand split (a0 b0 + a0 b1 + a1 b0 on v_mfma_f32_32x32x16_bf16: within E_u = 1e-4
+// |q_u| max|p| of the fp32 logit, the scan's own two-term bound), plus the sample bias, stored
+// as fp16 rounded toward -inf.  A stored value is then <= the approximate logit, so the K-th
+// largest stored value v has K sample items with fp32 logit >= v - E_u: the caller lowers the
+// k-th threshold by E_u (ncf_score_margin) and it stays a valid lower bound of the K-th largest.
+// Against the fp32 sample GEMM: 16x the matrix rate, half the bytes written and re-read (fp16).
+// Workgroup: 128 sample items staged in LDS (both planes), 4 waves x 32 users, each wave four
+// 32 x 32 tiles (one per 32 items).
+template <int T>
+__global__ __launch_bounds__(256) void k_sample16(const float* __restrict__ q, int64_t n_users,
+                                                  const uint16_t* __restrict__ items3,
+                                                  int64_t n_items, int64_t stride,
+                                                  const float* __restrict__ sbias, int64_t S,
+                                                  _Float16* __restrict__ out) {
+  constexpr int D = 64, J = 128;
+  __shared__ __attribute__((aligned(16))) uint16_t ps[T][J][kP3];
+  __shared__ float bs[J];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 31, h = lane >> 5;
+  const int64_t j0 = (int64_t)blockIdx.x * J;
+  const int64_t u0 = (int64_t)blockIdx.y * 128 + 32 * w;
+  // the sample rows' loads, then this lane's query split (the rows land meanwhile)
+  constexpr int CH = T * J * (D / 8);   // 16-B chunks
+  uint4 pv[CH / 256];
+#pragma unroll
+  for (int c = 0; c < CH / 256; ++c) {
+    const int e = tid + 256 * c, pl = e / (J * 8), jj = (e / 8) % J, k8 = (e % 8) * 8;
+    const int64_t j = j0 + jj;
+    pv[c] = j < S ? *reinterpret_cast<const uint4*>(items3 + (int64_t)pl * n_items * D + j * stride * D + k8)
+                  : make_uint4(0u, 0u, 0u, 0u);
+  }
+  const float bb0 = tid < J && j0 + tid < S ? sbias[j0 + tid] : 0.0f;
+  bf16x8_t a[T][4];
+  {
+    const int64_t u = u0 + i < n_users ? u0 + i : n_users - 1;
+    const float* qp = q + u * D + 32 * h;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float4 x = ld4(qp + 8 * t), y = ld4(qp + 8 * t + 4);
+      const float v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int jv = 0; jv < 8; ++jv) {
+        __bf16 b0, b1, b2;
+        split3(v[jv], b0, b1, b2);
+        a[0][t][jv] = b0;
+        if (T > 1) a[T > 1 ? 1 : 0][t][jv] = b1;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CH / 256; ++c) {
+    const int e = tid + 256 * c, pl = e / (J * 8), jj = (e / 8) % J, k8 = (e % 8) * 8;
+    *reinterpret_cast<uint4*>(&ps[pl][jj][k8]) = pv[c];
+  }
+  if (tid < J) bs[tid] = bb0;
+  __syncthreads();
+#pragma unroll
+  for (int jt = 0; jt < J / 32; ++jt) {
+    f32x16 acc = {};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const bf16x8_t b0 = *reinterpret_cast<const bf16x8_t*>(&ps[0][32 * jt + i][32 * h + 8 * t]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][t], b0, acc, 0, 0, 0);
+      if (T > 1) {
+        const bf16x8_t b1 = *reinterpret_cast<const bf16x8_t*>(&ps[T > 1 ? 1 : 0][32 * jt + i][32 * h + 8 * t]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][t], b1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[T > 1 ? 1 : 0][t], b0, acc, 0, 0, 0);
+      }
+    }
+    const int64_t j = j0 + 32 * jt + i;
+    if (j < S) {
+      const float b = bs[32 * jt + i];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t u = u0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (u < n_users)
+          out[u * S + j] = __builtin_bit_cast(_Float16, __ocml_cvtrtn_f16_f32(acc[r] + b));
+      }
+    }
+  }
+}
+
 template <bool RS>
 __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user_list,
                                                 int64_t n_users, const uint32_t* __restrict__ count,
@@ -1177,6 +1286,52 @@ extern "C" int ncf_score_kth(const float* logits, int64_t n_users, int64_t S, in
                        S, K, item_bias, stride, thr);
   }
   NCF_CHECK_LAUNCH("ncf_score_kth");
+  return NCF_OK;
+}
+
+// The fp16 threshold sample of k_sample16 (bias included, rounded down) and its k-th (LDS-
+// resident fp16 rows: S <= kKthLdsMax).
+extern "C" int ncf_score_sample_split16(const float* queries, int64_t n_users,
+                                        const uint16_t* items3, int64_t n_items, int64_t dim,
+                                        int64_t stride, const float* sample_bias, int64_t S,
+                                        uint16_t* out, void* stream) {
+  NCF_CHECK_ARG(dim == 64, "ncf_score_sample_split16: dim must be 64");
+  NCF_CHECK_ARG(n_users >= 0 && S >= 1 && stride >= 1 && (S - 1) * stride < n_items &&
+                    queries && items3 && sample_bias && out,
+                "ncf_score_sample_split16: bad args");
+  if (n_users == 0) return NCF_OK;
+  hipLaunchKernelGGL(k_sample16<2>, dim3((unsigned)ncf_cdiv(S, 128), (unsigned)ncf_cdiv(n_users, 128)),
+                     dim3(256), 0, (hipStream_t)stream, queries, n_users, items3, n_items, stride,
+                     sample_bias, S, reinterpret_cast<_Float16*>(out));
+  NCF_CHECK_LAUNCH("ncf_score_sample_split16");
+  return NCF_OK;
+}
+
+extern "C" int ncf_score_kth16(const uint16_t* logits, int64_t n_users, int64_t S, int K,
+                               float* thr, void* stream) {
+  NCF_CHECK_ARG(n_users >= 0 && S >= 1 && S <= kKthLdsMax && K >= 1 && logits && thr,
+                "ncf_score_kth16: bad size");
+  if (n_users == 0) return NCF_OK;
+  static bool attr = false;
+  if (!attr) {
+    const int bytes = (int)(sizeof(_Float16) * kKthLdsMax);
+    if (hipFuncSetAttribute((const void*)k_kth_lds<512, _Float16>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_kth_lds<1024, _Float16>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) {
+      ncf_set_error("ncf_score_kth16: %d B of LDS refused", bytes);
+      return NCF_ERR_LAUNCH;
+    }
+    attr = true;
+  }
+  const _Float16* l = reinterpret_cast<const _Float16*>(logits);
+  if (S > 16384)
+    hipLaunchKernelGGL((k_kth_lds<1024, _Float16>), dim3((unsigned)n_users), dim3(1024),
+                       sizeof(_Float16) * S, (hipStream_t)stream, l, S, K, nullptr, 1, thr);
+  else
+    hipLaunchKernelGGL((k_kth_lds<512, _Float16>), dim3((unsigned)n_users), dim3(512),
+                       sizeof(_Float16) * S, (hipStream_t)stream, l, S, K, nullptr, 1, thr);
+  NCF_CHECK_LAUNCH("ncf_score_kth16");
   return NCF_OK;
 }
 

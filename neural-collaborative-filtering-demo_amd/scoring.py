@@ -143,6 +143,10 @@ SAMPLE_CANDS = int(os.environ.get("NCF_SCORE_CANDS", "1024"))
 # the split scan's item split raised from the expected candidates per user (A/B knob)
 SIZED_SPLIT = os.environ.get("NCF_SCORE_SIZED", "1") != "0"
 KTH_LDS_MAX = int(os.environ.get("NCF_SCORE_KTH_MAX", "38912"))   # <= score.hip kKthLdsMax
+# the threshold sample on bf16 matrix cores, fp16 logits rounded down (ncf_score_sample_split16 +
+# ncf_score_kth16, its k-th lowered by the two-term bound) instead of the fp32 sample GEMM +
+# fp32 k-th (NCF_SCORE_SAMPLE16=0, A/B); needs the split index (p3, pmax)
+SAMPLE16 = os.environ.get("NCF_SCORE_SAMPLE16", "1") != "0"
 
 
 def _select(idx, rows, n, run, k, out_s, out_i, overflow, st, terms=None):
@@ -184,7 +188,11 @@ class _TopKRun:
         self.sbias = index.bias[::self.stride][:self.S].contiguous()
         e = lambda *sh, dt=torch.float32: torch.empty(*sh, dtype=dt, device=dev)  # noqa: E731
         self.uid = e(max(n, 1), dt=torch.int64)
-        self.q, self.sample, self.thr = e(max(n, 1), D), e(max(n, 1), self.S), e(max(n, 1))
+        self.s16 = (SAMPLE16 and index.p3 is not None and index.pmax is not None
+                    and self.S <= KTH_LDS_MAX)
+        self.q, self.thr = e(max(n, 1), D), e(max(n, 1))
+        self.sample = (torch.empty(max(n, 1), self.S, dtype=torch.int16, device=dev) if self.s16
+                       else e(max(n, 1), self.S))
         self.count = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
         self.cand_l, self.cand_i = e(max(n, 1), cap), e(max(n, 1), cap, dt=torch.int32)
         self.overflow = e(max(n, 1), dt=torch.int32)
@@ -202,10 +210,18 @@ class _TopKRun:
                   ptr(model.mf_norm.weight), ptr(model.mf_norm.bias), LN_EPS,
                   ptr(model.mf_output.weight), ptr(model.final[0].weight), ptr(self.q),
                   ptr(self.err), st)
-        _lib.call("ncf_gemm_f32", n, self.S, D, ptr(self.q), D, 0, ptr(p), D * self.stride, 1,
-                  ptr(self.sample), self.S, ptr(self.sbias), 0, st)
-        _lib.call("ncf_score_kth", ptr(self.sample), n, self.S, k, None, self.stride,
-                  ptr(self.thr), st)
+        if self.s16:
+            _lib.call("ncf_score_sample_split16", ptr(self.q), n, ptr(idx.p3), I, D, self.stride,
+                      ptr(self.sbias), self.S, ptr(self.sample), st)
+            _lib.call("ncf_score_kth16", ptr(self.sample), n, self.S, k, ptr(self.thr), st)
+            # (the k-th of the fp16 sample is a bound after the two-term error is taken off)
+            _lib.call("ncf_score_margin", ptr(self.q), None, n, D, ptr(idx.pmax), MARGIN_C[2],
+                      ptr(self.thr), st)
+        else:
+            _lib.call("ncf_gemm_f32", n, self.S, D, ptr(self.q), D, 0, ptr(p), D * self.stride, 1,
+                      ptr(self.sample), self.S, ptr(self.sbias), 0, st)
+            _lib.call("ncf_score_kth", ptr(self.sample), n, self.S, k, None, self.stride,
+                      ptr(self.thr), st)
         self.count.zero_()
         # expected candidates per user: k x I / S (the threshold sample's k-th over S items)
         _collect(idx, ptr(self.q), None, n, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),

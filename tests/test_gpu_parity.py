@@ -1139,6 +1139,29 @@ def test_one_term_scan_equals_two_term_scan(k, cap):
     assert torch.equal(s1, s2)
 
 
+@pytest.mark.parametrize("k,cap", [(10, 8192), (100, 8192), (50, 256)])
+def test_fp16_threshold_sample_equals_fp32_sample(k, cap, monkeypatch):
+    """The threshold sample on bf16 matrix cores with fp16 logits rounded down
+    (ncf_score_sample_split16 + ncf_score_kth16, the k-th lowered by the two-term bound) against
+    the fp32 sample GEMM + fp32 k-th: only the thresholds differ (both are valid lower bounds of
+    the K-th largest logit), so the top-k items and scores are the same bits; cap = 256 at
+    k = 50 takes the overflow re-run."""
+    from ncf_amd import scoring
+    from ncf_amd.scoring import ItemIndex, score_topk
+    torch.manual_seed(17)
+    U, I = 5000, 100003
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    users = torch.randperm(U)[:700]
+    idx = ItemIndex(m)
+    monkeypatch.setattr(scoring, "SAMPLE16", True)
+    s16, i16 = score_topk(m, users, k=k, index=idx, cap=cap)
+    monkeypatch.setattr(scoring, "SAMPLE16", False)
+    s32, i32 = score_topk(m, users, k=k, index=idx, cap=cap)
+    assert torch.equal(i16, i32)
+    assert torch.equal(s16, s32)
+
+
 @pytest.mark.parametrize("k,terms", [(10, 2), (100, 2), (100, 3), (10, 1)])
 def test_split_scan_item_split_sizing_is_invisible(k, terms, monkeypatch):
     """The split scan's item split raised from the expected candidates per user (k x I / S, the
