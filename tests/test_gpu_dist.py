@@ -24,7 +24,7 @@ TABLES = {"mf_user": "mf_embedding_collection.embedding_bags.user_id.weight",
           "mlp_user": "mlp_embedding_collection.embedding_bags.user_id.weight",
           "mf_item": "mf_embedding_collection.embedding_bags.product_id.weight",
           "mlp_item": "mlp_embedding_collection.embedding_bags.product_id.weight"}
-STEPS = 3
+STEPS = 6   # (>= 6: the overlapped rolling sweep runs on the plan stream across several steps)
 
 
 def setup():
