@@ -85,9 +85,13 @@ int ncf_gather_ln_gmf_scaled_fwd(const int64_t* user_ids, const int64_t* item_id
                                  const float* mf_beta, const float* mlp_gamma,
                                  const float* mlp_beta, const float* mf_out_w,
                                  const float* mf_out_b, float eps, const float* item_scale,
-                                 float scale_factor, float* mf_pred, float* mlp_user_ln,
-                                 float* mlp_item_ln, float* mf_user_ln, float* mf_item_ln,
-                                 int* err_flag, void* stream);
+                                 float scale_factor, int64_t group_rows, float* mf_pred,
+                                 float* mlp_user_ln, float* mlp_item_ln, float* mf_user_ln,
+                                 float* mf_item_ln, int* err_flag, void* stream);
+/* group_rows = G > 1 (training, SURVEY fact 6: a group's rows hold one user): the LN'd user rows
+ * (mlp_user_ln, mf_user_ln) are written only for a group's first row and for rows whose user
+ * differs from that row's; every other row's are the first row's (readers: ncf_attn_block_* and
+ * ncf_mlp_bwd's head with the same user_ids / group_rows).  0 or 1: every row written. */
 
 /* Row gather (+ optional LayerNorm): EBC forward as read by callers (app.py:156-184) and
  * get_user_embeddings / get_product_embeddings (architecture.py:383-407).                   */
@@ -98,8 +102,9 @@ int ncf_gather_ln_gmf_bf16_fwd(const int64_t* user_ids, const int64_t* item_ids,
                                int64_t num_users, int64_t num_items, int64_t dim,
                                const float* mf_gamma, const float* mf_beta, const float* mlp_gamma,
                                const float* mlp_beta, const float* mf_out_w, const float* mf_out_b,
-                               float eps, float* mf_pred, float* mlp_user_ln, float* mlp_item_ln,
-                               float* mf_user_ln, float* mf_item_ln, int* err_flag, void* stream);
+                               float eps, int64_t group_rows, float* mf_pred, float* mlp_user_ln,
+                               float* mlp_item_ln, float* mf_user_ln, float* mf_item_ln,
+                               int* err_flag, void* stream);
 int ncf_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t rows,
                     int64_t dim, const float* ln_gamma, const float* ln_beta, float eps,
                     float* out, int* err_flag, void* stream);
@@ -237,7 +242,7 @@ int ncf_attn_block_bwd(const float* grad_y, const float* q, const float* k, cons
                        const float* xi, float* const* grad_params, float* workspace,
                        int64_t workspace_floats, ncf_reduce_list* defer, float* grad_q,
                        float* grad_k, float* grad_v, float* grad_xu, float* grad_xi,
-                       void* stream);
+                       const int64_t* user_ids, void* stream);
 /* The same backward (fused weight gradients) after a forward that stashed nothing: q, k, v are
  * re-projected from xu / xi (+ the biases) and the core forward (probabilities, o) is re-run in
  * LDS with the forward's own arithmetic (same bits), instead of reading q/k/v/o/probs from HBM.
@@ -312,6 +317,10 @@ typedef struct ncf_head_args {
   float* grad_final_b;
   float* loss;
   double loss_denominator;
+  /* optional: the batch's user ids and group size (the gather's group_rows): a row whose user is
+   * its group's first row's user reads mf_user_ln at that first row (NULL / <= 1: its own) */
+  const int64_t* user_ids;
+  int64_t group_rows;
 } ncf_head_args;
 int64_t ncf_mlp_bwd_workspace(int64_t n);
 int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, const float* x,

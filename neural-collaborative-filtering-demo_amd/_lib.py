@@ -44,9 +44,9 @@ SIGNATURES = {
     "ncf_gather_ln_gmf_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P, F32,
                                     P, P, P, P, P, P, P]),
     "ncf_gather_ln_gmf_scaled_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P,
-                                           F32, P, F32, P, P, P, P, P, P, P]),
+                                           F32, P, F32, I64, P, P, P, P, P, P, P]),
     "ncf_gather_ln_gmf_bf16_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P,
-                                         F32, P, P, P, P, P, P, P]),
+                                         F32, I64, P, P, P, P, P, P, P]),
     "ncf_gather_rows": (I32, [P, I64, P, I64, I64, P, P, F32, P, P, P]),
     "ncf_gemm_f32": (I32, [I64, I64, I64, P, I64, I32, P, I64, I32, P, I64, P, I32, P]),
     "ncf_gemm_splitk_workspace": (I64, [I64, I64, I32]),
@@ -82,7 +82,7 @@ SIGNATURES = {
     "ncf_attn_block_bwd_rc": (I32, [P, P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, F32, U64, P,
                                     P, P, I64, P, P, P, P, P]),
     "ncf_attn_block_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, P, P, P, P, F32, U64, P, P,
-                                 P, P, P, P, I64, P, P, P, P, P, P, P]),
+                                 P, P, P, P, I64, P, P, P, P, P, P, P, P]),
     "ncf_relu_ln_dropout_fwd": (I32, [P, I64, I64, P, P, F32, F32, U64, P, P, P, P, P]),
     "ncf_relu_ln_dropout_bwd_workspace": (I64, [I64, I64]),
     "ncf_relu_ln_dropout_bwd": (I32, [P, P, P, P, P, I64, I64, F32, U64, P, P, P, P, P, P, I64,
@@ -197,7 +197,7 @@ class HeadArgs(ctypes.Structure):
                                  "grad_mf_user_ln", "grad_mf_item_ln", "grad_mlp_out_w",
                                  "grad_mlp_out_b", "grad_mf_out_w", "grad_mf_out_b",
                                  "grad_final_w", "grad_final_b", "loss")] + \
-        [("loss_denominator", ctypes.c_double)]
+        [("loss_denominator", ctypes.c_double), ("user_ids", P), ("group_rows", I64)]
 
 
 class TablePair(ctypes.Structure):

@@ -129,6 +129,38 @@ __device__ __forceinline__ bool ids_uniform(const int64_t* __restrict__ uid, int
   return __syncthreads_or(diff) == 0;
 }
 
+// The row holding row r's LayerNorm'd user row: with group_rows = M the gather
+// (ncf_gather_ln_gmf_scaled_fwd) writes it only for a group's first row and for rows whose user
+// differs from that row's; the others read the group's first row (the same bits).  (r < rows;
+// the workgroup's rows start at a group boundary.)
+__device__ __forceinline__ int src_row(const int64_t* __restrict__ uid, int r, int M) {
+  if (!uid || M <= 1) return r;
+  const int f = r - r % M;
+  return (r == f || uid[r] != uid[f]) ? r : f;
+}
+
+// Rp rows of X_u into S (rows >= `rows` zero), each from its source row (src_row), every load in
+// flight before the first LDS store
+template <int D>
+__device__ __forceinline__ void stage_in_src(float* __restrict__ S, const float* __restrict__ X,
+                                             const int64_t* __restrict__ uid, int M, int Rp,
+                                             int rows) {
+  constexpr int L4 = D / 4, P = AG<D>::kPitch;
+  constexpr int IT = (16 * AG<D>::NTmax * L4 + kThreads - 1) / kThreads;
+  float4 v[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int e = threadIdx.x + kThreads * it, r = e / L4, c = (e % L4) * 4;
+    v[it] = (e < Rp * L4 && r < rows) ? ld4(X + (int64_t)src_row(uid, r, M) * D + c)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int e = threadIdx.x + kThreads * it;
+    if (e < Rp * L4) *reinterpret_cast<float4*>(S + (e / L4) * P + (e % L4) * 4) = v[it];
+  }
+}
+
 // group gl's first row (row gl M of X) -> row gl of Y, for the G groups of the workgroup
 template <int D>
 __device__ __forceinline__ void gather_group_rows(float* __restrict__ Y, const float* __restrict__ X,
@@ -386,7 +418,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
     const float* __restrict__ wo, const float* __restrict__ bo, float scale, float p_drop,
     uint64_t seed, const ncf_step_clock* clock, float* __restrict__ Q, float* __restrict__ K,
     float* __restrict__ V, float* __restrict__ P, float* __restrict__ O, float* __restrict__ Y,
-    int core, const int64_t* __restrict__ uids) {
+    int core, const int64_t* __restrict__ uids, int share_q) {
   using G = AG<D>;
   constexpr int kPitch = G::kPitch;
   extern __shared__ float lds[];
@@ -417,7 +449,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
       const int e = threadIdx.x + kThreads * it, r = e / L4, c = (e % L4) * 4;
       vi[it] = (e < Rp * L4 && r < rows) ? ld4(xi + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if (core && M > 1 && uids) shq = ids_uniform(uids + r0, ng, M);
+    if (share_q && core && M > 1 && uids) shq = ids_uniform(uids + r0, ng, M);
     if (shq) {
       for (int e = threadIdx.x; e < G::kGroups * L4; e += kThreads) {
         const int gl = e / L4, c = (e % L4) * 4;
@@ -425,9 +457,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
         *reinterpret_cast<float4*>(S2 + gl * kPitch + c) = v;
       }
     } else if (core) {
-      float* const dst[1] = {S0};
-      const float* const src[1] = {xu + r0 * D};
-      stage_in_n<D, 1>(dst, src, Rp, rows);
+      stage_in_src<D>(S0, xu + r0 * D, uids ? uids + r0 : nullptr, M, Rp, rows);
     }
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
@@ -529,7 +559,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     const float* __restrict__ Xi, float* __restrict__ part, float* __restrict__ dQ,
     float* __restrict__ dK, float* __restrict__ dV, float* __restrict__ dXu,
     float* __restrict__ dXi, const float* __restrict__ bq, const float* __restrict__ bk,
-    const float* __restrict__ bv, const int64_t* __restrict__ uids) {
+    const float* __restrict__ bv, const int64_t* __restrict__ uids, int share_q) {
   using G = AG<D>;
   constexpr int kPitch = G::kPitch, kGroups = G::kGroups, kLinW = G::kLinW, L4 = D / 4;
   constexpr int H = D / HD;
@@ -573,7 +603,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
         v0[it] = in ? ld4(dY + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
         v2[it] = in ? ld4(Xi + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      if (M > 1 && uids) shq = ids_uniform(uids + r0, ng, M);
+      if (share_q && M > 1 && uids) shq = ids_uniform(uids + r0, ng, M);
       if (shq) {
         for (int e = threadIdx.x; e < kGroups * L4; e += kThreads) {
           const int gl = e / L4, c = (e % L4) * 4;
@@ -581,9 +611,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
           *reinterpret_cast<float4*>(S3 + gl * kPitch + c) = v;
         }
       } else {
-        float* const dst[1] = {S1};
-        const float* const src[1] = {Xu + r0 * D};
-        stage_in_n<D, 1>(dst, src, Rp, rows);
+        stage_in_src<D>(S1, Xu + r0 * D, uids ? uids + r0 : nullptr, M, Rp, rows);
       }
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
@@ -665,7 +693,8 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     for (int q = 0; q < kPre; ++q) {
       const int e = threadIdx.x + kThreads * q, r = e / L4, c = (e % L4) * 4;
       const bool in = e < Rp * L4 && r < rows;
-      pu[q] = in ? ld4(Xu + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      pu[q] = in ? ld4(Xu + (r0 + src_row(uids ? uids + r0 : nullptr, r, M)) * D + c)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
       pi[q] = in ? ld4(Xi + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
@@ -951,7 +980,8 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
   // the core runs unless the eval form applies (M == 1 without dropout: softmax == 1, o = v);
   // without q/k it stashes nothing (training with ncf_attn_block_bwd_rc)
   const int core = (q != nullptr || group_len > 1 || dropout_p > 0.0f) ? 1 : 0;
-  const int64_t* uids = share_ids(user_ids);
+  const int share_q = share_ids(user_ids) != nullptr;
+  const int64_t* uids = user_ids;   // (also the source rows of X_u: src_row)
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len;
   const size_t lds = fwd_lds_d((int)dim, M);
@@ -964,7 +994,7 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
     if (!attr) { allow_lds(k_attn_block_fwd<D_, HD>, fwd_lds<D_>(kMaxM)); attr = true; }         \
     hipLaunchKernelGGL((k_attn_block_fwd<D_, HD>), grid, dim3(kThreads), lds, st, xu, xi, groups, \
                        M, wq, bq, wk, bk, wv, bv, wo, bo, scale, dropout_p, seed, clock, q, k, v, \
-                       probs, o, y, core, uids);                                                 \
+                       probs, o, y, core, uids, share_q);                                        \
   }
   NCF_ABF(64, 8)
   NCF_ABF(64, 16)
@@ -1038,7 +1068,7 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
                                   float* const* grad_params, float* workspace,
                                   int64_t workspace_floats, ncf_reduce_list* defer,
                                   float* grad_q, float* grad_k, float* grad_v, float* grad_xu,
-                                  float* grad_xi, void* stream) {
+                                  float* grad_xi, const int64_t* user_ids, void* stream) {
   NCF_CHECK_ARG(groups >= 0 && ncf_attn_block_supported(dim, heads, group_len),
                 "ncf_attn_block_bwd: unsupported shape (D=%lld H=%lld M=%lld; need D=64 or 128, "
                 "M<=%d)", (long long)dim, (long long)heads, (long long)group_len, kMaxM);
@@ -1066,7 +1096,7 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
     if (!attr) { allow_lds(k_attn_block_bwd<D_, HD, false>, bwd_lds<D_>(kMaxM, D_ / HD, true)); attr = true; } \
     hipLaunchKernelGGL((k_attn_block_bwd<D_, HD, false>), grid, dim3(kThreads), lds, st, grad_y, q, k, \
                        v, probs, groups, M, wq, wk, wv, wo, scale, dropout_p, seed, clock, o, xu, xi, \
-                       part, grad_q, grad_k, grad_v, grad_xu, grad_xi, nullptr, nullptr, nullptr, nullptr); \
+                       part, grad_q, grad_k, grad_v, grad_xu, grad_xi, nullptr, nullptr, nullptr, user_ids, 0); \
   }
   NCF_ABB(64, 8)
   NCF_ABB(64, 16)
@@ -1115,7 +1145,8 @@ extern "C" int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const
                 (long long)group_len, (long long)heads);
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len, H = (int)heads;
-  const int64_t* uids = share_ids(user_ids);
+  const int share_q = share_ids(user_ids) != nullptr;
+  const int64_t* uids = user_ids;
   const size_t lds = bwd_lds_d((int)dim, M, H, true, true);
   const int nb = (int)ncf_cdiv(groups, groups_per_wg(dim));
   const dim3 grid((unsigned)nb);
@@ -1128,7 +1159,7 @@ extern "C" int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const
     hipLaunchKernelGGL((k_attn_block_bwd<D_, HD, true>), grid, dim3(kThreads), lds, st, grad_y,     \
                        nullptr, nullptr, nullptr, nullptr, groups, M, wq, wk, wv, wo, scale,       \
                        dropout_p, seed, clock, nullptr, xu, xi, workspace, nullptr, nullptr,       \
-                       nullptr, grad_xu, grad_xi, bq, bk, bv, uids);                               \
+                       nullptr, grad_xu, grad_xi, bq, bk, bv, uids, share_q);                      \
   }
   NCF_ABR(64, 8)
   NCF_ABR(64, 16)

@@ -45,18 +45,23 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
     const float* __restrict__ w_mf, const float* __restrict__ bias_mf, float eps,
     float* __restrict__ mf_pred, float* __restrict__ u_mlp_ln, float* __restrict__ i_mlp_ln,
     float* __restrict__ u_mf_ln, float* __restrict__ i_mf_ln, int* err,
-    const float* __restrict__ item_scale, float scale_factor) {
+    const float* __restrict__ item_scale, float scale_factor, int64_t G) {
   constexpr int L = D / 4;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t row = t / L;
   const int sub = (int)(t % L);
   if (row >= n) return;  // whole groups retire together
-  const int64_t u = safe_id(uid[row], nU, err, sub == 0);
+  const int64_t uraw = uid[row];
+  const int64_t u = safe_id(uraw, nU, err, sub == 0);
   const int64_t i = safe_id(iid[row], nI, err, sub == 0);
+  // G > 1 (groups of G rows, fact 6): a row whose user is its group's first row's user is that
+  // row's copy — its LN'd user rows are not written (the readers take the group's first row,
+  // ncf_src_row); only source rows load the user's MLP row
+  const bool src = G <= 1 || row % G == 0 || uraw != uid[row - row % G];
   const int c = sub * 4;
   // (BF: the table rows are bf16; widened exactly to fp32 here, everything after is fp32)
   const float4 xu_mf = ldp4<BF>(mfU, u * D + c), xi_mf = ldp4<BF>(mfI, i * D + c);
-  const float4 xu_ml = ldp4<BF>(mlpU, u * D + c), xi_ml = ldp4<BF>(mlpI, i * D + c);
+  const float4 xi_ml = ldp4<BF>(mlpI, i * D + c);
   const float4 gm = ld4(g_mf + c), bm = ld4(b_mf + c), gl = ld4(g_mlp + c), bl = ld4(b_mlp + c);
   const float4 yu = RowLN<D>::ln(xu_mf, gm, bm, eps);
   float4 yi = RowLN<D>::ln(xi_mf, gm, bm, eps);
@@ -72,9 +77,12 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
   float dot = yu.x * yi.x * w.x + yu.y * yi.y * w.y + yu.z * yi.z * w.z + yu.w * yi.w * w.w;
   dot = group_sum<L>(dot);
   if (sub == 0) mf_pred[row] = dot + bias_mf[0];
-  st4(u_mlp_ln + row * D + c, RowLN<D>::ln(xu_ml, gl, bl, eps));
+  if (src) {   // (uniform in the row's lane group: its shuffles stay within active lanes)
+    const float4 xu_ml = ldp4<BF>(mlpU, u * D + c);
+    st4(u_mlp_ln + row * D + c, RowLN<D>::ln(xu_ml, gl, bl, eps));
+    if (u_mf_ln) st4(u_mf_ln + row * D + c, yu);
+  }
   st4(i_mlp_ln + row * D + c, zi);
-  if (u_mf_ln) st4(u_mf_ln + row * D + c, yu);
   if (i_mf_ln) st4(i_mf_ln + row * D + c, yi);
 }
 
@@ -111,11 +119,11 @@ int launch_gather_ln_gmf(const int64_t* uid, const int64_t* iid, int64_t n, cons
                          const float* b_mlp, const float* w_mf, const float* bias_mf, float eps,
                          float* mf_pred, float* u_mlp_ln, float* i_mlp_ln, float* u_mf_ln,
                          float* i_mf_ln, int* err, const float* item_scale, float scale_factor,
-                         hipStream_t st) {
+                         int64_t G, hipStream_t st) {
   const int64_t threads = n * (D / 4);
   hipLaunchKernelGGL((k_gather_ln_gmf<D, BF>), dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st, uid, iid,
                      n, mfU, mfI, mlpU, mlpI, nU, nI, g_mf, b_mf, g_mlp, b_mlp, w_mf, bias_mf, eps,
-                     mf_pred, u_mlp_ln, i_mlp_ln, u_mf_ln, i_mf_ln, err, item_scale, scale_factor);
+                     mf_pred, u_mlp_ln, i_mlp_ln, u_mf_ln, i_mf_ln, err, item_scale, scale_factor, G);
   NCF_CHECK_LAUNCH("ncf_gather_ln_gmf_fwd");
   return NCF_OK;
 }
@@ -151,10 +159,10 @@ int launch_gather_ln_gmf_bf16(const int64_t* uid, const int64_t* iid, int64_t n,
                               const float* b_mlp, const float* w_mf, const float* bias_mf,
                               float eps, float* mf_pred, float* u_mlp_ln, float* i_mlp_ln,
                               float* u_mf_ln, float* i_mf_ln, int* err, const float* item_scale,
-                              float scale_factor, hipStream_t st) {
+                              float scale_factor, int64_t G, hipStream_t st) {
   return launch_gather_ln_gmf<D, true>(uid, iid, n, mfU, mfI, mlpU, mlpI, nU, nI, g_mf, b_mf, g_mlp,
                                        b_mlp, w_mf, bias_mf, eps, mf_pred, u_mlp_ln, i_mlp_ln,
-                                       u_mf_ln, i_mf_ln, err, item_scale, scale_factor, st);
+                                       u_mf_ln, i_mf_ln, err, item_scale, scale_factor, G, st);
 }
 
 #define NCF_DISPATCH_D(D, FN, ...)                                            \
@@ -173,9 +181,10 @@ extern "C" int ncf_gather_ln_gmf_scaled_fwd(
     const float* mf_item, const float* mlp_user, const float* mlp_item, int64_t num_users,
     int64_t num_items, int64_t dim, const float* mf_gamma, const float* mf_beta,
     const float* mlp_gamma, const float* mlp_beta, const float* mf_out_w, const float* mf_out_b,
-    float eps, const float* item_scale, float scale_factor, float* mf_pred, float* mlp_user_ln,
-    float* mlp_item_ln, float* mf_user_ln, float* mf_item_ln, int* err_flag, void* stream) {
-  NCF_CHECK_ARG(n >= 0, "ncf_gather_ln_gmf_fwd: n < 0");
+    float eps, const float* item_scale, float scale_factor, int64_t group_rows, float* mf_pred,
+    float* mlp_user_ln, float* mlp_item_ln, float* mf_user_ln, float* mf_item_ln, int* err_flag,
+    void* stream) {
+  NCF_CHECK_ARG(n >= 0 && group_rows >= 0, "ncf_gather_ln_gmf_fwd: n < 0");
   if (n == 0) return NCF_OK;
   NCF_CHECK_ARG(user_ids && item_ids && mf_user && mf_item && mlp_user && mlp_item && mf_pred &&
                     mlp_user_ln && mlp_item_ln && mf_gamma && mf_beta && mlp_gamma && mlp_beta &&
@@ -184,7 +193,7 @@ extern "C" int ncf_gather_ln_gmf_scaled_fwd(
   NCF_DISPATCH_D(dim, launch_gather_ln_gmf, user_ids, item_ids, n, mf_user, mf_item, mlp_user,
                  mlp_item, num_users, num_items, mf_gamma, mf_beta, mlp_gamma, mlp_beta, mf_out_w,
                  mf_out_b, eps, mf_pred, mlp_user_ln, mlp_item_ln, mf_user_ln, mf_item_ln,
-                 err_flag, item_scale, scale_factor, (hipStream_t)stream);
+                 err_flag, item_scale, scale_factor, group_rows, (hipStream_t)stream);
 }
 
 extern "C" int ncf_gather_ln_gmf_fwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
@@ -199,7 +208,7 @@ extern "C" int ncf_gather_ln_gmf_fwd(const int64_t* user_ids, const int64_t* ite
                                      void* stream) {
   return ncf_gather_ln_gmf_scaled_fwd(user_ids, item_ids, n, mf_user, mf_item, mlp_user, mlp_item,
                                       num_users, num_items, dim, mf_gamma, mf_beta, mlp_gamma,
-                                      mlp_beta, mf_out_w, mf_out_b, eps, nullptr, 0.0f, mf_pred,
+                                      mlp_beta, mf_out_w, mf_out_b, eps, nullptr, 0.0f, 0, mf_pred,
                                       mlp_user_ln, mlp_item_ln, mf_user_ln, mf_item_ln, err_flag,
                                       stream);
 }
@@ -236,9 +245,9 @@ extern "C" int ncf_gather_ln_gmf_bf16_fwd(
     const uint16_t* mf_item, const uint16_t* mlp_user, const uint16_t* mlp_item, int64_t num_users,
     int64_t num_items, int64_t dim, const float* mf_gamma, const float* mf_beta,
     const float* mlp_gamma, const float* mlp_beta, const float* mf_out_w, const float* mf_out_b,
-    float eps, float* mf_pred, float* mlp_user_ln, float* mlp_item_ln, float* mf_user_ln,
-    float* mf_item_ln, int* err_flag, void* stream) {
-  NCF_CHECK_ARG(n >= 0, "ncf_gather_ln_gmf_bf16_fwd: n < 0");
+    float eps, int64_t group_rows, float* mf_pred, float* mlp_user_ln, float* mlp_item_ln,
+    float* mf_user_ln, float* mf_item_ln, int* err_flag, void* stream) {
+  NCF_CHECK_ARG(n >= 0 && group_rows >= 0, "ncf_gather_ln_gmf_bf16_fwd: n < 0");
   if (n == 0) return NCF_OK;
   NCF_CHECK_ARG(user_ids && item_ids && mf_user && mf_item && mlp_user && mlp_item && mf_pred &&
                     mlp_user_ln && mlp_item_ln && mf_gamma && mf_beta && mlp_gamma && mlp_beta &&
@@ -251,5 +260,5 @@ extern "C" int ncf_gather_ln_gmf_bf16_fwd(
   NCF_DISPATCH_D(dim, launch_gather_ln_gmf_bf16, user_ids, item_ids, n, t0, t1, t2, t3, num_users,
                  num_items, mf_gamma, mf_beta, mlp_gamma, mlp_beta, mf_out_w, mf_out_b, eps,
                  mf_pred, mlp_user_ln, mlp_item_ln, mf_user_ln, mf_item_ln, err_flag, nullptr,
-                 0.0f, (hipStream_t)stream);
+                 0.0f, group_rows, (hipStream_t)stream);
 }

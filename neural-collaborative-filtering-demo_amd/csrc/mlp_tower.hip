@@ -783,10 +783,15 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
         ld_rs[pass] = L2.rstd[row];
         ld_x[pass] = ld4(L2.r + row * N2 + col);
       }
+      int64_t urow = row;   // (the gather's source row of this row's LN'd user row)
+      if (h.user_ids && h.group_rows > 1) {
+        const int64_t f = row - row % h.group_rows;
+        if (row != f && h.user_ids[row] == h.user_ids[f]) urow = f;
+      }
 #pragma unroll
       for (int c = 0; c < CM; ++c) {
         const int64_t o = row * K0 + 64 * c + col;
-        ld_u[pass][c] = ld4(h.mf_user_ln + o);
+        ld_u[pass][c] = ld4(h.mf_user_ln + urow * K0 + 64 * c + col);
         ld_it[pass][c] = ld4(h.mf_item_ln + o);
       }
     }

@@ -421,6 +421,7 @@ class ShardedTrainStep:
             h = w.cache.get("head_args")
             if h is not None:
                 h.targets, h.grad_prob = ptr(targets), None
+                h.user_ids = ptr(plan.extra["set"]["inv"][0])   # (this step's mini-table ids)
         scalars = (own["token"], own["nmax"], max(nu, ni))
         if next is not None and (not next[0].is_contiguous() or not next[1].is_contiguous()
                                  or next[0].dtype != torch.int64 or next[1].dtype != torch.int64):

@@ -25,6 +25,10 @@ from ._lib import ptr
 LN_EPS = 1e-5
 # bf16 configuration: the fused MLP tower's Linears on bf16 MFMA (NCF_BF16_MM=0: fp32 MFMA, A/B)
 BF16_MM = os.environ.get("NCF_BF16_MM", "1") != "0"
+# SURVEY fact 6 (a training group's M rows hold one user): the gather writes the LN'd user rows
+# once per group (group_rows = M) when every reader takes the group's row — the fused attention
+# block and the fused tower's head backward (NCF_GROUP_ROWS=0: every row, A/B; the same bits)
+GROUP_ROWS = os.environ.get("NCF_GROUP_ROWS", "1") != "0"
 _WGRAD_ROWS = int(os.environ.get("NCF_WGRAD_ROWS", "160"))
 
 
@@ -418,19 +422,22 @@ class NCFEngine:
             raise ValueError("the temporal (hour) path is forward_simple's: eval, one item per group")
         # a2-a4: 4 gathers + mf_norm/mlp_norm + GMF  (architecture.py:286-287, 305-312)
         t_scale, t_factor = (temporal[0], temporal[1]) if temporal is not None else (None, 0.0)
+        G = M if (GROUP_ROWS and train and M > 1 and temporal is None and self.attn_block(D, H, M)
+                  and self.mlp_fused(D, hid)) else 0
+        w.group_rows = G
         if bf16:    # bf16 tables (``tables`` holds them): rows widened to fp32 in the gather
             if temporal is not None:
                 raise ValueError("the bf16-table configuration is a training configuration")
             _lib.call("ncf_gather_ln_gmf_bf16_fwd", ptr(uid), ptr(iid), n, *tbp, n_users,
                       n_items, D, pp["mf_norm.weight"], pp["mf_norm.bias"],
                       pp["mlp_norm.weight"], pp["mlp_norm.bias"], pp["mf_output.weight"],
-                      pp["mf_output.bias"], LN_EPS, ptr(w.mf_pred), ptr(w.xu), ptr(w.xi),
+                      pp["mf_output.bias"], LN_EPS, G, ptr(w.mf_pred), ptr(w.xu), ptr(w.xi),
                       ptr(w.umf), ptr(w.imf), ptr(w.err), st)
         else:
             _lib.call("ncf_gather_ln_gmf_scaled_fwd", ptr(uid), ptr(iid), n, *tbp, n_users,
                       n_items, D, pp["mf_norm.weight"], pp["mf_norm.bias"],
                       pp["mlp_norm.weight"], pp["mlp_norm.bias"], pp["mf_output.weight"],
-                      pp["mf_output.bias"], LN_EPS, ptr(t_scale), float(t_factor),
+                      pp["mf_output.bias"], LN_EPS, ptr(t_scale), float(t_factor), G,
                       ptr(w.mf_pred), ptr(w.xu), ptr(w.xi), ptr(w.umf), ptr(w.imf), ptr(w.err), st)
         # a5: MultiHeadAttention over each group of M rows (architecture.py:315-326)
         att = m.user_product_attention
@@ -694,6 +701,8 @@ class NCFEngine:
                 h.grad_final_w, h.grad_final_b = ptr(gv("final.0.weight")), ptr(gv("final.0.bias"))
             h.prob, h.grad_prob, h.targets, h.loss = ptr(w.prob), ptr(gp), ptr(tg), ptr(w.loss)
             h.loss_denominator = float(loss_denominator)
+            # (the gather's source rows of the LN'd user rows: ncf_head_args.user_ids)
+            h.user_ids, h.group_rows = ptr(uid), getattr(w, "group_rows", 0)
             _lib.call("ncf_mlp_bwd_bf16" if bf16 and BF16_MM else "ncf_mlp_bwd", None, n, D,
                       ptr(w.y), addr,
                       len(hid), haddr, drop_p, seed,
@@ -762,7 +771,7 @@ class NCFEngine:
                           n // M, M, H, D, *pp["att_w"], drop_p, seed,
                           ptr(self.clock), ptr(w.o), ptr(w.xu), ptr(w.xi), gp[1], ptr(ws),
                           ws.numel(), w.red_list.address, None, None, None, ptr(w.dxu),
-                          ptr(w.dxi), st)
+                          ptr(w.dxi), ptr(uid), st)
         else:
             self._attention_bwd_unfused(w, drop_p, seed, joins, st)
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)

@@ -178,8 +178,8 @@ class StepTapes:
             w.red_list.count = 0
             w.wgrads = []
             h = w.cache.get("head_args")
-            if h is not None:         # (the loss gradient's address, read by ncf_mlp_bwd)
-                h.grad_prob = gp.data_ptr()
+            if h is not None:         # (the loss gradient's and the ids' addresses: ncf_mlp_bwd)
+                h.grad_prob, h.user_ids = gp.data_ptr(), uid.data_ptr()
             e.bwd.replay((uid.data_ptr(), iid.data_ptr(), gp.data_ptr(), st))
             owed, joined = e.bwd_post
             d._owed, d._joined = list(owed), joined

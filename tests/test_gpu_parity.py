@@ -787,6 +787,49 @@ def test_overlapped_sweep_bitwise_equals_dense(monkeypatch, graph, fork):
         assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
 
 
+@pytest.mark.parametrize("mixed", [False, True])
+def test_group_rows_bitwise_equals_every_row(monkeypatch, mixed):
+    """The gather writing each group's LN'd user rows once (group_rows = M; the
+    attention block and the tower's head backward reading the group's row) against every row
+    written: parameters and Adam moments bit-identical over 6 FusedTrainStep steps and one
+    reference-call-pattern step.  ``mixed``: a third of the groups hold several users (those rows
+    are their own source rows) and the last workgroup is ragged."""
+    from ncf_amd import engine as E
+    from ncf_amd.trainer import FusedTrainStep
+    U, I, B, M = 3000, 500, 61, 5
+    g = torch.Generator().manual_seed(23)
+    batches = []
+    for _ in range(6):
+        u = torch.randint(0, U, (B,), generator=g).repeat_interleave(M)
+        if mixed:
+            pick = torch.rand(B * M, generator=g) < 0.1
+            u = torch.where(pick & (torch.arange(B * M) % M != 0),
+                            torch.randint(0, U, (B * M,), generator=g), u)
+        i = torch.randint(0, I, (B * M,), generator=g)
+        t = torch.zeros(B, M)
+        t[:, 0] = 1
+        batches.append((u.to(DEV), i.to(DEV), t.reshape(-1, 1).to(DEV)))
+    out = []
+    for on in (True, False):
+        monkeypatch.setattr(E, "GROUP_ROWS", on)
+        torch.manual_seed(24)
+        m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.2, M - 1).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+        for u, i, t in batches:
+            step(u, i, t)
+        ws = next(iter(m.engine.ws.values()))
+        assert ws.group_rows == (M if on else 0)
+        step.sync()
+        out.append(({k: v.detach().cpu().clone() for k, v in m.state_dict().items()},
+                    {k: (v["exp_avg"].cpu().clone(), v["exp_avg_sq"].cpu().clone())
+                     for k, v in step.state.items()}))
+    for k in out[0][0]:
+        assert torch.equal(out[0][0][k], out[1][0][k]), k
+    for k in out[0][1]:
+        assert torch.equal(out[0][1][k][0], out[1][1][k][0]), k
+        assert torch.equal(out[0][1][k][1], out[1][1][k][1]), k
+
+
 def test_graph_replay_bitwise_equals_eager_clock():
     """hipGraph capture + replay of the whole training step (dropout on: the per-step stream
     comes from the device clock) == the same clock-driven steps run eagerly, bit for bit, across
