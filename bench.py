@@ -927,14 +927,21 @@ def main():
     #           table rows (LN recompute) in and 2 compact gradient rows out = N (16 D + 16) +
     #           (n_u + n_i) 16 D
     nu_ni = None
+    grows = 0
     try:
         ws_any = next(iter(model.engine.ws.values()))
         nu_ni = [int(x) for x in ws_any.num_unique.cpu().tolist()]
+        grows = int(getattr(ws_any, "group_rows", 0))
     except Exception:
         pass
+    # gather with group_rows = M (fact 6: a group's user rows read and LN'd rows written once):
+    # per row the item MF + MLP rows in and out, ids, mf_pred; per group the user's two rows in
+    # and out.  Every row written (group_rows 0): the four rows in and out per row.
+    g_bytes = (N * (16 * D + 20) + (N // grows) * 16 * D if grows > 1
+               else N * (16 * D + 16 + 16 * D + 4))
     hbm = {}
     for name, kern, nbytes in (
-            ("gather", "ncf_gather_ln_gmf_scaled_fwd", N * (16 * D + 16 + 16 * D + 4)),
+            ("gather", "ncf_gather_ln_gmf_scaled_fwd", g_bytes),
             ("scatter", "ncf_embedding_bwd_reduce",
              N * (16 * D + 16) + (sum(nu_ni) * 16 * D if nu_ni else 0))):
         if kern in totals:
@@ -947,6 +954,9 @@ def main():
                          "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS,
                          "frac": round(gbs / HBM_PEAK_GBS, 4),
                          "traffic": pm["bytes_per_launch"] if pm else None}
+    if "gather" in hbm:
+        hbm["gather"]["group_rows"] = grows
+        hbm["gather"]["round3_count_bytes"] = N * (16 * D + 16 + 16 * D + 4)
     if "scatter" in hbm:
         hbm["scatter"]["unique_rows"] = nu_ni
         hbm["scatter"]["note"] = ("segment reduce + LN backward only; the id sort before it "
