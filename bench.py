@@ -466,9 +466,13 @@ def c4_train(ncf, dev, warmup, steps, prime=0):
             step(u, i, t)
         torch.cuda.synchronize()
         prof, L.PROFILE = L.PROFILE, None
-        dfr.overlap = True
         for name, _, e0, e1 in prof:
             iso[name] = iso.get(name, 0.0) + e0.elapsed_time(e1) / 10
+        # the table Adam's exact work from the stamps (sweep on the step's stream)
+        acct = table_adam_accounting(step, batches, prime + warmup + steps + 30, 4, dfr, D)
+        dfr.overlap = True
+    else:
+        acct = None
     lin = ("ncf_attn_block_fwd", "ncf_attn_block_bwd", "ncf_mlp_fwd", "ncf_mlp_bwd",
            "ncf_gemm_rows", "ncf_gemm_f32", "ncf_wgrad_grouped", "ncf_relu_ln_dropout_fwd",
            "ncf_relu_ln_dropout_bwd", "ncf_attention_fwd", "ncf_attention_bwd")
@@ -487,7 +491,8 @@ def c4_train(ncf, dev, warmup, steps, prime=0):
                k: round(v, 4) for k, v in sorted(iso.items(), key=lambda x: -x[1])},
            "linear_ms_per_step": round(sum(v for k, v in iso.items() if k in lin), 4),
            "linear_kernels": "fused attention block + fused MLP tower (D = 128)"
-           if "ncf_attn_block_fwd" in iso and "ncf_mlp_fwd" in iso else "unfused"}
+           if "ncf_attn_block_fwd" in iso and "ncf_mlp_fwd" in iso else "unfused",
+           "table_adam_roofline": table_adam_roofline(acct, D) if acct else None}
     del step, model, batches
     torch.cuda.empty_cache()
     return out
