@@ -15,10 +15,8 @@
 //                      sum_n LNbwd(dy_n) == sum_pieces LNbwd(sum_piece dy_n): a hot id (a Zipf
 //                      head item with hundreds of occurrences) is spread over many groups instead
 //                      of serialising one.  dgamma/dbeta partials per block.
-//   multi-piece segments: every piece's group, once its rows are stored, counts itself in
-//                      (one atomic per piece, pcnt[segment]); the group that completes the count
-//                      adds the extra pieces to the first piece's rows in piece order (the
-//                      order, and so the bits, of a separate fix-up pass; no second launch).
+//   k_piece_fixup      adds the extra pieces of multi-piece segments to the first piece's row in
+//                      piece order.
 // Output per kind: compact grads [num_unique, D] for the GMF and MLP tables of that kind.
 // Deterministic: every sum has a fixed order.
 #include "segments.h"
@@ -30,13 +28,11 @@ namespace {
 // part[kind*nbr + block][0:D mf_g | D:2D mf_b | 2D:3D mlp_g | 3D:4D mlp_b]
 constexpr int kPW = NCF_PIECE_WAVES;   // waves per block
 template <int D, bool BF = false>
-__global__ __launch_bounds__(64 * kPW) __attribute__((amdgpu_waves_per_eu(4))) void k_piece_reduce_ln(
+__global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     const uint32_t* __restrict__ sv0, const uint32_t* __restrict__ sv1,
     const uint32_t* __restrict__ pstart0, const uint32_t* __restrict__ pstart1,
     const uint32_t* __restrict__ pseg0, const uint32_t* __restrict__ pseg1,
     const int64_t* __restrict__ uniq0, const int64_t* __restrict__ uniq1,
-    const uint32_t* __restrict__ fpiece0, const uint32_t* __restrict__ fpiece1,
-    uint32_t* __restrict__ pcnt0, uint32_t* __restrict__ pcnt1,
     const uint32_t* __restrict__ totals, const float* __restrict__ dy_mf0,
     const float* __restrict__ dy_mlp0, const float* __restrict__ dy_mf1,
     const float* __restrict__ dy_mlp1, const float* __restrict__ t_mf0,
@@ -53,8 +49,6 @@ __global__ __launch_bounds__(64 * kPW) __attribute__((amdgpu_waves_per_eu(4))) v
   const uint32_t* pstart = kind ? pstart1 : pstart0;
   const uint32_t* pseg = kind ? pseg1 : pseg0;
   const int64_t* uniq = kind ? uniq1 : uniq0;  // table row of each segment (caller's id space)
-  const uint32_t* fpiece = kind ? fpiece1 : fpiece0;
-  uint32_t* pcnt = kind ? pcnt1 : pcnt0;
   const float* dmf = kind ? dy_mf1 : dy_mf0;
   const float* dml = kind ? dy_mlp1 : dy_mlp0;
   const float* tmf = kind ? t_mf1 : t_mf0;
@@ -74,17 +68,14 @@ __global__ __launch_bounds__(64 * kPW) __attribute__((amdgpu_waves_per_eu(4))) v
     // occurrence positions (lane sub of the group holds occurrence j0 + sub) and their rows
     const int64_t p = p0 + sg;
     const bool act = p < Pn;
-    uint32_t ps = 0, info = 0, f0 = 0, f1 = 1;
+    uint32_t ps = 0, info = 0;
     int cnt = 0;
     float4 x_mf = make_float4(0, 0, 0, 0), x_ml = x_mf;
     if (act) {
       ps = pstart[p];
       cnt = (int)(pstart[p + 1] - ps);  // 1..PIECE
       info = pseg[p];
-      const uint32_t cc = info & ~FIRST_PIECE;
-      const int64_t id = uniq[cc];
-      f0 = fpiece[cc];                      // the segment's pieces [f0, f1)
-      f1 = fpiece[cc + 1];
+      const int64_t id = uniq[info & ~FIRST_PIECE];
       x_mf = ldp4<BF>(tmf, id * D + col);   // (BF: bf16 table rows, widened exactly)
       x_ml = ldp4<BF>(tml, id * D + col);
     }
@@ -141,27 +132,6 @@ __global__ __launch_bounds__(64 * kPW) __attribute__((amdgpu_waves_per_eu(4))) v
         ab.x += dy.x; ab.y += dy.y; ab.z += dy.z; ab.w += dy.w;
       }
     }
-    if (act && f1 - f0 > 1) {   // (uniform in the group)
-      // a multi-piece segment: this piece's rows are stored (G or xp); count it in, and the
-      // group completing the count adds the extras to the first piece's rows in piece order
-      __threadfence();
-      uint32_t old = 0;
-      if (sub == 0) old = atomicAdd(&pcnt[c], 1u);
-      old = __shfl(old, sg * L, 64);
-      if (old == f1 - f0 - 1) {
-        __threadfence();          // (acquire: the other pieces' rows, not stale L1 lines)
-        float4 a = ld4(Gmf + c * D + col), b = ld4(Gml + c * D + col);
-        const float* xe = xp + ((int64_t)f0 - c) * 2 * D + col;
-        for (uint32_t e = 0; e + 1 < f1 - f0; ++e, xe += 2 * D) {   // summed in piece order
-          const float4 x = ld4(xe), y = ld4(xe + D);
-          a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
-          b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
-        }
-        st4(Gmf + c * D + col, a);
-        st4(Gml + c * D + col, b);
-        if (sub == 0) pcnt[c] = 0u;   // ready for another reduce of the same dedup
-      }
-    }
   }
   // the wave's groups (lanes L apart hold the same columns), then the block's waves
 #pragma unroll
@@ -189,6 +159,47 @@ __global__ __launch_bounds__(64 * kPW) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
     for (int q = 0; q < kPW; ++q) a += red[q][i];
     out[i] = a;
+  }
+}
+
+// G[c] += extra pieces of segment c (in piece order); L lanes per segment
+template <int D>
+__global__ __launch_bounds__(256) void k_piece_fixup(
+    const uint32_t* __restrict__ fpiece0, const uint32_t* __restrict__ fpiece1,
+    const uint32_t* __restrict__ totals, const float* __restrict__ xp0,
+    const float* __restrict__ xp1, float* __restrict__ G_mf0, float* __restrict__ G_mlp0,
+    float* __restrict__ G_mf1, float* __restrict__ G_mlp1) {
+  constexpr int L = D / 4;
+  const int kind = blockIdx.y;
+  const uint32_t* fpiece = kind ? fpiece1 : fpiece0;
+  const float* xp = kind ? xp1 : xp0;
+  float* Gmf = kind ? G_mf1 : G_mf0;
+  float* Gml = kind ? G_mlp1 : G_mlp0;
+  const int64_t U = totals[kind];
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int col = (int)(t % L) * 4;
+  for (int64_t c = t / L; c < U; c += (int64_t)gridDim.x * blockDim.x / L) {
+    const uint32_t f0 = fpiece[c], f1 = fpiece[c + 1];
+    if (f1 - f0 <= 1) continue;
+    float4 a = ld4(Gmf + c * D + col), b = ld4(Gml + c * D + col);
+    const int64_t e1 = (int64_t)f1 - c - 1;
+    for (int64_t e0 = (int64_t)f0 - c; e0 < e1; e0 += 8) {   // 8 rows of loads in flight
+      float4 x[8], y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (e0 + u < e1) {
+          x[u] = ld4(xp + (e0 + u) * 2 * D + col);
+          y[u] = ld4(xp + (e0 + u) * 2 * D + D + col);
+        }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (e0 + u < e1) {   // summed in piece order
+          a.x += x[u].x; a.y += x[u].y; a.z += x[u].z; a.w += x[u].w;
+          b.x += y[u].x; b.y += y[u].y; b.z += y[u].z; b.w += y[u].w;
+        }
+    }
+    st4(Gmf + c * D + col, a);
+    st4(Gml + c * D + col, b);
   }
 }
 
@@ -496,15 +507,21 @@ int piece_reduce(const WS& w, int64_t n, const uint32_t* sv0, const uint32_t* sv
                  bool bf = false) {
   if (bf)
     hipLaunchKernelGGL((k_piece_reduce_ln<D, true>), dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1,
-                       w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.fpiece0, w.fpiece1,
-                       w.pcnt0, w.pcnt1, w.totals, dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1,
-                       gmf, gml, eps, Gmf0, Gml0, Gmf1, Gml1, w.xp0, w.xp1, w.part);
+                       w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
+                       dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
+                       Gmf1, Gml1, w.xp0, w.xp1, w.part);
   else
     hipLaunchKernelGGL((k_piece_reduce_ln<D, false>), dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1,
-                       w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.fpiece0, w.fpiece1,
-                       w.pcnt0, w.pcnt1, w.totals, dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1,
-                       gmf, gml, eps, Gmf0, Gml0, Gmf1, Gml1, w.xp0, w.xp1, w.part);
+                       w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
+                       dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
+                       Gmf1, Gml1, w.xp0, w.xp1, w.part);
   NCF_CHECK_LAUNCH("ncf_embedding_bwd(piece_reduce)");
+  constexpr int L = D / 4;
+  const int64_t fb = ncf_cdiv(n * L, 256);
+  hipLaunchKernelGGL(k_piece_fixup<D>, dim3((unsigned)(fb > 2048 ? 2048 : (fb < 1 ? 1 : fb)), 2),
+                     dim3(256), 0, st, w.fpiece0, w.fpiece1, w.totals, w.xp0, w.xp1, Gmf0, Gml0,
+                     Gmf1, Gml1);
+  NCF_CHECK_LAUNCH("ncf_embedding_bwd(fixup)");
   if (defer) {
     float* const outs[4] = {dgm, dbm, dgl, dbl};
     for (int q = 0; q < 4; ++q) {

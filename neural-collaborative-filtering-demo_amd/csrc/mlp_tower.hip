@@ -556,61 +556,9 @@ static_assert(kFwdVR <= 16 * kFwdRT, "forward rows per workgroup exceed its tile
 // (the partial of this workgroup; one deferred reduction sums the 256 partial rows).  16x16
 // output tiles, contraction over the rows k-permuted: lane group g covers rows [20g, 20g + 20).
 // A wave keeps its dlin column fragment (20 values) and sweeps its k tiles with it.
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-// The same partial with 32x32 output tiles of v_mfma_f32_32x32x2_f32 (fp32 path): one step reads
-// one A and one B float per lane for 4096 flop, twice the 16x16x4 step's 2048, so the phase
-// moves half the LDS operand bytes per flop.  Contraction k-permuted: lane half h covers rows
-// [40h, 40h + 40); a wave keeps its dlin column fragment (40 values) across its k tiles.
-template <int N, int K, int PG, int PX>
-__device__ __forceinline__ void wgrad_layer32(const float* __restrict__ G, const float* __restrict__ X,
-                                              float* __restrict__ out) {
-  constexpr int TN = N / 32, TK = K / 32, R2 = kRows / 2;
-  constexpr int TNW = TN >= kWaves ? TN / kWaves : 1;        // n tiles per wave
-  constexpr int WPN = TN >= kWaves ? 1 : kWaves / TN;        // waves per n tile
-  constexpr int TKW = TK / WPN;                              // k tiles per wave
-  static_assert(N % 32 == 0 && K % 32 == 0 && TK % WPN == 0 && R2 % 8 == 0, "wgrad32 tiling");
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, h = l >> 5;
-#pragma unroll
-  for (int jn = 0; jn < TNW; ++jn) {
-    const int tn = TN >= kWaves ? w + kWaves * jn : w % TN;
-    const int tk0 = TN >= kWaves ? 0 : (w / TN) * TKW;
-    float af[R2];
-#pragma unroll
-    for (int s = 0; s < R2; ++s) af[s] = G[(h * R2 + s) * PG + 32 * tn + r];
-    for (int jk = 0; jk < TKW; ++jk) {
-      const float* xb = X + (h * R2) * PX + 32 * (tk0 + jk) + r;
-      f32x16 acc0 = {}, acc1 = {};
-      constexpr int CH = 8;   // B operands in flight (register budget of the kernel: 176)
-#pragma unroll
-      for (int s0 = 0; s0 < R2; s0 += CH) {
-        float bx[CH];
-#pragma unroll
-        for (int s = 0; s < CH; ++s) bx[s] = xb[(s0 + s) * PX];
-#pragma unroll
-        for (int s = 0; s < CH; s += 2) {
-          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s0 + s], bx[s], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s0 + s + 1], bx[s + 1], acc1, 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      float* o = out + (32 * tn + 4 * h) * K + 32 * (tk0 + jk) + r;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) st_nt(o + ((q & 3) + 8 * (q >> 2)) * K, acc0[q] + acc1[q]);
-    }
-  }
-}
-
-#ifndef NCF_MLP_WG32
-#define NCF_MLP_WG32 1   // 32x32 weight-gradient tiles (0: the 16x16x4 form below, A/B builds)
-#endif
 template <int N, int K, int PG, int PX, bool BF = false>
 __device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const float* __restrict__ X,
                                             float* __restrict__ out) {
-  if constexpr (!BF && NCF_MLP_WG32) {
-    wgrad_layer32<N, K, PG, PX>(G, X, out);
-    return;
-  }
   constexpr int TN = N / 16, TK = K / 16, R4 = kRows / 4;
   constexpr int TNW = TN >= kWaves ? TN / kWaves : 1;        // n tiles per wave
   constexpr int WPN = TN >= kWaves ? 1 : kWaves / TN;        // waves per n tile

@@ -37,8 +37,6 @@ struct WS {
   uint32_t* ghist;     // [MAXP][2][MAXR]
   uint64_t* sstatus;   // [2][nb]
   uint32_t* totals;    // [4]: U0, U1, pieces0, pieces1
-  uint32_t *pcnt0, *pcnt1;   // [n + 2] per segment: pieces of it the embedding backward has
-                             // reduced (multi-piece segments; the last one resets it to 0)
   uint32_t* status;    // [passes][2][nb][R]  (R = 2^digit_bits)
   // sort buffers (ping-pong) and the 8-bit sort of the sharding path
   uint32_t *ka0, *va0, *ka1, *va1, *kb0, *vb0, *kb1, *vb1;
@@ -85,7 +83,6 @@ static inline int64_t ws_bytes(int64_t n, int64_t D) {
   b += round256(4 * (int64_t)MAXP * 2 * MAXR);
   b += round256(8 * 2 * nb);
   b += round256(4 * 4);
-  b += 2 * round256(4 * (n + 2));            // pcnt
   b += round256(4 * (int64_t)MAXP * 2 * nb * MAXR);
   b += 8 * round256(4 * (n + 64));
   b += round256(4 * 2 * 256 * nb);
@@ -114,8 +111,6 @@ static inline WS carve(void* base, int64_t n, int64_t D) {
   w.ghist = (uint32_t*)take(4 * (int64_t)MAXP * 2 * MAXR);
   w.sstatus = (uint64_t*)take(8 * 2 * (int64_t)w.nb);
   w.totals = (uint32_t*)take(4 * 4);
-  w.pcnt0 = (uint32_t*)take(4 * (n + 2));
-  w.pcnt1 = (uint32_t*)take(4 * (n + 2));
   w.status = (uint32_t*)take(4 * (int64_t)MAXP * 2 * w.nb * MAXR);
   const int64_t kb = 4 * (n + 64);
   w.ka0 = (uint32_t*)take(kb); w.va0 = (uint32_t*)take(kb);

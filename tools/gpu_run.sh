@@ -12,6 +12,8 @@
 #   c5prof           rocprofv3 --kernel-trace --stats over tools/score_bench.py
 #   ab:VAR=a,b       the short C2 bench with VAR=a and VAR=b, interleaved 3 times each
 #                    (ms/step + the per-kernel ms of each run -> TAG_ab.log)
+#   c5ab:VAR=a,b     tools/score_bench.py (10K users x 1M items, top-10 / top-100, eager, per-stage
+#                    ms) with VAR=a and VAR=b, interleaved twice each -> TAG_c5ab.log
 # Output: gpurun_out/TAG_<step>.log (+ .json / prof dirs).
 set -o pipefail
 TAG=$1
@@ -65,6 +67,15 @@ for what in "$@"; do
           f="$OUT/${TAG}_ab_$(basename "$v")_$k.log"
           env "$var=$v" timeout -k 10 200 python3 $QUICK > "$f" 2>&1 || { rc=$?; break 2; }
           python3 tools/bench_summ.py "$f" "$var=$v" >> "$OUT/${TAG}_ab.log" 2>&1
+        done
+      done ;;
+    c5ab:*)
+      spec="${what#c5ab:}"; var="${spec%%=*}"; vals="${spec#*=}"; va="${vals%%,*}"; vb="${vals#*,}"
+      rc=0
+      for k in 1 2; do
+        for v in "$va" "$vb"; do
+          echo "--- $var=$v ($k)" >> "$OUT/${TAG}_c5ab.log"
+          env "$var=$v" timeout -k 10 200 python3 tools/score_bench.py >> "$OUT/${TAG}_c5ab.log" 2>&1 || { rc=$?; break 2; }
         done
       done ;;
     *)
