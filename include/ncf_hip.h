@@ -534,7 +534,12 @@ int ncf_score_select_rescored(const int32_t* user_list, int64_t n_users, const u
                               int K, const float* queries, const float* items,
                               const float* item_bias, int64_t dim, const uint32_t* item_norm_max,
                               float c, float* out_score, int64_t* out_item, float* thr,
-                              uint32_t* overflow, void* stream);
+                              uint32_t* overflow, const float* thr_check, void* stream);
+/* thr_check (may be NULL): per user, a threshold T the collect was run below (its rank-j sample
+ * logit, j < K, before the margins) that is not a guaranteed bound of the K-th logit.  Every item
+ * with fp32 logit >= T was collected, so the K selected are exact iff K were found and the K-th
+ * re-scored logit is >= T; otherwise overflow[slot] = 2 and the caller re-runs the user from a
+ * guaranteed threshold (the sample's K-th). */
 int ncf_score_select(const int32_t* user_list, int64_t n_users, const uint32_t* count,
                      const float* cand_logit, const int32_t* cand_item, int64_t cap, int K,
                      float* out_score, int64_t* out_item, float* thr, uint32_t* overflow,

@@ -154,7 +154,7 @@ SIGNATURES = {
     "ncf_score_item_norm_max": (I32, [P, I64, I64, P, P]),
     "ncf_score_margin": (I32, [P, P, I64, I64, P, F32, P, P]),
     "ncf_score_select_rescored": (I32, [P, I64, P, P, P, I64, I32, P, P, P, I64, P, F32, P, P, P,
-                                        P, P]),
+                                        P, P, P]),
     "ncf_score_select": (I32, [P, I64, P, P, P, I64, I32, P, P, P, P, P]),
     "ncf_score_merge": (I32, [P, P, I64, I64, I32, P, P, P]),
     "ncf_temporal_fwd": (I32, [P, P, P, P, I64, P, P, P, P, I64, I64, P, P, P]),
@@ -420,7 +420,7 @@ def tapes_available() -> bool:
 # waiting streams are on this device).  Each record on the step's main queue stalls it: C2
 # fused step 0.3089-0.3103 ms with 0, 0.3107-0.3136 with 1, 0.3038-0.3050 with 2 (r3av_*; the
 # GPU suite green under 1 and 2)
-STREAM_EVENT_SCOPE = int(os.environ.get("NCF_EVENT_SCOPE", "2"))
+STREAM_EVENT_SCOPE = 2
 
 
 class RawEvent:

@@ -603,12 +603,10 @@ __device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const f
 // recomputed from r (act4's arithmetic: the same bits).  NCF_STAGE_BATCH = SB iterations' loads
 // issued before their uses (measured at C2, ms/step: SB 1 0.3075, 5 0.3100, 10 0.3087 — within
 // noise; the load-then-store loop's latency overlaps the other waves' work), default 1.
-// measured in-step (4 interleaved runs): k_mlp_bwd 90.3 us without, 92.4 us with the r1 stash
-// (the staging loop's extra LDS stores and the barrier before the column-sum scratch); off
-#ifndef NCF_MLP_STASH_R1
-#define NCF_MLP_STASH_R1 0
-#endif
-static_assert(128 + N1 + 2 <= kPQ, "the r1 stash fits Q's columns 128..257");
+// (Keeping layer 1's r rows in Q's free columns from this staging to its LayerNorm backward —
+// the R argument below — measured in-step, 4 interleaved runs: k_mlp_bwd 90.3 us without, 92.4
+// us with (the staging loop's extra LDS stores and the barrier before the column-sum scratch);
+// the tower passes R = NULL.)
 #ifndef NCF_STAGE_BATCH
 #define NCF_STAGE_BATCH 1
 #endif
@@ -857,7 +855,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
   NCF_STAMP(1, 2);
   // r1 kept in Q's columns 128..257 (free until stage a0; dlin2 uses columns 0..63) from the
   // a1 staging to the LayerNorm backward of layer 1: one HBM read of r1 instead of two
-  float* R1 = (NCF_MLP_STASH_R1 && fused_wgrad && !a.l[1].a) ? Q + 128 : nullptr;
+  float* R1 = nullptr;   // (the r1 stash: see stage_act)
   if (fused_wgrad) {   // dW2 = dlin2^T a1 (a1 staged in P, then overwritten by dX)
     stage_act<N1, kPP>(P, a.l[1], row0, rows, p, a.seed[1] + cs, R1);
     __syncthreads();

@@ -25,7 +25,9 @@
 //                             winners sorted (after 1/2-term scans: the candidates within 2 E_u of
 //                             the scan's K-th re-scored in fp32 first); when a user's list
 //                             overflowed, the K-th best candidate seen is a higher valid threshold
-//                             and the host re-runs 3-4 for those users.
+//                             and the host re-runs 3-4 for those users.  With a rank-j threshold
+//                             (j < K, a smaller sample: thr_check) it also checks that the K chosen
+//                             are provably the top K, and flags the user for a re-run if not.
 // Tilings: see k_collect (fp32) and k_collect3 (split bf16) below.
 #include "ncf_common.h"
 #include <algorithm>
@@ -552,9 +554,6 @@ constexpr int kUB3t = NCF_SCORE3_UB > 2 ? 2 : NCF_SCORE3_UB;   // (three-term sc
 #define NCF_SCORE3_NW 8
 #endif
 constexpr int kNW3 = NCF_SCORE3_NW;   // waves per workgroup (measured: 8 at one per CU 6.6 ms, 4 at two per CU 6.9)
-#ifndef NCF_SCORE3_XCD
-#define NCF_SCORE3_XCD 1
-#endif
 // Candidates staged per wave (its own LDS slice, dynamic LDS).  A full slice is written out
 // grouped by user: one global counter atomic per (user, flush) and each user's entries stored
 // contiguously, instead of one atomic and two scattered 4-byte stores per candidate (measured
@@ -642,12 +641,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     const uint16_t* __restrict__ items3, const float* __restrict__ bias, int64_t n_items,
     int64_t items_per_block, int ub, const float* __restrict__ thr, int64_t cap,
     uint32_t* __restrict__ count, float* __restrict__ cand_logit,
-    int32_t* __restrict__ cand_item) {
+    int32_t* __restrict__ cand_item, int pingpong) {
   constexpr int D = 64;
   __shared__ __attribute__((aligned(16))) uint16_t ps[3][T][kItemTile][kP3];
   __shared__ float bs[3][kItemTile];
   extern __shared__ __attribute__((aligned(16))) unsigned char slices3[];
-#if NCF_SCORE3_XCD
   // consecutive workgroups go round-robin to the 8 XCDs (each with its own L2): give every XCD a
   // contiguous run of the split-major order, so the user blocks of one item split share an L2
   int M = (int)blockIdx.x;
@@ -656,9 +654,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     if (per > 0 && (int)blockIdx.x < 8 * per) M = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
   }
   const int bx = M / ub, by = M % ub;
-#else
-  const int bx = (int)(blockIdx.x / ub), by = (int)(blockIdx.x % ub);
-#endif
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5;
   // the wave's UB blocks of 32 users (UB = 2: every staged B operand feeds two MFMA chains)
@@ -772,11 +767,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
     staged = 0;
   };
-  auto filt = [&](const f32x16& acc, int ub, int bb, int64_t t0) {
+  auto filt = [&](const f32x16& acc, int ub, float b, int64_t t0) {
     float th[16];
     th_of(ub, th);
     const int32_t item = (int32_t)(t0 + i);
-    const float b = bs[bb][i];
     const bool ivalid = t0 + i < it1;
     // Cheap reject first: max_r (acc[r] - th[r]) + b on packed fp32 (8 v_pk_add + 8 max).  The
     // margin keeps every lane the exact test below could accept (they round differently by at
@@ -824,11 +818,25 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
       for (int t = 0; t < 4; ++t) rd(0, t);
     }
+    // Ping-pong (pingpong != 0, 8 waves): waves 4-7 share their SIMDs with waves 0-3 and run
+    // each tile interval in the opposite order — filter the previous tile's accumulators first,
+    // then multiply this tile — so on every SIMD one wave's MFMAs overlap the other's filter
+    // VALU work instead of both multiplying, then both filtering, between the same barriers.
+    // (The accumulators carry the tile across the barrier; the tile's bias is kept in a
+    // register, its LDS buffer is restaged by then.)
+    // (one-term scan only: the two- and three-term forms have no registers to spare for it)
+    const bool lag = T == 1 && NW == 8 && pingpong && w >= 4;
+    f32x16 acc[UB];
+    float b_lag = 0.0f;
+    int64_t t_lag = -1;
     int bc = 0;
     for (int64_t t0 = it0; t0 < it1; t0 += kItemTile) {
       const int bn = bc == 2 ? 0 : bc + 1, bn2 = bn == 2 ? 0 : bn + 1;
       const bool has_next = t0 + kItemTile < it1;
-      f32x16 acc[UB];
+      if (lag && t_lag >= 0) {
+#pragma unroll
+        for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, b_lag, t_lag);
+      }
 #pragma unroll
       for (int ub = 0; ub < UB; ++ub)
 #pragma unroll
@@ -863,14 +871,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
           if (has_next) rd(bn, t);
         }
       }
+      if (lag) {
+        b_lag = bs[bc][i];
+        t_lag = t0;
+      } else {
 #pragma unroll
-      for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, bc, t0);
+        for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, bs[bc][i], t0);
+      }
       if (t0 + 2 * kItemTile < it1) {
         put(bn2);
         if (t0 + 3 * kItemTile < it1) fetch(t0 + 3 * kItemTile);
       }
       __syncthreads();
       bc = bn;
+    }
+    if (lag && t_lag >= 0) {
+#pragma unroll
+      for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, b_lag, t_lag);
     }
   }
   if (staged)
@@ -1005,7 +1022,8 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
                                                 float* __restrict__ out_score,
                                                 int64_t* __restrict__ out_item,
                                                 float* __restrict__ thr_out,
-                                                uint32_t* __restrict__ overflow) {
+                                                uint32_t* __restrict__ overflow,
+                                                const float* __restrict__ thr_check) {
   extern __shared__ unsigned long long sel[];   // [n2K] selected keys, then uint32 keys[cap]
   uint32_t* keys = reinterpret_cast<uint32_t*>(sel + n2K);
   __shared__ uint32_t hist[256];
@@ -1160,7 +1178,13 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
   }
   if (tid == 0) {
     const bool over = c_all > (uint32_t)cap;
-    overflow[slot] = over ? 1u : 0u;
+    // thr_check (a rank-j threshold, j < K: not a guaranteed bound of the K-th logit): the scan
+    // collected every item whose fp32 logit is >= thr_check[u], so the K selected are the top K
+    // iff K were selected and the K-th of them is >= it; else flag 2 (the host re-runs the user
+    // from the sample's K-th, a guaranteed bound)
+    const bool under = !over && thr_check &&
+        (ns < K || fkey_inv((uint32_t)(sel[K - 1] >> 32)) < thr_check[u]);
+    overflow[slot] = over ? 1u : (under ? 2u : 0u);
     // a valid higher threshold for a re-run: the K-th best of the candidates seen
     if (over && thr_out) thr_out[u] = fkey_inv((uint32_t)(sel[K - 1] >> 32));
   }
@@ -1422,6 +1446,10 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
     else
       n_cu = 256;
   }
+  static const int pingpong = [] {
+    const char* e = getenv("NCF_SCORE_PINGPONG");
+    return e ? atoi(e) : 1;
+  }();
   const int nub = terms == 3 ? kUB3t : kUB3;
   const int64_t upb = 32 * kNW3 * nub;   // users per workgroup
   const int64_t ub = (n_users + upb - 1) / upb;
@@ -1471,17 +1499,17 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
     hipLaunchKernelGGL((k_collect3<kUB3t, kNW3, 3>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
                        items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
-                       cand_item);
+                       cand_item, pingpong);
   else if (terms == 2)
     hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 2>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
                        items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
-                       cand_item);
+                       cand_item, pingpong);
   else
     hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 1>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
                        items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
-                       cand_item);
+                       cand_item, pingpong);
   NCF_CHECK_LAUNCH("ncf_score_collect_split");
   return NCF_OK;
 }
@@ -1504,7 +1532,7 @@ extern "C" int ncf_score_select(const int32_t* user_list, int64_t n_users, const
   }
   hipLaunchKernelGGL(k_select<false>, dim3((unsigned)n_users), dim3(256), lds, (hipStream_t)stream,
                      user_list, n_users, count, cand_logit, cand_item, cap, K, n2K, nullptr,
-                     nullptr, nullptr, nullptr, 0.0f, out_score, out_item, thr, overflow);
+                     nullptr, nullptr, nullptr, 0.0f, out_score, out_item, thr, overflow, nullptr);
   NCF_CHECK_LAUNCH("ncf_score_select");
   return NCF_OK;
 }
@@ -1518,7 +1546,8 @@ extern "C" int ncf_score_select_rescored(const int32_t* user_list, int64_t n_use
                                          const float* item_bias, int64_t dim,
                                          const uint32_t* item_norm_max, float c,
                                          float* out_score, int64_t* out_item, float* thr,
-                                         uint32_t* overflow, void* stream) {
+                                         uint32_t* overflow, const float* thr_check,
+                                         void* stream) {
   NCF_CHECK_ARG(dim == 64 && queries && items && item_bias && item_norm_max,
                 "ncf_score_select_rescored: dim must be 64, rows non-null");
   NCF_CHECK_ARG(n_users >= 0 && K >= 1 && cap >= K && cap <= kSelectMax,
@@ -1535,7 +1564,7 @@ extern "C" int ncf_score_select_rescored(const int32_t* user_list, int64_t n_use
   }
   hipLaunchKernelGGL(k_select<true>, dim3((unsigned)n_users), dim3(256), lds, (hipStream_t)stream,
                      user_list, n_users, count, cand_logit, cand_item, cap, K, n2K, queries, items,
-                     item_bias, item_norm_max, c, out_score, out_item, thr, overflow);
+                     item_bias, item_norm_max, c, out_score, out_item, thr, overflow, thr_check);
   NCF_CHECK_LAUNCH("ncf_score_select_rescored");
   return NCF_OK;
 }

@@ -30,10 +30,10 @@ from ._lib import ptr
 
 _KINDS = (("user", "mf_user", "mlp_user"), ("item", "mf_item", "mlp_item"))
 # Catch-up by claim (no id sort before the forward) when the batch was not sorted ahead;
-# NCF_CLAIM_CATCHUP=0: sort inline, then catch up the unique rows (A/B, tested equal).  The
+# CLAIM_CATCHUP = False: sort inline, then catch up the unique rows (tested equal).  The
 # claim path forks its id sort beside the forward (measured, drop-in step GPU-bound: 0.350-0.353
 # ms against 0.381-0.399 forked at a backward fork point; round 3)
-CLAIM_CATCHUP = os.environ.get("NCF_CLAIM_CATCHUP", "1") != "0"
+CLAIM_CATCHUP = True
 _SERIAL = itertools.count(1)      # distinguishes schedules in workspace caches (ids recycle)
 
 

@@ -157,7 +157,9 @@ class RcclExchange(ShardExchange):
         # communicator can wait on a hardware queue behind another communicator's (DESIGN 6:
         # 4 hardware queues per process).  ``side`` names the plan-stream role only.
         self.main = self._comm()
-        self.side = self.main
+        # (NCF_RCCL_COMMS=2: a second communicator for the plan-stream role, the round-3 form;
+        # A/B of the single communicator's cross-stream ordering cost)
+        self.side = self._comm() if os.environ.get("NCF_RCCL_COMMS", "1") == "2" else self.main
         W = self.world
         # host split arrays, one pair per call site: the collective reads them when it is
         # called, so a launch tape replays each site with the sizes written there for the step
@@ -198,6 +200,9 @@ class RcclExchange(ShardExchange):
         c = getattr(self, "main", None)
         if c is not None:
             _lib.call("ncf_comm_destroy", c)
+        c2 = getattr(self, "side", None)
+        if c2 is not None and c2 != c:
+            _lib.call("ncf_comm_destroy", c2)
         self.main = self.side = None
 
     def counts_issue(self, plan):

@@ -119,6 +119,7 @@ class _Binding:
         self.hp = _hp(group)
         self.uniform = True          # every parameter so far stepped on the shared counter
         self.step_t = torch.tensor(0.0)
+        self._step_np = self.step_t.numpy()   # (the same scalar: bumped without a torch op)
         self.m_flat = torch.zeros_like(eng.flat)
         self.v_flat = torch.zeros_like(eng.flat)
         self.moments = {k: {"exp_avg": _fresh_moments(p), "exp_avg_sq": _fresh_moments(p)}
@@ -236,18 +237,23 @@ class _Binding:
         if w is not None and (frozen or any(p.grad is not None for p in self.tables.values())):
             eng.materialize_table_grads(accumulate=True)
             w = None
-        dense_with = [(n, p) for n, p in self.dense if p.grad is not None]
         table_grads = [p for p in self.tables.values() if p.grad is not None]
-        if w is None and not table_grads and not dense_with:
-            return []
+        views = eng.grad_views()
+        if all(p.grad is gv for p, gv in views):
+            # the common case: every dense .grad is the view the backward assigned
+            dense_with, all_dense = self.dense, True
+        else:
+            dense_with = [(n, p) for n, p in self.dense if p.grad is not None]
+            if w is None and not table_grads and not dense_with:
+                return []
+            # dense gradients handed in as other tensors than the flat buffer's views: copied
+            # in first
+            for p, gv in views:
+                g = p.grad
+                if g is not None and g is not gv and g.data_ptr() != gv.data_ptr():
+                    gv.copy_(g)
+            all_dense = len(dense_with) == len(self.dense)
         eng.updates += 1
-        # dense gradients handed in as other tensors than the flat buffer's views: copied in
-        # first (their .grad normally ARE those views)
-        for p, gv in eng.grad_views():
-            g = p.grad
-            if g is not None and g is not gv and g.data_ptr() != gv.data_ptr():
-                gv.copy_(g)
-        all_dense = len(dense_with) == len(self.dense)
         d = self.D
         clocked = d is not None and w is not None
         if clocked and all_dense and self.uniform and not getattr(w, "slots_set", False):
@@ -265,7 +271,7 @@ class _Binding:
             if tp is None or not tp.step(w, run):
                 run()
             self.step += 1
-            self.step_t += 1
+            self._step_np += 1
             return self._all_params
         # --- tables
         if clocked:
@@ -307,7 +313,7 @@ class _Binding:
             if tables_stepped:
                 _lib.call("ncf_step_clock_advance", ptr(self.clock), self.base_seed, st)
         self.step += 1
-        self.step_t += 1
+        self._step_np += 1
         return self._all_params
 
     @property
@@ -315,6 +321,14 @@ class _Binding:
         c = self.__dict__.get("_allp")
         if c is None:
             c = self._allp = [p for _, p in self.dense] + list(self.tables.values())
+        return c
+
+    @property
+    def _all_ids(self):
+        """frozenset of id() of _all_params (what the pre-hook hides from torch's step)."""
+        c = self.__dict__.get("_allids")
+        if c is None:
+            c = self._allids = frozenset(id(p) for p in self._all_params)
         return c
 
 
@@ -356,17 +370,17 @@ def _restore_groups(opt):
             g["params"] = ps
 
 
-def _hide(opt, hidden):
-    """Take the parameters the fused step just updated out of the param groups for the
-    duration of torch's own step (restored by the post hook): torch's loop then never sees
-    them — one list swap per group instead of hiding and restoring every .grad."""
+def _hide(opt, hk):
+    """Take the parameters the fused step just updated (``hk``: frozenset of their id()) out of
+    the param groups for the duration of torch's own step (restored by the post hook): torch's
+    loop then never sees them — one list swap per group instead of hiding and restoring every
+    .grad."""
     cache = opt.__dict__.setdefault("_ncf_keep", {})
-    hk = frozenset(hidden)
     swap = []
     for g in opt.param_groups:
         ps = g["params"]
         c = cache.get(id(g))
-        if c is None or c[0] is not ps or c[1] != len(ps) or c[2] != hk:
+        if c is None or c[0] is not ps or c[1] != len(ps) or (c[2] is not hk and c[2] != hk):
             c = cache[id(g)] = (ps, len(ps), hk, [p for p in ps if id(p) not in hidden])
         if len(c[3]) != len(ps):
             swap.append((g, ps))
@@ -390,14 +404,15 @@ def _pre_hook(opt, args, kwargs):
         return None
     gmap = _group_of(opt)
     binds = _bindings(opt)
-    hidden = set()
+    hidden = None
     for m in models:
         b = binds.get(id(m))
         if b is None or not b.valid(m):
             if b is not None:
                 b.detach()
             b = binds[id(m)] = _Binding(m, opt, gmap[id(m.engine.table_params()["mf_user"])])
-        hidden.update(id(p) for p in b.run(opt, gmap))
+        if b.run(opt, gmap):
+            hidden = b._all_ids if hidden is None else hidden | b._all_ids
     if hidden:
         _hide(opt, hidden)
     return None

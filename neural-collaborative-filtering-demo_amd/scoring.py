@@ -96,16 +96,14 @@ def _param_version(model):
 
 
 # the candidate scan on bf16 matrix cores with split operands (fp32 accuracy, same candidate
-# sets; NCF_SCORE_SPLIT=0: the fp32 MFMA scan)
-SPLIT_SCAN = os.environ.get("NCF_SCORE_SPLIT", "1") != "0"
+# sets; an index without the planes, p3 = None, takes the fp32 MFMA scan)
+SPLIT_SCAN = True
 # terms per operand of the split scan: 1 (one bf16 product per pair) or 2 (three products) — the
 # thresholds lowered by the scan's error bound, the candidates near the K-th re-scored in fp32, so
 # the top-k are the same bits either way (tested) — or 3 (six products, fp32-accurate logits
 # straight from the scan).  Measured (10K users x 1M items, ms, top-10 / top-100): 1 term
 # 2.85 / 4.29 (scan 2.06 / 2.42), 2 terms 4.75 / 5.76 (scan 3.67 / 3.82), 3 terms 6.8 / 8.5
-SPLIT_TERMS = int(os.environ.get("NCF_SCORE_TERMS", "1"))
-if SPLIT_TERMS not in (1, 2, 3):
-    raise ValueError("NCF_SCORE_TERMS must be 1, 2 or 3")
+SPLIT_TERMS = 1
 # >= the scan's |logit error| / (|q|_2 max_i |p_i|_2) (Cauchy-Schwarz over the per-term errors),
 # with the fp32 accumulation and the fp32 re-scoring's own rounding: two terms (the dropped
 # products ~2^-16 relative): ~6.1e-5; one term (bf16 keeps 8 significant bits: each operand
@@ -139,34 +137,60 @@ def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st, expected=0, t
 # 1024 -> 7.5 ms, 2048 -> 7.7, cap / 2 = 4096 -> 8.3 at top-10 over 1M items), with the sample
 # kept within the k-th kernel's LDS-resident size (top-100: ~2570; a 30720-logit cap: 6.26 ms,
 # 38912: 5.90 ms), and never above cap / 2.
-SAMPLE_CANDS = int(os.environ.get("NCF_SCORE_CANDS", "1024"))
-# the split scan's item split raised from the expected candidates per user (A/B knob)
-SIZED_SPLIT = os.environ.get("NCF_SCORE_SIZED", "1") != "0"
-KTH_LDS_MAX = int(os.environ.get("NCF_SCORE_KTH_MAX", "38912"))   # <= score.hip kKthLdsMax
+SAMPLE_CANDS = 1024
+# the split scan's item split raised from the expected candidates per user (the launch's
+# expected_per_user: fewer per-wave LDS slice overflows; tested invisible in the results)
+SIZED_SPLIT = True
+KTH_LDS_MAX = 38912   # = score.hip kKthLdsMax
 # the threshold sample on bf16 matrix cores, fp16 logits rounded down (ncf_score_sample_split16 +
 # ncf_score_kth16, its k-th lowered by the two-term bound) instead of the fp32 sample GEMM +
-# fp32 k-th (NCF_SCORE_SAMPLE16=0, A/B); needs the split index (p3, pmax)
-SAMPLE16 = os.environ.get("NCF_SCORE_SAMPLE16", "1") != "0"
+# fp32 k-th (measured, 10K x 1M eager: top-100 4.25 -> 3.73 ms, top-10 2.78 -> 2.70); needs the
+# split index (p3, pmax); tests compare both
+SAMPLE16 = True
 
 
-def _select(idx, rows, n, run, k, out_s, out_i, overflow, st, terms=None):
+def _select(idx, rows, n, run, k, out_s, out_i, overflow, st, terms=None, check=None):
     """ncf_score_select(_rescored) of n users' candidate lists (fp32 re-scoring after a one- or
-    two-term scan; ``terms`` as the scan's)."""
+    two-term scan; ``terms`` as the scan's; ``check``: the rank-j thresholds to verify the
+    selection against, flag 2 where it is not provably the top k)."""
     if idx.pmax is not None:
         _lib.call("ncf_score_select_rescored", rows, n, ptr(run.count), ptr(run.cand_l),
                   ptr(run.cand_i), run.cap, k, ptr(run.q), ptr(idx.p), ptr(idx.bias),
                   idx.p.shape[1], ptr(idx.pmax), MARGIN_C[terms or _terms(idx)], out_s, out_i,
-                  ptr(run.thr), overflow,
-                  st)
+                  ptr(run.thr), overflow, check, st)
     else:
         _lib.call("ncf_score_select", rows, n, ptr(run.count), ptr(run.cand_l), ptr(run.cand_i),
                   run.cap, k, out_s, out_i, ptr(run.thr), overflow, st)
 
 
-def _sample_size(n_items: int, k: int, cap: int) -> int:
-    """Items in the threshold sample S: expected candidates ~ k * n_items / S."""
-    s = max(4096, -(-k * n_items // max(1, SAMPLE_CANDS)))
-    s = max(min(s, KTH_LDS_MAX), -(-2 * k * n_items // cap))
+# Rank-j thresholds (the fp16 sample path, k > RANK_J): the threshold is the sample's j-th
+# largest logit (j = RANK_J) instead of its k-th, over a sample k / j times smaller, aimed at
+# RANK_J * k expected candidates per user.  It is not a guaranteed bound of the k-th logit, so the
+# select verifies each user's result against it (every item at or above it was collected; the
+# k chosen are exact iff k were found and the k-th is at or above it) and flags the rest, which
+# are re-run from the sample's k-th (guaranteed).  The number of items at or above the j-th of a
+# sample of S ~ n_items / k is ~ Gamma(j) * k: below k with probability P(Gamma(16) < 1) ~ 1e-14
+# per user on exchangeable scores.  NCF_SCORE_RANK_J=0: the k-th always (A/B).
+RANK_J = int(os.environ.get("NCF_SCORE_RANK_J", "16"))
+SAMPLE_MIN = 4096   # items in the smallest threshold sample
+
+
+def _threshold_rank(k: int, cap: int, s16: bool) -> int:
+    """The sample rank whose logit is the collect threshold: k, or RANK_J (see above)."""
+    if s16 and RANK_J > 0 and k > RANK_J and RANK_J * k <= cap // 2:
+        return RANK_J
+    return k
+
+
+def _sample_size(n_items: int, k: int, cap: int, j: int = 0) -> int:
+    """Items in the threshold sample S: expected candidates ~ j * n_items / S (j = k by
+    default; j < k: the rank-j plan, S ~ n_items / k, RANK_J * k candidates expected)."""
+    j = j or k
+    if j < k:
+        s = max(SAMPLE_MIN, -(-j * n_items // (RANK_J * k)))
+    else:
+        s = max(SAMPLE_MIN, -(-k * n_items // max(1, SAMPLE_CANDS)))
+    s = max(min(s, KTH_LDS_MAX), -(-2 * j * n_items // cap))
     s = -(-s // 256) * 256
     return min(n_items, s)
 
@@ -182,15 +206,25 @@ class _TopKRun:
         if not 1 <= k <= min(I, cap):
             raise ValueError(f"k must be in [1, {min(I, cap)}]")
         self.index, self.n, self.k, self.cap = index, n, k, cap
-        self.S = _sample_size(I, k, cap)
+        s16 = SAMPLE16 and index.p3 is not None and index.pmax is not None
+        self.j = _threshold_rank(k, cap, s16)
+        self.S = _sample_size(I, k, cap, self.j)
         self.stride = I // self.S
         # the sample's item biases, contiguous: added in the sample GEMM's epilogue
         self.sbias = index.bias[::self.stride][:self.S].contiguous()
         e = lambda *sh, dt=torch.float32: torch.empty(*sh, dtype=dt, device=dev)  # noqa: E731
         self.uid = e(max(n, 1), dt=torch.int64)
-        self.s16 = (SAMPLE16 and index.p3 is not None and index.pmax is not None
-                    and self.S <= KTH_LDS_MAX)
+        self.s16 = s16 and self.S <= KTH_LDS_MAX
+        # (rank j only where the sample leaves >= 8 k candidates expected: a small catalogue's
+        # sample floor of 4096 items would otherwise put the j-th near the k-th item overall)
+        if self.j < k and (not self.s16 or self.j * I < 8 * k * self.S):
+            self.j = k
+            self.S = _sample_size(I, k, cap)
+            self.stride = I // self.S
+            self.sbias = index.bias[::self.stride][:self.S].contiguous()
         self.q, self.thr = e(max(n, 1), D), e(max(n, 1))
+        # the rank-j thresholds before the margins (the select's check)
+        self.thr_chk = e(max(n, 1)) if self.j < k else None
         self.sample = (torch.empty(max(n, 1), self.S, dtype=torch.int16, device=dev) if self.s16
                        else e(max(n, 1), self.S))
         self.count = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
@@ -213,7 +247,9 @@ class _TopKRun:
         if self.s16:
             _lib.call("ncf_score_sample_split16", ptr(self.q), n, ptr(idx.p3), I, D, self.stride,
                       ptr(self.sbias), self.S, ptr(self.sample), st)
-            _lib.call("ncf_score_kth16", ptr(self.sample), n, self.S, k, ptr(self.thr), st)
+            _lib.call("ncf_score_kth16", ptr(self.sample), n, self.S, self.j, ptr(self.thr), st)
+            if self.thr_chk is not None:
+                self.thr_chk.copy_(self.thr)
             # (the k-th of the fp16 sample is a bound after the two-term error is taken off)
             _lib.call("ncf_score_margin", ptr(self.q), None, n, D, ptr(idx.pmax), MARGIN_C[2],
                       ptr(self.thr), st)
@@ -225,12 +261,30 @@ class _TopKRun:
         self.count.zero_()
         # expected candidates per user: k x I / S (the threshold sample's k-th over S items)
         _collect(idx, ptr(self.q), None, n, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),
-                 ptr(self.cand_i), st, expected=-(-k * I // self.S) if SIZED_SPLIT else 0)
-        _select(idx, None, n, self, k, ptr(self.scores), ptr(self.items), ptr(self.overflow), st)
+                 ptr(self.cand_i), st, expected=-(-self.j * I // self.S) if SIZED_SPLIT else 0)
+        _select(idx, None, n, self, k, ptr(self.scores), ptr(self.items), ptr(self.overflow), st,
+                check=None if self.thr_chk is None else ptr(self.thr_chk))
+
+    def safe_thresholds(self, redo, st):
+        """Users flagged by the rank-j check: their threshold from the sample's k-th instead (the
+        fp32 sample GEMM over the same strided items, its k-th: k sample items at or above it, a
+        guaranteed bound; the re-run's collect lowers it by the scan's margin)."""
+        idx, k = self.index, self.k
+        p = idx.p
+        I, D = p.shape
+        q = self.q[redo].contiguous()
+        nr = q.shape[0]
+        sample = torch.empty(nr, self.S, device=p.device)
+        thr = torch.empty(nr, device=p.device)
+        _lib.call("ncf_gemm_f32", nr, self.S, D, ptr(q), D, 0, ptr(p), D * self.stride, 1,
+                  ptr(sample), self.S, ptr(self.sbias), 0, st)
+        _lib.call("ncf_score_kth", ptr(sample), nr, self.S, k, None, self.stride, ptr(thr), st)
+        self.thr[redo] = thr
 
     def redo_overflow(self, st):
-        """Re-run the users whose candidate list overflowed (eager; rare: the threshold sample
-        targets cap / 2 candidates)."""
+        """Re-run the users whose candidate list overflowed (flag 1) or whose rank-j result was
+        not provably exact (flag 2) (eager; rare: the threshold sample targets cap / 2
+        candidates at most, and a rank-j shortfall has probability ~1e-14 per user)."""
         idx, k, cap = self.index, self.k, self.cap
         p, bias = idx.p, idx.bias
         I, D = p.shape
@@ -244,6 +298,9 @@ class _TopKRun:
             redo = torch.nonzero(overflow).flatten()
             if redo.numel() == 0:
                 return
+            short = redo[overflow[redo] == 2]
+            if short.numel():
+                self.safe_thresholds(short, st)
             rows = redo.to(torch.int32)
             self.count[redo] = 0
             sub_s = torch.empty(rows.numel(), k, device=dev)

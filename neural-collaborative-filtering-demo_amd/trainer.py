@@ -33,7 +33,7 @@ log = logging.getLogger(__name__)
 # this step (else at attn_bwd), joined by the sweep's own join: no event record or wait of its
 # own on the step's queue, where each costs ~5 us (0.2986-0.2992 against 0.3020-0.3040 ms/step
 # at attn_bwd, r3ax_*).
-DEDUP_FORK = os.environ.get("NCF_DEDUP_FORK", "sweep")
+DEDUP_FORK = "sweep"
 
 
 class FusedTrainStep:

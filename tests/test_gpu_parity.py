@@ -1205,6 +1205,67 @@ def test_fp16_threshold_sample_equals_fp32_sample(k, cap, monkeypatch):
     assert torch.equal(s16, s32)
 
 
+@pytest.mark.parametrize("k,cap", [(100, 8192), (40, 8192), (100, 4096)])
+def test_rank_j_threshold_equals_kth_threshold(k, cap, monkeypatch):
+    """Rank-j thresholds (the sample's 16th largest logit over a sample ~k/16 times smaller,
+    the selection verified per user by ncf_score_select_rescored's thr_check) against the
+    sample's k-th: the same top-k items and score bits.  The sample floor is lowered so the
+    rank-j plan applies at 100003 items (it does from ~0.8M items at k = 100 by default)."""
+    from ncf_amd import scoring
+    from ncf_amd.scoring import ItemIndex, score_topk
+    torch.manual_seed(19)
+    U, I = 5000, 100003
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    users = torch.randperm(U)[:700]
+    idx = ItemIndex(m)
+    monkeypatch.setattr(scoring, "SAMPLE_MIN", 256)
+    monkeypatch.setattr(scoring, "RANK_J", 16)
+    plan = scoring._TopKRun(idx, 700, k, cap)
+    assert plan.s16 and plan.j == 16 and plan.thr_chk is not None, "the rank-j plan applies"
+    sj, ij = score_topk(m, users, k=k, index=idx, cap=cap)
+    monkeypatch.setattr(scoring, "RANK_J", 0)
+    assert scoring._TopKRun(idx, 700, k, cap).j == k
+    sk, ik = score_topk(m, users, k=k, index=idx, cap=cap)
+    assert torch.equal(ij, ik)
+    assert torch.equal(sj, sk)
+
+
+def test_rank_j_shortfall_reruns_from_kth(monkeypatch):
+    """A catalogue where the strided threshold sample holds the best items (their bias raised):
+    the sample's 16th logit then has fewer than k items at or above it, every user's check in the
+    select fails (flag 2), and the re-run from the sample's k-th gives the exact top k: the same
+    bits as the k-th-threshold pipeline on the same index."""
+    from ncf_amd import scoring
+    from ncf_amd.scoring import ItemIndex, score_topk
+    torch.manual_seed(23)
+    U, I, k = 2000, 100003, 100
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    users = torch.randperm(U)[:300]
+    idx = ItemIndex(m)
+    monkeypatch.setattr(scoring, "SAMPLE_MIN", 256)
+    monkeypatch.setattr(scoring, "RANK_J", 16)
+    plan = scoring._TopKRun(idx, 300, k, 8192)
+    assert plan.j == 16
+    idx.bias[:plan.S * plan.stride:plan.stride] += 5.0
+    calls = []
+    safe = scoring._TopKRun.safe_thresholds
+
+    def counted(self, redo, st):
+        calls.append(int(redo.numel()))
+        return safe(self, redo, st)
+    monkeypatch.setattr(scoring._TopKRun, "safe_thresholds", counted)
+    sj, ij = score_topk(m, users, k=k, index=idx)
+    assert calls and calls[0] == 300, f"every user re-run from the k-th ({calls})"
+    monkeypatch.setattr(scoring, "RANK_J", 0)
+    sk, ik = score_topk(m, users, k=k, index=idx)
+    assert torch.equal(ij, ik)
+    assert torch.equal(sj, sk)
+    # and those are the top k of the modified catalogue: the boosted sample items lead
+    assert bool((ik % plan.stride == 0).float().mean() > 0.9)
+
+
 @pytest.mark.parametrize("k,terms", [(10, 2), (100, 2), (100, 3), (10, 1)])
 def test_split_scan_item_split_sizing_is_invisible(k, terms, monkeypatch):
     """The split scan's item split raised from the expected candidates per user (k x I / S, the

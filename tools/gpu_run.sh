@@ -6,12 +6,17 @@
 #   t:<pytest -k>    the -m gpu tests matching the expression
 #   bench            python bench.py (defaults), JSON line -> gpurun_out/TAG_bench.json
 #   quick            bench.py --steps 100 --warmup 10 --no-c4 --no-score
+#   sharded          bench.py --sharded (the row-sharded step at world 1) -> TAG_sharded.json
+#   dropinhost       tools/dropin_host.py (host time of the reference call pattern, cProfile)
 #   prof             rocprofv3 --kernel-trace --stats over a short bench (C2 legs only)
 #   pmc              FETCH_SIZE / WRITE_SIZE passes over the same command (tools/pmc_run.sh;
 #                    -> profiles/TAG_pmc_traffic.json, copied to gpurun_out/)
+#   dropinprof       rocprofv3 --kernel-trace --stats over tools/dropin_host.py (gaps per phase)
+#   c5sq             SQ counters (tools/pmc_sq.sh, 3 passes) over tools/score_bench.py --k 10
 #   c5prof           rocprofv3 --kernel-trace --stats over tools/score_bench.py
 #   ab:VAR=a,b       the short C2 bench with VAR=a and VAR=b, interleaved 3 times each
 #                    (ms/step + the per-kernel ms of each run -> TAG_ab.log)
+#   sab:VAR=a,b      the row-sharded bench at world 1 (torchrun, 1 rank) with VAR=a / VAR=b, twice
 #   c5ab:VAR=a,b     tools/score_bench.py (10K users x 1M items, top-10 / top-100, eager, per-stage
 #                    ms) with VAR=a and VAR=b, interleaved twice each -> TAG_c5ab.log
 # Output: gpurun_out/TAG_<step>.log (+ .json / prof dirs).
@@ -44,9 +49,18 @@ for what in "$@"; do
         > "$OUT/${TAG}_quick.log" 2>&1
       rc=$?
       grep '^{' "$OUT/${TAG}_quick.log" | tail -1 > "$OUT/${TAG}_quick.json" ;;
+    sharded)
+      timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29517 bench.py --sharded --steps 200 --warmup 20 \
+        --no-c4 --no-score --no-cpu-baseline --no-dropin > "$OUT/${TAG}_sharded.log" 2>&1
+      rc=$?
+      grep '^{' "$OUT/${TAG}_sharded.log" | tail -1 > "$OUT/${TAG}_sharded.json" ;;
+    dropinhost)
+      timeout -k 10 300 python -u tools/dropin_host.py > "$OUT/${TAG}_dropinhost.log" 2>&1
+      rc=$? ;;
     prof)
       rm -rf "$OUT/${TAG}_prof"
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof" -o run -- \
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof" -o run -- \
         python3 $QUICK > "$OUT/${TAG}_prof.log" 2>&1
       rc=$? ;;
     pmc)
@@ -54,9 +68,19 @@ for what in "$@"; do
         > "$OUT/${TAG}_pmc.log" 2>&1
       rc=$?
       cp "profiles/${TAG}_pmc_traffic.json" "$OUT/" 2>/dev/null ;;
+    dropinprof)
+      rm -rf "$OUT/${TAG}_dropinprof"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_dropinprof" -o run -- \
+        python3 tools/dropin_host.py --warmup 150 --steps 60 > "$OUT/${TAG}_dropinprof.log" 2>&1
+      rc=$? ;;
+    c5sq)
+      SQ_CMD="python3 tools/score_bench.py --k 10 --reps 1" timeout -k 10 500 \
+        bash tools/pmc_sq.sh "${TAG}c5" > "$OUT/${TAG}_c5sq.log" 2>&1
+      rc=$?
+      python3 tools/pmc_sq_summary.py "${TAG}c5" collect,sample,kth,select >> "$OUT/${TAG}_c5sq.log" 2>&1 ;;
     c5prof)
       rm -rf "$OUT/${TAG}_c5prof"
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_c5prof" -o run -- \
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_c5prof" -o run -- \
         python3 tools/score_bench.py > "$OUT/${TAG}_c5prof.log" 2>&1
       rc=$? ;;
     ab:*)
@@ -67,6 +91,19 @@ for what in "$@"; do
           f="$OUT/${TAG}_ab_$(basename "$v")_$k.log"
           env "$var=$v" timeout -k 10 200 python3 $QUICK > "$f" 2>&1 || { rc=$?; break 2; }
           python3 tools/bench_summ.py "$f" "$var=$v" >> "$OUT/${TAG}_ab.log" 2>&1
+        done
+      done ;;
+    sab:*)
+      spec="${what#sab:}"; var="${spec%%=*}"; vals="${spec#*=}"; va="${vals%%,*}"; vb="${vals#*,}"
+      rc=0
+      for k in 1 2; do
+        for v in "$va" "$vb"; do
+          f="$OUT/${TAG}_sab_$(basename "$v")_$k.log"
+          env "$var=$v" timeout -k 10 200 python3 -m torch.distributed.run --nnodes=1 \
+            --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29518 bench.py --sharded \
+            --steps 100 --warmup 20 --prime 128 --no-c4 --no-score --no-cpu-baseline --no-dropin \
+            > "$f" 2>&1 || { rc=$?; break 2; }
+          python3 tools/bench_summ.py "$f" "$var=$v" >> "$OUT/${TAG}_sab.log" 2>&1
         done
       done ;;
     c5ab:*)
