@@ -695,6 +695,8 @@ def main():
     ap.add_argument("--users", type=int, default=1_000_000)
     ap.add_argument("--items", type=int, default=100_000)
     ap.add_argument("--groups", type=int, default=4096, help="interaction groups per GPU per step")
+    ap.add_argument("--batches", type=int, default=N_BATCHES,
+                    help="distinct resident batches the timed legs cycle through")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--infer-pairs", type=int, default=65536)
@@ -764,7 +766,7 @@ def main():
         model = model.to(dev).train()
         step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, graph=args.graph,
                               clock=False if args.no_clock else None)
-    batches = make_batches(U, I, B, M, N_BATCHES, dev, seed=100 + rank)
+    batches = make_batches(U, I, B, M, args.batches, dev, seed=100 + rank)
     torch.cuda.synchronize()
 
     # the single-GPU step sorts the next batch's ids on a side stream under the current step
@@ -817,7 +819,7 @@ def main():
         cyc8 = {"ms_per_step": round(dt8 / args.steps * 1e3, 4),
                 "value": round(N * args.steps / dt8, 1),
                 "note": "same step cycling over 8 resident batches (round 3's bench); the "
-                        f"headline cycles over {N_BATCHES} distinct batches"}
+                        f"headline cycles over {args.batches} distinct batches"}
     samples_s = N * world * args.steps / elapsed
     last = step.ops.last_loss if sharded else step.last_loss
     loss = float(last.item()) if last is not None else float("nan")
@@ -1127,7 +1129,7 @@ def main():
             "infer_config": f"eval forward (M=1), {npairs} resident (user,item) pairs per GPU",
             "infer": infer,
             "headline_8_batch_cycle": cyc8,
-            "resident_batches": N_BATCHES,
+            "resident_batches": args.batches,
             "c5_scoring": score,
             "c2_bf16_tables": bf16,
             "c4_train": c4,

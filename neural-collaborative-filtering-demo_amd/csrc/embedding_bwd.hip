@@ -27,6 +27,7 @@ namespace {
 
 // part[kind*nbr + block][0:D mf_g | D:2D mf_b | 2D:3D mlp_g | 3D:4D mlp_b]
 constexpr int kPW = NCF_PIECE_WAVES;   // waves per block
+constexpr int kRowBatch = 8;           // occurrence rows loaded per round (k_piece_reduce_ln)
 template <int D, bool BF = false>
 __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     const uint32_t* __restrict__ sv0, const uint32_t* __restrict__ sv1,
@@ -86,19 +87,22 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     for (int j0 = 0; j0 < cmax; j0 += L) {
       const uint32_t r = (j0 + sub < cnt) ? sv[ps + j0 + sub] : 0u;
       const int jn = min(L, cmax - j0);
-      for (int jj = 0; jj < jn; jj += 4) {   // 4 rows of loads in flight, summed in order
-        float4 a[4], b[4];
+      // kRowBatch rows of loads in flight, summed in order (8: a user's 5 occurrences in one
+      // round of loads instead of two)
+      for (int jj = 0; jj < jn; jj += kRowBatch) {
+        float4 a[kRowBatch], b[kRowBatch];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < kRowBatch; ++u) {
+          // (jj + u < jn: a batch may run past this group's L lanes when L < kRowBatch)
           const int64_t rr = __shfl(r, sg * L + jj + u, 64);
-          if (j0 + jj + u < cnt) {
+          if (jj + u < jn && j0 + jj + u < cnt) {
             a[u] = ld4(dmf + rr * D + col);
             b[u] = ld4(dml + rr * D + col);
           }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (j0 + jj + u < cnt) {
+        for (int u = 0; u < kRowBatch; ++u)
+          if (jj + u < jn && j0 + jj + u < cnt) {
             sm.x += a[u].x; sm.y += a[u].y; sm.z += a[u].z; sm.w += a[u].w;
             sl.x += b[u].x; sl.y += b[u].y; sl.z += b[u].z; sl.w += b[u].w;
           }

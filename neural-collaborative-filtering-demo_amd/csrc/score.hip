@@ -772,33 +772,41 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     th_of(ub, th);
     const int32_t item = (int32_t)(t0 + i);
     const bool ivalid = t0 + i < it1;
-    // Cheap reject first: max_r (acc[r] - th[r]) + b on packed fp32 (8 v_pk_add + 8 max).  The
-    // margin keeps every lane the exact test below could accept (they round differently by at
-    // most an ulp of |b|; the subtraction near a hit is exact, Sterbenz).
-    {
-      f32x2 m2 = {-INFINITY, -INFINITY};
+    // Cheap reject first: max_r (acc[r] - th[r]) + b on packed fp32 (8 v_pk_add + max3s),
+    // kept per group of 4 rows.  The margin keeps every lane the exact test below could accept
+    // (they round differently by at most an ulp of |b|; the subtraction near a hit is exact,
+    // Sterbenz).  At ~1 expected hit per 32 x 32 tile most tiles pass this test, so the exact
+    // per-row test runs only in the 4-row groups whose maximum passes it too (~1 of 4).
+    const float tol = -1e-6f * fabsf(b);
+    float gm[4];
 #pragma unroll
-      for (int r = 0; r < 16; r += 2)
-        m2 = __builtin_elementwise_max(m2, f32x2{acc[r], acc[r + 1]} - f32x2{th[r], th[r + 1]});
-      const bool near = ivalid && fmaxf(m2.x, m2.y) + b >= -1e-6f * fabsf(b);
-      if (!__ballot(near)) return;
+    for (int c = 0; c < 4; ++c) {
+      const f32x2 d0 = f32x2{acc[4 * c], acc[4 * c + 1]} - f32x2{th[4 * c], th[4 * c + 1]};
+      const f32x2 d1 = f32x2{acc[4 * c + 2], acc[4 * c + 3]} - f32x2{th[4 * c + 2], th[4 * c + 3]};
+      gm[c] = fmaxf(fmaxf(d0.x, d0.y), fmaxf(d1.x, d1.y));
     }
+    if (!__ballot(ivalid && fmaxf(fmaxf(gm[0], gm[1]), fmaxf(gm[2], gm[3])) + b >= tol)) return;
     // exact hits row by row: one wave mask per user row, slice offsets from mbcnt; the slice is
     // written out first when the row's hits would not fit (a row has at most 64)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const uint64_t hm = __ballot(ivalid && acc[r] + b >= th[r]);
-      if (hm == 0) continue;   // wave-uniform
-      const uint32_t nh = (uint32_t)__popcll(hm);
-      if (staged + nh > (uint32_t)kSlice3) wflush();
-      if ((hm >> lane) & 1) {
-        const uint32_t at = staged + __builtin_amdgcn_mbcnt_hi(
-            (uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-        wl[at] = acc[r] + b;
-        wi[at] = item;
-        wu[at] = (uint16_t)(32 * ub + (r & 3) + 8 * (r >> 2) + 4 * h);   // local user slot
+    for (int c = 0; c < 4; ++c) {
+      if (!__ballot(ivalid && gm[c] + b >= tol)) continue;   // wave-uniform
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int r = 4 * c + rr;
+        const uint64_t hm = __ballot(ivalid && acc[r] + b >= th[r]);
+        if (hm == 0) continue;   // wave-uniform
+        const uint32_t nh = (uint32_t)__popcll(hm);
+        if (staged + nh > (uint32_t)kSlice3) wflush();
+        if ((hm >> lane) & 1) {
+          const uint32_t at = staged + __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+          wl[at] = acc[r] + b;
+          wi[at] = item;
+          wu[at] = (uint16_t)(32 * ub + (r & 3) + 8 * (r >> 2) + 4 * h);   // local user slot
+        }
+        staged += nh;
       }
-      staged += nh;
     }
   };
   // Iteration t multiplies tile t (buffer t % 3, operands in registers, the reads of tile t + 1
@@ -825,7 +833,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     // (The accumulators carry the tile across the barrier; the tile's bias is kept in a
     // register, its LDS buffer is restaged by then.)
     // (one-term scan only: the two- and three-term forms have no registers to spare for it)
-    const bool lag = T == 1 && NW == 8 && pingpong && w >= 4;
+    const bool lag = T == 1 && NW == 8 && pingpong && __builtin_amdgcn_readfirstlane(w) >= 4;
     f32x16 acc[UB];
     float b_lag = 0.0f;
     int64_t t_lag = -1;

@@ -381,7 +381,7 @@ def _hide(opt, hk):
         ps = g["params"]
         c = cache.get(id(g))
         if c is None or c[0] is not ps or c[1] != len(ps) or (c[2] is not hk and c[2] != hk):
-            c = cache[id(g)] = (ps, len(ps), hk, [p for p in ps if id(p) not in hidden])
+            c = cache[id(g)] = (ps, len(ps), hk, [p for p in ps if id(p) not in hk])
         if len(c[3]) != len(ps):
             swap.append((g, ps))
             g["params"] = c[3]

@@ -334,3 +334,19 @@ def test_shard_struct_mirrors_match_header():
     assert wmax == _lib.SHARD_MAX_WORLD
     assert ctypes.sizeof(_lib.ShardRecv) == 4 * (1 + (wmax + 1) + wmax)
     assert [f[0] for f in _lib.ShardRecv._fields_] == ["world", "start", "n0"]
+
+
+def test_optimizer_hide_and_restore_param_groups():
+    """optim._hide takes the fused step's parameters out of torch's param groups for the
+    duration of its own step and the post hook restores them (host logic, no GPU)."""
+    from ncf_amd import optim as O
+    ps = [torch.nn.Parameter(torch.zeros(3)) for _ in range(5)]
+    opt = torch.optim.Adam([{"params": ps[:3]}, {"params": ps[3:]}], lr=1e-3)
+    before = [list(g["params"]) for g in opt.param_groups]
+    hk = frozenset(id(p) for p in ps[:4])
+    for _ in range(2):          # (the second call takes the cached lists)
+        O._hide(opt, hk)
+        assert [len(g["params"]) for g in opt.param_groups] == [0, 1]
+        assert opt.param_groups[1]["params"][0] is ps[4]
+        O._restore_groups(opt)
+        assert [list(g["params"]) for g in opt.param_groups] == before

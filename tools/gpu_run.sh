@@ -12,6 +12,7 @@
 #   pmc              FETCH_SIZE / WRITE_SIZE passes over the same command (tools/pmc_run.sh;
 #                    -> profiles/TAG_pmc_traffic.json, copied to gpurun_out/)
 #   dropinprof       rocprofv3 --kernel-trace --stats over tools/dropin_host.py (gaps per phase)
+#   c5pmc            FETCH_SIZE / WRITE_SIZE passes over tools/score_bench.py (-> TAG_c5_pmc_traffic.json)
 #   c5sq             SQ counters (tools/pmc_sq.sh, 3 passes) over tools/score_bench.py --k 10
 #   c5prof           rocprofv3 --kernel-trace --stats over tools/score_bench.py
 #   ab:VAR=a,b       the short C2 bench with VAR=a and VAR=b, interleaved 3 times each
@@ -26,6 +27,7 @@ shift
 OUT=gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+md5sum neural-collaborative-filtering-demo_amd/*.so > "$OUT/${TAG}_so.md5" 2>/dev/null
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
 QUICK="bench.py --steps 60 --warmup 10 --prime 128 --no-c4 --no-score --no-cpu-baseline --no-dropin"
 for what in "$@"; do
@@ -73,6 +75,11 @@ for what in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_dropinprof" -o run -- \
         python3 tools/dropin_host.py --warmup 150 --steps 60 > "$OUT/${TAG}_dropinprof.log" 2>&1
       rc=$? ;;
+    c5pmc)
+      PMC_CMD="python3 tools/score_bench.py --k 10 100 --reps 1" timeout -k 10 500 \
+        bash tools/pmc_run.sh "${TAG}_c5" > "$OUT/${TAG}_c5pmc.log" 2>&1
+      rc=$?
+      cp "profiles/${TAG}_c5_pmc_traffic.json" "$OUT/" 2>/dev/null ;;
     c5sq)
       SQ_CMD="python3 tools/score_bench.py --k 10 --reps 1" timeout -k 10 500 \
         bash tools/pmc_sq.sh "${TAG}c5" > "$OUT/${TAG}_c5sq.log" 2>&1
@@ -104,6 +111,23 @@ for what in "$@"; do
             --steps 100 --warmup 20 --prime 128 --no-c4 --no-score --no-cpu-baseline --no-dropin \
             > "$f" 2>&1 || { rc=$?; break 2; }
           python3 tools/bench_summ.py "$f" "$var=$v" >> "$OUT/${TAG}_sab.log" 2>&1
+        done
+      done ;;
+    dirsab:*)
+      # dirsab:DIR  the row-sharded bench at world 1 from DIR (another checkout, e.g. a git
+      # worktree of an earlier commit with its own built libraries) and from here, alternately
+      d="${what#dirsab:}"
+      rc=0
+      for k in 1 2; do
+        for where in "$d" .; do
+          f="$OUT/${TAG}_dirsab_$(basename "$where")_$k.log"
+          extra=""
+          [ "$where" = "." ] && extra="--batches 8"   # (the earlier bench cycled 8 batches)
+          (cd "$where" && timeout -k 10 200 python3 -m torch.distributed.run --nnodes=1 \
+            --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29519 bench.py --sharded \
+            --steps 100 --warmup 20 --prime 128 --no-c4 --no-score --no-cpu-baseline \
+            --no-dropin $extra) > "$f" 2>&1 || { rc=$?; break 2; }
+          python3 tools/bench_summ.py "$f" "dir=$where" >> "$OUT/${TAG}_dirsab.log" 2>&1
         done
       done ;;
     c5ab:*)
