@@ -27,7 +27,9 @@ namespace {
 
 // part[kind*nbr + block][0:D mf_g | D:2D mf_b | 2D:3D mlp_g | 3D:4D mlp_b]
 constexpr int kPW = NCF_PIECE_WAVES;   // waves per block
-constexpr int kRowBatch = 8;           // occurrence rows loaded per round (k_piece_reduce_ln)
+// occurrence rows loaded per round (k_piece_reduce_ln; 8 measured slower: the reduce + fix-up
+// 30.4-31.1 against 24.5-24.8 us in-step, the larger register set halving the resident waves)
+constexpr int kRowBatch = 4;
 template <int D, bool BF = false>
 __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     const uint32_t* __restrict__ sv0, const uint32_t* __restrict__ sv1,
@@ -87,8 +89,7 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     for (int j0 = 0; j0 < cmax; j0 += L) {
       const uint32_t r = (j0 + sub < cnt) ? sv[ps + j0 + sub] : 0u;
       const int jn = min(L, cmax - j0);
-      // kRowBatch rows of loads in flight, summed in order (8: a user's 5 occurrences in one
-      // round of loads instead of two)
+      // kRowBatch rows of loads in flight, summed in order
       for (int jj = 0; jj < jn; jj += kRowBatch) {
         float4 a[kRowBatch], b[kRowBatch];
 #pragma unroll

@@ -641,7 +641,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     const uint16_t* __restrict__ items3, const float* __restrict__ bias, int64_t n_items,
     int64_t items_per_block, int ub, const float* __restrict__ thr, int64_t cap,
     uint32_t* __restrict__ count, float* __restrict__ cand_logit,
-    int32_t* __restrict__ cand_item, int pingpong) {
+    int32_t* __restrict__ cand_item) {
   constexpr int D = 64;
   __shared__ __attribute__((aligned(16))) uint16_t ps[3][T][kItemTile][kP3];
   __shared__ float bs[3][kItemTile];
@@ -767,46 +767,41 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
     staged = 0;
   };
-  auto filt = [&](const f32x16& acc, int ub, float b, int64_t t0) {
+  auto filt = [&](const f32x16& acc, int ub, int bb, int64_t t0) {
     float th[16];
     th_of(ub, th);
     const int32_t item = (int32_t)(t0 + i);
+    const float b = bs[bb][i];
     const bool ivalid = t0 + i < it1;
-    // Cheap reject first: max_r (acc[r] - th[r]) + b on packed fp32 (8 v_pk_add + max3s),
-    // kept per group of 4 rows.  The margin keeps every lane the exact test below could accept
-    // (they round differently by at most an ulp of |b|; the subtraction near a hit is exact,
-    // Sterbenz).  At ~1 expected hit per 32 x 32 tile most tiles pass this test, so the exact
-    // per-row test runs only in the 4-row groups whose maximum passes it too (~1 of 4).
-    const float tol = -1e-6f * fabsf(b);
-    float gm[4];
+    // Cheap reject first: max_r (acc[r] - th[r]) + b on packed fp32 (8 v_pk_add + 8 max).  The
+    // margin keeps every lane the exact test below could accept (they round differently by at
+    // most an ulp of |b|; the subtraction near a hit is exact, Sterbenz).  (Keeping the maximum
+    // per group of 4 rows and testing rows only in the groups that pass measured slower: scan
+    // 2.19 against 2.05 ms at top-10.)
+    {
+      f32x2 m2 = {-INFINITY, -INFINITY};
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const f32x2 d0 = f32x2{acc[4 * c], acc[4 * c + 1]} - f32x2{th[4 * c], th[4 * c + 1]};
-      const f32x2 d1 = f32x2{acc[4 * c + 2], acc[4 * c + 3]} - f32x2{th[4 * c + 2], th[4 * c + 3]};
-      gm[c] = fmaxf(fmaxf(d0.x, d0.y), fmaxf(d1.x, d1.y));
+      for (int r = 0; r < 16; r += 2)
+        m2 = __builtin_elementwise_max(m2, f32x2{acc[r], acc[r + 1]} - f32x2{th[r], th[r + 1]});
+      const bool near = ivalid && fmaxf(m2.x, m2.y) + b >= -1e-6f * fabsf(b);
+      if (!__ballot(near)) return;
     }
-    if (!__ballot(ivalid && fmaxf(fmaxf(gm[0], gm[1]), fmaxf(gm[2], gm[3])) + b >= tol)) return;
     // exact hits row by row: one wave mask per user row, slice offsets from mbcnt; the slice is
     // written out first when the row's hits would not fit (a row has at most 64)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (!__ballot(ivalid && gm[c] + b >= tol)) continue;   // wave-uniform
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int r = 4 * c + rr;
-        const uint64_t hm = __ballot(ivalid && acc[r] + b >= th[r]);
-        if (hm == 0) continue;   // wave-uniform
-        const uint32_t nh = (uint32_t)__popcll(hm);
-        if (staged + nh > (uint32_t)kSlice3) wflush();
-        if ((hm >> lane) & 1) {
-          const uint32_t at = staged + __builtin_amdgcn_mbcnt_hi(
-              (uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-          wl[at] = acc[r] + b;
-          wi[at] = item;
-          wu[at] = (uint16_t)(32 * ub + (r & 3) + 8 * (r >> 2) + 4 * h);   // local user slot
-        }
-        staged += nh;
+    for (int r = 0; r < 16; ++r) {
+      const uint64_t hm = __ballot(ivalid && acc[r] + b >= th[r]);
+      if (hm == 0) continue;   // wave-uniform
+      const uint32_t nh = (uint32_t)__popcll(hm);
+      if (staged + nh > (uint32_t)kSlice3) wflush();
+      if ((hm >> lane) & 1) {
+        const uint32_t at = staged + __builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+        wl[at] = acc[r] + b;
+        wi[at] = item;
+        wu[at] = (uint16_t)(32 * ub + (r & 3) + 8 * (r >> 2) + 4 * h);   // local user slot
       }
+      staged += nh;
     }
   };
   // Iteration t multiplies tile t (buffer t % 3, operands in registers, the reads of tile t + 1
@@ -826,25 +821,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
       for (int t = 0; t < 4; ++t) rd(0, t);
     }
-    // Ping-pong (pingpong != 0, 8 waves): waves 4-7 share their SIMDs with waves 0-3 and run
-    // each tile interval in the opposite order — filter the previous tile's accumulators first,
-    // then multiply this tile — so on every SIMD one wave's MFMAs overlap the other's filter
-    // VALU work instead of both multiplying, then both filtering, between the same barriers.
-    // (The accumulators carry the tile across the barrier; the tile's bias is kept in a
-    // register, its LDS buffer is restaged by then.)
-    // (one-term scan only: the two- and three-term forms have no registers to spare for it)
-    const bool lag = T == 1 && NW == 8 && pingpong && __builtin_amdgcn_readfirstlane(w) >= 4;
-    f32x16 acc[UB];
-    float b_lag = 0.0f;
-    int64_t t_lag = -1;
     int bc = 0;
     for (int64_t t0 = it0; t0 < it1; t0 += kItemTile) {
       const int bn = bc == 2 ? 0 : bc + 1, bn2 = bn == 2 ? 0 : bn + 1;
       const bool has_next = t0 + kItemTile < it1;
-      if (lag && t_lag >= 0) {
-#pragma unroll
-        for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, b_lag, t_lag);
-      }
+      f32x16 acc[UB];
 #pragma unroll
       for (int ub = 0; ub < UB; ++ub)
 #pragma unroll
@@ -879,23 +860,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
           if (has_next) rd(bn, t);
         }
       }
-      if (lag) {
-        b_lag = bs[bc][i];
-        t_lag = t0;
-      } else {
+      // (Waves 4-7 filtering the previous tile before multiplying this one, so each SIMD
+      // overlaps one wave's MFMAs with its partner's filter, measured slower: scan 2.51-2.55
+      // against 2.19 ms at top-10.)
 #pragma unroll
-        for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, bs[bc][i], t0);
-      }
+      for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, bc, t0);
       if (t0 + 2 * kItemTile < it1) {
         put(bn2);
         if (t0 + 3 * kItemTile < it1) fetch(t0 + 3 * kItemTile);
       }
       __syncthreads();
       bc = bn;
-    }
-    if (lag && t_lag >= 0) {
-#pragma unroll
-      for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, b_lag, t_lag);
     }
   }
   if (staged)
@@ -1454,10 +1429,6 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
     else
       n_cu = 256;
   }
-  static const int pingpong = [] {
-    const char* e = getenv("NCF_SCORE_PINGPONG");
-    return e ? atoi(e) : 1;
-  }();
   const int nub = terms == 3 ? kUB3t : kUB3;
   const int64_t upb = 32 * kNW3 * nub;   // users per workgroup
   const int64_t ub = (n_users + upb - 1) / upb;
@@ -1507,17 +1478,17 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
     hipLaunchKernelGGL((k_collect3<kUB3t, kNW3, 3>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
                        items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
-                       cand_item, pingpong);
+                       cand_item);
   else if (terms == 2)
     hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 2>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
                        items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
-                       cand_item, pingpong);
+                       cand_item);
   else
     hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 1>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
                        items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
-                       cand_item, pingpong);
+                       cand_item);
   NCF_CHECK_LAUNCH("ncf_score_collect_split");
   return NCF_OK;
 }
