@@ -139,9 +139,10 @@ class ShardExchange:
 
 class RcclExchange(ShardExchange):
     """The same collectives issued through the C-ABI (``ncf_comm_*``: grouped ncclSend/ncclRecv
-    and ncclAllReduce on the step's own HIP streams) on one RCCL communicator of this library
-    (``main``; ``side`` is the same communicator in the plan-stream role: the pipelined count
-    exchange, the rows sent ahead and the dense all-reduce).  The communicators are created over
+    and ncclAllReduce on the step's own HIP streams) on two RCCL communicators of this library,
+    one per stream: ``main`` for the run's exchanges on the step's stream, ``side`` for the
+    pipelined count exchange, the rows sent ahead and the dense all-reduce on the plan stream
+    (the roles of ``group`` / ``plan_group``).  The communicators are created over
     ``group`` (unique ids broadcast by its rank 0).  Same results as ``ShardExchange``; none of
     the c10d per-call work (Work objects, stream-sync events, allocator bookkeeping)."""
 
@@ -149,17 +150,18 @@ class RcclExchange(ShardExchange):
         super().__init__(group, device, plan_group)
         if not _lib.query("ncf_comm_available"):
             raise RuntimeError("RcclExchange: librccl is not loaded in this process")
-        # ONE communicator for every collective of the step, whichever stream issues it: RCCL
-        # runs the operations of a communicator in the order they were issued on the host (each
-        # launch is ordered behind the communicator's previous one, whatever the user stream), so
-        # every rank executes the same sequence (counts / rows-ahead / dense all-reduce on the
-        # plan stream, row exchanges on the step's stream) and no spinning collective of one
-        # communicator can wait on a hardware queue behind another communicator's (DESIGN 6:
-        # 4 hardware queues per process).  ``side`` names the plan-stream role only.
+        # Two communicators, each used from ONE stream only: ``main`` on the step's stream (the
+        # row exchanges), ``side`` on the plan stream (the pipelined count exchange, the rows sent
+        # ahead, the dense all-reduce).  Every rank issues the same host program, so each stream
+        # — and each hardware queue two streams may share (4 per process) — receives
+        # the collectives in the same order on every rank: no rank can hold one communicator's
+        # collective in a queue ahead of another's that its peer runs first.  One communicator
+        # for both roles (NCF_RCCL_COMMS=1) makes RCCL order each collective behind the
+        # communicator's previous one across the two streams, which ties the plan stream (the
+        # next batch's sort, the overlapped sweep) to the step's: world 1, 0.48 against 0.35
+        # ms/step (gpurun_out/r4m_sab.log).
         self.main = self._comm()
-        # (NCF_RCCL_COMMS=2: a second communicator for the plan-stream role, the round-3 form;
-        # A/B of the single communicator's cross-stream ordering cost)
-        self.side = self._comm() if os.environ.get("NCF_RCCL_COMMS", "1") == "2" else self.main
+        self.side = self.main if os.environ.get("NCF_RCCL_COMMS", "2") == "1" else self._comm()
         W = self.world
         # host split arrays, one pair per call site: the collective reads them when it is
         # called, so a launch tape replays each site with the sizes written there for the step
