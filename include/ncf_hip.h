@@ -221,7 +221,8 @@ int ncf_attention_bwd(const float* q, const float* k, const float* v, const floa
 int ncf_attn_block_supported(int64_t dim, int64_t heads, int64_t group_len);
 /* user_ids (may be NULL): the user id of every row.  A workgroup whose groups each hold one user
  * (the reference's collate, data_prep.py:201) projects Q once per group (the same
- * bits as per row).                                                                          */
+ * bits as per row) and stashes it once per group, at the group's first row of q (the other rows
+ * of q are not written); ncf_attn_block_bwd given the same user_ids reads it there.           */
 int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t groups, int64_t group_len,
                        int64_t heads, int64_t dim, const float* wq, const float* bq,
                        const float* wk, const float* bk, const float* wv, const float* bv,

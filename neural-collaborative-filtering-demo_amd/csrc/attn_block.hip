@@ -202,9 +202,11 @@ __device__ __forceinline__ void stage_in(float* __restrict__ S, const float* __r
 // store.  (A load-then-store loop waits one HBM latency per iteration: stamped at 12K cycles
 // for the forward's two blocks and 20K for the backward's five, of 45K / 75K per workgroup.)
 // Rows >= `rows` are zeros.
+// Block `grp` (>= 0) is stored once per group (row gl M holds group gl's row, the forward's Q
+// stash with one user per group): its rows are read from their group's first row.
 template <int D, int NB>
 __device__ __forceinline__ void stage_in_n(float* const (&S)[NB], const float* const (&X)[NB],
-                                           int Rp, int rows) {
+                                           int Rp, int rows, int grp = -1, int M = 1) {
   constexpr int L4 = D / 4, P = AG<D>::kPitch;
   constexpr int IT = (16 * AG<D>::NTmax * L4 + kThreads - 1) / kThreads;
   float4 v[NB][IT];
@@ -213,7 +215,8 @@ __device__ __forceinline__ void stage_in_n(float* const (&S)[NB], const float* c
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int e = threadIdx.x + kThreads * it, r = e / L4, c = (e % L4) * 4;
-      v[b][it] = (e < Rp * L4 && r < rows) ? ld4(X[b] + (int64_t)r * D + c)
+      const int src = b == grp ? r - r % M : r;
+      v[b][it] = (e < Rp * L4 && r < rows) ? ld4(X[b] + (int64_t)src * D + c)
                                            : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
@@ -231,6 +234,17 @@ __device__ __forceinline__ void stage_out(float* __restrict__ X, const float* __
   constexpr int L = D / 4;
   for (int e = threadIdx.x; e < rows * L; e += blockDim.x) {
     const int r = e / L, c = (e % L) * 4;
+    st4(X + (int64_t)r * D + c, *reinterpret_cast<const float4*>(S + r * AG<D>::kPitch + c));
+  }
+}
+
+// rows 0, M, 2M, .. (each group's first row) of S into X (the per-group Q stash)
+template <int D>
+__device__ __forceinline__ void stage_out_groups(float* __restrict__ X, const float* __restrict__ S,
+                                                 int ng, int M) {
+  constexpr int L = D / 4;
+  for (int e = threadIdx.x; e < ng * L; e += blockDim.x) {
+    const int r = (e / L) * M, c = (e % L) * 4;
     st4(X + (int64_t)r * D + c, *reinterpret_cast<const float4*>(S + r * AG<D>::kPitch + c));
   }
 }
@@ -512,7 +526,14 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
   NCF_ASTAMP(0, 3);
   const float* src = S2;   // the out_proj input: O, or V when there is no core
   if (core) {
-    if (Q) stage_out<D>(Q + r0 * D, S0, rows);
+    // (one user per group: Q is stashed once per group, at the group's first row; the
+    // backward reads it there, deciding shq on the same ids)
+    if (Q) {
+      if (shq)
+        stage_out_groups<D>(Q + r0 * D, S0, ng, M);
+      else
+        stage_out<D>(Q + r0 * D, S0, rows);
+    }
     if (K) stage_out<D>(K + r0 * D, S1, rows);
     if (V) stage_out<D>(V + r0 * D, S2, rows);
     NCF_ASTAMP(0, 4);
@@ -669,14 +690,20 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
       __syncthreads();
     }
     attn_core_fwd<D, HD>(S1, S2, S3, S4, Pl, nullptr, g0, ng, M, scale, p_drop, seed);
-  } else if (wg) {
-    float* const dst[5] = {S0, S1, S2, S3, S4};
-    const float* const src[5] = {dY + r0 * D, Qg + r0 * D, Kg + r0 * D, Vg + r0 * D, Og + r0 * D};
-    stage_in_n<D, 5>(dst, src, Rp, rows);
   } else {
-    float* const dst[4] = {S0, S1, S2, S3};
-    const float* const src[4] = {dY + r0 * D, Qg + r0 * D, Kg + r0 * D, Vg + r0 * D};
-    stage_in_n<D, 4>(dst, src, Rp, rows);
+    // the forward stashed Q once per group where every group of the workgroup holds one user
+    // (the same test on the same ids); block 1 (Q) is then read from the group rows
+    const bool shq = share_q && M > 1 && uids && ids_uniform(uids + r0, ng, M);
+    if (wg) {
+      float* const dst[5] = {S0, S1, S2, S3, S4};
+      const float* const src[5] = {dY + r0 * D, Qg + r0 * D, Kg + r0 * D, Vg + r0 * D,
+                                   Og + r0 * D};
+      stage_in_n<D, 5>(dst, src, Rp, rows, shq ? 1 : -1, M);
+    } else {
+      float* const dst[4] = {S0, S1, S2, S3};
+      const float* const src[4] = {dY + r0 * D, Qg + r0 * D, Kg + r0 * D, Vg + r0 * D};
+      stage_in_n<D, 4>(dst, src, Rp, rows, shq ? 1 : -1, M);
+    }
   }
   if constexpr (PF) {
     frag_w<D>(wo, w, pw_o);
