@@ -1111,6 +1111,8 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
   }
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len, H = (int)heads;
+  // (the forward stashed Q once per group where it shared it: the same decision here)
+  const int share_q = share_ids(user_ids) != nullptr;
   const size_t lds = bwd_lds_d((int)dim, M, H, wg);
   const int nb = (int)ncf_cdiv(groups, groups_per_wg(dim));
   const dim3 grid((unsigned)nb);
@@ -1123,7 +1125,8 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
     if (!attr) { allow_lds(k_attn_block_bwd<D_, HD, false>, bwd_lds<D_>(kMaxM, D_ / HD, true)); attr = true; } \
     hipLaunchKernelGGL((k_attn_block_bwd<D_, HD, false>), grid, dim3(kThreads), lds, st, grad_y, q, k, \
                        v, probs, groups, M, wq, wk, wv, wo, scale, dropout_p, seed, clock, o, xu, xi, \
-                       part, grad_q, grad_k, grad_v, grad_xu, grad_xi, nullptr, nullptr, nullptr, user_ids, 0); \
+                       part, grad_q, grad_k, grad_v, grad_xu, grad_xi, nullptr, nullptr, nullptr, user_ids, \
+                       share_q);                                                                  \
   }
   NCF_ABB(64, 8)
   NCF_ABB(64, 16)
