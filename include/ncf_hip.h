@@ -215,7 +215,8 @@ int ncf_attention_bwd(const float* q, const float* k, const float* v, const floa
  * forward  q,k,v = LN rows x W^T + b, the core above (same P layout and dropout stream), y =
  *          o Wo^T + bo.  q = k = NULL: nothing is stashed (with M == 1 and no dropout this is
  *          the eval form, o = v; otherwise the core runs in LDS only, for ncf_attn_block_bwd_rc);
- *          probs/o required when q is given.
+ *          probs required when q is given; o may be NULL (not stashed: ncf_attn_block_bwd
+ *          given o = NULL recomputes it from probs and v with the forward's arithmetic).
  * backward from dY: dO = dY Wo, the core backward, dXu = dQ Wq, dXi = dK Wk + dV Wv, and the
  *          four Linear gradients (below).                                                     */
 int ncf_attn_block_supported(int64_t dim, int64_t heads, int64_t group_len);

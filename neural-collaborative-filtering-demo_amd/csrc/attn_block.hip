@@ -420,7 +420,39 @@ __device__ __forceinline__ void attn_core_fwd(const float* Qs, const float* Ks, 
   }
 }
 
-// per-workgroup partial of the four Linear gradients, in the flat parameter order
+// O = dropout(P) V from the forward's stashed probabilities (Pg, the [G][H][M][M] layout of
+// attn_core_fwd) and V in LDS: attn_core_fwd's own accumulation (the same pj, the same dropout
+// stream, fmaf over j in order), so O has the forward's bits without the forward stashing it.
+// Rows past the batch are left alone (the caller zeroes them).
+template <int D, int HD>
+__device__ __forceinline__ void attn_pv(const float* __restrict__ Pg, const float* Vs, float* Os,
+                                        int64_t g0, int ng, int M, float p_drop, uint64_t seed) {
+  constexpr int H = D / HD, kPitch = AG<D>::kPitch;
+  const float inv_keep = p_drop > 0.0f ? 1.0f / (1.0f - p_drop) : 1.0f;
+  const int ntask = ng * H * M;
+  for (int t = threadIdx.x; t < ntask; t += kThreads) {
+    const int i = t % M, h = (t / M) % H, gl = t / (M * H);
+    const int64_t tg = ((g0 + gl) * H + h) * M + i;
+    float o[HD];
+#pragma unroll
+    for (int d = 0; d < HD; ++d) o[d] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kMaxM; ++j)
+      if (j < M) {
+        const float pj = Pg[tg * M + j];
+        const float pd =
+            p_drop > 0.0f ? pj * ncf_dropout_scale(seed, (uint64_t)tg * M + j, p_drop, inv_keep) : pj;
+        const float* v = Vs + (gl * M + j) * kPitch + h * HD;
+#pragma unroll
+        for (int d = 0; d < HD; ++d) o[d] = fmaf(pd, v[d], o[d]);
+      }
+    float* dst = Os + (gl * M + i) * kPitch + h * HD;
+#pragma unroll
+    for (int d = 0; d < HD; d += 4) *reinterpret_cast<float4*>(dst + d) = make_float4(o[d], o[d + 1], o[d + 2], o[d + 3]);
+  }
+}
+
+// per-workgroup partial of the four Linear gradients, in the flat parameter order// per-workgroup partial of the four Linear gradients, in the flat parameter order
 // [q.weight | q.bias | k.weight | k.bias | v.weight | v.bias | out.weight | out.bias]
 // (AG<D>::kPartAttn floats)
 
@@ -694,11 +726,21 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     // the forward stashed Q once per group where every group of the workgroup holds one user
     // (the same test on the same ids); block 1 (Q) is then read from the group rows
     const bool shq = share_q && M > 1 && uids && ids_uniform(uids + r0, ng, M);
-    if (wg) {
+    if (wg && Og) {
       float* const dst[5] = {S0, S1, S2, S3, S4};
       const float* const src[5] = {dY + r0 * D, Qg + r0 * D, Kg + r0 * D, Vg + r0 * D,
                                    Og + r0 * D};
       stage_in_n<D, 5>(dst, src, Rp, rows, shq ? 1 : -1, M);
+    } else if (wg) {
+      // O not stashed: recomputed from the stashed P and V (attn_pv: the forward's bits)
+      float* const dst[4] = {S0, S1, S2, S3};
+      const float* const src[4] = {dY + r0 * D, Qg + r0 * D, Kg + r0 * D, Vg + r0 * D};
+      stage_in_n<D, 4>(dst, src, Rp, rows, shq ? 1 : -1, M);
+      for (int e = threadIdx.x; e < (Rp - rows) * L4; e += kThreads)   // padded rows: zeros
+        *reinterpret_cast<float4*>(S4 + (rows + e / L4) * kPitch + (e % L4) * 4) =
+            make_float4(0.f, 0.f, 0.f, 0.f);
+      __syncthreads();
+      attn_pv<D, HD>(Pg, S3, S4, g0, ng, M, p_drop, seed);
     } else {
       float* const dst[4] = {S0, S1, S2, S3};
       const float* const src[4] = {dY + r0 * D, Qg + r0 * D, Kg + r0 * D, Vg + r0 * D};
@@ -1002,8 +1044,9 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_attn_block_fwd: dropout_p out of [0,1)");
   NCF_CHECK_ARG(y != nullptr && (q != nullptr) == (k != nullptr),
                 "ncf_attn_block_fwd: q and k are given together (or neither)");
-  NCF_CHECK_ARG(q == nullptr || (probs != nullptr && o != nullptr),
-                "ncf_attn_block_fwd: a stashing forward needs probs and o");
+  NCF_CHECK_ARG(q == nullptr || probs != nullptr,
+                "ncf_attn_block_fwd: a stashing forward needs probs (o may be NULL: the backward "
+                "recomputes it from probs and v)");
   // the core runs unless the eval form applies (M == 1 without dropout: softmax == 1, o = v);
   // without q/k it stashes nothing (training with ncf_attn_block_bwd_rc)
   const int core = (q != nullptr || group_len > 1 || dropout_p > 0.0f) ? 1 : 0;
@@ -1101,8 +1144,8 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
                 "M<=%d)", (long long)dim, (long long)heads, (long long)group_len, kMaxM);
   NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_attn_block_bwd: dropout_p out of [0,1)");
   const bool wg = grad_params != nullptr;
-  NCF_CHECK_ARG(!wg || (o && xu && xi && workspace), "ncf_attn_block_bwd: the fused weight "
-                "gradients need o, xu, xi and a workspace");
+  NCF_CHECK_ARG(!wg || (xu && xi && workspace), "ncf_attn_block_bwd: the fused weight "
+                "gradients need xu, xi and a workspace");
   NCF_CHECK_ARG(wg || (grad_q && grad_k && grad_v),
                 "ncf_attn_block_bwd: without grad_params, grad_q/k/v are required");
   if (wg && workspace_floats < ncf_attn_block_bwd_workspace(groups)) {

@@ -32,6 +32,9 @@ BF16_MM = True
 # against 12.2-12.3 us)
 GROUP_ROWS = True
 _WGRAD_ROWS = 160
+# the fused attention forward's O stash (off: the backward recomputes O from the stashed P and V,
+# attn_pv, the same bits); NCF_ATTN_STASH_O=1: stash it (A/B)
+_STASH_O = os.environ.get("NCF_ATTN_STASH_O", "0") != "0"
 
 
 def _tptr(t) -> int:
@@ -455,7 +458,7 @@ class NCFEngine:
                       drop_p if train else 0.0, seed, ptr(self.clock),
                       ptr(w.q) if core else None, ptr(w.k) if core else None,
                       ptr(w.v) if core else None, ptr(w.P) if core else None,
-                      ptr(w.o) if core else None, ptr(w.y), ptr(uid), st)
+                      ptr(w.o) if core and _STASH_O else None, ptr(w.y), ptr(uid), st)
             # a7: MLP tower on [attn ‖ zeros_T] (architecture.py:329-344): the zero temporal
             # columns contribute nothing, so layer 0 reads only the first D columns of mlp.0.weight
             x, ldx, kin = w.y, D, D
@@ -771,7 +774,8 @@ class NCFEngine:
             else:
                 _lib.call("ncf_attn_block_bwd", ptr(w.dy), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P),
                           n // M, M, H, D, *pp["att_w"], drop_p, seed,
-                          ptr(self.clock), ptr(w.o), ptr(w.xu), ptr(w.xi), gp[1], ptr(ws),
+                          ptr(self.clock), ptr(w.o) if _STASH_O else None, ptr(w.xu), ptr(w.xi),
+                          gp[1], ptr(ws),
                           ws.numel(), w.red_list.address, None, None, None, ptr(w.dxu),
                           ptr(w.dxi), ptr(uid), st)
         else:

@@ -830,6 +830,41 @@ def test_group_rows_bitwise_equals_every_row(monkeypatch, mixed):
         assert torch.equal(out[0][1][k][1], out[1][1][k][1]), k
 
 
+def test_attn_o_recompute_bitwise_equals_o_stash(monkeypatch):
+    """The attention backward recomputing O = dropout(P) V from the forward's stashed P and V
+    (attn_pv, the forward's own accumulation; the forward then stashes no O) against the O
+    stash: parameters and Adam moments bit-identical over 6 FusedTrainStep steps with dropout,
+    the last workgroup ragged."""
+    from ncf_amd import engine as E
+    from ncf_amd.trainer import FusedTrainStep
+    U, I, B, M = 3000, 500, 61, 5
+    g = torch.Generator().manual_seed(37)
+    batches = []
+    for _ in range(6):
+        u = torch.randint(0, U, (B,), generator=g).repeat_interleave(M)
+        i = torch.randint(0, I, (B * M,), generator=g)
+        t = torch.zeros(B, M)
+        t[:, 0] = 1
+        batches.append((u.to(DEV), i.to(DEV), t.reshape(-1, 1).to(DEV)))
+    out = []
+    for stash in (True, False):
+        monkeypatch.setattr(E, "_STASH_O", stash)
+        torch.manual_seed(38)
+        m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.2, M - 1).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+        for u, i, t in batches:
+            step(u, i, t)
+        step.sync()
+        out.append(({k: v.detach().cpu().clone() for k, v in m.state_dict().items()},
+                    {k: (v["exp_avg"].cpu().clone(), v["exp_avg_sq"].cpu().clone())
+                     for k, v in step.state.items()}))
+    for k in out[0][0]:
+        assert torch.equal(out[0][0][k], out[1][0][k]), k
+    for k in out[0][1]:
+        assert torch.equal(out[0][1][k][0], out[1][1][k][0]), k
+        assert torch.equal(out[0][1][k][1], out[1][1][k][1]), k
+
+
 def test_graph_replay_bitwise_equals_eager_clock():
     """hipGraph capture + replay of the whole training step (dropout on: the per-step stream
     comes from the device clock) == the same clock-driven steps run eagerly, bit for bit, across
