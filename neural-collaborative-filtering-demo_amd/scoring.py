@@ -132,12 +132,15 @@ def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st, expected=0, t
                   count, cand_l, cand_i, st)
 
 
-# Expected candidates per user the threshold sample aims at: ~1024 (a bigger sample costs a
-# longer sample GEMM and k-th select, a smaller one more scan hits and select work; measured
-# 1024 -> 7.5 ms, 2048 -> 7.7, cap / 2 = 4096 -> 8.3 at top-10 over 1M items), with the sample
+# Expected candidates per user the threshold sample aims at: 512 (a bigger sample costs a
+# longer sample GEMM and k-th select, a smaller one more scan hits and select work; round 1,
+# fp32 scan: 1024 -> 7.5 ms, 2048 -> 7.7, cap / 2 = 4096 -> 8.3 at top-10 over 1M items), with the sample
 # kept within the k-th kernel's LDS-resident size (top-100: ~2570; a 30720-logit cap: 6.26 ms,
 # 38912: 5.90 ms), and never above cap / 2.
-SAMPLE_CANDS = 1024
+# (round 4, 10K x 1M eager, 2-4 interleaved runs: top-10 2.61-2.64 ms at 512 (scan 1.78-1.80,
+# sample + k-th 0.42) against 2.64-2.82 at 1024 (scan 1.99-2.04, sample + k-th 0.21) and
+# 2.99-3.16 at 2048; top-100 takes the rank-j plan, unaffected)
+SAMPLE_CANDS = 512
 # the split scan's item split raised from the expected candidates per user (the launch's
 # expected_per_user: fewer per-wave LDS slice overflows; tested invisible in the results)
 SIZED_SPLIT = True
