@@ -12,6 +12,13 @@
 // they read row 0 and raise bit 0 of *err (the Python layer turns that into IndexError).
 #include "ncf_common.h"
 
+// Every multiply and add below is its own IEEE operation (no fma contraction): which products the
+// backend fuses depends on how the SLP vectoriser packed the float4 lanes, so the one- and
+// two-float4-per-lane kernels (and ncf_gather_rows) would otherwise round differently.  With
+// contraction off their arithmetic is the written expression order and their outputs are the
+// same bits (tests/test_gpu_parity.py::test_gather_two_float4_lanes_bitwise_equals_one_float4).
+#pragma clang fp contract(off)
+
 namespace {
 
 template <int D>
@@ -86,6 +93,90 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
   if (i_mf_ln) st4(i_mf_ln + row * D + c, yi);
 }
 
+// The same with D/8 lanes per row, each holding two float4 (columns 4k and 4k + D/2): twice the
+// loads in flight per lane, half the waves, one shuffle step fewer per reduction.  Bit-identical
+// to the one-float4 kernel: a lane first adds its two halves' partial sums, which is the first level of
+// the D/4-lane xor tree (lane k + lane k + D/8), then the remaining levels run as before.
+template <int D>
+struct RowLN2 {
+  static constexpr int L = D / 8;
+  __device__ __forceinline__ static float s4(float4 x) { return x.x + x.y + x.z + x.w; }
+  __device__ __forceinline__ static float q4(float4 c) {
+    return c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w;
+  }
+  __device__ __forceinline__ static float4 aff(float4 c, float rstd, float4 g, float4 b) {
+    return make_float4(c.x * rstd * g.x + b.x, c.y * rstd * g.y + b.y, c.z * rstd * g.z + b.z,
+                       c.w * rstd * g.w + b.w);
+  }
+  __device__ __forceinline__ static void ln(float4& x0, float4& x1, float4 g0, float4 g1,
+                                            float4 b0, float4 b1, float eps) {
+    const float s = group_sum<L>(s4(x0) + s4(x1));
+    const float mean = s * (1.0f / D);
+    const float4 c0 = make_float4(x0.x - mean, x0.y - mean, x0.z - mean, x0.w - mean);
+    const float4 c1 = make_float4(x1.x - mean, x1.y - mean, x1.z - mean, x1.w - mean);
+    const float q = group_sum<L>(q4(c0) + q4(c1));
+    const float rstd = 1.0f / sqrtf(q * (1.0f / D) + eps);
+    x0 = aff(c0, rstd, g0, b0);
+    x1 = aff(c1, rstd, g1, b1);
+  }
+};
+
+// (same kernel name, third template argument = float4 per lane, so profiles keep one row for it)
+template <int D, bool BF, int F4>
+__global__ __launch_bounds__(256) void k_gather_ln_gmf(
+    const int64_t* __restrict__ uid, const int64_t* __restrict__ iid, int64_t n,
+    const float* __restrict__ mfU, const float* __restrict__ mfI, const float* __restrict__ mlpU,
+    const float* __restrict__ mlpI, int64_t nU, int64_t nI, const float* __restrict__ g_mf,
+    const float* __restrict__ b_mf, const float* __restrict__ g_mlp, const float* __restrict__ b_mlp,
+    const float* __restrict__ w_mf, const float* __restrict__ bias_mf, float eps,
+    float* __restrict__ mf_pred, float* __restrict__ u_mlp_ln, float* __restrict__ i_mlp_ln,
+    float* __restrict__ u_mf_ln, float* __restrict__ i_mf_ln, int* err, int64_t G) {
+  static_assert(F4 == 2, "two float4 per lane");
+  constexpr int L = D / 8, H2 = D / 2;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = t / L;
+  const int sub = (int)(t % L);
+  if (row >= n) return;  // whole groups retire together
+  const int64_t uraw = uid[row];
+  const int64_t u = safe_id(uraw, nU, err, sub == 0);
+  const int64_t i = safe_id(iid[row], nI, err, sub == 0);
+  const bool src = G <= 1 || row % G == 0 || uraw != uid[row - row % G];
+  const int c0 = sub * 4, c1 = c0 + H2;
+  float4 u0 = ldp4<BF>(mfU, u * D + c0), u1 = ldp4<BF>(mfU, u * D + c1);
+  float4 i0 = ldp4<BF>(mfI, i * D + c0), i1 = ldp4<BF>(mfI, i * D + c1);
+  float4 z0 = ldp4<BF>(mlpI, i * D + c0), z1 = ldp4<BF>(mlpI, i * D + c1);
+  float4 m0 = make_float4(0.f, 0.f, 0.f, 0.f), m1 = m0;
+  if (src) {   // (uniform in the row's lane group)
+    m0 = ldp4<BF>(mlpU, u * D + c0);
+    m1 = ldp4<BF>(mlpU, u * D + c1);
+  }
+  const float4 gm0 = ld4(g_mf + c0), gm1 = ld4(g_mf + c1), bm0 = ld4(b_mf + c0), bm1 = ld4(b_mf + c1);
+  const float4 gl0 = ld4(g_mlp + c0), gl1 = ld4(g_mlp + c1), bl0 = ld4(b_mlp + c0), bl1 = ld4(b_mlp + c1);
+  RowLN2<D>::ln(u0, u1, gm0, gm1, bm0, bm1, eps);
+  RowLN2<D>::ln(i0, i1, gm0, gm1, bm0, bm1, eps);
+  RowLN2<D>::ln(z0, z1, gl0, gl1, bl0, bl1, eps);
+  const float4 w0 = ld4(w_mf + c0), w1 = ld4(w_mf + c1);
+  const float d0 = u0.x * i0.x * w0.x + u0.y * i0.y * w0.y + u0.z * i0.z * w0.z + u0.w * i0.w * w0.w;
+  const float d1 = u1.x * i1.x * w1.x + u1.y * i1.y * w1.y + u1.z * i1.z * w1.z + u1.w * i1.w * w1.w;
+  const float dot = group_sum<L>(d0 + d1);
+  if (sub == 0) mf_pred[row] = dot + bias_mf[0];
+  if (src) {
+    RowLN2<D>::ln(m0, m1, gl0, gl1, bl0, bl1, eps);
+    st4(u_mlp_ln + row * D + c0, m0);
+    st4(u_mlp_ln + row * D + c1, m1);
+    if (u_mf_ln) {
+      st4(u_mf_ln + row * D + c0, u0);
+      st4(u_mf_ln + row * D + c1, u1);
+    }
+  }
+  st4(i_mlp_ln + row * D + c0, z0);
+  st4(i_mlp_ln + row * D + c1, z1);
+  if (i_mf_ln) {
+    st4(i_mf_ln + row * D + c0, i0);
+    st4(i_mf_ln + row * D + c1, i1);
+  }
+}
+
 // Plain row gather (EBC forward as seen by callers such as app.py:156-184) with optional LN
 // (get_user_embeddings / get_product_embeddings, architecture.py:383-407).
 // L2 = true: each (LN'd) row divided by its Euclidean norm (the ANN export of
@@ -120,6 +211,16 @@ int launch_gather_ln_gmf(const int64_t* uid, const int64_t* iid, int64_t n, cons
                          float* mf_pred, float* u_mlp_ln, float* i_mlp_ln, float* u_mf_ln,
                          float* i_mf_ln, int* err, const float* item_scale, float scale_factor,
                          int64_t G, hipStream_t st) {
+  // D/8 lanes per row (the same bits; measured in-step 11.4-11.6 us either way at C2, rocprof
+  // 10.1 against 10.3 us fp32 tables and 8.7 against 9.3 us bf16 tables)
+  if (D >= 32 && item_scale == nullptr) {
+    const int64_t threads = n * (D / 8);
+    hipLaunchKernelGGL((k_gather_ln_gmf<D, BF, 2>), dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st,
+                       uid, iid, n, mfU, mfI, mlpU, mlpI, nU, nI, g_mf, b_mf, g_mlp, b_mlp, w_mf,
+                       bias_mf, eps, mf_pred, u_mlp_ln, i_mlp_ln, u_mf_ln, i_mf_ln, err, G);
+    NCF_CHECK_LAUNCH("ncf_gather_ln_gmf_fwd");
+    return NCF_OK;
+  }
   const int64_t threads = n * (D / 4);
   hipLaunchKernelGGL((k_gather_ln_gmf<D, BF>), dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st, uid, iid,
                      n, mfU, mfI, mlpU, mlpI, nU, nI, g_mf, b_mf, g_mlp, b_mlp, w_mf, bias_mf, eps,

@@ -865,6 +865,42 @@ def test_attn_o_recompute_bitwise_equals_o_stash(monkeypatch):
         assert torch.equal(out[0][1][k][1], out[1][1][k][1]), k
 
 
+@pytest.mark.parametrize("D,G", [(32, 0), (64, 0), (64, 5), (128, 3), (256, 0)])
+def test_gather_two_float4_lanes_bitwise_equals_one_float4(D, G):
+    """k_gather_ln_gmf with D/8 lanes per row (two float4 each, the plain entry point's kernel)
+    against the D/4-lane kernel (taken by the scaled entry point; scale 1 + 0 * s == 1 exactly):
+    every output bit-identical, including the group-rows copy skip and out-of-range ids."""
+    from ncf_amd import _lib
+    g = torch.Generator().manual_seed(D + G)
+    U, I, n = 700, 300, 1003 if G == 0 else 200 * G
+    uid = torch.randint(0, U, (n,), generator=g)
+    if G:
+        uid = uid.view(-1, G)[:, :1].repeat(1, G).reshape(-1)
+        uid[G * 7 + 2] = 5          # a row that leaves its group's user
+    iid = torch.randint(0, I, (n,), generator=g)
+    iid[11] = I + 4                 # out of range: row 0 and the error bit
+    t = lambda *s: (torch.randn(*s, generator=g) * 0.7 + 0.1).to(DEV)
+    tabs = [t(U, D), t(I, D), t(U, D), t(I, D)]
+    par = [t(D), t(D), t(D), t(D), t(D), t(1)]
+    uid, iid = uid.to(DEV), iid.to(DEV)
+    P = lambda x: x.data_ptr()
+    res = []
+    for scaled in (False, True):
+        outs = [torch.full((n,), 7.0, device=DEV)] + [torch.full((n, D), 7.0, device=DEV)
+                                                      for _ in range(4)]
+        err = torch.zeros(1, dtype=torch.int32, device=DEV)
+        head = [P(uid), P(iid), n, *map(P, tabs), U, I, D, *map(P, par), 1e-5]
+        zs = torch.zeros(n, D, device=DEV) if scaled else None
+        _lib.call("ncf_gather_ln_gmf_scaled_fwd", *head, P(zs) if scaled else 0, 0.0, G,
+                  *map(P, outs), P(err), _lib.stream_ptr(DEV))
+        torch.cuda.synchronize()
+        res.append([o.cpu() for o in outs] + [err.cpu()])
+    assert res[0][-1].item() & 1
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a.view(torch.int32) if a.is_floating_point() else a,
+                           b.view(torch.int32) if b.is_floating_point() else b)
+
+
 def test_graph_replay_bitwise_equals_eager_clock():
     """hipGraph capture + replay of the whole training step (dropout on: the per-step stream
     comes from the device clock) == the same clock-driven steps run eagerly, bit for bit, across
