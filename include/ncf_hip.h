@@ -499,10 +499,14 @@ int ncf_score_kth(const float* logits, int64_t n_users, int64_t S, int K, const 
  * two-term split logit q_u . p_(j*stride) + sample_bias[j] (items3: the ncf_score_split_items
  * planes of the n_items rows), within 1e-4 |q_u| max|p| of the fp32 logit; then its k-th per
  * user (S <= 38912).  A valid threshold is the k-th lowered by that bound (ncf_score_margin with
- * c = 1e-4): replaces ncf_gemm_f32 + ncf_score_kth with half the bytes and 16x the MFMA rate. */
+ * c = 1e-4): replaces ncf_gemm_f32 + ncf_score_kth with half the bytes and 16x the MFMA rate.
+ * group = 8: out holds rows of Sg = ceil(S / 8), out[u*Sg + g] = the largest of the fp16 values of
+ * sample items 8g .. 8g + 7 (the K-th largest group maximum is <= the K-th largest sample logit:
+ * the same bound, 8x fewer bytes written and selected over); group = 1: rows of S. */
 int ncf_score_sample_split16(const float* queries, int64_t n_users, const uint16_t* items3,
                              int64_t n_items, int64_t dim, int64_t stride,
-                             const float* sample_bias, int64_t S, uint16_t* out, void* stream);
+                             const float* sample_bias, int64_t S, int64_t group, uint16_t* out,
+                             void* stream);
 int ncf_score_kth16(const uint16_t* logits, int64_t n_users, int64_t S, int K, float* thr,
                     void* stream);
 int ncf_score_collect(const float* queries, const int32_t* user_list, int64_t n_users,

@@ -146,7 +146,7 @@ SIGNATURES = {
     "ncf_score_queries": (I32, [P, I64, P, I64, I64, P, P, F32, P, P, P, P, P]),
     "ncf_score_item_bias": (I32, [P, I64, P, P, P, P, P]),
     "ncf_score_kth": (I32, [P, I64, I64, I32, P, I64, P, P]),
-    "ncf_score_sample_split16": (I32, [P, I64, P, I64, I64, I64, P, I64, P, P]),
+    "ncf_score_sample_split16": (I32, [P, I64, P, I64, I64, I64, P, I64, I64, P, P]),
     "ncf_score_kth16": (I32, [P, I64, I64, I32, P, P]),
     "ncf_score_collect": (I32, [P, P, I64, P, P, I64, I64, P, I64, P, P, P, P]),
     "ncf_score_split_items": (I32, [P, I64, I64, P, P]),

@@ -919,12 +919,20 @@ __device__ __forceinline__ void bitonic_desc(unsigned long long* keys, int n2) {
 // Against the fp32 sample GEMM: 16x the matrix rate, half the bytes written and re-read (fp16).
 // Workgroup: 128 sample items staged in LDS (both planes), 4 waves x 32 users, each wave four
 // 32 x 32 tiles (one per 32 items).
-template <int T>
+// G > 1: only the maximum of each group of G consecutive sample items is stored (out row length
+// Sg = ceil(S / G)), reduced across the G lanes that hold the group before the one rounding
+// (round-down is monotone: the stored value is the group's largest stored G = 1 value, bit for
+// bit).  The K-th largest group maximum v has K distinct items at or above it, so it is <= the
+// K-th largest of the whole sample and the same bound argument holds; the sample's write and
+// the k-th select's read shrink G times.
+template <int T, int G>
 __global__ __launch_bounds__(256) void k_sample16(const float* __restrict__ q, int64_t n_users,
                                                   const uint16_t* __restrict__ items3,
                                                   int64_t n_items, int64_t stride,
                                                   const float* __restrict__ sbias, int64_t S,
                                                   _Float16* __restrict__ out) {
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16 || G == 32, "group of lanes");
+  const int64_t Sg = (S + G - 1) / G;
   constexpr int D = 64, J = 128;
   __shared__ __attribute__((aligned(16))) uint16_t ps[T][J][kP3];
   __shared__ float bs[J];
@@ -980,13 +988,26 @@ __global__ __launch_bounds__(256) void k_sample16(const float* __restrict__ q, i
       }
     }
     const int64_t j = j0 + 32 * jt + i;
-    if (j < S) {
+    if constexpr (G == 1) {
+      if (j < S) {
+        const float b = bs[32 * jt + i];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t u = u0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (u < n_users)
+            out[u * S + j] = __builtin_bit_cast(_Float16, __ocml_cvtrtn_f16_f32(acc[r] + b));
+        }
+      }
+    } else {   // (j0 and the 32-item tiles are multiples of G: a group never spans two tiles)
       const float b = bs[32 * jt + i];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
+        float v = j < S ? acc[r] + b : -INFINITY;
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
         const int64_t u = u0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (u < n_users)
-          out[u * S + j] = __builtin_bit_cast(_Float16, __ocml_cvtrtn_f16_f32(acc[r] + b));
+        if (i % G == 0 && j < S && u < n_users)
+          out[u * Sg + j / G] = __builtin_bit_cast(_Float16, __ocml_cvtrtn_f16_f32(v));
       }
     }
   }
@@ -1301,15 +1322,20 @@ extern "C" int ncf_score_kth(const float* logits, int64_t n_users, int64_t S, in
 extern "C" int ncf_score_sample_split16(const float* queries, int64_t n_users,
                                         const uint16_t* items3, int64_t n_items, int64_t dim,
                                         int64_t stride, const float* sample_bias, int64_t S,
-                                        uint16_t* out, void* stream) {
+                                        int64_t group, uint16_t* out, void* stream) {
   NCF_CHECK_ARG(dim == 64, "ncf_score_sample_split16: dim must be 64");
   NCF_CHECK_ARG(n_users >= 0 && S >= 1 && stride >= 1 && (S - 1) * stride < n_items &&
-                    queries && items3 && sample_bias && out,
+                    (group == 1 || group == 8) && queries && items3 && sample_bias && out,
                 "ncf_score_sample_split16: bad args");
   if (n_users == 0) return NCF_OK;
-  hipLaunchKernelGGL(k_sample16<2>, dim3((unsigned)ncf_cdiv(S, 128), (unsigned)ncf_cdiv(n_users, 128)),
-                     dim3(256), 0, (hipStream_t)stream, queries, n_users, items3, n_items, stride,
-                     sample_bias, S, reinterpret_cast<_Float16*>(out));
+  const dim3 grid((unsigned)ncf_cdiv(S, 128), (unsigned)ncf_cdiv(n_users, 128));
+  _Float16* o = reinterpret_cast<_Float16*>(out);
+  if (group == 8)
+    hipLaunchKernelGGL((k_sample16<2, 8>), grid, dim3(256), 0, (hipStream_t)stream, queries,
+                       n_users, items3, n_items, stride, sample_bias, S, o);
+  else
+    hipLaunchKernelGGL((k_sample16<2, 1>), grid, dim3(256), 0, (hipStream_t)stream, queries,
+                       n_users, items3, n_items, stride, sample_bias, S, o);
   NCF_CHECK_LAUNCH("ncf_score_sample_split16");
   return NCF_OK;
 }

@@ -140,7 +140,7 @@ def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st, expected=0, t
 # (round 4, 10K x 1M eager, 2-4 interleaved runs: top-10 2.61-2.64 ms at 512 (scan 1.78-1.80,
 # sample + k-th 0.42) against 2.64-2.82 at 1024 (scan 1.99-2.04, sample + k-th 0.21) and
 # 2.99-3.16 at 2048; top-100 takes the rank-j plan, unaffected)
-SAMPLE_CANDS = 512
+SAMPLE_CANDS = int(os.environ.get("NCF_SCORE_SAMPLE_CANDS", "512"))
 # the split scan's item split raised from the expected candidates per user (the launch's
 # expected_per_user: fewer per-wave LDS slice overflows; tested invisible in the results)
 SIZED_SPLIT = True
@@ -150,6 +150,10 @@ KTH_LDS_MAX = 38912   # = score.hip kKthLdsMax
 # fp32 k-th (measured, 10K x 1M eager: top-100 4.25 -> 3.73 ms, top-10 2.78 -> 2.70); needs the
 # split index (p3, pmax); tests compare both
 SAMPLE16 = True
+# the fp16 sample keeps only the maximum of every SAMPLE_GROUP consecutive sample items (the k-th
+# largest group maximum bounds the k-th largest logit from below as well), where the sample
+# holds >= 8 j group maxima: 8x fewer bytes written and selected over; 1 = every logit
+SAMPLE_GROUP = int(os.environ.get("NCF_SCORE_SAMPLE_GROUP", "8"))
 
 
 def _select(idx, rows, n, run, k, out_s, out_i, overflow, st, terms=None, check=None):
@@ -225,10 +229,14 @@ class _TopKRun:
             self.S = _sample_size(I, k, cap)
             self.stride = I // self.S
             self.sbias = index.bias[::self.stride][:self.S].contiguous()
+        # sample group maxima (fp16 path): rows of Sg = ceil(S / G)
+        self.G = SAMPLE_GROUP if self.s16 and SAMPLE_GROUP > 1 and \
+            self.S // SAMPLE_GROUP >= 8 * self.j else 1
+        self.Sg = -(-self.S // self.G)
         self.q, self.thr = e(max(n, 1), D), e(max(n, 1))
         # the rank-j thresholds before the margins (the select's check)
         self.thr_chk = e(max(n, 1)) if self.j < k else None
-        self.sample = (torch.empty(max(n, 1), self.S, dtype=torch.int16, device=dev) if self.s16
+        self.sample = (torch.empty(max(n, 1), self.Sg, dtype=torch.int16, device=dev) if self.s16
                        else e(max(n, 1), self.S))
         self.count = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
         self.cand_l, self.cand_i = e(max(n, 1), cap), e(max(n, 1), cap, dt=torch.int32)
@@ -249,8 +257,8 @@ class _TopKRun:
                   ptr(self.err), st)
         if self.s16:
             _lib.call("ncf_score_sample_split16", ptr(self.q), n, ptr(idx.p3), I, D, self.stride,
-                      ptr(self.sbias), self.S, ptr(self.sample), st)
-            _lib.call("ncf_score_kth16", ptr(self.sample), n, self.S, self.j, ptr(self.thr), st)
+                      ptr(self.sbias), self.S, self.G, ptr(self.sample), st)
+            _lib.call("ncf_score_kth16", ptr(self.sample), n, self.Sg, self.j, ptr(self.thr), st)
             if self.thr_chk is not None:
                 self.thr_chk.copy_(self.thr)
             # (the k-th of the fp16 sample is a bound after the two-term error is taken off)

@@ -1276,6 +1276,55 @@ def test_fp16_threshold_sample_equals_fp32_sample(k, cap, monkeypatch):
     assert torch.equal(s16, s32)
 
 
+def test_sample_group_maxima_bitwise_equal_max_of_sample():
+    """ncf_score_sample_split16 with group 8 stores, per user, the largest fp16 value of every 8
+    consecutive sample items: bit for bit the max over the group of the group-1 sample (ragged
+    last group, users not a multiple of the 128-user tile)."""
+    from ncf_amd import _lib
+    from ncf_amd.scoring import ItemIndex
+    torch.manual_seed(29)
+    U, I, n, S, stride = 500, 30011, 300, 3003, 7
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    idx = ItemIndex(m)
+    assert idx.p3 is not None
+    q = torch.randn(n, 64, device=DEV)
+    sb = torch.randn(S, device=DEV)
+    full = torch.empty(n, S, dtype=torch.int16, device=DEV)
+    Sg = -(-S // 8)
+    grp = torch.empty(n, Sg, dtype=torch.int16, device=DEV)
+    st = _lib.stream_ptr(DEV)
+    for g, out in ((1, full), (8, grp)):
+        _lib.call("ncf_score_sample_split16", q.data_ptr(), n, idx.p3.data_ptr(), I, 64, stride,
+                  sb.data_ptr(), S, g, out.data_ptr(), st)
+    torch.cuda.synchronize()
+    f = full.view(torch.float16).float().cpu()
+    pad = torch.full((n, Sg * 8 - S), float("-inf"))
+    want = torch.cat([f, pad], 1).view(n, Sg, 8).amax(2)
+    assert torch.equal(grp.view(torch.float16).float().cpu(), want)
+
+
+@pytest.mark.parametrize("k", [10, 100])
+def test_sample_group_maxima_same_topk(k, monkeypatch):
+    """The C5 pipeline with the threshold sample's group maxima (SAMPLE_GROUP 8) against every
+    sample logit (1): the same top-k items and score bits (only the threshold may differ)."""
+    from ncf_amd import scoring
+    from ncf_amd.scoring import ItemIndex, score_topk
+    torch.manual_seed(31)
+    U, I = 5000, 100003
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    users = torch.randperm(U)[:700]
+    idx = ItemIndex(m)
+    assert scoring._TopKRun(idx, 700, k, 8192).G == 8
+    s8, i8 = score_topk(m, users, k=k, index=idx, cap=8192)
+    monkeypatch.setattr(scoring, "SAMPLE_GROUP", 1)
+    assert scoring._TopKRun(idx, 700, k, 8192).G == 1
+    s1, i1 = score_topk(m, users, k=k, index=idx, cap=8192)
+    assert torch.equal(i8, i1)
+    assert torch.equal(s8, s1)
+
+
 @pytest.mark.parametrize("k,cap", [(100, 8192), (40, 8192), (100, 4096)])
 def test_rank_j_threshold_equals_kth_threshold(k, cap, monkeypatch):
     """Rank-j thresholds (the sample's 16th largest logit over a sample ~k/16 times smaller,
