@@ -19,7 +19,6 @@ all-gathered (RCCL) and merged per user by ``ncf_score_merge``.  ``forward_simpl
 hour variant draws a fresh random projection on every call, architecture.py:437-442, so it has no
 reusable item side).  GPU only; no CPU fallback.
 """
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -140,7 +139,7 @@ def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st, expected=0, t
 # (round 4, 10K x 1M eager, 2-4 interleaved runs: top-10 2.61-2.64 ms at 512 (scan 1.78-1.80,
 # sample + k-th 0.42) against 2.64-2.82 at 1024 (scan 1.99-2.04, sample + k-th 0.21) and
 # 2.99-3.16 at 2048; top-100 takes the rank-j plan, unaffected)
-SAMPLE_CANDS = int(os.environ.get("NCF_SCORE_SAMPLE_CANDS", "512"))
+SAMPLE_CANDS = 512
 # the split scan's item split raised from the expected candidates per user (the launch's
 # expected_per_user: fewer per-wave LDS slice overflows; tested invisible in the results)
 SIZED_SPLIT = True
@@ -153,7 +152,7 @@ SAMPLE16 = True
 # the fp16 sample keeps only the maximum of every SAMPLE_GROUP consecutive sample items (the k-th
 # largest group maximum bounds the k-th largest logit from below as well), where the sample
 # holds >= 8 j group maxima: 8x fewer bytes written and selected over; 1 = every logit
-SAMPLE_GROUP = int(os.environ.get("NCF_SCORE_SAMPLE_GROUP", "8"))
+SAMPLE_GROUP = 8
 
 
 def _select(idx, rows, n, run, k, out_s, out_i, overflow, st, terms=None, check=None):
@@ -177,8 +176,8 @@ def _select(idx, rows, n, run, k, out_s, out_i, overflow, st, terms=None, check=
 # k chosen are exact iff k were found and the k-th is at or above it) and flags the rest, which
 # are re-run from the sample's k-th (guaranteed).  The number of items at or above the j-th of a
 # sample of S ~ n_items / k is ~ Gamma(j) * k: below k with probability P(Gamma(16) < 1) ~ 1e-14
-# per user on exchangeable scores.  NCF_SCORE_RANK_J=0: the k-th always (A/B).
-RANK_J = int(os.environ.get("NCF_SCORE_RANK_J", "16"))
+# per user on exchangeable scores.  RANK_J = 0: the k-th always.
+RANK_J = 16
 SAMPLE_MIN = 4096   # items in the smallest threshold sample
 
 
