@@ -133,6 +133,13 @@ __device__ __forceinline__ bool ids_uniform(const int64_t* __restrict__ uid, int
 // (ncf_gather_ln_gmf_scaled_fwd) writes it only for a group's first row and for rows whose user
 // differs from that row's; the others read the group's first row (the same bits).  (r < rows;
 // the workgroup's rows start at a group boundary.)
+// The per-workgroup record of the shared-Q decision, kept next to the stash: a forward that
+// stashed Q once per group (at each group's first row) writes this word into the first column of
+// the workgroup's second row, a row it never writes otherwise; a forward that stashed every row
+// overwrites it with a projection (a NaN carrying this payload never comes out of one).  The stash
+// backward reads the decision there instead of re-deciding it from the ids it is handed.
+constexpr uint32_t kQGroupTag = 0x7FC0A51Bu;
+
 __device__ __forceinline__ int src_row(const int64_t* __restrict__ uid, int r, int M) {
   if (!uid || M <= 1) return r;
   const int f = r - r % M;
@@ -452,7 +459,7 @@ __device__ __forceinline__ void attn_pv(const float* __restrict__ Pg, const floa
   }
 }
 
-// per-workgroup partial of the four Linear gradients, in the flat parameter order// per-workgroup partial of the four Linear gradients, in the flat parameter order
+// per-workgroup partial of the four Linear gradients, in the flat parameter order
 // [q.weight | q.bias | k.weight | k.bias | v.weight | v.bias | out.weight | out.bias]
 // (AG<D>::kPartAttn floats)
 
@@ -558,13 +565,15 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_fwd(
   NCF_ASTAMP(0, 3);
   const float* src = S2;   // the out_proj input: O, or V when there is no core
   if (core) {
-    // (one user per group: Q is stashed once per group, at the group's first row; the
-    // backward reads it there, deciding shq on the same ids)
+    // (one user per group: Q is stashed once per group, at the group's first row, and the
+    // decision recorded beside it; the backward reads both there)
     if (Q) {
-      if (shq)
+      if (shq) {
         stage_out_groups<D>(Q + r0 * D, S0, ng, M);
-      else
+        if (threadIdx.x == 0) reinterpret_cast<uint32_t*>(Q)[(r0 + 1) * D] = kQGroupTag;
+      } else {
         stage_out<D>(Q + r0 * D, S0, rows);
+      }
     }
     if (K) stage_out<D>(K + r0 * D, S1, rows);
     if (V) stage_out<D>(V + r0 * D, S2, rows);
@@ -642,6 +651,7 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
   float pw_o[D / 4], pw_q[D / 4], pw_k[D / 4], pw_v[D / 4];
   constexpr int kPre = (16 * G::NTmax * L4 + kThreads - 1) / kThreads;   // float4 per thread
   float4 pu[kPre], pi[kPre];   // X_u / X_i rows for the fused weight gradients
+  bool shq_src = false;        // (stash form) one user per group: X_u from the group rows
   if constexpr (RC) {
     // one user per group (the forward's test on the same ids: the same Q bits): only the G
     // group rows of X_u are read, straight into S3 (the Q projection's input)
@@ -723,9 +733,12 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     }
     attn_core_fwd<D, HD>(S1, S2, S3, S4, Pl, nullptr, g0, ng, M, scale, p_drop, seed);
   } else {
-    // the forward stashed Q once per group where every group of the workgroup holds one user
-    // (the same test on the same ids); block 1 (Q) is then read from the group rows
-    const bool shq = share_q && M > 1 && uids && ids_uniform(uids + r0, ng, M);
+    // the forward stashed Q once per group where every group of the workgroup holds one user,
+    // and recorded that next to the stash (kQGroupTag); block 1 (Q) is then read from the group
+    // rows.  (share_q is unused here: the record, not the ids handed to the backward, decides.)
+    const bool shq = M > 1 && Qg &&
+                     __float_as_uint(Qg[(r0 + 1) * D]) == kQGroupTag;
+    shq_src = shq;
     if (wg && Og) {
       float* const dst[5] = {S0, S1, S2, S3, S4};
       const float* const src[5] = {dY + r0 * D, Qg + r0 * D, Kg + r0 * D, Vg + r0 * D,
@@ -762,8 +775,9 @@ __global__ __launch_bounds__(kThreads) void k_attn_block_bwd(
     for (int q = 0; q < kPre; ++q) {
       const int e = threadIdx.x + kThreads * q, r = e / L4, c = (e % L4) * 4;
       const bool in = e < Rp * L4 && r < rows;
-      pu[q] = in ? ld4(Xu + (r0 + src_row(uids ? uids + r0 : nullptr, r, M)) * D + c)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      // (a shared-Q workgroup holds one user per group: its group's first row)
+      const int sr = shq_src ? r - r % M : src_row(uids ? uids + r0 : nullptr, r, M);
+      pu[q] = in ? ld4(Xu + (r0 + sr) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
       pi[q] = in ? ld4(Xi + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
@@ -1000,11 +1014,10 @@ void allow_lds(Kern k, size_t bytes) {
 }
 
 // Q from one row per group when the groups hold one user each (ids_uniform; checked per
-// workgroup on the device from the caller's ids).  NCF_ATTN_SHARE_Q=0: every row projected (A/B)
-const int64_t* share_ids(const int64_t* user_ids) {
-  const char* e = getenv("NCF_ATTN_SHARE_Q");
-  return (e && e[0] == '0') ? nullptr : user_ids;
-}
+// workgroup on the device from the caller's ids): always on when user_ids are given (the engine's
+// per-row A/B passes NULL ids with every row gathered, engine.ATTN_SHARE_Q).  The stash backward
+// takes the forward's recorded decision (kQGroupTag), not its own.
+constexpr int kShareQ = 1;
 
 // head widths the kernels are built for: hd in {8, 16, 32, 64} at D = 64, {16, 32, 64} at
 // D = 128 (the core keeps a head row of hd floats per lane in registers)
@@ -1050,7 +1063,7 @@ extern "C" int ncf_attn_block_fwd(const float* xu, const float* xi, int64_t grou
   // the core runs unless the eval form applies (M == 1 without dropout: softmax == 1, o = v);
   // without q/k it stashes nothing (training with ncf_attn_block_bwd_rc)
   const int core = (q != nullptr || group_len > 1 || dropout_p > 0.0f) ? 1 : 0;
-  const int share_q = share_ids(user_ids) != nullptr;
+  const int share_q = kShareQ;
   const int64_t* uids = user_ids;   // (also the source rows of X_u: src_row)
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len;
@@ -1154,8 +1167,8 @@ extern "C" int ncf_attn_block_bwd(const float* grad_y, const float* q, const flo
   }
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len, H = (int)heads;
-  // (the forward stashed Q once per group where it shared it: the same decision here)
-  const int share_q = share_ids(user_ids) != nullptr;
+  // (the forward recorded where it stashed Q once per group: the kernel reads that record)
+  const int share_q = kShareQ;
   const size_t lds = bwd_lds_d((int)dim, M, H, wg);
   const int nb = (int)ncf_cdiv(groups, groups_per_wg(dim));
   const dim3 grid((unsigned)nb);
@@ -1218,7 +1231,7 @@ extern "C" int ncf_attn_block_bwd_rc(const float* grad_y, const float* xu, const
                 (long long)group_len, (long long)heads);
   if (groups == 0) return NCF_OK;
   const int M = (int)group_len, H = (int)heads;
-  const int share_q = share_ids(user_ids) != nullptr;
+  const int share_q = kShareQ;
   const int64_t* uids = user_ids;
   const size_t lds = bwd_lds_d((int)dim, M, H, true, true);
   const int nb = (int)ncf_cdiv(groups, groups_per_wg(dim));

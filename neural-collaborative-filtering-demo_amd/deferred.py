@@ -35,6 +35,10 @@ _KINDS = (("user", "mf_user", "mlp_user"), ("item", "mf_item", "mlp_item"))
 # ms against 0.381-0.399 forked at a backward fork point; round 3)
 CLAIM_CATCHUP = True
 _SERIAL = itertools.count(1)      # distinguishes schedules in workspace caches (ids recycle)
+# Steps of per-step scalars filled past the furthest step asked for.  The replay kernels read the
+# scalars of up to 8 steps past their target (replay_uniform's prefetch, csrc/adam.hip), so the
+# pad must stay >= 16; tests shrink it to force table growth under a captured graph.
+SCALAR_PAD = 4096
 
 
 class DeferredTableAdam:
@@ -103,17 +107,17 @@ class DeferredTableAdam:
             return
         if self._hp_filled is None:
             first = 1
-            last = max(upto, first) + 4096
+            last = max(upto, first) + SCALAR_PAD
         elif self._hp_filled != hp:
             # an lr (or beta) change affects only steps not yet taken: the scalars of steps
             # <= t stay as they were, so rows still behind replay those steps as taken.  The
             # filled horizon is refilled in place (no growth unless `upto` lies beyond it): a
             # captured step graph holds this buffer's address
             first = min(self._filled + 1, self.t + 1)
-            last = self._filled if upto <= self._filled else upto + 4096
+            last = self._filled if upto <= self._filled else upto + SCALAR_PAD
         else:
             first = self._filled + 1
-            last = max(upto, first) + 4096
+            last = max(upto, first) + SCALAR_PAD
         first = max(1, first)
         last = max(last, first)
         host = np.empty(4 * (last - first + 1), dtype=np.float32)
@@ -121,8 +125,21 @@ class DeferredTableAdam:
                   host.ctypes.data)
         need = 4 * (last + 1)
         if self._table.numel() < need:
+            dev = self._table.device
+            if self._table.numel():
+                # The table moves.  Kernels already queued read the old buffer by address: the
+                # overlapped sweep on its side stream (apply ensures before it joins the sweep)
+                # and a captured step graph still replaying.  Freeing it under them would let the
+                # caching allocator hand it to other work (or, with the graph, leave it read after
+                # the caller drops the graph), so the device is drained first — the table grows
+                # once per doubling, rarely enough that the wait is noise.
+                if torch.cuda.is_current_stream_capturing():
+                    raise RuntimeError("deferred Adam: the per-step scalar table would move "
+                                       "inside a graph capture (ensure the horizon before "
+                                       "capturing)")
+                torch.cuda.synchronize(dev)
             grown = torch.zeros(max(need, 2 * self._table.numel()), dtype=torch.float32,
-                                device=self._table.device)
+                                device=dev)
             if self._table.numel():
                 grown[:self._table.numel()].copy_(self._table)
             self._table = grown

@@ -155,13 +155,13 @@ class RcclExchange(ShardExchange):
         # ahead, the dense all-reduce).  Every rank issues the same host program, so each stream
         # — and each hardware queue two streams may share (4 per process) — receives
         # the collectives in the same order on every rank: no rank can hold one communicator's
-        # collective in a queue ahead of another's that its peer runs first.  One communicator
-        # for both roles (NCF_RCCL_COMMS=1) makes RCCL order each collective behind the
-        # communicator's previous one across the two streams, which ties the plan stream (the
-        # next batch's sort, the overlapped sweep) to the step's: world 1, 0.48 against 0.35
-        # ms/step (gpurun_out/r4m_sab.log).
+        # collective in a queue ahead of another's that its peer runs first.  (One communicator
+        # for both roles, measured in round 4, makes RCCL order each collective behind the
+        # communicator's previous one across the two streams, which ties the plan stream — the
+        # next batch's sort, the overlapped sweep — to the step's: world 1, 0.48 against 0.35
+        # ms/step)
         self.main = self._comm()
-        self.side = self.main if os.environ.get("NCF_RCCL_COMMS", "2") == "1" else self._comm()
+        self.side = self._comm()
         W = self.world
         # host split arrays, one pair per call site: the collective reads them when it is
         # called, so a launch tape replays each site with the sizes written there for the step

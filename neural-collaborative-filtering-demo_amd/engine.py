@@ -31,6 +31,11 @@ BF16_MM = True
 # at C2, 3 interleaved runs each: 0.3001-0.3012 against 0.3017-0.3031 ms/step, gather 11.5-11.8
 # against 12.2-12.3 us)
 GROUP_ROWS = True
+# Fact 6 in the fused attention block: with the rows' user ids it projects Q once per group in
+# every workgroup whose groups each hold one user (attn_block.hip ids_uniform; the stash backward
+# reads the forward's recorded decision).  False (tests' per-row A/B): no ids are handed to the
+# block and every row is gathered (no group rows), so every row's Q is projected.
+ATTN_SHARE_Q = True
 _WGRAD_ROWS = 160
 # the fused attention forward's O stash (off: the backward recomputes O from the stashed P and V,
 # attn_pv, the same bits, tested).  Measured at C2, 3 interleaved runs each: forward 22.3-23.1
@@ -429,8 +434,8 @@ class NCFEngine:
             raise ValueError("the temporal (hour) path is forward_simple's: eval, one item per group")
         # a2-a4: 4 gathers + mf_norm/mlp_norm + GMF  (architecture.py:286-287, 305-312)
         t_scale, t_factor = (temporal[0], temporal[1]) if temporal is not None else (None, 0.0)
-        G = M if (GROUP_ROWS and train and M > 1 and temporal is None and self.attn_block(D, H, M)
-                  and self.mlp_fused(D, hid)) else 0
+        G = M if (GROUP_ROWS and ATTN_SHARE_Q and train and M > 1 and temporal is None
+                  and self.attn_block(D, H, M) and self.mlp_fused(D, hid)) else 0
         w.group_rows = G
         if bf16:    # bf16 tables (``tables`` holds them): rows widened to fp32 in the gather
             if temporal is not None:
@@ -460,7 +465,8 @@ class NCFEngine:
                       drop_p if train else 0.0, seed, ptr(self.clock),
                       ptr(w.q) if core else None, ptr(w.k) if core else None,
                       ptr(w.v) if core else None, ptr(w.P) if core else None,
-                      ptr(w.o) if core and _STASH_O else None, ptr(w.y), ptr(uid), st)
+                      ptr(w.o) if core and _STASH_O else None, ptr(w.y),
+                      ptr(uid) if ATTN_SHARE_Q else None, st)
             # a7: MLP tower on [attn ‖ zeros_T] (architecture.py:329-344): the zero temporal
             # columns contribute nothing, so layer 0 reads only the first D columns of mlp.0.weight
             x, ldx, kin = w.y, D, D
@@ -772,14 +778,14 @@ class NCFEngine:
                 _lib.call("ncf_attn_block_bwd_rc", ptr(w.dy), ptr(w.xu), ptr(w.xi), n // M, M, H, D,
                           wq, bq, wk, bk, wv, bv, wo, drop_p, seed, ptr(self.clock), gp[1],
                           ptr(ws), ws.numel(), w.red_list.address, ptr(w.dxu), ptr(w.dxi),
-                          ptr(uid), st)
+                          ptr(uid) if ATTN_SHARE_Q else None, st)
             else:
                 _lib.call("ncf_attn_block_bwd", ptr(w.dy), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P),
                           n // M, M, H, D, *pp["att_w"], drop_p, seed,
                           ptr(self.clock), ptr(w.o) if _STASH_O else None, ptr(w.xu), ptr(w.xi),
                           gp[1], ptr(ws),
                           ws.numel(), w.red_list.address, None, None, None, ptr(w.dxu),
-                          ptr(w.dxi), ptr(uid), st)
+                          ptr(w.dxi), ptr(uid) if ATTN_SHARE_Q else None, st)
         else:
             self._attention_bwd_unfused(w, drop_p, seed, joins, st)
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)

@@ -34,6 +34,9 @@ log = logging.getLogger(__name__)
 # own on the step's queue, where each costs ~5 us (0.2986-0.2992 against 0.3020-0.3040 ms/step
 # at attn_bwd, r3ax_*).
 DEDUP_FORK = "sweep"
+# Steps of per-step Adam scalars a captured step graph is given before it must be re-captured
+# (the scalar table cannot grow from inside a replay); tests shrink it to force re-captures.
+GRAPH_HORIZON = 1 << 16
 
 
 class FusedTrainStep:
@@ -303,9 +306,9 @@ class FusedTrainStep:
             table_at = d._table.data_ptr()
             d._ensure(d._filled)
             if d._table.data_ptr() != table_at:
-                self._g = None
+                self._drop_graph()
         if self._g is not None and self._g_consts != d._consts():
-            self._g = None              # betas / eps / weight decay are launch arguments
+            self._drop_graph()          # betas / eps / weight decay are launch arguments
         horizon_ok = d._filled >= d.t + 2
         if self._g is None or self._shape != shape or not horizon_ok:
             if self._eager_steps < self.warmup or not horizon_ok:
@@ -315,7 +318,7 @@ class FusedTrainStep:
                 self.step_count += 1
                 m.engine.updates += 1
                 self.last_loss = w.loss
-                self._g = None
+                self._drop_graph()
                 return w
             self._capture(user_ids, item_ids, targets, M, shape, dev)
         su, si, stg = self._static
@@ -340,9 +343,19 @@ class FusedTrainStep:
         self.last_loss = w.loss
         return w
 
+    def _drop_graph(self):
+        """Release the captured step graph.  Replays are asynchronous: the last one may still be
+        executing, and destroying its executable under it frees the kernel-argument buffers its
+        queued dispatches read.  The stream is drained first (a re-capture is rare: a new batch
+        geometry, the scalar horizon, a betas / eps / weight-decay change, a state load)."""
+        if self._g is not None:
+            torch.cuda.current_stream(self.model.engine.flat.device).synchronize()
+            self._g = None
+
     def _capture(self, user_ids, item_ids, targets, M, shape, dev):
         d = self.deferred
-        d._ensure(d.t + (1 << 16))          # scalar table horizon: no host copies inside the graph
+        self._drop_graph()
+        d._ensure(d.t + GRAPH_HORIZON)      # scalar table horizon: no host copies inside the graph
         self._static = (user_ids.reshape(-1).to(device=dev, dtype=torch.int64).clone(),
                         item_ids.reshape(-1).to(device=dev, dtype=torch.int64).clone(),
                         targets.reshape(-1, 1).to(device=dev, dtype=torch.float32).clone())
@@ -398,7 +411,7 @@ class FusedTrainStep:
             d._ensure(d.t + 2)
         if self.clock is not None:
             self.clock[0] = self.step_count      # ncf_step_clock.t (reserved = 0)
-        self._g = None                           # re-capture from the restored state
+        self._drop_graph()                       # re-capture from the restored state
         eng.updates += 1
 
     def export_optimizer_state(self, opt: torch.optim.Adam):

@@ -502,7 +502,7 @@ def test_non_adam_optimizer_gets_dense_table_grads(f2):
 
 # ----------------------------------------------------------------------------- deferred Adam
 def _fused_run(deferred, steps, sweep_every=64, U=3000, I=500, B=64, seed=11, dropout=0.0,
-               lr_at=None, **kw):
+               lr_at=None, on_step=None, **kw):
     from ncf_amd.trainer import FusedTrainStep
     torch.manual_seed(seed)
     m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, dropout, 4).to(DEV)
@@ -517,6 +517,8 @@ def _fused_run(deferred, steps, sweep_every=64, U=3000, I=500, B=64, seed=11, dr
         if lr_at and s in lr_at:
             step.lr = lr_at[s]          # (a scheduler's change between steps)
         step(u, i, t.reshape(-1, 1).to(DEV))
+        if on_step is not None:
+            on_step(step, s)
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}   # syncs deferred rows
     step.sync()
     mom = {k: (v["exp_avg"].cpu().clone(), v["exp_avg_sq"].cpu().clone()) for k, v in step.state.items()}
@@ -604,14 +606,15 @@ def test_attn_block_recompute_bitwise_equals_stash(monkeypatch, D, H, M, B, drop
 def test_attn_shared_q_matches_per_row(monkeypatch, D, H, M, B, uniform, rc):
     """Q projected once per interaction group (fact 6: the M rows of a group hold one user;
     attn_block.hip groups_uniform / put_tile_expand) against every row projected
-    (NCF_ATTN_SHARE_Q=0): same probabilities, gradients and table gradients.  With one user per
-    group the workgroups take the shared path; with a random user per row (uniform=False) none
-    does.  Both backward forms (stash, recompute)."""
+    (engine.ATTN_SHARE_Q = False): same probabilities, gradients and table gradients.  With one
+    user per group the workgroups take the shared path; with a random user per row
+    (uniform=False) none does.  Both backward forms (stash, recompute)."""
+    import ncf_amd.engine as E
     from ncf_amd.trainer import FusedTrainStep
     monkeypatch.setenv("NCF_ATTN_RC", rc)
     out = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("NCF_ATTN_SHARE_Q", flag)
+    for flag in (False, True):
+        monkeypatch.setattr(E, "ATTN_SHARE_Q", flag)
         torch.manual_seed(41)
         m = ncf.AdvancedNCF(400, 300, 5, 24, D, D, 32, [256, 128, 64], H, 0.2, M - 1).to(DEV)
         step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
@@ -865,6 +868,48 @@ def test_attn_o_recompute_bitwise_equals_o_stash(monkeypatch):
         assert torch.equal(out[0][1][k][1], out[1][1][k][1]), k
 
 
+@pytest.mark.parametrize("mixed", [False, True])
+def test_attn_stash_backward_reads_the_forwards_q_record(mixed):
+    """the stash backward takes the shared-Q decision the forward recorded
+    beside its per-group Q stash (attn_block.hip kQGroupTag), not the ids it is handed, so a
+    backward called without user ids reads the same Q rows.  After a training forward with ids
+    (one user per group; with ``mixed`` one group of the first workgroup has two users, so that
+    workgroup stashes every row and the others share), the backward with the ids and with NULL
+    ids give bit-identical dQ / dK / dV / dX_u / dX_i."""
+    from ncf_amd import _lib
+    from ncf_amd._lib import ptr
+    from ncf_amd.trainer import FusedTrainStep
+    U, I, B, M, D, H = 3000, 500, 45, 5, 64, 4
+    g = torch.Generator().manual_seed(7)
+    u = torch.randint(0, U, (B,), generator=g).repeat_interleave(M)
+    if mixed:
+        u[3 * M + 2] = (u[3 * M] + 1) % U
+    i = torch.randint(0, I, (B * M,), generator=g)
+    t = torch.zeros(B, M)
+    t[:, 0] = 1
+    u, i, t = u.to(DEV), i.to(DEV), t.reshape(-1, 1).to(DEV)
+    torch.manual_seed(3)
+    m = ncf.AdvancedNCF(U, I, 5, 24, D, D, 32, [256, 128, 64], H, 0.0, M - 1).to(DEV)
+    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+    w = step(u, i, t)
+    torch.cuda.synchronize()
+    a = m.user_product_attention
+    n = B * M
+    outs = []
+    for ids in (u, None):
+        dq, dk, dv, dxu, dxi = (torch.full((n, D), 7.0, device=DEV) for _ in range(5))
+        _lib.call("ncf_attn_block_bwd", ptr(w.dy), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P), B, M,
+                  H, D, ptr(a.q_proj.weight), ptr(a.k_proj.weight), ptr(a.v_proj.weight),
+                  ptr(a.out_proj.weight), 0.0, 0, ptr(m.engine.clock), None, ptr(w.xu),
+                  ptr(w.xi), None, None, 0, None, ptr(dq), ptr(dk), ptr(dv), ptr(dxu), ptr(dxi),
+                  ptr(ids) if ids is not None else None, _lib.stream_ptr(DEV))
+        torch.cuda.synchronize()
+        outs.append([x.cpu() for x in (dq, dk, dv, dxi, dxu)])
+    for name, x, y in zip(("dq", "dk", "dv", "dxi", "dxu"), outs[0], outs[1]):
+        assert torch.equal(x, y), name
+        assert not (x == 7.0).all(dim=1).any(), name       # every row written
+
+
 @pytest.mark.parametrize("D,G", [(32, 0), (64, 0), (64, 5), (128, 3), (256, 0)])
 def test_gather_two_float4_lanes_bitwise_equals_one_float4(D, G):
     """k_gather_ln_gmf with D/8 lanes per row (two float4 each, the plain entry point's kernel)
@@ -923,6 +968,38 @@ def test_graph_replay_lr_change_bitwise_equals_eager_clock():
     b_sd, b_m = _fused_run(True, 70, dropout=0.2, graph=True, lr_at=lr_at)
     c_sd, _ = _fused_run(True, 70, dropout=0.2, clock=True)
     assert any(not torch.equal(a_sd[k], c_sd[k]) for k in a_sd)      # the changes took effect
+    for k in a_sd:
+        assert torch.equal(a_sd[k], b_sd[k]), k
+    for k in a_m:
+        assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
+
+
+def test_graph_recapture_table_move_lr_change_bitwise_equals_eager_clock(monkeypatch):
+    """The geometry of round 4's r4i fault (an illegal address in the replay after an lr change
+    under graph=True): a capture horizon of 8 steps and a scalar pad of 16
+    make the step graph expire, get dropped and re-captured every few steps while the per-step
+    scalar table grows (moves) under it, with lr changes before, between and right at those
+    points.  Dropping a graph drains the stream first, a growing table drains the device; bit
+    for bit the eager clock path taking the same changes."""
+    import ncf_amd.deferred as de
+    import ncf_amd.trainer as tr
+    monkeypatch.setattr(tr, "GRAPH_HORIZON", 8)
+    monkeypatch.setattr(de, "SCALAR_PAD", 16)
+    lr_at = {5: 5e-4, 11: 2.5e-4, 12: 3e-4, 23: 4e-4, 24: 6e-4, 37: 2e-4}
+    seen = {"tables": set(), "captures": 0}
+    capture = tr.FusedTrainStep._capture
+
+    def counted(self, *a, **k):
+        seen["captures"] += 1
+        return capture(self, *a, **k)
+    monkeypatch.setattr(tr.FusedTrainStep, "_capture", counted)
+
+    def probe(step, s):
+        seen["tables"].add(step.deferred._table.data_ptr())
+    a_sd, a_m = _fused_run(True, 48, dropout=0.2, clock=True, lr_at=lr_at)
+    b_sd, b_m = _fused_run(True, 48, dropout=0.2, graph=True, lr_at=lr_at, on_step=probe)
+    assert len(seen["tables"]) >= 3, seen      # the table moved under the graph path
+    assert seen["captures"] >= 3, seen         # ... which re-captured several times
     for k in a_sd:
         assert torch.equal(a_sd[k], b_sd[k]), k
     for k in a_m:
