@@ -49,7 +49,13 @@ BF16_MFMA_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity
 # C-ABI entry point -> the kernel symbol rocprofv3 reports for it
 KERNEL_SYMBOL = {"ncf_attn_block_fwd": "k_attn_block_fwd", "ncf_attn_block_bwd": "k_attn_block_bwd",
                  "ncf_mlp_fwd": "k_mlp_fwd", "ncf_mlp_bwd": "k_mlp_bwd",
+                 "ncf_mlp_fwd_split": "k_mlp_fwd", "ncf_mlp_bwd_split": "k_mlp_bwd",
                  "ncf_wgrad_grouped": "k_wgrad_grouped"}
+# the tower's Linears on bf16 matrix cores through split operands: 6 bf16 products per fp32
+# product (engine.TOWER_SPLIT); their roofline is quoted as fp32-equivalent work against the fp32
+# MFMA peak, with the executed bf16 products against the bf16 peak beside it
+SPLIT_PRODUCTS = 6
+SPLIT_NAMES = ("ncf_mlp_fwd_split", "ncf_mlp_bwd_split")
 
 
 def pmc_traffic(kernel):
@@ -241,8 +247,8 @@ def cpu_baseline(model_sd, cfg, batches_cpu, budget_s):
     med = sorted(times)[len(times) // 2]
     return {"value": (B * M) / med, "unit": "samples/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model,
-            "sample": f"{k} timed C2 train steps (B={B} groups x M={M}, full 1M x 100K tables, "
-                      f"fp32, dense Adam) after 1 warm-up; median step {med * 1e3:.1f} ms; "
+            "sample": f"{k} timed train steps (B={B} groups x M={M}, full {U} x {I} tables, "
+                      f"D={D}, fp32, dense Adam) after 1 warm-up; median step {med * 1e3:.1f} ms; "
                       f"{threads} threads on {cpu_model}"}
 
 
@@ -267,6 +273,189 @@ def cpu_infer_baseline(model_sd, iu, ii, H, T, n_layers, budget_s):
             "kind": "port", "cpu_model": cpu_model,
             "sample": f"oracle eval forward over the same {iu.numel()} pairs (full 1M x 100K "
                       f"tables, fp32), median of {len(times)} calls: {med * 1e3:.1f} ms"}
+
+
+def embedding_rooflines(totals, per, steps, N, D, grows, nu_ni):
+    """HBM rooflines of the embedding gather and scatter from per-launch event times (SURVEY
+    8(d) algorithmic bytes per launch):
+      gather  (ncf_gather_ln_gmf_scaled_fwd), group_rows = M (fact 6: a group's user rows read
+              and its LN'd user rows written once): per row the item GMF + MLP rows in and out,
+              two int64 ids and mf_pred = N (16 D + 20), per group the user's two rows in and out
+              = (N / M) 16 D; every row written (group_rows 0): N (16 D + 16 + 16 D + 4);
+      scatter (ncf_embedding_bwd_reduce): 4 gradient rows in per sample + 2 ids, per unique row
+              the 2 table rows (LN recompute) in and 2 compact gradient rows out
+              = N (16 D + 16) + (n_u + n_i) 16 D."""
+    g_bytes = (N * (16 * D + 20) + (N // grows) * 16 * D if grows > 1
+               else N * (16 * D + 16 + 16 * D + 4))
+    hbm = {}
+    for name, kern, nbytes in (
+            ("gather", "ncf_gather_ln_gmf_scaled_fwd", g_bytes),
+            ("scatter", "ncf_embedding_bwd_reduce",
+             N * (16 * D + 16) + (sum(nu_ni) * 16 * D if nu_ni else 0))):
+        if kern in totals:
+            launches = len(per.get(kern, [])) / steps
+            ms = totals[kern] / max(launches, 1)
+            gbs = nbytes / (ms * 1e-3) / 1e9
+            pm = pmc_traffic({"ncf_gather_ln_gmf_scaled_fwd": "k_gather_ln_gmf",
+                              "ncf_embedding_bwd_reduce": "k_piece_reduce_ln"}[kern])
+            hbm[name] = {"entry_point": kern, "bytes_per_launch": nbytes, "ms_per_launch": round(ms, 4),
+                         "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS,
+                         "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "traffic": pm["bytes_per_launch"] if pm else None}
+    if "gather" in hbm:
+        hbm["gather"]["group_rows"] = grows
+        hbm["gather"]["round3_count_bytes"] = N * (16 * D + 16 + 16 * D + 4)
+    if "scatter" in hbm:
+        hbm["scatter"]["unique_rows"] = nu_ni
+        hbm["scatter"]["note"] = ("segment reduce + LN backward (+ the multi-piece fix-up); the id "
+                                  "sort before it (ncf_dedup_ids) is listed in kernel_ms_per_step")
+    return hbm
+
+
+def profiled_steps(step, batches, first, count, pipelined=True):
+    """count FusedTrainStep steps with HIP events around every C-ABI call: (per entry point
+    [(args, ms)], ms per step per entry point)."""
+    from ncf_amd import _lib as L
+    L.PROFILE = []
+    torch.cuda.synchronize()
+    for s in range(first, first + count):
+        u, i, t = batches[s % len(batches)]
+        if pipelined:
+            step(u, i, t, next=batches[(s + 1) % len(batches)][:2])
+        else:
+            step(u, i, t)
+    torch.cuda.synchronize()
+    prof, L.PROFILE = L.PROFILE, None
+    per = {}
+    for name, a, e0, e1 in prof:
+        per.setdefault(name, []).append((a, e0.elapsed_time(e1)))
+    return per, {k: sum(d for _, d in v) / count for k, v in per.items()}
+
+
+def embedding_large(ncf, dev, cfg, groups, warmup, steps):
+    """the embedding gather / scatter rooflines where their launch latency is
+    amortised — SURVEY 8(d)'s strong-scaling global batch (32,768 groups x M = 163,840 rows) on
+    ONE GPU, the same C2 tables and step (FusedTrainStep), per-launch HIP events."""
+    from ncf_amd.trainer import FusedTrainStep
+    U, I, D, T, H, hid, _, M = cfg
+    N = groups * M
+    torch.manual_seed(555)
+    m = ncf.AdvancedNCF(U, I, 10, 50, D, D, T, hid, H, 0.2, M - 1).to(dev).train()
+    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+    batches = make_batches(U, I, groups, M, 8, dev, seed=321)
+    for s in range(warmup):
+        u, i, t = batches[s % len(batches)]
+        step(u, i, t, next=batches[(s + 1) % len(batches)][:2])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(warmup, warmup + steps):
+        u, i, t = batches[s % len(batches)]
+        step(u, i, t, next=batches[(s + 1) % len(batches)][:2])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    per, totals = profiled_steps(step, batches, warmup + steps, steps)
+    w = next(iter(m.engine.ws.values()))
+    nu_ni = [int(x) for x in w.num_unique.cpu().tolist()]
+    hbm = embedding_rooflines(totals, per, steps, N, D, int(getattr(w, "group_rows", 0)), nu_ni)
+    out = {"config": f"C2 tables (1M x 100K, D=64), {groups} groups x M={M} = {N} rows per step "
+                     "on one GPU (SURVEY 8(d) strong-scaling global batch)",
+           "rows_per_step": N, "ms_per_step": round(dt / steps * 1e3, 4),
+           "value": round(N * steps / dt, 1), "unit": "samples/s", **hbm,
+           "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(totals.items(), key=lambda x: -x[1])}}
+    del step, m, batches
+    torch.cuda.empty_cache()
+    return out
+
+
+def small_batch_train(ncf, dev, cfg, warmup, steps, prime, init_sd=None, cpu_budget=0.0):
+    """C2 at the reference's default batch (batch_size 256,
+    /root/reference/config/config.yaml:65; N = 1,280 rows): the same FusedTrainStep.  Here the
+    dense-exact Adam's full-table replay (140.8M element-steps per step whatever the batch) sets
+    the pace, not the batch.  With ``init_sd``: the CPU oracle on the same configuration (BASELINE.md
+    section 2 quotes 4,037 samples/s on 8 cores for the reference itself)."""
+    from ncf_amd.trainer import FusedTrainStep
+    U, I, D, T, H, hid, B, M = cfg
+    torch.manual_seed(1234)
+    m = ncf.AdvancedNCF(U, I, 10, 50, D, D, T, hid, H, 0.2, M - 1).to(dev).train()
+    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+    batches = make_batches(U, I, B, M, N_BATCHES, dev, seed=256)
+
+    def run(first, count):
+        for s in range(first, first + count):
+            u, i, t = batches[s % len(batches)]
+            step(u, i, t, next=batches[(s + 1) % len(batches)][:2])
+    run(0, prime + warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(prime + warmup, steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    per, totals = profiled_steps(step, batches, prime + warmup + steps, min(steps, 50))
+    out = {"config": f"C2 at the reference's default batch: B={B} groups x M={M} = {B * M} rows "
+                     "(config.yaml:65), 1M x 100K, D=64, FusedTrainStep",
+           "value": round(B * M * steps / dt, 1), "unit": "samples/s",
+           "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warmup,
+           "prime_steps": prime,
+           "adam_steady_state": steady_state(prime, warmup, step.deferred.sweep_every),
+           "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(totals.items(), key=lambda x: -x[1])},
+           "reference_cpu_published": {"value": 4037, "unit": "samples/s",
+                                       "source": "BASELINE.md section 2 (8-core Xeon, measured by "
+                                                 "the survey on the reference itself)"}}
+    del step, m
+    torch.cuda.empty_cache()
+    if init_sd is not None:
+        cpu_b = [(u.cpu(), i.cpu(), t.cpu()) for (u, i, t) in batches[:4]]
+        out["cpu_baseline"] = cpu_baseline(init_sd, cfg, cpu_b, cpu_budget)
+        out["vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+    del batches
+    return out
+
+
+C1 = dict(U=943, I=1682, D=16, T=32, H=1, hid=[64, 32], B=256, M=5)
+
+
+def c1_line(ncf, dev, warmup, steps, prime, cpu_budget, with_cpu):
+    """BASELINE.json configs[0] / SURVEY 8(d) C1 (MovieLens-100K-shaped: 943 users x 1682 items,
+    D=16, H=1, MLP [64, 32], B=256 x M=5): the reference's CPU configuration.  The CPU oracle
+    timed on the host's cores (the baseline SURVEY 8(d) asks for), and the same step on the GPU
+    (FusedTrainStep; D = 16 runs the unfused attention / tower kernels)."""
+    from ncf_amd.trainer import FusedTrainStep
+    c = C1
+    U, I, D, T, H, hid, B, M = c["U"], c["I"], c["D"], c["T"], c["H"], c["hid"], c["B"], c["M"]
+    cfg = (U, I, D, T, H, hid, B, M)
+    torch.manual_seed(11)
+    m = ncf.AdvancedNCF(U, I, 10, 50, D, D, T, hid, H, 0.2, M - 1)
+    init = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev).train()
+    batches = make_batches(U, I, B, M, 64, dev, seed=943)
+    out = {"config": "C1: 943 users x 1682 items, D=16, H=1, MLP [64,32], T=32, B=256 x M=5, "
+                     "dropout 0.2, Adam lr 1e-3 wd 1e-5 (dense-exact)"}
+    try:
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+
+        def run(first, count):
+            for s in range(first, first + count):
+                u, i, t = batches[s % len(batches)]
+                step(u, i, t, next=batches[(s + 1) % len(batches)][:2])
+        run(0, prime + warmup)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(prime + warmup, steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        out.update({"value": round(B * M * steps / dt, 1), "unit": "samples/s",
+                    "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps})
+        del step
+    except Exception as e:     # recorded, not fatal to the headline
+        out["gpu_error"] = f"{type(e).__name__}: {e}"[:300]
+    if with_cpu:
+        cpu_b = [(u.cpu(), i.cpu(), t.cpu()) for (u, i, t) in batches[:4]]
+        out["cpu_baseline"] = cpu_baseline(init, cfg, cpu_b, cpu_budget)
+        if "value" in out:
+            out["vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+    del m, batches
+    torch.cuda.empty_cache()
+    return out
 
 
 def dropin_train(ncf, dev, cfg, batches, warmup, steps, prime=0):
@@ -474,6 +663,7 @@ def c4_train(ncf, dev, warmup, steps, prime=0):
     else:
         acct = None
     lin = ("ncf_attn_block_fwd", "ncf_attn_block_bwd", "ncf_mlp_fwd", "ncf_mlp_bwd",
+           "ncf_mlp_fwd_split", "ncf_mlp_bwd_split",
            "ncf_gemm_rows", "ncf_gemm_f32", "ncf_wgrad_grouped", "ncf_relu_ln_dropout_fwd",
            "ncf_relu_ln_dropout_bwd", "ncf_attention_fwd", "ncf_attention_bwd")
     mem = torch.cuda.max_memory_allocated(dev)
@@ -491,7 +681,8 @@ def c4_train(ncf, dev, warmup, steps, prime=0):
                k: round(v, 4) for k, v in sorted(iso.items(), key=lambda x: -x[1])},
            "linear_ms_per_step": round(sum(v for k, v in iso.items() if k in lin), 4),
            "linear_kernels": "fused attention block + fused MLP tower (D = 128)"
-           if "ncf_attn_block_fwd" in iso and "ncf_mlp_fwd" in iso else "unfused",
+           if "ncf_attn_block_fwd" in iso and ("ncf_mlp_fwd" in iso or "ncf_mlp_fwd_split" in iso)
+           else "unfused",
            "table_adam_roofline": table_adam_roofline(acct, D) if acct else None}
     del step, model, batches
     torch.cuda.empty_cache()
@@ -524,6 +715,32 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
     idx = ItemIndex(m, items=shard)
     torch.cuda.synchronize()
     index_ms = (time.perf_counter() - t0) * 1e3
+    # the rebuild's launches with HIP events: its roofline.  Per item it runs
+    # the eval forward with M = 1 (attention: v and out projections, 2 x 2 D^2 flop; tower + head
+    # 2 (D h1 + h1 h2 + h2 h3)), the GMF row's LayerNorm, the bias and the bf16 split planes
+    L.PROFILE = []
+    idx = ItemIndex(m, items=shard)
+    torch.cuda.synchronize()
+    iprof, L.PROFILE = L.PROFILE, None
+    ims = {}
+    for name, _, e0, e1 in iprof:
+        ims[name] = ims.get(name, 0.0) + e0.elapsed_time(e1)
+    D_ = 64
+    mlp_f_ = 2.0 * (D_ * 256 + 256 * 128 + 128 * 64)
+    idx_flops = n_local * (4.0 * D_ * D_ + mlp_f_)
+    idx_tf = idx_flops / (index_ms * 1e-3) / 1e12
+    mf_ms = ims.get("ncf_mlp_fwd", 0.0) + ims.get("ncf_mlp_fwd_split", 0.0)
+    mf_tf = n_local * mlp_f_ / (mf_ms * 1e-3) / 1e12 if mf_ms else 0.0
+    item_index = {"ms": round(index_ms, 3), "first_build_ms": round(index_cold_ms, 3),
+                  "kernel_ms": {k: round(v, 4) for k, v in sorted(ims.items(), key=lambda x: -x[1])},
+                  "flops": idx_flops,
+                  "roofline": {"bound": "mfma", "kernel": "k_mlp_fwd (item tower, M = 1)",
+                               "achieved": round(mf_tf, 2), "peak": FP32_MFMA_PEAK_TFS,
+                               "unit": "TFLOP/s", "frac": round(mf_tf / FP32_MFMA_PEAK_TFS, 4),
+                               "ms": round(mf_ms, 4)},
+                  "whole_build": {"achieved": round(idx_tf, 2), "peak": FP32_MFMA_PEAK_TFS,
+                                  "unit": "TFLOP/s", "frac": round(idx_tf / FP32_MFMA_PEAK_TFS, 4),
+                                  "note": "all item-side flops / the rebuild's wall time"}}
 
     def timed(fn):
         if world > 1:
@@ -547,7 +764,7 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
                      + ", hipGraph-captured"
                      + (f", item-sharded over {world} GPUs (all-gather + merge)" if world > 1 else ""),
            "scaling": "strong", "n_gpus": world, "item_index_ms": round(index_ms, 3),
-           "item_index_first_build_ms": round(index_cold_ms, 3)}
+           "item_index_first_build_ms": round(index_cold_ms, 3), "item_index": item_index}
     for k in ks:
         # the served form: the per-shard pipeline captured once as a hipGraph and replayed
         # (GraphedScorer); the eager launches are timed beside it with per-launch HIP events
@@ -592,19 +809,41 @@ def c5_scoring(dev, n_users, n_items, n_query, ks, cpu_budget, world=1, rank=0):
                                      "algorithmic_frac_of_fp32_peak":
                                          round(algo_tf / FP32_MFMA_PEAK_TFS, 4)}}
     if cpu_budget > 0 and rank == 0 and world == 1:
+        # the reference serving path (app.py:43-77: forward_simple over the items,
+        # then nlargest) on the CPU oracle for a 100-user slice, extrapolated linearly to the
+        # whole 10K x 1M job and labelled so.  Each user scores a 100K-item slice of the
+        # catalogue (the literal per-pair forward is ~1 us per pair on the host); stops early
+        # when the time budget runs out and extrapolates from the users done.
         from oracle import ncf_oracle as O
+        threads, cpu_model = host_cpu()
+        torch.set_num_threads(threads)
         p = {k: v.detach().cpu() for k, v in m.state_dict().items()}
         n_cpu = min(n_items, 100_000)
         items = torch.arange(n_cpu)
-        u = torch.full((n_cpu,), int(users[0]), dtype=torch.int64)
+        ucpu = users[:100].cpu()
+        with torch.no_grad():     # warm-up
+            O.forward_simple(p, torch.full((n_cpu,), int(ucpu[0]), dtype=torch.int64), items,
+                             num_heads=4, temporal_dim=32, n_layers=3)
+        done = 0
         t0 = time.perf_counter()
         with torch.no_grad():
-            O.forward_simple(p, u, items, num_heads=4, temporal_dim=32, n_layers=3)
+            for uu in ucpu.tolist():
+                sc = O.forward_simple(p, torch.full((n_cpu,), uu, dtype=torch.int64), items,
+                                      num_heads=4, temporal_dim=32, n_layers=3)
+                torch.topk(sc.reshape(-1), max(ks))
+                done += 1
+                if time.perf_counter() - t0 > cpu_budget:
+                    break
         dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": round(n_cpu / dt, 1), "unit": "pairs/s",
-                               "cores": torch.get_num_threads(), "kind": "port",
-                               "sample": f"oracle forward_simple (the reference serving path, "
-                                         f"literal per-pair forward) for 1 user x {n_cpu} items"}
+        rate = done * n_cpu / dt
+        out["cpu_baseline"] = {"value": round(rate, 1), "unit": "pairs/s", "cores": threads,
+                               "kind": "port", "cpu_model": cpu_model,
+                               "sample": f"oracle forward_simple + topk({max(ks)}) (the reference "
+                                         f"serving path, literal per-pair forward) for {done} "
+                                         f"users x {n_cpu} items, {threads} threads",
+                               "extrapolated_full_job_s": round(n_query * n_items / rate, 1),
+                               "extrapolated_note": f"linear extrapolation to {n_query} users x "
+                                                    f"{n_items} items (labelled: not run)"}
     del m, idx
     torch.cuda.empty_cache()
     return out
@@ -715,6 +954,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=("c2", "c4"),
                     help="c4: only the C4 (50M x 5M, D=128) training line on one GPU")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 line of the default run")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the B=256, C1 and large-batch embedding lines")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU, started here before anything touches the GPU
@@ -830,7 +1071,10 @@ def main():
     from ncf_amd import _lib as L
     L.PROFILE = []
     torch.cuda.synchronize()
-    run = step.eager if hasattr(step, "eager") else step   # the launches a graph replay runs
+    # the headline's own launch sequence (the pipelined step: the next batch sorted ahead, the
+    # sorted catch-up); with --graph the eager launches a replay runs (a graph cannot be
+    # instrumented per launch)
+    run = step.eager if (args.graph and hasattr(step, "eager")) else step
     run_steps(run, prime + args.warmup + args.steps, args.steps)
     torch.cuda.synchronize()
     prof, L.PROFILE = L.PROFILE, None
@@ -852,8 +1096,9 @@ def main():
     mlp_f = 2.0 * (D * hid[0] + hid[0] * hid[1] + hid[1] * hid[2])
     # (with the weight gradients fused into the tower backward, ncf_mlp_bwd carries dX + dW)
     per_sample = {"ncf_attn_block_fwd": 8.0 * D * D, "ncf_attn_block_bwd": 16.0 * D * D,
-                  "ncf_mlp_fwd": mlp_f,
+                  "ncf_mlp_fwd": mlp_f, "ncf_mlp_fwd_split": mlp_f,
                   "ncf_mlp_bwd": mlp_f if "ncf_wgrad_grouped" in totals else 2.0 * mlp_f,
+                  "ncf_mlp_bwd_split": 2.0 * mlp_f,
                   "ncf_wgrad_grouped": mlp_f}
     gemm_names = ("ncf_gemm_direct", "ncf_gemm_f32", "ncf_gemm_rows", "ncf_gemm_f32_splitk")
     mfma = {}
@@ -917,7 +1162,6 @@ def main():
                                                 "ncf_adam_pairs_catchup_claim_clock",
                                                 "ncf_adam_pairs_apply_clock",
                                                 "ncf_adam_pairs_sweep_rolling"))
-    tab_bytes = 2 * (U + I) * D * 24.0
     sweep_ms = sum(totals.get(k, 0.0) for k in ("ncf_adam_pairs_sweep_rolling",
                                                 "ncf_adam_sweep_rolling", "ncf_adam_sweep"))
     dfr = step.deferred if hasattr(step, "deferred") else getattr(
@@ -941,33 +1185,7 @@ def main():
         grows = int(getattr(ws_any, "group_rows", 0))
     except Exception:
         pass
-    # gather with group_rows = M (fact 6: a group's user rows read and LN'd rows written once):
-    # per row the item MF + MLP rows in and out, ids, mf_pred; per group the user's two rows in
-    # and out.  Every row written (group_rows 0): the four rows in and out per row.
-    g_bytes = (N * (16 * D + 20) + (N // grows) * 16 * D if grows > 1
-               else N * (16 * D + 16 + 16 * D + 4))
-    hbm = {}
-    for name, kern, nbytes in (
-            ("gather", "ncf_gather_ln_gmf_scaled_fwd", g_bytes),
-            ("scatter", "ncf_embedding_bwd_reduce",
-             N * (16 * D + 16) + (sum(nu_ni) * 16 * D if nu_ni else 0))):
-        if kern in totals:
-            launches = len(per.get(kern, [])) / args.steps
-            ms = totals[kern] / max(launches, 1)
-            gbs = nbytes / (ms * 1e-3) / 1e9
-            pm = pmc_traffic({"ncf_gather_ln_gmf_scaled_fwd": "k_gather_ln_gmf",
-                              "ncf_embedding_bwd_reduce": "k_piece_reduce_ln"}[kern])
-            hbm[name] = {"entry_point": kern, "bytes_per_launch": nbytes, "ms_per_launch": round(ms, 4),
-                         "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS,
-                         "frac": round(gbs / HBM_PEAK_GBS, 4),
-                         "traffic": pm["bytes_per_launch"] if pm else None}
-    if "gather" in hbm:
-        hbm["gather"]["group_rows"] = grows
-        hbm["gather"]["round3_count_bytes"] = N * (16 * D + 16 + 16 * D + 4)
-    if "scatter" in hbm:
-        hbm["scatter"]["unique_rows"] = nu_ni
-        hbm["scatter"]["note"] = ("segment reduce + LN backward only; the id sort before it "
-                                  "(ncf_dedup_ids) is listed in kernel_ms_per_step")
+    hbm = embedding_rooflines(totals, per, args.steps, N, D, grows, nu_ni)
     # --- inference pairs/s: eval forward (M = 1) on resident pairs
     model.eval()
     npairs = args.infer_pairs
@@ -1002,7 +1220,8 @@ def main():
     # attention block 2 x 2 D^2 flop; the tower + head 2 (D h1 + h1 h2 + h2 h3) flop
     inf_work = {"ncf_gather_ln_gmf_scaled_fwd": ("hbm", npairs * (16 * D + 16 + 8 * D + 4)),
                 "ncf_attn_block_fwd": ("mfma", npairs * 4.0 * D * D),
-                "ncf_mlp_fwd": ("mfma", npairs * mlp_f)}
+                "ncf_mlp_fwd": ("mfma", npairs * mlp_f),
+                "ncf_mlp_fwd_split": ("mfma", npairs * mlp_f)}
     inf_k = {}
     for name, (bound, work) in inf_work.items():
         if name in inf_ms:
@@ -1040,6 +1259,16 @@ def main():
         bf16 = bf16_train(ncf, dev, (U, I, D, T, H, hid, B, M), batches, args.warmup, args.steps,
                           prime)
         bf16["vs_fp32_step"] = round(bf16["value"] / samples_s, 4)
+
+    b256 = c1 = emb_large = None
+    if not sharded and not args.no_extra:
+        # the reference's default batch (config.yaml:65), C1 (configs[0]) and the embedding
+        # kernels at the strong-scaling global batch on one GPU
+        b256 = small_batch_train(ncf, dev, (U, I, D, T, H, hid, 256, M), args.warmup, args.steps,
+                                 prime, init_sd, args.cpu_budget)
+        emb_large = embedding_large(ncf, dev, (U, I, D, T, H, hid, B, M), 32768, 10, 20)
+        c1 = c1_line(ncf, dev, args.warmup, args.steps, prime, args.cpu_budget,
+                     init_sd is not None)
 
     c4 = None
     if not sharded and not args.no_c4:
@@ -1097,11 +1326,21 @@ def main():
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
                          "flops_per_launch": dom_flops, "ms_per_launch": round(dom_ms, 4),
+                         **({"matrix_cores": "bf16 (v_mfma_f32_16x16x32_bf16) on split operands: "
+                                             f"{SPLIT_PRODUCTS} bf16 products per fp32 product, "
+                                             "fp32-accurate; achieved/frac are fp32-equivalent "
+                                             "work against the fp32 MFMA peak",
+                             "executed_bf16_tflops": round(SPLIT_PRODUCTS * dom_tf, 2),
+                             "executed_frac_of_bf16_peak":
+                                 round(SPLIT_PRODUCTS * dom_tf / BF16_MFMA_PEAK_TFS, 4)}
+                            if dom in SPLIT_NAMES else {}),
                          **({"overlap": "measured in the step, beside the rolling table sweep "
                                         "on a side stream", "isolated": iso} if iso else {})},
             "mfma_class": {"kernels": "k_attn_block_fwd/bwd + k_mlp_fwd/bwd + k_wgrad_grouped "
-                                      "(fp32 MFMA v_mfma_f32_16x16x4_f32 / 32x32x2_f32: every "
-                                      "Linear of the step)",
+                                      "(every Linear of the step: fp32 MFMA "
+                                      "v_mfma_f32_16x16x4_f32, the tower on split-operand bf16 "
+                                      "MFMA when the *_split entry points run; fp32-equivalent "
+                                      "work against the fp32 MFMA peak)",
                            "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFS,
                            "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFS, 4),
                            "flops_per_step": gemm_flops, "launches_per_step": gemm_launches,
@@ -1118,9 +1357,9 @@ def main():
                                          "side stream, beside the backward kernels",
                            "sweep_every": sweep_every,
                            "steps_before_timing": prime + args.warmup,
-                           "dense_equivalent_GBps": round(tab_bytes / max(tab_ms * 1e-3, 1e-12) / 1e9, 1),
-                           "note": "dense schedule bytes (24 B x 140.8M elements) / time: above "
-                                   "HBM peak because untouched rows are caught up lazily",
+                           "element_steps_per_step": 2 * (U + I) * D,
+                           "note": "every table element takes one Adam step per step (dense-exact); "
+                                   "the roofline is the replay's VALU issue rate",
                            "roofline": adam_rf},
             "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(totals.items(), key=lambda x: -x[1])},
             "cpu_baseline": cpu,
@@ -1132,6 +1371,9 @@ def main():
             "resident_batches": args.batches,
             "c5_scoring": score,
             "c2_bf16_tables": bf16,
+            "c2_b256": b256,
+            "c1_train": c1,
+            "embedding_hbm_large": emb_large,
             "c4_train": c4,
             "final_loss": round(loss, 6),
         }

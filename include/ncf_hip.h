@@ -344,6 +344,21 @@ int ncf_mlp_bwd_bf16(const float* grad_a_last, int64_t n, int64_t dim, const flo
                      const ncf_head_args* head, float* grad_x, float* workspace,
                      int64_t workspace_floats, ncf_reduce_list* defer, void* stream);
 
+/* fp32 tower on bf16 matrix cores through split operands: every fp32 operand x = h + m + l
+ * (three bf16 terms, round to nearest), a product accumulated from the six bf16 products of
+ * order >= 2^-16 (v_mfma_f32_16x16x32_bf16, fp32 accumulate; the dropped terms are below 2^-24
+ * of it, fp32's own rounding level); row ops fp32.  Same arguments as ncf_mlp_fwd / _bwd.     */
+int ncf_mlp_fwd_split(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
+                      int64_t n_layers, const int64_t* hidden, float eps, float dropout_p,
+                      uint64_t seed, const ncf_step_clock* clock, const float* mlp_out_w,
+                      const float* mlp_out_b, const float* mf_pred, const float* final_w,
+                      const float* final_b, float* mlp_pred, float* prob, void* stream);
+int ncf_mlp_bwd_split(const float* grad_a_last, int64_t n, int64_t dim, const float* x,
+                      const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
+                      float dropout_p, uint64_t seed, const ncf_step_clock* clock,
+                      const ncf_head_args* head, float* grad_x, float* workspace,
+                      int64_t workspace_floats, ncf_reduce_list* defer, void* stream);
+
 /* ---- 8f rank 1: device-side training batches (data_prep.py:95-161, 181-313) --------------
  * ncf_alias_build (HOST function, once per dataset): Walker/Vose alias table of the
  *   inverse-popularity weights.

@@ -73,6 +73,8 @@ SIGNATURES = {
     "ncf_mlp_fwd": (I32, [P, I64, I64, P, I64, P, F32, F32, U64, P, P, P, P, P, P, P, P, P]),
     "ncf_mlp_fwd_bf16": (I32, [P, I64, I64, P, I64, P, F32, F32, U64, P, P, P, P, P, P, P, P, P]),
     "ncf_mlp_bwd_bf16": (I32, [P, I64, I64, P, P, I64, P, F32, U64, P, P, P, P, I64, P, P]),
+    "ncf_mlp_fwd_split": (I32, [P, I64, I64, P, I64, P, F32, F32, U64, P, P, P, P, P, P, P, P, P]),
+    "ncf_mlp_bwd_split": (I32, [P, I64, I64, P, P, I64, P, F32, U64, P, P, P, P, I64, P, P]),
     "ncf_mlp_bwd_workspace": (I64, [I64]),
     "ncf_mlp_bwd": (I32, [P, I64, I64, P, P, I64, P, F32, U64, P, P, P, P, I64, P, P]),
     "ncf_attn_block_fwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, F32, U64, P,

@@ -152,6 +152,46 @@ __device__ __forceinline__ f32x4 mfma_k32(bf16x8_t a, bf16x8_t b, f32x4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
 }
 
+// Split operands (MM = 3, the fp32 tower's Linears on bf16 matrix cores): every fp32 operand
+// x = h + m + l, three bf16 terms each rounded to nearest (h holds x's top 8 significant bits, m
+// the next 8, l the next 8: fp32's 24-bit significand; each residual is exact in fp32).  A
+// product a.b is accumulated from the six bf16 x bf16 products of order >= 2^-16 (ah bh, then
+// ah bm + am bh + ah bl + am bm + al bh into a second accumulator; every bf16 product is exact
+// in fp32); the three dropped ones are below 2^-24 |a||b| together, the fp32 MFMA's own rounding
+// level.  Six v_mfma_f32_16x16x32_bf16 (16 cycles each) replace eight v_mfma_f32_16x16x4_f32
+// (32 cycles each) per 16x16x32 tile.
+__device__ __forceinline__ void split3(float4 a, float4 b, bf16x8_t& h, bf16x8_t& m,
+                                       bf16x8_t& l) {
+  const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const __bf16 xh = (__bf16)x[k];
+    const float r1 = x[k] - (float)xh;
+    const __bf16 xm = (__bf16)r1;
+    const float r2 = r1 - (float)xm;
+    h[k] = xh;
+    m[k] = xm;
+    l[k] = (__bf16)r2;
+  }
+}
+struct Split3 {
+  bf16x8_t h, m, l;
+};
+__device__ __forceinline__ Split3 split3(float4 a, float4 b) {
+  Split3 s;
+  split3(a, b, s.h, s.m, s.l);
+  return s;
+}
+// hi += ah bh; lo += the five cross products (see split3)
+__device__ __forceinline__ void mfma_x3(const Split3& a, const Split3& b, f32x4& hi, f32x4& lo) {
+  hi = mfma_k32(a.h, b.h, hi);
+  lo = mfma_k32(a.h, b.m, lo);
+  lo = mfma_k32(a.m, b.h, lo);
+  lo = mfma_k32(a.h, b.l, lo);
+  lo = mfma_k32(a.m, b.m, lo);
+  lo = mfma_k32(a.l, b.h, lo);
+}
+
 __device__ __forceinline__ f32x4 mfma4(float4 a, float4 b, f32x4 acc) {
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
@@ -175,10 +215,64 @@ struct Split {
 };
 
 // Y[80 x N] = relu(X[80 x K] . W^T + b)   (W row-major [N][ldw], first K columns)
-template <int K, int N, int PX, int PY, int RT = kRT, bool BF = false>
+// lin_fwd on split operands (MM = 3): column slices innermost (one A split per row tile and k
+// chunk), weights split as they are loaded.
+template <int K, int N, int PX, int PY, int RT>
+__device__ __forceinline__ void lin_fwd_x3(const float* __restrict__ X, float* __restrict__ Y,
+                                           const float* __restrict__ W, int64_t ldw,
+                                           const float* __restrict__ bias) {
+  using Sp = Split<N, RT>;
+  constexpr int KQ = K / 4, CPW = Sp::CPW, RPW = Sp::RPW;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  const float* wp[CPW];
+#pragma unroll
+  for (int j = 0; j < CPW; ++j) wp[j] = W + (int64_t)(16 * Sp::cs(w, j) + i) * ldw + g * KQ;
+  f32x4 hi[CPW][RPW], lo[CPW][RPW];
+#pragma unroll
+  for (int j = 0; j < CPW; ++j)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) hi[j][r] = lo[j][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < KQ / 8; ++c) {
+    Split3 b[CPW];
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) b[j] = split3(ld4(wp[j] + 8 * c), ld4(wp[j] + 8 * c + 4));
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int rt = Sp::rt(w, r);
+      if (rt < RT) {
+        const float* xa = X + (16 * rt + i) * PX + g * KQ + 8 * c;
+        const Split3 a = split3(lds4(xa), lds4(xa + 4));
+#pragma unroll
+        for (int j = 0; j < CPW; ++j) mfma_x3(a, b[j], hi[j][r], lo[j][r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CPW; ++j) {
+    const int cs = Sp::cs(w, j);
+    const float bb = bias[16 * cs + i];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int rt = Sp::rt(w, r);
+      if (rt < RT) {
+        float* yp = Y + (16 * rt + 4 * g) * PY + 16 * cs + i;
+        const f32x4 v = hi[j][r] + lo[j][r];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) yp[e * PY] = fmaxf(v[e] + bb, 0.0f);
+      }
+    }
+  }
+}
+
+template <int K, int N, int PX, int PY, int RT = kRT, int MM = 0>
 __device__ __forceinline__ void lin_fwd(const float* __restrict__ X, float* __restrict__ Y,
                                         const float* __restrict__ W, int64_t ldw,
                                         const float* __restrict__ bias) {
+  if constexpr (MM == 3) {
+    lin_fwd_x3<K, N, PX, PY, RT>(X, Y, W, ldw, bias);
+    return;
+  }
   using Sp = Split<N, RT>;
   constexpr int KQ = K / 4;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
@@ -189,7 +283,7 @@ __device__ __forceinline__ void lin_fwd(const float* __restrict__ X, float* __re
     f32x4 acc[Sp::RPW];
 #pragma unroll
     for (int r = 0; r < Sp::RPW; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (BF) {
+    if constexpr (MM == 1) {
 #pragma unroll
       for (int c = 0; c < KQ / 8; ++c) {
         const bf16x8_t b = pk8(ld4(wp + 8 * c), ld4(wp + 8 * c + 4));
@@ -225,9 +319,73 @@ __device__ __forceinline__ void lin_fwd(const float* __restrict__ X, float* __re
 }
 
 // G[80 x NO] = DL[80 x KC] . W   (W row-major [KC][ldw], first NO columns)
-template <int KC, int NO, int PD, int PG, bool BF = false>
+// lin_bwd on split operands (MM = 3): the column-slice loop innermost, so each row tile's A
+// fragment (LDS) is split once per k chunk and feeds every column slice of the wave; the weight
+// columns come through one ring per slice.
+template <int KC, int NO, int PD, int PG>
+__device__ __forceinline__ void lin_bwd_x3(const float* __restrict__ DL, float* __restrict__ G,
+                                           const float* __restrict__ W, int64_t ldw) {
+  using Sp = Split<NO>;
+  constexpr int KQ = KC / 4, NC = KQ / 4, CPW = Sp::CPW, RPW = Sp::RPW;
+  static_assert(NC % 2 == 0, "split pairs of k chunks");
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  const float* wp[CPW];
+#pragma unroll
+  for (int j = 0; j < CPW; ++j) wp[j] = W + (int64_t)(g * KQ) * ldw + 16 * Sp::cs(w, j) + i;
+  auto chunk = [&](int j, int c) {
+    const float* q = wp[j] + (int64_t)(4 * c) * ldw;
+    return make_float4(q[0], q[ldw], q[2 * ldw], q[3 * ldw]);
+  };
+  f32x4 hi[CPW][RPW], lo[CPW][RPW];
+#pragma unroll
+  for (int j = 0; j < CPW; ++j)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) hi[j][r] = lo[j][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 nb[CPW][2];
+#pragma unroll
+  for (int j = 0; j < CPW; ++j) { nb[j][0] = chunk(j, 0); nb[j][1] = chunk(j, 1); }
+#pragma unroll
+  for (int c = 0; c < NC; c += 2) {
+    Split3 b[CPW];
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+      b[j] = split3(nb[j][0], nb[j][1]);
+      if (c + 2 < NC) { nb[j][0] = chunk(j, c + 2); nb[j][1] = chunk(j, c + 3); }
+    }
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int rt = Sp::rt(w, r);
+      if (rt < kRT) {
+        const float* da = DL + (16 * rt + i) * PD + g * KQ + 4 * c;
+        const Split3 a = split3(lds4(da), lds4(da + 4));
+#pragma unroll
+        for (int j = 0; j < CPW; ++j) mfma_x3(a, b[j], hi[j][r], lo[j][r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CPW; ++j) {
+    const int cs = Sp::cs(w, j);
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int rt = Sp::rt(w, r);
+      if (rt < kRT) {
+        float* gp = G + (16 * rt + 4 * g) * PG + 16 * cs + i;
+        const f32x4 v = hi[j][r] + lo[j][r];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gp[e * PG] = v[e];
+      }
+    }
+  }
+}
+
+template <int KC, int NO, int PD, int PG, int MM = 0>
 __device__ __forceinline__ void lin_bwd(const float* __restrict__ DL, float* __restrict__ G,
                                         const float* __restrict__ W, int64_t ldw) {
+  if constexpr (MM == 3) {
+    lin_bwd_x3<KC, NO, PD, PG>(DL, G, W, ldw);
+    return;
+  }
   using Sp = Split<NO>;
   constexpr int KQ = KC / 4;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
@@ -248,7 +406,7 @@ __device__ __forceinline__ void lin_bwd(const float* __restrict__ DL, float* __r
     float4 ring[D];
 #pragma unroll
     for (int c = 0; c < D; ++c) ring[c] = chunk(c);
-    if constexpr (BF) {
+    if constexpr (MM == 1) {
       static_assert(D % 2 == 0 && NC % 2 == 0, "bf16 pairs ring chunks");
 #pragma unroll
       for (int c = 0; c < NC; c += 2) {
@@ -488,7 +646,7 @@ __device__ __forceinline__ void ln_bwd(float* __restrict__ G, float* __restrict_
 
 // The forward in workgroups of VR valid rows staged as RT 16-row MFMA tiles (the padding rows
 // are zeros and are never stored).  VR < 16 RT lets two workgroups share a CU (A/B knob).
-template <int K0, int RT, int VR, bool BF = false>
+template <int K0, int RT, int VR, int MM = 0>
 __global__ __launch_bounds__(kThreads) void k_mlp_fwd(
     const float* __restrict__ xin, int64_t n, TowerArgs a, float eps, float p,
     const ncf_step_clock* clock, const float* __restrict__ w_out, const float* __restrict__ b_out,
@@ -518,21 +676,21 @@ __global__ __launch_bounds__(kThreads) void k_mlp_fwd(
   }
   __syncthreads();
   NCF_STAMP(0, 1);
-  lin_fwd<K0, N0, kPP, kPQ, RT, BF>(P, Q, a.l[0].w, a.l[0].ldw, a.l[0].b);
+  lin_fwd<K0, N0, kPP, kPQ, RT, MM>(P, Q, a.l[0].w, a.l[0].ldw, a.l[0].b);
   __syncthreads();
   NCF_STAMP(0, 2);
   ln_fwd<N0, kPQ, RT>(Q, row0, rows, a.l[0], eps, p, a.seed[0] + cs, nullptr, nullptr, nullptr,
                       nullptr, nullptr, nullptr, nullptr);
   __syncthreads();
   NCF_STAMP(0, 3);
-  lin_fwd<N0, N1, kPQ, kPP, RT, BF>(Q, P, a.l[1].w, a.l[1].ldw, a.l[1].b);
+  lin_fwd<N0, N1, kPQ, kPP, RT, MM>(Q, P, a.l[1].w, a.l[1].ldw, a.l[1].b);
   __syncthreads();
   NCF_STAMP(0, 4);
   ln_fwd<N1, kPP, RT>(P, row0, rows, a.l[1], eps, p, a.seed[1] + cs, nullptr, nullptr, nullptr,
                       nullptr, nullptr, nullptr, nullptr);
   __syncthreads();
   NCF_STAMP(0, 5);
-  lin_fwd<N1, N2, kPP, kPQ, RT, BF>(P, Q, a.l[2].w, a.l[2].ldw, a.l[2].b);
+  lin_fwd<N1, N2, kPP, kPQ, RT, MM>(P, Q, a.l[2].w, a.l[2].ldw, a.l[2].b);
   __syncthreads();
   NCF_STAMP(0, 6);
   ln_fwd<N2, kPQ, RT>(Q, row0, rows, a.l[2], eps, p, a.seed[2] + cs, w_out, b_out, mf_pred, w_fin,
@@ -556,9 +714,55 @@ static_assert(kFwdVR <= 16 * kFwdRT, "forward rows per workgroup exceed its tile
 // (the partial of this workgroup; one deferred reduction sums the 256 partial rows).  16x16
 // output tiles, contraction over the rows k-permuted: lane group g covers rows [20g, 20g + 20).
 // A wave keeps its dlin column fragment (20 values) and sweeps its k tiles with it.
-template <int N, int K, int PG, int PX, bool BF = false>
+// Split operands (MM = 3): the 20 rows of lane group g as three k-steps of 8 (rows 20 g + 8 t +
+// e, the last step's rows past 20 zero) of v_mfma_f32_16x16x32_bf16; the dlin fragment is split
+// once per n tile, the activation fragment once per (n, k) tile.
+template <int N, int K, int PG, int PX>
+__device__ __forceinline__ void wgrad_layer_x3(const float* __restrict__ G,
+                                               const float* __restrict__ X,
+                                               float* __restrict__ out) {
+  constexpr int TN = N / 16, TK = K / 16, R4 = kRows / 4;
+  constexpr int TNW = TN >= kWaves ? TN / kWaves : 1;
+  constexpr int WPN = TN >= kWaves ? 1 : kWaves / TN;
+  constexpr int TKW = TK / WPN;
+  static_assert(R4 == 20, "three k-steps of 8 rows per lane group");
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  auto frag = [&](const float* base, int pitch, int t) {   // rows 20 g + 8 t .. + 7 (<= 19)
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 8 * t + e < R4 ? base[(g * R4 + 8 * t + e) * pitch] : 0.0f;
+    return split3(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
+  };
+#pragma unroll
+  for (int jn = 0; jn < TNW; ++jn) {
+    const int tn = TN >= kWaves ? w + kWaves * jn : w % TN;
+    const int tk0 = TN >= kWaves ? 0 : (w / TN) * TKW;
+    const Split3 a0 = frag(G + 16 * tn + i, PG, 0), a1 = frag(G + 16 * tn + i, PG, 1),
+                 a2 = frag(G + 16 * tn + i, PG, 2);
+#pragma unroll 2
+    for (int jk = 0; jk < TKW; ++jk) {
+      const int tk = tk0 + jk;
+      const float* xb = X + 16 * tk + i;
+      f32x4 hi = {0.f, 0.f, 0.f, 0.f}, lo = {0.f, 0.f, 0.f, 0.f};
+      mfma_x3(a0, frag(xb, PX, 0), hi, lo);
+      mfma_x3(a1, frag(xb, PX, 1), hi, lo);
+      mfma_x3(a2, frag(xb, PX, 2), hi, lo);
+      float* o = out + (16 * tn + 4 * g) * K + 16 * tk + i;
+      const f32x4 v = hi + lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) st_nt(o + e * K, v[e]);
+    }
+  }
+}
+
+template <int N, int K, int PG, int PX, int MM = 0>
 __device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const float* __restrict__ X,
                                             float* __restrict__ out) {
+  if constexpr (MM == 3) {
+    wgrad_layer_x3<N, K, PG, PX>(G, X, out);
+    return;
+  }
+  constexpr bool BF = MM == 1;
   constexpr int TN = N / 16, TK = K / 16, R4 = kRows / 4;
   constexpr int TNW = TN >= kWaves ? TN / kWaves : 1;        // n tiles per wave
   constexpr int WPN = TN >= kWaves ? 1 : kWaves / TN;        // waves per n tile
@@ -823,7 +1027,7 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
   __syncthreads();
 }
 
-template <int K0, bool BF = false>
+template <int K0, int MM = 0>
 __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ g_last, int64_t n,
                                                       TowerArgs a, float p,
                                                       const ncf_step_clock* clock,
@@ -860,11 +1064,11 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_act<N1, kPP>(P, a.l[1], row0, rows, p, a.seed[1] + cs, R1);
     __syncthreads();
     NCF_STAMP(1, 3);
-    wgrad_layer<N2, N1, kPQ, kPP, BF>(Q, P, pp + T::kW2);
+    wgrad_layer<N2, N1, kPQ, kPP, MM>(Q, P, pp + T::kW2);
     __syncthreads();
     NCF_STAMP(1, 4);
   }
-  lin_bwd<N2, N1, kPQ, kPP, BF>(Q, P, a.l[2].w, a.l[2].ldw);
+  lin_bwd<N2, N1, kPQ, kPP, MM>(Q, P, a.l[2].w, a.l[2].ldw);
   __syncthreads();
   NCF_STAMP(1, 5);
   ln_bwd<N1, kPP>(P, Q, row0, rows, a.l[1], p, a.seed[1] + cs, pp + 3 * N2, R1);
@@ -873,11 +1077,11 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_act<N0, kPQ>(Q, a.l[0], row0, rows, p, a.seed[0] + cs);
     __syncthreads();
     NCF_STAMP(1, 7);
-    wgrad_layer<N1, N0, kPP, kPQ, BF>(P, Q, pp + T::kW1);
+    wgrad_layer<N1, N0, kPP, kPQ, MM>(P, Q, pp + T::kW1);
     __syncthreads();
     NCF_STAMP(1, 8);
   }
-  lin_bwd<N1, N0, kPP, kPQ, BF>(P, Q, a.l[1].w, a.l[1].ldw);
+  lin_bwd<N1, N0, kPP, kPQ, MM>(P, Q, a.l[1].w, a.l[1].ldw);
   __syncthreads();
   NCF_STAMP(1, 9);
   ln_bwd<N0, kPQ>(Q, P, row0, rows, a.l[0], p, a.seed[0] + cs, pp + 3 * (N2 + N1));
@@ -886,11 +1090,11 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_rows<K0, kPP>(P, xin, row0, rows);
     __syncthreads();
     NCF_STAMP(1, 11);
-    wgrad_layer<N0, K0, kPQ, kPP, BF>(Q, P, pp + T::kW0);
+    wgrad_layer<N0, K0, kPQ, kPP, MM>(Q, P, pp + T::kW0);
     __syncthreads();
     NCF_STAMP(1, 12);
   }
-  lin_bwd<N0, K0, kPQ, kPP, BF>(Q, P, a.l[0].w, a.l[0].ldw);
+  lin_bwd<N0, K0, kPQ, kPP, MM>(Q, P, a.l[0].w, a.l[0].ldw);
   __syncthreads();
   NCF_STAMP(1, 13);
   for (int e = threadIdx.x; e < rows * (K0 / 4); e += kThreads) {
@@ -942,23 +1146,23 @@ extern "C" int ncf_mlp_fused_supported(int64_t dim, int64_t n_layers, const int6
   return tower_ok(dim, n_layers, hidden) ? 1 : 0;
 }
 
-template <int K0, bool BF>
+template <int K0, int MM>
 static void launch_fwd(const float* x, int64_t n, const TowerArgs& a, float eps, float dropout_p,
                        const ncf_step_clock* clock, const float* mlp_out_w, const float* mlp_out_b,
                        const float* mf_pred, const float* final_w, const float* final_b,
                        float* mlp_pred, float* prob, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_mlp_fwd<K0, kFwdRT, kFwdVR, BF>,
+    (void)hipFuncSetAttribute((const void*)k_mlp_fwd<K0, kFwdRT, kFwdVR, MM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsFwd);
     attr = true;
   }
-  hipLaunchKernelGGL((k_mlp_fwd<K0, kFwdRT, kFwdVR, BF>), dim3((unsigned)ncf_cdiv(n, kFwdVR)),
+  hipLaunchKernelGGL((k_mlp_fwd<K0, kFwdRT, kFwdVR, MM>), dim3((unsigned)ncf_cdiv(n, kFwdVR)),
                      dim3(kThreads), kLdsFwd, st, x, n, a, eps, dropout_p, clock, mlp_out_w,
                      mlp_out_b, mf_pred, final_w, final_b, mlp_pred, prob);
 }
 
-template <bool BF>
+template <int MM>
 static int mlp_fwd_impl(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
                         int64_t n_layers, const int64_t* hidden, float eps, float dropout_p,
                         uint64_t seed, const ncf_step_clock* clock, const float* mlp_out_w,
@@ -973,10 +1177,10 @@ static int mlp_fwd_impl(const float* x, int64_t n, int64_t dim, const ncf_mlp_la
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   if (dim == 64)
-    launch_fwd<64, BF>(x, n, a, eps, dropout_p, clock, mlp_out_w, mlp_out_b, mf_pred, final_w,
+    launch_fwd<64, MM>(x, n, a, eps, dropout_p, clock, mlp_out_w, mlp_out_b, mf_pred, final_w,
                        final_b, mlp_pred, prob, st);
   else
-    launch_fwd<128, BF>(x, n, a, eps, dropout_p, clock, mlp_out_w, mlp_out_b, mf_pred, final_w,
+    launch_fwd<128, MM>(x, n, a, eps, dropout_p, clock, mlp_out_w, mlp_out_b, mf_pred, final_w,
                         final_b, mlp_pred, prob, st);
   NCF_CHECK_LAUNCH("ncf_mlp_fwd");
   return NCF_OK;
@@ -1040,23 +1244,23 @@ static int defer_tower(const TowerArgs& a, const ncf_head_args* head, const ncf_
   return rc;
 }
 
-template <int K0, bool BF>
+template <int K0, int MM>
 static void launch_bwd(const float* grad_a_last, int64_t n, const TowerArgs& a, float dropout_p,
                        const ncf_step_clock* clock, float* grad_x, float* workspace,
                        const ncf_head_args& h, int fused_head, float inv_n, const float* x, int fw,
                        hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_mlp_bwd<K0, BF>,
+    (void)hipFuncSetAttribute((const void*)k_mlp_bwd<K0, MM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
     attr = true;
   }
-  hipLaunchKernelGGL((k_mlp_bwd<K0, BF>), dim3((unsigned)ncf_cdiv(n, kRows)), dim3(kThreads), kLds,
+  hipLaunchKernelGGL((k_mlp_bwd<K0, MM>), dim3((unsigned)ncf_cdiv(n, kRows)), dim3(kThreads), kLds,
                      st, grad_a_last, n, a, dropout_p, clock, grad_x, workspace, h, fused_head,
                      inv_n, x, fw);
 }
 
-template <bool BF>
+template <int MM>
 static int mlp_bwd_impl(const float* grad_a_last, int64_t n, int64_t dim, const float* x,
                         const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
                         float dropout_p, uint64_t seed, const ncf_step_clock* clock,
@@ -1102,10 +1306,10 @@ static int mlp_bwd_impl(const float* grad_a_last, int64_t n, int64_t dim, const 
   const int nb = (int)ncf_cdiv(n, kRows);
   hipStream_t st = (hipStream_t)stream;
   if (dim == 64)
-    launch_bwd<64, BF>(grad_a_last, n, a, dropout_p, clock, grad_x, workspace, h, head ? 1 : 0,
+    launch_bwd<64, MM>(grad_a_last, n, a, dropout_p, clock, grad_x, workspace, h, head ? 1 : 0,
                        inv_n, x, fw ? 1 : 0, st);
   else
-    launch_bwd<128, BF>(grad_a_last, n, a, dropout_p, clock, grad_x, workspace, h, head ? 1 : 0,
+    launch_bwd<128, MM>(grad_a_last, n, a, dropout_p, clock, grad_x, workspace, h, head ? 1 : 0,
                         inv_n, x, fw ? 1 : 0, st);
   NCF_CHECK_LAUNCH("ncf_mlp_bwd");
   ncf_reduce_list local;
@@ -1127,7 +1331,7 @@ extern "C" int ncf_mlp_fwd(const float* x, int64_t n, int64_t dim, const ncf_mlp
                            uint64_t seed, const ncf_step_clock* clock, const float* mlp_out_w,
                            const float* mlp_out_b, const float* mf_pred, const float* final_w,
                            const float* final_b, float* mlp_pred, float* prob, void* stream) {
-  return mlp_fwd_impl<false>(x, n, dim, layers, n_layers, hidden, eps, dropout_p, seed, clock,
+  return mlp_fwd_impl<0>(x, n, dim, layers, n_layers, hidden, eps, dropout_p, seed, clock,
                              mlp_out_w, mlp_out_b, mf_pred, final_w, final_b, mlp_pred, prob,
                              stream);
 }
@@ -1137,7 +1341,7 @@ extern "C" int ncf_mlp_bwd(const float* grad_a_last, int64_t n, int64_t dim, con
                            float dropout_p, uint64_t seed, const ncf_step_clock* clock,
                            const ncf_head_args* head, float* grad_x, float* workspace,
                            int64_t workspace_floats, ncf_reduce_list* defer, void* stream) {
-  return mlp_bwd_impl<false>(grad_a_last, n, dim, x, layers, n_layers, hidden, dropout_p, seed,
+  return mlp_bwd_impl<0>(grad_a_last, n, dim, x, layers, n_layers, hidden, dropout_p, seed,
                              clock, head, grad_x, workspace, workspace_floats, defer, stream);
 }
 
@@ -1148,7 +1352,7 @@ extern "C" int ncf_mlp_fwd_bf16(const float* x, int64_t n, int64_t dim, const nc
                                 uint64_t seed, const ncf_step_clock* clock, const float* mlp_out_w,
                                 const float* mlp_out_b, const float* mf_pred, const float* final_w,
                                 const float* final_b, float* mlp_pred, float* prob, void* stream) {
-  return mlp_fwd_impl<true>(x, n, dim, layers, n_layers, hidden, eps, dropout_p, seed, clock,
+  return mlp_fwd_impl<1>(x, n, dim, layers, n_layers, hidden, eps, dropout_p, seed, clock,
                             mlp_out_w, mlp_out_b, mf_pred, final_w, final_b, mlp_pred, prob,
                             stream);
 }
@@ -1158,6 +1362,28 @@ extern "C" int ncf_mlp_bwd_bf16(const float* grad_a_last, int64_t n, int64_t dim
                                 float dropout_p, uint64_t seed, const ncf_step_clock* clock,
                                 const ncf_head_args* head, float* grad_x, float* workspace,
                                 int64_t workspace_floats, ncf_reduce_list* defer, void* stream) {
-  return mlp_bwd_impl<true>(grad_a_last, n, dim, x, layers, n_layers, hidden, dropout_p, seed,
+  return mlp_bwd_impl<1>(grad_a_last, n, dim, x, layers, n_layers, hidden, dropout_p, seed,
                             clock, head, grad_x, workspace, workspace_floats, defer, stream);
+}
+
+// The fp32 tower with its three Linears (forward dX, backward dX and dW) on bf16 matrix cores
+// through split operands (split3 / mfma_x3: six bf16 products per fp32 product, the dropped terms
+// below 2^-24 of it; fp32 accumulation); every row op stays fp32.  Same arguments as ncf_mlp_fwd
+// / ncf_mlp_bwd.
+extern "C" int ncf_mlp_fwd_split(const float* x, int64_t n, int64_t dim, const ncf_mlp_layer* layers,
+                                 int64_t n_layers, const int64_t* hidden, float eps, float dropout_p,
+                                 uint64_t seed, const ncf_step_clock* clock, const float* mlp_out_w,
+                                 const float* mlp_out_b, const float* mf_pred, const float* final_w,
+                                 const float* final_b, float* mlp_pred, float* prob, void* stream) {
+  return mlp_fwd_impl<3>(x, n, dim, layers, n_layers, hidden, eps, dropout_p, seed, clock,
+                         mlp_out_w, mlp_out_b, mf_pred, final_w, final_b, mlp_pred, prob, stream);
+}
+
+extern "C" int ncf_mlp_bwd_split(const float* grad_a_last, int64_t n, int64_t dim, const float* x,
+                                 const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
+                                 float dropout_p, uint64_t seed, const ncf_step_clock* clock,
+                                 const ncf_head_args* head, float* grad_x, float* workspace,
+                                 int64_t workspace_floats, ncf_reduce_list* defer, void* stream) {
+  return mlp_bwd_impl<3>(grad_a_last, n, dim, x, layers, n_layers, hidden, dropout_p, seed, clock,
+                         head, grad_x, workspace, workspace_floats, defer, stream);
 }

@@ -190,6 +190,14 @@ __device__ __forceinline__ void st_logit4<_Float16>(_Float16* p, float4 v) {   /
   *reinterpret_cast<h4*>(p) = h4{(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
 }
 
+// The bin range [vmin, vmax] spans the FINITE sample values only: an fp16 sample logit below
+// -65504 is stored as -inf (rounded toward -inf, k_sample16), and a -inf (or a NaN) in the range
+// would make its scale 0 / NaN and every value fall into bin 0.  Non-finite values clamp into
+// bin 0 (below the range; a +inf cannot occur: the rounding saturates at 65504), so the
+// threshold stays a valid lower bound whatever the sample holds.
+__device__ __forceinline__ float fin_lo(float x) { return __builtin_isfinite(x) ? x : -INFINITY; }
+__device__ __forceinline__ float fin_hi(float x) { return __builtin_isfinite(x) ? x : INFINITY; }
+
 template <int NT, typename E = float>
 __global__ __launch_bounds__(NT) void k_kth_lds(const E* __restrict__ logits, int64_t S,
                                                  int K, const float* __restrict__ bias,
@@ -224,15 +232,15 @@ __global__ __launch_bounds__(NT) void k_kth_lds(const E* __restrict__ logits, in
                                           x.w + bias[(j + 3) * stride])
                             : x;
       st_logit4<E>(kth_vals + j, v);
-      vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
-      vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+      vmax = fmaxf(vmax, fmaxf(fmaxf(fin_lo(v.x), fin_lo(v.y)), fmaxf(fin_lo(v.z), fin_lo(v.w))));
+      vmin = fminf(vmin, fminf(fminf(fin_hi(v.x), fin_hi(v.y)), fminf(fin_hi(v.z), fin_hi(v.w))));
     }
   }
   for (int64_t j = 4 * S4 + tid; j < S; j += NT) {
     const float v = bias ? (float)row[j] + bias[j * stride] : (float)row[j];
     kth_vals[j] = (E)v;
-    vmax = fmaxf(vmax, v);
-    vmin = fminf(vmin, v);
+    vmax = fmaxf(vmax, fin_lo(v));
+    vmin = fminf(vmin, fin_hi(v));
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {

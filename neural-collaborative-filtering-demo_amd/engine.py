@@ -25,6 +25,10 @@ from ._lib import ptr
 LN_EPS = 1e-5
 # bf16 configuration: the fused MLP tower's Linears on bf16 MFMA (False: fp32 MFMA)
 BF16_MM = True
+# fp32 configuration: the fused MLP tower's Linears on bf16 matrix cores through split operands
+# (ncf_mlp_fwd_split / _bwd_split: six bf16 products per fp32 product, fp32-accurate) instead of
+# the fp32 MFMA (False)
+TOWER_SPLIT = True
 # SURVEY fact 6 (a training group's M rows hold one user): the gather writes the LN'd user rows
 # once per group (group_rows = M) when every reader takes the group's row — the fused attention
 # block and the fused tower's head backward (False: every row; the same bits, tested; measured
@@ -477,7 +481,7 @@ class NCFEngine:
         if temporal is None and self.mlp_fused(D, hid):
             # a7 + a8: the whole tower and the head in one launch (mlp_tower.hip)
             _, addr, _, haddr = self._mlp_layers(w, train, bwd=False)
-            _lib.call("ncf_mlp_fwd_bf16" if bf16 and BF16_MM else "ncf_mlp_fwd", ptr(x), n, D, addr,
+            _lib.call(self._tower_entry("ncf_mlp_fwd", bf16), ptr(x), n, D, addr,
                       len(hid),
                       haddr, LN_EPS, drop_p if train else 0.0, seed, ptr(self.clock),
                       pp["mlp_output.weight"],
@@ -558,6 +562,14 @@ class NCFEngine:
         if ok is None:
             ok = self._mlp_ok[key] = bool(_lib.query("ncf_attn_block_supported", D, H, M))
         return ok
+
+    @staticmethod
+    def _tower_entry(base: str, bf16: bool) -> str:
+        """The fused tower's entry point: bf16 tables -> single-term bf16 MFMA (BF16_MM); fp32
+        -> split-operand bf16 MFMA (TOWER_SPLIT) or the fp32 MFMA."""
+        if bf16 and BF16_MM:
+            return base + "_bf16"
+        return base + "_split" if (TOWER_SPLIT and not bf16) else base
 
     def attn_rc(self, D: int, H: int, M: int) -> bool:
         """Whether the training forward of the attention block stashes nothing and its backward
@@ -716,7 +728,7 @@ class NCFEngine:
             h.loss_denominator = float(loss_denominator)
             # (the gather's source rows of the LN'd user rows: ncf_head_args.user_ids)
             h.user_ids, h.group_rows = ptr(uid), getattr(w, "group_rows", 0)
-            _lib.call("ncf_mlp_bwd_bf16" if bf16 and BF16_MM else "ncf_mlp_bwd", None, n, D,
+            _lib.call(self._tower_entry("ncf_mlp_bwd", bf16), None, n, D,
                       ptr(w.y), addr,
                       len(hid), haddr, drop_p, seed,
                       ptr(self.clock), ctypes.addressof(h), ptr(w.dy), ptr(w.site("mlp")),

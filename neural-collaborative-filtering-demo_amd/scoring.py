@@ -284,11 +284,17 @@ class _TopKRun:
         I, D = p.shape
         q = self.q[redo].contiguous()
         nr = q.shape[0]
-        sample = torch.empty(nr, self.S, device=p.device)
+        # (a sample sized for the k-th itself, ~k I / S candidates within cap: the rank-j
+        # sample's S ~ I / k would expect ~k^2 of them, over the cap at k = 100, and cost every
+        # flagged user a further overflow round)
+        S = _sample_size(I, k, self.cap)
+        stride = I // S
+        sbias = idx.bias[::stride][:S].contiguous()
+        sample = torch.empty(nr, S, device=p.device)
         thr = torch.empty(nr, device=p.device)
-        _lib.call("ncf_gemm_f32", nr, self.S, D, ptr(q), D, 0, ptr(p), D * self.stride, 1,
-                  ptr(sample), self.S, ptr(self.sbias), 0, st)
-        _lib.call("ncf_score_kth", ptr(sample), nr, self.S, k, None, self.stride, ptr(thr), st)
+        _lib.call("ncf_gemm_f32", nr, S, D, ptr(q), D, 0, ptr(p), D * stride, 1,
+                  ptr(sample), S, ptr(sbias), 0, st)
+        _lib.call("ncf_score_kth", ptr(sample), nr, S, k, None, stride, ptr(thr), st)
         self.thr[redo] = thr
 
     def redo_overflow(self, st):

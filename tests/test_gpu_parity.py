@@ -644,12 +644,16 @@ def test_attn_shared_q_matches_per_row(monkeypatch, D, H, M, B, uniform, rc):
 @pytest.mark.parametrize("wgrad", ["1", "0"])
 @pytest.mark.parametrize("B,drop,D", [(37, 0.2, 64), (64, 0.0, 64), (1, 0.2, 64), (300, 0.2, 64),
                                       (37, 0.2, 128), (64, 0.0, 128), (300, 0.2, 128)])
-def test_mlp_tower_matches_unfused(monkeypatch, B, drop, D, wgrad):
+@pytest.mark.parametrize("split", [True, False])
+def test_mlp_tower_matches_unfused(monkeypatch, B, drop, D, wgrad, split):
     """The one-launch MLP tower (mlp_tower.hip, forward + backward) vs the per-layer launches
     (GEMM + rowops + head), same dropout stream: probabilities, saved activations, dense and
     compact table gradients agree to the grads tolerance; n = 5B rows not a multiple of the
-    32-row tile exercises the ragged last workgroup.  D = 128 is C4's input width."""
+    32-row tile exercises the ragged last workgroup.  D = 128 is C4's input width.  ``split``:
+    the fused tower's Linears on split-operand bf16 MFMA (engine.TOWER_SPLIT) or fp32 MFMA."""
+    import ncf_amd.engine as E
     from ncf_amd.trainer import FusedTrainStep
+    monkeypatch.setattr(E, "TOWER_SPLIT", split)
     out = []
     monkeypatch.setenv("NCF_MLP_WGRAD", wgrad)
     for flag in ("0", "1"):
@@ -686,6 +690,46 @@ def test_mlp_tower_matches_unfused(monkeypatch, B, drop, D, wgrad):
     torch.testing.assert_close(b["grad"], a["grad"], rtol=1e-4, atol=1e-6)
     for k in a["G"]:
         torch.testing.assert_close(b["G"][k], a["G"][k], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_mlp_tower_split_matches_fp32_mfma(monkeypatch, D):
+    """The fused tower on split-operand bf16 MFMA (ncf_mlp_fwd_split / ncf_mlp_bwd_split: x =
+    h + m + l in bf16, six products per fp32 product) against the same tower on fp32 MFMA, two
+    training steps with dropout: probabilities, loss, the saved pre-LN rows, dense and compact
+    table gradients at fp32 rounding distance (much tighter than the grads tolerance)."""
+    import ncf_amd.engine as E
+    from ncf_amd.trainer import FusedTrainStep
+    out = []
+    for split in (False, True):
+        monkeypatch.setattr(E, "TOWER_SPLIT", split)
+        torch.manual_seed(71)
+        m = ncf.AdvancedNCF(600, 400, 5, 24, D, D, 32, [256, 128, 64], 4, 0.2, 4).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+        g = torch.Generator().manual_seed(72)
+        for _ in range(2):
+            u = torch.randint(0, 600, (77,), generator=g).repeat_interleave(5).to(DEV)
+            i = torch.randint(0, 400, (385,), generator=g).to(DEV)
+            t = torch.zeros(77, 5)
+            t[:, 0] = 1
+            w = step(u, i, t.reshape(-1, 1).to(DEV))
+        torch.cuda.synchronize()
+        nu = w.num_unique.cpu().tolist()
+        out.append(dict(prob=w.prob.cpu().clone(), loss=w.loss.cpu().clone(),
+                        r=[x.cpu().clone() for x in w.r], grad=m.engine.flat_grad.cpu().clone(),
+                        G={k: v[:nu[0 if k.endswith("user") else 1]].cpu().clone()
+                           for k, v in w.G.items()}))
+    a, b = out
+    dp = (b["prob"] - a["prob"]).abs().max().item()
+    dg = ((b["grad"] - a["grad"]).abs() / (a["grad"].abs() + 1e-6)).max().item()
+    print(f"split vs fp32 MFMA D={D}: |dprob| {dp:.3g}, max rel dgrad {dg:.3g}")
+    torch.testing.assert_close(b["prob"], a["prob"], rtol=0, atol=5e-7)
+    torch.testing.assert_close(b["loss"], a["loss"], rtol=1e-6, atol=1e-7)
+    for x, y in zip(b["r"], a["r"]):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(b["grad"], a["grad"], rtol=2e-5, atol=1e-7)
+    for k in a["G"]:
+        torch.testing.assert_close(b["G"][k], a["G"][k], rtol=2e-5, atol=1e-8)
 
 
 def test_mlp_tower_eval_matches_unfused(monkeypatch):
@@ -1351,6 +1395,33 @@ def test_fp16_threshold_sample_equals_fp32_sample(k, cap, monkeypatch):
     s32, i32 = score_topk(m, users, k=k, index=idx, cap=cap)
     assert torch.equal(i16, i32)
     assert torch.equal(s16, s32)
+
+
+def test_fp16_sample_with_overflowing_bias_equals_fp32_sample(monkeypatch):
+    """item biases far outside the fp16 range.  A third of the items get -1e6 (their
+    fp16 sample logits round down to -inf) and a few get +1e5 (they saturate at 65504): the k-th
+    select's bin range covers the finite sample values only (k_kth_lds fin_lo / fin_hi), so the
+    fp16-sample pipeline still returns the fp32-sample pipeline's top-k bits, and the boosted items
+    lead every user's list."""
+    from ncf_amd import scoring
+    from ncf_amd.scoring import ItemIndex, score_topk
+    torch.manual_seed(19)
+    U, I = 4000, 60013
+    m = ncf.AdvancedNCF(U, I, 5, 24).to(DEV)
+    m.eval()
+    users = torch.randperm(U)[:300]
+    idx = ItemIndex(m)
+    idx.bias[::3] = -1e6
+    boost = torch.tensor([5, 7001, 33333], device=DEV)
+    idx.bias[boost] = 1e5
+    out = []
+    for s16 in (True, False):
+        monkeypatch.setattr(scoring, "SAMPLE16", s16)
+        out.append(score_topk(m, users, k=10, index=idx))
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][0], out[1][0])
+    top3 = out[0][1][:, :3].sort(dim=1).values
+    assert torch.equal(top3, boost.sort().values.expand_as(top3))
 
 
 def test_sample_group_maxima_bitwise_equal_max_of_sample():

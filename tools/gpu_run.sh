@@ -29,7 +29,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 md5sum neural-collaborative-filtering-demo_amd/*.so > "$OUT/${TAG}_so.md5" 2>/dev/null
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
-QUICK="bench.py --steps 60 --warmup 10 --prime 128 --no-c4 --no-score --no-cpu-baseline --no-dropin"
+QUICK="bench.py --steps 60 --warmup 10 --prime 128 --no-c4 --no-score --no-cpu-baseline --no-dropin --no-extra"
 for what in "$@"; do
   echo "== $TAG $what $(date +%T)"
   case "$what" in
@@ -47,7 +47,7 @@ for what in "$@"; do
       rc=$?
       grep '^{' "$OUT/${TAG}_bench.log" | tail -1 > "$OUT/${TAG}_bench.json" ;;
     quick)
-      timeout -k 10 300 python -u bench.py --steps 100 --warmup 10 --no-c4 --no-score \
+      timeout -k 10 300 python -u bench.py --steps 100 --warmup 10 --no-c4 --no-score --no-extra \
         > "$OUT/${TAG}_quick.log" 2>&1
       rc=$?
       grep '^{' "$OUT/${TAG}_quick.log" | tail -1 > "$OUT/${TAG}_quick.json" ;;
