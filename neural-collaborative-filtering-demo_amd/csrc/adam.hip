@@ -533,8 +533,19 @@ __global__ __launch_bounds__(256) void k_adam_flat_close(float* __restrict__ p,
                                                          uint64_t base_seed, AdamScalars s) {
   const int32_t step = clock->t + step_rel;
   const float ns = table[4 * step], bc = table[4 * step + 1];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  // float4 per lane (the flat buffers are 16-B aligned), a short scalar tail; the same adam1 per
+  // element as the scalar loop (bit-identical)
+  const int64_t n4 = n >> 2;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n4;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float4 pp = ld4(p + 4 * e), mm = ld4(m + 4 * e), vv = ld4(v + 4 * e);
+    adam4(pp, mm, vv, ld4(g + 4 * e), ns, bc, s);
+    st4(p + 4 * e, pp);
+    st4(m + 4 * e, mm);
+    st4(v + 4 * e, vv);
+  }
+  if (blockIdx.x == 0 && (int64_t)threadIdx.x < n - 4 * n4) {
+    const int64_t i = 4 * n4 + threadIdx.x;
     float pp = p[i], mm = m[i], vv = v[i];
     adam1(pp, mm, vv, g[i], ns, bc, s);
     p[i] = pp;
@@ -924,7 +935,13 @@ extern "C" int ncf_adam_flat_clock_close(float* param, const float* grad, float*
                                          uint64_t base_seed, void* stream) {
   NCF_CHECK_ARG(n >= 1 && param && grad && exp_avg && exp_avg_sq && step_table && clock,
                 "ncf_adam_flat_clock_close: bad args");
-  hipLaunchKernelGGL(k_adam_flat_close, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+  NCF_CHECK_ARG(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
+                "ncf_adam_flat_clock_close: buffers must be 16-B aligned");
+  // every block's arrival is one same-address atomic on the clock word: at most 64 blocks
+  // (was one per 256 elements, 328 at C2: the serialised atomics held the launch ~3 us)
+  int64_t nb = ((n >> 2) + 255) / 256;
+  nb = nb < 1 ? 1 : (nb > 64 ? 64 : nb);
+  hipLaunchKernelGGL(k_adam_flat_close, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream,
                      param, grad, exp_avg, exp_avg_sq, n, step_table, step_rel, clock, base_seed,
                      consts_of(beta1, beta2, eps, weight_decay));
   NCF_CHECK_LAUNCH("ncf_adam_flat_clock_close");

@@ -683,7 +683,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_fwd(
                       nullptr, nullptr, nullptr, nullptr);
   __syncthreads();
   NCF_STAMP(0, 3);
-  lin_fwd<N0, N1, kPQ, kPP, RT, MM>(Q, P, a.l[1].w, a.l[1].ldw, a.l[1].b);
+  lin_fwd<N0, N1, kPQ, kPP, RT, (MM == 3 ? 0 : MM)>(Q, P, a.l[1].w, a.l[1].ldw, a.l[1].b);
   __syncthreads();
   NCF_STAMP(0, 4);
   ln_fwd<N1, kPP, RT>(P, row0, rows, a.l[1], eps, p, a.seed[1] + cs, nullptr, nullptr, nullptr,
@@ -714,54 +714,10 @@ static_assert(kFwdVR <= 16 * kFwdRT, "forward rows per workgroup exceed its tile
 // (the partial of this workgroup; one deferred reduction sums the 256 partial rows).  16x16
 // output tiles, contraction over the rows k-permuted: lane group g covers rows [20g, 20g + 20).
 // A wave keeps its dlin column fragment (20 values) and sweeps its k tiles with it.
-// Split operands (MM = 3): the 20 rows of lane group g as three k-steps of 8 (rows 20 g + 8 t +
-// e, the last step's rows past 20 zero) of v_mfma_f32_16x16x32_bf16; the dlin fragment is split
-// once per n tile, the activation fragment once per (n, k) tile.
-template <int N, int K, int PG, int PX>
-__device__ __forceinline__ void wgrad_layer_x3(const float* __restrict__ G,
-                                               const float* __restrict__ X,
-                                               float* __restrict__ out) {
-  constexpr int TN = N / 16, TK = K / 16, R4 = kRows / 4;
-  constexpr int TNW = TN >= kWaves ? TN / kWaves : 1;
-  constexpr int WPN = TN >= kWaves ? 1 : kWaves / TN;
-  constexpr int TKW = TK / WPN;
-  static_assert(R4 == 20, "three k-steps of 8 rows per lane group");
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-  auto frag = [&](const float* base, int pitch, int t) {   // rows 20 g + 8 t .. + 7 (<= 19)
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = 8 * t + e < R4 ? base[(g * R4 + 8 * t + e) * pitch] : 0.0f;
-    return split3(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
-  };
-#pragma unroll
-  for (int jn = 0; jn < TNW; ++jn) {
-    const int tn = TN >= kWaves ? w + kWaves * jn : w % TN;
-    const int tk0 = TN >= kWaves ? 0 : (w / TN) * TKW;
-    const Split3 a0 = frag(G + 16 * tn + i, PG, 0), a1 = frag(G + 16 * tn + i, PG, 1),
-                 a2 = frag(G + 16 * tn + i, PG, 2);
-#pragma unroll 2
-    for (int jk = 0; jk < TKW; ++jk) {
-      const int tk = tk0 + jk;
-      const float* xb = X + 16 * tk + i;
-      f32x4 hi = {0.f, 0.f, 0.f, 0.f}, lo = {0.f, 0.f, 0.f, 0.f};
-      mfma_x3(a0, frag(xb, PX, 0), hi, lo);
-      mfma_x3(a1, frag(xb, PX, 1), hi, lo);
-      mfma_x3(a2, frag(xb, PX, 2), hi, lo);
-      float* o = out + (16 * tn + 4 * g) * K + 16 * tk + i;
-      const f32x4 v = hi + lo;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) st_nt(o + e * K, v[e]);
-    }
-  }
-}
-
 template <int N, int K, int PG, int PX, int MM = 0>
 __device__ __forceinline__ void wgrad_layer(const float* __restrict__ G, const float* __restrict__ X,
                                             float* __restrict__ out) {
-  if constexpr (MM == 3) {
-    wgrad_layer_x3<N, K, PG, PX>(G, X, out);
-    return;
-  }
+  static_assert(MM == 0 || MM == 1, "weight gradients: fp32 or single-term bf16 MFMA");
   constexpr bool BF = MM == 1;
   constexpr int TN = N / 16, TK = K / 16, R4 = kRows / 4;
   constexpr int TNW = TN >= kWaves ? TN / kWaves : 1;        // n tiles per wave
@@ -1042,6 +998,10 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
   const int rows = (int)min<int64_t>(kRows, n - row0);
   const uint64_t cs = clock ? clock->seed : 0ull;
   using T = Lay<K0>;
+  // MM = 3: the three dX Linears on split operands; the weight gradients stay on fp32 MFMA
+  // (their activation operand would be split once per (n, k) tile: VALU-bound, measured slower,
+  // round 5: wgrad1 29.3K vs 26.9K cycles, lin1 bwd 21.8K vs 30.8K)
+  constexpr int WM = MM == 3 ? 0 : MM;
   float* pp = part + (int64_t)blockIdx.x * T::kPartW;
   NCF_STAMP(1, 0);
   if (fused_head) {
@@ -1064,7 +1024,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_act<N1, kPP>(P, a.l[1], row0, rows, p, a.seed[1] + cs, R1);
     __syncthreads();
     NCF_STAMP(1, 3);
-    wgrad_layer<N2, N1, kPQ, kPP, MM>(Q, P, pp + T::kW2);
+    wgrad_layer<N2, N1, kPQ, kPP, WM>(Q, P, pp + T::kW2);
     __syncthreads();
     NCF_STAMP(1, 4);
   }
@@ -1077,7 +1037,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_act<N0, kPQ>(Q, a.l[0], row0, rows, p, a.seed[0] + cs);
     __syncthreads();
     NCF_STAMP(1, 7);
-    wgrad_layer<N1, N0, kPP, kPQ, MM>(P, Q, pp + T::kW1);
+    wgrad_layer<N1, N0, kPP, kPQ, WM>(P, Q, pp + T::kW1);
     __syncthreads();
     NCF_STAMP(1, 8);
   }
@@ -1090,7 +1050,7 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
     stage_rows<K0, kPP>(P, xin, row0, rows);
     __syncthreads();
     NCF_STAMP(1, 11);
-    wgrad_layer<N0, K0, kPQ, kPP, MM>(Q, P, pp + T::kW0);
+    wgrad_layer<N0, K0, kPQ, kPP, WM>(Q, P, pp + T::kW0);
     __syncthreads();
     NCF_STAMP(1, 12);
   }

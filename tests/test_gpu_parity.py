@@ -695,9 +695,11 @@ def test_mlp_tower_matches_unfused(monkeypatch, B, drop, D, wgrad, split):
 @pytest.mark.parametrize("D", [64, 128])
 def test_mlp_tower_split_matches_fp32_mfma(monkeypatch, D):
     """The fused tower on split-operand bf16 MFMA (ncf_mlp_fwd_split / ncf_mlp_bwd_split: x =
-    h + m + l in bf16, six products per fp32 product) against the same tower on fp32 MFMA, two
-    training steps with dropout: probabilities, loss, the saved pre-LN rows, dense and compact
-    table gradients at fp32 rounding distance (much tighter than the grads tolerance)."""
+    h + m + l in bf16, six products per fp32 product) against the same tower on fp32 MFMA, with
+    dropout.  The first step (same weights): probabilities, loss, the saved pre-LN rows, dense
+    and compact table gradients at fp32 rounding distance (much tighter than the grads
+    tolerance).  The second step runs on weights one Adam step apart, where Adam turns rounding
+    noise in near-zero gradients into +-lr moves: held to the F2 tolerances."""
     import ncf_amd.engine as E
     from ncf_amd.trainer import FusedTrainStep
     out = []
@@ -707,29 +709,35 @@ def test_mlp_tower_split_matches_fp32_mfma(monkeypatch, D):
         m = ncf.AdvancedNCF(600, 400, 5, 24, D, D, 32, [256, 128, 64], 4, 0.2, 4).to(DEV)
         step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
         g = torch.Generator().manual_seed(72)
+        rec = []
         for _ in range(2):
             u = torch.randint(0, 600, (77,), generator=g).repeat_interleave(5).to(DEV)
             i = torch.randint(0, 400, (385,), generator=g).to(DEV)
             t = torch.zeros(77, 5)
             t[:, 0] = 1
             w = step(u, i, t.reshape(-1, 1).to(DEV))
-        torch.cuda.synchronize()
-        nu = w.num_unique.cpu().tolist()
-        out.append(dict(prob=w.prob.cpu().clone(), loss=w.loss.cpu().clone(),
-                        r=[x.cpu().clone() for x in w.r], grad=m.engine.flat_grad.cpu().clone(),
-                        G={k: v[:nu[0 if k.endswith("user") else 1]].cpu().clone()
-                           for k, v in w.G.items()}))
-    a, b = out
-    dp = (b["prob"] - a["prob"]).abs().max().item()
-    dg = ((b["grad"] - a["grad"]).abs() / (a["grad"].abs() + 1e-6)).max().item()
-    print(f"split vs fp32 MFMA D={D}: |dprob| {dp:.3g}, max rel dgrad {dg:.3g}")
-    torch.testing.assert_close(b["prob"], a["prob"], rtol=0, atol=5e-7)
-    torch.testing.assert_close(b["loss"], a["loss"], rtol=1e-6, atol=1e-7)
-    for x, y in zip(b["r"], a["r"]):
-        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(b["grad"], a["grad"], rtol=2e-5, atol=1e-7)
-    for k in a["G"]:
-        torch.testing.assert_close(b["G"][k], a["G"][k], rtol=2e-5, atol=1e-8)
+            torch.cuda.synchronize()
+            nu = w.num_unique.cpu().tolist()
+            rec.append(dict(prob=w.prob.cpu().clone(), loss=w.loss.cpu().clone(),
+                            r=[x.cpu().clone() for x in w.r],
+                            grad=m.engine.flat_grad.cpu().clone(),
+                            G={k: v[:nu[0 if k.endswith("user") else 1]].cpu().clone()
+                               for k, v in w.G.items()}))
+        out.append(rec)
+    for s_, (a, b) in enumerate(zip(out[0], out[1])):
+        dp = (b["prob"] - a["prob"]).abs().max().item()
+        dg = (b["grad"] - a["grad"]).abs().max().item()
+        print(f"split vs fp32 MFMA D={D} step {s_}: |dprob| {dp:.3g}, max |dgrad| {dg:.3g}")
+        tight = s_ == 0
+        torch.testing.assert_close(b["prob"], a["prob"], rtol=0, atol=5e-7 if tight else 2e-6)
+        torch.testing.assert_close(b["loss"], a["loss"], rtol=1e-6, atol=1e-7)
+        for x, y in zip(b["r"], a["r"]):
+            torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6 if tight else 1e-4)
+        torch.testing.assert_close(b["grad"], a["grad"], rtol=2e-5 if tight else 1e-4,
+                                   atol=1e-7 if tight else 1e-6)
+        for k in a["G"]:
+            torch.testing.assert_close(b["G"][k], a["G"][k], rtol=2e-5 if tight else 1e-4,
+                                       atol=1e-8 if tight else 1e-6)
 
 
 def test_mlp_tower_eval_matches_unfused(monkeypatch):

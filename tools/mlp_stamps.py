@@ -27,8 +27,13 @@ BWD = ["head bwd", "ln2 bwd", "stage a1", "wgrad2", "lin2 bwd", "ln1 bwd", "stag
 
 
 def main():
+    import ncf_amd.engine as E
     from ncf_amd import _lib
     from ncf_amd.trainer import FusedTrainStep
+    # --fp32: the tower on fp32 MFMA (engine.TOWER_SPLIT off); default: the engine's setting
+    if "--fp32" in sys.argv:
+        E.TOWER_SPLIT = False
+    print(f"tower split operands: {E.TOWER_SPLIT}")
     dev = torch.device("cuda", 0)
     U, I, B, M = 1_000_000, 100_000, 4096, 5
     m = ncf.AdvancedNCF(U, I, 10, 50, 64, 64, 32, [256, 128, 64], 4, 0.2, M - 1).to(dev).train()
