@@ -50,7 +50,8 @@ BF16_MFMA_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity
 KERNEL_SYMBOL = {"ncf_attn_block_fwd": "k_attn_block_fwd", "ncf_attn_block_bwd": "k_attn_block_bwd",
                  "ncf_mlp_fwd": "k_mlp_fwd", "ncf_mlp_bwd": "k_mlp_bwd",
                  "ncf_mlp_fwd_split": "k_mlp_fwd", "ncf_mlp_bwd_split": "k_mlp_bwd",
-                 "ncf_wgrad_grouped": "k_wgrad_grouped"}
+                 "ncf_wgrad_grouped": "k_wgrad_grouped",
+                 "ncf_attn_mlp_fwd": "k_attn_mlp_fwd", "ncf_attn_mlp_bwd": "k_attn_mlp_bwd"}
 # the tower's Linears on bf16 matrix cores through split operands: 6 bf16 products per fp32
 # product (engine.TOWER_SPLIT); their roofline is quoted as fp32-equivalent work against the fp32
 # MFMA peak, with the executed bf16 products against the bf16 peak beside it
@@ -1092,6 +1093,8 @@ def main():
     #   ncf_mlp_bwd         2 x (D h1 + h1 h2 + h2 h3)   (dX of the three Linears), plus the
     #                       same again for their weight gradients when computed inside it
     #   ncf_wgrad_grouped   2 x (D h1 + h1 h2 + h2 h3)   (the MLP weight gradients, unfused path)
+    #   ncf_attn_mlp_fwd / _bwd: the attention block and the tower fused into one launch per
+    #                       direction (tower_fused.hip, D = 64 / M = 5): the sums of the above
     # plus any unfused ncf_gemm_* launch (2 M N K, first three arguments).
     mlp_f = 2.0 * (D * hid[0] + hid[0] * hid[1] + hid[1] * hid[2])
     # (with the weight gradients fused into the tower backward, ncf_mlp_bwd carries dX + dW)
@@ -1099,7 +1102,9 @@ def main():
                   "ncf_mlp_fwd": mlp_f, "ncf_mlp_fwd_split": mlp_f,
                   "ncf_mlp_bwd": mlp_f if "ncf_wgrad_grouped" in totals else 2.0 * mlp_f,
                   "ncf_mlp_bwd_split": 2.0 * mlp_f,
-                  "ncf_wgrad_grouped": mlp_f}
+                  "ncf_wgrad_grouped": mlp_f,
+                  "ncf_attn_mlp_fwd": 8.0 * D * D + mlp_f,
+                  "ncf_attn_mlp_bwd": 16.0 * D * D + 2.0 * mlp_f}
     gemm_names = ("ncf_gemm_direct", "ncf_gemm_f32", "ncf_gemm_rows", "ncf_gemm_f32_splitk")
     mfma = {}
     for k, f in per_sample.items():
@@ -1336,7 +1341,9 @@ def main():
                             if dom in SPLIT_NAMES else {}),
                          **({"overlap": "measured in the step, beside the rolling table sweep "
                                         "on a side stream", "isolated": iso} if iso else {})},
-            "mfma_class": {"kernels": "k_attn_block_fwd/bwd + k_mlp_fwd/bwd + k_wgrad_grouped "
+            "mfma_class": {"kernels": "k_attn_mlp_fwd/bwd (the attention block and the tower "
+                                      "fused, D = 64) or k_attn_block_fwd/bwd + k_mlp_fwd/bwd, + "
+                                      "k_wgrad_grouped when unfused "
                                       "(every Linear of the step: fp32 MFMA "
                                       "v_mfma_f32_16x16x4_f32, the tower on split-operand bf16 "
                                       "MFMA when the *_split entry points run; fp32-equivalent "

@@ -359,6 +359,38 @@ int ncf_mlp_bwd_split(const float* grad_a_last, int64_t n, int64_t dim, const fl
                       const ncf_head_args* head, float* grad_x, float* workspace,
                       int64_t workspace_floats, ncf_reduce_list* defer, void* stream);
 
+/* a5 + a7 + a8 forward fused (C2 training geometry: D = 64, groups of M = 5 rows, hidden
+ * [256,128,64]): ncf_attn_block_fwd (training stash q/k/v/probs, no o) then ncf_mlp_fwd on its
+ * output y in ONE launch, the attention output handed to the tower in LDS (y still written for
+ * the backward's layer-0 weight gradient).  tower_mode: 0 fp32 MFMA, 1 bf16, 3 split operands.
+ * Same results as the two launches.                                                           */
+int ncf_attn_mlp_fused_supported(int64_t dim, int64_t heads, int64_t group_len, int64_t n_layers,
+                                 const int64_t* hidden);
+int ncf_attn_mlp_fwd(const float* xu, const float* xi, int64_t groups, int64_t heads,
+                     const float* wq, const float* bq, const float* wk, const float* bk,
+                     const float* wv, const float* bv, const float* wo, const float* bo,
+                     float dropout_p, uint64_t seed, const ncf_step_clock* clock, float* q,
+                     float* k, float* v, float* probs, float* y, const int64_t* user_ids,
+                     const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
+                     float eps, const float* mlp_out_w, const float* mlp_out_b,
+                     const float* mf_pred, const float* final_w, const float* final_b,
+                     float* mlp_pred, float* prob, int32_t tower_mode, void* stream);
+/* ... and the backward: ncf_mlp_bwd (head fused, weight gradients fused, x = y) then
+ * ncf_attn_block_bwd on its input gradient in ONE launch, that gradient handed over in LDS
+ * (never written to HBM).  The tower's partials in tower_workspace (ncf_mlp_bwd_workspace(n)),
+ * the attention's in attn_workspace (ncf_attn_block_bwd_workspace(groups)); both deferred into
+ * `defer` (required).  Same results as the two launches.                                       */
+int ncf_attn_mlp_bwd(int64_t groups, int64_t heads, const float* y, const ncf_mlp_layer* layers,
+                     int64_t n_layers, const int64_t* hidden, float dropout_p, uint64_t seed,
+                     const ncf_step_clock* clock, const ncf_head_args* head,
+                     float* tower_workspace, int64_t tower_workspace_floats, const float* q,
+                     const float* k, const float* v, const float* probs, const float* wq,
+                     const float* wk, const float* wv, const float* wo, const float* xu,
+                     const float* xi, float* const* attn_grad_params, float* attn_workspace,
+                     int64_t attn_workspace_floats, float* grad_xu, float* grad_xi,
+                     const int64_t* user_ids, ncf_reduce_list* defer, int32_t tower_mode,
+                     void* stream);
+
 /* ---- 8f rank 1: device-side training batches (data_prep.py:95-161, 181-313) --------------
  * ncf_alias_build (HOST function, once per dataset): Walker/Vose alias table of the
  *   inverse-popularity weights.
@@ -725,8 +757,19 @@ int ncf_adam_pairs_catchup_clock(const ncf_table_pair* pairs, int npairs, int64_
                                  double beta1, double beta2, double eps, double weight_decay,
                                  void* stream);
 /* Stamps at or above NCF_STAMP_LOCK (0x40000000) compare above any target: the catch-up kernels
- * leave such rows alone (reserved; no entry point sets it). */
+ * leave such rows alone.  ncf_adam_pairs_catchup_lock_clock with lock = 1 sets it on the listed
+ * rows (caught up through the target, their gradient step of this step still to come; the
+ * apply writes the plain stamp back); with lock = 0 and target_rel = 1 it is the early catch-up
+ * of the NEXT batch's rows through the step now running, on a side stream beside its backward
+ * (rows of this step's batch are locked and skipped).  The reference's Adam.step over every row
+ * (src/model/trainer.py:285) gives the same values: the skipped step of an unlisted row is a
+ * zero-gradient one. */
 #define NCF_STAMP_LOCK 0x40000000
+int ncf_adam_pairs_catchup_lock_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
+                                      const uint32_t* count, int64_t max_n, int32_t target_rel,
+                                      int32_t lock, const ncf_step_clock* clock,
+                                      const float* step_table, double beta1, double beta2,
+                                      double eps, double weight_decay, void* stream);
 /* The catch-up of the rows named by RAW id lists (ids0 for pairs[0], ids1 for pairs[1], n
  * occurrences each, duplicates allowed): the first occurrence of a row to raise its stamp to the
  * target (atomicMax) replays it, the others skip: the same rows, bit-identical, with no dedup

@@ -64,6 +64,11 @@ SIGNATURES = {
     "ncf_attention_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P, P, P]),
     "ncf_attn_block_supported": (I32, [I64, I64, I64]),
     "ncf_mlp_fused_supported": (I32, [I64, I64, P]),
+    "ncf_attn_mlp_fused_supported": (I32, [I64, I64, I64, I64, P]),
+    "ncf_attn_mlp_fwd": (I32, [P, P, I64, I64, P, P, P, P, P, P, P, P, F32, U64, P, P, P, P, P, P,
+                               P, P, I64, P, F32, P, P, P, P, P, P, P, I32, P]),
+    "ncf_attn_mlp_bwd": (I32, [I64, I64, P, P, I64, P, F32, U64, P, P, P, I64, P, P, P, P, P, P,
+                               P, P, P, P, P, P, I64, P, P, P, P, I32, P]),
     "ncf_alias_build": (I32, [P, I64, P, P]),
     "ncf_group_metrics_workspace": (I64, [I64, I64]),
     "ncf_group_metrics": (I32, [P, P, I64, I64, P, I64, F32, P, P, I64, P]),
@@ -135,6 +140,8 @@ SIGNATURES = {
     "ncf_adam_sweep_rolling": (I32, [P, P, P, P, P, P, I64, I64, I32, I64, P, I32, P, P, F64, F64,
                                      F64, F64, P]),
     "ncf_adam_pairs_catchup_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
+    "ncf_adam_pairs_catchup_lock_clock": (I32, [P, I32, I64, P, I64, I32, I32, P, P, F64, F64, F64,
+                                                F64, P]),
     "ncf_adam_pairs_catchup_claim_clock": (I32, [P, I32, I64, P, P, I64, I32, P, P, F64, F64, F64,
                                                  F64, P]),
     "ncf_adam_pairs_apply_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),

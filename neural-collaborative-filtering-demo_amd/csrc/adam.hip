@@ -469,14 +469,20 @@ __global__ __launch_bounds__(256) void k_pairs_apply(const PairArgs a, const uin
   const int64_t row = a.ids[k][c];
   const int64_t o = row * D + sub * 4;
   const float ns = table[4 * step], bc = table[4 * step + 1];
-  float4 p0 = ldp4<BF>(t.p0, o), m0 = ld4(t.m0 + o), v0 = ld4(t.v0 + o);
-  adam4(p0, m0, v0, ld4(t.G0 + c * D + sub * 4), ns, bc, s);
-  stp4<BF>(t.p0, o, p0); st4(t.m0 + o, m0); st4(t.v0 + o, v0);
-  if (t.p1) {
-    float4 p1 = ldp4<BF>(t.p1, o), m1 = ld4(t.m1 + o), v1 = ld4(t.v1 + o);
-    adam4(p1, m1, v1, ld4(t.G1 + c * D + sub * 4), ns, bc, s);
-    stp4<BF>(t.p1, o, p1); st4(t.m1 + o, m1); st4(t.v1 + o, v1);
+  // every load of both tables before any store: the compiler cannot know the two tables' rows
+  // do not alias, and in program order the second table's loads would wait for the first
+  // one's stores (two dependent HBM round trips per row instead of one)
+  const bool two = t.p1 != nullptr;
+  const int64_t og = c * D + sub * 4;
+  float4 p0 = ldp4<BF>(t.p0, o), m0 = ld4(t.m0 + o), v0 = ld4(t.v0 + o), g0 = ld4(t.G0 + og);
+  float4 p1 = {0.f, 0.f, 0.f, 0.f}, m1 = p1, v1 = p1, g1 = p1;
+  if (two) {
+    p1 = ldp4<BF>(t.p1, o); m1 = ld4(t.m1 + o); v1 = ld4(t.v1 + o); g1 = ld4(t.G1 + og);
   }
+  adam4(p0, m0, v0, g0, ns, bc, s);
+  if (two) adam4(p1, m1, v1, g1, ns, bc, s);
+  stp4<BF>(t.p0, o, p0); st4(t.m0 + o, m0); st4(t.v0 + o, v0);
+  if (two) { stp4<BF>(t.p1, o, p1); st4(t.m1 + o, m1); st4(t.v1 + o, v1); }
   if (sub == 0) a.stamp[k][row] = step;
 }
 
@@ -959,6 +965,27 @@ extern "C" int ncf_adam_pairs_catchup_clock(const ncf_table_pair* pairs, int npa
   NCF_DISPATCH_DIM(dim, pairs_catchup_d, pair_args(pairs, npairs), npairs, count, max_n,
                    target_rel, clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
                    (hipStream_t)stream);
+}
+
+// lock = 1: every listed row is also marked in flight (stamp = target | NCF_STAMP_LOCK) until the
+// step's apply writes its plain stamp: a catch-up of OTHER rows running meanwhile (the next
+// batch's, ahead of time on a side stream) leaves this step's rows alone.  target_rel = 1 with
+// lock = 0 is that early catch-up: rows current through the step now running, whose gradient
+// step is a zero-gradient one because they are not in its batch (locked rows skipped).
+extern "C" int ncf_adam_pairs_catchup_lock_clock(const ncf_table_pair* pairs, int npairs,
+                                                 int64_t dim, const uint32_t* count,
+                                                 int64_t max_n, int32_t target_rel, int32_t lock,
+                                                 const ncf_step_clock* clock,
+                                                 const float* step_table, double beta1,
+                                                 double beta2, double eps, double weight_decay,
+                                                 void* stream) {
+  NCF_CHECK_ARG(pairs && npairs >= 1 && npairs <= 2 && count && clock && step_table &&
+                    (lock == 0 || lock == 1),
+                "ncf_adam_pairs_catchup_lock_clock: bad args");
+  if (max_n <= 0) return NCF_OK;
+  NCF_DISPATCH_DIM(dim, pairs_catchup_d, pair_args(pairs, npairs), npairs, count, max_n,
+                   target_rel, clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
+                   (hipStream_t)stream, lock);
 }
 
 template <int D>

@@ -39,6 +39,15 @@ _SERIAL = itertools.count(1)      # distinguishes schedules in workspace caches 
 # scalars of up to 8 steps past their target (replay_uniform's prefetch, csrc/adam.hip), so the
 # pad must stay >= 16; tests shrink it to force table growth under a captured graph.
 SCALAR_PAD = 4096
+# Early catch-up: with the next batch sorted a step ahead (FusedTrainStep's
+# next=), its rows that this step's batch does not touch are caught up through this step on the
+# side stream, behind the rolling sweep and beside the backward; this step's own rows are locked
+# by its catch-up (NCF_STAMP_LOCK) and skipped.  The next step's catch-up then finds its rows
+# current.  Same replays, bit-identical (tested).  Off: measured slower at C2 (round 5,
+# tools/step_ab.py, 3 interleaved runs each: 0.2942-0.2957 ms/step without, 0.3004 with, the
+# replay beside the backward slows it more than it saves on the critical path; round 3 found
+# the same for three placements of it)
+EARLY_CATCHUP = False
 
 
 class DeferredTableAdam:
@@ -91,12 +100,25 @@ class DeferredTableAdam:
         # to ~96 us, both off the critical path's sum).
         # Several comma-separated fork points split the slice into that many consecutive row
         # ranges, one launched at each (ncf_adam_pairs_sweep_rolling_part).
-        self.fork_points = os.environ.get("NCF_SWEEP_FORK", "mlp_bwd").split(",")
+        # Default: "tower" when the step runs the attention block and the tower fused
+        # (tower_fused.hip: the sweep beside the fused forward and backward; round 5, 3
+        # interleaved runs each: 0.2879-0.2908 ms/step, forked at mlp_bwd 0.3056-0.3074, the
+        # unfused step 0.2972-0.3006), else "mlp_bwd" (unfused at "tower": 0.3107-0.3119).
+        env = os.environ.get("NCF_SWEEP_FORK")
+        self.fork_points = env.split(",") if env else [self._default_fork(engine)]
         self._owed = []           # parts of a closed step's rolling sweep not launched yet
         self._side = None
         self._ev = None
         self._joined = True
         engine.deferred = self
+
+    @staticmethod
+    def _default_fork(engine):
+        m = engine.model
+        D, H, M = m.mlp_embedding_dim, m.num_heads, 1 + m.negative_samples
+        fused = (m.mf_embedding_dim == D and
+                 engine.attn_tower_step(D, H, M, list(m.mlp_hidden_dims)))
+        return "tower" if fused else "mlp_bwd"
 
     # ---- per-step scalar table (index 4s .. 4s+3 = step s: gradient-step and zero-gradient-step
     #      scalars, ncf_adam_step_scalars)
@@ -347,9 +369,12 @@ class DeferredTableAdam:
         if self.clock is not None and n > 0:   # both kinds in one launch
             self._ensure(self.t + 1)
             pairs = self._pairs_for(w)
-            _lib.call("ncf_adam_pairs_catchup_clock", ctypes.addressof(pairs), 2,
-                      m.mlp_embedding_dim, ptr(w.num_unique), n, 0, ptr(self.clock),
+            # (locked: an early catch-up of the next batch may run during this step)
+            lock = 1 if EARLY_CATCHUP else 0
+            _lib.call("ncf_adam_pairs_catchup_lock_clock", ctypes.addressof(pairs), 2,
+                      m.mlp_embedding_dim, ptr(w.num_unique), n, 0, lock, ptr(self.clock),
                       ptr(self._table), *self._consts(), st)
+            self._locked = bool(lock)
             return
         self.catchup_rows("user", w.uniq_u, w.num_unique, 0, n, st)
         self.catchup_rows("item", w.uniq_i, w.num_unique, 1, n, st)
@@ -365,6 +390,7 @@ class DeferredTableAdam:
         n = w.g.n
         self._ensure(self.t + 1)
         pairs = self._pairs_for(w)
+        self._locked = False          # (no early catch-up during a claim-path step)
         _lib.call("ncf_adam_pairs_catchup_claim_clock", ctypes.addressof(pairs), 2,
                   m.mlp_embedding_dim, ptr(uid), ptr(iid), n, 0, ptr(self.clock),
                   ptr(self._table), *self._consts(), st)
@@ -397,6 +423,29 @@ class DeferredTableAdam:
                   w.emb_ws.numel(), side.cuda_stream)
         self._dedup_evs[1].record(side.cuda_stream)
         w.dedup_ev = self._dedup_evs[1]
+
+    def early_catchup(self, rows, n, stream):
+        """The next batch's unique rows (``rows``: a dedup set's uniq_u / uniq_i / num_unique)
+        caught up through the step now running, on `stream` (ordered after their sort and
+        joined before this step's apply).  Only when this step's catch-up locked its own rows;
+        returns whether it was queued."""
+        if not (EARLY_CATCHUP and self.clock is not None and getattr(self, "_locked", False)
+                and n > 0):
+            return False
+        self._ensure(self.t + 2)
+        cache = self.__dict__.setdefault("_early_pairs", {})
+        key = (getattr(self, "_gen", 0), rows["uniq_u"].data_ptr(), rows["uniq_i"].data_ptr())
+        pairs = cache.get(key)
+        if pairs is None:
+            if len(cache) > 8:
+                cache.clear()
+            pairs = cache[key] = self._pairs()
+            for k, ids in enumerate((rows["uniq_u"], rows["uniq_i"])):
+                pairs[k].row_ids = ptr(ids)
+        _lib.call("ncf_adam_pairs_catchup_lock_clock", ctypes.addressof(pairs), 2,
+                  self.engine.model.mlp_embedding_dim, ptr(rows["num_unique"]), n, 1, 0,
+                  ptr(self.clock), ptr(self._table), *self._consts(), stream)
+        return True
 
     # ---- after the backward: this step's gradient on the touched rows
     def apply(self, w, st):

@@ -34,6 +34,13 @@ BF16_MM = True
 # instead of 2.4e-6: outside the full-size bound against the fp32 oracle (tests/
 # test_gpu_fullsize.py).  Off: the headline keeps the fp32 oracle's trajectory.
 TOWER_SPLIT = False
+# C2 training geometry (D = 64, M = 5: the attention workgroup's 16 groups = the tower's 80-row
+# tile): the attention block and the MLP tower as ONE launch per direction (tower_fused.hip,
+# ncf_attn_mlp_fwd / ncf_attn_mlp_bwd; the same device code and bits as the two launches each
+# way).  Measured at C2 (tools/step_ab.py, 3 interleaved runs each, ms/step): fused with the
+# rolling sweep forked before it 0.2879-0.2908, two launches each way 0.2972-0.3006 (isolated:
+# forward 57 against 22 + 42 us, backward 105-109 against 37 + 85 us).  False: two launches.
+FUSE_ATTN_TOWER = True
 # SURVEY fact 6 (a training group's M rows hold one user): the gather writes the LN'd user rows
 # once per group (group_rows = M) when every reader takes the group's row — the fused attention
 # block and the fused tower's head backward (False: every row; the same bits, tested; measured
@@ -462,6 +469,24 @@ class NCFEngine:
                       ptr(w.mf_pred), ptr(w.xu), ptr(w.xi), ptr(w.umf), ptr(w.imf), ptr(w.err), st)
         # a5: MultiHeadAttention over each group of M rows (architecture.py:315-326)
         att = m.user_product_attention
+        if train and temporal is None and self.attn_tower_step(D, H, M, hid):
+            # a5 + a7 + a8 in one launch (tower_fused.hip): the attention block, then the tower
+            # and head on its output tile in LDS
+            self._sweep_fork("tower")
+            _, addr, _, haddr = self._mlp_layers(w, train, bwd=False)
+            mode = {"ncf_mlp_fwd": 0, "ncf_mlp_fwd_bf16": 1,
+                    "ncf_mlp_fwd_split": 3}[self._tower_entry("ncf_mlp_fwd", bf16)]
+            a_ = "user_product_attention."
+            _lib.call("ncf_attn_mlp_fwd", ptr(w.xu), ptr(w.xi), n // M, H,
+                      pp[a_ + "q_proj.weight"], pp[a_ + "q_proj.bias"], pp[a_ + "k_proj.weight"],
+                      pp[a_ + "k_proj.bias"], pp[a_ + "v_proj.weight"], pp[a_ + "v_proj.bias"],
+                      pp[a_ + "out_proj.weight"], pp[a_ + "out_proj.bias"], drop_p, seed,
+                      ptr(self.clock), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P), ptr(w.y),
+                      ptr(uid) if ATTN_SHARE_Q else None, addr, len(hid), haddr, LN_EPS,
+                      pp["mlp_output.weight"], pp["mlp_output.bias"], ptr(w.mf_pred),
+                      pp["final.0.weight"], pp["final.0.bias"], ptr(w.mlp_pred), ptr(w.prob),
+                      mode, st)
+            return w
         if temporal is None and self.attn_block(D, H, M):
             # projections + core + out_proj in one launch (attn_block.hip)
             # training: nothing stashed when the backward recomputes q/k/v/P/o (attn_rc)
@@ -567,6 +592,27 @@ class NCFEngine:
         if ok is None:
             ok = self._mlp_ok[key] = bool(_lib.query("ncf_attn_block_supported", D, H, M))
         return ok
+
+    def attn_mlp_fused(self, D: int, H: int, M: int, hid) -> bool:
+        """Whether the one-launch attention block + tower forward (tower_fused.hip) covers this
+        geometry (D = 64, M = 5, [256, 128, 64]) and is switched on (FUSE_ATTN_TOWER)."""
+        if not FUSE_ATTN_TOWER:
+            return False
+        key = ("attn_mlp", D, H, M, tuple(hid))
+        ok = self._mlp_ok.get(key)
+        if ok is None:
+            harr = (ctypes.c_int64 * len(hid))(*hid)
+            ok = self._mlp_ok[key] = bool(_lib.query("ncf_attn_mlp_fused_supported", D, H, M,
+                                                      len(hid), ctypes.addressof(harr)))
+        return ok
+
+    def attn_tower_step(self, D: int, H: int, M: int, hid) -> bool:
+        """Whether a training step of this geometry runs the attention block and the tower as
+        one launch per direction (tower_fused.hip): the fused attention block with its stash,
+        the fused tower with its weight gradients, and the fused kernels' geometry."""
+        return (self.attn_block(D, H, M) and self.mlp_fused(D, hid) and self.mlp_fused_wgrad()
+                and not self.attn_rc(D, H, M) and not _STASH_O
+                and self.attn_mlp_fused(D, H, M, hid))
 
     @staticmethod
     def _tower_entry(base: str, bf16: bool) -> str:
@@ -681,6 +727,28 @@ class NCFEngine:
         if hook is not None:
             hook(at)
 
+    def _zero_temporal_cols(self, m, hid, D, st):
+        """Gradient columns of mlp.0 that see the all-zero temporal input: exactly 0, and no
+        kernel ever writes them — zeroed once per gradient buffer."""
+        if self._zero_cols_of is self.flat_grad:
+            return
+        ldw = m.mlp[0].weight.shape[1]
+        if ldw > D:
+            _lib.call("ncf_fill_2d", ptr(self.grad_view("mlp.0.weight")[:, D:]), hid[0], ldw - D,
+                      ldw, 0.0, st)
+        self._zero_cols_of = self.flat_grad
+
+    def _attn_grad_ptrs(self, w):
+        """Address of the 8 attention parameter-gradient pointers (q/k/v/out weight, bias)."""
+        gp = w.cache.get("attn_grads")
+        if gp is None:
+            names = [f"user_product_attention.{nm}.{t}" for nm in ("q_proj", "k_proj", "v_proj",
+                                                                    "out_proj")
+                     for t in ("weight", "bias")]
+            arr = (ctypes.c_void_p * 8)(*[ptr(self.grad_view(x)) for x in names])
+            gp = w.cache["attn_grads"] = (arr, ctypes.addressof(arr))
+        return gp[1]
+
     def backward(self, w: Workspace, uid, iid, grad_prob: Optional[torch.Tensor],
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,
                  loss_denominator: float = 0.0, tables=None, rows=None, uniq=None,
@@ -733,21 +801,34 @@ class NCFEngine:
             h.loss_denominator = float(loss_denominator)
             # (the gather's source rows of the LN'd user rows: ncf_head_args.user_ids)
             h.user_ids, h.group_rows = ptr(uid), getattr(w, "group_rows", 0)
+        fused_all = fused and self.mlp_fused_wgrad()
+        pp = self.pp()
+        fused_ta = fused_all and self.attn_tower_step(D, H, M, hid)
+        if fused_ta:
+            # tower + head backward, then the attention backward on the tower's input gradient
+            # in LDS, in one launch (tower_fused.hip); the forward's stash q/k/v/P either way
+            self._zero_temporal_cols(m, hid, D, st)
+            mode = {"ncf_mlp_bwd": 0, "ncf_mlp_bwd_bf16": 1,
+                    "ncf_mlp_bwd_split": 3}[self._tower_entry("ncf_mlp_bwd", bf16)]
+            gpa = self._attn_grad_ptrs(w)
+            ws = w.site("attn")
+            _lib.call("ncf_attn_mlp_bwd", n // M, H, ptr(w.y), addr, len(hid), haddr, drop_p,
+                      seed, ptr(self.clock), ctypes.addressof(h), ptr(w.site("mlp")),
+                      w.site("mlp").numel(), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P),
+                      *pp["att_w"], ptr(w.xu), ptr(w.xi), gpa, ptr(ws), ws.numel(),
+                      ptr(w.dxu), ptr(w.dxi), ptr(uid) if ATTN_SHARE_Q else None,
+                      w.red_list.address, mode, st)
+            self._sweep_fork("mlp_bwd_after")
+            self._sweep_fork("attn_bwd", w)
+        elif fused:
             _lib.call(self._tower_entry("ncf_mlp_bwd", bf16), None, n, D,
                       ptr(w.y), addr,
                       len(hid), haddr, drop_p, seed,
                       ptr(self.clock), ctypes.addressof(h), ptr(w.dy), ptr(w.site("mlp")),
                       w.site("mlp").numel(), w.red_list.address, st)
             self._sweep_fork("mlp_bwd_after")     # (a fork point right behind the tower backward)
-        fused_all = fused and self.mlp_fused_wgrad()
-        if fused_all and self._zero_cols_of is not self.flat_grad:
-            # gradient columns of mlp.0 that see the all-zero temporal input: exactly 0, and no
-            # kernel ever writes them — zero once per gradient buffer
-            ldw = m.mlp[0].weight.shape[1]
-            if ldw > D:
-                _lib.call("ncf_fill_2d", ptr(gv("mlp.0.weight")[:, D:]), hid[0], ldw - D, ldw,
-                          0.0, st)
-            self._zero_cols_of = self.flat_grad
+        elif fused_all:
+            self._zero_temporal_cols(m, hid, D, st)
         for l in (() if fused_all else reversed(range(len(hid)))):
             h = hid[l]
             lin, ln = m.mlp[4 * l], m.mlp[4 * l + 2]
@@ -777,33 +858,29 @@ class NCFEngine:
                 dx = w.dy if l == 0 else w.da[l - 1]
                 self._gemm(w.dlin[l], h, 0, lin.weight, ldw, 0, dx, kin, n, kin, h, st=st)
         # a5 backward: out_proj, core, q/k/v projections
-        self._sweep_fork("attn_bwd", w)
-        pp = self.pp()
-        if self.attn_block(D, H, M):
+        if fused_ta:
+            pass     # (in the fused launch above)
+        elif self.attn_block(D, H, M):
+            self._sweep_fork("attn_bwd", w)
             # core + projections backward and the four Linear gradients in one launch
-            gp = w.cache.get("attn_grads")
-            if gp is None:
-                names = [f"user_product_attention.{nm}.{t}" for nm in ("q_proj", "k_proj", "v_proj",
-                                                                        "out_proj")
-                         for t in ("weight", "bias")]
-                arr = (ctypes.c_void_p * 8)(*[ptr(gv(x)) for x in names])
-                gp = w.cache["attn_grads"] = (arr, ctypes.addressof(arr))
+            gpa = self._attn_grad_ptrs(w)
             ws = w.site("attn")
             if self.attn_rc(D, H, M):
                 wq, wk, wv, wo = pp["att_w"]
                 bq, bk, bv = pp["att_b"]
                 _lib.call("ncf_attn_block_bwd_rc", ptr(w.dy), ptr(w.xu), ptr(w.xi), n // M, M, H, D,
-                          wq, bq, wk, bk, wv, bv, wo, drop_p, seed, ptr(self.clock), gp[1],
+                          wq, bq, wk, bk, wv, bv, wo, drop_p, seed, ptr(self.clock), gpa,
                           ptr(ws), ws.numel(), w.red_list.address, ptr(w.dxu), ptr(w.dxi),
                           ptr(uid) if ATTN_SHARE_Q else None, st)
             else:
                 _lib.call("ncf_attn_block_bwd", ptr(w.dy), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P),
                           n // M, M, H, D, *pp["att_w"], drop_p, seed,
                           ptr(self.clock), ptr(w.o) if _STASH_O else None, ptr(w.xu), ptr(w.xi),
-                          gp[1], ptr(ws),
+                          gpa, ptr(ws),
                           ws.numel(), w.red_list.address, None, None, None, ptr(w.dxu),
                           ptr(w.dxi), ptr(uid) if ATTN_SHARE_Q else None, st)
         else:
+            self._sweep_fork("attn_bwd", w)
             self._attention_bwd_unfused(w, drop_p, seed, joins, st)
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)
         self._sweep_fork("emb_bwd", w)

@@ -205,6 +205,8 @@ class FusedTrainStep:
         m = self.model
         if side is not None:
             self._enqueue_dedup(s, w, uid, iid, side)
+            # its rows this step does not touch caught up through this step behind the sort
+            self.deferred.early_catchup(s, uid.numel(), side.cuda_stream)
             # the sweep's done-event re-recorded behind the sort: the step's sweep join (before
             # the clock advance) then orders the sort too, and the next step waits for nothing
             d = self.deferred

@@ -502,21 +502,27 @@ def test_non_adam_optimizer_gets_dense_table_grads(f2):
 
 # ----------------------------------------------------------------------------- deferred Adam
 def _fused_run(deferred, steps, sweep_every=64, U=3000, I=500, B=64, seed=11, dropout=0.0,
-               lr_at=None, on_step=None, **kw):
+               lr_at=None, on_step=None, pipelined=False, **kw):
+    """``pipelined``: every step is told the next batch (FusedTrainStep(next=...): the id sort
+    and the early catch-up of the next batch's rows run a step ahead on the side stream)."""
     from ncf_amd.trainer import FusedTrainStep
     torch.manual_seed(seed)
     m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, dropout, 4).to(DEV)
     step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5, deferred=deferred, sweep_every=sweep_every,
                           **kw)
     g = torch.Generator().manual_seed(seed + 1)
+    batches = []
     for s in range(steps):
         u = torch.randint(0, U, (B,), generator=g).repeat_interleave(5).to(DEV)
         i = torch.randint(0, I, (B * 5,), generator=g).to(DEV)
         t = torch.zeros(B, 5)
         t[:, 0] = 1
+        batches.append((u, i, t.reshape(-1, 1).to(DEV)))
+    for s, (u, i, t) in enumerate(batches):
         if lr_at and s in lr_at:
             step.lr = lr_at[s]          # (a scheduler's change between steps)
-        step(u, i, t.reshape(-1, 1).to(DEV))
+        nxt = batches[s + 1][:2] if pipelined and s + 1 < steps else None
+        step(u, i, t, next=nxt)
         if on_step is not None:
             on_step(step, s)
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}   # syncs deferred rows
@@ -740,6 +746,51 @@ def test_mlp_tower_split_matches_fp32_mfma(monkeypatch, D):
                                        atol=1e-8 if tight else 1e-6)
 
 
+@pytest.mark.parametrize("tables", ["fp32", "bf16"])
+def test_attn_tower_fused_bitwise_equals_two_launches(monkeypatch, tables):
+    """The attention block and the MLP tower as one launch per direction (tower_fused.hip:
+    ncf_attn_mlp_fwd hands the attention's output to the tower in LDS, ncf_attn_mlp_bwd the
+    tower's input gradient to the attention backward) against the two launches each way
+    (ncf_attn_block_fwd -> y -> ncf_mlp_fwd; ncf_mlp_bwd -> dy -> ncf_attn_block_bwd): the same
+    device code, so the same bits — probabilities, parameters and Adam moments over 6 training
+    steps with dropout and a ragged last workgroup (B = 61 groups), and with bf16 tables
+    (single-term bf16 tower)."""
+    import ncf_amd.engine as E
+    from ncf_amd.trainer import FusedTrainStep
+    U, I, B, M = 3000, 500, 61, 5
+    g = torch.Generator().manual_seed(81)
+    batches = []
+    for _ in range(6):
+        u = torch.randint(0, U, (B,), generator=g).repeat_interleave(M)
+        i = torch.randint(0, I, (B * M,), generator=g)
+        t = torch.zeros(B, M)
+        t[:, 0] = 1
+        batches.append((u.to(DEV), i.to(DEV), t.reshape(-1, 1).to(DEV)))
+    out = []
+    for fused in (True, False):
+        monkeypatch.setattr(E, "FUSE_ATTN_TOWER", fused)
+        torch.manual_seed(82)
+        m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.2, M - 1).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5,
+                              table_dtype=torch.bfloat16 if tables == "bf16" else torch.float32)
+        assert m.engine.attn_mlp_fused(64, 4, M, [256, 128, 64]) == fused
+        probs = []
+        for u, i, t in batches:
+            w = step(u, i, t)
+            probs.append(w.prob.cpu().clone())
+        step.sync()
+        out.append((probs, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()},
+                    {k: (v["exp_avg"].cpu().clone(), v["exp_avg_sq"].cpu().clone())
+                     for k, v in step.state.items()}))
+    (pa, sa, ma), (pb, sb, mb) = out
+    for x, y in zip(pa, pb):
+        assert torch.equal(x, y)
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+    for k in ma:
+        assert torch.equal(ma[k][0], mb[k][0]) and torch.equal(ma[k][1], mb[k][1]), k
+
+
 def test_mlp_tower_eval_matches_unfused(monkeypatch):
     res = []
     for flag in ("0", "1"):
@@ -784,6 +835,42 @@ def test_clock_mode_bitwise_equals_dense():
     still bit-identical to the dense sweep."""
     a_sd, a_m = _fused_run(False, 70)
     b_sd, b_m = _fused_run(True, 70, clock=True)
+    for k in a_sd:
+        assert torch.equal(a_sd[k], b_sd[k]), k
+    for k in a_m:
+        assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
+
+
+@pytest.mark.parametrize("tables", ["fp32", "bf16"])
+def test_early_catchup_bitwise_equals_dense(monkeypatch, tables):
+    """The next batch's rows caught up a step ahead on the side stream (deferred.EARLY_CATCHUP:
+    this step's rows locked by its catch-up, NCF_STAMP_LOCK, and skipped) against the dense
+    sweep, bit for bit, parameters and both moments, over 40 steps of heavily overlapping
+    batches (400 users, 150 items: most rows of a batch are in the previous one too) with a
+    rolling sweep every 4 steps crossing the locked rows; the early catch-up must have run on
+    every step but the last.  bf16 tables: against the same pipelined schedule without the
+    early catch-up (the dense bf16 sweep leaves the fp32 parameter copies stale)."""
+    import ncf_amd.deferred as Dm
+    ran = []
+    orig = Dm.DeferredTableAdam.early_catchup
+
+    def count(self, *a):
+        r = orig(self, *a)
+        ran.append(r)
+        return r
+    monkeypatch.setattr(Dm.DeferredTableAdam, "early_catchup", count)
+    dt = torch.bfloat16 if tables == "bf16" else torch.float32
+    kw = dict(sweep_every=4, U=400, I=150, pipelined=True, clock=True, overlap_sweep=True,
+              table_dtype=dt)
+    if tables == "bf16":
+        monkeypatch.setattr(Dm, "EARLY_CATCHUP", False)
+        a_sd, a_m = _fused_run(True, 40, **kw)
+        assert not any(ran)
+        monkeypatch.setattr(Dm, "EARLY_CATCHUP", True)
+    else:
+        a_sd, a_m = _fused_run(False, 40, U=400, I=150)
+    b_sd, b_m = _fused_run(True, 40, **kw)
+    assert sum(ran) >= 38, ran
     for k in a_sd:
         assert torch.equal(a_sd[k], b_sd[k]), k
     for k in a_m:

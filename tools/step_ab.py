@@ -1,0 +1,108 @@
+"""C2 step time (the bench's training step: FusedTrainStep with next=, overlapped sweep, 256
+resident Zipf batches) under module-constant variants, interleaved in one process so the box's
+drift hits every variant alike (GPU only).
+    python tools/step_ab.py [--steps 200] [--reps 3] VARIANT [VARIANT ...]
+VARIANT: name=module.CONST:value[,module.CONST:value][,sweep:N][,env:NAME:value]  e.g.
+    base=engine.FUSE_ATTN_TOWER:1  nofuse=engine.FUSE_ATTN_TOWER:0  noearly=deferred.EARLY_CATCHUP:0
+Per variant: ms/step of each repetition and the per-entry-point ms/step of one profiled run."""
+import argparse
+import importlib
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _ncf_pkg  # noqa: E402
+import bench  # noqa: E402
+
+ncf = _ncf_pkg.load()
+from ncf_amd import _lib  # noqa: E402
+from ncf_amd.trainer import FusedTrainStep  # noqa: E402
+
+
+def parse(spec):
+    """-> (name, [(module, const, value)], FusedTrainStep kwargs); ``sweep:N`` sets sweep_every."""
+    name, _, body = spec.partition("=")
+    sets, kw = [], {}
+    for item in filter(None, body.split(",")):
+        path, _, val = item.partition(":")
+        if path == "sweep":
+            kw["sweep_every"] = int(val)
+            continue
+        if path == "env":     # env:NAME:value ('+' for ',' inside the value)
+            k, _, v = val.partition(":")
+            kw.setdefault("_env", {})[k] = v.replace("+", ",")
+            continue
+        mod, _, const = path.rpartition(".")
+        m = importlib.import_module("ncf_amd." + mod)
+        old = getattr(m, const)
+        sets.append((m, const, type(old)(int(val)) if isinstance(old, (bool, int)) else type(old)(val)))
+    return name, sets, kw
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("variants", nargs="+")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    U, I, D, B, M = 1_000_000, 100_000, 64, 4096, 5
+    batches = bench.make_batches(U, I, B, M, 256, dev, seed=3)
+    variants = [parse(v) for v in args.variants]
+    defaults = {(m, c): getattr(m, c) for _, sets, _ in variants for m, c, _ in sets}
+    res = {name: [] for name, _, _ in variants}
+    prof = {}
+    for rep in range(args.reps):
+        for name, sets, kw in variants:
+            for (m, c), v in defaults.items():
+                setattr(m, c, v)
+            for m, c, v in sets:
+                setattr(m, c, v)
+            env = kw.get("_env", {})
+            saved = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            torch.manual_seed(5)
+            model = ncf.AdvancedNCF(U, I, 10, 50, D, D, 32, [256, 128, 64], 4, 0.2, M - 1).to(dev).train()
+            step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5,
+                                  **{k: v for k, v in kw.items() if k != "_env"})
+            for k, v in saved.items():     # (read by the constructors above only)
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+            def run(first, count):
+                for s in range(first, first + count):
+                    u, i, t = batches[s % len(batches)]
+                    step(u, i, t, next=batches[(s + 1) % len(batches)][:2])
+            run(0, 150)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run(150, args.steps)
+            torch.cuda.synchronize()
+            res[name].append((time.perf_counter() - t0) / args.steps * 1e3)
+            if rep == 0:
+                _lib.PROFILE = []
+                run(150 + args.steps, 20)
+                torch.cuda.synchronize()
+                p, _lib.PROFILE = _lib.PROFILE, None
+                per = {}
+                for nm, _, e0, e1 in p:
+                    per[nm] = per.get(nm, 0.0) + e0.elapsed_time(e1) * 1e3 / 20
+                prof[name] = per
+            print(f"rep {rep} {name:12s} {res[name][-1]:.4f} ms/step", flush=True)
+            del step, model
+            torch.cuda.empty_cache()
+    for name, _, _ in variants:
+        v = sorted(res[name])
+        print(f"== {name:12s} ms/step {' '.join(f'{x:.4f}' for x in res[name])}  min {v[0]:.4f}")
+        for k, us in sorted(prof[name].items(), key=lambda x: -x[1]):
+            if us >= 1.0:
+                print(f"     {k:40s} {us:7.1f} us/step")
+
+
+if __name__ == "__main__":
+    main()

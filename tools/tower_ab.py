@@ -17,10 +17,10 @@ ncf = _ncf_pkg.load()
 from ncf_amd import _lib  # noqa: E402
 from ncf_amd.trainer import FusedTrainStep  # noqa: E402
 
-NAMES = ("ncf_mlp_bwd", "ncf_mlp_bwd_split", "ncf_mlp_bwd_bf16", "ncf_mlp_fwd", "ncf_mlp_fwd_split",
+NAMES = ("ncf_attn_mlp_fwd", "ncf_attn_mlp_bwd", "ncf_mlp_bwd", "ncf_mlp_bwd_split", "ncf_mlp_bwd_bf16", "ncf_mlp_fwd", "ncf_mlp_fwd_split",
          "ncf_mlp_fwd_bf16", "ncf_attn_block_fwd",
          "ncf_attn_block_bwd", "ncf_reduce_batch", "ncf_embedding_bwd_reduce",
-         "ncf_gather_ln_gmf_scaled_fwd", "ncf_adam_pairs_apply_clock", "ncf_adam_pairs_catchup_clock",
+         "ncf_gather_ln_gmf_scaled_fwd", "ncf_adam_pairs_apply_clock", "ncf_adam_pairs_catchup_clock", "ncf_adam_pairs_catchup_lock_clock",
          "ncf_adam_flat_clock_close")
 
 
