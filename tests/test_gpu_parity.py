@@ -660,6 +660,9 @@ def test_mlp_tower_matches_unfused(monkeypatch, B, drop, D, wgrad, split):
     import ncf_amd.engine as E
     from ncf_amd.trainer import FusedTrainStep
     monkeypatch.setattr(E, "TOWER_SPLIT", split)
+    # (the tower's own launch: fused behind the attention block its dy never reaches HBM;
+    # test_attn_tower_fused_bitwise_equals_two_launches holds that form to this one)
+    monkeypatch.setattr(E, "FUSE_ATTN_TOWER", False)
     out = []
     monkeypatch.setenv("NCF_MLP_WGRAD", wgrad)
     for flag in ("0", "1"):
