@@ -507,6 +507,23 @@ int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_users, int64_t 
                              const int64_t* uniq_items, float* grad_mf_gamma, float* grad_mf_beta,
                              float* grad_mlp_gamma, float* grad_mlp_beta, void* workspace,
                              int64_t workspace_bytes, ncf_reduce_list* defer, void* stream);
+/* The same reduce writing unique row c's two gradient rows at row out_rows_*[c] (stride out_ld
+ * floats) of the four gradient pointers: the row-sharded step hands its send buffer ([mf | mlp]
+ * halves of 2 D floats per row: grad_mf_* = buf, grad_mlp_* = buf + D, out_ld = 2 D) instead of
+ * compact rows it then re-orders (ncf_shard_rows). */
+int ncf_embedding_bwd_reduce_rows(int64_t n, int64_t dim, int64_t num_users, int64_t num_items,
+                                  const float* dy_mf_user, const float* dy_mlp_user,
+                                  const float* dy_mf_item, const float* dy_mlp_item,
+                                  const float* mf_user, const float* mlp_user,
+                                  const float* mf_item, const float* mlp_item,
+                                  const float* mf_gamma, const float* mlp_gamma, float eps,
+                                  float* grad_mf_user, float* grad_mlp_user, float* grad_mf_item,
+                                  float* grad_mlp_item, const int64_t* uniq_users,
+                                  const int64_t* uniq_items, const int32_t* out_rows_users,
+                                  const int32_t* out_rows_items, int64_t out_ld,
+                                  float* grad_mf_gamma, float* grad_mf_beta,
+                                  float* grad_mlp_gamma, float* grad_mlp_beta, void* workspace,
+                                  int64_t workspace_bytes, ncf_reduce_list* defer, void* stream);
 /* bf16-table configuration: the same reduce with bf16 table rows (uint16 bit patterns). */
 int ncf_embedding_bwd_reduce_bf16(int64_t n, int64_t dim, int64_t num_users, int64_t num_items,
                                   const float* dy_mf_user, const float* dy_mlp_user,
@@ -529,7 +546,9 @@ int ncf_scatter_compact_rows(float* dense_grad, int64_t dim, const int64_t* uniq
 
 /* ---- C5: batch candidate scoring (app.py:44-75 forward_simple over all products + nlargest) ---
  * Factorised eval logit(u, i) = q_u . p_i + bias_i (score.hip header); results ordered by
- * (logit desc, item id asc).  dim must be 64.  Pipeline: queries -> sample logits (ncf_gemm_f32
+ * (logit desc, item id asc).  dim must be 64, except ncf_score_queries: its table rows may be 16,
+ * 32 or 64 wide and its query rows are always 64 floats (zero-padded; the item rows of an index
+ * over a narrower table are padded the same way).  Pipeline: queries -> sample logits (ncf_gemm_f32
  * with a strided B) -> ncf_score_kth thresholds -> ncf_score_collect candidates ->
  * ncf_score_select top-K (overflow[slot] = 1: re-run 3-4 for those slots with the returned thr). */
 int ncf_score_queries(const int64_t* user_ids, int64_t n, const float* mf_user, int64_t rows,
@@ -781,6 +800,17 @@ int ncf_adam_pairs_catchup_claim_clock(const ncf_table_pair* pairs, int npairs, 
                                        int32_t target_rel, const ncf_step_clock* clock,
                                        const float* step_table, double beta1, double beta2,
                                        double eps, double weight_decay, void* stream);
+/* The owner side of the row-sharded step (distributed.py): ncf_shard_owner_gradsum (the W
+ * requesters' gradient rows of each unique row, summed in rank order: got[pos[c][s]], -1 = not
+ * sent) and ncf_adam_pairs_apply_clock in ONE launch, the same bits; pairs' g0 / g1 unused.
+ * Replaces the sharded EBC's gradient exchange + Adam.step of torchrec's pipeline (the
+ * reference's single-process trainer.py:285). */
+int ncf_adam_pairs_apply_gsum_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
+                                    const uint32_t* count, int64_t max_n, int32_t step_rel,
+                                    const float* got, const int32_t* pos0, const int32_t* pos1,
+                                    int world, const ncf_step_clock* clock,
+                                    const float* step_table, double beta1, double beta2,
+                                    double eps, double weight_decay, void* stream);
 int ncf_adam_pairs_apply_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
                                const uint32_t* count, int64_t max_n, int32_t step_rel,
                                const ncf_step_clock* clock, const float* step_table, double beta1,

@@ -116,6 +116,9 @@ SIGNATURES = {
     "ncf_comm_destroy": (I32, [P]),
     "ncf_comm_alltoallv": (I32, [P, P, P, P, P, I64, P]),
     "ncf_comm_allreduce_sum_f32": (I32, [P, P, I64, P]),
+    "ncf_embedding_bwd_reduce_rows": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32,
+                                            P, P, P, P, P, P, P, P, I64, P, P, P, P, P, I64, P,
+                                            P]),
     "ncf_embedding_bwd_reduce": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
                                        P, P, P, P, P, P, P, P, P, I64, P, P]),
     "ncf_embedding_bwd_reduce_bf16": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32,
@@ -144,6 +147,8 @@ SIGNATURES = {
                                                 F64, P]),
     "ncf_adam_pairs_catchup_claim_clock": (I32, [P, I32, I64, P, P, I64, I32, P, P, F64, F64, F64,
                                                  F64, P]),
+    "ncf_adam_pairs_apply_gsum_clock": (I32, [P, I32, I64, P, I64, I32, P, P, P, I32, P, P, F64,
+                                              F64, F64, F64, P]),
     "ncf_adam_pairs_apply_clock": (I32, [P, I32, I64, P, I64, I32, P, P, F64, F64, F64, F64, P]),
     "ncf_adam_pairs_sweep_rolling": (I32, [P, I32, I64, I32, I32, P, P, F64, F64, F64, F64, P]),
     "ncf_adam_pairs_sweep_rolling_part": (I32, [P, I32, I64, I32, I32, I32, I32, P, P, F64, F64, F64,

@@ -291,10 +291,27 @@ class AdvancedNCF(nn.Module):
                                           "not part of the accelerated path; call model.eval()")
             return forward_simple_hour(self, user_ids, product_ids, hour)
         eng = self._engine
-        drop_p = float(self.dropout) if self.training else 0.0
-        if drop_p > 0:
-            raise NotImplementedError("forward_simple in training mode (dropout active) is not "
-                                      "part of the accelerated path; call model.eval()")
+        if self.training and torch.is_grad_enabled():
+            # training mode (the reference's nn.Dropout layers active): the training forward with
+            # one item per group — the attention over a single key — through the same autograd
+            # function as forward(), so loss.backward() reaches every parameter; the dropout
+            # masks come from this package's stream (as in forward())
+            drop_p = float(self.dropout)
+            seed = (int(torch.randint(0, 2 ** 62, (1,)).item())
+                    if drop_p > 0 and eng.clock is None else 0)
+            dev = eng.flat.device if eng.flat is not None else user_ids.device
+            uid = user_ids.reshape(-1).to(device=dev, dtype=torch.int64).contiguous()
+            iid = product_ids.reshape(-1).to(device=dev, dtype=torch.int64).contiguous()
+            if uid.numel() != iid.numel():
+                raise ValueError("forward_simple: user_ids and product_ids differ in length")
+            out = _NCFTrainFunction.apply(eng, uid, iid, 1, drop_p, seed, self._anchor)
+            if getattr(self, "validate_ids", True):
+                ws = eng.ws[(uid.numel(), 1, True)]
+                if self.validate_ids != "sync":
+                    eng.check_ids_async(ws)
+                else:
+                    eng.check_ids(ws)
+            return out.view(-1)
         w = eng.forward(user_ids, product_ids, 1, False, 0.0, 0)
         eng.check_ids(w)
         return w.prob.clone()

@@ -486,6 +486,49 @@ __global__ __launch_bounds__(256) void k_pairs_apply(const PairArgs a, const uin
   if (sub == 0) a.stamp[k][row] = step;
 }
 
+// The owner side of the row-sharded step: the gradient of unique row c is the sum, in rank order,
+// of the rows the W requesters sent for it (got[pos[c][s]]: [mf | mlp] halves of 2 D floats, -1
+// where rank s did not touch the row) — summed here, in the order ncf_shard_owner_gradsum sums
+// them (0 + x == x exactly: the same bits), then applied as k_pairs_apply does.
+template <int D, bool BF = false>
+__global__ __launch_bounds__(256) void k_pairs_apply_gsum(const PairArgs a, const uint32_t* __restrict__ count,
+                                                          int64_t max_n, int32_t step_rel,
+                                                          const ncf_step_clock* clock,
+                                                          const float* __restrict__ table,
+                                                          AdamScalars s,
+                                                          const float* __restrict__ got,
+                                                          const int32_t* __restrict__ pos0,
+                                                          const int32_t* __restrict__ pos1, int W) {
+  constexpr int L = D / 4;
+  const int k = blockIdx.y;
+  const int64_t tt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = tt / L;
+  const int sub = (int)(tt % L);
+  if (c >= max_n || c >= (int64_t)count[k]) return;
+  const int32_t step = clock->t + step_rel;
+  const TablePtrs& t = a.t[k];
+  const int64_t row = a.ids[k][c];
+  const int64_t o = row * D + sub * 4;
+  const float ns = table[4 * step], bc = table[4 * step + 1];
+  float4 p0 = ldp4<BF>(t.p0, o), m0 = ld4(t.m0 + o), v0 = ld4(t.v0 + o);
+  float4 p1 = ldp4<BF>(t.p1, o), m1 = ld4(t.m1 + o), v1 = ld4(t.v1 + o);
+  float4 g0 = make_float4(0.f, 0.f, 0.f, 0.f), g1 = g0;
+  const int32_t* pp = (k ? pos1 : pos0) + c * W;
+  for (int r = 0; r < W; ++r) {
+    const int32_t j = pp[r];
+    if (j < 0) continue;
+    const float4 x = ld4(got + (int64_t)j * 2 * D + sub * 4);
+    const float4 y = ld4(got + (int64_t)j * 2 * D + D + sub * 4);
+    g0.x += x.x; g0.y += x.y; g0.z += x.z; g0.w += x.w;
+    g1.x += y.x; g1.y += y.y; g1.z += y.z; g1.w += y.w;
+  }
+  adam4(p0, m0, v0, g0, ns, bc, s);
+  adam4(p1, m1, v1, g1, ns, bc, s);
+  stp4<BF>(t.p0, o, p0); st4(t.m0 + o, m0); st4(t.v0 + o, v0);
+  stp4<BF>(t.p1, o, p1); st4(t.m1 + o, m1); st4(t.v1 + o, v1);
+  if (sub == 0) a.stamp[k][row] = step;
+}
+
 // part `part` of `nparts` (consecutive row ranges) of the slice of step clock->t + step_rel
 template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void k_pairs_sweep(const PairArgs a, int32_t every,
@@ -754,6 +797,20 @@ int pairs_apply_d(PairArgs a, int n, const uint32_t* count, int64_t max_n, int32
   else
     hipLaunchKernelGGL((k_pairs_apply<D, false>), dim3(ncf_cdiv(max_n * (D / 4), 256), n), dim3(256), 0, st, a, count, max_n, rel, clock, table, s);
   NCF_CHECK_LAUNCH("ncf_adam_pairs_apply_clock");
+  return NCF_OK;
+}
+
+template <int D>
+int pairs_apply_gsum_d(PairArgs a, int n, const uint32_t* count, int64_t max_n, int32_t rel,
+                       const ncf_step_clock* clock, const float* table, AdamScalars s,
+                       const float* got, const int32_t* pos0, const int32_t* pos1, int W,
+                       hipStream_t st) {
+  const dim3 grid(ncf_cdiv(max_n * (D / 4), 256), n);
+  if (a.bf)
+    hipLaunchKernelGGL((k_pairs_apply_gsum<D, true>), grid, dim3(256), 0, st, a, count, max_n, rel, clock, table, s, got, pos0, pos1, W);
+  else
+    hipLaunchKernelGGL((k_pairs_apply_gsum<D, false>), grid, dim3(256), 0, st, a, count, max_n, rel, clock, table, s, got, pos0, pos1, W);
+  NCF_CHECK_LAUNCH("ncf_adam_pairs_apply_gsum_clock");
   return NCF_OK;
 }
 
@@ -1034,6 +1091,26 @@ extern "C" int ncf_adam_pairs_apply_clock(const ncf_table_pair* pairs, int npair
   NCF_DISPATCH_DIM(dim, pairs_apply_d, pair_args(pairs, npairs), npairs, count, max_n, step_rel,
                    clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
                    (hipStream_t)stream);
+}
+
+// ncf_shard_owner_gradsum + ncf_adam_pairs_apply_clock in one launch (the pairs' g0 / g1 unused)
+extern "C" int ncf_adam_pairs_apply_gsum_clock(const ncf_table_pair* pairs, int npairs,
+                                               int64_t dim, const uint32_t* count, int64_t max_n,
+                                               int32_t step_rel, const float* got,
+                                               const int32_t* pos0, const int32_t* pos1,
+                                               int world, const ncf_step_clock* clock,
+                                               const float* step_table, double beta1,
+                                               double beta2, double eps, double weight_decay,
+                                               void* stream) {
+  NCF_CHECK_ARG(pairs && npairs >= 1 && npairs <= 2 && count && clock && step_table && got &&
+                    pos0 && pos1 && world >= 1,
+                "ncf_adam_pairs_apply_gsum_clock: bad args");
+  for (int k = 0; k < npairs; ++k)
+    NCF_CHECK_ARG(pairs[k].p1, "ncf_adam_pairs_apply_gsum_clock: both tables of a pair");
+  if (max_n <= 0) return NCF_OK;
+  NCF_DISPATCH_DIM(dim, pairs_apply_gsum_d, pair_args(pairs, npairs), npairs, count, max_n,
+                   step_rel, clock, step_table, consts_of(beta1, beta2, eps, weight_decay), got,
+                   pos0, pos1, world, (hipStream_t)stream);
 }
 
 extern "C" int ncf_adam_pairs_sweep_rolling(const ncf_table_pair* pairs, int npairs, int64_t dim,

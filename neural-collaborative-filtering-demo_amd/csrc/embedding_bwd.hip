@@ -43,10 +43,12 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     const float* __restrict__ t_mlp1, const float* __restrict__ g_mf,
     const float* __restrict__ g_mlp, float eps, float* __restrict__ G_mf0,
     float* __restrict__ G_mlp0, float* __restrict__ G_mf1, float* __restrict__ G_mlp1,
-    float* __restrict__ xp0, float* __restrict__ xp1, float* __restrict__ part) {
+    float* __restrict__ xp0, float* __restrict__ xp1, float* __restrict__ part,
+    const int32_t* __restrict__ omap0, const int32_t* __restrict__ omap1, int64_t ldo) {
   constexpr int L = D / 4;
   constexpr int S = 64 / L;  // lane groups (pieces) per wave
   __shared__ __attribute__((aligned(16))) float red[kPW][4 * D];
+  const int32_t* omap = blockIdx.y ? omap1 : omap0;   // output row of segment c (NULL: c)
   const int kind = blockIdx.y;
   const uint32_t* sv = kind ? sv1 : sv0;
   const uint32_t* pstart = kind ? pstart1 : pstart0;
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
       if (act) {
         const float4 dx = make_float4(rstd * (gd.x - m1 - h.x * m2), rstd * (gd.y - m1 - h.y * m2),
                                       rstd * (gd.z - m1 - h.z * m2), rstd * (gd.w - m1 - h.w * m2));
-        float* dst = first ? (tbl ? Gml : Gmf) + c * D
+        float* dst = first ? (tbl ? Gml : Gmf) + (omap ? (int64_t)omap[c] : c) * ldo
                            : xp + (p - c - 1) * 2 * D + tbl * D;  // extra piece e = p - c - 1
         st4(dst + col, dx);
         float4& ag = tbl ? a_gl : a_gm;
@@ -173,9 +175,11 @@ __global__ __launch_bounds__(256) void k_piece_fixup(
     const uint32_t* __restrict__ fpiece0, const uint32_t* __restrict__ fpiece1,
     const uint32_t* __restrict__ totals, const float* __restrict__ xp0,
     const float* __restrict__ xp1, float* __restrict__ G_mf0, float* __restrict__ G_mlp0,
-    float* __restrict__ G_mf1, float* __restrict__ G_mlp1) {
+    float* __restrict__ G_mf1, float* __restrict__ G_mlp1, const int32_t* __restrict__ omap0,
+    const int32_t* __restrict__ omap1, int64_t ldo) {
   constexpr int L = D / 4;
   const int kind = blockIdx.y;
+  const int32_t* omap = kind ? omap1 : omap0;
   const uint32_t* fpiece = kind ? fpiece1 : fpiece0;
   const float* xp = kind ? xp1 : xp0;
   float* Gmf = kind ? G_mf1 : G_mf0;
@@ -186,7 +190,8 @@ __global__ __launch_bounds__(256) void k_piece_fixup(
   for (int64_t c = t / L; c < U; c += (int64_t)gridDim.x * blockDim.x / L) {
     const uint32_t f0 = fpiece[c], f1 = fpiece[c + 1];
     if (f1 - f0 <= 1) continue;
-    float4 a = ld4(Gmf + c * D + col), b = ld4(Gml + c * D + col);
+    const int64_t orow = (omap ? (int64_t)omap[c] : c) * ldo;
+    float4 a = ld4(Gmf + orow + col), b = ld4(Gml + orow + col);
     const int64_t e1 = (int64_t)f1 - c - 1;
     for (int64_t e0 = (int64_t)f0 - c; e0 < e1; e0 += 8) {   // 8 rows of loads in flight
       float4 x[8], y[8];
@@ -203,8 +208,8 @@ __global__ __launch_bounds__(256) void k_piece_fixup(
           b.x += y[u].x; b.y += y[u].y; b.z += y[u].z; b.w += y[u].w;
         }
     }
-    st4(Gmf + c * D + col, a);
-    st4(Gml + c * D + col, b);
+    st4(Gmf + orow + col, a);
+    st4(Gml + orow + col, b);
   }
 }
 
@@ -509,23 +514,24 @@ int piece_reduce(const WS& w, int64_t n, const uint32_t* sv0, const uint32_t* sv
                  const float* tmf1, const float* tml1, const float* gmf, const float* gml,
                  float eps, float* Gmf0, float* Gml0, float* Gmf1, float* Gml1, float* dgm,
                  float* dbm, float* dgl, float* dbl, ncf_reduce_list* defer, hipStream_t st,
-                 bool bf = false) {
+                 bool bf = false, const int32_t* omap0 = nullptr, const int32_t* omap1 = nullptr,
+                 int64_t ldo = D) {
   if (bf)
     hipLaunchKernelGGL((k_piece_reduce_ln<D, true>), dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1,
                        w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
                        dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
-                       Gmf1, Gml1, w.xp0, w.xp1, w.part);
+                       Gmf1, Gml1, w.xp0, w.xp1, w.part, omap0, omap1, ldo);
   else
     hipLaunchKernelGGL((k_piece_reduce_ln<D, false>), dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1,
                        w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
                        dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
-                       Gmf1, Gml1, w.xp0, w.xp1, w.part);
+                       Gmf1, Gml1, w.xp0, w.xp1, w.part, omap0, omap1, ldo);
   NCF_CHECK_LAUNCH("ncf_embedding_bwd(piece_reduce)");
   constexpr int L = D / 4;
   const int64_t fb = ncf_cdiv(n * L, 256);
   hipLaunchKernelGGL(k_piece_fixup<D>, dim3((unsigned)(fb > 2048 ? 2048 : (fb < 1 ? 1 : fb)), 2),
                      dim3(256), 0, st, w.fpiece0, w.fpiece1, w.totals, w.xp0, w.xp1, Gmf0, Gml0,
-                     Gmf1, Gml1);
+                     Gmf1, Gml1, omap0, omap1, ldo);
   NCF_CHECK_LAUNCH("ncf_embedding_bwd(fixup)");
   if (defer) {
     float* const outs[4] = {dgm, dbm, dgl, dbl};
@@ -560,7 +566,8 @@ static int embedding_bwd_reduce(bool bf, int64_t n, int64_t dim, int64_t num_use
                                         float* grad_mf_beta, float* grad_mlp_gamma,
                                         float* grad_mlp_beta, void* workspace,
                                         int64_t workspace_bytes, ncf_reduce_list* defer,
-                                        void* stream) {
+                                        void* stream, const int32_t* omap0 = nullptr,
+                                        const int32_t* omap1 = nullptr, int64_t ldo = 0) {
   NCF_CHECK_ARG(n >= 0 && n < (1ll << 30), "ncf_embedding_bwd_reduce: bad n");
   NCF_CHECK_ARG(dim == 16 || dim == 32 || dim == 64 || dim == 128 || dim == 256,
                 "ncf_embedding_bwd_reduce: dim must be 16/32/64/128/256");
@@ -572,7 +579,8 @@ static int embedding_bwd_reduce(bool bf, int64_t n, int64_t dim, int64_t num_use
   WS w = carve(workspace, n, dim);
   uint32_t *k0, *v0, *k1, *v1;
   sorted_bufs(w, sort_passes(num_users, num_items), &k0, &v0, &k1, &v1);
-  if (n > 0 && use_pos_reduce()) {
+  const bool mapped = omap0 != nullptr;
+  if (n > 0 && use_pos_reduce() && !mapped) {
     switch (dim) {
 #define POS(DD)                                                                                   \
   case DD:                                                                                        \
@@ -592,7 +600,7 @@ static int embedding_bwd_reduce(bool bf, int64_t n, int64_t dim, int64_t num_use
                             dy_mf_item, dy_mlp_item, mf_user, mlp_user, mf_item, mlp_item,        \
                             mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user, grad_mf_item,  \
                             grad_mlp_item, grad_mf_gamma, grad_mf_beta, grad_mlp_gamma,           \
-                            grad_mlp_beta, defer, st, bf);
+                            grad_mlp_beta, defer, st, bf, omap0, omap1, mapped ? ldo : DD);
     SEG(16) SEG(32) SEG(64) SEG(128) SEG(256)
 #undef SEG
   }
@@ -619,6 +627,29 @@ extern "C" int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_user
                               grad_mlp_item, uniq_users, uniq_items, grad_mf_gamma, grad_mf_beta,
                               grad_mlp_gamma, grad_mlp_beta, workspace, workspace_bytes, defer,
                               stream);
+}
+
+// The same with each unique row's two gradient rows written at row out_rows[c] of row stride
+// out_ld (floats) of the four output pointers (the row-sharded step: straight into its send
+// buffer, [mf | mlp] halves of 2 D floats per row, instead of compact rows it then re-orders).
+extern "C" int ncf_embedding_bwd_reduce_rows(
+    int64_t n, int64_t dim, int64_t num_users, int64_t num_items, const float* dy_mf_user,
+    const float* dy_mlp_user, const float* dy_mf_item, const float* dy_mlp_item,
+    const float* mf_user, const float* mlp_user, const float* mf_item, const float* mlp_item,
+    const float* mf_gamma, const float* mlp_gamma, float eps, float* grad_mf_user,
+    float* grad_mlp_user, float* grad_mf_item, float* grad_mlp_item, const int64_t* uniq_users,
+    const int64_t* uniq_items, const int32_t* out_rows_users, const int32_t* out_rows_items,
+    int64_t out_ld, float* grad_mf_gamma, float* grad_mf_beta, float* grad_mlp_gamma,
+    float* grad_mlp_beta, void* workspace, int64_t workspace_bytes, ncf_reduce_list* defer,
+    void* stream) {
+  NCF_CHECK_ARG(out_rows_users && out_rows_items && out_ld >= dim,
+                "ncf_embedding_bwd_reduce_rows: out_rows and out_ld >= dim required");
+  return embedding_bwd_reduce(false, n, dim, num_users, num_items, dy_mf_user, dy_mlp_user,
+                              dy_mf_item, dy_mlp_item, mf_user, mlp_user, mf_item, mlp_item,
+                              mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user, grad_mf_item,
+                              grad_mlp_item, uniq_users, uniq_items, grad_mf_gamma, grad_mf_beta,
+                              grad_mlp_gamma, grad_mlp_beta, workspace, workspace_bytes, defer,
+                              stream, out_rows_users, out_rows_items, out_ld);
 }
 
 // The same with bf16 table rows (the LayerNorm recompute reads them; gradients stay fp32).

@@ -45,7 +45,10 @@ __device__ __forceinline__ float fkey_inv(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
 
-// ---- 1. queries: q = w0 * LN(U_mf[id]) (.) w_mf; L = D/4 lanes per row
+// ---- 1. queries: q = w0 * LN(U_mf[id]) (.) w_mf; L = D/4 lanes per row.  The rows are kQD = 64
+// floats wide whatever the table's D: a D < 64 row is zero-padded (the item index pads its rows
+// the same way, so every dot product is the D-term one — the scan kernels are 64-deep)
+constexpr int kQD = 64;
 template <int D>
 __global__ void k_queries(const int64_t* __restrict__ ids, int64_t n, const float* __restrict__ table,
                           int64_t rows, const float* __restrict__ gamma,
@@ -69,10 +72,12 @@ __global__ void k_queries(const int64_t* __restrict__ ids, int64_t n, const floa
   const float rstd = 1.0f / sqrtf(var + eps);
   const float4 g = ld4(gamma + c), b = ld4(beta + c), w = ld4(w_mf + c);
   const float w0 = final_w[0];
-  st4(q + r * D + c, make_float4(w0 * ((xc.x * rstd * g.x + b.x) * w.x),
-                                 w0 * ((xc.y * rstd * g.y + b.y) * w.y),
-                                 w0 * ((xc.z * rstd * g.z + b.z) * w.z),
-                                 w0 * ((xc.w * rstd * g.w + b.w) * w.w)));
+  st4(q + r * kQD + c, make_float4(w0 * ((xc.x * rstd * g.x + b.x) * w.x),
+                                   w0 * ((xc.y * rstd * g.y + b.y) * w.y),
+                                   w0 * ((xc.z * rstd * g.z + b.z) * w.z),
+                                   w0 * ((xc.w * rstd * g.w + b.w) * w.w)));
+#pragma unroll
+  for (int pc = D + c; pc < kQD; pc += D) st4(q + r * kQD + pc, make_float4(0.f, 0.f, 0.f, 0.f));
 }
 
 // bias_i = w1 * mlp_item_i + (w0 * b_mf + b_final)
@@ -1260,11 +1265,16 @@ extern "C" int ncf_score_queries(const int64_t* user_ids, int64_t n, const float
                                  const float* mf_beta, float eps, const float* mf_out_w,
                                  const float* final_w, float* queries, int* err_flag,
                                  void* stream) {
-  NCF_CHECK_ARG(n >= 0 && dim == 64, "ncf_score_queries: dim must be 64");
+  NCF_CHECK_ARG(n >= 0 && (dim == 16 || dim == 32 || dim == 64),
+                "ncf_score_queries: dim must be 16, 32 or 64");
   if (n == 0) return NCF_OK;
-  hipLaunchKernelGGL(k_queries<64>, dim3(ncf_cdiv(n * 16, 256)), dim3(256), 0, (hipStream_t)stream,
-                     user_ids, n, mf_user, rows, mf_gamma, mf_beta, eps, mf_out_w, final_w, queries,
-                     err_flag);
+#define NCF_QUERIES(DD)                                                                           \
+  if (dim == DD)                                                                                  \
+    hipLaunchKernelGGL(k_queries<DD>, dim3(ncf_cdiv(n * (DD / 4), 256)), dim3(256), 0,            \
+                       (hipStream_t)stream, user_ids, n, mf_user, rows, mf_gamma, mf_beta, eps,     \
+                       mf_out_w, final_w, queries, err_flag);
+  NCF_QUERIES(16) NCF_QUERIES(32) NCF_QUERIES(64)
+#undef NCF_QUERIES
   NCF_CHECK_LAUNCH("ncf_score_queries");
   return NCF_OK;
 }

@@ -48,6 +48,9 @@ SCALAR_PAD = 4096
 # replay beside the backward slows it more than it saves on the critical path; round 3 found
 # the same for three placements of it)
 EARLY_CATCHUP = False
+# HIP stream priority of the overlapped sweep's side stream (torch.cuda.Stream priority: 0 the
+# default, -1 high)
+SIDE_PRIORITY = 0
 
 
 class DeferredTableAdam:
@@ -308,7 +311,7 @@ class DeferredTableAdam:
     def side_stream(self):
         """The overlapped sweep's stream (created on first use)."""
         if self._side is None:
-            self._side = torch.cuda.Stream(self.clock.device)
+            self._side = torch.cuda.Stream(self.clock.device, priority=SIDE_PRIORITY)
             self._ev = (_lib.RawEvent(stream_only=True), _lib.RawEvent(stream_only=True))
         return self._side
 

@@ -49,6 +49,12 @@ from ._lib import ptr
 SLOT_NEXT_U, SLOT_NEXT_I, SLOT_TARGETS, SLOT_STREAM = 0, 1, 2, 3
 SLOT_TOKEN, SLOT_NMAX, SLOT_NUNI = 4, 5, 6
 TAPE_SHARDED = os.environ.get("NCF_TAPE", "1") != "0"
+# The owner's rank-order gradient sum inside the table Adam's apply (ncf_adam_pairs_apply_gsum_clock,
+# one launch and no compact gradient round trip; False: ncf_shard_owner_gradsum + the apply)
+GSUM_APPLY = True
+# The requester's table gradients written by the embedding backward straight into its send
+# buffer (ncf_embedding_bwd_reduce_rows; False: compact rows, then ncf_shard_rows)
+GRAD_ROWS = True
 
 
 class ShardExchange:
@@ -744,15 +750,19 @@ class HipShardOps:
         if self._bufs.get("arange_n") != ar.numel():
             torch.arange(ar.numel(), out=ar)
             self._bufs["arange_n"] = ar.numel()
+        g = self._buf("send_grads", (max(2 * n, 1), 2 * D))      # (nu + ni <= 2 n rows)
+        # the table gradients straight into the send buffer at their send positions
+        # (GRAD_ROWS; else compact rows, then ncf_shard_rows re-orders them)
         eng.backward(w, inv_u, inv_i, None, targets, drop_p, seed,
                      loss_denominator=loss_denominator, tables=mini,
-                     rows=(self.W * self.Ru, self.W * self.Ri), uniq=(ar, ar))
+                     rows=(self.W * self.Ru, self.W * self.Ri), uniq=(ar, ar),
+                     grad_rows=(g, s["spos"][0], s["spos"][1]) if GRAD_ROWS else None)
         eng.pending = None
-        g = self._buf("send_grads", (max(2 * n, 1), 2 * D))      # (nu + ni <= 2 n rows)
-        _lib.call_tagged("ncf_shard_rows", {4: SLOT_NUNI}, ptr(g), ptr(s["spos"][0]),
-                         ptr(s["spos"][1]), ptr(s["num_unique"]), max(nu, ni), D,
-                         ptr(w.G["mf_user"]), ptr(w.G["mlp_user"]), ptr(w.G["mf_item"]),
-                         ptr(w.G["mlp_item"]), 1, st)
+        if not GRAD_ROWS:
+            _lib.call_tagged("ncf_shard_rows", {4: SLOT_NUNI}, ptr(g), ptr(s["spos"][0]),
+                             ptr(s["spos"][1]), ptr(s["num_unique"]), max(nu, ni), D,
+                             ptr(w.G["mf_user"]), ptr(w.G["mlp_user"]), ptr(w.G["mf_item"]),
+                             ptr(w.G["mlp_item"]), 1, st)
         self.last_loss = w.loss
         return g[:nu + ni], w.loss
 
@@ -760,14 +770,22 @@ class HipShardOps:
     def owner_apply(self, own, got):
         st = self._st()
         uq, pos, nmax, G = own["uniq"], own["pos"], own["nmax"], own["G"]
-        _lib.call_tagged("ncf_shard_owner_gradsum", {4: SLOT_NMAX}, ptr(got), ptr(pos[0]),
-                         ptr(pos[1]), ptr(self.cnt), nmax, self.W, self.D, ptr(G[0]), ptr(G[1]),
-                         ptr(G[2]), ptr(G[3]), st)
         d = self.deferred
+        if not GSUM_APPLY:
+            _lib.call_tagged("ncf_shard_owner_gradsum", {4: SLOT_NMAX}, ptr(got), ptr(pos[0]),
+                             ptr(pos[1]), ptr(self.cnt), nmax, self.W, self.D, ptr(G[0]),
+                             ptr(G[1]), ptr(G[2]), ptr(G[3]), st)
         d._ensure(d.t + 1)
         d.sweep_join()
         d._settle(st)
-        if nmax > 0:
+        if nmax > 0 and GSUM_APPLY:
+            # the rank-order gradient sum inside the apply (one launch, the same bits)
+            pairs = self._pairs(uq)
+            _lib.call_tagged("ncf_adam_pairs_apply_gsum_clock", {4: SLOT_NMAX},
+                             ctypes.addressof(pairs), 2, self.D, ptr(self.cnt), nmax, 1, ptr(got),
+                             ptr(pos[0]), ptr(pos[1]), self.W, ptr(self.clock), ptr(d._table),
+                             *d._consts(), st)
+        elif nmax > 0:
             pairs = self._pairs(uq, G)
             _lib.call_tagged("ncf_adam_pairs_apply_clock", {4: SLOT_NMAX}, ctypes.addressof(pairs),
                              2, self.D, ptr(self.cnt), nmax, 1, ptr(self.clock), ptr(d._table),

@@ -752,12 +752,14 @@ class NCFEngine:
     def backward(self, w: Workspace, uid, iid, grad_prob: Optional[torch.Tensor],
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,
                  loss_denominator: float = 0.0, tables=None, rows=None, uniq=None,
-                 reduce_async: bool = False, bf16: bool = False):
+                 reduce_async: bool = False, bf16: bool = False, grad_rows=None):
         """Gradients of every used parameter.  Dense grads land in the flat grad buffer; table
         grads stay compact (self.pending) for the fused Adam step.  ``reduce_async``: the
         deferred reductions (every dense gradient) run on a side stream, beside whatever the
         caller queues next that does not read them (the table Adam); the caller must call
-        ``join_reductions()`` before reading the dense gradients."""
+        ``join_reductions()`` before reading the dense gradients.  ``grad_rows = (buf, rows_u,
+        rows_i)``: the table gradients of unique row c go to row rows_*[c] of buf ([mf | mlp]
+        halves, 2 D floats per row: the row-sharded step's send buffer) instead of w.G."""
         m = self.model
         g = w.g
         n, D, H, M, hid = g.n, g.D, g.H, g.M, g.hidden
@@ -901,14 +903,27 @@ class NCFEngine:
                       ptr(w.uniq_u), ptr(w.uniq_i), ptr(self.slot_u), ptr(self.slot_i),
                       ptr(w.num_unique), ptr(w.emb_ws), w.emb_ws.numel(), st)
             w.slots_set = True
-        _lib.call("ncf_embedding_bwd_reduce_bf16" if bf16 else "ncf_embedding_bwd_reduce", n, D,
-                  d_rows[0], d_rows[1],
-                  ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), *tbp,
-                  pp["mf_norm.weight"], pp["mlp_norm.weight"], LN_EPS, ptr(G["mf_user"]),
-                  ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(uq_u),
-                  ptr(uq_i), self.gptr("mf_norm.weight"), self.gptr("mf_norm.bias"),
-                  self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
-                  w.emb_ws.numel(), w.red_list.address, st)
+        if grad_rows is not None:
+            if bf16:
+                raise ValueError("grad_rows: fp32 tables only")
+            gb, ru_, ri_ = grad_rows
+            gmf, gml = ptr(gb), ptr(gb) + 4 * D
+            _lib.call("ncf_embedding_bwd_reduce_rows", n, D, d_rows[0], d_rows[1],
+                      ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), *tbp,
+                      pp["mf_norm.weight"], pp["mlp_norm.weight"], LN_EPS, gmf, gml, gmf, gml,
+                      ptr(uq_u), ptr(uq_i), ptr(ru_), ptr(ri_), 2 * D,
+                      self.gptr("mf_norm.weight"), self.gptr("mf_norm.bias"),
+                      self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
+                      w.emb_ws.numel(), w.red_list.address, st)
+        else:
+            _lib.call("ncf_embedding_bwd_reduce_bf16" if bf16 else "ncf_embedding_bwd_reduce", n,
+                      D, d_rows[0], d_rows[1],
+                      ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), *tbp,
+                      pp["mf_norm.weight"], pp["mlp_norm.weight"], LN_EPS, ptr(G["mf_user"]),
+                      ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(uq_u),
+                      ptr(uq_i), self.gptr("mf_norm.weight"), self.gptr("mf_norm.bias"),
+                      self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
+                      w.emb_ws.numel(), w.red_list.address, st)
         self.join(dev, joins)
         self._sweep_fork("reduce")
         if reduce_async:

@@ -29,6 +29,7 @@ from .engine import LN_EPS
 
 K_MF_U = "mf_embedding_collection.embedding_bags.user_id.weight"
 K_MF_I = "mf_embedding_collection.embedding_bags.product_id.weight"
+QD = 64   # the scan's row width (ncf_score_queries pads narrower rows to it)
 
 
 class ItemIndex:
@@ -44,8 +45,10 @@ class ItemIndex:
             raise RuntimeError("ncf_amd scoring runs on the MI355X only (no CPU fallback)")
         I = model.num_products
         D = model.mf_embedding_dim
-        if D != 64 or model.mlp_embedding_dim != 64:
-            raise NotImplementedError("the scoring kernels are specialised for D = 64")
+        if D not in (16, 32, 64):
+            # (the scan kernels are 64 deep: narrower rows are zero-padded to 64, which leaves
+            # every dot product the D-term one; a wider D would need a second k chunk)
+            raise NotImplementedError("the scoring kernels take D = 16, 32 or 64")
         st = _lib.stream_ptr(dev)
         if items is None:
             ids = torch.arange(I, dtype=torch.int64, device=dev)
@@ -57,11 +60,18 @@ class ItemIndex:
             self.ids = ids
             I = ids.numel()
         table = model.mf_embedding_collection.embedding_bags["product_id"].weight
-        self.p = torch.empty(I, D, device=dev)
+        self.dim = D
         err = torch.zeros(1, dtype=torch.int32, device=dev)
+        pD = torch.empty(I, D, device=dev)
         _lib.call("ncf_gather_rows", ptr(ids), I, ptr(table), model.num_products, D,
                   ptr(model.mf_norm.weight),
-                  ptr(model.mf_norm.bias), LN_EPS, ptr(self.p), ptr(err), st)
+                  ptr(model.mf_norm.bias), LN_EPS, ptr(pD), ptr(err), st)
+        if D == QD:
+            self.p = pD
+        else:   # zero-padded to the scan's 64-deep rows (the queries are padded alike)
+            self.p = torch.zeros(I, QD, device=dev)
+            self.p[:, :D].copy_(pD)
+            del pD
         # mlp_item(i): the eval forward's MLP prediction depends on the item only (M = 1)
         mlp_item = torch.empty(I, device=dev)
         zeros = torch.zeros(max(1, min(I, chunk)), dtype=torch.int64, device=dev)
@@ -78,11 +88,11 @@ class ItemIndex:
         self.pmax = None   # max_i |p_i| (float bits) for the 1/2-term scan's threshold margin
         self.terms = SPLIT_TERMS   # operand terms of the split scan (with pmax; else 3)
         if SPLIT_SCAN:
-            self.p3 = torch.empty(3, I, D, dtype=torch.int16, device=dev)
-            _lib.call("ncf_score_split_items", ptr(self.p), I, D, ptr(self.p3), st)
+            self.p3 = torch.empty(3, I, QD, dtype=torch.int16, device=dev)
+            _lib.call("ncf_score_split_items", ptr(self.p), I, QD, ptr(self.p3), st)
             if SPLIT_TERMS < 3:
                 self.pmax = torch.empty(1, dtype=torch.int32, device=dev)
-                _lib.call("ncf_score_item_norm_max", ptr(self.p), I, D, ptr(self.pmax), st)
+                _lib.call("ncf_score_item_norm_max", ptr(self.p), I, QD, ptr(self.pmax), st)
         self.version = _param_version(model)
 
     def valid_for(self, model) -> bool:
@@ -250,7 +260,8 @@ class _TopKRun:
         p, bias = idx.p, idx.bias
         I, D = p.shape
         table = model.mf_embedding_collection.embedding_bags["user_id"].weight
-        _lib.call("ncf_score_queries", ptr(self.uid), n, ptr(table), model.num_users, D,
+        _lib.call("ncf_score_queries", ptr(self.uid), n, ptr(table), model.num_users,
+                  model.mf_embedding_dim,
                   ptr(model.mf_norm.weight), ptr(model.mf_norm.bias), LN_EPS,
                   ptr(model.mf_output.weight), ptr(model.final[0].weight), ptr(self.q),
                   ptr(self.err), st)

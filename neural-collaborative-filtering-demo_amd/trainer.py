@@ -37,6 +37,9 @@ DEDUP_FORK = "sweep"
 # Steps of per-step Adam scalars a captured step graph is given before it must be re-captured
 # (the scalar table cannot grow from inside a replay); tests shrink it to force re-captures.
 GRAPH_HORIZON = 1 << 16
+# The dense-gradient reductions on a side stream beside the table Adam's apply (engine.backward
+# reduce_async; joined before the flat Adam close)
+REDUCE_ASYNC = False
 
 
 class FusedTrainStep:
@@ -140,10 +143,9 @@ class FusedTrainStep:
         prep = self.deferred.prepare if self.deferred is not None else None
         w = eng.forward(user_ids, item_ids, M, True, drop_p, seed, prepare=prep,
                         tables=self.tables_lp, bf16=self.bf16)
-        # (reduce_async=True would run the dense-gradient reductions beside the table Adam:
-        # measured neutral here and slower on the row-sharded step, so off)
+        # (REDUCE_ASYNC: the dense-gradient reductions beside the table Adam)
         eng.backward(w, user_ids, item_ids, None, targets, drop_p, seed, tables=self.tables_lp,
-                     bf16=self.bf16)
+                     bf16=self.bf16, reduce_async=REDUCE_ASYNC and not self.graph)
         st = _lib.stream_ptr(eng.flat.device)
         b1, b2 = self.betas
         if self.deferred is not None:

@@ -177,6 +177,67 @@ def test_train_vs_oracle(U, I, D, H, hidden, B, M):
         assert_params_close(k, sd[k].cpu().numpy(), ref[k].numpy(), zs, 1e-3, atol=5e-6)
 
 
+def test_forward_simple_train_mode_vs_oracle():
+    """forward_simple(users, items) in training mode (architecture.py:409-485 under
+    model.train(): one item per group, the attention over a single key) is differentiable: two
+    steps of forward_simple -> BCE -> backward -> torch.optim.Adam against the oracle's training
+    step with negative_samples = 0 (the same math), probabilities / loss / step-0 gradients and
+    the parameters after both steps (dropout 0: the reference's masks are torch's RNG).  With
+    dropout active the output is a fresh draw every call and the backward runs."""
+    U, I, D, H, hidden, B = 700, 300, 64, 4, [256, 128, 64], 333
+    torch.manual_seed(13)
+    m = ncf.AdvancedNCF(U, I, 5, 24, D, D, 32, hidden, H, 0.0, 4)
+    ref = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(DEV).train()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+    oopt = O.AdamState(lr=1e-3, weight_decay=1e-5)
+    gen = torch.Generator().manual_seed(14)
+    zones = {}
+    for step in range(2):
+        users = torch.randint(0, U, (B,), generator=gen)
+        items = (torch.rand(B, generator=gen) ** 3 * I).long().clamp_max(I - 1)
+        t = (torch.rand(B, generator=gen) < 0.3).float()
+        out = m.forward_simple(users.to(DEV), items.to(DEV))
+        assert out.shape == (B,) and out.requires_grad
+        loss = torch.nn.functional.binary_cross_entropy(out, t.to(DEV))
+        opt.zero_grad()
+        loss.backward()
+        if step == 0:
+            m.engine.materialize_table_grads()
+            grads = {n: p.grad.detach().cpu() for n, p in m.named_parameters() if p.grad is not None}
+        opt.step()
+        before = {k: v.clone() for k, v in ref.items()}
+        prob, oloss, ograds = O.train_step(ref, oopt, users, items, t.reshape(-1, 1),
+                                           negative_samples=0, num_heads=H, temporal_dim=32,
+                                           n_layers=len(hidden))
+        for k, v in ograds.items():
+            zones.setdefault(k, []).append(zone_from_grads(v.numpy(), before[k].numpy(), 1e-5))
+        assert (out.detach().cpu() - prob.reshape(-1)).abs().max().item() < 5e-6
+        assert abs(loss.item() - float(oloss)) < 5e-6
+        if step == 0:
+            for k, v in ograds.items():
+                np.testing.assert_allclose(grads[k].numpy(), v.numpy(), rtol=2e-4, atol=2e-6,
+                                           err_msg=k)
+    sd = m.state_dict()
+    for k, zs in zones.items():
+        assert_params_close(k, sd[k].cpu().numpy(), ref[k].numpy(), zs, 1e-3, atol=5e-6)
+    # dropout active: fresh masks per call, gradients flow
+    torch.manual_seed(15)
+    md = ncf.AdvancedNCF(U, I, 5, 24, D, D, 32, hidden, H, 0.5, 4).to(DEV).train()
+    u = torch.randint(0, U, (B,), device=DEV)
+    i = torch.randint(0, I, (B,), device=DEV)
+    a, b = md.forward_simple(u, i), md.forward_simple(u, i)
+    assert not torch.equal(a, b)
+    md.eval()
+    with torch.no_grad():
+        e = md.forward_simple(u, i)
+    md.train()
+    a.sum().backward()
+    g = md.mlp[0].weight.grad
+    assert g is not None and torch.isfinite(g).all() and g.abs().sum() > 0
+    assert (a - e).abs().max().item() > 1e-4      # not the eval output
+
+
 # ----------------------------------------------------------------------------- op level (F4)
 @pytest.mark.parametrize("tag", ["mha5", "mha50", "mha5_h1"])
 def test_f4_mha(f4, tag):
@@ -1420,6 +1481,30 @@ def test_score_topk_vs_oracle(k, cap):
             gs = ref[r, got].numpy()
             os_ = ref[r, order].numpy()
             np.testing.assert_allclose(gs, os_, atol=1e-6)
+        np.testing.assert_allclose(s[r].cpu().numpy(), ref[r, got].numpy(), atol=1e-6)
+
+
+@pytest.mark.parametrize("D,H,hidden", [(16, 1, [64, 32]), (32, 2, [256, 128, 64])])
+def test_score_topk_narrow_dims_vs_oracle(D, H, hidden):
+    """The C5 scorer for a model narrower than 64 (C1: D = 16, one head, MLP [64, 32]; and D =
+    32): query and item rows zero-padded to the scan's 64-deep rows (ncf_score_queries,
+    ItemIndex), against the oracle's score_factorised: the same top-k (except between oracle
+    scores tied within 1e-6) and scores within 1e-6."""
+    from oracle import ncf_oracle as O
+    from ncf_amd.scoring import score_topk
+    torch.manual_seed(31)
+    U, I, k = 943, 1682, 10
+    m = ncf.AdvancedNCF(U, I, 5, 24, D, D, 32, hidden, H, 0.2, 4).to(DEV).eval()
+    users = torch.randint(0, U, (61,))
+    s, it = score_topk(m, users, k=k)
+    p = {kk: v.detach().cpu() for kk, v in m.state_dict().items()}
+    ref = O.score_factorised(p, users, torch.arange(I), temporal_dim=32,
+                             n_layers=len(hidden)).double()
+    for r in range(len(users)):
+        order = torch.argsort(-ref[r], stable=True)[:k].tolist()
+        got = it[r].cpu().tolist()
+        if got != order:
+            np.testing.assert_allclose(ref[r, got].numpy(), ref[r, order].numpy(), atol=1e-6)
         np.testing.assert_allclose(s[r].cpu().numpy(), ref[r, got].numpy(), atol=1e-6)
 
 

@@ -31,6 +31,9 @@ def parse(spec):
         if path == "sweep":
             kw["sweep_every"] = int(val)
             continue
+        if path == "prio":    # prio:P: the steps run on a stream of priority P
+            kw["_prio"] = int(val)
+            continue
         if path == "env":     # env:NAME:value ('+' for ',' inside the value)
             k, _, v = val.partition(":")
             kw.setdefault("_env", {})[k] = v.replace("+", ",")
@@ -67,7 +70,12 @@ def main():
             torch.manual_seed(5)
             model = ncf.AdvancedNCF(U, I, 10, 50, D, D, 32, [256, 128, 64], 4, 0.2, M - 1).to(dev).train()
             step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5,
-                                  **{k: v for k, v in kw.items() if k != "_env"})
+                                  **{k: v for k, v in kw.items() if not k.startswith("_")})
+            prio = kw.get("_prio")
+            pstream = torch.cuda.Stream(dev, priority=prio) if prio is not None else None
+            if pstream is not None:
+                pstream.wait_stream(torch.cuda.current_stream(dev))
+                torch.cuda.set_stream(pstream)
             for k, v in saved.items():     # (read by the constructors above only)
                 if v is None:
                     os.environ.pop(k, None)
@@ -94,6 +102,9 @@ def main():
                     per[nm] = per.get(nm, 0.0) + e0.elapsed_time(e1) * 1e3 / 20
                 prof[name] = per
             print(f"rep {rep} {name:12s} {res[name][-1]:.4f} ms/step", flush=True)
+            if pstream is not None:
+                torch.cuda.synchronize()
+                torch.cuda.set_stream(torch.cuda.default_stream(dev))
             del step, model
             torch.cuda.empty_cache()
     for name, _, _ in variants:
