@@ -96,6 +96,17 @@ int ncf_gather_ln_gmf_scaled_fwd(const int64_t* user_ids, const int64_t* item_id
 /* Row gather (+ optional LayerNorm): EBC forward as read by callers (app.py:156-184) and
  * get_user_embeddings / get_product_embeddings (architecture.py:383-407).                   */
 /* bf16-table configuration: the training gather over bf16 table rows (fp32 outputs). */
+/* ncf_gather_ln_gmf_fwd over tables whose rows are table_ld floats apart (>= dim; the
+ * row-sharded step's received rows read in place: [mf | mlp] halves, table_ld = 2 D). */
+int ncf_gather_ln_gmf_ld_fwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
+                             const float* mf_user, const float* mf_item, const float* mlp_user,
+                             const float* mlp_item, int64_t num_users, int64_t num_items,
+                             int64_t dim, int64_t table_ld, const float* mf_gamma,
+                             const float* mf_beta, const float* mlp_gamma, const float* mlp_beta,
+                             const float* mf_out_w, const float* mf_out_b, float eps,
+                             int64_t group_rows, float* mf_pred, float* mlp_user_ln,
+                             float* mlp_item_ln, float* mf_user_ln, float* mf_item_ln,
+                             int* err_flag, void* stream);
 int ncf_gather_ln_gmf_bf16_fwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n,
                                const uint16_t* mf_user, const uint16_t* mf_item,
                                const uint16_t* mlp_user, const uint16_t* mlp_item,
@@ -510,7 +521,8 @@ int ncf_embedding_bwd_reduce(int64_t n, int64_t dim, int64_t num_users, int64_t 
 /* The same reduce writing unique row c's two gradient rows at row out_rows_*[c] (stride out_ld
  * floats) of the four gradient pointers: the row-sharded step hands its send buffer ([mf | mlp]
  * halves of 2 D floats per row: grad_mf_* = buf, grad_mlp_* = buf + D, out_ld = 2 D) instead of
- * compact rows it then re-orders (ncf_shard_rows). */
+ * compact rows it then re-orders (ncf_shard_rows); the four table pointers' rows are table_ld
+ * floats apart (its received rows read in place: 2 D). */
 int ncf_embedding_bwd_reduce_rows(int64_t n, int64_t dim, int64_t num_users, int64_t num_items,
                                   const float* dy_mf_user, const float* dy_mlp_user,
                                   const float* dy_mf_item, const float* dy_mlp_item,
@@ -521,7 +533,7 @@ int ncf_embedding_bwd_reduce_rows(int64_t n, int64_t dim, int64_t num_users, int
                                   float* grad_mlp_item, const int64_t* uniq_users,
                                   const int64_t* uniq_items, const int32_t* out_rows_users,
                                   const int32_t* out_rows_items, int64_t out_ld,
-                                  float* grad_mf_gamma, float* grad_mf_beta,
+                                  int64_t table_ld, float* grad_mf_gamma, float* grad_mf_beta,
                                   float* grad_mlp_gamma, float* grad_mlp_beta, void* workspace,
                                   int64_t workspace_bytes, ncf_reduce_list* defer, void* stream);
 /* bf16-table configuration: the same reduce with bf16 table rows (uint16 bit patterns). */
@@ -673,6 +685,12 @@ typedef struct ncf_shard_plan_out {
   int32_t* spos0;
   int32_t* spos1;
   int32_t* bounds;
+  /* optional (NULL: not written): spos as int64, and each row's send position
+   * rows0/1[r] = spos0/1[inv0/1[r]] — the row-sharded step reads its received rows in place */
+  int64_t* spos64_0;
+  int64_t* spos64_1;
+  int64_t* rows0;
+  int64_t* rows1;
 } ncf_shard_plan_out;
 typedef struct ncf_shard_recv {
   int32_t world;

@@ -41,6 +41,8 @@ SIGNATURES = {
     "ncf_event_synchronize": (I32, [P]),
     "ncf_memcpy_async": (I32, [P, P, I64, P]),
     "ncf_device_count": (I32, []),
+    "ncf_gather_ln_gmf_ld_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, I64, P, P, P, P, P, P,
+                                       F32, I64, P, P, P, P, P, P, P]),
     "ncf_gather_ln_gmf_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P, F32,
                                     P, P, P, P, P, P, P]),
     "ncf_gather_ln_gmf_scaled_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P,
@@ -117,8 +119,8 @@ SIGNATURES = {
     "ncf_comm_alltoallv": (I32, [P, P, P, P, P, I64, P]),
     "ncf_comm_allreduce_sum_f32": (I32, [P, P, I64, P]),
     "ncf_embedding_bwd_reduce_rows": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32,
-                                            P, P, P, P, P, P, P, P, I64, P, P, P, P, P, I64, P,
-                                            P]),
+                                            P, P, P, P, P, P, P, P, I64, I64, P, P, P, P, P, I64,
+                                            P, P]),
     "ncf_embedding_bwd_reduce": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
                                        P, P, P, P, P, P, P, P, P, I64, P, P]),
     "ncf_embedding_bwd_reduce_bf16": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32,
@@ -229,7 +231,8 @@ SHARD_MAX_WORLD = 64
 class ShardPlanOut(ctypes.Structure):
     """ncf_shard_plan_out (include/ncf_hip.h)."""
     _fields_ = [(f, P) for f in ("keys0", "keys1", "uniq0", "uniq1", "num_unique", "inv0", "inv1",
-                                 "counts", "send", "spos0", "spos1", "bounds")]
+                                 "counts", "send", "spos0", "spos1", "bounds", "spos64_0",
+                                 "spos64_1", "rows0", "rows1")]
 
 
 class ShardRecv(ctypes.Structure):

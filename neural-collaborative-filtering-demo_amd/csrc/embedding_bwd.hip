@@ -44,7 +44,8 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     const float* __restrict__ g_mlp, float eps, float* __restrict__ G_mf0,
     float* __restrict__ G_mlp0, float* __restrict__ G_mf1, float* __restrict__ G_mlp1,
     float* __restrict__ xp0, float* __restrict__ xp1, float* __restrict__ part,
-    const int32_t* __restrict__ omap0, const int32_t* __restrict__ omap1, int64_t ldo) {
+    const int32_t* __restrict__ omap0, const int32_t* __restrict__ omap1, int64_t ldo,
+    int64_t ldt) {
   constexpr int L = D / 4;
   constexpr int S = 64 / L;  // lane groups (pieces) per wave
   __shared__ __attribute__((aligned(16))) float red[kPW][4 * D];
@@ -81,8 +82,8 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
       cnt = (int)(pstart[p + 1] - ps);  // 1..PIECE
       info = pseg[p];
       const int64_t id = uniq[info & ~FIRST_PIECE];
-      x_mf = ldp4<BF>(tmf, id * D + col);   // (BF: bf16 table rows, widened exactly)
-      x_ml = ldp4<BF>(tml, id * D + col);
+      x_mf = ldp4<BF>(tmf, id * ldt + col);   // (BF: bf16 table rows, widened exactly)
+      x_ml = ldp4<BF>(tml, id * ldt + col);
     }
     int cmax = cnt;   // the wave's longest piece: loop bounds stay wave-uniform
 #pragma unroll
@@ -515,17 +516,17 @@ int piece_reduce(const WS& w, int64_t n, const uint32_t* sv0, const uint32_t* sv
                  float eps, float* Gmf0, float* Gml0, float* Gmf1, float* Gml1, float* dgm,
                  float* dbm, float* dgl, float* dbl, ncf_reduce_list* defer, hipStream_t st,
                  bool bf = false, const int32_t* omap0 = nullptr, const int32_t* omap1 = nullptr,
-                 int64_t ldo = D) {
+                 int64_t ldo = D, int64_t ldt = D) {
   if (bf)
     hipLaunchKernelGGL((k_piece_reduce_ln<D, true>), dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1,
                        w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
                        dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
-                       Gmf1, Gml1, w.xp0, w.xp1, w.part, omap0, omap1, ldo);
+                       Gmf1, Gml1, w.xp0, w.xp1, w.part, omap0, omap1, ldo, ldt);
   else
     hipLaunchKernelGGL((k_piece_reduce_ln<D, false>), dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1,
                        w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
                        dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
-                       Gmf1, Gml1, w.xp0, w.xp1, w.part, omap0, omap1, ldo);
+                       Gmf1, Gml1, w.xp0, w.xp1, w.part, omap0, omap1, ldo, ldt);
   NCF_CHECK_LAUNCH("ncf_embedding_bwd(piece_reduce)");
   constexpr int L = D / 4;
   const int64_t fb = ncf_cdiv(n * L, 256);
@@ -567,7 +568,8 @@ static int embedding_bwd_reduce(bool bf, int64_t n, int64_t dim, int64_t num_use
                                         float* grad_mlp_beta, void* workspace,
                                         int64_t workspace_bytes, ncf_reduce_list* defer,
                                         void* stream, const int32_t* omap0 = nullptr,
-                                        const int32_t* omap1 = nullptr, int64_t ldo = 0) {
+                                        const int32_t* omap1 = nullptr, int64_t ldo = 0,
+                                        int64_t ldt = 0) {
   NCF_CHECK_ARG(n >= 0 && n < (1ll << 30), "ncf_embedding_bwd_reduce: bad n");
   NCF_CHECK_ARG(dim == 16 || dim == 32 || dim == 64 || dim == 128 || dim == 256,
                 "ncf_embedding_bwd_reduce: dim must be 16/32/64/128/256");
@@ -579,7 +581,7 @@ static int embedding_bwd_reduce(bool bf, int64_t n, int64_t dim, int64_t num_use
   WS w = carve(workspace, n, dim);
   uint32_t *k0, *v0, *k1, *v1;
   sorted_bufs(w, sort_passes(num_users, num_items), &k0, &v0, &k1, &v1);
-  const bool mapped = omap0 != nullptr;
+  const bool mapped = omap0 != nullptr || (ldt != 0 && ldt != dim);
   if (n > 0 && use_pos_reduce() && !mapped) {
     switch (dim) {
 #define POS(DD)                                                                                   \
@@ -600,7 +602,8 @@ static int embedding_bwd_reduce(bool bf, int64_t n, int64_t dim, int64_t num_use
                             dy_mf_item, dy_mlp_item, mf_user, mlp_user, mf_item, mlp_item,        \
                             mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user, grad_mf_item,  \
                             grad_mlp_item, grad_mf_gamma, grad_mf_beta, grad_mlp_gamma,           \
-                            grad_mlp_beta, defer, st, bf, omap0, omap1, mapped ? ldo : DD);
+                            grad_mlp_beta, defer, st, bf, omap0, omap1, omap0 ? ldo : DD,     \
+                            ldt ? ldt : DD);
     SEG(16) SEG(32) SEG(64) SEG(128) SEG(256)
 #undef SEG
   }
@@ -639,17 +642,18 @@ extern "C" int ncf_embedding_bwd_reduce_rows(
     const float* mf_gamma, const float* mlp_gamma, float eps, float* grad_mf_user,
     float* grad_mlp_user, float* grad_mf_item, float* grad_mlp_item, const int64_t* uniq_users,
     const int64_t* uniq_items, const int32_t* out_rows_users, const int32_t* out_rows_items,
-    int64_t out_ld, float* grad_mf_gamma, float* grad_mf_beta, float* grad_mlp_gamma,
-    float* grad_mlp_beta, void* workspace, int64_t workspace_bytes, ncf_reduce_list* defer,
-    void* stream) {
-  NCF_CHECK_ARG(out_rows_users && out_rows_items && out_ld >= dim,
-                "ncf_embedding_bwd_reduce_rows: out_rows and out_ld >= dim required");
+    int64_t out_ld, int64_t table_ld, float* grad_mf_gamma, float* grad_mf_beta,
+    float* grad_mlp_gamma, float* grad_mlp_beta, void* workspace, int64_t workspace_bytes,
+    ncf_reduce_list* defer, void* stream) {
+  NCF_CHECK_ARG(out_rows_users && out_rows_items && out_ld >= dim && table_ld >= dim &&
+                    table_ld % 4 == 0,
+                "ncf_embedding_bwd_reduce_rows: out_rows, out_ld >= dim, table_ld >= dim");
   return embedding_bwd_reduce(false, n, dim, num_users, num_items, dy_mf_user, dy_mlp_user,
                               dy_mf_item, dy_mlp_item, mf_user, mlp_user, mf_item, mlp_item,
                               mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user, grad_mf_item,
                               grad_mlp_item, uniq_users, uniq_items, grad_mf_gamma, grad_mf_beta,
                               grad_mlp_gamma, grad_mlp_beta, workspace, workspace_bytes, defer,
-                              stream, out_rows_users, out_rows_items, out_ld);
+                              stream, out_rows_users, out_rows_items, out_ld, table_ld);
 }
 
 // The same with bf16 table rows (the LayerNorm recompute reads them; gradients stay fp32).

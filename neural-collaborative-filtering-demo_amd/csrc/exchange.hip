@@ -95,6 +95,20 @@ __global__ void k_shard_send(const int64_t* __restrict__ uq0, const int64_t* __r
   (k ? spos1 : spos0)[c] = pos;
 }
 
+// rows?[r] = spos?[inv?[r]]: row r's send position (its received row, read in place by the
+// forward gather); the int64 copies of spos are the embedding backward's table-row ids
+__global__ void k_shard_rowpos(const int64_t* __restrict__ inv0, const int64_t* __restrict__ inv1,
+                               const int32_t* __restrict__ spos0, const int32_t* __restrict__ spos1,
+                               const uint32_t* __restrict__ num_unique, int64_t n,
+                               int64_t* __restrict__ sp64_0, int64_t* __restrict__ sp64_1,
+                               int64_t* __restrict__ rows0, int64_t* __restrict__ rows1) {
+  const int k = blockIdx.y;
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t* sp = k ? spos1 : spos0;
+  if (r < n) (k ? rows1 : rows0)[r] = (int64_t)sp[(k ? inv1 : inv0)[r]];
+  if (r < (int64_t)num_unique[k]) (k ? sp64_1 : sp64_0)[r] = (int64_t)sp[r];
+}
+
 // ---- owner ---------------------------------------------------------------------------------
 // source rank and kind of received entry j
 __device__ __forceinline__ void recv_src(const ncf_shard_recv& L, int32_t j, int& s, int& kind) {
@@ -290,6 +304,12 @@ extern "C" int ncf_shard_plan(const int64_t* user_ids, const int64_t* item_ids, 
                        o->uniq1, o->num_unique, world, R0, R1, o->bounds, o->send, o->spos0,
                        o->spos1);
     NCF_CHECK_LAUNCH("ncf_shard_plan(send)");
+    if (o->spos64_0 && o->spos64_1 && o->rows0 && o->rows1) {
+      hipLaunchKernelGGL(k_shard_rowpos, dim3(ncf_cdiv(n, 256), 2), dim3(256), 0, st, o->inv0,
+                         o->inv1, o->spos0, o->spos1, o->num_unique, n, o->spos64_0, o->spos64_1,
+                         o->rows0, o->rows1);
+      NCF_CHECK_LAUNCH("ncf_shard_plan(rowpos)");
+    }
   }
   return NCF_OK;
 }

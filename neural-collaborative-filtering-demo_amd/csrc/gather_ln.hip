@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
     const float* __restrict__ w_mf, const float* __restrict__ bias_mf, float eps,
     float* __restrict__ mf_pred, float* __restrict__ u_mlp_ln, float* __restrict__ i_mlp_ln,
     float* __restrict__ u_mf_ln, float* __restrict__ i_mf_ln, int* err,
-    const float* __restrict__ item_scale, float scale_factor, int64_t G) {
+    const float* __restrict__ item_scale, float scale_factor, int64_t G, int64_t ldt) {
   constexpr int L = D / 4;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t row = t / L;
@@ -67,8 +67,9 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
   const bool src = G <= 1 || row % G == 0 || uraw != uid[row - row % G];
   const int c = sub * 4;
   // (BF: the table rows are bf16; widened exactly to fp32 here, everything after is fp32)
-  const float4 xu_mf = ldp4<BF>(mfU, u * D + c), xi_mf = ldp4<BF>(mfI, i * D + c);
-  const float4 xi_ml = ldp4<BF>(mlpI, i * D + c);
+  // (ldt: the tables' row stride in elements — D, or the row-sharded step's received rows)
+  const float4 xu_mf = ldp4<BF>(mfU, u * ldt + c), xi_mf = ldp4<BF>(mfI, i * ldt + c);
+  const float4 xi_ml = ldp4<BF>(mlpI, i * ldt + c);
   const float4 gm = ld4(g_mf + c), bm = ld4(b_mf + c), gl = ld4(g_mlp + c), bl = ld4(b_mlp + c);
   const float4 yu = RowLN<D>::ln(xu_mf, gm, bm, eps);
   float4 yi = RowLN<D>::ln(xi_mf, gm, bm, eps);
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
   dot = group_sum<L>(dot);
   if (sub == 0) mf_pred[row] = dot + bias_mf[0];
   if (src) {   // (uniform in the row's lane group: its shuffles stay within active lanes)
-    const float4 xu_ml = ldp4<BF>(mlpU, u * D + c);
+    const float4 xu_ml = ldp4<BF>(mlpU, u * ldt + c);
     st4(u_mlp_ln + row * D + c, RowLN<D>::ln(xu_ml, gl, bl, eps));
     if (u_mf_ln) st4(u_mf_ln + row * D + c, yu);
   }
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
     const float* __restrict__ b_mf, const float* __restrict__ g_mlp, const float* __restrict__ b_mlp,
     const float* __restrict__ w_mf, const float* __restrict__ bias_mf, float eps,
     float* __restrict__ mf_pred, float* __restrict__ u_mlp_ln, float* __restrict__ i_mlp_ln,
-    float* __restrict__ u_mf_ln, float* __restrict__ i_mf_ln, int* err, int64_t G) {
+    float* __restrict__ u_mf_ln, float* __restrict__ i_mf_ln, int* err, int64_t G, int64_t ldt) {
   static_assert(F4 == 2, "two float4 per lane");
   constexpr int L = D / 8, H2 = D / 2;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -142,13 +143,13 @@ __global__ __launch_bounds__(256) void k_gather_ln_gmf(
   const int64_t i = safe_id(iid[row], nI, err, sub == 0);
   const bool src = G <= 1 || row % G == 0 || uraw != uid[row - row % G];
   const int c0 = sub * 4, c1 = c0 + H2;
-  float4 u0 = ldp4<BF>(mfU, u * D + c0), u1 = ldp4<BF>(mfU, u * D + c1);
-  float4 i0 = ldp4<BF>(mfI, i * D + c0), i1 = ldp4<BF>(mfI, i * D + c1);
-  float4 z0 = ldp4<BF>(mlpI, i * D + c0), z1 = ldp4<BF>(mlpI, i * D + c1);
+  float4 u0 = ldp4<BF>(mfU, u * ldt + c0), u1 = ldp4<BF>(mfU, u * ldt + c1);
+  float4 i0 = ldp4<BF>(mfI, i * ldt + c0), i1 = ldp4<BF>(mfI, i * ldt + c1);
+  float4 z0 = ldp4<BF>(mlpI, i * ldt + c0), z1 = ldp4<BF>(mlpI, i * ldt + c1);
   float4 m0 = make_float4(0.f, 0.f, 0.f, 0.f), m1 = m0;
   if (src) {   // (uniform in the row's lane group)
-    m0 = ldp4<BF>(mlpU, u * D + c0);
-    m1 = ldp4<BF>(mlpU, u * D + c1);
+    m0 = ldp4<BF>(mlpU, u * ldt + c0);
+    m1 = ldp4<BF>(mlpU, u * ldt + c1);
   }
   const float4 gm0 = ld4(g_mf + c0), gm1 = ld4(g_mf + c1), bm0 = ld4(b_mf + c0), bm1 = ld4(b_mf + c1);
   const float4 gl0 = ld4(g_mlp + c0), gl1 = ld4(g_mlp + c1), bl0 = ld4(b_mlp + c0), bl1 = ld4(b_mlp + c1);
@@ -210,21 +211,22 @@ int launch_gather_ln_gmf(const int64_t* uid, const int64_t* iid, int64_t n, cons
                          const float* b_mlp, const float* w_mf, const float* bias_mf, float eps,
                          float* mf_pred, float* u_mlp_ln, float* i_mlp_ln, float* u_mf_ln,
                          float* i_mf_ln, int* err, const float* item_scale, float scale_factor,
-                         int64_t G, hipStream_t st) {
+                         int64_t G, hipStream_t st, int64_t ldt = D) {
   // D/8 lanes per row (the same bits; measured in-step 11.4-11.6 us either way at C2, rocprof
   // 10.1 against 10.3 us fp32 tables and 8.7 against 9.3 us bf16 tables)
   if (D >= 32 && item_scale == nullptr) {
     const int64_t threads = n * (D / 8);
     hipLaunchKernelGGL((k_gather_ln_gmf<D, BF, 2>), dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st,
                        uid, iid, n, mfU, mfI, mlpU, mlpI, nU, nI, g_mf, b_mf, g_mlp, b_mlp, w_mf,
-                       bias_mf, eps, mf_pred, u_mlp_ln, i_mlp_ln, u_mf_ln, i_mf_ln, err, G);
+                       bias_mf, eps, mf_pred, u_mlp_ln, i_mlp_ln, u_mf_ln, i_mf_ln, err, G, ldt);
     NCF_CHECK_LAUNCH("ncf_gather_ln_gmf_fwd");
     return NCF_OK;
   }
   const int64_t threads = n * (D / 4);
   hipLaunchKernelGGL((k_gather_ln_gmf<D, BF>), dim3(ncf_cdiv(threads, 256)), dim3(256), 0, st, uid, iid,
                      n, mfU, mfI, mlpU, mlpI, nU, nI, g_mf, b_mf, g_mlp, b_mlp, w_mf, bias_mf, eps,
-                     mf_pred, u_mlp_ln, i_mlp_ln, u_mf_ln, i_mf_ln, err, item_scale, scale_factor, G);
+                     mf_pred, u_mlp_ln, i_mlp_ln, u_mf_ln, i_mf_ln, err, item_scale, scale_factor, G,
+                     ldt);
   NCF_CHECK_LAUNCH("ncf_gather_ln_gmf_fwd");
   return NCF_OK;
 }
@@ -295,6 +297,42 @@ extern "C" int ncf_gather_ln_gmf_scaled_fwd(
                  mlp_item, num_users, num_items, mf_gamma, mf_beta, mlp_gamma, mlp_beta, mf_out_w,
                  mf_out_b, eps, mf_pred, mlp_user_ln, mlp_item_ln, mf_user_ln, mf_item_ln,
                  err_flag, item_scale, scale_factor, group_rows, (hipStream_t)stream);
+}
+
+// The same gather over tables whose rows are table_ld elements apart (>= dim): the row-sharded
+// step reads its received rows in place ([mf | mlp] halves of 2 D floats: mf_* = rows, mlp_* =
+// rows + D, table_ld = 2 D) instead of copying them into compact mini tables first.
+template <int D>
+int launch_gather_ln_gmf_ld(const int64_t* uid, const int64_t* iid, int64_t n, const float* mfU,
+                            const float* mfI, const float* mlpU, const float* mlpI, int64_t nU,
+                            int64_t nI, const float* g_mf, const float* b_mf, const float* g_mlp,
+                            const float* b_mlp, const float* w_mf, const float* bias_mf,
+                            float eps, float* mf_pred, float* u_mlp_ln, float* i_mlp_ln,
+                            float* u_mf_ln, float* i_mf_ln, int* err, int64_t G, int64_t ldt,
+                            hipStream_t st) {
+  return launch_gather_ln_gmf<D, false>(uid, iid, n, mfU, mfI, mlpU, mlpI, nU, nI, g_mf, b_mf,
+                                        g_mlp, b_mlp, w_mf, bias_mf, eps, mf_pred, u_mlp_ln,
+                                        i_mlp_ln, u_mf_ln, i_mf_ln, err, nullptr, 0.0f, G, st, ldt);
+}
+
+extern "C" int ncf_gather_ln_gmf_ld_fwd(
+    const int64_t* user_ids, const int64_t* item_ids, int64_t n, const float* mf_user,
+    const float* mf_item, const float* mlp_user, const float* mlp_item, int64_t num_users,
+    int64_t num_items, int64_t dim, int64_t table_ld, const float* mf_gamma, const float* mf_beta,
+    const float* mlp_gamma, const float* mlp_beta, const float* mf_out_w, const float* mf_out_b,
+    float eps, int64_t group_rows, float* mf_pred, float* mlp_user_ln, float* mlp_item_ln,
+    float* mf_user_ln, float* mf_item_ln, int* err_flag, void* stream) {
+  NCF_CHECK_ARG(n >= 0 && group_rows >= 0 && table_ld >= dim && table_ld % 4 == 0,
+                "ncf_gather_ln_gmf_ld_fwd: bad n / group_rows / table_ld");
+  if (n == 0) return NCF_OK;
+  NCF_CHECK_ARG(user_ids && item_ids && mf_user && mf_item && mlp_user && mlp_item && mf_pred &&
+                    mlp_user_ln && mlp_item_ln && mf_gamma && mf_beta && mlp_gamma && mlp_beta &&
+                    mf_out_w && mf_out_b,
+                "ncf_gather_ln_gmf_ld_fwd: null pointer");
+  NCF_DISPATCH_D(dim, launch_gather_ln_gmf_ld, user_ids, item_ids, n, mf_user, mf_item, mlp_user,
+                 mlp_item, num_users, num_items, mf_gamma, mf_beta, mlp_gamma, mlp_beta, mf_out_w,
+                 mf_out_b, eps, mf_pred, mlp_user_ln, mlp_item_ln, mf_user_ln, mf_item_ln,
+                 err_flag, group_rows, table_ld, (hipStream_t)stream);
 }
 
 extern "C" int ncf_gather_ln_gmf_fwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n,

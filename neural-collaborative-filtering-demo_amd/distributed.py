@@ -55,6 +55,10 @@ GSUM_APPLY = True
 # The requester's table gradients written by the embedding backward straight into its send
 # buffer (ncf_embedding_bwd_reduce_rows; False: compact rows, then ncf_shard_rows)
 GRAD_ROWS = True
+# The requester's forward gather and embedding backward read the received rows in place (each
+# batch row at its send position; ncf_gather_ln_gmf_ld_fwd, table_ld = 2 D) instead of copying
+# them into compact mini tables first (ncf_shard_rows); needs GRAD_ROWS
+BACK_ROWS = True
 
 
 class ShardExchange:
@@ -434,7 +438,9 @@ class ShardedTrainStep:
             h = w.cache.get("head_args")
             if h is not None:
                 h.targets, h.grad_prob = ptr(targets), None
-                h.user_ids = ptr(plan.extra["set"]["inv"][0])   # (this step's mini-table ids)
+                # (this step's user row ids: send positions read in place, or mini-table ids)
+                h.user_ids = ptr(plan.extra["set"]["rowpos" if BACK_ROWS and GRAD_ROWS
+                                                  else "inv"][0])
         scalars = (own["token"], own["nmax"], max(nu, ni))
         if next is not None and (not next[0].is_contiguous() or not next[1].is_contiguous()
                                  or next[0].dtype != torch.int64 or next[1].dtype != torch.int64):
@@ -595,6 +601,8 @@ class HipShardOps:
                 inv=[torch.empty(cap, **i64) for _ in range(2)],
                 counts=torch.zeros(self.W, 2, **i64), send=torch.empty(2 * cap, **i32),
                 spos=[torch.empty(cap, **i32) for _ in range(2)],
+                spos64=[torch.empty(cap, **i64) for _ in range(2)],
+                rowpos=[torch.empty(cap, **i64) for _ in range(2)],
                 bounds=torch.empty(3 * (self.W + 1), **i32),
                 counts_both=torch.zeros(2 * self.W, 2, **i64),
                 counts_host=torch.zeros(2 * self.W, 2, dtype=torch.int64, pin_memory=True),
@@ -610,6 +618,8 @@ class HipShardOps:
             o.counts, o.send = ptr(s["counts"]), ptr(s["send"])
             o.spos0, o.spos1 = ptr(s["spos"][0]), ptr(s["spos"][1])
             o.bounds = ptr(s["bounds"])
+            o.spos64_0, o.spos64_1 = ptr(s["spos64"][0]), ptr(s["spos64"][1])
+            o.rows0, o.rows1 = ptr(s["rowpos"][0]), ptr(s["rowpos"][1])
         return s
 
     def mark_entry(self):
@@ -725,38 +735,55 @@ class HipShardOps:
         n = plan.extra["n"]
         nu, ni = plan.totals()
         D = self.D
-        # mini tables: four [n][D] slabs of one buffer sized for the batch (unique rows <= n)
-        base = ptr(self._buf("mini", (4, max(n, 1), D)))
-        slab = 4 * max(n, 1) * D
-        mini = {"mf_user": base, "mlp_user": base + slab, "mf_item": base + 2 * slab,
-                "mlp_item": base + 3 * slab}
-        _lib.call_tagged("ncf_shard_rows", {4: SLOT_NUNI}, ptr(back), ptr(s["spos"][0]),
-                         ptr(s["spos"][1]), ptr(s["num_unique"]), max(nu, ni), D, mini["mf_user"],
-                         mini["mlp_user"], mini["mf_item"], mini["mlp_item"], 0, st)
+        back_rows = BACK_ROWS and GRAD_ROWS
+        if back_rows:
+            # the received rows read in place: [mf | mlp] halves, 2 D floats a row, each batch row
+            # at its send position (the plan's rowpos)
+            bp = ptr(back)
+            mini = {"mf_user": bp, "mlp_user": bp + 4 * D, "mf_item": bp, "mlp_item": bp + 4 * D}
+        else:
+            # mini tables: four [n][D] slabs of one buffer sized for the batch (unique rows <= n)
+            base = ptr(self._buf("mini", (4, max(n, 1), D)))
+            slab = 4 * max(n, 1) * D
+            mini = {"mf_user": base, "mlp_user": base + slab, "mf_item": base + 2 * slab,
+                    "mlp_item": base + 3 * slab}
+            _lib.call_tagged("ncf_shard_rows", {4: SLOT_NUNI}, ptr(back), ptr(s["spos"][0]),
+                             ptr(s["spos"][1]), ptr(s["num_unique"]), max(nu, ni), D,
+                             mini["mf_user"], mini["mlp_user"], mini["mf_item"],
+                             mini["mlp_item"], 0, st)
         m = self.model
         drop_p = float(m.dropout)
         seed = 0      # the dropout stream comes from the device clock's per-step seed
-        inv_u, inv_i = s["inv"][0][:n], s["inv"][1][:n]
+        if back_rows:
+            inv_u, inv_i = s["rowpos"][0][:n], s["rowpos"][1][:n]
+            rb = max(nu + ni, 1)           # (rows of the received buffer)
+            bounds, ld = (rb, rb), 2 * D
+            uq = (s["spos64"][0], s["spos64"][1])
+        else:
+            inv_u, inv_i = s["inv"][0][:n], s["inv"][1][:n]
+            # (mini-table bounds: the batch size, a bound of the unique-row counts that does not
+            # change per step; the plan's inverse ids are always in range)
+            bounds, ld = (max(n, 1), max(n, 1)), None
+            ar = self._buf("arange", (max(n, 1),), torch.int64)
+            if self._bufs.get("arange_n") != ar.numel():
+                torch.arange(ar.numel(), out=ar)
+                self._bufs["arange_n"] = ar.numel()
+            uq = (ar, ar)
         w = eng.workspace(n, self.M, True)
         w.emb_ws = s["ws"]            # the plan's dedup segments drive the segment reduce
 
         def mark(wk, u, i, st_):
             wk.deduped = True
-        # (mini-table bounds: the batch size, a bound of the unique-row counts that does not
-        # change per step; the plan's inverse ids are always in range)
         eng.forward(inv_u, inv_i, self.M, True, drop_p, seed, prepare=mark, tables=mini,
-                    rows=(max(n, 1), max(n, 1)))
-        ar = self._buf("arange", (max(n, 1),), torch.int64)
-        if self._bufs.get("arange_n") != ar.numel():
-            torch.arange(ar.numel(), out=ar)
-            self._bufs["arange_n"] = ar.numel()
+                    rows=bounds, table_ld=ld)
         g = self._buf("send_grads", (max(2 * n, 1), 2 * D))      # (nu + ni <= 2 n rows)
         # the table gradients straight into the send buffer at their send positions
         # (GRAD_ROWS; else compact rows, then ncf_shard_rows re-orders them)
         eng.backward(w, inv_u, inv_i, None, targets, drop_p, seed,
                      loss_denominator=loss_denominator, tables=mini,
-                     rows=(self.W * self.Ru, self.W * self.Ri), uniq=(ar, ar),
-                     grad_rows=(g, s["spos"][0], s["spos"][1]) if GRAD_ROWS else None)
+                     rows=(self.W * self.Ru, self.W * self.Ri), uniq=uq,
+                     grad_rows=(g, s["spos"][0], s["spos"][1]) if GRAD_ROWS else None,
+                     table_ld=ld)
         eng.pending = None
         if not GRAD_ROWS:
             _lib.call_tagged("ncf_shard_rows", {4: SLOT_NUNI}, ptr(g), ptr(s["spos"][0]),

@@ -411,13 +411,14 @@ class NCFEngine:
 
     def forward(self, uid: torch.Tensor, iid: torch.Tensor, M: int, train: bool,
                 drop_p: float, seed: int, prepare=None, tables=None, rows=None,
-                temporal=None, bf16: bool = False) -> Workspace:
+                temporal=None, bf16: bool = False, table_ld: Optional[int] = None) -> Workspace:
         """AdvancedNCF.forward (architecture.py:258-381) on single-id bags; returns the workspace
         holding prob (and, when ``train``, everything the backward needs).  ``prepare(w, uid,
         iid, stream)`` runs before the gathers (the deferred Adam dedups the ids there and
         brings exactly those rows current).  ``temporal = (item_scale [n,D], factor, te [n,T])``
         is forward_simple's hour path (eval, M = 1): item rows scaled in the gather and the MLP
-        fed [attention ‖ te] instead of [attention ‖ 0]."""
+        fed [attention ‖ te] instead of [attention ‖ 0].  ``table_ld``: the ``tables`` rows are
+        that many floats apart (the row-sharded step's received rows read in place)."""
         dev = self._check_device()
         self.ensure_layout()
         m = self.model
@@ -453,7 +454,15 @@ class NCFEngine:
         G = M if (GROUP_ROWS and ATTN_SHARE_Q and train and M > 1 and temporal is None
                   and self.attn_block(D, H, M) and self.mlp_fused(D, hid)) else 0
         w.group_rows = G
-        if bf16:    # bf16 tables (``tables`` holds them): rows widened to fp32 in the gather
+        if table_ld is not None and table_ld != D:
+            if bf16 or temporal is not None:
+                raise ValueError("table_ld: fp32 tables, no temporal scaling")
+            _lib.call("ncf_gather_ln_gmf_ld_fwd", ptr(uid), ptr(iid), n, *tbp, n_users, n_items, D,
+                      int(table_ld), pp["mf_norm.weight"], pp["mf_norm.bias"],
+                      pp["mlp_norm.weight"], pp["mlp_norm.bias"], pp["mf_output.weight"],
+                      pp["mf_output.bias"], LN_EPS, G, ptr(w.mf_pred), ptr(w.xu), ptr(w.xi),
+                      ptr(w.umf), ptr(w.imf), ptr(w.err), st)
+        elif bf16:    # bf16 tables (``tables`` holds them): rows widened to fp32 in the gather
             if temporal is not None:
                 raise ValueError("the bf16-table configuration is a training configuration")
             _lib.call("ncf_gather_ln_gmf_bf16_fwd", ptr(uid), ptr(iid), n, *tbp, n_users,
@@ -752,7 +761,8 @@ class NCFEngine:
     def backward(self, w: Workspace, uid, iid, grad_prob: Optional[torch.Tensor],
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,
                  loss_denominator: float = 0.0, tables=None, rows=None, uniq=None,
-                 reduce_async: bool = False, bf16: bool = False, grad_rows=None):
+                 reduce_async: bool = False, bf16: bool = False, grad_rows=None,
+                 table_ld: Optional[int] = None):
         """Gradients of every used parameter.  Dense grads land in the flat grad buffer; table
         grads stay compact (self.pending) for the fused Adam step.  ``reduce_async``: the
         deferred reductions (every dense gradient) run on a side stream, beside whatever the
@@ -903,6 +913,8 @@ class NCFEngine:
                       ptr(w.uniq_u), ptr(w.uniq_i), ptr(self.slot_u), ptr(self.slot_i),
                       ptr(w.num_unique), ptr(w.emb_ws), w.emb_ws.numel(), st)
             w.slots_set = True
+        if table_ld is not None and table_ld != D and grad_rows is None:
+            raise ValueError("table_ld: the backward takes it with grad_rows only")
         if grad_rows is not None:
             if bf16:
                 raise ValueError("grad_rows: fp32 tables only")
@@ -911,7 +923,7 @@ class NCFEngine:
             _lib.call("ncf_embedding_bwd_reduce_rows", n, D, d_rows[0], d_rows[1],
                       ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi), *tbp,
                       pp["mf_norm.weight"], pp["mlp_norm.weight"], LN_EPS, gmf, gml, gmf, gml,
-                      ptr(uq_u), ptr(uq_i), ptr(ru_), ptr(ri_), 2 * D,
+                      ptr(uq_u), ptr(uq_i), ptr(ru_), ptr(ri_), 2 * D, int(table_ld or D),
                       self.gptr("mf_norm.weight"), self.gptr("mf_norm.bias"),
                       self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
                       w.emb_ws.numel(), w.red_list.address, st)

@@ -329,7 +329,7 @@ def test_shard_struct_mirrors_match_header():
     body = hdr[hdr.index("typedef struct ncf_shard_plan_out"):hdr.index("} ncf_shard_plan_out;")]
     names = re.findall(r"\*\s*(\w+);", body)
     assert names == [f[0] for f in _lib.ShardPlanOut._fields_]
-    assert ctypes.sizeof(_lib.ShardPlanOut) == 12 * 8
+    assert ctypes.sizeof(_lib.ShardPlanOut) == 16 * 8
     wmax = int(re.search(r"#define NCF_SHARD_MAX_WORLD (\d+)", hdr).group(1))
     assert wmax == _lib.SHARD_MAX_WORLD
     assert ctypes.sizeof(_lib.ShardRecv) == 4 * (1 + (wmax + 1) + wmax)
