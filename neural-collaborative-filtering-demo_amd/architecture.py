@@ -305,9 +305,10 @@ class AdvancedNCF(nn.Module):
             if uid.numel() != iid.numel():
                 raise ValueError("forward_simple: user_ids and product_ids differ in length")
             out = _NCFTrainFunction.apply(eng, uid, iid, 1, drop_p, seed, self._anchor)
-            if getattr(self, "validate_ids", True):
+            v = getattr(self, "validate_ids", True)
+            if v:
                 ws = eng.ws[(uid.numel(), 1, True)]
-                if self.validate_ids != "sync":
+                if v != "sync":
                     eng.check_ids_async(ws)
                 else:
                     eng.check_ids(ws)

@@ -756,7 +756,9 @@ class HipShardOps:
         seed = 0      # the dropout stream comes from the device clock's per-step seed
         if back_rows:
             inv_u, inv_i = s["rowpos"][0][:n], s["rowpos"][1][:n]
-            rb = max(nu + ni, 1)           # (rows of the received buffer)
+            # (bound of the send positions: 2 n >= nu + ni, fixed per batch size — a launch tape
+            # replays this call's scalars, so a per-step count would go stale)
+            rb = max(2 * n, 1)
             bounds, ld = (rb, rb), 2 * D
             uq = (s["spos64"][0], s["spos64"][1])
         else:
