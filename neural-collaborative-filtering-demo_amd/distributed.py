@@ -47,7 +47,7 @@ from ._lib import ptr
 # launch-tape slots of the row-sharded step (tapes.py): pointer ranges first (the next batch's
 # ids, the targets, the compute stream), then the per-step scalars
 SLOT_NEXT_U, SLOT_NEXT_I, SLOT_TARGETS, SLOT_STREAM = 0, 1, 2, 3
-SLOT_TOKEN, SLOT_NMAX, SLOT_NUNI = 4, 5, 6
+SLOT_TOKEN, SLOT_NMAX, SLOT_NUNI, SLOT_TOKEN_NEXT = 4, 5, 6, 7
 TAPE_SHARDED = os.environ.get("NCF_TAPE", "1") != "0"
 # The owner's rank-order gradient sum inside the table Adam's apply (ncf_adam_pairs_apply_gsum_clock,
 # one launch and no compact gradient round trip; False: ncf_shard_owner_gradsum + the apply)
@@ -59,6 +59,13 @@ GRAD_ROWS = True
 # batch row at its send position; ncf_gather_ln_gmf_ld_fwd, table_ld = 2 D) instead of copying
 # them into compact mini tables first (ncf_shard_rows); needs GRAD_ROWS
 BACK_ROWS = True
+# The owner's claim of the next step's rows (dedup + positions, ncf_shard_owner_prepare) run a
+# step ahead on the plan stream, right behind the exchange that sends them (ahead mode); the step
+# itself then only catches those rows up.  Same bits (tools/shard_bisect.py).  Off: measured at
+# world 1 (2 interleaved runs each) 0.3292 / 0.3638 ms/step against 0.3305 / 0.3282 without —
+# the claim leaves the critical path (17.7 -> 5.7 us) but the plan stream's extra work beside
+# the fused backward slows it by as much (110 -> 122 us)
+CLAIM_AHEAD = False
 
 
 class ShardExchange:
@@ -342,20 +349,46 @@ class ShardedTrainStep:
         self.x.counts_issue(p)
         return p
 
+    def _claims_ahead(self):
+        return CLAIM_AHEAD and hasattr(self.ops, "owner_claim")
+
+    def _claim_ahead(self, nxt, ahead, token_slot=SLOT_TOKEN):
+        """Step t+1's owner claim (dedup + positions of the rows it was just sent) on the plan
+        stream behind their exchange; the ahead event is recorded again behind it, so the step
+        that uses it waits for both.  Returns its owner state (owner_host)."""
+        ops = self.ops
+        own = ops.owner_host(nxt)
+        ps = nxt.stream
+        ops.owner_claim(ahead[0], own, ps.cuda_stream, token_slot)
+        ev = ahead[1]
+        if isinstance(ev, _lib.RawEvent):
+            ev.record(ps.cuda_stream)
+        elif ev is not None:
+            ev.record(ps)
+        return own
+
+    def _settle_pending(self, pend):
+        """A pending next-step plan that is not used (other ids came): its launches on the plan
+        stream must be behind the step before the buffers of its set are written again."""
+        if pend is not None and pend[3] is not None:
+            self.x.wait_ahead(*pend[3])
+
     def __call__(self, user_ids, item_ids, targets, next=None):
         if self.tapes is not None and self.tapes.usable(self.ops.deferred, self.ops.eng):
             return self._call_taped(user_ids, item_ids, targets, next)
         ops, X = self.ops, self.x
         ops.mark_entry()          # ids of this call and of `next` exist from here on
         pend, self._pending = self._pending, None
-        ahead = None
+        ahead = own = None
         if pend is not None and pend[0] is user_ids and pend[1] is item_ids:
             plan, ahead = pend[2], pend[3]   # planned (and its rows sent) one call ago
+            own = pend[4]                    # (and claimed by their owners, CLAIM_AHEAD)
         else:
+            self._settle_pending(pend)
             plan = self.plan(user_ids, item_ids)
         X.counts_wait(plan)
         if next is not None:      # plan step t+1 now: it runs under this step's GPU work
-            self._pending = [next[0], next[1], self.plan(next[0], next[1]), None]
+            self._pending = [next[0], next[1], self.plan(next[0], next[1]), None, None]
         ops.begin(plan)
         send_splits, recv_splits = plan.splits()
         if ahead is not None:
@@ -363,7 +396,10 @@ class ShardedTrainStep:
             X.wait_ahead(*ahead)
         else:
             recv = X.exchange(plan.send, send_splits, recv_splits)
-        own = ops.owner_prepare(recv, plan)
+        if own is not None:       # claimed a step ahead: its rows only need catching up
+            ops.owner_catchup(own)
+        else:
+            own = ops.owner_prepare(recv, plan)
         rows = ops.owner_gather(own, recv)
         back = X.exchange(rows, recv_splits, send_splits, slot="rows")
         grads, loss = ops.compute(plan, back, user_ids, item_ids, targets,
@@ -372,6 +408,8 @@ class ShardedTrainStep:
             nxt = self._pending[2]
             X.counts_wait(nxt)
             self._pending[3] = X.exchange_ahead(nxt)
+            if self._claims_ahead():
+                self._pending[4] = self._claim_ahead(nxt, self._pending[3])
         ar = X.all_reduce_start(ops.dense_grad())
         got = X.exchange(grads, send_splits, recv_splits, slot="grads")
         ops.owner_apply(own, got)
@@ -398,10 +436,11 @@ class ShardedTrainStep:
         ops.eng.ensure_layout()   # (as eng.forward would; a re-pack moves the signature)
         ops.mark_entry()
         pend, self._pending = self._pending, None
-        ahead = None
+        ahead = own_ahead = None
         if pend is not None and pend[0] is user_ids and pend[1] is item_ids:
-            plan, ahead = pend[2], pend[3]
+            plan, ahead, own_ahead = pend[2], pend[3], pend[4]
         else:
+            self._settle_pending(pend)
             plan = self.plan(user_ids, item_ids)
         X.counts_wait(plan)
         n = plan.extra["n"]
@@ -409,10 +448,10 @@ class ShardedTrainStep:
         if next is not None:
             nu_, ni_ = next[0].reshape(-1), next[1].reshape(-1)
             nplan = ops.plan_host(nu_, ni_)
-            self._pending = [next[0], next[1], nplan, None]
+            self._pending = [next[0], next[1], nplan, None, None]
         targets = targets.reshape(-1).to(device=ops.dev, dtype=torch.float32).contiguous()
         send_splits, recv_splits = plan.splits()
-        own = ops.owner_host(plan)
+        own = own_ahead if own_ahead is not None else ops.owner_host(plan)
         nu, ni = plan.totals()
         X.site("recv", send_splits, recv_splits)
         X.site("rows", recv_splits, send_splits)
@@ -420,7 +459,7 @@ class ShardedTrainStep:
         T.horizon(d)
         k_set = plan.extra["set"]["k"]
         key_a = ("a", n, k_set, None if nplan is None else nplan.extra["set"]["k"],
-                 ahead is not None, own["nmax"] > 0)
+                 ahead is not None, own["nmax"] > 0, own_ahead is not None)
         nn_ = 8 * n if next is not None else 0
         ranges = (ptr(next[0]) if next is not None else 0, nn_,
                   ptr(next[1]) if next is not None else 0, nn_, ptr(targets), 4 * n, st, 1)
@@ -457,7 +496,10 @@ class ShardedTrainStep:
                 X.wait_ahead(*ahead)
             else:
                 recv = X.exchange(plan.send, send_splits, recv_splits, slot="recv")
-            ops.owner_prepare(recv, plan, own)
+            if own_ahead is not None:
+                ops.owner_catchup(own)
+            else:
+                ops.owner_prepare(recv, plan, own)
             rows = ops.owner_gather(own, recv)
             back = X.exchange(rows, recv_splits, send_splits, slot="rows")
             res["grads"], res["loss"] = ops.compute(plan, back, user_ids, item_ids, targets,
@@ -471,6 +513,7 @@ class ShardedTrainStep:
             ops.last_loss = res["loss"]
         # the next plan's sizes (for its rows' exchange ahead), then the rest of the step
         nahead = None
+        own_next = None
         if self.ahead and self._pending is not None:
             nxt = self._pending[2]
             X.counts_wait(nxt)
@@ -478,21 +521,30 @@ class ShardedTrainStep:
             nahead = nxt.extra["set"]["k"]
             X.site(f"ahead{nahead}", s_, r_)
             ahead_out = X.exchange_out(nxt.send, r_, f"ahead{nahead}")
+            if self._claims_ahead():
+                own_next = ops.owner_host(nxt)      # (host side; its claim is in segment B)
         grads = res["grads"]
         X.exchange_out(grads, recv_splits, "grads")
-        key_b = ("b", n, k_set, nahead, own["nmax"] > 0)
+        key_b = ("b", n, k_set, nahead, own["nmax"] > 0, own_next is not None)
         sig = self._signature()
+        scalars_b = scalars + ((own_next["token"],) if own_next is not None else (0,))
 
         def seg_b():
             if nahead is not None:
                 self._pending[3] = X.exchange_ahead(self._pending[2])
+                if own_next is not None:
+                    ops.owner_claim(self._pending[3][0], own_next,
+                                    self._pending[2].stream.cuda_stream, SLOT_TOKEN_NEXT)
+                    self._pending[3][1].record(self._pending[2].stream.cuda_stream)
             ar = X.all_reduce_start(ops.dense_grad())
             got = X.exchange(grads, send_splits, recv_splits, slot="grads")
             ops.owner_apply(own, got)
             X.all_reduce_wait(ar)
             ops.dense_step()
-        replayed = T.run(key_b, sig, self._pre(), (0, 0, 0, 0, 0, 0, st, 1), scalars, seg_b,
+        replayed = T.run(key_b, sig, self._pre(), (0, 0, 0, 0, 0, 0, st, 1), scalars_b, seg_b,
                          self._post_b)
+        if own_next is not None:
+            self._pending[4] = own_next
         if replayed:
             if nahead is not None:
                 self._pending[3] = (ahead_out, X._ahead_ev[nahead])
@@ -555,12 +607,16 @@ class HipShardOps:
         self.last_loss = None
         # owner side: claim tokens and row -> unique index, one int32 per local row and kind
         ru, ri = model.num_users, model.num_products
-        self.mark = [torch.zeros(ru, dtype=torch.int32, device=self.dev),
-                     torch.zeros(ri, dtype=torch.int32, device=self.dev)]
-        self.uidx = [torch.zeros(ru, dtype=torch.int32, device=self.dev),
-                     torch.zeros(ri, dtype=torch.int32, device=self.dev)]
+        # (one set per plan-buffer set: a step's owner claim may run a step ahead, on the plan
+        # stream, while the previous step still reads its own)
+        self.marks = [[torch.zeros(ru, dtype=torch.int32, device=self.dev),
+                       torch.zeros(ri, dtype=torch.int32, device=self.dev)] for _ in range(2)]
+        self.uidxs = [[torch.zeros(ru, dtype=torch.int32, device=self.dev),
+                       torch.zeros(ri, dtype=torch.int32, device=self.dev)] for _ in range(2)]
+        self.mark, self.uidx = self.marks[0], self.uidxs[0]
         self.token = 0
-        self.cnt = torch.zeros(2, dtype=torch.int32, device=self.dev)
+        self.cnts = [torch.zeros(2, dtype=torch.int32, device=self.dev) for _ in range(2)]
+        self.cnt = self.cnts[0]
         self.plan_stream = torch.cuda.Stream(self.dev)
         if self.deferred.overlap and os.environ.get("NCF_SHARD_SWEEP_ON_PLAN", "1") != "0":
             # the overlapped sweep on the plan's stream, not a stream of its own: world 1,
@@ -660,8 +716,9 @@ class HipShardOps:
         plan.extra["set"]["ready"].wait(self._st())
 
     # 2. owner side: sort-free dedup of the received rows, catch-up, gather
-    def _layout(self, counts):
-        L = self._recv_layout = getattr(self, "_recv_layout", None) or _lib.ShardRecv()
+    def _layout(self, counts, par=0):
+        ls = self.__dict__.setdefault("_recv_layouts", [None, None])
+        L = ls[par] = ls[par] or _lib.ShardRecv()
         L.world = self.W
         off = 0
         for s in range(self.W):
@@ -673,37 +730,50 @@ class HipShardOps:
 
     def owner_host(self, plan):
         """Host side of the owner phase of a step: the receive layout (one persistent host
-        struct), the claim token and the sizes; the buffers sized for them."""
-        L = self._layout(plan.recv_counts)
+        struct per plan-buffer set), the claim token and the sizes; the buffers sized for them
+        (the per-step ones of the plan's set: its claim may run a step ahead)."""
+        par = plan.extra["set"]["k"]
+        L = self._layout(plan.recv_counts, par)
         tu = sum(c[0] for c in plan.recv_counts)
         ti = sum(c[1] for c in plan.recv_counts)
         nmax = max(tu, ti)
-        uq = [self._buf("own_uq0", (max(tu, 1),), torch.int64),
-              self._buf("own_uq1", (max(ti, 1),), torch.int64)]
-        pos = [self._buf("own_pos0", (max(tu, 1), self.W), torch.int32),
-               self._buf("own_pos1", (max(ti, 1), self.W), torch.int32)]
+        # (both sets' buffers grown together: a launch tape's signature holds their addresses,
+        # and a set first allocated a few steps in would drop the tapes recorded before)
+        for q in (1 - par, par):       # (par last: its buffers are the ones returned)
+            uq = [self._buf(f"own_uq0_{q}", (max(tu, 1),), torch.int64),
+                  self._buf(f"own_uq1_{q}", (max(ti, 1),), torch.int64)]
+            pos = [self._buf(f"own_pos0_{q}", (max(tu, 1), self.W), torch.int32),
+                   self._buf(f"own_pos1_{q}", (max(ti, 1), self.W), torch.int32)]
         self.token += 1
         total = L.start[self.W]
         rows = self._buf("own_rows", (max(total, 1), 2 * self.D))[:total]
         G = [self._buf(f"own_g{j}", (max(nmax, 1), self.D)) for j in range(4)]
         return {"layout": L, "uniq": uq, "pos": pos, "nmax": nmax, "token": self.token,
-                "rows": rows, "G": G}
+                "rows": rows, "G": G, "par": par, "cnt": self.cnts[par]}
+
+    def owner_claim(self, recv, own, st, token_slot=SLOT_TOKEN):
+        """The owner's sort-free dedup of the received rows (claim + positions) on stream st."""
+        L, uq, pos, par = own["layout"], own["uniq"], own["pos"], own["par"]
+        mk, ux = self.marks[par], self.uidxs[par]
+        _lib.call_tagged("ncf_shard_owner_prepare", {2: token_slot}, ptr(recv), ctypes.addressof(L),
+                         own["token"], ptr(mk[0]), ptr(mk[1]), ptr(ux[0]), ptr(ux[1]),
+                         mk[0].numel(), mk[1].numel(), ptr(uq[0]), ptr(uq[1]), ptr(own["cnt"]),
+                         ptr(pos[0]), ptr(pos[1]), ptr(self.err), st)
+
+    def owner_catchup(self, own):
+        """The claimed rows caught up through the current step (on the step's stream)."""
+        d = self.deferred
+        if own["nmax"] > 0:
+            d._ensure(d.t + 1)
+            pairs = self._pairs(own["uniq"])
+            _lib.call_tagged("ncf_adam_pairs_catchup_clock", {4: SLOT_NMAX},
+                             ctypes.addressof(pairs), 2, self.D, ptr(own["cnt"]), own["nmax"], 0,
+                             ptr(self.clock), ptr(d._table), *d._consts(), self._st())
 
     def owner_prepare(self, recv, plan, own=None):
-        st = self._st()
         own = own or self.owner_host(plan)
-        L, uq, pos, nmax = own["layout"], own["uniq"], own["pos"], own["nmax"]
-        _lib.call_tagged("ncf_shard_owner_prepare", {2: SLOT_TOKEN}, ptr(recv), ctypes.addressof(L),
-                         own["token"], ptr(self.mark[0]), ptr(self.mark[1]), ptr(self.uidx[0]),
-                         ptr(self.uidx[1]), self.mark[0].numel(), self.mark[1].numel(), ptr(uq[0]),
-                         ptr(uq[1]), ptr(self.cnt), ptr(pos[0]), ptr(pos[1]), ptr(self.err), st)
-        d = self.deferred
-        if nmax > 0:
-            d._ensure(d.t + 1)
-            pairs = self._pairs(uq)
-            _lib.call_tagged("ncf_adam_pairs_catchup_clock", {4: SLOT_NMAX},
-                             ctypes.addressof(pairs), 2, self.D, ptr(self.cnt), nmax, 0,
-                             ptr(self.clock), ptr(d._table), *d._consts(), st)
+        self.owner_claim(recv, own, self._st())
+        self.owner_catchup(own)
         return own
 
     def _pairs(self, uq, G=None):
@@ -798,11 +868,11 @@ class HipShardOps:
     # 5. owner side: sum received gradients per unique row (rank order), apply the step
     def owner_apply(self, own, got):
         st = self._st()
-        uq, pos, nmax, G = own["uniq"], own["pos"], own["nmax"], own["G"]
+        uq, pos, nmax, G, cnt = own["uniq"], own["pos"], own["nmax"], own["G"], own["cnt"]
         d = self.deferred
         if not GSUM_APPLY:
             _lib.call_tagged("ncf_shard_owner_gradsum", {4: SLOT_NMAX}, ptr(got), ptr(pos[0]),
-                             ptr(pos[1]), ptr(self.cnt), nmax, self.W, self.D, ptr(G[0]),
+                             ptr(pos[1]), ptr(cnt), nmax, self.W, self.D, ptr(G[0]),
                              ptr(G[1]), ptr(G[2]), ptr(G[3]), st)
         d._ensure(d.t + 1)
         d.sweep_join()
@@ -811,13 +881,13 @@ class HipShardOps:
             # the rank-order gradient sum inside the apply (one launch, the same bits)
             pairs = self._pairs(uq)
             _lib.call_tagged("ncf_adam_pairs_apply_gsum_clock", {4: SLOT_NMAX},
-                             ctypes.addressof(pairs), 2, self.D, ptr(self.cnt), nmax, 1, ptr(got),
+                             ctypes.addressof(pairs), 2, self.D, ptr(cnt), nmax, 1, ptr(got),
                              ptr(pos[0]), ptr(pos[1]), self.W, ptr(self.clock), ptr(d._table),
                              *d._consts(), st)
         elif nmax > 0:
             pairs = self._pairs(uq, G)
             _lib.call_tagged("ncf_adam_pairs_apply_clock", {4: SLOT_NMAX}, ctypes.addressof(pairs),
-                             2, self.D, ptr(self.cnt), nmax, 1, ptr(self.clock), ptr(d._table),
+                             2, self.D, ptr(cnt), nmax, 1, ptr(self.clock), ptr(d._table),
                              *d._consts(), st)
         d.advance(st)                               # rolling sweep of step t + 1 (clock)
 

@@ -165,16 +165,19 @@ class Workspace:
         off, size = self.site_off[name]
         return self.red_ws[off:off + size]
 
-    def run_reductions(self, st):
-        """All gradient reductions deferred by this backward, in two launches."""
+    def run_reductions(self, st, scratch: str = "red_scratch"):
+        """All gradient reductions deferred by this backward so far, in two launches (``scratch``:
+        the workspace attribute of the scratch buffer — the early reductions on a side stream
+        take a second one, so both batches can be in flight)."""
         lst = self.red_list
         if lst.count == 0:
             return
         need = _lib.query("ncf_reduce_batch_scratch", lst.address)
-        if self.red_scratch.numel() < need:
-            self.red_scratch = torch.empty(need, dtype=torch.float32, device=self.red_ws.device)
-        _lib.call("ncf_reduce_batch", lst.address, ptr(self.red_scratch), self.red_scratch.numel(),
-                  st)
+        buf = getattr(self, scratch, None)
+        if buf is None or buf.numel() < need:
+            buf = torch.empty(max(need, 1), dtype=torch.float32, device=self.red_ws.device)
+            setattr(self, scratch, buf)
+        _lib.call("ncf_reduce_batch", lst.address, ptr(buf), buf.numel(), st)
         lst.count = 0
 
 
@@ -762,12 +765,15 @@ class NCFEngine:
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,
                  loss_denominator: float = 0.0, tables=None, rows=None, uniq=None,
                  reduce_async: bool = False, bf16: bool = False, grad_rows=None,
-                 table_ld: Optional[int] = None):
+                 table_ld: Optional[int] = None, reduce_side=None):
         """Gradients of every used parameter.  Dense grads land in the flat grad buffer; table
         grads stay compact (self.pending) for the fused Adam step.  ``reduce_async``: the
         deferred reductions (every dense gradient) run on a side stream, beside whatever the
         caller queues next that does not read them (the table Adam); the caller must call
-        ``join_reductions()`` before reading the dense gradients.  ``grad_rows = (buf, rows_u,
+        ``join_reductions()`` before reading the dense gradients.  ``reduce_side`` (a stream
+        whose queued work the step joins before its dense Adam): the tower and attention
+        reductions run there right after the fused tower/attention backward, beside the
+        embedding backward and the table Adam (join_reductions orders them).  ``grad_rows = (buf, rows_u,
         rows_i)``: the table gradients of unique row c go to row rows_*[c] of buf ([mf | mlp]
         halves, 2 D floats per row: the row-sharded step's send buffer) instead of w.G."""
         m = self.model
@@ -894,6 +900,20 @@ class NCFEngine:
         else:
             self._sweep_fork("attn_bwd", w)
             self._attention_bwd_unfused(w, drop_p, seed, joins, st)
+        if reduce_side is not None and fused_ta and not reduce_async:
+            # the dense-gradient reductions of the fused backward on the side stream now, beside
+            # the embedding backward and the table Adam (its own scratch; joined before the
+            # flat Adam by join_reductions)
+            ev = getattr(self, "_early_red_ev", None)
+            if ev is None:
+                ev = self._early_red_ev = (_lib.RawEvent(stream_only=True),
+                                           _lib.RawEvent(stream_only=True))
+            side = reduce_side.cuda_stream
+            ev[0].record(st)
+            ev[0].wait(side)
+            w.run_reductions(side, scratch="red_scratch_side")
+            ev[1].record(side)
+            self._early_red_pending = True
         # a2/a3 backward: segment-reduce + mf_norm/mlp_norm backward (compact table grads)
         self._sweep_fork("emb_bwd", w)
         if tables is None:
@@ -958,6 +978,9 @@ class NCFEngine:
         if getattr(self, "_red_pending", False):
             torch.cuda.current_stream(self.flat.device).wait_event(self._red_ev[1])
             self._red_pending = False
+        if getattr(self, "_early_red_pending", False):
+            self._early_red_ev[1].wait(_lib.stream_ptr(self.flat.device))
+            self._early_red_pending = False
 
     def _attention_bwd_unfused(self, w, drop_p, seed, joins, st):
         """a5 backward as separate launches (any geometry the unfused forward takes)."""

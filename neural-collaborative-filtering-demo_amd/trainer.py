@@ -38,8 +38,13 @@ DEDUP_FORK = "sweep"
 # (the scalar table cannot grow from inside a replay); tests shrink it to force re-captures.
 GRAPH_HORIZON = 1 << 16
 # The dense-gradient reductions on a side stream beside the table Adam's apply (engine.backward
-# reduce_async; joined before the flat Adam close)
+# reduce_async, a stream of its own; joined before the flat Adam close): measured slower (0.379
+# against 0.288 ms/step: a third stream shares a hardware queue)
 REDUCE_ASYNC = False
+# The fused tower/attention backward's reductions queued on the overlapped sweep's side stream
+# right after that kernel (engine.backward reduce_side), beside the embedding backward and the
+# table Adam; joined before the flat Adam close
+EARLY_REDUCE = True
 
 
 class FusedTrainStep:
@@ -144,8 +149,12 @@ class FusedTrainStep:
         w = eng.forward(user_ids, item_ids, M, True, drop_p, seed, prepare=prep,
                         tables=self.tables_lp, bf16=self.bf16)
         # (REDUCE_ASYNC: the dense-gradient reductions beside the table Adam)
+        d = self.deferred
+        side = (d.side_stream() if EARLY_REDUCE and d is not None and d.overlap and not self.graph
+                and not REDUCE_ASYNC else None)
         eng.backward(w, user_ids, item_ids, None, targets, drop_p, seed, tables=self.tables_lp,
-                     bf16=self.bf16, reduce_async=REDUCE_ASYNC and not self.graph)
+                     bf16=self.bf16, reduce_async=REDUCE_ASYNC and not self.graph,
+                     reduce_side=side)
         st = _lib.stream_ptr(eng.flat.device)
         b1, b2 = self.betas
         if self.deferred is not None:

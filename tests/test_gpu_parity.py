@@ -1286,6 +1286,14 @@ def test_sharded_step_world1_bitwise_equals_fused(exchange, ahead):
         dist.destroy_process_group()
 
 
+def test_sharded_step_claim_ahead_bitwise_equals_fused(monkeypatch):
+    """The owner claim of the next step's rows run a step ahead on the plan stream
+    (distributed.CLAIM_AHEAD, off by default): the same bits as the fused step."""
+    import ncf_amd.distributed as Dist
+    monkeypatch.setattr(Dist, "CLAIM_AHEAD", True)
+    test_sharded_step_world1_bitwise_equals_fused("rccl", True)
+
+
 def test_comm_alltoallv_and_allreduce_single_rank():
     """ncf_comm_alltoallv / ncf_comm_allreduce_sum_f32 on a one-rank communicator: the
     all-to-all is a copy of the first send_rows rows (any row width, empty splits), the sum

@@ -36,8 +36,17 @@ def main():
         run(140, 100)
         torch.cuda.synchronize()
         side = step.deferred._side
-        print(f"k={k} side stream {side.cuda_stream:#x}: "
-              f"{(time.perf_counter() - t0) / 100 * 1e3:.4f} ms/step", flush=True)
+        ms = (time.perf_counter() - t0) / 100 * 1e3
+        from ncf_amd import _lib
+        _lib.PROFILE = []
+        run(240, 20)
+        torch.cuda.synchronize()
+        prof, _lib.PROFILE = _lib.PROFILE, None
+        per = {}
+        for nm, _, e0, e1 in prof:
+            per[nm] = per.get(nm, 0.0) + e0.elapsed_time(e1) * 1e3 / 20
+        top = " ".join(f"{k_[4:18]}={v:.0f}" for k_, v in sorted(per.items(), key=lambda x: -x[1])[:7])
+        print(f"k={k} side stream {side.cuda_stream:#x}: {ms:.4f} ms/step | {top}", flush=True)
         del step, model, held
         torch.cuda.empty_cache()
 
