@@ -43,8 +43,10 @@ GRAPH_HORIZON = 1 << 16
 REDUCE_ASYNC = False
 # The fused tower/attention backward's reductions queued on the overlapped sweep's side stream
 # right after that kernel (engine.backward reduce_side), beside the embedding backward and the
-# table Adam; joined before the flat Adam close
-EARLY_REDUCE = True
+# table Adam; joined before the flat Adam close.  Same bits (the bitwise suite runs it).  Off:
+# measured slower (3 interleaved runs each: 0.3028 / 0.3033 against 0.2866 / 0.2888 ms/step —
+# the 105 MB of partials read beside the embedding backward and the apply slow both)
+EARLY_REDUCE = False
 
 
 class FusedTrainStep:

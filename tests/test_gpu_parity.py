@@ -932,11 +932,24 @@ def test_early_catchup_bitwise_equals_dense(monkeypatch, tables):
         monkeypatch.setattr(Dm, "EARLY_CATCHUP", False)
         a_sd, a_m = _fused_run(True, 40, **kw)
         assert not any(ran)
-        monkeypatch.setattr(Dm, "EARLY_CATCHUP", True)
     else:
         a_sd, a_m = _fused_run(False, 40, U=400, I=150)
+    monkeypatch.setattr(Dm, "EARLY_CATCHUP", True)     # (off by default)
     b_sd, b_m = _fused_run(True, 40, **kw)
     assert sum(ran) >= 38, ran
+    for k in a_sd:
+        assert torch.equal(a_sd[k], b_sd[k]), k
+    for k in a_m:
+        assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
+
+
+def test_early_reduce_bitwise_equals_dense(monkeypatch):
+    """The fused backward's dense-gradient reductions on the sweep's side stream
+    (trainer.EARLY_REDUCE, off by default) against the dense sweep, bit for bit."""
+    import ncf_amd.trainer as Tr
+    monkeypatch.setattr(Tr, "EARLY_REDUCE", True)
+    a_sd, a_m = _fused_run(False, 30)
+    b_sd, b_m = _fused_run(True, 30, clock=True, overlap_sweep=True, pipelined=True)
     for k in a_sd:
         assert torch.equal(a_sd[k], b_sd[k]), k
     for k in a_m:
