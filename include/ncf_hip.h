@@ -788,6 +788,23 @@ typedef struct ncf_table_pair {
   int64_t rows;
   int64_t param_dtype;
 } ncf_table_pair;
+/* The reduce with the deferred table Adam's apply of the step fused in (FusedTrainStep): each
+ * unique row's two gradient rows, once complete (in the reduce for a segment of one piece, in
+ * the fix-up for longer ones), step that row as ncf_adam_pairs_apply_clock(pairs, 2, dim,
+ * num_unique, n, step_rel, ...) would, and stamp it; the compact gradients are still written.
+ * pairs[k] (k = users, items): the two tables (p0 GMF, p1 MLP; the rows the reduce reads), their
+ * moments and stamps.  Same bits as the reduce followed by the apply (trainer.py:285's
+ * Adam.step on the touched rows, fused into the backward of :282). */
+int ncf_embedding_bwd_reduce_apply_clock(
+    int64_t n, int64_t dim, int64_t num_users, int64_t num_items, const float* dy_mf_user,
+    const float* dy_mlp_user, const float* dy_mf_item, const float* dy_mlp_item,
+    const float* mf_gamma, const float* mlp_gamma, float eps, float* grad_mf_user,
+    float* grad_mlp_user, float* grad_mf_item, float* grad_mlp_item, const int64_t* uniq_users,
+    const int64_t* uniq_items, float* grad_mf_gamma, float* grad_mf_beta, float* grad_mlp_gamma,
+    float* grad_mlp_beta, void* workspace, int64_t workspace_bytes, ncf_reduce_list* defer,
+    const ncf_table_pair* pairs, int32_t step_rel, const ncf_step_clock* clock,
+    const float* step_table, double beta1, double beta2, double eps_adam, double weight_decay,
+    void* stream);
 int ncf_adam_pairs_catchup_clock(const ncf_table_pair* pairs, int npairs, int64_t dim,
                                  const uint32_t* count, int64_t max_n, int32_t target_rel,
                                  const ncf_step_clock* clock, const float* step_table,

@@ -121,6 +121,9 @@ SIGNATURES = {
     "ncf_embedding_bwd_reduce_rows": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32,
                                             P, P, P, P, P, P, P, P, I64, I64, P, P, P, P, P, I64,
                                             P, P]),
+    "ncf_embedding_bwd_reduce_apply_clock": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, F32, P, P,
+                                                   P, P, P, P, P, P, P, P, P, I64, P, P, I32, P,
+                                                   P, F64, F64, F64, F64, P]),
     "ncf_embedding_bwd_reduce": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
                                        P, P, P, P, P, P, P, P, P, I64, P, P]),
     "ncf_embedding_bwd_reduce_bf16": (I32, [I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32,

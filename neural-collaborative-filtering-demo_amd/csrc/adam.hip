@@ -14,62 +14,12 @@
 // per-step traffic is exactly p, m, v read+write (24 B/element) + 4 B/row slot + the touched rows.
 // HBM-bound: float4 per lane, grid-stride over the table.
 #include "ncf_common.h"
+#include "adam_math.h"
+
+using namespace ncf_adam;
 
 namespace {
 
-struct AdamScalars {
-  float neg_step, w1, b2, c2, inv_bc2_sqrt, eps, wd;
-  float b1, k1, k2;   // zero-gradient step: beta1, (1-beta1) wd, (1-beta2) wd^2
-  float ra, rb;       // zero-gradient step s: inv_bc2_sqrt / neg_step, eps / neg_step
-};
-
-// One Adam element update, written as explicit fmas with the hardware square root and
-// reciprocal (v_sqrt_f32 / v_rcp_f32, ~1 ulp) and 1/sqrt(1-b2^t) folded on the host:
-//   g' = g + wd*p;  m += (1-b1)(g' - m);  v = b2 v + (1-b2) g'^2
-//   p += (-lr/(1-b1^t)) * m * 1/(sqrt(v) * 1/sqrt(1-b2^t) + eps)
-// 11 VALU ops (2 transcendental) per element-step.  Every kernel that applies a step (dense
-// sweep, deferred catch-up, touched-row apply) calls this one function with the same fp32
-// scalars, so the deferred schedule reproduces the dense schedule bit for bit; against torch's
-// correctly rounded CPU Adam the difference is ~1 ulp of the step (parity tests: abs 1e-6).
-__device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, float neg_step,
-                                      float inv_bc, const AdamScalars& s) {
-  g = __builtin_fmaf(s.wd, p, g);
-  m = __builtin_fmaf(s.w1, g - m, m);
-  v = __builtin_fmaf(s.c2 * g, g, v * s.b2);
-  const float denom = __builtin_fmaf(__builtin_amdgcn_sqrtf(v), inv_bc, s.eps);
-  p = __builtin_fmaf(neg_step * m, __builtin_amdgcn_rcpf(denom), p);
-}
-
-// The step of an element whose gradient is zero (an untouched table row: weight decay only),
-// the same update with the constants folded (9 VALU ops, 2 transcendental, instead of 11):
-//   m = b1 m + ((1-b1) wd) p;   v = b2 v + ((1-b2) wd^2) p p
-//   p += m / (sqrt(v) ra + rb),   ra = inv_bc2_sqrt / neg_step, rb = eps / neg_step
-// Used by every schedule for exactly the untouched elements (the dense sweep for rows without a
-// gradient slot, the deferred replay for the zero-gradient steps it owes), so the schedules stay
-// bit-identical to each other; against torch's Adam it differs by rounding (~1 ulp of m, v).
-__device__ __forceinline__ void adam0(float& p, float& m, float& v, float ra, float rb,
-                                      const AdamScalars& s) {
-  m = __builtin_fmaf(s.b1, m, s.k1 * p);
-  v = __builtin_fmaf(s.k2 * p, p, v * s.b2);
-  const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(v), ra, rb);
-  p = __builtin_fmaf(m, __builtin_amdgcn_rcpf(den), p);
-}
-
-__device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, const AdamScalars& s) {
-  adam1(p, m, v, g, s.neg_step, s.inv_bc2_sqrt, s);
-}
-
-__device__ __forceinline__ void adam4(float4& p, float4& m, float4& v, float4 g, float ns,
-                                      float bc, const AdamScalars& s) {
-  adam1(p.x, m.x, v.x, g.x, ns, bc, s);
-  adam1(p.y, m.y, v.y, g.y, ns, bc, s);
-  adam1(p.z, m.z, v.z, g.z, ns, bc, s);
-  adam1(p.w, m.w, v.w, g.w, ns, bc, s);
-}
-
-__device__ __forceinline__ void adam4(float4& p, float4& m, float4& v, float4 g, const AdamScalars& s) {
-  adam4(p, m, v, g, s.neg_step, s.inv_bc2_sqrt, s);
-}
 
 template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void k_adam_table(float* __restrict__ p, float* __restrict__ m,
@@ -615,27 +565,6 @@ __global__ __launch_bounds__(256) void k_adam_flat_close(float* __restrict__ p,
   }
 }
 
-AdamScalars make_scalars(double lr, double beta1, double beta2, double eps, double wd, double step) {
-  AdamScalars s;
-  const double bc1 = 1.0 - pow(beta1, step);
-  const double bc2 = 1.0 - pow(beta2, step);
-  s.neg_step = (float)(-(lr / bc1));
-  s.w1 = (float)(1.0 - beta1);
-  s.b2 = (float)beta2;
-  s.c2 = (float)(1.0 - beta2);
-  s.inv_bc2_sqrt = (float)(1.0 / sqrt(bc2));
-  s.eps = (float)eps;
-  s.wd = (float)wd;
-  s.b1 = (float)beta1;
-  s.k1 = (float)((1.0 - beta1) * wd);
-  s.k2 = (float)((1.0 - beta2) * wd * wd);
-  // zero-gradient form: ns folded into the denominator (lr == 0: a finite huge denominator, the
-  // step vanishes instead of 0 * inf)
-  const double ns = -(lr / bc1);
-  s.ra = ns != 0.0 ? (float)((1.0 / sqrt(bc2)) / ns) : -3.0e38f;
-  s.rb = ns != 0.0 ? (float)(eps / ns) : -3.0e38f;
-  return s;
-}
 
 int grid_for(int64_t work) {
   int64_t b = (work + 255) / 256;
@@ -727,12 +656,6 @@ extern "C" int ncf_scatter_compact_rows(float* dense_grad, int64_t dim, const in
 }
 
 namespace {
-AdamScalars consts_of(double beta1, double beta2, double eps, double wd) {
-  AdamScalars s = make_scalars(1.0, beta1, beta2, eps, wd, 1.0);
-  s.neg_step = 0.f;
-  s.inv_bc2_sqrt = 1.f;
-  return s;
-}
 
 template <int D>
 int catchup_d(TablePtrs t, const int64_t* ids, const uint32_t* count, int kind, int64_t max_n,

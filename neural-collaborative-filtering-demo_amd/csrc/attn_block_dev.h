@@ -826,7 +826,7 @@ __device__ __forceinline__ void attn_block_bwd_body(
       const int e = threadIdx.x + kThreads * q, r = e / L4, c = (e % L4) * 4;
       const bool in = e < Rp * L4 && r < rows;
       // (a shared-Q workgroup holds one user per group: its group's first row)
-      const int sr = shq_src ? r - r % M : src_row(uids ? uids + r0 : nullptr, r, M);
+      const int sr = !in ? 0 : shq_src ? r - r % M : src_row(uids ? uids + r0 : nullptr, r, M);
       pu[q] = in ? ld4(Xu + (r0 + sr) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
       pi[q] = in ? ld4(Xi + (r0 + r) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }

@@ -20,10 +20,42 @@
 // Output per kind: compact grads [num_unique, D] for the GMF and MLP tables of that kind.
 // Deterministic: every sum has a fixed order.
 #include "segments.h"
+#include "adam_math.h"
 
 using namespace ncf_seg;
 
 namespace {
+
+// The table Adam fused into the reduce (ncf_embedding_bwd_reduce_apply_clock): per kind the
+// moments and stamps of the two tables (the parameters are the tables the reduce reads), the
+// step clock and the per-step scalar table — the arithmetic of k_pairs_apply (adam.hip).
+struct ApplyArgs {
+  float* m[2][2];            // [kind][mf, mlp]
+  float* v[2][2];
+  float* p[2][2];            // the parameters (the reduce's table pointers, writable)
+  int32_t* stamp[2];
+  const ncf_step_clock* clock;
+  const float* table;
+  ncf_adam::AdamScalars s;
+  int32_t step_rel;
+  int on;
+};
+
+// Adam of row `row` of kind k with the two gradient rows (this lane's float4 of each)
+template <bool BF>
+__device__ __forceinline__ void apply_row(const ApplyArgs& ap, int k, int64_t row, int64_t col,
+                                          int D, float4 g0, float4 g1, bool stamp_lane) {
+  const int32_t step = ap.clock->t + ap.step_rel;
+  const float ns = ap.table[4 * step], bc = ap.table[4 * step + 1];
+  const int64_t o = row * D + col;
+  float4 p0 = ldp4<BF>(ap.p[k][0], o), m0 = ld4(ap.m[k][0] + o), v0 = ld4(ap.v[k][0] + o);
+  float4 p1 = ldp4<BF>(ap.p[k][1], o), m1 = ld4(ap.m[k][1] + o), v1 = ld4(ap.v[k][1] + o);
+  ncf_adam::adam4(p0, m0, v0, g0, ns, bc, ap.s);
+  ncf_adam::adam4(p1, m1, v1, g1, ns, bc, ap.s);
+  stp4<BF>(ap.p[k][0], o, p0); st4(ap.m[k][0] + o, m0); st4(ap.v[k][0] + o, v0);
+  stp4<BF>(ap.p[k][1], o, p1); st4(ap.m[k][1] + o, m1); st4(ap.v[k][1] + o, v1);
+  if (stamp_lane) ap.stamp[k][row] = step;
+}
 
 // part[kind*nbr + block][0:D mf_g | D:2D mf_b | 2D:3D mlp_g | 3D:4D mlp_b]
 constexpr int kPW = NCF_PIECE_WAVES;   // waves per block
@@ -45,7 +77,7 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     float* __restrict__ G_mlp0, float* __restrict__ G_mf1, float* __restrict__ G_mlp1,
     float* __restrict__ xp0, float* __restrict__ xp1, float* __restrict__ part,
     const int32_t* __restrict__ omap0, const int32_t* __restrict__ omap1, int64_t ldo,
-    int64_t ldt) {
+    int64_t ldt, const ApplyArgs ap) {
   constexpr int L = D / 4;
   constexpr int S = 64 / L;  // lane groups (pieces) per wave
   __shared__ __attribute__((aligned(16))) float red[kPW][4 * D];
@@ -114,6 +146,9 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
     }
     const int64_t c = info & ~FIRST_PIECE;
     const bool first = (info & FIRST_PIECE) != 0;
+    // (fused apply: a segment of one piece is complete here; longer ones in the fix-up)
+    const bool single = first && !(p + 1 < Pn && !(pseg[p + 1] & FIRST_PIECE));
+    float4 gdx[2];
     // two LayerNorm backwards (GMF row, MLP row) per group
 #pragma unroll
     for (int tbl = 0; tbl < 2; ++tbl) {
@@ -134,12 +169,15 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
         float* dst = first ? (tbl ? Gml : Gmf) + (omap ? (int64_t)omap[c] : c) * ldo
                            : xp + (p - c - 1) * 2 * D + tbl * D;  // extra piece e = p - c - 1
         st4(dst + col, dx);
+        gdx[tbl] = dx;
         float4& ag = tbl ? a_gl : a_gm;
         float4& ab = tbl ? a_bl : a_bm;
         ag.x += dy.x * h.x; ag.y += dy.y * h.y; ag.z += dy.z * h.z; ag.w += dy.w * h.w;
         ab.x += dy.x; ab.y += dy.y; ab.z += dy.z; ab.w += dy.w;
       }
     }
+    if (ap.on && act && single)
+      apply_row<BF>(ap, kind, uniq[c], col, D, gdx[0], gdx[1], sub == 0);
   }
   // the wave's groups (lanes L apart hold the same columns), then the block's waves
 #pragma unroll
@@ -171,13 +209,14 @@ __global__ __launch_bounds__(64 * kPW) void k_piece_reduce_ln(
 }
 
 // G[c] += extra pieces of segment c (in piece order); L lanes per segment
-template <int D>
+template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void k_piece_fixup(
     const uint32_t* __restrict__ fpiece0, const uint32_t* __restrict__ fpiece1,
     const uint32_t* __restrict__ totals, const float* __restrict__ xp0,
     const float* __restrict__ xp1, float* __restrict__ G_mf0, float* __restrict__ G_mlp0,
     float* __restrict__ G_mf1, float* __restrict__ G_mlp1, const int32_t* __restrict__ omap0,
-    const int32_t* __restrict__ omap1, int64_t ldo) {
+    const int32_t* __restrict__ omap1, int64_t ldo, const int64_t* __restrict__ uniq0,
+    const int64_t* __restrict__ uniq1, const ApplyArgs ap) {
   constexpr int L = D / 4;
   const int kind = blockIdx.y;
   const int32_t* omap = kind ? omap1 : omap0;
@@ -211,6 +250,7 @@ __global__ __launch_bounds__(256) void k_piece_fixup(
     }
     st4(Gmf + orow + col, a);
     st4(Gml + orow + col, b);
+    if (ap.on) apply_row<BF>(ap, kind, (kind ? uniq1 : uniq0)[c], col, D, a, b, col == 0);
   }
 }
 
@@ -516,23 +556,31 @@ int piece_reduce(const WS& w, int64_t n, const uint32_t* sv0, const uint32_t* sv
                  float eps, float* Gmf0, float* Gml0, float* Gmf1, float* Gml1, float* dgm,
                  float* dbm, float* dgl, float* dbl, ncf_reduce_list* defer, hipStream_t st,
                  bool bf = false, const int32_t* omap0 = nullptr, const int32_t* omap1 = nullptr,
-                 int64_t ldo = D, int64_t ldt = D) {
+                 int64_t ldo = D, int64_t ldt = D, const ApplyArgs* apply = nullptr) {
+  ApplyArgs ap{};
+  if (apply) ap = *apply;
   if (bf)
     hipLaunchKernelGGL((k_piece_reduce_ln<D, true>), dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1,
                        w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
                        dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
-                       Gmf1, Gml1, w.xp0, w.xp1, w.part, omap0, omap1, ldo, ldt);
+                       Gmf1, Gml1, w.xp0, w.xp1, w.part, omap0, omap1, ldo, ldt, ap);
   else
     hipLaunchKernelGGL((k_piece_reduce_ln<D, false>), dim3(w.nbr, 2), dim3(64 * kPW), 0, st, sv0, sv1,
                        w.pstart0, w.pstart1, w.pseg0, w.pseg1, uniq0, uniq1, w.totals,
                        dmf0, dml0, dmf1, dml1, tmf0, tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0,
-                       Gmf1, Gml1, w.xp0, w.xp1, w.part, omap0, omap1, ldo, ldt);
+                       Gmf1, Gml1, w.xp0, w.xp1, w.part, omap0, omap1, ldo, ldt, ap);
   NCF_CHECK_LAUNCH("ncf_embedding_bwd(piece_reduce)");
   constexpr int L = D / 4;
   const int64_t fb = ncf_cdiv(n * L, 256);
-  hipLaunchKernelGGL(k_piece_fixup<D>, dim3((unsigned)(fb > 2048 ? 2048 : (fb < 1 ? 1 : fb)), 2),
-                     dim3(256), 0, st, w.fpiece0, w.fpiece1, w.totals, w.xp0, w.xp1, Gmf0, Gml0,
-                     Gmf1, Gml1, omap0, omap1, ldo);
+  const dim3 fgrid((unsigned)(fb > 2048 ? 2048 : (fb < 1 ? 1 : fb)), 2);
+  if (bf)
+    hipLaunchKernelGGL((k_piece_fixup<D, true>), fgrid, dim3(256), 0, st, w.fpiece0, w.fpiece1,
+                       w.totals, w.xp0, w.xp1, Gmf0, Gml0, Gmf1, Gml1, omap0, omap1, ldo, uniq0,
+                       uniq1, ap);
+  else
+    hipLaunchKernelGGL((k_piece_fixup<D, false>), fgrid, dim3(256), 0, st, w.fpiece0, w.fpiece1,
+                       w.totals, w.xp0, w.xp1, Gmf0, Gml0, Gmf1, Gml1, omap0, omap1, ldo, uniq0,
+                       uniq1, ap);
   NCF_CHECK_LAUNCH("ncf_embedding_bwd(fixup)");
   if (defer) {
     float* const outs[4] = {dgm, dbm, dgl, dbl};
@@ -569,7 +617,7 @@ static int embedding_bwd_reduce(bool bf, int64_t n, int64_t dim, int64_t num_use
                                         int64_t workspace_bytes, ncf_reduce_list* defer,
                                         void* stream, const int32_t* omap0 = nullptr,
                                         const int32_t* omap1 = nullptr, int64_t ldo = 0,
-                                        int64_t ldt = 0) {
+                                        int64_t ldt = 0, const ApplyArgs* apply = nullptr) {
   NCF_CHECK_ARG(n >= 0 && n < (1ll << 30), "ncf_embedding_bwd_reduce: bad n");
   NCF_CHECK_ARG(dim == 16 || dim == 32 || dim == 64 || dim == 128 || dim == 256,
                 "ncf_embedding_bwd_reduce: dim must be 16/32/64/128/256");
@@ -581,7 +629,7 @@ static int embedding_bwd_reduce(bool bf, int64_t n, int64_t dim, int64_t num_use
   WS w = carve(workspace, n, dim);
   uint32_t *k0, *v0, *k1, *v1;
   sorted_bufs(w, sort_passes(num_users, num_items), &k0, &v0, &k1, &v1);
-  const bool mapped = omap0 != nullptr || (ldt != 0 && ldt != dim);
+  const bool mapped = omap0 != nullptr || (ldt != 0 && ldt != dim) || apply != nullptr;
   if (n > 0 && use_pos_reduce() && !mapped) {
     switch (dim) {
 #define POS(DD)                                                                                   \
@@ -603,7 +651,7 @@ static int embedding_bwd_reduce(bool bf, int64_t n, int64_t dim, int64_t num_use
                             mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user, grad_mf_item,  \
                             grad_mlp_item, grad_mf_gamma, grad_mf_beta, grad_mlp_gamma,           \
                             grad_mlp_beta, defer, st, bf, omap0, omap1, omap0 ? ldo : DD,     \
-                            ldt ? ldt : DD);
+                            ldt ? ldt : DD, apply);
     SEG(16) SEG(32) SEG(64) SEG(128) SEG(256)
 #undef SEG
   }
@@ -654,6 +702,48 @@ extern "C" int ncf_embedding_bwd_reduce_rows(
                               grad_mlp_item, uniq_users, uniq_items, grad_mf_gamma, grad_mf_beta,
                               grad_mlp_gamma, grad_mlp_beta, workspace, workspace_bytes, defer,
                               stream, out_rows_users, out_rows_items, out_ld, table_ld);
+}
+
+// The reduce with the deferred table Adam's apply of this step fused in (FusedTrainStep): each
+// unique row's two gradient rows, once complete (in the reduce for a segment of one piece, in
+// the fix-up for longer ones), step that row's parameters and moments as
+// ncf_adam_pairs_apply_clock(pairs, 2, dim, num_unique, n, step_rel, ...) would, and stamp it;
+// the compact gradients are still written.  pairs[k]: p0/m0/v0 (GMF), p1/m1/v1 (MLP) and stamp
+// of kind k (users, items); its p0 / p1 are the tables the reduce reads (mf_*, mlp_*), its
+// param_dtype says whether they are bf16.  Same bits as the reduce followed by the apply.
+extern "C" int ncf_embedding_bwd_reduce_apply_clock(
+    int64_t n, int64_t dim, int64_t num_users, int64_t num_items, const float* dy_mf_user,
+    const float* dy_mlp_user, const float* dy_mf_item, const float* dy_mlp_item,
+    const float* mf_gamma, const float* mlp_gamma, float eps, float* grad_mf_user,
+    float* grad_mlp_user, float* grad_mf_item, float* grad_mlp_item, const int64_t* uniq_users,
+    const int64_t* uniq_items, float* grad_mf_gamma, float* grad_mf_beta, float* grad_mlp_gamma,
+    float* grad_mlp_beta, void* workspace, int64_t workspace_bytes, ncf_reduce_list* defer,
+    const ncf_table_pair* pairs, int32_t step_rel, const ncf_step_clock* clock,
+    const float* step_table, double beta1, double beta2, double eps_adam, double weight_decay,
+    void* stream) {
+  NCF_CHECK_ARG(pairs && clock && step_table, "ncf_embedding_bwd_reduce_apply_clock: bad args");
+  ApplyArgs ap{};
+  for (int k = 0; k < 2; ++k) {
+    NCF_CHECK_ARG(pairs[k].p0 && pairs[k].m0 && pairs[k].v0 && pairs[k].p1 && pairs[k].m1 &&
+                      pairs[k].v1 && pairs[k].stamp &&
+                      pairs[k].param_dtype == pairs[0].param_dtype,
+                  "ncf_embedding_bwd_reduce_apply_clock: incomplete table pair");
+    ap.p[k][0] = pairs[k].p0; ap.m[k][0] = pairs[k].m0; ap.v[k][0] = pairs[k].v0;
+    ap.p[k][1] = pairs[k].p1; ap.m[k][1] = pairs[k].m1; ap.v[k][1] = pairs[k].v1;
+    ap.stamp[k] = pairs[k].stamp;
+  }
+  ap.clock = clock;
+  ap.table = step_table;
+  ap.s = ncf_adam::consts_of(beta1, beta2, eps_adam, weight_decay);
+  ap.step_rel = step_rel;
+  ap.on = 1;
+  const bool bf = pairs[0].param_dtype == NCF_DTYPE_BF16;
+  return embedding_bwd_reduce(bf, n, dim, num_users, num_items, dy_mf_user, dy_mlp_user,
+                              dy_mf_item, dy_mlp_item, pairs[0].p0, pairs[0].p1, pairs[1].p0,
+                              pairs[1].p1, mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user,
+                              grad_mf_item, grad_mlp_item, uniq_users, uniq_items, grad_mf_gamma,
+                              grad_mf_beta, grad_mlp_gamma, grad_mlp_beta, workspace,
+                              workspace_bytes, defer, stream, nullptr, nullptr, 0, 0, &ap);
 }
 
 // The same with bf16 table rows (the LayerNorm recompute reads them; gradients stay fp32).

@@ -6,6 +6,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "ncf_hip.h"  // the public C-ABI: every extern "C" definition is checked against it
 
@@ -26,9 +27,27 @@ void ncf_set_error(const char* fmt, ...);
     }                                            \
   } while (0)
 
+// NCF_DEBUG_SYNC=1 (fault triage only): every launch is followed by a device synchronise, so
+// a kernel that faults is named by the launch that raised it (printed to stderr).
+static inline bool ncf_debug_sync() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("NCF_DEBUG_SYNC");
+    on = (e && e[0] == '1') ? 1 : 0;
+  }
+  return on != 0;
+}
+
 #define NCF_CHECK_LAUNCH(name)                                                   \
   do {                                                                           \
     hipError_t e_ = hipGetLastError();                                           \
+    if (e_ == hipSuccess && ncf_debug_sync()) {                                  \
+      e_ = hipDeviceSynchronize();                                               \
+      if (e_ != hipSuccess) {                                                    \
+        fprintf(stderr, "NCF_DEBUG_SYNC: %s: %s\n", name, hipGetErrorString(e_)); \
+        fflush(stderr);                                                          \
+      }                                                                          \
+    }                                                                            \
     if (e_ != hipSuccess) {                                                      \
       ncf_set_error("%s: launch failed: %s", name, hipGetErrorString(e_));       \
       return NCF_ERR_LAUNCH;                                                     \

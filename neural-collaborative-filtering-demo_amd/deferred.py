@@ -450,6 +450,16 @@ class DeferredTableAdam:
                   ptr(self.clock), ptr(self._table), *self._consts(), stream)
         return True
 
+    def fused_apply_args(self, w):
+        """The arguments of the apply fused into the embedding backward (engine.backward
+        fused_apply): this step's touched rows stepped where their gradient rows complete, as
+        apply() would step them after it.  None without the device clock."""
+        if self.clock is None or w.g.n == 0:
+            return None
+        self._ensure(self.t + 1)
+        pairs = self._pairs_for(w)
+        return (ctypes.addressof(pairs), ptr(self.clock), ptr(self._table)) + self._consts()
+
     # ---- after the backward: this step's gradient on the touched rows
     def apply(self, w, st):
         n = w.g.n
@@ -457,11 +467,12 @@ class DeferredTableAdam:
             self._ensure(self.t + 1)
             self.sweep_join()
             self._settle(st)
-            if n > 0:
+            if n > 0 and not getattr(w, "applied", False):
                 pairs = self._pairs_for(w)
                 _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2,
                           self.engine.model.mlp_embedding_dim, ptr(w.num_unique), n, 1,
                           ptr(self.clock), ptr(self._table), *self._consts(), st)
+            w.applied = False
             self.advance(st)
             return
         self.apply_rows("user", w.uniq_u, w.num_unique, 0, n, w.G["mf_user"], w.G["mlp_user"], st)

@@ -765,7 +765,7 @@ class NCFEngine:
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,
                  loss_denominator: float = 0.0, tables=None, rows=None, uniq=None,
                  reduce_async: bool = False, bf16: bool = False, grad_rows=None,
-                 table_ld: Optional[int] = None, reduce_side=None):
+                 table_ld: Optional[int] = None, reduce_side=None, fused_apply=None):
         """Gradients of every used parameter.  Dense grads land in the flat grad buffer; table
         grads stay compact (self.pending) for the fused Adam step.  ``reduce_async``: the
         deferred reductions (every dense gradient) run on a side stream, beside whatever the
@@ -773,7 +773,10 @@ class NCFEngine:
         ``join_reductions()`` before reading the dense gradients.  ``reduce_side`` (a stream
         whose queued work the step joins before its dense Adam): the tower and attention
         reductions run there right after the fused tower/attention backward, beside the
-        embedding backward and the table Adam (join_reductions orders them).  ``grad_rows = (buf, rows_u,
+        embedding backward and the table Adam (join_reductions orders them).  ``fused_apply``
+        (DeferredTableAdam.fused_apply_args): the table Adam's apply of this step runs inside the
+        embedding backward (ncf_embedding_bwd_reduce_apply_clock; w.applied tells the deferred
+        schedule).  ``grad_rows = (buf, rows_u,
         rows_i)``: the table gradients of unique row c go to row rows_*[c] of buf ([mf | mlp]
         halves, 2 D floats per row: the row-sharded step's send buffer) instead of w.G."""
         m = self.model
@@ -947,6 +950,17 @@ class NCFEngine:
                       self.gptr("mf_norm.weight"), self.gptr("mf_norm.bias"),
                       self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
                       w.emb_ws.numel(), w.red_list.address, st)
+        elif fused_apply is not None:
+            pa, clk, tab, b1, b2, eps_a, wd = fused_apply
+            _lib.call("ncf_embedding_bwd_reduce_apply_clock", n, D, d_rows[0], d_rows[1],
+                      ptr(w.dumf), ptr(w.dxu), ptr(w.dimf), ptr(w.dxi),
+                      pp["mf_norm.weight"], pp["mlp_norm.weight"], LN_EPS, ptr(G["mf_user"]),
+                      ptr(G["mlp_user"]), ptr(G["mf_item"]), ptr(G["mlp_item"]), ptr(uq_u),
+                      ptr(uq_i), self.gptr("mf_norm.weight"), self.gptr("mf_norm.bias"),
+                      self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
+                      w.emb_ws.numel(), w.red_list.address, pa, 1, clk, tab, b1, b2, eps_a, wd,
+                      st)
+            w.applied = True
         else:
             _lib.call("ncf_embedding_bwd_reduce_bf16" if bf16 else "ncf_embedding_bwd_reduce", n,
                       D, d_rows[0], d_rows[1],

@@ -47,6 +47,10 @@ REDUCE_ASYNC = False
 # measured slower (3 interleaved runs each: 0.3028 / 0.3033 against 0.2866 / 0.2888 ms/step —
 # the 105 MB of partials read beside the embedding backward and the apply slow both)
 EARLY_REDUCE = False
+# The deferred table Adam's apply of the step fused into the embedding backward
+# (ncf_embedding_bwd_reduce_apply_clock: a row steps where its gradient rows complete; the same
+# bits as the separate apply)
+FUSE_APPLY = True
 
 
 class FusedTrainStep:
@@ -154,9 +158,10 @@ class FusedTrainStep:
         d = self.deferred
         side = (d.side_stream() if EARLY_REDUCE and d is not None and d.overlap and not self.graph
                 and not REDUCE_ASYNC else None)
+        fa = d.fused_apply_args(w) if FUSE_APPLY and d is not None else None
         eng.backward(w, user_ids, item_ids, None, targets, drop_p, seed, tables=self.tables_lp,
                      bf16=self.bf16, reduce_async=REDUCE_ASYNC and not self.graph,
-                     reduce_side=side)
+                     reduce_side=side, fused_apply=fa)
         st = _lib.stream_ptr(eng.flat.device)
         b1, b2 = self.betas
         if self.deferred is not None:

@@ -142,6 +142,12 @@ for what in "$@"; do
     *)
       echo "unknown step $what"; exit 2 ;;
   esac
+  # a GPU fault in any log of this step ends the session (exit 99): nothing more runs on the card
+  if grep -qsE "illegal memory access|Memory access fault|GPU fault|hipErrorLaunchFailure|HSA_STATUS_ERROR" \
+      "$OUT/${TAG}_"*"${what%%:*}"*.log; then
+    echo "== $TAG $what: GPU fault in the log, stopping"
+    rc=99
+  fi
   echo "== $TAG $what rc=$rc $(date +%T)"
   if [ $rc -ne 0 ]; then
     tail -40 "$OUT/${TAG}_"*"${what%%:*}"*.log 2>/dev/null

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 T=${1:-r05y}
 bash tools/gpu_run.sh $T fullsize; rc=$?
-[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc   # (99: a GPU fault)
 bash tools/gpu_run.sh $T tests; rc=$?
-[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc   # (99: a GPU fault)
 bash tools/gpu_run.sh $T bench sharded prof pmc
