@@ -15,7 +15,7 @@ Zipf(1.05), negatives uniform; random-init weights.  Inputs are resident in HBM 
 (torchrun's env: RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) before this
 process touches the GPU, and exits with their status; fewer than N visible GPUs is an error.
 
-Every timed leg first runs ``prime`` steps (2 x the deferred Adam's sweep_every = 128 by
+Every timed leg first runs ``prime`` steps (2 x the deferred Adam's sweep_every = 256 by
 default) before its W counted warm-up steps: the deferred table schedule replays, per swept
 row, the zero-gradient steps since that row's stamp, and every stamp starts at 0, so before
 step 2 x sweep_every a sweep replays less than its steady-state share.  Priming puts every leg
@@ -89,7 +89,7 @@ ADAM_REPLAY_SLOTS = {64: 16.19, 128: 15.25}
 # chip VALU issue rate: 256 CUs x 4 SIMDs x 32 lanes per cycle x 2.4 GHz = 78.64 T lane-slots/s
 # (= the 157.3 TF fp32 vector peak with an FMA counted as 2 flops; MI355X_MICROARCH.md)
 VALU_SLOTS_PEAK_T = 78.64
-SWEEP_EVERY = 64  # the deferred table Adam's rolling-sweep period (FusedTrainStep / optim.py)
+SWEEP_EVERY = 128  # the longest rolling-sweep period of the legs (FusedTrainStep's; optim.py: 64)
 
 
 def prime_steps(args) -> int:
@@ -924,14 +924,14 @@ def table_adam_roofline(acct, D):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # the deferred table Adam reaches steady state after 2 x sweep_every (= 128) steps: before
+    # the deferred table Adam reaches steady state after 2 x sweep_every (= 256) steps: before
     # that its rolling sweep replays fewer zero-gradient steps per row than it will later, so
     # the default warm-up covers that transient and the timed region spans >= 3 sweep cycles
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--prime", type=int, default=-1,
                     help="untimed priming steps before the warm-up of every training leg "
-                         "(default 2 x sweep_every = 128: deferred-Adam steady state)")
+                         "(default 2 x sweep_every = 256: deferred-Adam steady state)")
     ap.add_argument("--dry-launch", action="store_true",
                     help="test the --gpus N launcher: ranks join a gloo group and report (no GPU)")
     ap.add_argument("--users", type=int, default=1_000_000)

@@ -48,6 +48,12 @@ SCALAR_PAD = 4096
 # replay beside the backward slows it more than it saves on the critical path; round 3 found
 # the same for three placements of it)
 EARLY_CATCHUP = False
+# Late catch-up: the same catch-up of the next batch's rows, queued once this step's table Adam
+# has run inside the embedding backward (trainer.FUSE_APPLY) — on the side stream behind the
+# sweep and the sort, beside the dense-gradient reductions (memory-bound, like it) instead of
+# beside the compute-bound backward; nothing to lock (the step's rows already carry its stamp).
+# The next step then skips its own catch-up launch for that batch.
+LATE_CATCHUP = True
 # HIP stream priority of the overlapped sweep's side stream (torch.cuda.Stream priority: 0 the
 # default, -1 high)
 SIDE_PRIORITY = 0
@@ -371,6 +377,12 @@ class DeferredTableAdam:
         w.deduped = True
         if self.clock is not None and n > 0:   # both kinds in one launch
             self._ensure(self.t + 1)
+            if getattr(w, "late_t", None) == self.t:
+                # (the late catch-up of the previous step brought this very set current through
+                # step t: its catch-up would replay nothing)
+                w.late_t = None
+                self._locked = False
+                return
             pairs = self._pairs_for(w)
             # (locked: an early catch-up of the next batch may run during this step)
             lock = 1 if EARLY_CATCHUP else 0
@@ -435,6 +447,21 @@ class DeferredTableAdam:
         if not (EARLY_CATCHUP and self.clock is not None and getattr(self, "_locked", False)
                 and n > 0):
             return False
+        self._catchup_next(rows, n, stream)
+        return True
+
+    def late_catchup(self, rows, n, stream):
+        """The next batch's unique rows (a dedup set, as early_catchup) caught up through the
+        step now running, on `stream`, which must be ordered after this step's table apply (the
+        apply fused into the embedding backward) and its sweep; the set is marked, so the next
+        step's prepare skips its catch-up.  The caller joins `stream` before the clock advance."""
+        if self.clock is None or n <= 0:
+            return False
+        self._catchup_next(rows, n, stream)
+        rows["late_t"] = self.t + 1
+        return True
+
+    def _catchup_next(self, rows, n, stream):
         self._ensure(self.t + 2)
         cache = self.__dict__.setdefault("_early_pairs", {})
         key = (getattr(self, "_gen", 0), rows["uniq_u"].data_ptr(), rows["uniq_i"].data_ptr())
@@ -448,7 +475,6 @@ class DeferredTableAdam:
         _lib.call("ncf_adam_pairs_catchup_lock_clock", ctypes.addressof(pairs), 2,
                   self.engine.model.mlp_embedding_dim, ptr(rows["num_unique"]), n, 1, 0,
                   ptr(self.clock), ptr(self._table), *self._consts(), stream)
-        return True
 
     def fused_apply_args(self, w):
         """The arguments of the apply fused into the embedding backward (engine.backward

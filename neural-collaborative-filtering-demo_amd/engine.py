@@ -765,7 +765,8 @@ class NCFEngine:
                  targets: Optional[torch.Tensor], drop_p: float, seed: int,
                  loss_denominator: float = 0.0, tables=None, rows=None, uniq=None,
                  reduce_async: bool = False, bf16: bool = False, grad_rows=None,
-                 table_ld: Optional[int] = None, reduce_side=None, fused_apply=None):
+                 table_ld: Optional[int] = None, reduce_side=None, fused_apply=None,
+                 tables_done=None):
         """Gradients of every used parameter.  Dense grads land in the flat grad buffer; table
         grads stay compact (self.pending) for the fused Adam step.  ``reduce_async``: the
         deferred reductions (every dense gradient) run on a side stream, beside whatever the
@@ -776,7 +777,8 @@ class NCFEngine:
         embedding backward and the table Adam (join_reductions orders them).  ``fused_apply``
         (DeferredTableAdam.fused_apply_args): the table Adam's apply of this step runs inside the
         embedding backward (ncf_embedding_bwd_reduce_apply_clock; w.applied tells the deferred
-        schedule).  ``grad_rows = (buf, rows_u,
+        schedule).  ``tables_done()`` is called right after the embedding backward is queued
+        (before the dense-gradient reductions).  ``grad_rows = (buf, rows_u,
         rows_i)``: the table gradients of unique row c go to row rows_*[c] of buf ([mf | mlp]
         halves, 2 D floats per row: the row-sharded step's send buffer) instead of w.G."""
         m = self.model
@@ -970,6 +972,8 @@ class NCFEngine:
                       ptr(uq_i), self.gptr("mf_norm.weight"), self.gptr("mf_norm.bias"),
                       self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
                       w.emb_ws.numel(), w.red_list.address, st)
+        if tables_done is not None:
+            tables_done()
         self.join(dev, joins)
         self._sweep_fork("reduce")
         if reduce_async:

@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from . import deferred as deferred_mod
 from ._lib import ptr
 
 log = logging.getLogger(__name__)
@@ -51,6 +52,12 @@ EARLY_REDUCE = False
 # (ncf_embedding_bwd_reduce_apply_clock: a row steps where its gradient rows complete; the same
 # bits as the separate apply)
 FUSE_APPLY = True
+# The rolling sweep's period (every row current at least every SWEEP_EVERY steps).  A longer
+# period halves the sweep's HBM traffic beside the forward; the replayed element-steps are the
+# same in total (moved from the sweep to the catch-up, which now runs beside the reductions:
+# deferred.LATE_CATCHUP).  At C2 steady state, 3 interleaved runs each: 0.2703 / 0.2709 ms/step
+# at 128 against 0.2769-0.2794 at 64 (tools/step_ab.py, primed 2 x the period).
+SWEEP_EVERY = 128
 
 
 class FusedTrainStep:
@@ -69,7 +76,7 @@ class FusedTrainStep:
     the two are bit-identical).  Inputs are copied into static buffers before each replay."""
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5,
-                 deferred: bool = True, sweep_every: int = 64, graph: bool = False,
+                 deferred: bool = True, sweep_every: int = SWEEP_EVERY, graph: bool = False,
                  clock: Optional[bool] = None, warmup: int = 2, concurrent: Optional[bool] = None,
                  overlap_sweep: Optional[bool] = None, table_dtype: torch.dtype = torch.float32):
         self.model = model
@@ -159,9 +166,11 @@ class FusedTrainStep:
         side = (d.side_stream() if EARLY_REDUCE and d is not None and d.overlap and not self.graph
                 and not REDUCE_ASYNC else None)
         fa = d.fused_apply_args(w) if FUSE_APPLY and d is not None else None
+        late, self._late_next = getattr(self, "_late_next", None), None
+        done = (lambda: self._late_catchup(*late)) if late is not None and fa is not None else None
         eng.backward(w, user_ids, item_ids, None, targets, drop_p, seed, tables=self.tables_lp,
                      bf16=self.bf16, reduce_async=REDUCE_ASYNC and not self.graph,
-                     reduce_side=side, fused_apply=fa)
+                     reduce_side=side, fused_apply=fa, tables_done=done)
         st = _lib.stream_ptr(eng.flat.device)
         b1, b2 = self.betas
         if self.deferred is not None:
@@ -192,6 +201,24 @@ class FusedTrainStep:
                       ptr(self.v_flat), eng.flat.numel(), self.lr, b1, b2, self.eps, self.wd,
                       float(self.step_count + 1), st)
         return w
+
+    def _late_catchup(self, s, n):
+        """deferred.LATE_CATCHUP: the next batch's rows (dedup set s, sorted on the side stream)
+        caught up through this step there, after this step's table apply (queued just before, in
+        the embedding backward) — beside the dense-gradient reductions; the step's sweep join
+        (before the clock advance) waits for it."""
+        d = self.deferred
+        side = d.side_stream()
+        ev = self._event()
+        ev.record(_lib.stream_ptr(self.model.engine.flat.device))
+        ev.wait(side.cuda_stream)
+        if _lib.PROFILE is not None:     # (the per-launch instrumentation times it on its stream)
+            with torch.cuda.stream(side):
+                d.late_catchup(s, n, side.cuda_stream)
+        else:
+            d.late_catchup(s, n, side.cuda_stream)
+        d.sweep_done(side.cuda_stream)
+        d._joined = False
 
     # ---- pipelined dedup: the id sort of step t+1 runs on a side stream under step t
     def _event(self):
@@ -224,7 +251,10 @@ class FusedTrainStep:
         if side is not None:
             self._enqueue_dedup(s, w, uid, iid, side)
             # its rows this step does not touch caught up through this step behind the sort
-            self.deferred.early_catchup(s, uid.numel(), side.cuda_stream)
+            # (early), or once this step's apply has run (late: _late_catchup)
+            if not self.deferred.early_catchup(s, uid.numel(), side.cuda_stream) and \
+                    deferred_mod.LATE_CATCHUP and FUSE_APPLY:
+                self._late_next = (s, uid.numel())
             # the sweep's done-event re-recorded behind the sort: the step's sweep join (before
             # the clock advance) then orders the sort too, and the next step waits for nothing
             d = self.deferred
@@ -241,6 +271,7 @@ class FusedTrainStep:
         m = self.model
         u = uid.reshape(-1)
         i = iid.reshape(-1)
+        s.pop("late_t", None)
         _lib.call("ncf_dedup_ids", ptr(u), ptr(i), u.numel(), w.g.D, m.num_users,
                   m.num_products, ptr(s["uniq_u"]), ptr(s["uniq_i"]), None, None,
                   ptr(s["num_unique"]), ptr(s["emb_ws"]), s["emb_ws"].numel(), side.cuda_stream)
@@ -258,6 +289,7 @@ class FusedTrainStep:
         s = sets[sets[2]]
         w.emb_ws, w.uniq_u, w.uniq_i, w.num_unique = s["emb_ws"], s["uniq_u"], s["uniq_i"], s["num_unique"]
         w.prededuped = None
+        late_t, w.late_t = s.pop("late_t", None), None
         if pend is not None:
             cur = torch.cuda.current_stream(self.model.engine.flat.device)
             if pend[2] is None:               # sorted behind the sweep: joined with it
@@ -266,6 +298,7 @@ class FusedTrainStep:
                 pend[2].wait(cur.cuda_stream)  # (also orders a stale prefetch before reuse)
             if pend[0] is uid and pend[1] is iid:
                 w.prededuped = True
+                w.late_t = late_t
 
     def __call__(self, user_ids: torch.Tensor, item_ids: torch.Tensor, targets: torch.Tensor,
                  M: Optional[int] = None, next=None):

@@ -884,12 +884,13 @@ def test_attn_block_eval_forward_matches_unfused(monkeypatch):
     torch.testing.assert_close(res[1], res[0], rtol=0, atol=2e-6)
 
 
-@pytest.mark.parametrize("sweep_every", [64, 0])
-def test_deferred_adam_bitwise_equals_dense(sweep_every):
-    """The deferred schedule reproduces the dense-exact sweep bit for bit (70 steps: crosses a
-    periodic sweep at 64; sweep_every=0 exercises long catch-up chains only)."""
-    a_sd, a_m = _fused_run(False, 70)
-    b_sd, b_m = _fused_run(True, 70, sweep_every=sweep_every)
+@pytest.mark.parametrize("sweep_every,steps", [(64, 70), (128, 140), (0, 70)])
+def test_deferred_adam_bitwise_equals_dense(sweep_every, steps):
+    """The deferred schedule reproduces the dense-exact sweep bit for bit (crossing a periodic
+    sweep at 64 / at 128, FusedTrainStep's default; sweep_every=0 exercises long catch-up chains
+    only)."""
+    a_sd, a_m = _fused_run(False, steps)
+    b_sd, b_m = _fused_run(True, steps, sweep_every=sweep_every)
     for k in a_sd:
         assert torch.equal(a_sd[k], b_sd[k]), k
     for k in a_m:
@@ -954,6 +955,51 @@ def test_early_reduce_bitwise_equals_dense(monkeypatch):
         assert torch.equal(a_sd[k], b_sd[k]), k
     for k in a_m:
         assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
+
+
+@pytest.mark.parametrize("tables", ["fp32", "bf16"])
+def test_fused_apply_bitwise_equals_separate_apply(monkeypatch, tables):
+    """The table Adam's apply fused into the embedding backward (trainer.FUSE_APPLY,
+    ncf_embedding_bwd_reduce_apply_clock: single-piece segments step in the reduce, longer ones in
+    the fix-up) against the separate ncf_adam_pairs_apply_clock launch, bit for bit: 24 steps with
+    dropout, the overlapped sweep every 8 steps, the pipelined sort, hot items (40 of them: long
+    multi-piece segments) and fp32 / bf16 tables."""
+    import ncf_amd.trainer as Tr
+    out = []
+    for fuse in (False, True):
+        monkeypatch.setattr(Tr, "FUSE_APPLY", fuse)
+        out.append(_fused_run(True, 24, sweep_every=8, I=40, dropout=0.2, clock=True,
+                              overlap_sweep=True, pipelined=True,
+                              table_dtype=torch.bfloat16 if tables == "bf16" else torch.float32))
+    (a_sd, a_m), (b_sd, b_m) = out
+    for k in a_sd:
+        assert torch.equal(a_sd[k], b_sd[k]), k
+    for k in a_m:
+        assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
+
+
+def test_late_catchup_bitwise_equals_dense(monkeypatch):
+    """The next batch's catch-up queued behind this step's fused table apply, beside the
+    dense-gradient reductions (deferred.LATE_CATCHUP), and the next step skipping its own
+    catch-up, against the dense schedule bit for bit (dropout, sweep every 8 steps); and against
+    the late catch-up off."""
+    import ncf_amd.deferred as Dm
+    import ncf_amd.trainer as Tr
+    monkeypatch.setattr(Tr, "FUSE_APPLY", True)
+    pairs = []
+    for drop in (0.2, 0.0):
+        runs = []
+        for late in (True, False):
+            monkeypatch.setattr(Dm, "LATE_CATCHUP", late)
+            runs.append(_fused_run(True, 30, sweep_every=8, dropout=drop, clock=True,
+                                   overlap_sweep=True, pipelined=True))
+        pairs.append(runs)
+    pairs.append([pairs[1][0], _fused_run(False, 30)])   # (the dense schedule: no dropout)
+    for (b_sd, b_m), (a_sd, a_m) in pairs:
+        for k in a_sd:
+            assert torch.equal(a_sd[k], b_sd[k]), k
+        for k in a_m:
+            assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
 
 
 def test_pipelined_dedup_bitwise_equals_inline():

@@ -86,15 +86,17 @@ def main():
                 for s in range(first, first + count):
                     u, i, t = batches[s % len(batches)]
                     step(u, i, t, next=batches[(s + 1) % len(batches)][:2])
-            run(0, 150)
+            # (the deferred schedule's steady state: 2 x sweep_every steps, bench.py's prime)
+            p0 = max(150, 2 * int(step.deferred.sweep_every if step.deferred else 0) + 20)
+            run(0, p0)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            run(150, args.steps)
+            run(p0, args.steps)
             torch.cuda.synchronize()
             res[name].append((time.perf_counter() - t0) / args.steps * 1e3)
             if rep == 0:
                 _lib.PROFILE = []
-                run(150 + args.steps, 20)
+                run(p0 + args.steps, 20)
                 torch.cuda.synchronize()
                 p, _lib.PROFILE = _lib.PROFILE, None
                 per = {}
