@@ -1026,6 +1026,105 @@ __global__ __launch_bounds__(256) void k_sample16(const float* __restrict__ q, i
   }
 }
 
+// The group-maxima form of k_sample16 (G = 8) with the MFMA operands swapped: items are the A
+// operand (rows of the accumulator) and users the B operand (its columns), and the 32 items of a
+// tile are laid along the rows so that the eight accumulator registers a lane holds for rows
+// {0-3, 8-11} + 4h (and {16-19, 24-27} + 4h) are eight consecutive sample items: a group's
+// maximum is a register max, no cross-lane shuffles.  The lane's group maxima go to LDS and
+// leave as whole 32-byte runs of each user's row (16 groups per workgroup), instead of 2-byte
+// stores scattered over 32 rows.  Users vary fastest over the grid, so the ~80 workgroups that
+// read one 128-item block of the sample run back to back (one fetch per XCD, not one per user
+// block).  The same products in the same order per element (p0 q0, p1 q0, p0 q1 against k_sample16's
+// q0 p0, q0 p1, q1 p0), the same rounding: bit for bit k_sample16<T, 8>.
+template <int T>
+__global__ __launch_bounds__(256) void k_sample16t(const float* __restrict__ q, int64_t n_users,
+                                                   const uint16_t* __restrict__ items3,
+                                                   int64_t n_items, int64_t stride,
+                                                   const float* __restrict__ sbias, int64_t S,
+                                                   _Float16* __restrict__ out) {
+  constexpr int D = 64, J = 128, G = 8, NG = J / G;
+  const int64_t Sg = (S + G - 1) / G;
+  __shared__ __attribute__((aligned(16))) uint16_t ps[T][J][kP3];
+  __shared__ float bs[J];
+  __shared__ _Float16 og[4][32][NG + 2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 31, h = lane >> 5;
+  const int64_t u0 = (int64_t)blockIdx.x * 128 + 32 * w;
+  const int64_t j0 = (int64_t)blockIdx.y * J;
+  constexpr int CH = T * J * (D / 8);   // 16-B chunks
+  uint4 pv[CH / 256];
+#pragma unroll
+  for (int c = 0; c < CH / 256; ++c) {
+    const int e = tid + 256 * c, pl = e / (J * 8), jj = (e / 8) % J, k8 = (e % 8) * 8;
+    const int64_t j = j0 + jj;
+    pv[c] = j < S ? *reinterpret_cast<const uint4*>(items3 + (int64_t)pl * n_items * D + j * stride * D + k8)
+                  : make_uint4(0u, 0u, 0u, 0u);
+  }
+  const float bb0 = tid < J && j0 + tid < S ? sbias[j0 + tid] : 0.0f;
+  bf16x8_t b[T][4];   // this lane's user (column i), k = 32 h + 8 t .. + 7 of chunk t
+  {
+    const int64_t u = u0 + i < n_users ? u0 + i : n_users - 1;
+    const float* qp = q + u * D + 32 * h;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float4 x = ld4(qp + 8 * t), y = ld4(qp + 8 * t + 4);
+      const float v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int jv = 0; jv < 8; ++jv) {
+        __bf16 b0, b1, b2;
+        split3(v[jv], b0, b1, b2);
+        b[0][t][jv] = b0;
+        if (T > 1) b[T > 1 ? 1 : 0][t][jv] = b1;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CH / 256; ++c) {
+    const int e = tid + 256 * c, pl = e / (J * 8), jj = (e / 8) % J, k8 = (e % 8) * 8;
+    *reinterpret_cast<uint4*>(&ps[pl][jj][k8]) = pv[c];
+  }
+  if (tid < J) bs[tid] = j0 + tid < S ? bb0 : -INFINITY;   // (past S: the group max's -inf)
+  __syncthreads();
+  // accumulator row m = (r & 3) + 8 (r >> 2) + 4 h holds tile item it(m): rows of register
+  // quarter q = r >> 2 and half h -> group 2 (q >> 1) + h, position (r & 3) + 4 (q & 1)
+  const int mrow = i;   // this lane's A row
+  const int it_a = 8 * (2 * ((mrow >> 3) >> 1) + ((mrow >> 2) & 1)) + (mrow & 3) + 4 * ((mrow >> 3) & 1);
+#pragma unroll
+  for (int jt = 0; jt < J / 32; ++jt) {
+    f32x16 acc = {};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(&ps[0][32 * jt + it_a][32 * h + 8 * t]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[0][t], acc, 0, 0, 0);
+      if (T > 1) {
+        const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(&ps[T > 1 ? 1 : 0][32 * jt + it_a][32 * h + 8 * t]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[0][t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[T > 1 ? 1 : 0][t], acc, 0, 0, 0);
+      }
+    }
+    float g[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const float* bg = bs + 32 * jt + 8 * (2 * half + h);   // the group's 8 biases (broadcast)
+      float v = -INFINITY;
+#pragma unroll
+      for (int r = 8 * half; r < 8 * half + 8; ++r)
+        v = fmaxf(v, acc[r] + bg[(r & 3) + 4 * ((r >> 2) & 1)]);
+      g[half] = v;
+    }
+    og[w][i][4 * jt + h] = __builtin_bit_cast(_Float16, __ocml_cvtrtn_f16_f32(g[0]));
+    og[w][i][4 * jt + 2 + h] = __builtin_bit_cast(_Float16, __ocml_cvtrtn_f16_f32(g[1]));
+  }
+  __syncthreads();
+  // the wave's 32 users x 16 groups: 16 consecutive lanes write one user's 32-byte run
+  const int64_t g0 = j0 / G;
+#pragma unroll
+  for (int s = 0; s < 32 * NG / 64; ++s) {
+    const int e = lane + 64 * s, uu = e / NG, gl = e % NG;
+    const int64_t u = u0 + uu;
+    if (u < n_users && g0 + gl < Sg) out[u * Sg + g0 + gl] = og[w][uu][gl];
+  }
+}
+
 template <bool RS>
 __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user_list,
                                                 int64_t n_users, const uint32_t* __restrict__ count,
@@ -1348,10 +1447,12 @@ extern "C" int ncf_score_sample_split16(const float* queries, int64_t n_users,
   if (n_users == 0) return NCF_OK;
   const dim3 grid((unsigned)ncf_cdiv(S, 128), (unsigned)ncf_cdiv(n_users, 128));
   _Float16* o = reinterpret_cast<_Float16*>(out);
-  if (group == 8)
-    hipLaunchKernelGGL((k_sample16<2, 8>), grid, dim3(256), 0, (hipStream_t)stream, queries,
+  if (group == 8) {
+    NCF_CHECK_ARG(ncf_cdiv(S, 128) <= 65535, "ncf_score_sample_split16: S too large");
+    const dim3 gt((unsigned)ncf_cdiv(n_users, 128), (unsigned)ncf_cdiv(S, 128));
+    hipLaunchKernelGGL((k_sample16t<2>), gt, dim3(256), 0, (hipStream_t)stream, queries,
                        n_users, items3, n_items, stride, sample_bias, S, o);
-  else
+  } else
     hipLaunchKernelGGL((k_sample16<2, 1>), grid, dim3(256), 0, (hipStream_t)stream, queries,
                        n_users, items3, n_items, stride, sample_bias, S, o);
   NCF_CHECK_LAUNCH("ncf_score_sample_split16");

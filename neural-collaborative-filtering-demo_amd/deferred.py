@@ -487,12 +487,16 @@ class DeferredTableAdam:
         return (ctypes.addressof(pairs), ptr(self.clock), ptr(self._table)) + self._consts()
 
     # ---- after the backward: this step's gradient on the touched rows
-    def apply(self, w, st):
+    def apply(self, w, st, late_join: bool = False):
+        """``late_join`` (the step's table apply already ran inside the embedding backward): the
+        side stream is not joined here; the caller joins it (sweep_join) before the clock
+        advance.  Only when no sweep part is owed (those run on st and must follow the join)."""
         n = w.g.n
         if self.clock is not None:
             self._ensure(self.t + 1)
-            self.sweep_join()
-            self._settle(st)
+            if not (late_join and getattr(w, "applied", False) and not self._owed):
+                self.sweep_join()
+                self._settle(st)
             if n > 0 and not getattr(w, "applied", False):
                 pairs = self._pairs_for(w)
                 _lib.call("ncf_adam_pairs_apply_clock", ctypes.addressof(pairs), 2,

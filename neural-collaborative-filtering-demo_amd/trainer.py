@@ -58,6 +58,14 @@ FUSE_APPLY = True
 # deferred.LATE_CATCHUP).  At C2 steady state, 3 interleaved runs each: 0.2703 / 0.2709 ms/step
 # at 128 against 0.2769-0.2794 at 64 (tools/step_ab.py, primed 2 x the period).
 SWEEP_EVERY = 128
+# The step's join of the side stream (sweep, next sort, late catch-up) after the dense Adam
+# rather than before it: the flat Adam (ncf_adam_flat_clock) runs first, then the join, then the
+# clock advance (ncf_step_clock_advance) that the side kernels must not see early.  A join whose
+# event is still pending costs the queue ~10 us after the signal (tools/event_cost.py); placed
+# later, the side work is usually complete when the queue reaches it.  Off: measured neutral
+# (3 interleaved runs each, 0.2706 / 0.2714 against 0.2706 / 0.2707 ms/step: the separate
+# clock-advance launch costs what the later join saves)
+SPLIT_CLOSE = False
 
 
 class FusedTrainStep:
@@ -173,8 +181,10 @@ class FusedTrainStep:
                      reduce_side=side, fused_apply=fa, tables_done=done)
         st = _lib.stream_ptr(eng.flat.device)
         b1, b2 = self.betas
+        split = (SPLIT_CLOSE and self.deferred is not None and self.clock is not None
+                 and not self.graph and self.deferred.overlap)
         if self.deferred is not None:
-            self.deferred.apply(w, st)
+            self.deferred.apply(w, st, late_join=split)
         elif self.bf16:      # dense bf16 sweep (the reference schedule of the bf16 tables)
             D = self.model.mlp_embedding_dim
             for key, lp in self.tables_lp.items():
@@ -189,7 +199,13 @@ class FusedTrainStep:
             key_of = {id(p): k for k, p in self.tables.items()}
             eng.adam_tables(hp, lambda p: self.state[key_of[id(p)]], float(self.step_count + 1), st)
         eng.join_reductions()
-        if self.clock is not None:
+        if self.clock is not None and split:
+            _lib.call("ncf_adam_flat_clock", ptr(eng.flat), ptr(eng.flat_grad), ptr(self.m_flat),
+                      ptr(self.v_flat), eng.flat.numel(), ptr(self.deferred._table), 1,
+                      ptr(self.clock), b1, b2, self.eps, self.wd, st)
+            self.deferred.sweep_join()       # (the clock advance below changes its target)
+            _lib.call("ncf_step_clock_advance", ptr(self.clock), self.base_seed, st)
+        elif self.clock is not None:
             if self.deferred is not None:
                 self.deferred.sweep_join()   # (the clock advance below changes its target)
             _lib.call("ncf_adam_flat_clock_close", ptr(eng.flat), ptr(eng.flat_grad),

@@ -982,7 +982,8 @@ def test_late_catchup_bitwise_equals_dense(monkeypatch):
     """The next batch's catch-up queued behind this step's fused table apply, beside the
     dense-gradient reductions (deferred.LATE_CATCHUP), and the next step skipping its own
     catch-up, against the dense schedule bit for bit (dropout, sweep every 8 steps); and against
-    the late catch-up off."""
+    the late catch-up off, and the step's side-stream join before the flat Adam instead of after
+    it (trainer.SPLIT_CLOSE)."""
     import ncf_amd.deferred as Dm
     import ncf_amd.trainer as Tr
     monkeypatch.setattr(Tr, "FUSE_APPLY", True)
@@ -995,6 +996,10 @@ def test_late_catchup_bitwise_equals_dense(monkeypatch):
                                    overlap_sweep=True, pipelined=True))
         pairs.append(runs)
     pairs.append([pairs[1][0], _fused_run(False, 30)])   # (the dense schedule: no dropout)
+    monkeypatch.setattr(Dm, "LATE_CATCHUP", True)
+    monkeypatch.setattr(Tr, "SPLIT_CLOSE", False)      # the side stream joined before the flat Adam
+    pairs.append([pairs[0][0], _fused_run(True, 30, sweep_every=8, dropout=0.2, clock=True,
+                                          overlap_sweep=True, pipelined=True)])
     for (b_sd, b_m), (a_sd, a_m) in pairs:
         for k in a_sd:
             assert torch.equal(a_sd[k], b_sd[k]), k

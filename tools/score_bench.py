@@ -1,7 +1,10 @@
 """C5 scoring micro-benchmark (GPU only): 10K users x 1M items top-K through ncf_amd.scoring.
 
-    python tools/score_bench.py [--users 10000] [--items 1000000] [--k 10 100]
-Prints per-stage device times and pairs/s."""
+    python tools/score_bench.py [--users 10000] [--items 1000000] [--k 10 100] [--graph]
+        [--set scoring.CONST=value ...]
+Prints per-stage device times and pairs/s (eager), and with --graph the GraphedScorer time (the
+bench's C5 line).  --set overrides ncf_amd module constants before anything runs (A/B)."""
+import importlib
 import argparse
 import os
 import sys
@@ -14,7 +17,7 @@ import _ncf_pkg  # noqa: E402
 
 ncf = _ncf_pkg.load()
 from ncf_amd import _lib  # noqa: E402
-from ncf_amd.scoring import ItemIndex, score_topk  # noqa: E402
+from ncf_amd.scoring import GraphedScorer, ItemIndex, score_topk  # noqa: E402
 
 
 def main():
@@ -24,7 +27,16 @@ def main():
     ap.add_argument("--num-users", type=int, default=1000000)
     ap.add_argument("--k", type=int, nargs="+", default=[10, 100])
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--set", nargs="*", default=[])
     a = ap.parse_args()
+    for spec in a.set:
+        path, _, val = spec.partition("=")
+        mod, _, const = path.rpartition(".")
+        mm = importlib.import_module("ncf_amd." + mod)
+        old = getattr(mm, const)
+        setattr(mm, const, type(old)(int(val)) if isinstance(old, (bool, int)) else type(old)(val))
+        print(f"set {path} = {getattr(mm, const)!r}", flush=True)
     dev = torch.device("cuda")
     torch.manual_seed(0)
     m = ncf.AdvancedNCF(a.num_users, a.items, 5, 24).to(dev)
@@ -65,6 +77,18 @@ def main():
         pairs = a.users * a.items
         print(f"k={k}: {best * 1e3:.2f} ms  {pairs / best / 1e9:.1f} G pairs/s  "
               + " ".join(f"{n}={v:.2f}ms" for n, v in per.items()), flush=True)
+        if a.graph:
+            sc = GraphedScorer(m, n_users=a.users, k=k, index=idx)
+            sc(users, copy=False)
+            torch.cuda.synchronize()
+            g = 1e9
+            for _ in range(max(3, a.reps)):
+                t0 = time.perf_counter()
+                sc(users, copy=False)
+                torch.cuda.synchronize()
+                g = min(g, time.perf_counter() - t0)
+            print(f"k={k}: graphed {g * 1e3:.3f} ms", flush=True)
+            del sc
 
 
 if __name__ == "__main__":
