@@ -566,7 +566,18 @@ constexpr int kUB3t = NCF_SCORE3_UB > 2 ? 2 : NCF_SCORE3_UB;   // (three-term sc
 #ifndef NCF_SCORE3_NW
 #define NCF_SCORE3_NW 8
 #endif
-constexpr int kNW3 = NCF_SCORE3_NW;   // waves per workgroup (measured: 8 at one per CU 6.6 ms, 4 at two per CU 6.9)
+constexpr int kNW3 = NCF_SCORE3_NW;
+#ifndef NCF_SCAN_NB
+#define NCF_SCAN_NB 0
+#endif
+// the one-term scan without the per-tile barrier: measured no faster (graphed top-10 2.33 / 2.34
+// against 2.31 / 2.32 ms; scan 1.89-1.91 against 1.86-1.87 ms, r5zi) — the waits it removes were
+// on LDS bandwidth (the per-tile threshold and operand reads), not on the barrier itself
+constexpr bool kScanNB = NCF_SCAN_NB != 0;
+#ifndef NCF_SCAN_MINTH
+#define NCF_SCAN_MINTH 1
+#endif
+constexpr bool kScanMinTh = NCF_SCAN_MINTH != 0;   // the register-only first reject (k_collect3)   // waves per workgroup (measured: 8 at one per CU 6.6 ms, 4 at two per CU 6.9)
 // Candidates staged per wave (its own LDS slice, dynamic LDS).  A full slice is written out
 // grouped by user: one global counter atomic per (user, flush) and each user's entries stored
 // contiguously, instead of one atomic and two scattered 4-byte stores per candidate (measured
@@ -648,7 +659,12 @@ __device__ __forceinline__ void flush_grouped(
   wave_lds_sync();
 }
 
-template <int UB, int NW, int T>
+// NB (one-term scan only): no shared item tiles and no workgroup barrier — every wave loads its
+// own B operands (the 32 items' 16-byte fragments of each MFMA step) straight into registers, one
+// tile ahead, and runs at its own pace; the eight waves of a workgroup read the same item lines,
+// which L1 / L2 serve.  (The shared-tile form parks each wave at the per-tile barrier until the
+// slowest wave's filter is done: 38% of the wave time at top-10, r4h SQ counters.)
+template <int UB, int NW, int T, bool NB = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_collect3(
     const float* __restrict__ q, const int32_t* __restrict__ user_list, int64_t n_users,
     const uint16_t* __restrict__ items3, const float* __restrict__ bias, int64_t n_items,
@@ -709,6 +725,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       t[4 * c] = x.x; t[4 * c + 1] = x.y; t[4 * c + 2] = x.z; t[4 * c + 3] = x.w;
     }
   };
+  // (kScanMinTh) the smallest threshold of the 16 users each lane's rows hold, per user block
+  float thmin[UB];
+  if constexpr (kScanMinTh) {
+    wave_lds_sync();
+#pragma unroll
+    for (int ub = 0; ub < UB; ++ub) {
+      float t[16];
+      th_of(ub, t);
+      float m = t[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) m = fminf(m, t[r]);
+      thmin[ub] = m;
+    }
+  }
   const int64_t it0 = (int64_t)bx * items_per_block;
   const int64_t it1 = min(n_items, it0 + items_per_block);
   // staging: thread (item sj, column group sk) holds 4 bf16 of each of the 3 planes of the next
@@ -780,11 +810,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
     staged = 0;
   };
-  auto filt = [&](const f32x16& acc, int ub, int bb, int64_t t0) {
+  auto filt = [&](const f32x16& acc, int ub, float b, int64_t t0) {
+    const int32_t item = (int32_t)(t0 + i);
+    if constexpr (kScanMinTh) {
+      // Weakest test first, from registers: the lane's largest logit against the smallest of its
+      // 16 users' thresholds.  Exact, no margin: a row the exact test accepts has
+      // fl(acc[r] + b) >= th[r] >= thmin, and fl(max acc + b) >= fl(acc[r] + b) (rounding is
+      // monotone).  Only tiles it passes read the 16 thresholds from LDS.
+      f32x2 mx = {acc[0], acc[1]};
+#pragma unroll
+      for (int r = 2; r < 16; r += 2) mx = __builtin_elementwise_max(mx, f32x2{acc[r], acc[r + 1]});
+      if (!__ballot(t0 + i < it1 && fmaxf(mx.x, mx.y) + b >= thmin[ub])) return;
+    }
     float th[16];
     th_of(ub, th);
-    const int32_t item = (int32_t)(t0 + i);
-    const float b = bs[bb][i];
     const bool ivalid = t0 + i < it1;
     // Cheap reject first: max_r (acc[r] - th[r]) + b on packed fp32 (8 v_pk_add + 8 max).  The
     // margin keeps every lane the exact test below could accept (they round differently by at
@@ -821,7 +860,43 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   // issued behind each step's MFMAs), filters it, stores tile t + 2 into buffer (t + 2) % 3 (it
   // held tile t - 1, whose reads completed before the previous barrier), loads tile t + 3 into
   // the ring, and ends at the barrier that publishes tile t + 2.
-  if (it0 < it1) {
+  if constexpr (NB) {
+    static_assert(T == 1, "the barrier-free scan is the one-term scan");
+    wave_lds_sync();   // (this wave's thresholds, written above)
+    if (it0 < it1) {
+      uint4 bcur[4], bnxt[4];
+      float bcur_b = 0.f, bnxt_b = 0.f;
+      auto gload = [&](int64_t t0, uint4 (&v)[4], float& bb) {
+        const int64_t item = t0 + i;
+        const int64_t src = item < it1 ? item : it0;   // clamped, unconditional
+        const uint16_t* base = items3 + src * D + 32 * h;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = *reinterpret_cast<const uint4*>(base + 8 * t);
+        bb = bias[src];
+      };
+      gload(it0, bcur, bcur_b);
+      for (int64_t t0 = it0; t0 < it1; t0 += kItemTile) {
+        if (t0 + kItemTile < it1) gload(t0 + kItemTile, bnxt, bnxt_b);
+        f32x16 acc[UB];
+#pragma unroll
+        for (int ub = 0; ub < UB; ++ub)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[ub][r] = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const bf16x8_t b0 = __builtin_bit_cast(bf16x8_t, bcur[t]);
+#pragma unroll
+          for (int ub = 0; ub < UB; ++ub)
+            acc[ub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ub][t], b0, acc[ub], 0, 0, 0);
+        }
+#pragma unroll
+        for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, bcur_b, t0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bcur[t] = bnxt[t];
+        bcur_b = bnxt_b;
+      }
+    }
+  } else if (it0 < it1) {
     fetch(it0);
     put(0);
     if (it0 + kItemTile < it1) {
@@ -877,7 +952,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       // overlaps one wave's MFMAs with its partner's filter, measured slower: scan 2.51-2.55
       // against 2.19 ms at top-10.)
 #pragma unroll
-      for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, bc, t0);
+      for (int ub = 0; ub < UB; ++ub) filt(acc[ub], ub, bs[bc][i], t0);
       if (t0 + 2 * kItemTile < it1) {
         put(bn2);
         if (t0 + 3 * kItemTile < it1) fetch(t0 + 3 * kItemTile);
@@ -1610,7 +1685,7 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
     const hipError_t e1 = hipFuncSetAttribute((const void*)k_collect3<kUB3, kNW3, 2>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)(kNW3 * slice3_bytes<kUB3, 2>()));
-    const hipError_t e2 = hipFuncSetAttribute((const void*)k_collect3<kUB3, kNW3, 1>,
+    const hipError_t e2 = hipFuncSetAttribute((const void*)k_collect3<kUB3, kNW3, 1, kScanNB>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)(kNW3 * slice3_bytes<kUB3, 1>()));
     if (e0 != hipSuccess || e1 != hipSuccess || e2 != hipSuccess) {
@@ -1630,7 +1705,7 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
                        items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
                        cand_item);
   else
-    hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 1>), dim3((unsigned)(splits * ub)),
+    hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 1, kScanNB>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
                        items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
                        cand_item);
