@@ -150,6 +150,10 @@ def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st, expected=0, t
 # sample + k-th 0.42) against 2.64-2.82 at 1024 (scan 1.99-2.04, sample + k-th 0.21) and
 # 2.99-3.16 at 2048; top-100 takes the rank-j plan, unaffected)
 SAMPLE_CANDS = 512
+# the collect scans its users in threshold order (see _TopKRun.launch).  Off: measured slower
+# (graphed top-10 2.21 / 2.23 against 2.15 / 2.16 ms, r5zk: the scan no faster — the thresholds
+# of a user block are already close — and the sort on top)
+SORT_USERS = False
 # the split scan's item split raised from the expected candidates per user (the launch's
 # expected_per_user: fewer per-wave LDS slice overflows; tested invisible in the results)
 SIZED_SPLIT = True
@@ -280,8 +284,15 @@ class _TopKRun:
             _lib.call("ncf_score_kth", ptr(self.sample), n, self.S, k, None, self.stride,
                       ptr(self.thr), st)
         self.count.zero_()
+        # the scan's users in threshold order (SORT_USERS): its 32-user blocks then hold users of
+        # near-equal thresholds, so its first reject (a lane's best logit against the smallest
+        # of its 16 users' thresholds) is nearly as tight as the per-user test
+        rows = None
+        if SORT_USERS and n >= 64:
+            self.order = torch.argsort(self.thr[:n]).to(torch.int32)
+            rows = ptr(self.order)
         # expected candidates per user: k x I / S (the threshold sample's k-th over S items)
-        _collect(idx, ptr(self.q), None, n, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),
+        _collect(idx, ptr(self.q), rows, n, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),
                  ptr(self.cand_i), st, expected=-(-self.j * I // self.S) if SIZED_SPLIT else 0)
         _select(idx, None, n, self, k, ptr(self.scores), ptr(self.items), ptr(self.overflow), st,
                 check=None if self.thr_chk is None else ptr(self.thr_chk))
