@@ -285,21 +285,28 @@ def embedding_rooflines(totals, per, steps, N, D, grows, nu_ni, pmc=True):
               = (N / M) 16 D; every row written (group_rows 0): N (16 D + 16 + 16 D + 4);
       scatter (ncf_embedding_bwd_reduce): 4 gradient rows in per sample + 2 ids, per unique row
               the 2 table rows (LN recompute) in and 2 compact gradient rows out
-              = N (16 D + 16) + (n_u + n_i) 16 D."""
+              = N (16 D + 16) + (n_u + n_i) 16 D;
+      scatter + apply (ncf_embedding_bwd_reduce_apply_clock, the table Adam fused in): the same,
+              and per unique row its 2 parameter rows out and 4 moment rows in and out, and the
+              stamp = N (16 D + 16) + (n_u + n_i) (56 D + 4)."""
     g_bytes = (N * (16 * D + 20) + (N // grows) * 16 * D if grows > 1
                else N * (16 * D + 16 + 16 * D + 4))
     hbm = {}
+    fused = "ncf_embedding_bwd_reduce_apply_clock" in totals
     for name, kern, nbytes in (
             ("gather", "ncf_gather_ln_gmf_scaled_fwd", g_bytes),
-            ("scatter", "ncf_embedding_bwd_reduce",
-             N * (16 * D + 16) + (sum(nu_ni) * 16 * D if nu_ni else 0))):
+            ("scatter", "ncf_embedding_bwd_reduce_apply_clock" if fused else "ncf_embedding_bwd_reduce",
+             N * (16 * D + 16) + (sum(nu_ni) * ((56 * D + 4) if fused else 16 * D)
+                                  if nu_ni else 0))):
         if kern in totals:
             launches = len(per.get(kern, [])) / steps
             ms = totals[kern] / max(launches, 1)
             gbs = nbytes / (ms * 1e-3) / 1e9
             # (the committed PMC summaries are of the C2 launch: not quoted for other sizes)
             pm = pmc_traffic({"ncf_gather_ln_gmf_scaled_fwd": "k_gather_ln_gmf",
-                              "ncf_embedding_bwd_reduce": "k_piece_reduce_ln"}[kern]) if pmc else None
+                              "ncf_embedding_bwd_reduce": "k_piece_reduce_ln",
+                              "ncf_embedding_bwd_reduce_apply_clock": "k_piece_reduce_ln"}[kern]) \
+                if pmc else None
             hbm[name] = {"entry_point": kern, "bytes_per_launch": nbytes, "ms_per_launch": round(ms, 4),
                          "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS,
                          "frac": round(gbs / HBM_PEAK_GBS, 4),
@@ -309,8 +316,10 @@ def embedding_rooflines(totals, per, steps, N, D, grows, nu_ni, pmc=True):
         hbm["gather"]["round3_count_bytes"] = N * (16 * D + 16 + 16 * D + 4)
     if "scatter" in hbm:
         hbm["scatter"]["unique_rows"] = nu_ni
-        hbm["scatter"]["note"] = ("segment reduce + LN backward (+ the multi-piece fix-up); the id "
-                                  "sort before it (ncf_dedup_ids) is listed in kernel_ms_per_step")
+        hbm["scatter"]["note"] = ("segment reduce + LN backward (+ the multi-piece fix-up)"
+                                  + (" with the table Adam apply fused in" if fused else "")
+                                  + "; the id sort before it (ncf_dedup_ids) is listed in "
+                                  "kernel_ms_per_step")
     return hbm
 
 
@@ -1167,6 +1176,7 @@ def main():
                                                 "ncf_adam_sweep_rolling",
                                                 "ncf_adam_pairs_catchup_clock",
                                                 "ncf_adam_pairs_catchup_claim_clock",
+                                                "ncf_adam_pairs_catchup_lock_clock",
                                                 "ncf_adam_pairs_apply_clock",
                                                 "ncf_adam_pairs_sweep_rolling"))
     sweep_ms = sum(totals.get(k, 0.0) for k in ("ncf_adam_pairs_sweep_rolling",
@@ -1359,7 +1369,11 @@ def main():
             "embedding_hbm": hbm,
             "adam_steady_state": steady,
             "prime_steps": prime,
-            "table_adam": {"kernels": "deferred dense-exact Adam (catch-up + apply + 1/64 sweep)",
+            "table_adam": {"kernels": "deferred dense-exact Adam (catch-up + apply + 1/%s sweep%s)"
+                                      % (sweep_every, "; the apply runs inside the embedding "
+                                         "backward (ncf_embedding_bwd_reduce_apply_clock) and is "
+                                         "not counted here" if "ncf_embedding_bwd_reduce_apply_clock"
+                                         in totals else ""),
                            "ms_per_step": round(tab_ms, 4),
                            "sweep_us_per_step": round(1e3 * sweep_ms, 2),
                            "sweep_overlapped": bool(dfr is not None and getattr(dfr, "overlap", False)),

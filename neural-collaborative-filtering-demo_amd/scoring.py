@@ -193,6 +193,11 @@ def _select(idx, rows, n, run, k, out_s, out_i, overflow, st, terms=None, check=
 # per user on exchangeable scores.  RANK_J = 0: the k-th always.
 RANK_J = 16
 SAMPLE_MIN = 4096   # items in the smallest threshold sample
+# Rank-j sample size factor f: S ~ f n_items / k, so ~RANK_J k / f candidates per user are
+# expected and a user needs the guaranteed re-run with probability P(Gamma(RANK_J) < f)
+# (f = 2: ~4e-10 per user).  Measured at top-100 (10K x 1M, graphed): f = 1 2.62 / 2.68 ms, f = 2
+# 3.29 / 3.33, f = 3 3.28 / 3.41 (r5zl: the larger samples' scans were slower, not faster)
+RANK_SAMPLE_F = 1
 
 
 def _threshold_rank(k: int, cap: int, s16: bool) -> int:
@@ -207,7 +212,7 @@ def _sample_size(n_items: int, k: int, cap: int, j: int = 0) -> int:
     default; j < k: the rank-j plan, S ~ n_items / k, RANK_J * k candidates expected)."""
     j = j or k
     if j < k:
-        s = max(SAMPLE_MIN, -(-j * n_items // (RANK_J * k)))
+        s = max(SAMPLE_MIN, -(-j * n_items * RANK_SAMPLE_F // (RANK_J * k)))
     else:
         s = max(SAMPLE_MIN, -(-k * n_items // max(1, SAMPLE_CANDS)))
     s = max(min(s, KTH_LDS_MAX), -(-2 * j * n_items // cap))
