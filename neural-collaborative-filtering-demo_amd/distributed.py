@@ -52,6 +52,9 @@ TAPE_SHARDED = os.environ.get("NCF_TAPE", "1") != "0"
 # The owner's rank-order gradient sum inside the table Adam's apply (ncf_adam_pairs_apply_gsum_clock,
 # one launch and no compact gradient round trip; False: ncf_shard_owner_gradsum + the apply)
 GSUM_APPLY = True
+# rolling-sweep period of the row-sharded step's deferred table Adam (its catch-up runs on the
+# owner's critical path, so FusedTrainStep's longer period is measured separately)
+SWEEP_EVERY = 64
 # The requester's table gradients written by the embedding backward straight into its send
 # buffer (ncf_embedding_bwd_reduce_rows; False: compact rows, then ncf_shard_rows)
 GRAD_ROWS = True
@@ -578,7 +581,8 @@ class HipShardOps:
     """Per-rank work of the sharded step on the MI355X (HIP kernels through the C-ABI)."""
 
     def __init__(self, model, num_users: int, num_items: int, world: int, lr=1e-3,
-                 betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, sweep_every=64):
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, sweep_every=None):
+        sweep_every = SWEEP_EVERY if sweep_every is None else sweep_every
         from .deferred import DeferredTableAdam
         if world > _lib.SHARD_MAX_WORLD:
             raise ValueError(f"world size {world} > {_lib.SHARD_MAX_WORLD}")
