@@ -52,9 +52,10 @@ TAPE_SHARDED = os.environ.get("NCF_TAPE", "1") != "0"
 # The owner's rank-order gradient sum inside the table Adam's apply (ncf_adam_pairs_apply_gsum_clock,
 # one launch and no compact gradient round trip; False: ncf_shard_owner_gradsum + the apply)
 GSUM_APPLY = True
-# rolling-sweep period of the row-sharded step's deferred table Adam (its catch-up runs on the
-# owner's critical path, so FusedTrainStep's longer period is measured separately)
-SWEEP_EVERY = 64
+# rolling-sweep period of the row-sharded step's deferred table Adam.  Its catch-up runs on the
+# owner's critical path, so FusedTrainStep's longer period was measured here separately: world 1,
+# 2 interleaved runs each, 0.3255 / 0.3268 ms/step at 128 against 0.3301 / 0.3302 at 64 (r5zo)
+SWEEP_EVERY = 128
 # The requester's table gradients written by the embedding backward straight into its send
 # buffer (ncf_embedding_bwd_reduce_rows; False: compact rows, then ncf_shard_rows)
 GRAD_ROWS = True
