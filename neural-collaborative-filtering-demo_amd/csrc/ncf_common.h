@@ -219,10 +219,15 @@ __global__ __launch_bounds__(256) void k_reduce_parts(const float* __restrict__ 
 }
 
 constexpr int NCF_REDUCE_PB = 64;
+// up to this many partials reduce in ONE stage (4 waves x 64 partials per output column); more
+// take two stages (chunks of NCF_REDUCE_PB, then the chunk rows).  256 covers the C2 step's
+// per-workgroup partial sets (256 tower / attention workgroups), so its reductions need no
+// second launch (was 2 x NCF_REDUCE_PB = 128)
+constexpr int NCF_REDUCE_ONE_STAGE = 256;
 
 // scratch floats needed by ncf_reduce_parts for P partials of length L
 static inline int64_t ncf_reduce_scratch(int P, int64_t L) {
-  return P > 2 * NCF_REDUCE_PB ? (int64_t)((P + NCF_REDUCE_PB - 1) / NCF_REDUCE_PB) * L : 0;
+  return P > NCF_REDUCE_ONE_STAGE ? (int64_t)((P + NCF_REDUCE_PB - 1) / NCF_REDUCE_PB) * L : 0;
 }
 
 // Reduce P partial rows; two deterministic stages when P is large (needs `scratch` of
@@ -232,7 +237,7 @@ static inline void ncf_reduce_parts(const float* part, int P, int64_t stride, in
                                     float* scratch = nullptr) {
   if (L <= 0) return;
   const unsigned gx = (unsigned)((L + 63) / 64);
-  if (scratch && P > 2 * NCF_REDUCE_PB) {
+  if (scratch && P > NCF_REDUCE_ONE_STAGE) {
     const int chunks = (P + NCF_REDUCE_PB - 1) / NCF_REDUCE_PB;
     hipLaunchKernelGGL(k_reduce_parts<>, dim3(gx, chunks), dim3(256), 0, st, part, P,
                        NCF_REDUCE_PB, stride, L, scratch, 0, L, L);

@@ -6,8 +6,8 @@
 // embedding LayerNorms).  None of them is on the critical path of the backward (only dX is), so
 // instead of two small launches each, the list is run at the end of the backward:
 //   stage 1: one 256-thread block per (descriptor, 64 outputs, chunk of <= 64 partials); a
-//            descriptor with P <= 128 partials finishes here, otherwise each chunk writes its own
-//            row of `scratch`;
+//            descriptor with P <= NCF_REDUCE_ONE_STAGE (256) partials finishes here, otherwise
+//            each chunk writes its own row of `scratch`;
 //   stage 2: sums the chunk rows of the multi-chunk descriptors in chunk order.
 // The summation order of every output depends only on (P, chunking) — never on scheduling —
 // and is the order of ncf_reduce_parts (ncf_common.h), so a deferred reduction is bit-identical
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void k_reduce_batch2(const BatchArgs a,
   store_out(d, i, (ws[0] + ws[1]) + (ws[2] + ws[3]));
 }
 
-int chunks_of(int P) { return P > 2 * kPB ? (P + kPB - 1) / kPB : 1; }
+int chunks_of(int P) { return P > NCF_REDUCE_ONE_STAGE ? (P + kPB - 1) / kPB : 1; }
 
 }  // namespace
 

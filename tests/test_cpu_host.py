@@ -153,18 +153,19 @@ def test_to_keeps_flat_layout():
 
 def test_reduce_list_layout_and_scratch_query():
     """ncf_reduce_desc / ncf_reduce_list mirror the header layout; the batch scratch query is
-    host arithmetic: one [chunks, L] block per descriptor with P > 128 partials (64 per chunk)."""
+    host arithmetic: one [chunks, L] block per descriptor with P > 256 partials (64 per chunk;
+    up to 256 reduce in one stage)."""
     import ctypes
     assert ctypes.sizeof(_lib.ReduceDesc) == 56
     assert ctypes.sizeof(_lib.ReduceList) == 8 + 56 * _lib.REDUCE_LIST_MAX
     src = open(HEADER).read()
     assert f"#define NCF_REDUCE_LIST_MAX {_lib.REDUCE_LIST_MAX}" in src
     lst = _lib.ReduceList()
-    for P, L in ((100, 33), (160, 4096), (1024, 768)):
+    for P, L in ((100, 33), (256, 4096), (260, 512), (1024, 768)):
         d = lst.d[lst.count]
         d.part, d.out, d.stride, d.ldo, d.L, d.cols, d.P, d.scale = 8, 8, L, L, L, L, P, 1.0
         lst.count += 1
-    assert _lib.query("ncf_reduce_batch_scratch", lst.address) == 3 * 4096 + 16 * 768
+    assert _lib.query("ncf_reduce_batch_scratch", lst.address) == 5 * 512 + 16 * 768
     empty = _lib.ReduceList()
     assert _lib.load().ncf_reduce_batch(empty.address, None, 0, None) == 0  # nothing to launch
 
