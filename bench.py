@@ -59,12 +59,21 @@ SPLIT_PRODUCTS = 6
 SPLIT_NAMES = ("ncf_mlp_fwd_split", "ncf_mlp_bwd_split")
 
 
+PMC_SUMMARIES = ("r05f_c5_pmc_traffic.json", "r05f_pmc_traffic.json")   # (run r05f, final HEAD)
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/*_pmc_traffic.json, made by tools/pmc_traffic.py from separate FETCH_SIZE and
     WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction applied); None when absent."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    # the summaries taken at the round's final HEAD first (then the newest name)
+    for name in PMC_SUMMARIES:
+        pref = os.path.join(ROOT, "profiles", name)
+        if pref in files:
+            files.remove(pref)
+            files.append(pref)
     if not kernel:
         return None
     for fn in reversed(files):   # the newest summary that has the kernel
