@@ -81,11 +81,15 @@ def run_schedule(schedule, data, monkeypatch, lr_at=None):
     return snapshot(m, opt), m, opt
 
 
-def test_hooked_deferred_bitwise_equals_dense_hook(monkeypatch):
+@pytest.mark.parametrize("every,steps", [(64, 70), (128, 140)])
+def test_hooked_deferred_bitwise_equals_dense_hook(monkeypatch, every, steps):
     """torch.optim.Adam.step() through the hook: the deferred schedule (catch-up in the
-    forward, apply + 1/64 sweep in the step) == the dense per-step table sweep, bit for bit,
-    over 70 steps (crossing a full sweep cycle), params and the optimizer's torch-format state."""
-    data = batches(70)
+    forward, apply + 1/every sweep in the step) == the dense per-step table sweep, bit for bit,
+    crossing a full sweep cycle (128: optim.SWEEP_EVERY's default), params and the optimizer's
+    torch-format state."""
+    from ncf_amd import optim as O
+    monkeypatch.setattr(O, "SWEEP_EVERY", every)
+    data = batches(steps)
     a, _, _ = run_schedule("dense", data, monkeypatch)
     b, m, opt = run_schedule("deferred", data, monkeypatch)
     assert_same(a, b)
