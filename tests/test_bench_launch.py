@@ -58,3 +58,22 @@ def test_priming_rule():
     assert bench.prime_steps(A) == 2 * bench.SWEEP_EVERY
     A.prime = 3
     assert bench.prime_steps(A) == 3
+
+
+def test_embedding_rooflines_byte_models():
+    """bench.embedding_rooflines prices the scatter by the entry point that ran: the plain
+    reduce N (16 D + 16) + U 16 D, the reduce with the table Adam fused in
+    N (16 D + 16) + U (56 D + 4) (its parameter rows out, moment rows in and out, the stamp);
+    and the PMC summary quoted first is the round's final one."""
+    import bench
+    N, D, U = 20480, 64, (4000, 20000)
+    per = {"ncf_gather_ln_gmf_scaled_fwd": [None] * 10}
+    for kern, per_row in (("ncf_embedding_bwd_reduce", 16 * D),
+                          ("ncf_embedding_bwd_reduce_apply_clock", 56 * D + 4)):
+        totals = {"ncf_gather_ln_gmf_scaled_fwd": 0.01, kern: 0.03}
+        p = dict(per, **{kern: [None] * 10})
+        hbm = bench.embedding_rooflines(totals, p, 10, N, D, 5, U, pmc=False)
+        assert hbm["scatter"]["entry_point"] == kern
+        assert hbm["scatter"]["bytes_per_launch"] == N * (16 * D + 16) + sum(U) * per_row
+    src = bench.pmc_traffic("k_attn_mlp_bwd")
+    assert src is None or src["source"].startswith(bench.PMC_SUMMARIES[-1])
