@@ -10,6 +10,10 @@ OBJ="${NCF_OBJ:-$SRC/build}"
 mkdir -p "$OBJ"
 rm -f "$OBJ"/*.o
 FLAGS=(--offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$SRC" -I"$ROOT/include" -Wall -Wno-unused-function ${NCF_EXTRA_FLAGS:-})
+# build identity compiled into capi.hip (ncf_build_info; checked by _lib.load())
+ABI_HASH="$(python3 "$ROOT/neural-collaborative-filtering-demo_amd/_abi.py" abi)"
+SRC_HASH="$(python3 "$ROOT/neural-collaborative-filtering-demo_amd/_abi.py" src "$SRC")"
+NCF_FLAGS_capi="${NCF_FLAGS_capi:-} -DNCF_ABI_HASH=\"$ABI_HASH\" -DNCF_SRC_HASH=\"$SRC_HASH\""
 pids=()
 for f in "$SRC"/*.hip; do
   b="$(basename "$f" .hip)"

@@ -43,6 +43,11 @@ int ncf_step_clock_advance(ncf_step_clock* clock, uint64_t base_seed, void* stre
 int ncf_version(void);
 const char* ncf_last_error(void);
 int ncf_device_count(void);
+/* Build identity: "abi=<16 hex> src=<16 hex>", the hash of the ctypes table the library was built
+ * against (_lib.SIGNATURES) and of the kernel sources it was compiled from (_abi.py).  The
+ * loader refuses a library whose hashes differ from the Python side and sources beside it.
+ * (Packaging plumbing: the reference is pure Python and has no compiled library to match.)   */
+const char* ncf_build_info(void);
 
 /* Cross-stream ordering (hipEventRecord / hipStreamWaitEvent, events created without timing).
  * Replaces: the torch.cuda.Event record / wait_event pairs of the step's fork / join points
@@ -217,6 +222,14 @@ int ncf_attention_fwd(const float* q, const float* k, const float* v, int64_t gr
                       int64_t group_len, int64_t heads, int64_t dim, float dropout_p,
                       uint64_t seed, const ncf_step_clock* clock, float* probs, float* out,
                       void* stream);
+/* The same with MultiHeadAttention.forward's mask (architecture.py:36, 47-48: scores.masked_fill(
+ * mask == 0, -inf)): mask [groups, heads, L, L] bytes (0 = masked; a broadcast mask expanded by
+ * the caller).  Masked probabilities are exactly 0, so ncf_attention_bwd applies unchanged; a
+ * fully masked row is NaN, as the reference's softmax over all -inf makes it.               */
+int ncf_attention_fwd_masked(const float* q, const float* k, const float* v, int64_t groups,
+                             int64_t group_len, int64_t heads, int64_t dim, float dropout_p,
+                             uint64_t seed, const ncf_step_clock* clock, const uint8_t* mask,
+                             float* probs, float* out, void* stream);
 int ncf_attention_bwd(const float* q, const float* k, const float* v, const float* probs,
                       const float* grad_out, int64_t groups, int64_t group_len, int64_t heads,
                       int64_t dim, float dropout_p, uint64_t seed, const ncf_step_clock* clock,

@@ -15,7 +15,8 @@ import threading
 import torch  # noqa: F401  (must precede the CDLL: binds libncf_hip to torch's HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("NCF_HIP_LIB") or os.path.join(_HERE, "libncf_hip.so")   # env: A/B builds
+_DEFAULT_LIB = os.path.join(_HERE, "libncf_hip.so")
+LIB_PATH = os.environ.get("NCF_HIP_LIB") or _DEFAULT_LIB   # env: A/B builds
 
 
 class NCFLibraryError(RuntimeError):
@@ -41,6 +42,7 @@ SIGNATURES = {
     "ncf_event_synchronize": (I32, [P]),
     "ncf_memcpy_async": (I32, [P, P, I64, P]),
     "ncf_device_count": (I32, []),
+    "ncf_build_info": (ctypes.c_char_p, []),
     "ncf_gather_ln_gmf_ld_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, I64, P, P, P, P, P, P,
                                        F32, I64, P, P, P, P, P, P, P]),
     "ncf_gather_ln_gmf_fwd": (I32, [P, P, I64, P, P, P, P, I64, I64, I64, P, P, P, P, P, P, F32,
@@ -63,6 +65,7 @@ SIGNATURES = {
     "ncf_colsum_workspace": (I64, [I64, I64]),
     "ncf_colsum": (I32, [P, I64, I64, I64, P, I32, P, I64, P]),
     "ncf_attention_fwd": (I32, [P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P]),
+    "ncf_attention_fwd_masked": (I32, [P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P, P]),
     "ncf_attention_bwd": (I32, [P, P, P, P, P, I64, I64, I64, I64, F32, U64, P, P, P, P, P, P]),
     "ncf_attn_block_supported": (I32, [I64, I64, I64]),
     "ncf_mlp_fused_supported": (I32, [I64, I64, P]),
@@ -274,6 +277,7 @@ def load(path: str = LIB_PATH):
         except OSError as e:
             _load_error = f"cannot load {path}: {e}"
             raise NCFLibraryError(_load_error) from e
+        check_build(lib, path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = res
@@ -283,13 +287,44 @@ def load(path: str = LIB_PATH):
         return lib
 
 
+def build_info(lib) -> dict:
+    """{"abi": .., "src": ..} compiled into the library (ncf_build_info)."""
+    try:
+        fn = lib.ncf_build_info
+    except AttributeError:
+        return {}
+    fn.restype, fn.argtypes = ctypes.c_char_p, []
+    return dict(kv.split("=", 1) for kv in fn().decode().split())
+
+
+def check_build(lib, path: str = LIB_PATH):
+    """Refuse a library built against another C-ABI table than SIGNATURES, or from other kernel
+    sources than the ones beside this package (a stale build: _abi.py).  The sources are not
+    checked when they are absent, nor for a library named by NCF_HIP_LIB (an A/B build from
+    another source tree)."""
+    from . import _abi
+    info = build_info(lib)
+    want_abi = _abi.abi_hash(SIGNATURES)
+    if info.get("abi") != want_abi:
+        raise NCFLibraryError(f"{path} was built against another C-ABI table (abi "
+                              f"{info.get('abi')} != {want_abi}): rebuild (./build_ext.sh)")
+    want_src = _abi.src_hash() if os.path.abspath(path) == _DEFAULT_LIB else ""
+    if want_src and info.get("src") != want_src:
+        raise NCFLibraryError(f"{path} is stale: built from other kernel sources (src "
+                              f"{info.get('src')} != {want_src}): rebuild (./build_ext.sh)")
+
+
 # name -> CPython wrapper of the entry point (_ncffast, built beside the library by
 # build_ext.sh from SIGNATURES): the same call without ctypes' per-argument conversion
 FAST = {}
 
 
+# The CPython fast-call binding (_ncffast) when it is built (False: ctypes alone, A/B of host time)
+FASTCALL = True
+
+
 def _bind_fast(lib):
-    if os.environ.get("NCF_FASTCALL", "1") == "0":
+    if not FASTCALL:
         return
     try:
         from . import _ncffast

@@ -10,6 +10,11 @@
 //
 // Layout: Q, K, V, O are [N, D] row-major with N = B*L; head h owns columns [h*hd, (h+1)*hd).
 // P (saved for backward) is the pre-dropout softmax [B, H, L, L].
+//
+// Mask (ncf_attention_fwd_masked; :47-48 scores.masked_fill(mask == 0, -inf)): a [B, H, L, L]
+// byte per score, 0 = masked.  A masked score is -inf before the softmax, so its probability is
+// exactly 0 and the backward needs no mask (dS = P (dP - sum P dP) is 0 there); a row with every
+// score masked is NaN, as torch's softmax over all -inf makes it.
 #include "ncf_common.h"
 
 namespace {
@@ -20,7 +25,8 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const float* __restrict__ Q,
                                                   const float* __restrict__ V, int64_t B, int L,
                                                   int H, float scale, float p_drop,
                                                   uint64_t seed, const ncf_step_clock* clock, float* __restrict__ P,
-                                                  float* __restrict__ O) {
+                                                  float* __restrict__ O,
+                                                  const uint8_t* __restrict__ mask) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= B * H * L) return;
   if (clock) seed += clock->seed;  // per-step stream of a captured step
@@ -42,6 +48,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const float* __restrict__ Q,
 #pragma unroll
       for (int d = 0; d < HD; ++d) acc = fmaf(qr[d], k[d], acc);
       s[j] = acc / scale;
+      if (mask && mask[t * L + j] == 0) s[j] = -INFINITY;
       mx = fmaxf(mx, s[j]);
     }
   }
@@ -49,7 +56,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const float* __restrict__ Q,
 #pragma unroll
   for (int j = 0; j < LMAX; ++j)
     if (j < L) {
-      s[j] = expf(s[j] - mx);
+      s[j] = mx == -INFINITY ? NAN : expf(s[j] - mx);
       sum += s[j];
     }
   float o[HD];
@@ -172,10 +179,11 @@ __global__ __launch_bounds__(256) void k_attn_bwd_kv(const float* __restrict__ Q
 
 template <int HD, int LMAX>
 int fwd_l(const float* Q, const float* K, const float* V, int64_t B, int L, int H, float p,
-          uint64_t seed, const ncf_step_clock* clock, float* P, float* O, hipStream_t st) {
+          uint64_t seed, const ncf_step_clock* clock, float* P, float* O, hipStream_t st,
+          const uint8_t* mask) {
   const int64_t n = B * H * L;
   hipLaunchKernelGGL((k_attn_fwd<HD, LMAX>), dim3(ncf_cdiv(n, 256)), dim3(256), 0, st, Q, K, V, B,
-                     L, H, sqrtf((float)HD), p, seed, clock, P, O);
+                     L, H, sqrtf((float)HD), p, seed, clock, P, O, mask);
   NCF_CHECK_LAUNCH("ncf_attention_fwd");
   return NCF_OK;
 }
@@ -197,9 +205,10 @@ int bwd_l(const float* Q, const float* K, const float* V, const float* P, const 
 
 template <int HD>
 int fwd_hd(const float* Q, const float* K, const float* V, int64_t B, int L, int H, float p,
-           uint64_t seed, const ncf_step_clock* clock, float* P, float* O, hipStream_t st) {
-  if (L <= 8) return fwd_l<HD, 8>(Q, K, V, B, L, H, p, seed, clock, P, O, st);
-  return fwd_l<HD, 64>(Q, K, V, B, L, H, p, seed, clock, P, O, st);
+           uint64_t seed, const ncf_step_clock* clock, float* P, float* O, hipStream_t st,
+           const uint8_t* mask) {
+  if (L <= 8) return fwd_l<HD, 8>(Q, K, V, B, L, H, p, seed, clock, P, O, st, mask);
+  return fwd_l<HD, 64>(Q, K, V, B, L, H, p, seed, clock, P, O, st, mask);
 }
 
 template <int HD>
@@ -212,9 +221,10 @@ int bwd_hd(const float* Q, const float* K, const float* V, const float* P, const
 
 }  // namespace
 
-extern "C" int ncf_attention_fwd(const float* q, const float* k, const float* v, int64_t groups,
-                                 int64_t group_len, int64_t heads, int64_t dim, float dropout_p,
-                                 uint64_t seed, const ncf_step_clock* clock, float* probs, float* out, void* stream) {
+static int attention_fwd(const float* q, const float* k, const float* v, int64_t groups,
+                         int64_t group_len, int64_t heads, int64_t dim, float dropout_p,
+                         uint64_t seed, const ncf_step_clock* clock, float* probs, float* out,
+                         const uint8_t* mask, void* stream) {
   NCF_CHECK_ARG(groups >= 0 && group_len >= 1 && group_len <= 64 && heads >= 1 && dim % heads == 0,
                 "ncf_attention_fwd: bad shape (groups=%lld L=%lld H=%lld D=%lld; L<=64)",
                 (long long)groups, (long long)group_len, (long long)heads, (long long)dim);
@@ -223,13 +233,30 @@ extern "C" int ncf_attention_fwd(const float* q, const float* k, const float* v,
   hipStream_t st = (hipStream_t)stream;
   const int L = (int)group_len, H = (int)heads;
   switch (dim / heads) {
-    case 8: return fwd_hd<8>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st);
-    case 16: return fwd_hd<16>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st);
-    case 32: return fwd_hd<32>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st);
-    case 64: return fwd_hd<64>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st);
+    case 8: return fwd_hd<8>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st, mask);
+    case 16: return fwd_hd<16>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st, mask);
+    case 32: return fwd_hd<32>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st, mask);
+    case 64: return fwd_hd<64>(q, k, v, groups, L, H, dropout_p, seed, clock, probs, out, st, mask);
   }
   ncf_set_error("ncf_attention_fwd: head dim %lld unsupported (8/16/32/64)", (long long)(dim / heads));
   return NCF_ERR_ARG;
+}
+
+extern "C" int ncf_attention_fwd(const float* q, const float* k, const float* v, int64_t groups,
+                                 int64_t group_len, int64_t heads, int64_t dim, float dropout_p,
+                                 uint64_t seed, const ncf_step_clock* clock, float* probs, float* out, void* stream) {
+  return attention_fwd(q, k, v, groups, group_len, heads, dim, dropout_p, seed, clock, probs, out,
+                       nullptr, stream);
+}
+
+extern "C" int ncf_attention_fwd_masked(const float* q, const float* k, const float* v,
+                                        int64_t groups, int64_t group_len, int64_t heads,
+                                        int64_t dim, float dropout_p, uint64_t seed,
+                                        const ncf_step_clock* clock, const uint8_t* mask,
+                                        float* probs, float* out, void* stream) {
+  NCF_CHECK_ARG(mask != nullptr, "ncf_attention_fwd_masked: NULL mask");
+  return attention_fwd(q, k, v, groups, group_len, heads, dim, dropout_p, seed, clock, probs, out,
+                       mask, stream);
 }
 
 extern "C" int ncf_attention_bwd(const float* q, const float* k, const float* v, const float* probs,

@@ -15,6 +15,15 @@ extern "C" const char* ncf_last_error(void) { return g_err; }
 
 extern "C" int ncf_version(void) { return 10000; }  // 1.0.0
 
+// Build identity (build_ext.sh passes both hashes for this file: _abi.py)
+#ifndef NCF_ABI_HASH
+#define NCF_ABI_HASH "unset"
+#endif
+#ifndef NCF_SRC_HASH
+#define NCF_SRC_HASH "unset"
+#endif
+extern "C" const char* ncf_build_info(void) { return "abi=" NCF_ABI_HASH " src=" NCF_SRC_HASH; }
+
 // Sanity probe used by the loader: returns the HIP device count seen by the runtime the
 // library is bound to (torch's libamdhip64 when torch is imported first).
 extern "C" int ncf_device_count(void) {

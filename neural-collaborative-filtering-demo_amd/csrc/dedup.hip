@@ -249,8 +249,7 @@ __global__ __launch_bounds__(256) void k_segments(
     uint32_t* __restrict__ pstart0, uint32_t* __restrict__ pstart1, uint32_t* __restrict__ pseg0,
     uint32_t* __restrict__ pseg1, uint32_t* __restrict__ fpiece0, uint32_t* __restrict__ fpiece1,
     int64_t* __restrict__ uniq0, int64_t* __restrict__ uniq1, int32_t* __restrict__ slot0,
-    int32_t* __restrict__ slot1, uint32_t* __restrict__ totals, uint32_t* __restrict__ num_unique,
-    uint32_t* __restrict__ cpos0, uint32_t* __restrict__ cpos1) {
+    int32_t* __restrict__ slot1, uint32_t* __restrict__ totals, uint32_t* __restrict__ num_unique) {
   constexpr uint64_t F_AGG = 1ull << 62, F_INCL = 2ull << 62, M31 = (1ull << 31) - 1;
   __shared__ uint32_t ws_s[16], ws_p[16];
   __shared__ uint32_t s_tile, s_es, s_ep;
@@ -347,7 +346,6 @@ __global__ __launch_bounds__(256) void k_segments(
   uint32_t* fpiece = kind ? fpiece1 : fpiece0;
   int64_t* uniq = kind ? uniq1 : uniq0;
   int32_t* slot = kind ? slot1 : slot0;
-  uint32_t* cpos = kind ? cpos1 : cpos0;
   uint32_t bs = s_es, bp = s_ep;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -356,7 +354,6 @@ __global__ __launch_bounds__(256) void k_segments(
     const int64_t i = (int64_t)tile * TILE + r * 256 + tid;
     if (i >= n) continue;
     const uint32_t c = bs + pre_s + sr[r] - 1;  // segment of position i
-    cpos[i] = c;
     if (sh[r]) {
       start[c] = (uint32_t)i;
       uniq[c] = (int64_t)key[r];
@@ -458,7 +455,7 @@ extern "C" int ncf_dedup_ids2(const int64_t* ids0, int64_t n0, int64_t rows0, co
   hipLaunchKernelGGL(k_segments, dim3(w.nb, 2), dim3(256), 0, st, ki0, ki1, n0, n1, w.nb,
                      w.sstatus, w.tickets + 2 * MAXP, w.segoff, w.start0, w.start1, w.pstart0,
                      w.pstart1, w.pseg0, w.pseg1, w.fpiece0, w.fpiece1, uniq0, uniq1,
-                     slot0, slot1, w.totals, num_unique, w.cpos0, w.cpos1);
+                     slot0, slot1, w.totals, num_unique);
   NCF_CHECK_LAUNCH("ncf_dedup_ids(segments)");
   return NCF_OK;
 }

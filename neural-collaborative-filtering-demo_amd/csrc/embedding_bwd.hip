@@ -254,214 +254,6 @@ __global__ __launch_bounds__(256) void k_piece_fixup(
   }
 }
 
-// Position-ordered form of the same reduce (NCF_EMB_POS=1; measured slower, see use_pos_reduce):
-// the pieces are the same (segments cut
-// at every sorted position multiple of PIECE = 16), but a wave owns the 16 sorted positions of
-// one piece SLOT instead of a lane group owning one piece.  Every wave has the same work, and
-// its loads are not chained through piece records: lanes 0-15 read the 16 sorted (key, position,
-// segment) triples at once (round 1), then each group of L = D/4 lanes loads the gradient rows
-// of its PG = L/4 positions, all in flight together, and the table-row ids of the pieces starting
-// there (round 2); the table rows of those pieces (round 3) load while the gradient rows go
-// through LDS.  The group owning a piece's first position sums the piece in position order (the
-// order of k_piece_reduce_ln: bit-identical rows) and applies the two LayerNorm backwards.  A
-// piece that continues a segment from the previous slot (only a slot's first piece can) goes to
-// the extras row of its slot, xp[slot]; k_pos_fixup adds those in slot order.
-template <int D, int NW, bool BF = false>
-__global__ __launch_bounds__(64 * NW) void k_pos_reduce_ln(
-    const uint32_t* __restrict__ sk0, const uint32_t* __restrict__ sk1,
-    const uint32_t* __restrict__ sv0, const uint32_t* __restrict__ sv1,
-    const uint32_t* __restrict__ cpos0, const uint32_t* __restrict__ cpos1, int64_t n,
-    const int64_t* __restrict__ uniq0, const int64_t* __restrict__ uniq1,
-    const float* __restrict__ dy_mf0, const float* __restrict__ dy_mlp0,
-    const float* __restrict__ dy_mf1, const float* __restrict__ dy_mlp1,
-    const float* __restrict__ t_mf0, const float* __restrict__ t_mlp0,
-    const float* __restrict__ t_mf1, const float* __restrict__ t_mlp1,
-    const float* __restrict__ g_mf, const float* __restrict__ g_mlp, float eps,
-    float* __restrict__ G_mf0, float* __restrict__ G_mlp0, float* __restrict__ G_mf1,
-    float* __restrict__ G_mlp1, float* __restrict__ xp0, float* __restrict__ xp1,
-    float* __restrict__ part) {
-  constexpr int L = D / 4;          // lanes per row
-  constexpr int G = 64 / L;         // lane groups per wave
-  constexpr int PG = PIECE / G;     // positions per group
-  static_assert(PIECE == 16 && PG >= 1 && PG * G == PIECE, "one piece slot per wave");
-  // dynamic LDS: rs[NW][PIECE][2][L] float4 (dy_mf | dy_mlp rows), then red[NW][4D] floats
-  extern __shared__ float4 lds4[];
-  float4 (*rs)[PIECE][2][L] = reinterpret_cast<float4 (*)[PIECE][2][L]>(lds4);
-  float (*red)[4 * D] = reinterpret_cast<float (*)[4 * D]>(lds4 + NW * PIECE * 2 * L);
-  const int kind = blockIdx.y;
-  const uint32_t* sk = kind ? sk1 : sk0;
-  const uint32_t* sv = kind ? sv1 : sv0;
-  const uint32_t* cpos = kind ? cpos1 : cpos0;
-  const int64_t* uniq = kind ? uniq1 : uniq0;
-  const float* dmf = kind ? dy_mf1 : dy_mf0;
-  const float* dml = kind ? dy_mlp1 : dy_mlp0;
-  const float* tmf = kind ? t_mf1 : t_mf0;
-  const float* tml = kind ? t_mlp1 : t_mlp0;
-  float* Gmf = kind ? G_mf1 : G_mf0;
-  float* Gml = kind ? G_mlp1 : G_mlp0;
-  float* xp = kind ? xp1 : xp0;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int g = lane / L, sub = lane % L, col = sub * 4;
-  const int64_t slot = (int64_t)blockIdx.x * NW + w;
-  const int64_t base = slot * PIECE;
-  const int nv = (int)max<int64_t>(0, min<int64_t>(PIECE, n - base));   // valid positions
-  float4 a_gm = make_float4(0, 0, 0, 0), a_bm = a_gm, a_gl = a_gm, a_bl = a_gm;
-  // round 1: lanes 0-15 hold the slot's sorted positions (lanes 16+ repeat them)
-  const int q16 = lane & (PIECE - 1);
-  uint32_t key = 0xFFFFFFFFu, r = 0, cs = 0;
-  if (q16 < nv) {
-    key = sk[base + q16];
-    r = sv[base + q16];
-    cs = cpos[base + q16];
-  }
-  uint32_t prev = __shfl(key, (lane & ~(PIECE - 1)) + ((q16 + PIECE - 1) & (PIECE - 1)), 64);
-  if (q16 == 0) prev = (base > 0 && nv > 0) ? sk[base - 1] : 0xFFFFFFFFu;
-  const bool seg_head = q16 < nv && (base + q16 == 0 || key != prev);
-  const uint32_t hm = (uint32_t)__ballot(seg_head) & 0xFFFFu;               // segment heads
-  const uint32_t pm = (uint32_t)__ballot(q16 < nv && (q16 == 0 || seg_head)) & 0xFFFFu;  // piece starts
-  // round 2: this group's gradient rows (all in flight) and the table-row ids of its pieces
-  // (every lane active here: the shuffles read lanes 0-15, which later branches may disable)
-  float4 dm[PG], dl[PG];
-  int64_t tid[PG];
-  uint32_t cj[PG];
-#pragma unroll
-  for (int j = 0; j < PG; ++j) {
-    const int q = g * PG + j;
-    const int64_t rr = (int64_t)__shfl(r, q, 64);
-    const uint32_t c = (uint32_t)__shfl(cs, q, 64);
-    cj[j] = c;
-    dm[j] = make_float4(0, 0, 0, 0);
-    dl[j] = dm[j];
-    tid[j] = 0;
-    if (q < nv) {
-      dm[j] = ld4(dmf + rr * D + col);
-      dl[j] = ld4(dml + rr * D + col);
-    }
-    if ((pm >> q) & 1u) tid[j] = uniq[c];
-  }
-  // round 3: the table rows of the pieces starting here (the LN inputs)
-  float4 xm[PG], xl[PG];
-#pragma unroll
-  for (int j = 0; j < PG; ++j) {
-    const int q = g * PG + j;
-    xm[j] = make_float4(0, 0, 0, 0);
-    xl[j] = xm[j];
-    if ((pm >> q) & 1u) {
-      xm[j] = ldp4<BF>(tmf, tid[j] * D + col);
-      xl[j] = ldp4<BF>(tml, tid[j] * D + col);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < PG; ++j) {
-    const int q = g * PG + j;
-    rs[w][q][0][sub] = dm[j];
-    rs[w][q][1][sub] = dl[j];
-  }
-  __syncthreads();
-  const float4 gm = ld4(g_mf + col), gl = ld4(g_mlp + col);
-#pragma unroll
-  for (int j = 0; j < PG; ++j) {
-    const int q = g * PG + j;
-    if (!((pm >> q) & 1u)) continue;   // (uniform in the group)
-    const uint32_t after = pm >> (q + 1);
-    const int end = min(nv, after ? q + 1 + __builtin_ctz(after) : PIECE);
-    float4 sm = make_float4(0, 0, 0, 0), sl = sm;
-    for (int p = q; p < end; ++p) {   // position order, as k_piece_reduce_ln
-      const float4 a = rs[w][p][0][sub], b = rs[w][p][1][sub];
-      sm.x += a.x; sm.y += a.y; sm.z += a.z; sm.w += a.w;
-      sl.x += b.x; sl.y += b.y; sl.z += b.z; sl.w += b.w;
-    }
-    const bool first = (hm >> q) & 1u;
-    const int64_t c = (int64_t)cj[j];
-#pragma unroll
-    for (int tbl = 0; tbl < 2; ++tbl) {
-      const float4 x = tbl ? xl[j] : xm[j];
-      const float4 dy = tbl ? sl : sm;
-      const float4 gg = tbl ? gl : gm;
-      const float mean = group_sum<L>(x.x + x.y + x.z + x.w) * (1.0f / D);
-      const float4 xc = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
-      const float var = group_sum<L>(xc.x * xc.x + xc.y * xc.y + xc.z * xc.z + xc.w * xc.w) * (1.0f / D);
-      const float rstd = 1.0f / sqrtf(var + eps);
-      const float4 h = make_float4(xc.x * rstd, xc.y * rstd, xc.z * rstd, xc.w * rstd);
-      const float4 gd = make_float4(dy.x * gg.x, dy.y * gg.y, dy.z * gg.z, dy.w * gg.w);
-      const float m1 = group_sum<L>(gd.x + gd.y + gd.z + gd.w) * (1.0f / D);
-      const float m2 = group_sum<L>(gd.x * h.x + gd.y * h.y + gd.z * h.z + gd.w * h.w) * (1.0f / D);
-      const float4 dx = make_float4(rstd * (gd.x - m1 - h.x * m2), rstd * (gd.y - m1 - h.y * m2),
-                                    rstd * (gd.z - m1 - h.z * m2), rstd * (gd.w - m1 - h.w * m2));
-      float* dst = first ? (tbl ? Gml : Gmf) + c * D : xp + slot * 2 * D + tbl * D;
-      st4(dst + col, dx);
-      float4& ag = tbl ? a_gl : a_gm;
-      float4& ab = tbl ? a_bl : a_bm;
-      ag.x += dy.x * h.x; ag.y += dy.y * h.y; ag.z += dy.z * h.z; ag.w += dy.w * h.w;
-      ab.x += dy.x; ab.y += dy.y; ab.z += dy.z; ab.w += dy.w;
-    }
-  }
-  // the wave's groups (lanes L apart hold the same columns), then the block's waves
-#pragma unroll
-  for (int o = L; o < 64; o <<= 1) {
-    a_gm.x += __shfl_xor(a_gm.x, o, 64); a_gm.y += __shfl_xor(a_gm.y, o, 64);
-    a_gm.z += __shfl_xor(a_gm.z, o, 64); a_gm.w += __shfl_xor(a_gm.w, o, 64);
-    a_bm.x += __shfl_xor(a_bm.x, o, 64); a_bm.y += __shfl_xor(a_bm.y, o, 64);
-    a_bm.z += __shfl_xor(a_bm.z, o, 64); a_bm.w += __shfl_xor(a_bm.w, o, 64);
-    a_gl.x += __shfl_xor(a_gl.x, o, 64); a_gl.y += __shfl_xor(a_gl.y, o, 64);
-    a_gl.z += __shfl_xor(a_gl.z, o, 64); a_gl.w += __shfl_xor(a_gl.w, o, 64);
-    a_bl.x += __shfl_xor(a_bl.x, o, 64); a_bl.y += __shfl_xor(a_bl.y, o, 64);
-    a_bl.z += __shfl_xor(a_bl.z, o, 64); a_bl.w += __shfl_xor(a_bl.w, o, 64);
-  }
-  if (g == 0) {
-    float* rr = red[w];
-    st4(rr + col, a_gm);
-    st4(rr + D + col, a_bm);
-    st4(rr + 2 * D + col, a_gl);
-    st4(rr + 3 * D + col, a_bl);
-  }
-  __syncthreads();
-  float* out = part + ((int64_t)kind * gridDim.x + blockIdx.x) * 4 * D;
-  for (int i = threadIdx.x; i < 4 * D; i += 64 * NW) {
-    float a = 0.0f;
-#pragma unroll
-    for (int q = 0; q < NW; ++q) a += red[q][i];
-    out[i] = a;
-  }
-}
-
-// G[c] += the extras rows of segment c's later slots, in slot order.  One lane group per slot
-// boundary: the boundary at slot b continues a segment when sk[16b] == sk[16b - 1]; the group of
-// the FIRST continuation of a segment (its head in slot b - 1) sums them all.
-template <int D>
-__global__ __launch_bounds__(256) void k_pos_fixup(
-    const uint32_t* __restrict__ sk0, const uint32_t* __restrict__ sk1,
-    const uint32_t* __restrict__ cpos0, const uint32_t* __restrict__ cpos1,
-    const uint32_t* __restrict__ start0, const uint32_t* __restrict__ start1, int64_t n,
-    const float* __restrict__ xp0, const float* __restrict__ xp1, float* __restrict__ G_mf0,
-    float* __restrict__ G_mlp0, float* __restrict__ G_mf1, float* __restrict__ G_mlp1) {
-  constexpr int L = D / 4;
-  const int kind = blockIdx.y;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t b = t / L + 1;           // slot boundary b: between positions 16b - 1 and 16b
-  const int col = (int)(t % L) * 4;
-  const int64_t i = b * PIECE;
-  if (i >= n) return;
-  const uint32_t* sk = kind ? sk1 : sk0;
-  if (sk[i] != sk[i - 1]) return;        // a new segment starts at the boundary
-  const uint32_t c = (kind ? cpos1 : cpos0)[i];
-  const uint32_t* start = kind ? start1 : start0;
-  const int64_t s0 = start[c];
-  if (s0 < (b - 1) * PIECE) return;      // an earlier boundary of this segment owns it
-  const int64_t last = ((int64_t)start[c + 1] - 1) / PIECE;
-  const float* xp = kind ? xp1 : xp0;
-  float* Gmf = kind ? G_mf1 : G_mf0;
-  float* Gml = kind ? G_mlp1 : G_mlp0;
-  float4 a = ld4(Gmf + (int64_t)c * D + col), e = ld4(Gml + (int64_t)c * D + col);
-  for (int64_t s = b; s <= last; ++s) {
-    const float4 x = ld4(xp + s * 2 * D + col), y = ld4(xp + s * 2 * D + D + col);
-    a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
-    e.x += y.x; e.y += y.y; e.z += y.z; e.w += y.w;
-  }
-  st4(Gmf + (int64_t)c * D + col, a);
-  st4(Gml + (int64_t)c * D + col, e);
-}
-
 __global__ void k_ln_param_scatter(const float* __restrict__ red, int D, float* gm, float* bm,
                                    float* gl, float* bl) {
   for (int i = threadIdx.x; i < 4 * D; i += blockDim.x) {
@@ -476,76 +268,6 @@ __global__ void k_slot_reset(const int64_t* __restrict__ uniq, const uint32_t* _
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= max_n || c >= (int64_t)totals[kind]) return;
   slot[uniq[c]] = -1;
-}
-
-// position-ordered reduce: waves per block (LDS: NW x 16 x 2 rows + NW x 4D floats)
-template <int D>
-constexpr int pos_waves() { return D >= 128 ? 4 : 8; }
-// NCF_EMB_POS=1: the position-ordered kernels.  Measured at C2 (one MI355X, bench.py): 30.7 us
-// per embedding backward against 25.6 us for the piece-record kernels (default), step 0.3179 vs
-// 0.3151 ms — kept as an option (A/B, parity tests)
-static bool use_pos_reduce() {
-  const char* e = getenv("NCF_EMB_POS");
-  return e && e[0] == '1';
-}
-
-template <int D>
-int pos_reduce(const WS& w, int64_t n, const uint32_t* sk0, const uint32_t* sk1,
-               const uint32_t* sv0, const uint32_t* sv1, const int64_t* uniq0,
-               const int64_t* uniq1, const float* dmf0, const float* dml0, const float* dmf1,
-               const float* dml1, const float* tmf0, const float* tml0, const float* tmf1,
-               const float* tml1, const float* gmf, const float* gml, float eps, float* Gmf0,
-               float* Gml0, float* Gmf1, float* Gml1, float* dgm, float* dbm, float* dgl,
-               float* dbl, ncf_reduce_list* defer, hipStream_t st, bool bf) {
-  constexpr int NW = pos_waves<D>();
-  constexpr size_t lds = sizeof(float4) * NW * PIECE * 2 * (D / 4) + sizeof(float) * NW * 4 * D;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e0 = hipFuncSetAttribute((const void*)k_pos_reduce_ln<D, NW, true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipError_t e1 = hipFuncSetAttribute((const void*)k_pos_reduce_ln<D, NW, false>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e0 != hipSuccess || e1 != hipSuccess) {
-      ncf_set_error("ncf_embedding_bwd: %zu B of LDS refused", lds);
-      return NCF_ERR_LAUNCH;
-    }
-    attr = true;
-  }
-  const int64_t slots = ncf_cdiv(n, PIECE);
-  const int nblk = (int)ncf_cdiv(slots, NW);
-  if (2 * nblk > 2 * w.nbr) {   // (the partial rows are sized for the piece layout's grid)
-    ncf_set_error("ncf_embedding_bwd: partial buffer too small");
-    return NCF_ERR_WORKSPACE;
-  }
-  if (bf)
-    hipLaunchKernelGGL((k_pos_reduce_ln<D, NW, true>), dim3(nblk, 2), dim3(64 * NW), lds, st, sk0, sk1,
-                       sv0, sv1, w.cpos0, w.cpos1, n, uniq0, uniq1, dmf0, dml0, dmf1, dml1, tmf0,
-                       tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0, Gmf1, Gml1, w.xp0, w.xp1, w.part);
-  else
-    hipLaunchKernelGGL((k_pos_reduce_ln<D, NW, false>), dim3(nblk, 2), dim3(64 * NW), lds, st, sk0, sk1,
-                       sv0, sv1, w.cpos0, w.cpos1, n, uniq0, uniq1, dmf0, dml0, dmf1, dml1, tmf0,
-                       tml0, tmf1, tml1, gmf, gml, eps, Gmf0, Gml0, Gmf1, Gml1, w.xp0, w.xp1, w.part);
-  NCF_CHECK_LAUNCH("ncf_embedding_bwd(pos_reduce)");
-  constexpr int L = D / 4;
-  if (slots > 1) {
-    const int64_t fb = ncf_cdiv((slots - 1) * L, 256);
-    hipLaunchKernelGGL(k_pos_fixup<D>, dim3((unsigned)fb, 2), dim3(256), 0, st, sk0, sk1, w.cpos0,
-                       w.cpos1, w.start0, w.start1, n, w.xp0, w.xp1, Gmf0, Gml0, Gmf1, Gml1);
-    NCF_CHECK_LAUNCH("ncf_embedding_bwd(pos_fixup)");
-  }
-  if (defer) {
-    float* const outs[4] = {dgm, dbm, dgl, dbl};
-    for (int q = 0; q < 4; ++q) {
-      const int rc = ncf_defer(defer, w.part + q * D, 2 * nblk, 4 * D, D, outs[q], 0, D, D);
-      if (rc) return rc;
-    }
-    return NCF_OK;
-  }
-  float* red = w.part + (int64_t)2 * w.nbr * 4 * D;
-  ncf_reduce_parts(w.part, 2 * nblk, 4 * D, 4 * D, red, 0, 4 * D, 4 * D, st, w.red_scratch);
-  hipLaunchKernelGGL(k_ln_param_scatter, dim3(1), dim3(256), 0, st, red, D, dgm, dbm, dgl, dbl);
-  NCF_CHECK_LAUNCH("ncf_embedding_bwd(finalize)");
-  return NCF_OK;
 }
 
 template <int D>
@@ -629,20 +351,6 @@ static int embedding_bwd_reduce(bool bf, int64_t n, int64_t dim, int64_t num_use
   WS w = carve(workspace, n, dim);
   uint32_t *k0, *v0, *k1, *v1;
   sorted_bufs(w, sort_passes(num_users, num_items), &k0, &v0, &k1, &v1);
-  const bool mapped = omap0 != nullptr || (ldt != 0 && ldt != dim) || apply != nullptr;
-  if (n > 0 && use_pos_reduce() && !mapped) {
-    switch (dim) {
-#define POS(DD)                                                                                   \
-  case DD:                                                                                        \
-    return pos_reduce<DD>(w, n, k0, k1, v0, v1, uniq_users, uniq_items, dy_mf_user, dy_mlp_user,  \
-                          dy_mf_item, dy_mlp_item, mf_user, mlp_user, mf_item, mlp_item,          \
-                          mf_gamma, mlp_gamma, eps, grad_mf_user, grad_mlp_user, grad_mf_item,    \
-                          grad_mlp_item, grad_mf_gamma, grad_mf_beta, grad_mlp_gamma,             \
-                          grad_mlp_beta, defer, st, bf);
-      POS(16) POS(32) POS(64) POS(128) POS(256)
-#undef POS
-    }
-  }
   switch (dim) {
 #define SEG(DD)                                                                                   \
   case DD:                                                                                        \

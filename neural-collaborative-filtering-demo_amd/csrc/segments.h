@@ -10,8 +10,6 @@
 //                                       for a segment's first piece, first piece of segment
 //                                       c = fpiece[c], Pn = totals[2 + kind];
 //   segoff[kind][tile]                — segments starting before sort tile `tile`;
-//   cpos[i]                           — the segment of sorted position i (the position-ordered
-//                                       segment reduce of embedding_bwd.hip reads it).
 #pragma once
 #include "ncf_common.h"
 
@@ -44,7 +42,6 @@ struct WS {
   // segments / pieces
   uint32_t* segoff;    // [2][nb]
   uint32_t *start0, *start1, *pstart0, *pstart1, *pseg0, *pseg1, *fpiece0, *fpiece1;
-  uint32_t *cpos0, *cpos1;
   float *xp0, *xp1;    // [extras][2D] LayerNorm-backward rows of the non-first pieces
   float* part;         // [2 * nbr + 1][4D] dgamma/dbeta partials
   float* red_scratch;
@@ -90,7 +87,6 @@ static inline int64_t ws_bytes(int64_t n, int64_t D) {
   b += 2 * round256(4 * (n + 2));            // start
   b += 4 * round256(4 * pieces_max(n));      // pstart, pseg
   b += 2 * round256(4 * (n + 2));            // fpiece
-  b += 2 * round256(4 * (n + 2));            // cpos
   b += 2 * round256(4 * extras_max(n) * 2 * D);
   b += round256(4 * (2 * nbr + 1) * 4 * D);
   b += round256(4 * ncf_reduce_scratch(2 * nbr, 4 * D) + 4);
@@ -127,8 +123,6 @@ static inline WS carve(void* base, int64_t n, int64_t D) {
   w.pseg1 = (uint32_t*)take(4 * pieces_max(n));
   w.fpiece0 = (uint32_t*)take(4 * (n + 2));
   w.fpiece1 = (uint32_t*)take(4 * (n + 2));
-  w.cpos0 = (uint32_t*)take(4 * (n + 2));
-  w.cpos1 = (uint32_t*)take(4 * (n + 2));
   w.xp0 = (float*)take(4 * extras_max(n) * 2 * D);
   w.xp1 = (float*)take(4 * extras_max(n) * 2 * D);
   w.part = (float*)take(4 * (2 * (int64_t)w.nbr + 1) * 4 * D);

@@ -19,7 +19,6 @@ contraction-free arithmetic, so the result is bit-identical to the dense sweep (
 work moves from HBM traffic (24 B/element/step) to VALU (~15 flops/element/step, amortised).
 """
 import ctypes
-import os
 import itertools
 
 import numpy as np
@@ -57,6 +56,12 @@ LATE_CATCHUP = True
 # HIP stream priority of the overlapped sweep's side stream (torch.cuda.Stream priority: 0 the
 # default, -1 high)
 SIDE_PRIORITY = 0
+# The overlapped rolling sweep (below) for FusedTrainStep and the optimizer hook: on (False: the
+# sweep on the step's own stream)
+OVERLAP_SWEEP = True
+# Fork point(s) of the overlapped sweep (None: the geometry's default, _default_fork; else a
+# comma-separated list, see DeferredTableAdam.__init__)
+SWEEP_FORK = None
 
 
 class DeferredTableAdam:
@@ -113,8 +118,7 @@ class DeferredTableAdam:
         # (tower_fused.hip: the sweep beside the fused forward and backward; round 5, 3
         # interleaved runs each: 0.2879-0.2908 ms/step, forked at mlp_bwd 0.3056-0.3074, the
         # unfused step 0.2972-0.3006), else "mlp_bwd" (unfused at "tower": 0.3107-0.3119).
-        env = os.environ.get("NCF_SWEEP_FORK")
-        self.fork_points = env.split(",") if env else [self._default_fork(engine)]
+        self.fork_points = SWEEP_FORK.split(",") if SWEEP_FORK else [self._default_fork(engine)]
         self._owed = []           # parts of a closed step's rolling sweep not launched yet
         self._side = None
         self._ev = None

@@ -32,7 +32,6 @@ torch reference backend.
 """
 import ctypes
 import math
-import os
 import random
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -48,7 +47,15 @@ from ._lib import ptr
 # ids, the targets, the compute stream), then the per-step scalars
 SLOT_NEXT_U, SLOT_NEXT_I, SLOT_TARGETS, SLOT_STREAM = 0, 1, 2, 3
 SLOT_TOKEN, SLOT_NMAX, SLOT_NUNI, SLOT_TOKEN_NEXT = 4, 5, 6, 7
-TAPE_SHARDED = os.environ.get("NCF_TAPE", "1") != "0"
+TAPE_SHARDED = True
+# The next step's rows sent to their owners during this step (on the side communicator)
+SHARD_AHEAD = True
+# The owner's rolling sweep overlapped on a side stream, and queued on the plan stream
+SHARD_OVERLAP_SWEEP = True
+SWEEP_ON_PLAN = True
+# The exchange implementation (None: RCCL through the C-ABI on the nccl backend, torch
+# collectives otherwise; "rccl" / "torch" force one)
+EXCHANGE = None
 # The owner's rank-order gradient sum inside the table Adam's apply (ncf_adam_pairs_apply_gsum_clock,
 # one launch and no compact gradient round trip; False: ncf_shard_owner_gradsum + the apply)
 GSUM_APPLY = True
@@ -337,8 +344,8 @@ class ShardedTrainStep:
     def __init__(self, ops, exchange: ShardExchange, ahead: Optional[bool] = None):
         self.ops, self.x = ops, exchange
         self._pending = None      # [user_ids, item_ids, Plan, (recv, event) | None] planned ahead
-        # send the next step's rows to their owners during this step (env NCF_SHARD_AHEAD=0: off)
-        self.ahead = ahead if ahead is not None else os.environ.get("NCF_SHARD_AHEAD", "1") != "0"
+        # send the next step's rows to their owners during this step (SHARD_AHEAD)
+        self.ahead = ahead if ahead is not None else bool(SHARD_AHEAD)
         # launch tapes (HIP ops + C-ABI collectives): the two launch segments of a step (split
         # at the host wait for the next plan's sizes) recorded once per geometry and replayed.
         # World 1 only: a replay of recorded RCCL collectives at world > 1 has not run on
@@ -603,8 +610,7 @@ class HipShardOps:
         self.clock = torch.tensor([0, self.base_seed], dtype=torch.int64, device=self.dev)
         self.deferred = DeferredTableAdam(self.eng, lr, betas, eps, weight_decay, sweep_every,
                                           clock=self.clock,
-                                          overlap_sweep=os.environ.get("NCF_SHARD_OVERLAP_SWEEP",
-                                                                       "1") != "0")
+                                          overlap_sweep=bool(SHARD_OVERLAP_SWEEP))
         self.m_flat = torch.zeros_like(self.eng.flat)
         self.v_flat = torch.zeros_like(self.eng.flat)
         self.step_count = 0
@@ -623,7 +629,7 @@ class HipShardOps:
         self.cnts = [torch.zeros(2, dtype=torch.int32, device=self.dev) for _ in range(2)]
         self.cnt = self.cnts[0]
         self.plan_stream = torch.cuda.Stream(self.dev)
-        if self.deferred.overlap and os.environ.get("NCF_SHARD_SWEEP_ON_PLAN", "1") != "0":
+        if self.deferred.overlap and SWEEP_ON_PLAN:
             # the overlapped sweep on the plan's stream, not a stream of its own: world 1,
             # ms/step (interleaved, 3 runs each): sweep serial 0.378-0.385, overlapped on its
             # own stream 0.40-0.43, overlapped on the plan stream 0.361-0.365 (hardware queues
@@ -927,7 +933,7 @@ def make_sharded_step(model_factory, num_users, num_items, group=None, plan_grou
     Dense parameters are broadcast from rank 0 so every replica starts identical.  A second
     communicator for the pipelined plan's count exchange is created unless given.
     ``exchange``: "rccl" (the C-ABI collectives, default on the nccl backend) or "torch"
-    (torch.distributed collectives); env NCF_EXCHANGE overrides the default."""
+    (torch.distributed collectives); the module's EXCHANGE overrides the default."""
     world = dist.get_world_size(group)
     model = model_factory(shard_rows(num_users, world), shard_rows(num_items, world))
     dev = model.mf_norm.weight.device
@@ -938,7 +944,7 @@ def make_sharded_step(model_factory, num_users, num_items, group=None, plan_grou
         ranks = list(range(world)) if group is None else dist.get_process_group_ranks(group)
         plan_group = dist.new_group(ranks)
     ops = HipShardOps(model, num_users, num_items, world, **adam)
-    kind = exchange or os.environ.get("NCF_EXCHANGE") or (
+    kind = exchange or EXCHANGE or (
         "rccl" if dist.get_backend(group) == "nccl" else "torch")
     if kind not in ("rccl", "torch"):
         raise ValueError(f"exchange must be 'rccl' or 'torch', not {kind!r}")

@@ -13,7 +13,6 @@ Data layout in HBM (fp32 throughout — the reference computes in fp32):
 """
 import ctypes
 import math
-import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -53,6 +52,15 @@ GROUP_ROWS = True
 # block and every row is gathered (no group rows), so every row's Q is projected.
 ATTN_SHARE_Q = True
 _WGRAD_ROWS = 160
+# Geometry switches, read when an engine is built (tests and A/B runs set them before building a
+# model): the one-launch MLP tower (False: per-layer GEMM + row launches), its fused weight
+# gradients (False: the grouped weight-gradient launch), the one-launch attention block (False:
+# projection GEMMs + attention.hip core), and the attention backward recomputing q/k/v/P/o
+# instead of reading the forward's stash (off: measured slower, below)
+MLP_FUSED = True
+MLP_WGRAD = True
+ATTN_BLOCK = True
+ATTN_RC = False
 # the fused attention forward's O stash (off: the backward recomputes O from the stashed P and V,
 # attn_pv, the same bits, tested).  Measured at C2, 3 interleaved runs each: forward 22.3-23.1
 # against 23.0-23.2 us, backward 38.3-38.9 against 37.9-38.0 us, forward HBM 25.7 against
@@ -204,12 +212,11 @@ class NCFEngine:
         self._events = None
         self._ev_i = 0
         self._mlp_ok = {}
-        # NCF_* switches read once per engine (the tests set them before building a model)
-        env = os.environ.get
-        self._env_mlp_fused = env("NCF_MLP_FUSED", "1") != "0"
-        self._env_mlp_wgrad = env("NCF_MLP_WGRAD", "1") != "0"
-        self._env_attn_block = env("NCF_ATTN_BLOCK", "1") != "0"
-        self._env_attn_rc = env("NCF_ATTN_RC", "0") != "0"
+        # the module's geometry switches as they were when this engine was built
+        self._env_mlp_fused = bool(MLP_FUSED)
+        self._env_mlp_wgrad = bool(MLP_WGRAD)
+        self._env_attn_block = bool(ATTN_BLOCK)
+        self._env_attn_rc = bool(ATTN_RC)
         from .tapes import StepTapes
         self.tapes = StepTapes(self)   # launch tapes of the reference call pattern (tapes.py)
         self.updates = 0          # parameter writes by the HIP kernels (torch's _version misses them)
@@ -547,7 +554,7 @@ class NCFEngine:
 
     def mlp_fused(self, D: int, hid) -> bool:
         """Whether the one-launch MLP tower (mlp_tower.hip) covers this geometry;
-        NCF_MLP_FUSED=0 forces the per-layer launches (A/B measurement, parity tests)."""
+        MLP_FUSED = False forces the per-layer launches (A/B measurement, parity tests)."""
         if not self._env_mlp_fused:
             return False
         key = (D, tuple(hid))
@@ -560,7 +567,7 @@ class NCFEngine:
 
     def mlp_fused_wgrad(self) -> bool:
         """The tower backward also computes the three MLP weight gradients (per-workgroup
-        partials); NCF_MLP_WGRAD=0 leaves them to the grouped weight-gradient launch."""
+        partials); MLP_WGRAD = False leaves them to the grouped weight-gradient launch."""
         return self._env_mlp_wgrad
 
     def _mlp_layers(self, w, train: bool, bwd: bool):
@@ -596,7 +603,7 @@ class NCFEngine:
 
     def attn_block(self, D: int, H: int, M: int) -> bool:
         """Whether the one-launch attention block (attn_block.hip) covers this geometry;
-        NCF_ATTN_BLOCK=0 forces the unfused launches (A/B measurement, parity tests)."""
+        ATTN_BLOCK = False forces the unfused launches (A/B measurement, parity tests)."""
         if not self._env_attn_block:
             return False
         key = ("attn", D, H, M)
@@ -637,7 +644,7 @@ class NCFEngine:
     def attn_rc(self, D: int, H: int, M: int) -> bool:
         """Whether the training forward of the attention block stashes nothing and its backward
         recomputes q/k/v, the probabilities and o from the LN'd rows (ncf_attn_block_bwd_rc:
-        27.9 MB less HBM traffic per C2 step).  Off by default (NCF_ATTN_RC=1 turns it on):
+        27.9 MB less HBM traffic per C2 step).  Off by default (ATTN_RC):
         measured at C2 the forward gains 3 us and the backward loses 6-7 us (its serial
         re-projection + core prologue costs more than reading the stash back)."""
         if not self._env_attn_rc:

@@ -32,7 +32,7 @@ def _wgrad(dY, X, dW, n, m_out, k_in, dbias=None):
 
 class _MHAFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, mod, drop_p, seed, q_in, k_in, v_in, wq, bq, wk, bk, wv, bv, wo, bo):
+    def forward(ctx, mod, drop_p, seed, mask, q_in, k_in, v_in, wq, bq, wk, bk, wv, bv, wo, bo):
         Bn, L, D = q_in.shape
         H = mod.num_heads
         n = Bn * L
@@ -43,8 +43,12 @@ class _MHAFunction(torch.autograd.Function):
         _gemm(xq, D, 0, wq, D, 1, q, D, n, D, D, bq)
         _gemm(xk, D, 0, wk, D, 1, k, D, n, D, D, bk)
         _gemm(xv, D, 0, wv, D, 1, v, D, n, D, D, bv)
-        _lib.call("ncf_attention_fwd", ptr(q), ptr(k), ptr(v), Bn, L, H, D, drop_p, seed, None, ptr(P),
-                  ptr(o), _lib.stream_ptr(dev))
+        if mask is None:
+            _lib.call("ncf_attention_fwd", ptr(q), ptr(k), ptr(v), Bn, L, H, D, drop_p, seed, None,
+                      ptr(P), ptr(o), _lib.stream_ptr(dev))
+        else:    # [Bn, H, L, L] bytes, 0 = masked (architecture.py:47-48)
+            _lib.call("ncf_attention_fwd_masked", ptr(q), ptr(k), ptr(v), Bn, L, H, D, drop_p, seed,
+                      None, ptr(mask), ptr(P), ptr(o), _lib.stream_ptr(dev))
         _gemm(o, D, 0, wo, D, 1, y, D, n, D, D, bo)
         ctx.save_for_backward(xq, xk, xv, q, k, v, P, o, wq, wk, wv, wo)
         ctx.meta = (Bn, L, D, H, drop_p, seed)
@@ -73,22 +77,31 @@ class _MHAFunction(torch.autograd.Function):
             gx = torch.empty(n, D, device=dev)
             _gemm(dX, D, 0, W, D, 0, gx, D, n, D, D)
             outs.append(gx.view(Bn, L, D))
-        return (None, None, None, outs[0], outs[1], outs[2], g["wq"], gb["bq"], g["wk"], gb["bk"],
+        return (None, None, None, None, outs[0], outs[1], outs[2], g["wq"], gb["bq"], g["wk"], gb["bk"],
                 g["wv"], gb["bv"], g["wo"], gb["bo"])
 
 
 def mha_forward(mod, query, key, value, mask=None):
     """MultiHeadAttention.forward (architecture.py:35-57): query/key/value [B, L, D] (a 2-D
-    [B, D] input is a length-1 sequence, as the reference's .view(batch, -1, H, hd) makes it)."""
-    if mask is not None:
-        raise NotImplementedError("attention mask is never passed on the reference path")
+    [B, D] input is a length-1 sequence, as the reference's .view(batch, -1, H, hd) makes it).
+    ``mask`` (:36, :47-48): any tensor that broadcasts against the scores [B, H, L, L]; where it
+    is 0 the score is -inf before the softmax (ncf_attention_fwd_masked)."""
     _require_cuda(query)
     squeeze = query.dim() == 2
     if squeeze:
         query, key, value = query.unsqueeze(1), key.unsqueeze(1), value.unsqueeze(1)
+    if key.shape[1] != query.shape[1] or value.shape[1] != key.shape[1]:
+        raise NotImplementedError("MultiHeadAttention: key/value length must equal the query's "
+                                  "on this path (every reference call site passes equal lengths)")
     drop_p = float(mod.dropout.p) if mod.training else 0.0
     seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0 else 0
-    y = _MHAFunction.apply(mod, drop_p, seed, query, key, value, mod.q_proj.weight, mod.q_proj.bias,
+    m8 = None
+    if mask is not None:
+        Bn, L = query.shape[0], query.shape[1]
+        m = torch.as_tensor(mask, device=query.device)
+        # masked_fill(mask == 0, .) broadcasts the mask against the scores [B, H, L, L]
+        m8 = torch.broadcast_to(m != 0, (Bn, mod.num_heads, L, L)).to(torch.uint8).contiguous()
+    y = _MHAFunction.apply(mod, drop_p, seed, m8, query, key, value, mod.q_proj.weight, mod.q_proj.bias,
                            mod.k_proj.weight, mod.k_proj.bias, mod.v_proj.weight, mod.v_proj.bias,
                            mod.out_proj.weight, mod.out_proj.bias)
     return y  # a 2-D input comes back [B, 1, D], as the reference's .view(batch, -1, D) makes it

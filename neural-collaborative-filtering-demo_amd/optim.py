@@ -26,7 +26,6 @@ torch's own step (so torch's loop never sees them) and put back afterwards.
 other than plain Adam (amsgrad, maximize, capturable, differentiable, tensor lr, other classes)
 receive materialised dense table gradients and run unchanged.
 """
-import os
 import weakref
 
 import torch
@@ -109,6 +108,7 @@ class _Binding:
     torch-format state."""
 
     def __init__(self, model, opt, group):
+        from . import deferred as deferred_mod
         from .deferred import DeferredTableAdam
         eng = model.engine
         eng.ensure_layout()
@@ -136,7 +136,7 @@ class _Binding:
         if SCHEDULE == "deferred":
             self.D = DeferredTableAdam(eng, lr, betas, eps, wd, SWEEP_EVERY,
                                        moments=self.moments, clock=self.clock,
-                                       overlap_sweep=os.environ.get("NCF_OVERLAP_SWEEP", "1") != "0")
+                                       overlap_sweep=deferred_mod.OVERLAP_SWEEP)
             eng.clock = self.clock
         self.adopt(opt)
 

@@ -20,15 +20,14 @@ A tape is replayed only when the host state its Python code branches on equals t
 was recorded in (``_pre`` keys) and the buffers it names are the same (``_signature``); the host
 state the replayed code would have left is then set as that code sets it (``_post``).  Anything
 else -- gradient accumulation, a frozen table, an lr change that moves the scalar table, an
-instrumented run -- takes the eager path for that phase.  NCF_TAPE=0 turns tapes off.
+instrumented run -- takes the eager path for that phase.  ENABLED = False turns tapes off.
 """
-import os
 
 import torch
 
 from . import _lib
 
-ENABLED = os.environ.get("NCF_TAPE", "1") != "0"
+ENABLED = True
 RECORD_AFTER = 2          # consecutive eager steps of one geometry before its tapes are recorded
 
 

@@ -11,7 +11,6 @@ the reference trainer is out of scope; batches are (KeyedJaggedTensor, targets[N
 BCE + backward kernels, fused Adam — identical math, one kernel sequence on one stream.  It is
 what the benchmark times (and what a production trainer uses).
 """
-import os
 import logging
 from typing import Any, Dict, Optional  # noqa: F401
 
@@ -129,7 +128,7 @@ class FusedTrainStep:
             eng.clock = self.clock
         self.deferred = None
         if overlap_sweep is None:    # the overlapped rolling sweep (deferred.py): on by default
-            overlap_sweep = os.environ.get("NCF_OVERLAP_SWEEP", "1") != "0"
+            overlap_sweep = deferred_mod.OVERLAP_SWEEP
         if deferred:
             from .deferred import DeferredTableAdam
             self.deferred = DeferredTableAdam(eng, lr, betas, eps, weight_decay, sweep_every,

@@ -41,15 +41,19 @@ def linear(x: Tensor, w: Tensor, b: Tensor) -> Tensor:
 
 
 def mha(p: Dict[str, Tensor], pre: str, q_in: Tensor, k_in: Tensor, v_in: Tensor,
-        num_heads: int, drop_mask: Optional[Tensor] = None) -> Tensor:
+        num_heads: int, drop_mask: Optional[Tensor] = None,
+        mask: Optional[Tensor] = None) -> Tensor:
     """MultiHeadAttention.forward (architecture.py:35-57): per-head softmax(QK^T/sqrt(hd))V,
-    dropout on the weights (:51), merge heads, out_proj.  q_in/k_in/v_in: [B, L, D]."""
+    dropout on the weights (:51), merge heads, out_proj.  q_in/k_in/v_in: [B, L, D].  ``mask``
+    (:36, :47-48): scores.masked_fill(mask == 0, -inf), broadcast against [B, H, L, L]."""
     B, L, D = q_in.shape
     hd = D // num_heads
     q = linear(q_in, p[pre + "q_proj.weight"], p[pre + "q_proj.bias"]).view(B, -1, num_heads, hd).transpose(1, 2)
     k = linear(k_in, p[pre + "k_proj.weight"], p[pre + "k_proj.bias"]).view(B, -1, num_heads, hd).transpose(1, 2)
     v = linear(v_in, p[pre + "v_proj.weight"], p[pre + "v_proj.bias"]).view(B, -1, num_heads, hd).transpose(1, 2)
     s = (q @ k.transpose(-2, -1)) / math.sqrt(hd)               # :33, :45
+    if mask is not None:
+        s = s.masked_fill(mask == 0, float("-inf"))              # :47-48
     a = torch.softmax(s, dim=-1)                                 # :50
     if drop_mask is not None:
         a = a * drop_mask

@@ -53,6 +53,36 @@ def test_library_exports_every_symbol():
     assert _lib.query("ncf_embedding_bwd_workspace", 20480, 64) > 0
 
 
+def test_library_build_identity_is_checked(monkeypatch, tmp_path):
+    """The library carries the hash of the ctypes table and of the kernel sources it was built
+    from (ncf_build_info, _abi.py); _lib.load() refuses a library whose table differs from
+    SIGNATURES, or whose sources differ from the ones beside the package (a stale build: the
+    r05y fault's first suspect, VERDICT r5 / ADVICE r5)."""
+    from ncf_amd import _abi
+    lib = _lib.load()
+    info = _lib.build_info(lib)
+    assert info["abi"] == _abi.abi_hash(_lib.SIGNATURES)
+    assert info["src"] == _abi.src_hash()
+    _lib.check_build(lib)
+    changed = dict(_lib.SIGNATURES)
+    changed["ncf_fill_2d"] = (_lib.I32, changed["ncf_fill_2d"][1][:-1])   # one argument fewer
+    monkeypatch.setattr(_lib, "SIGNATURES", changed)
+    with pytest.raises(_lib.NCFLibraryError, match="C-ABI"):
+        _lib.check_build(lib)
+    monkeypatch.undo()
+    # an edited kernel source without a rebuild
+    csrc = tmp_path / "csrc"
+    csrc.mkdir()
+    for f in _abi.source_files():
+        if f.endswith((".hip", ".h")) and os.path.dirname(f) == _abi.CSRC:
+            (csrc / os.path.basename(f)).write_bytes(open(f, "rb").read())
+    (csrc / "adam.hip").write_bytes((csrc / "adam.hip").read_bytes() + b"\n// edited\n")
+    monkeypatch.setattr(_abi, "CSRC", str(csrc))
+    monkeypatch.setattr(_abi.src_hash, "__defaults__", (str(csrc),))
+    with pytest.raises(_lib.NCFLibraryError, match="stale"):
+        _lib.check_build(lib)
+
+
 def test_code_object_is_gfx950():
     out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", _lib.LIB_PATH],
                          capture_output=True, text=True)

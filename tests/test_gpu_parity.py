@@ -18,6 +18,8 @@ from tests.parity import (assert_moment_close, assert_params_close, zone_from_gr
 
 pytestmark = pytest.mark.gpu
 ncf = _ncf_pkg.load()
+from ncf_amd import deferred as _D  # noqa: E402
+from ncf_amd import engine as _E  # noqa: E402
 DEV = torch.device("cuda:0")
 
 
@@ -256,6 +258,53 @@ def test_f4_mha(f4, tag):
                                    err_msg=n)
 
 
+@pytest.mark.parametrize("kind", ["causal", "padding", "per_head"])
+def test_mha_mask_vs_oracle(f4, kind):
+    """MultiHeadAttention.forward's mask (architecture.py:36, 47-48: masked_fill(mask == 0,
+    -inf) broadcast against the [B, H, L, L] scores) on the F4 mha5 module and inputs: a causal
+    [L, L] mask, a key-padding [B, 1, 1, L] mask and a random per-head [B, H, L, L] mask (every
+    row keeps at least one key), forward and backward against the oracle's restatement with the
+    same mask (the reference's fixtures hold no masked call: that part of the pin is the
+    restatement of :47-48).  A fully masked row comes out NaN, as torch's softmax makes it."""
+    Bn, L, D, H = [int(x) for x in f4["mha5/shape"]]
+    w = T(sub(f4, "mha5/w/"))
+    mod = ncf.MultiHeadAttention(D, H, dropout=0.0)
+    mod.load_state_dict(w)
+    mod = mod.to(DEV)
+    g = torch.Generator().manual_seed(3)
+    if kind == "causal":
+        mask = torch.tril(torch.ones(L, L, dtype=torch.bool))
+    elif kind == "padding":
+        lens = torch.randint(1, L + 1, (Bn,), generator=g)
+        mask = (torch.arange(L)[None, :] < lens[:, None]).view(Bn, 1, 1, L)
+    else:
+        mask = torch.rand(Bn, H, L, L, generator=g) < 0.6
+        mask[..., 0] = True
+    qkv = [torch.from_numpy(f4[f"mha5/{n}"]) for n in "qkv"]
+    gy = torch.from_numpy(f4["mha5/gy"])
+    xs = [t.to(DEV).requires_grad_(True) for t in qkv]
+    y = mod(*xs, mask=mask.to(DEV))
+    y.backward(gy.to(DEV))
+    ps = {f"a.{k}": v.clone().requires_grad_(True) for k, v in w.items()}
+    rs = [t.clone().requires_grad_(True) for t in qkv]
+    ry = O.mha(ps, "a.", *rs, H, mask=mask)
+    ry.backward(gy)
+    torch.testing.assert_close(y.detach().cpu(), ry.detach(), atol=2e-5, rtol=1e-5)
+    for a_, b_ in zip(xs, rs):
+        torch.testing.assert_close(a_.grad.cpu(), b_.grad, atol=2e-5, rtol=1e-4)
+    for n, p in mod.named_parameters():
+        torch.testing.assert_close(p.grad.cpu(), ps[f"a.{n}"].grad, atol=5e-5, rtol=1e-4)
+    # a fully masked row (group 0, head 0, query 0): NaN in that group's outputs, like torch
+    if kind == "per_head":
+        m2 = mask.clone()
+        m2[0, 0, 0, :] = False
+        with torch.no_grad():
+            y2 = mod(*[t.detach() for t in xs], mask=m2.to(DEV)).cpu()
+            r2 = O.mha({k: v.detach() for k, v in ps.items()}, "a.", *qkv, H, mask=m2)
+        assert torch.isnan(y2[0]).any() and torch.equal(torch.isnan(y2), torch.isnan(r2))
+        torch.testing.assert_close(y2[1:], r2[1:], atol=2e-5, rtol=1e-5)
+
+
 def test_f4_temporal(f4):
     te = ncf.TemporalEncoding(32)
     te.load_state_dict({**T(sub(f4, "te/w/")), "pe": torch.from_numpy(f4["te/pe"])})
@@ -425,56 +474,6 @@ def test_embedding_bwd_segment_reduce():
     assert int((su != -1).sum()) == 0 and int((si != -1).sum()) == 0
 
 
-@pytest.mark.parametrize("D,n", [(64, 9000), (16, 1000), (32, 4099), (128, 2051), (64, 17), (64, 1)])
-def test_position_reduce_equals_piece_reduce(monkeypatch, D, n):
-    """The position-ordered embedding backward (k_pos_reduce_ln + k_pos_fixup, NCF_EMB_POS=1)
-    against the piece-record form (the default): the same pieces summed in the same order, so every
-    compact table-gradient row agrees to fp32 rounding of the LayerNorm backward; dgamma/dbeta
-    partials sum in another order.  Heavy duplication (multi-slot segments), ragged n,
-    D = 16 .. 128."""
-    from ncf_amd import _lib
-    U, I = 5000, 700
-    g = torch.Generator().manual_seed(D + n)
-    uid = torch.randint(0, U, (n,), generator=g)
-    uid[: n // 3] = 4321
-    iid = (torch.rand(n, generator=g) ** 4 * I).long()
-    tabs = [torch.randn(r, D, generator=g).to(DEV) for r in (U, U, I, I)]
-    dys = [torch.randn(n, D, generator=g).to(DEV) for _ in range(4)]
-    gm, gl = torch.randn(D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
-    ud, idd = uid.to(DEV), iid.to(DEV)
-    P = lambda t: t.data_ptr()  # noqa: E731
-    res = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("NCF_EMB_POS", flag)
-        G = [torch.zeros(n, D, device=DEV) for _ in range(4)]
-        uu, ui = (torch.empty(n, dtype=torch.int64, device=DEV) for _ in range(2))
-        su = torch.full((U,), -1, dtype=torch.int32, device=DEV)
-        si = torch.full((I,), -1, dtype=torch.int32, device=DEV)
-        nu = torch.zeros(2, dtype=torch.int32, device=DEV)
-        pg = [torch.empty(D, device=DEV) for _ in range(4)]
-        ws = torch.empty(_lib.query("ncf_embedding_bwd_workspace", n, D), dtype=torch.uint8, device=DEV)
-        _lib.call("ncf_embedding_bwd", P(ud), P(idd), n, D, U, I, *[P(x) for x in dys],
-                  *[P(x) for x in (tabs[0], tabs[1], tabs[2], tabs[3])], P(gm), P(gl), 1e-5,
-                  *[P(x) for x in G], P(uu), P(ui), P(su), P(si), P(nu), *[P(x) for x in pg],
-                  P(ws), ws.numel(), _lib.stream_ptr(DEV))
-        torch.cuda.synchronize()
-        nun = nu.cpu().tolist()
-        res.append(([G[0][:nun[0]].cpu(), G[1][:nun[0]].cpu(), G[2][:nun[1]].cpu(),
-                     G[3][:nun[1]].cpu()], [x.cpu() for x in pg]))
-    (g0, p0), (g1, p1) = res
-    # the same pieces summed in the same order; the two kernels' LayerNorm backward may fuse
-    # its multiply-adds differently (-ffp-contract), so rows agree to fp32 rounding
-    diffs = [(b - a).abs().max().item() for a, b in zip(g0, g1)]
-    print(f"pos vs piece reduce D={D} n={n}: max |dG| per table {diffs}, bitwise "
-          f"{[torch.equal(a, b) for a, b in zip(g0, g1)]}")
-    # (a misassigned piece or occurrence would differ by O(1); summed over a 3000-occurrence
-    # segment's 188 pieces, per-piece rounding differences reach ~1e-5 relative)
-    for a, b in zip(g0, g1):
-        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
-    for a, b in zip(p0, p1):
-        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-4)
-
-
 def test_adam_table_kernel_matches_torch():
     from ncf_amd import _lib
     rows, D = 1000, 64
@@ -506,7 +505,7 @@ def test_adam_table_kernel_matches_torch():
 def test_dropout_statistics(monkeypatch):
     # per-layer weight-gradient launches: the forward then saves the dropped activations a
     # (the fused tower backward recomputes them instead)
-    monkeypatch.setenv("NCF_MLP_WGRAD", "0")
+    monkeypatch.setattr(_E, "MLP_WGRAD", False)
     torch.manual_seed(0)
     m = ncf.AdvancedNCF(1000, 500, 5, 24, dropout=0.2).to(DEV)
     n = 4096 * 5
@@ -604,7 +603,7 @@ def test_attn_block_matches_unfused(monkeypatch, D, H, M, B):
     from ncf_amd.trainer import FusedTrainStep
     out = []
     for flag in ("0", "1"):
-        monkeypatch.setenv("NCF_ATTN_BLOCK", flag)
+        monkeypatch.setattr(_E, "ATTN_BLOCK", (flag) == "1")
         torch.manual_seed(21)
         m = ncf.AdvancedNCF(400, 300, 5, 24, D, D, 32, [256, 128, 64], H, 0.2, M - 1).to(DEV)
         step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
@@ -640,7 +639,7 @@ def test_attn_block_recompute_bitwise_equals_stash(monkeypatch, D, H, M, B, drop
     from ncf_amd.trainer import FusedTrainStep
     out = []
     for flag in ("0", "1"):
-        monkeypatch.setenv("NCF_ATTN_RC", flag)
+        monkeypatch.setattr(_E, "ATTN_RC", (flag) == "1")
         torch.manual_seed(23)
         m = ncf.AdvancedNCF(400, 300, 5, 24, D, D, 32, [256, 128, 64], H, drop, M - 1).to(DEV)
         step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
@@ -678,7 +677,7 @@ def test_attn_shared_q_matches_per_row(monkeypatch, D, H, M, B, uniform, rc):
     (uniform=False) none does.  Both backward forms (stash, recompute)."""
     import ncf_amd.engine as E
     from ncf_amd.trainer import FusedTrainStep
-    monkeypatch.setenv("NCF_ATTN_RC", rc)
+    monkeypatch.setattr(_E, "ATTN_RC", (rc) == "1")
     out = []
     for flag in (False, True):
         monkeypatch.setattr(E, "ATTN_SHARE_Q", flag)
@@ -725,9 +724,9 @@ def test_mlp_tower_matches_unfused(monkeypatch, B, drop, D, wgrad, split):
     # test_attn_tower_fused_bitwise_equals_two_launches holds that form to this one)
     monkeypatch.setattr(E, "FUSE_ATTN_TOWER", False)
     out = []
-    monkeypatch.setenv("NCF_MLP_WGRAD", wgrad)
+    monkeypatch.setattr(_E, "MLP_WGRAD", (wgrad) == "1")
     for flag in ("0", "1"):
-        monkeypatch.setenv("NCF_MLP_FUSED", flag)
+        monkeypatch.setattr(_E, "MLP_FUSED", (flag) == "1")
         torch.manual_seed(31)
         m = ncf.AdvancedNCF(400, 300, 5, 24, D, D, 32, [256, 128, 64], 4, drop, 4).to(DEV)
         step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
@@ -860,7 +859,7 @@ def test_attn_tower_fused_bitwise_equals_two_launches(monkeypatch, tables):
 def test_mlp_tower_eval_matches_unfused(monkeypatch):
     res = []
     for flag in ("0", "1"):
-        monkeypatch.setenv("NCF_MLP_FUSED", flag)
+        monkeypatch.setattr(_E, "MLP_FUSED", (flag) == "1")
         torch.manual_seed(33)
         m = ncf.AdvancedNCF(300, 200, 5, 24).to(DEV).eval()
         u = torch.randint(0, 300, (1001,), device=DEV)
@@ -874,7 +873,7 @@ def test_attn_block_eval_forward_matches_unfused(monkeypatch):
     """Eval (M = 1): the block's no-core form (o = v) vs the unfused v/out projections."""
     res = []
     for flag in ("0", "1"):
-        monkeypatch.setenv("NCF_ATTN_BLOCK", flag)
+        monkeypatch.setattr(_E, "ATTN_BLOCK", (flag) == "1")
         torch.manual_seed(23)
         m = ncf.AdvancedNCF(300, 200, 5, 24).to(DEV).eval()
         u = torch.randint(0, 300, (1000,), device=DEV)
@@ -1050,7 +1049,7 @@ def test_overlapped_sweep_bitwise_equals_dense(monkeypatch, graph, fork):
     (ncf_adam_pairs_sweep_rolling_part), a part whose fork point the step never passes settled
     before the apply) is bit-identical to the dense sweep, eager and hipGraph-captured ("off":
     the sweep on the step's own stream)."""
-    monkeypatch.setenv("NCF_SWEEP_FORK", fork)
+    monkeypatch.setattr(_D, "SWEEP_FORK", fork)
     a_sd, a_m = _fused_run(False, 70)
     b_sd, b_m = _fused_run(True, 70, clock=True, graph=graph, overlap_sweep=fork != "off")
     for k in a_sd:
@@ -1059,15 +1058,22 @@ def test_overlapped_sweep_bitwise_equals_dense(monkeypatch, graph, fork):
         assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
 
 
+@pytest.mark.parametrize("fuse_apply,early_reduce", [(True, False), (False, False),
+                                                     (True, True), (False, True)])
 @pytest.mark.parametrize("mixed", [False, True])
-def test_group_rows_bitwise_equals_every_row(monkeypatch, mixed):
+def test_group_rows_bitwise_equals_every_row(monkeypatch, mixed, fuse_apply, early_reduce):
     """The gather writing each group's LN'd user rows once (group_rows = M; the
     attention block and the tower's head backward reading the group's row) against every row
-    written: parameters and Adam moments bit-identical over 6 FusedTrainStep steps and one
-    reference-call-pattern step.  ``mixed``: a third of the groups hold several users (those rows
-    are their own source rows) and the last workgroup is ragged."""
+    written: parameters and Adam moments bit-identical over 6 FusedTrainStep steps.  ``mixed``:
+    a third of the groups hold several users (those rows are their own source rows) and the last
+    workgroup is ragged.  Over the schedule switches the r05y fault could have run under
+    (trainer.FUSE_APPLY, trainer.EARLY_REDUCE; tests/test_gpu_guard.py audits the same paths
+    for reads past any buffer's end)."""
     from ncf_amd import engine as E
+    from ncf_amd import trainer as Tr
     from ncf_amd.trainer import FusedTrainStep
+    monkeypatch.setattr(Tr, "FUSE_APPLY", fuse_apply)
+    monkeypatch.setattr(Tr, "EARLY_REDUCE", early_reduce)
     U, I, B, M = 3000, 500, 61, 5
     g = torch.Generator().manual_seed(23)
     batches = []
@@ -1100,6 +1106,51 @@ def test_group_rows_bitwise_equals_every_row(monkeypatch, mixed):
     for k in out[0][1]:
         assert torch.equal(out[0][1][k][0], out[1][1][k][0]), k
         assert torch.equal(out[0][1][k][1], out[1][1][k][1]), k
+
+
+def test_step_teardown_with_side_work_queued_then_new_step():
+    """A FusedTrainStep dropped right after a step that queued side-stream work (the next
+    batch's id sort behind the overlapped sweep, the late catch-up, the early reductions), with
+    no host sync, and a second model + step built and run at once: the caching allocator hands
+    the second one blocks the first one freed (same stream), so any work of the first still
+    touching them would corrupt it.  The second run is bit for bit the same run made after a
+    device drain.  Covers the dedup fork at the step's entry (a side stream the step does NOT
+    join before it returns) as well as the default fork behind the sweep."""
+    import gc
+    import ncf_amd.trainer as Tr
+    from ncf_amd.trainer import FusedTrainStep
+    U, I, B = 3000, 500, 61
+
+    def leave_in_flight(seed):
+        torch.manual_seed(seed)
+        m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.2, 4).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5, sweep_every=8)
+        g = torch.Generator().manual_seed(seed)
+        bs = [(torch.randint(0, U, (B,), generator=g).repeat_interleave(5).to(DEV),
+               torch.randint(0, I, (B * 5,), generator=g).to(DEV)) for _ in range(6)]
+        t = torch.zeros(B, 5)
+        t[:, 0] = 1
+        t = t.reshape(-1, 1).to(DEV)
+        for s_ in range(5):
+            step(bs[s_][0], bs[s_][1], t, next=bs[s_ + 1])   # the last prefetch never consumed
+
+    ref = _fused_run(True, 12, sweep_every=8, B=B, seed=31, dropout=0.2, clock=True,
+                     overlap_sweep=True, pipelined=True)
+    for fork, early in (("sweep", False), ("entry", True)):
+        old = (Tr.DEDUP_FORK, Tr.EARLY_REDUCE)
+        Tr.DEDUP_FORK, Tr.EARLY_REDUCE = fork, early
+        try:
+            leave_in_flight(7)       # (its objects are unreachable on return: freed now)
+            gc.collect()
+            got = _fused_run(True, 12, sweep_every=8, B=B, seed=31, dropout=0.2, clock=True,
+                             overlap_sweep=True, pipelined=True)
+        finally:
+            Tr.DEDUP_FORK, Tr.EARLY_REDUCE = old
+        for k in ref[0]:
+            assert torch.equal(ref[0][k], got[0][k]), (fork, k)
+        for k in ref[1]:
+            assert torch.equal(ref[1][k][0], got[1][k][0]), (fork, k)
+            assert torch.equal(ref[1][k][1], got[1][k][1]), (fork, k)
 
 
 def test_attn_o_recompute_bitwise_equals_o_stash(monkeypatch):

@@ -28,6 +28,15 @@ OUT=gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 md5sum neural-collaborative-filtering-demo_amd/*.so > "$OUT/${TAG}_so.md5" 2>/dev/null
+# the build identity compiled into the library next to the hashes of this tree (_abi.py)
+python3 - >> "$OUT/${TAG}_so.md5" 2>&1 <<'PYEOF'
+import ctypes, subprocess
+lib = ctypes.CDLL("neural-collaborative-filtering-demo_amd/libncf_hip.so")
+lib.ncf_build_info.restype = ctypes.c_char_p
+tree = [subprocess.run(["python3", "neural-collaborative-filtering-demo_amd/_abi.py", k],
+                       capture_output=True, text=True).stdout.strip() for k in ("abi", "src")]
+print("library:", lib.ncf_build_info().decode(), "| tree: abi=%s src=%s" % tuple(tree))
+PYEOF
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
 QUICK="bench.py --steps 60 --warmup 10 --prime 128 --no-c4 --no-score --no-cpu-baseline --no-dropin --no-extra"
 for what in "$@"; do
