@@ -45,11 +45,11 @@ __device__ __forceinline__ float fkey_inv(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
 
-// ---- 1. queries: q = w0 * LN(U_mf[id]) (.) w_mf; L = D/4 lanes per row.  The rows are kQD = 64
-// floats wide whatever the table's D: a D < 64 row is zero-padded (the item index pads its rows
-// the same way, so every dot product is the D-term one — the scan kernels are 64-deep)
-constexpr int kQD = 64;
-template <int D>
+// ---- 1. queries: q = w0 * LN(U_mf[id]) (.) w_mf; L = D/4 lanes per row.  The rows are QD =
+// max(64, D) floats wide: a D < 64 row is zero-padded (the item index pads its rows the same way,
+// so every dot product is the D-term one — the scan kernels are 64-deep; D = 128 rows are
+// scanned 128-deep by the fp32 scan, k_collect<128>)
+template <int D, int kQD = (D > 64 ? D : 64)>
 __global__ void k_queries(const int64_t* __restrict__ ids, int64_t n, const float* __restrict__ table,
                           int64_t rows, const float* __restrict__ gamma,
                           const float* __restrict__ beta, float eps,
@@ -355,9 +355,10 @@ __global__ __launch_bounds__(256) void k_score_margin(const float* __restrict__ 
 
 // ---- 3. MFMA scan + threshold filter
 // fp32 tiling (k_collect): a 512-thread workgroup owns 256 users (8 waves x 32), keeps each
-// wave's q rows in registers (k-permuted: MFMA step s uses k = s + 32h), and streams 32-item tiles
-// of p through double-buffered LDS ([32][65] pitch: conflict-free); per tile a wave issues 32
-// v_mfma_f32_32x32x2_f32 and filters its 32x32 logits against 16 per-lane thresholds.  Hits are
+// wave's q rows in registers (k-permuted: MFMA step s uses k = s + (D/2)h), and streams 32-item
+// tiles of p through double-buffered LDS ([32][D+1] pitch: conflict-free); per tile a wave issues
+// D/2 v_mfma_f32_32x32x2_f32 and filters its 32x32 logits against 16 per-lane thresholds (D = 64,
+// or 128: the C4 model's width, two k chunks per tile).  Hits are
 // staged in LDS (one LDS atomic per wave and tile) and flushed to the global per-user lists in
 // parallel bursts (a global atomic per hit made the wave wait thousands of cycles per tile).
 constexpr int kUsersPerBlock = 256;  // 8 waves x 32
@@ -375,7 +376,9 @@ __global__ __launch_bounds__(512) void k_collect(
     int64_t items_per_block, const float* __restrict__ thr, int64_t cap,
     uint32_t* __restrict__ count, float* __restrict__ cand_logit,
     int32_t* __restrict__ cand_item) {
-  static_assert(D == 64, "scoring kernel is specialised for D = 64 (one 64-deep k chunk)");
+  static_assert(D == 64 || D == 128, "the fp32 scan takes 64- or 128-deep rows");
+  constexpr int KH = D / 2;      // k per lane half (MFMA step s: k = s + KH h)
+  constexpr int NV = D / 64;     // float4 per thread to stage a 32 x D tile
   __shared__ float ps[2][kItemTile][D + 1];
   __shared__ float bs[2][kItemTile];
   // Candidates are staged in LDS (an LDS atomic returns in ~100 cycles; a global one in
@@ -393,11 +396,11 @@ __global__ __launch_bounds__(512) void k_collect(
   const int64_t my_slot = slot0 + i;
   const bool uvalid = my_slot < n_users;
   const int64_t my_user = uvalid ? (user_list ? user_list[my_slot] : my_slot) : 0;
-  float a[32];
+  float a[KH];
   {
-    const float* qp = q + my_user * D + 32 * h;
+    const float* qp = q + my_user * D + KH * h;
 #pragma unroll
-    for (int v = 0; v < 8; ++v) {
+    for (int v = 0; v < KH / 4; ++v) {
       const float4 x = ld4(qp + 4 * v);
       a[4 * v] = x.x; a[4 * v + 1] = x.y; a[4 * v + 2] = x.z; a[4 * v + 3] = x.w;
     }
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(512) void k_collect(
   // iteration, which also drains the next tile's prefetch and exposes its HBM latency (measured:
   // the matrix cores idle half the time).
 #pragma unroll
-  for (int k = 0; k < 32; ++k) asm volatile("" ::"v"(a[k]));
+  for (int k = 0; k < KH; ++k) asm volatile("" ::"v"(a[k]));
   // thresholds of the 16 users whose logits this lane holds: row (r&3) + 8(r>>2) + 4h
   float th[16];
   int64_t urow[16];
@@ -420,18 +423,19 @@ __global__ __launch_bounds__(512) void k_collect(
   }
   const int64_t it0 = (int64_t)blockIdx.x * items_per_block;
   const int64_t it1 = min(n_items, it0 + items_per_block);
-  // staging: 512 threads x one float4 = one 32 x 64 tile
+  // staging: 512 threads x NV float4 = one 32 x D tile
   const int sj = tid >> 4, sk = (tid & 15) * 4;
-  auto fetch = [&](int64_t t0, float4& v, float& bv) {
+  auto fetch = [&](int64_t t0, float4 (&v)[NV], float& bv) {
     const int64_t item = t0 + sj;
     const int64_t src = item < it1 ? item : it0;  // clamped, unconditional
-    v = ld4(items + src * D + sk);
+#pragma unroll
+    for (int c = 0; c < NV; ++c) v[c] = ld4(items + src * D + sk + 64 * c);
     bv = bias[src];
   };
   // register ring of kPD staged tiles: the load of tile t + kPD is issued while tile t is
   // multiplied, so a tile's HBM latency hides behind kPD tiles of MFMAs (one tile alone,
   // ~2K cycles per wave, is shorter than a loaded HBM miss)
-  float4 pv[kPD];
+  float4 pv[kPD][NV];
   float pb[kPD];
 #pragma unroll
   for (int d = 0; d < kPD; ++d)
@@ -449,13 +453,22 @@ __global__ __launch_bounds__(512) void k_collect(
     }
   };
   for (int64_t t0 = it0; t0 < it1; t0 += kItemTile) {
-    float4 cur = pv[0];
+    float4 cur[NV];
     float cb = pb[0];
 #pragma unroll
+    for (int c = 0; c < NV; ++c) cur[c] = pv[0][c];
+#pragma unroll
     for (int d = 1; d < kPD; ++d)   // (static slot selection: the ring rotates by one)
-      if (slot == d) { cur = pv[d]; cb = pb[d]; }
-    ps[buf][sj][sk] = cur.x; ps[buf][sj][sk + 1] = cur.y;
-    ps[buf][sj][sk + 2] = cur.z; ps[buf][sj][sk + 3] = cur.w;
+      if (slot == d) {
+#pragma unroll
+        for (int c = 0; c < NV; ++c) cur[c] = pv[d][c];
+        cb = pb[d];
+      }
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      float* dst = &ps[buf][sj][sk + 64 * c];
+      dst[0] = cur[c].x; dst[1] = cur[c].y; dst[2] = cur[c].z; dst[3] = cur[c].w;
+    }
     if ((tid & 15) == 0) bs[buf][sj] = cb;
     __syncthreads();
     {
@@ -476,9 +489,9 @@ __global__ __launch_bounds__(512) void k_collect(
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-    const float* pb_row = &ps[buf][i][32 * h];
+    const float* pb_row = &ps[buf][i][KH * h];
 #pragma unroll
-    for (int s = 0; s < 32; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], pb_row[s], acc, 0, 0, 0);
+    for (int s = 0; s < KH; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], pb_row[s], acc, 0, 0, 0);
     const int64_t item = t0 + i;
     const float b = bs[buf][i];
     const bool ivalid = item < it1;
@@ -1439,15 +1452,15 @@ extern "C" int ncf_score_queries(const int64_t* user_ids, int64_t n, const float
                                  const float* mf_beta, float eps, const float* mf_out_w,
                                  const float* final_w, float* queries, int* err_flag,
                                  void* stream) {
-  NCF_CHECK_ARG(n >= 0 && (dim == 16 || dim == 32 || dim == 64),
-                "ncf_score_queries: dim must be 16, 32 or 64");
+  NCF_CHECK_ARG(n >= 0 && (dim == 16 || dim == 32 || dim == 64 || dim == 128),
+                "ncf_score_queries: dim must be 16, 32, 64 or 128");
   if (n == 0) return NCF_OK;
 #define NCF_QUERIES(DD)                                                                           \
   if (dim == DD)                                                                                  \
     hipLaunchKernelGGL(k_queries<DD>, dim3(ncf_cdiv(n * (DD / 4), 256)), dim3(256), 0,            \
                        (hipStream_t)stream, user_ids, n, mf_user, rows, mf_gamma, mf_beta, eps,     \
                        mf_out_w, final_w, queries, err_flag);
-  NCF_QUERIES(16) NCF_QUERIES(32) NCF_QUERIES(64)
+  NCF_QUERIES(16) NCF_QUERIES(32) NCF_QUERIES(64) NCF_QUERIES(128)
 #undef NCF_QUERIES
   NCF_CHECK_LAUNCH("ncf_score_queries");
   return NCF_OK;
@@ -1566,7 +1579,7 @@ extern "C" int ncf_score_collect(const float* queries, const int32_t* user_list,
                                  const float* items, const float* item_bias, int64_t n_items,
                                  int64_t dim, const float* thr, int64_t cap, uint32_t* count,
                                  float* cand_logit, int32_t* cand_item, void* stream) {
-  NCF_CHECK_ARG(dim == 64, "ncf_score_collect: dim must be 64");
+  NCF_CHECK_ARG(dim == 64 || dim == 128, "ncf_score_collect: dim must be 64 or 128");
   NCF_CHECK_ARG(n_users >= 0 && n_items >= 0 && n_items < (1ll << 31) && cap >= 1,
                 "ncf_score_collect: bad size");
   if (n_users == 0 || n_items == 0) return NCF_OK;
@@ -1580,9 +1593,14 @@ extern "C" int ncf_score_collect(const float* queries, const int32_t* user_list,
   per = (per + kItemTile - 1) / kItemTile * kItemTile;
   splits = (n_items + per - 1) / per;
   NCF_CHECK_ARG(ub < 65536, "ncf_score_collect: too many users per call (max %d)", 65535 * 256);
-  hipLaunchKernelGGL(k_collect<64>, dim3((unsigned)splits, (unsigned)ub), dim3(512), 0,
-                     (hipStream_t)stream, queries, user_list, n_users, items, item_bias, n_items,
-                     per, thr, cap, count, cand_logit, cand_item);
+  if (dim == 64)
+    hipLaunchKernelGGL(k_collect<64>, dim3((unsigned)splits, (unsigned)ub), dim3(512), 0,
+                       (hipStream_t)stream, queries, user_list, n_users, items, item_bias, n_items,
+                       per, thr, cap, count, cand_logit, cand_item);
+  else
+    hipLaunchKernelGGL(k_collect<128>, dim3((unsigned)splits, (unsigned)ub), dim3(512), 0,
+                       (hipStream_t)stream, queries, user_list, n_users, items, item_bias, n_items,
+                       per, thr, cap, count, cand_logit, cand_item);
   NCF_CHECK_LAUNCH("ncf_score_collect");
   return NCF_OK;
 }

@@ -86,6 +86,7 @@ class Geometry:
     T: int
     H: int
     hidden: List[int]
+    Dm: int = 0     # the MF tables' width (mf_embedding_dim); 0: the same as D
 
 
 class Workspace:
@@ -94,12 +95,20 @@ class Workspace:
     def __init__(self, g: Geometry, device, train: bool):
         f = dict(device=device, dtype=torch.float32)
         n, D = g.n, g.D
+        Dm = g.Dm or D
         self.g = g
         e = lambda *s: torch.empty(*s, **f)  # noqa: E731
         self.mf_pred, self.mlp_pred, self.prob = e(n), e(n), e(n)
         self.xu, self.xi, self.q, self.k, self.v, self.o, self.y = (e(n, D) for _ in range(7))
-        self.umf = e(n, D) if train else None
-        self.imf = e(n, D) if train else None
+        self.umf = e(n, Dm) if train else None
+        self.imf = e(n, Dm) if train else None
+        if Dm != D:
+            # split widths (mf_embedding_dim != mlp_embedding_dim): the gather and the embedding
+            # backward run once per collection; each run's second pair of outputs is scratch
+            self.split = {"rows_m": e(2, n, Dm), "rows_l": e(2, n, D), "pred": e(n),
+                          "zero_w": torch.zeros(D, **f)}
+        else:
+            self.split = None
         self.P = e(max(1, g.B * g.H * g.M * g.M))
         self.r = [e(n, h) for h in g.hidden]
         self.a = [e(n, h) for h in g.hidden]
@@ -110,7 +119,8 @@ class Workspace:
         self.cache = {}             # ctypes argument blocks built once per workspace
         if not train:
             return
-        self.dumf, self.dimf, self.dxu, self.dxi = (e(n, D) for _ in range(4))
+        self.dumf, self.dimf = e(n, Dm), e(n, Dm)
+        self.dxu, self.dxi = e(n, D), e(n, D)
         self.dq, self.dk, self.dv, self.do, self.dy = (e(n, D) for _ in range(5))
         self.dS = e(max(1, g.B * g.H * g.M * g.M))
         self.dlin = [e(n, h) for h in g.hidden]
@@ -136,7 +146,14 @@ class Workspace:
         self.wg_ws = []             # partials of the grouped launches in flight (one per slot)
         self.emb_ws = torch.empty(_lib.query("ncf_embedding_bwd_workspace", n, D),
                                   dtype=torch.uint8, device=device)
-        self.G = {k: e(n, D) for k in ("mf_user", "mlp_user", "mf_item", "mlp_item")}
+        self.G = {k: e(n, Dm if k.startswith("mf") else D)
+                  for k in ("mf_user", "mlp_user", "mf_item", "mlp_item")}
+        if Dm != D:      # the MF collection's own dedup workspace (its segment layout is per width)
+            self.emb_ws_m = torch.empty(_lib.query("ncf_embedding_bwd_workspace", n, Dm),
+                                        dtype=torch.uint8, device=device)
+            self.split["uniq"] = torch.empty(2, max(1, n), dtype=torch.int64, device=device)
+            self.split["num_unique"] = torch.zeros(2, dtype=torch.int32, device=device)
+            self.split["ln"] = torch.empty(4, max(D, Dm), **f)
         self.uniq_u = torch.empty(max(1, n), dtype=torch.int64, device=device)
         self.uniq_i = torch.empty(max(1, n), dtype=torch.int64, device=device)
         self.num_unique = torch.zeros(2, dtype=torch.int32, device=device)
@@ -368,7 +385,8 @@ class NCFEngine:
         if w is None:
             m = self.model
             g = Geometry(n=n, M=M, B=n // M, D=m.mlp_embedding_dim, T=m.temporal_dim,
-                         H=m.num_heads, hidden=list(m.mlp_hidden_dims))
+                         H=m.num_heads, hidden=list(m.mlp_hidden_dims),
+                         Dm=m.mf_embedding_dim)
             dev = self.model.mf_norm.weight.device
             w = Workspace(g, dev, train)
             w.err = self.err_flag(dev)
@@ -443,8 +461,14 @@ class NCFEngine:
             return w
         st = _lib.stream_ptr(dev)
         D, H, T, hid = m.mlp_embedding_dim, m.num_heads, m.temporal_dim, list(m.mlp_hidden_dims)
-        if m.mf_embedding_dim != D:
-            raise NotImplementedError("mf_embedding_dim must equal mlp_embedding_dim on this path")
+        split = m.mf_embedding_dim != D
+        if split and temporal is not None:
+            # the reference scales the MLP item rows by (1 + 0.3 te) with te of the MF width
+            # (architecture.py:436-456): a broadcast error there unless the widths agree
+            raise RuntimeError(f"forward_simple(hour): the temporal scale has {m.mf_embedding_dim} "
+                               f"columns, the MLP item rows {D}")
+        if split and (bf16 or (table_ld is not None and table_ld != D)):
+            raise ValueError("mf_embedding_dim != mlp_embedding_dim: fp32 tables, no table_ld")
         pp = self.pp()
         if tables is None:
             tbp = (pp["t_mf_user"], pp["t_mf_item"], pp["t_mlp_user"], pp["t_mlp_item"])
@@ -464,7 +488,24 @@ class NCFEngine:
         G = M if (GROUP_ROWS and ATTN_SHARE_Q and train and M > 1 and temporal is None
                   and self.attn_block(D, H, M) and self.mlp_fused(D, hid)) else 0
         w.group_rows = G
-        if table_ld is not None and table_ld != D:
+        if split:
+            # the two collections at their own widths (architecture.py:153-190, 305-312): the MF
+            # run writes mf_pred (and the LN'd GMF rows for the backward), its MLP-side outputs
+            # are scratch; the MLP run writes X_u / X_i, its GMF (a zero weight) is scratch
+            Dm, sp = m.mf_embedding_dim, w.split
+            mfu, mfi, mlu, mli = tbp
+            _lib.call("ncf_gather_ln_gmf_scaled_fwd", ptr(uid), ptr(iid), n, mfu, mfi, mfu, mfi,
+                      n_users, n_items, Dm, pp["mf_norm.weight"], pp["mf_norm.bias"],
+                      pp["mf_norm.weight"], pp["mf_norm.bias"], pp["mf_output.weight"],
+                      pp["mf_output.bias"], LN_EPS, None, 0.0, 0, ptr(w.mf_pred),
+                      ptr(sp["rows_m"][0]), ptr(sp["rows_m"][1]), ptr(w.umf), ptr(w.imf),
+                      ptr(w.err), st)
+            _lib.call("ncf_gather_ln_gmf_scaled_fwd", ptr(uid), ptr(iid), n, mlu, mli, mlu, mli,
+                      n_users, n_items, D, pp["mlp_norm.weight"], pp["mlp_norm.bias"],
+                      pp["mlp_norm.weight"], pp["mlp_norm.bias"], ptr(sp["zero_w"]),
+                      pp["mf_output.bias"], LN_EPS, None, 0.0, 0, ptr(sp["pred"]), ptr(w.xu),
+                      ptr(w.xi), None, None, ptr(w.err), st)
+        elif table_ld is not None and table_ld != D:
             if bf16 or temporal is not None:
                 raise ValueError("table_ld: fp32 tables, no temporal scaling")
             _lib.call("ncf_gather_ln_gmf_ld_fwd", ptr(uid), ptr(iid), n, *tbp, n_users, n_items, D,
@@ -557,6 +598,8 @@ class NCFEngine:
         MLP_FUSED = False forces the per-layer launches (A/B measurement, parity tests)."""
         if not self._env_mlp_fused:
             return False
+        if self.model.mf_embedding_dim != self.model.mlp_embedding_dim:
+            return False        # (its head backward reads the GMF rows at the tower's width)
         key = (D, tuple(hid))
         ok = self._mlp_ok.get(key)
         if ok is None:
@@ -806,7 +849,7 @@ class NCFEngine:
         if not fused:
             _lib.call("ncf_head_bwd", ptr(w.prob), ptr(gp), ptr(tg), ptr(w.mf_pred), ptr(w.mlp_pred),
                       ptr(w.a[-1]), n, hid[-1], ptr(m.mlp_output.weight), ptr(m.final[0].weight),
-                      ptr(w.umf), ptr(w.imf), D, ptr(m.mf_output.weight), ptr(w.da[-1]), ptr(w.dumf),
+                      ptr(w.umf), ptr(w.imf), g.Dm or D, ptr(m.mf_output.weight), ptr(w.da[-1]), ptr(w.dumf),
                       ptr(w.dimf), ptr(gv("mlp_output.weight")), ptr(gv("mlp_output.bias")),
                       ptr(gv("mf_output.weight")), ptr(gv("mf_output.bias")),
                       ptr(gv("final.0.weight")), ptr(gv("final.0.bias")), ptr(w.loss),
@@ -947,7 +990,11 @@ class NCFEngine:
             w.slots_set = True
         if table_ld is not None and table_ld != D and grad_rows is None:
             raise ValueError("table_ld: the backward takes it with grad_rows only")
-        if grad_rows is not None:
+        if w.split is not None:
+            if grad_rows is not None or fused_apply is not None or bf16:
+                raise ValueError("mf_embedding_dim != mlp_embedding_dim: the dense table schedule")
+            self._embedding_bwd_split(w, uid, iid, tbp, d_rows, st)
+        elif grad_rows is not None:
             if bf16:
                 raise ValueError("grad_rows: fp32 tables only")
             gb, ru_, ri_ = grad_rows
@@ -998,6 +1045,33 @@ class NCFEngine:
             w.run_reductions(st)
         self.pending = w
 
+    def _embedding_bwd_split(self, w, uid, iid, tbp, d_rows, st):
+        """a2/a3 backward when the collections differ in width: the segment reduce + LayerNorm
+        backward once per collection, each with its own dedup workspace (the segment layout is
+        carved per width); each run's second table pair is scratch.  The inline dedup of the
+        MLP run (above, with the slot maps) and the MF run's give the same unique-id order."""
+        m = self.model
+        n, D, Dm = w.g.n, w.g.D, w.g.Dm
+        sp = w.split
+        mfu, mlu, mfi, mli = tbp
+        _lib.call("ncf_dedup_ids", ptr(uid), ptr(iid), n, Dm, m.num_users, m.num_products,
+                  ptr(sp["uniq"][0]), ptr(sp["uniq"][1]), None, None, ptr(sp["num_unique"]),
+                  ptr(w.emb_ws_m), w.emb_ws_m.numel(), st)
+        G, sm, sl, ln = w.G, sp["rows_m"], sp["rows_l"], sp["ln"]
+        _lib.call("ncf_embedding_bwd_reduce", n, Dm, d_rows[0], d_rows[1], ptr(w.dumf),
+                  ptr(w.dumf), ptr(w.dimf), ptr(w.dimf), mfu, mfu, mfi, mfi,
+                  self.pp()["mf_norm.weight"], self.pp()["mf_norm.weight"], LN_EPS,
+                  ptr(G["mf_user"]), ptr(sm[0]), ptr(G["mf_item"]), ptr(sm[1]),
+                  ptr(sp["uniq"][0]), ptr(sp["uniq"][1]), self.gptr("mf_norm.weight"),
+                  self.gptr("mf_norm.bias"), ptr(ln[0]), ptr(ln[1]), ptr(w.emb_ws_m),
+                  w.emb_ws_m.numel(), w.red_list.address, st)
+        _lib.call("ncf_embedding_bwd_reduce", n, D, d_rows[0], d_rows[1], ptr(w.dxu), ptr(w.dxu),
+                  ptr(w.dxi), ptr(w.dxi), mlu, mlu, mli, mli, self.pp()["mlp_norm.weight"],
+                  self.pp()["mlp_norm.weight"], LN_EPS, ptr(sl[0]), ptr(G["mlp_user"]),
+                  ptr(sl[1]), ptr(G["mlp_item"]), ptr(w.uniq_u), ptr(w.uniq_i), ptr(ln[2]),
+                  ptr(ln[3]), self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"),
+                  ptr(w.emb_ws), w.emb_ws.numel(), w.red_list.address, st)
+
     def join_reductions(self):
         """The current stream waits for the side-stream reductions of the last backward."""
         if getattr(self, "_red_pending", False):
@@ -1044,8 +1118,8 @@ class NCFEngine:
         """Dense-exact Adam over the four tables using the pending compact grads."""
         w = self.pending
         tb = self.table_params()
-        D = self.model.mlp_embedding_dim
         for key, p in tb.items():
+            D = p.shape[1]       # (the MF and MLP collections may differ in width)
             if w is None and p.grad is None:
                 continue  # torch.optim.Adam skips parameters whose grad is None
             lr, b1, b2, eps, wd = hp_for(p)
@@ -1090,10 +1164,10 @@ class NCFEngine:
         if w is None:
             return
         st = _lib.stream_ptr(w.prob.device)
-        D = self.model.mlp_embedding_dim
         for key, p in self.table_params().items():
             if not p.requires_grad:
                 continue
+            D = p.shape[1]
             kind = 0 if key.endswith("user") else 1
             add = accumulate and p.grad is not None
             dst = torch.zeros_like(p) if (add or p.grad is None) else p.grad.zero_()

@@ -133,7 +133,9 @@ class _Binding:
         self.clock = torch.tensor([0, self.base_seed], dtype=torch.int64, device=dev)
         lr, betas, eps, wd = self.hp
         self.D = None
-        if SCHEDULE == "deferred":
+        # (the deferred schedule steps an MF and an MLP table as one pair of one width: with
+        # mf_embedding_dim != mlp_embedding_dim the dense per-step sweep, equally exact, runs)
+        if SCHEDULE == "deferred" and model.mf_embedding_dim == model.mlp_embedding_dim:
             self.D = DeferredTableAdam(eng, lr, betas, eps, wd, SWEEP_EVERY,
                                        moments=self.moments, clock=self.clock,
                                        overlap_sweep=deferred_mod.OVERLAP_SWEEP)

@@ -45,10 +45,12 @@ class ItemIndex:
             raise RuntimeError("ncf_amd scoring runs on the MI355X only (no CPU fallback)")
         I = model.num_products
         D = model.mf_embedding_dim
-        if D not in (16, 32, 64):
+        if D not in (16, 32, 64, 128):
             # (the scan kernels are 64 deep: narrower rows are zero-padded to 64, which leaves
-            # every dot product the D-term one; a wider D would need a second k chunk)
-            raise NotImplementedError("the scoring kernels take D = 16, 32 or 64")
+            # every dot product the D-term one; D = 128 — the C4 model — takes the fp32 scan's
+            # 128-deep form, k_collect<128>, with the fp32 threshold sample)
+            raise NotImplementedError("the scoring kernels take D = 16, 32, 64 or 128")
+        qd = max(QD, D)
         st = _lib.stream_ptr(dev)
         if items is None:
             ids = torch.arange(I, dtype=torch.int64, device=dev)
@@ -66,10 +68,10 @@ class ItemIndex:
         _lib.call("ncf_gather_rows", ptr(ids), I, ptr(table), model.num_products, D,
                   ptr(model.mf_norm.weight),
                   ptr(model.mf_norm.bias), LN_EPS, ptr(pD), ptr(err), st)
-        if D == QD:
+        if D == qd:
             self.p = pD
         else:   # zero-padded to the scan's 64-deep rows (the queries are padded alike)
-            self.p = torch.zeros(I, QD, device=dev)
+            self.p = torch.zeros(I, qd, device=dev)
             self.p[:, :D].copy_(pD)
             del pD
         # mlp_item(i): the eval forward's MLP prediction depends on the item only (M = 1)
@@ -87,7 +89,7 @@ class ItemIndex:
         self.p3 = None
         self.pmax = None   # max_i |p_i| (float bits) for the 1/2-term scan's threshold margin
         self.terms = SPLIT_TERMS   # operand terms of the split scan (with pmax; else 3)
-        if SPLIT_SCAN:
+        if SPLIT_SCAN and qd == QD:    # (the split planes and their scan are 64 deep)
             self.p3 = torch.empty(3, I, QD, dtype=torch.int16, device=dev)
             _lib.call("ncf_score_split_items", ptr(self.p), I, QD, ptr(self.p3), st)
             if SPLIT_TERMS < 3:

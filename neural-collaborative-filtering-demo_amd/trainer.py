@@ -89,6 +89,13 @@ class FusedTrainStep:
         self.model = model
         self.deferred = None
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        if model.mf_embedding_dim != model.mlp_embedding_dim:
+            # the deferred schedule steps an MF and an MLP table as one pair of one width: the
+            # dense per-step sweep (the same values) when the collections differ
+            if graph or clock or table_dtype != torch.float32:
+                raise ValueError("mf_embedding_dim != mlp_embedding_dim: fp32 tables, eager, "
+                                 "the dense table schedule")
+            deferred, clock = False, False
         self.step_count = 0
         eng = model.engine
         eng.ensure_layout()
