@@ -697,9 +697,14 @@ def c4_train(ncf, dev, warmup, steps, prime=0):
            "table_params": 2 * (U + I) * D, "hbm_peak_GB": round(mem / 1e9, 1),
            "build_s": round(build_s, 1), "final_loss": round(loss, 6),
            "finite": bool(math.isfinite(loss)),
-           "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(per.items(), key=lambda x: -x[1])},
-           "kernel_ms_per_step_sweep_not_overlapped": {
+           # per-launch kernel times: measured with the rolling sweep on the step's own stream,
+           # where a launch's event span is its own kernel's
+           "kernel_ms_per_step": {
                k: round(v, 4) for k, v in sorted(iso.items(), key=lambda x: -x[1])},
+           # the default (overlapped) step: event spans on the launching stream while the sweep
+           # runs beside it on another — the time a launch's stream waited, not its kernel time
+           "launch_span_ms_per_step_overlapped": {
+               k: round(v, 4) for k, v in sorted(per.items(), key=lambda x: -x[1])},
            "linear_ms_per_step": round(sum(v for k, v in iso.items() if k in lin), 4),
            "linear_kernels": "fused attention block + fused MLP tower (D = 128)"
            if "ncf_attn_block_fwd" in iso and ("ncf_mlp_fwd" in iso or "ncf_mlp_fwd_split" in iso)
