@@ -432,7 +432,7 @@ class DeferredTableAdam:
         dev = self.clock.device
         side = getattr(self, "_dedup_side", None)
         if side is None or side.device != dev:
-            side = self._dedup_side = torch.cuda.Stream(dev)
+            side = self._dedup_side = torch.cuda.Stream(dev, priority=SIDE_PRIORITY)
             self._dedup_evs = [_lib.RawEvent(stream_only=True) for _ in range(2)]
         cur = st
         self._dedup_evs[0].record(cur)

@@ -17,10 +17,20 @@ from ncf_amd.trainer import FusedTrainStep  # noqa: E402
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--priority", type=int, default=None,
+                    help="deferred.SIDE_PRIORITY for the side streams (default: the module's)")
+    ap.add_argument("--builds", type=int, default=16)
+    a = ap.parse_args()
+    from ncf_amd import deferred as Dm
+    if a.priority is not None:
+        Dm.SIDE_PRIORITY = a.priority
+    print(f"side stream priority {Dm.SIDE_PRIORITY}", flush=True)
     dev = torch.device("cuda", 0)
     U, I, D, B, M = 1_000_000, 100_000, 64, 4096, 5
     batches = bench.make_batches(U, I, B, M, 64, dev, seed=3)
-    for k in list(range(8)) + list(range(8)):
+    for k in [j % 8 for j in range(a.builds)]:
         held = [torch.cuda.Stream(dev) for _ in range(k)]
         torch.manual_seed(5)
         model = ncf.AdvancedNCF(U, I, 10, 50, D, D, 32, [256, 128, 64], 4, 0.2, M - 1).to(dev).train()
