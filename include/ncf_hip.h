@@ -491,6 +491,11 @@ int ncf_head_bwd(const float* prob, const float* grad_prob, const float* targets
  * mlp_norm backward.  Produces compact per-unique-id gradients and slot maps (slot[id] = c);
  * the dense [rows, D] gradient is never materialised.                                       */
 int64_t ncf_embedding_bwd_workspace(int64_t n, int64_t dim);
+/* The largest per-kind id count ncf_dedup_ids sorts in its one-launch form (bitonic sort in LDS,
+ * one workgroup per kind; larger batches take the multi-launch radix sort).  Returns the previous
+ * value; n < 0 only reads it, n is capped at 2048.  The two forms leave the same workspace
+ * contents (tested); the setter exists for that A/B.                                        */
+int64_t ncf_dedup_set_small_max(int64_t n);
 int ncf_embedding_bwd(const int64_t* user_ids, const int64_t* item_ids, int64_t n, int64_t dim,
                       int64_t num_users, int64_t num_items, const float* dy_mf_user,
                       const float* dy_mlp_user, const float* dy_mf_item, const float* dy_mlp_item,

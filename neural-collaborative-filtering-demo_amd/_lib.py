@@ -107,6 +107,7 @@ SIGNATURES = {
     "ncf_embedding_bwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, P, P, P, P, F32, P, P,
                                 P, P, P, P, P, P, P, P, P, P, P, P, I64, P]),
     "ncf_dedup_ids": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, P, P, I64, P]),
+    "ncf_dedup_set_small_max": (I64, [I64]),
     "ncf_dedup_ids2": (I32, [P, I64, I64, P, I64, I64, I64, P, P, P, P, P, P, I64, P]),
     "ncf_dedup_inverse": (I32, [I64, I64, I64, I64, I64, P, P, P, I64, P]),
     "ncf_shard_plan": (I32, [P, P, I64, I32, I64, I64, I64, P, P, I64, P, P]),

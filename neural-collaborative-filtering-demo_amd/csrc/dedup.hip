@@ -368,6 +368,131 @@ __global__ __launch_bounds__(256) void k_segments(
   }
 }
 
+// ---- small batches (every kind <= kSmallMax ids): the whole dedup in ONE launch, one workgroup
+// per kind.  The (key, position) pairs sort as 64-bit words (key << 32 | position: the stable
+// order of the radix sort, positions breaking ties) by a bitonic network in LDS, then the segment
+// and piece heads are ranked by a workgroup scan.  Every output the multi-launch path leaves in
+// the workspace (sorted pairs in the buffers its pass count ends in, segments, pieces, segment
+// offsets per sort tile, totals, uniq ids, slot maps, counts) is written with the same values.
+// The reference call pattern's batch (config.yaml:65: 256 groups of 5 = 1,280 ids) sorted in 5
+// dependent launches (a memset, keys + histograms, two radix passes, segments) took ~37 us.
+constexpr int kSmallMax = 2048;
+__global__ __launch_bounds__(1024) void k_dedup_small(
+    const int64_t* __restrict__ ids0, int64_t rows0, const int64_t* __restrict__ ids1,
+    int64_t rows1, int64_t n0, int64_t n1, int nbmax, uint32_t* __restrict__ ko0,
+    uint32_t* __restrict__ vo0, uint32_t* __restrict__ ko1, uint32_t* __restrict__ vo1,
+    uint32_t* __restrict__ segoff, uint32_t* __restrict__ start0, uint32_t* __restrict__ start1,
+    uint32_t* __restrict__ pstart0, uint32_t* __restrict__ pstart1, uint32_t* __restrict__ pseg0,
+    uint32_t* __restrict__ pseg1, uint32_t* __restrict__ fpiece0, uint32_t* __restrict__ fpiece1,
+    int64_t* __restrict__ uniq0, int64_t* __restrict__ uniq1, int32_t* __restrict__ slot0,
+    int32_t* __restrict__ slot1, uint32_t* __restrict__ totals, uint32_t* __restrict__ num_unique) {
+  __shared__ uint64_t s[kSmallMax];
+  __shared__ uint32_t wsum_s[16], wsum_p[16];
+  const int kind = blockIdx.y;
+  const int n = (int)(kind ? n1 : n0);
+  const int64_t rows = kind ? rows1 : rows0;
+  const int64_t* ids = kind ? ids1 : ids0;
+  uint32_t* ko = kind ? ko1 : ko0;
+  uint32_t* vo = kind ? vo1 : vo0;
+  uint32_t* start = kind ? start1 : start0;
+  uint32_t* pstart = kind ? pstart1 : pstart0;
+  uint32_t* pseg = kind ? pseg1 : pseg0;
+  uint32_t* fpiece = kind ? fpiece1 : fpiece0;
+  int64_t* uniq = kind ? uniq1 : uniq0;
+  int32_t* slot = kind ? slot1 : slot0;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (n == 0) {
+    if (tid == 0) {
+      if (num_unique) num_unique[kind] = 0;
+      totals[kind] = 0;
+      totals[2 + kind] = 0;
+      start[0] = 0;
+      pstart[0] = 0;
+      fpiece[0] = 0;
+    }
+    return;
+  }
+  int N2 = 2;
+  while (N2 < n) N2 <<= 1;
+  for (int i = tid; i < N2; i += 1024)
+    s[i] = i < n ? ((uint64_t)clamp_key(ids[i], rows) << 32 | (uint32_t)i) : ~0ull;
+  __syncthreads();
+  // bitonic sort, ascending: N2 / 2 compare-exchanges per stage, one per thread (N2 <= 2048)
+  for (int k = 2; k <= N2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = tid; t < (N2 >> 1); t += 1024) {
+        const int i = 2 * j * (t / j) + (t % j), l = i + j;
+        const uint64_t a = s[i], b = s[l];
+        const bool up = (i & k) == 0;
+        if ((a > b) == up) { s[i] = b; s[l] = a; }
+      }
+      __syncthreads();
+    }
+  }
+  // heads: thread tid holds sorted positions 2 tid and 2 tid + 1
+  uint32_t key[2], cs[2], cp[2];
+  bool sh[2], ph[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int i = 2 * tid + e;
+    key[e] = i < n ? (uint32_t)(s[i] >> 32) : 0u;
+    sh[e] = i < n && (i == 0 || key[e] != (uint32_t)(s[i - 1] >> 32));
+    ph[e] = i < n && (sh[e] || (i % PIECE) == 0);
+  }
+  // inclusive ranks: within the thread, the wave (ballot counts), then the earlier waves
+  const uint32_t ts = (uint32_t)sh[0] + (uint32_t)sh[1], tp = (uint32_t)ph[0] + (uint32_t)ph[1];
+  uint32_t is = ts, ip = tp;   // inclusive wave scans of the per-thread counts
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t xs = __shfl_up(is, o, 64), xp = __shfl_up(ip, o, 64);
+    if (lane >= o) { is += xs; ip += xp; }
+  }
+  if (lane == 63) { wsum_s[w] = is; wsum_p[w] = ip; }
+  __syncthreads();
+  uint32_t bs = 0, bp = 0, U = 0, Pn = 0;
+  for (int q = 0; q < 16; ++q) {
+    if (q < w) { bs += wsum_s[q]; bp += wsum_p[q]; }
+    U += wsum_s[q];
+    Pn += wsum_p[q];
+  }
+  cs[0] = bs + is - ts + (uint32_t)sh[0];   // inclusive segment count at position 2 tid
+  cs[1] = cs[0] + (uint32_t)sh[1];
+  cp[0] = bp + ip - tp + (uint32_t)ph[0];
+  cp[1] = cp[0] + (uint32_t)ph[1];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int i = 2 * tid + e;
+    if (i >= n) continue;
+    ko[i] = key[e];
+    vo[i] = (uint32_t)s[i];
+    const uint32_t c = cs[e] - 1;   // segment of position i
+    if (sh[e]) {
+      start[c] = (uint32_t)i;
+      uniq[c] = (int64_t)key[e];
+      if (slot) slot[key[e]] = (int32_t)c;
+    }
+    if (ph[e]) {
+      const uint32_t p = cp[e] - 1;
+      pstart[p] = (uint32_t)i;
+      pseg[p] = c | (sh[e] ? FIRST_PIECE : 0u);
+      if (sh[e]) fpiece[c] = p;
+    }
+    // segments starting before sort tile i / TILE (the multi-launch path's look-back offsets)
+    if (i % TILE == 0) segoff[(int64_t)kind * nbmax + i / TILE] = cs[e] - (uint32_t)sh[e];
+  }
+  if (tid == 0) {
+    totals[kind] = U;
+    totals[2 + kind] = Pn;
+    if (num_unique) num_unique[kind] = U;
+    start[U] = (uint32_t)n;
+    pstart[Pn] = (uint32_t)n;
+    fpiece[U] = Pn;
+  }
+}
+
+// the largest per-kind id count the one-launch form takes (ncf_dedup_set_small_max: A/B, tests)
+static int64_t g_small_max = kSmallMax;
+
 // inverse map of a dedup: inv[position] = compact index of its id
 __global__ __launch_bounds__(256) void k_seg_inverse(const uint32_t* __restrict__ sk0,
                                                      const uint32_t* __restrict__ sk1,
@@ -432,6 +557,16 @@ extern "C" int ncf_dedup_ids2(const int64_t* ids0, int64_t n0, int64_t rows0, co
     (void)hipMemsetAsync(w.totals, 0, 4 * sizeof(uint32_t), st);
     return NCF_OK;
   }
+  if (n <= g_small_max) {
+    uint32_t *k0, *v0, *k1, *v1;
+    sorted_bufs(w, passes, &k0, &v0, &k1, &v1);
+    hipLaunchKernelGGL(k_dedup_small, dim3(1, 2), dim3(1024), 0, st, ids0, rows0, ids1, rows1, n0,
+                       n1, w.nb, k0, v0, k1, v1, w.segoff, w.start0, w.start1, w.pstart0,
+                       w.pstart1, w.pseg0, w.pseg1, w.fpiece0, w.fpiece1, uniq0, uniq1, slot0,
+                       slot1, w.totals, num_unique);
+    NCF_CHECK_LAUNCH("ncf_dedup_ids(small)");
+    return NCF_OK;
+  }
   (void)hipMemsetAsync(workspace, 0, (size_t)w.zero_bytes(workspace, passes, bits), st);
   hipLaunchKernelGGL(k_keys_hist, dim3(w.nb, 2), dim3(256), 0, st, ids0, rows0, ids1, rows1, n0,
                      n1, bits, passes, w.ka0, w.va0, w.ka1, w.va1, w.ghist, num_unique, w.start0,
@@ -471,6 +606,12 @@ extern "C" int ncf_dedup_ids(const int64_t* user_ids, const int64_t* item_ids, i
 }
 
 extern "C" int64_t ncf_embedding_bwd_workspace(int64_t n, int64_t dim) { return ws_bytes(n, dim); }
+
+extern "C" int64_t ncf_dedup_set_small_max(int64_t n) {
+  const int64_t prev = g_small_max;
+  if (n >= 0) g_small_max = n < kSmallMax ? n : kSmallMax;
+  return prev;
+}
 
 // inv[position] = compact index, for the dedup held in `workspace` (ncf_dedup_ids2, same args)
 extern "C" int ncf_dedup_inverse(int64_t n0, int64_t n1, int64_t rows0, int64_t rows1, int64_t dim,

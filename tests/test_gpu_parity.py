@@ -1553,11 +1553,22 @@ def test_gemm_direct_and_splitk_rowsum_vs_torch(a_t, b_t, Mm, Nn, Kk):
         np.testing.assert_allclose(db.cpu().numpy(), A.double().sum(1).float().numpy(),
                                    atol=2e-5 * (Kk ** 0.5), rtol=1e-5)
 
-@pytest.mark.parametrize("n0,n1", [(1, 1), (1023, 1025), (5000, 3000), (70000, 20480), (0, 7)])
+@pytest.fixture(params=["small", "radix"])
+def dedup_form(request):
+    """The one-launch small-batch dedup (<= 2048 ids per kind) and the multi-launch radix sort."""
+    from ncf_amd import _lib
+    prev = _lib.query("ncf_dedup_set_small_max", 2048 if request.param == "small" else 0)
+    yield request.param
+    _lib.query("ncf_dedup_set_small_max", prev)
+
+
+@pytest.mark.parametrize("n0,n1", [(1, 1), (1023, 1025), (2048, 17), (5000, 3000),
+                                   (70000, 20480), (0, 7)])
 @pytest.mark.parametrize("rows0,rows1", [(1, 2000), (1 << 20, 100000), (1 << 23, 3)])
-def test_dedup_ids_vs_numpy(n0, n1, rows0, rows1):
+def test_dedup_ids_vs_numpy(n0, n1, rows0, rows1, dedup_form):
     """Onesweep radix dedup (1, 2 and 3 passes; ragged tiles; look-back over many tiles; a
-    Zipf-hot id): uniq ids == np.unique, counts, slot maps and the inverse map."""
+    Zipf-hot id) and the one-launch form for batches <= 2048 ids: uniq ids == np.unique, counts,
+    slot maps and the inverse map (which reads the sorted pairs and per-tile segment offsets)."""
     from ncf_amd import _lib
     rng = np.random.default_rng(n0 * 31 + n1 + rows0 % 97)
     ids = []
@@ -1589,6 +1600,49 @@ def test_dedup_ids_vs_numpy(n0, n1, rows0, rows1):
         s = slot[k].cpu().numpy()
         np.testing.assert_array_equal(s[u], np.arange(len(u)))
         assert (np.delete(s, u) == -1).all()
+
+
+@pytest.mark.parametrize("n,D", [(1280, 64), (40, 16), (2048, 128), (17, 64)])
+def test_dedup_small_form_bitwise_equals_radix(n, D):
+    """The one-launch small-batch dedup leaves the segments / pieces the embedding backward reads
+    exactly as the multi-launch radix sort does: the compact table gradients, the LayerNorm
+    parameter gradients, uniq ids and counts bit for bit (1,280 ids = the reference's default
+    batch, 256 groups x 5; hot ids spanning several pieces)."""
+    from ncf_amd import _lib
+    g = torch.Generator().manual_seed(n + D)
+    U, I = 1_000_000, 100_000
+    uid = torch.randint(0, U, (n // 5 + 1,), generator=g).repeat_interleave(5)[:n]
+    iid = (torch.rand(n, generator=g) ** 3 * I).long()
+    tabs = [torch.randn(r, D, generator=g).to(DEV) for r in (U, U, I, I)]
+    dys = [torch.randn(n, D, generator=g).to(DEV) for _ in range(4)]
+    gm, gl = torch.randn(D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    ud, idd = uid.to(DEV), iid.to(DEV)
+    P = lambda t: t.data_ptr()  # noqa: E731
+    st = _lib.stream_ptr(DEV)
+    res = []
+    for small in (2048, 0):
+        prev = _lib.query("ncf_dedup_set_small_max", small)
+        try:
+            ws = torch.full((_lib.query("ncf_embedding_bwd_workspace", n, D),), 0x5A,
+                            dtype=torch.uint8, device=DEV)
+            uq = [torch.full((n,), -7, dtype=torch.int64, device=DEV) for _ in range(2)]
+            nu = torch.zeros(2, dtype=torch.int32, device=DEV)
+            G = [torch.zeros(n, D, device=DEV) for _ in range(4)]
+            pg = [torch.zeros(D, device=DEV) for _ in range(4)]
+            _lib.call("ncf_dedup_ids", P(ud), P(idd), n, D, U, I, P(uq[0]), P(uq[1]), None, None,
+                      P(nu), P(ws), ws.numel(), st)
+            _lib.call("ncf_embedding_bwd_reduce", n, D, U, I, *[P(x) for x in dys],
+                      *[P(x) for x in (tabs[0], tabs[1], tabs[2], tabs[3])], P(gm), P(gl), 1e-5,
+                      *[P(x) for x in G], P(uq[0]), P(uq[1]), *[P(x) for x in pg], P(ws),
+                      ws.numel(), None, st)
+            torch.cuda.synchronize()
+        finally:
+            _lib.query("ncf_dedup_set_small_max", prev)
+        res.append((nu.cpu(), [u.cpu() for u in uq], [x.cpu() for x in G], [x.cpu() for x in pg]))
+    (n0, u0, g0, p0), (n1, u1, g1, p1) = res
+    assert torch.equal(n0, n1)
+    for a, b in zip(u0 + g0 + p0, u1 + g1 + p1):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("shapes", [
