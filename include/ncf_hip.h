@@ -605,10 +605,17 @@ int ncf_score_sample_split16(const float* queries, int64_t n_users, const uint16
                              void* stream);
 int ncf_score_kth16(const uint16_t* logits, int64_t n_users, int64_t S, int K, float* thr,
                     void* stream);
+/* A candidate of a user's list: its scan logit and item (shard-local index).  One 8-byte record
+ * per candidate, [n_users][cap] of them: a run of one user's candidates lands in one contiguous
+ * span (two 4-byte arrays put every run in two).                                             */
+typedef struct ncf_score_cand {
+  float logit;
+  int32_t item;
+} ncf_score_cand;
 int ncf_score_collect(const float* queries, const int32_t* user_list, int64_t n_users,
                       const float* items, const float* item_bias, int64_t n_items, int64_t dim,
-                      const float* thr, int64_t cap, uint32_t* count, float* cand_logit,
-                      int32_t* cand_item, void* stream);
+                      const float* thr, int64_t cap, uint32_t* count, ncf_score_cand* cand,
+                      void* stream);
 /* ncf_score_collect on the bf16 matrix cores at fp32 accuracy: every operand split into three
  * bf16 terms (24 significant bits), six products per logit accumulated in fp32.  items3: the
  * three bf16 planes [3][n_items][dim] of `items` (ncf_score_split_items).  Same candidate sets
@@ -619,8 +626,8 @@ int ncf_score_split_items(const float* items, int64_t n_items, int64_t dim, uint
 int ncf_score_collect_split(const float* queries, const int32_t* user_list, int64_t n_users,
                             const uint16_t* items3, const float* item_bias, int64_t n_items,
                             int64_t dim, const float* thr, int64_t cap, uint32_t* count,
-                            float* cand_logit, int32_t* cand_item, int terms,
-                            int64_t expected_per_user, void* stream);
+                            ncf_score_cand* cand, int terms, int64_t expected_per_user,
+                            void* stream);
 /* expected_per_user: the candidates per user the thresholds aim at (0: unknown); sizes the item
  * split so a wave's candidates fit its LDS slice (fewer, grouped global writes).
  * terms = 2: the scan takes only x0 + x1 of each operand (three products a0b0 + a0b1 + a1b0):
@@ -632,8 +639,7 @@ int ncf_score_item_norm_max(const float* items, int64_t n_items, int64_t dim, ui
 int ncf_score_margin(const float* queries, const int32_t* user_list, int64_t n_users, int64_t dim,
                      const uint32_t* item_norm_max, float c, float* thr, void* stream);
 int ncf_score_select_rescored(const int32_t* user_list, int64_t n_users, const uint32_t* count,
-                              const float* cand_logit, const int32_t* cand_item, int64_t cap,
-                              int K, const float* queries, const float* items,
+                              const ncf_score_cand* cand, int64_t cap, int K, const float* queries, const float* items,
                               const float* item_bias, int64_t dim, const uint32_t* item_norm_max,
                               float c, float* out_score, int64_t* out_item, float* thr,
                               uint32_t* overflow, const float* thr_check, void* stream);
@@ -643,7 +649,7 @@ int ncf_score_select_rescored(const int32_t* user_list, int64_t n_users, const u
  * re-scored logit is >= T; otherwise overflow[slot] = 2 and the caller re-runs the user from a
  * guaranteed threshold (the sample's K-th). */
 int ncf_score_select(const int32_t* user_list, int64_t n_users, const uint32_t* count,
-                     const float* cand_logit, const int32_t* cand_item, int64_t cap, int K,
+                     const ncf_score_cand* cand, int64_t cap, int K,
                      float* out_score, int64_t* out_item, float* thr, uint32_t* overflow,
                      void* stream);
 /* Item-sharded scoring: merge per-user lists of L = W*K (score, global item id)

@@ -171,14 +171,14 @@ SIGNATURES = {
     "ncf_score_kth": (I32, [P, I64, I64, I32, P, I64, P, P]),
     "ncf_score_sample_split16": (I32, [P, I64, P, I64, I64, I64, P, I64, I64, P, P]),
     "ncf_score_kth16": (I32, [P, I64, I64, I32, P, P]),
-    "ncf_score_collect": (I32, [P, P, I64, P, P, I64, I64, P, I64, P, P, P, P]),
+    "ncf_score_collect": (I32, [P, P, I64, P, P, I64, I64, P, I64, P, P, P]),
     "ncf_score_split_items": (I32, [P, I64, I64, P, P]),
-    "ncf_score_collect_split": (I32, [P, P, I64, P, P, I64, I64, P, I64, P, P, P, I32, I64, P]),
+    "ncf_score_collect_split": (I32, [P, P, I64, P, P, I64, I64, P, I64, P, P, I32, I64, P]),
     "ncf_score_item_norm_max": (I32, [P, I64, I64, P, P]),
     "ncf_score_margin": (I32, [P, P, I64, I64, P, F32, P, P]),
-    "ncf_score_select_rescored": (I32, [P, I64, P, P, P, I64, I32, P, P, P, I64, P, F32, P, P, P,
+    "ncf_score_select_rescored": (I32, [P, I64, P, P, I64, I32, P, P, P, I64, P, F32, P, P, P,
                                         P, P, P]),
-    "ncf_score_select": (I32, [P, I64, P, P, P, I64, I32, P, P, P, P, P]),
+    "ncf_score_select": (I32, [P, I64, P, P, I64, I32, P, P, P, P, P]),
     "ncf_score_merge": (I32, [P, P, I64, I64, I32, P, P, P]),
     "ncf_temporal_fwd": (I32, [P, P, P, P, I64, P, P, P, P, I64, I64, P, P, P]),
     "ncf_temporal_bwd": (I32, [P, P, P, I64, P, I64, P, P, P, P]),

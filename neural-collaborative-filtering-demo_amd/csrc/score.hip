@@ -374,8 +374,7 @@ __global__ __launch_bounds__(512) void k_collect(
     const float* __restrict__ q, const int32_t* __restrict__ user_list, int64_t n_users,
     const float* __restrict__ items, const float* __restrict__ bias, int64_t n_items,
     int64_t items_per_block, const float* __restrict__ thr, int64_t cap,
-    uint32_t* __restrict__ count, float* __restrict__ cand_logit,
-    int32_t* __restrict__ cand_item) {
+    uint32_t* __restrict__ count, ncf_score_cand* __restrict__ cand) {
   static_assert(D == 64 || D == 128, "the fp32 scan takes 64- or 128-deep rows");
   constexpr int KH = D / 2;      // k per lane half (MFMA step s: k = s + KH h)
   constexpr int NV = D / 64;     // float4 per thread to stage a 32 x D tile
@@ -446,10 +445,7 @@ __global__ __launch_bounds__(512) void k_collect(
     for (uint32_t e = threadIdx.x; e < m; e += blockDim.x) {
       const int32_t u = cu[e];
       const uint32_t pos = atomicAdd(&count[u], 1u);
-      if (pos < cap) {
-        cand_logit[(int64_t)u * cap + pos] = cl[e];
-        cand_item[(int64_t)u * cap + pos] = ci[e];
-      }
+      if (pos < cap) cand[(int64_t)u * cap + pos] = ncf_score_cand{cl[e], ci[e]};
     }
   };
   for (int64_t t0 = it0; t0 < it1; t0 += kItemTile) {
@@ -520,10 +516,7 @@ __global__ __launch_bounds__(512) void k_collect(
             cu[base] = (int32_t)urow[r];
           } else {   // staging full within this tile: straight to the global list
             const uint32_t pos = atomicAdd(&count[urow[r]], 1u);
-            if (pos < cap) {
-              cand_logit[urow[r] * cap + pos] = lg;
-              cand_item[urow[r] * cap + pos] = (int32_t)item;
-            }
+            if (pos < cap) cand[urow[r] * cap + pos] = ncf_score_cand{lg, (int32_t)item};
           }
           ++base;
         }
@@ -628,8 +621,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 template <int NU>
 __device__ __forceinline__ void flush_grouped(
     uint32_t staged, int64_t slot0, const int32_t* __restrict__ user_list,
-    uint32_t* __restrict__ count, int64_t cap, float* __restrict__ cand_logit,
-    int32_t* __restrict__ cand_item, const float* wl, const int32_t* wi, const uint16_t* wu,
+    uint32_t* __restrict__ count, int64_t cap, ncf_score_cand* __restrict__ cand,
+    const float* wl, const int32_t* wi, const uint16_t* wu,
     uint16_t* wr, uint16_t* wp, uint32_t* ucnt, uint32_t* uoff, uint32_t* ubase) {
   const int lane = threadIdx.x & 63;
   for (int k = lane; k < NU; k += 64) ucnt[k] = 0u;
@@ -665,8 +658,7 @@ __device__ __forceinline__ void flush_grouped(
     if (pos < cap) {
       const int64_t s = slot0 + k;
       const int64_t u = user_list ? (int64_t)user_list[s] : s;
-      cand_logit[u * cap + pos] = wl[e];
-      cand_item[u * cap + pos] = wi[e];
+      cand[u * cap + pos] = ncf_score_cand{wl[e], wi[e]};
     }
   }
   wave_lds_sync();
@@ -682,8 +674,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     const float* __restrict__ q, const int32_t* __restrict__ user_list, int64_t n_users,
     const uint16_t* __restrict__ items3, const float* __restrict__ bias, int64_t n_items,
     int64_t items_per_block, int ub, const float* __restrict__ thr, int64_t cap,
-    uint32_t* __restrict__ count, float* __restrict__ cand_logit,
-    int32_t* __restrict__ cand_item) {
+    uint32_t* __restrict__ count, ncf_score_cand* __restrict__ cand) {
   constexpr int D = 64;
   __shared__ __attribute__((aligned(16))) uint16_t ps[3][T][kItemTile][kP3];
   __shared__ float bs[3][kItemTile];
@@ -816,10 +807,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       const int64_t sl = slot0 + wu[e];
       const int64_t u = user_list ? (int64_t)user_list[sl] : sl;
       const uint32_t pos = atomicAdd(&count[u], 1u);
-      if (pos < cap) {
-        cand_logit[u * cap + pos] = wl[e];
-        cand_item[u * cap + pos] = wi[e];
-      }
+      if (pos < cap) cand[u * cap + pos] = ncf_score_cand{wl[e], wi[e]};
     }
     staged = 0;
   };
@@ -975,7 +963,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
   }
   if (staged)
-    flush_grouped<NU>(staged, slot0, user_list, count, cap, cand_logit, cand_item, wl, wi, wu, wr,
+    flush_grouped<NU>(staged, slot0, user_list, count, cap, cand, wl, wi, wu, wr,
                       wp, ucnt, uoff, ubase);
 }
 
@@ -1216,8 +1204,7 @@ __global__ __launch_bounds__(256) void k_sample16t(const float* __restrict__ q, 
 template <bool RS>
 __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user_list,
                                                 int64_t n_users, const uint32_t* __restrict__ count,
-                                                const float* __restrict__ cand_logit,
-                                                const int32_t* __restrict__ cand_item,
+                                                const ncf_score_cand* __restrict__ cand,
                                                 int64_t cap, int K, int n2K,
                                                 const float* __restrict__ q,
                                                 const float* __restrict__ items,
@@ -1239,8 +1226,7 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
   const int64_t u = user_list ? user_list[slot] : slot;
   const uint32_t c_all = count[u];
   const int nc = (int)(c_all < cap ? c_all : cap);
-  const float* cl = cand_logit + u * cap;
-  const int32_t* ci = cand_item + u * cap;
+  const ncf_score_cand* cc = cand + u * cap;   // (logit, item) records
   // block min / max of the keys of the members (key != 0) and their number
   auto key_range = [&](uint32_t& kmin, uint32_t& kmax, uint32_t& nmem) {
     kmin = 0xFFFFFFFFu; kmax = 0; nmem = 0;
@@ -1308,7 +1294,7 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
                         nb, (uint32_t)K, need, eq);
   };
   if (tid == 0) s_n = 0;
-  for (int j = tid; j < nc; j += 256) keys[j] = fkey(cl[j]);
+  for (int j = tid; j < nc; j += 256) keys[j] = fkey(cc[j].logit);
   __syncthreads();
   uint32_t kmin, kmax, nmem;
   key_range(kmin, kmax, nmem);
@@ -1329,8 +1315,9 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
       lo = va - (2.0f * e * 1.0001f + 1e-6f * fabsf(va));
     }
     for (int j = tid; j < nc; j += 256) {
-      if (cl[j] < lo) { keys[j] = 0; continue; }
-      const int64_t it = ci[j];
+      const ncf_score_cand rc = cc[j];
+      if (rc.logit < lo) { keys[j] = 0; continue; }
+      const int64_t it = rc.item;
       const float* pr = items + it * 64;
       float d = 0.0f;
 #pragma unroll
@@ -1356,14 +1343,14 @@ __global__ __launch_bounds__(256) void k_select(const int32_t* __restrict__ user
       tie_all = false;
       uint32_t need2 = 0, eq2 = 0;
       t2 = radix([&](int j) { return keys[j] == t; },
-                 [&](int j) { return 0xFFFFFFFFu - (uint32_t)ci[j]; }, 32, need, &need2, &eq2);
+                 [&](int j) { return 0xFFFFFFFFu - (uint32_t)cc[j].item; }, 32, need, &need2, &eq2);
     }
   }
   for (int j = tid; j < nc; j += 256) {
     const uint32_t k = keys[j];
     if (k == 0) continue;
     if (ne > K && k < t) continue;
-    const uint32_t nid = 0xFFFFFFFFu - (uint32_t)ci[j];
+    const uint32_t nid = 0xFFFFFFFFu - (uint32_t)cc[j].item;
     if (ne > K && k == t && !tie_all && nid < t2) continue;
     const uint32_t pos = atomicAdd(&s_n, 1u);   // (exactly min(ne, K) arrive)
     if (pos < (uint32_t)n2K) sel[pos] = ((unsigned long long)k << 32) | (unsigned long long)nid;
@@ -1578,7 +1565,7 @@ extern "C" int ncf_score_kth16(const uint16_t* logits, int64_t n_users, int64_t 
 extern "C" int ncf_score_collect(const float* queries, const int32_t* user_list, int64_t n_users,
                                  const float* items, const float* item_bias, int64_t n_items,
                                  int64_t dim, const float* thr, int64_t cap, uint32_t* count,
-                                 float* cand_logit, int32_t* cand_item, void* stream) {
+                                 ncf_score_cand* cand, void* stream) {
   NCF_CHECK_ARG(dim == 64 || dim == 128, "ncf_score_collect: dim must be 64 or 128");
   NCF_CHECK_ARG(n_users >= 0 && n_items >= 0 && n_items < (1ll << 31) && cap >= 1,
                 "ncf_score_collect: bad size");
@@ -1596,11 +1583,11 @@ extern "C" int ncf_score_collect(const float* queries, const int32_t* user_list,
   if (dim == 64)
     hipLaunchKernelGGL(k_collect<64>, dim3((unsigned)splits, (unsigned)ub), dim3(512), 0,
                        (hipStream_t)stream, queries, user_list, n_users, items, item_bias, n_items,
-                       per, thr, cap, count, cand_logit, cand_item);
+                       per, thr, cap, count, cand);
   else
     hipLaunchKernelGGL(k_collect<128>, dim3((unsigned)splits, (unsigned)ub), dim3(512), 0,
                        (hipStream_t)stream, queries, user_list, n_users, items, item_bias, n_items,
-                       per, thr, cap, count, cand_logit, cand_item);
+                       per, thr, cap, count, cand);
   NCF_CHECK_LAUNCH("ncf_score_collect");
   return NCF_OK;
 }
@@ -1648,7 +1635,7 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
                                        int64_t n_users, const uint16_t* items3,
                                        const float* item_bias, int64_t n_items, int64_t dim,
                                        const float* thr, int64_t cap, uint32_t* count,
-                                       float* cand_logit, int32_t* cand_item, int terms,
+                                       ncf_score_cand* cand, int terms,
                                        int64_t expected_per_user, void* stream) {
   NCF_CHECK_ARG(terms >= 1 && terms <= 3, "ncf_score_collect_split: terms must be 1, 2 or 3");
   NCF_CHECK_ARG(dim == 64, "ncf_score_collect_split: dim must be 64");
@@ -1715,24 +1702,21 @@ extern "C" int ncf_score_collect_split(const float* queries, const int32_t* user
   if (terms == 3)
     hipLaunchKernelGGL((k_collect3<kUB3t, kNW3, 3>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
-                       items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
-                       cand_item);
+                       items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand);
   else if (terms == 2)
     hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 2>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
-                       items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
-                       cand_item);
+                       items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand);
   else
     hipLaunchKernelGGL((k_collect3<kUB3, kNW3, 1, kScanNB>), dim3((unsigned)(splits * ub)),
                        dim3(64 * kNW3), dyn, (hipStream_t)stream, queries, user_list, n_users,
-                       items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand_logit,
-                       cand_item);
+                       items3, item_bias, n_items, per, (int)ub, thr, cap, count, cand);
   NCF_CHECK_LAUNCH("ncf_score_collect_split");
   return NCF_OK;
 }
 
 extern "C" int ncf_score_select(const int32_t* user_list, int64_t n_users, const uint32_t* count,
-                                const float* cand_logit, const int32_t* cand_item, int64_t cap,
+                                const ncf_score_cand* cand, int64_t cap,
                                 int K, float* out_score, int64_t* out_item, float* thr,
                                 uint32_t* overflow, void* stream) {
   NCF_CHECK_ARG(n_users >= 0 && K >= 1 && cap >= K && cap <= kSelectMax,
@@ -1748,7 +1732,7 @@ extern "C" int ncf_score_select(const int32_t* user_list, int64_t n_users, const
     attr = true;
   }
   hipLaunchKernelGGL(k_select<false>, dim3((unsigned)n_users), dim3(256), lds, (hipStream_t)stream,
-                     user_list, n_users, count, cand_logit, cand_item, cap, K, n2K, nullptr,
+                     user_list, n_users, count, cand, cap, K, n2K, nullptr,
                      nullptr, nullptr, nullptr, 0.0f, out_score, out_item, thr, overflow, nullptr);
   NCF_CHECK_LAUNCH("ncf_score_select");
   return NCF_OK;
@@ -1757,8 +1741,8 @@ extern "C" int ncf_score_select(const int32_t* user_list, int64_t n_users, const
 // ncf_score_select with every candidate's logit recomputed in fp32 from queries [.., 64] and
 // items [n_items, 64] + item_bias (the two-term split scan's candidates)
 extern "C" int ncf_score_select_rescored(const int32_t* user_list, int64_t n_users,
-                                         const uint32_t* count, const float* cand_logit,
-                                         const int32_t* cand_item, int64_t cap, int K,
+                                         const uint32_t* count, const ncf_score_cand* cand,
+                                         int64_t cap, int K,
                                          const float* queries, const float* items,
                                          const float* item_bias, int64_t dim,
                                          const uint32_t* item_norm_max, float c,
@@ -1780,7 +1764,7 @@ extern "C" int ncf_score_select_rescored(const int32_t* user_list, int64_t n_use
     attr = true;
   }
   hipLaunchKernelGGL(k_select<true>, dim3((unsigned)n_users), dim3(256), lds, (hipStream_t)stream,
-                     user_list, n_users, count, cand_logit, cand_item, cap, K, n2K, queries, items,
+                     user_list, n_users, count, cand, cap, K, n2K, queries, items,
                      item_bias, item_norm_max, c, out_score, out_item, thr, overflow, thr_check);
   NCF_CHECK_LAUNCH("ncf_score_select_rescored");
   return NCF_OK;

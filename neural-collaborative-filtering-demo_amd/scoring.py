@@ -127,7 +127,7 @@ def _terms(idx):
     return idx.terms if idx.pmax is not None else 3
 
 
-def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st, expected=0, terms=None):
+def _collect(idx, q, rows, n, thr, cap, count, cand, st, expected=0, terms=None):
     """ncf_score_collect(_split) of n queried users over the index's items (``expected``: the
     candidates per user the thresholds aim at, which sizes the split scan's item split;
     ``terms``: the split scan's operand terms, default the index's)."""
@@ -137,10 +137,10 @@ def _collect(idx, q, rows, n, thr, cap, count, cand_l, cand_i, st, expected=0, t
         if terms < 3:   # lower the thresholds by the scan's error bound first
             _lib.call("ncf_score_margin", q, rows, n, D, ptr(idx.pmax), MARGIN_C[terms], thr, st)
         _lib.call("ncf_score_collect_split", q, rows, n, ptr(idx.p3), ptr(idx.bias), I, D, thr,
-                  cap, count, cand_l, cand_i, terms, int(expected), st)
+                  cap, count, cand, terms, int(expected), st)
     else:
         _lib.call("ncf_score_collect", q, rows, n, ptr(idx.p), ptr(idx.bias), I, D, thr, cap,
-                  count, cand_l, cand_i, st)
+                  count, cand, st)
 
 
 # Expected candidates per user the threshold sample aims at: 512 (a bigger sample costs a
@@ -176,13 +176,11 @@ def _select(idx, rows, n, run, k, out_s, out_i, overflow, st, terms=None, check=
     two-term scan; ``terms`` as the scan's; ``check``: the rank-j thresholds to verify the
     selection against, flag 2 where it is not provably the top k)."""
     if idx.pmax is not None:
-        _lib.call("ncf_score_select_rescored", rows, n, ptr(run.count), ptr(run.cand_l),
-                  ptr(run.cand_i), run.cap, k, ptr(run.q), ptr(idx.p), ptr(idx.bias),
+        _lib.call("ncf_score_select_rescored", rows, n, ptr(run.count), ptr(run.cand), run.cap, k, ptr(run.q), ptr(idx.p), ptr(idx.bias),
                   idx.p.shape[1], ptr(idx.pmax), MARGIN_C[terms or _terms(idx)], out_s, out_i,
                   ptr(run.thr), overflow, check, st)
     else:
-        _lib.call("ncf_score_select", rows, n, ptr(run.count), ptr(run.cand_l), ptr(run.cand_i),
-                  run.cap, k, out_s, out_i, ptr(run.thr), overflow, st)
+        _lib.call("ncf_score_select", rows, n, ptr(run.count), ptr(run.cand), run.cap, k, out_s, out_i, ptr(run.thr), overflow, st)
 
 
 # Rank-j thresholds (the fp16 sample path, k > RANK_J): the threshold is the sample's j-th
@@ -259,7 +257,8 @@ class _TopKRun:
         self.sample = (torch.empty(max(n, 1), self.Sg, dtype=torch.int16, device=dev) if self.s16
                        else e(max(n, 1), self.S))
         self.count = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
-        self.cand_l, self.cand_i = e(max(n, 1), cap), e(max(n, 1), cap, dt=torch.int32)
+        # (logit f32, item i32) records, ncf_score_cand: one 8-byte store per candidate
+        self.cand = e(max(n, 1), cap, 2, dt=torch.int32)
         self.overflow = e(max(n, 1), dt=torch.int32)
         self.scores, self.items = e(n, k), e(n, k, dt=torch.int64)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -299,8 +298,8 @@ class _TopKRun:
             self.order = torch.argsort(self.thr[:n]).to(torch.int32)
             rows = ptr(self.order)
         # expected candidates per user: k x I / S (the threshold sample's k-th over S items)
-        _collect(idx, ptr(self.q), rows, n, ptr(self.thr), cap, ptr(self.count), ptr(self.cand_l),
-                 ptr(self.cand_i), st, expected=-(-self.j * I // self.S) if SIZED_SPLIT else 0)
+        _collect(idx, ptr(self.q), rows, n, ptr(self.thr), cap, ptr(self.count), ptr(self.cand),
+                 st, expected=-(-self.j * I // self.S) if SIZED_SPLIT else 0)
         _select(idx, None, n, self, k, ptr(self.scores), ptr(self.items), ptr(self.overflow), st,
                 check=None if self.thr_chk is None else ptr(self.thr_chk))
 
@@ -352,7 +351,7 @@ class _TopKRun:
             sub_i = torch.empty(rows.numel(), k, dtype=torch.int64, device=dev)
             sub_o = torch.empty(rows.numel(), dtype=torch.int32, device=dev)
             _collect(idx, ptr(self.q), ptr(rows), rows.numel(), ptr(self.thr), cap,
-                     ptr(self.count), ptr(self.cand_l), ptr(self.cand_i), st, terms=terms)
+                     ptr(self.count), ptr(self.cand), st, terms=terms)
             _select(idx, ptr(rows), rows.numel(), self, k, ptr(sub_s), ptr(sub_i), ptr(sub_o), st,
                     terms=terms)
             self.scores[redo] = sub_s
