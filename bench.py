@@ -51,7 +51,8 @@ KERNEL_SYMBOL = {"ncf_attn_block_fwd": "k_attn_block_fwd", "ncf_attn_block_bwd":
                  "ncf_mlp_fwd": "k_mlp_fwd", "ncf_mlp_bwd": "k_mlp_bwd",
                  "ncf_mlp_fwd_split": "k_mlp_fwd", "ncf_mlp_bwd_split": "k_mlp_bwd",
                  "ncf_wgrad_grouped": "k_wgrad_grouped",
-                 "ncf_attn_mlp_fwd": "k_attn_mlp_fwd", "ncf_attn_mlp_bwd": "k_attn_mlp_bwd"}
+                 "ncf_attn_mlp_fwd": "k_attn_mlp_fwd", "ncf_attn_mlp_bwd": "k_attn_mlp_bwd",
+                 "ncf_attn_mlp_fwd_small": "k_attn_mlp_fwd", "ncf_attn_mlp_bwd_small": "k_attn_mlp_bwd"}
 # the tower's Linears on bf16 matrix cores through split operands: 6 bf16 products per fp32
 # product (engine.TOWER_SPLIT); their roofline is quoted as fp32-equivalent work against the fp32
 # MFMA peak, with the executed bf16 products against the bf16 peak beside it
@@ -1129,7 +1130,9 @@ def main():
                   "ncf_mlp_bwd_split": 2.0 * mlp_f,
                   "ncf_wgrad_grouped": mlp_f,
                   "ncf_attn_mlp_fwd": 8.0 * D * D + mlp_f,
-                  "ncf_attn_mlp_bwd": 16.0 * D * D + 2.0 * mlp_f}
+                  "ncf_attn_mlp_bwd": 16.0 * D * D + 2.0 * mlp_f,
+                  "ncf_attn_mlp_fwd_small": 8.0 * D * D + mlp_f,
+                  "ncf_attn_mlp_bwd_small": 16.0 * D * D + 2.0 * mlp_f}
     gemm_names = ("ncf_gemm_direct", "ncf_gemm_f32", "ncf_gemm_rows", "ncf_gemm_f32_splitk")
     mfma = {}
     for k, f in per_sample.items():

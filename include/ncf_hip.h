@@ -414,6 +414,39 @@ int ncf_attn_mlp_bwd(int64_t groups, int64_t heads, const float* y, const ncf_ml
                      int64_t attn_workspace_floats, float* grad_xu, float* grad_xi,
                      const int64_t* user_ids, ncf_reduce_list* defer, int32_t tower_mode,
                      void* stream);
+/* Partial floats of the fused backward for `groups` groups: the tower's (which = 0) and the
+ * attention block's (which = 1) workspaces; at least ncf_mlp_bwd_workspace(5 groups) /
+ * ncf_attn_block_bwd_workspace(groups) ask for.                                              */
+int64_t ncf_attn_mlp_bwd_workspace(int64_t groups, int32_t which);
+/* The same three entry points (and the workspace query) in small-batch tiles: 3 groups (15 rows)
+ * per workgroup instead of 16 (tower_fused_small.hip).  The reference's default batch of 256
+ * groups (config.yaml:65) then fills 86 workgroups instead of 16.  Forward outputs and input
+ * gradients are the same bits as the 80-row tiles'; the weight gradients are the same sums
+ * grouped per workgroup differently (fp32 rounding).  Workspaces from
+ * ncf_attn_mlp_bwd_workspace_small (more partial sets than the 80-row tiles leave).         */
+int ncf_attn_mlp_fused_supported_small(int64_t dim, int64_t heads, int64_t group_len,
+                                       int64_t n_layers, const int64_t* hidden);
+int ncf_attn_mlp_fwd_small(const float* xu, const float* xi, int64_t groups, int64_t heads,
+                           const float* wq, const float* bq, const float* wk, const float* bk,
+                           const float* wv, const float* bv, const float* wo, const float* bo,
+                           float dropout_p, uint64_t seed, const ncf_step_clock* clock, float* q,
+                           float* k, float* v, float* probs, float* y, const int64_t* user_ids,
+                           const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
+                           float eps, const float* mlp_out_w, const float* mlp_out_b,
+                           const float* mf_pred, const float* final_w, const float* final_b,
+                           float* mlp_pred, float* prob, int32_t tower_mode, void* stream);
+int ncf_attn_mlp_bwd_small(int64_t groups, int64_t heads, const float* y,
+                           const ncf_mlp_layer* layers, int64_t n_layers, const int64_t* hidden,
+                           float dropout_p, uint64_t seed, const ncf_step_clock* clock,
+                           const ncf_head_args* head, float* tower_workspace,
+                           int64_t tower_workspace_floats, const float* q, const float* k,
+                           const float* v, const float* probs, const float* wq, const float* wk,
+                           const float* wv, const float* wo, const float* xu, const float* xi,
+                           float* const* attn_grad_params, float* attn_workspace,
+                           int64_t attn_workspace_floats, float* grad_xu, float* grad_xi,
+                           const int64_t* user_ids, ncf_reduce_list* defer, int32_t tower_mode,
+                           void* stream);
+int64_t ncf_attn_mlp_bwd_workspace_small(int64_t groups, int32_t which);
 
 /* ---- 8f rank 1: device-side training batches (data_prep.py:95-161, 181-313) --------------
  * ncf_alias_build (HOST function, once per dataset): Walker/Vose alias table of the

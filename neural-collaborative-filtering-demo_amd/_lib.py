@@ -74,6 +74,13 @@ SIGNATURES = {
                                P, P, I64, P, F32, P, P, P, P, P, P, P, I32, P]),
     "ncf_attn_mlp_bwd": (I32, [I64, I64, P, P, I64, P, F32, U64, P, P, P, I64, P, P, P, P, P, P,
                                P, P, P, P, P, P, I64, P, P, P, P, I32, P]),
+    "ncf_attn_mlp_fwd_small": (I32, [P, P, I64, I64, P, P, P, P, P, P, P, P, F32, U64, P, P, P, P, P, P,
+                               P, P, I64, P, F32, P, P, P, P, P, P, P, I32, P]),
+    "ncf_attn_mlp_bwd_small": (I32, [I64, I64, P, P, I64, P, F32, U64, P, P, P, I64, P, P, P, P, P, P,
+                               P, P, P, P, P, P, I64, P, P, P, P, I32, P]),
+    "ncf_attn_mlp_bwd_workspace": (I64, [I64, I32]),
+    "ncf_attn_mlp_bwd_workspace_small": (I64, [I64, I32]),
+    "ncf_attn_mlp_fused_supported_small": (I32, [I64, I64, I64, I64, P]),
     "ncf_alias_build": (I32, [P, I64, P, P]),
     "ncf_group_metrics_workspace": (I64, [I64, I64]),
     "ncf_group_metrics": (I32, [P, P, I64, I64, P, I64, F32, P, P, I64, P]),

@@ -37,13 +37,21 @@ namespace {
 #ifndef NCF_BWD_RING
 #define NCF_BWD_RING 4
 #endif
-constexpr int kRT = 5;                 // 16-row MFMA row tiles per workgroup
-constexpr int kRows = 16 * kRT;        // 80 rows: 256 workgroups = one per CU at 20,480 rows
+// 16-row MFMA row tiles per workgroup: 5 (80 rows: 256 workgroups = one per CU at 20,480 rows);
+// tower_fused_small.hip builds the same code with 1 (the small-batch tiles)
+#ifndef NCF_MLP_RT
+#define NCF_MLP_RT 5
+#endif
+constexpr int kRT = NCF_MLP_RT;
+constexpr int kRows = 16 * kRT;
 constexpr int kThreads = 512;          // 8 waves
 constexpr int kWaves = kThreads / 64;
 constexpr int kPQ = 260;   // pitch of buffer Q (<= 256 columns)
 constexpr int kPP = 132;   // pitch of buffer P (<= 128 columns; also the 8 x 3 x 256 scratch)
 constexpr int N0 = 256, N1 = 128, N2 = 64;
+// floats of buffer P in the backward: its rows, or the layer-0 LayerNorm backward's column-sum
+// scratch (8 waves x 3 x 256) where the tile has fewer than 47 rows
+constexpr int kPSize = kRows * kPP > kWaves * 3 * N0 ? kRows * kPP : kWaves * 3 * N0;
 // Partial-row layout per input width K0 (= D, the embedding width: 64 or 128).
 // Head partials (offsets): the flat gradient buffer's order of the head parameters, each 16-B
 // aligned: mf_output.weight [K0] @0, mf_output.bias @K0, mlp_output.weight [64] @K0+4,
@@ -1002,7 +1010,8 @@ __device__ __forceinline__ void head_bwd(float* __restrict__ G, float* __restric
 
 // dx == NULL: the input gradient stays in buffer P (rows x K0, pitch kPP) for a consumer fused
 // behind this body (the attention backward, tower_fused.hip)
-template <int K0, int MM = 0>
+// VR: the workgroup's rows (<= kRows: a tile of whole attention groups, tower_fused.hip)
+template <int K0, int MM = 0, int VR = kRows>
 __device__ __forceinline__ void mlp_bwd_body(float* __restrict__ lds, const float* __restrict__ g_last, int64_t n,
                                                       TowerArgs a, float p,
                                                       const ncf_step_clock* clock,
@@ -1010,10 +1019,11 @@ __device__ __forceinline__ void mlp_bwd_body(float* __restrict__ lds, const floa
                                                       float* __restrict__ part, ncf_head_args h,
                                                       int fused_head, float inv_n,
                                                       const float* __restrict__ xin, int fused_wgrad) {
+  static_assert(VR <= kRows, "rows per workgroup exceed the tile");
   float* Q = lds;
   float* P = lds + kRows * kPQ;
-  const int64_t row0 = (int64_t)blockIdx.x * kRows;
-  const int rows = (int)min<int64_t>(kRows, n - row0);
+  const int64_t row0 = (int64_t)blockIdx.x * VR;
+  const int rows = (int)min<int64_t>(VR, n - row0);
   const uint64_t cs = clock ? clock->seed : 0ull;
   using T = Lay<K0>;
   // MM = 3: the three dX Linears on split operands; the weight gradients stay on fp32 MFMA
@@ -1100,10 +1110,11 @@ __global__ __launch_bounds__(kThreads) void k_mlp_bwd(const float* __restrict__ 
                        fused_wgrad);
 }
 
-constexpr size_t kLds = sizeof(float) * kRows * (kPQ + kPP);
+constexpr size_t kLds = sizeof(float) * (kRows * kPQ + kPSize);
 constexpr size_t kLdsFwd = sizeof(float) * 16 * kFwdRT * (kPQ + kPP);
-static_assert(kWaves * 3 * N0 <= kRows * kPP, "ln_bwd scratch must fit in buffer P");
-static_assert(kWaves * Lay<128>::kHeadW <= kRows * kPP, "head scratch must fit in buffer P");
+static_assert(kWaves * 3 * N0 <= kPSize, "ln_bwd scratch must fit in buffer P");
+static_assert(kWaves * Lay<128>::kHeadW <= kPSize, "head scratch must fit in buffer P");
+static_assert(kWaves * 3 * N1 <= kRows * kPQ, "ln_bwd scratch of layer 1 must fit in buffer Q");
 static_assert(128 <= kPP - 4, "a 128-wide input fits buffer P");
 
 bool tower_ok(int64_t dim, int64_t n_layers, const int64_t* hidden) {

@@ -40,6 +40,11 @@ TOWER_SPLIT = False
 # rolling sweep forked before it 0.2879-0.2908, two launches each way 0.2972-0.3006 (isolated:
 # forward 57 against 22 + 42 us, backward 105-109 against 37 + 85 us).  False: two launches.
 FUSE_ATTN_TOWER = True
+# Batches of fewer interaction groups than this run the fused attention + tower in small-batch
+# tiles (ncf_attn_mlp_*_small: 3 groups = 15 rows per workgroup instead of 16 groups = 80 rows),
+# so a small batch spreads over more CUs (256 groups, the reference's default batch: 86
+# workgroups instead of 16).  0: always the 80-row tiles.
+SMALL_TILE_GROUPS = 2048
 # SURVEY fact 6 (a training group's M rows hold one user): the gather writes the LN'd user rows
 # once per group (group_rows = M) when every reader takes the group's row — the fused attention
 # block and the fused tower's head backward (False: every row; the same bits, tested; measured
@@ -133,8 +138,13 @@ class Workspace:
         sites = [("head", _lib.query("ncf_head_bwd_workspace", n, g.hidden[-1], D))]
         for l, h in enumerate(g.hidden):
             sites.append((f"relu{l}", _lib.query("ncf_relu_ln_dropout_bwd_workspace", n, h)))
-        sites.append(("mlp", _lib.query("ncf_mlp_bwd_workspace", n)))
-        sites.append(("attn", _lib.query("ncf_attn_block_bwd_workspace", g.B)))
+        mlp_ws = _lib.query("ncf_mlp_bwd_workspace", n)
+        attn_ws = _lib.query("ncf_attn_block_bwd_workspace", g.B)
+        if g.B < SMALL_TILE_GROUPS:     # (the small-batch tiles leave more partial sets)
+            mlp_ws = max(mlp_ws, _lib.query("ncf_attn_mlp_bwd_workspace_small", g.B, 0))
+            attn_ws = max(attn_ws, _lib.query("ncf_attn_mlp_bwd_workspace_small", g.B, 1))
+        sites.append(("mlp", mlp_ws))
+        sites.append(("attn", attn_ws))
         self.site_off, off = {}, 0
         for name, size in sites:
             self.site_off[name] = (off, size)
@@ -537,7 +547,7 @@ class NCFEngine:
             mode = {"ncf_mlp_fwd": 0, "ncf_mlp_fwd_bf16": 1,
                     "ncf_mlp_fwd_split": 3}[self._tower_entry("ncf_mlp_fwd", bf16)]
             a_ = "user_product_attention."
-            _lib.call("ncf_attn_mlp_fwd", ptr(w.xu), ptr(w.xi), n // M, H,
+            _lib.call("ncf_attn_mlp_fwd" + self._tiles(n // M), ptr(w.xu), ptr(w.xi), n // M, H,
                       pp[a_ + "q_proj.weight"], pp[a_ + "q_proj.bias"], pp[a_ + "k_proj.weight"],
                       pp[a_ + "k_proj.bias"], pp[a_ + "v_proj.weight"], pp[a_ + "v_proj.bias"],
                       pp[a_ + "out_proj.weight"], pp[a_ + "out_proj.bias"], drop_p, seed,
@@ -667,6 +677,12 @@ class NCFEngine:
             ok = self._mlp_ok[key] = bool(_lib.query("ncf_attn_mlp_fused_supported", D, H, M,
                                                       len(hid), ctypes.addressof(harr)))
         return ok
+
+    @staticmethod
+    def _tiles(groups: int) -> str:
+        """The fused attention + tower entry points' suffix for a batch of `groups` groups:
+        the small-batch tiles below SMALL_TILE_GROUPS."""
+        return "_small" if groups < SMALL_TILE_GROUPS else ""
 
     def attn_tower_step(self, D: int, H: int, M: int, hid) -> bool:
         """Whether a training step of this geometry runs the attention block and the tower as
@@ -885,7 +901,8 @@ class NCFEngine:
                     "ncf_mlp_bwd_split": 3}[self._tower_entry("ncf_mlp_bwd", bf16)]
             gpa = self._attn_grad_ptrs(w)
             ws = w.site("attn")
-            _lib.call("ncf_attn_mlp_bwd", n // M, H, ptr(w.y), addr, len(hid), haddr, drop_p,
+            _lib.call("ncf_attn_mlp_bwd" + self._tiles(n // M), n // M, H, ptr(w.y), addr, len(hid),
+                      haddr, drop_p,
                       seed, ptr(self.clock), ctypes.addressof(h), ptr(w.site("mlp")),
                       w.site("mlp").numel(), ptr(w.q), ptr(w.k), ptr(w.v), ptr(w.P),
                       *pp["att_w"], ptr(w.xu), ptr(w.xi), gpa, ptr(ws), ws.numel(),

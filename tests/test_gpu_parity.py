@@ -881,6 +881,7 @@ def test_attn_tower_fused_bitwise_equals_two_launches(monkeypatch, tables):
     (single-term bf16 tower)."""
     import ncf_amd.engine as E
     from ncf_amd.trainer import FusedTrainStep
+    monkeypatch.setattr(E, "SMALL_TILE_GROUPS", 0)     # (80-row tiles, as the two launches)
     U, I, B, M = 3000, 500, 61, 5
     g = torch.Generator().manual_seed(81)
     batches = []
@@ -913,6 +914,58 @@ def test_attn_tower_fused_bitwise_equals_two_launches(monkeypatch, tables):
         assert torch.equal(sa[k], sb[k]), k
     for k in ma:
         assert torch.equal(ma[k][0], mb[k][0]) and torch.equal(ma[k][1], mb[k][1]), k
+
+
+@pytest.mark.parametrize("B", [256, 61, 7])
+def test_small_batch_tiles_vs_80_row_tiles(monkeypatch, B):
+    """The fused attention + tower in small-batch tiles (tower_fused_small.hip: 3 groups = 15 rows
+    per workgroup; engine.SMALL_TILE_GROUPS) against the 80-row tiles on the same batches: the
+    forward's probabilities and the first backward's row gradients (the compact table gradients)
+    bit for bit (every row computed by the same device code), the dense gradients to fp32
+    rounding of the partial sums' grouping, and 4 training steps (dropout on, B = 256: the
+    reference's default batch, config.yaml:65; 61 and 7: ragged last workgroups) to 1e-6."""
+    import ncf_amd.engine as E
+    from ncf_amd.trainer import FusedTrainStep
+    U, I, M = 3000, 500, 5
+    g = torch.Generator().manual_seed(B)
+    batches = []
+    for _ in range(4):
+        u = torch.randint(0, U, (B,), generator=g).repeat_interleave(M)
+        i = (torch.rand(B * M, generator=g) ** 2 * I).long()
+        t = torch.zeros(B, M)
+        t[:, 0] = 1
+        batches.append((u.to(DEV), i.to(DEV), t.reshape(-1, 1).to(DEV)))
+    out = []
+    for small in (True, False):
+        monkeypatch.setattr(E, "SMALL_TILE_GROUPS", 1 << 30 if small else 0)
+        torch.manual_seed(91)
+        m = ncf.AdvancedNCF(U, I, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.2, M - 1).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+        probs, first = [], None
+        for s_, (u, i, t) in enumerate(batches):
+            w = step(u, i, t)
+            probs.append(w.prob.cpu().clone())
+            if s_ == 0:
+                torch.cuda.synchronize()
+                nu = w.num_unique.cpu().tolist()
+                first = ({k: v[:nu[0 if k.endswith("user") else 1]].cpu().clone()
+                          for k, v in w.G.items()}, m.engine.flat_grad.cpu().clone())
+        step.sync()
+        out.append((probs, first, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}))
+    (pa, (ga, fa), sa), (pb, (gb, fb), sb) = out
+    assert torch.equal(pa[0], pb[0])
+    for k in ga:
+        assert torch.equal(ga[k], gb[k]), k
+    torch.testing.assert_close(fa, fb, rtol=1e-5, atol=1e-7)
+    for x, y in zip(pa, pb):
+        torch.testing.assert_close(x, y, rtol=0, atol=1e-6)
+    # parameters: Adam's first steps are lr x sign(g), so an element whose gradient is summation
+    # noise (e.g. k_proj.bias, exactly 0 in exact arithmetic) may step either way in the two runs
+    # (at most 2 lr per step apart); every other element agrees to 1e-5
+    for k in sa:
+        d = (sa[k] - sb[k]).abs()
+        assert d.max().item() <= 4 * 2e-3 + 1e-6, k
+        assert (d > 1e-5).float().mean().item() < 0.02, k
 
 
 def test_mlp_tower_eval_matches_unfused(monkeypatch):
