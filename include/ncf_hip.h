@@ -641,10 +641,10 @@ int ncf_score_kth16(const uint16_t* logits, int64_t n_users, int64_t S, int K, f
 /* A candidate of a user's list: its scan logit and item (shard-local index).  One 8-byte record
  * per candidate, [n_users][cap] of them: a run of one user's candidates lands in one contiguous
  * span (two 4-byte arrays put every run in two).                                             */
-typedef struct ncf_score_cand {
+typedef struct __attribute__((aligned(8))) ncf_score_cand {
   float logit;
   int32_t item;
-} ncf_score_cand;
+} ncf_score_cand;   /* (8-byte aligned: one 64-bit store per candidate) */
 int ncf_score_collect(const float* queries, const int32_t* user_list, int64_t n_users,
                       const float* items, const float* item_bias, int64_t n_items, int64_t dim,
                       const float* thr, int64_t cap, uint32_t* count, ncf_score_cand* cand,
