@@ -92,14 +92,24 @@ class DeferredTableAdam:
             engine.deferred.detach()    # the previous schedule settles its lagging rows first
         self.t = 0
         self.synced_t = 0
+        self.late_skips = 0         # steps whose catch-up the previous step's late catch-up made
         self._table = torch.zeros(0, dtype=torch.float32, device=dev)
         self._filled = 0
         self._hp_filled = None      # (lr, beta1, beta2) the filled scalars were computed with
         # Overlapped rolling sweep (clock path; FusedTrainStep and the optimizer hook turn it
         # on): the sweep closing step T is launched during step T+1, after its catch-up, on a
-        # side stream, and joined before step T+1's table apply.  Rows of step T+1's batch are
-        # current by then (stamp >= T) and skipped; every other row of the slice is touched by
-        # the sweep alone.  Same arithmetic, bit-identical results (tested).
+        # side stream, and joined before the clock advance.  Rows of step T+1's batch are current
+        # by then (stamp >= T) and skipped; every other row of the slice is touched by the sweep
+        # alone.  Same arithmetic, bit-identical results (tested).
+        # Invariant that lets the table apply run before the join (trainer.FUSE_APPLY: the apply
+        # inside the embedding backward, the sweep possibly still running beside it): the sweep
+        # targets clock->t (step_rel 0) and every row of the batch was caught up to t before the
+        # fork (every engine fork point — tower, mlp_bwd, mlp_bwd_after, attn_bwd, emb_bwd,
+        # reduce — lies after engine.forward's prepare; a part whose point the step never passes
+        # is settled on the step's stream in apply(), behind the fused apply, where those rows
+        # stand at t + 1 and are skipped all the same), so the sweep skips exactly the rows
+        # the apply steps from t to t + 1: no row is stepped twice.  A fork point placed before
+        # prepare, or a sweep target past t (step_rel > 0 in sweep_fork), would break this.
         self.overlap = bool(overlap_sweep)
         if self.overlap and clock is None:
             raise ValueError("the overlapped sweep needs the device step clock")
@@ -312,7 +322,7 @@ class DeferredTableAdam:
         if _lib.PROFILE is not None:     # per-launch instrumentation times it on its stream
             with torch.cuda.stream(self._side):
                 self._rolling(side, 0, part, len(self.fork_points))
-        else:
+        else:     # (step_rel 0: the target is clock->t, which the batch's rows already reached)
             self._rolling(side, 0, part, len(self.fork_points))
         self._ev[1].record(side)
         self._owed.remove(part)
@@ -386,6 +396,7 @@ class DeferredTableAdam:
                 # step t: its catch-up would replay nothing)
                 w.late_t = None
                 self._locked = False
+                self.late_skips += 1
                 return
             pairs = self._pairs_for(w)
             # (locked: an early catch-up of the next batch may run during this step)
@@ -483,7 +494,9 @@ class DeferredTableAdam:
     def fused_apply_args(self, w):
         """The arguments of the apply fused into the embedding backward (engine.backward
         fused_apply): this step's touched rows stepped where their gradient rows complete, as
-        apply() would step them after it.  None without the device clock."""
+        apply() would step them after it.  None without the device clock.  The overlapped sweep
+        may still run beside that apply (joined later, in apply()/sweep_join): safe by the
+        invariant stated in __init__ (sweep target t <= every batch row's stamp)."""
         if self.clock is None or w.g.n == 0:
             return None
         self._ensure(self.t + 1)

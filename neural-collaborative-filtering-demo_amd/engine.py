@@ -1007,6 +1007,7 @@ class NCFEngine:
             w.slots_set = True
         if table_ld is not None and table_ld != D and grad_rows is None:
             raise ValueError("table_ld: the backward takes it with grad_rows only")
+        applied = False
         if w.split is not None:
             if grad_rows is not None or fused_apply is not None or bf16:
                 raise ValueError("mf_embedding_dim != mlp_embedding_dim: the dense table schedule")
@@ -1033,7 +1034,7 @@ class NCFEngine:
                       self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
                       w.emb_ws.numel(), w.red_list.address, pa, 1, clk, tab, b1, b2, eps_a, wd,
                       st)
-            w.applied = True
+            w.applied = applied = True
         else:
             _lib.call("ncf_embedding_bwd_reduce_bf16" if bf16 else "ncf_embedding_bwd_reduce", n,
                       D, d_rows[0], d_rows[1],
@@ -1043,7 +1044,7 @@ class NCFEngine:
                       ptr(uq_i), self.gptr("mf_norm.weight"), self.gptr("mf_norm.bias"),
                       self.gptr("mlp_norm.weight"), self.gptr("mlp_norm.bias"), ptr(w.emb_ws),
                       w.emb_ws.numel(), w.red_list.address, st)
-        if tables_done is not None:
+        if tables_done is not None and applied:    # (only behind a queued table apply)
             tables_done()
         self.join(dev, joins)
         self._sweep_fork("reduce")

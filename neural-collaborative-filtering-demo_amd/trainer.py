@@ -173,6 +173,7 @@ class FusedTrainStep:
         if drop_p > 0 and self.clock is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         prep = self.deferred.prepare if self.deferred is not None else None
+        self._late_next = None     # set by this step's prefetch (_prefetch_dedup), at the sweep fork
         w = eng.forward(user_ids, item_ids, M, True, drop_p, seed, prepare=prep,
                         tables=self.tables_lp, bf16=self.bf16)
         # (REDUCE_ASYNC: the dense-gradient reductions beside the table Adam)
@@ -180,8 +181,9 @@ class FusedTrainStep:
         side = (d.side_stream() if EARLY_REDUCE and d is not None and d.overlap and not self.graph
                 and not REDUCE_ASYNC else None)
         fa = d.fused_apply_args(w) if FUSE_APPLY and d is not None else None
-        late, self._late_next = getattr(self, "_late_next", None), None
-        done = (lambda: self._late_catchup(*late)) if late is not None and fa is not None else None
+        # (the late catch-up is read when the table apply has been queued, not here: the sweep
+        # fork, and with it the next batch's prefetch, may sit in the backward — "mlp_bwd")
+        done = self._tables_done if fa is not None else None
         eng.backward(w, user_ids, item_ids, None, targets, drop_p, seed, tables=self.tables_lp,
                      bf16=self.bf16, reduce_async=REDUCE_ASYNC and not self.graph,
                      reduce_side=side, fused_apply=fa, tables_done=done)
@@ -223,6 +225,14 @@ class FusedTrainStep:
                       ptr(self.v_flat), eng.flat.numel(), self.lr, b1, b2, self.eps, self.wd,
                       float(self.step_count + 1), st)
         return w
+
+    def _tables_done(self):
+        """Engine hook, right after the embedding backward with the table apply fused in was
+        queued: the late catch-up of the next batch's rows, if this step's prefetch sorted them
+        (at the sweep fork, in the forward or the backward) and no early catch-up ran."""
+        late, self._late_next = self._late_next, None
+        if late is not None:
+            self._late_catchup(*late)
 
     def _late_catchup(self, s, n):
         """deferred.LATE_CATCHUP: the next batch's rows (dedup set s, sorted on the side stream)

@@ -1093,24 +1093,39 @@ def test_late_catchup_bitwise_equals_dense(monkeypatch):
     """The next batch's catch-up queued behind this step's fused table apply, beside the
     dense-gradient reductions (deferred.LATE_CATCHUP), and the next step skipping its own
     catch-up, against the dense schedule bit for bit (dropout, sweep every 8 steps); and against
-    the late catch-up off, and the step's side-stream join before the flat Adam instead of after
-    it (trainer.SPLIT_CLOSE)."""
+    the late catch-up off, and the step's side-stream join after the flat Adam instead of before
+    it (trainer.SPLIT_CLOSE: apply(late_join) -> ncf_adam_flat_clock -> sweep_join -> the separate
+    clock advance).  The skip must have happened on every step but the first (deferred
+    late_skips), with the sweep forked at the default point of this geometry and in the backward
+    ("mlp_bwd": the prefetch, and the late catch-up, queued after the forward)."""
     import ncf_amd.deferred as Dm
     import ncf_amd.trainer as Tr
     monkeypatch.setattr(Tr, "FUSE_APPLY", True)
+    seen = []
+    orig = Dm.DeferredTableAdam.prepare
+
+    def prep(self, *a):
+        seen.append(self)
+        return orig(self, *a)
+    monkeypatch.setattr(Dm.DeferredTableAdam, "prepare", prep)
+
+    def run(late, **kw):
+        seen.clear()
+        monkeypatch.setattr(Dm, "LATE_CATCHUP", late)
+        out = _fused_run(True, 30, sweep_every=8, clock=True, overlap_sweep=True, pipelined=True,
+                         **kw)
+        skips = max(d.late_skips for d in seen)
+        assert (skips >= 28) if late else skips == 0, (late, kw, skips)
+        return out
     pairs = []
     for drop in (0.2, 0.0):
-        runs = []
-        for late in (True, False):
-            monkeypatch.setattr(Dm, "LATE_CATCHUP", late)
-            runs.append(_fused_run(True, 30, sweep_every=8, dropout=drop, clock=True,
-                                   overlap_sweep=True, pipelined=True))
-        pairs.append(runs)
+        pairs.append([run(late, dropout=drop) for late in (True, False)])
     pairs.append([pairs[1][0], _fused_run(False, 30)])   # (the dense schedule: no dropout)
-    monkeypatch.setattr(Dm, "LATE_CATCHUP", True)
-    monkeypatch.setattr(Tr, "SPLIT_CLOSE", False)      # the side stream joined before the flat Adam
-    pairs.append([pairs[0][0], _fused_run(True, 30, sweep_every=8, dropout=0.2, clock=True,
-                                          overlap_sweep=True, pipelined=True)])
+    monkeypatch.setattr(Tr, "SPLIT_CLOSE", True)       # the side stream joined after the flat Adam
+    pairs.append([pairs[0][0], run(True, dropout=0.2)])
+    monkeypatch.setattr(Tr, "SPLIT_CLOSE", False)
+    monkeypatch.setattr(Dm, "SWEEP_FORK", "mlp_bwd")    # the prefetch inside the backward
+    pairs.append([pairs[0][0], run(True, dropout=0.2)])
     for (b_sd, b_m), (a_sd, a_m) in pairs:
         for k in a_sd:
             assert torch.equal(a_sd[k], b_sd[k]), k
