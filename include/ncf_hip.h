@@ -176,6 +176,10 @@ typedef struct ncf_reduce_list {
   ncf_reduce_desc d[NCF_REDUCE_LIST_MAX];
 } ncf_reduce_list;
 int64_t ncf_reduce_batch_scratch(const ncf_reduce_list* list);
+/* Stage lanes of 16 bytes (four adjacent columns per lane) for descriptors whose L, stride and
+ * partial base allow it (default on; same bits either way).  on < 0 queries.  Returns the
+ * previous setting.  (Round 6: the batch's reductions' loads widened.)                       */
+int64_t ncf_reduce_set_vec(int64_t on);
 int ncf_reduce_batch(const ncf_reduce_list* list, float* scratch, int64_t scratch_floats,
                      void* stream);
 

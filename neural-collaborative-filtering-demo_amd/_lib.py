@@ -61,6 +61,7 @@ SIGNATURES = {
     "ncf_wgrad_grouped_workspace": (I64, [P, I32]),
     "ncf_wgrad_grouped": (I32, [P, I32, P, I64, P, P]),
     "ncf_reduce_batch_scratch": (I64, [P]),
+    "ncf_reduce_set_vec": (I64, [I64]),
     "ncf_reduce_batch": (I32, [P, P, I64, P]),
     "ncf_colsum_workspace": (I64, [I64, I64]),
     "ncf_colsum": (I32, [P, I64, I64, I64, P, I32, P, I64, P]),

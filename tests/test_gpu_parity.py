@@ -475,6 +475,49 @@ def test_reduce_batch_matches_inline_reduce():
         np.testing.assert_allclose(out.cpu().double().numpy(), exp.numpy(), rtol=1e-5, atol=1e-4)
 
 
+def test_reduce_batch_vec_lanes_bitwise_equal_scalar():
+    """ncf_reduce_batch with 16-byte lanes (four columns per lane, ncf_reduce_set_vec: the
+    default) against one column per lane, bit for bit: one- and two-stage descriptors (P up to
+    1000), L and stride multiples of 4 (vec) beside ones that are not (scalar in the same
+    launch), a partial base 8 bytes off a 16-byte boundary (scalar), accumulate and scale."""
+    from ncf_amd import _lib
+    g = torch.Generator().manual_seed(9)
+    specs = []
+    for j in range(27):
+        P = [1, 5, 64, 129, 256, 257, 1000, 300, 2][j % 9]
+        L = [4, 64, 300, 1024, 7, 66, 2048][j % 7]
+        stride = L + [0, 4, 1][j % 3]
+        off = 2 if j % 5 == 4 else 0
+        cols = 1 if j % 2 == 0 else L
+        specs.append((P, L, stride, off, cols, j % 3 == 0, [1.0, 0.25][j % 2]))
+    parts = [torch.randn(P * stride + off, generator=g).to(DEV) for P, L, stride, off, *_ in specs]
+    outs0 = [torch.randn(((L + cols - 1) // cols) * (cols + 2), generator=g).to(DEV)
+             for P, L, stride, off, cols, *_ in specs]
+    res = []
+    for vec in (0, 1):
+        prev = _lib.query("ncf_reduce_set_vec", vec)
+        try:
+            lst = _lib.ReduceList()
+            outs = [o.clone() for o in outs0]
+            for (P, L, stride, off, cols, acc, scale), part, out in zip(specs, parts, outs):
+                d = lst.d[lst.count]
+                d.part, d.out, d.stride, d.ldo = part.data_ptr() + 4 * off, out.data_ptr(), stride, cols + 2
+                d.L, d.cols, d.P, d.accumulate, d.scale = L, cols, P, int(acc), scale
+                lst.count += 1
+            scr = torch.empty(max(1, _lib.query("ncf_reduce_batch_scratch", lst.address)), device=DEV)
+            _lib.call("ncf_reduce_batch", lst.address, scr.data_ptr(), scr.numel(), _lib.stream_ptr(DEV))
+            torch.cuda.synchronize()
+            res.append(outs)
+        finally:
+            _lib.query("ncf_reduce_set_vec", prev)
+    for k, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), (k, specs[k])
+    P, L, stride, off, cols, acc, scale = specs[1]      # and the sums themselves
+    s = parts[1][:P * stride].view(P, stride)[:, :L].double().sum(0).cpu() * scale
+    np.testing.assert_allclose(res[1][1].cpu().double().view(-1, cols + 2)[:, :cols].reshape(-1)[:L]
+                               .numpy(), s.numpy(), rtol=1e-5, atol=1e-4)
+
+
 def test_embedding_bwd_segment_reduce():
     """Sort + segment-reduce + LN backward against a torch fp64 index_add reference, with heavy
     duplication (one id repeated 3000x), empty tables rows and 3 radix passes."""
