@@ -2,7 +2,8 @@
 resident Zipf batches) under module-constant variants, interleaved in one process so the box's
 drift hits every variant alike (GPU only).
     python tools/step_ab.py [--steps 200] [--reps 3] VARIANT [VARIANT ...]
-VARIANT: name=module.CONST:value[,module.CONST:value][,sweep:N][,env:NAME:value]  e.g.
+VARIANT: name=module.CONST:value[,module.CONST:value][,sweep:N][,env:NAME:value][,c:SETTER:v]
+(c: a C-ABI setter taking one int64, e.g. c:ncf_reduce_set_vec:0, restored after the variant)  e.g.
     base=engine.FUSE_ATTN_TOWER:1  nofuse=engine.FUSE_ATTN_TOWER:0  noearly=deferred.EARLY_CATCHUP:0
 Per variant: ms/step of each repetition and the per-entry-point ms/step of one profiled run."""
 import argparse
@@ -34,6 +35,10 @@ def parse(spec):
         if path == "prio":    # prio:P: the steps run on a stream of priority P
             kw["_prio"] = int(val)
             continue
+        if path == "c":       # c:SETTER:value (a C-ABI setter, int64 in, previous value out)
+            fn, _, v = val.partition(":")
+            kw.setdefault("_c", []).append((fn, int(v)))
+            continue
         if path == "env":     # env:NAME:value ('+' for ',' inside the value)
             k, _, v = val.partition(":")
             kw.setdefault("_env", {})[k] = v.replace("+", ",")
@@ -64,6 +69,7 @@ def main():
                 setattr(m, c, v)
             for m, c, v in sets:
                 setattr(m, c, v)
+            csaved = [(fn, _lib.query(fn, v)) for fn, v in kw.get("_c", [])]
             env = kw.get("_env", {})
             saved = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
@@ -109,6 +115,8 @@ def main():
                 torch.cuda.set_stream(torch.cuda.default_stream(dev))
             del step, model
             torch.cuda.empty_cache()
+            for fn, v in reversed(csaved):
+                _lib.query(fn, v)
     for name, _, _ in variants:
         v = sorted(res[name])
         print(f"== {name:12s} ms/step {' '.join(f'{x:.4f}' for x in res[name])}  min {v[0]:.4f}")
