@@ -16,6 +16,14 @@ the library name it).  A clean run therefore shows that no kernel on the path re
 of any buffer the path allocated.
 
 The allocations are freed (after a device synchronise) when the context exits.
+
+``poison=True`` fills every ``torch.empty`` / ``empty_like`` allocation (NaN for floating
+dtypes, 1 for integers: a valid index, so a stray read changes results instead of faulting)
+instead of leaving it uninitialised: a kernel that reads such a buffer before anything wrote it
+then sees the same values in every process, whatever ran before (fresh driver memory is usually
+zero, recycled memory holds an earlier buffer's bytes — the other way a run can depend on its
+process history).  ``poison`` may also be a predicate on the allocation site ("file.py:line") to
+poison a subset (bisection).
 """
 import contextlib
 import ctypes
@@ -108,8 +116,9 @@ def _wrap(p: int, shape, dtype, dev: int, keep: list) -> torch.Tensor:
 class GuardArena:
     """The reservations made while a ``guarded()`` context is active."""
 
-    def __init__(self, device_index: int = 0, log=None):
+    def __init__(self, device_index: int = 0, log=None, poison=False):
         self.dev = device_index
+        self.poison = poison
         # ``log``: a path; every reservation is appended to it as it is made ("va end nbytes
         # shape dtype site"), so the address of a fault names the buffer it fell behind
         self.log = open(log, "a", buffering=1) if log else None
@@ -150,20 +159,28 @@ class GuardArena:
         self.bytes += nbytes
         return (va.value + mapped - nbytes) & ~15
 
-    def tensor(self, shape, dtype) -> torch.Tensor:
+    def tensor(self, shape, dtype, uninit=False) -> torch.Tensor:
         shape = tuple(int(s) for s in shape)
         n = 1
         for s in shape:
             n *= s
         es = torch.empty(0, dtype=dtype).element_size()
         p = self.raw(n * es)
-        if self.log is not None:
+        site = "?"
+        if self.log is not None or callable(self.poison):
             import traceback
-            site = next((f"{os.path.basename(f.filename)}:{f.lineno}"
-                         for f in reversed(traceback.extract_stack()[:-1])
-                         if "guard_alloc" not in f.filename), "?")
-            self.log.write(f"{p:#x} {p + n * es:#x} {n * es} {list(shape)} {dtype} {site}\n")
-        return _wrap(p, shape, dtype, self.dev, self._keep)
+            fr = [f"{os.path.basename(f.filename)}:{f.lineno}"
+                  for f in reversed(traceback.extract_stack()[:-1])
+                  if "guard_alloc" not in f.filename]
+            site = "<".join(fr[:2]) or "?"     # (two frames: helpers allocate for their callers)
+        pois = uninit and n > 0 and (self.poison(site) if callable(self.poison) else bool(self.poison))
+        if self.log is not None:
+            self.log.write(f"{p:#x} {p + n * es:#x} {n * es} {list(shape)} {dtype} {site}"
+                           f"{' poisoned' if pois else ''}\n")
+        t = _wrap(p, shape, dtype, self.dev, self._keep)
+        if pois:
+            t.fill_(float("nan") if t.is_floating_point() else 1)
+        return t
 
     def free(self):
         torch.cuda.synchronize()
@@ -187,10 +204,10 @@ def _is_cuda(device) -> bool:
 
 
 @contextlib.contextmanager
-def guarded(device_index: int = 0, log=None):
+def guarded(device_index: int = 0, log=None, poison=False):
     """Route the package's CUDA allocations through a GuardArena while the context is active;
     yields the arena (``arena.copy(t)`` puts a caller tensor behind a guard too)."""
-    arena = GuardArena(device_index, log)
+    arena = GuardArena(device_index, log, poison)
     orig = {k: getattr(torch, k) for k in ("empty", "zeros", "ones", "full", "empty_like",
                                           "zeros_like", "ones_like")}
 
@@ -205,7 +222,7 @@ def guarded(device_index: int = 0, log=None):
         return tuple(size)
 
     def make(shape, dtype, fill):
-        t = arena.tensor(shape, dtype or torch.get_default_dtype())
+        t = arena.tensor(shape, dtype or torch.get_default_dtype(), uninit=fill is None)
         if fill is not None:
             t.fill_(fill)
         return t
