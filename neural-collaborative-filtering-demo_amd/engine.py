@@ -135,7 +135,7 @@ class Workspace:
         # red_list and run by one ncf_reduce_batch at its end, so each producing call site keeps
         # its partials in its own slice of `red_ws` until then; the weight gradients are queued
         # in `wgrads` and run as one grouped launch (wg_ws holds their slab partials).
-        sites = [("head", _lib.query("ncf_head_bwd_workspace", n, g.hidden[-1], D))]
+        sites = [("head", _lib.query("ncf_head_bwd_workspace", n, g.hidden[-1], max(D, Dm)))]
         for l, h in enumerate(g.hidden):
             sites.append((f"relu{l}", _lib.query("ncf_relu_ln_dropout_bwd_workspace", n, h)))
         mlp_ws = _lib.query("ncf_mlp_bwd_workspace", n)
