@@ -90,6 +90,12 @@ class _DLManaged(ctypes.Structure):
                 ("deleter", ctypes.c_void_p)]
 
 
+# The DLPack structs the guarded tensors were made from, for the life of the process: torch
+# reads a struct's `deleter` field when the tensor made from it dies, which can be after the
+# arena that made it is gone (a tensor kept alive by a reference cycle until a later gc pass).
+# Kept per arena only, that read hit freed memory (a segfault, or a garbage call, at the gc).
+_KEEP = []
+
 _capsule_new = ctypes.pythonapi.PyCapsule_New
 _capsule_new.restype = ctypes.py_object
 _capsule_new.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
@@ -135,7 +141,7 @@ class GuardArena:
         self.live = []                      # (va, reserved, mapped, handle)
         self.count = 0
         self.bytes = 0
-        self._keep = []                     # DLPack structs the tensors were made from
+        self._keep = _KEEP                  # DLPack structs the tensors were made from
 
     def raw(self, nbytes: int) -> int:
         """A device address whose [addr, addr + nbytes) ends <= 16 B before unmapped space."""

@@ -47,13 +47,17 @@ def run(cfg, poison, steps=6):
             bs.append((arena.copy(u.to(DEV)), arena.copy(i.to(DEV)),
                        arena.copy(t.reshape(-1, 1).to(DEV))))
         step = Tr.FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+        flags = torch.zeros(steps, dtype=torch.int32).pin_memory()
         for s, (u, i, t) in enumerate(bs):
             nxt = bs[s + 1][:2] if cfg.pipelined and s + 1 < len(bs) else None
             step(u, i, t, next=nxt)
+            flags[s:s + 1].copy_(m.engine._err, non_blocking=True)   # (no host sync)
         step.sync()
         torch.cuda.synchronize()
         eng = m.engine
         err = int(eng._err.item())
+        if err:
+            print(f"    id flag per step: {flags.tolist()}", flush=True)
         eng._err.zero_()
         eng._err_async = None
         sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}

@@ -4,7 +4,7 @@ what the memory held before (fixed by poisoning) from a cross-stream race (fixed
 event scope) from state left by an earlier run (fixed by collecting it between runs).
 
     python tools/repeat_diag.py [--k 5] [--fuse-apply 0] [--pipelined 0] MODE [MODE ...]
-MODE: plain | noguard | poison | scope0 | scope1 | gc | nosmall"""
+MODE: plain | noguard | poison | scope0 | scope1 | gc | nosmall | collect | alt"""
 import argparse
 import contextlib
 import gc
@@ -41,8 +41,12 @@ def main():
             orig = GB.guarded
             GB.guarded = lambda poison=False, **kw: _NoGuard()
         res = []
+
+        def collect(site):      # (per-allocation stack walk: slow host allocations, no poison)
+            return False
         for r in range(cfg.k):
-            out = GB.run(cfg, mode == "poison")
+            slow = mode == "collect" or (mode == "alt" and r % 2 == 0)
+            out = GB.run(cfg, collect if slow else mode == "poison")
             res.append(out)
             ok, bad, errs = GB.same(res[0], out)
             print(f"{mode} rep {r}: same_as_first {ok} err {out[2]} differ {len(bad)} {bad[:3]}",
