@@ -95,6 +95,10 @@ class _DLManaged(ctypes.Structure):
 # arena that made it is gone (a tensor kept alive by a reference cycle until a later gc pass).
 # Kept per arena only, that read hit freed memory (a segfault, or a garbage call, at the gc).
 _KEEP = []
+# Keep each reservation's virtual range reserved (unmapped) after the arena frees it, so no later
+# arena in the process is handed the same addresses: a stale pointer into a freed arena then
+# faults instead of reaching a newer buffer, and the driver never re-maps a range it just unmapped.
+HOLD_VA = os.environ.get("NCF_GUARD_HOLD_VA") == "1"
 
 _capsule_new = ctypes.pythonapi.PyCapsule_New
 _capsule_new.restype = ctypes.py_object
@@ -194,7 +198,8 @@ class GuardArena:
         for va, reserved, mapped, handle in reversed(self.live):
             h.hipMemUnmap(ctypes.c_void_p(va), ctypes.c_size_t(mapped))
             h.hipMemRelease(handle)
-            h.hipMemAddressFree(ctypes.c_void_p(va), ctypes.c_size_t(reserved))
+            if not HOLD_VA:
+                h.hipMemAddressFree(ctypes.c_void_p(va), ctypes.c_size_t(reserved))
         self.live = []
         if self.log is not None:
             self.log.close()
