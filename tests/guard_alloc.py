@@ -97,8 +97,14 @@ class _DLManaged(ctypes.Structure):
 _KEEP = []
 # Keep each reservation's virtual range reserved (unmapped) after the arena frees it, so no later
 # arena in the process is handed the same addresses: a stale pointer into a freed arena then
-# faults instead of reaching a newer buffer, and the driver never re-maps a range it just unmapped.
-HOLD_VA = os.environ.get("NCF_GUARD_HOLD_VA") == "1"
+# faults instead of reaching a newer buffer, and no range is mapped again after an unmap.
+# Measured (tools/guard_bisect.py, runs r06d-r06h): with the ranges released, the SECOND guarded
+# run of a process read wrong batch ids from its fourth step on in 7 of 7 processes (different
+# results, the gather's id flag raised), while no buffer it allocated was read before written
+# (poisoned runs are bit-identical) and with the ranges held 3 of 3 processes ran clean with no
+# fault (nothing touched a freed range): accesses through re-mapped addresses, not this package's
+# kernels, were reading other memory.  Held by default; NCF_GUARD_HOLD_VA=0 releases them.
+HOLD_VA = os.environ.get("NCF_GUARD_HOLD_VA", "1") == "1"
 
 _capsule_new = ctypes.pythonapi.PyCapsule_New
 _capsule_new.restype = ctypes.py_object
