@@ -7,7 +7,8 @@
 // 80-row chain of phases (95 us for the fused backward); in 15-row tiles it
 // runs 86, each with a fifth of the row work.  The device code is the same (attn_block_dev.h,
 // mlp_tower_dev.h compiled with these geometry constants; internal linkage per translation unit),
-// so every row's forward and input gradient are the same bits as in 80-row tiles; the weight
+// so every row's forward output is the same bits as in 80-row tiles; its input gradients agree to
+// fp32 rounding (the backward's row-tile GEMMs run over another tile count) and the weight
 // gradients sum the same rows in other per-workgroup groupings (fp32 rounding of the partials).
 #define NCF_ATTN_G64 3
 #define NCF_MLP_RT 1

@@ -4,7 +4,7 @@ what the memory held before (fixed by poisoning) from a cross-stream race (fixed
 event scope) from state left by an earlier run (fixed by collecting it between runs).
 
     python tools/repeat_diag.py [--k 5] [--fuse-apply 0] [--pipelined 0] MODE [MODE ...]
-MODE: plain | noguard | poison | scope0 | scope1 | gc | nosmall | collect | alt"""
+MODE: plain | noguard | poison | scope0 | scope1 | gc | nosmall | collect | alt | noguard_ec"""
 import argparse
 import contextlib
 import gc
@@ -37,7 +37,7 @@ def main():
             _lib.STREAM_EVENT_SCOPE = 1
         if mode == "nosmall":
             _lib.query("ncf_dedup_set_small_max", 0)
-        if mode == "noguard":
+        if mode in ("noguard", "noguard_ec"):
             orig = GB.guarded
             GB.guarded = lambda poison=False, **kw: _NoGuard()
         res = []
@@ -51,13 +51,22 @@ def main():
             ok, bad, errs = GB.same(res[0], out)
             print(f"{mode} rep {r}: same_as_first {ok} err {out[2]} differ {len(bad)} {bad[:3]}",
                   flush=True)
-            if mode == "gc":
+            if mode in ("gc", "noguard_ec"):
                 gc.collect()
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
+            if mode == "noguard_ec":
+                # a large allocation freed back to the driver between runs (test_gpu_c4's full-size
+                # tables do this before the parity tests): the next run's segments may be handed
+                # addresses that were mapped to other memory
+                big = torch.empty(int(8e9), dtype=torch.uint8, device="cuda")
+                big.fill_(7)
+                del big
                 torch.cuda.synchronize()
                 torch.cuda.empty_cache()
         _lib.STREAM_EVENT_SCOPE = scope0
         _lib.query("ncf_dedup_set_small_max", small0)
-        if mode == "noguard":
+        if mode in ("noguard", "noguard_ec"):
             GB.guarded = orig
 
 
