@@ -241,7 +241,8 @@ def test_split_widths_fused_step_equals_reference_call_pattern():
     for k in out[0]:
         d = (out[1][k] - out[0][k]).abs()
         assert d.max().item() <= 3 * 2e-3 + 1e-6, (k, d.max().item())
-        assert (d > 1e-6).float().mean().item() < 0.01, (k, (d > 1e-6).float().mean().item())
+        # (k_proj.bias: its exact gradient is 0 — softmax ignores a per-query constant)
+        assert (d > 1e-6).sum().item() <= max(2, 0.01 * d.numel()), (k, (d > 1e-6).sum().item())
 
 
 def test_forward_simple_train_mode_vs_oracle():
