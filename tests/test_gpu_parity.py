@@ -22,6 +22,19 @@ from ncf_amd import deferred as _D  # noqa: E402
 from ncf_amd import engine as _E  # noqa: E402
 DEV = torch.device("cuda:0")
 
+# Tests that hold two code paths to the same bits where one of them runs the fused attention +
+# tower: both sides in its 80-row tiles (the small-batch tiles, engine.SMALL_TILE_GROUPS, round the
+# input gradients differently: test_small_batch_tiles_vs_80_row_tiles compares the two forms)
+_EIGHTY_ROW_TILES = {"test_attn_block_recompute_bitwise_equals_stash",
+                     "test_attn_o_recompute_bitwise_equals_o_stash",
+                     "test_attn_shared_q_matches_per_row"}
+
+
+@pytest.fixture(autouse=True)
+def _eighty_row_tiles(request, monkeypatch):
+    if request.node.originalname in _EIGHTY_ROW_TILES:
+        monkeypatch.setattr(_E, "SMALL_TILE_GROUPS", 0)
+
 
 def kjt(u, i):
     u = torch.as_tensor(u, dtype=torch.long)
