@@ -43,8 +43,10 @@ FUSE_ATTN_TOWER = True
 # Batches of fewer interaction groups than this run the fused attention + tower in small-batch
 # tiles (ncf_attn_mlp_*_small: 3 groups = 15 rows per workgroup instead of 16 groups = 80 rows),
 # so a small batch spreads over more CUs (256 groups, the reference's default batch: 86
-# workgroups instead of 16).  0: always the 80-row tiles.
-SMALL_TILE_GROUPS = 2048
+# workgroups instead of 16).  0: always the 80-row tiles.  Up to 768 groups (256 small
+# workgroups, one per CU) the small tiles win; measured C2 steps (ms, small / 80-row tiles, run
+# r06j/r06c): 256 groups 0.1657 / 0.2084, 768 groups 0.1827 / 0.2078, 1536 groups 0.2848 / 0.2209.
+SMALL_TILE_GROUPS = 3 * 256 + 1
 # SURVEY fact 6 (a training group's M rows hold one user): the gather writes the LN'd user rows
 # once per group (group_rows = M) when every reader takes the group's row — the fused attention
 # block and the fused tower's head backward (False: every row; the same bits, tested; measured
