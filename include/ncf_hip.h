@@ -40,6 +40,10 @@ typedef struct ncf_step_clock {
 } ncf_step_clock;
 int ncf_step_clock_advance(ncf_step_clock* clock, uint64_t base_seed, void* stream);
 
+/* One wavefront waiting `microseconds` (<= 1e6) of wall-clock time on `stream`: the overlap
+ * probe of a step's side streams (two spins on two streams finish in about one span when the
+ * streams reach the GPU through different hardware queues).                                   */
+int ncf_stream_spin(int64_t microseconds, void* stream);
 int ncf_version(void);
 const char* ncf_last_error(void);
 int ncf_device_count(void);

@@ -96,3 +96,29 @@ extern "C" int ncf_memcpy_async(void* dst, const void* src, int64_t bytes, void*
   if (r != hipSuccess) { ncf_set_error("hipMemcpyAsync: %s", hipGetErrorString(r)); return NCF_ERR_LAUNCH; }
   return NCF_OK;
 }
+
+// A one-wavefront kernel that waits `microseconds` of wall-clock time on `stream` (the
+// side-stream overlap probe: two of them on two streams finish in about one span when the
+// streams reach the GPU through different hardware queues, in two when they share one).
+// Every wave leaves once the span has passed (bounded by the argument check: at most 1 s).
+__global__ void k_stream_spin(int64_t ticks) {
+  const int64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+extern "C" int ncf_stream_spin(int64_t microseconds, void* stream) {
+  NCF_CHECK_ARG(microseconds >= 0 && microseconds <= 1000000,
+                "ncf_stream_spin: microseconds in [0, 1e6]");
+  static int rate_khz = 0;
+  if (rate_khz <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+        rate_khz <= 0)
+      rate_khz = 100000;   // (the 100 MHz constant clock of CDNA3/4)
+  }
+  const int64_t ticks = microseconds * (int64_t)rate_khz / 1000;
+  hipLaunchKernelGGL(k_stream_spin, dim3(1), dim3(64), 0, (hipStream_t)stream, ticks);
+  NCF_CHECK_LAUNCH("ncf_stream_spin");
+  return NCF_OK;
+}

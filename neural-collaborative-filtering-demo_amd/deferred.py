@@ -134,6 +134,8 @@ class DeferredTableAdam:
         self._ev = None
         self._joined = True
         engine.deferred = self
+        if self.overlap and not torch.cuda.is_current_stream_capturing():
+            self.side_stream()     # (picked and checked here, outside any stream capture)
 
     @staticmethod
     def _default_fork(engine):
@@ -330,8 +332,8 @@ class DeferredTableAdam:
 
     def side_stream(self):
         """The overlapped sweep's stream (created on first use)."""
-        if self._side is None:
-            self._side = torch.cuda.Stream(self.clock.device, priority=SIDE_PRIORITY)
+        if self._side is None:     # (one that runs beside the step's stream: _lib.side_stream)
+            self._side = _lib.side_stream(self.clock.device, SIDE_PRIORITY)
             self._ev = (_lib.RawEvent(stream_only=True), _lib.RawEvent(stream_only=True))
         return self._side
 
@@ -443,7 +445,7 @@ class DeferredTableAdam:
         dev = self.clock.device
         side = getattr(self, "_dedup_side", None)
         if side is None or side.device != dev:
-            side = self._dedup_side = torch.cuda.Stream(dev, priority=SIDE_PRIORITY)
+            side = self._dedup_side = _lib.side_stream(dev, SIDE_PRIORITY)
             self._dedup_evs = [_lib.RawEvent(stream_only=True) for _ in range(2)]
         cur = st
         self._dedup_evs[0].record(cur)

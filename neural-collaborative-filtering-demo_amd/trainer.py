@@ -294,7 +294,7 @@ class FusedTrainStep:
             self._pending = (uid, iid, None)
             return
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(eng.flat.device)
+            self._side = _lib.side_stream(eng.flat.device)
         side = self._side
         entry.wait(side.cuda_stream)
         self._enqueue_dedup(s, w, uid, iid, side)

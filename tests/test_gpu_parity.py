@@ -2753,3 +2753,23 @@ def test_adam_flat_clock_close_equals_two_launches():
     for a, b in ((ps[0], ps[1]), (ms[0], ms[1]), (vs[0], vs[1]), (clocks[0], clocks[1])):
         assert torch.equal(a, b)
     assert int(clocks[1][0].item()) == 4          # t = 4, reserved (high word) = 0
+
+
+def test_side_streams_run_beside_the_step():
+    """the deferred schedule's side stream (the overlapped sweep, the next
+    batch's sort, the late catch-up) runs beside the step's stream whichever streams the process
+    took from torch's pool before the step was built (GPU_MAX_HW_QUEUES = 4: a pool stream can
+    share the step's hardware queue; _lib.side_stream probes and skips those), and the probe
+    itself tells a shared queue apart (a stream with itself serialises)."""
+    from ncf_amd import _lib
+    from ncf_amd.trainer import FusedTrainStep
+    main = torch.cuda.current_stream(DEV)
+    assert not _lib.streams_overlap(main, main)          # one queue: two spans, not one
+    for k in range(8):
+        held = [torch.cuda.Stream(DEV) for _ in range(k)]
+        torch.manual_seed(5)
+        m = ncf.AdvancedNCF(300, 200, 5, 24, 64, 64, 32, [256, 128, 64], 4, 0.2, 4).to(DEV)
+        step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5)
+        assert step.deferred is not None and step.deferred.overlap
+        assert _lib.streams_overlap(step.deferred._side, main), k
+        del step, m, held
