@@ -60,7 +60,7 @@ SPLIT_PRODUCTS = 6
 SPLIT_NAMES = ("ncf_mlp_fwd_split", "ncf_mlp_bwd_split")
 
 
-PMC_SUMMARIES = ("r05f_c5_pmc_traffic.json", "r05f_pmc_traffic.json")   # (run r05f, final HEAD)
+PMC_SUMMARIES = ("r06_c5_pmc_traffic.json", "r06_pmc_traffic.json")   # (run r06k)
 
 
 def pmc_traffic(kernel):
