@@ -55,17 +55,21 @@ struct WS {
 static inline int nb_of(int64_t n) { return n == 0 ? 1 : ncf_cdiv(n, TILE); }
 static inline int64_t pieces_max(int64_t n) { return n + n / PIECE + 2; }
 static inline int64_t extras_max(int64_t n) { return n / PIECE + 2; }
-#ifndef NCF_PIECE_WAVES
-#define NCF_PIECE_WAVES 8
-#endif
 // piece-reduce blocks: NCF_PIECE_WAVES waves, each reducing 64 / (D/4) pieces at a time (one per
-// group of D/4 lanes)
+// group of D/4 lanes).  4-wave blocks: the fused-apply reduce holds 164 VGPRs (3 waves per SIMD),
+// so 8-wave blocks left one block (8 waves) per CU and 4-wave blocks fit three (12 waves); capped
+// at 768 blocks (three per CU, grid-stride beyond) so the dgamma/dbeta partial rows stay as few as
+// with 8-wave blocks.  C2, interleaved A/B (r06m, r06n): the reduce + fused apply 42.1-42.9 ->
+// 36.7-37.5 us, the batch's reductions +0.7 us.
+#ifndef NCF_PIECE_WAVES
+#define NCF_PIECE_WAVES 4
+#endif
 static inline int nbr_of(int64_t n, int64_t D) {
   const int64_t per = (int64_t)NCF_PIECE_WAVES * (D >= 256 ? 1 : 256 / D);
   int64_t b = (pieces_max(n) + per - 1) / per;
   if (b < 1) b = 1;
 #ifndef NCF_PIECE_BLOCKS_MAX
-#define NCF_PIECE_BLOCKS_MAX 2048
+#define NCF_PIECE_BLOCKS_MAX 768
 #endif
   if (b > NCF_PIECE_BLOCKS_MAX) b = NCF_PIECE_BLOCKS_MAX;
   return (int)b;
