@@ -523,6 +523,15 @@ def dropin_train(ncf, dev, cfg, batches, warmup, steps, prime=0):
     run(prime + warmup + steps, n_item, item=True)
     torch.cuda.synchronize()
     dt_item = time.perf_counter() - t1
+    # the same loop with the backward on the calling thread (what ncf_amd.trainer.Trainer's
+    # train_epoch does: torch.autograd.set_multithreading_enabled(False) around the epoch)
+    with torch.autograd.set_multithreading_enabled(False):
+        run(prime + warmup + steps + n_item, 20)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        run(prime + warmup + steps + n_item + 20, steps)
+        torch.cuda.synchronize()
+        dt_ct = time.perf_counter() - t2
     # per-phase breakdown (a separate region: host perf_counter around each call of the loop,
     # and a torch event on the current stream at each phase boundary).  host_us: the Python
     # call's duration; gpu_us: stream time from the phase's first enqueued work to its last
@@ -531,7 +540,7 @@ def dropin_train(ncf, dev, cfg, batches, warmup, steps, prime=0):
     nb = min(steps, 50)
     host = {k: 0.0 for k in phases}
     evs = []
-    first = prime + warmup + steps + n_item
+    first = prime + warmup + steps + n_item + 20 + steps
     torch.cuda.synchronize()
     for s_ in range(first, first + nb):
         f, t = feats[s_ % len(feats)]
@@ -572,6 +581,11 @@ def dropin_train(ncf, dev, cfg, batches, warmup, steps, prime=0):
                                              and b.D is not None else None),
            "schedule": "deferred" if b is not None and b.D is not None else "dense",
            "final_loss": round(float(loss.detach()), 6),
+           "calling_thread_backward": {"ms_per_step": round(dt_ct / steps * 1e3, 4),
+                                       "value": round(B * M * steps / dt_ct, 1), "steps": steps,
+                                       "note": "the same loop under torch.autograd."
+                                               "set_multithreading_enabled(False), as "
+                                               "ncf_amd.trainer.Trainer.train_epoch runs it"},
            "with_loss_item": {"ms_per_step": round(dt_item / n_item * 1e3, 4),
                               "value": round(B * M * n_item / dt_item, 1), "steps": n_item,
                               "note": "plus loss.item() every batch (trainer.py:289)"},
@@ -1287,6 +1301,8 @@ def main():
         dropin = dropin_train(ncf, dev, (U, I, D, T, H, hid, B, M), batches, args.warmup,
                               args.steps, prime)
         dropin["vs_fused_step"] = round(dropin["value"] / samples_s, 4)
+        ct = dropin["calling_thread_backward"]
+        ct["vs_fused_step"] = round(ct["value"] / samples_s, 4)
 
     bf16 = None
     if not sharded:

@@ -65,6 +65,12 @@ SWEEP_EVERY = 128
 # (3 interleaved runs each, 0.2706 / 0.2714 against 0.2706 / 0.2707 ms/step: the separate
 # clock-advance launch costs what the later join saves)
 SPLIT_CLOSE = False
+# Trainer.train_epoch runs loss.backward() on the calling thread (torch's autograd otherwise hands
+# every backward of CUDA tensors to a per-device worker thread and waits for it: two thread
+# wake-ups per step, on a host that is the bottleneck of this loop).  The reference loop at C2
+# (tools/dropin_host.py, run r06p): 0.368 -> 0.317 ms/step.  Scoped to the epoch (the
+# torch.autograd.set_multithreading_enabled context manager); the numbers are the same bits.
+CALLING_THREAD_BACKWARD = True
 
 
 class FusedTrainStep:
@@ -536,6 +542,10 @@ class ModelTrainer:
         end of the epoch (the reference reads it, and three accuracies, with .item() every
         batch for its progress bar: four host syncs per step)."""
         self.model.train()
+        with torch.autograd.set_multithreading_enabled(not CALLING_THREAD_BACKWARD):
+            return self._train_epoch(train_loader)
+
+    def _train_epoch(self, train_loader) -> float:
         total_loss, num_batches = None, 0
         for batch_idx, (features, targets) in enumerate(train_loader):
             base_batch_size = len(features.lengths()) // len(features.keys())
