@@ -628,7 +628,10 @@ class HipShardOps:
         self.token = 0
         self.cnts = [torch.zeros(2, dtype=torch.int32, device=self.dev) for _ in range(2)]
         self.cnt = self.cnts[0]
-        self.plan_stream = torch.cuda.Stream(self.dev)
+        # (one that runs beside the step's stream: _lib.side_stream probes the pool's streams
+        # for a hardware queue of their own — with the plan on the step's queue the world-1
+        # step took 0.453-0.461 ms instead of 0.33, run r06q)
+        self.plan_stream = _lib.side_stream(self.dev)
         if self.deferred.overlap and SWEEP_ON_PLAN:
             # the overlapped sweep on the plan's stream, not a stream of its own: world 1,
             # ms/step (interleaved, 3 runs each): sweep serial 0.378-0.385, overlapped on its

@@ -260,7 +260,7 @@ class NCFEngine:
         if not self.concurrent:   # serial: "side streams" are the current stream itself
             return [torch.cuda.current_stream(dev)] * k
         if self._side is None or self._side[0].device != dev:
-            self._side = [torch.cuda.Stream(dev) for _ in range(2)]
+            self._side = [_lib.side_stream(dev) for _ in range(2)]
             self._events = [torch.cuda.Event() for _ in range(16)]
         cur = torch.cuda.current_stream(dev)
         ev = self._next_event()
@@ -1052,7 +1052,7 @@ class NCFEngine:
         self._sweep_fork("reduce")
         if reduce_async:
             if getattr(self, "_red_side", None) is None:
-                self._red_side = torch.cuda.Stream(dev)
+                self._red_side = _lib.side_stream(dev)
                 self._red_ev = (torch.cuda.Event(), torch.cuda.Event())
             side = self._red_side
             self._red_ev[0].record()
