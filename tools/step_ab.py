@@ -46,7 +46,13 @@ def parse(spec):
         mod, _, const = path.rpartition(".")
         m = importlib.import_module("ncf_amd." + mod)
         old = getattr(m, const)
-        sets.append((m, const, type(old)(int(val)) if isinstance(old, (bool, int)) else type(old)(val)))
+        if isinstance(old, (bool, int)):
+            v = type(old)(int(val))
+        elif old is None or isinstance(old, str):    # ('+' for ',' inside a string value)
+            v = val.replace("+", ",")
+        else:
+            v = type(old)(val)
+        sets.append((m, const, v))
     return name, sets, kw
 
 
