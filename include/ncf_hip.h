@@ -44,6 +44,10 @@ int ncf_step_clock_advance(ncf_step_clock* clock, uint64_t base_seed, void* stre
  * probe of a step's side streams (two spins on two streams finish in about one span when the
  * streams reach the GPU through different hardware queues).                                   */
 int ncf_stream_spin(int64_t microseconds, void* stream);
+/* A stream restricted to `keep_per8` of every 8 compute units (hipExtStreamCreateWithCUMask;
+ * its own hardware queue), and its destruction.  Side-stream placement knob.                   */
+int ncf_stream_create_cu_mask(int32_t keep_per8, void** out);
+int ncf_stream_destroy(void* stream);
 int ncf_version(void);
 const char* ncf_last_error(void);
 int ncf_device_count(void);

@@ -63,6 +63,8 @@ SIGNATURES = {
     "ncf_reduce_batch_scratch": (I64, [P]),
     "ncf_reduce_set_vec": (I64, [I64]),
     "ncf_stream_spin": (I32, [I64, P]),
+    "ncf_stream_create_cu_mask": (I32, [I32, P]),
+    "ncf_stream_destroy": (I32, [P]),
     "ncf_reduce_batch": (I32, [P, P, I64, P]),
     "ncf_colsum_workspace": (I64, [I64, I64]),
     "ncf_colsum": (I32, [P, I64, I64, I64, P, I32, P, I64, P]),
@@ -547,6 +549,21 @@ def streams_overlap(side, main, us: int = 400) -> bool:
 
 # Side streams tried before giving up on one that runs beside the step's stream
 SIDE_STREAM_TRIES = 8
+
+
+_MASKED = []     # CU-masked streams made here (alive for the process)
+
+
+def masked_stream(device, keep_per8: int):
+    """A torch stream (ExternalStream) whose kernels use `keep_per8` of every 8 CUs."""
+    out = ctypes.c_void_p()
+    lib = _lib if _lib is not None else load()
+    with torch.cuda.device(device):
+        check(lib.ncf_stream_create_cu_mask(int(keep_per8), ctypes.byref(out)),
+              "ncf_stream_create_cu_mask")
+    s = torch.cuda.ExternalStream(out.value, device=device)
+    _MASKED.append(s)
+    return s
 
 
 def side_stream(device, priority: int = 0, main=None):

@@ -122,3 +122,41 @@ extern "C" int ncf_stream_spin(int64_t microseconds, void* stream) {
   NCF_CHECK_LAUNCH("ncf_stream_spin");
   return NCF_OK;
 }
+
+// A stream whose kernels run only on `keep_per8` of every 8 compute units (the CUs whose index
+// mod 8 is below it; hipExtStreamCreateWithCUMask): side work such as the rolling table sweep
+// then leaves the other CUs to the step's kernels (A/B knob, deferred.SIDE_CU_KEEP).  A
+// CU-masked stream gets a hardware queue of its own.  Destroy with ncf_stream_destroy.
+extern "C" int ncf_stream_create_cu_mask(int32_t keep_per8, void** out) {
+  NCF_CHECK_ARG(out && keep_per8 >= 1 && keep_per8 <= 8, "ncf_stream_create_cu_mask: bad args");
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) {
+    ncf_set_error("ncf_stream_create_cu_mask: no CU count");
+    return NCF_ERR_LAUNCH;
+  }
+  uint32_t mask[32] = {0};
+  const int words = (n + 31) / 32;
+  NCF_CHECK_ARG(words <= 32, "ncf_stream_create_cu_mask: more than 1024 CUs");
+  for (int i = 0; i < n; ++i)
+    if (i % 8 < keep_per8) mask[i / 32] |= 1u << (i % 32);
+  hipStream_t s = nullptr;
+  const hipError_t r = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
+  if (r != hipSuccess) {
+    ncf_set_error("hipExtStreamCreateWithCUMask: %s", hipGetErrorString(r));
+    return NCF_ERR_LAUNCH;
+  }
+  *out = (void*)s;
+  return NCF_OK;
+}
+
+extern "C" int ncf_stream_destroy(void* stream) {
+  if (!stream) return NCF_OK;
+  const hipError_t r = hipStreamDestroy((hipStream_t)stream);
+  if (r != hipSuccess) {
+    ncf_set_error("hipStreamDestroy: %s", hipGetErrorString(r));
+    return NCF_ERR_LAUNCH;
+  }
+  return NCF_OK;
+}

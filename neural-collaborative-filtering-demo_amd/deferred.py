@@ -56,6 +56,9 @@ LATE_CATCHUP = True
 # HIP stream priority of the overlapped sweep's side stream (torch.cuda.Stream priority: 0 the
 # default, -1 high)
 SIDE_PRIORITY = 0
+# The side stream's kernels on `SIDE_CU_KEEP` of every 8 CUs (a CU-masked stream, its own
+# hardware queue); 0: a pool stream on every CU (the default, _lib.side_stream)
+SIDE_CU_KEEP = 0
 # The overlapped rolling sweep (below) for FusedTrainStep and the optimizer hook: on (False: the
 # sweep on the step's own stream)
 OVERLAP_SWEEP = True
@@ -333,7 +336,8 @@ class DeferredTableAdam:
     def side_stream(self):
         """The overlapped sweep's stream (created on first use)."""
         if self._side is None:     # (one that runs beside the step's stream: _lib.side_stream)
-            self._side = _lib.side_stream(self.clock.device, SIDE_PRIORITY)
+            self._side = (_lib.masked_stream(self.clock.device, SIDE_CU_KEEP) if SIDE_CU_KEEP
+                          else _lib.side_stream(self.clock.device, SIDE_PRIORITY))
             self._ev = (_lib.RawEvent(stream_only=True), _lib.RawEvent(stream_only=True))
         return self._side
 
