@@ -23,15 +23,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pipe", action="store_true", help="pipelined dedup (next=, the bench's form)")
     ap.add_argument("--groups", type=int, default=4096, help="B (256: the reference's batch)")
+    ap.add_argument("--graph", action="store_true", help="FusedTrainStep(graph=True): hipGraph replay")
     a = ap.parse_args()
     dev = torch.device("cuda")
     U, I, B, M = 1_000_000, 100_000, a.groups, 5
     torch.manual_seed(0)
     model = ncf.AdvancedNCF(U, I, 10, 50).to(dev).train()
-    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5)
+    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, graph=a.graph)
     batches = bench.make_batches(U, I, B, M, 8, dev, seed=5)
     def one(s):
-        if a.pipe:
+        if a.pipe and not a.graph:
             step(*batches[s % 8], next=batches[(s + 1) % 8][:2])
         else:
             step(*batches[s % 8])
