@@ -47,6 +47,9 @@ int ncf_stream_spin(int64_t microseconds, void* stream);
 /* A stream restricted to `keep_per8` of every 8 compute units (hipExtStreamCreateWithCUMask;
  * its own hardware queue), and its destruction.  Side-stream placement knob.                   */
 int ncf_stream_create_cu_mask(int32_t keep_per8, void** out);
+/* Blocks per CU the rolling table sweep launches at most (grid-stride beyond; default 16).
+ * per_cu <= 0 queries.  Returns the previous value.  (A/B: the overlapped sweep's footprint.) */
+int64_t ncf_adam_sweep_set_blocks(int64_t per_cu);
 int ncf_stream_destroy(void* stream);
 int ncf_version(void);
 const char* ncf_last_error(void);

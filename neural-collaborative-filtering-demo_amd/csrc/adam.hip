@@ -737,16 +737,22 @@ int pairs_apply_gsum_d(PairArgs a, int n, const uint32_t* count, int64_t max_n, 
   return NCF_OK;
 }
 
+// blocks per CU (x 256) the rolling sweep launches at most, per kind (grid-stride beyond): the
+// sweep shares the CUs with the step's kernels when it is overlapped (A/B knob,
+// ncf_adam_sweep_set_blocks)
+int64_t g_sweep_blocks_per_cu = 16;
+
 template <int D>
 int pairs_sweep_d(PairArgs a, int n, int32_t every, int32_t rel, const ncf_step_clock* clock,
                   const float* table, AdamScalars s, hipStream_t st, int part = 0, int nparts = 1) {
   int64_t slice = 0;
   for (int k = 0; k < n; ++k) slice = max(slice, (a.rows[k] + every - 1) / every);
   slice = (slice + nparts - 1) / nparts;
+  const int gx = (int)min((int64_t)grid_for(slice * Replay<D>::LPR), 256 * g_sweep_blocks_per_cu);
   if (a.bf)
-    hipLaunchKernelGGL((k_pairs_sweep<D, true>), dim3(grid_for(slice * Replay<D>::LPR), n), dim3(256), 0, st, a, every, rel, clock, table, s, part, nparts);
+    hipLaunchKernelGGL((k_pairs_sweep<D, true>), dim3(gx, n), dim3(256), 0, st, a, every, rel, clock, table, s, part, nparts);
   else
-    hipLaunchKernelGGL((k_pairs_sweep<D, false>), dim3(grid_for(slice * Replay<D>::LPR), n), dim3(256), 0, st, a, every, rel, clock, table, s, part, nparts);
+    hipLaunchKernelGGL((k_pairs_sweep<D, false>), dim3(gx, n), dim3(256), 0, st, a, every, rel, clock, table, s, part, nparts);
   NCF_CHECK_LAUNCH("ncf_adam_pairs_sweep_rolling");
   return NCF_OK;
 }
@@ -1063,4 +1069,10 @@ extern "C" int ncf_adam_pairs_sweep_rolling_part(const ncf_table_pair* pairs, in
   NCF_DISPATCH_DIM(dim, pairs_sweep_d, pair_args(pairs, npairs), npairs, sweep_every, step_rel,
                    clock, step_table, consts_of(beta1, beta2, eps, weight_decay),
                    (hipStream_t)stream, part, nparts);
+}
+
+extern "C" int64_t ncf_adam_sweep_set_blocks(int64_t per_cu) {
+  const int64_t prev = g_sweep_blocks_per_cu;
+  if (per_cu > 0) g_sweep_blocks_per_cu = per_cu < 64 ? per_cu : 64;
+  return prev;
 }
