@@ -505,6 +505,12 @@ int ncf_temporal_bwd(const int64_t* hour, const int64_t* day, const int64_t* mon
 /* ---- a7: MLP tower row ops (ReLU -> LayerNorm -> Dropout), architecture.py:233-239 --------
  * Backward also returns grad_bias = column sums of grad_lin (the bias gradient of the Linear
  * that feeds the ReLU; nullable).                                                            */
+/* out[r, c] = x[r, c] * keep-scale of (r, c / group) from the package's dropout stream (seed);
+ * the keep-scales optionally to scales[rows][cols / group].  group = 1: nn.Dropout per element;
+ * group = head dim: attention-weight dropout over a single key (CategoryHierarchy in training
+ * mode, architecture.py:45-51, 114-117).  In place allowed.                                    */
+int ncf_dropout_rows(const float* x, int64_t rows, int64_t cols, int64_t group, float dropout_p,
+                     uint64_t seed, float* out, float* scales, void* stream);
 int ncf_relu_ln_dropout_fwd(float* relu_in, int64_t n, int64_t width, const float* gamma,
                             const float* beta, float eps, float dropout_p, uint64_t seed,
                             const ncf_step_clock* clock, float* out, float* mean, float* rstd,

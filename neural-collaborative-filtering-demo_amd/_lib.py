@@ -66,6 +66,7 @@ SIGNATURES = {
     "ncf_stream_create_cu_mask": (I32, [I32, P]),
     "ncf_stream_destroy": (I32, [P]),
     "ncf_adam_sweep_set_blocks": (I64, [I64]),
+    "ncf_dropout_rows": (I32, [P, I64, I64, I64, F32, U64, P, P, P]),
     "ncf_reduce_batch": (I32, [P, P, I64, P]),
     "ncf_colsum_workspace": (I64, [I64, I64]),
     "ncf_colsum": (I32, [P, I64, I64, I64, P, I32, P, I64, P]),

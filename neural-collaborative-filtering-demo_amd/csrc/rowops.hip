@@ -246,3 +246,34 @@ extern "C" int ncf_relu_ln_dropout_bwd(const float* grad_out, const float* relu_
   NCF_DISPATCH_W(width, bwd_w, grad_out, relu_in, mean, rstd, gamma, n, dropout_p, seed, clock, grad_lin,
                  grad_gamma, grad_beta, grad_bias, workspace, defer, (hipStream_t)stream);
 }
+
+// out[r, c] = x[r, c] * keep-scale of mask element (r, c / group) (nn.Dropout with the package's
+// dropout stream: ncf_dropout_scale of index r * (cols / group) + c / group); the keep-scales
+// optionally to scales[r, c / group].  group = 1: per element; group = head dim: one decision per
+// (row, head) — attention-weight dropout over a single key (CategoryHierarchy's MultiHeadAttention
+// on [n, D] inputs: the softmax over one key is 1, architecture.py:45-51).  In place allowed.
+__global__ void k_dropout_rows(const float* x, int64_t rows, int64_t cols, int64_t group, float p,
+                               uint64_t seed, float inv_keep, float* out, float* scales) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int64_t r = i / cols, c = i % cols, per = cols / group;
+  const int64_t m = r * per + c / group;
+  const float s = ncf_dropout_scale(seed, (uint64_t)m, p, inv_keep);
+  out[i] = x[i] * s;
+  if (scales && c % group == 0) scales[m] = s;
+}
+
+extern "C" int ncf_dropout_rows(const float* x, int64_t rows, int64_t cols, int64_t group,
+                                float dropout_p, uint64_t seed, float* out, float* scales,
+                                void* stream) {
+  NCF_CHECK_ARG(x && out && rows >= 0 && cols >= 1 && group >= 1 && cols % group == 0,
+                "ncf_dropout_rows: bad args (cols a multiple of group)");
+  NCF_CHECK_ARG(dropout_p >= 0.0f && dropout_p < 1.0f, "ncf_dropout_rows: dropout_p out of [0,1)");
+  const int64_t n = rows * cols;
+  if (n == 0) return NCF_OK;
+  hipLaunchKernelGGL(k_dropout_rows, dim3((unsigned)ncf_cdiv(n, 256)), dim3(256), 0,
+                     (hipStream_t)stream, x, rows, cols, group, dropout_p, seed,
+                     1.0f / (1.0f - dropout_p), out, scales);
+  NCF_CHECK_LAUNCH("ncf_dropout_rows");
+  return NCF_OK;
+}

@@ -157,8 +157,10 @@ def category_hierarchy_forward(mod, department_ids, category_ids):
     if torch.is_grad_enabled() and w.requires_grad:
         with torch.no_grad():
             return category_hierarchy_forward(mod, department_ids, category_ids)
-    if mod.training and mod.dropout.p > 0:
-        raise NotImplementedError("CategoryHierarchy in training mode is not on the accelerated path")
+    p_attn = float(mod.hierarchy_attn.dropout.p) if mod.training else 0.0
+    p_out = float(mod.dropout.p) if mod.training else 0.0
+    if p_attn > 0 or p_out > 0:
+        return _category_hierarchy_train(mod, department_ids, category_ids, p_attn, p_out)
     dev = w.device
     dept_ids = department_ids.reshape(-1).to(device=dev, dtype=torch.int64)
     cat_ids = category_ids.reshape(-1).to(device=dev, dtype=torch.int64)
@@ -177,6 +179,46 @@ def category_hierarchy_forward(mod, department_ids, category_ids):
     mean, rstd = torch.empty(n * n, device=dev), torch.empty(n * n, device=dev)
     _lib.call("ncf_relu_ln_dropout_fwd", ptr(h), n * n, D, ptr(mod.norm.weight), ptr(mod.norm.bias),
               LN_EPS, 0.0, 0, None, ptr(out), ptr(mean), ptr(rstd), _lib.stream_ptr(dev))
+    return out.view(n, n, D)
+
+
+def _category_hierarchy_train(mod, department_ids, category_ids, p_attn, p_out, seed=None,
+                              scales=None):
+    """CategoryHierarchy.forward in training mode (architecture.py:111-119 with its dropouts
+    active): the attention over one key has weight 1, which the attention's nn.Dropout (:51)
+    keeps (x 1/(1-p)) or drops per (row, head); out_proj; the module's nn.Dropout (:117) per
+    element; then the broadcast residual + LayerNorm of the eval path.  Masks come from the
+    package's dropout stream (`seed`, fresh per call like forward()'s); ``scales`` (a dict) receives
+    the keep-scales ("attn" [n, H], "out" [n, D]) for tests.  No autograd (as the eval path)."""
+    w = mod.department_embed.weight
+    dev = w.device
+    dept_ids = department_ids.reshape(-1).to(device=dev, dtype=torch.int64)
+    cat_ids = category_ids.reshape(-1).to(device=dev, dtype=torch.int64)
+    n = dept_ids.numel()
+    att = mod.hierarchy_attn
+    D = w.shape[1]
+    H = att.num_heads
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    st = _lib.stream_ptr(dev)
+    dept = gather_rows(w, dept_ids)
+    v = torch.empty(n, D, device=dev)
+    _gemm(dept, D, 0, att.v_proj.weight, D, 1, v, D, n, D, D, att.v_proj.bias)
+    sa = torch.empty(n, H, device=dev) if scales is not None else None
+    _lib.call("ncf_dropout_rows", ptr(v), n, D, D // H, p_attn, seed, ptr(v), ptr(sa), st)
+    a = torch.empty(n, D, device=dev)
+    _gemm(v, D, 0, att.out_proj.weight, D, 1, a, D, n, D, D, att.out_proj.bias)
+    so = torch.empty(n, D, device=dev) if scales is not None else None
+    _lib.call("ncf_dropout_rows", ptr(a), n, D, 1, p_out, seed ^ 0x5DEECE66D, ptr(a), ptr(so), st)
+    if scales is not None:
+        scales["attn"], scales["out"] = sa, so
+    a_idx = torch.arange(n, device=dev).repeat_interleave(n)      # row a*n+b <- a[a] + cat[b]
+    h = gather_rows(mod.category_embed.weight, cat_ids.repeat(n))
+    h += gather_rows(a, a_idx)
+    out = torch.empty(n * n, D, device=dev)
+    mean, rstd = torch.empty(n * n, device=dev), torch.empty(n * n, device=dev)
+    _lib.call("ncf_relu_ln_dropout_fwd", ptr(h), n * n, D, ptr(mod.norm.weight), ptr(mod.norm.bias),
+              LN_EPS, 0.0, 0, None, ptr(out), ptr(mean), ptr(rstd), st)
     return out.view(n, n, D)
 
 

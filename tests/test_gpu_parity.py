@@ -427,6 +427,53 @@ def test_f5_scoring_and_embeddings(f5):
     np.testing.assert_allclose(pe["category"].cpu().numpy(), f5["emb_item_category"], atol=1e-5)
 
 
+def test_category_hierarchy_train_mode_vs_oracle(f5):
+    """CategoryHierarchy.forward in training mode (architecture.py:111-119, its two nn.Dropouts
+    active; the drop-in used to refuse it): against a float64 restatement of the reference
+    module on the F5 model's department / category tables with the kernel's own keep-scales
+    (the attention weight over the single key: one keep-or-drop per (row, head); the output:
+    one per element), fresh masks per call, keep fractions near 1 - p, and p = 0 equal to eval."""
+    from ncf_amd import ops
+    sd = T(sub(f5, "sd/"))
+    nu = sd["mf_embedding_collection.embedding_bags.user_id.weight"].shape[0]
+    m = ncf.AdvancedNCF(nu, 366, 5, 24, dropout=0.3).to(DEV)
+    m.load_state_dict(sd, strict=True)
+    ch = m.category_hierarchy.train()
+    g = torch.Generator().manual_seed(3)
+    n = 48
+    dept = torch.randint(0, 5, (n,), generator=g)
+    cat = torch.randint(0, 24, (n,), generator=g)
+    scales = {}
+    with torch.no_grad():
+        out = ops._category_hierarchy_train(ch, dept.to(DEV), cat.to(DEV), 0.3, 0.3, seed=77,
+                                            scales=scales)
+    D = ch.department_embed.weight.shape[1]
+    H = ch.hierarchy_attn.num_heads
+    P = {k: v.detach().cpu().double() for k, v in ch.state_dict().items()}
+    sa, so = scales["attn"].cpu().double(), scales["out"].cpu().double()
+    v = P["department_embed.weight"][dept] @ P["hierarchy_attn.v_proj.weight"].T + \
+        P["hierarchy_attn.v_proj.bias"]                                  # softmax over 1 key = 1
+    v = (v.view(n, H, D // H) * sa[:, :, None]).reshape(n, D)           # attention dropout (:51)
+    a = (v @ P["hierarchy_attn.out_proj.weight"].T + P["hierarchy_attn.out_proj.bias"]) * so
+    h = a[:, None, :] + P["category_embed.weight"][cat][None, :, :]     # [n,1,D] + [n,D] (:119)
+    ref = torch.nn.functional.layer_norm(h, (D,), P["norm.weight"], P["norm.bias"], 1e-5)
+    np.testing.assert_allclose(out.cpu().double().numpy(), ref.numpy(), atol=2e-5, rtol=1e-5)
+    for x, cnt in ((sa, n * H), (so, n * D)):
+        assert all(abs(u) < 1e-9 or abs(u - 1 / 0.7) < 1e-5 for u in x.unique().tolist())
+        keep = (x > 0).double().mean().item()
+        assert abs(keep - 0.7) < 4 * (0.21 / cnt) ** 0.5 + 0.01, keep
+    # the public module: runs in training mode, fresh masks per call; p = 0 is the eval output
+    with torch.no_grad():
+        y1 = ch(dept.to(DEV), cat.to(DEV))
+        y2 = ch(dept.to(DEV), cat.to(DEV))
+        assert y1.shape == (n, n, D) and not torch.equal(y1, y2)
+        ch.eval()
+        ye = ch(dept.to(DEV), cat.to(DEV))
+        ch.train()
+        z = ops._category_hierarchy_train(ch, dept.to(DEV), cat.to(DEV), 0.0, 0.0, seed=5)
+    torch.testing.assert_close(z, ye, rtol=1e-6, atol=2e-6)
+
+
 # ----------------------------------------------------------------------------- kernels vs torch
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("Mm,Nn,Kk", [(77, 130, 45), (256, 64, 1000), (1, 5, 3)])
