@@ -286,9 +286,11 @@ class AdvancedNCF(nn.Module):
         reference's temporal variant, including its fresh random projection per call."""
         if hour is not None:
             from .ops import forward_simple_hour
-            if self.training and float(self.dropout) > 0:
-                raise NotImplementedError("forward_simple in training mode (dropout active) is "
-                                          "not part of the accelerated path; call model.eval()")
+            if (self.training and torch.is_grad_enabled()
+                    and any(p.requires_grad for p in self.parameters())):
+                # (its forward runs in training mode, dropout included, under torch.no_grad())
+                raise NotImplementedError("forward_simple(hour=...) has no backward on the "
+                                          "accelerated path; call it under torch.no_grad()")
             return forward_simple_hour(self, user_ids, product_ids, hour)
         eng = self._engine
         if self.training and torch.is_grad_enabled():

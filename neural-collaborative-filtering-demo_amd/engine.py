@@ -595,8 +595,10 @@ class NCFEngine:
             ldw = lin.weight.shape[1]
             self._gemm(x, ldx, 0, lin.weight, ldw, 1, w.r[l], h, n, h, kin, bias=lin.bias,
                        relu=True, st=st)
+            # (forward_simple(hour) in training mode passes its dropout here with train=False)
             _lib.call("ncf_relu_ln_dropout_fwd", ptr(w.r[l]), n, h, ptr(ln.weight), ptr(ln.bias),
-                      LN_EPS, drop_p if train else 0.0, (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1),
+                      LN_EPS, drop_p if train or temporal is not None else 0.0,
+                      (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1),
                       ptr(self.clock), ptr(w.a[l]), ptr(w.mean[l]), ptr(w.rstd[l]), st)
             x, ldx, kin = w.a[l], h, h
         # a8: mlp_output + final Linear(2,1) + Sigmoid (architecture.py:345, 353-354)
@@ -728,6 +730,11 @@ class NCFEngine:
             # softmax over a single key is exactly 1 -> the core returns V unchanged
             self._gemm(w.xi, D, 0, att.v_proj.weight, D, 1, w.v, D, n, D, D, bias=att.v_proj.bias, st=st)
             src = w.v
+            if temporal is not None and drop_p > 0:
+                # forward_simple(hour) in training mode: the attention's nn.Dropout on that
+                # weight of 1 (architecture.py:51): kept (x 1/(1-p)) or dropped per (row, head)
+                _lib.call("ncf_dropout_rows", ptr(w.v), n, D, D // H, drop_p, seed, ptr(w.v),
+                          None, st)
         else:
             side = self.fork(dev, 2)
             for sd, (X, lin, Y) in zip(side, ((w.xu, att.q_proj, w.q), (w.xi, att.k_proj, w.k))):

@@ -222,7 +222,7 @@ def _category_hierarchy_train(mod, department_ids, category_ids, p_attn, p_out, 
     return out.view(n, n, D)
 
 
-def forward_simple_hour(model, user_ids, product_ids, hour, projection=None):
+def forward_simple_hour(model, user_ids, product_ids, hour, projection=None, seed=None):
     """AdvancedNCF.forward_simple(user_ids, product_ids, hour) (architecture.py:409-485).
 
     te = hour_E[hour] (TemporalEncoding.hour_embed, :434); when temporal_dim != D the reference
@@ -248,6 +248,12 @@ def forward_simple_hour(model, user_ids, product_ids, hour, projection=None):
                   m.mf_embedding_dim, ptr(b_p), 0, _lib.stream_ptr(dev))
     else:
         tp = te
-    w = eng.forward(user_ids, product_ids, 1, False, 0.0, 0, temporal=(tp, 0.3, te))
+    # training mode (the reference's nn.Dropout layers active, :458-473): the attention's
+    # dropout on its single-key weight and the tower's after every LayerNorm, from the package's
+    # dropout stream (a fresh seed per call unless given); no backward through this path
+    drop_p = float(m.dropout) if m.training else 0.0
+    if drop_p > 0 and seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    w = eng.forward(user_ids, product_ids, 1, False, drop_p, seed or 0, temporal=(tp, 0.3, te))
     eng.check_ids(w)
     return w.prob.clone()

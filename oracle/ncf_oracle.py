@@ -122,11 +122,12 @@ def forward_simple(p, user_ids, product_ids, *, num_heads, temporal_dim, n_layer
 
 
 def forward_simple_hour(p, user_ids, product_ids, hour, proj_w, proj_b, *, num_heads,
-                        n_layers) -> Tensor:
+                        n_layers, attn_drop=None, mlp_masks=None) -> Tensor:
     """AdvancedNCF.forward_simple(hour=h) (architecture.py:409-485).  The reference builds a
     fresh nn.Linear(T, D) inside the call when T != D (:437-442); its weights are inputs here.
     Item rows of both paths are scaled by (1 + 0.3 * proj(hour_E[h])) (:444, :456-458); the MLP
-    input is [attention ‖ hour_E[h]] (:467-468)."""
+    input is [attention ‖ hour_E[h]] (:467-468).  Training mode: ``attn_drop`` = the keep-scales of
+    the attention weights ([B, H, 1, 1], :51) and ``mlp_masks`` those of the tower's dropouts."""
     te = p["temporal_encoding.hour_embed.weight"][hour]
     D = p[K_MF_U].shape[1]
     tp = linear(te, proj_w, proj_b) if te.shape[1] != D else te
@@ -137,8 +138,9 @@ def forward_simple_hour(p, user_ids, product_ids, hour, proj_w, proj_b, *, num_h
     g, b = p["mlp_norm.weight"], p["mlp_norm.bias"]
     u_mlp = layer_norm(p[K_MLP_U][user_ids], g, b)
     i_mlp = layer_norm(p[K_MLP_I][product_ids], g, b) * (1 + 0.3 * tp)
-    att = mha(p, ATT, u_mlp[:, None], i_mlp[:, None], i_mlp[:, None], num_heads)[:, 0]
-    h = mlp_tower(p, torch.cat([att, te], 1), n_layers)
+    att = mha(p, ATT, u_mlp[:, None], i_mlp[:, None], i_mlp[:, None], num_heads,
+              drop_mask=attn_drop)[:, 0]
+    h = mlp_tower(p, torch.cat([att, te], 1), n_layers, masks=mlp_masks)
     mlp_pred = linear(h, p["mlp_output.weight"], p["mlp_output.bias"])
     z = linear(torch.cat([mf_pred, mlp_pred], 1), p["final.0.weight"], p["final.0.bias"])
     return torch.sigmoid(z).squeeze(-1)

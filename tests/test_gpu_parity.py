@@ -2399,6 +2399,52 @@ def test_f6_forward_simple_hour(f5, f6):
     np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), atol=2e-6)
 
 
+def test_forward_simple_hour_train_mode_vs_oracle(f5):
+    """forward_simple(hour=h) in training mode (the reference's dropouts active, architecture.py:
+    458-473; the drop-in used to refuse it): under torch.no_grad() against the oracle with the
+    kernels' own keep-scales (the attention's single-key weight per (row, head); the tower's per
+    element after each LayerNorm), recovered from ncf_dropout_rows on the same dropout stream;
+    fresh masks per call; with gradients enabled it refuses (no backward on this path)."""
+    from ncf_amd import _lib
+    from ncf_amd.ops import forward_simple_hour
+    from oracle import ncf_oracle as O
+    sd = T(sub(f5, "sd/"))
+    nu = sd["mf_embedding_collection.embedding_bags.user_id.weight"].shape[0]
+    m = ncf.AdvancedNCF(nu, 366, 5, 24, dropout=0.25).to(DEV)
+    m.load_state_dict(sd, strict=True)
+    m.train()
+    n, H, D, hid = 366, 4, 64, [256, 128, 64]
+    items = torch.arange(n, device=DEV)
+    u, h = torch.full_like(items, 2), torch.full_like(items, 7)
+    g = torch.Generator().manual_seed(4)
+    pw, pb = torch.randn(D, 32, generator=g) * 0.1, torch.randn(D, generator=g) * 0.1
+    seed = 12345
+
+    def keep(cols, group, sd_):
+        s_ = torch.empty(n, cols // group, device=DEV)
+        o_ = torch.empty(n, cols, device=DEV)
+        x_ = torch.ones(n, cols, device=DEV)
+        _lib.call("ncf_dropout_rows", x_.data_ptr(), n, cols, group, 0.25, sd_, o_.data_ptr(),
+                  s_.data_ptr(), _lib.stream_ptr(DEV))
+        return s_.cpu()
+    with torch.no_grad():
+        got = forward_simple_hour(m, u, items, h, projection=(pw, pb), seed=seed)
+        again = forward_simple_hour(m, u, items, h, projection=(pw, pb), seed=seed)
+        other = forward_simple_hour(m, u, items, h, projection=(pw, pb), seed=seed + 1)
+        sa = keep(D, D // H, seed).view(n, H, 1, 1)
+        ms = [keep(w_, 1, (seed + 0x9E37 * (l + 1)) & (2 ** 63 - 1)) for l, w_ in enumerate(hid)]
+        with pytest.raises(NotImplementedError):
+            with torch.enable_grad():
+                m.forward_simple(u, items, h)
+        fresh = m.forward_simple(u, items, h)
+    assert torch.equal(got, again) and not torch.equal(got, other) and not torch.equal(got, fresh)
+    p = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ref = O.forward_simple_hour(p, u.cpu(), items.cpu(), h.cpu(), pw, pb, num_heads=H, n_layers=3,
+                                attn_drop=sa, mlp_masks=ms)
+    np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), atol=2e-6)
+    assert ((sa == 0).float().mean() - 0.25).abs() < 0.06
+
+
 # ----------------------------------------------------------------------------- 8f: negatives
 def _sampler_case():
     """40 products; users with histories of 0..5 items, one with 38 of 40 (the fallback path is
