@@ -136,6 +136,10 @@ class DeferredTableAdam:
         self._side = None
         self._ev = None
         self._joined = True
+        # a late catch-up left running past its step (trainer.LATE_DETACHED): the event the next
+        # user of the tables waits for (late_join), and the clock copy it reads its target from
+        self._late_ev = None
+        self._late_clock = None
         engine.deferred = self
         if self.overlap and not torch.cuda.is_current_stream_capturing():
             self.side_stream()     # (picked and checked here, outside any stream capture)
@@ -346,6 +350,14 @@ class DeferredTableAdam:
         it) is what the step's sweep join waits for."""
         self._ev[1].record(stream)
 
+    def late_join(self, st=None):
+        """Stream st (default: the current stream) waits for a late catch-up that was left
+        running past the step that queued it (trainer.LATE_DETACHED): before anything on st
+        reads or steps table rows again (the next prepare, a flush, a sync)."""
+        ev, self._late_ev = self._late_ev, None
+        if ev is not None:
+            ev.wait(st if st is not None else _lib.stream_ptr(self.clock.device))
+
     def sweep_join(self):
         """The current stream waits for the side-stream sweep (before the step's apply and the
         clock advance that would change the sweep's target under it)."""
@@ -363,6 +375,7 @@ class DeferredTableAdam:
     def flush(self, st):
         """Settle any owed / in-flight sweep on the current stream (before full sweeps or
         anything that reads the tables from the host side)."""
+        self.late_join(st)
         self.sweep_join()
         self._settle(st)
 
@@ -385,6 +398,7 @@ class DeferredTableAdam:
         eng = self.engine
         m = eng.model
         n = w.g.n
+        self.late_join(st)
         if (CLAIM_CATCHUP and self.clock is not None and n > 0 and not getattr(w, "prededuped", None)
                 and not torch.cuda.is_current_stream_capturing()):
             self._prepare_claim(w, uid, iid, st)
@@ -471,18 +485,18 @@ class DeferredTableAdam:
         self._catchup_next(rows, n, stream)
         return True
 
-    def late_catchup(self, rows, n, stream):
+    def late_catchup(self, rows, n, stream, clock=None):
         """The next batch's unique rows (a dedup set, as early_catchup) caught up through the
         step now running, on `stream`, which must be ordered after this step's table apply (the
         apply fused into the embedding backward) and its sweep; the set is marked, so the next
         step's prepare skips its catch-up.  The caller joins `stream` before the clock advance."""
         if self.clock is None or n <= 0:
             return False
-        self._catchup_next(rows, n, stream)
+        self._catchup_next(rows, n, stream, clock)
         rows["late_t"] = self.t + 1
         return True
 
-    def _catchup_next(self, rows, n, stream):
+    def _catchup_next(self, rows, n, stream, clock=None):
         self._ensure(self.t + 2)
         cache = self.__dict__.setdefault("_early_pairs", {})
         key = (getattr(self, "_gen", 0), rows["uniq_u"].data_ptr(), rows["uniq_i"].data_ptr())
@@ -495,7 +509,8 @@ class DeferredTableAdam:
                 pairs[k].row_ids = ptr(ids)
         _lib.call("ncf_adam_pairs_catchup_lock_clock", ctypes.addressof(pairs), 2,
                   self.engine.model.mlp_embedding_dim, ptr(rows["num_unique"]), n, 1, 0,
-                  ptr(self.clock), ptr(self._table), *self._consts(), stream)
+                  ptr(self.clock if clock is None else clock), ptr(self._table), *self._consts(),
+                  stream)
 
     def fused_apply_args(self, w):
         """The arguments of the apply fused into the embedding backward (engine.backward
@@ -566,6 +581,8 @@ class DeferredTableAdam:
 
     def sync(self):
         """Catch every row up to the current step (tables + moments become the dense values)."""
+        if self.clock is not None:
+            self.late_join()
         if self.t == 0 or self.synced_t == self.t:
             return
         self._sweep(_lib.stream_ptr(self.tables["mf_user"].device))

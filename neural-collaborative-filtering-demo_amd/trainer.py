@@ -71,6 +71,13 @@ SPLIT_CLOSE = False
 # (tools/dropin_host.py, run r06p): 0.368 -> 0.317 ms/step.  Scoped to the epoch (the
 # torch.autograd.set_multithreading_enabled context manager); the numbers are the same bits.
 CALLING_THREAD_BACKWARD = True
+# The late catch-up of the next batch's rows (deferred.LATE_CATCHUP) left running past the step:
+# the step's join before the clock advance waits for the sweep and the sort only, the late
+# catch-up reads its target from a copy of the clock taken before that join, and the next user
+# of the tables waits for it (deferred.late_join: the next prepare, a flush, a sync).  Without
+# it the step's stream reached that join before the catch-up (~30 us, queued behind the apply)
+# was done and resumed ~10 us after it (rocprof r06k: an 11.5 us gap before the flat Adam).
+LATE_DETACHED = True
 
 
 class FusedTrainStep:
@@ -247,16 +254,34 @@ class FusedTrainStep:
         (before the clock advance) waits for it."""
         d = self.deferred
         side = d.side_stream()
+        clk = None
+        if LATE_DETACHED:
+            # the clock as this step's catch-up needs it, copied on the side stream ahead of the
+            # step's join (the advance after that join cannot overtake the copy)
+            if d._late_clock is None:
+                d._late_clock = torch.zeros_like(self.clock)
+            clk = d._late_clock
+            _lib.call("ncf_memcpy_async", ptr(clk), ptr(self.clock), 16, side.cuda_stream)
+            d.sweep_done(side.cuda_stream)
+            d._joined = False
         ev = self._event()
         ev.record(_lib.stream_ptr(self.model.engine.flat.device))
         ev.wait(side.cuda_stream)
         if _lib.PROFILE is not None:     # (the per-launch instrumentation times it on its stream)
             with torch.cuda.stream(side):
-                d.late_catchup(s, n, side.cuda_stream)
+                d.late_catchup(s, n, side.cuda_stream, clk)
         else:
-            d.late_catchup(s, n, side.cuda_stream)
-        d.sweep_done(side.cuda_stream)
-        d._joined = False
+            d.late_catchup(s, n, side.cuda_stream, clk)
+        if LATE_DETACHED:
+            evs = getattr(self, "_late_evs", None)
+            if evs is None:
+                evs = self._late_evs = [_lib.RawEvent(stream_only=True) for _ in range(2)]
+            evs.reverse()
+            evs[0].record(side.cuda_stream)
+            d._late_ev = evs[0]
+        else:
+            d.sweep_done(side.cuda_stream)
+            d._joined = False
 
     # ---- pipelined dedup: the id sort of step t+1 runs on a side stream under step t
     def _event(self):
