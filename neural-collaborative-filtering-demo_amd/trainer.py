@@ -255,18 +255,18 @@ class FusedTrainStep:
         d = self.deferred
         side = d.side_stream()
         clk = None
+        if LATE_DETACHED and d._late_clock is None:
+            d._late_clock = torch.zeros_like(self.clock)
+        ev = self._event()     # (also orders the copy below after the copy buffer's creation)
+        ev.record(_lib.stream_ptr(self.model.engine.flat.device))
+        ev.wait(side.cuda_stream)
         if LATE_DETACHED:
             # the clock as this step's catch-up needs it, copied on the side stream ahead of the
             # step's join (the advance after that join cannot overtake the copy)
-            if d._late_clock is None:
-                d._late_clock = torch.zeros_like(self.clock)
             clk = d._late_clock
             _lib.call("ncf_memcpy_async", ptr(clk), ptr(self.clock), 16, side.cuda_stream)
             d.sweep_done(side.cuda_stream)
             d._joined = False
-        ev = self._event()
-        ev.record(_lib.stream_ptr(self.model.engine.flat.device))
-        ev.wait(side.cuda_stream)
         if _lib.PROFILE is not None:     # (the per-launch instrumentation times it on its stream)
             with torch.cuda.stream(side):
                 d.late_catchup(s, n, side.cuda_stream, clk)
