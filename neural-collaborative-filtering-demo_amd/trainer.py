@@ -77,7 +77,10 @@ CALLING_THREAD_BACKWARD = True
 # of the tables waits for it (deferred.late_join: the next prepare, a flush, a sync).  Without
 # it the step's stream reached that join before the catch-up (~30 us, queued behind the apply)
 # was done and resumed ~10 us after it (rocprof r06k: an 11.5 us gap before the flat Adam).
-LATE_DETACHED = True
+# Off: measured neutral (run r06zf, 3 interleaved runs each: min 0.2726 ms/step on, 0.2713 off;
+# the gap moves to the next step's prepare, where the catch-up is still running beside the
+# forward's head).  Bitwise-green either way (the late catch-up / early catch-up tests).
+LATE_DETACHED = False
 
 
 class FusedTrainStep:
