@@ -1,7 +1,7 @@
 """C2 step time (the bench's training step: FusedTrainStep with next=, overlapped sweep, 256
 resident Zipf batches) under module-constant variants, interleaved in one process so the box's
 drift hits every variant alike (GPU only).
-    python tools/step_ab.py [--steps 200] [--reps 3] VARIANT [VARIANT ...]
+    python tools/step_ab.py [--steps 200] [--reps 3] [--groups 4096] VARIANT [VARIANT ...]
 VARIANT: name=module.CONST:value[,module.CONST:value][,sweep:N][,env:NAME:value][,c:SETTER:v]
 (c: a C-ABI setter taking one int64, e.g. c:ncf_reduce_set_vec:0, restored after the variant)  e.g.
     base=engine.FUSE_ATTN_TOWER:1  nofuse=engine.FUSE_ATTN_TOWER:0  noearly=deferred.EARLY_CATCHUP:0
@@ -60,10 +60,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--groups", type=int, default=4096, help="B (4096: C2; 256: the reference's)")
     ap.add_argument("variants", nargs="+")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    U, I, D, B, M = 1_000_000, 100_000, 64, 4096, 5
+    U, I, D, B, M = 1_000_000, 100_000, 64, args.groups, 5
     batches = bench.make_batches(U, I, B, M, 256, dev, seed=3)
     variants = [parse(v) for v in args.variants]
     defaults = {(m, c): getattr(m, c) for _, sets, _ in variants for m, c, _ in sets}
