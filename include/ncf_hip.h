@@ -39,6 +39,10 @@ typedef struct ncf_step_clock {
   uint64_t seed;
 } ncf_step_clock;
 int ncf_step_clock_advance(ncf_step_clock* clock, uint64_t base_seed, void* stream);
+/* Sets *clock = {t, 0, seed} on `stream` (a side stream's own copy of the step clock, set from the
+ * host's step counter: kernels queued there read their step targets from it while the step's
+ * stream advances the live clock without waiting for them). */
+int ncf_step_clock_set(ncf_step_clock* clock, int32_t t, uint64_t seed, void* stream);
 
 /* One wavefront waiting `microseconds` (<= 1e6) of wall-clock time on `stream`: the overlap
  * probe of a step's side streams (two spins on two streams finish in about one span when the

@@ -158,6 +158,7 @@ SIGNATURES = {
                                   F64, F64, P]),
     "ncf_adam_sweep": (I32, [P, P, P, P, P, P, I64, I64, I64, P, I32, P, F64, F64, F64, F64, P]),
     "ncf_step_clock_advance": (I32, [P, U64, P]),
+    "ncf_step_clock_set": (I32, [P, I32, U64, P]),
     "ncf_adam_rows_catchup_clock": (I32, [P, P, P, P, P, P, I64, P, P, I32, I64, P, I32, P, P, F64,
                                           F64, F64, F64, P]),
     "ncf_adam_rows_apply_clock": (I32, [P, P, P, P, P, P, P, P, I64, P, P, I32, I64, P, I32, P, P,

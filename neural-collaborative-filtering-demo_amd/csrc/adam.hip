@@ -520,6 +520,12 @@ __global__ void k_clock_advance(ncf_step_clock* clock, uint64_t base_seed) {
   clock_advance(clock, base_seed);
 }
 
+__global__ void k_clock_set(ncf_step_clock* clock, int32_t t, uint64_t seed) {
+  clock->t = t;
+  clock->reserved = 0;
+  clock->seed = seed;
+}
+
 // k_adam_flat_clock + k_clock_advance in one launch: every block counts itself done in
 // clock->reserved after its threads have read the clock; the last one advances the clock and
 // re-arms the counter (0 between launches).
@@ -856,6 +862,13 @@ extern "C" int ncf_step_clock_advance(ncf_step_clock* clock, uint64_t base_seed,
   NCF_CHECK_ARG(clock, "ncf_step_clock_advance: null clock");
   hipLaunchKernelGGL(k_clock_advance, dim3(1), dim3(1), 0, (hipStream_t)stream, clock, base_seed);
   NCF_CHECK_LAUNCH("ncf_step_clock_advance");
+  return NCF_OK;
+}
+
+extern "C" int ncf_step_clock_set(ncf_step_clock* clock, int32_t t, uint64_t seed, void* stream) {
+  NCF_CHECK_ARG(clock && t >= 0, "ncf_step_clock_set: null clock or t < 0");
+  hipLaunchKernelGGL(k_clock_set, dim3(1), dim3(1), 0, (hipStream_t)stream, clock, t, seed);
+  NCF_CHECK_LAUNCH("ncf_step_clock_set");
   return NCF_OK;
 }
 

@@ -140,6 +140,9 @@ class DeferredTableAdam:
         # user of the tables waits for (late_join), and the clock copy it reads its target from
         self._late_ev = None
         self._late_clock = None
+        self._side_t = None        # the t the side clock was last set to (side_clock)
+        self._side_ordered_t = -1  # the side stream is ordered after the table apply closing t + 1
+        self._live_pending = False  # a sweep part reading the live clock awaits the step's join
         engine.deferred = self
         if self.overlap and not torch.cuda.is_current_stream_capturing():
             self.side_stream()     # (picked and checked here, outside any stream capture)
@@ -299,19 +302,20 @@ class DeferredTableAdam:
                 r0 = k * sl
                 self._sweep_range(kind, r0, max(0, min(rows, r0 + sl) - r0), st)
 
-    def _rolling(self, st, step_rel, part=0, nparts=1):
+    def _rolling(self, st, step_rel, part=0, nparts=1, clock=None):
         """Rolling sweep closing step clock->t + step_rel (slice of that step; part `part` of
-        `nparts` consecutive row ranges of it)."""
+        `nparts` consecutive row ranges of it); ``clock``: a side clock (side_clock) instead of
+        the live one."""
         pairs = self.__dict__.get("_sweep_pairs") or self.__dict__.setdefault("_sweep_pairs",
                                                                                self._pairs())
         D = self.engine.model.mlp_embedding_dim
+        clk = ptr(self.clock if clock is None else clock)
         if nparts == 1:
             _lib.call("ncf_adam_pairs_sweep_rolling", ctypes.addressof(pairs), 2, D,
-                      self.sweep_every, step_rel, ptr(self.clock), ptr(self._table),
-                      *self._consts(), st)
+                      self.sweep_every, step_rel, clk, ptr(self._table), *self._consts(), st)
         else:
             _lib.call("ncf_adam_pairs_sweep_rolling_part", ctypes.addressof(pairs), 2, D,
-                      self.sweep_every, step_rel, part, nparts, ptr(self.clock), ptr(self._table),
+                      self.sweep_every, step_rel, part, nparts, clk, ptr(self._table),
                       *self._consts(), st)
 
     def sweep_fork(self, at="mlp_bwd"):
@@ -336,6 +340,7 @@ class DeferredTableAdam:
         self._ev[1].record(side)
         self._owed.remove(part)
         self._joined = False
+        self._live_pending = True      # (it reads the live clock: joined before the advance)
 
     def side_stream(self):
         """The overlapped sweep's stream (created on first use)."""
@@ -364,6 +369,47 @@ class DeferredTableAdam:
         if not self._joined:
             self._ev[1].wait(_lib.stream_ptr(self.clock.device))
             self._joined = True
+            self._live_pending = False
+
+    # ---- trainer.SIDE_AHEAD: the side stream's work off the step's queue
+    def side_clock(self, st):
+        """The side stream's own step clock, t = the host's step counter, set on stream st (the
+        side stream) when that changed: the late catch-up and the sweep queued there read their
+        targets from it, so the step's stream advances the live clock without joining them."""
+        if self._late_clock is None:
+            # (no fill: written by ncf_step_clock_set on the side stream before any reader)
+            self._late_clock = torch.empty_like(self.clock)
+        if self._side_t != self.t:
+            _lib.call("ncf_step_clock_set", ptr(self._late_clock), self.t, 0, st)
+            self._side_t = self.t
+        return self._late_clock
+
+    def side_ordered(self):
+        """The side stream has waited for the table apply closing step t + 1 (the trainer's
+        tables-done event): after this step's advance, its owed sweep may run there."""
+        self._side_ordered_t = self.t
+
+    def sweep_owed(self, side):
+        """Every owed part of the closed step's rolling sweep on stream `side` now, its target
+        (t) from the side clock, when that stream is ordered after the closed step's table
+        apply (side_ordered; else the parts stay owed for the engine's fork points).  The
+        batch rows of that step carry its stamp and are skipped, the next batch's rows were
+        caught up ahead of it on the same stream (the late catch-up), every other row is the
+        sweep's alone; a catch-up on the step's stream first joins it (prepare)."""
+        if not self._owed or self._side_ordered_t != self.t - 1:
+            return False
+        clk = self.side_clock(side)
+        n = len(self.fork_points)
+        for part in sorted(self._owed):
+            if _lib.PROFILE is not None:   # (per-launch instrumentation times it on its stream)
+                with torch.cuda.stream(self._side):
+                    self._rolling(side, 0, part, n, clock=clk)
+            else:
+                self._rolling(side, 0, part, n, clock=clk)
+        self._owed = []
+        self._ev[1].record(side)
+        self._joined = False
+        return True
 
     def _settle(self, st):
         """Parts of the owed sweep whose fork point this step did not pass: on stream st, now
@@ -418,6 +464,8 @@ class DeferredTableAdam:
                 self._locked = False
                 self.late_skips += 1
                 return
+            # (a sweep still running on the side stream may hold rows of this batch: SIDE_AHEAD)
+            self.sweep_join()
             pairs = self._pairs_for(w)
             # (locked: an early catch-up of the next batch may run during this step)
             lock = 1 if EARLY_CATCHUP else 0
@@ -439,6 +487,7 @@ class DeferredTableAdam:
         m = self.engine.model
         n = w.g.n
         self._ensure(self.t + 1)
+        self.sweep_join()             # (a side sweep left running past its step: SIDE_AHEAD)
         pairs = self._pairs_for(w)
         self._locked = False          # (no early catch-up during a claim-path step)
         _lib.call("ncf_adam_pairs_catchup_claim_clock", ctypes.addressof(pairs), 2,

@@ -12,6 +12,7 @@ BCE + backward kernels, fused Adam — identical math, one kernel sequence on on
 what the benchmark times (and what a production trainer uses).
 """
 import logging
+import weakref
 from typing import Any, Dict, Optional  # noqa: F401
 
 import torch
@@ -81,6 +82,25 @@ CALLING_THREAD_BACKWARD = True
 # the gap moves to the next step's prepare, where the catch-up is still running beside the
 # forward's head).  Bitwise-green either way (the late catch-up / early catch-up tests).
 LATE_DETACHED = False
+# The side stream's work of a step queued at the step's entry, off the step's queue: the next
+# batch's id sort, then the rolling sweep owed by the closed step, their step targets read from a
+# side copy of the clock set from the host's counter (deferred.side_clock), and the late catch-up
+# at the table apply as before, from the same copy.  The step's stream records one event (the
+# table apply done) and waits once (for the late catch-up, before the next gather): no fork
+# event at the tower, no join before the clock advance.  Three dedup sets (the sort at the entry
+# of step T + 1 writes the set of step T - 1, whose reductions are queued before the event the
+# side stream waited for in step T).
+SIDE_AHEAD = False
+
+
+def _join_side_streams(dev, streams):
+    """FusedTrainStep finalizer: the current stream of `dev` waits for each side stream."""
+    try:
+        cur = torch.cuda.current_stream(dev)
+        for s in streams:
+            cur.wait_stream(s)
+    except Exception:       # (interpreter shutdown: the runtime may be gone already)
+        pass
 
 
 class FusedTrainStep:
@@ -167,6 +187,13 @@ class FusedTrainStep:
         self._static = None
         self._w = None
         self._eager_steps = 0
+        # side streams whose work may outlive a step (SIDE_AHEAD; the dedup fork at "entry"):
+        # when the step is dropped, the stream it was built on waits for them before the
+        # caching allocator can hand their buffers (the model's, this step's) to new work there
+        self._side_streams = []
+        if self.deferred is not None and self.deferred._side is not None:
+            self._side_streams.append(self.deferred._side)
+        weakref.finalize(self, _join_side_streams, dev, self._side_streams)
 
     @property
     def lr(self):
@@ -189,7 +216,6 @@ class FusedTrainStep:
         if drop_p > 0 and self.clock is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         prep = self.deferred.prepare if self.deferred is not None else None
-        self._late_next = None     # set by this step's prefetch (_prefetch_dedup), at the sweep fork
         w = eng.forward(user_ids, item_ids, M, True, drop_p, seed, prepare=prep,
                         tables=self.tables_lp, bf16=self.bf16)
         # (REDUCE_ASYNC: the dense-gradient reductions beside the table Adam)
@@ -207,8 +233,11 @@ class FusedTrainStep:
         b1, b2 = self.betas
         split = (SPLIT_CLOSE and self.deferred is not None and self.clock is not None
                  and not self.graph and self.deferred.overlap)
+        # (SIDE_AHEAD: no join of the side stream in the step unless a sweep part reading the
+        # live clock was forked in it — the closed step's sweep could not run at the entry)
+        free = self._ahead() and not d._live_pending
         if self.deferred is not None:
-            self.deferred.apply(w, st, late_join=split)
+            self.deferred.apply(w, st, late_join=split or free)
         elif self.bf16:      # dense bf16 sweep (the reference schedule of the bf16 tables)
             D = self.model.mlp_embedding_dim
             for key, lp in self.tables_lp.items():
@@ -230,7 +259,7 @@ class FusedTrainStep:
             self.deferred.sweep_join()       # (the clock advance below changes its target)
             _lib.call("ncf_step_clock_advance", ptr(self.clock), self.base_seed, st)
         elif self.clock is not None:
-            if self.deferred is not None:
+            if self.deferred is not None and not free:
                 self.deferred.sweep_join()   # (the clock advance below changes its target)
             _lib.call("ncf_adam_flat_clock_close", ptr(eng.flat), ptr(eng.flat_grad),
                       ptr(self.m_flat), ptr(self.v_flat), eng.flat.numel(),
@@ -249,6 +278,12 @@ class FusedTrainStep:
         late, self._late_next = self._late_next, None
         if late is not None:
             self._late_catchup(*late)
+        elif self._ahead():      # (the closed step's sweep may then run at the next entry)
+            d = self.deferred
+            ev = self._event()
+            ev.record(_lib.stream_ptr(self.model.engine.flat.device))
+            ev.wait(d.side_stream().cuda_stream)
+            d.side_ordered()
 
     def _late_catchup(self, s, n):
         """deferred.LATE_CATCHUP: the next batch's rows (dedup set s, sorted on the side stream)
@@ -258,12 +293,16 @@ class FusedTrainStep:
         d = self.deferred
         side = d.side_stream()
         clk = None
-        if LATE_DETACHED and d._late_clock is None:
+        ahead = self._ahead()
+        if LATE_DETACHED and not ahead and d._late_clock is None:
             d._late_clock = torch.zeros_like(self.clock)
         ev = self._event()     # (also orders the copy below after the copy buffer's creation)
         ev.record(_lib.stream_ptr(self.model.engine.flat.device))
         ev.wait(side.cuda_stream)
-        if LATE_DETACHED:
+        if ahead:
+            d.side_ordered()
+            clk = d.side_clock(side.cuda_stream)
+        elif LATE_DETACHED:
             # the clock as this step's catch-up needs it, copied on the side stream ahead of the
             # step's join (the advance after that join cannot overtake the copy)
             clk = d._late_clock
@@ -275,7 +314,7 @@ class FusedTrainStep:
                 d.late_catchup(s, n, side.cuda_stream, clk)
         else:
             d.late_catchup(s, n, side.cuda_stream, clk)
-        if LATE_DETACHED:
+        if LATE_DETACHED or ahead:
             evs = getattr(self, "_late_evs", None)
             if evs is None:
                 evs = self._late_evs = [_lib.RawEvent(stream_only=True) for _ in range(2)]
@@ -297,21 +336,33 @@ class FusedTrainStep:
         return ring[0][ring[1]]
 
     def _dedup_sets(self, w):
-        """Two sets of the dedup outputs (sorted segments, unique ids, counts) for workspace w:
-        the workspace's own buffers and a twin, alternating between consecutive steps."""
-        sets = w.cache.get("dedup_sets")
+        """A ring of sets of the dedup outputs (sorted segments, unique ids, counts) for
+        workspace w, used in turn by consecutive steps: the workspace's own buffers and a twin
+        (a third with SIDE_AHEAD).  {"ring": [...], "i": the current step's set}."""
+        k = 3 if self._ahead() else 2
+        sets = w.cache.get(("dedup_sets", k))
         if sets is None:
             a = dict(emb_ws=w.emb_ws, uniq_u=w.uniq_u, uniq_i=w.uniq_i, num_unique=w.num_unique)
-            b = {k: torch.empty_like(v) for k, v in a.items()}
-            sets = w.cache["dedup_sets"] = [a, b, 0]
+            ring = [a] + [{n: torch.empty_like(v) for n, v in a.items()} for _ in range(k - 1)]
+            sets = w.cache[("dedup_sets", k)] = {"ring": ring, "i": 0}
         return sets
+
+    @staticmethod
+    def _next_set(sets):
+        return sets["ring"][(sets["i"] + 1) % len(sets["ring"])]
+
+    def _ahead(self):
+        """SIDE_AHEAD applies: eager, the overlapped sweep, the late catch-up behind the fused
+        table apply."""
+        d = self.deferred
+        return (SIDE_AHEAD and not self.graph and d is not None and d.overlap and FUSE_APPLY
+                and deferred_mod.LATE_CATCHUP and not deferred_mod.EARLY_CATCHUP)
 
     def _prefetch_dedup(self, w, uid, iid, entry, side=None):
         """Dedup of the NEXT step's ids into the idle set, on the side stream, after `entry`
         (the start of this step: the run that last used that set is complete there).  With
         ``side`` (and no entry): on that stream, already ordered after such a point."""
-        sets = self._dedup_sets(w)
-        s = sets[1 - sets[2]]
+        s = self._next_set(self._dedup_sets(w))
         eng = self.model.engine
         m = self.model
         if side is not None:
@@ -329,9 +380,26 @@ class FusedTrainStep:
             return
         if getattr(self, "_side", None) is None:
             self._side = _lib.side_stream(eng.flat.device)
+            self._side_streams.append(self._side)
         side = self._side
         entry.wait(side.cuda_stream)
         self._enqueue_dedup(s, w, uid, iid, side)
+
+    def _entry_side(self, w, uid, next):
+        """SIDE_AHEAD, at the step's entry, on the deferred schedule's side stream (ordered
+        after the previous step's table apply by its tables-done event, nothing recorded on the
+        step's stream): the next batch's id sort into the next set of the ring, then the
+        rolling sweep the previous step owes (deferred.sweep_owed, its target from the side
+        clock)."""
+        d = self.deferred
+        side = d.side_stream()
+        d.side_clock(side.cuda_stream)
+        if next is not None and next[0].numel() == uid.numel():
+            s = self._next_set(self._dedup_sets(w))
+            self._enqueue_dedup(s, w, next[0], next[1], side)
+            self._late_next = (s, next[0].numel())
+        if d.sweep_owed(side.cuda_stream):
+            self.model.engine.fork_hook = None
 
     def _enqueue_dedup(self, s, w, uid, iid, side):
         m = self.model
@@ -345,24 +413,27 @@ class FusedTrainStep:
         ev.record(side.cuda_stream)
         self._pending = (uid, iid, ev)          # the caller's objects: matched by identity
 
-    def _activate_dedup(self, w, uid, iid):
+    def _activate_dedup(self, w, uid, iid, ahead=False):
         """Point w at this step's dedup set: the prefetched one when it was made for these ids
         (the step then waits for its event instead of sorting), else the next set, sorted
         inline by the deferred Adam's prepare."""
         sets = self._dedup_sets(w)
         pend, self._pending = getattr(self, "_pending", None), None
-        sets[2] = 1 - sets[2]
-        s = sets[sets[2]]
+        sets["i"] = (sets["i"] + 1) % len(sets["ring"])
+        s = sets["ring"][sets["i"]]
         w.emb_ws, w.uniq_u, w.uniq_i, w.num_unique = s["emb_ws"], s["uniq_u"], s["uniq_i"], s["num_unique"]
         w.prededuped = None
         late_t, w.late_t = s.pop("late_t", None), None
         if pend is not None:
             cur = torch.cuda.current_stream(self.model.engine.flat.device)
+            mine = pend[0] is uid and pend[1] is iid
             if pend[2] is None:               # sorted behind the sweep: joined with it
                 self.deferred.sweep_join()
-            else:
+            elif not (ahead and mine and late_t is not None):
                 pend[2].wait(cur.cuda_stream)  # (also orders a stale prefetch before reuse)
-            if pend[0] is uid and pend[1] is iid:
+            # (else: the late catch-up queued behind that sort, which the step's prepare
+            # waits for, orders it — deferred.late_join)
+            if mine:
                 w.prededuped = True
                 w.late_t = late_t
 
@@ -373,15 +444,19 @@ class FusedTrainStep:
         call must pass those very tensor objects, unmodified, to use the prefetched sort."""
         m = self.model
         M = M or (1 + m.negative_samples)
+        self._late_next = None     # set by this step's prefetch (_prefetch_dedup / _entry_side)
         if not self.graph:
             pipe = self.deferred is not None and self.clock is not None and (
                 next is not None or getattr(self, "_pending", None) is not None)
+            ahead = self._ahead()
             if pipe:
                 eng = m.engine
                 eng.ensure_layout()
                 w0 = eng.workspace(user_ids.numel(), M, True)
-                self._activate_dedup(w0, user_ids, item_ids)
-                if next is not None and next[0].numel() == user_ids.numel():
+                self._activate_dedup(w0, user_ids, item_ids, ahead)
+                if ahead:
+                    self._entry_side(w0, user_ids, next)
+                elif next is not None and next[0].numel() == user_ids.numel():
                     if DEDUP_FORK == "entry":
                         # (recorded only here: an event record costs the queue a few us)
                         entry = self._event()

@@ -1247,11 +1247,62 @@ def test_late_catchup_bitwise_equals_dense(monkeypatch):
             assert torch.equal(a_m[k][0], b_m[k][0]) and torch.equal(a_m[k][1], b_m[k][1]), k
 
 
-def test_pipelined_dedup_bitwise_equals_inline():
+@pytest.mark.parametrize("tables", ["fp32", "bf16"])
+def test_side_ahead_bitwise_equals_dense(monkeypatch, tables):
+    """trainer.SIDE_AHEAD: the next batch's sort and the closed step's rolling sweep queued on the
+    side stream at the step's entry (their targets from the side clock, ncf_step_clock_set), the
+    late catch-up behind the table apply from the same clock, no fork event and no join of the
+    side stream in the step (three dedup sets).  Against the default schedule bit for bit —
+    parameters and both moments, dropout on, sweep every 8 steps, 30 steps (fp32 tables: also
+    the dense schedule through the default one, test_late_catchup_bitwise_equals_dense).  The
+    sweep must have run at the entry on every step after the second, the late catch-up's skip
+    on every step after the first, and no sweep part forked at an engine fork point."""
+    import ncf_amd.deferred as Dm
+    import ncf_amd.trainer as Tr
+    dt = torch.bfloat16 if tables == "bf16" else torch.float32
+    kw = dict(sweep_every=8, dropout=0.2, clock=True, overlap_sweep=True, pipelined=True,
+              table_dtype=dt)
+    ref = _fused_run(True, 30, **kw)
+    seen, owed, forks = [], [], []
+    orig_p, orig_o, orig_f = (Dm.DeferredTableAdam.prepare, Dm.DeferredTableAdam.sweep_owed,
+                              Dm.DeferredTableAdam.sweep_fork)
+
+    def prep(self, *a):
+        seen.append(self)
+        return orig_p(self, *a)
+
+    def sw(self, *a):
+        r = orig_o(self, *a)
+        owed.append(r)
+        return r
+
+    def fk(self, *a, **k):
+        n = len(self._owed)
+        r = orig_f(self, *a, **k)
+        forks.append(n - len(self._owed))
+        return r
+    monkeypatch.setattr(Dm.DeferredTableAdam, "prepare", prep)
+    monkeypatch.setattr(Dm.DeferredTableAdam, "sweep_owed", sw)
+    monkeypatch.setattr(Dm.DeferredTableAdam, "sweep_fork", fk)
+    monkeypatch.setattr(Tr, "SIDE_AHEAD", True)
+    got = _fused_run(True, 30, **kw)
+    assert max(d.late_skips for d in seen) >= 28
+    assert sum(owed) >= 28 and sum(forks) == 0, (owed, forks)
+    for k in ref[0]:
+        assert torch.equal(ref[0][k], got[0][k]), k
+    for k in ref[1]:
+        assert torch.equal(ref[1][k][0], got[1][k][0]) and torch.equal(ref[1][k][1], got[1][k][1]), k
+
+
+@pytest.mark.parametrize("ahead", [False, True])
+def test_pipelined_dedup_bitwise_equals_inline(monkeypatch, ahead):
     """FusedTrainStep(next=...) sorts the next batch's ids on a side stream under the current
-    step (two alternating dedup buffer sets); results are bit for bit those of the inline sort,
-    including a step whose prefetch is discarded (ids not the ones announced)."""
+    step (two alternating dedup buffer sets; three with trainer.SIDE_AHEAD, the sort queued at
+    the step's entry); results are bit for bit those of the inline sort, including a step whose
+    prefetch is discarded (ids not the ones announced) and a step told no next batch."""
+    import ncf_amd.trainer as Tr
     from ncf_amd.trainer import FusedTrainStep
+    monkeypatch.setattr(Tr, "SIDE_AHEAD", ahead)
     U, I, B = 3000, 500, 64
     g = torch.Generator().manual_seed(21)
     batches = []
@@ -1271,6 +1322,8 @@ def test_pipelined_dedup_bitwise_equals_inline():
                 step(u, i, t)
             elif s_ == 4:      # announce a different batch: the prefetch must be ignored
                 step(u, i, t, next=(batches[0][0], batches[0][1]))
+            elif s_ == 6:      # no next batch: the following step sorts inline
+                step(u, i, t)
             else:
                 nxt = batches[s_ + 1][:2] if s_ + 1 < len(batches) else None
                 step(u, i, t, next=nxt)
@@ -1377,16 +1430,17 @@ def test_step_teardown_with_side_work_queued_then_new_step():
 
     ref = _fused_run(True, 12, sweep_every=8, B=B, seed=31, dropout=0.2, clock=True,
                      overlap_sweep=True, pipelined=True)
-    for fork, early in (("sweep", False), ("entry", True)):
-        old = (Tr.DEDUP_FORK, Tr.EARLY_REDUCE)
-        Tr.DEDUP_FORK, Tr.EARLY_REDUCE = fork, early
+    for fork, early, ahead in (("sweep", False, False), ("entry", True, False),
+                               ("sweep", False, True)):
+        old = (Tr.DEDUP_FORK, Tr.EARLY_REDUCE, Tr.SIDE_AHEAD)
+        Tr.DEDUP_FORK, Tr.EARLY_REDUCE, Tr.SIDE_AHEAD = fork, early, ahead
         try:
             leave_in_flight(7)       # (its objects are unreachable on return: freed now)
             gc.collect()
             got = _fused_run(True, 12, sweep_every=8, B=B, seed=31, dropout=0.2, clock=True,
                              overlap_sweep=True, pipelined=True)
         finally:
-            Tr.DEDUP_FORK, Tr.EARLY_REDUCE = old
+            Tr.DEDUP_FORK, Tr.EARLY_REDUCE, Tr.SIDE_AHEAD = old
         for k in ref[0]:
             assert torch.equal(ref[0][k], got[0][k]), (fork, k)
         for k in ref[1]:
