@@ -89,7 +89,10 @@ LATE_DETACHED = False
 # table apply done) and waits once (for the late catch-up, before the next gather): no fork
 # event at the tower, no join before the clock advance.  Three dedup sets (the sort at the entry
 # of step T + 1 writes the set of step T - 1, whose reductions are queued before the event the
-# side stream waited for in step T).
+# side stream waited for in step T).  Off: measured slower (run r06zj, tools/step_ab.py, 3
+# interleaved runs each: C2 min 0.2795 against 0.2698 ms/step, B = 256 0.1669 against 0.1637 —
+# the sweep beside the reductions and the next gather runs longer than beside the fused forward
+# (64 against 50 us), more than the fork event it saves); bit-identical (its tests run it).
 SIDE_AHEAD = False
 
 
