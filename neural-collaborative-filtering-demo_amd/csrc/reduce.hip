@@ -18,7 +18,11 @@ namespace {
 
 constexpr int kPB = 64;          // partials per stage-1 chunk
 constexpr int kMaxPerLaunch = 24; // descriptors per launch (kernel-argument size)
-bool VEC_LANES = true;            // ncf_reduce_set_vec: A/B against one column per lane
+// ncf_reduce_set_vec: 0 one column per lane, 1 four columns per lane (16-byte loads, 16 in
+// flight per thread), 2 the same with 32 in flight per thread (two chunk iterations' loads
+// issued together: the grid of the batch's reductions holds only ~5 waves per CU at C2, so the
+// bytes in flight per wave set the rate)
+int VEC_LANES = 2;
 
 struct BatchArgs {
   ncf_reduce_desc d[kMaxPerLaunch];
@@ -48,11 +52,27 @@ template <> __device__ __forceinline__ float4 zero<float4>() { return make_float
 // Stage-1 sum of wave w's partials (rows pb + w, pb + w + 4, ... < pe) at element(s) i: T = float
 // (one column per lane) or float4 (four adjacent columns per lane, 16-byte loads: each column's
 // additions are the scalar form's, in the same order — the same bits).
-template <typename T>
+template <typename T, bool DEEP = false>
 __device__ __forceinline__ T stage1_sum(const float* __restrict__ part, int64_t stride, int64_t i,
                                         int pb, int pe, int w) {
   T a0 = zero<T>(), a1 = zero<T>(), a2 = zero<T>(), a3 = zero<T>();
   int p = pb + w;
+  if (DEEP) {
+    // 32 loads in flight (two iterations of the loop below at once; the same additions in the
+    // same order: accumulator j % 4 takes partial p + 4j, j ascending)
+    for (; p + 124 < pe; p += 128) {
+      T v[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) v[j] = *(const T*)(part + (int64_t)(p + 4 * j) * stride + i);
+#pragma unroll
+      for (int j = 0; j < 32; j += 4) {
+        a0 += v[j];
+        a1 += v[j + 1];
+        a2 += v[j + 2];
+        a3 += v[j + 3];
+      }
+    }
+  }
   // 16 loads in flight per thread (a full 64-partial chunk in one batch), summed in the order
   // of the loop below (accumulator j % 4 takes partial p + 4j): the same bits, without the
   // four dependent rounds of HBM latency
@@ -88,6 +108,7 @@ __global__ __launch_bounds__(256) void k_reduce_batch1(const BatchArgs a, float*
   const ncf_reduce_desc& d = a.d[di];
   const int ch = a.chunks[di];
   const bool vec = a.vec[di] != 0;
+  const bool deep = a.vec[di] == 2;
   const int vw = vec ? 4 : 1;
   const uint32_t local = blockIdx.x - a.first[di];
   const uint32_t gx = (uint32_t)((d.L + 64 * vw - 1) / (64 * vw));
@@ -99,7 +120,9 @@ __global__ __launch_bounds__(256) void k_reduce_batch1(const BatchArgs a, float*
   const int pe = ch > 1 ? min(d.P, pb + kPB) : d.P;
   if (vec) {
     float4 s = zero<float4>();
-    if (i < d.L) s = stage1_sum<float4>(d.part, d.stride, i, pb, pe, w);
+    if (i < d.L)
+      s = deep ? stage1_sum<float4, true>(d.part, d.stride, i, pb, pe, w)
+               : stage1_sum<float4>(d.part, d.stride, i, pb, pe, w);
     red[w][l] = s;
     __syncthreads();
     if (w == 0 && i < d.L) {
@@ -173,8 +196,8 @@ int chunks_of(int P) { return P > NCF_REDUCE_ONE_STAGE ? (P + kPB - 1) / kPB : 1
 }  // namespace
 
 extern "C" int64_t ncf_reduce_set_vec(int64_t on) {
-  const bool was = VEC_LANES;
-  if (on >= 0) VEC_LANES = on != 0;
+  const int was = VEC_LANES;
+  if (on >= 0) VEC_LANES = on > 2 ? 2 : (int)on;
   return was;
 }
 
@@ -209,13 +232,13 @@ extern "C" int ncf_reduce_batch(const ncf_reduce_list* list, float* scratch,
       NCF_CHECK_ARG(d.part && d.out && d.L >= 0 && d.P >= 1 && d.cols >= 1 && d.stride >= d.L,
                     "ncf_reduce_batch: bad descriptor %d", base + j);
       const int c = chunks_of(d.P);
-      const bool vec = VEC_LANES && d.L % 4 == 0 && d.stride % 4 == 0 &&
+      const bool vec = VEC_LANES > 0 && d.L % 4 == 0 && d.stride % 4 == 0 &&
                        ((uintptr_t)d.part & 15) == 0 &&
                        (c == 1 || (scr_off % 4 == 0 && ((uintptr_t)scratch & 15) == 0));
       const int vw = vec ? 4 : 1;
       const uint32_t gx = (uint32_t)((d.L + 64 * vw - 1) / (64 * vw));
       a1.d[a1.count] = d;
-      a1.vec[a1.count] = vec;
+      a1.vec[a1.count] = vec ? VEC_LANES : 0;
       a1.chunks[a1.count] = c;
       a1.first[a1.count] = b1;
       a1.scr[a1.count] = c > 1 ? scr_off : 0;

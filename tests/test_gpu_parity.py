@@ -546,10 +546,11 @@ def test_reduce_batch_matches_inline_reduce():
 
 
 def test_reduce_batch_vec_lanes_bitwise_equal_scalar():
-    """ncf_reduce_batch with 16-byte lanes (four columns per lane, ncf_reduce_set_vec: the
-    default) against one column per lane, bit for bit: one- and two-stage descriptors (P up to
-    1000), L and stride multiples of 4 (vec) beside ones that are not (scalar in the same
-    launch), a partial base 8 bytes off a 16-byte boundary (scalar), accumulate and scale."""
+    """ncf_reduce_batch with 16-byte lanes (four columns per lane, ncf_reduce_set_vec 1; 2, the
+    default: 32 loads in flight per thread) against one column per lane, bit for bit: one- and
+    two-stage descriptors (P up to 1000), L and stride multiples of 4 (vec) beside ones that are
+    not (scalar in the same launch), a partial base 8 bytes off a 16-byte boundary (scalar),
+    accumulate and scale."""
     from ncf_amd import _lib
     g = torch.Generator().manual_seed(9)
     specs = []
@@ -564,7 +565,7 @@ def test_reduce_batch_vec_lanes_bitwise_equal_scalar():
     outs0 = [torch.randn(((L + cols - 1) // cols) * (cols + 2), generator=g).to(DEV)
              for P, L, stride, off, cols, *_ in specs]
     res = []
-    for vec in (0, 1):
+    for vec in (0, 1, 2):
         prev = _lib.query("ncf_reduce_set_vec", vec)
         try:
             lst = _lib.ReduceList()
@@ -580,8 +581,8 @@ def test_reduce_batch_vec_lanes_bitwise_equal_scalar():
             res.append(outs)
         finally:
             _lib.query("ncf_reduce_set_vec", prev)
-    for k, (a, b) in enumerate(zip(*res)):
-        assert torch.equal(a, b), (k, specs[k])
+    for k, (a, *b) in enumerate(zip(*res)):
+        assert all(torch.equal(a, x) for x in b), (k, specs[k])
     P, L, stride, off, cols, acc, scale = specs[1]      # and the sums themselves
     s = parts[1][:P * stride].view(P, stride)[:, :L].double().sum(0).cpu() * scale
     np.testing.assert_allclose(res[1][1].cpu().double().view(-1, cols + 2)[:, :cols].reshape(-1)[:L]
