@@ -19,10 +19,11 @@ namespace {
 constexpr int kPB = 64;          // partials per stage-1 chunk
 constexpr int kMaxPerLaunch = 24; // descriptors per launch (kernel-argument size)
 // ncf_reduce_set_vec: 0 one column per lane, 1 four columns per lane (16-byte loads, 16 in
-// flight per thread), 2 the same with 32 in flight per thread (two chunk iterations' loads
-// issued together: the grid of the batch's reductions holds only ~5 waves per CU at C2, so the
-// bytes in flight per wave set the rate)
-int VEC_LANES = 2;
+// flight per thread; the default), 2 the same with 32 in flight per thread (two chunk
+// iterations' loads issued together).  2 measured neutral (run r06zk, 3 interleaved runs each:
+// C2 min 0.2652 against 0.2660 ms/step, the batch's reductions 36.1 against 36.9 us; B = 256
+// 14.8 against 12.6 us): the ~5 waves per CU of the grid already keep enough bytes in flight
+int VEC_LANES = 1;
 
 struct BatchArgs {
   ncf_reduce_desc d[kMaxPerLaunch];

@@ -546,8 +546,8 @@ def test_reduce_batch_matches_inline_reduce():
 
 
 def test_reduce_batch_vec_lanes_bitwise_equal_scalar():
-    """ncf_reduce_batch with 16-byte lanes (four columns per lane, ncf_reduce_set_vec 1; 2, the
-    default: 32 loads in flight per thread) against one column per lane, bit for bit: one- and
+    """ncf_reduce_batch with 16-byte lanes (four columns per lane, ncf_reduce_set_vec 1, the
+    default; 2: 32 loads in flight per thread) against one column per lane, bit for bit: one- and
     two-stage descriptors (P up to 1000), L and stride multiples of 4 (vec) beside ones that are
     not (scalar in the same launch), a partial base 8 bytes off a 16-byte boundary (scalar),
     accumulate and scale."""
