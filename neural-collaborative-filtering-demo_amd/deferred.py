@@ -45,8 +45,19 @@ SCALAR_PAD = 4096
 # current.  Same replays, bit-identical (tested).  Off: measured slower at C2 (round 5,
 # tools/step_ab.py, 3 interleaved runs each: 0.2942-0.2957 ms/step without, 0.3004 with, the
 # replay beside the backward slows it more than it saves on the critical path; round 3 found
-# the same for three placements of it)
-EARLY_CATCHUP = False
+# the same for three placements of it).  Smaller batches leave CUs idle beside the backward
+# (the reference's default batch of 256 groups fills 86 of 256 CUs) and the late catch-up's
+# wait sits on their step's critical path; run r06zl / r06zm, tools/step_ab.py, 3 interleaved
+# runs each, min ms/step late -> early: B = 256 groups 0.1622 -> 0.1516, 1,024 0.2131 -> 0.2027,
+# 2,048 0.2180 -> 0.2143, 4,096 (C2) 0.2669 -> 0.2689.  None (the default): on for batches of at
+# most EARLY_CATCHUP_ROWS rows (early_on); True / False: always / never.
+EARLY_CATCHUP = None
+EARLY_CATCHUP_ROWS = 10240
+
+
+def early_on(n: int) -> bool:
+    """Whether a batch of n rows takes the early catch-up (EARLY_CATCHUP)."""
+    return bool(EARLY_CATCHUP) if EARLY_CATCHUP is not None else n <= EARLY_CATCHUP_ROWS
 # Late catch-up: the same catch-up of the next batch's rows, queued once this step's table Adam
 # has run inside the embedding backward (trainer.FUSE_APPLY) — on the side stream behind the
 # sweep and the sort, beside the dense-gradient reductions (memory-bound, like it) instead of
@@ -468,7 +479,7 @@ class DeferredTableAdam:
             self.sweep_join()
             pairs = self._pairs_for(w)
             # (locked: an early catch-up of the next batch may run during this step)
-            lock = 1 if EARLY_CATCHUP else 0
+            lock = 1 if early_on(n) else 0
             _lib.call("ncf_adam_pairs_catchup_lock_clock", ctypes.addressof(pairs), 2,
                       m.mlp_embedding_dim, ptr(w.num_unique), n, 0, lock, ptr(self.clock),
                       ptr(self._table), *self._consts(), st)
@@ -528,7 +539,7 @@ class DeferredTableAdam:
         caught up through the step now running, on `stream` (ordered after their sort and
         joined before this step's apply).  Only when this step's catch-up locked its own rows;
         returns whether it was queued."""
-        if not (EARLY_CATCHUP and self.clock is not None and getattr(self, "_locked", False)
+        if not (early_on(n) and self.clock is not None and getattr(self, "_locked", False)
                 and n > 0):
             return False
         self._catchup_next(rows, n, stream)

@@ -356,10 +356,10 @@ class FusedTrainStep:
 
     def _ahead(self):
         """SIDE_AHEAD applies: eager, the overlapped sweep, the late catch-up behind the fused
-        table apply."""
+        table apply (deferred.EARLY_CATCHUP = False)."""
         d = self.deferred
         return (SIDE_AHEAD and not self.graph and d is not None and d.overlap and FUSE_APPLY
-                and deferred_mod.LATE_CATCHUP and not deferred_mod.EARLY_CATCHUP)
+                and deferred_mod.LATE_CATCHUP and deferred_mod.EARLY_CATCHUP is False)
 
     def _prefetch_dedup(self, w, uid, iid, entry, side=None):
         """Dedup of the NEXT step's ids into the idle set, on the side stream, after `entry`

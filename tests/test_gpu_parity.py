@@ -1161,7 +1161,7 @@ def test_early_catchup_bitwise_equals_dense(monkeypatch, tables):
         assert not any(ran)
     else:
         a_sd, a_m = _fused_run(False, 40, U=400, I=150)
-    monkeypatch.setattr(Dm, "EARLY_CATCHUP", True)     # (off by default)
+    monkeypatch.setattr(Dm, "EARLY_CATCHUP", True)     # (on by default below 10,240 rows)
     b_sd, b_m = _fused_run(True, 40, **kw)
     assert sum(ran) >= 38, ran
     for k in a_sd:
@@ -1216,6 +1216,7 @@ def test_late_catchup_bitwise_equals_dense(monkeypatch):
     import ncf_amd.deferred as Dm
     import ncf_amd.trainer as Tr
     monkeypatch.setattr(Tr, "FUSE_APPLY", True)
+    monkeypatch.setattr(Dm, "EARLY_CATCHUP", False)     # (on by default at this batch size)
     seen = []
     orig = Dm.DeferredTableAdam.prepare
 
@@ -1263,6 +1264,7 @@ def test_side_ahead_bitwise_equals_dense(monkeypatch, tables):
     dt = torch.bfloat16 if tables == "bf16" else torch.float32
     kw = dict(sweep_every=8, dropout=0.2, clock=True, overlap_sweep=True, pipelined=True,
               table_dtype=dt)
+    monkeypatch.setattr(Dm, "EARLY_CATCHUP", False)     # (SIDE_AHEAD rides the late catch-up)
     ref = _fused_run(True, 30, **kw)
     seen, owed, forks = [], [], []
     orig_p, orig_o, orig_f = (Dm.DeferredTableAdam.prepare, Dm.DeferredTableAdam.sweep_owed,
@@ -1301,9 +1303,12 @@ def test_pipelined_dedup_bitwise_equals_inline(monkeypatch, ahead):
     step (two alternating dedup buffer sets; three with trainer.SIDE_AHEAD, the sort queued at
     the step's entry); results are bit for bit those of the inline sort, including a step whose
     prefetch is discarded (ids not the ones announced) and a step told no next batch."""
+    import ncf_amd.deferred as Dm
     import ncf_amd.trainer as Tr
     from ncf_amd.trainer import FusedTrainStep
     monkeypatch.setattr(Tr, "SIDE_AHEAD", ahead)
+    if ahead:
+        monkeypatch.setattr(Dm, "EARLY_CATCHUP", False)
     U, I, B = 3000, 500, 64
     g = torch.Generator().manual_seed(21)
     batches = []
@@ -1433,15 +1438,17 @@ def test_step_teardown_with_side_work_queued_then_new_step():
                      overlap_sweep=True, pipelined=True)
     for fork, early, ahead in (("sweep", False, False), ("entry", True, False),
                                ("sweep", False, True)):
-        old = (Tr.DEDUP_FORK, Tr.EARLY_REDUCE, Tr.SIDE_AHEAD)
+        old = (Tr.DEDUP_FORK, Tr.EARLY_REDUCE, Tr.SIDE_AHEAD, _D.EARLY_CATCHUP)
         Tr.DEDUP_FORK, Tr.EARLY_REDUCE, Tr.SIDE_AHEAD = fork, early, ahead
+        if ahead:
+            _D.EARLY_CATCHUP = False
         try:
             leave_in_flight(7)       # (its objects are unreachable on return: freed now)
             gc.collect()
             got = _fused_run(True, 12, sweep_every=8, B=B, seed=31, dropout=0.2, clock=True,
                              overlap_sweep=True, pipelined=True)
         finally:
-            Tr.DEDUP_FORK, Tr.EARLY_REDUCE, Tr.SIDE_AHEAD = old
+            Tr.DEDUP_FORK, Tr.EARLY_REDUCE, Tr.SIDE_AHEAD, _D.EARLY_CATCHUP = old
         for k in ref[0]:
             assert torch.equal(ref[0][k], got[0][k]), (fork, k)
         for k in ref[1]:

@@ -48,6 +48,8 @@ def parse(spec):
         old = getattr(m, const)
         if isinstance(old, (bool, int)):
             v = type(old)(int(val))
+        elif old is None and (val == "None" or val.lstrip("-").isdigit()):
+            v = None if val == "None" else bool(int(val))    # (a tri-state switch: None / 0 / 1)
         elif old is None or isinstance(old, str):    # ('+' for ',' inside a string value)
             v = val.replace("+", ",")
         else:
