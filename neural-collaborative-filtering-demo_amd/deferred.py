@@ -127,7 +127,8 @@ class DeferredTableAdam:
         self.overlap = bool(overlap_sweep)
         if self.overlap and clock is None:
             raise ValueError("the overlapped sweep needs the device step clock")
-        # Where the engine forks it ("mlp_bwd": before the MLP tower backward; "mlp_bwd_after":
+        # Where the engine forks it ("gather": after the catch-up, before the gathers;
+        # "mlp_bwd": before the MLP tower backward; "mlp_bwd_after":
         # right after its launch (round 3: 0.337-0.344 vs 0.312 ms); "tower": before the tower
         # forward; "attn_bwd", "emb_bwd", "reduce": before those backward launches); the step
         # joins it before the table apply (a join before the clock-advancing close measured the

@@ -491,6 +491,7 @@ class NCFEngine:
         w.deduped = False
         if prepare is not None:
             prepare(w, uid, iid, st)
+            self._sweep_fork("gather")     # (a fork point after prepare, before the gather)
         else:
             self.sync_tables()
         if temporal is not None and (train or M != 1):
