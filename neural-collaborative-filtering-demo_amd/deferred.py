@@ -76,6 +76,12 @@ OVERLAP_SWEEP = True
 # Fork point(s) of the overlapped sweep (None: the geometry's default, _default_fork; else a
 # comma-separated list, see DeferredTableAdam.__init__)
 SWEEP_FORK = None
+# With the default fork point, batches of at most GATHER_FORK_ROWS rows fork the sweep before
+# their gathers instead ("gather"): the small-batch step leaves most CUs idle beside its short
+# kernels, and the sweep started earlier ends earlier (run r06zp, tools/step_ab.py, 3
+# interleaved runs each, min ms/step tower -> gather: B = 256 groups 0.1506 -> 0.1420; C2, 4,096
+# groups, 0.2655 -> 0.2864: there the sweep beside the gather and the forward slows both)
+GATHER_FORK_ROWS = 5120
 
 
 class DeferredTableAdam:
@@ -145,6 +151,7 @@ class DeferredTableAdam:
         # unfused step 0.2972-0.3006), else "mlp_bwd" (unfused at "tower": 0.3107-0.3119).
         self.fork_points = SWEEP_FORK.split(",") if SWEEP_FORK else [self._default_fork(engine)]
         self._owed = []           # parts of a closed step's rolling sweep not launched yet
+        self._rows_now = None     # the current step's batch rows (prepare; cleared by advance)
         self._side = None
         self._ev = None
         self._joined = True
@@ -301,6 +308,7 @@ class DeferredTableAdam:
         than sweep_every steps behind and the catch-up work is spread evenly over the steps.
         With the overlapped sweep it is only owed here and launched by the next sweep_fork."""
         self.t += 1
+        self._rows_now = None
         self.engine.pending = None
         if self.sweep_every and self.clock is not None and self.overlap:
             self._owed = list(range(len(self.fork_points)))
@@ -334,10 +342,8 @@ class DeferredTableAdam:
         """During step T+1 (clock->t = T, after its catch-up), at the engine's fork point `at`:
         launch the part of the owed sweep of step T registered there on the side stream; it
         overlaps everything the current stream does until sweep_join."""
-        if at not in self.fork_points:
-            return
-        part = self.fork_points.index(at)
-        if part not in self._owed:
+        part = self.fork_part(at)
+        if part is None or part not in self._owed:
             return
         side = self.side_stream().cuda_stream
         dev = self.clock.device
@@ -353,6 +359,15 @@ class DeferredTableAdam:
         self._owed.remove(part)
         self._joined = False
         self._live_pending = True      # (it reads the live clock: joined before the advance)
+
+    def fork_part(self, at):
+        """The part of the owed sweep forked at engine fork point `at`, or None: fork_points,
+        except that with the default single fork point a batch of at most GATHER_FORK_ROWS rows
+        forks it at "gather"."""
+        if (SWEEP_FORK is None and len(self.fork_points) == 1 and self._rows_now is not None
+                and self._rows_now <= GATHER_FORK_ROWS):
+            return 0 if at == "gather" else None
+        return self.fork_points.index(at) if at in self.fork_points else None
 
     def side_stream(self):
         """The overlapped sweep's stream (created on first use)."""
@@ -456,6 +471,7 @@ class DeferredTableAdam:
         eng = self.engine
         m = eng.model
         n = w.g.n
+        self._rows_now = n
         self.late_join(st)
         if (CLAIM_CATCHUP and self.clock is not None and n > 0 and not getattr(w, "prededuped", None)
                 and not torch.cuda.is_current_stream_capturing()):

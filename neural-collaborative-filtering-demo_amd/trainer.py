@@ -472,7 +472,7 @@ class FusedTrainStep:
                             if eng.fork_hook is not hook:
                                 return
                             d = self.deferred
-                            if DEDUP_FORK == "sweep" and d.overlap and at in d.fork_points \
+                            if DEDUP_FORK == "sweep" and d.overlap and d.fork_part(at) is not None \
                                     and not d._joined:
                                 # the overlapped sweep was just forked here: the sort queues
                                 # behind it on its stream, ordered by the sweep's own fork

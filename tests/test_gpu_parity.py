@@ -1342,6 +1342,7 @@ def test_pipelined_dedup_bitwise_equals_inline(monkeypatch, ahead):
                                         (False, "tower,mlp_bwd,reduce"),
                                         (True, "tower,attn_bwd"),
                                         (False, "emb_bwd,nowhere"),
+                                        (False, "gather"), (True, "gather"),
                                         (False, "off")])
 def test_overlapped_sweep_bitwise_equals_dense(monkeypatch, graph, fork):
     """The overlapped rolling sweep (side stream; the default fork point is the tower
