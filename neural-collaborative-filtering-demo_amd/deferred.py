@@ -79,9 +79,10 @@ SWEEP_FORK = None
 # With the default fork point, batches of at most GATHER_FORK_ROWS rows fork the sweep before
 # their gathers instead ("gather"): the small-batch step leaves most CUs idle beside its short
 # kernels, and the sweep started earlier ends earlier (run r06zp, tools/step_ab.py, 3
-# interleaved runs each, min ms/step tower -> gather: B = 256 groups 0.1506 -> 0.1420; C2, 4,096
-# groups, 0.2655 -> 0.2864: there the sweep beside the gather and the forward slows both)
-GATHER_FORK_ROWS = 5120
+# interleaved runs each, min ms/step tower -> gather: B = 256 groups 0.1506 -> 0.1420; run
+# r06zq: 1,024 groups 0.2018 -> 0.2042, 2,048 0.2172 -> 0.2165; C2, 4,096 groups, 0.2655 ->
+# 0.2864: there the sweep beside the gather and the forward slows both)
+GATHER_FORK_ROWS = 2560
 
 
 class DeferredTableAdam:
