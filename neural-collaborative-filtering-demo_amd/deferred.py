@@ -80,7 +80,8 @@ SWEEP_FORK = None
 # their gathers instead ("gather"): the small-batch step leaves most CUs idle beside its short
 # kernels, and the sweep started earlier ends earlier (run r06zp, tools/step_ab.py, 3
 # interleaved runs each, min ms/step tower -> gather: B = 256 groups 0.1506 -> 0.1420; run
-# r06zq: 1,024 groups 0.2018 -> 0.2042, 2,048 0.2172 -> 0.2165; C2, 4,096 groups, 0.2655 ->
+# r06zr / r06zq: 512 groups 0.1732 -> 0.1693, 1,024 0.2018 -> 0.2042, 2,048 0.2172 -> 0.2165;
+# C2, 4,096 groups, 0.2655 ->
 # 0.2864: there the sweep beside the gather and the forward slows both)
 GATHER_FORK_ROWS = 2560
 
