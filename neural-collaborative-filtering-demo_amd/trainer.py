@@ -94,11 +94,6 @@ LATE_DETACHED = False
 # the sweep beside the reductions and the next gather runs longer than beside the fused forward
 # (64 against 50 us), more than the fork event it saves); bit-identical (its tests run it).
 SIDE_AHEAD = False
-# A one-wave wall-clock spin of LATE_SPIN_US microseconds queued on the side stream ahead of the
-# late catch-up's wait for the table apply (ncf_stream_spin): a queue that reaches a wait before
-# its signal resumes ~10 us after it (tools/event_cost.py), so the side queue arriving just
-# after the signal starts the catch-up sooner.  0: off.
-LATE_SPIN_US = 0
 
 
 def _join_side_streams(dev, streams):
@@ -306,8 +301,6 @@ class FusedTrainStep:
             d._late_clock = torch.zeros_like(self.clock)
         ev = self._event()     # (also orders the copy below after the copy buffer's creation)
         ev.record(_lib.stream_ptr(self.model.engine.flat.device))
-        if LATE_SPIN_US > 0:
-            _lib.call("ncf_stream_spin", int(LATE_SPIN_US), side.cuda_stream)
         ev.wait(side.cuda_stream)
         if ahead:
             d.side_ordered()
