@@ -99,6 +99,8 @@ SIDE_AHEAD = False
 def _join_side_streams(dev, streams):
     """FusedTrainStep finalizer: the current stream of `dev` waits for each side stream."""
     try:
+        if torch.cuda.is_current_stream_capturing():
+            return          # (not inside another step's graph capture: nothing may join it)
         cur = torch.cuda.current_stream(dev)
         for s in streams:
             cur.wait_stream(s)
