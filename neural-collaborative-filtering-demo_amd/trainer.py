@@ -56,7 +56,8 @@ FUSE_APPLY = True
 # period halves the sweep's HBM traffic beside the forward; the replayed element-steps are the
 # same in total (moved from the sweep to the catch-up, which now runs beside the reductions:
 # deferred.LATE_CATCHUP).  At C2 steady state, 3 interleaved runs each: 0.2703 / 0.2709 ms/step
-# at 128 against 0.2769-0.2794 at 64 (tools/step_ab.py, primed 2 x the period).
+# at 128 against 0.2769-0.2794 at 64 (tools/step_ab.py, primed 2 x the period); round 6 (run
+# r06zx, min of 3): 128 0.2653, 192 0.2632, 256 0.2669 — within the runs' spread, 128 stays.
 SWEEP_EVERY = 128
 # The step's join of the side stream (sweep, next sort, late catch-up) after the dense Adam
 # rather than before it: the flat Adam (ncf_adam_flat_clock) runs first, then the join, then the
